@@ -1,0 +1,207 @@
+/*
+ * ocppo.h — C-ABI of libocppo_hip.so, the MI355X (gfx950) kernels behind the OC-CleanRL PPO
+ * actor-learner hot path.
+ *
+ * The reference (BluemlJ/oc_cleanrl) is pure Python; there is no FFI to mirror. Each entry point
+ * below replaces one stock-PyTorch op sequence of `cleanrl/ppo_atari_oc.py` (and its DP twin
+ * `cleanrl/ppo_atari_multigpu.py`); the replaced lines are cited per function. A caller binds the
+ * library with ctypes and passes torch `data_ptr()`s.
+ *
+ * Conventions (all functions):
+ *   - every pointer is a caller-owned DEVICE pointer unless stated otherwise; nothing allocates;
+ *   - `stream` is a hipStream_t (NULL = legacy default stream); every launch is asynchronous and
+ *     graph-capturable (no host sync, no hipMalloc, no memcpy to host inside);
+ *   - the return value is 0 on success, otherwise an OCPPO_E_* code; ocppo_last_error() returns
+ *     a thread-local message for the last failure. Nothing throws or aborts across the ABI;
+ *   - results are deterministic: fixed-order reductions, no floating-point atomics;
+ *   - scalar hyper-parameters are passed as double, exactly as the reference's Python floats,
+ *     and rounded to f32 inside the library exactly where PyTorch rounds them.
+ *   - all buffers are step-major: element (t, n) of a [T, N] rollout array is at t*N + n
+ *     (ppo_atari_oc.py:452-459, flattened at :550-555).
+ */
+#ifndef OCPPO_H
+#define OCPPO_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OCPPO_ABI_VERSION 1
+
+/* status codes */
+#define OCPPO_OK 0
+#define OCPPO_E_INVALID 1   /* bad argument (null pointer, size, dtype) */
+#define OCPPO_E_LAUNCH 2    /* hipGetLastError() after a launch */
+#define OCPPO_E_WORKSPACE 3 /* workspace missing or too small */
+
+/* element types used by the obs storage / frame arguments */
+#define OCPPO_F32 0
+#define OCPPO_BF16 1
+#define OCPPO_U8 2
+
+/* layout of the `stats` output of ocppo_ppo_loss_fwd_bwd (all f32) */
+#define OCPPO_STAT_LOSS 0          /* loss = pg - ent_coef*entropy + vf_coef*v_loss   :599-602 */
+#define OCPPO_STAT_PG_LOSS 1       /* pg_loss                                        :581-583 */
+#define OCPPO_STAT_V_LOSS 2        /* v_loss                                         :585-597 */
+#define OCPPO_STAT_ENTROPY 3       /* entropy_loss = mean(entropy)                   :599     */
+#define OCPPO_STAT_OLD_APPROX_KL 4 /* mean(-logratio)                                :573     */
+#define OCPPO_STAT_APPROX_KL 5     /* mean((ratio-1) - logratio)                     :574     */
+#define OCPPO_STAT_CLIPFRAC 6      /* mean(|ratio-1| > clip_coef)                    :575     */
+#define OCPPO_STAT_ADV_MEAN 7      /* minibatch advantage mean used by the norm      :577-579 */
+#define OCPPO_STAT_ADV_STD 8       /* minibatch advantage std (unbiased)             :577-579 */
+#define OCPPO_NUM_STATS 9
+
+typedef void* ocppo_stream_t; /* hipStream_t */
+
+#if defined(__GNUC__) || defined(__clang__)
+#define OCPPO_API __attribute__((visibility("default")))
+#else
+#define OCPPO_API
+#endif
+
+OCPPO_API int ocppo_abi_version(void);
+OCPPO_API const char* ocppo_last_error(void);
+
+/* ---------------------------------------------------------------------------------------------
+ * GAE — replaces the reverse Python loop of ppo_atari_oc.py:533-547 (identical in ppo.py:218-231
+ * and ppo_atari_multigpu.py:288-301); 9 ATen launches per step → one kernel per rollout.
+ *   rewards, values, dones : [T, N] f32;   next_value, next_done : [N] f32
+ *   advantages, returns    : [T, N] f32 outputs (returns = advantages + values)
+ * f32 arithmetic in the reference's exact op order (no FMA contraction), so the result is
+ * bit-identical to the PyTorch loop:  delta = (r + (f32(gamma)*nv)*nnt) - v;
+ *                                     A = delta + (f32(gamma*lambda)*nnt)*A'
+ * ------------------------------------------------------------------------------------------- */
+OCPPO_API int ocppo_gae(ocppo_stream_t stream, const float* rewards, const float* values, const float* dones,
+              const float* next_value, const float* next_done, int64_t T, int64_t N, double gamma,
+              double gae_lambda, float* advantages, float* returns);
+
+/* ---------------------------------------------------------------------------------------------
+ * Minibatch advantage statistics — the (mean, unbiased std) pair of ppo_atari_oc.py:577-579 for
+ * `num_mb` minibatches at once. Minibatch k holds b_advantages[perm[k*M + i]], i < M.
+ *   perm : [num_mb*M] int64 (the np.random.shuffle'd b_inds of :561, all epochs concatenated)
+ *   out  : [num_mb, 2] f32 = {mean, std}
+ * ------------------------------------------------------------------------------------------- */
+OCPPO_API int ocppo_minibatch_adv_stats(ocppo_stream_t stream, const float* b_advantages, const int64_t* perm,
+                              int64_t M, int64_t num_mb, float* out);
+
+/* ---------------------------------------------------------------------------------------------
+ * Fused PPO minibatch loss, forward AND backward — replaces ppo_atari_oc.py:566-602 from the
+ * network's raw outputs onward (Categorical log-softmax / log_prob / entropy of
+ * architectures/ppo.py:89-95, ratio, KL stats, clipfrac, advantage norm, clipped surrogate,
+ * clipped value loss, entropy bonus) plus the autograd backward of that graph down to the
+ * network outputs.
+ *   logits    : [M, A] f32 raw actor outputs;  new_value : [M] f32 critic outputs
+ *   mb_inds   : [M] int64 indices into the b_* batch arrays, or NULL (inputs already gathered,
+ *               b_*[i] is element i)
+ *   b_actions : int64 [B]; b_logprobs, b_advantages, b_returns, b_values : f32 [B]
+ *   adv_stats : [2] f32 {mean, std} from ocppo_minibatch_adv_stats, or NULL to compute them
+ *               here (then workspace must be given); ignored when norm_adv == 0
+ *   dlogits   : [M, A] f32 = dLoss/dlogits;  dvalue : [M] f32 = dLoss/dnew_value
+ *   stats     : [OCPPO_NUM_STATS] f32 (layout above)
+ *   workspace : device scratch of ocppo_ppo_loss_workspace_bytes(M, A) bytes; it must be zeroed
+ *               once after allocation and then never touched by the caller (its ticket word is
+ *               reset by the kernel itself, so the call can be replayed from a graph).
+ * Gradient rules follow autograd exactly: torch.max splits the gradient 1/2-1/2 on ties, clamp
+ * passes it at the bounds.
+ * ------------------------------------------------------------------------------------------- */
+OCPPO_API size_t ocppo_ppo_loss_workspace_bytes(int64_t M, int64_t A);
+OCPPO_API int ocppo_ppo_loss_fwd_bwd(ocppo_stream_t stream, const float* logits, const float* new_value,
+                           int64_t M, int64_t A, const int64_t* mb_inds, const int64_t* b_actions,
+                           const float* b_logprobs, const float* b_advantages,
+                           const float* b_returns, const float* b_values, const float* adv_stats,
+                           double clip_coef, double ent_coef, double vf_coef, int norm_adv,
+                           int clip_vloss, float* dlogits, float* dvalue, float* stats,
+                           void* workspace, size_t workspace_bytes);
+
+/* ---------------------------------------------------------------------------------------------
+ * Rollout action head — replaces Categorical(logits).sample() / log_prob / entropy of
+ * architectures/ppo.py:91-95 and the storage writes of ppo_atari_oc.py:506-510.
+ * torch's sampler (Categorical.sample → multinomial(probs, 1, True)) draws q ~ Exp(1) of shape
+ * [N, A] and returns argmax(probs / q); `noise` must be that q (e.g. from
+ * torch.empty(N, A).exponential_() on the same generator), so actions are bit-identical.
+ *   logits : [N, A] f32; noise : [N, A] f32
+ *   action_out : [N] int64 (e.g. &actions[t*N]);  logprob_out : [N] f32 (&logprobs[t*N])
+ *   entropy_out : [N] f32 or NULL
+ *   value_in / value_out : critic output [N] copied into &values[t*N] (both NULL to skip)
+ * ------------------------------------------------------------------------------------------- */
+OCPPO_API int ocppo_categorical_sample(ocppo_stream_t stream, const float* logits, const float* noise,
+                             int64_t N, int64_t A, int64_t* action_out, float* logprob_out,
+                             float* entropy_out, const float* value_in, float* value_out);
+
+/* log_prob(action) and entropy() of Categorical(logits) for given actions (architectures/ppo.py
+ * :92-95 with `action` passed) and the matching backward. */
+OCPPO_API int ocppo_categorical_logprob_entropy(ocppo_stream_t stream, const float* logits,
+                                      const int64_t* actions, int64_t N, int64_t A,
+                                      float* logprob_out, float* entropy_out);
+OCPPO_API int ocppo_categorical_logprob_entropy_bwd(ocppo_stream_t stream, const float* logits,
+                                          const int64_t* actions, const float* grad_logprob,
+                                          const float* grad_entropy, int64_t N, int64_t A,
+                                          float* dlogits);
+
+/* ---------------------------------------------------------------------------------------------
+ * Rollout store — replaces ppo_atari_oc.py:502-503 and :512-514 (host float32 conversion,
+ * pageable H2D copies and `obs[step] = next_obs`) with one device pass per env step that also
+ * performs the frame stacking the reference does in N env subprocesses.
+ *   frame      : [N, D] newest frame per env, dtype frame_dtype (OCPPO_F32 object vectors of
+ *                OCAtari obj mode, D = F; or OCPPO_U8 grayscale 84x84 pixels, D = 7056)
+ *   reward     : [N] f32;  done : [N] f32 (0/1)
+ *   prev_obs   : [N, W, D] stacked obs of the previous step, dtype obs_dtype (rollout slot t)
+ *   obs_out    : [N, W, D] new stacked obs, dtype obs_dtype (rollout slot t+1)
+ *   net_obs    : [N, W, D] f32 copy of obs_out for the network forward (may be NULL)
+ *   reward_out : [N] f32 (&rewards[t*N]);  done_out : [N] f32 (&dones[(t+1)*N]); either may be NULL
+ * Stacking: obs_out[n] = prev_obs[n][1:] ++ frame[n]; on done[n] every slot is frame[n] (the
+ * gymnasium FrameStack reset fill). Conversion to bf16 is round-to-nearest-even and exact for
+ * the integer-valued obs of both modes (|x| <= 256).
+ * ------------------------------------------------------------------------------------------- */
+OCPPO_API int ocppo_rollout_store(ocppo_stream_t stream, const void* frame, int frame_dtype,
+                        const float* reward, const float* done, int64_t N, int64_t W, int64_t D,
+                        const void* prev_obs, void* obs_out, int obs_dtype, float* net_obs,
+                        float* reward_out, float* done_out);
+
+/* Fill a whole stacked-obs slot from one frame per env (env reset, ppo_atari_oc.py:464-465). */
+OCPPO_API int ocppo_obs_reset(ocppo_stream_t stream, const void* frame, int frame_dtype, int64_t N,
+                    int64_t W, int64_t D, void* obs_out, int obs_dtype, float* net_obs);
+
+/* ---------------------------------------------------------------------------------------------
+ * Minibatch gather — replaces `b_obs[mb_inds]` of ppo_atari_oc.py:566-567:
+ *   dst[i, :] = f32(src[idx[i], :]),  src [B, R] of dtype src_dtype, dst [M, R] f32.
+ * ------------------------------------------------------------------------------------------- */
+OCPPO_API int ocppo_gather_rows(ocppo_stream_t stream, const void* src, int src_dtype, const int64_t* idx,
+                      int64_t M, int64_t R, float* dst);
+
+/* ---------------------------------------------------------------------------------------------
+ * Reward normalisation of SB3 VecNormalize(norm_obs=False, norm_reward=True) as wrapped at
+ * ppo_atari_oc.py:414 (stable-baselines3 2.0.0, not in the reference tree), on device in f64:
+ *   ret = ret*gamma + r;  rms.update(ret) (batch mean/var over N, Chan merge);
+ *   r' = clip(r / sqrt(rms.var + epsilon), -clip, clip);  ret[done] = 0
+ *   ret_state : [N] f64;  rms_state : [3] f64 = {mean, var, count} (init {0, 1, 1e-4})
+ *   reward_out : [N] f32 (may alias nothing; typically &rewards[t*N])
+ * ------------------------------------------------------------------------------------------- */
+OCPPO_API int ocppo_vecnorm_reward(ocppo_stream_t stream, const float* reward, const float* done, int64_t N,
+                         double gamma, double epsilon, double clip_reward, double* ret_state,
+                         double* rms_state, float* reward_out);
+
+/* ---------------------------------------------------------------------------------------------
+ * Synthetic device-resident env (benchmark / test harness; ALE and OCAtari are not available).
+ * Not a reference component. Counter-based hashing of (seed, env, step) gives reproducible
+ * frames: object mode x~U{0..159}, y~U{0..209}, w,h~U{1..16} per 4-feature object; pixel mode
+ * 84x84 u8 with ~90% zeros; reward = +-1 w.p. 0.005 each; done w.p. 1/3500 (Pong-v5 episode
+ * lengths). `actions` shift the first object's y so the env reacts to the policy.
+ *   frame_out : [N, D] (f32 for obj, u8 for pixels); reward_out, done_out : [N] f32
+ *   step_base : device int64 read at run time (graph replays advance it), the hashed step id is
+ *               step_base[0] + step_offset
+ *   ep_state  : [N, 5] f32 = {running return, running length, finished-episode return sum,
+ *               finished-episode length sum, finished-episode count}, updated in place (may be
+ *               NULL); the RecordEpisodeStatistics counters behind ppo_atari_oc.py:516-529
+ * ------------------------------------------------------------------------------------------- */
+OCPPO_API int ocppo_synth_env_step(ocppo_stream_t stream, uint64_t seed, const int64_t* step_base,
+                         int64_t step_offset, const int64_t* actions, int64_t N, int64_t D, int pixel_mode,
+                         void* frame_out, float* reward_out, float* done_out, float* ep_state);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OCPPO_H */

@@ -1,0 +1,85 @@
+"""ctypes binding of libocppo_hip.so (the C-ABI declared in include/ocppo.h).
+
+torch is imported first on purpose: torch ships libamdhip64.so with soname libamdhip64.so.7, and
+libocppo_hip.so's NEEDED entry is that soname, so loading ours after torch reuses torch's HIP
+runtime (one runtime per process, shared streams and graph capture).
+
+There is no CPU fallback: if the library is missing, importing this module raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import re
+from pathlib import Path
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+PKG = Path(__file__).resolve().parent
+LIB_PATH = PKG / "lib" / "libocppo_hip.so"
+HEADER = PKG.parent / "include" / "ocppo.h"
+
+# constants mirrored from include/ocppo.h (checked against the header by tests/test_abi.py)
+OCPPO_ABI_VERSION = 1
+OCPPO_OK, OCPPO_E_INVALID, OCPPO_E_LAUNCH, OCPPO_E_WORKSPACE = 0, 1, 2, 3
+OCPPO_F32, OCPPO_BF16, OCPPO_U8 = 0, 1, 2
+STAT_NAMES = ("loss", "pg_loss", "v_loss", "entropy", "old_approx_kl", "approx_kl", "clipfrac",
+              "adv_mean", "adv_std")
+OCPPO_NUM_STATS = len(STAT_NAMES)
+
+P, I64, U64, D, I, SZ = (ctypes.c_void_p, ctypes.c_int64, ctypes.c_uint64, ctypes.c_double,
+                         ctypes.c_int, ctypes.c_size_t)
+
+SIGNATURES: dict[str, tuple[type, list]] = {
+    "ocppo_abi_version": (I, []),
+    "ocppo_last_error": (ctypes.c_char_p, []),
+    "ocppo_gae": (I, [P, P, P, P, P, P, I64, I64, D, D, P, P]),
+    "ocppo_minibatch_adv_stats": (I, [P, P, P, I64, I64, P]),
+    "ocppo_ppo_loss_workspace_bytes": (SZ, [I64, I64]),
+    "ocppo_ppo_loss_fwd_bwd": (I, [P, P, P, I64, I64, P, P, P, P, P, P, P, D, D, D, I, I, P, P, P,
+                                   P, SZ]),
+    "ocppo_categorical_sample": (I, [P, P, P, I64, I64, P, P, P, P, P]),
+    "ocppo_categorical_logprob_entropy": (I, [P, P, P, I64, I64, P, P]),
+    "ocppo_categorical_logprob_entropy_bwd": (I, [P, P, P, P, P, I64, I64, P]),
+    "ocppo_rollout_store": (I, [P, P, I, P, P, I64, I64, I64, P, P, I, P, P, P]),
+    "ocppo_obs_reset": (I, [P, P, I, I64, I64, I64, P, I, P]),
+    "ocppo_gather_rows": (I, [P, P, I, P, I64, I64, P]),
+    "ocppo_vecnorm_reward": (I, [P, P, P, I64, D, D, D, P, P, P]),
+    "ocppo_synth_env_step": (I, [P, U64, P, I64, P, I64, I64, I, P, P, P, P]),
+}
+
+
+class OcppoError(RuntimeError):
+    """A C-ABI call returned a non-zero status."""
+
+
+def header_functions() -> list[str]:
+    """Names of every function the header declares (the ABI contract)."""
+    text = HEADER.read_text()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[\w\s\*]*?\b(ocppo_\w+)\s*\(", text, re.M)))
+
+
+def _load() -> ctypes.CDLL:
+    if not LIB_PATH.exists():
+        raise ImportError(
+            f"{LIB_PATH} is missing: the HIP extension is required (no CPU fallback). "
+            "Build it with `python -m oc_cleanrl_amd.build`.")
+    lib = ctypes.CDLL(str(LIB_PATH))
+    for name, (restype, argtypes) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = restype
+        fn.argtypes = argtypes
+    ver = lib.ocppo_abi_version()
+    if ver != OCPPO_ABI_VERSION:
+        raise ImportError(f"{LIB_PATH}: ABI version {ver}, expected {OCPPO_ABI_VERSION}; rebuild")
+    return lib
+
+
+LIB = _load()
+
+
+def call(name: str, *args) -> None:
+    """Invoke a status-returning entry point and raise OcppoError on failure."""
+    rc = getattr(LIB, name)(*args)
+    if rc != OCPPO_OK:
+        msg = LIB.ocppo_last_error().decode(errors="replace")
+        raise OcppoError(f"{name} failed (status {rc}): {msg}")

@@ -1,0 +1,540 @@
+// Fused PPO minibatch loss (forward + backward), minibatch advantage statistics and the
+// Categorical action head.
+//
+// Replaces, from the network's raw outputs onward, cleanrl/ppo_atari_oc.py:566-602 (ratio, KL
+// stats, clipfrac, advantage normalisation, clipped surrogate, clipped value loss, entropy bonus)
+// and torch.distributions.Categorical as used by architectures/ppo.py:89-95, plus the autograd
+// backward of all of it down to d loss / d logits and d loss / d value.
+//
+// Every per-element quantity is computed in f32 in PyTorch's op order (no contraction), and the
+// backward follows autograd's formulas: max() splits the gradient 1/2-1/2 on ties, clamp() passes
+// it at the bounds, softmax/logsumexp backward as in ATen. Reductions use a fixed order (per-thread
+// strided sums, wave butterfly, waves in order, blocks in order), so results are run-to-run
+// bit-identical; they differ from ATen's own reduction trees only in the last bits.
+//
+// Roofline of the loss kernel: HBM/latency bound, (8A + 36) algorithmic bytes per element
+// (logits 4A + value 4 + index 8 + action 8 + old logprob/adv/return/value 16 in; dlogits 4A + dv 4
+// out). At the configs (M = 4096) one launch moves 344 KB and is launch/latency bound.
+#include <cfloat>
+
+#include "ocppo_common.h"
+
+namespace ocppo {
+
+constexpr int kLossThreads = 256;  // one element per thread, one 256-element tile per workgroup
+constexpr int kNumPartials = 6;    // pg, v, entropy, old_kl, kl, clipfrac
+constexpr size_t kTicketBytes = 256;
+
+// Row statistics of Categorical(logits=l): lse, normalised logits ln = l - lse, probs = softmax(ln)
+// (torch/distributions/categorical.py: logits - logits.logsumexp(-1), then logits_to_probs).
+template <int AMAX>
+__device__ __forceinline__ void categorical_row(const float (&l)[AMAX], int A, float& lse,
+                                                float (&ln)[AMAX], float (&p)[AMAX]) {
+  float m = l[0];
+#pragma unroll
+  for (int j = 1; j < AMAX; ++j)
+    if (j < A) m = fmaxf(m, l[j]);
+  const float mm = (fabsf(m) == INFINITY) ? 0.f : m;  // ATen masks infinite maxima
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < AMAX; ++j)
+    if (j < A) s += expf(l[j] - m);
+  lse = logf(s) + mm;
+  float m2 = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < AMAX; ++j)
+    if (j < A) {
+      ln[j] = l[j] - lse;
+      m2 = fmaxf(m2, ln[j]);
+    }
+  float s2 = 0.f;
+#pragma unroll
+  for (int j = 0; j < AMAX; ++j)
+    if (j < A) {
+      p[j] = expf(ln[j] - m2);
+      s2 += p[j];
+    }
+#pragma unroll
+  for (int j = 0; j < AMAX; ++j)
+    if (j < A) p[j] = p[j] / s2;
+}
+
+// entropy = -(clamp(ln, min=lowest) * p).sum(-1)   (Categorical.entropy)
+template <int AMAX>
+__device__ __forceinline__ float categorical_entropy(const float (&ln)[AMAX],
+                                                     const float (&p)[AMAX], int A) {
+  float acc = 0.f;
+#pragma unroll
+  for (int j = 0; j < AMAX; ++j)
+    if (j < A) acc += fmaxf(ln[j], -FLT_MAX) * p[j];
+  return -acc;
+}
+
+// Backward of (log_prob(a), entropy()) w.r.t. the raw logits, for upstream grads g_lp and g_h.
+template <int AMAX>
+__device__ __forceinline__ void categorical_backward(const float (&l)[AMAX], float lse,
+                                                     const float (&ln)[AMAX],
+                                                     const float (&p)[AMAX], int A, int64_t a,
+                                                     float g_lp, float g_h, float (&dl)[AMAX]) {
+  const float dplp = -g_h;  // entropy = -sum(p_log_p)
+  float dot = 0.f;          // softmax backward: sum_k dprobs_k * p_k, dprobs_k = dplp * ln_k
+#pragma unroll
+  for (int j = 0; j < AMAX; ++j)
+    if (j < A) dot += (dplp * ln[j]) * p[j];
+  float S = 0.f;
+#pragma unroll
+  for (int j = 0; j < AMAX; ++j)
+    if (j < A) {
+      const float dprob = dplp * ln[j];
+      float d = dplp * p[j];               // through the clamped normalised logits
+      d = d + p[j] * (dprob - dot);        // through probs = softmax(ln)
+      if (j == a) d = d + g_lp;            // through log_prob's gather
+      dl[j] = d;
+      S += d;
+    }
+#pragma unroll
+  for (int j = 0; j < AMAX; ++j)  // ln = l - logsumexp(l)
+    if (j < A) dl[j] = dl[j] - S * expf(l[j] - lse);
+}
+
+// ---- minibatch advantage statistics ------------------------------------------------------------
+// grid = num_mb, one workgroup per minibatch; two passes (mean, then sum of squared deviations).
+__global__ __launch_bounds__(256) void adv_stats_kernel(const float* __restrict__ adv,
+                                                        const int64_t* __restrict__ perm,
+                                                        int64_t M, float* __restrict__ out) {
+  __shared__ float scratch[16];
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * M;
+  float s = 0.f;
+  for (int64_t i = threadIdx.x; i < M; i += blockDim.x) s += adv[perm ? perm[base + i] : base + i];
+  s = block_sum(s, scratch);
+  const float mean = s / static_cast<float>(M);
+  float q = 0.f;
+  for (int64_t i = threadIdx.x; i < M; i += blockDim.x) {
+    const float d = adv[perm ? perm[base + i] : base + i] - mean;
+    q += d * d;
+  }
+  q = block_sum(q, scratch);
+  if (threadIdx.x == 0) {
+    out[2 * blockIdx.x + 0] = mean;
+    out[2 * blockIdx.x + 1] = sqrtf(q / static_cast<float>(M - 1));  // unbiased, torch.std()
+  }
+}
+
+// ---- fused loss ----------------------------------------------------------------------------------
+struct LossParams {
+  const float* logits;
+  const float* new_value;
+  const int64_t* mb_inds;
+  const int64_t* b_actions;
+  const float* b_logprobs;
+  const float* b_adv;
+  const float* b_ret;
+  const float* b_val;
+  const float* adv_stats;
+  float* dlogits;
+  float* dvalue;
+  float* stats;
+  unsigned* ticket;
+  float* partials;  // [gridDim.x][kNumPartials]
+  int64_t M;
+  int A;
+  int norm_adv, clip_vloss;
+  float clip, clip_lo, clip_hi;  // f32(c), f32(1-c), f32(1+c)
+  float ent_coef, vf_coef;
+  float g_pg, g_h, g_v;  // upstream grads reaching mean(pg), mean(entropy), mean(v_loss_max)
+  float inv_m;           // f32(1/M) for the reported means
+};
+
+template <int AMAX>
+__global__ __launch_bounds__(kLossThreads) void ppo_loss_kernel(LossParams P) {
+  extern __shared__ __attribute__((aligned(16))) float tile[];  // [kLossThreads * A]
+  __shared__ float red[kLossThreads / kWave][kNumPartials];
+  __shared__ int s_last;
+
+  const int A = P.A;
+  const int64_t i0 = static_cast<int64_t>(blockIdx.x) * kLossThreads;
+  const int64_t cnt = (P.M - i0) < kLossThreads ? (P.M - i0) : kLossThreads;
+  const int tid = threadIdx.x;
+
+  // stage this tile's logits rows (contiguous [cnt*A] floats) with coalesced loads
+  for (int64_t e = tid; e < cnt * A; e += kLossThreads) tile[e] = P.logits[i0 * A + e];
+  __syncthreads();
+
+  float part[kNumPartials] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float dl[AMAX];
+  const bool active = tid < cnt;
+  if (active) {
+    const int64_t i = i0 + tid;
+    const int64_t b = P.mb_inds ? P.mb_inds[i] : i;
+    const int64_t a = P.b_actions[b];
+    const float old_lp = P.b_logprobs[b];
+    const float adv = P.b_adv[b];
+    const float R = P.b_ret[b];
+    const float v_old = P.b_val[b];
+    const float v = P.new_value[i];
+
+    float l[AMAX], ln[AMAX], p[AMAX];
+#pragma unroll
+    for (int j = 0; j < AMAX; ++j) l[j] = j < A ? tile[tid * A + j] : 0.f;
+    float lse;
+    categorical_row<AMAX>(l, A, lse, ln, p);
+    float new_lp = 0.f;
+#pragma unroll
+    for (int j = 0; j < AMAX; ++j)
+      if (j == a) new_lp = ln[j];
+    const float H = categorical_entropy<AMAX>(ln, p, A);
+
+    // ratio and no-grad diagnostics (:569-575)
+    const float logratio = new_lp - old_lp;
+    const float ratio = expf(logratio);
+    part[3] = -logratio;
+    part[4] = (ratio - 1.0f) - logratio;
+    part[5] = fabsf(ratio - 1.0f) > P.clip ? 1.f : 0.f;
+
+    // advantage normalisation (:577-579)
+    float advn = adv;
+    if (P.norm_adv) advn = (adv - P.adv_stats[0]) / (P.adv_stats[1] + 1e-8f);
+
+    // clipped surrogate (:581-583)
+    const float nadv = -advn;
+    const float pg1 = nadv * ratio;
+    const float rc = fminf(fmaxf(ratio, P.clip_lo), P.clip_hi);
+    const float pg2 = nadv * rc;
+    part[0] = fmaxf(pg1, pg2);
+
+    // value loss (:585-597)
+    const float du = v - R;
+    const float vu = du * du;
+    float dv;
+    if (P.clip_vloss) {
+      const float dvv = v - v_old;
+      const float dvc = fminf(fmaxf(dvv, -P.clip), P.clip);
+      const float vcl = v_old + dvc;
+      const float dc = vcl - R;
+      const float vc = dc * dc;
+      part[1] = fmaxf(vu, vc);
+      const float gu = vu > vc ? P.g_v : (vu == vc ? P.g_v / 2.f : 0.f);
+      const float gc = vc > vu ? P.g_v : (vu == vc ? P.g_v / 2.f : 0.f);
+      const float tu = gu * (2.0f * du);
+      float tc = gc * (2.0f * dc);
+      tc = (dvv >= -P.clip && dvv <= P.clip) ? tc : 0.f;
+      dv = tu + tc;
+    } else {
+      part[1] = vu;
+      dv = P.g_v * (2.0f * du);
+    }
+    part[2] = H;
+
+    // backward of the surrogate to new_logprob
+    const float g1 = pg1 > pg2 ? P.g_pg : (pg1 == pg2 ? P.g_pg / 2.f : 0.f);
+    const float g2 = pg2 > pg1 ? P.g_pg : (pg1 == pg2 ? P.g_pg / 2.f : 0.f);
+    const float dr1 = g1 * nadv;
+    const float dr2 = (ratio >= P.clip_lo && ratio <= P.clip_hi) ? g2 * nadv : 0.f;
+    const float dratio = dr1 + dr2;
+    const float dnew_lp = dratio * ratio;  // exp backward, then logratio = new - old
+
+    categorical_backward<AMAX>(l, lse, ln, p, A, a, dnew_lp, P.g_h, dl);
+    P.dvalue[i] = dv;
+  }
+  __syncthreads();  // everyone has read its logits row; reuse the tile for dlogits
+  if (active) {
+#pragma unroll
+    for (int j = 0; j < AMAX; ++j)
+      if (j < A) tile[tid * A + j] = dl[j];
+  }
+  __syncthreads();
+  for (int64_t e = tid; e < cnt * A; e += kLossThreads) P.dlogits[i0 * A + e] = tile[e];
+
+  // per-block partial sums in a fixed order
+  const int lane = tid & (kWave - 1), wid = tid / kWave;
+#pragma unroll
+  for (int k = 0; k < kNumPartials; ++k) {
+    const float w = wave_sum(part[k]);
+    if (lane == 0) red[wid][k] = w;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    unsigned* tk = P.ticket;
+#pragma unroll
+    for (int k = 0; k < kNumPartials; ++k) {
+      float s = red[0][k];
+      for (int w = 1; w < kLossThreads / kWave; ++w) s += red[w][k];
+      __hip_atomic_store(&P.partials[blockIdx.x * kNumPartials + k], s, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned prev = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (prev == gridDim.x - 1) ? 1 : 0;
+    if (s_last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+  if (!s_last) return;
+
+  // last workgroup: combine the partials of every block in block order
+  float tot[kNumPartials] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (unsigned blk = tid; blk < gridDim.x; blk += kLossThreads) {
+#pragma unroll
+    for (int k = 0; k < kNumPartials; ++k)
+      tot[k] += __hip_atomic_load(&P.partials[blk * kNumPartials + k], __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+  }
+#pragma unroll
+  for (int k = 0; k < kNumPartials; ++k) {
+    const float w = wave_sum(tot[k]);
+    __syncthreads();
+    if (lane == 0) red[wid][k] = w;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float s[kNumPartials];
+#pragma unroll
+    for (int k = 0; k < kNumPartials; ++k) {
+      s[k] = red[0][k];
+      for (int w = 1; w < kLossThreads / kWave; ++w) s[k] += red[w][k];
+    }
+    const float pg_loss = s[0] * P.inv_m;
+    const float v_loss = P.clip_vloss ? 0.5f * (s[1] * P.inv_m) : 0.5f * (s[1] * P.inv_m);
+    const float ent = s[2] * P.inv_m;
+    const float loss = (pg_loss - P.ent_coef * ent) + v_loss * P.vf_coef;
+    P.stats[OCPPO_STAT_LOSS] = loss;
+    P.stats[OCPPO_STAT_PG_LOSS] = pg_loss;
+    P.stats[OCPPO_STAT_V_LOSS] = v_loss;
+    P.stats[OCPPO_STAT_ENTROPY] = ent;
+    P.stats[OCPPO_STAT_OLD_APPROX_KL] = s[3] * P.inv_m;
+    P.stats[OCPPO_STAT_APPROX_KL] = s[4] * P.inv_m;
+    P.stats[OCPPO_STAT_CLIPFRAC] = s[5] * P.inv_m;
+    P.stats[OCPPO_STAT_ADV_MEAN] = P.norm_adv ? P.adv_stats[0] : 0.f;
+    P.stats[OCPPO_STAT_ADV_STD] = P.norm_adv ? P.adv_stats[1] : 0.f;
+    __hip_atomic_store(P.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+  }
+}
+
+// ---- Categorical action head ---------------------------------------------------------------------
+template <int AMAX>
+__global__ __launch_bounds__(256) void categorical_sample_kernel(
+    const float* __restrict__ logits, const float* __restrict__ noise, int64_t N, int A,
+    int64_t* __restrict__ action_out, float* __restrict__ logprob_out,
+    float* __restrict__ entropy_out, const float* __restrict__ value_in,
+    float* __restrict__ value_out) {
+  const int64_t n = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float l[AMAX], ln[AMAX], p[AMAX];
+#pragma unroll
+  for (int j = 0; j < AMAX; ++j) l[j] = j < A ? logits[n * A + j] : 0.f;
+  float lse;
+  categorical_row<AMAX>(l, A, lse, ln, p);
+  // torch.multinomial(probs, 1) fast path: argmax(probs / q), q ~ Exp(1); first index on ties
+  int best = 0;
+  float best_q = p[0] / noise[n * A];
+#pragma unroll
+  for (int j = 1; j < AMAX; ++j)
+    if (j < A) {
+      const float q = p[j] / noise[n * A + j];
+      if (q > best_q || (q != q && best_q == best_q)) {  // argmax propagates NaN like ATen
+        best_q = q;
+        best = j;
+      }
+    }
+  float lp = 0.f;
+#pragma unroll
+  for (int j = 0; j < AMAX; ++j)
+    if (j == best) lp = ln[j];
+  action_out[n] = best;
+  logprob_out[n] = lp;
+  if (entropy_out) entropy_out[n] = categorical_entropy<AMAX>(ln, p, A);
+  if (value_in && value_out) value_out[n] = value_in[n];
+}
+
+template <int AMAX>
+__global__ __launch_bounds__(256) void categorical_lp_ent_kernel(
+    const float* __restrict__ logits, const int64_t* __restrict__ actions, int64_t N, int A,
+    float* __restrict__ logprob_out, float* __restrict__ entropy_out) {
+  const int64_t n = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float l[AMAX], ln[AMAX], p[AMAX];
+#pragma unroll
+  for (int j = 0; j < AMAX; ++j) l[j] = j < A ? logits[n * A + j] : 0.f;
+  float lse;
+  categorical_row<AMAX>(l, A, lse, ln, p);
+  const int64_t a = actions[n];
+  float lp = 0.f;
+#pragma unroll
+  for (int j = 0; j < AMAX; ++j)
+    if (j == a) lp = ln[j];
+  if (logprob_out) logprob_out[n] = lp;
+  if (entropy_out) entropy_out[n] = categorical_entropy<AMAX>(ln, p, A);
+}
+
+template <int AMAX>
+__global__ __launch_bounds__(256) void categorical_lp_ent_bwd_kernel(
+    const float* __restrict__ logits, const int64_t* __restrict__ actions,
+    const float* __restrict__ g_lp, const float* __restrict__ g_h, int64_t N, int A,
+    float* __restrict__ dlogits) {
+  const int64_t n = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float l[AMAX], ln[AMAX], p[AMAX], dl[AMAX];
+#pragma unroll
+  for (int j = 0; j < AMAX; ++j) l[j] = j < A ? logits[n * A + j] : 0.f;
+  float lse;
+  categorical_row<AMAX>(l, A, lse, ln, p);
+  categorical_backward<AMAX>(l, lse, ln, p, A, actions[n], g_lp ? g_lp[n] : 0.f,
+                             g_h ? g_h[n] : 0.f, dl);
+#pragma unroll
+  for (int j = 0; j < AMAX; ++j)
+    if (j < A) dlogits[n * A + j] = dl[j];
+}
+
+constexpr int kMaxActions = 32;
+
+}  // namespace ocppo
+
+using namespace ocppo;
+
+static size_t loss_partials_offset() { return kTicketBytes; }
+static size_t loss_stats_offset(int64_t M) {
+  const size_t nb = static_cast<size_t>(ceil_div(M, kLossThreads));
+  return kTicketBytes + ((nb * kNumPartials * sizeof(float) + 15) / 16) * 16;
+}
+
+extern "C" size_t ocppo_ppo_loss_workspace_bytes(int64_t M, int64_t A) {
+  (void)A;
+  if (M <= 0) return kTicketBytes;
+  return loss_stats_offset(M) + 16;
+}
+
+extern "C" int ocppo_minibatch_adv_stats(ocppo_stream_t stream, const float* b_advantages,
+                                         const int64_t* perm, int64_t M, int64_t num_mb,
+                                         float* out) {
+  OCPPO_REQUIRE(M > 0 && num_mb > 0 && num_mb <= INT32_MAX,
+                "ocppo_minibatch_adv_stats: bad sizes M=%lld num_mb=%lld", (long long)M,
+                (long long)num_mb);
+  OCPPO_REQUIRE(b_advantages && out, "ocppo_minibatch_adv_stats: null pointer");
+  hipLaunchKernelGGL(adv_stats_kernel, dim3(num_mb), dim3(256), 0, as_stream(stream),
+                     b_advantages, perm, M, out);
+  return check_launch("ocppo_minibatch_adv_stats");
+}
+
+extern "C" int ocppo_ppo_loss_fwd_bwd(ocppo_stream_t stream, const float* logits,
+                                      const float* new_value, int64_t M, int64_t A,
+                                      const int64_t* mb_inds, const int64_t* b_actions,
+                                      const float* b_logprobs, const float* b_advantages,
+                                      const float* b_returns, const float* b_values,
+                                      const float* adv_stats, double clip_coef, double ent_coef,
+                                      double vf_coef, int norm_adv, int clip_vloss, float* dlogits,
+                                      float* dvalue, float* stats, void* workspace,
+                                      size_t workspace_bytes) {
+  OCPPO_REQUIRE(M > 0 && A > 0 && A <= kMaxActions && M <= (int64_t)INT32_MAX * kLossThreads,
+                "ocppo_ppo_loss_fwd_bwd: bad sizes M=%lld A=%lld (A <= %d)", (long long)M,
+                (long long)A, kMaxActions);
+  OCPPO_REQUIRE(logits && new_value && b_actions && b_logprobs && b_advantages && b_returns &&
+                    b_values && dlogits && dvalue && stats,
+                "ocppo_ppo_loss_fwd_bwd: null pointer");
+  if (!workspace || workspace_bytes < ocppo_ppo_loss_workspace_bytes(M, A))
+    return fail(OCPPO_E_WORKSPACE, "ocppo_ppo_loss_fwd_bwd: workspace needs %zu bytes, got %zu",
+                ocppo_ppo_loss_workspace_bytes(M, A), workspace_bytes);
+  hipStream_t s = as_stream(stream);
+  char* ws = static_cast<char*>(workspace);
+  if (norm_adv && !adv_stats) {
+    float* st = reinterpret_cast<float*>(ws + loss_stats_offset(M));
+    hipLaunchKernelGGL(adv_stats_kernel, dim3(1), dim3(256), 0, s, b_advantages, mb_inds, M, st);
+    if (int rc = check_launch("ocppo_ppo_loss_fwd_bwd/adv_stats")) return rc;
+    adv_stats = st;
+  }
+  LossParams P;
+  P.logits = logits;
+  P.new_value = new_value;
+  P.mb_inds = mb_inds;
+  P.b_actions = b_actions;
+  P.b_logprobs = b_logprobs;
+  P.b_adv = b_advantages;
+  P.b_ret = b_returns;
+  P.b_val = b_values;
+  P.adv_stats = adv_stats;
+  P.dlogits = dlogits;
+  P.dvalue = dvalue;
+  P.stats = stats;
+  P.ticket = reinterpret_cast<unsigned*>(ws);
+  P.partials = reinterpret_cast<float*>(ws + loss_partials_offset());
+  P.M = M;
+  P.A = static_cast<int>(A);
+  P.norm_adv = norm_adv ? 1 : 0;
+  P.clip_vloss = clip_vloss ? 1 : 0;
+  P.clip = static_cast<float>(clip_coef);
+  P.clip_lo = static_cast<float>(1.0 - clip_coef);
+  P.clip_hi = static_cast<float>(1.0 + clip_coef);
+  P.ent_coef = static_cast<float>(ent_coef);
+  P.vf_coef = static_cast<float>(vf_coef);
+  const float fm = static_cast<float>(M);
+  // autograd: mean() backward divides the upstream grad by numel; the upstream grads are
+  // d loss/d pg_loss = 1, d loss/d entropy_loss = -ent_coef, d loss/d v_loss_max.mean() = vf*0.5
+  P.g_pg = 1.0f / fm;
+  P.g_h = (-1.0f * P.ent_coef) / fm;
+  P.g_v = (P.vf_coef * 0.5f) / fm;
+  P.inv_m = 1.0f / fm;
+  const int64_t nb = ceil_div(M, kLossThreads);
+  const size_t lds = sizeof(float) * kLossThreads * A;
+  if (A <= 8)
+    hipLaunchKernelGGL(ppo_loss_kernel<8>, dim3(nb), dim3(kLossThreads), lds, s, P);
+  else
+    hipLaunchKernelGGL(ppo_loss_kernel<kMaxActions>, dim3(nb), dim3(kLossThreads), lds, s, P);
+  return check_launch("ocppo_ppo_loss_fwd_bwd");
+}
+
+extern "C" int ocppo_categorical_sample(ocppo_stream_t stream, const float* logits,
+                                        const float* noise, int64_t N, int64_t A,
+                                        int64_t* action_out, float* logprob_out,
+                                        float* entropy_out, const float* value_in,
+                                        float* value_out) {
+  OCPPO_REQUIRE(N >= 0 && A > 0 && A <= kMaxActions, "ocppo_categorical_sample: bad sizes");
+  if (N == 0) return OCPPO_OK;
+  OCPPO_REQUIRE(logits && noise && action_out && logprob_out,
+                "ocppo_categorical_sample: null pointer");
+  const dim3 grid(ceil_div(N, 256));
+  hipStream_t s = as_stream(stream);
+  if (A <= 8)
+    hipLaunchKernelGGL(categorical_sample_kernel<8>, grid, dim3(256), 0, s, logits, noise, N,
+                       (int)A, action_out, logprob_out, entropy_out, value_in, value_out);
+  else
+    hipLaunchKernelGGL(categorical_sample_kernel<kMaxActions>, grid, dim3(256), 0, s, logits,
+                       noise, N, (int)A, action_out, logprob_out, entropy_out, value_in, value_out);
+  return check_launch("ocppo_categorical_sample");
+}
+
+extern "C" int ocppo_categorical_logprob_entropy(ocppo_stream_t stream, const float* logits,
+                                                 const int64_t* actions, int64_t N, int64_t A,
+                                                 float* logprob_out, float* entropy_out) {
+  OCPPO_REQUIRE(N >= 0 && A > 0 && A <= kMaxActions,
+                "ocppo_categorical_logprob_entropy: bad sizes");
+  if (N == 0) return OCPPO_OK;
+  OCPPO_REQUIRE(logits && actions, "ocppo_categorical_logprob_entropy: null pointer");
+  const dim3 grid(ceil_div(N, 256));
+  hipStream_t s = as_stream(stream);
+  if (A <= 8)
+    hipLaunchKernelGGL(categorical_lp_ent_kernel<8>, grid, dim3(256), 0, s, logits, actions, N,
+                       (int)A, logprob_out, entropy_out);
+  else
+    hipLaunchKernelGGL(categorical_lp_ent_kernel<kMaxActions>, grid, dim3(256), 0, s, logits,
+                       actions, N, (int)A, logprob_out, entropy_out);
+  return check_launch("ocppo_categorical_logprob_entropy");
+}
+
+extern "C" int ocppo_categorical_logprob_entropy_bwd(ocppo_stream_t stream, const float* logits,
+                                                     const int64_t* actions,
+                                                     const float* grad_logprob,
+                                                     const float* grad_entropy, int64_t N,
+                                                     int64_t A, float* dlogits) {
+  OCPPO_REQUIRE(N >= 0 && A > 0 && A <= kMaxActions,
+                "ocppo_categorical_logprob_entropy_bwd: bad sizes");
+  if (N == 0) return OCPPO_OK;
+  OCPPO_REQUIRE(logits && actions && dlogits, "ocppo_categorical_logprob_entropy_bwd: null pointer");
+  const dim3 grid(ceil_div(N, 256));
+  hipStream_t s = as_stream(stream);
+  if (A <= 8)
+    hipLaunchKernelGGL(categorical_lp_ent_bwd_kernel<8>, grid, dim3(256), 0, s, logits, actions,
+                       grad_logprob, grad_entropy, N, (int)A, dlogits);
+  else
+    hipLaunchKernelGGL(categorical_lp_ent_bwd_kernel<kMaxActions>, grid, dim3(256), 0, s, logits,
+                       actions, grad_logprob, grad_entropy, N, (int)A, dlogits);
+  return check_launch("ocppo_categorical_logprob_entropy_bwd");
+}

@@ -1,0 +1,409 @@
+// Rollout-side kernels: the per-step store with device frame stacking (replaces
+// cleanrl/ppo_atari_oc.py:502-503 and :512-514), the minibatch obs gather (replaces
+// `b_obs[mb_inds]` at :566-567), VecNormalize reward normalisation (the SB3 wrapper of :414) and
+// the synthetic device env used by the benchmark and tests.
+//
+// All kernels are HBM streams: one 4-element group per thread, 8-16 B per lane per access,
+// consecutive lanes on consecutive addresses.
+#include "ocppo_common.h"
+
+namespace ocppo {
+
+// ---- vector element I/O: VEC elements of dtype DT as one aligned access -----------------------
+template <int DT, int VEC> struct VecIO {
+  // generic fallback (VEC == 1 or unaligned sizes)
+  __device__ static void load(const void* p, int64_t i, float (&v)[VEC]) {
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) v[k] = Elem<DT>::load(static_cast<const typename Elem<DT>::T*>(p), i + k);
+  }
+  __device__ static void store(void* p, int64_t i, const float (&v)[VEC]) {
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) Elem<DT>::store(static_cast<typename Elem<DT>::T*>(p), i + k, v[k]);
+  }
+};
+template <> struct VecIO<OCPPO_F32, 4> {
+  __device__ static void load(const void* p, int64_t i, float (&v)[4]) {
+    const float4 x = *reinterpret_cast<const float4*>(static_cast<const float*>(p) + i);
+    v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+  }
+  __device__ static void store(void* p, int64_t i, const float (&v)[4]) {
+    *reinterpret_cast<float4*>(static_cast<float*>(p) + i) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+};
+template <> struct VecIO<OCPPO_BF16, 4> {
+  __device__ static void load(const void* p, int64_t i, float (&v)[4]) {
+    const uint2 x = *reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(p) + i);
+    v[0] = __uint_as_float(x.x << 16); v[1] = __uint_as_float(x.x & 0xFFFF0000u);
+    v[2] = __uint_as_float(x.y << 16); v[3] = __uint_as_float(x.y & 0xFFFF0000u);
+  }
+  __device__ static void store(void* p, int64_t i, const float (&v)[4]) {
+    uint2 x;
+    x.x = static_cast<uint32_t>(f32_to_bf16(v[0])) | (static_cast<uint32_t>(f32_to_bf16(v[1])) << 16);
+    x.y = static_cast<uint32_t>(f32_to_bf16(v[2])) | (static_cast<uint32_t>(f32_to_bf16(v[3])) << 16);
+    *reinterpret_cast<uint2*>(static_cast<uint16_t*>(p) + i) = x;
+  }
+};
+template <> struct VecIO<OCPPO_U8, 4> {
+  __device__ static void load(const void* p, int64_t i, float (&v)[4]) {
+    const uint32_t x = *reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(p) + i);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = static_cast<float>((x >> (8 * k)) & 0xFFu);
+  }
+  __device__ static void store(void* p, int64_t i, const float (&v)[4]) {
+    uint32_t x = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float f = v[k] < 0.f ? 0.f : (v[k] > 255.f ? 255.f : v[k]);
+      x |= static_cast<uint32_t>(__float2int_rn(f)) << (8 * k);
+    }
+    *reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(p) + i) = x;
+  }
+};
+
+inline int grid_for(int64_t work, int block) {
+  int64_t g = ceil_div(work, block);
+  const int64_t cap = 256 * 16;  // 256 CUs x 16 blocks: grid-stride beyond that
+  return static_cast<int>(g < cap ? (g > 0 ? g : 1) : cap);
+}
+
+// ---- rollout store ----------------------------------------------------------------------------
+// obs_out[n, w, :] = done[n] || w == W-1 ? frame[n, :] : prev_obs[n, w+1, :]
+template <int FDT, int ODT, int VEC>
+__global__ __launch_bounds__(256) void rollout_store_kernel(
+    const void* __restrict__ frame, const float* __restrict__ reward,
+    const float* __restrict__ done, int64_t N, int W, int64_t D, const void* __restrict__ prev,
+    void* __restrict__ out, float* __restrict__ net, float* __restrict__ reward_out,
+    float* __restrict__ done_out) {
+  const int64_t DG = D / VEC;
+  const int64_t groups = N * W * DG;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t g = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; g < groups;
+       g += stride) {
+    const int64_t n = g / (W * DG);
+    const int64_t rem = g - n * W * DG;
+    const int w = static_cast<int>(rem / DG);
+    const int64_t k = (rem - static_cast<int64_t>(w) * DG) * VEC;
+    float v[VEC];
+    if (w == W - 1 || done[n] != 0.f)
+      VecIO<FDT, VEC>::load(frame, n * D + k, v);
+    else
+      VecIO<ODT, VEC>::load(prev, (n * W + w + 1) * D + k, v);
+    const int64_t o = (n * W + w) * D + k;
+    VecIO<ODT, VEC>::store(out, o, v);
+    if (net) {  // the network sees exactly what the rollout buffer holds
+      float back[VEC];
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) back[q] = Elem<ODT>::roundtrip(v[q]);
+      VecIO<OCPPO_F32, VEC>::store(net, o, back);
+    }
+    if (g < N) {
+      if (reward_out) reward_out[g] = reward[g];
+      if (done_out) done_out[g] = done[g];
+    }
+  }
+}
+
+template <int FDT, int ODT, int VEC>
+__global__ __launch_bounds__(256) void obs_reset_kernel(const void* __restrict__ frame, int64_t N,
+                                                        int W, int64_t D, void* __restrict__ out,
+                                                        float* __restrict__ net) {
+  const int64_t DG = D / VEC;
+  const int64_t groups = N * W * DG;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t g = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; g < groups;
+       g += stride) {
+    const int64_t n = g / (W * DG);
+    const int64_t rem = g - n * W * DG;
+    const int w = static_cast<int>(rem / DG);
+    const int64_t k = (rem - static_cast<int64_t>(w) * DG) * VEC;
+    float v[VEC];
+    VecIO<FDT, VEC>::load(frame, n * D + k, v);
+    const int64_t o = (n * W + w) * D + k;
+    VecIO<ODT, VEC>::store(out, o, v);
+    if (net) {
+      float back[VEC];
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) back[q] = Elem<ODT>::roundtrip(v[q]);
+      VecIO<OCPPO_F32, VEC>::store(net, o, back);
+    }
+  }
+}
+
+// ---- minibatch gather: dst[i, :] = f32(src[idx[i], :]) -------------------------------------------
+template <int SDT, int VEC>
+__global__ __launch_bounds__(256) void gather_rows_kernel(const void* __restrict__ src,
+                                                          const int64_t* __restrict__ idx,
+                                                          int64_t M, int64_t R,
+                                                          float* __restrict__ dst) {
+  const int64_t RG = R / VEC;
+  const int64_t groups = M * RG;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t g = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; g < groups;
+       g += stride) {
+    const int64_t i = g / RG;
+    const int64_t k = (g - i * RG) * VEC;
+    const int64_t row = idx[i];
+    float v[VEC];
+    VecIO<SDT, VEC>::load(src, row * R + k, v);
+    VecIO<OCPPO_F32, VEC>::store(dst, i * R + k, v);
+  }
+}
+
+// ---- VecNormalize(norm_obs=False, norm_reward=True) -----------------------------------------------
+// One workgroup (the reduction spans the env axis). f64 like SB3's numpy code.
+// `out` may alias `reward` (in-place normalisation of a rollout row): each element is read and
+// written by the same thread.
+__global__ __launch_bounds__(1024) void vecnorm_reward_kernel(
+    const float* reward, const float* __restrict__ done, int64_t N, double gamma, double eps,
+    double clip, double* __restrict__ ret, double* __restrict__ rms, float* out) {
+  __shared__ double scratch[16];
+  __shared__ double s_var;
+  double s = 0.0;
+  for (int64_t n = threadIdx.x; n < N; n += blockDim.x) {
+    const double r = ret[n] * gamma + static_cast<double>(reward[n]);
+    ret[n] = r;
+    s += r;
+  }
+  s = block_sum(s, scratch);
+  const double bmean = s / static_cast<double>(N);
+  double q = 0.0;
+  for (int64_t n = threadIdx.x; n < N; n += blockDim.x) {
+    const double d = ret[n] - bmean;
+    q += d * d;
+  }
+  q = block_sum(q, scratch);
+  if (threadIdx.x == 0) {
+    const double bvar = q / static_cast<double>(N);
+    const double bcount = static_cast<double>(N);
+    const double mean = rms[0], var = rms[1], count = rms[2];
+    // RunningMeanStd.update_from_moments (Chan et al. parallel merge)
+    const double delta = bmean - mean;
+    const double tot = count + bcount;
+    const double new_mean = mean + delta * bcount / tot;
+    const double m_a = var * count;
+    const double m_b = bvar * bcount;
+    const double m2 = m_a + m_b + delta * delta * count * bcount / (count + bcount);
+    const double new_var = m2 / (count + bcount);
+    rms[0] = new_mean;
+    rms[1] = new_var;
+    rms[2] = bcount + count;
+    s_var = new_var;
+  }
+  __syncthreads();
+  const double denom = sqrt(s_var + eps);
+  for (int64_t n = threadIdx.x; n < N; n += blockDim.x) {
+    double r = static_cast<double>(reward[n]) / denom;
+    r = r < -clip ? -clip : (r > clip ? clip : r);
+    out[n] = static_cast<float>(r);
+    if (done[n] != 0.f) ret[n] = 0.0;
+  }
+}
+
+// ---- synthetic env ------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+__device__ __forceinline__ float unit24(uint64_t h) {  // exact multiple of 2^-24 in [0, 1)
+  return static_cast<float>(h >> 40) * (1.0f / 16777216.0f);
+}
+
+template <bool PIXELS>
+__global__ __launch_bounds__(256) void synth_env_kernel(uint64_t seed,
+                                                        const int64_t* __restrict__ step_base,
+                                                        int64_t step_offset,
+                                                        const int64_t* __restrict__ actions,
+                                                        int64_t N, int64_t D, void* frame_out,
+                                                        float* __restrict__ reward_out,
+                                                        float* __restrict__ done_out,
+                                                        float* __restrict__ ep) {
+  const uint64_t step = static_cast<uint64_t>(step_base[0] + step_offset);
+  const int64_t total = N * D;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t g = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; g < total;
+       g += stride) {
+    const int64_t n = g / D;
+    const int64_t k = g - n * D;
+    const uint64_t key = splitmix64(splitmix64(splitmix64(seed) + step) + static_cast<uint64_t>(n));
+    const uint64_t h = splitmix64(key + static_cast<uint64_t>(k));
+    const int64_t a = actions ? actions[n] : 0;
+    if (PIXELS) {
+      uint32_t v = (h % 10u == 0u) ? static_cast<uint32_t>((h >> 8) & 0xFFu) : 0u;
+      if (k < 84) v = static_cast<uint32_t>((a * 37) & 0xFF);
+      static_cast<uint8_t*>(frame_out)[g] = static_cast<uint8_t>(v);
+    } else {
+      const int field = static_cast<int>(k & 3);
+      uint64_t v;
+      if (field == 0) v = h % 160u;
+      else if (field == 1) v = (k == 1) ? (h % 210u + 7u * static_cast<uint64_t>(a)) % 210u : h % 210u;
+      else v = 1u + h % 16u;
+      static_cast<float*>(frame_out)[g] = static_cast<float>(v);
+    }
+    if (k == 0) {
+      const float ur = unit24(splitmix64(key ^ 0x5DEECE66Dull));
+      const float r = ur < 0.005f ? 1.f : (ur < 0.01f ? -1.f : 0.f);
+      const float ud = unit24(splitmix64(key ^ 0xB5297A4Dull));
+      const float d = ud < (1.0f / 3500.0f) ? 1.f : 0.f;
+      reward_out[n] = r;
+      done_out[n] = d;
+      if (ep) {
+        float* e = ep + n * 5;
+        const float run_ret = e[0] + r, run_len = e[1] + 1.f;
+        if (d != 0.f) {
+          e[2] += run_ret;
+          e[3] += run_len;
+          e[4] += 1.f;
+          e[0] = 0.f;
+          e[1] = 0.f;
+        } else {
+          e[0] = run_ret;
+          e[1] = run_len;
+        }
+      }
+    }
+  }
+}
+
+template <int FDT, int ODT>
+int launch_store(hipStream_t s, const void* frame, const float* reward, const float* done,
+                 int64_t N, int64_t W, int64_t D, const void* prev, void* out, float* net,
+                 float* rout, float* dout) {
+  if (D % 4 == 0) {
+    const int64_t groups = N * W * (D / 4);
+    hipLaunchKernelGGL((rollout_store_kernel<FDT, ODT, 4>), dim3(grid_for(groups, 256)), dim3(256),
+                       0, s, frame, reward, done, N, (int)W, D, prev, out, net, rout, dout);
+  } else {
+    const int64_t groups = N * W * D;
+    hipLaunchKernelGGL((rollout_store_kernel<FDT, ODT, 1>), dim3(grid_for(groups, 256)), dim3(256),
+                       0, s, frame, reward, done, N, (int)W, D, prev, out, net, rout, dout);
+  }
+  return check_launch("ocppo_rollout_store");
+}
+
+template <int FDT, int ODT>
+int launch_reset(hipStream_t s, const void* frame, int64_t N, int64_t W, int64_t D, void* out,
+                 float* net) {
+  if (D % 4 == 0) {
+    const int64_t groups = N * W * (D / 4);
+    hipLaunchKernelGGL((obs_reset_kernel<FDT, ODT, 4>), dim3(grid_for(groups, 256)), dim3(256), 0,
+                       s, frame, N, (int)W, D, out, net);
+  } else {
+    const int64_t groups = N * W * D;
+    hipLaunchKernelGGL((obs_reset_kernel<FDT, ODT, 1>), dim3(grid_for(groups, 256)), dim3(256), 0,
+                       s, frame, N, (int)W, D, out, net);
+  }
+  return check_launch("ocppo_obs_reset");
+}
+
+template <int SDT>
+int launch_gather(hipStream_t s, const void* src, const int64_t* idx, int64_t M, int64_t R,
+                  float* dst) {
+  if (R % 4 == 0) {
+    const int64_t groups = M * (R / 4);
+    hipLaunchKernelGGL((gather_rows_kernel<SDT, 4>), dim3(grid_for(groups, 256)), dim3(256), 0, s,
+                       src, idx, M, R, dst);
+  } else {
+    const int64_t groups = M * R;
+    hipLaunchKernelGGL((gather_rows_kernel<SDT, 1>), dim3(grid_for(groups, 256)), dim3(256), 0, s,
+                       src, idx, M, R, dst);
+  }
+  return check_launch("ocppo_gather_rows");
+}
+
+static bool valid_dtype(int dt) { return dt == OCPPO_F32 || dt == OCPPO_BF16 || dt == OCPPO_U8; }
+
+}  // namespace ocppo
+
+using namespace ocppo;
+
+extern "C" int ocppo_rollout_store(ocppo_stream_t stream, const void* frame, int frame_dtype,
+                                   const float* reward, const float* done, int64_t N, int64_t W,
+                                   int64_t D, const void* prev_obs, void* obs_out, int obs_dtype,
+                                   float* net_obs, float* reward_out, float* done_out) {
+  OCPPO_REQUIRE(N >= 0 && W >= 1 && D >= 1 && W <= 64, "ocppo_rollout_store: bad sizes");
+  OCPPO_REQUIRE(frame_dtype == OCPPO_F32 || frame_dtype == OCPPO_U8,
+                "ocppo_rollout_store: frame dtype must be OCPPO_F32 or OCPPO_U8");
+  OCPPO_REQUIRE(valid_dtype(obs_dtype), "ocppo_rollout_store: bad obs dtype %d", obs_dtype);
+  if (N == 0) return OCPPO_OK;
+  OCPPO_REQUIRE(frame && reward && done && prev_obs && obs_out, "ocppo_rollout_store: null pointer");
+  OCPPO_REQUIRE(prev_obs != obs_out, "ocppo_rollout_store: prev_obs must not alias obs_out");
+  hipStream_t s = as_stream(stream);
+#define OCPPO_STORE(F, O)                                                                  \
+  if (frame_dtype == F && obs_dtype == O)                                                  \
+    return launch_store<F, O>(s, frame, reward, done, N, W, D, prev_obs, obs_out, net_obs, \
+                              reward_out, done_out);
+  OCPPO_STORE(OCPPO_F32, OCPPO_F32)
+  OCPPO_STORE(OCPPO_F32, OCPPO_BF16)
+  OCPPO_STORE(OCPPO_F32, OCPPO_U8)
+  OCPPO_STORE(OCPPO_U8, OCPPO_F32)
+  OCPPO_STORE(OCPPO_U8, OCPPO_BF16)
+  OCPPO_STORE(OCPPO_U8, OCPPO_U8)
+#undef OCPPO_STORE
+  return fail(OCPPO_E_INVALID, "ocppo_rollout_store: unsupported dtype pair");
+}
+
+extern "C" int ocppo_obs_reset(ocppo_stream_t stream, const void* frame, int frame_dtype, int64_t N,
+                               int64_t W, int64_t D, void* obs_out, int obs_dtype, float* net_obs) {
+  OCPPO_REQUIRE(N >= 0 && W >= 1 && D >= 1 && W <= 64, "ocppo_obs_reset: bad sizes");
+  OCPPO_REQUIRE(frame_dtype == OCPPO_F32 || frame_dtype == OCPPO_U8,
+                "ocppo_obs_reset: frame dtype must be OCPPO_F32 or OCPPO_U8");
+  OCPPO_REQUIRE(valid_dtype(obs_dtype), "ocppo_obs_reset: bad obs dtype %d", obs_dtype);
+  if (N == 0) return OCPPO_OK;
+  OCPPO_REQUIRE(frame && obs_out, "ocppo_obs_reset: null pointer");
+  hipStream_t s = as_stream(stream);
+#define OCPPO_RESET(F, O) \
+  if (frame_dtype == F && obs_dtype == O) return launch_reset<F, O>(s, frame, N, W, D, obs_out, net_obs);
+  OCPPO_RESET(OCPPO_F32, OCPPO_F32)
+  OCPPO_RESET(OCPPO_F32, OCPPO_BF16)
+  OCPPO_RESET(OCPPO_F32, OCPPO_U8)
+  OCPPO_RESET(OCPPO_U8, OCPPO_F32)
+  OCPPO_RESET(OCPPO_U8, OCPPO_BF16)
+  OCPPO_RESET(OCPPO_U8, OCPPO_U8)
+#undef OCPPO_RESET
+  return fail(OCPPO_E_INVALID, "ocppo_obs_reset: unsupported dtype pair");
+}
+
+extern "C" int ocppo_gather_rows(ocppo_stream_t stream, const void* src, int src_dtype,
+                                 const int64_t* idx, int64_t M, int64_t R, float* dst) {
+  OCPPO_REQUIRE(M >= 0 && R >= 1, "ocppo_gather_rows: bad sizes");
+  OCPPO_REQUIRE(valid_dtype(src_dtype), "ocppo_gather_rows: bad dtype %d", src_dtype);
+  if (M == 0) return OCPPO_OK;
+  OCPPO_REQUIRE(src && idx && dst, "ocppo_gather_rows: null pointer");
+  hipStream_t s = as_stream(stream);
+  if (src_dtype == OCPPO_F32) return launch_gather<OCPPO_F32>(s, src, idx, M, R, dst);
+  if (src_dtype == OCPPO_BF16) return launch_gather<OCPPO_BF16>(s, src, idx, M, R, dst);
+  return launch_gather<OCPPO_U8>(s, src, idx, M, R, dst);
+}
+
+extern "C" int ocppo_vecnorm_reward(ocppo_stream_t stream, const float* reward, const float* done,
+                                    int64_t N, double gamma, double epsilon, double clip_reward,
+                                    double* ret_state, double* rms_state, float* reward_out) {
+  OCPPO_REQUIRE(N >= 1, "ocppo_vecnorm_reward: bad size N=%lld", (long long)N);
+  OCPPO_REQUIRE(reward && done && ret_state && rms_state && reward_out,
+                "ocppo_vecnorm_reward: null pointer");
+  hipLaunchKernelGGL(vecnorm_reward_kernel, dim3(1), dim3(1024), 0, as_stream(stream), reward, done,
+                     N, gamma, epsilon, clip_reward, ret_state, rms_state, reward_out);
+  return check_launch("ocppo_vecnorm_reward");
+}
+
+extern "C" int ocppo_synth_env_step(ocppo_stream_t stream, uint64_t seed, const int64_t* step_base,
+                                    int64_t step_offset, const int64_t* actions, int64_t N,
+                                    int64_t D, int pixel_mode, void* frame_out, float* reward_out,
+                                    float* done_out, float* ep_state) {
+  OCPPO_REQUIRE(N >= 0 && D >= 1, "ocppo_synth_env_step: bad sizes");
+  if (N == 0) return OCPPO_OK;
+  OCPPO_REQUIRE(step_base && frame_out && reward_out && done_out,
+                "ocppo_synth_env_step: null pointer");
+  const dim3 grid(grid_for(N * D, 256));
+  if (pixel_mode)
+    hipLaunchKernelGGL(synth_env_kernel<true>, grid, dim3(256), 0, as_stream(stream), seed,
+                       step_base, step_offset, actions, N, D, frame_out, reward_out, done_out,
+                       ep_state);
+  else
+    hipLaunchKernelGGL(synth_env_kernel<false>, grid, dim3(256), 0, as_stream(stream), seed,
+                       step_base, step_offset, actions, N, D, frame_out, reward_out, done_out,
+                       ep_state);
+  return check_launch("ocppo_synth_env_step");
+}

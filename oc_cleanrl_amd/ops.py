@@ -1,0 +1,320 @@
+"""torch-facing wrappers of the HIP kernels (libocppo_hip.so).
+
+Every function takes CUDA (HIP) tensors, validates shapes/dtypes/devices on the host before any
+launch, and launches on the current torch stream of the tensors' device, so everything here is
+asynchronous and capturable into a torch.cuda.CUDAGraph (hipGraph). There is no CPU fallback: a
+CPU tensor is an error.
+
+Reference lines replaced are cited per function (paths relative to the reference checkout).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from ._lib import OCPPO_BF16, OCPPO_F32, OCPPO_U8, STAT_NAMES, call
+
+_DTYPE_CODE = {torch.float32: OCPPO_F32, torch.bfloat16: OCPPO_BF16, torch.uint8: OCPPO_U8}
+
+
+def _check(t: torch.Tensor, name: str, dtype: torch.dtype | None = None, device=None,
+           numel: int | None = None) -> int:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name}: expected a tensor, got {type(t).__name__}")
+    if t.device.type != "cuda":
+        raise ValueError(f"{name}: HIP kernels need a GPU tensor, got device {t.device}")
+    if device is not None and t.device != device:
+        raise ValueError(f"{name}: on {t.device}, expected {device}")
+    if dtype is not None and t.dtype != dtype:
+        raise ValueError(f"{name}: dtype {t.dtype}, expected {dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: must be contiguous")
+    if numel is not None and t.numel() != numel:
+        raise ValueError(f"{name}: has {t.numel()} elements, expected {numel}")
+    return t.data_ptr()
+
+
+def _opt(t, *a, **k) -> int | None:
+    return None if t is None else _check(t, *a, **k)
+
+
+def _stream(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+# ---------------------------------------------------------------------------------------------
+# GAE (ppo_atari_oc.py:533-547)
+# ---------------------------------------------------------------------------------------------
+def gae(rewards, values, dones, next_value, next_done, gamma: float, gae_lambda: float,
+        advantages=None, returns=None):
+    """Advantages and returns of one rollout; [T, N] f32 in, ([T, N], [T, N]) out.
+
+    Bit-identical to the reference loop. `next_value` may be [N] or [1, N] (as produced by
+    `agent.get_value(next_obs).reshape(1, -1)`).
+    """
+    if rewards.dim() != 2:
+        raise ValueError(f"rewards must be [T, N], got {tuple(rewards.shape)}")
+    T, N = rewards.shape
+    dev = rewards.device
+    f = torch.float32
+    if advantages is None:
+        advantages = torch.empty_like(rewards)
+    if returns is None:
+        returns = torch.empty_like(rewards)
+    call("ocppo_gae", _stream(dev), _check(rewards, "rewards", f, dev),
+         _check(values, "values", f, dev, T * N), _check(dones, "dones", f, dev, T * N),
+         _check(next_value, "next_value", f, dev, N), _check(next_done, "next_done", f, dev, N),
+         T, N, float(gamma), float(gae_lambda), _check(advantages, "advantages", f, dev, T * N),
+         _check(returns, "returns", f, dev, T * N))
+    return advantages, returns
+
+
+# ---------------------------------------------------------------------------------------------
+# minibatch advantage statistics (ppo_atari_oc.py:577-579)
+# ---------------------------------------------------------------------------------------------
+def minibatch_adv_stats(b_advantages, perm, minibatch_size: int, out=None):
+    """(mean, unbiased std) of b_advantages over each minibatch of `perm` → [num_mb, 2]."""
+    dev = b_advantages.device
+    if perm.numel() % minibatch_size:
+        raise ValueError("perm length must be a multiple of minibatch_size")
+    num_mb = perm.numel() // minibatch_size
+    if out is None:
+        out = torch.empty((num_mb, 2), dtype=torch.float32, device=dev)
+    call("ocppo_minibatch_adv_stats", _stream(dev),
+         _check(b_advantages, "b_advantages", torch.float32, dev),
+         _check(perm, "perm", torch.int64, dev), minibatch_size, num_mb,
+         _check(out, "out", torch.float32, dev, 2 * num_mb))
+    return out
+
+
+# ---------------------------------------------------------------------------------------------
+# fused PPO loss (ppo_atari_oc.py:566-602 from the network outputs on)
+# ---------------------------------------------------------------------------------------------
+class LossWorkspace:
+    """Device scratch for ppo_loss_fwd_bwd (zeroed once; the kernel re-arms its ticket)."""
+
+    def __init__(self, M: int, A: int, device):
+        n = _lib.LIB.ocppo_ppo_loss_workspace_bytes(M, A)
+        self.nbytes = int(n)
+        self.buf = torch.zeros(self.nbytes, dtype=torch.uint8, device=device)
+        self.M, self.A = M, A
+
+
+def ppo_loss_fwd_bwd(logits, new_value, b_actions, b_logprobs, b_advantages, b_returns, b_values,
+                     *, mb_inds=None, adv_stats=None, clip_coef: float, ent_coef: float,
+                     vf_coef: float, norm_adv: bool, clip_vloss: bool, dlogits=None, dvalue=None,
+                     stats=None, workspace: LossWorkspace | None = None):
+    """One launch: loss statistics [9] plus dLoss/dlogits [M, A] and dLoss/dvalue [M].
+
+    `b_*` are the flattened batch arrays (b_actions int64); `mb_inds` selects the minibatch
+    (None = the b_* arrays are already the minibatch). Returns (stats, dlogits, dvalue); stats
+    layout = _lib.STAT_NAMES.
+    """
+    if logits.dim() != 2:
+        raise ValueError(f"logits must be [M, A], got {tuple(logits.shape)}")
+    M, A = logits.shape
+    dev = logits.device
+    f = torch.float32
+    B = b_logprobs.numel()
+    if mb_inds is None and B != M:
+        raise ValueError("without mb_inds the batch arrays must have M elements")
+    if mb_inds is not None and mb_inds.numel() != M:
+        raise ValueError(f"mb_inds has {mb_inds.numel()} elements, logits has M={M} rows")
+    if dlogits is None:
+        dlogits = torch.empty_like(logits)
+    if dvalue is None:
+        dvalue = torch.empty(M, dtype=f, device=dev)
+    if stats is None:
+        stats = torch.empty(len(STAT_NAMES), dtype=f, device=dev)
+    if workspace is None:
+        workspace = LossWorkspace(M, A, dev)
+    call("ocppo_ppo_loss_fwd_bwd", _stream(dev), _check(logits, "logits", f, dev),
+         _check(new_value, "new_value", f, dev, M), M, A,
+         _opt(mb_inds, "mb_inds", torch.int64, dev, M),
+         _check(b_actions, "b_actions", torch.int64, dev, B),
+         _check(b_logprobs, "b_logprobs", f, dev, B),
+         _check(b_advantages, "b_advantages", f, dev, B), _check(b_returns, "b_returns", f, dev, B),
+         _check(b_values, "b_values", f, dev, B),
+         _opt(adv_stats, "adv_stats", f, dev, 2) if norm_adv else None,
+         float(clip_coef), float(ent_coef), float(vf_coef), int(bool(norm_adv)),
+         int(bool(clip_vloss)), _check(dlogits, "dlogits", f, dev, M * A),
+         _check(dvalue, "dvalue", f, dev, M), _check(stats, "stats", f, dev, len(STAT_NAMES)),
+         workspace.buf.data_ptr(), workspace.nbytes)
+    return stats, dlogits, dvalue
+
+
+class _PPOLoss(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, new_value, b_actions, b_logprobs, b_advantages, b_returns, b_values,
+                mb_inds, adv_stats, cfg):
+        stats, dlogits, dvalue = ppo_loss_fwd_bwd(
+            logits.detach().contiguous(), new_value.detach().reshape(-1).contiguous(), b_actions,
+            b_logprobs, b_advantages, b_returns, b_values, mb_inds=mb_inds, adv_stats=adv_stats,
+            **cfg)
+        ctx.save_for_backward(dlogits, dvalue)
+        ctx.value_shape = new_value.shape
+        ctx.mark_non_differentiable(stats)
+        loss = stats[0].clone()
+        return loss, stats
+
+    @staticmethod
+    def backward(ctx, grad_loss, grad_stats):
+        dlogits, dvalue = ctx.saved_tensors
+        return (dlogits * grad_loss, (dvalue * grad_loss).view(ctx.value_shape), None, None, None,
+                None, None, None, None, None)
+
+
+def ppo_loss(logits, new_value, b_actions, b_logprobs, b_advantages, b_returns, b_values,
+             mb_inds=None, adv_stats=None, *, clip_coef, ent_coef, vf_coef, norm_adv=True,
+             clip_vloss=True):
+    """Differentiable fused PPO loss: returns (loss, stats). Only `loss` carries gradient."""
+    cfg = dict(clip_coef=clip_coef, ent_coef=ent_coef, vf_coef=vf_coef, norm_adv=norm_adv,
+               clip_vloss=clip_vloss)
+    return _PPOLoss.apply(logits, new_value, b_actions, b_logprobs, b_advantages, b_returns,
+                          b_values, mb_inds, adv_stats, cfg)
+
+
+# ---------------------------------------------------------------------------------------------
+# Categorical action head (architectures/ppo.py:89-95)
+# ---------------------------------------------------------------------------------------------
+def categorical_sample(logits, noise, action_out=None, logprob_out=None, entropy_out=None,
+                       value_in=None, value_out=None):
+    """argmax(softmax(logits) / noise) with log_prob and entropy; noise ~ Exp(1) [N, A]."""
+    N, A = logits.shape
+    dev = logits.device
+    f = torch.float32
+    if action_out is None:
+        action_out = torch.empty(N, dtype=torch.int64, device=dev)
+    if logprob_out is None:
+        logprob_out = torch.empty(N, dtype=f, device=dev)
+    if (value_in is None) != (value_out is None):
+        raise ValueError("value_in and value_out go together")
+    call("ocppo_categorical_sample", _stream(dev), _check(logits, "logits", f, dev),
+         _check(noise, "noise", f, dev, N * A), N, A,
+         _check(action_out, "action_out", torch.int64, dev, N),
+         _check(logprob_out, "logprob_out", f, dev, N), _opt(entropy_out, "entropy_out", f, dev, N),
+         _opt(value_in, "value_in", f, dev, N), _opt(value_out, "value_out", f, dev, N))
+    return action_out, logprob_out, entropy_out
+
+
+class _CategoricalLogProbEntropy(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, actions):
+        N, A = logits.shape
+        dev = logits.device
+        lp = torch.empty(N, dtype=torch.float32, device=dev)
+        ent = torch.empty(N, dtype=torch.float32, device=dev)
+        lg = logits.detach().contiguous()
+        act = actions.detach().reshape(-1).long().contiguous()
+        call("ocppo_categorical_logprob_entropy", _stream(dev),
+             _check(lg, "logits", torch.float32, dev), _check(act, "actions", torch.int64, dev, N),
+             N, A, lp.data_ptr(), ent.data_ptr())
+        ctx.save_for_backward(lg, act)
+        return lp, ent
+
+    @staticmethod
+    def backward(ctx, g_lp, g_ent):
+        lg, act = ctx.saved_tensors
+        N, A = lg.shape
+        dev = lg.device
+        dl = torch.empty_like(lg)
+        g_lp = None if g_lp is None else g_lp.contiguous()
+        g_ent = None if g_ent is None else g_ent.contiguous()
+        call("ocppo_categorical_logprob_entropy_bwd", _stream(dev), lg.data_ptr(), act.data_ptr(),
+             _opt(g_lp, "grad_logprob", torch.float32, dev, N),
+             _opt(g_ent, "grad_entropy", torch.float32, dev, N), N, A, dl.data_ptr())
+        return dl, None
+
+
+def categorical_logprob_entropy(logits, actions):
+    """(log_prob(actions), entropy()) of Categorical(logits=logits), differentiable in logits."""
+    return _CategoricalLogProbEntropy.apply(logits, actions)
+
+
+# ---------------------------------------------------------------------------------------------
+# rollout store / reset (ppo_atari_oc.py:502-503, 512-514), minibatch gather (:566-567)
+# ---------------------------------------------------------------------------------------------
+def rollout_store(frame, reward, done, prev_obs, obs_out, net_obs=None, reward_out=None,
+                  done_out=None):
+    """obs_out = stack(prev_obs[:, 1:], frame) (reset-filled where done), plus reward/done rows.
+
+    frame [N, D] f32|u8; prev_obs/obs_out [N, W, D] f32|bf16|u8; net_obs [N, W, D] f32.
+    """
+    N, D = frame.shape[0], frame[0].numel()
+    W = obs_out.shape[1]
+    dev = frame.device
+    if tuple(obs_out.shape[:2]) != (N, W) or obs_out[0, 0].numel() != D:
+        raise ValueError(f"obs_out {tuple(obs_out.shape)} does not match frame {tuple(frame.shape)}")
+    if prev_obs.shape != obs_out.shape or prev_obs.dtype != obs_out.dtype:
+        raise ValueError("prev_obs and obs_out must have the same shape and dtype")
+    if frame.dtype not in (torch.float32, torch.uint8) or obs_out.dtype not in _DTYPE_CODE:
+        raise ValueError(f"unsupported dtypes frame={frame.dtype} obs={obs_out.dtype}")
+    f = torch.float32
+    call("ocppo_rollout_store", _stream(dev), _check(frame, "frame", None, dev),
+         _DTYPE_CODE[frame.dtype], _check(reward, "reward", f, dev, N),
+         _check(done, "done", f, dev, N), N, W, D, _check(prev_obs, "prev_obs", None, dev),
+         _check(obs_out, "obs_out", None, dev), _DTYPE_CODE[obs_out.dtype],
+         _opt(net_obs, "net_obs", f, dev, N * W * D), _opt(reward_out, "reward_out", f, dev, N),
+         _opt(done_out, "done_out", f, dev, N))
+
+
+def obs_reset(frame, obs_out, net_obs=None):
+    N, D = frame.shape[0], frame[0].numel()
+    W = obs_out.shape[1]
+    dev = frame.device
+    if obs_out.numel() != N * W * D:
+        raise ValueError("obs_out does not match frame")
+    call("ocppo_obs_reset", _stream(dev), _check(frame, "frame", None, dev),
+         _DTYPE_CODE[frame.dtype], N, W, D, _check(obs_out, "obs_out", None, dev),
+         _DTYPE_CODE[obs_out.dtype], _opt(net_obs, "net_obs", torch.float32, dev, N * W * D))
+
+
+def gather_rows(src, idx, out=None):
+    """out[i] = float32(src[idx[i]]) for src [B, ...] f32|bf16|u8 → out [M, ...] f32."""
+    dev = src.device
+    M = idx.numel()
+    R = src[0].numel() if src.shape[0] else 0
+    if out is None:
+        out = torch.empty((M,) + tuple(src.shape[1:]), dtype=torch.float32, device=dev)
+    if src.dtype not in _DTYPE_CODE:
+        raise ValueError(f"unsupported src dtype {src.dtype}")
+    call("ocppo_gather_rows", _stream(dev), _check(src, "src", None, dev), _DTYPE_CODE[src.dtype],
+         _check(idx, "idx", torch.int64, dev, M), M, R,
+         _check(out, "out", torch.float32, dev, M * R))
+    return out
+
+
+# ---------------------------------------------------------------------------------------------
+# VecNormalize reward normalisation (ppo_atari_oc.py:414, SB3 2.0.0 semantics)
+# ---------------------------------------------------------------------------------------------
+def vecnorm_reward(reward, done, ret_state, rms_state, reward_out, gamma=0.99, epsilon=1e-8,
+                   clip_reward=10.0):
+    N = reward.numel()
+    dev = reward.device
+    f = torch.float32
+    call("ocppo_vecnorm_reward", _stream(dev), _check(reward, "reward", f, dev),
+         _check(done, "done", f, dev, N), N, float(gamma), float(epsilon), float(clip_reward),
+         _check(ret_state, "ret_state", torch.float64, dev, N),
+         _check(rms_state, "rms_state", torch.float64, dev, 3),
+         _check(reward_out, "reward_out", f, dev, N))
+    return reward_out
+
+
+# ---------------------------------------------------------------------------------------------
+# synthetic env (harness)
+# ---------------------------------------------------------------------------------------------
+def synth_env_step(seed: int, step_base, step_offset: int, actions, frame_out, reward_out,
+                   done_out, ep_state=None):
+    N = reward_out.numel()
+    D = frame_out[0].numel()
+    dev = frame_out.device
+    pixel = frame_out.dtype == torch.uint8
+    if not pixel and frame_out.dtype != torch.float32:
+        raise ValueError("frame_out must be f32 (objects) or u8 (pixels)")
+    call("ocppo_synth_env_step", _stream(dev), seed & 0xFFFFFFFFFFFFFFFF,
+         _check(step_base, "step_base", torch.int64, dev, 1), int(step_offset),
+         _opt(actions, "actions", torch.int64, dev, N), N, D, int(pixel),
+         _check(frame_out, "frame_out", None, dev, N * D),
+         _check(reward_out, "reward_out", torch.float32, dev, N),
+         _check(done_out, "done_out", torch.float32, dev, N),
+         _opt(ep_state, "ep_state", torch.float32, dev, N * 5))

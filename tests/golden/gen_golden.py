@@ -1,0 +1,243 @@
+"""Generate the golden fixtures under tests/golden/ FROM THE REFERENCE ITSELF.
+
+Runs only in the build container, where the reference checkout is mounted read-only at
+/root/reference (it never travels to the GPU box; only the .npz/.json outputs are committed).
+
+What is executed (nothing is copied into this repo):
+  * cleanrl/architectures/ppo.py is imported as a module (PPObj, PPODefault: pure torch);
+  * the GAE block cleanrl/ppo_atari_oc.py:533-547 and the minibatch-update block :566-610 are read
+    as text by line range, dedented, compiled and exec'd against seeded torch CPU tensors with a
+    real PPObj agent (the scripts themselves cannot be imported: tyro, gymnasium, SB3, ocatari
+    are not installed).
+
+Fixtures:
+  gae_{T}x{N}.npz     inputs + advantages/returns of the reference loop
+  loss_{name}.npz     minibatch inputs, the actor/critic outputs (logits, value) and their
+                      autograd grads, and the loss scalars, from the reference update block
+  sample_{name}.npz   logits, the Exp(1) noise torch draws, and Categorical.sample()/log_prob/
+                      entropy from PPObj.get_action_and_value under a fixed seed
+  ppobj_small.npz     a small PPObj's state_dict + input + reference outputs
+  init_{name}.json    per-parameter checksums of seeded default-size agents + outputs on a fixed
+                      input (pins layer order, state-dict keys and orthogonal init order)
+
+    python tests/golden/gen_golden.py
+"""
+from __future__ import annotations
+
+import json
+import sys
+import textwrap
+import types
+from pathlib import Path
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.optim as optim
+
+REF = Path("/root/reference")
+OUT = Path(__file__).resolve().parent
+SCRIPT = REF / "cleanrl" / "ppo_atari_oc.py"
+GAE_LINES = (533, 547)
+UPDATE_LINES = (566, 610)
+
+sys.dont_write_bytecode = True
+sys.path.insert(0, str(REF / "cleanrl"))
+from architectures.ppo import PPODefault, PPObj  # noqa: E402  (the reference's own modules)
+
+
+def block(lines):
+    src = SCRIPT.read_text().splitlines()[lines[0] - 1:lines[1]]
+    return compile(textwrap.dedent("\n".join(src)), f"{SCRIPT}:{lines[0]}-{lines[1]}", "exec")
+
+
+GAE_CODE = block(GAE_LINES)
+UPDATE_CODE = block(UPDATE_LINES)
+
+
+class Space:
+    def __init__(self, shape=None, n=None):
+        self.shape = shape
+        self.n = n
+
+
+class Envs:
+    def __init__(self, obs_shape, n_actions):
+        self.observation_space = Space(shape=obs_shape)
+        self.action_space = Space(shape=(), n=n_actions)
+
+
+# ---------------------------------------------------------------------------------------------
+def gen_gae(T, N, kind, seed):
+    rng = np.random.default_rng(seed)
+    if kind == "jaxtest":  # the distributions of tests/test_jax_compute_gae.py:76-87
+        dones = rng.integers(0, 2, (T, N)).astype(np.float32)
+        values = rng.random((T, N), dtype=np.float32)
+        rewards = rng.uniform(-1, 1, (T, N)).astype(np.float32)
+        next_value = rng.random(N, dtype=np.float32)
+        next_done = rng.integers(0, 2, N).astype(np.float32)
+    else:  # synthetic Pong-like rollout
+        u = rng.random((T, N))
+        rewards = np.where(u < 0.005, 1.0, np.where(u < 0.01, -1.0, 0.0)).astype(np.float32)
+        rewards = rewards + (rng.standard_normal((T, N)) * 0.05).astype(np.float32)
+        dones = (rng.random((T, N)) < 0.02).astype(np.float32)
+        values = (rng.standard_normal((T, N)) * 3).astype(np.float32)
+        next_value = (rng.standard_normal(N) * 3).astype(np.float32)
+        next_done = (rng.random(N) < 0.02).astype(np.float32)
+    nv_t = torch.from_numpy(next_value)
+    agent = types.SimpleNamespace(get_value=lambda x: nv_t.reshape(N, 1))
+    args = types.SimpleNamespace(num_steps=T, gamma=0.99, gae_lambda=0.95)
+    ns = dict(torch=torch, agent=agent, args=args, device="cpu", next_obs=None,
+              rewards=torch.from_numpy(rewards), values=torch.from_numpy(values),
+              dones=torch.from_numpy(dones), next_done=torch.from_numpy(next_done))
+    exec(GAE_CODE, ns)
+    np.savez_compressed(OUT / f"gae_{T}x{N}.npz", rewards=rewards, values=values, dones=dones,
+                        next_value=next_value, next_done=next_done, gamma=0.99, gae_lambda=0.95,
+                        advantages=ns["advantages"].numpy(), returns=ns["returns"].numpy())
+
+
+# ---------------------------------------------------------------------------------------------
+def gen_loss(name, *, norm_adv, clip_vloss, B=1024, M=256, F=6, A=6, seed=0, clip_coef=0.1,
+             ties=False):
+    torch.manual_seed(seed)
+    rng = np.random.default_rng(seed)
+    agent = PPObj(Envs((4, F), A), "cpu", (32, 64), (32,))
+    b_obs = torch.from_numpy(rng.integers(0, 160, (B, 4, F)).astype(np.float32))
+    with torch.no_grad():
+        hid = agent.network(b_obs)
+        lg = agent.actor(hid)
+        val = agent.critic(hid).view(-1)
+        dist = torch.distributions.Categorical(logits=lg)
+        b_actions = dist.sample()
+        lp = dist.log_prob(b_actions)
+    spread = torch.from_numpy((rng.standard_normal(B) * 0.15).astype(np.float32))
+    b_logprobs = lp + spread
+    if ties:  # ratio == 1 exactly for a quarter of the batch: every max() ties there
+        b_logprobs[: B // 4] = lp[: B // 4]
+    b_values = val + torch.from_numpy((rng.standard_normal(B) * 0.3).astype(np.float32))
+    b_returns = val + torch.from_numpy((rng.standard_normal(B) * 1.0).astype(np.float32))
+    b_advantages = torch.from_numpy((rng.standard_normal(B) * 2.0).astype(np.float32))
+    mb_inds = rng.permutation(B)[:M]
+
+    captured = {}
+
+    def grab(key):
+        def hook(mod, inp, out):
+            out.retain_grad()
+            captured[key] = out
+        return hook
+
+    h1 = agent.actor.register_forward_hook(grab("logits"))
+    h2 = agent.critic.register_forward_hook(grab("value"))
+    args = types.SimpleNamespace(clip_coef=clip_coef, norm_adv=norm_adv, clip_vloss=clip_vloss,
+                                 ent_coef=0.01, vf_coef=0.5, max_grad_norm=0.5, track=False,
+                                 minibatch_size=M)
+    optimizer = optim.Adam(agent.parameters(), lr=2.5e-4, eps=1e-5)
+    ns = dict(torch=torch, nn=nn, np=np, agent=agent, args=args, optimizer=optimizer,
+              b_obs=b_obs, b_actions=b_actions, b_logprobs=b_logprobs,
+              b_advantages=b_advantages, b_returns=b_returns, b_values=b_values,
+              mb_inds=mb_inds, clipfracs=[], start=0)
+    exec(UPDATE_CODE, ns)
+    h1.remove()
+    h2.remove()
+    mba = b_advantages[mb_inds]
+    stats = np.array([ns["loss"].item(), ns["pg_loss"].item(), ns["v_loss"].item(),
+                      ns["entropy_loss"].item(), ns["old_approx_kl"].item(),
+                      ns["approx_kl"].item(), ns["clipfracs"][-1],
+                      mba.mean().item() if norm_adv else 0.0,
+                      mba.std().item() if norm_adv else 0.0], np.float32)
+    np.savez_compressed(
+        OUT / f"loss_{name}.npz", logits=captured["logits"].detach().numpy(),
+        new_value=captured["value"].detach().numpy().reshape(-1),
+        dlogits=captured["logits"].grad.numpy(),
+        dvalue=captured["value"].grad.numpy().reshape(-1), mb_inds=mb_inds.astype(np.int64),
+        b_actions=b_actions.numpy().astype(np.int64), b_logprobs=b_logprobs.numpy(),
+        b_advantages=b_advantages.numpy(), b_returns=b_returns.numpy(),
+        b_values=b_values.numpy(), stats=stats, clip_coef=clip_coef, ent_coef=0.01, vf_coef=0.5,
+        norm_adv=norm_adv, clip_vloss=clip_vloss, grad_norm=float(ns["gn"]))
+
+
+# ---------------------------------------------------------------------------------------------
+def gen_sample(name, N, A, F, seed):
+    torch.manual_seed(1234)
+    agent = PPObj(Envs((4, F), A), "cpu", (32, 64), (32,))
+    # scale the actor up so the policy is far from uniform (more informative argmax cases)
+    with torch.no_grad():
+        agent.actor.weight.mul_(40.0)
+    rng = np.random.default_rng(seed)
+    x = torch.from_numpy(rng.integers(0, 160, (N, 4, F)).astype(np.float32))
+    captured = {}
+    h = agent.actor.register_forward_hook(lambda m, i, o: captured.__setitem__("logits", o))
+    torch.manual_seed(seed)
+    with torch.no_grad():
+        action, logprob, entropy, value = agent.get_action_and_value(x)
+    h.remove()
+    torch.manual_seed(seed)
+    noise = torch.empty((N, A), dtype=torch.float32).exponential_()
+    np.savez_compressed(OUT / f"sample_{name}.npz", logits=captured["logits"].numpy(),
+                        noise=noise.numpy(), action=action.numpy().astype(np.int64),
+                        logprob=logprob.numpy(), entropy=entropy.numpy(),
+                        value=value.numpy().reshape(-1))
+
+
+# ---------------------------------------------------------------------------------------------
+def gen_ppobj_small():
+    torch.manual_seed(7)
+    agent = PPObj(Envs((4, 6), 6), "cpu", (16, 32), (16,))
+    rng = np.random.default_rng(7)
+    x = torch.from_numpy(rng.integers(0, 160, (32, 4, 6)).astype(np.float32))
+    with torch.no_grad():
+        hid = agent.network(x)
+        logits = agent.actor(hid)
+        value = agent.get_value(x)
+    sd = {f"sd::{k}": v.numpy() for k, v in agent.state_dict().items()}
+    np.savez_compressed(OUT / "ppobj_small.npz", x=x.numpy(), logits=logits.numpy(),
+                        value=value.numpy(), encoder_dims=np.array([16, 32]),
+                        decoder_dims=np.array([16]), **sd)
+
+
+def gen_init(name, ctor, obs_shape, A, seed, x_scale):
+    torch.manual_seed(seed)
+    agent = ctor(Envs(obs_shape, A))
+    rng = np.random.default_rng(seed)
+    x = torch.from_numpy((rng.random((4,) + obs_shape) * x_scale).astype(np.float32).round())
+    with torch.no_grad():
+        hid = agent.network(x)
+        logits = agent.actor(hid)
+        value = agent.critic(hid)
+    info = {
+        "seed": seed, "obs_shape": list(obs_shape), "n_actions": A, "x_scale": x_scale,
+        "num_params": int(sum(p.numel() for p in agent.parameters())),
+        "params": {k: {"shape": list(v.shape), "sum": float(v.double().sum()),
+                       "abs_sum": float(v.double().abs().sum())}
+                   for k, v in agent.state_dict().items()},
+        "logits": logits.double().numpy().tolist(), "value": value.double().numpy().tolist(),
+    }
+    (OUT / f"init_{name}.json").write_text(json.dumps(info, indent=1))
+
+
+def main():
+    torch.set_num_threads(8)
+    gen_gae(16, 8, "synthetic", 1)
+    gen_gae(123, 7, "jaxtest", 42)
+    gen_gae(128, 128, "synthetic", 2)
+    gen_loss("norm_clip", norm_adv=True, clip_vloss=True, seed=0)
+    gen_loss("nonorm_clip", norm_adv=False, clip_vloss=True, seed=1)
+    gen_loss("norm_noclip", norm_adv=True, clip_vloss=False, seed=2)
+    gen_loss("nonorm_noclip", norm_adv=False, clip_vloss=False, seed=3)
+    gen_loss("ties", norm_adv=True, clip_vloss=True, seed=4, ties=True)
+    gen_loss("cartpole_c02", norm_adv=True, clip_vloss=True, seed=5, F=4, A=2, clip_coef=0.2,
+             B=512, M=128)
+    gen_loss("a18", norm_adv=True, clip_vloss=True, seed=6, A=18)
+    gen_sample("n128_a6", 128, 6, 12, 42)
+    gen_sample("n256_a4", 256, 4, 6, 43)
+    gen_sample("n64_a18", 64, 18, 6, 44)
+    gen_ppobj_small()
+    gen_init("ppobj_f12_a6", lambda e: PPObj(e, "cpu", (256, 512, 1024, 512), (512,)), (4, 12), 6,
+             1, 160.0)
+    gen_init("ppodefault_a4", lambda e: PPODefault(e, "cpu"), (4, 84, 84), 4, 1, 255.0)
+    print("fixtures written to", OUT)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,72 @@
+"""The C-ABI library loads without a GPU and exports every function include/ocppo.h declares;
+argument validation and the error channel work without launching anything."""
+import ctypes
+import re
+
+import pytest
+
+from conftest import ROOT
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from oc_cleanrl_amd import _lib
+
+    return _lib
+
+
+def test_header_functions_exported(lib):
+    names = lib.header_functions()
+    assert len(names) >= 14
+    for n in names:
+        assert hasattr(lib.LIB, n), f"{n} declared in include/ocppo.h but not exported"
+        assert n in lib.SIGNATURES, f"{n} has no ctypes signature"
+    assert set(lib.SIGNATURES) == set(names)
+
+
+def test_header_constants_match_python(lib):
+    text = (ROOT / "include" / "ocppo.h").read_text()
+    consts = dict(re.findall(r"#define (OCPPO_\w+) (\d+)", text))
+    assert int(consts["OCPPO_ABI_VERSION"]) == lib.OCPPO_ABI_VERSION == lib.LIB.ocppo_abi_version()
+    assert int(consts["OCPPO_F32"]) == lib.OCPPO_F32
+    assert int(consts["OCPPO_BF16"]) == lib.OCPPO_BF16
+    assert int(consts["OCPPO_U8"]) == lib.OCPPO_U8
+    assert int(consts["OCPPO_NUM_STATS"]) == lib.OCPPO_NUM_STATS
+    stat_names = re.findall(r"#define OCPPO_STAT_(\w+) (\d+)", text)
+    assert [n.lower() for n, _ in sorted(stat_names, key=lambda x: int(x[1]))] == list(lib.STAT_NAMES)
+
+
+def test_only_c_abi_is_exported():
+    import subprocess
+
+    out = subprocess.run(["nm", "-D", "--defined-only",
+                          str(ROOT / "oc_cleanrl_amd" / "lib" / "libocppo_hip.so")],
+                         capture_output=True, text=True, check=True).stdout
+    syms = [l.split()[-1] for l in out.splitlines() if l.split()[1] in ("T", "D", "B", "W", "V")]
+    assert all(s.startswith("ocppo_") for s in syms), [s for s in syms if not s.startswith("ocppo_")]
+
+
+def test_invalid_arguments_report_errors_without_launch(lib):
+    L = lib.LIB
+    rc = L.ocppo_gae(None, None, None, None, None, None, 8, 4, 0.99, 0.95, None, None)
+    assert rc == lib.OCPPO_E_INVALID
+    assert b"null pointer" in L.ocppo_last_error()
+    rc = L.ocppo_ppo_loss_fwd_bwd(None, None, None, 16, 64, *([None] * 7), 0.1, 0.01, 0.5, 1, 1,
+                                  None, None, None, None, 0)
+    assert rc == lib.OCPPO_E_INVALID and b"A <= 32" in L.ocppo_last_error()
+    dummy = ctypes.c_void_p(16)
+    rc = L.ocppo_ppo_loss_fwd_bwd(None, dummy, dummy, 16, 6, None, dummy, dummy, dummy, dummy,
+                                  dummy, None, 0.1, 0.01, 0.5, 1, 1, dummy, dummy, dummy, None, 0)
+    assert rc == lib.OCPPO_E_WORKSPACE
+    with pytest.raises(lib.OcppoError, match="ocppo_gather_rows"):
+        lib.call("ocppo_gather_rows", None, None, 7, None, 4, 4, None)
+
+
+def test_zero_sized_calls_are_noops(lib):
+    assert lib.LIB.ocppo_gae(None, None, None, None, None, None, 0, 0, 0.99, 0.95, None, None) == 0
+    assert lib.LIB.ocppo_gather_rows(None, None, 0, None, 0, 4, None) == 0
+
+
+def test_workspace_size_is_host_only(lib):
+    n = lib.LIB.ocppo_ppo_loss_workspace_bytes(4096, 6)
+    assert n >= 256 + 16 * 6 * 4 and n % 16 == 0

@@ -1,0 +1,327 @@
+"""HIP kernels vs the oracle (and the reference fixtures), through the C-ABI (-m gpu)."""
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, golden
+from oracle import ocppo_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def T(x, dev, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(x))
+    return t.to(dev) if dtype is None else t.to(device=dev, dtype=dtype)
+
+
+def bits(t):
+    return t.detach().cpu().numpy().view(np.uint32)
+
+
+@pytest.fixture(scope="module")
+def ops():
+    from oc_cleanrl_amd import ops
+
+    return ops
+
+
+# ---------------------------------------------------------------------------------------------
+# GAE: bit-exact
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("name", sorted(os.path.basename(p) for p in glob.glob(str(GOLDEN / "gae_*.npz"))))
+def test_gae_golden_bitwise(ops, dev, name):
+    z = golden(name)
+    adv, ret = ops.gae(T(z["rewards"], dev), T(z["values"], dev), T(z["dones"], dev),
+                       T(z["next_value"], dev), T(z["next_done"], dev), float(z["gamma"]),
+                       float(z["gae_lambda"]))
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(adv), z["advantages"].view(np.uint32))
+    assert np.array_equal(bits(ret), z["returns"].view(np.uint32))
+
+
+@pytest.mark.parametrize("T_,N", [(1, 1), (128, 1), (7, 5), (128, 128), (200, 130), (64, 1001),
+                                  (128, 1024), (128, 65536), (16, 65540), (33, 262144)])
+def test_gae_random_bitwise_vs_oracle(ops, dev, T_, N):
+    rng = np.random.default_rng(T_ * 7919 + N)
+    r = rng.standard_normal((T_, N)).astype(np.float32)
+    v = (rng.standard_normal((T_, N)) * 3).astype(np.float32)
+    d = (rng.random((T_, N)) < 0.1).astype(np.float32)
+    nv = rng.standard_normal(N).astype(np.float32)
+    nd = (rng.random(N) < 0.1).astype(np.float32)
+    adv, ret = ops.gae(T(r, dev), T(v, dev), T(d, dev), T(nv, dev), T(nd, dev), 0.99, 0.95)
+    ea, er = O.gae(r, v, d, nv, nd, 0.99, 0.95)
+    assert np.array_equal(bits(adv), ea.view(np.uint32))
+    assert np.array_equal(bits(ret), er.view(np.uint32))
+
+
+def test_gae_rejects_bad_shapes(ops, dev):
+    r = torch.zeros(8, 4, device=dev)
+    with pytest.raises(ValueError):
+        ops.gae(r, r, r, torch.zeros(3, device=dev), torch.zeros(4, device=dev), 0.99, 0.95)
+    with pytest.raises(ValueError):
+        ops.gae(r.cpu(), r, r, r[0], r[0], 0.99, 0.95)
+
+
+# ---------------------------------------------------------------------------------------------
+# fused PPO loss
+# ---------------------------------------------------------------------------------------------
+def _loss_args(z, dev):
+    return (T(z["logits"], dev), T(z["new_value"], dev), T(z["b_actions"], dev),
+            T(z["b_logprobs"], dev), T(z["b_advantages"], dev), T(z["b_returns"], dev),
+            T(z["b_values"], dev))
+
+
+def _cfg(z):
+    return dict(clip_coef=float(z["clip_coef"]), ent_coef=float(z["ent_coef"]),
+                vf_coef=float(z["vf_coef"]), norm_adv=bool(z["norm_adv"]),
+                clip_vloss=bool(z["clip_vloss"]))
+
+
+@pytest.mark.parametrize("name", sorted(os.path.basename(p) for p in glob.glob(str(GOLDEN / "loss_*.npz"))))
+def test_loss_golden(ops, dev, name):
+    z = golden(name)
+    stats, dl, dv = ops.ppo_loss_fwd_bwd(*_loss_args(z, dev), mb_inds=T(z["mb_inds"], dev),
+                                         **_cfg(z))
+    np.testing.assert_allclose(stats.cpu().numpy(), z["stats"], rtol=2e-6, atol=3e-7)
+    sl = np.abs(z["dlogits"]).max()
+    np.testing.assert_allclose(dl.cpu().numpy(), z["dlogits"], rtol=0, atol=1e-6 * sl)
+    np.testing.assert_allclose(dv.cpu().numpy(), z["dvalue"], rtol=0,
+                               atol=1e-6 * np.abs(z["dvalue"]).max())
+
+
+@pytest.mark.parametrize("M,A,B", [(1, 6, 1), (255, 4, 1000), (4096, 6, 16384), (8192, 4, 32768),
+                                   (5000, 18, 5000), (65536, 6, 131072)])
+@pytest.mark.parametrize("norm_adv,clip_vloss", [(True, True), (False, False)])
+def test_loss_random_vs_oracle(ops, dev, M, A, B, norm_adv, clip_vloss):
+    if M == 1 and norm_adv:
+        pytest.skip("std of one element is NaN in the reference too")
+    rng = np.random.default_rng(M + A)
+    logits = (rng.standard_normal((M, A)) * 2).astype(np.float32)
+    b_actions = rng.integers(0, A, B).astype(np.int64)
+    b_logprobs = (rng.standard_normal(B) * 0.2 - 1.7).astype(np.float32)
+    b_adv = (rng.standard_normal(B) * 2).astype(np.float32)
+    b_ret = rng.standard_normal(B).astype(np.float32)
+    b_val = rng.standard_normal(B).astype(np.float32)
+    v = (b_val[:M] + rng.standard_normal(M) * 0.2).astype(np.float32)
+    mb = rng.permutation(B)[:M].astype(np.int64)
+    cfg = dict(clip_coef=0.1, ent_coef=0.01, vf_coef=0.5, norm_adv=norm_adv, clip_vloss=clip_vloss)
+    stats, dl, dv = ops.ppo_loss_fwd_bwd(T(logits, dev), T(v, dev), T(b_actions, dev),
+                                         T(b_logprobs, dev), T(b_adv, dev), T(b_ret, dev),
+                                         T(b_val, dev), mb_inds=T(mb, dev), **cfg)
+    es, edl, edv = O.ppo_loss_fwd_bwd(logits, v, b_actions, b_logprobs, b_adv, b_ret, b_val, mb,
+                                      **cfg)
+    np.testing.assert_allclose(stats.cpu().numpy(), es, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(dl.cpu().numpy(), edl, rtol=0, atol=2e-6 * np.abs(edl).max())
+    np.testing.assert_allclose(dv.cpu().numpy(), edv, rtol=0, atol=2e-6 * np.abs(edv).max())
+
+
+def test_loss_deterministic_and_graph_replayable(ops, dev):
+    z = golden("loss_norm_clip.npz")
+    args = _loss_args(z, dev)
+    mb = T(z["mb_inds"], dev)
+    ws = ops.LossWorkspace(len(z["mb_inds"]), z["logits"].shape[1], dev)
+    s1, d1, v1 = ops.ppo_loss_fwd_bwd(*args, mb_inds=mb, workspace=ws, **_cfg(z))
+    s1, d1, v1 = s1.clone(), d1.clone(), v1.clone()
+    st = torch.empty(9, device=dev)
+    dl = torch.empty_like(d1)
+    dv = torch.empty_like(v1)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        ops.ppo_loss_fwd_bwd(*args, mb_inds=mb, workspace=ws, stats=st, dlogits=dl, dvalue=dv,
+                             **_cfg(z))
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        ops.ppo_loss_fwd_bwd(*args, mb_inds=mb, workspace=ws, stats=st, dlogits=dl, dvalue=dv,
+                             **_cfg(z))
+    for _ in range(3):
+        st.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(st, s1) and torch.equal(dl, d1) and torch.equal(dv, v1)
+
+
+def test_loss_precomputed_adv_stats_match(ops, dev):
+    z = golden("loss_norm_clip.npz")
+    args = _loss_args(z, dev)
+    mb = T(z["mb_inds"], dev)
+    st = ops.minibatch_adv_stats(args[4], mb, len(z["mb_inds"]))
+    np.testing.assert_allclose(st.cpu().numpy()[0], z["stats"][7:9], rtol=1e-6)
+    a = ops.ppo_loss_fwd_bwd(*args, mb_inds=mb, **_cfg(z))
+    b = ops.ppo_loss_fwd_bwd(*args, mb_inds=mb, adv_stats=st[0], **_cfg(z))
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+
+
+def test_minibatch_adv_stats_many(ops, dev):
+    rng = np.random.default_rng(3)
+    B, M = 16384, 4096
+    adv = (rng.standard_normal(B) * 3 + 0.5).astype(np.float32)
+    perm = np.concatenate([rng.permutation(B) for _ in range(4)]).astype(np.int64)
+    st = ops.minibatch_adv_stats(T(adv, dev), T(perm, dev), M)
+    np.testing.assert_allclose(st.cpu().numpy(), O.adv_stats(adv, perm, M), rtol=2e-6)
+
+
+def test_loss_autograd_function(ops, dev):
+    z = golden("loss_ties.npz")
+    lg = T(z["logits"], dev).requires_grad_(True)
+    v = T(z["new_value"], dev).view(-1, 1).requires_grad_(True)
+    a = _loss_args(z, dev)
+    loss, stats = ops.ppo_loss(lg, v, *a[2:], mb_inds=T(z["mb_inds"], dev), **_cfg(z))
+    (2.0 * loss).backward()
+    np.testing.assert_allclose(lg.grad.cpu().numpy(), 2 * z["dlogits"], rtol=0,
+                               atol=2e-6 * np.abs(z["dlogits"]).max())
+    np.testing.assert_allclose(v.grad.view(-1).cpu().numpy(), 2 * z["dvalue"], rtol=0,
+                               atol=2e-6 * np.abs(z["dvalue"]).max())
+    assert float(loss) == pytest.approx(float(z["stats"][0]), rel=2e-6)
+
+
+# ---------------------------------------------------------------------------------------------
+# Categorical action head
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("name", sorted(os.path.basename(p) for p in glob.glob(str(GOLDEN / "sample_*.npz"))))
+def test_sample_golden(ops, dev, name):
+    z = golden(name)
+    N = len(z["action"])
+    val = torch.arange(N, dtype=torch.float32, device=dev)
+    vout = torch.empty(N, device=dev)
+    ent = torch.empty(N, device=dev)
+    a, lp, _ = ops.categorical_sample(T(z["logits"], dev), T(z["noise"], dev), entropy_out=ent,
+                                      value_in=val, value_out=vout)
+    assert np.array_equal(a.cpu().numpy(), z["action"])
+    np.testing.assert_allclose(lp.cpu().numpy(), z["logprob"], rtol=1e-6, atol=2e-6)
+    np.testing.assert_allclose(ent.cpu().numpy(), z["entropy"], rtol=1e-6, atol=2e-6)
+    assert torch.equal(vout, val)
+
+
+@pytest.mark.parametrize("A", [2, 4, 6, 18])
+def test_sample_matches_torch_categorical_on_device(ops, dev, A):
+    """Same generator state → torch's own Categorical.sample() and our kernel pick the same
+    actions (torch draws Exp(1) noise of shape [N, A] and takes argmax(probs / noise))."""
+    N = 8192
+    g = torch.Generator(device=dev)
+    logits = torch.randn(N, A, device=dev, generator=g.manual_seed(5)) * 3
+    g.manual_seed(11)
+    dist = torch.distributions.Categorical(logits=logits)
+    ref = torch.multinomial(dist.probs, 1, True, generator=g).view(-1)
+    g.manual_seed(11)
+    noise = torch.empty(N, A, device=dev).exponential_(generator=g)
+    a, lp, _ = ops.categorical_sample(logits, noise)
+    assert torch.equal(a, ref)
+    torch.testing.assert_close(lp, dist.log_prob(a), rtol=1e-6, atol=2e-6)
+
+
+@pytest.mark.parametrize("A", [4, 18])
+def test_logprob_entropy_fwd_bwd_vs_torch(ops, dev, A):
+    N = 3000
+    logits = (torch.randn(N, A, device=dev) * 2).requires_grad_(True)
+    act = torch.randint(0, A, (N,), device=dev)
+    lp, ent = ops.categorical_logprob_entropy(logits, act)
+    g1, g2 = torch.randn(N, device=dev), torch.randn(N, device=dev)
+    ((lp * g1).sum() + (ent * g2).sum()).backward()
+    ours = logits.grad.clone()
+    logits.grad = None
+    d = torch.distributions.Categorical(logits=logits)
+    rl, re = d.log_prob(act), d.entropy()
+    ((rl * g1).sum() + (re * g2).sum()).backward()
+    torch.testing.assert_close(lp, rl.detach(), rtol=1e-6, atol=2e-6)
+    torch.testing.assert_close(ent, re.detach(), rtol=1e-6, atol=2e-6)
+    torch.testing.assert_close(ours, logits.grad, rtol=1e-5, atol=2e-6)
+
+
+# ---------------------------------------------------------------------------------------------
+# rollout store / reset / gather: bit-exact
+# ---------------------------------------------------------------------------------------------
+STORE_DT = {"f32": torch.float32, "bf16": torch.bfloat16, "u8": torch.uint8}
+
+
+@pytest.mark.parametrize("obs_dt", ["f32", "bf16", "u8"])
+@pytest.mark.parametrize("pixel,N,D", [(False, 128, 12), (False, 7, 6), (False, 5, 3),
+                                       (True, 16, 7056), (True, 3, 5)])
+def test_rollout_store_bitwise(ops, dev, obs_dt, pixel, N, D):
+    rng = np.random.default_rng(N * D)
+    W = 4
+    hi = 256 if pixel else 210
+    prev = rng.integers(0, hi, (N, W, D)).astype(np.float32)
+    frame = rng.integers(0, hi, (N, D))
+    frame = frame.astype(np.uint8) if pixel else frame.astype(np.float32)
+    done = (rng.random(N) < 0.3).astype(np.float32)
+    reward = rng.standard_normal(N).astype(np.float32)
+    dt = STORE_DT[obs_dt]
+    prev_t = T(prev, dev).to(dt)
+    out = torch.empty_like(prev_t)
+    net = torch.empty(N, W, D, device=dev)
+    rout = torch.empty(N, device=dev)
+    dout = torch.empty(N, device=dev)
+    ops.rollout_store(T(frame, dev), T(reward, dev), T(done, dev), prev_t, out, net, rout, dout)
+    exp = O.rollout_store(frame.astype(np.float32), done, prev, obs_dt)
+    assert np.array_equal(out.float().cpu().numpy(), exp)
+    assert np.array_equal(net.cpu().numpy(), exp)
+    assert torch.equal(rout.cpu(), torch.from_numpy(reward))
+    assert torch.equal(dout.cpu(), torch.from_numpy(done))
+
+
+def test_bf16_conversion_rounds_to_nearest_even(ops, dev):
+    x = torch.tensor([[1.0 + 2 ** -8, 1.0 + 3 * 2 ** -8, 300.5, -0.0]], device=dev)
+    prev = torch.zeros(1, 1, 4, dtype=torch.bfloat16, device=dev)
+    out = torch.empty_like(prev)
+    ops.rollout_store(x, torch.zeros(1, device=dev), torch.ones(1, device=dev), prev, out)
+    assert torch.equal(out.view(-1), x.view(-1).to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("src_dt", ["f32", "bf16", "u8"])
+@pytest.mark.parametrize("B,shape,M", [(16384, (4, 12), 4096), (300, (4, 84, 84), 64),
+                                       (50, (3, 5), 77)])
+def test_gather_rows_bitwise(ops, dev, src_dt, B, shape, M):
+    rng = np.random.default_rng(B + M)
+    src = rng.integers(0, 256, (B,) + shape).astype(np.float32)
+    idx = rng.integers(0, B, M).astype(np.int64)
+    out = ops.gather_rows(T(src, dev).to(STORE_DT[src_dt]), T(idx, dev))
+    assert np.array_equal(out.cpu().numpy(), src[idx])
+
+
+def test_obs_reset(ops, dev):
+    frame = torch.randint(0, 256, (9, 7056), dtype=torch.uint8, device=dev)
+    out = torch.empty(9, 4, 7056, dtype=torch.bfloat16, device=dev)
+    net = torch.empty(9, 4, 7056, device=dev)
+    ops.obs_reset(frame, out, net)
+    assert torch.equal(net, frame.float()[:, None].expand(9, 4, 7056))
+    assert torch.equal(out.float(), net)
+
+
+# ---------------------------------------------------------------------------------------------
+# VecNormalize reward normalisation (f64) and the synthetic env
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("N", [1, 128, 1500])
+def test_vecnorm_vs_oracle(ops, dev, N):
+    rng = np.random.default_rng(N)
+    ret_t = torch.zeros(N, dtype=torch.float64, device=dev)
+    rms_t = torch.tensor([0.0, 1.0, 1e-4], dtype=torch.float64, device=dev)
+    ret, rms = np.zeros(N), (0.0, 1.0, 1e-4)
+    for step in range(20):
+        r = np.where(rng.random(N) < 0.1, rng.choice([-1.0, 1.0], N), 0.0).astype(np.float32)
+        d = (rng.random(N) < 0.05).astype(np.float32)
+        out_t = torch.empty(N, device=dev)
+        ops.vecnorm_reward(T(r, dev), T(d, dev), ret_t, rms_t, out_t)
+        out, ret, rms = O.vecnorm_reward(r, d, ret, rms)
+        np.testing.assert_allclose(out_t.cpu().numpy(), out, rtol=1e-6, atol=1e-7)
+        np.testing.assert_allclose(ret_t.cpu().numpy(), ret, rtol=1e-12, atol=1e-12)
+        np.testing.assert_allclose(rms_t.cpu().numpy(), np.array(rms), rtol=1e-12)
+
+
+@pytest.mark.parametrize("pixel,N,D", [(False, 128, 12), (False, 33, 6), (True, 8, 7056)])
+def test_synth_env_bitwise_vs_oracle(ops, dev, pixel, N, D):
+    base = torch.tensor([1000], dtype=torch.int64, device=dev)
+    acts = torch.arange(N, device=dev) % 6
+    frame = torch.empty(N, D, dtype=torch.uint8 if pixel else torch.float32, device=dev)
+    rew = torch.empty(N, device=dev)
+    done = torch.empty(N, device=dev)
+    ops.synth_env_step(42, base, 5, acts, frame, rew, done)
+    ef, er, ed = O.synth_env_step(42, 1005, acts.cpu().numpy(), N, D, pixel)
+    assert np.array_equal(frame.cpu().numpy(), ef)
+    assert np.array_equal(rew.cpu().numpy(), er)
+    assert np.array_equal(done.cpu().numpy(), ed)

@@ -1,0 +1,115 @@
+"""Pin the oracle (oracle/ocppo_oracle.py) to the reference's own outputs (tests/golden/*, made by
+tests/golden/gen_golden.py from cleanrl/ppo_atari_oc.py and cleanrl/architectures/ppo.py)."""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, golden
+from oracle import ocppo_oracle as O
+
+GAE_FILES = sorted(os.path.basename(p) for p in glob.glob(str(GOLDEN / "gae_*.npz")))
+LOSS_FILES = sorted(os.path.basename(p) for p in glob.glob(str(GOLDEN / "loss_*.npz")))
+SAMPLE_FILES = sorted(os.path.basename(p) for p in glob.glob(str(GOLDEN / "sample_*.npz")))
+
+
+def test_fixture_inventory():
+    assert len(GAE_FILES) == 3 and len(LOSS_FILES) == 7 and len(SAMPLE_FILES) == 3
+
+
+@pytest.mark.parametrize("name", GAE_FILES)
+def test_gae_bitwise(name):
+    z = golden(name)
+    adv, ret = O.gae(z["rewards"], z["values"], z["dones"], z["next_value"], z["next_done"],
+                     float(z["gamma"]), float(z["gae_lambda"]))
+    # bit-identical to the reference loop (ppo_atari_oc.py:533-547), like test_jax_compute_gae's ==
+    assert np.array_equal(adv.view(np.uint32), z["advantages"].view(np.uint32))
+    assert np.array_equal(ret.view(np.uint32), z["returns"].view(np.uint32))
+
+
+@pytest.mark.parametrize("name", SAMPLE_FILES)
+def test_categorical_sample_matches_torch(name):
+    z = golden(name)
+    a, lp, ent = O.categorical_sample(z["logits"], z["noise"])
+    assert np.array_equal(a, z["action"])  # actions bit-exact given torch's Exp(1) draw
+    np.testing.assert_allclose(lp, z["logprob"], rtol=1e-6, atol=2e-6)
+    np.testing.assert_allclose(ent, z["entropy"], rtol=1e-6, atol=2e-6)
+    lp2, ent2 = O.categorical_logprob_entropy(z["logits"], z["action"])
+    assert np.array_equal(lp2, lp) and np.array_equal(ent2, ent)
+
+
+@pytest.mark.parametrize("name", LOSS_FILES)
+def test_ppo_loss_matches_reference_autograd(name):
+    z = golden(name)
+    stats, dl, dv = O.ppo_loss_fwd_bwd(
+        z["logits"], z["new_value"], z["b_actions"], z["b_logprobs"], z["b_advantages"],
+        z["b_returns"], z["b_values"], z["mb_inds"], clip_coef=float(z["clip_coef"]),
+        ent_coef=float(z["ent_coef"]), vf_coef=float(z["vf_coef"]), norm_adv=bool(z["norm_adv"]),
+        clip_vloss=bool(z["clip_vloss"]))
+    np.testing.assert_allclose(stats, z["stats"], rtol=2e-6, atol=2e-7)
+    scale = np.abs(z["dlogits"]).max()
+    np.testing.assert_allclose(dl, z["dlogits"], rtol=0, atol=1e-6 * scale)
+    np.testing.assert_allclose(dv, z["dvalue"], rtol=0, atol=1e-6 * np.abs(z["dvalue"]).max())
+
+
+def test_ties_fixture_really_ties():
+    z = golden("loss_ties.npz")
+    # a quarter of the batch has ratio == 1 exactly: the surrogate's max() ties there
+    lp, _ = O.categorical_logprob_entropy(z["logits"], z["b_actions"][z["mb_inds"]])
+    assert np.sum(lp == z["b_logprobs"][z["mb_inds"]]) > 0
+
+
+def test_adv_stats_against_loss_fixture():
+    z = golden("loss_norm_clip.npz")
+    st = O.adv_stats(z["b_advantages"], z["mb_inds"], len(z["mb_inds"]))[0]
+    np.testing.assert_allclose(st, z["stats"][7:9], rtol=1e-6)
+
+
+def test_categorical_backward_matches_finite_difference():
+    rng = np.random.default_rng(0)
+    l = rng.standard_normal((5, 6)).astype(np.float64)
+    a = rng.integers(0, 6, 5)
+    g_lp, g_h = rng.standard_normal(5), rng.standard_normal(5)
+
+    def f(x):
+        lp, h = O.categorical_logprob_entropy(x.astype(np.float32), a)
+        return float(np.sum(g_lp * lp + g_h * h))
+
+    d = O.categorical_backward(l.astype(np.float32), a, g_lp, g_h)
+    eps = 1e-2
+    for i in range(5):
+        for j in range(6):
+            e = np.zeros_like(l)
+            e[i, j] = eps
+            fd = (f(l + e) - f(l - e)) / (2 * eps)
+            assert abs(fd - d[i, j]) < 2e-3
+
+
+def test_store_and_gather_oracle():
+    rng = np.random.default_rng(0)
+    prev = rng.integers(0, 200, (3, 4, 5)).astype(np.float32)
+    frame = rng.integers(0, 200, (3, 5)).astype(np.float32)
+    out = O.rollout_store(frame, np.array([0, 1, 0], np.float32), prev)
+    assert np.array_equal(out[0, :3], prev[0, 1:]) and np.array_equal(out[0, 3], frame[0])
+    assert all(np.array_equal(out[1, w], frame[1]) for w in range(4))
+    assert np.array_equal(O.to_storage(out, "bf16"), out)  # integers <= 256 are exact in bf16
+    g = O.gather_rows(out.reshape(3, -1), [2, 0])
+    assert np.array_equal(g[0], out[2].reshape(-1))
+
+
+def test_vecnorm_oracle_first_step():
+    r = np.array([1.0, 0.0, -1.0, 0.0], np.float32)
+    out, ret, rms = O.vecnorm_reward(r, np.array([0, 0, 1, 0], np.float32), np.zeros(4),
+                                     (0.0, 1.0, 1e-4))
+    assert rms[2] == pytest.approx(4 + 1e-4)
+    assert ret[2] == 0.0 and ret[0] == 1.0
+    assert np.all(np.abs(out) <= 10)
+
+
+def test_synth_env_oracle_ranges():
+    f, r, d = O.synth_env_step(42, 7, np.arange(64) % 6, 64, 12, False)
+    assert f.shape == (64, 12) and np.all(f == np.round(f))
+    assert f[:, 0::4].max() < 160 and f[:, 1::4].max() < 210 and f[:, 2::4].min() >= 1
+    p, _, _ = O.synth_env_step(42, 7, None, 4, 7056, True)
+    assert p.dtype == np.uint8 and (p == 0).mean() > 0.8
