@@ -1,0 +1,181 @@
+"""Benchmark: PPO actor-learner SPS + PPO updates/sec, ALE/Pong-v5 obj-mode (synthetic env), PPO_OBJ.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+A "step" is one PPO iteration of the reference loop (cleanrl/ppo_atari_oc.py:469-617) on every
+rank: a T=128-step rollout of local_num_envs=128 envs (BASELINE config 2 per GPU; config 4 =
+1024 envs over 8 GPUs), GAE, and update_epochs=4 x num_minibatches=4 minibatch updates with an
+RCCL gradient all-reduce per minibatch when N > 1 (ppo_atari_multigpu semantics, weak scaling).
+value = env steps of all ranks / max-over-ranks wall time of the K timed iterations.
+
+Rank 0 prints ONE JSON line. Extra fields: `roofline` (dominant HIP kernel of this package, live
+HIP-event timing over the timed region), `kernels` (every HIP kernel's mean launch duration and
+algorithmic GB/s), `cpu_baseline` (the oracle's CPU port of the same loop timed on this host, N=1).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import torch
+import torch.distributed as dist
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
+
+
+def kernel_bytes(tr) -> dict:
+    """ALGORITHMIC bytes per launch of each timed HIP kernel."""
+    N, T, M, A = tr.N, tr.T, tr.M, tr.A
+    W, D = tr.obs_shape[0], int(torch.tensor(tr.obs_shape[1:]).prod())
+    sb = tr.obs.element_size()
+    fb = tr.env.frame.element_size()
+    return {
+        # read r, v, d [T,N] + next v/d [N]; write adv, ret [T,N]
+        "gae": 20 * T * N + 8 * N,
+        # logits 4A + value 4 + index 8 + action 8 + 4 gathered f32 in; dlogits 4A + dv 4 out
+        "ppo_loss": (8 * A + 36) * M,
+        # index 8 + row read (storage dtype) + f32 row write
+        "gather": M * (8 + W * D * (sb + 4)),
+        # prev slot (W-1 frames) + new frame + done in; slot + f32 net obs out; reward/done rows
+        "rollout_store": N * ((W - 1) * D * sb + D * fb + W * D * (sb + 4) + 16),
+        # logits + noise in, action i64 + logprob + value copy out
+        "action_head": N * (8 * A + 8 + 4 + 8),
+        # actions in; frame + reward + done + episode counters out (read-modify-write)
+        "env_step": N * (8 + D * fb + 8 + 2 * 20),
+        # reward, done, ret (f64) in; ret out, reward out, twice over ret for mean/var
+        "vecnorm": N * (4 + 4 + 8 + 8 + 8 + 4),
+        # perm index + gathered advantage, twice (mean pass, variance pass)
+        "adv_stats": 2 * tr.E * tr.B * (8 + 4),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--envs-per-gpu", type=int, default=128)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-iterations", type=int, default=3)
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true")
+    opt = ap.parse_args()
+
+    from oc_cleanrl_amd.args import Args, finalize
+    from oc_cleanrl_amd.trainer import PPOTrainer
+
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != opt.gpus:
+        if world == 1 and opt.gpus > 1:
+            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run")
+    device = torch.device(f"cuda:{local_rank}")
+    torch.cuda.set_device(device)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    args = Args(env_id="ALE/Pong-v5", obs_mode="obj", architecture="PPO_OBJ",
+                num_envs=opt.envs_per_gpu * world, num_steps=128, num_features=12,
+                total_timesteps=10_000_000, cuda_graphs=not opt.no_graphs, save_model=False)
+    args = finalize(args, world)
+    tr = PPOTrainer(args, device, rank, world, kernel_timing=not opt.no_kernel_timing, log=False)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(device)
+
+    for _ in range(opt.warmup):
+        tr.train_iteration(collect_metrics=True)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(opt.steps):
+        tr.train_iteration(collect_metrics=True)
+    barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t)
+
+    env_steps = opt.steps * args.num_steps * args.local_num_envs * world
+    updates = opt.steps * args.update_epochs * args.num_minibatches
+    kb = kernel_bytes(tr)
+    kernels = {}
+    if not opt.no_kernel_timing:
+        for name, us in tr.timer.measure().items():
+            n = tr.timer.per_iter.get(name, 0)
+            nbytes = kb.get(name)
+            kernels[name] = {"mean_us": round(us, 3), "launches_per_iter": n,
+                             "us_per_iter": round(us * n, 2)}
+            if nbytes:
+                kernels[name].update(bytes=nbytes, GBps=round(nbytes / (us * 1e-6) / 1e9, 2))
+    timed = [k for k in kernels if "GBps" in kernels[k]]
+    dom = max(timed, key=lambda k: kernels[k]["us_per_iter"]) if timed else None
+    roofline = None
+    if dom:
+        ach = kernels[dom]["GBps"]
+        roofline = {"kernel": dom, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5),
+                    "traffic": None, "bytes_per_launch": kb[dom],
+                    "mean_launch_us": kernels[dom]["mean_us"]}
+
+    cpu = None
+    if rank == 0 and world == 1 and not opt.no_cpu_baseline:
+        from oracle.cpu_learner import time_cpu_baseline  # CPU baseline leg (oracle port)
+
+        threads = min(16, os.cpu_count() or 1)
+        r = time_cpu_baseline(iterations=opt.cpu_iterations, threads=threads, num_envs=128,
+                              num_steps=128)
+        cpu = {"value": round(r["sps"], 1), "unit": "env steps/s", "cores": threads,
+               "kind": "port",
+               "updates_per_sec": round(r["updates_per_sec"], 3),
+               "sample": f"{opt.cpu_iterations} PPO iterations of config 2 (128 envs x 128 steps, "
+                         f"16 minibatch updates of 4096) on CPU torch, {r['seconds']:.1f} s"}
+
+    if rank == 0:
+        sps = env_steps / dt
+        line = {
+            "metric": "env steps/sec (SPS) + PPO updates/sec, ALE/Pong-v5 obj-mode, 1/2/4/8 MI355X",
+            "value": round(sps, 1),
+            "unit": "env steps/s",
+            "n_gpus": world,
+            "steps": opt.steps,
+            "warmup": opt.warmup,
+            "ms_per_step": round(1e3 * dt / opt.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic (device-resident Pong-obj env; random-init PPObj)",
+            "config": {"workload": "ppo_atari_oc.py Pong-v5 obj PPO_OBJ (BASELINE config 2 per GPU)",
+                       "local_num_envs": args.local_num_envs, "num_envs": args.num_envs,
+                       "num_steps": args.num_steps, "num_features": args.num_features,
+                       "minibatch_size": args.local_minibatch_size,
+                       "update_epochs": args.update_epochs,
+                       "num_minibatches": args.num_minibatches,
+                       "obs_storage": str(tr.obs_dtype).replace("torch.", ""),
+                       "cuda_graphs": args.cuda_graphs,
+                       "parallelism": f"dp{world}"},
+            "updates_per_sec": round(updates / dt, 2),
+            "roofline": roofline,
+            "kernels": kernels,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,178 @@
+"""Agents with the reference's duck-typed interface and module layout.
+
+`PPObj` and `PPODefault` mirror cleanrl/architectures/ppo.py:15-95 module for module (same
+nn.Sequential indices, so `state_dict()` keys such as `network.0.weight`, `actor.weight`,
+`critic.bias` interchange with the reference's `.cleanrl_model` checkpoints), and construct and
+initialise their layers in the same order (orthogonal init, architectures/ppo.py:9-13), so a
+seeded construction reproduces the reference's weights bit for bit.
+
+The network forward/backward stays in PyTorch (hipBLASLt / MIOpen); what changes is the action
+head: `get_action_and_value` samples, scores and takes the entropy with the HIP Categorical
+kernels (one launch instead of logsumexp/softmax/multinomial/gather/entropy chains, and no
+host sync — torch's multinomial syncs on `probs.max() < inf`). The sampler consumes the default
+device generator exactly like torch's Categorical.sample (an Exp(1) draw of shape [B, A]), so
+actions are bit-identical to the reference's under the same seed.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import ops
+
+
+def layer_init(layer, std=np.sqrt(2), bias_const=0.0):
+    """Orthogonal weight, constant bias (architectures/ppo.py:9-13, common.py:7-10)."""
+    nn.init.orthogonal_(layer.weight, std)
+    if layer.bias is not None:
+        nn.init.constant_(layer.bias, bias_const)
+    return layer
+
+
+class NormalizeImg(nn.Module):
+    """x / 255 (architectures/common.py:19-22)."""
+
+    @staticmethod
+    def forward(x):
+        return x / 255.0
+
+
+class Predictor(nn.Module):
+    """Greedy `predict` used by the eval harness (architectures/common.py:13-16)."""
+
+    def predict(self, x, states=None, **_):
+        with torch.no_grad():
+            dev = next(self.parameters()).device
+            logits = self.actor(self.network(torch.as_tensor(np.asarray(x), dtype=torch.float32,
+                                                             device=dev)))
+            return np.argmax(logits.cpu().numpy(), axis=1), states
+
+
+class _ActorCritic(Predictor):
+    """Shared interface: network → (actor logits, critic value)."""
+
+    def get_value(self, x):
+        return self.critic(self.network(x))
+
+    def logits_and_value(self, x):
+        hidden = self.network(x)
+        return self.actor(hidden), self.critic(hidden)
+
+    def get_action_and_value(self, x, action=None):
+        """(action [B] i64, log_prob [B], entropy [B], value [B, 1]) like the reference."""
+        logits, value = self.logits_and_value(x)
+        if action is None:
+            noise = torch.empty_like(logits, dtype=torch.float32).exponential_()
+            ent = torch.empty(logits.shape[0], dtype=torch.float32, device=logits.device)
+            act, lp, _ = ops.categorical_sample(logits.detach().float().contiguous(), noise,
+                                                entropy_out=ent)
+            if torch.is_grad_enabled() and logits.requires_grad:
+                lp, ent = ops.categorical_logprob_entropy(logits.float(), act)
+            return act, lp, ent, value
+        lp, ent = ops.categorical_logprob_entropy(logits.float(), action)
+        return action, lp, ent, value
+
+
+class PPODefault(_ActorCritic):
+    """NatureCNN agent (architectures/ppo.py:15-57)."""
+
+    def __init__(self, envs, device=None, normalize=True):
+        super().__init__()
+        self.device = device
+        dims = tuple(envs.observation_space.shape)
+        self.network = nn.Sequential(
+            layer_init(nn.Conv2d(dims[0], 32, 8, stride=4)),
+            nn.ReLU(),
+            layer_init(nn.Conv2d(32, 64, 4, stride=2)),
+            nn.ReLU(),
+            layer_init(nn.Conv2d(64, 64, 3, stride=1)),
+            nn.ReLU(),
+        )
+        if normalize:
+            self.network.insert(0, NormalizeImg())
+        self.network.append(nn.Flatten())
+        with torch.no_grad():
+            feat_dim = self.network(torch.zeros((1,) + dims)).flatten().shape[0]
+        self.network.append(layer_init(nn.Linear(feat_dim, 512)))
+        self.network.append(nn.ReLU())
+        self.actor = layer_init(nn.Linear(512, envs.action_space.n), std=0.01)
+        self.critic = layer_init(nn.Linear(512, 1), std=1)
+
+
+class PPObj(_ActorCritic):
+    """Object-centric MLP agent (architectures/ppo.py:60-95): a per-frame Linear encoder on the
+    last (feature) dim, Flatten over the frame stack, a Linear decoder, actor and critic heads."""
+
+    def __init__(self, envs, device=None, encoder_dims=(128, 64), decoder_dims=(32,)):
+        super().__init__()
+        self.device = device
+        dims = tuple(envs.observation_space.shape)
+        layers = nn.ModuleList()
+        in_dim = dims[-1]
+        for l in encoder_dims:
+            layers.append(layer_init(nn.Linear(in_dim, l)))
+            layers.append(nn.ReLU())
+            in_dim = l
+        layers.append(nn.Flatten())
+        in_dim *= int(np.prod(dims[:-1], dtype=int))
+        l = in_dim
+        for l in decoder_dims:
+            layers.append(layer_init(nn.Linear(in_dim, l)))
+            layers.append(nn.ReLU())
+            in_dim = l
+        self.network = nn.Sequential(*layers)
+        self.actor = layer_init(nn.Linear(l, envs.action_space.n), std=0.01)
+        self.critic = layer_init(nn.Linear(l, 1), std=1)
+
+
+class CartPoleAgent(_ActorCritic):
+    """The tanh-MLP agent of cleanrl/ppo.py:100-126 (config 1), separate actor/critic trunks.
+
+    Exposed through the same logits_and_value interface; `network` is the identity so the
+    actor/critic Sequentials see the raw observation, as in the reference.
+    """
+
+    def __init__(self, envs, device=None):
+        super().__init__()
+        self.device = device
+        n = int(np.array(envs.observation_space.shape).prod())
+        self.critic = nn.Sequential(
+            layer_init(nn.Linear(n, 64)), nn.Tanh(), layer_init(nn.Linear(64, 64)), nn.Tanh(),
+            layer_init(nn.Linear(64, 1), std=1.0))
+        self.actor = nn.Sequential(
+            layer_init(nn.Linear(n, 64)), nn.Tanh(), layer_init(nn.Linear(64, 64)), nn.Tanh(),
+            layer_init(nn.Linear(64, envs.action_space.n), std=0.01))
+        self.network = nn.Identity()
+
+
+class Space:
+    """Minimal gym-like space (shape / n) for constructing agents without gymnasium."""
+
+    def __init__(self, shape=(), n=None):
+        self.shape = tuple(shape)
+        self.n = n
+
+
+class EnvSpec:
+    """`envs`-like object exposing observation_space / action_space (what the agents read)."""
+
+    def __init__(self, obs_shape, n_actions):
+        self.observation_space = Space(obs_shape)
+        self.action_space = Space((), n_actions)
+        self.single_observation_space = self.observation_space
+        self.single_action_space = self.action_space
+
+
+def make_agent(architecture: str, obs_shape, n_actions, device=None, encoder_dims=(256, 512, 1024, 512),
+               decoder_dims=(512,)):
+    """Architecture switch of ppo_atari_oc.py:435-440 for the supported agents."""
+    spec = EnvSpec(obs_shape, n_actions)
+    if architecture == "PPO_OBJ":
+        return PPObj(spec, device, tuple(encoder_dims), tuple(decoder_dims))
+    if architecture == "PPO":
+        return PPODefault(spec, device)
+    if architecture == "CARTPOLE_MLP":
+        return CartPoleAgent(spec, device)
+    raise NotImplementedError(f"Architecture {architecture} is not supported by oc_cleanrl_amd "
+                              "(supported: PPO_OBJ, PPO, CARTPOLE_MLP)")

@@ -1,0 +1,195 @@
+"""`Args` — the flag surface of cleanrl/ppo_atari_oc.py:63-190 (plus the DP fields of
+cleanrl/ppo_atari_multigpu.py:55-102) with the same names and defaults, and a tyro-compatible
+command line (tyro is not installed here): `--num-envs 8` and `--num_envs 8` both work, booleans
+accept `--flag`, `--no-flag` and `--flag True|False`, tuples take several values.
+
+Fields this build adds are grouped at the end and marked "[oc_cleanrl_amd]".
+"""
+from __future__ import annotations
+
+import argparse
+import dataclasses
+import os
+import sys
+from dataclasses import dataclass, field
+from typing import Optional
+
+OBS_MODES = (
+    "dqn", "obj", "masked_dqn_bin", "masked_dqn_pixels", "masked_dqn_planes",
+    "masked_dqn_grayscale", "masked_dqn_pixel_planes", "masked_dqn_parallelplanes",
+    "masked_dqn_bin+pixels", "masked_dqn_pixels+pixels", "masked_dqn_planes+pixels",
+    "masked_dqn_grayscale+pixels", "masked_dqn_pixel_planes+pixels",
+)
+
+# ALE v5 minimal action-set sizes of the games the configs name
+ACTION_COUNTS = {"ALE/Pong-v5": 6, "ALE/Breakout-v5": 4, "ALE/SpaceInvaders-v5": 6,
+                 "CartPole-v1": 2}
+
+
+@dataclass
+class Args:
+    # General (ppo_atari_oc.py:66-74)
+    exp_name: str = "ppo_atari_oc"
+    seed: int = 42
+    torch_deterministic: bool = True
+    cuda: bool = True
+
+    # Environment (:77-96)
+    env_id: str = "ALE/Pong-v5"
+    obs_mode: str = "dqn"
+    buffer_window_size: int = 4
+    backend: str = "Synthetic"  # reference: OCAtari | HackAtari | Gym (ALE not available here)
+    modifs: str = ""
+    new_rf: str = ""
+    frameskip: int = 4
+
+    # Tracking (:99-116)
+    track: bool = False
+    wandb_project_name: str = "OCCAM"
+    wandb_entity: str = "AIML_OC"
+    wandb_dir: Optional[str] = None
+    capture_video: bool = False
+    ckpt: str = ""
+    logging_level: int = 40
+    author: str = "JB"
+    checkpoint_interval: int = 1_000_000
+
+    # Algorithm (:119-152)
+    architecture: str = "PPO"
+    total_timesteps: int = 10_000_000
+    learning_rate: float = 2.5e-4
+    num_envs: int = 10
+    num_steps: int = 128
+    anneal_lr: bool = True
+    gamma: float = 0.99
+    gae_lambda: float = 0.95
+    num_minibatches: int = 4
+    update_epochs: int = 4
+    norm_adv: bool = True
+    clip_coef: float = 0.1
+    clip_vloss: bool = True
+    ent_coef: float = 0.01
+    vf_coef: float = 0.5
+    max_grad_norm: float = 0.5
+    target_kl: Optional[float] = None
+
+    # Transformer parameters (:155-162; those architectures are out of scope, kept for the CLI)
+    emb_dim: int = 128
+    num_heads: int = 64
+    num_blocks: int = 1
+    patch_size: int = 12
+
+    # PPObj network (:165-168)
+    encoder_dims: tuple = (256, 512, 1024, 512)
+    decoder_dims: tuple = (512,)
+
+    # HackAtari / imperfect detection / planes (:171-185)
+    test_modifs: str = ""
+    detection_failure_probability: float = 0.0
+    mislabeling_probability: float = 0.0
+    noise_std: float = 0.0
+    extra_planes: int = 0
+    v2: bool = False
+
+    # runtime (:188-193)
+    batch_size: int = 0
+    minibatch_size: int = 0
+    num_iterations: int = 0
+    masked_wrapper: Optional[str] = None
+    add_pixels: bool = False
+
+    # data parallelism (ppo_atari_multigpu.py:55-102, 166-173)
+    local_num_envs: int = 0  # 0 → num_envs // world_size
+    backend_dist: str = "nccl"  # reference flag `--backend` (gloo|nccl|mpi) clashes with the env
+    device_ids: tuple = ()      # backend above, hence the rename
+    world_size: int = 1
+    local_batch_size: int = 0
+    local_minibatch_size: int = 0
+
+    # [oc_cleanrl_amd] additions
+    num_features: int = 12     # object-vector width F per frame of the synthetic obj env (unpinned
+                               # upstream: OCAtari is un-vendored; 12 = x,y,w,h x 3 Pong objects)
+    obs_storage: str = "auto"  # rollout obs dtype: auto | f32 | bf16 | u8 (auto = exact & compact)
+    cuda_graphs: bool = True   # capture rollout and update into hipGraphs
+    vecnorm_reward: bool = True  # VecNormalize(norm_reward=True) of ppo_atari_oc.py:414
+    log_dir: str = "runs"
+    save_model: bool = True
+    metrics_every: int = 1     # read the device-side metrics every N iterations
+
+
+def _flag_names(name: str) -> list[str]:
+    names = [f"--{name}"]
+    if "_" in name:
+        names.append(f"--{name.replace('_', '-')}")
+    return names
+
+
+def _parse_bool(s: str) -> bool:
+    if s.lower() in ("1", "true", "yes", "on"):
+        return True
+    if s.lower() in ("0", "false", "no", "off"):
+        return False
+    raise argparse.ArgumentTypeError(f"expected a boolean, got {s!r}")
+
+
+def parse_args(argv=None, defaults: dict | None = None) -> Args:
+    """tyro-like CLI over Args. `defaults` overrides dataclass defaults (e.g. per-script)."""
+    base = Args(**(defaults or {}))
+    ap = argparse.ArgumentParser(description="oc_cleanrl_amd PPO (ppo_atari_oc.py surface)")
+    for f in dataclasses.fields(Args):
+        cur = getattr(base, f.name)
+        names = _flag_names(f.name)
+        if isinstance(cur, bool):
+            ap.add_argument(*names, dest=f.name, nargs="?", const=True, type=_parse_bool,
+                            default=cur)
+            ap.add_argument(*[n.replace("--", "--no-", 1) for n in names], dest=f.name,
+                            action="store_false")
+        elif isinstance(cur, tuple):
+            ap.add_argument(*names, dest=f.name, nargs="*", type=int, default=cur)
+        elif f.name in ("target_kl",):
+            ap.add_argument(*names, dest=f.name, type=lambda s: None if s == "None" else float(s),
+                            default=cur)
+        elif cur is None:
+            ap.add_argument(*names, dest=f.name, type=str, default=cur)
+        else:
+            ap.add_argument(*names, dest=f.name, type=type(cur), default=cur)
+    ns = ap.parse_args(sys.argv[1:] if argv is None else argv)
+    d = vars(ns)
+    d["encoder_dims"] = tuple(d["encoder_dims"])
+    d["decoder_dims"] = tuple(d["decoder_dims"])
+    d["device_ids"] = tuple(d["device_ids"])
+    if d["obs_mode"] not in OBS_MODES:
+        ap.error(f"--obs_mode must be one of {OBS_MODES}")
+    return Args(**d)
+
+
+def finalize(args: Args, world_size: int = 1) -> Args:
+    """Derived sizes (ppo_atari_oc.py:344-356; DP: ppo_atari_multigpu.py:166-173)."""
+    args.world_size = world_size
+    if world_size > 1 or args.local_num_envs:
+        if not args.local_num_envs:
+            if args.num_envs % world_size:
+                raise ValueError(f"num_envs={args.num_envs} is not divisible by {world_size}")
+            args.local_num_envs = args.num_envs // world_size
+        args.num_envs = args.local_num_envs * world_size
+    else:
+        args.local_num_envs = args.num_envs
+    args.local_batch_size = int(args.local_num_envs * args.num_steps)
+    args.local_minibatch_size = int(args.local_batch_size // args.num_minibatches)
+    args.batch_size = int(args.num_envs * args.num_steps)
+    args.minibatch_size = int(args.batch_size // args.num_minibatches)
+    args.num_iterations = args.total_timesteps // args.batch_size
+    if "masked" in args.obs_mode:
+        raise NotImplementedError("masked_* observation modes need the un-vendored ocatari_wrappers"
+                                  " (out of scope); use obs_mode dqn or obj")
+    if args.obs_mode == "obj" and args.architecture != "PPO_OBJ":
+        raise AssertionError('"obj" observations only work with "PPO_OBJ" architecture!')
+    if args.local_batch_size % args.num_minibatches:
+        raise ValueError("local batch size must be divisible by num_minibatches")
+    return args
+
+
+def env_rank() -> tuple[int, int, int]:
+    """(rank, local_rank, world_size) from the torchrun environment."""
+    return (int(os.getenv("RANK", "0")), int(os.getenv("LOCAL_RANK", "0")),
+            int(os.getenv("WORLD_SIZE", "1")))

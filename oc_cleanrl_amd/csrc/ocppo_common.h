@@ -23,6 +23,10 @@ int fail(int code, const char* fmt, ...);
     if (!(cond)) return ::ocppo::fail(OCPPO_E_INVALID, __VA_ARGS__); \
   } while (0)
 
+// hipGetLastError() reports the last error of ANY runtime call on this thread (e.g. a benign
+// failed query inside torch). Clear it before our launches so check_launch sees only ours.
+inline void clear_stale_error() { (void)hipGetLastError(); }
+
 // Check the launch that was just issued (also valid while the stream is being captured).
 inline int check_launch(const char* what) {
   hipError_t e = hipGetLastError();

@@ -135,6 +135,7 @@ extern "C" int ocppo_gae(ocppo_stream_t stream, const float* rewards, const floa
   // f32(gamma * gae_lambda) with the product taken in double (Python floats).
   const float g = static_cast<float>(gamma);
   const float gl = static_cast<float>(gamma * gae_lambda);
+  clear_stale_error();
   hipStream_t s = as_stream(stream);
   if (N >= 64 * 1024) {
     constexpr int TILE = 256;

@@ -98,26 +98,77 @@ __device__ __forceinline__ void categorical_backward(const float (&l)[AMAX], flo
 }
 
 // ---- minibatch advantage statistics ------------------------------------------------------------
-// grid = num_mb, one workgroup per minibatch; two passes (mean, then sum of squared deviations).
-__global__ __launch_bounds__(256) void adv_stats_kernel(const float* __restrict__ adv,
-                                                        const int64_t* __restrict__ perm,
-                                                        int64_t M, float* __restrict__ out) {
-  __shared__ float scratch[16];
+// grid = num_mb, one 1024-thread workgroup per minibatch. Each thread first issues all of its
+// index loads, then all of its gathered loads (VPT in flight instead of a dependent chain), keeps
+// the values in registers, and runs the two passes (mean, then squared deviations) from there.
+constexpr int kStatsThreads = 1024;
+template <int VPT>
+__global__ __launch_bounds__(kStatsThreads) void adv_stats_kernel(const float* __restrict__ adv,
+                                                                  const int64_t* __restrict__ perm,
+                                                                  int64_t M, float* __restrict__ out) {
+  __shared__ float scratch[kStatsThreads / kWave];
   const int64_t base = static_cast<int64_t>(blockIdx.x) * M;
+  int64_t idx[VPT];
+  float x[VPT];
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int64_t i = threadIdx.x + static_cast<int64_t>(k) * kStatsThreads;
+    idx[k] = i < M ? (perm ? perm[base + i] : base + i) : -1;
+  }
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) x[k] = idx[k] >= 0 ? adv[idx[k]] : 0.f;
   float s = 0.f;
-  for (int64_t i = threadIdx.x; i < M; i += blockDim.x) s += adv[perm ? perm[base + i] : base + i];
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) s += x[k];
   s = block_sum(s, scratch);
   const float mean = s / static_cast<float>(M);
   float q = 0.f;
-  for (int64_t i = threadIdx.x; i < M; i += blockDim.x) {
+#pragma unroll
+  for (int k = 0; k < VPT; ++k)
+    if (idx[k] >= 0) {
+      const float d = x[k] - mean;
+      q += d * d;
+    }
+  q = block_sum(q, scratch);
+  if (threadIdx.x == 0) {
+    out[2 * blockIdx.x + 0] = mean;
+    out[2 * blockIdx.x + 1] = sqrtf(q / static_cast<float>(M - 1));  // unbiased, torch.std()
+  }
+}
+
+// Any M: strided loops, values re-gathered for the second pass.
+__global__ __launch_bounds__(kStatsThreads) void adv_stats_kernel_any(
+    const float* __restrict__ adv, const int64_t* __restrict__ perm, int64_t M,
+    float* __restrict__ out) {
+  __shared__ float scratch[kStatsThreads / kWave];
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * M;
+  float s = 0.f;
+  for (int64_t i = threadIdx.x; i < M; i += kStatsThreads) s += adv[perm ? perm[base + i] : base + i];
+  s = block_sum(s, scratch);
+  const float mean = s / static_cast<float>(M);
+  float q = 0.f;
+  for (int64_t i = threadIdx.x; i < M; i += kStatsThreads) {
     const float d = adv[perm ? perm[base + i] : base + i] - mean;
     q += d * d;
   }
   q = block_sum(q, scratch);
   if (threadIdx.x == 0) {
     out[2 * blockIdx.x + 0] = mean;
-    out[2 * blockIdx.x + 1] = sqrtf(q / static_cast<float>(M - 1));  // unbiased, torch.std()
+    out[2 * blockIdx.x + 1] = sqrtf(q / static_cast<float>(M - 1));
   }
+}
+
+static void launch_adv_stats(hipStream_t s, const float* adv, const int64_t* perm, int64_t M,
+                             int64_t num_mb, float* out) {
+  const dim3 grid(static_cast<unsigned>(num_mb)), block(kStatsThreads);
+  if (M <= 1 * kStatsThreads)
+    hipLaunchKernelGGL(adv_stats_kernel<1>, grid, block, 0, s, adv, perm, M, out);
+  else if (M <= 4 * kStatsThreads)
+    hipLaunchKernelGGL(adv_stats_kernel<4>, grid, block, 0, s, adv, perm, M, out);
+  else if (M <= 16 * kStatsThreads)
+    hipLaunchKernelGGL(adv_stats_kernel<16>, grid, block, 0, s, adv, perm, M, out);
+  else
+    hipLaunchKernelGGL(adv_stats_kernel_any, grid, block, 0, s, adv, perm, M, out);
 }
 
 // ---- fused loss ----------------------------------------------------------------------------------
@@ -156,23 +207,27 @@ __global__ __launch_bounds__(kLossThreads) void ppo_loss_kernel(LossParams P) {
   const int64_t cnt = (P.M - i0) < kLossThreads ? (P.M - i0) : kLossThreads;
   const int tid = threadIdx.x;
 
+  // issue this element's index and gathered loads first, so their latency overlaps the staging
+  const bool active = tid < cnt;
+  const int64_t i = i0 + tid;
+  int64_t a = 0;
+  float old_lp = 0.f, adv = 0.f, R = 0.f, v_old = 0.f, v = 0.f;
+  if (active) {
+    const int64_t b = P.mb_inds ? P.mb_inds[i] : i;
+    a = P.b_actions[b];
+    old_lp = P.b_logprobs[b];
+    adv = P.b_adv[b];
+    R = P.b_ret[b];
+    v_old = P.b_val[b];
+    v = P.new_value[i];
+  }
   // stage this tile's logits rows (contiguous [cnt*A] floats) with coalesced loads
   for (int64_t e = tid; e < cnt * A; e += kLossThreads) tile[e] = P.logits[i0 * A + e];
   __syncthreads();
 
   float part[kNumPartials] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   float dl[AMAX];
-  const bool active = tid < cnt;
   if (active) {
-    const int64_t i = i0 + tid;
-    const int64_t b = P.mb_inds ? P.mb_inds[i] : i;
-    const int64_t a = P.b_actions[b];
-    const float old_lp = P.b_logprobs[b];
-    const float adv = P.b_adv[b];
-    const float R = P.b_ret[b];
-    const float v_old = P.b_val[b];
-    const float v = P.new_value[i];
-
     float l[AMAX], ln[AMAX], p[AMAX];
 #pragma unroll
     for (int j = 0; j < AMAX; ++j) l[j] = j < A ? tile[tid * A + j] : 0.f;
@@ -262,11 +317,13 @@ __global__ __launch_bounds__(kLossThreads) void ppo_loss_kernel(LossParams P) {
       __hip_atomic_store(&P.partials[blockIdx.x * kNumPartials + k], s, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    // hand-off (MI355X_MICROARCH.md "Valid forms", table row 1): the partials are written
+    // through with sc1 stores, drained, then ONE agent-scope atomic add signals; the last adder
+    // reads them with sc1 loads only. No release/acquire fence, so the dlogits lines this block
+    // just dirtied are not written back from L2 here.
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned prev = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_last = (prev == gridDim.x - 1) ? 1 : 0;
-    if (s_last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
   __syncthreads();
   if (!s_last) return;
@@ -294,7 +351,7 @@ __global__ __launch_bounds__(kLossThreads) void ppo_loss_kernel(LossParams P) {
       for (int w = 1; w < kLossThreads / kWave; ++w) s[k] += red[w][k];
     }
     const float pg_loss = s[0] * P.inv_m;
-    const float v_loss = P.clip_vloss ? 0.5f * (s[1] * P.inv_m) : 0.5f * (s[1] * P.inv_m);
+    const float v_loss = 0.5f * (s[1] * P.inv_m);
     const float ent = s[2] * P.inv_m;
     const float loss = (pg_loss - P.ent_coef * ent) + v_loss * P.vf_coef;
     P.stats[OCPPO_STAT_LOSS] = loss;
@@ -410,8 +467,8 @@ extern "C" int ocppo_minibatch_adv_stats(ocppo_stream_t stream, const float* b_a
                 "ocppo_minibatch_adv_stats: bad sizes M=%lld num_mb=%lld", (long long)M,
                 (long long)num_mb);
   OCPPO_REQUIRE(b_advantages && out, "ocppo_minibatch_adv_stats: null pointer");
-  hipLaunchKernelGGL(adv_stats_kernel, dim3(num_mb), dim3(256), 0, as_stream(stream),
-                     b_advantages, perm, M, out);
+  clear_stale_error();
+  launch_adv_stats(as_stream(stream), b_advantages, perm, M, num_mb, out);
   return check_launch("ocppo_minibatch_adv_stats");
 }
 
@@ -433,11 +490,12 @@ extern "C" int ocppo_ppo_loss_fwd_bwd(ocppo_stream_t stream, const float* logits
   if (!workspace || workspace_bytes < ocppo_ppo_loss_workspace_bytes(M, A))
     return fail(OCPPO_E_WORKSPACE, "ocppo_ppo_loss_fwd_bwd: workspace needs %zu bytes, got %zu",
                 ocppo_ppo_loss_workspace_bytes(M, A), workspace_bytes);
+  clear_stale_error();
   hipStream_t s = as_stream(stream);
   char* ws = static_cast<char*>(workspace);
   if (norm_adv && !adv_stats) {
     float* st = reinterpret_cast<float*>(ws + loss_stats_offset(M));
-    hipLaunchKernelGGL(adv_stats_kernel, dim3(1), dim3(256), 0, s, b_advantages, mb_inds, M, st);
+    launch_adv_stats(s, b_advantages, mb_inds, M, 1, st);
     if (int rc = check_launch("ocppo_ppo_loss_fwd_bwd/adv_stats")) return rc;
     adv_stats = st;
   }
@@ -491,6 +549,7 @@ extern "C" int ocppo_categorical_sample(ocppo_stream_t stream, const float* logi
   OCPPO_REQUIRE(logits && noise && action_out && logprob_out,
                 "ocppo_categorical_sample: null pointer");
   const dim3 grid(ceil_div(N, 256));
+  clear_stale_error();
   hipStream_t s = as_stream(stream);
   if (A <= 8)
     hipLaunchKernelGGL(categorical_sample_kernel<8>, grid, dim3(256), 0, s, logits, noise, N,
@@ -509,6 +568,7 @@ extern "C" int ocppo_categorical_logprob_entropy(ocppo_stream_t stream, const fl
   if (N == 0) return OCPPO_OK;
   OCPPO_REQUIRE(logits && actions, "ocppo_categorical_logprob_entropy: null pointer");
   const dim3 grid(ceil_div(N, 256));
+  clear_stale_error();
   hipStream_t s = as_stream(stream);
   if (A <= 8)
     hipLaunchKernelGGL(categorical_lp_ent_kernel<8>, grid, dim3(256), 0, s, logits, actions, N,
@@ -529,6 +589,7 @@ extern "C" int ocppo_categorical_logprob_entropy_bwd(ocppo_stream_t stream, cons
   if (N == 0) return OCPPO_OK;
   OCPPO_REQUIRE(logits && actions && dlogits, "ocppo_categorical_logprob_entropy_bwd: null pointer");
   const dim3 grid(ceil_div(N, 256));
+  clear_stale_error();
   hipStream_t s = as_stream(stream);
   if (A <= 8)
     hipLaunchKernelGGL(categorical_lp_ent_bwd_kernel<8>, grid, dim3(256), 0, s, logits, actions,

@@ -329,6 +329,7 @@ extern "C" int ocppo_rollout_store(ocppo_stream_t stream, const void* frame, int
   if (N == 0) return OCPPO_OK;
   OCPPO_REQUIRE(frame && reward && done && prev_obs && obs_out, "ocppo_rollout_store: null pointer");
   OCPPO_REQUIRE(prev_obs != obs_out, "ocppo_rollout_store: prev_obs must not alias obs_out");
+  clear_stale_error();
   hipStream_t s = as_stream(stream);
 #define OCPPO_STORE(F, O)                                                                  \
   if (frame_dtype == F && obs_dtype == O)                                                  \
@@ -352,6 +353,7 @@ extern "C" int ocppo_obs_reset(ocppo_stream_t stream, const void* frame, int fra
   OCPPO_REQUIRE(valid_dtype(obs_dtype), "ocppo_obs_reset: bad obs dtype %d", obs_dtype);
   if (N == 0) return OCPPO_OK;
   OCPPO_REQUIRE(frame && obs_out, "ocppo_obs_reset: null pointer");
+  clear_stale_error();
   hipStream_t s = as_stream(stream);
 #define OCPPO_RESET(F, O) \
   if (frame_dtype == F && obs_dtype == O) return launch_reset<F, O>(s, frame, N, W, D, obs_out, net_obs);
@@ -371,6 +373,7 @@ extern "C" int ocppo_gather_rows(ocppo_stream_t stream, const void* src, int src
   OCPPO_REQUIRE(valid_dtype(src_dtype), "ocppo_gather_rows: bad dtype %d", src_dtype);
   if (M == 0) return OCPPO_OK;
   OCPPO_REQUIRE(src && idx && dst, "ocppo_gather_rows: null pointer");
+  clear_stale_error();
   hipStream_t s = as_stream(stream);
   if (src_dtype == OCPPO_F32) return launch_gather<OCPPO_F32>(s, src, idx, M, R, dst);
   if (src_dtype == OCPPO_BF16) return launch_gather<OCPPO_BF16>(s, src, idx, M, R, dst);
@@ -383,6 +386,7 @@ extern "C" int ocppo_vecnorm_reward(ocppo_stream_t stream, const float* reward, 
   OCPPO_REQUIRE(N >= 1, "ocppo_vecnorm_reward: bad size N=%lld", (long long)N);
   OCPPO_REQUIRE(reward && done && ret_state && rms_state && reward_out,
                 "ocppo_vecnorm_reward: null pointer");
+  clear_stale_error();
   hipLaunchKernelGGL(vecnorm_reward_kernel, dim3(1), dim3(1024), 0, as_stream(stream), reward, done,
                      N, gamma, epsilon, clip_reward, ret_state, rms_state, reward_out);
   return check_launch("ocppo_vecnorm_reward");
@@ -397,6 +401,7 @@ extern "C" int ocppo_synth_env_step(ocppo_stream_t stream, uint64_t seed, const 
   OCPPO_REQUIRE(step_base && frame_out && reward_out && done_out,
                 "ocppo_synth_env_step: null pointer");
   const dim3 grid(grid_for(N * D, 256));
+  clear_stale_error();
   if (pixel_mode)
     hipLaunchKernelGGL(synth_env_kernel<true>, grid, dim3(256), 0, as_stream(stream), seed,
                        step_base, step_offset, actions, N, D, frame_out, reward_out, done_out,

@@ -39,6 +39,8 @@ def _opt(t, *a, **k) -> int | None:
 
 
 def _stream(device: torch.device) -> int:
+    if device.type != "cuda":
+        raise ValueError(f"HIP kernels need GPU tensors, got device {device} (no CPU fallback)")
     return torch.cuda.current_stream(device).cuda_stream
 
 

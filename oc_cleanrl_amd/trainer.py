@@ -1,0 +1,418 @@
+"""The PPO actor-learner: cleanrl/ppo_atari_oc.py:339-729 (and its data-parallel twin
+cleanrl/ppo_atari_multigpu.py:162-403) rebuilt around HBM-resident rollout storage, HIP kernels
+for the memory-bound glue and hipGraph replay.
+
+One PPO iteration on one GPU (rank):
+  rollout graph  : T x [agent fwd (PyTorch GEMMs) → Exp(1) draw → HIP action head (writes
+                   actions/logprobs/values rows) → HIP env step → HIP VecNormalize → HIP store
+                   (frame stack + bf16/u8 rollout slot + f32 network input + reward/done rows)]
+                   → bootstrap value → HIP GAE → HIP minibatch advantage stats
+  update graph(s): per minibatch: HIP obs gather → agent fwd → HIP fused loss fwd+bwd (dlogits,
+                   dvalue) → autograd backward of the network into a flat grad buffer →
+                   [RCCL all-reduce SUM of the flat buffer, / world] → clip_grad_norm_ → Adam
+One host sync per iteration (metrics), none per step or per minibatch.
+
+Storage layout (step-major like the reference, :452-459): obs [T+1, N, W, ...] in the rollout
+dtype (slot T is the next iteration's slot 0), actions [T, N] i64, logprobs/rewards [T, N] f32,
+dones/values [T+1, N] f32 (row T = next_done / next_value, the bootstrap of :534).
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+import time
+from dataclasses import asdict
+from pathlib import Path
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from . import ops
+from .agents import make_agent
+from .args import Args
+from .envs import SyntheticAtariEnv
+
+
+def storage_dtype(args: Args, pixels: bool) -> torch.dtype:
+    """Rollout obs dtype. `auto` picks the narrowest EXACT type: u8 for ALE pixels, bf16 for
+    integer object coordinates (|x| <= 256), f32 when detection noise makes them fractional."""
+    choice = args.obs_storage
+    if choice == "auto":
+        if pixels:
+            return torch.uint8
+        return torch.bfloat16 if args.noise_std == 0.0 else torch.float32
+    return {"f32": torch.float32, "bf16": torch.bfloat16, "u8": torch.uint8}[choice]
+
+
+class FlatGrads:
+    """All parameter grads as views of ONE persistent f32 buffer: the DP all-reduce is a single
+    in-place RCCL call (ppo_atari_multigpu.py:360-374 builds the same flat vector with torch.cat
+    and copies it back every minibatch)."""
+
+    def __init__(self, params):
+        self.params = [p for p in params if p.requires_grad]
+        n = sum(p.numel() for p in self.params)
+        dev = self.params[0].device
+        self.buf = torch.zeros(n, dtype=torch.float32, device=dev)
+        off = 0
+        for p in self.params:
+            p.grad = self.buf[off:off + p.numel()].view_as(p)
+            off += p.numel()
+        self.numel = n
+
+    def zero(self):
+        self.buf.zero_()
+
+    def allreduce_mean(self, group=None):
+        ws = dist.get_world_size(group)
+        dist.all_reduce(self.buf, op=dist.ReduceOp.SUM, group=group)
+        self.buf.div_(ws)
+
+
+class KernelTimer:
+    """Per-launch device durations of this package's HIP kernels.
+
+    On ROCm an event cannot be recorded inside a captured graph (torch rejects external events;
+    hipEventRecordWithFlags(.., hipEventRecordExternal) returns hipErrorInvalidValue during
+    capture), so the timed region itself cannot be bracketed per kernel. Instead every bracketed
+    launch site keeps the closure of its first eager launch (same buffers, same stream) and
+    `measure()` replays `reps` back-to-back copies of exactly that launch as one hipGraph between
+    two HIP events: mean launch duration = elapsed / reps (includes the ~1 us graph-node gap;
+    cross-checked against rocprofv3 --kernel-trace in profiles/)."""
+
+    def __init__(self, enabled: bool):
+        self.enabled = enabled
+        self.sites: dict = {}
+        self.per_iter: dict = {}
+        self._counting = True
+        self.mean_us: dict = {}
+
+    def bracket(self, name, fn):
+        if self.enabled and not torch.cuda.is_current_stream_capturing():
+            self.sites.setdefault(name, fn)
+            if self._counting:
+                self.per_iter[name] = self.per_iter.get(name, 0) + 1
+        return fn()
+
+    def end_iteration(self):
+        self._counting = False
+
+    def measure(self, reps: int = 64, rounds: int = 5) -> dict:
+        for name, fn in self.sites.items():
+            fn()
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for _ in range(reps):
+                    fn()
+            g.replay()
+            a = torch.cuda.Event(enable_timing=True)
+            b = torch.cuda.Event(enable_timing=True)
+            a.record()
+            for _ in range(rounds):
+                g.replay()
+            b.record()
+            torch.cuda.synchronize()
+            self.mean_us[name] = 1e3 * a.elapsed_time(b) / (reps * rounds)
+            del g
+        return self.mean_us
+
+
+class PPOTrainer:
+    def __init__(self, args: Args, device, rank: int = 0, world_size: int = 1,
+                 kernel_timing: bool = False, log: bool = True):
+        self.args = args
+        self.dev = torch.device(device)
+        self.rank, self.world = rank, world_size
+        self.log_enabled = log and rank == 0
+        a = args
+        if a.backend != "Synthetic":
+            raise NotImplementedError(f"env backend {a.backend!r} needs ALE/OCAtari (not available);"
+                                      " use --backend Synthetic")
+        torch.use_deterministic_algorithms(a.torch_deterministic)
+        torch.backends.cudnn.deterministic = a.torch_deterministic
+        torch.backends.cudnn.benchmark = False
+
+        # seeding as ppo_atari_multigpu.py:208-212, 230-231: identical init on every rank, then
+        # rank-dependent sampling / env / shuffle streams
+        self.seed = a.seed + rank
+        self.np_rng = np.random.RandomState(self.seed)  # np.random.shuffle stream of :561
+        torch.manual_seed(a.seed)
+
+        self.N = a.local_num_envs
+        self.T = a.num_steps
+        self.env = SyntheticAtariEnv(a.env_id, a.obs_mode, self.N, a.num_features, self.seed,
+                                     self.dev, a.buffer_window_size)
+        self.pixels = self.env.pixels
+        self.A = self.env.n_actions
+        self.obs_shape = self.env.single_obs_shape
+        self.agent = make_agent(a.architecture, self.obs_shape, self.A, self.dev, a.encoder_dims,
+                                a.decoder_dims).to(self.dev)
+        torch.manual_seed(self.seed)
+        self.grads = FlatGrads(self.agent.parameters())
+        self.params = self.grads.params
+        self.lr = torch.tensor(a.learning_rate, dtype=torch.float32, device=self.dev)
+        self.optimizer = torch.optim.Adam(self.params, lr=self.lr, eps=1e-5, fused=True,
+                                          capturable=True)
+
+        T, N = self.T, self.N
+        f32 = torch.float32
+        dev = self.dev
+        self.obs_dtype = storage_dtype(a, self.pixels)
+        self.obs = torch.zeros((T + 1, N) + self.obs_shape, dtype=self.obs_dtype, device=dev)
+        self.net_obs = torch.zeros((N,) + self.obs_shape, dtype=f32, device=dev)
+        self.actions = torch.zeros((T, N), dtype=torch.int64, device=dev)
+        self.logprobs = torch.zeros((T, N), dtype=f32, device=dev)
+        self.rewards = torch.zeros((T, N), dtype=f32, device=dev)
+        self.dones = torch.zeros((T + 1, N), dtype=f32, device=dev)
+        self.values = torch.zeros((T + 1, N), dtype=f32, device=dev)
+        self.advantages = torch.zeros((T, N), dtype=f32, device=dev)
+        self.returns = torch.zeros((T, N), dtype=f32, device=dev)
+        self.noise = torch.zeros((N, self.A), dtype=f32, device=dev)
+        self.ret_state = torch.zeros(N, dtype=torch.float64, device=dev)
+        self.rms_state = torch.tensor([0.0, 1.0, 1e-4], dtype=torch.float64, device=dev)
+
+        # update-phase buffers
+        self.B = a.local_batch_size
+        self.M = a.local_minibatch_size
+        self.E = a.update_epochs
+        self.nmb = a.num_minibatches
+        self.b_inds = np.arange(self.B)
+        self.perm_host = torch.empty(self.E * self.B, dtype=torch.int64, pin_memory=True)
+        self.perm_dev = torch.zeros(self.E * self.B, dtype=torch.int64, device=dev)
+        self.perm_event = torch.cuda.Event()
+        self.perm_event.record()
+        self.adv_stats = torch.zeros((self.E * self.nmb, 2), dtype=f32, device=dev)
+        self.mb_obs = torch.zeros((self.M,) + self.obs_shape, dtype=f32, device=dev)
+        self.dlogits = torch.zeros((self.M, self.A), dtype=f32, device=dev)
+        self.dvalue = torch.zeros(self.M, dtype=f32, device=dev)
+        self.stats = torch.zeros((self.E * self.nmb, len(ops.STAT_NAMES)), dtype=f32, device=dev)
+        self.loss_ws = ops.LossWorkspace(self.M, self.A, dev)
+        self.b_obs = self.obs[:T].view((T * N,) + self.obs_shape)
+
+        self.timer = KernelTimer(kernel_timing)
+        self.graphs_ready = False
+        self.g_rollout = None
+        self.g_update: list = []
+        self.g_opt = None
+        self.iteration = 0
+        self.global_step = 0
+        self.last_metrics: dict = {}
+        self._reset_env()
+
+    # ------------------------------------------------------------------------------------------
+    def _reset_env(self):
+        frame = self.env.reset()
+        ops.obs_reset(frame, self.obs[self.T], self.net_obs)
+        self.dones[self.T].zero_()
+
+    def _rollout_step(self, t: int):
+        a = self.args
+        logits, value = self.agent.logits_and_value(self.net_obs)
+        self.noise.exponential_()
+        self.timer.bracket("action_head", lambda: ops.categorical_sample(
+            logits, self.noise, self.actions[t], self.logprobs[t], None, value.view(-1),
+            self.values[t]))
+        self.timer.bracket("env_step", lambda: self.env.step(self.actions[t], t))
+        if a.vecnorm_reward:
+            self.timer.bracket("vecnorm", lambda: ops.vecnorm_reward(
+                self.env.reward, self.env.done, self.ret_state, self.rms_state, self.rewards[t]))
+        self.timer.bracket("rollout_store", lambda: ops.rollout_store(
+            self.env.frame, self.env.reward, self.env.done, self.obs[t], self.obs[t + 1],
+            self.net_obs, None if a.vecnorm_reward else self.rewards[t], self.dones[t + 1]))
+
+    def _rollout(self):
+        """Rollout (:500-530) + bootstrap + GAE (:533-547) + minibatch adv stats (:577-579)."""
+        a = self.args
+        T = self.T
+        with torch.no_grad():
+            self.obs[0].copy_(self.obs[T])
+            self.dones[0].copy_(self.dones[T])
+            for t in range(T):
+                self._rollout_step(t)
+            self.env.advance(T)
+            self.values[T].copy_(self.agent.get_value(self.net_obs).view(-1))
+            self.timer.bracket("gae", lambda: ops.gae(
+                self.rewards, self.values[:T], self.dones[:T], self.values[T], self.dones[T],
+                a.gamma, a.gae_lambda, self.advantages, self.returns))
+            if a.norm_adv:
+                self.timer.bracket("adv_stats", lambda: ops.minibatch_adv_stats(
+                    self.advantages.view(-1), self.perm_dev, self.M, out=self.adv_stats))
+
+    def _forward_backward(self, j: int):
+        """Minibatch j: gather, forward, fused loss, backward into the flat grad buffer."""
+        a = self.args
+        idx = self.perm_dev[j * self.M:(j + 1) * self.M]
+        self.timer.bracket("gather", lambda: ops.gather_rows(self.b_obs, idx, self.mb_obs))
+        logits, value = self.agent.logits_and_value(self.mb_obs)
+        lg, vv = logits.detach(), value.detach().view(-1)  # the timer's closure must not hold
+        self.timer.bracket("ppo_loss", lambda: ops.ppo_loss_fwd_bwd(  # the autograd graph
+            lg, vv, self.actions.view(-1),
+            self.logprobs.view(-1), self.advantages.view(-1), self.returns.view(-1),
+            self.values[:self.T].reshape(-1), mb_inds=idx,
+            adv_stats=self.adv_stats[j] if a.norm_adv else None, clip_coef=a.clip_coef,
+            ent_coef=a.ent_coef, vf_coef=a.vf_coef, norm_adv=a.norm_adv,
+            clip_vloss=a.clip_vloss, dlogits=self.dlogits, dvalue=self.dvalue,
+            stats=self.stats[j], workspace=self.loss_ws))
+        self.grads.zero()
+        torch.autograd.backward([logits, value], [self.dlogits, self.dvalue.view(-1, 1)])
+
+    def _opt_step(self):
+        nn.utils.clip_grad_norm_(self.params, self.args.max_grad_norm)
+        self.optimizer.step()
+
+    def _update_epoch(self, epoch: int):
+        for k in range(self.nmb):
+            self._forward_backward(epoch * self.nmb + k)
+            if self.world > 1:
+                self.grads.allreduce_mean()
+            self._opt_step()
+
+    # ------------------------------------------------------------------------------------------
+    def _shuffle(self):
+        """np.random.shuffle(b_inds) once per epoch (:561), all epochs up front, then one async
+        copy to the device (the previous iteration's copy finished at its metrics sync)."""
+        self.perm_event.synchronize()  # the previous async copy out of perm_host is done
+        out = self.perm_host.numpy()
+        for e in range(self.E):
+            self.np_rng.shuffle(self.b_inds)
+            out[e * self.B:(e + 1) * self.B] = self.b_inds
+        self.perm_dev.copy_(self.perm_host, non_blocking=True)
+        self.perm_event.record()
+
+    def _capture(self):
+        """Capture the rollout and the update into hipGraphs (after one eager warm-up iteration,
+        which has also created the Adam state)."""
+        torch.cuda.synchronize(self.dev)
+        self.g_rollout = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.g_rollout):
+            self._rollout()
+        pool = self.g_rollout.pool()
+        if self.world == 1:
+            for e in range(self.E):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=pool):
+                    self._update_epoch(e)
+                self.g_update.append(g)
+        else:
+            for j in range(self.E * self.nmb):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=pool):
+                    self._forward_backward(j)
+                self.g_update.append(g)
+            self.g_opt = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.g_opt, pool=pool):
+                self._opt_step()
+        self.graphs_ready = True
+
+    def _run_update(self):
+        a = self.args
+        for e in range(self.E):
+            if self.graphs_ready:
+                if self.world == 1:
+                    self.g_update[e].replay()
+                else:
+                    for k in range(self.nmb):
+                        self.g_update[e * self.nmb + k].replay()
+                        self.grads.allreduce_mean()
+                        self.g_opt.replay()
+            else:
+                self._update_epoch(e)
+            if a.target_kl is not None:
+                kl = float(self.stats[e * self.nmb + self.nmb - 1, 5])
+                if kl > a.target_kl:
+                    break
+
+    # ------------------------------------------------------------------------------------------
+    def train_iteration(self, collect_metrics: bool = True) -> dict:
+        """One PPO iteration (:469-670)."""
+        a = self.args
+        self.iteration += 1
+        if a.anneal_lr:
+            frac = 1.0 - (self.iteration - 1.0) / max(a.num_iterations, 1)
+            self.lr.fill_(frac * a.learning_rate)
+        self._shuffle()
+        use_graphs = a.cuda_graphs and self.iteration > 1
+        if use_graphs and not self.graphs_ready:
+            self._capture()
+        if self.graphs_ready:
+            self.g_rollout.replay()
+        else:
+            self._rollout()
+        self._run_update()
+        self.timer.end_iteration()
+        self.global_step += self.N * self.T * self.world
+        m = {}
+        if collect_metrics:
+            m = self._metrics()
+        return m
+
+    def _metrics(self) -> dict:
+        """Device-side scalars → host once (the reference syncs with .item() ~20 times)."""
+        a = self.args
+        y_true = self.returns.double().view(-1)
+        y_pred = self.values[:self.T].double().reshape(-1)
+        var_y = torch.var(y_true, unbiased=False)
+        ev = 1 - torch.var(y_true - y_pred, unbiased=False) / var_y
+        stats = self.stats.cpu().numpy()  # sync point
+        ep_ret, ep_len, ep_n = self.env.pop_episode_stats()
+        last = stats[-1]
+        m = {
+            "charts/learning_rate": float(self.lr),
+            "losses/value_loss": float(last[2]),
+            "losses/policy_loss": float(last[1]),
+            "losses/entropy": float(last[3]),
+            "losses/old_approx_kl": float(last[4]),
+            "losses/approx_kl": float(last[5]),
+            "losses/clipfrac": float(np.mean(stats[:, 6])),
+            "losses/explained_variance": float("nan") if float(var_y) == 0 else float(ev),
+            "losses/loss": float(last[0]),
+        }
+        if ep_n > 0:
+            m["charts/Episodic_Original_Reward"] = ep_ret / ep_n
+            m["charts/Episodic_Length"] = ep_len / ep_n
+        self.last_metrics = m
+        return m
+
+    # ------------------------------------------------------------------------------------------
+    def state_dict_checkpoint(self) -> dict:
+        """The `.cleanrl_model` payload of ppo_atari_oc.py:486-490."""
+        return {"model_weights": self.agent.state_dict(), "args": asdict(self.args),
+                "Timesteps": self.iteration * self.args.batch_size}
+
+    def save(self, path):
+        torch.save(self.state_dict_checkpoint(), path)
+
+
+def run(args: Args, device=None, rank: int = 0, world_size: int = 1) -> PPOTrainer:
+    """The script body: iterations, SPS, metrics JSONL, checkpoints (rank 0)."""
+    if device is None:
+        device = torch.device(f"cuda:{rank % max(torch.cuda.device_count(), 1)}")
+    tr = PPOTrainer(args, device, rank, world_size)
+    run_name = f"{args.env_id}__{args.exp_name}__{args.seed}__{int(time.time())}".replace("/", "_")
+    run_dir = Path(args.log_dir) / run_name
+    writer = None
+    if rank == 0:
+        run_dir.mkdir(parents=True, exist_ok=True)
+        (run_dir / "args.json").write_text(json.dumps(asdict(args), indent=1, default=str))
+        writer = open(run_dir / "metrics.jsonl", "w")
+    start = time.time()
+    for it in range(1, args.num_iterations + 1):
+        if it % args.checkpoint_interval == 0 and rank == 0 and args.save_model:
+            tr.save(run_dir / f"{args.exp_name}_{it}.cleanrl_model")
+        collect = (it % args.metrics_every == 0) or it == args.num_iterations
+        m = tr.train_iteration(collect_metrics=collect)
+        if writer and m:
+            m["charts/SPS"] = int(tr.global_step / (time.time() - start))
+            m["global_step"] = tr.global_step
+            writer.write(json.dumps(m) + "\n")
+            writer.flush()
+    if rank == 0 and args.save_model:
+        torch.save({"model_weights": tr.agent.state_dict(), "args": asdict(args)},
+                   run_dir / f"{args.exp_name}_final.cleanrl_model")
+    if writer:
+        writer.close()
+    return tr

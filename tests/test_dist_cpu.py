@@ -1,0 +1,93 @@
+"""Data-parallel semantics of ppo_atari_multigpu.py:360-377 on CPU with gloo, world_size 2:
+the flat-buffer gradient all-reduce (FlatGrads) leaves every rank with the mean gradient and
+identical parameters after clip_grad_norm_ + Adam, equal to a single-process run on the mean."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+import torch.nn as nn
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _model():
+    torch.manual_seed(0)  # identical init on every rank (ppo_atari_multigpu.py:210, 230)
+    return nn.Sequential(nn.Linear(6, 16), nn.ReLU(), nn.Linear(16, 3))
+
+
+def _data(rank):
+    g = torch.Generator().manual_seed(100 + rank)  # rank-dependent rollout shard
+    return torch.randn(32, 6, generator=g), torch.randn(32, 3, generator=g)
+
+
+def _step(model, flat, x, y, world):
+    from oc_cleanrl_amd.trainer import FlatGrads  # noqa: F401
+
+    flat.zero()
+    loss = ((model(x) - y) ** 2).mean()
+    loss.backward()
+    if world > 1:
+        flat.allreduce_mean()
+    nn.utils.clip_grad_norm_(model.parameters(), 0.5)
+
+
+def _worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oc_cleanrl_amd.trainer import FlatGrads
+
+    model = _model()
+    flat = FlatGrads(model.parameters())
+    opt = torch.optim.Adam(model.parameters(), lr=1e-2, eps=1e-5)
+    for it in range(3):
+        x, y = _data(rank * 10 + it)
+        _step(model, flat, x, y, world)
+        opt.step()
+    out[rank] = torch.cat([p.detach().flatten() for p in model.parameters()])
+    dist.destroy_process_group()
+
+
+def test_flat_grads_are_views():
+    from oc_cleanrl_amd.trainer import FlatGrads
+
+    m = _model()
+    f = FlatGrads(m.parameters())
+    assert f.numel == sum(p.numel() for p in m.parameters())
+    ((m(torch.randn(4, 6)) ** 2).sum()).backward()
+    assert torch.equal(f.buf, torch.cat([p.grad.flatten() for p in m.parameters()]))
+    f.zero()
+    assert all(float(p.grad.abs().sum()) == 0 for p in m.parameters())
+
+
+def test_two_rank_gloo_allreduce_matches_single_process():
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(2, port, out), nprocs=2, join=True)
+    p0, p1 = out[0], out[1]
+    assert torch.equal(p0, p1), "replicas diverged"
+    # single-process reference: mean of the two ranks' grads each step
+    from oc_cleanrl_amd.trainer import FlatGrads
+
+    model = _model()
+    flat = FlatGrads(model.parameters())
+    opt = torch.optim.Adam(model.parameters(), lr=1e-2, eps=1e-5)
+    for it in range(3):
+        gs = []
+        for rank in range(2):
+            flat.zero()
+            x, y = _data(rank * 10 + it)
+            ((model(x) - y) ** 2).mean().backward()
+            gs.append(flat.buf.clone())
+        flat.buf.copy_((gs[0] + gs[1]) / 2)
+        nn.utils.clip_grad_norm_(model.parameters(), 0.5)
+        opt.step()
+    ref = torch.cat([p.detach().flatten() for p in model.parameters()])
+    torch.testing.assert_close(p0, ref, rtol=1e-6, atol=1e-7)
