@@ -1,0 +1,153 @@
+"""Per-kernel microbenchmark of libocppo_hip.so at the config sizes and at scaled sizes.
+
+Each case builds its inputs on the GPU, captures `reps` back-to-back launches of ONE kernel into a
+hipGraph, and times `rounds` replays with HIP events: mean launch duration = elapsed / (reps x
+rounds). Algorithmic bytes per launch are the DESIGN.md figures, so GB/s = bytes / duration.
+
+    python tools/kernel_bench.py                       # all kernels, config + scaled, JSON lines
+    python tools/kernel_bench.py --kernel gae --size scaled --reps 20   # one case (for rocprofv3)
+
+Scaled sizes are chosen to stream well past the 256 MiB Infinity Cache so that HBM, not the
+on-die caches, bounds them.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+from pathlib import Path
+
+import torch
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+
+from oc_cleanrl_amd import ops  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0
+
+SIZES = {
+    # name: {size: params}
+    "gae": {"config": dict(T=128, N=128), "scaled": dict(T=128, N=262144)},
+    "ppo_loss": {"config": dict(M=4096, A=6, B=16384), "scaled": dict(M=4 * 1024 * 1024, A=6, B=4 * 1024 * 1024)},
+    "gather": {"config": dict(M=4096, B=16384, R=48), "scaled": dict(M=1 << 20, B=1 << 20, R=48)},
+    "rollout_store": {"config": dict(N=128, W=4, D=12), "scaled": dict(N=1 << 20, W=4, D=12)},
+    "action_head": {"config": dict(N=128, A=6), "scaled": dict(N=4 * 1024 * 1024, A=6)},
+    "env_step": {"config": dict(N=128, D=12), "scaled": dict(N=4 * 1024 * 1024, D=12)},
+    "adv_stats": {"config": dict(M=4096, nmb=16, B=16384), "scaled": dict(M=65536, nmb=64, B=1 << 20)},
+}
+
+
+def make_case(name: str, p: dict, dev):
+    """Returns (launch closure, algorithmic bytes per launch)."""
+    g = torch.Generator(device=dev).manual_seed(0)
+    f32 = torch.float32
+    if name == "gae":
+        T, N = p["T"], p["N"]
+        r = torch.randn(T, N, device=dev, generator=g)
+        v = torch.randn(T, N, device=dev, generator=g)
+        d = (torch.rand(T, N, device=dev, generator=g) < 0.01).float()
+        nv, nd = torch.randn(N, device=dev, generator=g), torch.zeros(N, device=dev)
+        adv, ret = torch.empty_like(r), torch.empty_like(r)
+        return (lambda: ops.gae(r, v, d, nv, nd, 0.99, 0.95, adv, ret)), 20 * T * N + 8 * N
+    if name == "ppo_loss":
+        M, A, B = p["M"], p["A"], p["B"]
+        logits = torch.randn(M, A, device=dev, generator=g)
+        val = torch.randn(M, device=dev, generator=g)
+        acts = torch.randint(0, A, (B,), device=dev, generator=g)
+        lp, adv, ret, bv = (torch.randn(B, device=dev, generator=g) for _ in range(4))
+        idx = torch.randperm(B, device=dev, generator=g)[:M]
+        st = ops.minibatch_adv_stats(adv, idx, M)
+        ws = ops.LossWorkspace(M, A, dev)
+        dl, dv, stats = torch.empty_like(logits), torch.empty(M, device=dev), torch.empty(9, device=dev)
+        fn = lambda: ops.ppo_loss_fwd_bwd(  # noqa: E731
+            logits, val, acts, lp, adv, ret, bv, mb_inds=idx, adv_stats=st[0], clip_coef=0.1,
+            ent_coef=0.01, vf_coef=0.5, norm_adv=True, clip_vloss=True, dlogits=dl, dvalue=dv,
+            stats=stats, workspace=ws)
+        return fn, (8 * A + 36) * M
+    if name == "gather":
+        M, B, R = p["M"], p["B"], p["R"]
+        src = torch.randint(0, 200, (B, R), device=dev, generator=g).to(torch.bfloat16)
+        idx = torch.randperm(B, device=dev, generator=g)[:M]
+        out = torch.empty(M, R, device=dev)
+        return (lambda: ops.gather_rows(src, idx, out)), M * (8 + R * 6)
+    if name == "rollout_store":
+        N, W, D = p["N"], p["W"], p["D"]
+        frame = torch.randint(0, 200, (N, D), device=dev, generator=g).float()
+        rew, done = torch.randn(N, device=dev, generator=g), torch.zeros(N, device=dev)
+        prev = torch.randint(0, 200, (N, W, D), device=dev, generator=g).to(torch.bfloat16)
+        out = torch.empty_like(prev)
+        net = torch.empty(N, W, D, device=dev)
+        ro, do = torch.empty(N, device=dev), torch.empty(N, device=dev)
+        fn = lambda: ops.rollout_store(frame, rew, done, prev, out, net, ro, do)  # noqa: E731
+        return fn, N * ((W - 1) * D * 2 + D * 4 + W * D * 6 + 16)
+    if name == "action_head":
+        N, A = p["N"], p["A"]
+        logits = torch.randn(N, A, device=dev, generator=g)
+        noise = torch.empty(N, A, device=dev).exponential_(generator=g)
+        act, lp = torch.empty(N, dtype=torch.int64, device=dev), torch.empty(N, device=dev)
+        vi, vo = torch.randn(N, device=dev, generator=g), torch.empty(N, device=dev)
+        fn = lambda: ops.categorical_sample(logits, noise, act, lp, None, vi, vo)  # noqa: E731
+        return fn, N * (8 * A + 8 + 4 + 8)
+    if name == "env_step":
+        N, D = p["N"], p["D"]
+        base = torch.zeros(1, dtype=torch.int64, device=dev)
+        acts = torch.randint(0, 6, (N,), device=dev, generator=g)
+        frame = torch.empty(N, D, device=dev)
+        rew, done = torch.empty(N, device=dev), torch.empty(N, device=dev)
+        ep = torch.zeros(N, 5, device=dev)
+        fn = lambda: ops.synth_env_step(42, base, 0, acts, frame, rew, done, ep)  # noqa: E731
+        return fn, N * (8 + D * 4 + 8 + 2 * 20)
+    if name == "adv_stats":
+        M, nmb, B = p["M"], p["nmb"], p["B"]
+        adv = torch.randn(B, device=dev, generator=g)
+        reps = (nmb * M + B - 1) // B
+        perm = torch.cat([torch.randperm(B, device=dev, generator=g) for _ in range(reps)])[:nmb * M]
+        out = torch.empty(nmb, 2, device=dev)
+        return (lambda: ops.minibatch_adv_stats(adv, perm, M, out)), 2 * nmb * M * 12
+    raise KeyError(name)
+
+
+def time_case(fn, reps=20, rounds=5) -> float:
+    fn()
+    torch.cuda.synchronize()
+    gr = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gr):
+        for _ in range(reps):
+            fn()
+    gr.replay()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(rounds):
+        gr.replay()
+    b.record()
+    torch.cuda.synchronize()
+    return 1e3 * a.elapsed_time(b) / (reps * rounds)
+
+
+def run_case(name, size, dev, reps=20, rounds=5) -> dict:
+    fn, nbytes = make_case(name, SIZES[name][size], dev)
+    us = time_case(fn, reps, rounds)
+    gbs = nbytes / (us * 1e-6) / 1e9
+    return {"kernel": name, "size": size, "params": SIZES[name][size], "mean_us": round(us, 3),
+            "bytes": nbytes, "GBps": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--kernel", default="all")
+    ap.add_argument("--size", default="all", choices=["all", "config", "scaled"])
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--rounds", type=int, default=5)
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    names = list(SIZES) if a.kernel == "all" else [a.kernel]
+    sizes = ["config", "scaled"] if a.size == "all" else [a.size]
+    for n in names:
+        for s in sizes:
+            print(json.dumps(run_case(n, s, dev, a.reps, a.rounds)), flush=True)
+            torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
