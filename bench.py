@@ -41,20 +41,21 @@ def kernel_bytes(tr) -> dict:
     return {
         # read r, v, d [T,N] + next v/d [N]; write adv, ret [T,N]
         "gae": 20 * T * N + 8 * N,
-        # logits 4A + value 4 + index 8 + action 8 + 4 gathered f32 in; dlogits 4A + dv 4 out
-        "ppo_loss": (8 * A + 36) * M,
+        # logits 4A + value 4 + action 8 + old logprob/adv/return/value 16 in (contiguous,
+        # prepared); dlogits 4A + dv 4 out
+        "ppo_loss": (8 * A + 28) * M,
         # index 8 + row read (storage dtype) + f32 row write
         "gather": M * (8 + W * D * (sb + 4)),
-        # prev slot (W-1 frames) + new frame + done in; slot + f32 net obs out; reward/done rows
-        "rollout_store": N * ((W - 1) * D * sb + D * fb + W * D * (sb + 4) + 16),
-        # logits + noise in, action i64 + logprob + value copy out
-        "action_head": N * (8 * A + 8 + 4 + 8),
+        # prev slot (W-1 frames) + new frame + done in; slot + f32 net obs out; done row; fused
+        # VecNormalize: reward in, ret f64 read/write (2 passes), reward out
+        "rollout_store": N * ((W - 1) * D * sb + D * fb + W * D * (sb + 4) + 8 + 4 + 24 + 4),
+        # hidden row + noise in; action i64 + logprob + value out (the A+1 weight rows are shared,
+        # L2-resident: counted once per launch)
+        "action_head": N * (4 * tr.H + 4 * A + 16) + 4 * (A + 1) * (tr.H + 1),
         # actions in; frame + reward + done + episode counters out (read-modify-write)
         "env_step": N * (8 + D * fb + 8 + 2 * 20),
-        # reward, done, ret (f64) in; ret out, reward out, twice over ret for mean/var
-        "vecnorm": N * (4 + 4 + 8 + 8 + 8 + 4),
-        # perm index + gathered advantage, twice (mean pass, variance pass)
-        "adv_stats": 2 * tr.E * tr.B * (8 + 4),
+        # perm index + 5 gathered per-sample values in, 5 written in minibatch order
+        "mb_prepare": tr.E * tr.B * (8 + 2 * (8 + 16)),
     }
 
 

@@ -87,6 +87,19 @@ OCPPO_API int ocppo_gae(ocppo_stream_t stream, const float* rewards, const float
 OCPPO_API int ocppo_minibatch_adv_stats(ocppo_stream_t stream, const float* b_advantages, const int64_t* perm,
                               int64_t M, int64_t num_mb, float* out);
 
+/* Minibatch prepare: the statistics above AND the per-sample records of every minibatch gathered
+ * into minibatch order, mb_*[k*M + i] = b_*[perm[k*M + i]] (SoA), so that each
+ * ocppo_ppo_loss_fwd_bwd launch can take the already-gathered arrays (mb_inds = NULL) instead of
+ * five scattered loads per element (ppo_atari_oc.py:569-593 index b_* by mb_inds).
+ *   M <= 16384; adv_stats : [num_mb, 2] or NULL (statistics skipped). */
+OCPPO_API int ocppo_minibatch_prepare(ocppo_stream_t stream, const int64_t* perm, int64_t M,
+                                      int64_t num_mb, const int64_t* b_actions,
+                                      const float* b_logprobs, const float* b_advantages,
+                                      const float* b_returns, const float* b_values,
+                                      int64_t* mb_actions, float* mb_logprobs,
+                                      float* mb_advantages, float* mb_returns, float* mb_values,
+                                      float* adv_stats);
+
 /* ---------------------------------------------------------------------------------------------
  * Fused PPO minibatch loss, forward AND backward — replaces ppo_atari_oc.py:566-602 from the
  * network's raw outputs onward (Categorical log-softmax / log_prob / entropy of
@@ -117,6 +130,33 @@ OCPPO_API int ocppo_ppo_loss_fwd_bwd(ocppo_stream_t stream, const float* logits,
                            void* workspace, size_t workspace_bytes);
 
 /* ---------------------------------------------------------------------------------------------
+ * Gradient clipping + Adam over ONE flat buffer — replaces
+ * `nn.utils.clip_grad_norm_(agent.parameters(), max_grad_norm); optimizer.step()` of
+ * ppo_atari_oc.py:608-610 (torch.optim.Adam(lr, eps=1e-5), betas (0.9, 0.999)) and the
+ * `grads / world_size` of ppo_atari_multigpu.py:369-374 (grad_scale = 1/world_size).
+ *   params, grads, exp_avg, exp_avg_sq : [P] f32, 16-byte aligned; every parameter tensor of the
+ *                                        agent is a view into `params` (grads likewise)
+ *   lr       : device f32 scalar (annealed in place, graph-replay safe)
+ *   scalars  : device f32[OCPPO_OPT_NUM_SCALARS], zero-initialised; the step count lives here and
+ *              total_norm (the value clip_grad_norm_ returns) is reported here
+ *   max_norm : <= 0 disables clipping
+ * Math per element, f32: g = (g*grad_scale)*clip; m = b1*m + (1-b1)*g; v = b2*v + (1-b2)*g*g;
+ * p -= (lr/(1-b1^t)) * m / (sqrt(v)/sqrt(1-b2^t) + eps)  (ATen's fused-Adam formula).
+ * ------------------------------------------------------------------------------------------- */
+#define OCPPO_OPT_STEP 0
+#define OCPPO_OPT_TOTAL_NORM 1
+#define OCPPO_OPT_CLIP_COEF 2
+#define OCPPO_OPT_STEP_SIZE 3
+#define OCPPO_OPT_BC2_SQRT 4
+#define OCPPO_OPT_NUM_SCALARS 8
+OCPPO_API size_t ocppo_clip_adam_workspace_bytes(int64_t P);
+OCPPO_API int ocppo_clip_adam_step(ocppo_stream_t stream, float* params, const float* grads,
+                                   float* exp_avg, float* exp_avg_sq, int64_t P, const float* lr,
+                                   double beta1, double beta2, double eps, double grad_scale,
+                                   double max_norm, float* scalars, void* workspace,
+                                   size_t workspace_bytes);
+
+/* ---------------------------------------------------------------------------------------------
  * Rollout action head — replaces Categorical(logits).sample() / log_prob / entropy of
  * architectures/ppo.py:91-95 and the storage writes of ppo_atari_oc.py:506-510.
  * torch's sampler (Categorical.sample → multinomial(probs, 1, True)) draws q ~ Exp(1) of shape
@@ -130,6 +170,21 @@ OCPPO_API int ocppo_ppo_loss_fwd_bwd(ocppo_stream_t stream, const float* logits,
 OCPPO_API int ocppo_categorical_sample(ocppo_stream_t stream, const float* logits, const float* noise,
                              int64_t N, int64_t A, int64_t* action_out, float* logprob_out,
                              float* entropy_out, const float* value_in, float* value_out);
+
+/* Fused rollout policy head: logits = hidden @ w_actor^T + b_actor, value = hidden . w_critic +
+ * b_critic, then the sampler above — replaces the actor/critic Linear layers AND the sampler of
+ * architectures/ppo.py:89-95 for one rollout step (PPObj / PPODefault, shared hidden layer).
+ *   hidden : [N, H] f32 (decoder output);  w_actor : [A, H];  b_actor : [A];  w_critic : [H];
+ *   b_critic : [1];  noise : [N, A] Exp(1);  value_out : [N] (&values[t*N]);
+ *   entropy_out, logits_out ([N, A]) may be NULL.
+ * Logits differ from a GEMM's only by f32 summation order; actions are bit-exact w.r.t. the
+ * sampler applied to the logits this kernel computes (returned in logits_out). */
+OCPPO_API int ocppo_policy_head_sample(ocppo_stream_t stream, const float* hidden, int64_t N,
+                                       int64_t H, const float* w_actor, const float* b_actor,
+                                       const float* w_critic, const float* b_critic,
+                                       const float* noise, int64_t A, int64_t* action_out,
+                                       float* logprob_out, float* entropy_out, float* value_out,
+                                       float* logits_out);
 
 /* log_prob(action) and entropy() of Categorical(logits) for given actions (architectures/ppo.py
  * :92-95 with `action` passed) and the matching backward. */
@@ -183,6 +238,16 @@ OCPPO_API int ocppo_gather_rows(ocppo_stream_t stream, const void* src, int src_
 OCPPO_API int ocppo_vecnorm_reward(ocppo_stream_t stream, const float* reward, const float* done, int64_t N,
                          double gamma, double epsilon, double clip_reward, double* ret_state,
                          double* rms_state, float* reward_out);
+
+/* Rollout store and VecNormalize reward normalisation in ONE launch (one workgroup normalises the
+ * N rewards, the others store): ocppo_rollout_store (reward_out unused) + ocppo_vecnorm_reward.
+ * reward_out (normalised, typically &rewards[t*N]) must not alias reward. */
+OCPPO_API int ocppo_rollout_store_vecnorm(ocppo_stream_t stream, const void* frame, int frame_dtype,
+                                          const float* reward, const float* done, int64_t N,
+                                          int64_t W, int64_t D, const void* prev_obs, void* obs_out,
+                                          int obs_dtype, float* net_obs, float* done_out,
+                                          double gamma, double epsilon, double clip_reward,
+                                          double* ret_state, double* rms_state, float* reward_out);
 
 /* ---------------------------------------------------------------------------------------------
  * Synthetic device-resident env (benchmark / test harness; ALE and OCAtari are not available).

@@ -34,16 +34,22 @@ SIGNATURES: dict[str, tuple[type, list]] = {
     "ocppo_last_error": (ctypes.c_char_p, []),
     "ocppo_gae": (I, [P, P, P, P, P, P, I64, I64, D, D, P, P]),
     "ocppo_minibatch_adv_stats": (I, [P, P, P, I64, I64, P]),
+    "ocppo_minibatch_prepare": (I, [P, P, I64, I64, P, P, P, P, P, P, P, P, P, P, P]),
     "ocppo_ppo_loss_workspace_bytes": (SZ, [I64, I64]),
     "ocppo_ppo_loss_fwd_bwd": (I, [P, P, P, I64, I64, P, P, P, P, P, P, P, D, D, D, I, I, P, P, P,
                                    P, SZ]),
+    "ocppo_clip_adam_workspace_bytes": (SZ, [I64]),
+    "ocppo_clip_adam_step": (I, [P, P, P, P, P, I64, P, D, D, D, D, D, P, P, SZ]),
     "ocppo_categorical_sample": (I, [P, P, P, I64, I64, P, P, P, P, P]),
+    "ocppo_policy_head_sample": (I, [P, P, I64, I64, P, P, P, P, P, I64, P, P, P, P, P]),
     "ocppo_categorical_logprob_entropy": (I, [P, P, P, I64, I64, P, P]),
     "ocppo_categorical_logprob_entropy_bwd": (I, [P, P, P, P, P, I64, I64, P]),
     "ocppo_rollout_store": (I, [P, P, I, P, P, I64, I64, I64, P, P, I, P, P, P]),
     "ocppo_obs_reset": (I, [P, P, I, I64, I64, I64, P, I, P]),
     "ocppo_gather_rows": (I, [P, P, I, P, I64, I64, P]),
     "ocppo_vecnorm_reward": (I, [P, P, P, I64, D, D, D, P, P, P]),
+    "ocppo_rollout_store_vecnorm": (I, [P, P, I, P, P, I64, I64, I64, P, P, I, P, P, D, D, D, P,
+                                        P, P]),
     "ocppo_synth_env_step": (I, [P, U64, P, I64, P, I64, I64, I, P, P, P, P]),
 }
 

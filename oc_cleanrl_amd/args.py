@@ -112,6 +112,7 @@ class Args:
     obs_storage: str = "auto"  # rollout obs dtype: auto | f32 | bf16 | u8 (auto = exact & compact)
     cuda_graphs: bool = True   # capture rollout and update into hipGraphs
     vecnorm_reward: bool = True  # VecNormalize(norm_reward=True) of ppo_atari_oc.py:414
+    fused_optimizer: bool = True  # HIP clip_grad_norm_ + Adam over flat buffers (else torch's)
     log_dir: str = "runs"
     save_model: bool = True
     metrics_every: int = 1     # read the device-side metrics every N iterations

@@ -136,6 +136,61 @@ __global__ __launch_bounds__(kStatsThreads) void adv_stats_kernel(const float* _
   }
 }
 
+// Minibatch prepare: adv_stats_kernel<VPT> plus the per-sample records of every minibatch gathered
+// into minibatch order (SoA), so that each loss launch reads contiguous arrays (no index, no
+// scattered 4-8 B loads). One workgroup per minibatch; all gathers of a thread are in flight
+// together.
+template <int VPT>
+__global__ __launch_bounds__(kStatsThreads) void minibatch_prepare_kernel(
+    const int64_t* __restrict__ perm, int64_t M, const int64_t* __restrict__ b_act,
+    const float* __restrict__ b_lp, const float* __restrict__ b_adv, const float* __restrict__ b_ret,
+    const float* __restrict__ b_val, int64_t* __restrict__ mb_act, float* __restrict__ mb_lp,
+    float* __restrict__ mb_adv, float* __restrict__ mb_ret, float* __restrict__ mb_val,
+    float* __restrict__ stats) {
+  __shared__ float scratch[kStatsThreads / kWave];
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * M;
+  int64_t idx[VPT];
+  float x[VPT];
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int64_t i = threadIdx.x + static_cast<int64_t>(k) * kStatsThreads;
+    idx[k] = i < M ? perm[base + i] : -1;
+  }
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int64_t i = base + threadIdx.x + static_cast<int64_t>(k) * kStatsThreads;
+    if (idx[k] >= 0) {
+      const int64_t b = idx[k];
+      x[k] = b_adv[b];
+      mb_act[i] = b_act[b];
+      mb_lp[i] = b_lp[b];
+      mb_ret[i] = b_ret[b];
+      mb_val[i] = b_val[b];
+      mb_adv[i] = x[k];
+    } else {
+      x[k] = 0.f;
+    }
+  }
+  if (!stats) return;
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) s += x[k];
+  s = block_sum(s, scratch);
+  const float mean = s / static_cast<float>(M);
+  float q = 0.f;
+#pragma unroll
+  for (int k = 0; k < VPT; ++k)
+    if (idx[k] >= 0) {
+      const float d = x[k] - mean;
+      q += d * d;
+    }
+  q = block_sum(q, scratch);
+  if (threadIdx.x == 0) {
+    stats[2 * blockIdx.x + 0] = mean;
+    stats[2 * blockIdx.x + 1] = sqrtf(q / static_cast<float>(M - 1));
+  }
+}
+
 // Any M: strided loops, values re-gathered for the second pass.
 __global__ __launch_bounds__(kStatsThreads) void adv_stats_kernel_any(
     const float* __restrict__ adv, const int64_t* __restrict__ perm, int64_t M,
@@ -444,6 +499,81 @@ __global__ __launch_bounds__(256) void categorical_lp_ent_bwd_kernel(
 
 constexpr int kMaxActions = 32;
 
+// ---- fused rollout policy head ---------------------------------------------------------------------
+// logits = hidden @ W_actor^T + b_actor, value = hidden @ w_critic + b_critic, then the Categorical
+// sample of categorical_sample_kernel. One wave per env: lane l owns hidden[4l + 256k .. +3]
+// (16-B loads, 1 KiB per wave instruction) and the same slice of the A+1 weight rows (L2-resident,
+// shared by every wave), accumulates A+1 partial dots, and a butterfly reduces them (fixed order).
+// Replaces the actor and critic Linear launches + the sampler of architectures/ppo.py:89-95 for a
+// rollout step (the GEMMs have only A+1 = 7 output columns).
+template <int AMAX>
+__global__ __launch_bounds__(256) void policy_head_sample_kernel(
+    const float* __restrict__ hidden, int64_t N, int H, const float* __restrict__ wa,
+    const float* __restrict__ ba, const float* __restrict__ wc, const float* __restrict__ bc,
+    const float* __restrict__ noise, int A, int64_t* __restrict__ action_out,
+    float* __restrict__ logprob_out, float* __restrict__ entropy_out,
+    float* __restrict__ value_out, float* __restrict__ logits_out) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t n = static_cast<int64_t>(blockIdx.x) * (blockDim.x / kWave) + threadIdx.x / kWave;
+  if (n >= N) return;  // wave-uniform
+  const float* h = hidden + n * H;
+  float acc[AMAX + 1];
+#pragma unroll
+  for (int j = 0; j <= AMAX; ++j) acc[j] = 0.f;
+  if ((H & 3) == 0) {
+    for (int k = 4 * lane; k < H; k += 4 * kWave) {
+      const float4 x = *reinterpret_cast<const float4*>(h + k);
+#pragma unroll
+      for (int j = 0; j < AMAX; ++j)
+        if (j < A) {
+          const float4 w = *reinterpret_cast<const float4*>(wa + static_cast<int64_t>(j) * H + k);
+          acc[j] += x.x * w.x + x.y * w.y + x.z * w.z + x.w * w.w;
+        }
+      const float4 w = *reinterpret_cast<const float4*>(wc + k);
+      acc[AMAX] += x.x * w.x + x.y * w.y + x.z * w.z + x.w * w.w;
+    }
+  } else {
+    for (int k = lane; k < H; k += kWave) {
+      const float x = h[k];
+#pragma unroll
+      for (int j = 0; j < AMAX; ++j)
+        if (j < A) acc[j] += x * wa[static_cast<int64_t>(j) * H + k];
+      acc[AMAX] += x * wc[k];
+    }
+  }
+  float l[AMAX];
+#pragma unroll
+  for (int j = 0; j < AMAX; ++j) l[j] = j < A ? wave_sum(acc[j]) + ba[j] : 0.f;
+  const float value = wave_sum(acc[AMAX]) + bc[0];
+  if (lane != 0) return;
+  float ln[AMAX], p[AMAX], lse;
+  categorical_row<AMAX>(l, A, lse, ln, p);
+  int best = 0;
+  float best_q = p[0] / noise[n * A];
+#pragma unroll
+  for (int j = 1; j < AMAX; ++j)
+    if (j < A) {
+      const float q = p[j] / noise[n * A + j];
+      if (q > best_q || (q != q && best_q == best_q)) {
+        best_q = q;
+        best = j;
+      }
+    }
+  float lp = 0.f;
+#pragma unroll
+  for (int j = 0; j < AMAX; ++j)
+    if (j == best) lp = ln[j];
+  action_out[n] = best;
+  logprob_out[n] = lp;
+  value_out[n] = value;
+  if (entropy_out) entropy_out[n] = categorical_entropy<AMAX>(ln, p, A);
+  if (logits_out) {
+#pragma unroll
+    for (int j = 0; j < AMAX; ++j)
+      if (j < A) logits_out[n * A + j] = l[j];
+  }
+}
+
 }  // namespace ocppo
 
 using namespace ocppo;
@@ -598,4 +728,61 @@ extern "C" int ocppo_categorical_logprob_entropy_bwd(ocppo_stream_t stream, cons
     hipLaunchKernelGGL(categorical_lp_ent_bwd_kernel<kMaxActions>, grid, dim3(256), 0, s, logits,
                        actions, grad_logprob, grad_entropy, N, (int)A, dlogits);
   return check_launch("ocppo_categorical_logprob_entropy_bwd");
+}
+
+extern "C" int ocppo_policy_head_sample(ocppo_stream_t stream, const float* hidden, int64_t N,
+                                        int64_t H, const float* w_actor, const float* b_actor,
+                                        const float* w_critic, const float* b_critic,
+                                        const float* noise, int64_t A, int64_t* action_out,
+                                        float* logprob_out, float* entropy_out, float* value_out,
+                                        float* logits_out) {
+  OCPPO_REQUIRE(N >= 0 && H > 0 && H <= INT32_MAX && A > 0 && A <= kMaxActions,
+                "ocppo_policy_head_sample: bad sizes N=%lld H=%lld A=%lld", (long long)N,
+                (long long)H, (long long)A);
+  if (N == 0) return OCPPO_OK;
+  OCPPO_REQUIRE(hidden && w_actor && b_actor && w_critic && b_critic && noise && action_out &&
+                    logprob_out && value_out,
+                "ocppo_policy_head_sample: null pointer");
+  const dim3 grid(static_cast<unsigned>(ceil_div(N, 4))), block(256);
+  clear_stale_error();
+  hipStream_t s = as_stream(stream);
+  if (A <= 8)
+    hipLaunchKernelGGL(policy_head_sample_kernel<8>, grid, block, 0, s, hidden, N, (int)H, w_actor,
+                       b_actor, w_critic, b_critic, noise, (int)A, action_out, logprob_out,
+                       entropy_out, value_out, logits_out);
+  else
+    hipLaunchKernelGGL(policy_head_sample_kernel<kMaxActions>, grid, block, 0, s, hidden, N,
+                       (int)H, w_actor, b_actor, w_critic, b_critic, noise, (int)A, action_out,
+                       logprob_out, entropy_out, value_out, logits_out);
+  return check_launch("ocppo_policy_head_sample");
+}
+
+extern "C" int ocppo_minibatch_prepare(ocppo_stream_t stream, const int64_t* perm, int64_t M,
+                                       int64_t num_mb, const int64_t* b_actions,
+                                       const float* b_logprobs, const float* b_advantages,
+                                       const float* b_returns, const float* b_values,
+                                       int64_t* mb_actions, float* mb_logprobs,
+                                       float* mb_advantages, float* mb_returns, float* mb_values,
+                                       float* adv_stats) {
+  OCPPO_REQUIRE(M > 0 && num_mb > 0 && num_mb <= INT32_MAX && M <= 16 * kStatsThreads,
+                "ocppo_minibatch_prepare: bad sizes M=%lld num_mb=%lld (M <= %d)", (long long)M,
+                (long long)num_mb, 16 * kStatsThreads);
+  OCPPO_REQUIRE(perm && b_actions && b_logprobs && b_advantages && b_returns && b_values &&
+                    mb_actions && mb_logprobs && mb_advantages && mb_returns && mb_values,
+                "ocppo_minibatch_prepare: null pointer");
+  clear_stale_error();
+  hipStream_t s = as_stream(stream);
+  const dim3 grid(static_cast<unsigned>(num_mb)), block(kStatsThreads);
+#define OCPPO_PREP(V)                                                                            \
+  hipLaunchKernelGGL(minibatch_prepare_kernel<V>, grid, block, 0, s, perm, M, b_actions,         \
+                     b_logprobs, b_advantages, b_returns, b_values, mb_actions, mb_logprobs,     \
+                     mb_advantages, mb_returns, mb_values, adv_stats)
+  if (M <= kStatsThreads)
+    OCPPO_PREP(1);
+  else if (M <= 4 * kStatsThreads)
+    OCPPO_PREP(4);
+  else
+    OCPPO_PREP(16);
+#undef OCPPO_PREP
+  return check_launch("ocppo_minibatch_prepare");
 }

@@ -1,0 +1,162 @@
+// Gradient-norm clipping + Adam over ONE flat parameter / gradient / moment buffer
+// (replaces `nn.utils.clip_grad_norm_(agent.parameters(), max_grad_norm); optimizer.step()` of
+// cleanrl/ppo_atari_oc.py:608-610 with torch.optim.Adam(eps=1e-5), and the `/ world_size` of the
+// DP all-reduce, ppo_atari_multigpu.py:369-374).
+//
+//   norm kernel : grid-strided partial sums of (g * grad_scale)^2 per workgroup (16-B loads),
+//                 written through (sc1) + one agent-scope ticket; the last workgroup combines the
+//                 partials in workgroup order and prepares the step scalars:
+//                 total_norm, clip = min(max_norm / (total_norm + 1e-6), 1), step += 1,
+//                 step_size = lr / (1 - beta1^step), bc2_sqrt = sqrt(1 - beta2^step)
+//   adam kernel : g = (g * grad_scale) * clip;  m = beta1*m + (1-beta1)*g;
+//                 v = beta2*v + (1-beta2)*g*g;  p -= step_size * m / (sqrt(v)/bc2_sqrt + eps)
+//                 (the formula of ATen's fused Adam), 16-B vectors, 28 B of HBM per parameter.
+#include "ocppo_common.h"
+
+namespace ocppo {
+
+constexpr int kOptThreads = 256;
+constexpr int kOptBlocks = 1024;  // grid-stride cap for the norm pass (partials in workspace)
+
+// scalars layout (f32): see include/ocppo.h OCPPO_OPT_*
+enum { S_STEP = 0, S_TOTAL_NORM = 1, S_CLIP = 2, S_STEP_SIZE = 3, S_BC2_SQRT = 4 };
+
+__global__ __launch_bounds__(kOptThreads) void grad_norm_kernel(
+    const float* __restrict__ g, int64_t P, float grad_scale, float max_norm,
+    const float* __restrict__ lr, float beta1, float beta2, float* __restrict__ scalars,
+    float* __restrict__ partials, unsigned* __restrict__ ticket) {
+  __shared__ float red[kOptThreads / kWave];
+  __shared__ int s_last;
+  float acc = 0.f;
+  const int64_t P4 = P / 4;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kOptThreads;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kOptThreads + threadIdx.x; i < P4; i += stride) {
+    const float4 x = reinterpret_cast<const float4*>(g)[i];
+    const float a = x.x * grad_scale, b = x.y * grad_scale, c = x.z * grad_scale, d = x.w * grad_scale;
+    acc += a * a + b * b + c * c + d * d;
+  }
+  if (blockIdx.x == 0)
+    for (int64_t i = 4 * P4 + threadIdx.x; i < P; i += kOptThreads) {
+      const float a = g[i] * grad_scale;
+      acc += a * a;
+    }
+  const float w = wave_sum(acc);
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  if (lane == 0) red[wid] = w;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s = red[0];
+    for (int k = 1; k < kOptThreads / kWave; ++k) s += red[k];
+    __hip_atomic_store(&partials[blockIdx.x], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = prev == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  float t = 0.f;
+  for (unsigned b = threadIdx.x; b < gridDim.x; b += kOptThreads)
+    t += __hip_atomic_load(&partials[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const float tw = wave_sum(t);
+  __syncthreads();
+  if (lane == 0) red[wid] = tw;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s = red[0];
+    for (int k = 1; k < kOptThreads / kWave; ++k) s += red[k];
+    const float total = sqrtf(s);
+    float clip = 1.f;
+    if (max_norm > 0.f) {
+      clip = max_norm / (total + 1e-6f);
+      clip = clip < 1.f ? clip : 1.f;
+    }
+    const float step = scalars[S_STEP] + 1.f;
+    const float bc1 = 1.f - powf(beta1, step);
+    const float bc2 = 1.f - powf(beta2, step);
+    scalars[S_STEP] = step;
+    scalars[S_TOTAL_NORM] = total;
+    scalars[S_CLIP] = clip;
+    scalars[S_STEP_SIZE] = lr[0] / bc1;
+    scalars[S_BC2_SQRT] = sqrtf(bc2);
+    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+  }
+}
+
+__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, float b1, float b2,
+                                          float step_size, float bc2_sqrt, float eps) {
+  m = b1 * m + (1.f - b1) * g;
+  v = b2 * v + (1.f - b2) * g * g;
+  const float denom = sqrtf(v) / bc2_sqrt + eps;
+  p = p - step_size * m / denom;
+}
+
+__global__ __launch_bounds__(kOptThreads) void adam_kernel(
+    float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+    float* __restrict__ v, int64_t P, float grad_scale, float b1, float b2, float eps,
+    const float* __restrict__ scalars) {
+  const float clip = scalars[S_CLIP], step_size = scalars[S_STEP_SIZE],
+              bc2_sqrt = scalars[S_BC2_SQRT];
+  const int64_t P4 = P / 4;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kOptThreads;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kOptThreads + threadIdx.x; i < P4; i += stride) {
+    float4 pp = reinterpret_cast<float4*>(p)[i];
+    const float4 gg = reinterpret_cast<const float4*>(g)[i];
+    float4 mm = reinterpret_cast<float4*>(m)[i];
+    float4 vv = reinterpret_cast<float4*>(v)[i];
+    adam_elem(pp.x, (gg.x * grad_scale) * clip, mm.x, vv.x, b1, b2, step_size, bc2_sqrt, eps);
+    adam_elem(pp.y, (gg.y * grad_scale) * clip, mm.y, vv.y, b1, b2, step_size, bc2_sqrt, eps);
+    adam_elem(pp.z, (gg.z * grad_scale) * clip, mm.z, vv.z, b1, b2, step_size, bc2_sqrt, eps);
+    adam_elem(pp.w, (gg.w * grad_scale) * clip, mm.w, vv.w, b1, b2, step_size, bc2_sqrt, eps);
+    reinterpret_cast<float4*>(p)[i] = pp;
+    reinterpret_cast<float4*>(m)[i] = mm;
+    reinterpret_cast<float4*>(v)[i] = vv;
+  }
+  if (blockIdx.x == 0)
+    for (int64_t i = 4 * P4 + threadIdx.x; i < P; i += kOptThreads)
+      adam_elem(p[i], (g[i] * grad_scale) * clip, m[i], v[i], b1, b2, step_size, bc2_sqrt, eps);
+}
+
+}  // namespace ocppo
+
+using namespace ocppo;
+
+extern "C" size_t ocppo_clip_adam_workspace_bytes(int64_t P) {
+  (void)P;
+  return 256 + kOptBlocks * sizeof(float);
+}
+
+extern "C" int ocppo_clip_adam_step(ocppo_stream_t stream, float* params, const float* grads,
+                                    float* exp_avg, float* exp_avg_sq, int64_t P, const float* lr,
+                                    double beta1, double beta2, double eps, double grad_scale,
+                                    double max_norm, float* scalars, void* workspace,
+                                    size_t workspace_bytes) {
+  OCPPO_REQUIRE(P > 0, "ocppo_clip_adam_step: bad size P=%lld", (long long)P);
+  OCPPO_REQUIRE(params && grads && exp_avg && exp_avg_sq && lr && scalars,
+                "ocppo_clip_adam_step: null pointer");
+  OCPPO_REQUIRE((reinterpret_cast<uintptr_t>(params) | reinterpret_cast<uintptr_t>(grads) |
+                 reinterpret_cast<uintptr_t>(exp_avg) | reinterpret_cast<uintptr_t>(exp_avg_sq)) %
+                        16 == 0,
+                "ocppo_clip_adam_step: buffers must be 16-byte aligned");
+  if (!workspace || workspace_bytes < ocppo_clip_adam_workspace_bytes(P))
+    return fail(OCPPO_E_WORKSPACE, "ocppo_clip_adam_step: workspace needs %zu bytes, got %zu",
+                ocppo_clip_adam_workspace_bytes(P), workspace_bytes);
+  char* ws = static_cast<char*>(workspace);
+  unsigned* ticket = reinterpret_cast<unsigned*>(ws);
+  float* partials = reinterpret_cast<float*>(ws + 256);
+  int64_t nb = ceil_div(P / 4 > 0 ? P / 4 : 1, kOptThreads);
+  nb = nb < kOptBlocks ? nb : kOptBlocks;
+  clear_stale_error();
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(grad_norm_kernel, dim3(static_cast<unsigned>(nb)), dim3(kOptThreads), 0, s,
+                     grads, P, static_cast<float>(grad_scale), static_cast<float>(max_norm), lr,
+                     static_cast<float>(beta1), static_cast<float>(beta2), scalars, partials,
+                     ticket);
+  if (int rc = check_launch("ocppo_clip_adam_step/norm")) return rc;
+  int64_t na = ceil_div(P / 4 > 0 ? P / 4 : 1, kOptThreads);
+  na = na < 256 * 8 ? na : 256 * 8;
+  hipLaunchKernelGGL(adam_kernel, dim3(static_cast<unsigned>(na)), dim3(kOptThreads), 0, s, params,
+                     grads, exp_avg, exp_avg_sq, P, static_cast<float>(grad_scale),
+                     static_cast<float>(beta1), static_cast<float>(beta2),
+                     static_cast<float>(eps), scalars);
+  return check_launch("ocppo_clip_adam_step/adam");
+}

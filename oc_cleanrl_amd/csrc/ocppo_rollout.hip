@@ -68,17 +68,19 @@ inline int grid_for(int64_t work, int block) {
 
 // ---- rollout store ----------------------------------------------------------------------------
 // obs_out[n, w, :] = done[n] || w == W-1 ? frame[n, :] : prev_obs[n, w+1, :]
+// Work split over `nblk` workgroups starting at workgroup `blk` (grid-stride).
 template <int FDT, int ODT, int VEC>
-__global__ __launch_bounds__(256) void rollout_store_kernel(
-    const void* __restrict__ frame, const float* __restrict__ reward,
-    const float* __restrict__ done, int64_t N, int W, int64_t D, const void* __restrict__ prev,
-    void* __restrict__ out, float* __restrict__ net, float* __restrict__ reward_out,
-    float* __restrict__ done_out) {
+__device__ __forceinline__ void store_groups(int64_t blk, int64_t nblk, const void* __restrict__ frame,
+                                             const float* __restrict__ reward,
+                                             const float* __restrict__ done, int64_t N, int W,
+                                             int64_t D, const void* __restrict__ prev,
+                                             void* __restrict__ out, float* __restrict__ net,
+                                             float* __restrict__ reward_out,
+                                             float* __restrict__ done_out) {
   const int64_t DG = D / VEC;
   const int64_t groups = N * W * DG;
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
-  for (int64_t g = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; g < groups;
-       g += stride) {
+  const int64_t stride = nblk * blockDim.x;
+  for (int64_t g = blk * blockDim.x + threadIdx.x; g < groups; g += stride) {
     const int64_t n = g / (W * DG);
     const int64_t rem = g - n * W * DG;
     const int w = static_cast<int>(rem / DG);
@@ -101,6 +103,16 @@ __global__ __launch_bounds__(256) void rollout_store_kernel(
       if (done_out) done_out[g] = done[g];
     }
   }
+}
+
+template <int FDT, int ODT, int VEC>
+__global__ __launch_bounds__(256) void rollout_store_kernel(
+    const void* __restrict__ frame, const float* __restrict__ reward,
+    const float* __restrict__ done, int64_t N, int W, int64_t D, const void* __restrict__ prev,
+    void* __restrict__ out, float* __restrict__ net, float* __restrict__ reward_out,
+    float* __restrict__ done_out) {
+  store_groups<FDT, ODT, VEC>(blockIdx.x, gridDim.x, frame, reward, done, N, W, D, prev, out, net,
+                              reward_out, done_out);
 }
 
 template <int FDT, int ODT, int VEC>
@@ -150,12 +162,13 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const void* __restrict
 }
 
 // ---- VecNormalize(norm_obs=False, norm_reward=True) -----------------------------------------------
-// One workgroup (the reduction spans the env axis). f64 like SB3's numpy code.
-// `out` may alias `reward` (in-place normalisation of a rollout row): each element is read and
-// written by the same thread.
-__global__ __launch_bounds__(1024) void vecnorm_reward_kernel(
-    const float* reward, const float* __restrict__ done, int64_t N, double gamma, double eps,
-    double clip, double* __restrict__ ret, double* __restrict__ rms, float* out) {
+// One workgroup (the reduction spans the env axis). f64 like SB3's numpy code. `out` may alias
+// `reward` (in-place normalisation of a rollout row): each element is read and written by the same
+// thread.
+__device__ __forceinline__ void vecnorm_block(const float* reward, const float* __restrict__ done,
+                                              int64_t N, double gamma, double eps, double clip,
+                                              double* __restrict__ ret, double* __restrict__ rms,
+                                              float* out) {
   __shared__ double scratch[16];
   __shared__ double s_var;
   double s = 0.0;
@@ -197,6 +210,30 @@ __global__ __launch_bounds__(1024) void vecnorm_reward_kernel(
     out[n] = static_cast<float>(r);
     if (done[n] != 0.f) ret[n] = 0.0;
   }
+}
+
+__global__ __launch_bounds__(1024) void vecnorm_reward_kernel(
+    const float* reward, const float* __restrict__ done, int64_t N, double gamma, double eps,
+    double clip, double* __restrict__ ret, double* __restrict__ rms, float* out) {
+  vecnorm_block(reward, done, N, gamma, eps, clip, ret, rms, out);
+}
+
+// Store + VecNormalize in ONE launch: workgroup 0 normalises the rewards of all N envs (f64
+// reduction), workgroups 1.. do the frame-stack store. Both halves only read the env outputs, so
+// they need no ordering between them.
+template <int FDT, int ODT, int VEC>
+__global__ __launch_bounds__(256) void store_vecnorm_kernel(
+    const void* __restrict__ frame, const float* __restrict__ reward,
+    const float* __restrict__ done, int64_t N, int W, int64_t D, const void* __restrict__ prev,
+    void* __restrict__ out, float* __restrict__ net, float* __restrict__ done_out, double gamma,
+    double eps, double clip, double* __restrict__ ret, double* __restrict__ rms,
+    float* __restrict__ reward_out) {
+  if (blockIdx.x == 0) {
+    vecnorm_block(reward, done, N, gamma, eps, clip, ret, rms, reward_out);
+    return;
+  }
+  store_groups<FDT, ODT, VEC>(blockIdx.x - 1, gridDim.x - 1, frame, reward, done, N, W, D, prev,
+                              out, net, nullptr, done_out);
 }
 
 // ---- synthetic env ------------------------------------------------------------------------------
@@ -280,6 +317,31 @@ int launch_store(hipStream_t s, const void* frame, const float* reward, const fl
                        0, s, frame, reward, done, N, (int)W, D, prev, out, net, rout, dout);
   }
   return check_launch("ocppo_rollout_store");
+}
+
+struct VecNormArgs {
+  double gamma, eps, clip;
+  double* ret;
+  double* rms;
+  float* reward_out;
+};
+
+template <int FDT, int ODT>
+int launch_store_vecnorm(hipStream_t s, const void* frame, const float* reward, const float* done,
+                         int64_t N, int64_t W, int64_t D, const void* prev, void* out, float* net,
+                         float* dout, const VecNormArgs& vn) {
+  if (D % 4 == 0) {
+    const int64_t groups = N * W * (D / 4);
+    hipLaunchKernelGGL((store_vecnorm_kernel<FDT, ODT, 4>), dim3(1 + grid_for(groups, 256)),
+                       dim3(256), 0, s, frame, reward, done, N, (int)W, D, prev, out, net, dout,
+                       vn.gamma, vn.eps, vn.clip, vn.ret, vn.rms, vn.reward_out);
+  } else {
+    const int64_t groups = N * W * D;
+    hipLaunchKernelGGL((store_vecnorm_kernel<FDT, ODT, 1>), dim3(1 + grid_for(groups, 256)),
+                       dim3(256), 0, s, frame, reward, done, N, (int)W, D, prev, out, net, dout,
+                       vn.gamma, vn.eps, vn.clip, vn.ret, vn.rms, vn.reward_out);
+  }
+  return check_launch("ocppo_rollout_store_vecnorm");
 }
 
 template <int FDT, int ODT>
@@ -411,4 +473,37 @@ extern "C" int ocppo_synth_env_step(ocppo_stream_t stream, uint64_t seed, const 
                        step_base, step_offset, actions, N, D, frame_out, reward_out, done_out,
                        ep_state);
   return check_launch("ocppo_synth_env_step");
+}
+
+extern "C" int ocppo_rollout_store_vecnorm(ocppo_stream_t stream, const void* frame,
+                                           int frame_dtype, const float* reward, const float* done,
+                                           int64_t N, int64_t W, int64_t D, const void* prev_obs,
+                                           void* obs_out, int obs_dtype, float* net_obs,
+                                           float* done_out, double gamma, double epsilon,
+                                           double clip_reward, double* ret_state,
+                                           double* rms_state, float* reward_out) {
+  OCPPO_REQUIRE(N >= 1 && W >= 1 && D >= 1 && W <= 64, "ocppo_rollout_store_vecnorm: bad sizes");
+  OCPPO_REQUIRE(frame_dtype == OCPPO_F32 || frame_dtype == OCPPO_U8,
+                "ocppo_rollout_store_vecnorm: frame dtype must be OCPPO_F32 or OCPPO_U8");
+  OCPPO_REQUIRE(valid_dtype(obs_dtype), "ocppo_rollout_store_vecnorm: bad obs dtype %d", obs_dtype);
+  OCPPO_REQUIRE(frame && reward && done && prev_obs && obs_out && ret_state && rms_state &&
+                    reward_out,
+                "ocppo_rollout_store_vecnorm: null pointer");
+  OCPPO_REQUIRE(prev_obs != obs_out, "ocppo_rollout_store_vecnorm: prev_obs must not alias obs_out");
+  OCPPO_REQUIRE(reward_out != reward, "ocppo_rollout_store_vecnorm: reward_out must not alias reward");
+  const VecNormArgs vn{gamma, epsilon, clip_reward, ret_state, rms_state, reward_out};
+  clear_stale_error();
+  hipStream_t s = as_stream(stream);
+#define OCPPO_SV(F, O)                                                                       \
+  if (frame_dtype == F && obs_dtype == O)                                                    \
+    return launch_store_vecnorm<F, O>(s, frame, reward, done, N, W, D, prev_obs, obs_out,    \
+                                      net_obs, done_out, vn);
+  OCPPO_SV(OCPPO_F32, OCPPO_F32)
+  OCPPO_SV(OCPPO_F32, OCPPO_BF16)
+  OCPPO_SV(OCPPO_F32, OCPPO_U8)
+  OCPPO_SV(OCPPO_U8, OCPPO_F32)
+  OCPPO_SV(OCPPO_U8, OCPPO_BF16)
+  OCPPO_SV(OCPPO_U8, OCPPO_U8)
+#undef OCPPO_SV
+  return fail(OCPPO_E_INVALID, "ocppo_rollout_store_vecnorm: unsupported dtype pair");
 }

@@ -89,6 +89,37 @@ def minibatch_adv_stats(b_advantages, perm, minibatch_size: int, out=None):
     return out
 
 
+def minibatch_prepare(perm, minibatch_size: int, b_actions, b_logprobs, b_advantages, b_returns,
+                      b_values, out: dict | None = None, with_stats: bool = True):
+    """Gather every minibatch's per-sample arrays into minibatch order (+ adv stats).
+
+    Returns dict(actions, logprobs, advantages, returns, values: [num_mb*M], adv_stats [num_mb,2])."""
+    dev = perm.device
+    M = minibatch_size
+    n = perm.numel()
+    if n % M:
+        raise ValueError("perm length must be a multiple of minibatch_size")
+    num_mb = n // M
+    B = b_logprobs.numel()
+    f = torch.float32
+    if out is None:
+        out = {"actions": torch.empty(n, dtype=torch.int64, device=dev),
+               **{k: torch.empty(n, dtype=f, device=dev)
+                  for k in ("logprobs", "advantages", "returns", "values")},
+               "adv_stats": torch.empty((num_mb, 2), dtype=f, device=dev)}
+    call("ocppo_minibatch_prepare", _stream(dev), _check(perm, "perm", torch.int64, dev), M,
+         num_mb, _check(b_actions, "b_actions", torch.int64, dev, B),
+         _check(b_logprobs, "b_logprobs", f, dev, B), _check(b_advantages, "b_advantages", f, dev, B),
+         _check(b_returns, "b_returns", f, dev, B), _check(b_values, "b_values", f, dev, B),
+         _check(out["actions"], "mb_actions", torch.int64, dev, n),
+         _check(out["logprobs"], "mb_logprobs", f, dev, n),
+         _check(out["advantages"], "mb_advantages", f, dev, n),
+         _check(out["returns"], "mb_returns", f, dev, n),
+         _check(out["values"], "mb_values", f, dev, n),
+         _check(out["adv_stats"], "adv_stats", f, dev, 2 * num_mb) if with_stats else None)
+    return out
+
+
 # ---------------------------------------------------------------------------------------------
 # fused PPO loss (ppo_atari_oc.py:566-602 from the network outputs on)
 # ---------------------------------------------------------------------------------------------
@@ -199,6 +230,31 @@ def categorical_sample(logits, noise, action_out=None, logprob_out=None, entropy
     return action_out, logprob_out, entropy_out
 
 
+def policy_head_sample(hidden, w_actor, b_actor, w_critic, b_critic, noise, action_out=None,
+                       logprob_out=None, value_out=None, entropy_out=None, logits_out=None):
+    """Fused actor/critic heads + Categorical sample for a rollout step (no autograd)."""
+    N, H = hidden.shape
+    A = w_actor.shape[0]
+    dev = hidden.device
+    f = torch.float32
+    if tuple(w_actor.shape) != (A, H) or w_critic.numel() != H or b_actor.numel() != A:
+        raise ValueError("head weights do not match hidden")
+    if action_out is None:
+        action_out = torch.empty(N, dtype=torch.int64, device=dev)
+    if logprob_out is None:
+        logprob_out = torch.empty(N, dtype=f, device=dev)
+    if value_out is None:
+        value_out = torch.empty(N, dtype=f, device=dev)
+    call("ocppo_policy_head_sample", _stream(dev), _check(hidden, "hidden", f, dev), N, H,
+         _check(w_actor, "w_actor", f, dev), _check(b_actor, "b_actor", f, dev, A),
+         _check(w_critic, "w_critic", f, dev, H), _check(b_critic, "b_critic", f, dev, 1),
+         _check(noise, "noise", f, dev, N * A), A,
+         _check(action_out, "action_out", torch.int64, dev, N),
+         _check(logprob_out, "logprob_out", f, dev, N), _opt(entropy_out, "entropy_out", f, dev, N),
+         _check(value_out, "value_out", f, dev, N), _opt(logits_out, "logits_out", f, dev, N * A))
+    return action_out, logprob_out, value_out
+
+
 class _CategoricalLogProbEntropy(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, actions):
@@ -258,6 +314,28 @@ def rollout_store(frame, reward, done, prev_obs, obs_out, net_obs=None, reward_o
          _check(obs_out, "obs_out", None, dev), _DTYPE_CODE[obs_out.dtype],
          _opt(net_obs, "net_obs", f, dev, N * W * D), _opt(reward_out, "reward_out", f, dev, N),
          _opt(done_out, "done_out", f, dev, N))
+
+
+def rollout_store_vecnorm(frame, reward, done, prev_obs, obs_out, net_obs, done_out, ret_state,
+                          rms_state, reward_out, gamma=0.99, epsilon=1e-8, clip_reward=10.0):
+    """rollout_store + vecnorm_reward in one launch (reward_out gets the normalised reward)."""
+    N, D = frame.shape[0], frame[0].numel()
+    W = obs_out.shape[1]
+    dev = frame.device
+    if prev_obs.shape != obs_out.shape or prev_obs.dtype != obs_out.dtype:
+        raise ValueError("prev_obs and obs_out must have the same shape and dtype")
+    if tuple(obs_out.shape[:2]) != (N, W) or obs_out[0, 0].numel() != D:
+        raise ValueError(f"obs_out {tuple(obs_out.shape)} does not match frame {tuple(frame.shape)}")
+    f = torch.float32
+    call("ocppo_rollout_store_vecnorm", _stream(dev), _check(frame, "frame", None, dev),
+         _DTYPE_CODE[frame.dtype], _check(reward, "reward", f, dev, N),
+         _check(done, "done", f, dev, N), N, W, D, _check(prev_obs, "prev_obs", None, dev),
+         _check(obs_out, "obs_out", None, dev), _DTYPE_CODE[obs_out.dtype],
+         _opt(net_obs, "net_obs", f, dev, N * W * D), _opt(done_out, "done_out", f, dev, N),
+         float(gamma), float(epsilon), float(clip_reward),
+         _check(ret_state, "ret_state", torch.float64, dev, N),
+         _check(rms_state, "rms_state", torch.float64, dev, 3),
+         _check(reward_out, "reward_out", f, dev, N))
 
 
 def obs_reset(frame, obs_out, net_obs=None):
@@ -320,3 +398,54 @@ def synth_env_step(seed: int, step_base, step_offset: int, actions, frame_out, r
          _check(reward_out, "reward_out", torch.float32, dev, N),
          _check(done_out, "done_out", torch.float32, dev, N),
          _opt(ep_state, "ep_state", torch.float32, dev, N * 5))
+
+
+# ---------------------------------------------------------------------------------------------
+# clip_grad_norm_ + Adam over flat buffers (ppo_atari_oc.py:608-610)
+# ---------------------------------------------------------------------------------------------
+OPT_STEP, OPT_TOTAL_NORM, OPT_CLIP_COEF = 0, 1, 2
+
+
+class FlatAdam:
+    """Adam (torch.optim.Adam semantics, eps as given) + global-norm gradient clipping over ONE
+    flat f32 parameter buffer. Construct it over the module's parameters: every parameter becomes
+    a view of `self.params` and its `.grad` a view of `self.grads` (so the DP all-reduce is one
+    call). `step()` is two HIP launches and is graph-capturable (step count, lr on device)."""
+
+    def __init__(self, params, lr: float, betas=(0.9, 0.999), eps: float = 1e-8,
+                 max_grad_norm: float = 0.0):
+        params = [p for p in params if p.requires_grad]
+        dev = params[0].device
+        n = sum(p.numel() for p in params)
+        self.numel = n
+        self.params = torch.empty(n, dtype=torch.float32, device=dev)
+        self.grads = torch.zeros(n, dtype=torch.float32, device=dev)
+        off = 0
+        for p in params:
+            k = p.numel()
+            if p.dtype != torch.float32:
+                raise ValueError("FlatAdam needs f32 parameters")
+            self.params[off:off + k].copy_(p.detach().reshape(-1))
+            p.data = self.params[off:off + k].view_as(p)
+            p.grad = self.grads[off:off + k].view_as(p)
+            off += k
+        self.param_list = params
+        self.exp_avg = torch.zeros_like(self.params)
+        self.exp_avg_sq = torch.zeros_like(self.params)
+        self.lr = torch.tensor(float(lr), dtype=torch.float32, device=dev)
+        self.scalars = torch.zeros(8, dtype=torch.float32, device=dev)
+        self.betas = (float(betas[0]), float(betas[1]))
+        self.eps = float(eps)
+        self.max_grad_norm = float(max_grad_norm)
+        nb = _lib.LIB.ocppo_clip_adam_workspace_bytes(n)
+        self.ws = torch.zeros(int(nb), dtype=torch.uint8, device=dev)
+
+    def zero_grad(self):
+        self.grads.zero_()
+
+    def step(self, grad_scale: float = 1.0):
+        dev = self.params.device
+        call("ocppo_clip_adam_step", _stream(dev), self.params.data_ptr(), self.grads.data_ptr(),
+             self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(), self.numel,
+             self.lr.data_ptr(), self.betas[0], self.betas[1], self.eps, float(grad_scale),
+             self.max_grad_norm, self.scalars.data_ptr(), self.ws.data_ptr(), self.ws.numel())

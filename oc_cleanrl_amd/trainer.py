@@ -152,11 +152,23 @@ class PPOTrainer:
         self.agent = make_agent(a.architecture, self.obs_shape, self.A, self.dev, a.encoder_dims,
                                 a.decoder_dims).to(self.dev)
         torch.manual_seed(self.seed)
-        self.grads = FlatGrads(self.agent.parameters())
-        self.params = self.grads.params
-        self.lr = torch.tensor(a.learning_rate, dtype=torch.float32, device=self.dev)
-        self.optimizer = torch.optim.Adam(self.params, lr=self.lr, eps=1e-5, fused=True,
-                                          capturable=True)
+        self.fused_head = isinstance(self.agent.actor, nn.Linear) and \
+            isinstance(self.agent.critic, nn.Linear)
+        self.H = self.agent.actor.in_features if self.fused_head else 0
+        if a.fused_optimizer:
+            # every parameter becomes a view of one flat buffer; clip + Adam = 2 HIP launches
+            self.optimizer = ops.FlatAdam(self.agent.parameters(), lr=a.learning_rate, eps=1e-5,
+                                          max_grad_norm=a.max_grad_norm)
+            self.params = self.optimizer.param_list
+            self.grad_buf = self.optimizer.grads
+            self.lr = self.optimizer.lr
+        else:
+            grads = FlatGrads(self.agent.parameters())
+            self.params = grads.params
+            self.grad_buf = grads.buf
+            self.lr = torch.tensor(a.learning_rate, dtype=torch.float32, device=self.dev)
+            self.optimizer = torch.optim.Adam(self.params, lr=self.lr, eps=1e-5, fused=True,
+                                              capturable=True)
 
         T, N = self.T, self.N
         f32 = torch.float32
@@ -185,7 +197,11 @@ class PPOTrainer:
         self.perm_dev = torch.zeros(self.E * self.B, dtype=torch.int64, device=dev)
         self.perm_event = torch.cuda.Event()
         self.perm_event.record()
-        self.adv_stats = torch.zeros((self.E * self.nmb, 2), dtype=f32, device=dev)
+        nmbt = self.E * self.nmb
+        self.mb = {"actions": torch.zeros(nmbt * self.M, dtype=torch.int64, device=dev),
+                   **{k: torch.zeros(nmbt * self.M, dtype=f32, device=dev)
+                      for k in ("logprobs", "advantages", "returns", "values")},
+                   "adv_stats": torch.zeros((nmbt, 2), dtype=f32, device=dev)}
         self.mb_obs = torch.zeros((self.M,) + self.obs_shape, dtype=f32, device=dev)
         self.dlogits = torch.zeros((self.M, self.A), dtype=f32, device=dev)
         self.dvalue = torch.zeros(self.M, dtype=f32, device=dev)
@@ -210,19 +226,31 @@ class PPOTrainer:
         self.dones[self.T].zero_()
 
     def _rollout_step(self, t: int):
+        """One env step of the rollout (:500-514): network trunk (PyTorch) → fused HIP policy
+        head (actor+critic GEMVs + Categorical sample, writes actions/logprobs/values rows) →
+        env → fused HIP store (+ VecNormalize) of the next obs slot and reward/done rows."""
         a = self.args
-        logits, value = self.agent.logits_and_value(self.net_obs)
-        self.noise.exponential_()
-        self.timer.bracket("action_head", lambda: ops.categorical_sample(
-            logits, self.noise, self.actions[t], self.logprobs[t], None, value.view(-1),
-            self.values[t]))
+        ag = self.agent
+        self.noise.exponential_()  # the Exp(1) draw torch's Categorical.sample makes
+        if self.fused_head:
+            hidden = ag.network(self.net_obs)
+            self.timer.bracket("action_head", lambda: ops.policy_head_sample(
+                hidden, ag.actor.weight, ag.actor.bias, ag.critic.weight, ag.critic.bias,
+                self.noise, self.actions[t], self.logprobs[t], self.values[t]))
+        else:
+            logits, value = ag.logits_and_value(self.net_obs)
+            self.timer.bracket("action_head", lambda: ops.categorical_sample(
+                logits, self.noise, self.actions[t], self.logprobs[t], None, value.view(-1),
+                self.values[t]))
         self.timer.bracket("env_step", lambda: self.env.step(self.actions[t], t))
         if a.vecnorm_reward:
-            self.timer.bracket("vecnorm", lambda: ops.vecnorm_reward(
-                self.env.reward, self.env.done, self.ret_state, self.rms_state, self.rewards[t]))
-        self.timer.bracket("rollout_store", lambda: ops.rollout_store(
-            self.env.frame, self.env.reward, self.env.done, self.obs[t], self.obs[t + 1],
-            self.net_obs, None if a.vecnorm_reward else self.rewards[t], self.dones[t + 1]))
+            self.timer.bracket("rollout_store", lambda: ops.rollout_store_vecnorm(
+                self.env.frame, self.env.reward, self.env.done, self.obs[t], self.obs[t + 1],
+                self.net_obs, self.dones[t + 1], self.ret_state, self.rms_state, self.rewards[t]))
+        else:
+            self.timer.bracket("rollout_store", lambda: ops.rollout_store(
+                self.env.frame, self.env.reward, self.env.done, self.obs[t], self.obs[t + 1],
+                self.net_obs, self.rewards[t], self.dones[t + 1]))
 
     def _rollout(self):
         """Rollout (:500-530) + bootstrap + GAE (:533-547) + minibatch adv stats (:577-579)."""
@@ -238,9 +266,11 @@ class PPOTrainer:
             self.timer.bracket("gae", lambda: ops.gae(
                 self.rewards, self.values[:T], self.dones[:T], self.values[T], self.dones[T],
                 a.gamma, a.gae_lambda, self.advantages, self.returns))
-            if a.norm_adv:
-                self.timer.bracket("adv_stats", lambda: ops.minibatch_adv_stats(
-                    self.advantages.view(-1), self.perm_dev, self.M, out=self.adv_stats))
+            # every minibatch's per-sample records in minibatch order + its adv (mean, std)
+            self.timer.bracket("mb_prepare", lambda: ops.minibatch_prepare(
+                self.perm_dev, self.M, self.actions.view(-1), self.logprobs.view(-1),
+                self.advantages.view(-1), self.returns.view(-1), self.values[:T].reshape(-1),
+                out=self.mb, with_stats=a.norm_adv))
 
     def _forward_backward(self, j: int):
         """Minibatch j: gather, forward, fused loss, backward into the flat grad buffer."""
@@ -249,26 +279,37 @@ class PPOTrainer:
         self.timer.bracket("gather", lambda: ops.gather_rows(self.b_obs, idx, self.mb_obs))
         logits, value = self.agent.logits_and_value(self.mb_obs)
         lg, vv = logits.detach(), value.detach().view(-1)  # the timer's closure must not hold
+        sl = slice(j * self.M, (j + 1) * self.M)
+        mb = self.mb
         self.timer.bracket("ppo_loss", lambda: ops.ppo_loss_fwd_bwd(  # the autograd graph
-            lg, vv, self.actions.view(-1),
-            self.logprobs.view(-1), self.advantages.view(-1), self.returns.view(-1),
-            self.values[:self.T].reshape(-1), mb_inds=idx,
-            adv_stats=self.adv_stats[j] if a.norm_adv else None, clip_coef=a.clip_coef,
+            lg, vv, mb["actions"][sl], mb["logprobs"][sl], mb["advantages"][sl],
+            mb["returns"][sl], mb["values"][sl], mb_inds=None,
+            adv_stats=mb["adv_stats"][j] if a.norm_adv else None, clip_coef=a.clip_coef,
             ent_coef=a.ent_coef, vf_coef=a.vf_coef, norm_adv=a.norm_adv,
             clip_vloss=a.clip_vloss, dlogits=self.dlogits, dvalue=self.dvalue,
             stats=self.stats[j], workspace=self.loss_ws))
-        self.grads.zero()
+        self.grad_buf.zero_()
         torch.autograd.backward([logits, value], [self.dlogits, self.dvalue.view(-1, 1)])
 
+    def _allreduce(self):
+        """DP exchange (ppo_atari_multigpu.py:360-374): ONE in-place RCCL all-reduce of the flat
+        grad buffer; the `/ world_size` is folded into the optimizer step (grad_scale)."""
+        dist.all_reduce(self.grad_buf, op=dist.ReduceOp.SUM)
+        if not self.args.fused_optimizer:
+            self.grad_buf.div_(self.world)
+
     def _opt_step(self):
-        nn.utils.clip_grad_norm_(self.params, self.args.max_grad_norm)
-        self.optimizer.step()
+        if self.args.fused_optimizer:
+            self.optimizer.step(grad_scale=1.0 / self.world)
+        else:
+            nn.utils.clip_grad_norm_(self.params, self.args.max_grad_norm)
+            self.optimizer.step()
 
     def _update_epoch(self, epoch: int):
         for k in range(self.nmb):
             self._forward_backward(epoch * self.nmb + k)
             if self.world > 1:
-                self.grads.allreduce_mean()
+                self._allreduce()
             self._opt_step()
 
     # ------------------------------------------------------------------------------------------
@@ -317,7 +358,7 @@ class PPOTrainer:
                 else:
                     for k in range(self.nmb):
                         self.g_update[e * self.nmb + k].replay()
-                        self.grads.allreduce_mean()
+                        self._allreduce()
                         self.g_opt.replay()
             else:
                 self._update_epoch(e)
@@ -380,11 +421,17 @@ class PPOTrainer:
     # ------------------------------------------------------------------------------------------
     def state_dict_checkpoint(self) -> dict:
         """The `.cleanrl_model` payload of ppo_atari_oc.py:486-490."""
-        return {"model_weights": self.agent.state_dict(), "args": asdict(self.args),
+        return {"model_weights": _own_tensors(self.agent.state_dict()), "args": asdict(self.args),
                 "Timesteps": self.iteration * self.args.batch_size}
 
     def save(self, path):
         torch.save(self.state_dict_checkpoint(), path)
+
+
+def _own_tensors(sd: dict) -> dict:
+    """Parameters are views of the optimizer's flat buffer: save standalone copies so the
+    checkpoint holds exactly the reference's tensors."""
+    return {k: v.detach().clone() for k, v in sd.items()}
 
 
 def run(args: Args, device=None, rank: int = 0, world_size: int = 1) -> PPOTrainer:
@@ -411,7 +458,7 @@ def run(args: Args, device=None, rank: int = 0, world_size: int = 1) -> PPOTrain
             writer.write(json.dumps(m) + "\n")
             writer.flush()
     if rank == 0 and args.save_model:
-        torch.save({"model_weights": tr.agent.state_dict(), "args": asdict(args)},
+        torch.save({"model_weights": _own_tensors(tr.agent.state_dict()), "args": asdict(args)},
                    run_dir / f"{args.exp_name}_final.cleanrl_model")
     if writer:
         writer.close()

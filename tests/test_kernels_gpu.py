@@ -325,3 +325,158 @@ def test_synth_env_bitwise_vs_oracle(ops, dev, pixel, N, D):
     assert np.array_equal(frame.cpu().numpy(), ef)
     assert np.array_equal(rew.cpu().numpy(), er)
     assert np.array_equal(done.cpu().numpy(), ed)
+
+
+# ---------------------------------------------------------------------------------------------
+# fused rollout policy head; fused store + VecNormalize
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("N,H,A", [(128, 512, 6), (256, 512, 4), (7, 64, 18), (33, 100, 6),
+                                   (4096, 512, 6)])
+def test_policy_head_sample(ops, dev, N, H, A):
+    g = torch.Generator(device=dev).manual_seed(N + H + A)
+    hidden = torch.relu(torch.randn(N, H, device=dev, generator=g))
+    wa = torch.randn(A, H, device=dev, generator=g) * 0.05
+    ba = torch.randn(A, device=dev, generator=g) * 0.1
+    wc = torch.randn(1, H, device=dev, generator=g)
+    bc = torch.randn(1, device=dev, generator=g)
+    noise = torch.empty(N, A, device=dev).exponential_(generator=g)
+    logits = torch.empty(N, A, device=dev)
+    ent = torch.empty(N, device=dev)
+    act, lp, val = ops.policy_head_sample(hidden, wa, ba, wc, bc, noise, entropy_out=ent,
+                                          logits_out=logits)
+    ref_logits = torch.nn.functional.linear(hidden, wa, ba)
+    ref_value = torch.nn.functional.linear(hidden, wc, bc).view(-1)
+    torch.testing.assert_close(logits, ref_logits, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(val, ref_value, rtol=1e-5, atol=1e-4)
+    # the sampler applied to the head's own logits: bit-exact actions / log-probs / entropy
+    a2, lp2, e2 = ops.categorical_sample(logits, noise, entropy_out=torch.empty(N, device=dev))
+    assert torch.equal(act, a2) and torch.equal(lp, lp2) and torch.equal(ent, e2)
+
+
+@pytest.mark.parametrize("pixel,N,D", [(False, 128, 12), (True, 16, 7056), (False, 1000, 6)])
+def test_store_vecnorm_equals_separate_kernels(ops, dev, pixel, N, D):
+    rng = np.random.default_rng(N)
+    W = 4
+    frame = rng.integers(0, 200, (N, D))
+    frame = T(frame.astype(np.uint8) if pixel else frame.astype(np.float32), dev)
+    prev = T(rng.integers(0, 200, (N, W, D)).astype(np.float32), dev).to(torch.bfloat16)
+    done = T((rng.random(N) < 0.2).astype(np.float32), dev)
+    rew = T(np.where(rng.random(N) < 0.3, 1.0, 0.0).astype(np.float32), dev)
+    ret0 = T(rng.standard_normal(N), dev)
+    rms0 = torch.tensor([0.1, 2.0, 50.0], dtype=torch.float64, device=dev)
+    outs = []
+    for fused in (False, True):
+        ret, rms = ret0.clone(), rms0.clone()
+        o = torch.empty_like(prev)
+        net = torch.empty(N, W, D, device=dev)
+        dout, rout = torch.empty(N, device=dev), torch.empty(N, device=dev)
+        if fused:
+            ops.rollout_store_vecnorm(frame, rew, done, prev, o, net, dout, ret, rms, rout)
+        else:
+            ops.rollout_store(frame, rew, done, prev, o, net, None, dout)
+            ops.vecnorm_reward(rew, done, ret, rms, rout)
+        outs.append((o, net, dout, rout, ret, rms))
+    for x, y in zip(*outs):
+        assert torch.equal(x, y)
+
+
+# ---------------------------------------------------------------------------------------------
+# fused clip_grad_norm_ + Adam over flat buffers
+# ---------------------------------------------------------------------------------------------
+def _mlp(dev, seed=0):
+    torch.manual_seed(seed)
+    return torch.nn.Sequential(torch.nn.Linear(12, 64), torch.nn.ReLU(), torch.nn.Linear(64, 33),
+                               torch.nn.ReLU(), torch.nn.Linear(33, 7)).to(dev)
+
+
+@pytest.mark.parametrize("max_norm,scale", [(0.5, 1.0), (0.0, 1.0), (100.0, 0.25)])
+def test_flat_adam_matches_torch_adam_and_clip(ops, dev, max_norm, scale):
+    a, b = _mlp(dev), _mlp(dev)
+    opt_ref = torch.optim.Adam(a.parameters(), lr=2.5e-4, eps=1e-5)
+    opt = ops.FlatAdam(b.parameters(), lr=2.5e-4, eps=1e-5, max_grad_norm=max_norm)
+    g = torch.Generator(device=dev).manual_seed(1)
+    for it in range(5):
+        x = torch.randn(256, 12, device=dev, generator=g) * 3
+        for p in a.parameters():
+            p.grad = None
+        (a(x) ** 2).mean().backward()
+        for p in a.parameters():
+            p.grad.mul_(scale)
+        gn = torch.nn.utils.clip_grad_norm_(a.parameters(), max_norm) if max_norm > 0 else None
+        opt_ref.step()
+        opt.zero_grad()
+        (b(x) ** 2).mean().backward()
+        opt.step(grad_scale=scale)
+        if gn is not None:
+            torch.testing.assert_close(opt.scalars[1], gn, rtol=1e-5, atol=0)
+    for p, q in zip(a.parameters(), b.parameters()):
+        torch.testing.assert_close(q, p, rtol=2e-5, atol=2e-7)
+    assert float(opt.scalars[0]) == 5.0
+
+
+def test_flat_adam_vs_oracle_bit_level(ops, dev):
+    rng = np.random.default_rng(0)
+    P = 1000003  # not a multiple of 4: exercises the scalar tail
+    p0 = rng.standard_normal(P).astype(np.float32)
+    w = torch.nn.Parameter(T(p0, dev))
+    opt = ops.FlatAdam([w], lr=2.5e-4, eps=1e-5, max_grad_norm=0.5)
+    p, m, v, step = p0, np.zeros(P, np.float32), np.zeros(P, np.float32), 0
+    for it in range(3):
+        gr = (rng.standard_normal(P) * 0.01).astype(np.float32)
+        opt.grads.copy_(T(gr, dev))
+        opt.step()
+        p, m, v, step, total = O.clip_adam_step(p, gr, m, v, step, 2.5e-4, max_norm=0.5)
+        np.testing.assert_allclose(float(opt.scalars[1]), total, rtol=1e-5)
+        np.testing.assert_allclose(opt.exp_avg.cpu().numpy(), m, rtol=2e-6, atol=1e-12)
+        np.testing.assert_allclose(w.detach().cpu().numpy(), p, rtol=1e-6, atol=1e-9)
+
+
+def test_flat_adam_graph_replay(ops, dev):
+    net = _mlp(dev)
+    opt = ops.FlatAdam(net.parameters(), lr=1e-3, eps=1e-5, max_grad_norm=0.5)
+    x = torch.randn(64, 12, device=dev)
+
+    def step():
+        opt.zero_grad()
+        (net(x) ** 2).mean().backward()
+        opt.step()
+
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        step()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        step()
+    before = opt.params.clone()
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    assert float(opt.scalars[0]) == 4.0 and not torch.equal(before, opt.params)
+
+
+def test_minibatch_prepare_then_loss_equals_indexed_loss(ops, dev):
+    rng = np.random.default_rng(9)
+    B, M, A = 16384, 4096, 6
+    b_act = T(rng.integers(0, A, B).astype(np.int64), dev)
+    b_lp, b_adv, b_ret, b_val = (T(rng.standard_normal(B).astype(np.float32), dev) for _ in range(4))
+    perm = T(np.concatenate([rng.permutation(B) for _ in range(2)]).astype(np.int64), dev)
+    mb = ops.minibatch_prepare(perm, M, b_act, b_lp, b_adv, b_ret, b_val)
+    ref_st = ops.minibatch_adv_stats(b_adv, perm, M)
+    assert torch.equal(mb["adv_stats"], ref_st)
+    for k, src in (("actions", b_act), ("logprobs", b_lp), ("advantages", b_adv),
+                   ("returns", b_ret), ("values", b_val)):
+        assert torch.equal(mb[k], src[perm])
+    logits = T(rng.standard_normal((M, A)).astype(np.float32), dev)
+    v = T(rng.standard_normal(M).astype(np.float32), dev)
+    cfg = dict(clip_coef=0.1, ent_coef=0.01, vf_coef=0.5, norm_adv=True, clip_vloss=True)
+    j = 1
+    sl = slice(j * M, (j + 1) * M)
+    a = ops.ppo_loss_fwd_bwd(logits, v, b_act, b_lp, b_adv, b_ret, b_val, mb_inds=perm[sl],
+                             adv_stats=ref_st[j], **cfg)
+    b = ops.ppo_loss_fwd_bwd(logits, v, mb["actions"][sl], mb["logprobs"][sl],
+                             mb["advantages"][sl], mb["returns"][sl], mb["values"][sl],
+                             adv_stats=mb["adv_stats"][j], **cfg)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)

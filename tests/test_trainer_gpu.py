@@ -25,9 +25,10 @@ def run_iters(args, n, dev):
     return tr, ms
 
 
-def test_graph_replay_matches_eager(dev):
-    a, ma = run_iters(small_args(cuda_graphs=False), 3, dev)
-    b, mb = run_iters(small_args(cuda_graphs=True), 3, dev)
+@pytest.mark.parametrize("fused_opt", [True, False])
+def test_graph_replay_matches_eager(dev, fused_opt):
+    a, ma = run_iters(small_args(cuda_graphs=False, fused_optimizer=fused_opt), 3, dev)
+    b, mb = run_iters(small_args(cuda_graphs=True, fused_optimizer=fused_opt), 3, dev)
     assert b.graphs_ready and not a.graphs_ready
     assert torch.equal(a.actions, b.actions)
     assert torch.equal(a.advantages, b.advantages)
@@ -98,3 +99,11 @@ def test_agent_get_action_and_value_api(dev):
     torch.testing.assert_close(ent2, d.entropy(), rtol=1e-6, atol=2e-6)
     lp2.sum().backward()
     assert ag.actor.weight.grad is not None
+
+
+def test_fused_optimizer_tracks_torch_adam(dev):
+    """Same seed, same rollout: HIP clip+Adam and torch clip_grad_norm_ + Adam stay close."""
+    a, _ = run_iters(small_args(fused_optimizer=True), 2, dev)
+    b, _ = run_iters(small_args(fused_optimizer=False), 2, dev)
+    for p, q in zip(a.agent.parameters(), b.agent.parameters()):
+        torch.testing.assert_close(p, q, rtol=1e-4, atol=1e-5)

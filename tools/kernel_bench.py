@@ -34,7 +34,10 @@ SIZES = {
     "rollout_store": {"config": dict(N=128, W=4, D=12), "scaled": dict(N=1 << 20, W=4, D=12)},
     "action_head": {"config": dict(N=128, A=6), "scaled": dict(N=4 * 1024 * 1024, A=6)},
     "env_step": {"config": dict(N=128, D=12), "scaled": dict(N=4 * 1024 * 1024, D=12)},
-    "adv_stats": {"config": dict(M=4096, nmb=16, B=16384), "scaled": dict(M=65536, nmb=64, B=1 << 20)},
+    "adv_stats": {"config": dict(M=4096, nmb=16, B=16384), "scaled": dict(M=16384, nmb=256, B=1 << 20)},
+    "mb_prepare": {"config": dict(M=4096, nmb=16, B=16384), "scaled": dict(M=16384, nmb=256, B=1 << 20)},
+    "ppo_loss_prepared": {"config": dict(M=4096, A=6), "scaled": dict(M=4 * 1024 * 1024, A=6)},
+    "policy_head": {"config": dict(N=128, H=512, A=6), "scaled": dict(N=262144, H=512, A=6)},
 }
 
 
@@ -105,6 +108,39 @@ def make_case(name: str, p: dict, dev):
         perm = torch.cat([torch.randperm(B, device=dev, generator=g) for _ in range(reps)])[:nmb * M]
         out = torch.empty(nmb, 2, device=dev)
         return (lambda: ops.minibatch_adv_stats(adv, perm, M, out)), 2 * nmb * M * 12
+    if name == "mb_prepare":
+        M, nmb, B = p["M"], p["nmb"], p["B"]
+        reps = (nmb * M + B - 1) // B
+        perm = torch.cat([torch.randperm(B, device=dev, generator=g) for _ in range(reps)])[:nmb * M]
+        acts = torch.randint(0, 6, (B,), device=dev, generator=g)
+        lp, adv, ret, bv = (torch.randn(B, device=dev, generator=g) for _ in range(4))
+        out = ops.minibatch_prepare(perm, M, acts, lp, adv, ret, bv)
+        fn = lambda: ops.minibatch_prepare(perm, M, acts, lp, adv, ret, bv, out=out)  # noqa: E731
+        return fn, nmb * M * (8 + 2 * (8 + 16))
+    if name == "ppo_loss_prepared":
+        M, A = p["M"], p["A"]
+        logits = torch.randn(M, A, device=dev, generator=g)
+        val = torch.randn(M, device=dev, generator=g)
+        acts = torch.randint(0, A, (M,), device=dev, generator=g)
+        lp, adv, ret, bv = (torch.randn(M, device=dev, generator=g) for _ in range(4))
+        st = torch.tensor([0.1, 1.3], device=dev)
+        ws = ops.LossWorkspace(M, A, dev)
+        dl, dv, stats = torch.empty_like(logits), torch.empty(M, device=dev), torch.empty(9, device=dev)
+        fn = lambda: ops.ppo_loss_fwd_bwd(  # noqa: E731
+            logits, val, acts, lp, adv, ret, bv, adv_stats=st, clip_coef=0.1, ent_coef=0.01,
+            vf_coef=0.5, norm_adv=True, clip_vloss=True, dlogits=dl, dvalue=dv, stats=stats,
+            workspace=ws)
+        return fn, (8 * A + 28) * M
+    if name == "policy_head":
+        N, H, A = p["N"], p["H"], p["A"]
+        hid = torch.relu(torch.randn(N, H, device=dev, generator=g))
+        wa, ba = torch.randn(A, H, device=dev, generator=g) * 0.05, torch.zeros(A, device=dev)
+        wc, bc = torch.randn(1, H, device=dev, generator=g), torch.zeros(1, device=dev)
+        noise = torch.empty(N, A, device=dev).exponential_(generator=g)
+        act, lp = torch.empty(N, dtype=torch.int64, device=dev), torch.empty(N, device=dev)
+        vo = torch.empty(N, device=dev)
+        fn = lambda: ops.policy_head_sample(hid, wa, ba, wc, bc, noise, act, lp, vo)  # noqa: E731
+        return fn, N * (4 * H + 4 * A + 16) + 4 * (A + 1) * (H + 1)
     raise KeyError(name)
 
 
