@@ -250,6 +250,41 @@ OCPPO_API int ocppo_rollout_store_vecnorm(ocppo_stream_t stream, const void* fra
                                           double* ret_state, double* rms_state, float* reward_out);
 
 /* ---------------------------------------------------------------------------------------------
+ * DQN (config 5, dqn_atari_oc.py) — HBM replay buffer with stable-baselines3 2.0.0
+ * ReplayBuffer(optimize_memory_usage=True, handle_timeout_termination=False) semantics
+ * (:317-325 add at :369, sample at :377), epsilon-greedy (:345-350) and the fused TD target +
+ * MSE loss forward/backward (:378-382). Replay layout: obs [size, E, D] (storage dtype),
+ * actions [size, E] i64, rewards/dones [size, E] f32, state = device i64 {pos, full} (zeroed).
+ * Sampling law = SB3's (indices in [0, pos) or (randint(1, size) + pos) % size once full, env
+ * index uniform); random bits from a counter-based stream (device counter, +1 per call), not numpy.
+ * ------------------------------------------------------------------------------------------- */
+OCPPO_API size_t ocppo_replay_workspace_bytes(void);
+OCPPO_API int ocppo_replay_add(ocppo_stream_t stream, const void* obs, const void* next_obs,
+                               int obs_dtype, const int64_t* actions, const float* rewards,
+                               const float* dones, int64_t E, int64_t D, int64_t* state,
+                               int64_t size, void* rb_obs, int rb_dtype, int64_t* rb_actions,
+                               float* rb_rewards, float* rb_dones, void* workspace);
+/* obs_out / next_obs_out : [B, D] f32; indices_out : [B, 2] {slot, env} or NULL */
+OCPPO_API int ocppo_replay_sample(ocppo_stream_t stream, uint64_t seed, int64_t* counter,
+                                  const int64_t* state, int64_t size, int64_t E, int64_t D,
+                                  const void* rb_obs, int rb_dtype, const int64_t* rb_actions,
+                                  const float* rb_rewards, const float* rb_dones, int64_t B,
+                                  float* obs_out, float* next_obs_out, int64_t* actions_out,
+                                  float* rewards_out, float* dones_out, int64_t* indices_out);
+/* step : device i64 global step; epsilon_out : device f32 or NULL */
+OCPPO_API int ocppo_epsilon_greedy(ocppo_stream_t stream, const float* q, int64_t E, int64_t A,
+                                   uint64_t seed, const int64_t* step, double start_e,
+                                   double end_e, double duration, int64_t* actions,
+                                   float* epsilon_out);
+/* q, q_next : [B, A] f32 (q_network(obs), target_network(next_obs)); dq : [B, A] = d loss / d q;
+ * stats : [2] = {td_loss, mean(old_val)} (losses/td_loss, losses/q_values of :385-386)
+ *   td = r + (f32(gamma) * max_a q_next) * (1 - d);  old = q[b, a_b];  loss = mean((td - old)^2) */
+OCPPO_API int ocppo_td_loss_fwd_bwd(ocppo_stream_t stream, const float* q, const float* q_next,
+                                    const int64_t* actions, const float* rewards,
+                                    const float* dones, int64_t B, int64_t A, double gamma,
+                                    float* dq, float* stats);
+
+/* ---------------------------------------------------------------------------------------------
  * Synthetic device-resident env (benchmark / test harness; ALE and OCAtari are not available).
  * Not a reference component. Counter-based hashing of (seed, env, step) gives reproducible
  * frames: object mode x~U{0..159}, y~U{0..209}, w,h~U{1..16} per 4-feature object; pixel mode

@@ -50,6 +50,12 @@ SIGNATURES: dict[str, tuple[type, list]] = {
     "ocppo_vecnorm_reward": (I, [P, P, P, I64, D, D, D, P, P, P]),
     "ocppo_rollout_store_vecnorm": (I, [P, P, I, P, P, I64, I64, I64, P, P, I, P, P, D, D, D, P,
                                         P, P]),
+    "ocppo_replay_workspace_bytes": (SZ, []),
+    "ocppo_replay_add": (I, [P, P, P, I, P, P, P, I64, I64, P, I64, P, I, P, P, P, P]),
+    "ocppo_replay_sample": (I, [P, U64, P, P, I64, I64, I64, P, I, P, P, P, I64, P, P, P, P, P,
+                                P]),
+    "ocppo_epsilon_greedy": (I, [P, P, I64, I64, U64, P, D, D, D, P, P]),
+    "ocppo_td_loss_fwd_bwd": (I, [P, P, P, P, P, P, I64, I64, D, P, P]),
     "ocppo_synth_env_step": (I, [P, U64, P, I64, P, I64, I64, I, P, P, P, P]),
 }
 

@@ -49,14 +49,62 @@ class Predictor(nn.Module):
             return np.argmax(logits.cpu().numpy(), axis=1), states
 
 
+class _LinearReLU(torch.autograd.Function):
+    """relu(x @ W^T + b) as ONE hipBLASLt GEMM with a bias+ReLU epilogue
+    (torch._addmm_activation), with autograd's own linear+ReLU backward (ATen has no derivative
+    for _addmm_activation): g' = threshold_backward(g, out, 0); dx = g' W; dW = g'^T x; db = sum g'."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        out = torch._addmm_activation(b, x, w.t(), use_gelu=False)
+        ctx.save_for_backward(x, w, out)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w, out = ctx.saved_tensors
+        gp = torch.ops.aten.threshold_backward(g, out, 0)
+        dx = gp.mm(w) if ctx.needs_input_grad[0] else None
+        dw = gp.t().mm(x) if ctx.needs_input_grad[1] else None
+        db = gp.sum(0) if ctx.needs_input_grad[2] else None
+        return dx, dw, db
+
+
+def linear_relu(x, lin: nn.Linear):
+    lead = x.shape[:-1]
+    y = _LinearReLU.apply(x.reshape(-1, x.shape[-1]), lin.weight, lin.bias)
+    return y.view(*lead, y.shape[-1])
+
+
+def fused_trunk(seq: nn.Sequential, x):
+    """Run `seq` with every Linear→ReLU pair as one fused GEMM (same math, fewer launches).
+    Used on GPU tensors; module structure and state-dict keys are untouched."""
+    mods = list(seq)
+    i = 0
+    while i < len(mods):
+        m = mods[i]
+        if (isinstance(m, nn.Linear) and m.bias is not None and i + 1 < len(mods)
+                and isinstance(mods[i + 1], nn.ReLU) and x.is_cuda and x.dtype == torch.float32):
+            x = linear_relu(x, m)
+            i += 2
+        else:
+            x = m(x)
+            i += 1
+    return x
+
+
 class _ActorCritic(Predictor):
     """Shared interface: network → (actor logits, critic value)."""
 
+    def trunk(self, x):
+        return fused_trunk(self.network, x) if isinstance(self.network, nn.Sequential) \
+            else self.network(x)
+
     def get_value(self, x):
-        return self.critic(self.network(x))
+        return self.critic(self.trunk(x))
 
     def logits_and_value(self, x):
-        hidden = self.network(x)
+        hidden = self.trunk(x)
         return self.actor(hidden), self.critic(hidden)
 
     def get_action_and_value(self, x, action=None):

@@ -449,3 +449,94 @@ class FlatAdam:
              self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(), self.numel,
              self.lr.data_ptr(), self.betas[0], self.betas[1], self.eps, float(grad_scale),
              self.max_grad_norm, self.scalars.data_ptr(), self.ws.data_ptr(), self.ws.numel())
+
+
+# ---------------------------------------------------------------------------------------------
+# DQN (config 5): HBM replay buffer, epsilon-greedy, fused TD target + MSE (dqn_atari_oc.py)
+# ---------------------------------------------------------------------------------------------
+class ReplayBuffer:
+    """SB3 ReplayBuffer(optimize_memory_usage=True, handle_timeout_termination=False) in HBM
+    (dqn_atari_oc.py:317-325): obs [size, E, D] in an exact compact dtype, next obs of slot i at
+    slot i+1; device {pos, full} state so add/sample are graph-replayable."""
+
+    def __init__(self, size: int, n_envs: int, obs_shape, device, obs_dtype=torch.uint8,
+                 seed: int = 0):
+        self.size, self.E = int(size), int(n_envs)
+        self.obs_shape = tuple(obs_shape)
+        self.D = 1
+        for d in self.obs_shape:
+            self.D *= d
+        dev = torch.device(device)
+        self.device = dev
+        self.obs = torch.zeros((self.size, self.E) + self.obs_shape, dtype=obs_dtype, device=dev)
+        self.actions = torch.zeros((self.size, self.E), dtype=torch.int64, device=dev)
+        self.rewards = torch.zeros((self.size, self.E), dtype=torch.float32, device=dev)
+        self.dones = torch.zeros((self.size, self.E), dtype=torch.float32, device=dev)
+        self.state = torch.zeros(2, dtype=torch.int64, device=dev)  # pos, full
+        self.counter = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.ws = torch.zeros(int(_lib.LIB.ocppo_replay_workspace_bytes()), dtype=torch.uint8,
+                              device=dev)
+        self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+
+    def add(self, obs, next_obs, actions, rewards, dones):
+        dev = self.device
+        f = torch.float32
+        if obs.dtype not in (torch.float32, torch.uint8) or next_obs.dtype != obs.dtype:
+            raise ValueError("obs/next_obs must both be f32 or u8")
+        n = self.E * self.D
+        call("ocppo_replay_add", _stream(dev), _check(obs, "obs", None, dev, n),
+             _check(next_obs, "next_obs", None, dev, n), _DTYPE_CODE[obs.dtype],
+             _check(actions, "actions", torch.int64, dev, self.E),
+             _check(rewards, "rewards", f, dev, self.E), _check(dones, "dones", f, dev, self.E),
+             self.E, self.D, self.state.data_ptr(), self.size, self.obs.data_ptr(),
+             _DTYPE_CODE[self.obs.dtype], self.actions.data_ptr(), self.rewards.data_ptr(),
+             self.dones.data_ptr(), self.ws.data_ptr())
+
+    def sample(self, batch_size: int, out: dict | None = None, with_indices: bool = False):
+        dev = self.device
+        B = int(batch_size)
+        if out is None:
+            out = {"observations": torch.empty((B,) + self.obs_shape, device=dev),
+                   "next_observations": torch.empty((B,) + self.obs_shape, device=dev),
+                   "actions": torch.empty((B, 1), dtype=torch.int64, device=dev),
+                   "rewards": torch.empty((B, 1), device=dev),
+                   "dones": torch.empty((B, 1), device=dev)}
+            if with_indices:
+                out["indices"] = torch.empty((B, 2), dtype=torch.int64, device=dev)
+        call("ocppo_replay_sample", _stream(dev), self.seed, self.counter.data_ptr(),
+             self.state.data_ptr(), self.size, self.E, self.D, self.obs.data_ptr(),
+             _DTYPE_CODE[self.obs.dtype], self.actions.data_ptr(), self.rewards.data_ptr(),
+             self.dones.data_ptr(), B, out["observations"].data_ptr(),
+             out["next_observations"].data_ptr(), out["actions"].data_ptr(),
+             out["rewards"].data_ptr(), out["dones"].data_ptr(),
+             out["indices"].data_ptr() if "indices" in out else None)
+        return out
+
+
+def epsilon_greedy(q, seed: int, step, start_e: float, end_e: float, duration: float,
+                   actions_out=None, epsilon_out=None):
+    E, A = q.shape
+    dev = q.device
+    if actions_out is None:
+        actions_out = torch.empty(E, dtype=torch.int64, device=dev)
+    call("ocppo_epsilon_greedy", _stream(dev), _check(q, "q", torch.float32, dev), E, A,
+         int(seed) & 0xFFFFFFFFFFFFFFFF, _check(step, "step", torch.int64, dev, 1), float(start_e),
+         float(end_e), float(duration), _check(actions_out, "actions", torch.int64, dev, E),
+         _opt(epsilon_out, "epsilon_out", torch.float32, dev, 1))
+    return actions_out
+
+
+def td_loss_fwd_bwd(q, q_next, actions, rewards, dones, gamma: float, dq=None, stats=None):
+    """(stats [2] = {td_loss, mean q(s,a)}, dq [B, A] = d loss / d q)."""
+    B, A = q.shape
+    dev = q.device
+    f = torch.float32
+    if dq is None:
+        dq = torch.empty_like(q)
+    if stats is None:
+        stats = torch.empty(2, dtype=f, device=dev)
+    call("ocppo_td_loss_fwd_bwd", _stream(dev), _check(q, "q", f, dev),
+         _check(q_next, "q_next", f, dev, B * A), _check(actions, "actions", torch.int64, dev, B),
+         _check(rewards, "rewards", f, dev, B), _check(dones, "dones", f, dev, B), B, A,
+         float(gamma), _check(dq, "dq", f, dev, B * A), _check(stats, "stats", f, dev, 2))
+    return stats, dq

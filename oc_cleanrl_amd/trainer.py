@@ -233,7 +233,7 @@ class PPOTrainer:
         ag = self.agent
         self.noise.exponential_()  # the Exp(1) draw torch's Categorical.sample makes
         if self.fused_head:
-            hidden = ag.network(self.net_obs)
+            hidden = ag.trunk(self.net_obs)
             self.timer.bracket("action_head", lambda: ops.policy_head_sample(
                 hidden, ag.actor.weight, ag.actor.bias, ag.critic.weight, ag.critic.bias,
                 self.noise, self.actions[t], self.logprobs[t], self.values[t]))

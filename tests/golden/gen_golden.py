@@ -16,6 +16,8 @@ Fixtures:
                       autograd grads, and the loss scalars, from the reference update block
   sample_{name}.npz   logits, the Exp(1) noise torch draws, and Categorical.sample()/log_prob/
                       entropy from PPObj.get_action_and_value under a fixed seed
+  td_{name}.npz       dqn_atari_oc.py:378-382 (TD target, gathered Q, MSE loss) exec'd with stub
+                      Q / target networks, plus d loss / d q by autograd
   ppobj_small.npz     a small PPObj's state_dict + input + reference outputs
   init_{name}.json    per-parameter checksums of seeded default-size agents + outputs on a fixed
                       input (pins layer order, state-dict keys and orthogonal init order)
@@ -40,19 +42,22 @@ OUT = Path(__file__).resolve().parent
 SCRIPT = REF / "cleanrl" / "ppo_atari_oc.py"
 GAE_LINES = (533, 547)
 UPDATE_LINES = (566, 610)
+DQN_SCRIPT = REF / "cleanrl" / "dqn_atari_oc.py"
+TD_LINES = (378, 382)
 
 sys.dont_write_bytecode = True
 sys.path.insert(0, str(REF / "cleanrl"))
 from architectures.ppo import PPODefault, PPObj  # noqa: E402  (the reference's own modules)
 
 
-def block(lines):
-    src = SCRIPT.read_text().splitlines()[lines[0] - 1:lines[1]]
-    return compile(textwrap.dedent("\n".join(src)), f"{SCRIPT}:{lines[0]}-{lines[1]}", "exec")
+def block(lines, script=SCRIPT):
+    src = script.read_text().splitlines()[lines[0] - 1:lines[1]]
+    return compile(textwrap.dedent("\n".join(src)), f"{script}:{lines[0]}-{lines[1]}", "exec")
 
 
 GAE_CODE = block(GAE_LINES)
 UPDATE_CODE = block(UPDATE_LINES)
+TD_CODE = block(TD_LINES, DQN_SCRIPT)
 
 
 class Space:
@@ -216,6 +221,27 @@ def gen_init(name, ctor, obs_shape, A, seed, x_scale):
     (OUT / f"init_{name}.json").write_text(json.dumps(info, indent=1))
 
 
+def gen_td(name, B, A, seed):
+    """dqn_atari_oc.py:378-382 with stub q / target networks returning seeded Q values."""
+    rng = np.random.default_rng(seed)
+    q = torch.from_numpy((rng.standard_normal((B, A)) * 2).astype(np.float32)).requires_grad_(True)
+    q_next = torch.from_numpy((rng.standard_normal((B, A)) * 2).astype(np.float32))
+    data = types.SimpleNamespace(
+        observations=torch.zeros(B, 1), next_observations=torch.zeros(B, 1),
+        actions=torch.from_numpy(rng.integers(0, A, (B, 1))),
+        rewards=torch.from_numpy(rng.choice([-1.0, 0.0, 0.0, 0.0, 1.0], (B, 1)).astype(np.float32)),
+        dones=torch.from_numpy((rng.random((B, 1)) < 0.2).astype(np.float32)))
+    ns = dict(torch=torch, F=torch.nn.functional, data=data, args=types.SimpleNamespace(gamma=0.99),
+              q_network=lambda x: q, target_network=lambda x: q_next)
+    exec(TD_CODE, ns)
+    ns["loss"].backward()
+    np.savez_compressed(OUT / f"td_{name}.npz", q=q.detach().numpy(), q_next=q_next.numpy(),
+                        actions=data.actions.numpy().reshape(-1), rewards=data.rewards.numpy().reshape(-1),
+                        dones=data.dones.numpy().reshape(-1), gamma=0.99,
+                        td_target=ns["td_target"].numpy(), loss=ns["loss"].item(),
+                        q_values=ns["old_val"].mean().item(), dq=q.grad.numpy())
+
+
 def main():
     torch.set_num_threads(8)
     gen_gae(16, 8, "synthetic", 1)
@@ -232,6 +258,8 @@ def main():
     gen_sample("n128_a6", 128, 6, 12, 42)
     gen_sample("n256_a4", 256, 4, 6, 43)
     gen_sample("n64_a18", 64, 18, 6, 44)
+    gen_td("b32_a6", 32, 6, 11)
+    gen_td("b256_a18", 256, 18, 12)
     gen_ppobj_small()
     gen_init("ppobj_f12_a6", lambda e: PPObj(e, "cpu", (256, 512, 1024, 512), (512,)), (4, 12), 6,
              1, 160.0)

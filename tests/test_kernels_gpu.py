@@ -427,7 +427,10 @@ def test_flat_adam_vs_oracle_bit_level(ops, dev):
         opt.step()
         p, m, v, step, total = O.clip_adam_step(p, gr, m, v, step, 2.5e-4, max_norm=0.5)
         np.testing.assert_allclose(float(opt.scalars[1]), total, rtol=1e-5)
-        np.testing.assert_allclose(opt.exp_avg.cpu().numpy(), m, rtol=2e-6, atol=1e-12)
+        # the clip coefficient (f32 on device, f64 norm in the oracle) may differ by an ulp,
+        # so compare at the scale of the moments / the update, not element-relative
+        np.testing.assert_allclose(opt.exp_avg.cpu().numpy(), m, rtol=0,
+                                   atol=2e-6 * np.abs(m).max())
         np.testing.assert_allclose(w.detach().cpu().numpy(), p, rtol=1e-6, atol=1e-9)
 
 
@@ -480,3 +483,56 @@ def test_minibatch_prepare_then_loss_equals_indexed_loss(ops, dev):
                              adv_stats=mb["adv_stats"][j], **cfg)
     for x, y in zip(a, b):
         assert torch.equal(x, y)
+
+
+# ---------------------------------------------------------------------------------------------
+# DQN: fused TD loss, epsilon-greedy, HBM replay buffer
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("name", ["td_b32_a6.npz", "td_b256_a18.npz"])
+def test_td_loss_golden(ops, dev, name):
+    z = golden(name)
+    stats, dq = ops.td_loss_fwd_bwd(T(z["q"], dev), T(z["q_next"], dev), T(z["actions"], dev),
+                                    T(z["rewards"], dev), T(z["dones"], dev), float(z["gamma"]))
+    np.testing.assert_allclose(stats.cpu().numpy(), [z["loss"], z["q_values"]], rtol=1e-6)
+    assert np.array_equal(dq.cpu().numpy().view(np.uint32), z["dq"].view(np.uint32))
+
+
+def test_epsilon_greedy(ops, dev):
+    q = torch.randn(64, 6, device=dev)
+    step = torch.tensor([10_000_000], dtype=torch.int64, device=dev)  # epsilon = end_e
+    eps = torch.empty(1, device=dev)
+    a = ops.epsilon_greedy(q, 1, step, 1.0, 0.0, 1000.0, epsilon_out=eps)
+    assert float(eps) == 0.0 and torch.equal(a, q.argmax(1))
+    step.fill_(0)  # epsilon = 1: every action random, uniform over A
+    seen = torch.zeros(6, device=dev)
+    for t in range(200):
+        step.fill_(t)
+        a = ops.epsilon_greedy(q, 1, step, 1.0, 1.0, 1e9)
+        seen += torch.bincount(a, minlength=6).float()
+    assert seen.min() > 0.1 * seen.mean()
+
+
+@pytest.mark.parametrize("dt", [torch.uint8, torch.bfloat16])
+def test_replay_buffer_semantics(ops, dev, dt):
+    from oracle import ocppo_oracle as O
+
+    size, E, shape = 10, 2, (4, 3)
+    rb = ops.ReplayBuffer(size, E, shape, dev, obs_dtype=dt, seed=3)
+    frames = [torch.full((E,) + shape, float(i), device=dev) + torch.arange(E, device=dev).view(E, 1, 1) * 100
+              for i in range(14)]
+    for i in range(13):  # wraps around once
+        rb.add(frames[i], frames[i + 1], torch.full((E,), i, device=dev, dtype=torch.int64),
+               torch.full((E,), float(i), device=dev), torch.zeros(E, device=dev))
+        st = rb.state.cpu().tolist()
+        assert st == [(i + 1) % size, int(i + 1 >= size)]
+        out = rb.sample(64, with_indices=True)
+        idx = out["indices"].cpu().numpy()
+        allowed = O.replay_sample_law(st[0], st[1], size, 64)
+        assert set(idx[:, 0].tolist()) <= allowed
+        # obs of slot s is transition s's obs, the next obs is slot s+1's content
+        for b in range(64):
+            s, e = idx[b]
+            tr = int(out["actions"][b])  # action == transition number
+            assert float(out["rewards"][b]) == tr
+            assert torch.equal(out["observations"][b], frames[tr][e].float())
+            assert torch.equal(out["next_observations"][b], frames[tr + 1][e].float())

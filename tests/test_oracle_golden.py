@@ -113,3 +113,13 @@ def test_synth_env_oracle_ranges():
     assert f[:, 0::4].max() < 160 and f[:, 1::4].max() < 210 and f[:, 2::4].min() >= 1
     p, _, _ = O.synth_env_step(42, 7, None, 4, 7056, True)
     assert p.dtype == np.uint8 and (p == 0).mean() > 0.8
+
+
+@pytest.mark.parametrize("name", ["td_b32_a6.npz", "td_b256_a18.npz"])
+def test_td_loss_matches_reference(name):
+    z = golden(name)
+    stats, dq, td = O.td_loss_fwd_bwd(z["q"], z["q_next"], z["actions"], z["rewards"], z["dones"],
+                                      float(z["gamma"]))
+    assert np.array_equal(td.view(np.uint32), z["td_target"].view(np.uint32))  # bit-exact
+    np.testing.assert_allclose(stats, [z["loss"], z["q_values"]], rtol=1e-6)
+    assert np.array_equal(dq.view(np.uint32), z["dq"].view(np.uint32))  # bit-exact

@@ -107,3 +107,20 @@ def test_fused_optimizer_tracks_torch_adam(dev):
     b, _ = run_iters(small_args(fused_optimizer=False), 2, dev)
     for p, q in zip(a.agent.parameters(), b.agent.parameters()):
         torch.testing.assert_close(p, q, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("arch,obs", [("PPO_OBJ", (4, 12)), ("PPO", (4, 84, 84))])
+def test_fused_trunk_matches_module_forward_and_grads(dev, arch, obs):
+    from oc_cleanrl_amd.agents import make_agent
+
+    torch.manual_seed(0)
+    ag = make_agent(arch, obs, 6, dev, (64, 128), (64,)).to(dev)
+    x = torch.randint(0, 160, (32,) + obs, device=dev).float()
+    h1 = ag.network(x)
+    h2 = ag.trunk(x)
+    torch.testing.assert_close(h2, h1, rtol=1e-6, atol=1e-6)
+    g = torch.randn_like(h1)
+    gr1 = torch.autograd.grad(h1, list(ag.parameters()), g)
+    gr2 = torch.autograd.grad(h2, list(ag.parameters()), g)
+    for a, b in zip(gr1, gr2):
+        torch.testing.assert_close(b, a, rtol=1e-5, atol=1e-6)
