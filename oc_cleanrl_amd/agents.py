@@ -49,31 +49,81 @@ class Predictor(nn.Module):
             return np.argmax(logits.cpu().numpy(), axis=1), states
 
 
-class _LinearReLU(torch.autograd.Function):
-    """relu(x @ W^T + b) as ONE hipBLASLt GEMM with a bias+ReLU epilogue
-    (torch._addmm_activation), with autograd's own linear+ReLU backward (ATen has no derivative
-    for _addmm_activation): g' = threshold_backward(g, out, 0); dx = g' W; dW = g'^T x; db = sum g'."""
+def _splitk(rows: int, k: int, n: int) -> int:
+    """K-split for the weight-gradient GEMM dW = g^T x (rows = reduction length): hipBLASLt's
+    default kernels leave the tall-skinny update shapes at 2-42 TFLOP/s; a batched GEMM over
+    row chunks + a sum restores 100+ TFLOP/s (tools/exp_gemm_shapes.py, gfx950)."""
+    if rows < 8192:
+        return 8 if k * n <= 16384 and rows % 8 == 0 else 1
+    if k * n <= 16384:
+        s = 16
+    elif k * n <= 131072:
+        s = 4
+    else:
+        s = 8
+    while rows % s:
+        s //= 2
+    return max(s, 1)
+
+
+def _weight_grad(g, x, out=None):
+    """dW = g^T x (g [rows, n], x [rows, k]) with the split-K rule; written into `out` if given."""
+    rows, n = g.shape
+    k = x.shape[1]
+    s = _splitk(rows, k, n)
+    if s == 1:
+        return torch.mm(g.t(), x, out=out) if out is not None else g.t().mm(x)
+    part = torch.bmm(g.view(s, rows // s, n).transpose(1, 2), x.view(s, rows // s, k))
+    return torch.sum(part, 0, out=out) if out is not None else part.sum(0)
+
+
+def _direct(p) -> bool:
+    """Parameters owned by ops.FlatAdam get their grads written in place (no AccumulateGrad)."""
+    return getattr(p, "_ocppo_direct_grad", False) and p.grad is not None
+
+
+class _LinearAct(torch.autograd.Function):
+    """y = act(x @ W^T + b), act = ReLU (one hipBLASLt GEMM with a bias+ReLU epilogue,
+    torch._addmm_activation) or identity (addmm). Backward = autograd's linear(+ReLU) formulas
+    (threshold_backward, dX = g'W, dW = g'^T x, db = sum g') with a split-K weight gradient, and
+    for FlatAdam-owned parameters dW/db are written straight into the flat grad buffer."""
 
     @staticmethod
-    def forward(ctx, x, w, b):
-        out = torch._addmm_activation(b, x, w.t(), use_gelu=False)
-        ctx.save_for_backward(x, w, out)
+    def forward(ctx, x, w, b, relu: bool):
+        out = torch._addmm_activation(b, x, w.t(), use_gelu=False) if relu else \
+            torch.addmm(b, x, w.t())
+        ctx.relu = relu
+        ctx.save_for_backward(x, w, out if relu else None)
+        ctx.w, ctx.b = w, b
         return out
 
     @staticmethod
     def backward(ctx, g):
         x, w, out = ctx.saved_tensors
-        gp = torch.ops.aten.threshold_backward(g, out, 0)
+        gp = torch.ops.aten.threshold_backward(g, out, 0) if ctx.relu else g.contiguous()
         dx = gp.mm(w) if ctx.needs_input_grad[0] else None
-        dw = gp.t().mm(x) if ctx.needs_input_grad[1] else None
-        db = gp.sum(0) if ctx.needs_input_grad[2] else None
-        return dx, dw, db
+        dw = db = None
+        if ctx.needs_input_grad[1]:
+            if _direct(ctx.w):
+                _weight_grad(gp, x, out=ctx.w.grad)
+            else:
+                dw = _weight_grad(gp, x)
+        if ctx.needs_input_grad[2]:
+            if _direct(ctx.b):
+                torch.sum(gp, 0, out=ctx.b.grad)
+            else:
+                db = gp.sum(0)
+        return dx, dw, db, None
+
+
+def linear_act(x, lin: nn.Linear, relu: bool):
+    lead = x.shape[:-1]
+    y = _LinearAct.apply(x.reshape(-1, x.shape[-1]), lin.weight, lin.bias, relu)
+    return y.view(*lead, y.shape[-1])
 
 
 def linear_relu(x, lin: nn.Linear):
-    lead = x.shape[:-1]
-    y = _LinearReLU.apply(x.reshape(-1, x.shape[-1]), lin.weight, lin.bias)
-    return y.view(*lead, y.shape[-1])
+    return linear_act(x, lin, True)
 
 
 def fused_trunk(seq: nn.Sequential, x):
@@ -100,12 +150,18 @@ class _ActorCritic(Predictor):
         return fused_trunk(self.network, x) if isinstance(self.network, nn.Sequential) \
             else self.network(x)
 
+    def _head(self, lin, h):
+        if isinstance(lin, nn.Linear) and lin.bias is not None and h.is_cuda and \
+                h.dtype == torch.float32:
+            return linear_act(h, lin, False)
+        return lin(h)
+
     def get_value(self, x):
-        return self.critic(self.trunk(x))
+        return self._head(self.critic, self.trunk(x))
 
     def logits_and_value(self, x):
         hidden = self.trunk(x)
-        return self.actor(hidden), self.critic(hidden)
+        return self._head(self.actor, hidden), self._head(self.critic, hidden)
 
     def get_action_and_value(self, x, action=None):
         """(action [B] i64, log_prob [B], entropy [B], value [B, 1]) like the reference."""

@@ -16,7 +16,8 @@
 namespace ocppo {
 
 constexpr int kOptThreads = 256;
-constexpr int kOptBlocks = 1024;  // grid-stride cap for the norm pass (partials in workspace)
+constexpr int kOptBlocks = 256;  // grid-stride cap for the norm pass: one workgroup per CU keeps
+                                 // the ticket fan-in at 256 arrivals (~3-4 us, MI355X "fanin")
 
 // scalars layout (f32): see include/ocppo.h OCPPO_OPT_*
 enum { S_STEP = 0, S_TOTAL_NORM = 1, S_CLIP = 2, S_STEP_SIZE = 3, S_BC2_SQRT = 4 };

@@ -428,6 +428,7 @@ class FlatAdam:
             self.params[off:off + k].copy_(p.detach().reshape(-1))
             p.data = self.params[off:off + k].view_as(p)
             p.grad = self.grads[off:off + k].view_as(p)
+            p._ocppo_direct_grad = True  # agents.py's autograd Functions write grads in place
             off += k
         self.param_list = params
         self.exp_avg = torch.zeros_like(self.params)

@@ -155,6 +155,10 @@ class PPOTrainer:
         self.fused_head = isinstance(self.agent.actor, nn.Linear) and \
             isinstance(self.agent.critic, nn.Linear)
         self.H = self.agent.actor.in_features if self.fused_head else 0
+        # every parameter's grad is written in place by agents._LinearAct (no zero-fill needed)
+        # when the agent is a Linear/ReLU stack owned by the fused optimizer
+        self.direct_grads = a.fused_optimizer and self.fused_head and all(
+            isinstance(m, (nn.Linear, nn.ReLU, nn.Flatten)) for m in self.agent.network)
         if a.fused_optimizer:
             # every parameter becomes a view of one flat buffer; clip + Adam = 2 HIP launches
             self.optimizer = ops.FlatAdam(self.agent.parameters(), lr=a.learning_rate, eps=1e-5,
@@ -288,7 +292,8 @@ class PPOTrainer:
             ent_coef=a.ent_coef, vf_coef=a.vf_coef, norm_adv=a.norm_adv,
             clip_vloss=a.clip_vloss, dlogits=self.dlogits, dvalue=self.dvalue,
             stats=self.stats[j], workspace=self.loss_ws))
-        self.grad_buf.zero_()
+        if not self.direct_grads:
+            self.grad_buf.zero_()
         torch.autograd.backward([logits, value], [self.dlogits, self.dvalue.view(-1, 1)])
 
     def _allreduce(self):

@@ -120,7 +120,7 @@ def test_fused_trunk_matches_module_forward_and_grads(dev, arch, obs):
     h2 = ag.trunk(x)
     torch.testing.assert_close(h2, h1, rtol=1e-6, atol=1e-6)
     g = torch.randn_like(h1)
-    gr1 = torch.autograd.grad(h1, list(ag.parameters()), g)
-    gr2 = torch.autograd.grad(h2, list(ag.parameters()), g)
-    for a, b in zip(gr1, gr2):
-        torch.testing.assert_close(b, a, rtol=1e-5, atol=1e-6)
+    gr1 = torch.autograd.grad(h1, list(ag.network.parameters()), g)
+    gr2 = torch.autograd.grad(h2, list(ag.network.parameters()), g)
+    for a, b in zip(gr1, gr2):  # split-K weight grads: summation order differs
+        torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-5 * float(a.abs().max()))
