@@ -130,20 +130,6 @@ OCPPO_API int ocppo_ppo_loss_fwd_bwd(ocppo_stream_t stream, const float* logits,
                            void* workspace, size_t workspace_bytes);
 
 /* ---------------------------------------------------------------------------------------------
- * Backward of y = relu(x W^T + b) up to its GEMMs in one pass (the PPObj/NatureCNN-head Linear
- * layers, architectures/ppo.py:60-84, backward reached from ppo_atari_oc.py:607):
- *   relu = 1 : gp = (y > 0) ? g : 0 (ATen threshold_backward) and db = column sums of gp
- *   relu = 0 : db = column sums of g (y, gp unused) — the bias gradient of a plain Linear
- *   g, y, gp : [R, C] f32;  db : [C] f32;  deterministic (fixed-order partials + ticket)
- *   workspace : ocppo_relu_bias_grad_workspace_bytes(R, C) bytes, zeroed once, then re-armed by
- *               the kernel (graph-replayable; one workspace per concurrently-running call)
- * ------------------------------------------------------------------------------------------- */
-OCPPO_API size_t ocppo_relu_bias_grad_workspace_bytes(int64_t R, int64_t C);
-OCPPO_API int ocppo_relu_bias_grad(ocppo_stream_t stream, const float* g, const float* y,
-                                   int64_t R, int64_t C, int relu, float* gp, float* db,
-                                   void* workspace, size_t workspace_bytes);
-
-/* ---------------------------------------------------------------------------------------------
  * Gradient clipping + Adam over ONE flat buffer — replaces
  * `nn.utils.clip_grad_norm_(agent.parameters(), max_grad_norm); optimizer.step()` of
  * ppo_atari_oc.py:608-610 (torch.optim.Adam(lr, eps=1e-5), betas (0.9, 0.999)) and the

@@ -38,8 +38,6 @@ SIGNATURES: dict[str, tuple[type, list]] = {
     "ocppo_ppo_loss_workspace_bytes": (SZ, [I64, I64]),
     "ocppo_ppo_loss_fwd_bwd": (I, [P, P, P, I64, I64, P, P, P, P, P, P, P, D, D, D, I, I, P, P, P,
                                    P, SZ]),
-    "ocppo_relu_bias_grad_workspace_bytes": (SZ, [I64, I64]),
-    "ocppo_relu_bias_grad": (I, [P, P, P, I64, I64, I, P, P, P, SZ]),
     "ocppo_clip_adam_workspace_bytes": (SZ, [I64]),
     "ocppo_clip_adam_step": (I, [P, P, P, P, P, I64, P, D, D, D, D, D, P, P, SZ]),
     "ocppo_categorical_sample": (I, [P, P, P, I64, I64, P, P, P, P, P]),

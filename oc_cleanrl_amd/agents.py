@@ -100,33 +100,19 @@ class _LinearAct(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         x, w, out = ctx.saved_tensors
-        g = g.contiguous()
-        db = None
-        want_db = ctx.needs_input_grad[2]
-        direct_b = want_db and _direct(ctx.b)
-        if g.dtype == torch.float32:
-            # one HIP pass: threshold_backward (ReLU) and the bias column sums
-            if ctx.relu or want_db:
-                gp, dbt = ops.relu_bias_grad(g, out, db=ctx.b.grad if direct_b else None,
-                                             relu=ctx.relu)
-                gp = gp if ctx.relu else g
-                db = None if (direct_b or not want_db) else dbt
-            else:
-                gp = g
-        else:
-            gp = torch.ops.aten.threshold_backward(g, out, 0) if ctx.relu else g
-            if want_db:
-                if direct_b:
-                    torch.sum(gp, 0, out=ctx.b.grad)
-                else:
-                    db = gp.sum(0)
+        gp = torch.ops.aten.threshold_backward(g, out, 0) if ctx.relu else g.contiguous()
         dx = gp.mm(w) if ctx.needs_input_grad[0] else None
-        dw = None
+        dw = db = None
         if ctx.needs_input_grad[1]:
             if _direct(ctx.w):
                 _weight_grad(gp, x, out=ctx.w.grad)
             else:
                 dw = _weight_grad(gp, x)
+        if ctx.needs_input_grad[2]:
+            if _direct(ctx.b):
+                torch.sum(gp, 0, out=ctx.b.grad)
+            else:
+                db = gp.sum(0)
         return dx, dw, db, None
 
 

@@ -541,38 +541,3 @@ def td_loss_fwd_bwd(q, q_next, actions, rewards, dones, gamma: float, dq=None, s
          _check(rewards, "rewards", f, dev, B), _check(dones, "dones", f, dev, B), B, A,
          float(gamma), _check(dq, "dq", f, dev, B * A), _check(stats, "stats", f, dev, 2))
     return stats, dq
-
-
-# ---------------------------------------------------------------------------------------------
-# ReLU backward + bias gradient (the Linear/ReLU layers' backward up to the GEMMs)
-# ---------------------------------------------------------------------------------------------
-_WS_CACHE: dict = {}
-
-
-def _workspace(key, nbytes: int, device) -> torch.Tensor:
-    """Persistent zeroed scratch per (call site, shape); kernels re-arm their own tickets.
-    Allocated on first (eager) use so graph capture reuses it."""
-    k = (key, int(nbytes), str(device))
-    buf = _WS_CACHE.get(k)
-    if buf is None:
-        buf = torch.zeros(int(nbytes), dtype=torch.uint8, device=device)
-        _WS_CACHE[k] = buf
-    return buf
-
-
-def relu_bias_grad(g, y=None, gp=None, db=None, relu: bool = True, site=None):
-    """(gp, db): gp = (y > 0) ? g : 0, db = gp.sum(0)  [relu]; db = g.sum(0) [not relu]."""
-    R, C = g.shape
-    dev = g.device
-    f = torch.float32
-    if relu and gp is None:
-        gp = torch.empty_like(g)
-    if db is None:
-        db = torch.empty(C, dtype=f, device=dev)
-    nb = _lib.LIB.ocppo_relu_bias_grad_workspace_bytes(R, C)
-    ws = _workspace(("relu_bias_grad", site, R, C), nb, dev)
-    call("ocppo_relu_bias_grad", _stream(dev), _check(g, "g", f, dev),
-         _check(y, "y", f, dev, R * C) if relu else None, R, C, int(bool(relu)),
-         _check(gp, "gp", f, dev, R * C) if relu else None, _check(db, "db", f, dev, C),
-         ws.data_ptr(), ws.numel())
-    return gp, db

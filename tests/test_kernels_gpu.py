@@ -536,18 +536,3 @@ def test_replay_buffer_semantics(ops, dev, dt):
             assert float(out["rewards"][b]) == tr
             assert torch.equal(out["observations"][b], frames[tr][e].float())
             assert torch.equal(out["next_observations"][b], frames[tr + 1][e].float())
-
-
-@pytest.mark.parametrize("R,C", [(16384, 1024), (16384, 256), (4096, 512), (4096, 6), (33, 7),
-                                 (1, 300)])
-@pytest.mark.parametrize("relu", [True, False])
-def test_relu_bias_grad(ops, dev, R, C, relu):
-    g = torch.randn(R, C, device=dev)
-    y = torch.relu(torch.randn(R, C, device=dev))
-    gp, db = ops.relu_bias_grad(g, y, relu=relu)
-    ref = torch.ops.aten.threshold_backward(g, y, 0) if relu else g
-    if relu:
-        assert torch.equal(gp, ref)
-    torch.testing.assert_close(db, ref.sum(0), rtol=1e-5, atol=1e-5 * R ** 0.5)
-    gp2, db2 = ops.relu_bias_grad(g, y, relu=relu)  # re-armed tickets, deterministic
-    assert torch.equal(db, db2)
