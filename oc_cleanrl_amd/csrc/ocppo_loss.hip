@@ -21,7 +21,8 @@
 
 namespace ocppo {
 
-constexpr int kLossThreads = 256;  // one element per thread, one 256-element tile per workgroup
+constexpr int kLossThreads = 256;  // one element per thread, 256-element tiles
+constexpr int kLossMaxBlocks = 1024;  // grid cap: 4 workgroups per CU; bounds the ticket fan-in
 constexpr int kNumPartials = 6;    // pg, v, entropy, old_kl, kl, clipfrac
 constexpr size_t kTicketBytes = 256;
 
@@ -252,35 +253,71 @@ struct LossParams {
 };
 
 template <int AMAX>
+struct LossTileRegs {
+  int64_t a;
+  float old_lp, adv, R, v_old, v;
+  float lg[AMAX];  // this thread's coalesced share of the tile's [cnt*A] logits
+};
+
+// Loads tile `tl`'s per-element records (element tid) and logits chunk into registers.
+template <int AMAX>
+__device__ __forceinline__ void loss_tile_load(const LossParams& P, int64_t tl, int64_t ntiles,
+                                               int tid, LossTileRegs<AMAX>& r) {
+  r.a = 0;
+  r.old_lp = r.adv = r.R = r.v_old = r.v = 0.f;
+  if (tl >= ntiles) return;
+  const int64_t i0 = tl * kLossThreads;
+  const int64_t cnt = (P.M - i0) < kLossThreads ? (P.M - i0) : kLossThreads;
+  if (tid < cnt) {
+    const int64_t i = i0 + tid;
+    const int64_t b = P.mb_inds ? P.mb_inds[i] : i;
+    r.a = P.b_actions[b];
+    r.old_lp = P.b_logprobs[b];
+    r.adv = P.b_adv[b];
+    r.R = P.b_ret[b];
+    r.v_old = P.b_val[b];
+    r.v = P.new_value[i];
+  }
+#pragma unroll
+  for (int k = 0; k < AMAX; ++k) {
+    const int64_t e = static_cast<int64_t>(k) * kLossThreads + tid;
+    r.lg[k] = (k < P.A && e < cnt * P.A) ? P.logits[i0 * P.A + e] : 0.f;
+  }
+}
+
+template <int AMAX>
 __global__ __launch_bounds__(kLossThreads) void ppo_loss_kernel(LossParams P) {
   extern __shared__ __attribute__((aligned(16))) float tile[];  // [kLossThreads * A]
   __shared__ float red[kLossThreads / kWave][kNumPartials];
   __shared__ int s_last;
 
   const int A = P.A;
-  const int64_t i0 = static_cast<int64_t>(blockIdx.x) * kLossThreads;
-  const int64_t cnt = (P.M - i0) < kLossThreads ? (P.M - i0) : kLossThreads;
   const int tid = threadIdx.x;
-
-  // issue this element's index and gathered loads first, so their latency overlaps the staging
+  float part[kNumPartials] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const int64_t ntiles = (P.M + kLossThreads - 1) / kLossThreads;
+  // grid-stride over 256-element tiles (the grid is capped at kLossMaxBlocks so the ticket
+  // fan-in stays bounded); each thread accumulates its partials over its tiles in order.
+  // Software-pipelined: the next tile's records and logits chunk are loaded into registers
+  // before the current tile is computed.
+  LossTileRegs<AMAX> nxt;
+  loss_tile_load<AMAX>(P, blockIdx.x, ntiles, tid, nxt);
+  for (int64_t tl = blockIdx.x; tl < ntiles; tl += gridDim.x) {
+  const int64_t i0 = tl * kLossThreads;
+  const int64_t cnt = (P.M - i0) < kLossThreads ? (P.M - i0) : kLossThreads;
   const bool active = tid < cnt;
   const int64_t i = i0 + tid;
-  int64_t a = 0;
-  float old_lp = 0.f, adv = 0.f, R = 0.f, v_old = 0.f, v = 0.f;
-  if (active) {
-    const int64_t b = P.mb_inds ? P.mb_inds[i] : i;
-    a = P.b_actions[b];
-    old_lp = P.b_logprobs[b];
-    adv = P.b_adv[b];
-    R = P.b_ret[b];
-    v_old = P.b_val[b];
-    v = P.new_value[i];
+  const LossTileRegs<AMAX> cur = nxt;
+  const int64_t a = cur.a;
+  const float old_lp = cur.old_lp, adv = cur.adv, R = cur.R, v_old = cur.v_old, v = cur.v;
+  // stage this tile's logits rows (contiguous [cnt*A] floats, loaded coalesced) in LDS
+#pragma unroll
+  for (int k = 0; k < AMAX; ++k) {
+    const int64_t e = static_cast<int64_t>(k) * kLossThreads + tid;
+    if (k < A && e < cnt * A) tile[e] = cur.lg[k];
   }
-  // stage this tile's logits rows (contiguous [cnt*A] floats) with coalesced loads
-  for (int64_t e = tid; e < cnt * A; e += kLossThreads) tile[e] = P.logits[i0 * A + e];
+  loss_tile_load<AMAX>(P, tl + gridDim.x, ntiles, tid, nxt);
   __syncthreads();
 
-  float part[kNumPartials] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   float dl[AMAX];
   if (active) {
     float l[AMAX], ln[AMAX], p[AMAX];
@@ -297,9 +334,9 @@ __global__ __launch_bounds__(kLossThreads) void ppo_loss_kernel(LossParams P) {
     // ratio and no-grad diagnostics (:569-575)
     const float logratio = new_lp - old_lp;
     const float ratio = expf(logratio);
-    part[3] = -logratio;
-    part[4] = (ratio - 1.0f) - logratio;
-    part[5] = fabsf(ratio - 1.0f) > P.clip ? 1.f : 0.f;
+    part[3] += -logratio;
+    part[4] += (ratio - 1.0f) - logratio;
+    part[5] += fabsf(ratio - 1.0f) > P.clip ? 1.f : 0.f;
 
     // advantage normalisation (:577-579)
     float advn = adv;
@@ -310,7 +347,7 @@ __global__ __launch_bounds__(kLossThreads) void ppo_loss_kernel(LossParams P) {
     const float pg1 = nadv * ratio;
     const float rc = fminf(fmaxf(ratio, P.clip_lo), P.clip_hi);
     const float pg2 = nadv * rc;
-    part[0] = fmaxf(pg1, pg2);
+    part[0] += fmaxf(pg1, pg2);
 
     // value loss (:585-597)
     const float du = v - R;
@@ -322,7 +359,7 @@ __global__ __launch_bounds__(kLossThreads) void ppo_loss_kernel(LossParams P) {
       const float vcl = v_old + dvc;
       const float dc = vcl - R;
       const float vc = dc * dc;
-      part[1] = fmaxf(vu, vc);
+      part[1] += fmaxf(vu, vc);
       const float gu = vu > vc ? P.g_v : (vu == vc ? P.g_v / 2.f : 0.f);
       const float gc = vc > vu ? P.g_v : (vu == vc ? P.g_v / 2.f : 0.f);
       const float tu = gu * (2.0f * du);
@@ -330,10 +367,10 @@ __global__ __launch_bounds__(kLossThreads) void ppo_loss_kernel(LossParams P) {
       tc = (dvv >= -P.clip && dvv <= P.clip) ? tc : 0.f;
       dv = tu + tc;
     } else {
-      part[1] = vu;
+      part[1] += vu;
       dv = P.g_v * (2.0f * du);
     }
-    part[2] = H;
+    part[2] += H;
 
     // backward of the surrogate to new_logprob
     const float g1 = pg1 > pg2 ? P.g_pg : (pg1 == pg2 ? P.g_pg / 2.f : 0.f);
@@ -354,6 +391,8 @@ __global__ __launch_bounds__(kLossThreads) void ppo_loss_kernel(LossParams P) {
   }
   __syncthreads();
   for (int64_t e = tid; e < cnt * A; e += kLossThreads) P.dlogits[i0 * A + e] = tile[e];
+  __syncthreads();  // the next tile restages the LDS tile
+  }
 
   // per-block partial sums in a fixed order
   const int lane = tid & (kWave - 1), wid = tid / kWave;
@@ -574,6 +613,174 @@ __global__ __launch_bounds__(256) void policy_head_sample_kernel(
   }
 }
 
+// Fast path of the head for A <= 7 actions and H = 256*CH. Each wave keeps the A+1 weight rows
+// in registers (CH*8 float4 per lane) and owns a group of E consecutive environments (E = 1 at
+// the config sizes, up to 64 when N is large). Per environment: the hidden row (next one in
+// flight), A+1 dot products padded to 8, reduced by a reduce-scatter butterfly -- xor 32 / 16 / 8
+// halve the set of values each lane carries (4 + 2 + 1 shuffles), xor 4 / 2 / 1 finish one value
+// per 8-lane group -- so lane 8j holds logit j (j = 7: the value); 8 lanes park them in LDS.
+// Then lane e runs environment e's categorical (a wave64 VALU op costs the same for 1 or 64
+// active lanes, so batching the ~500-instruction tail over E lanes is what makes large N
+// HBM-bound) and the per-env outputs are stored coalesced.
+constexpr int kHeadWavesPerBlock = 4;
+
+template <int CH>
+__device__ __forceinline__ void head_load_row(const float* __restrict__ hidden, int64_t n, int lane,
+                                              float4 (&x)[CH]) {
+  const float4* h4 = reinterpret_cast<const float4*>(hidden + n * (256 * CH));
+#pragma unroll
+  for (int c = 0; c < CH; ++c) x[c] = h4[c * kWave + lane];
+}
+
+// The A+1 (padded to 8) dot products of one hidden row against the register-resident weights,
+// reduce-scattered so that lane 8j ends with value j (see above).
+template <int CH>
+__device__ __forceinline__ float head_dots(const float4 (&x)[CH], const float4 (&w)[8][CH],
+                                           int lane) {
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    acc[j] = 0.f;
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+      acc[j] += x[c].x * w[j][c].x + x[c].y * w[j][c].y + x[c].z * w[j][c].z + x[c].w * w[j][c].w;
+  }
+  const bool b5 = lane & 32, b4 = lane & 16, b3 = lane & 8;
+  float s4[4], s2[2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float send = b5 ? acc[i] : acc[i + 4];
+    s4[i] = (b5 ? acc[i + 4] : acc[i]) + __shfl_xor(send, 32);
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const float send = b4 ? s4[i] : s4[i + 2];
+    s2[i] = (b4 ? s4[i + 2] : s4[i]) + __shfl_xor(send, 16);
+  }
+  float t = (b3 ? s2[1] : s2[0]) + __shfl_xor(b3 ? s2[0] : s2[1], 8);
+  t += __shfl_xor(t, 4);
+  t += __shfl_xor(t, 2);
+  t += __shfl_xor(t, 1);
+  return t;
+}
+
+// Categorical tail for one environment given its A logits (l[7] = value) and Exp(1) noise:
+// writes action, log-prob, value, entropy, logits.
+__device__ __forceinline__ void head_tail(const float (&l)[8], const float (&nzj)[7], int A,
+                                          int64_t n, int64_t* __restrict__ action_out,
+                                          float* __restrict__ logprob_out,
+                                          float* __restrict__ entropy_out,
+                                          float* __restrict__ value_out,
+                                          float* __restrict__ logits_out, bool store) {
+  float ln[8], p[8], lse;
+  categorical_row<8>(l, A, lse, ln, p);
+  int best = 0;
+  float best_q = p[0] / nzj[0];
+#pragma unroll
+  for (int j = 1; j < 7; ++j)
+    if (j < A) {
+      const float q = p[j] / nzj[j];
+      if (q > best_q || (q != q && best_q == best_q)) {
+        best_q = q;
+        best = j;
+      }
+    }
+  float lp = 0.f;
+#pragma unroll
+  for (int j = 0; j < 7; ++j)
+    if (j == best) lp = ln[j];
+  if (!store) return;
+  action_out[n] = best;
+  logprob_out[n] = lp;
+  value_out[n] = l[7];
+  if (entropy_out) entropy_out[n] = categorical_entropy<8>(ln, p, A);
+  if (logits_out) {
+#pragma unroll
+    for (int j = 0; j < 7; ++j)
+      if (j < A) logits_out[n * A + j] = l[j];
+  }
+}
+
+template <int CH>
+__global__ __launch_bounds__(256) void policy_head_fast_kernel(
+    const float* __restrict__ hidden, int64_t N, int E, const float* __restrict__ wa,
+    const float* __restrict__ ba, const float* __restrict__ wc, const float* __restrict__ bc,
+    const float* __restrict__ noise, int A, int64_t* __restrict__ action_out,
+    float* __restrict__ logprob_out, float* __restrict__ entropy_out,
+    float* __restrict__ value_out, float* __restrict__ logits_out) {
+  constexpr int H = 256 * CH;
+  __shared__ float s_logit[kHeadWavesPerBlock][kWave][9];  // [wave][env in group][8 (+pad)]
+  const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+  const int64_t nwaves = static_cast<int64_t>(gridDim.x) * kHeadWavesPerBlock;
+  const int64_t ngroups = (N + E - 1) / E;
+  int64_t g = static_cast<int64_t>(blockIdx.x) * kHeadWavesPerBlock + wv;
+  if (g >= ngroups) return;  // wave-uniform
+  const int jo = lane >> 3;  // the value this lane's 8-lane group ends up owning
+  const float bias = jo < A ? ba[jo] : (jo == 7 ? bc[0] : 0.f);
+  float4 w[8][CH];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float* wrow = j == 7 ? wc : wa + j * H;
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+      w[j][c] = (j < A || j == 7) ? reinterpret_cast<const float4*>(wrow)[c * kWave + lane]
+                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  if (E == 1) {  // config sizes: one environment per wave, wave-uniform tail via v_readlane
+    float nz = lane < A ? noise[g * A + lane] : 1.f;
+    float4 x[CH];
+    head_load_row<CH>(hidden, g, lane, x);
+    for (; g < ngroups; g += nwaves) {
+      const float t = head_dots<CH>(x, w, lane) + bias;
+      float l[8], nzj[7];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        l[j] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t), 8 * j));
+#pragma unroll
+      for (int j = 0; j < 7; ++j)
+        nzj[j] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(nz), j));
+      head_tail(l, nzj, A, g, action_out, logprob_out, entropy_out, value_out, nullptr, lane == 0);
+      const float mine = __shfl(t, 8 * (lane & 7));  // all lanes take part in the permute
+      if (logits_out && lane < A) logits_out[g * A + lane] = mine;
+      if (g + nwaves < ngroups) {
+        head_load_row<CH>(hidden, g + nwaves, lane, x);
+        nz = lane < A ? noise[(g + nwaves) * A + lane] : 1.f;
+      }
+    }
+    return;
+  }
+  for (; g < ngroups; g += nwaves) {
+    const int64_t n0 = g * E;
+    const int cnt = static_cast<int>((N - n0) < E ? (N - n0) : E);
+    const int64_t nt = n0 + lane;  // this lane's environment in the tail
+    float nzj[7];
+#pragma unroll
+    for (int j = 0; j < 7; ++j) nzj[j] = (lane < cnt && j < A) ? noise[nt * A + j] : 1.f;
+    float4 x[CH], xn[CH];
+    head_load_row<CH>(hidden, n0, lane, x);
+    for (int e = 0; e < cnt; ++e) {
+      if (e + 1 < cnt) head_load_row<CH>(hidden, n0 + e + 1, lane, xn);
+      const float t = head_dots<CH>(x, w, lane);
+      if ((lane & 7) == 0) s_logit[wv][e][jo] = t + bias;
+#pragma unroll
+      for (int c = 0; c < CH; ++c) x[c] = xn[c];
+    }
+    // the LDS rows were written by this wave only; LDS executes one wave's ops in order
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (lane < cnt) {
+      float l[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) l[j] = s_logit[wv][lane][j];
+      head_tail(l, nzj, A, nt, action_out, logprob_out, entropy_out, value_out, logits_out, true);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();  // the tail's LDS reads precede the next group's writes
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
 }  // namespace ocppo
 
 using namespace ocppo;
@@ -660,7 +867,8 @@ extern "C" int ocppo_ppo_loss_fwd_bwd(ocppo_stream_t stream, const float* logits
   P.g_h = (-1.0f * P.ent_coef) / fm;
   P.g_v = (P.vf_coef * 0.5f) / fm;
   P.inv_m = 1.0f / fm;
-  const int64_t nb = ceil_div(M, kLossThreads);
+  int64_t nb = ceil_div(M, kLossThreads);
+  nb = nb < kLossMaxBlocks ? nb : kLossMaxBlocks;
   const size_t lds = sizeof(float) * kLossThreads * A;
   if (A <= 8)
     hipLaunchKernelGGL(ppo_loss_kernel<8>, dim3(nb), dim3(kLossThreads), lds, s, P);
@@ -746,7 +954,28 @@ extern "C" int ocppo_policy_head_sample(ocppo_stream_t stream, const float* hidd
   const dim3 grid(static_cast<unsigned>(ceil_div(N, 4))), block(256);
   clear_stale_error();
   hipStream_t s = as_stream(stream);
-  if (A <= 8)
+  const bool aligned = ((reinterpret_cast<uintptr_t>(hidden) | reinterpret_cast<uintptr_t>(w_actor) |
+                         reinterpret_cast<uintptr_t>(w_critic)) & 15) == 0;
+  if (A <= 7 && H % 256 == 0 && H <= 256 * 4 && aligned) {
+    // one wave per group of E environments; E = 1 while N fits 12 (CH > 2: 8) waves per CU,
+    // doubling up to 64 environments per wave beyond that
+    const int64_t cap = H <= 512 ? 256 * 12 : 256 * 8;
+    int E = 1;
+    while (E < 64 && ceil_div(N, static_cast<int64_t>(E)) > cap) E *= 2;
+    const int64_t waves = ceil_div(N, static_cast<int64_t>(E));
+    const dim3 hgrid(static_cast<unsigned>(ceil_div(waves, kHeadWavesPerBlock)));
+#define OCPPO_HEAD(CH)                                                                           \
+  hipLaunchKernelGGL(policy_head_fast_kernel<CH>, hgrid, dim3(kWave * kHeadWavesPerBlock), 0, s, \
+                     hidden, N, E, w_actor, b_actor, w_critic, b_critic, noise, (int)A,          \
+                     action_out, logprob_out, entropy_out, value_out, logits_out)
+    switch (H / 256) {
+      case 1: OCPPO_HEAD(1); break;
+      case 2: OCPPO_HEAD(2); break;
+      case 3: OCPPO_HEAD(3); break;
+      default: OCPPO_HEAD(4); break;
+    }
+#undef OCPPO_HEAD
+  } else if (A <= 8)
     hipLaunchKernelGGL(policy_head_sample_kernel<8>, grid, block, 0, s, hidden, N, (int)H, w_actor,
                        b_actor, w_critic, b_critic, noise, (int)A, action_out, logprob_out,
                        entropy_out, value_out, logits_out);

@@ -406,6 +406,20 @@ def synth_env_step(seed: int, step_base, step_offset: int, actions, frame_out, r
 OPT_STEP, OPT_TOTAL_NORM, OPT_CLIP_COEF = 0, 1, 2
 
 
+FLAT_ALIGN = 64  # floats: every parameter / grad view in a flat buffer starts 256-B aligned
+
+
+def flat_offsets(params):
+    """Offsets of `params` in one flat f32 buffer, each rounded up to FLAT_ALIGN elements so the
+    views keep the 16-B alignment the vectorised kernels (policy head, Adam) need; returns
+    (offsets, total length)."""
+    offs, off = [], 0
+    for p in params:
+        offs.append(off)
+        off += -(-p.numel() // FLAT_ALIGN) * FLAT_ALIGN
+    return offs, off
+
+
 class FlatAdam:
     """Adam (torch.optim.Adam semantics, eps as given) + global-norm gradient clipping over ONE
     flat f32 parameter buffer. Construct it over the module's parameters: every parameter becomes
@@ -416,12 +430,12 @@ class FlatAdam:
                  max_grad_norm: float = 0.0):
         params = [p for p in params if p.requires_grad]
         dev = params[0].device
-        n = sum(p.numel() for p in params)
+        offs, n = flat_offsets(params)
         self.numel = n
-        self.params = torch.empty(n, dtype=torch.float32, device=dev)
+        # zero padding between parameters is a fixed point of clip + Adam (g = m = v = p = 0)
+        self.params = torch.zeros(n, dtype=torch.float32, device=dev)
         self.grads = torch.zeros(n, dtype=torch.float32, device=dev)
-        off = 0
-        for p in params:
+        for p, off in zip(params, offs):
             k = p.numel()
             if p.dtype != torch.float32:
                 raise ValueError("FlatAdam needs f32 parameters")
@@ -429,7 +443,6 @@ class FlatAdam:
             p.data = self.params[off:off + k].view_as(p)
             p.grad = self.grads[off:off + k].view_as(p)
             p._ocppo_direct_grad = True  # agents.py's autograd Functions write grads in place
-            off += k
         self.param_list = params
         self.exp_avg = torch.zeros_like(self.params)
         self.exp_avg_sq = torch.zeros_like(self.params)

@@ -54,13 +54,11 @@ class FlatGrads:
 
     def __init__(self, params):
         self.params = [p for p in params if p.requires_grad]
-        n = sum(p.numel() for p in self.params)
+        offs, n = ops.flat_offsets(self.params)
         dev = self.params[0].device
         self.buf = torch.zeros(n, dtype=torch.float32, device=dev)
-        off = 0
-        for p in self.params:
+        for p, off in zip(self.params, offs):
             p.grad = self.buf[off:off + p.numel()].view_as(p)
-            off += p.numel()
         self.numel = n
 
     def zero(self):

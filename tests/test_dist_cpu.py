@@ -59,9 +59,15 @@ def test_flat_grads_are_views():
 
     m = _model()
     f = FlatGrads(m.parameters())
-    assert f.numel == sum(p.numel() for p in m.parameters())
+    from oc_cleanrl_amd.ops import FLAT_ALIGN, flat_offsets
+
+    offs, n = flat_offsets(list(m.parameters()))
+    assert f.numel == n and all(o % FLAT_ALIGN == 0 for o in offs)
     ((m(torch.randn(4, 6)) ** 2).sum()).backward()
-    assert torch.equal(f.buf, torch.cat([p.grad.flatten() for p in m.parameters()]))
+    for p, o in zip(m.parameters(), offs):
+        assert p.grad.data_ptr() == f.buf.data_ptr() + 4 * o
+    live = sum(p.numel() for p in m.parameters())
+    assert int((f.buf != 0).sum()) <= live  # padding stays zero
     f.zero()
     assert all(float(p.grad.abs().sum()) == 0 for p in m.parameters())
 

@@ -93,7 +93,8 @@ def test_loss_golden(ops, dev, name):
 
 
 @pytest.mark.parametrize("M,A,B", [(1, 6, 1), (255, 4, 1000), (4096, 6, 16384), (8192, 4, 32768),
-                                   (5000, 18, 5000), (65536, 6, 131072)])
+                                   (5000, 18, 5000), (65536, 6, 131072),
+                                   (300000, 6, 300000)])  # > grid cap: blocks walk tiles
 @pytest.mark.parametrize("norm_adv,clip_vloss", [(True, True), (False, False)])
 def test_loss_random_vs_oracle(ops, dev, M, A, B, norm_adv, clip_vloss):
     if M == 1 and norm_adv:
@@ -331,7 +332,9 @@ def test_synth_env_bitwise_vs_oracle(ops, dev, pixel, N, D):
 # fused rollout policy head; fused store + VecNormalize
 # ---------------------------------------------------------------------------------------------
 @pytest.mark.parametrize("N,H,A", [(128, 512, 6), (256, 512, 4), (7, 64, 18), (33, 100, 6),
-                                   (4096, 512, 6)])
+                                   (4096, 512, 6), (65, 256, 7), (9, 1024, 1), (130, 768, 3),
+                                   (5, 2048, 6), (17, 512, 8),
+                                   (300001, 512, 6), (20000, 1024, 3)])  # E > 1 env per wave
 def test_policy_head_sample(ops, dev, N, H, A):
     g = torch.Generator(device=dev).manual_seed(N + H + A)
     hidden = torch.relu(torch.randn(N, H, device=dev, generator=g))
@@ -416,20 +419,22 @@ def test_flat_adam_matches_torch_adam_and_clip(ops, dev, max_norm, scale):
 
 def test_flat_adam_vs_oracle_bit_level(ops, dev):
     rng = np.random.default_rng(0)
-    P = 1000003  # not a multiple of 4: exercises the scalar tail
+    P = 1000003  # the flat buffer pads it to a multiple of ops.FLAT_ALIGN; padding stays zero
     p0 = rng.standard_normal(P).astype(np.float32)
     w = torch.nn.Parameter(T(p0, dev))
     opt = ops.FlatAdam([w], lr=2.5e-4, eps=1e-5, max_grad_norm=0.5)
+    assert opt.numel % ops.FLAT_ALIGN == 0 and opt.numel >= P
     p, m, v, step = p0, np.zeros(P, np.float32), np.zeros(P, np.float32), 0
     for it in range(3):
         gr = (rng.standard_normal(P) * 0.01).astype(np.float32)
-        opt.grads.copy_(T(gr, dev))
+        opt.grads[:P].copy_(T(gr, dev))
         opt.step()
+        assert float(opt.params[P:].abs().sum()) == 0 and float(opt.exp_avg_sq[P:].abs().sum()) == 0
         p, m, v, step, total = O.clip_adam_step(p, gr, m, v, step, 2.5e-4, max_norm=0.5)
         np.testing.assert_allclose(float(opt.scalars[1]), total, rtol=1e-5)
         # the clip coefficient (f32 on device, f64 norm in the oracle) may differ by an ulp,
         # so compare at the scale of the moments / the update, not element-relative
-        np.testing.assert_allclose(opt.exp_avg.cpu().numpy(), m, rtol=0,
+        np.testing.assert_allclose(opt.exp_avg[:P].cpu().numpy(), m, rtol=0,
                                    atol=2e-6 * np.abs(m).max())
         np.testing.assert_allclose(w.detach().cpu().numpy(), p, rtol=1e-6, atol=1e-9)
 
@@ -536,3 +541,26 @@ def test_replay_buffer_semantics(ops, dev, dt):
             assert float(out["rewards"][b]) == tr
             assert torch.equal(out["observations"][b], frames[tr][e].float())
             assert torch.equal(out["next_observations"][b], frames[tr + 1][e].float())
+
+
+def test_clip_adam_abi_scalar_tail(ops, dev):
+    """ocppo_clip_adam_step called through the C ABI with P % 4 != 0 (the scalar tail)."""
+    from oc_cleanrl_amd import _lib
+
+    rng = np.random.default_rng(3)
+    P = 1003
+    p0 = rng.standard_normal(P).astype(np.float32)
+    gr = (rng.standard_normal(P) * 0.1).astype(np.float32)
+    p, g = T(p0, dev), T(gr, dev)
+    m, v = torch.zeros(P, device=dev), torch.zeros(P, device=dev)
+    lr = torch.tensor([1e-3], device=dev)
+    sc = torch.zeros(8, device=dev)
+    ws = torch.zeros(int(_lib.LIB.ocppo_clip_adam_workspace_bytes(P)), dtype=torch.uint8, device=dev)
+    _lib.call("ocppo_clip_adam_step", torch.cuda.current_stream(dev).cuda_stream, p.data_ptr(),
+              g.data_ptr(), m.data_ptr(), v.data_ptr(), P, lr.data_ptr(), 0.9, 0.999, 1e-5, 0.5,
+              0.5, sc.data_ptr(), ws.data_ptr(), ws.numel())
+    ep, em, ev, step, total = O.clip_adam_step(p0, gr, np.zeros(P, np.float32),
+                                               np.zeros(P, np.float32), 0, 1e-3, max_norm=0.5,
+                                               grad_scale=0.5)
+    np.testing.assert_allclose(float(sc[1]), total, rtol=1e-5)
+    np.testing.assert_allclose(p.cpu().numpy(), ep, rtol=1e-6, atol=1e-9)
