@@ -103,4 +103,79 @@ __device__ __forceinline__ T block_sum(T v, T* scratch) {
   return r;
 }
 
+// ---- two-level last-block hand-off -------------------------------------------------------------
+// A grid-wide reduction of NP per-block partials without a second launch. Blocks arrive on one of
+// G = ceil(nb / 32) group tickets (one 128-B line each, so arrivals on any one address stay <= 32
+// instead of nb); the last block of a group combines its group's partials and arrives on the
+// global ticket; the last group's combiner produces the total. Every hand-off follows
+// MI355X_MICROARCH.md "Valid forms" row 1: write-through (sc1) stores, drained with
+// s_waitcnt vmcnt(0), then ONE agent-scope relaxed atomic; the receiver reads with sc1 loads.
+// No release/acquire fence, so the block's other dirty lines are not written back here.
+// Tickets re-arm themselves (graph replay). Sums run over lanes by a fixed butterfly, so the
+// result is deterministic for a given grid.
+constexpr int kHandoffGroup = 32;
+constexpr int kHandoffMaxGroups = 64;  // nb <= 2048
+constexpr int kHandoffMaxBlocks = kHandoffGroup * kHandoffMaxGroups;
+constexpr int kTicketStride = 32;      // unsigned per 128-B line
+constexpr size_t kHandoffTicketBytes = (1 + kHandoffMaxGroups) * kTicketStride * sizeof(unsigned);
+
+// Call from every thread of the block; `mine` must be valid in thread 0. Returns true (in every
+// thread) only in the final block, where `total` is valid in threads 0..63.
+template <int NP>
+__device__ __forceinline__ bool handoff_combine(const float (&mine)[NP], unsigned* tickets,
+                                                float* partials, float* gpartials,
+                                                float (&total)[NP], int* s_flag) {
+  const unsigned nb = gridDim.x, b = blockIdx.x;
+  const unsigned g = b / kHandoffGroup, G = (nb + kHandoffGroup - 1) / kHandoffGroup;
+  const unsigned gsize = (nb - g * kHandoffGroup) < kHandoffGroup ? (nb - g * kHandoffGroup)
+                                                                   : kHandoffGroup;
+  unsigned* gt = tickets + (1 + g) * kTicketStride;
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < NP; ++k)
+      __hip_atomic_store(&partials[b * NP + k], mine[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned prev = __hip_atomic_fetch_add(gt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *s_flag = prev == gsize - 1;
+  }
+  __syncthreads();
+  if (!*s_flag) return false;
+  __syncthreads();  // everyone has read the flag before thread 0 reuses it
+  if (threadIdx.x < kWave) {
+    const unsigned lane = threadIdx.x;
+    float v[NP];
+#pragma unroll
+    for (int k = 0; k < NP; ++k)
+      v[k] = lane < gsize ? __hip_atomic_load(&partials[(g * kHandoffGroup + lane) * NP + k],
+                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                          : 0.f;
+#pragma unroll
+    for (int k = 0; k < NP; ++k) v[k] = wave_sum(v[k]);
+    if (lane == 0) {
+      __hip_atomic_store(gt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm group
+#pragma unroll
+      for (int k = 0; k < NP; ++k)
+        __hip_atomic_store(&gpartials[g * NP + k], v[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned prev =
+          __hip_atomic_fetch_add(tickets, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *s_flag = prev == G - 1;
+    }
+  }
+  __syncthreads();
+  if (!*s_flag) return false;
+  if (threadIdx.x < kWave) {
+    const unsigned lane = threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      const float v = lane < G ? __hip_atomic_load(&gpartials[lane * NP + k], __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT)
+                               : 0.f;
+      total[k] = wave_sum(v);
+    }
+    if (lane == 0) __hip_atomic_store(tickets, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  return true;
+}
+
 }  // namespace ocppo

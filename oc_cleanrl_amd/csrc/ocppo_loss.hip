@@ -22,9 +22,9 @@
 namespace ocppo {
 
 constexpr int kLossThreads = 256;  // one element per thread, 256-element tiles
-constexpr int kLossMaxBlocks = 1024;  // grid cap: 4 workgroups per CU; bounds the ticket fan-in
+constexpr int kLossMaxBlocks = 1792;  // grid cap: 7 workgroups per CU (the A <= 6 kernels' occupancy)
 constexpr int kNumPartials = 6;    // pg, v, entropy, old_kl, kl, clipfrac
-constexpr size_t kTicketBytes = 256;
+constexpr size_t kTicketBytes = kHandoffTicketBytes;
 
 // Row statistics of Categorical(logits=l): lse, normalised logits ln = l - lse, probs = softmax(ln)
 // (torch/distributions/categorical.py: logits - logits.logsumexp(-1), then logits_to_probs).
@@ -96,6 +96,64 @@ __device__ __forceinline__ void categorical_backward(const float (&l)[AMAX], flo
 #pragma unroll
   for (int j = 0; j < AMAX; ++j)  // ln = l - logsumexp(l)
     if (j < A) dl[j] = dl[j] - S * expf(l[j] - lse);
+}
+
+// Loss-kernel form of the row statistics: lse (hence ln = l - lse and the log-prob) exactly as
+// above, but the probabilities reuse the logsumexp pass, p = exp(l - m) * (1 / s), instead of a
+// second softmax over ln: mathematically the same softmax (torch evaluates it as
+// softmax(l - lse)), here within an ulp or two of it, for A exps instead of 2A and one division.
+// Only the loss uses it (checked to 1e-6 of scale against the reference's autograd fixtures); the
+// sampler keeps categorical_row so sampled actions stay bit-identical to torch's.
+template <int AMAX>
+__device__ __forceinline__ void categorical_row_loss(const float (&l)[AMAX], int A, float& lse,
+                                                     float (&ln)[AMAX], float (&p)[AMAX]) {
+  float m = l[0];
+#pragma unroll
+  for (int j = 1; j < AMAX; ++j)
+    if (j < A) m = fmaxf(m, l[j]);
+  const float mm = (fabsf(m) == INFINITY) ? 0.f : m;
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < AMAX; ++j)
+    if (j < A) {
+      p[j] = expf(l[j] - m);
+      s += p[j];
+    }
+  lse = logf(s) + mm;
+  const float rs = 1.0f / s;
+#pragma unroll
+  for (int j = 0; j < AMAX; ++j)
+    if (j < A) {
+      ln[j] = l[j] - lse;
+      p[j] = p[j] * rs;
+    }
+}
+
+// categorical_backward with exp(l - lse) (logsumexp's backward) taken as the row's p.
+template <int AMAX>
+__device__ __forceinline__ void categorical_backward_loss(const float (&ln)[AMAX],
+                                                          const float (&p)[AMAX], int A,
+                                                          int64_t a, float g_lp, float g_h,
+                                                          float (&dl)[AMAX]) {
+  const float dplp = -g_h;
+  float dot = 0.f;
+#pragma unroll
+  for (int j = 0; j < AMAX; ++j)
+    if (j < A) dot += (dplp * ln[j]) * p[j];
+  float S = 0.f;
+#pragma unroll
+  for (int j = 0; j < AMAX; ++j)
+    if (j < A) {
+      const float dprob = dplp * ln[j];
+      float d = dplp * p[j];
+      d = d + p[j] * (dprob - dot);
+      if (j == a) d = d + g_lp;
+      dl[j] = d;
+      S += d;
+    }
+#pragma unroll
+  for (int j = 0; j < AMAX; ++j)
+    if (j < A) dl[j] = dl[j] - S * p[j];
 }
 
 // ---- minibatch advantage statistics ------------------------------------------------------------
@@ -242,7 +300,8 @@ struct LossParams {
   float* dvalue;
   float* stats;
   unsigned* ticket;
-  float* partials;  // [gridDim.x][kNumPartials]
+  float* partials;   // [gridDim.x][kNumPartials]
+  float* gpartials;  // [groups][kNumPartials]
   int64_t M;
   int A;
   int norm_adv, clip_vloss;
@@ -261,8 +320,8 @@ struct LossTileRegs {
 
 // Loads tile `tl`'s per-element records (element tid) and logits chunk into registers.
 template <int AMAX>
-__device__ __forceinline__ void loss_tile_load(const LossParams& P, int64_t tl, int64_t ntiles,
-                                               int tid, LossTileRegs<AMAX>& r) {
+__device__ __forceinline__ void loss_tile_load(const LossParams& P, int A, int64_t tl,
+                                               int64_t ntiles, int tid, LossTileRegs<AMAX>& r) {
   r.a = 0;
   r.old_lp = r.adv = r.R = r.v_old = r.v = 0.f;
   if (tl >= ntiles) return;
@@ -278,20 +337,24 @@ __device__ __forceinline__ void loss_tile_load(const LossParams& P, int64_t tl, 
     r.v_old = P.b_val[b];
     r.v = P.new_value[i];
   }
+  const float* lrow = P.logits + i0 * A;
+  const int n = static_cast<int>(cnt) * A;
 #pragma unroll
   for (int k = 0; k < AMAX; ++k) {
-    const int64_t e = static_cast<int64_t>(k) * kLossThreads + tid;
-    r.lg[k] = (k < P.A && e < cnt * P.A) ? P.logits[i0 * P.A + e] : 0.f;
+    const int e = k * kLossThreads + tid;
+    r.lg[k] = (k < A && e < n) ? lrow[e] : 0.f;
   }
 }
 
-template <int AMAX>
-__global__ __launch_bounds__(kLossThreads) void ppo_loss_kernel(LossParams P) {
+// AMAX = the compile-time row width; EXACT: A == AMAX (the Atari minimal action-set sizes are
+// instantiated exactly, so the per-action loops carry no `j < A` guards), else A <= AMAX at run time.
+template <int AMAX, bool EXACT>
+__device__ __forceinline__ void ppo_loss_body(const LossParams& P) {
   extern __shared__ __attribute__((aligned(16))) float tile[];  // [kLossThreads * A]
   __shared__ float red[kLossThreads / kWave][kNumPartials];
   __shared__ int s_last;
 
-  const int A = P.A;
+  const int A = EXACT ? AMAX : P.A;
   const int tid = threadIdx.x;
   float part[kNumPartials] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   const int64_t ntiles = (P.M + kLossThreads - 1) / kLossThreads;
@@ -300,7 +363,7 @@ __global__ __launch_bounds__(kLossThreads) void ppo_loss_kernel(LossParams P) {
   // Software-pipelined: the next tile's records and logits chunk are loaded into registers
   // before the current tile is computed.
   LossTileRegs<AMAX> nxt;
-  loss_tile_load<AMAX>(P, blockIdx.x, ntiles, tid, nxt);
+  loss_tile_load<AMAX>(P, A, blockIdx.x, ntiles, tid, nxt);
   for (int64_t tl = blockIdx.x; tl < ntiles; tl += gridDim.x) {
   const int64_t i0 = tl * kLossThreads;
   const int64_t cnt = (P.M - i0) < kLossThreads ? (P.M - i0) : kLossThreads;
@@ -310,12 +373,13 @@ __global__ __launch_bounds__(kLossThreads) void ppo_loss_kernel(LossParams P) {
   const int64_t a = cur.a;
   const float old_lp = cur.old_lp, adv = cur.adv, R = cur.R, v_old = cur.v_old, v = cur.v;
   // stage this tile's logits rows (contiguous [cnt*A] floats, loaded coalesced) in LDS
+  const int tile_n = static_cast<int>(cnt) * A;
 #pragma unroll
   for (int k = 0; k < AMAX; ++k) {
-    const int64_t e = static_cast<int64_t>(k) * kLossThreads + tid;
-    if (k < A && e < cnt * A) tile[e] = cur.lg[k];
+    const int e = k * kLossThreads + tid;
+    if (k < A && e < tile_n) tile[e] = cur.lg[k];
   }
-  loss_tile_load<AMAX>(P, tl + gridDim.x, ntiles, tid, nxt);
+  loss_tile_load<AMAX>(P, A, tl + gridDim.x, ntiles, tid, nxt);
   __syncthreads();
 
   float dl[AMAX];
@@ -324,7 +388,7 @@ __global__ __launch_bounds__(kLossThreads) void ppo_loss_kernel(LossParams P) {
 #pragma unroll
     for (int j = 0; j < AMAX; ++j) l[j] = j < A ? tile[tid * A + j] : 0.f;
     float lse;
-    categorical_row<AMAX>(l, A, lse, ln, p);
+    categorical_row_loss<AMAX>(l, A, lse, ln, p);
     float new_lp = 0.f;
 #pragma unroll
     for (int j = 0; j < AMAX; ++j)
@@ -380,7 +444,7 @@ __global__ __launch_bounds__(kLossThreads) void ppo_loss_kernel(LossParams P) {
     const float dratio = dr1 + dr2;
     const float dnew_lp = dratio * ratio;  // exp backward, then logratio = new - old
 
-    categorical_backward<AMAX>(l, lse, ln, p, A, a, dnew_lp, P.g_h, dl);
+    categorical_backward_loss<AMAX>(ln, p, A, a, dnew_lp, P.g_h, dl);
     P.dvalue[i] = dv;
   }
   __syncthreads();  // everyone has read its logits row; reuse the tile for dlogits
@@ -390,7 +454,8 @@ __global__ __launch_bounds__(kLossThreads) void ppo_loss_kernel(LossParams P) {
       if (j < A) tile[tid * A + j] = dl[j];
   }
   __syncthreads();
-  for (int64_t e = tid; e < cnt * A; e += kLossThreads) P.dlogits[i0 * A + e] = tile[e];
+  float* drow = P.dlogits + i0 * A;
+  for (int e = tid; e < tile_n; e += kLossThreads) drow[e] = tile[e];
   __syncthreads();  // the next tile restages the LDS tile
   }
 
@@ -402,48 +467,16 @@ __global__ __launch_bounds__(kLossThreads) void ppo_loss_kernel(LossParams P) {
     if (lane == 0) red[wid][k] = w;
   }
   __syncthreads();
+  float mine[kNumPartials], s[kNumPartials];
   if (tid == 0) {
-    unsigned* tk = P.ticket;
 #pragma unroll
     for (int k = 0; k < kNumPartials; ++k) {
-      float s = red[0][k];
-      for (int w = 1; w < kLossThreads / kWave; ++w) s += red[w][k];
-      __hip_atomic_store(&P.partials[blockIdx.x * kNumPartials + k], s, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
+      mine[k] = red[0][k];
+      for (int w = 1; w < kLossThreads / kWave; ++w) mine[k] += red[w][k];
     }
-    // hand-off (MI355X_MICROARCH.md "Valid forms", table row 1): the partials are written
-    // through with sc1 stores, drained, then ONE agent-scope atomic add signals; the last adder
-    // reads them with sc1 loads only. No release/acquire fence, so the dlogits lines this block
-    // just dirtied are not written back from L2 here.
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned prev = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = (prev == gridDim.x - 1) ? 1 : 0;
   }
-  __syncthreads();
-  if (!s_last) return;
-
-  // last workgroup: combine the partials of every block in block order
-  float tot[kNumPartials] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (unsigned blk = tid; blk < gridDim.x; blk += kLossThreads) {
-#pragma unroll
-    for (int k = 0; k < kNumPartials; ++k)
-      tot[k] += __hip_atomic_load(&P.partials[blk * kNumPartials + k], __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_AGENT);
-  }
-#pragma unroll
-  for (int k = 0; k < kNumPartials; ++k) {
-    const float w = wave_sum(tot[k]);
-    __syncthreads();
-    if (lane == 0) red[wid][k] = w;
-  }
-  __syncthreads();
+  if (!handoff_combine<kNumPartials>(mine, P.ticket, P.partials, P.gpartials, s, &s_last)) return;
   if (tid == 0) {
-    float s[kNumPartials];
-#pragma unroll
-    for (int k = 0; k < kNumPartials; ++k) {
-      s[k] = red[0][k];
-      for (int w = 1; w < kLossThreads / kWave; ++w) s[k] += red[w][k];
-    }
     const float pg_loss = s[0] * P.inv_m;
     const float v_loss = 0.5f * (s[1] * P.inv_m);
     const float ent = s[2] * P.inv_m;
@@ -457,8 +490,21 @@ __global__ __launch_bounds__(kLossThreads) void ppo_loss_kernel(LossParams P) {
     P.stats[OCPPO_STAT_CLIPFRAC] = s[5] * P.inv_m;
     P.stats[OCPPO_STAT_ADV_MEAN] = P.norm_adv ? P.adv_stats[0] : 0.f;
     P.stats[OCPPO_STAT_ADV_STD] = P.norm_adv ? P.adv_stats[1] : 0.f;
-    __hip_atomic_store(P.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
   }
+}
+
+template <int AMAX, bool EXACT>
+__global__ __launch_bounds__(kLossThreads) void ppo_loss_kernel(LossParams P) {
+  ppo_loss_body<AMAX, EXACT>(P);
+}
+
+// Small exact action sets (A <= 6) fit 72 VGPRs without spilling: ask for 7 waves per SIMD (the
+// grid cap, kLossMaxBlocks, is sized for it) instead of the 4 the hand-off's live ranges cost.
+template <int AMAX>
+__global__ __launch_bounds__(kLossThreads) __attribute__((amdgpu_waves_per_eu(7)))
+void ppo_loss_kernel_small(LossParams P) {
+  static_assert(AMAX <= 6, "register budget sized for A <= 6");
+  ppo_loss_body<AMAX, true>(P);
 }
 
 // ---- Categorical action head ---------------------------------------------------------------------
@@ -785,10 +831,18 @@ __global__ __launch_bounds__(256) void policy_head_fast_kernel(
 
 using namespace ocppo;
 
+// workspace: [tickets | per-block partials | per-group partials | adv stats (2 floats)]
+static int64_t loss_blocks(int64_t M) {
+  const int64_t nb = ceil_div(M, kLossThreads);
+  return nb < kLossMaxBlocks ? nb : kLossMaxBlocks;
+}
+static size_t round16(size_t n) { return (n + 15) / 16 * 16; }
 static size_t loss_partials_offset() { return kTicketBytes; }
+static size_t loss_gpartials_offset(int64_t M) {
+  return kTicketBytes + round16(static_cast<size_t>(loss_blocks(M)) * kNumPartials * sizeof(float));
+}
 static size_t loss_stats_offset(int64_t M) {
-  const size_t nb = static_cast<size_t>(ceil_div(M, kLossThreads));
-  return kTicketBytes + ((nb * kNumPartials * sizeof(float) + 15) / 16) * 16;
+  return loss_gpartials_offset(M) + round16(kHandoffMaxGroups * kNumPartials * sizeof(float));
 }
 
 extern "C" size_t ocppo_ppo_loss_workspace_bytes(int64_t M, int64_t A) {
@@ -851,6 +905,7 @@ extern "C" int ocppo_ppo_loss_fwd_bwd(ocppo_stream_t stream, const float* logits
   P.stats = stats;
   P.ticket = reinterpret_cast<unsigned*>(ws);
   P.partials = reinterpret_cast<float*>(ws + loss_partials_offset());
+  P.gpartials = reinterpret_cast<float*>(ws + loss_gpartials_offset(M));
   P.M = M;
   P.A = static_cast<int>(A);
   P.norm_adv = norm_adv ? 1 : 0;
@@ -867,13 +922,22 @@ extern "C" int ocppo_ppo_loss_fwd_bwd(ocppo_stream_t stream, const float* logits
   P.g_h = (-1.0f * P.ent_coef) / fm;
   P.g_v = (P.vf_coef * 0.5f) / fm;
   P.inv_m = 1.0f / fm;
-  int64_t nb = ceil_div(M, kLossThreads);
-  nb = nb < kLossMaxBlocks ? nb : kLossMaxBlocks;
+  const int64_t nb = loss_blocks(M);
+  static_assert(kLossMaxBlocks <= kHandoffMaxBlocks, "hand-off capacity");
   const size_t lds = sizeof(float) * kLossThreads * A;
-  if (A <= 8)
-    hipLaunchKernelGGL(ppo_loss_kernel<8>, dim3(nb), dim3(kLossThreads), lds, s, P);
-  else
-    hipLaunchKernelGGL(ppo_loss_kernel<kMaxActions>, dim3(nb), dim3(kLossThreads), lds, s, P);
+  const dim3 g(static_cast<unsigned>(nb)), b(kLossThreads);
+  switch (A) {
+    case 3: hipLaunchKernelGGL(ppo_loss_kernel_small<3>, g, b, lds, s, P); break;
+    case 4: hipLaunchKernelGGL(ppo_loss_kernel_small<4>, g, b, lds, s, P); break;
+    case 6: hipLaunchKernelGGL(ppo_loss_kernel_small<6>, g, b, lds, s, P); break;
+    case 9: hipLaunchKernelGGL((ppo_loss_kernel<9, true>), g, b, lds, s, P); break;
+    case 18: hipLaunchKernelGGL((ppo_loss_kernel<18, true>), g, b, lds, s, P); break;
+    default:
+      if (A <= 8)
+        hipLaunchKernelGGL((ppo_loss_kernel<8, false>), g, b, lds, s, P);
+      else
+        hipLaunchKernelGGL((ppo_loss_kernel<kMaxActions, false>), g, b, lds, s, P);
+  }
   return check_launch("ocppo_ppo_loss_fwd_bwd");
 }
 
