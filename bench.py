@@ -12,7 +12,10 @@ value = env steps of all ranks / max-over-ranks wall time of the K timed iterati
 
 Rank 0 prints ONE JSON line. Extra fields: `roofline` (dominant HIP kernel of this package, live
 HIP-event timing over the timed region), `kernels` (every HIP kernel's mean launch duration and
-algorithmic GB/s), `cpu_baseline` (the oracle's CPU port of the same loop timed on this host, N=1).
+algorithmic GB/s), `roofline_scaled` (N=1: the north-star kernels -- GAE, fused PPO loss -- and the
+rollout head re-timed at streaming sizes, where HBM rather than launch latency bounds them; same
+algorithmic-byte formulas, tools/kernel_bench.py cases), `cpu_baseline` (the oracle's CPU port of
+the same loop timed on this host, N=1).
 """
 from __future__ import annotations
 
@@ -30,6 +33,19 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
+# HBM bytes per launch from rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE, separate passes) of
+# the same launch shapes: tools/profile_round.sh -> tools/summarize_profiles.py
+PMC_SUMMARY = ROOT / "profiles" / "r01b" / "pmc_summary.json"
+PMC_KEYS = {"action_head": "policy_head_config", "gae": "gae_config",
+            "ppo_loss": "ppo_loss_prepared_config"}
+
+
+def pmc_traffic(key):
+    try:
+        rec = json.loads(PMC_SUMMARY.read_text())["kernels"][key]
+        return rec.get("traffic_bytes"), str(PMC_SUMMARY.relative_to(ROOT))
+    except (OSError, KeyError, ValueError):
+        return None, None
 
 
 def kernel_bytes(tr) -> dict:
@@ -69,6 +85,7 @@ def main():
     ap.add_argument("--cpu-iterations", type=int, default=3)
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--no-scaled", action="store_true", help="skip roofline_scaled")
     opt = ap.parse_args()
 
     from oc_cleanrl_amd.args import Args, finalize
@@ -126,10 +143,24 @@ def main():
     roofline = None
     if dom:
         ach = kernels[dom]["GBps"]
+        traffic, src = pmc_traffic(PMC_KEYS.get(dom, ""))
         roofline = {"kernel": dom, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5),
-                    "traffic": None, "bytes_per_launch": kb[dom],
+                    "traffic": traffic, "traffic_source": src, "bytes_per_launch": kb[dom],
                     "mean_launch_us": kernels[dom]["mean_us"]}
+
+    scaled = None
+    if rank == 0 and world == 1 and not opt.no_scaled:
+        from tools.kernel_bench import run_case
+
+        scaled = {}
+        for name in ("gae", "ppo_loss_prepared", "policy_head"):
+            r = run_case(name, "scaled", device, reps=10, rounds=5)
+            traffic, _ = pmc_traffic(f"{name}_scaled")
+            scaled[name] = {"params": r["params"], "mean_us": r["mean_us"], "bytes": r["bytes"],
+                            "achieved": r["GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": r["frac"], "traffic": traffic}
+            torch.cuda.empty_cache()
 
     cpu = None
     if rank == 0 and world == 1 and not opt.no_cpu_baseline:
@@ -170,6 +201,7 @@ def main():
                        "parallelism": f"dp{world}"},
             "updates_per_sec": round(updates / dt, 2),
             "roofline": roofline,
+            "roofline_scaled": scaled,
             "kernels": kernels,
             "cpu_baseline": cpu,
         }
