@@ -59,7 +59,7 @@ def kernel_bytes(tr) -> dict:
         "gae": 20 * T * N + 8 * N,
         # logits 4A + value 4 + action 8 + old logprob/adv/return/value 16 in (contiguous,
         # prepared); dlogits 4A + dv 4 out
-        "ppo_loss": (8 * A + 28) * M,
+        "ppo_loss": (8 * A + 32) * M,
         # index 8 + row read (storage dtype) + f32 row write
         "gather": M * (8 + W * D * (sb + 4)),
         # prev slot (W-1 frames) + new frame + done in; slot + f32 net obs out; done row; fused
@@ -72,6 +72,9 @@ def kernel_bytes(tr) -> dict:
         "env_step": N * (8 + D * fb + 8 + 2 * 20),
         # perm index + 5 gathered per-sample values in, 5 written in minibatch order
         "mb_prepare": tr.E * tr.B * (8 + 2 * (8 + 16)),
+        # fresh encoding row + done + W-1 shifted slots in; W slots out
+        "frame_cache": (N * (4 + 4 * tr.enc_cache.shape[2] * (2 * tr.enc_cache.shape[1]))
+                        if tr.enc_cache is not None else None),
     }
 
 
@@ -86,6 +89,8 @@ def main():
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--no-scaled", action="store_true", help="skip roofline_scaled")
+    ap.add_argument("--set", action="append", default=[], metavar="FIELD=VALUE",
+                    help="override an Args field (experiments; e.g. --set rollout_frame_cache=0)")
     opt = ap.parse_args()
 
     from oc_cleanrl_amd.args import Args, finalize
@@ -105,6 +110,10 @@ def main():
     args = Args(env_id="ALE/Pong-v5", obs_mode="obj", architecture="PPO_OBJ",
                 num_envs=opt.envs_per_gpu * world, num_steps=128, num_features=12,
                 total_timesteps=10_000_000, cuda_graphs=not opt.no_graphs, save_model=False)
+    for kv in opt.set:
+        k, v = kv.split("=", 1)
+        cur = getattr(args, k)
+        setattr(args, k, (v.lower() in ("1", "true", "yes")) if isinstance(cur, bool) else type(cur)(v))
     args = finalize(args, world)
     tr = PPOTrainer(args, device, rank, world, kernel_timing=not opt.no_kernel_timing, log=False)
 

@@ -221,6 +221,19 @@ OCPPO_API int ocppo_obs_reset(ocppo_stream_t stream, const void* frame, int fram
                     int64_t W, int64_t D, void* obs_out, int obs_dtype, float* net_obs);
 
 /* ---------------------------------------------------------------------------------------------
+ * Frame-encoding cache of the rollout forward (PPObj, architectures/ppo.py:60-84, whose encoder
+ * is applied to each stacked frame on its own). `agent.get_action_and_value(next_obs)` at
+ * ppo_atari_oc.py:506 re-encodes all W stacked frames every step although W-1 of them were
+ * encoded at the previous steps under the same weights; with this entry point the caller encodes
+ * only the newest frame and shifts the cache like the frame stack (same reset fill as
+ * ocppo_rollout_store):
+ *   enc[n, w, :] = done[n] != 0 || w == W-1 ? fresh[n, :] : enc[n, w+1, :]   (in place)
+ * enc [N, W, E] f32, fresh [N, E] f32 with row stride ld_fresh (>= E), done [N] f32 or NULL.
+ * ------------------------------------------------------------------------------------------- */
+OCPPO_API int ocppo_frame_cache_shift(ocppo_stream_t stream, float* enc, const float* fresh,
+                            int64_t ld_fresh, const float* done, int64_t N, int64_t W, int64_t E);
+
+/* ---------------------------------------------------------------------------------------------
  * Minibatch gather — replaces `b_obs[mb_inds]` of ppo_atari_oc.py:566-567:
  *   dst[i, :] = f32(src[idx[i], :]),  src [B, R] of dtype src_dtype, dst [M, R] f32.
  * ------------------------------------------------------------------------------------------- */

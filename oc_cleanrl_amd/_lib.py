@@ -9,13 +9,16 @@ There is no CPU fallback: if the library is missing, importing this module raise
 from __future__ import annotations
 
 import ctypes
+import os
 import re
 from pathlib import Path
 
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 PKG = Path(__file__).resolve().parent
-LIB_PATH = PKG / "lib" / "libocppo_hip.so"
+# OCPPO_LIB: load another build of the same C-ABI (experiments, e.g. a probe variant); default
+# is the in-tree build
+LIB_PATH = Path(os.environ.get("OCPPO_LIB", PKG / "lib" / "libocppo_hip.so"))
 HEADER = PKG.parent / "include" / "ocppo.h"
 
 # constants mirrored from include/ocppo.h (checked against the header by tests/test_abi.py)
@@ -47,6 +50,7 @@ SIGNATURES: dict[str, tuple[type, list]] = {
     "ocppo_rollout_store": (I, [P, P, I, P, P, I64, I64, I64, P, P, I, P, P, P]),
     "ocppo_obs_reset": (I, [P, P, I, I64, I64, I64, P, I, P]),
     "ocppo_gather_rows": (I, [P, P, I, P, I64, I64, P]),
+    "ocppo_frame_cache_shift": (I, [P, P, P, I64, P, I64, I64, I64]),
     "ocppo_vecnorm_reward": (I, [P, P, P, I64, D, D, D, P, P, P]),
     "ocppo_rollout_store_vecnorm": (I, [P, P, I, P, P, I64, I64, I64, P, P, I, P, P, D, D, D, P,
                                         P, P]),

@@ -228,6 +228,22 @@ class PPObj(_ActorCritic):
         self.network = nn.Sequential(*layers)
         self.actor = layer_init(nn.Linear(l, envs.action_space.n), std=0.01)
         self.critic = layer_init(nn.Linear(l, 1), std=1)
+        self._flat = len(encoder_dims) * 2  # index of the Flatten in self.network
+
+    # The encoder acts on each stacked frame alone (Linear on the last dim), so the rollout can
+    # encode only the newest frame per step and keep the rest in a cache (ops.frame_cache_shift).
+    @property
+    def encoding_dim(self) -> int:
+        return self.network[self._flat - 2].out_features
+
+    def encode(self, x):
+        """Per-frame encoder output: [..., F] -> [..., E]."""
+        return fused_trunk(self.network[:self._flat], x)
+
+    def decode(self, enc):
+        """Flatten + decoder on the stacked frame encodings [B, W, E] -> hidden [B, H];
+        decode(encode(x)) == trunk(x)."""
+        return fused_trunk(self.network[self._flat:], enc)
 
 
 class CartPoleAgent(_ActorCritic):

@@ -116,6 +116,7 @@ class Args:
     log_dir: str = "runs"
     save_model: bool = True
     metrics_every: int = 1     # read the device-side metrics every N iterations
+    rollout_frame_cache: bool = False  # PPO_OBJ rollout: encode only the newest frame per step
 
 
 def _flag_names(name: str) -> list[str]:

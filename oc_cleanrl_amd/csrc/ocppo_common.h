@@ -114,7 +114,7 @@ __device__ __forceinline__ T block_sum(T v, T* scratch) {
 // Tickets re-arm themselves (graph replay). Sums run over lanes by a fixed butterfly, so the
 // result is deterministic for a given grid.
 constexpr int kHandoffGroup = 32;
-constexpr int kHandoffMaxGroups = 64;  // nb <= 2048
+constexpr int kHandoffMaxGroups = 256;  // nb <= 8192
 constexpr int kHandoffMaxBlocks = kHandoffGroup * kHandoffMaxGroups;
 constexpr int kTicketStride = 32;      // unsigned per 128-B line
 constexpr size_t kHandoffTicketBytes = (1 + kHandoffMaxGroups) * kTicketStride * sizeof(unsigned);
@@ -168,9 +168,9 @@ __device__ __forceinline__ bool handoff_combine(const float (&mine)[NP], unsigne
     const unsigned lane = threadIdx.x;
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
-      const float v = lane < G ? __hip_atomic_load(&gpartials[lane * NP + k], __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT)
-                               : 0.f;
+      float v = 0.f;  // group partials lane, lane + 64, ... in a fixed order
+      for (unsigned q = lane; q < G; q += kWave)
+        v += __hip_atomic_load(&gpartials[q * NP + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       total[k] = wave_sum(v);
     }
     if (lane == 0) __hip_atomic_store(tickets, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

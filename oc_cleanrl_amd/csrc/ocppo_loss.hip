@@ -346,119 +346,11 @@ __device__ __forceinline__ void loss_tile_load(const LossParams& P, int A, int64
   }
 }
 
-// AMAX = the compile-time row width; EXACT: A == AMAX (the Atari minimal action-set sizes are
-// instantiated exactly, so the per-action loops carry no `j < A` guards), else A <= AMAX at run time.
-template <int AMAX, bool EXACT>
-__device__ __forceinline__ void ppo_loss_body(const LossParams& P) {
-  extern __shared__ __attribute__((aligned(16))) float tile[];  // [kLossThreads * A]
+// Block partials (fixed order) -> two-level hand-off -> the minibatch means in the last block.
+__device__ __forceinline__ void loss_finish(const LossParams& P, const float (&part)[kNumPartials]) {
   __shared__ float red[kLossThreads / kWave][kNumPartials];
   __shared__ int s_last;
-
-  const int A = EXACT ? AMAX : P.A;
   const int tid = threadIdx.x;
-  float part[kNumPartials] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  const int64_t ntiles = (P.M + kLossThreads - 1) / kLossThreads;
-  // grid-stride over 256-element tiles (the grid is capped at kLossMaxBlocks so the ticket
-  // fan-in stays bounded); each thread accumulates its partials over its tiles in order.
-  // Software-pipelined: the next tile's records and logits chunk are loaded into registers
-  // before the current tile is computed.
-  LossTileRegs<AMAX> nxt;
-  loss_tile_load<AMAX>(P, A, blockIdx.x, ntiles, tid, nxt);
-  for (int64_t tl = blockIdx.x; tl < ntiles; tl += gridDim.x) {
-  const int64_t i0 = tl * kLossThreads;
-  const int64_t cnt = (P.M - i0) < kLossThreads ? (P.M - i0) : kLossThreads;
-  const bool active = tid < cnt;
-  const int64_t i = i0 + tid;
-  const LossTileRegs<AMAX> cur = nxt;
-  const int64_t a = cur.a;
-  const float old_lp = cur.old_lp, adv = cur.adv, R = cur.R, v_old = cur.v_old, v = cur.v;
-  // stage this tile's logits rows (contiguous [cnt*A] floats, loaded coalesced) in LDS
-  const int tile_n = static_cast<int>(cnt) * A;
-#pragma unroll
-  for (int k = 0; k < AMAX; ++k) {
-    const int e = k * kLossThreads + tid;
-    if (k < A && e < tile_n) tile[e] = cur.lg[k];
-  }
-  loss_tile_load<AMAX>(P, A, tl + gridDim.x, ntiles, tid, nxt);
-  __syncthreads();
-
-  float dl[AMAX];
-  if (active) {
-    float l[AMAX], ln[AMAX], p[AMAX];
-#pragma unroll
-    for (int j = 0; j < AMAX; ++j) l[j] = j < A ? tile[tid * A + j] : 0.f;
-    float lse;
-    categorical_row_loss<AMAX>(l, A, lse, ln, p);
-    float new_lp = 0.f;
-#pragma unroll
-    for (int j = 0; j < AMAX; ++j)
-      if (j == a) new_lp = ln[j];
-    const float H = categorical_entropy<AMAX>(ln, p, A);
-
-    // ratio and no-grad diagnostics (:569-575)
-    const float logratio = new_lp - old_lp;
-    const float ratio = expf(logratio);
-    part[3] += -logratio;
-    part[4] += (ratio - 1.0f) - logratio;
-    part[5] += fabsf(ratio - 1.0f) > P.clip ? 1.f : 0.f;
-
-    // advantage normalisation (:577-579)
-    float advn = adv;
-    if (P.norm_adv) advn = (adv - P.adv_stats[0]) / (P.adv_stats[1] + 1e-8f);
-
-    // clipped surrogate (:581-583)
-    const float nadv = -advn;
-    const float pg1 = nadv * ratio;
-    const float rc = fminf(fmaxf(ratio, P.clip_lo), P.clip_hi);
-    const float pg2 = nadv * rc;
-    part[0] += fmaxf(pg1, pg2);
-
-    // value loss (:585-597)
-    const float du = v - R;
-    const float vu = du * du;
-    float dv;
-    if (P.clip_vloss) {
-      const float dvv = v - v_old;
-      const float dvc = fminf(fmaxf(dvv, -P.clip), P.clip);
-      const float vcl = v_old + dvc;
-      const float dc = vcl - R;
-      const float vc = dc * dc;
-      part[1] += fmaxf(vu, vc);
-      const float gu = vu > vc ? P.g_v : (vu == vc ? P.g_v / 2.f : 0.f);
-      const float gc = vc > vu ? P.g_v : (vu == vc ? P.g_v / 2.f : 0.f);
-      const float tu = gu * (2.0f * du);
-      float tc = gc * (2.0f * dc);
-      tc = (dvv >= -P.clip && dvv <= P.clip) ? tc : 0.f;
-      dv = tu + tc;
-    } else {
-      part[1] += vu;
-      dv = P.g_v * (2.0f * du);
-    }
-    part[2] += H;
-
-    // backward of the surrogate to new_logprob
-    const float g1 = pg1 > pg2 ? P.g_pg : (pg1 == pg2 ? P.g_pg / 2.f : 0.f);
-    const float g2 = pg2 > pg1 ? P.g_pg : (pg1 == pg2 ? P.g_pg / 2.f : 0.f);
-    const float dr1 = g1 * nadv;
-    const float dr2 = (ratio >= P.clip_lo && ratio <= P.clip_hi) ? g2 * nadv : 0.f;
-    const float dratio = dr1 + dr2;
-    const float dnew_lp = dratio * ratio;  // exp backward, then logratio = new - old
-
-    categorical_backward_loss<AMAX>(ln, p, A, a, dnew_lp, P.g_h, dl);
-    P.dvalue[i] = dv;
-  }
-  __syncthreads();  // everyone has read its logits row; reuse the tile for dlogits
-  if (active) {
-#pragma unroll
-    for (int j = 0; j < AMAX; ++j)
-      if (j < A) tile[tid * A + j] = dl[j];
-  }
-  __syncthreads();
-  float* drow = P.dlogits + i0 * A;
-  for (int e = tid; e < tile_n; e += kLossThreads) drow[e] = tile[e];
-  __syncthreads();  // the next tile restages the LDS tile
-  }
-
   // per-block partial sums in a fixed order
   const int lane = tid & (kWave - 1), wid = tid / kWave;
 #pragma unroll
@@ -493,6 +385,144 @@ __device__ __forceinline__ void ppo_loss_body(const LossParams& P) {
   }
 }
 
+// One element of the fused loss: forward terms accumulated into part[], and the autograd
+// backward of the minibatch loss to this row's logits (dl) and new value (dv).
+// adv_mean / adv_den: the minibatch mean and std + 1e-8 (f32, as torch rounds them), read from
+// P.adv_stats ONCE per thread by the caller: a load inside the element loop makes the compiler
+// drain every outstanding (prefetch) load with it.
+template <int AMAX>
+__device__ __forceinline__ void loss_element(const LossParams& P, int A, const float (&l)[AMAX],
+                                             int64_t a, float old_lp, float adv, float R,
+                                             float v_old, float v, float adv_mean, float adv_den,
+                                             float (&part)[kNumPartials], float (&dl)[AMAX],
+                                             float& dv) {
+#ifdef OCPPO_LOSS_PROBE  // bandwidth probe build (tools/): same traffic, trivial arithmetic
+  dv = v + R + v_old + adv + old_lp;
+  part[0] += dv;
+#pragma unroll
+  for (int j = 0; j < AMAX; ++j) dl[j] = l[j] + (j == a ? 1.f : 0.f);
+  return;
+#endif
+  float ln[AMAX], p[AMAX];
+  float lse;
+  categorical_row_loss<AMAX>(l, A, lse, ln, p);
+  float new_lp = 0.f;
+#pragma unroll
+  for (int j = 0; j < AMAX; ++j)
+    if (j == a) new_lp = ln[j];
+  const float H = categorical_entropy<AMAX>(ln, p, A);
+
+  // ratio and no-grad diagnostics (:569-575)
+  const float logratio = new_lp - old_lp;
+  const float ratio = expf(logratio);
+  part[3] += -logratio;
+  part[4] += (ratio - 1.0f) - logratio;
+  part[5] += fabsf(ratio - 1.0f) > P.clip ? 1.f : 0.f;
+
+  // advantage normalisation (:577-579)
+  float advn = adv;
+  if (P.norm_adv) advn = (adv - adv_mean) / adv_den;
+
+  // clipped surrogate (:581-583)
+  const float nadv = -advn;
+  const float pg1 = nadv * ratio;
+  const float rc = fminf(fmaxf(ratio, P.clip_lo), P.clip_hi);
+  const float pg2 = nadv * rc;
+  part[0] += fmaxf(pg1, pg2);
+
+  // value loss (:585-597)
+  const float du = v - R;
+  const float vu = du * du;
+  if (P.clip_vloss) {
+    const float dvv = v - v_old;
+    const float dvc = fminf(fmaxf(dvv, -P.clip), P.clip);
+    const float vcl = v_old + dvc;
+    const float dc = vcl - R;
+    const float vc = dc * dc;
+    part[1] += fmaxf(vu, vc);
+    const float gu = vu > vc ? P.g_v : (vu == vc ? P.g_v / 2.f : 0.f);
+    const float gc = vc > vu ? P.g_v : (vu == vc ? P.g_v / 2.f : 0.f);
+    const float tu = gu * (2.0f * du);
+    float tc = gc * (2.0f * dc);
+    tc = (dvv >= -P.clip && dvv <= P.clip) ? tc : 0.f;
+    dv = tu + tc;
+  } else {
+    part[1] += vu;
+    dv = P.g_v * (2.0f * du);
+  }
+  part[2] += H;
+
+  // backward of the surrogate to new_logprob
+  const float g1 = pg1 > pg2 ? P.g_pg : (pg1 == pg2 ? P.g_pg / 2.f : 0.f);
+  const float g2 = pg2 > pg1 ? P.g_pg : (pg1 == pg2 ? P.g_pg / 2.f : 0.f);
+  const float dr1 = g1 * nadv;
+  const float dr2 = (ratio >= P.clip_lo && ratio <= P.clip_hi) ? g2 * nadv : 0.f;
+  const float dratio = dr1 + dr2;
+  const float dnew_lp = dratio * ratio;  // exp backward, then logratio = new - old
+
+  categorical_backward_loss<AMAX>(ln, p, A, a, dnew_lp, P.g_h, dl);
+}
+
+// AMAX = the compile-time row width; EXACT: A == AMAX (the Atari minimal action-set sizes are
+// instantiated exactly, so the per-action loops carry no `j < A` guards), else A <= AMAX at run time.
+template <int AMAX, bool EXACT>
+__device__ __forceinline__ void ppo_loss_body(const LossParams& P) {
+  extern __shared__ __attribute__((aligned(16))) float tile[];  // [kLossThreads * A]
+
+  const int A = EXACT ? AMAX : P.A;
+  const int tid = threadIdx.x;
+  float part[kNumPartials] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const float adv_mean = P.norm_adv ? P.adv_stats[0] : 0.f;
+  const float adv_den = P.norm_adv ? P.adv_stats[1] + 1e-8f : 1.f;
+  const int64_t ntiles = (P.M + kLossThreads - 1) / kLossThreads;
+  // grid-stride over 256-element tiles (the grid is capped at kLossMaxBlocks so the ticket
+  // fan-in stays bounded); each thread accumulates its partials over its tiles in order.
+  // Software-pipelined: the next tile's records and logits chunk are loaded into registers
+  // before the current tile is computed.
+  LossTileRegs<AMAX> nxt;
+  loss_tile_load<AMAX>(P, A, blockIdx.x, ntiles, tid, nxt);
+  for (int64_t tl = blockIdx.x; tl < ntiles; tl += gridDim.x) {
+  const int64_t i0 = tl * kLossThreads;
+  const int64_t cnt = (P.M - i0) < kLossThreads ? (P.M - i0) : kLossThreads;
+  const bool active = tid < cnt;
+  const int64_t i = i0 + tid;
+  const LossTileRegs<AMAX> cur = nxt;
+  const int64_t a = cur.a;
+  const float old_lp = cur.old_lp, adv = cur.adv, R = cur.R, v_old = cur.v_old, v = cur.v;
+  // stage this tile's logits rows (contiguous [cnt*A] floats, loaded coalesced) in LDS
+  const int tile_n = static_cast<int>(cnt) * A;
+#pragma unroll
+  for (int k = 0; k < AMAX; ++k) {
+    const int e = k * kLossThreads + tid;
+    if (k < A && e < tile_n) tile[e] = cur.lg[k];
+  }
+  loss_tile_load<AMAX>(P, A, tl + gridDim.x, ntiles, tid, nxt);
+  __syncthreads();
+
+  float dl[AMAX];
+  if (active) {
+    float l[AMAX];
+#pragma unroll
+    for (int j = 0; j < AMAX; ++j) l[j] = j < A ? tile[tid * A + j] : 0.f;
+    float dv;
+    loss_element<AMAX>(P, A, l, a, old_lp, adv, R, v_old, v, adv_mean, adv_den, part, dl, dv);
+    P.dvalue[i] = dv;
+  }
+  __syncthreads();  // everyone has read its logits row; reuse the tile for dlogits
+  if (active) {
+#pragma unroll
+    for (int j = 0; j < AMAX; ++j)
+      if (j < A) tile[tid * A + j] = dl[j];
+  }
+  __syncthreads();
+  float* drow = P.dlogits + i0 * A;
+  for (int e = tid; e < tile_n; e += kLossThreads) drow[e] = tile[e];
+  __syncthreads();  // the next tile restages the LDS tile
+  }
+
+  loss_finish(P, part);
+}
+
 template <int AMAX, bool EXACT>
 __global__ __launch_bounds__(kLossThreads) void ppo_loss_kernel(LossParams P) {
   ppo_loss_body<AMAX, EXACT>(P);
@@ -505,6 +535,140 @@ __global__ __launch_bounds__(kLossThreads) __attribute__((amdgpu_waves_per_eu(7)
 void ppo_loss_kernel_small(LossParams P) {
   static_assert(AMAX <= 6, "register budget sized for A <= 6");
   ppo_loss_body<AMAX, true>(P);
+}
+
+// Streaming form for large minibatches with records already in minibatch order (mb_inds == NULL,
+// as ocppo_minibatch_prepare leaves them): each thread owns kLossVec CONSECUTIVE elements, so
+// every per-element array moves as one 16-B load or store per lane (actions: two), and the
+// [kLossTile, A] logits / dlogits tiles pass through LDS as coalesced 16-B vectors (A per lane).
+// 4x fewer tiles, barriers and load instructions per element than ppo_loss_kernel; the arithmetic
+// per element is the same loss_element, so dlogits / dvalue are bit-identical to it. The tail tile
+// (M % kLossTile elements) takes guarded scalar accesses.
+constexpr int kLossVec = 4;
+constexpr int kLossTile = kLossThreads * kLossVec;
+
+// Registers of one full tile for one thread: kLossVec consecutive records + its A float4s of the
+// tile's logits (coalesced: float4 k*256 + tid of the tile).
+template <int A>
+struct LossVecRegs {
+  int64_t act[kLossVec];
+  float olp[kLossVec], adv[kLossVec], ret[kLossVec], vold[kLossVec], vnew[kLossVec];
+  float4 lg[A];
+};
+
+template <int A>
+__device__ __forceinline__ void loss_vec_load(const LossParams& P, int64_t tl, int tid,
+                                              LossVecRegs<A>& r) {
+  const int64_t e0 = tl * kLossTile + static_cast<int64_t>(tid) * kLossVec;
+  const longlong2 a01 = *reinterpret_cast<const longlong2*>(P.b_actions + e0);
+  const longlong2 a23 = *reinterpret_cast<const longlong2*>(P.b_actions + e0 + 2);
+  r.act[0] = a01.x; r.act[1] = a01.y; r.act[2] = a23.x; r.act[3] = a23.y;
+  const float4 x0 = *reinterpret_cast<const float4*>(P.b_logprobs + e0);
+  const float4 x1 = *reinterpret_cast<const float4*>(P.b_adv + e0);
+  const float4 x2 = *reinterpret_cast<const float4*>(P.b_ret + e0);
+  const float4 x3 = *reinterpret_cast<const float4*>(P.b_val + e0);
+  const float4 x4 = *reinterpret_cast<const float4*>(P.new_value + e0);
+  r.olp[0] = x0.x; r.olp[1] = x0.y; r.olp[2] = x0.z; r.olp[3] = x0.w;
+  r.adv[0] = x1.x; r.adv[1] = x1.y; r.adv[2] = x1.z; r.adv[3] = x1.w;
+  r.ret[0] = x2.x; r.ret[1] = x2.y; r.ret[2] = x2.z; r.ret[3] = x2.w;
+  r.vold[0] = x3.x; r.vold[1] = x3.y; r.vold[2] = x3.z; r.vold[3] = x3.w;
+  r.vnew[0] = x4.x; r.vnew[1] = x4.y; r.vnew[2] = x4.z; r.vnew[3] = x4.w;
+  const float4* lsrc = reinterpret_cast<const float4*>(P.logits + tl * kLossTile * A);
+#pragma unroll
+  for (int k = 0; k < A; ++k) r.lg[k] = lsrc[k * kLossThreads + tid];
+}
+
+// Tile compute + write-back shared by the full and the tail tiles. `rec` holds the records of
+// this thread's kLossVec rows; the tile's logits are in LDS.
+template <int A, bool FULL>
+__device__ __forceinline__ void loss_vec_tile(const LossParams& P, float* tile, int64_t i0,
+                                              int64_t cnt, int tid, const LossVecRegs<A>& rec,
+                                              float adv_mean, float adv_den,
+                                              float (&part)[kNumPartials]) {
+  const int64_t e0 = i0 + static_cast<int64_t>(tid) * kLossVec;
+  float dl[kLossVec][A];
+  float dv[kLossVec];
+#pragma unroll
+  for (int r = 0; r < kLossVec; ++r) {
+    const int row = tid * kLossVec + r;
+    if (FULL || row < cnt) {
+      float l[A];
+#pragma unroll
+      for (int j = 0; j < A; ++j) l[j] = tile[row * A + j];
+      loss_element<A>(P, A, l, rec.act[r], rec.olp[r], rec.adv[r], rec.ret[r], rec.vold[r],
+                      rec.vnew[r], adv_mean, adv_den, part, dl[r], dv[r]);
+    } else {
+      dv[r] = 0.f;
+#pragma unroll
+      for (int j = 0; j < A; ++j) dl[r][j] = 0.f;
+    }
+  }
+  __syncthreads();  // every row has been read: the tile takes dlogits
+#pragma unroll
+  for (int r = 0; r < kLossVec; ++r)
+#pragma unroll
+    for (int j = 0; j < A; ++j) tile[(tid * kLossVec + r) * A + j] = dl[r][j];
+  __syncthreads();
+  float* ddst = P.dlogits + i0 * A;
+  if (FULL) {
+    *reinterpret_cast<float4*>(P.dvalue + e0) = make_float4(dv[0], dv[1], dv[2], dv[3]);
+#pragma unroll
+    for (int k = 0; k < A; ++k)
+      reinterpret_cast<float4*>(ddst)[k * kLossThreads + tid] =
+          reinterpret_cast<const float4*>(tile)[k * kLossThreads + tid];
+  } else {
+#pragma unroll
+    for (int r = 0; r < kLossVec; ++r)
+      if (e0 + r < P.M) P.dvalue[e0 + r] = dv[r];
+    const int n = static_cast<int>(cnt) * A;
+    for (int e = tid; e < n; e += kLossThreads) ddst[e] = tile[e];
+  }
+}
+
+// One tile per block up to the hand-off's 8192 blocks (M <= 8M elements); larger M walks tiles.
+// No software pipelining: co-resident blocks (4 per CU) overlap each other's loads and
+// arithmetic, while a loop carrying a prefetch across the tile's stores makes the compiler wait
+// for those stores (vmcnt is in order) at every tile.
+template <int A>
+__global__ __launch_bounds__(kLossThreads) void ppo_loss_vec_kernel(LossParams P) {
+  extern __shared__ __attribute__((aligned(16))) float tile[];  // [kLossTile * A]
+  const int tid = threadIdx.x;
+  float part[kNumPartials] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const float adv_mean = P.norm_adv ? P.adv_stats[0] : 0.f;
+  const float adv_den = P.norm_adv ? P.adv_stats[1] + 1e-8f : 1.f;
+  const int64_t ntiles = (P.M + kLossTile - 1) / kLossTile;
+  LossVecRegs<A> rec;
+  for (int64_t tl = blockIdx.x; tl < ntiles; tl += gridDim.x) {
+    const int64_t i0 = tl * kLossTile;
+    const int64_t cnt = (P.M - i0) < kLossTile ? (P.M - i0) : kLossTile;
+    if (tl != blockIdx.x) __syncthreads();  // the previous tile's LDS reads are done
+    if (cnt == kLossTile) {
+      loss_vec_load<A>(P, tl, tid, rec);
+#pragma unroll
+      for (int k = 0; k < A; ++k) reinterpret_cast<float4*>(tile)[k * kLossThreads + tid] = rec.lg[k];
+      __syncthreads();
+      loss_vec_tile<A, true>(P, tile, i0, cnt, tid, rec, adv_mean, adv_den, part);
+    } else {  // the tail tile: guarded scalar accesses
+      const int64_t e0 = i0 + static_cast<int64_t>(tid) * kLossVec;
+#pragma unroll
+      for (int r = 0; r < kLossVec; ++r) {
+        const int64_t e = e0 + r;
+        const bool ok = e < P.M;
+        rec.act[r] = ok ? P.b_actions[e] : 0;
+        rec.olp[r] = ok ? P.b_logprobs[e] : 0.f;
+        rec.adv[r] = ok ? P.b_adv[e] : 0.f;
+        rec.ret[r] = ok ? P.b_ret[e] : 0.f;
+        rec.vold[r] = ok ? P.b_val[e] : 0.f;
+        rec.vnew[r] = ok ? P.new_value[e] : 0.f;
+      }
+      const float* lsrc = P.logits + i0 * A;
+      const int n = static_cast<int>(cnt) * A;
+      for (int e = tid; e < n; e += kLossThreads) tile[e] = lsrc[e];
+      __syncthreads();
+      loss_vec_tile<A, false>(P, tile, i0, cnt, tid, rec, adv_mean, adv_den, part);
+    }
+  }
+  loss_finish(P, part);
 }
 
 // ---- Categorical action head ---------------------------------------------------------------------
@@ -836,10 +1000,20 @@ static int64_t loss_blocks(int64_t M) {
   const int64_t nb = ceil_div(M, kLossThreads);
   return nb < kLossMaxBlocks ? nb : kLossMaxBlocks;
 }
+static int64_t loss_blocks_vec(int64_t M) {
+  const int64_t nb = ceil_div(M, kLossTile);
+  return nb < kHandoffMaxBlocks ? nb : kHandoffMaxBlocks;
+}
+#ifndef OCPPO_LOSS_VEC_MIN_M  // experiments (tools/build_variant.py) move the switch-over
+#define OCPPO_LOSS_VEC_MIN_M (256 * kLossTile)
+#endif
+constexpr int64_t kLossVecMinM = OCPPO_LOSS_VEC_MIN_M;
+static bool aligned16(const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; }
 static size_t round16(size_t n) { return (n + 15) / 16 * 16; }
 static size_t loss_partials_offset() { return kTicketBytes; }
 static size_t loss_gpartials_offset(int64_t M) {
-  return kTicketBytes + round16(static_cast<size_t>(loss_blocks(M)) * kNumPartials * sizeof(float));
+  const int64_t nb = loss_blocks(M) > loss_blocks_vec(M) ? loss_blocks(M) : loss_blocks_vec(M);
+  return kTicketBytes + round16(static_cast<size_t>(nb) * kNumPartials * sizeof(float));
 }
 static size_t loss_stats_offset(int64_t M) {
   return loss_gpartials_offset(M) + round16(kHandoffMaxGroups * kNumPartials * sizeof(float));
@@ -922,8 +1096,27 @@ extern "C" int ocppo_ppo_loss_fwd_bwd(ocppo_stream_t stream, const float* logits
   P.g_h = (-1.0f * P.ent_coef) / fm;
   P.g_v = (P.vf_coef * 0.5f) / fm;
   P.inv_m = 1.0f / fm;
-  const int64_t nb = loss_blocks(M);
   static_assert(kLossMaxBlocks <= kHandoffMaxBlocks, "hand-off capacity");
+  // streaming form: contiguous (prepared) records, 16-B aligned arrays, at least one full tile per
+  // CU (below that the 256-element tiles of ppo_loss_kernel spread the latency over more CUs)
+  const bool vec_ok = !mb_inds && M >= kLossVecMinM &&
+                      (A == 3 || A == 4 || A == 6 || A == 9 || A == 18) &&
+                      aligned16(logits) && aligned16(new_value) && aligned16(b_actions) &&
+                      aligned16(b_logprobs) && aligned16(b_advantages) && aligned16(b_returns) &&
+                      aligned16(b_values) && aligned16(dlogits) && aligned16(dvalue);
+  if (vec_ok) {
+    const dim3 g(static_cast<unsigned>(loss_blocks_vec(M))), b(kLossThreads);
+    const size_t lds = sizeof(float) * kLossTile * A;
+    switch (A) {
+      case 3: hipLaunchKernelGGL(ppo_loss_vec_kernel<3>, g, b, lds, s, P); break;
+      case 4: hipLaunchKernelGGL(ppo_loss_vec_kernel<4>, g, b, lds, s, P); break;
+      case 6: hipLaunchKernelGGL(ppo_loss_vec_kernel<6>, g, b, lds, s, P); break;
+      case 9: hipLaunchKernelGGL(ppo_loss_vec_kernel<9>, g, b, lds, s, P); break;
+      default: hipLaunchKernelGGL(ppo_loss_vec_kernel<18>, g, b, lds, s, P); break;
+    }
+    return check_launch("ocppo_ppo_loss_fwd_bwd");
+  }
+  const int64_t nb = loss_blocks(M);
   const size_t lds = sizeof(float) * kLossThreads * A;
   const dim3 g(static_cast<unsigned>(nb)), b(kLossThreads);
   switch (A) {

@@ -374,6 +374,41 @@ int launch_gather(hipStream_t s, const void* src, const int64_t* idx, int64_t M,
   return check_launch("ocppo_gather_rows");
 }
 
+// ---- frame-encoding cache of the rollout (PPObj: the encoder acts on each frame alone) ---------
+// enc[n, w, :] = done[n] != 0 || w == W-1 ? fresh[n, :] : enc[n, w+1, :]   (in place)
+// The same shift + reset fill as store_groups applies to the stacked frames, applied to their
+// encoder outputs: at rollout step t only the newest frame is encoded (N rows instead of N*W).
+// One thread owns one (n, VEC-column group) and walks w upward, so every slot w+1 is read before
+// it is overwritten.
+template <int VEC>
+__global__ __launch_bounds__(256) void frame_cache_shift_kernel(float* __restrict__ enc,
+                                                                const float* __restrict__ fresh,
+                                                                int64_t ld_fresh,
+                                                                const float* __restrict__ done,
+                                                                int64_t N, int W, int64_t E) {
+  const int64_t EG = E / VEC;
+  const int64_t groups = N * EG;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t g = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; g < groups;
+       g += stride) {
+    const int64_t n = g / EG;
+    const int64_t k = (g - n * EG) * VEC;
+    float nv[VEC];
+    VecIO<OCPPO_F32, VEC>::load(fresh, n * ld_fresh + k, nv);
+    float* row = enc + n * W * E + k;
+    if (done != nullptr && done[n] != 0.f) {
+      for (int w = 0; w < W; ++w) VecIO<OCPPO_F32, VEC>::store(row, w * E, nv);
+    } else {
+      for (int w = 0; w + 1 < W; ++w) {
+        float v[VEC];
+        VecIO<OCPPO_F32, VEC>::load(row, (w + 1) * E, v);
+        VecIO<OCPPO_F32, VEC>::store(row, w * E, v);
+      }
+      VecIO<OCPPO_F32, VEC>::store(row, (W - 1) * E, nv);
+    }
+  }
+}
+
 static bool valid_dtype(int dt) { return dt == OCPPO_F32 || dt == OCPPO_BF16 || dt == OCPPO_U8; }
 
 }  // namespace ocppo
@@ -506,4 +541,25 @@ extern "C" int ocppo_rollout_store_vecnorm(ocppo_stream_t stream, const void* fr
   OCPPO_SV(OCPPO_U8, OCPPO_U8)
 #undef OCPPO_SV
   return fail(OCPPO_E_INVALID, "ocppo_rollout_store_vecnorm: unsupported dtype pair");
+}
+
+extern "C" int ocppo_frame_cache_shift(ocppo_stream_t stream, float* enc, const float* fresh,
+                                       int64_t ld_fresh, const float* done, int64_t N, int64_t W,
+                                       int64_t E) {
+  OCPPO_REQUIRE(N >= 0 && W >= 1 && W <= 64 && E >= 1 && ld_fresh >= E,
+                "ocppo_frame_cache_shift: bad sizes");
+  if (N == 0) return OCPPO_OK;
+  OCPPO_REQUIRE(enc && fresh, "ocppo_frame_cache_shift: null pointer");
+  clear_stale_error();
+  hipStream_t s = as_stream(stream);
+  const bool vec = E % 4 == 0 && ld_fresh % 4 == 0 &&
+                   reinterpret_cast<uintptr_t>(enc) % 16 == 0 &&
+                   reinterpret_cast<uintptr_t>(fresh) % 16 == 0;
+  if (vec)
+    hipLaunchKernelGGL(frame_cache_shift_kernel<4>, dim3(grid_for(N * (E / 4), 256)), dim3(256), 0,
+                       s, enc, fresh, ld_fresh, done, N, (int)W, E);
+  else
+    hipLaunchKernelGGL(frame_cache_shift_kernel<1>, dim3(grid_for(N * E, 256)), dim3(256), 0, s,
+                       enc, fresh, ld_fresh, done, N, (int)W, E);
+  return check_launch("ocppo_frame_cache_shift");
 }

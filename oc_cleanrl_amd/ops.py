@@ -349,6 +349,26 @@ def obs_reset(frame, obs_out, net_obs=None):
          _DTYPE_CODE[obs_out.dtype], _opt(net_obs, "net_obs", torch.float32, dev, N * W * D))
 
 
+def frame_cache_shift(enc, fresh, done=None):
+    """In-place shift of the rollout's frame-encoding cache (PPObj): enc [N, W, E] f32,
+    fresh [N, E] f32 (row stride may exceed E), done [N] f32 or None:
+    enc[n, w] = fresh[n] if done[n] or w == W-1 else enc[n, w+1]  (the frame stack's own rule,
+    ppo_atari_oc.py:506 re-encoding all W frames every step is what this saves)."""
+    dev = enc.device
+    if enc.dim() != 3 or fresh.dim() != 2:
+        raise ValueError(f"enc must be [N, W, E] and fresh [N, E], got {tuple(enc.shape)}, "
+                         f"{tuple(fresh.shape)}")
+    N, W, E = enc.shape
+    if tuple(fresh.shape) != (N, E) or fresh.stride(1) != 1 or fresh.dtype != torch.float32 \
+            or fresh.device != dev:
+        raise ValueError("fresh must be an f32 [N, E] row-major view on enc's device")
+    _stream(fresh.device)
+    call("ocppo_frame_cache_shift", _stream(dev), _check(enc, "enc", torch.float32, dev),
+         fresh.data_ptr(), fresh.stride(0) if N > 1 else E,
+         _opt(done, "done", torch.float32, dev, N), N, W, E)
+    return enc
+
+
 def gather_rows(src, idx, out=None):
     """out[i] = float32(src[idx[i]]) for src [B, ...] f32|bf16|u8 → out [M, ...] f32."""
     dev = src.device

@@ -31,7 +31,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from . import ops
-from .agents import make_agent
+from .agents import PPObj, make_agent
 from .args import Args
 from .envs import SyntheticAtariEnv
 
@@ -153,6 +153,10 @@ class PPOTrainer:
         self.fused_head = isinstance(self.agent.actor, nn.Linear) and \
             isinstance(self.agent.critic, nn.Linear)
         self.H = self.agent.actor.in_features if self.fused_head else 0
+        # PPObj's encoder sees one frame at a time: the rollout keeps the W frame encodings of
+        # every env in a cache and encodes only the newest frame per step
+        self.frame_cache = (a.rollout_frame_cache and self.fused_head and
+                            isinstance(self.agent, PPObj) and len(a.encoder_dims) > 0)
         # every parameter's grad is written in place by agents._LinearAct (no zero-fill needed)
         # when the agent is a Linear/ReLU stack owned by the fused optimizer
         self.direct_grads = a.fused_optimizer and self.fused_head and all(
@@ -185,7 +189,11 @@ class PPOTrainer:
         self.values = torch.zeros((T + 1, N), dtype=f32, device=dev)
         self.advantages = torch.zeros((T, N), dtype=f32, device=dev)
         self.returns = torch.zeros((T, N), dtype=f32, device=dev)
-        self.noise = torch.zeros((N, self.A), dtype=f32, device=dev)
+        # the Exp(1) draws torch's Categorical.sample makes ([N, A] per step), for the whole rollout
+        # in one generator call instead of T launches
+        self.noise = torch.zeros((T, N, self.A), dtype=f32, device=dev)
+        self.enc_cache = (torch.zeros((N, self.obs_shape[0], self.agent.encoding_dim), dtype=f32,
+                                      device=dev) if self.frame_cache else None)
         self.ret_state = torch.zeros(N, dtype=torch.float64, device=dev)
         self.rms_state = torch.tensor([0.0, 1.0, 1e-4], dtype=torch.float64, device=dev)
 
@@ -227,22 +235,36 @@ class PPOTrainer:
         ops.obs_reset(frame, self.obs[self.T], self.net_obs)
         self.dones[self.T].zero_()
 
+    def _policy_hidden(self, t: int):
+        """Trunk output for net_obs at rollout step t (t == T: the bootstrap of :534). With the
+        frame cache: step 0 encodes all W frames (the weights changed since the last rollout),
+        later steps encode only the newest frame and shift the cache with done row t."""
+        ag = self.agent
+        if not self.frame_cache:
+            return ag.trunk(self.net_obs)
+        if t == 0:
+            self.enc_cache.copy_(ag.encode(self.net_obs))
+        else:
+            fresh = ag.encode(self.net_obs[:, -1])
+            self.timer.bracket("frame_cache", lambda: ops.frame_cache_shift(
+                self.enc_cache, fresh, self.dones[t]))
+        return ag.decode(self.enc_cache)
+
     def _rollout_step(self, t: int):
         """One env step of the rollout (:500-514): network trunk (PyTorch) → fused HIP policy
         head (actor+critic GEMVs + Categorical sample, writes actions/logprobs/values rows) →
         env → fused HIP store (+ VecNormalize) of the next obs slot and reward/done rows."""
         a = self.args
         ag = self.agent
-        self.noise.exponential_()  # the Exp(1) draw torch's Categorical.sample makes
         if self.fused_head:
-            hidden = ag.trunk(self.net_obs)
+            hidden = self._policy_hidden(t)
             self.timer.bracket("action_head", lambda: ops.policy_head_sample(
                 hidden, ag.actor.weight, ag.actor.bias, ag.critic.weight, ag.critic.bias,
-                self.noise, self.actions[t], self.logprobs[t], self.values[t]))
+                self.noise[t], self.actions[t], self.logprobs[t], self.values[t]))
         else:
             logits, value = ag.logits_and_value(self.net_obs)
             self.timer.bracket("action_head", lambda: ops.categorical_sample(
-                logits, self.noise, self.actions[t], self.logprobs[t], None, value.view(-1),
+                logits, self.noise[t], self.actions[t], self.logprobs[t], None, value.view(-1),
                 self.values[t]))
         self.timer.bracket("env_step", lambda: self.env.step(self.actions[t], t))
         if a.vecnorm_reward:
@@ -261,10 +283,15 @@ class PPOTrainer:
         with torch.no_grad():
             self.obs[0].copy_(self.obs[T])
             self.dones[0].copy_(self.dones[T])
+            self.noise.exponential_()
             for t in range(T):
                 self._rollout_step(t)
             self.env.advance(T)
-            self.values[T].copy_(self.agent.get_value(self.net_obs).view(-1))
+            if self.frame_cache:
+                self.values[T].copy_(self.agent._head(self.agent.critic,
+                                                      self._policy_hidden(T)).view(-1))
+            else:
+                self.values[T].copy_(self.agent.get_value(self.net_obs).view(-1))
             self.timer.bracket("gae", lambda: ops.gae(
                 self.rewards, self.values[:T], self.dones[:T], self.values[T], self.dones[T],
                 a.gamma, a.gae_lambda, self.advantages, self.returns))

@@ -119,6 +119,35 @@ def test_loss_random_vs_oracle(ops, dev, M, A, B, norm_adv, clip_vloss):
     np.testing.assert_allclose(dv.cpu().numpy(), edv, rtol=0, atol=2e-6 * np.abs(edv).max())
 
 
+@pytest.mark.parametrize("M,A", [(262144, 6), (262144 + 777, 6), (1 << 20, 4), (300001, 3),
+                                 (262147, 9), (270000, 18)])
+def test_loss_streaming_form_vs_oracle_and_tile_form(ops, dev, M, A):
+    """Prepared (contiguous) records at M >= 256 x 1024 take the 16-B-per-lane streaming kernel:
+    same per-element arithmetic as the 256-element-tile kernel (dlogits / dvalue bit-identical),
+    stats within f32 summation-order noise, both against the oracle."""
+    rng = np.random.default_rng(M + A)
+    logits = (rng.standard_normal((M, A)) * 2).astype(np.float32)
+    acts = rng.integers(0, A, M).astype(np.int64)
+    lp = (rng.standard_normal(M) * 0.2 - 1.7).astype(np.float32)
+    adv = (rng.standard_normal(M) * 2).astype(np.float32)
+    ret = rng.standard_normal(M).astype(np.float32)
+    val = rng.standard_normal(M).astype(np.float32)
+    v = (val + rng.standard_normal(M) * 0.2).astype(np.float32)
+    cfg = dict(clip_coef=0.1, ent_coef=0.01, vf_coef=0.5, norm_adv=True, clip_vloss=True)
+    args = [T(x, dev) for x in (logits, v, acts, lp, adv, ret, val)]
+    st = ops.minibatch_adv_stats(args[4], torch.arange(M, device=dev), M)[0]
+    s_vec, d_vec, v_vec = ops.ppo_loss_fwd_bwd(*args, adv_stats=st, **cfg)
+    # the tile kernel: same records through an identity index
+    ident = torch.arange(M, device=dev)
+    s_til, d_til, v_til = ops.ppo_loss_fwd_bwd(*args, mb_inds=ident, adv_stats=st, **cfg)
+    assert torch.equal(d_vec, d_til) and torch.equal(v_vec, v_til)
+    torch.testing.assert_close(s_vec, s_til, rtol=2e-6, atol=1e-7)
+    es, edl, edv = O.ppo_loss_fwd_bwd(logits, v, acts, lp, adv, ret, val, np.arange(M), **cfg)
+    np.testing.assert_allclose(s_vec.cpu().numpy(), es, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(d_vec.cpu().numpy(), edl, rtol=0, atol=2e-6 * np.abs(edl).max())
+    np.testing.assert_allclose(v_vec.cpu().numpy(), edv, rtol=0, atol=2e-6 * np.abs(edv).max())
+
+
 def test_loss_deterministic_and_graph_replayable(ops, dev):
     z = golden("loss_norm_clip.npz")
     args = _loss_args(z, dev)
@@ -283,6 +312,33 @@ def test_gather_rows_bitwise(ops, dev, src_dt, B, shape, M):
     idx = rng.integers(0, B, M).astype(np.int64)
     out = ops.gather_rows(T(src, dev).to(STORE_DT[src_dt]), T(idx, dev))
     assert np.array_equal(out.cpu().numpy(), src[idx])
+
+
+@pytest.mark.parametrize("N,W,E,ld", [(128, 4, 512, 512), (128, 4, 512, 1536), (7, 3, 5, 9),
+                                       (1, 4, 12, 12), (300, 2, 64, 64)])
+def test_frame_cache_shift_bitwise(ops, dev, N, W, E, ld):
+    """The rollout's encoding cache follows the frame stack's shift / reset-fill rule exactly."""
+    rng = np.random.default_rng(N * W + E)
+    enc = rng.standard_normal((N, W, E)).astype(np.float32)
+    big = rng.standard_normal((N, ld)).astype(np.float32)
+    done = (rng.random(N) < 0.3).astype(np.float32)
+    enc_t = T(enc, dev)
+    fresh = T(big, dev)[:, :E]
+    ops.frame_cache_shift(enc_t, fresh, T(done, dev))
+    exp = O.frame_cache_shift(enc, big[:, :E], done)
+    assert np.array_equal(enc_t.cpu().numpy(), exp)
+    # done=None: a pure shift
+    enc_t = T(enc, dev)
+    ops.frame_cache_shift(enc_t, fresh)
+    assert np.array_equal(enc_t.cpu().numpy(), O.frame_cache_shift(enc, big[:, :E], done * 0))
+
+
+def test_frame_cache_shift_rejects_bad_shapes(ops, dev):
+    enc = torch.zeros(4, 4, 8, device=dev)
+    with pytest.raises(ValueError):
+        ops.frame_cache_shift(enc, torch.zeros(4, 7, device=dev))
+    with pytest.raises(ValueError):
+        ops.frame_cache_shift(enc, torch.zeros(4, 8, device="cpu"))
 
 
 def test_obs_reset(ops, dev):

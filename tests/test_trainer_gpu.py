@@ -124,3 +124,29 @@ def test_fused_trunk_matches_module_forward_and_grads(dev, arch, obs):
     gr2 = torch.autograd.grad(h2, list(ag.network.parameters()), g)
     for a, b in zip(gr1, gr2):  # split-K weight grads: summation order differs
         torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-5 * float(a.abs().max()))
+
+
+def test_rollout_frame_cache_matches_full_trunk(dev):
+    """Encoding only the newest frame per step (cache + shift) gives the same policy as
+    re-encoding all W stacked frames (ppo_atari_oc.py:506), up to GEMM summation order."""
+    args = small_args(encoder_dims=(32, 64, 48), decoder_dims=(64,), cuda_graphs=False,
+                      rollout_frame_cache=True)
+    a, _ = run_iters(args, 1, dev)
+    assert a.frame_cache
+    with torch.no_grad():
+        a._rollout()  # a rollout under fixed weights, no update after it
+        torch.cuda.synchronize()
+        # the cache holds the encodings of the bootstrap obs (step T)
+        torch.testing.assert_close(a.agent.decode(a.enc_cache), a.agent.trunk(a.net_obs),
+                                   rtol=1e-5, atol=1e-5)
+        # every step's stored value = the critic on the full stacked obs of that step
+        T, N = a.T, a.N
+        full = a.agent.get_value(a.obs[:T + 1].float().view((T + 1) * N, *a.obs_shape))
+        torch.testing.assert_close(a.values, full.view(T + 1, N), rtol=1e-5, atol=1e-5)
+    b, _ = run_iters(small_args(encoder_dims=(32, 64, 48), decoder_dims=(64,),
+                                rollout_frame_cache=False), 2, dev)
+    c, _ = run_iters(small_args(encoder_dims=(32, 64, 48), decoder_dims=(64,),
+                                rollout_frame_cache=True), 2, dev)
+    assert not b.frame_cache and c.frame_cache
+    same = (c.actions == b.actions).float().mean().item()
+    assert same > 0.99, same

@@ -130,7 +130,7 @@ def make_case(name: str, p: dict, dev):
             logits, val, acts, lp, adv, ret, bv, adv_stats=st, clip_coef=0.1, ent_coef=0.01,
             vf_coef=0.5, norm_adv=True, clip_vloss=True, dlogits=dl, dvalue=dv, stats=stats,
             workspace=ws)
-        return fn, (8 * A + 28) * M
+        return fn, (8 * A + 32) * M
     if name == "policy_head":
         N, H, A = p["N"], p["H"], p["A"]
         hid = torch.relu(torch.randn(N, H, device=dev, generator=g))
