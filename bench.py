@@ -83,7 +83,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--envs-per-gpu", type=int, default=128)
+    ap.add_argument("--config", type=int, default=2, choices=(2, 3),
+                    help="BASELINE config: 2 = Pong obj PPO_OBJ (the headline; 4 = 2 per GPU), "
+                         "3 = Breakout dqn-pixels NatureCNN, 256 envs")
+    ap.add_argument("--envs-per-gpu", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-iterations", type=int, default=3)
     ap.add_argument("--no-graphs", action="store_true")
@@ -107,9 +110,19 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=device)
 
-    args = Args(env_id="ALE/Pong-v5", obs_mode="obj", architecture="PPO_OBJ",
-                num_envs=opt.envs_per_gpu * world, num_steps=128, num_features=12,
-                total_timesteps=10_000_000, cuda_graphs=not opt.no_graphs, save_model=False)
+    if opt.config == 3:
+        envs = opt.envs_per_gpu or 256
+        # MIOpen's deterministic convolution algorithms (use_deterministic_algorithms(True), the
+        # reference default) are naive kernels on gfx950, ~30x slower for NatureCNN: config 3 is
+        # measured with torch_deterministic=False (our own HIP kernels are deterministic anyway)
+        args = Args(env_id="ALE/Breakout-v5", obs_mode="dqn", architecture="PPO",
+                    num_envs=envs * world, num_steps=128, total_timesteps=10_000_000,
+                    cuda_graphs=not opt.no_graphs, save_model=False, torch_deterministic=False)
+    else:
+        envs = opt.envs_per_gpu or 128
+        args = Args(env_id="ALE/Pong-v5", obs_mode="obj", architecture="PPO_OBJ",
+                    num_envs=envs * world, num_steps=128, num_features=12,
+                    total_timesteps=10_000_000, cuda_graphs=not opt.no_graphs, save_model=False)
     for kv in opt.set:
         k, v = kv.split("=", 1)
         cur = getattr(args, k)
@@ -159,7 +172,7 @@ def main():
                     "mean_launch_us": kernels[dom]["mean_us"]}
 
     scaled = None
-    if rank == 0 and world == 1 and not opt.no_scaled:
+    if rank == 0 and world == 1 and not opt.no_scaled and opt.config == 2:
         from tools.kernel_bench import run_case
 
         scaled = {}
@@ -172,7 +185,7 @@ def main():
             torch.cuda.empty_cache()
 
     cpu = None
-    if rank == 0 and world == 1 and not opt.no_cpu_baseline:
+    if rank == 0 and world == 1 and not opt.no_cpu_baseline and opt.config == 2:
         from oracle.cpu_learner import time_cpu_baseline  # CPU baseline leg (oracle port)
 
         threads = min(16, os.cpu_count() or 1)
@@ -187,7 +200,9 @@ def main():
     if rank == 0:
         sps = env_steps / dt
         line = {
-            "metric": "env steps/sec (SPS) + PPO updates/sec, ALE/Pong-v5 obj-mode, 1/2/4/8 MI355X",
+            "metric": "env steps/sec (SPS) + PPO updates/sec, ALE/Pong-v5 obj-mode, 1/2/4/8 MI355X"
+                      if opt.config == 2 else
+                      "env steps/sec (SPS) + PPO updates/sec, ALE/Breakout-v5 dqn pixels, 1 MI355X",
             "value": round(sps, 1),
             "unit": "env steps/s",
             "n_gpus": world,
@@ -198,8 +213,11 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "fp32",
-            "data": "synthetic (device-resident Pong-obj env; random-init PPObj)",
-            "config": {"workload": "ppo_atari_oc.py Pong-v5 obj PPO_OBJ (BASELINE config 2 per GPU)",
+            "data": "synthetic (device-resident Pong-obj env; random-init PPObj)" if opt.config == 2
+                    else "synthetic (device-resident 84x84 u8 frames; random-init NatureCNN)",
+            "config": {"workload": "ppo_atari_oc.py Pong-v5 obj PPO_OBJ (BASELINE config 2 per GPU)"
+                       if opt.config == 2 else
+                       "ppo_atari_oc.py Breakout-v5 dqn NatureCNN (BASELINE config 3)",
                        "local_num_envs": args.local_num_envs, "num_envs": args.num_envs,
                        "num_steps": args.num_steps, "num_features": args.num_features,
                        "minibatch_size": args.local_minibatch_size,
@@ -207,6 +225,7 @@ def main():
                        "num_minibatches": args.num_minibatches,
                        "obs_storage": str(tr.obs_dtype).replace("torch.", ""),
                        "cuda_graphs": args.cuda_graphs,
+                       "torch_deterministic": args.torch_deterministic,
                        "parallelism": f"dp{world}"},
             "updates_per_sec": round(updates / dt, 2),
             "roofline": roofline,

@@ -234,6 +234,20 @@ OCPPO_API int ocppo_frame_cache_shift(ocppo_stream_t stream, float* enc, const f
                             int64_t ld_fresh, const float* done, int64_t N, int64_t W, int64_t E);
 
 /* ---------------------------------------------------------------------------------------------
+ * Rollout-batch Linear(+ReLU): y[M, N] = act(x[M, K] @ w[N, K]^T + b[N]) in f32 on the matrix
+ * cores (v_mfma_f32_16x16x4_f32: exact f32 products, f32 accumulation; summation order differs
+ * from the BLAS library's). Replaces the nn.Linear(+nn.ReLU) layers of architectures/ppo.py:60-84
+ * (PPObj) and the NatureCNN head :36-46 in the rollout forward of ppo_atari_oc.py:506, :534
+ * (no autograd: the rollout runs under torch.no_grad()), where M is the number of envs (or envs x
+ * frames) and the library's large tiles leave the chip idle.
+ *   x : row stride ldx (>= K); w : nn.Linear weight, row-major [N, K]; b : [N] or NULL;
+ *   y : row stride ldy (>= N); relu : 0 = identity, 1 = max(., 0) after the bias.
+ * ------------------------------------------------------------------------------------------- */
+OCPPO_API int ocppo_linear_act(ocppo_stream_t stream, const float* x, int64_t ldx, const float* w,
+                     const float* b, float* y, int64_t ldy, int64_t M, int64_t N, int64_t K,
+                     int relu);
+
+/* ---------------------------------------------------------------------------------------------
  * Minibatch gather — replaces `b_obs[mb_inds]` of ppo_atari_oc.py:566-567:
  *   dst[i, :] = f32(src[idx[i], :]),  src [B, R] of dtype src_dtype, dst [M, R] f32.
  * ------------------------------------------------------------------------------------------- */

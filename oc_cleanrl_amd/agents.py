@@ -116,9 +116,27 @@ class _LinearAct(torch.autograd.Function):
         return dx, dw, db, None
 
 
+# Rollout-sized inference batches (no autograd) of the shapes where the HIP f32-MFMA kernel beats
+# the BLAS library's (tools/exp_rollout_linear.py on MI355X: K <= 64 at up to 512 rows, K <= 256 at
+# up to 128 rows); everything else, and every autograd forward, stays on hipBLASLt.
+HIP_ROLLOUT_LINEAR = True
+
+
+def _hip_linear_ok(x2, lin: nn.Linear) -> bool:
+    if not HIP_ROLLOUT_LINEAR or torch.is_grad_enabled() or not x2.is_cuda or \
+            x2.dtype != torch.float32 or (x2.shape[0] > 1 and x2.stride(1) != 1):
+        return False
+    M, K = x2.shape
+    return (K <= 64 and M <= 512) or (K <= 256 and M <= 128)
+
+
 def linear_act(x, lin: nn.Linear, relu: bool):
     lead = x.shape[:-1]
-    y = _LinearAct.apply(x.reshape(-1, x.shape[-1]), lin.weight, lin.bias, relu)
+    x2 = x.reshape(-1, x.shape[-1])
+    if _hip_linear_ok(x2, lin):
+        y = ops.linear_act(x2, lin.weight, lin.bias, relu)
+    else:
+        y = _LinearAct.apply(x2, lin.weight, lin.bias, relu)
     return y.view(*lead, y.shape[-1])
 
 
@@ -127,16 +145,21 @@ def linear_relu(x, lin: nn.Linear):
 
 
 def fused_trunk(seq: nn.Sequential, x):
-    """Run `seq` with every Linear→ReLU pair as one fused GEMM (same math, fewer launches).
-    Used on GPU tensors; module structure and state-dict keys are untouched."""
+    """Run `seq` with every Linear→ReLU pair as one fused GEMM (same math, fewer launches) and
+    every other biased Linear through the same path (so FlatAdam-owned grads are written in place,
+    never accumulated). Used on GPU tensors; module structure and state-dict keys are untouched."""
     mods = list(seq)
     i = 0
     while i < len(mods):
         m = mods[i]
-        if (isinstance(m, nn.Linear) and m.bias is not None and i + 1 < len(mods)
-                and isinstance(mods[i + 1], nn.ReLU) and x.is_cuda and x.dtype == torch.float32):
+        fusable = (isinstance(m, nn.Linear) and m.bias is not None and x.is_cuda
+                   and x.dtype == torch.float32)
+        if fusable and i + 1 < len(mods) and isinstance(mods[i + 1], nn.ReLU):
             x = linear_relu(x, m)
             i += 2
+        elif fusable:
+            x = linear_act(x, m, False)
+            i += 1
         else:
             x = m(x)
             i += 1

@@ -116,7 +116,8 @@ class Args:
     log_dir: str = "runs"
     save_model: bool = True
     metrics_every: int = 1     # read the device-side metrics every N iterations
-    rollout_frame_cache: bool = False  # PPO_OBJ rollout: encode only the newest frame per step
+    rollout_frame_cache: bool = True  # PPO_OBJ rollout: encode only the newest frame per step
+    conv_benchmark: bool = False  # cudnn.benchmark (MIOpen Find) for the NatureCNN convolutions
 
 
 def _flag_names(name: str) -> list[str]:
@@ -134,11 +135,12 @@ def _parse_bool(s: str) -> bool:
     raise argparse.ArgumentTypeError(f"expected a boolean, got {s!r}")
 
 
-def parse_args(argv=None, defaults: dict | None = None) -> Args:
-    """tyro-like CLI over Args. `defaults` overrides dataclass defaults (e.g. per-script)."""
-    base = Args(**(defaults or {}))
-    ap = argparse.ArgumentParser(description="oc_cleanrl_amd PPO (ppo_atari_oc.py surface)")
-    for f in dataclasses.fields(Args):
+def parse_dataclass(cls, argv=None, defaults: dict | None = None, description: str = ""):
+    """tyro-like CLI over the dataclass `cls`. `defaults` overrides its defaults."""
+    base = cls(**(defaults or {}))
+    ap = argparse.ArgumentParser(description=description)
+    tuples = []
+    for f in dataclasses.fields(cls):
         cur = getattr(base, f.name)
         names = _flag_names(f.name)
         if isinstance(cur, bool):
@@ -147,6 +149,7 @@ def parse_args(argv=None, defaults: dict | None = None) -> Args:
             ap.add_argument(*[n.replace("--", "--no-", 1) for n in names], dest=f.name,
                             action="store_false")
         elif isinstance(cur, tuple):
+            tuples.append(f.name)
             ap.add_argument(*names, dest=f.name, nargs="*", type=int, default=cur)
         elif f.name in ("target_kl",):
             ap.add_argument(*names, dest=f.name, type=lambda s: None if s == "None" else float(s),
@@ -157,12 +160,16 @@ def parse_args(argv=None, defaults: dict | None = None) -> Args:
             ap.add_argument(*names, dest=f.name, type=type(cur), default=cur)
     ns = ap.parse_args(sys.argv[1:] if argv is None else argv)
     d = vars(ns)
-    d["encoder_dims"] = tuple(d["encoder_dims"])
-    d["decoder_dims"] = tuple(d["decoder_dims"])
-    d["device_ids"] = tuple(d["device_ids"])
-    if d["obs_mode"] not in OBS_MODES:
+    for k in tuples:
+        d[k] = tuple(d[k])
+    if "obs_mode" in d and d["obs_mode"] not in OBS_MODES:
         ap.error(f"--obs_mode must be one of {OBS_MODES}")
-    return Args(**d)
+    return cls(**d)
+
+
+def parse_args(argv=None, defaults: dict | None = None) -> Args:
+    """tyro-like CLI over Args. `defaults` overrides dataclass defaults (e.g. per-script)."""
+    return parse_dataclass(Args, argv, defaults, "oc_cleanrl_amd PPO (ppo_atari_oc.py surface)")
 
 
 def finalize(args: Args, world_size: int = 1) -> Args:

@@ -197,7 +197,7 @@ extern "C" int ocppo_replay_add(ocppo_stream_t stream, const void* obs, const vo
   OCPPO_REQUIRE(obs && next_obs && actions && rewards && dones && state && rb_obs && rb_actions &&
                     rb_rewards && rb_dones && workspace,
                 "ocppo_replay_add: null pointer");
-  OCPPO_REQUIRE((obs_dtype == OCPPO_F32 || obs_dtype == OCPPO_U8) &&
+  OCPPO_REQUIRE((obs_dtype == OCPPO_F32 || obs_dtype == OCPPO_BF16 || obs_dtype == OCPPO_U8) &&
                     (rb_dtype == OCPPO_F32 || rb_dtype == OCPPO_BF16 || rb_dtype == OCPPO_U8),
                 "ocppo_replay_add: bad dtypes");
   int64_t g = ceil_div(E * D, 256);
@@ -218,6 +218,9 @@ extern "C" int ocppo_replay_add(ocppo_stream_t stream, const void* obs, const vo
   OCPPO_ADD(OCPPO_U8, OCPPO_F32)
   OCPPO_ADD(OCPPO_U8, OCPPO_BF16)
   OCPPO_ADD(OCPPO_U8, OCPPO_U8)
+  OCPPO_ADD(OCPPO_BF16, OCPPO_F32)
+  OCPPO_ADD(OCPPO_BF16, OCPPO_BF16)
+  OCPPO_ADD(OCPPO_BF16, OCPPO_U8)
 #undef OCPPO_ADD
   return fail(OCPPO_E_INVALID, "ocppo_replay_add: unsupported dtype pair");
 }

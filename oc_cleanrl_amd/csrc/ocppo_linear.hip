@@ -1,0 +1,184 @@
+// Rollout-batch Linear(+ReLU) on the f32 matrix cores: y = act(x W^T + b) for the few-hundred-row
+// batches of the rollout forward (cleanrl/ppo_atari_oc.py:506 `agent.get_action_and_value(next_obs)`
+// and :534 `agent.get_value(next_obs)` through the PPObj / NatureCNN-head Linear layers of
+// architectures/ppo.py:60-84 and :36-46).
+//
+// Why not the BLAS library: at M = 128..512 rows every layer is a few hundred 16x16 output tiles;
+// the library's fp32 kernels take 6-10 us per layer there (1-60 TFLOP/s, tools/exp_rollout_gemms.py)
+// because their macro tiles leave most of the 256 CUs idle. Here:
+//   * one workgroup per 16x16 output tile, S waves per workgroup splitting K (S chosen so the
+//     launch has >= ~2048 waves, i.e. >= 2 per SIMD), partial tiles summed through LDS in wave
+//     order (deterministic);
+//   * v_mfma_f32_16x16x4_f32 (exact f32 products, one rounding per product, f32 accumulation);
+//     operands come straight from global memory as one 16-B load per lane per 16-wide K chunk for
+//     both x (row-major [M, K]) and W (nn.Linear's [N, K]) -- MFMA j of a chunk takes element j
+//     of every lane's float4, so the 4 MFMAs of a chunk together cover its 16 k values, the same
+//     permutation on A and B;
+//   * XCD-aware tile order: workgroups b and b+8 share an XCD (round-robin dispatch), and each
+//     XCD gets a contiguous range of output-column tiles, so it streams 1/8 of W through its L2;
+//   * bias + ReLU fused in the epilogue (torch._addmm_activation's order: acc + b, then max(., 0)).
+// Roofline: MFMA-bound in principle (2*M*N*K flops), latency-bound at these sizes.
+#include "ocppo_common.h"
+
+namespace ocppo {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+constexpr int kLinMaxWaves = 8;
+
+// One wave's share of a 16x16 tile: chunks [c0, c1) of 16 k values. All operand loads of a group
+// of up to CH chunks are issued before its MFMAs, so the wave pays one L2 / Infinity-Cache round
+// trip per group instead of one per chunk.
+template <int CH, bool VEC>
+__device__ __forceinline__ void linear_wave_chunks(const float* xr, const float* wr, bool rok,
+                                                   bool cok, int K, int g, int c0, int c1,
+                                                   floatx4& acc0, floatx4& acc1) {
+  for (int cb = c0; cb < c1; cb += CH) {
+    float4 a[CH], bb[CH];
+#pragma unroll
+    for (int q = 0; q < CH; ++q) {
+      const int k = (cb + q) * 16 + 4 * g;
+      const bool live = cb + q < c1;
+      if (VEC && k + 3 < K) {
+        a[q] = (live && rok) ? *reinterpret_cast<const float4*>(xr + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+        bb[q] = (live && cok) ? *reinterpret_cast<const float4*>(wr + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+      } else {
+        const bool lr = live && rok, lc = live && cok;
+        a[q].x = (lr && k + 0 < K) ? xr[k + 0] : 0.f;
+        a[q].y = (lr && k + 1 < K) ? xr[k + 1] : 0.f;
+        a[q].z = (lr && k + 2 < K) ? xr[k + 2] : 0.f;
+        a[q].w = (lr && k + 3 < K) ? xr[k + 3] : 0.f;
+        bb[q].x = (lc && k + 0 < K) ? wr[k + 0] : 0.f;
+        bb[q].y = (lc && k + 1 < K) ? wr[k + 1] : 0.f;
+        bb[q].z = (lc && k + 2 < K) ? wr[k + 2] : 0.f;
+        bb[q].w = (lc && k + 3 < K) ? wr[k + 3] : 0.f;
+      }
+    }
+    // two accumulator chains (the 16x16x4 f32 MFMA's dependent latency is 40 cycles vs a
+    // 32-cycle issue interval); zero operands of dead chunks add exact zeros
+#pragma unroll
+    for (int q = 0; q < CH; ++q) {
+      floatx4& acc = (q & 1) ? acc1 : acc0;
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[q].x, bb[q].x, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[q].y, bb[q].y, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[q].z, bb[q].z, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[q].w, bb[q].w, acc, 0, 0, 0);
+    }
+  }
+}
+
+// VEC: x / W rows are 16-B aligned with K % 4 == 0 (float4 operand loads); else scalar loads.
+template <int S, int CH, bool RELU, bool VEC>
+__global__ __launch_bounds__(64 * S) void linear_rows_kernel(
+    const float* __restrict__ x, int64_t ldx, const float* __restrict__ w,
+    const float* __restrict__ bias, float* __restrict__ y, int64_t ldy, int M, int N, int K,
+    int ntm, int tiles) {
+  __shared__ floatx4 red[S > 1 ? S - 1 : 1][64];
+  const int b = blockIdx.x;
+  const int per_xcd = (tiles + 7) / 8;
+  const int t = (b % 8) * per_xcd + b / 8;  // XCD-contiguous tile ranges
+  if (t >= tiles) return;
+  const int tm = t % ntm, tn = t / ntm;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int g = lane >> 4, c16 = lane & 15;
+  const int row = tm * 16 + c16;  // A operand row of this lane
+  const int col = tn * 16 + c16;  // B operand column (W row) of this lane
+  const bool rok = row < M, cok = col < N;
+  const float* xr = x + static_cast<int64_t>(rok ? row : 0) * ldx;
+  const float* wr = w + static_cast<int64_t>(cok ? col : 0) * K;
+
+  const int nch = (K + 15) / 16;
+  const int cpw = (nch + S - 1) / S;
+  const int c0 = wv * cpw;
+  const int c1 = c0 + cpw < nch ? c0 + cpw : nch;
+  floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  linear_wave_chunks<CH, VEC>(xr, wr, rok, cok, K, g, c0, c1, acc0, acc1);
+  floatx4 acc = acc0 + acc1;
+  if (S > 1) {
+    if (wv > 0) red[wv - 1][lane] = acc;
+    __syncthreads();
+    if (wv > 0) return;
+#pragma unroll
+    for (int q = 0; q < S - 1; ++q) acc += red[q][lane];
+  }
+  // C/D layout of 16x16 MFMA: column lane & 15, rows 4 * (lane >> 4) + r
+  const int ocol = tn * 16 + c16;
+  if (ocol >= N) return;
+  const float bv = bias ? bias[ocol] : 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int orow = tm * 16 + 4 * g + r;
+    if (orow < M) {
+      float v = acc[r] + bv;
+      if (RELU) v = fmaxf(v, 0.f);
+      y[static_cast<int64_t>(orow) * ldy + ocol] = v;
+    }
+  }
+}
+
+template <int S, int CH, bool RELU>
+static void launch_linear_sc(hipStream_t s, bool vec, const float* x, int64_t ldx, const float* w,
+                             const float* b, float* y, int64_t ldy, int M, int N, int K) {
+  const int ntm = (M + 15) / 16, ntn = (N + 15) / 16, tiles = ntm * ntn;
+  const dim3 grid(8 * ((tiles + 7) / 8)), block(64 * S);
+  if (vec)
+    hipLaunchKernelGGL((linear_rows_kernel<S, CH, RELU, true>), grid, block, 0, s, x, ldx, w, b,
+                       y, ldy, M, N, K, ntm, tiles);
+  else
+    hipLaunchKernelGGL((linear_rows_kernel<S, CH, RELU, false>), grid, block, 0, s, x, ldx, w, b,
+                       y, ldy, M, N, K, ntm, tiles);
+}
+
+template <int S, bool RELU>
+static void launch_linear_s(hipStream_t s, int cpw, bool vec, const float* x, int64_t ldx,
+                            const float* w, const float* b, float* y, int64_t ldy, int M, int N,
+                            int K) {
+  if (cpw <= 2)
+    launch_linear_sc<S, 2, RELU>(s, vec, x, ldx, w, b, y, ldy, M, N, K);
+  else if (cpw <= 4)
+    launch_linear_sc<S, 4, RELU>(s, vec, x, ldx, w, b, y, ldy, M, N, K);
+  else
+    launch_linear_sc<S, 8, RELU>(s, vec, x, ldx, w, b, y, ldy, M, N, K);
+}
+
+template <bool RELU>
+static void launch_linear(hipStream_t s, bool vec, const float* x, int64_t ldx, const float* w,
+                          const float* b, float* y, int64_t ldy, int M, int N, int K) {
+  const int64_t tiles = static_cast<int64_t>((M + 15) / 16) * ((N + 15) / 16);
+  const int nch = (K + 15) / 16;
+  int S = 1;  // K split: >= ~4096 waves (4 per SIMD), >= 2 chunks per wave
+  while (S < kLinMaxWaves && tiles * S < 4096 && nch >= 2 * S * 2) S *= 2;
+  const int cpw = (nch + S - 1) / S;
+  switch (S) {
+    case 1: launch_linear_s<1, RELU>(s, cpw, vec, x, ldx, w, b, y, ldy, M, N, K); break;
+    case 2: launch_linear_s<2, RELU>(s, cpw, vec, x, ldx, w, b, y, ldy, M, N, K); break;
+    case 4: launch_linear_s<4, RELU>(s, cpw, vec, x, ldx, w, b, y, ldy, M, N, K); break;
+    default: launch_linear_s<8, RELU>(s, cpw, vec, x, ldx, w, b, y, ldy, M, N, K); break;
+  }
+}
+
+}  // namespace ocppo
+
+using namespace ocppo;
+
+extern "C" int ocppo_linear_act(ocppo_stream_t stream, const float* x, int64_t ldx, const float* w,
+                                const float* b, float* y, int64_t ldy, int64_t M, int64_t N,
+                                int64_t K, int relu) {
+  OCPPO_REQUIRE(M >= 0 && N >= 1 && K >= 1 && M <= INT32_MAX && N <= INT32_MAX && K <= INT32_MAX,
+                "ocppo_linear_act: bad sizes M=%lld N=%lld K=%lld", (long long)M, (long long)N,
+                (long long)K);
+  OCPPO_REQUIRE(ldx >= K && ldy >= N, "ocppo_linear_act: leading dimensions ldx=%lld ldy=%lld",
+                (long long)ldx, (long long)ldy);
+  if (M == 0) return OCPPO_OK;
+  OCPPO_REQUIRE(x && w && y, "ocppo_linear_act: null pointer");
+  OCPPO_REQUIRE((M + 15) / 16 * ((N + 15) / 16) <= INT32_MAX / 8, "ocppo_linear_act: too large");
+  const bool vec = K % 4 == 0 && ldx % 4 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0 &&
+                   reinterpret_cast<uintptr_t>(w) % 16 == 0;
+  clear_stale_error();
+  hipStream_t s = as_stream(stream);
+  if (relu)
+    launch_linear<true>(s, vec, x, ldx, w, b, y, ldy, (int)M, (int)N, (int)K);
+  else
+    launch_linear<false>(s, vec, x, ldx, w, b, y, ldy, (int)M, (int)N, (int)K);
+  return check_launch("ocppo_linear_act");
+}

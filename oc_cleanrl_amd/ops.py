@@ -349,6 +349,32 @@ def obs_reset(frame, obs_out, net_obs=None):
          _DTYPE_CODE[obs_out.dtype], _opt(net_obs, "net_obs", torch.float32, dev, N * W * D))
 
 
+def linear_act(x, weight, bias=None, relu: bool = False, out=None):
+    """y = act(x @ weight.T + bias) on the f32 matrix cores, for rollout-sized batches (no
+    autograd). x [M, K] f32 with unit column stride (row stride may exceed K, e.g. a frame slice
+    of the stacked obs); weight [N, K] contiguous (nn.Linear.weight); bias [N] or None."""
+    if x.dim() != 2 or weight.dim() != 2:
+        raise ValueError(f"x must be [M, K] and weight [N, K], got {tuple(x.shape)}, "
+                         f"{tuple(weight.shape)}")
+    M, K = x.shape
+    N = weight.shape[0]
+    dev = x.device
+    if weight.shape[1] != K:
+        raise ValueError(f"weight is {tuple(weight.shape)}, x has K={K}")
+    if x.dtype != torch.float32 or (M > 1 and x.stride(1) != 1) or x.device.type != "cuda":
+        raise ValueError("x must be an f32 GPU tensor with unit column stride")
+    ldx = x.stride(0) if M > 1 else K
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=dev)
+    if tuple(out.shape) != (M, N) or (M > 1 and out.stride(1) != 1) or out.dtype != torch.float32:
+        raise ValueError("out must be an f32 [M, N] tensor with unit column stride")
+    ldy = out.stride(0) if M > 1 else N
+    call("ocppo_linear_act", _stream(dev), x.data_ptr(), ldx,
+         _check(weight, "weight", torch.float32, dev), _opt(bias, "bias", torch.float32, dev, N),
+         out.data_ptr(), ldy, M, N, K, 1 if relu else 0)
+    return out
+
+
 def frame_cache_shift(enc, fresh, done=None):
     """In-place shift of the rollout's frame-encoding cache (PPObj): enc [N, W, E] f32,
     fresh [N, E] f32 (row stride may exceed E), done [N] f32 or None:
@@ -515,8 +541,8 @@ class ReplayBuffer:
     def add(self, obs, next_obs, actions, rewards, dones):
         dev = self.device
         f = torch.float32
-        if obs.dtype not in (torch.float32, torch.uint8) or next_obs.dtype != obs.dtype:
-            raise ValueError("obs/next_obs must both be f32 or u8")
+        if obs.dtype not in _DTYPE_CODE or next_obs.dtype != obs.dtype:
+            raise ValueError("obs/next_obs must both be f32, bf16 or u8")
         n = self.E * self.D
         call("ocppo_replay_add", _stream(dev), _check(obs, "obs", None, dev, n),
              _check(next_obs, "next_obs", None, dev, n), _DTYPE_CODE[obs.dtype],

@@ -132,7 +132,7 @@ class PPOTrainer:
                                       " use --backend Synthetic")
         torch.use_deterministic_algorithms(a.torch_deterministic)
         torch.backends.cudnn.deterministic = a.torch_deterministic
-        torch.backends.cudnn.benchmark = False
+        torch.backends.cudnn.benchmark = a.conv_benchmark
 
         # seeding as ppo_atari_multigpu.py:208-212, 230-231: identical init on every rank, then
         # rank-dependent sampling / env / shuffle streams
@@ -219,6 +219,11 @@ class PPOTrainer:
         self.loss_ws = ops.LossWorkspace(self.M, self.A, dev)
         self.b_obs = self.obs[:T].view((T * N,) + self.obs_shape)
 
+        # The update of the NatureCNN agent runs eagerly: capturing its MIOpen convolution
+        # backward at Atari minibatch sizes (8192 x 4 x 84 x 84) segfaults inside hipGraph
+        # capture_end on ROCm 7.0 / torch 2.10 (its kernels are large enough that launch overhead
+        # is noise anyway); the rollout is still captured.
+        self.graph_update = a.cuda_graphs and not self.pixels
         self.timer = KernelTimer(kernel_timing)
         self.graphs_ready = False
         self.g_rollout = None
@@ -362,7 +367,9 @@ class PPOTrainer:
         with torch.cuda.graph(self.g_rollout):
             self._rollout()
         pool = self.g_rollout.pool()
-        if self.world == 1:
+        if not self.graph_update:
+            pass
+        elif self.world == 1:
             for e in range(self.E):
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, pool=pool):
@@ -382,7 +389,7 @@ class PPOTrainer:
     def _run_update(self):
         a = self.args
         for e in range(self.E):
-            if self.graphs_ready:
+            if self.graphs_ready and self.graph_update:
                 if self.world == 1:
                     self.g_update[e].replay()
                 else:

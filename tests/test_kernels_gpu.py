@@ -341,6 +341,42 @@ def test_frame_cache_shift_rejects_bad_shapes(ops, dev):
         ops.frame_cache_shift(enc, torch.zeros(4, 8, device="cpu"))
 
 
+@pytest.mark.parametrize("M,K,N,ldx", [(128, 12, 256, 48), (512, 256, 512, 256), (128, 2048, 512, 2048),
+                                      (37, 7, 19, 7), (1, 512, 1024, 512), (130, 1024, 513, 1028),
+                                      (256, 3136, 512, 3136), (16, 16, 16, 16)])
+@pytest.mark.parametrize("relu", [True, False])
+def test_linear_act_vs_torch(ops, dev, M, K, N, ldx, relu):
+    """Rollout Linear(+ReLU) on the f32 matrix cores: within f32 summation-order error of
+    F.linear (error bound relative to sum |x*w|, the f32 dot-product error scale)."""
+    g = torch.Generator(device=dev).manual_seed(M * K + N)
+    big = torch.randn(M, ldx, device=dev, generator=g) * 3
+    x = big[:, :K]
+    w = torch.randn(N, K, device=dev, generator=g) * 0.05
+    b = torch.randn(N, device=dev, generator=g)
+    y = ops.linear_act(x, w, b, relu)
+    ref = x.double() @ w.double().t() + b.double()
+    if relu:
+        ref = torch.relu(ref)
+    scale = (x.double().abs() @ w.double().abs().t() + b.double().abs()).max().item()
+    assert (y.double() - ref).abs().max().item() <= 4e-7 * scale
+    # no bias, strided output rows
+    full = torch.full((M, N + 3), 7.0, device=dev)
+    out = full[:, :N]
+    ops.linear_act(x, w, None, False, out)
+    ref0 = x.double() @ w.double().t()
+    assert (out.double() - ref0).abs().max().item() <= 4e-7 * scale
+    assert torch.all(full[:, N:] == 7.0)
+
+
+def test_linear_act_deterministic(ops, dev):
+    x = torch.randn(128, 2048, device=dev)
+    w = torch.randn(512, 2048, device=dev)
+    b = torch.randn(512, device=dev)
+    y1 = ops.linear_act(x, w, b, True)
+    y2 = ops.linear_act(x, w, b, True)
+    assert torch.equal(y1, y2)
+
+
 def test_obs_reset(ops, dev):
     frame = torch.randint(0, 256, (9, 7056), dtype=torch.uint8, device=dev)
     out = torch.empty(9, 4, 7056, dtype=torch.bfloat16, device=dev)

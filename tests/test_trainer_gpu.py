@@ -139,10 +139,13 @@ def test_rollout_frame_cache_matches_full_trunk(dev):
         # the cache holds the encodings of the bootstrap obs (step T)
         torch.testing.assert_close(a.agent.decode(a.enc_cache), a.agent.trunk(a.net_obs),
                                    rtol=1e-5, atol=1e-5)
-        # every step's stored value = the critic on the full stacked obs of that step
+        # every step's stored value = the critic on the full stacked obs of that step. The two
+        # paths run different f32 GEMM kernels (the rollout's HIP MFMA kernel at N rows vs
+        # hipBLASLt at (T+1)N rows); obs features up to 210 put hidden units at O(100), so the
+        # summation-order difference is ~1e-7 x that per layer
         T, N = a.T, a.N
         full = a.agent.get_value(a.obs[:T + 1].float().view((T + 1) * N, *a.obs_shape))
-        torch.testing.assert_close(a.values, full.view(T + 1, N), rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(a.values, full.view(T + 1, N), rtol=1e-4, atol=1e-4)
     b, _ = run_iters(small_args(encoder_dims=(32, 64, 48), decoder_dims=(64,),
                                 rollout_frame_cache=False), 2, dev)
     c, _ = run_iters(small_args(encoder_dims=(32, 64, 48), decoder_dims=(64,),
