@@ -248,6 +248,30 @@ OCPPO_API int ocppo_linear_act(ocppo_stream_t stream, const float* x, int64_t ld
                      int relu);
 
 /* ---------------------------------------------------------------------------------------------
+ * Frame-deduplicated PPObj minibatch encoder — replaces the per-slot encoder work inside
+ * `agent.get_action_and_value(b_obs[mb_inds], ...)` of ppo_atari_oc.py:566 for the PPObj network
+ * (architectures/ppo.py:60-84: Linear on the last dim of every stacked frame). Slot k of the
+ * stored obs[t, n] ([T+1, N, W, F], step-major) is env n's frame of step max(t-(W-1)+k, r), r the
+ * latest reset in (t-(W-1), t] (dones[r, n] = 1); its timeline id is u = (s+W-1)*N + n.
+ *   frames_gather : x_out[c, :] = f32(frame uniq[c]) for the C (padded: id -1 -> zeros) distinct
+ *                   frames of one minibatch;
+ *   frames_expand : h_out[i, k, :] = enc[pos_of[u(perm[i], k)], :]  ([M, W, E], the decoder input);
+ *   frames_scatter: denc[c, :] = sum of dh[i, k, :] over the uses of frame uniq[c] by the samples
+ *                   of minibatch `mb` (inv[b] = position of sample b in the epoch permutation;
+ *                   sample b belongs to minibatch inv[b] / M), fixed order -> deterministic.
+ * W <= 16; dones [T+1, N] f32 with row r = "obs[r] starts an episode".
+ * ------------------------------------------------------------------------------------------- */
+OCPPO_API int ocppo_frames_gather(ocppo_stream_t stream, const void* obs, int obs_dtype, int64_t T,
+                        int64_t N, int64_t W, int64_t F, const int32_t* uniq, int64_t C,
+                        float* x_out);
+OCPPO_API int ocppo_frames_expand(ocppo_stream_t stream, const float* enc, int64_t C, int64_t E,
+                        const int32_t* pos_of, const int64_t* perm, int64_t M, const float* dones,
+                        int64_t T, int64_t N, int64_t W, float* h_out);
+OCPPO_API int ocppo_frames_scatter(ocppo_stream_t stream, const float* dh, int64_t M, int64_t E,
+                         const int32_t* uniq, int64_t C, const int32_t* inv, int64_t mb,
+                         const float* dones, int64_t T, int64_t N, int64_t W, float* denc_out);
+
+/* ---------------------------------------------------------------------------------------------
  * Minibatch gather — replaces `b_obs[mb_inds]` of ppo_atari_oc.py:566-567:
  *   dst[i, :] = f32(src[idx[i], :]),  src [B, R] of dtype src_dtype, dst [M, R] f32.
  * ------------------------------------------------------------------------------------------- */

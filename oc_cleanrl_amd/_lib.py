@@ -52,6 +52,9 @@ SIGNATURES: dict[str, tuple[type, list]] = {
     "ocppo_gather_rows": (I, [P, P, I, P, I64, I64, P]),
     "ocppo_frame_cache_shift": (I, [P, P, P, I64, P, I64, I64, I64]),
     "ocppo_linear_act": (I, [P, P, I64, P, P, P, I64, I64, I64, I64, I]),
+    "ocppo_frames_gather": (I, [P, P, I, I64, I64, I64, I64, P, I64, P]),
+    "ocppo_frames_expand": (I, [P, P, I64, I64, P, P, I64, P, I64, I64, I64, P]),
+    "ocppo_frames_scatter": (I, [P, P, I64, I64, P, I64, P, I64, P, I64, I64, I64, P]),
     "ocppo_vecnorm_reward": (I, [P, P, P, I64, D, D, D, P, P, P]),
     "ocppo_rollout_store_vecnorm": (I, [P, P, I, P, P, I64, I64, I64, P, P, I, P, P, D, D, D, P,
                                         P, P]),

@@ -117,6 +117,8 @@ class Args:
     save_model: bool = True
     metrics_every: int = 1     # read the device-side metrics every N iterations
     rollout_frame_cache: bool = True  # PPO_OBJ rollout: encode only the newest frame per step
+    update_frame_dedup: bool = True  # PPO_OBJ update: encode each distinct frame of a minibatch once
+    prefetch_shuffle: bool = True  # shuffle (+ frame plan) of the next iteration while the GPU runs
     conv_benchmark: bool = False  # cudnn.benchmark (MIOpen Find) for the NatureCNN convolutions
 
 

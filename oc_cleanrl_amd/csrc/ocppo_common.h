@@ -77,6 +77,63 @@ template <> struct Elem<OCPPO_U8> {
   }
 };
 
+// ---- vector element I/O: VEC elements of dtype DT as one aligned access -----------------------
+template <int DT, int VEC> struct VecIO {
+  // generic fallback (VEC == 1 or unaligned sizes)
+  __device__ static void load(const void* p, int64_t i, float (&v)[VEC]) {
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) v[k] = Elem<DT>::load(static_cast<const typename Elem<DT>::T*>(p), i + k);
+  }
+  __device__ static void store(void* p, int64_t i, const float (&v)[VEC]) {
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) Elem<DT>::store(static_cast<typename Elem<DT>::T*>(p), i + k, v[k]);
+  }
+};
+template <> struct VecIO<OCPPO_F32, 4> {
+  __device__ static void load(const void* p, int64_t i, float (&v)[4]) {
+    const float4 x = *reinterpret_cast<const float4*>(static_cast<const float*>(p) + i);
+    v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+  }
+  __device__ static void store(void* p, int64_t i, const float (&v)[4]) {
+    *reinterpret_cast<float4*>(static_cast<float*>(p) + i) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+};
+template <> struct VecIO<OCPPO_BF16, 4> {
+  __device__ static void load(const void* p, int64_t i, float (&v)[4]) {
+    const uint2 x = *reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(p) + i);
+    v[0] = __uint_as_float(x.x << 16); v[1] = __uint_as_float(x.x & 0xFFFF0000u);
+    v[2] = __uint_as_float(x.y << 16); v[3] = __uint_as_float(x.y & 0xFFFF0000u);
+  }
+  __device__ static void store(void* p, int64_t i, const float (&v)[4]) {
+    uint2 x;
+    x.x = static_cast<uint32_t>(f32_to_bf16(v[0])) | (static_cast<uint32_t>(f32_to_bf16(v[1])) << 16);
+    x.y = static_cast<uint32_t>(f32_to_bf16(v[2])) | (static_cast<uint32_t>(f32_to_bf16(v[3])) << 16);
+    *reinterpret_cast<uint2*>(static_cast<uint16_t*>(p) + i) = x;
+  }
+};
+template <> struct VecIO<OCPPO_U8, 4> {
+  __device__ static void load(const void* p, int64_t i, float (&v)[4]) {
+    const uint32_t x = *reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(p) + i);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = static_cast<float>((x >> (8 * k)) & 0xFFu);
+  }
+  __device__ static void store(void* p, int64_t i, const float (&v)[4]) {
+    uint32_t x = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float f = v[k] < 0.f ? 0.f : (v[k] > 255.f ? 255.f : v[k]);
+      x |= static_cast<uint32_t>(__float2int_rn(f)) << (8 * k);
+    }
+    *reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(p) + i) = x;
+  }
+};
+
+inline int grid_for(int64_t work, int block) {
+  int64_t g = ceil_div(work, block);
+  const int64_t cap = 256 * 16;  // 256 CUs x 16 blocks: grid-stride beyond that
+  return static_cast<int>(g < cap ? (g > 0 ? g : 1) : cap);
+}
+
 // ---- deterministic reductions -----------------------------------------------------------------
 // Butterfly over the 64 lanes: every lane ends with the same value, combined in a fixed order.
 template <typename T>

@@ -1,0 +1,222 @@
+// Frame-deduplicated PPObj minibatch encoder (obs_mode "obj"): the update's forward/backward of
+// cleanrl/ppo_atari_oc.py:566 `agent.get_action_and_value(b_obs[mb_inds], ...)` through the
+// per-frame Linear encoder of architectures/ppo.py:60-84.
+//
+// The PPObj encoder acts on every stacked frame alone, and the W frames of a stored observation
+// obs[t, n] are frames of env n's timeline: slot k holds the frame of step s = t - (W-1) + k, or,
+// when the env was reset at step r in (t-(W-1), t] (dones[r, n] = 1: obs[r] is the reset stack,
+// every slot the first frame), the frame of step max(s, r). A minibatch of M samples therefore
+// needs the encodings of far fewer than M*W distinct frames (about 0.68 of the env-steps when a
+// quarter of the batch is drawn at random and W = 4): the trainer encodes the C distinct frames
+// of each minibatch once (a fixed capacity C per minibatch, planned on the host from the
+// permutation), expands them to [M, W, E] for the decoder, and in the backward pass sums each
+// frame's W-slot gradients back onto its single row. Same math as encoding every slot (the rows
+// are the same frames); the weight-gradient sums group the uses of a frame first, so the f32
+// summation order differs from autograd's.
+//
+// Timeline id of a frame: u = (s + W - 1) * N + n, s in [-(W-1), T-1]; frames with s < 0 are the
+// older slots of obs[0] (the previous iteration's last stack), s >= 0 the newest slot of obs[s].
+//
+// All three kernels are HBM streams (16-B accesses, one row segment per lane); the per-row index
+// work is a handful of scalar loads in the block prologue.
+#include "ocppo_common.h"
+
+namespace ocppo {
+
+constexpr int kFramesMaxW = 16;
+
+// Latest reset step in (t-(W-1), t] of env n, or INT_MIN when there is none.
+__device__ __forceinline__ int latest_reset(const float* __restrict__ dones, int t, int64_t n,
+                                            int64_t N, int W) {
+  const int lo = t - W + 2 > 0 ? t - W + 2 : 0;
+  for (int r = t; r >= lo; --r)
+    if (dones[r * N + n] != 0.f) return r;
+  return INT32_MIN;
+}
+
+// x_out[c, :] = f32(frame of timeline id uniq[c]) (zeros for padding ids < 0)
+template <int DT>
+__global__ __launch_bounds__(256) void frames_gather_kernel(const void* __restrict__ obs,
+                                                            int64_t N, int W, int64_t F,
+                                                            const int32_t* __restrict__ uniq,
+                                                            int64_t C, float* __restrict__ x_out) {
+  const int64_t total = C * F;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t g = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; g < total;
+       g += stride) {
+    const int64_t c = g / F;
+    const int64_t f = g - c * F;
+    const int32_t u = uniq[c];
+    float v = 0.f;
+    if (u >= 0) {
+      const int64_t s = u / N - (W - 1);
+      const int64_t n = u - (s + W - 1) * N;
+      const int64_t src = s >= 0 ? ((s * N + n) * W + (W - 1)) * F + f
+                                 : ((n * W) + (W - 1 + s)) * F + f;
+      v = Elem<DT>::load(static_cast<const typename Elem<DT>::T*>(obs), src);
+    }
+    x_out[g] = v;
+  }
+}
+
+// h[i, k, :] = enc[pos_of[u(i, k)], :] for the M samples perm[0..M) (b = t*N + n)
+template <int VEC>
+__global__ __launch_bounds__(256) void frames_expand_kernel(
+    const float* __restrict__ enc, int64_t E, const int32_t* __restrict__ pos_of,
+    const int64_t* __restrict__ perm, int64_t M, const float* __restrict__ dones, int64_t N,
+    int W, float* __restrict__ h_out) {
+  __shared__ int32_t src_row[kFramesMaxW];
+  const int64_t groups = W * E / VEC;
+  for (int64_t i = blockIdx.x; i < M; i += gridDim.x) {
+    __syncthreads();  // src_row of the previous row is no longer read
+    if (threadIdx.x < W) {
+      const int64_t b = perm[i];
+      const int t = static_cast<int>(b / N);
+      const int64_t n = b - t * N;
+      const int r = latest_reset(dones, t, n, N, W);
+      int s = t - (W - 1) + static_cast<int>(threadIdx.x);
+      s = s > r ? s : r;
+      src_row[threadIdx.x] = pos_of[(s + W - 1) * N + n];
+    }
+    __syncthreads();
+    float* dst = h_out + i * W * E;
+    for (int64_t q = threadIdx.x; q < groups; q += blockDim.x) {
+      const int64_t e = q * VEC;
+      const int k = static_cast<int>(e / E);
+      const int64_t col = e - k * E;
+      float v[VEC];
+      VecIO<OCPPO_F32, VEC>::load(enc, src_row[k] * E + col, v);
+      VecIO<OCPPO_F32, VEC>::store(dst, e, v);
+    }
+  }
+}
+
+// denc[c, :] = sum over the (sample row i, slot k) uses of frame uniq[c] in minibatch `mb` of
+// dh[i, k, :], in the fixed order (t ascending, k ascending); zeros for padding ids.
+template <int VEC>
+__global__ __launch_bounds__(128) void frames_scatter_kernel(
+    const float* __restrict__ dh, int64_t M, int64_t E, const int32_t* __restrict__ uniq,
+    int64_t C, const int32_t* __restrict__ inv, int64_t mb, const float* __restrict__ dones,
+    int64_t T, int64_t N, int W, float* __restrict__ denc) {
+  __shared__ int64_t uses[kFramesMaxW * kFramesMaxW];
+  __shared__ int n_uses;
+  const int64_t groups = E / VEC;
+  for (int64_t c = blockIdx.x; c < C; c += gridDim.x) {
+    __syncthreads();  // the previous row's use list is no longer read
+    if (threadIdx.x == 0) {
+      int cnt = 0;
+      const int32_t u = uniq[c];
+      if (u >= 0) {
+        const int s = static_cast<int>(u / N) - (W - 1);
+        const int64_t n = u - (s + W - 1) * N;
+        const int t_hi = s + W - 1 < T - 1 ? s + W - 1 : static_cast<int>(T - 1);
+        for (int t = s > 0 ? s : 0; t <= t_hi; ++t) {
+          const int32_t p = inv[t * N + n];
+          if (p / M != mb) continue;
+          const int64_t row = p - mb * M;
+          const int r = latest_reset(dones, t, n, N, W);
+          for (int k = 0; k < W; ++k) {
+            int sk = t - (W - 1) + k;
+            sk = sk > r ? sk : r;
+            if (sk == s) uses[cnt++] = row * W + k;
+          }
+        }
+      }
+      n_uses = cnt;
+    }
+    __syncthreads();
+    const int cnt = n_uses;
+    float* dst = denc + c * E;
+    for (int64_t q = threadIdx.x; q < groups; q += blockDim.x) {
+      const int64_t e = q * VEC;
+      float acc[VEC];
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) acc[v] = 0.f;
+      for (int j = 0; j < cnt; ++j) {
+        float x[VEC];
+        VecIO<OCPPO_F32, VEC>::load(dh, uses[j] * E + e, x);
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) acc[v] += x[v];
+      }
+      VecIO<OCPPO_F32, VEC>::store(dst, e, acc);
+    }
+  }
+}
+
+static bool aligned16(const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; }
+
+}  // namespace ocppo
+
+using namespace ocppo;
+
+extern "C" int ocppo_frames_gather(ocppo_stream_t stream, const void* obs, int obs_dtype,
+                                   int64_t T, int64_t N, int64_t W, int64_t F,
+                                   const int32_t* uniq, int64_t C, float* x_out) {
+  OCPPO_REQUIRE(T >= 1 && N >= 1 && W >= 1 && W <= kFramesMaxW && F >= 1 && C >= 0 &&
+                    (T + W - 1) * N < INT32_MAX,
+                "ocppo_frames_gather: bad sizes");
+  if (C == 0) return OCPPO_OK;
+  OCPPO_REQUIRE(obs && uniq && x_out, "ocppo_frames_gather: null pointer");
+  clear_stale_error();
+  hipStream_t s = as_stream(stream);
+  const int g = grid_for(C * F, 256);
+  switch (obs_dtype) {
+    case OCPPO_F32:
+      hipLaunchKernelGGL(frames_gather_kernel<OCPPO_F32>, dim3(g), dim3(256), 0, s, obs, N,
+                         (int)W, F, uniq, C, x_out);
+      break;
+    case OCPPO_BF16:
+      hipLaunchKernelGGL(frames_gather_kernel<OCPPO_BF16>, dim3(g), dim3(256), 0, s, obs, N,
+                         (int)W, F, uniq, C, x_out);
+      break;
+    case OCPPO_U8:
+      hipLaunchKernelGGL(frames_gather_kernel<OCPPO_U8>, dim3(g), dim3(256), 0, s, obs, N,
+                         (int)W, F, uniq, C, x_out);
+      break;
+    default:
+      return fail(OCPPO_E_INVALID, "ocppo_frames_gather: bad obs dtype %d", obs_dtype);
+  }
+  return check_launch("ocppo_frames_gather");
+}
+
+extern "C" int ocppo_frames_expand(ocppo_stream_t stream, const float* enc, int64_t C, int64_t E,
+                                   const int32_t* pos_of, const int64_t* perm, int64_t M,
+                                   const float* dones, int64_t T, int64_t N, int64_t W,
+                                   float* h_out) {
+  OCPPO_REQUIRE(C >= 1 && E >= 1 && M >= 0 && T >= 1 && N >= 1 && W >= 1 && W <= kFramesMaxW &&
+                    (T + W - 1) * N < INT32_MAX,
+                "ocppo_frames_expand: bad sizes");
+  if (M == 0) return OCPPO_OK;
+  OCPPO_REQUIRE(enc && pos_of && perm && dones && h_out, "ocppo_frames_expand: null pointer");
+  clear_stale_error();
+  hipStream_t s = as_stream(stream);
+  const int g = static_cast<int>(M < 8192 ? M : 8192);
+  if (E % 4 == 0 && aligned16(enc) && aligned16(h_out))
+    hipLaunchKernelGGL(frames_expand_kernel<4>, dim3(g), dim3(256), 0, s, enc, E, pos_of, perm, M,
+                       dones, N, (int)W, h_out);
+  else
+    hipLaunchKernelGGL(frames_expand_kernel<1>, dim3(g), dim3(256), 0, s, enc, E, pos_of, perm, M,
+                       dones, N, (int)W, h_out);
+  return check_launch("ocppo_frames_expand");
+}
+
+extern "C" int ocppo_frames_scatter(ocppo_stream_t stream, const float* dh, int64_t M, int64_t E,
+                                    const int32_t* uniq, int64_t C, const int32_t* inv,
+                                    int64_t mb, const float* dones, int64_t T, int64_t N,
+                                    int64_t W, float* denc_out) {
+  OCPPO_REQUIRE(M >= 1 && E >= 1 && C >= 0 && mb >= 0 && T >= 1 && N >= 1 && W >= 1 &&
+                    W <= kFramesMaxW && (T + W - 1) * N < INT32_MAX && T * N < INT32_MAX,
+                "ocppo_frames_scatter: bad sizes");
+  if (C == 0) return OCPPO_OK;
+  OCPPO_REQUIRE(dh && uniq && inv && dones && denc_out, "ocppo_frames_scatter: null pointer");
+  clear_stale_error();
+  hipStream_t s = as_stream(stream);
+  const int g = static_cast<int>(C < 16384 ? C : 16384);
+  if (E % 4 == 0 && aligned16(dh) && aligned16(denc_out))
+    hipLaunchKernelGGL(frames_scatter_kernel<4>, dim3(g), dim3(128), 0, s, dh, M, E, uniq, C, inv,
+                       mb, dones, T, N, (int)W, denc_out);
+  else
+    hipLaunchKernelGGL(frames_scatter_kernel<1>, dim3(g), dim3(128), 0, s, dh, M, E, uniq, C, inv,
+                       mb, dones, T, N, (int)W, denc_out);
+  return check_launch("ocppo_frames_scatter");
+}

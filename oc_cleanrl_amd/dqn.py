@@ -175,6 +175,9 @@ class DQNTrainer:
         self.args = a
         self.dev = torch.device(device)
         torch.use_deterministic_algorithms(a.torch_deterministic)
+        # deterministic mode also NaN-fills every torch.empty (a debugging aid: ~300 fill launches per
+        # iteration here); nothing reads uninitialised memory, so results are unaffected
+        torch.utils.deterministic.fill_uninitialized_memory = False
         torch.backends.cudnn.deterministic = a.torch_deterministic
         torch.backends.cudnn.benchmark = False
         torch.manual_seed(a.seed)

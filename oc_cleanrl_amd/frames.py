@@ -1,0 +1,133 @@
+"""Frame-deduplicated PPObj minibatch forward/backward (obs_mode "obj", PPO_OBJ agent).
+
+The update of ppo_atari_oc.py:566 runs `agent.get_action_and_value(b_obs[mb_inds], ...)`, and
+PPObj's encoder (architectures/ppo.py:60-84) is a Linear stack on the last dim, i.e. on every
+stacked frame alone. The W frames of a stored observation obs[t, n] are frames of env n's own
+timeline (slot k = the frame of step t-(W-1)+k, clipped to the latest reset), so a minibatch of M
+samples holds only ~0.69·M·W distinct frames when it is a random quarter of the batch (W = 4).
+
+Per minibatch the trainer therefore
+  1. gathers the C distinct frames once                    (HIP `ocppo_frames_gather`),
+  2. runs the encoder on C rows instead of M·W             (hipBLASLt, autograd),
+  3. expands the C encodings to the [M, W, E] decoder input (HIP `ocppo_frames_expand`),
+and in the backward pass sums each frame's slot gradients back onto its row
+(HIP `ocppo_frames_scatter`, fixed order, deterministic). The rows are the same frames, so the
+forward is identical to encoding every slot; only the f32 summation order of the encoder's
+weight gradients differs (the uses of one frame are summed first).
+
+The plan (which frames each minibatch needs) depends only on the epoch permutations, so it is
+built on the host from the shuffle (`FramePlanner`), as a superset that ignores resets (a reset
+only maps a slot onto a later frame of the same window, which is in the set already), and copied
+to the device with the permutation; every minibatch gets the same fixed capacity `cap` (padding
+ids -1 encode to rows whose gradient is exactly zero), so the update stays graph-capturable.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import ops
+
+
+class FramePlanner:
+    """Host-side plan of the distinct frames of every minibatch of an iteration.
+
+    Layout of one plan (int32, one contiguous pinned buffer so it is ONE H2D copy):
+      uniq  [J, cap]           timeline ids of the distinct frames of minibatch j, ascending,
+                               padded with -1 (J = epochs x minibatches)
+      pos_of[J, (T+W-1)*N]     row of each timeline id in minibatch j's encoding
+      inv   [E, T*N]           position of each sample in epoch e's permutation
+    Timeline id of env n's frame of step s (s in [-(W-1), T-1]): u = (s + W - 1) * N + n.
+    """
+
+    def __init__(self, T: int, N: int, W: int, M: int, epochs: int, num_minibatches: int,
+                 cap: int | None = None, headroom: float = 1.05, align: int = 2048):
+        self.T, self.N, self.W, self.M = T, N, W, M
+        self.E, self.nmb = epochs, num_minibatches
+        self.J = epochs * num_minibatches
+        self.B = T * N
+        self.U = (T + W - 1) * N
+        self.headroom, self.align = headroom, align
+        self.cap = cap
+        self.counts = np.zeros(self.J, np.int64)
+
+    def size(self, cap: int) -> int:
+        return self.J * cap + self.J * self.U + self.E * self.B
+
+    def views(self, buf, cap: int):
+        """(uniq [J, cap], pos_of [J, U], inv [E, B]) views of a flat int32 buffer."""
+        J, U = self.J, self.U
+        uniq = buf[:J * cap].reshape(J, cap)
+        pos_of = buf[J * cap:J * cap + J * U].reshape(J, U)
+        inv = buf[J * cap + J * U:self.size(cap)].reshape(self.E, self.B)
+        return uniq, pos_of, inv
+
+    def cap_for(self, counts) -> int:
+        """Capacity for the largest minibatch + headroom, rounded up to `align` rows: hipBLASLt's
+        f32 tiles quantise badly between multiples of 2048 rows on gfx950 (encoder fwd+bwd at
+        [10240, 12032, 12288, 16384] rows: 802, 1002, 896, 1088 us; tools/exp_dedup_rows.py)."""
+        c = int(np.ceil(int(counts.max()) * self.headroom / self.align) * self.align)
+        return min(max(c, self.align), self.M * self.W)
+
+    def plan(self, perm: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
+        """perm [E*B] (the epochs' shuffles, ppo_atari_oc.py:561) -> (used [J, U] bool,
+        inv [E, B] int32); sets self.counts (distinct frames per minibatch).
+
+        Frame (s, n) is used by minibatch k of epoch e iff one of the samples t in
+        [s, s+W-1] of env n is in it: with mb[t, n] = inv_e[t*N + n] // M that is an OR of W
+        shifted copies of (mb == k) along t -- a few [T+W-1, N] array passes per minibatch."""
+        T, N, W, M, J, U, B = self.T, self.N, self.W, self.M, self.J, self.U, self.B
+        inv = np.empty((self.E, B), np.int32)
+        ar = np.arange(B, dtype=np.int32)
+        used = np.zeros((J, T + W - 1, N), bool)
+        for e in range(self.E):
+            inv[e, perm[e * B:(e + 1) * B]] = ar
+            mb = (inv[e] // M).reshape(T, N)
+            for k in range(self.nmb):
+                eq = mb == k
+                u = used[e * self.nmb + k]
+                for i in range(W):  # frame row s' = s + W - 1 is used by sample t = s' - i
+                    u[i:i + T] |= eq
+        used = used.reshape(J, U)
+        self.counts = np.count_nonzero(used, axis=1)
+        return used, inv
+
+    def fill(self, buf: np.ndarray, cap: int, used, inv) -> None:
+        """Write a plan into the flat int32 buffer laid out for capacity `cap`."""
+        uniq, po, iv = self.views(buf, cap)
+        uniq.fill(-1)
+        for j in range(self.J):
+            nz = np.flatnonzero(used[j])
+            uniq[j, :len(nz)] = nz
+        np.cumsum(used, axis=1, dtype=np.int32, out=po)
+        po -= 1  # row of a used id; unused ids are never looked up
+        iv[...] = inv
+
+
+class _FramesExpand(torch.autograd.Function):
+    """h [M, W, E] = enc[pos_of[slot frame ids]]; backward = deterministic per-frame slot sum."""
+
+    @staticmethod
+    def forward(ctx, enc, pos_of, perm, dones, uniq, inv, mb, T, N, W):
+        ctx.save_for_backward(uniq, inv, dones)
+        ctx.geom = (int(mb), T, N, W, perm.numel())
+        return ops.frames_expand(enc, pos_of, perm, dones, T, N, W)
+
+    @staticmethod
+    def backward(ctx, dh):
+        uniq, inv, dones = ctx.saved_tensors
+        mb, T, N, W, M = ctx.geom
+        denc = ops.frames_scatter(dh.contiguous().view(M, W, -1), uniq, inv, mb, dones, T, N, W)
+        return denc, None, None, None, None, None, None, None, None, None
+
+
+def minibatch_hidden(agent, obs, dones, uniq, pos_of, inv, perm, mb: int):
+    """Decoder output of PPObj for the samples `perm` (one minibatch) from the rollout obs
+    [T+1, N, W, F] with each distinct frame encoded once; autograd flows to every parameter.
+    `mb` is the minibatch's index within its epoch (inv is that epoch's inverse permutation)."""
+    T1, N, W, _ = obs.shape
+    T = T1 - 1
+    x = ops.frames_gather(obs, uniq)
+    enc = agent.encode(x)
+    h = _FramesExpand.apply(enc.contiguous(), pos_of, perm, dones, uniq, inv, mb, T, N, W)
+    return agent.decode(h)

@@ -375,6 +375,65 @@ def linear_act(x, weight, bias=None, relu: bool = False, out=None):
     return out
 
 
+# ---------------------------------------------------------------------------------------------
+# Frame-deduplicated PPObj minibatch encoder (ppo_atari_oc.py:566 through architectures/ppo.py:60-84)
+# ---------------------------------------------------------------------------------------------
+def _obs_TNWF(obs):
+    if obs.dim() != 4:
+        raise ValueError(f"obs must be [T+1, N, W, F], got {tuple(obs.shape)}")
+    T1, N, W, F = obs.shape
+    return T1 - 1, N, W, F
+
+
+def frames_gather(obs, uniq, out=None):
+    """x[c, :] = f32(frame with timeline id uniq[c]) of the rollout obs [T+1, N, W, F]
+    (padding ids < 0 give zero rows). uniq [C] int32 -> x [C, F] f32."""
+    T, N, W, F = _obs_TNWF(obs)
+    dev = obs.device
+    C = uniq.numel()
+    if out is None:
+        out = torch.empty((C, F), dtype=torch.float32, device=dev)
+    call("ocppo_frames_gather", _stream(dev), _check(obs, "obs", None, dev),
+         _DTYPE_CODE[obs.dtype], T, N, W, F, _check(uniq, "uniq", torch.int32, dev), C,
+         _check(out, "out", torch.float32, dev, C * F))
+    return out
+
+
+def frames_expand(enc, pos_of, perm, dones, T: int, N: int, W: int, out=None):
+    """h[i, k, :] = enc[pos_of[timeline id of slot k of sample perm[i]]] -> [M, W, E] f32.
+    enc [C, E] f32, pos_of [(T+W-1)*N] int32, perm [M] int64, dones [T+1, N] f32."""
+    C, E = enc.shape
+    M = perm.numel()
+    dev = enc.device
+    if out is None:
+        out = torch.empty((M, W, E), dtype=torch.float32, device=dev)
+    call("ocppo_frames_expand", _stream(dev), _check(enc, "enc", torch.float32, dev), C, E,
+         _check(pos_of, "pos_of", torch.int32, dev, (T + W - 1) * N),
+         _check(perm, "perm", torch.int64, dev), M,
+         _check(dones, "dones", torch.float32, dev, (T + 1) * N), T, N, W,
+         _check(out, "out", torch.float32, dev, M * W * E))
+    return out
+
+
+def frames_scatter(dh, uniq, inv, mb: int, dones, T: int, N: int, W: int, out=None):
+    """Backward of frames_expand: denc[c, :] = sum of dh[i, k, :] over the uses of frame uniq[c]
+    by minibatch `mb` (inv [T*N] int32: position of each sample in the epoch permutation).
+    dh [M, W, E] f32 -> denc [C, E] f32, deterministic."""
+    M = dh.shape[0]
+    E = dh.shape[-1]
+    if dh.numel() != M * W * E:
+        raise ValueError(f"dh must be [M, W, E] with W={W}, got {tuple(dh.shape)}")
+    C = uniq.numel()
+    dev = dh.device
+    if out is None:
+        out = torch.empty((C, E), dtype=torch.float32, device=dev)
+    call("ocppo_frames_scatter", _stream(dev), _check(dh, "dh", torch.float32, dev), M, E,
+         _check(uniq, "uniq", torch.int32, dev), C, _check(inv, "inv", torch.int32, dev, T * N),
+         int(mb), _check(dones, "dones", torch.float32, dev, (T + 1) * N), T, N, W,
+         _check(out, "out", torch.float32, dev, C * E))
+    return out
+
+
 def frame_cache_shift(enc, fresh, done=None):
     """In-place shift of the rollout's frame-encoding cache (PPObj): enc [N, W, E] f32,
     fresh [N, E] f32 (row stride may exceed E), done [N] f32 or None:

@@ -30,7 +30,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
-from . import ops
+from . import frames, ops
 from .agents import PPObj, make_agent
 from .args import Args
 from .envs import SyntheticAtariEnv
@@ -131,6 +131,9 @@ class PPOTrainer:
             raise NotImplementedError(f"env backend {a.backend!r} needs ALE/OCAtari (not available);"
                                       " use --backend Synthetic")
         torch.use_deterministic_algorithms(a.torch_deterministic)
+        # deterministic mode also NaN-fills every torch.empty (a debugging aid: ~300 fill launches per
+        # iteration here); nothing reads uninitialised memory, so results are unaffected
+        torch.utils.deterministic.fill_uninitialized_memory = False
         torch.backends.cudnn.deterministic = a.torch_deterministic
         torch.backends.cudnn.benchmark = a.conv_benchmark
 
@@ -205,8 +208,20 @@ class PPOTrainer:
         self.b_inds = np.arange(self.B)
         self.perm_host = torch.empty(self.E * self.B, dtype=torch.int64, pin_memory=True)
         self.perm_dev = torch.zeros(self.E * self.B, dtype=torch.int64, device=dev)
+        # the next iteration's shuffle is drawn and copied while the GPU runs this one; it lands
+        # in perm_stage and is moved into perm_dev (which the graphs read) at iteration start
+        self.perm_stage = torch.zeros_like(self.perm_dev)
+        self.staged = False
         self.perm_event = torch.cuda.Event()
         self.perm_event.record()
+        # PPObj update with every distinct frame of a minibatch encoded once (frames.py)
+        W = self.obs_shape[0]
+        self.frame_dedup = (a.update_frame_dedup and isinstance(self.agent, PPObj) and
+                            not self.pixels and len(self.obs_shape) == 2 and
+                            len(a.encoder_dims) > 0 and 1 <= W <= 16)
+        self.planner = (frames.FramePlanner(T, N, W, a.local_minibatch_size, a.update_epochs,
+                                            a.num_minibatches) if self.frame_dedup else None)
+        self.plan_host = self.plan_stage = self.plan_dev = self.plan = None
         nmbt = self.E * self.nmb
         self.mb = {"actions": torch.zeros(nmbt * self.M, dtype=torch.int64, device=dev),
                    **{k: torch.zeros(nmbt * self.M, dtype=f32, device=dev)
@@ -310,8 +325,16 @@ class PPOTrainer:
         """Minibatch j: gather, forward, fused loss, backward into the flat grad buffer."""
         a = self.args
         idx = self.perm_dev[j * self.M:(j + 1) * self.M]
-        self.timer.bracket("gather", lambda: ops.gather_rows(self.b_obs, idx, self.mb_obs))
-        logits, value = self.agent.logits_and_value(self.mb_obs)
+        ag = self.agent
+        if self.frame_dedup:
+            e, k = divmod(j, self.nmb)
+            uniq, pos_of, inv = self.plan
+            hidden = frames.minibatch_hidden(ag, self.obs, self.dones, uniq[j], pos_of[j], inv[e],
+                                             idx, k)
+            logits, value = ag._head(ag.actor, hidden), ag._head(ag.critic, hidden)
+        else:
+            self.timer.bracket("gather", lambda: ops.gather_rows(self.b_obs, idx, self.mb_obs))
+            logits, value = ag.logits_and_value(self.mb_obs)
         lg, vv = logits.detach(), value.detach().view(-1)  # the timer's closure must not hold
         sl = slice(j * self.M, (j + 1) * self.M)
         mb = self.mb
@@ -349,15 +372,47 @@ class PPOTrainer:
 
     # ------------------------------------------------------------------------------------------
     def _shuffle(self):
-        """np.random.shuffle(b_inds) once per epoch (:561), all epochs up front, then one async
-        copy to the device (the previous iteration's copy finished at its metrics sync)."""
-        self.perm_event.synchronize()  # the previous async copy out of perm_host is done
+        """np.random.shuffle(b_inds) once per epoch (:561), all epochs up front, plus (frame
+        dedup) the minibatches' frame plan; one async copy each into the staging buffers. Runs
+        for iteration i+1 while the GPU executes iteration i (same RNG stream order)."""
+        self.perm_event.synchronize()  # the previous async copies out of the host buffers are done
         out = self.perm_host.numpy()
         for e in range(self.E):
             self.np_rng.shuffle(self.b_inds)
             out[e * self.B:(e + 1) * self.B] = self.b_inds
-        self.perm_dev.copy_(self.perm_host, non_blocking=True)
+        if self.frame_dedup:
+            used, inv = self.planner.plan(out)
+            cap = self.planner.cap
+            if cap is None or int(self.planner.counts.max()) > cap:
+                self._alloc_plan(self.planner.cap_for(self.planner.counts))
+            self.planner.fill(self.plan_host.numpy(), self.planner.cap, used, inv)
+            self.plan_stage.copy_(self.plan_host, non_blocking=True)
+        self.perm_stage.copy_(self.perm_host, non_blocking=True)
         self.perm_event.record()
+        self.staged = True
+
+    def _alloc_plan(self, cap: int):
+        """(Re)size the frame-plan buffers for `cap` distinct frames per minibatch. A resize
+        after capture waits for the GPU and drops the graphs (they hold the old addresses)."""
+        if self.plan_dev is not None:
+            torch.cuda.synchronize(self.dev)
+            self.graphs_ready = False
+            self.g_rollout, self.g_update, self.g_opt = None, [], None
+        self.planner.cap = cap
+        n = self.planner.size(cap)
+        self.plan_host = torch.empty(n, dtype=torch.int32, pin_memory=True)
+        self.plan_stage = torch.zeros(n, dtype=torch.int32, device=self.dev)
+        self.plan_dev = torch.zeros(n, dtype=torch.int32, device=self.dev)
+        self.plan = self.planner.views(self.plan_dev, cap)
+
+    def _load_staged(self):
+        """Move the staged shuffle / frame plan into the buffers the graphs read."""
+        if not self.staged:
+            self._shuffle()
+        self.perm_dev.copy_(self.perm_stage)
+        if self.frame_dedup:
+            self.plan_dev.copy_(self.plan_stage)
+        self.staged = False
 
     def _capture(self):
         """Capture the rollout and the update into hipGraphs (after one eager warm-up iteration,
@@ -412,7 +467,7 @@ class PPOTrainer:
         if a.anneal_lr:
             frac = 1.0 - (self.iteration - 1.0) / max(a.num_iterations, 1)
             self.lr.fill_(frac * a.learning_rate)
-        self._shuffle()
+        self._load_staged()
         use_graphs = a.cuda_graphs and self.iteration > 1
         if use_graphs and not self.graphs_ready:
             self._capture()
@@ -421,6 +476,8 @@ class PPOTrainer:
         else:
             self._rollout()
         self._run_update()
+        if a.prefetch_shuffle:
+            self._shuffle()  # host work of the next iteration, overlapped with this one's GPU work
         self.timer.end_iteration()
         self.global_step += self.N * self.T * self.world
         m = {}

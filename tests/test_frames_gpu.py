@@ -1,0 +1,110 @@
+"""Frame-deduplicated PPObj minibatch kernels (ocppo_frames_gather / _expand / _scatter) on the
+GPU through the C-ABI, against the oracle's restatement (bit-exact), plus the trainer's dedup
+update against the plain per-slot update (ppo_atari_oc.py:566-605 through PPObj)."""
+import numpy as np
+import pytest
+import torch
+
+from oc_cleanrl_amd import ops
+from oc_cleanrl_amd.frames import FramePlanner
+from oracle import ocppo_oracle as O
+from test_frames_cpu import _rollout
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(T, N, W, F, M, E, nmb, p_done, seed, dev, dtype=torch.bfloat16):
+    rng = np.random.default_rng(seed)
+    obs, dones = _rollout(T, N, W, F, p_done, rng, (rng.random(N) < 0.3).astype(np.float32))
+    pl = FramePlanner(T, N, W, M, E, nmb)
+    perm = np.concatenate([rng.permutation(T * N) for _ in range(E)]).astype(np.int64)
+    used, inv = pl.plan(perm)
+    cap = pl.cap_for(pl.counts)
+    buf = np.zeros(pl.size(cap), np.int32)
+    pl.fill(buf, cap, used, inv)
+    d_buf = torch.from_numpy(buf).to(dev)
+    return dict(obs=obs, dones=dones, perm=perm, plan=pl.views(buf, cap), pl=pl, cap=cap,
+                d_obs=torch.from_numpy(obs).to(dev).to(dtype), d_dones=torch.from_numpy(dones).to(dev),
+                d_perm=torch.from_numpy(perm).to(dev), d_plan=pl.views(d_buf, cap))
+
+
+@pytest.mark.parametrize("T,N,W,F,M,E,nmb,p_done", [
+    (16, 8, 4, 12, 32, 2, 4, 0.2),     # resets in every window
+    (9, 5, 3, 6, 15, 1, 3, 0.5),       # ragged sizes, odd W / F
+    (24, 7, 4, 12, 42, 1, 4, 0.0),     # no resets
+    (12, 4, 1, 12, 12, 2, 4, 0.3),     # W = 1
+    (10, 3, 16, 5, 10, 1, 3, 0.1),     # W = 16 (the kernels' maximum)
+])
+def test_frames_kernels_match_oracle(dev, T, N, W, F, M, E, nmb, p_done):
+    s = _setup(T, N, W, F, M, E, nmb, p_done, 11, dev)
+    uniq, pos_of, inv = s["plan"]
+    du, dp, di = s["d_plan"]
+    Ed = 20
+    rng = np.random.default_rng(5)
+    for j in range(E * nmb):
+        e, k = divmod(j, nmb)
+        x = ops.frames_gather(s["d_obs"], du[j])
+        assert np.array_equal(x.cpu().numpy(), O.frames_gather(s["obs"], uniq[j]))
+        enc = rng.standard_normal((s["cap"], Ed)).astype(np.float32)
+        mb = s["perm"][j * M:(j + 1) * M]
+        h = ops.frames_expand(torch.from_numpy(enc).to(dev), dp[j], s["d_perm"][j * M:(j + 1) * M],
+                              s["d_dones"], T, N, W)
+        assert np.array_equal(h.cpu().numpy(), O.frames_expand(enc, pos_of[j], mb, s["dones"], N, W))
+        dh = rng.standard_normal((M, W, Ed)).astype(np.float32)
+        denc = ops.frames_scatter(torch.from_numpy(dh).to(dev), du[j], di[e], k, s["d_dones"], T, N, W)
+        want = O.frames_scatter(dh, uniq[j], inv[e], k, s["dones"], T, N, W)
+        assert np.array_equal(denc.cpu().numpy(), want)  # same summation order: bit-exact
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32, torch.uint8])
+def test_frames_at_config_size_reproduce_the_minibatch(dev, dtype):
+    """Config 2 sizes (T=128, N=128, W=4, F=12, 4 x 4 minibatches of 4096): the deduplicated
+    frames, expanded, ARE b_obs[mb_inds] bit for bit; scatter is expand's adjoint."""
+    T, N, W, F, M, E, nmb = 128, 128, 4, 12, 4096, 4, 4
+    s = _setup(T, N, W, F, M, E, nmb, 1 / 50, 3, dev, dtype)
+    du, dp, di = s["d_plan"]
+    b_obs = s["d_obs"][:T].reshape(T * N, W, F).float()
+    g = torch.Generator(device=dev).manual_seed(0)
+    for j in range(E * nmb):
+        e, k = divmod(j, nmb)
+        idx = s["d_perm"][j * M:(j + 1) * M]
+        x = ops.frames_gather(s["d_obs"], du[j])
+        h = ops.frames_expand(x, dp[j], idx, s["d_dones"], T, N, W)
+        assert torch.equal(h, b_obs[idx])
+        enc = torch.randn((s["cap"], 16), device=dev, generator=g, dtype=torch.float64).float()
+        dh = torch.randn((M, W, 16), device=dev, generator=g, dtype=torch.float64).float()
+        he = ops.frames_expand(enc, dp[j], idx, s["d_dones"], T, N, W)
+        denc = ops.frames_scatter(dh, du[j], di[e], k, s["d_dones"], T, N, W)
+        lhs = torch.dot(he.double().ravel(), dh.double().ravel())
+        rhs = torch.dot(enc.double().ravel(), denc.double().ravel())
+        torch.testing.assert_close(lhs, rhs, rtol=1e-5, atol=1e-3)
+        assert torch.all(denc[int(s["pl"].counts[j]):] == 0)
+
+
+def test_trainer_dedup_update_matches_per_slot_update(dev):
+    """One minibatch's loss and gradients with the dedup encoder == the per-slot encoder (the
+    reference's b_obs[mb_inds] forward) up to f32 summation order."""
+    from oc_cleanrl_amd.args import Args, finalize
+    from oc_cleanrl_amd.trainer import PPOTrainer
+
+    args = finalize(Args(env_id="ALE/Pong-v5", obs_mode="obj", architecture="PPO_OBJ",
+                         num_envs=64, num_steps=32, num_minibatches=4, update_epochs=2,
+                         total_timesteps=64 * 32 * 10, encoder_dims=(64, 128), decoder_dims=(128,),
+                         save_model=False, cuda_graphs=False), 1)
+    tr = PPOTrainer(args, dev)
+    assert tr.frame_dedup
+    tr.train_iteration()
+    tr._load_staged()
+    with torch.no_grad():
+        tr._rollout()
+    for j in (0, 5):
+        tr.frame_dedup = True
+        tr._forward_backward(j)
+        g1, st1 = tr.grad_buf.clone(), tr.stats[j].clone()
+        tr.frame_dedup = False
+        tr._forward_backward(j)
+        g2, st2 = tr.grad_buf.clone(), tr.stats[j].clone()
+        torch.testing.assert_close(st1, st2, rtol=1e-5, atol=1e-6)
+        scale = g2.abs().max()
+        torch.testing.assert_close(g1, g2, rtol=0, atol=2e-5 * float(scale))
+        assert not torch.equal(g1, torch.zeros_like(g1))
