@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define OCPPO_ABI_VERSION 1
+#define OCPPO_ABI_VERSION 2
 
 /* status codes */
 #define OCPPO_OK 0
@@ -205,8 +205,11 @@ OCPPO_API int ocppo_categorical_logprob_entropy_bwd(ocppo_stream_t stream, const
  *   reward     : [N] f32;  done : [N] f32 (0/1)
  *   prev_obs   : [N, W, D] stacked obs of the previous step, dtype obs_dtype (rollout slot t)
  *   obs_out    : [N, W, D] new stacked obs, dtype obs_dtype (rollout slot t+1)
- *   net_obs    : [N, W, D] f32 copy of obs_out for the network forward (may be NULL)
+ *   net_obs    : f32 copy of obs_out for the network forward (may be NULL when net_layout = 0)
  *   reward_out : [N] f32 (&rewards[t*N]);  done_out : [N] f32 (&dones[(t+1)*N]); either may be NULL
+ *   net_layout : 0 = net_obs [N, W, D] like obs_out; 1 = channels-last [N, D, W] (the NHWC input
+ *                of a channels_last NatureCNN, 16-B aligned; MIOpen's NHWC convolutions then
+ *                need no transpose)
  * Stacking: obs_out[n] = prev_obs[n][1:] ++ frame[n]; on done[n] every slot is frame[n] (the
  * gymnasium FrameStack reset fill). Conversion to bf16 is round-to-nearest-even and exact for
  * the integer-valued obs of both modes (|x| <= 256).
@@ -214,11 +217,13 @@ OCPPO_API int ocppo_categorical_logprob_entropy_bwd(ocppo_stream_t stream, const
 OCPPO_API int ocppo_rollout_store(ocppo_stream_t stream, const void* frame, int frame_dtype,
                         const float* reward, const float* done, int64_t N, int64_t W, int64_t D,
                         const void* prev_obs, void* obs_out, int obs_dtype, float* net_obs,
-                        float* reward_out, float* done_out);
+                        float* reward_out, float* done_out, int net_layout);
 
-/* Fill a whole stacked-obs slot from one frame per env (env reset, ppo_atari_oc.py:464-465). */
+/* Fill a whole stacked-obs slot from one frame per env (env reset, ppo_atari_oc.py:464-465);
+ * net_layout as in ocppo_rollout_store. */
 OCPPO_API int ocppo_obs_reset(ocppo_stream_t stream, const void* frame, int frame_dtype, int64_t N,
-                    int64_t W, int64_t D, void* obs_out, int obs_dtype, float* net_obs);
+                    int64_t W, int64_t D, void* obs_out, int obs_dtype, float* net_obs,
+                    int net_layout);
 
 /* ---------------------------------------------------------------------------------------------
  * Frame-encoding cache of the rollout forward (PPObj, architectures/ppo.py:60-84, whose encoder
@@ -278,6 +283,12 @@ OCPPO_API int ocppo_frames_scatter(ocppo_stream_t stream, const float* dh, int64
 OCPPO_API int ocppo_gather_rows(ocppo_stream_t stream, const void* src, int src_dtype, const int64_t* idx,
                       int64_t M, int64_t R, float* dst);
 
+/* The same gather into channels-last rows (the NHWC input of a channels_last NatureCNN):
+ *   dst[i, p, c] = f32(src[idx[i], c, p]),  src [B, C, P] (C stacked frames of P pixels),
+ *   dst [M, P, C] f32, 16-B aligned. */
+OCPPO_API int ocppo_gather_rows_cl(ocppo_stream_t stream, const void* src, int src_dtype,
+                         const int64_t* idx, int64_t M, int64_t C, int64_t P, float* dst);
+
 /* ---------------------------------------------------------------------------------------------
  * Reward normalisation of SB3 VecNormalize(norm_obs=False, norm_reward=True) as wrapped at
  * ppo_atari_oc.py:414 (stable-baselines3 2.0.0, not in the reference tree), on device in f64:
@@ -298,7 +309,7 @@ OCPPO_API int ocppo_rollout_store_vecnorm(ocppo_stream_t stream, const void* fra
                                           int64_t W, int64_t D, const void* prev_obs, void* obs_out,
                                           int obs_dtype, float* net_obs, float* done_out,
                                           double gamma, double epsilon, double clip_reward,
-                                          double* ret_state, double* rms_state, float* reward_out);
+                                          double* ret_state, double* rms_state, float* reward_out, int net_layout);
 
 /* ---------------------------------------------------------------------------------------------
  * DQN (config 5, dqn_atari_oc.py) — HBM replay buffer with stable-baselines3 2.0.0

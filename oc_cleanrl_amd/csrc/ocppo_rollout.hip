@@ -48,17 +48,77 @@ __device__ __forceinline__ void store_groups(int64_t blk, int64_t nblk, const vo
   }
 }
 
+// Same store with the f32 network copy in channels-last order: net[n, p, w] (= NHWC for pixel
+// stacks [N, W, 84, 84]; what MIOpen's NHWC convolutions read without a transpose). One thread per
+// (env, VEC consecutive elements of the frame): it produces all W slots of those elements, so the
+// W x VEC network values it writes are contiguous (W == 4: one 16-B store per element).
 template <int FDT, int ODT, int VEC>
+__device__ __forceinline__ void store_groups_cl(int64_t blk, int64_t nblk,
+                                                const void* __restrict__ frame,
+                                                const float* __restrict__ reward,
+                                                const float* __restrict__ done, int64_t N, int W,
+                                                int64_t D, const void* __restrict__ prev,
+                                                void* __restrict__ out, float* __restrict__ net,
+                                                float* __restrict__ reward_out,
+                                                float* __restrict__ done_out) {
+  const int64_t DG = D / VEC;
+  const int64_t groups = N * DG;
+  const int64_t stride = nblk * blockDim.x;
+  for (int64_t g = blk * blockDim.x + threadIdx.x; g < groups; g += stride) {
+    const int64_t n = g / DG;
+    const int64_t k = (g - n * DG) * VEC;
+    const bool reset = done[n] != 0.f;
+    float* dst = net + (n * D + k) * W;
+    if (W == 4) {
+      float v[4][VEC];
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        if (w == 3 || reset)
+          VecIO<FDT, VEC>::load(frame, n * D + k, v[w]);
+        else
+          VecIO<ODT, VEC>::load(prev, (n * 4 + w + 1) * D + k, v[w]);
+        VecIO<ODT, VEC>::store(out, (n * 4 + w) * D + k, v[w]);
+      }
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) {
+        float px[4] = {Elem<ODT>::roundtrip(v[0][q]), Elem<ODT>::roundtrip(v[1][q]),
+                       Elem<ODT>::roundtrip(v[2][q]), Elem<ODT>::roundtrip(v[3][q])};
+        VecIO<OCPPO_F32, 4>::store(dst, 4 * q, px);  // net is 16-B aligned (host check)
+      }
+    } else {
+      for (int w = 0; w < W; ++w) {
+        float v[VEC];
+        if (w == W - 1 || reset)
+          VecIO<FDT, VEC>::load(frame, n * D + k, v);
+        else
+          VecIO<ODT, VEC>::load(prev, (n * W + w + 1) * D + k, v);
+        VecIO<ODT, VEC>::store(out, (n * W + w) * D + k, v);
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) dst[q * W + w] = Elem<ODT>::roundtrip(v[q]);
+      }
+    }
+    if (g < N) {
+      if (reward_out) reward_out[g] = reward[g];
+      if (done_out) done_out[g] = done[g];
+    }
+  }
+}
+
+template <int FDT, int ODT, int VEC, bool CL>
 __global__ __launch_bounds__(256) void rollout_store_kernel(
     const void* __restrict__ frame, const float* __restrict__ reward,
     const float* __restrict__ done, int64_t N, int W, int64_t D, const void* __restrict__ prev,
     void* __restrict__ out, float* __restrict__ net, float* __restrict__ reward_out,
     float* __restrict__ done_out) {
-  store_groups<FDT, ODT, VEC>(blockIdx.x, gridDim.x, frame, reward, done, N, W, D, prev, out, net,
-                              reward_out, done_out);
+  if (CL)
+    store_groups_cl<FDT, ODT, VEC>(blockIdx.x, gridDim.x, frame, reward, done, N, W, D, prev, out,
+                                   net, reward_out, done_out);
+  else
+    store_groups<FDT, ODT, VEC>(blockIdx.x, gridDim.x, frame, reward, done, N, W, D, prev, out,
+                                net, reward_out, done_out);
 }
 
-template <int FDT, int ODT, int VEC>
+template <int FDT, int ODT, int VEC, bool CL>
 __global__ __launch_bounds__(256) void obs_reset_kernel(const void* __restrict__ frame, int64_t N,
                                                         int W, int64_t D, void* __restrict__ out,
                                                         float* __restrict__ net) {
@@ -79,7 +139,12 @@ __global__ __launch_bounds__(256) void obs_reset_kernel(const void* __restrict__
       float back[VEC];
 #pragma unroll
       for (int q = 0; q < VEC; ++q) back[q] = Elem<ODT>::roundtrip(v[q]);
-      VecIO<OCPPO_F32, VEC>::store(net, o, back);
+      if (CL) {
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) net[(n * D + k + q) * W + w] = back[q];
+      } else {
+        VecIO<OCPPO_F32, VEC>::store(net, o, back);
+      }
     }
   }
 }
@@ -101,6 +166,45 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const void* __restrict
     float v[VEC];
     VecIO<SDT, VEC>::load(src, row * R + k, v);
     VecIO<OCPPO_F32, VEC>::store(dst, i * R + k, v);
+  }
+}
+
+// ---- minibatch gather into channels-last order: dst[i, p, c] = f32(src[idx[i], c, p]) ------------
+// src rows [C, P] (C stacked frames of P elements), dst rows [P, C]: the NHWC network input of a
+// channels_last NatureCNN. One thread per (row, VEC consecutive elements): C loads of VEC, then
+// VEC x C contiguous f32 (C == 4: one 16-B store per element).
+template <int SDT, int VEC>
+__global__ __launch_bounds__(256) void gather_rows_cl_kernel(const void* __restrict__ src,
+                                                             const int64_t* __restrict__ idx,
+                                                             int64_t M, int C, int64_t P,
+                                                             float* __restrict__ dst) {
+  const int64_t PG = P / VEC;
+  const int64_t groups = M * PG;
+  const int64_t R = C * P;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t g = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; g < groups;
+       g += stride) {
+    const int64_t i = g / PG;
+    const int64_t k = (g - i * PG) * VEC;
+    const int64_t row = idx[i];
+    float* out = dst + i * R + k * C;
+    if (C == 4) {
+      float v[4][VEC];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) VecIO<SDT, VEC>::load(src, row * R + c * P + k, v[c]);
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) {
+        float px[4] = {v[0][q], v[1][q], v[2][q], v[3][q]};
+        VecIO<OCPPO_F32, 4>::store(out, 4 * q, px);  // dst is 16-B aligned (host check)
+      }
+    } else {
+      for (int c = 0; c < C; ++c) {
+        float v[VEC];
+        VecIO<SDT, VEC>::load(src, row * R + c * P + k, v);
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) out[q * C + c] = v[q];
+      }
+    }
   }
 }
 
@@ -164,7 +268,7 @@ __global__ __launch_bounds__(1024) void vecnorm_reward_kernel(
 // Store + VecNormalize in ONE launch: workgroup 0 normalises the rewards of all N envs (f64
 // reduction), workgroups 1.. do the frame-stack store. Both halves only read the env outputs, so
 // they need no ordering between them.
-template <int FDT, int ODT, int VEC>
+template <int FDT, int ODT, int VEC, bool CL>
 __global__ __launch_bounds__(256) void store_vecnorm_kernel(
     const void* __restrict__ frame, const float* __restrict__ reward,
     const float* __restrict__ done, int64_t N, int W, int64_t D, const void* __restrict__ prev,
@@ -175,8 +279,12 @@ __global__ __launch_bounds__(256) void store_vecnorm_kernel(
     vecnorm_block(reward, done, N, gamma, eps, clip, ret, rms, reward_out);
     return;
   }
-  store_groups<FDT, ODT, VEC>(blockIdx.x - 1, gridDim.x - 1, frame, reward, done, N, W, D, prev,
-                              out, net, nullptr, done_out);
+  if (CL)
+    store_groups_cl<FDT, ODT, VEC>(blockIdx.x - 1, gridDim.x - 1, frame, reward, done, N, W, D,
+                                   prev, out, net, nullptr, done_out);
+  else
+    store_groups<FDT, ODT, VEC>(blockIdx.x - 1, gridDim.x - 1, frame, reward, done, N, W, D, prev,
+                                out, net, nullptr, done_out);
 }
 
 // ---- synthetic env ------------------------------------------------------------------------------
@@ -246,19 +354,24 @@ __global__ __launch_bounds__(256) void synth_env_kernel(uint64_t seed,
   }
 }
 
-template <int FDT, int ODT>
+// Grid of a store launch: one group per (env, slot, VEC elements), or per (env, VEC elements)
+// when the network copy is channels-last (the thread then writes every slot).
+inline int64_t store_groups_count(int64_t N, int64_t W, int64_t D, int vec, bool cl) {
+  return cl ? N * (D / vec) : N * W * (D / vec);
+}
+
+template <int FDT, int ODT, bool CL>
 int launch_store(hipStream_t s, const void* frame, const float* reward, const float* done,
                  int64_t N, int64_t W, int64_t D, const void* prev, void* out, float* net,
                  float* rout, float* dout) {
-  if (D % 4 == 0) {
-    const int64_t groups = N * W * (D / 4);
-    hipLaunchKernelGGL((rollout_store_kernel<FDT, ODT, 4>), dim3(grid_for(groups, 256)), dim3(256),
-                       0, s, frame, reward, done, N, (int)W, D, prev, out, net, rout, dout);
-  } else {
-    const int64_t groups = N * W * D;
-    hipLaunchKernelGGL((rollout_store_kernel<FDT, ODT, 1>), dim3(grid_for(groups, 256)), dim3(256),
-                       0, s, frame, reward, done, N, (int)W, D, prev, out, net, rout, dout);
-  }
+  if (D % 4 == 0)
+    hipLaunchKernelGGL((rollout_store_kernel<FDT, ODT, 4, CL>),
+                       dim3(grid_for(store_groups_count(N, W, D, 4, CL), 256)), dim3(256), 0, s,
+                       frame, reward, done, N, (int)W, D, prev, out, net, rout, dout);
+  else
+    hipLaunchKernelGGL((rollout_store_kernel<FDT, ODT, 1, CL>),
+                       dim3(grid_for(store_groups_count(N, W, D, 1, CL), 256)), dim3(256), 0, s,
+                       frame, reward, done, N, (int)W, D, prev, out, net, rout, dout);
   return check_launch("ocppo_rollout_store");
 }
 
@@ -269,35 +382,34 @@ struct VecNormArgs {
   float* reward_out;
 };
 
-template <int FDT, int ODT>
+template <int FDT, int ODT, bool CL>
 int launch_store_vecnorm(hipStream_t s, const void* frame, const float* reward, const float* done,
                          int64_t N, int64_t W, int64_t D, const void* prev, void* out, float* net,
                          float* dout, const VecNormArgs& vn) {
-  if (D % 4 == 0) {
-    const int64_t groups = N * W * (D / 4);
-    hipLaunchKernelGGL((store_vecnorm_kernel<FDT, ODT, 4>), dim3(1 + grid_for(groups, 256)),
-                       dim3(256), 0, s, frame, reward, done, N, (int)W, D, prev, out, net, dout,
-                       vn.gamma, vn.eps, vn.clip, vn.ret, vn.rms, vn.reward_out);
-  } else {
-    const int64_t groups = N * W * D;
-    hipLaunchKernelGGL((store_vecnorm_kernel<FDT, ODT, 1>), dim3(1 + grid_for(groups, 256)),
-                       dim3(256), 0, s, frame, reward, done, N, (int)W, D, prev, out, net, dout,
-                       vn.gamma, vn.eps, vn.clip, vn.ret, vn.rms, vn.reward_out);
-  }
+  if (D % 4 == 0)
+    hipLaunchKernelGGL((store_vecnorm_kernel<FDT, ODT, 4, CL>),
+                       dim3(1 + grid_for(store_groups_count(N, W, D, 4, CL), 256)), dim3(256), 0,
+                       s, frame, reward, done, N, (int)W, D, prev, out, net, dout, vn.gamma,
+                       vn.eps, vn.clip, vn.ret, vn.rms, vn.reward_out);
+  else
+    hipLaunchKernelGGL((store_vecnorm_kernel<FDT, ODT, 1, CL>),
+                       dim3(1 + grid_for(store_groups_count(N, W, D, 1, CL), 256)), dim3(256), 0,
+                       s, frame, reward, done, N, (int)W, D, prev, out, net, dout, vn.gamma,
+                       vn.eps, vn.clip, vn.ret, vn.rms, vn.reward_out);
   return check_launch("ocppo_rollout_store_vecnorm");
 }
 
-template <int FDT, int ODT>
+template <int FDT, int ODT, bool CL>
 int launch_reset(hipStream_t s, const void* frame, int64_t N, int64_t W, int64_t D, void* out,
                  float* net) {
   if (D % 4 == 0) {
     const int64_t groups = N * W * (D / 4);
-    hipLaunchKernelGGL((obs_reset_kernel<FDT, ODT, 4>), dim3(grid_for(groups, 256)), dim3(256), 0,
-                       s, frame, N, (int)W, D, out, net);
+    hipLaunchKernelGGL((obs_reset_kernel<FDT, ODT, 4, CL>), dim3(grid_for(groups, 256)), dim3(256),
+                       0, s, frame, N, (int)W, D, out, net);
   } else {
     const int64_t groups = N * W * D;
-    hipLaunchKernelGGL((obs_reset_kernel<FDT, ODT, 1>), dim3(grid_for(groups, 256)), dim3(256), 0,
-                       s, frame, N, (int)W, D, out, net);
+    hipLaunchKernelGGL((obs_reset_kernel<FDT, ODT, 1, CL>), dim3(grid_for(groups, 256)), dim3(256),
+                       0, s, frame, N, (int)W, D, out, net);
   }
   return check_launch("ocppo_obs_reset");
 }
@@ -316,6 +428,20 @@ int launch_gather(hipStream_t s, const void* src, const int64_t* idx, int64_t M,
   }
   return check_launch("ocppo_gather_rows");
 }
+
+template <int SDT>
+int launch_gather_cl(hipStream_t s, const void* src, const int64_t* idx, int64_t M, int64_t C,
+                     int64_t P, float* dst) {
+  if (P % 4 == 0)
+    hipLaunchKernelGGL((gather_rows_cl_kernel<SDT, 4>), dim3(grid_for(M * (P / 4), 256)), dim3(256),
+                       0, s, src, idx, M, (int)C, P, dst);
+  else
+    hipLaunchKernelGGL((gather_rows_cl_kernel<SDT, 1>), dim3(grid_for(M * P, 256)), dim3(256), 0,
+                       s, src, idx, M, (int)C, P, dst);
+  return check_launch("ocppo_gather_rows_cl");
+}
+
+static bool aligned16(const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; }
 
 // ---- frame-encoding cache of the rollout (PPObj: the encoder acts on each frame alone) ---------
 // enc[n, w, :] = done[n] != 0 || w == W-1 ? fresh[n, :] : enc[n, w+1, :]   (in place)
@@ -361,8 +487,11 @@ using namespace ocppo;
 extern "C" int ocppo_rollout_store(ocppo_stream_t stream, const void* frame, int frame_dtype,
                                    const float* reward, const float* done, int64_t N, int64_t W,
                                    int64_t D, const void* prev_obs, void* obs_out, int obs_dtype,
-                                   float* net_obs, float* reward_out, float* done_out) {
+                                   float* net_obs, float* reward_out, float* done_out,
+                                   int net_layout) {
   OCPPO_REQUIRE(N >= 0 && W >= 1 && D >= 1 && W <= 64, "ocppo_rollout_store: bad sizes");
+  OCPPO_REQUIRE(net_layout == 0 || (net_layout == 1 && net_obs && aligned16(net_obs)),
+                "ocppo_rollout_store: net_layout must be 0, or 1 with a 16-B aligned net_obs");
   OCPPO_REQUIRE(frame_dtype == OCPPO_F32 || frame_dtype == OCPPO_U8,
                 "ocppo_rollout_store: frame dtype must be OCPPO_F32 or OCPPO_U8");
   OCPPO_REQUIRE(valid_dtype(obs_dtype), "ocppo_rollout_store: bad obs dtype %d", obs_dtype);
@@ -371,10 +500,12 @@ extern "C" int ocppo_rollout_store(ocppo_stream_t stream, const void* frame, int
   OCPPO_REQUIRE(prev_obs != obs_out, "ocppo_rollout_store: prev_obs must not alias obs_out");
   clear_stale_error();
   hipStream_t s = as_stream(stream);
-#define OCPPO_STORE(F, O)                                                                  \
-  if (frame_dtype == F && obs_dtype == O)                                                  \
-    return launch_store<F, O>(s, frame, reward, done, N, W, D, prev_obs, obs_out, net_obs, \
-                              reward_out, done_out);
+#define OCPPO_STORE(F, O)                                                                     \
+  if (frame_dtype == F && obs_dtype == O)                                                     \
+    return net_layout ? launch_store<F, O, true>(s, frame, reward, done, N, W, D, prev_obs,   \
+                                                 obs_out, net_obs, reward_out, done_out)      \
+                      : launch_store<F, O, false>(s, frame, reward, done, N, W, D, prev_obs,  \
+                                                  obs_out, net_obs, reward_out, done_out);
   OCPPO_STORE(OCPPO_F32, OCPPO_F32)
   OCPPO_STORE(OCPPO_F32, OCPPO_BF16)
   OCPPO_STORE(OCPPO_F32, OCPPO_U8)
@@ -386,8 +517,10 @@ extern "C" int ocppo_rollout_store(ocppo_stream_t stream, const void* frame, int
 }
 
 extern "C" int ocppo_obs_reset(ocppo_stream_t stream, const void* frame, int frame_dtype, int64_t N,
-                               int64_t W, int64_t D, void* obs_out, int obs_dtype, float* net_obs) {
+                               int64_t W, int64_t D, void* obs_out, int obs_dtype, float* net_obs,
+                               int net_layout) {
   OCPPO_REQUIRE(N >= 0 && W >= 1 && D >= 1 && W <= 64, "ocppo_obs_reset: bad sizes");
+  OCPPO_REQUIRE(net_layout == 0 || net_layout == 1, "ocppo_obs_reset: bad net_layout");
   OCPPO_REQUIRE(frame_dtype == OCPPO_F32 || frame_dtype == OCPPO_U8,
                 "ocppo_obs_reset: frame dtype must be OCPPO_F32 or OCPPO_U8");
   OCPPO_REQUIRE(valid_dtype(obs_dtype), "ocppo_obs_reset: bad obs dtype %d", obs_dtype);
@@ -395,8 +528,10 @@ extern "C" int ocppo_obs_reset(ocppo_stream_t stream, const void* frame, int fra
   OCPPO_REQUIRE(frame && obs_out, "ocppo_obs_reset: null pointer");
   clear_stale_error();
   hipStream_t s = as_stream(stream);
-#define OCPPO_RESET(F, O) \
-  if (frame_dtype == F && obs_dtype == O) return launch_reset<F, O>(s, frame, N, W, D, obs_out, net_obs);
+#define OCPPO_RESET(F, O)                                                                 \
+  if (frame_dtype == F && obs_dtype == O)                                                 \
+    return net_layout ? launch_reset<F, O, true>(s, frame, N, W, D, obs_out, net_obs)     \
+                      : launch_reset<F, O, false>(s, frame, N, W, D, obs_out, net_obs);
   OCPPO_RESET(OCPPO_F32, OCPPO_F32)
   OCPPO_RESET(OCPPO_F32, OCPPO_BF16)
   OCPPO_RESET(OCPPO_F32, OCPPO_U8)
@@ -418,6 +553,21 @@ extern "C" int ocppo_gather_rows(ocppo_stream_t stream, const void* src, int src
   if (src_dtype == OCPPO_F32) return launch_gather<OCPPO_F32>(s, src, idx, M, R, dst);
   if (src_dtype == OCPPO_BF16) return launch_gather<OCPPO_BF16>(s, src, idx, M, R, dst);
   return launch_gather<OCPPO_U8>(s, src, idx, M, R, dst);
+}
+
+extern "C" int ocppo_gather_rows_cl(ocppo_stream_t stream, const void* src, int src_dtype,
+                                    const int64_t* idx, int64_t M, int64_t C, int64_t P,
+                                    float* dst) {
+  OCPPO_REQUIRE(M >= 0 && C >= 1 && C <= 64 && P >= 1, "ocppo_gather_rows_cl: bad sizes");
+  OCPPO_REQUIRE(valid_dtype(src_dtype), "ocppo_gather_rows_cl: bad dtype %d", src_dtype);
+  if (M == 0) return OCPPO_OK;
+  OCPPO_REQUIRE(src && idx && dst, "ocppo_gather_rows_cl: null pointer");
+  OCPPO_REQUIRE(aligned16(dst), "ocppo_gather_rows_cl: dst must be 16-B aligned");
+  clear_stale_error();
+  hipStream_t s = as_stream(stream);
+  if (src_dtype == OCPPO_F32) return launch_gather_cl<OCPPO_F32>(s, src, idx, M, C, P, dst);
+  if (src_dtype == OCPPO_BF16) return launch_gather_cl<OCPPO_BF16>(s, src, idx, M, C, P, dst);
+  return launch_gather_cl<OCPPO_U8>(s, src, idx, M, C, P, dst);
 }
 
 extern "C" int ocppo_vecnorm_reward(ocppo_stream_t stream, const float* reward, const float* done,
@@ -459,8 +609,10 @@ extern "C" int ocppo_rollout_store_vecnorm(ocppo_stream_t stream, const void* fr
                                            void* obs_out, int obs_dtype, float* net_obs,
                                            float* done_out, double gamma, double epsilon,
                                            double clip_reward, double* ret_state,
-                                           double* rms_state, float* reward_out) {
+                                           double* rms_state, float* reward_out, int net_layout) {
   OCPPO_REQUIRE(N >= 1 && W >= 1 && D >= 1 && W <= 64, "ocppo_rollout_store_vecnorm: bad sizes");
+  OCPPO_REQUIRE(net_layout == 0 || (net_layout == 1 && net_obs && aligned16(net_obs)),
+                "ocppo_rollout_store_vecnorm: net_layout must be 0, or 1 with a 16-B aligned net_obs");
   OCPPO_REQUIRE(frame_dtype == OCPPO_F32 || frame_dtype == OCPPO_U8,
                 "ocppo_rollout_store_vecnorm: frame dtype must be OCPPO_F32 or OCPPO_U8");
   OCPPO_REQUIRE(valid_dtype(obs_dtype), "ocppo_rollout_store_vecnorm: bad obs dtype %d", obs_dtype);
@@ -472,10 +624,14 @@ extern "C" int ocppo_rollout_store_vecnorm(ocppo_stream_t stream, const void* fr
   const VecNormArgs vn{gamma, epsilon, clip_reward, ret_state, rms_state, reward_out};
   clear_stale_error();
   hipStream_t s = as_stream(stream);
-#define OCPPO_SV(F, O)                                                                       \
-  if (frame_dtype == F && obs_dtype == O)                                                    \
-    return launch_store_vecnorm<F, O>(s, frame, reward, done, N, W, D, prev_obs, obs_out,    \
-                                      net_obs, done_out, vn);
+#define OCPPO_SV(F, O)                                                                        \
+  if (frame_dtype == F && obs_dtype == O)                                                     \
+    return net_layout ? launch_store_vecnorm<F, O, true>(s, frame, reward, done, N, W, D,     \
+                                                         prev_obs, obs_out, net_obs,          \
+                                                         done_out, vn)                        \
+                      : launch_store_vecnorm<F, O, false>(s, frame, reward, done, N, W, D,    \
+                                                          prev_obs, obs_out, net_obs,         \
+                                                          done_out, vn);
   OCPPO_SV(OCPPO_F32, OCPPO_F32)
   OCPPO_SV(OCPPO_F32, OCPPO_BF16)
   OCPPO_SV(OCPPO_F32, OCPPO_U8)

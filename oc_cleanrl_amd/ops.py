@@ -38,6 +38,22 @@ def _opt(t, *a, **k) -> int | None:
     return None if t is None else _check(t, *a, **k)
 
 
+def _net_obs(net_obs, N: int, W: int, D: int, device):
+    """(pointer, layout) of a rollout network-input buffer: a contiguous [N, W, ...] f32 tensor
+    (layout 0) or a channels_last [N, W, H, X] one (layout 1: memory [N, H, X, W], the NHWC input
+    of a channels_last NatureCNN)."""
+    if net_obs is None:
+        return None, 0
+    if net_obs.is_contiguous():
+        return _check(net_obs, "net_obs", torch.float32, device, N * W * D), 0
+    if net_obs.dim() == 4 and net_obs.is_contiguous(memory_format=torch.channels_last) and \
+            tuple(net_obs.shape[:2]) == (N, W) and net_obs[0, 0].numel() == D:
+        if net_obs.dtype != torch.float32 or net_obs.device != device:
+            raise ValueError(f"net_obs: expected float32 on {device}")
+        return net_obs.data_ptr(), 1
+    raise ValueError("net_obs must be contiguous [N, W, ...] or channels_last [N, W, H, X]")
+
+
 def _stream(device: torch.device) -> int:
     if device.type != "cuda":
         raise ValueError(f"HIP kernels need GPU tensors, got device {device} (no CPU fallback)")
@@ -296,7 +312,8 @@ def rollout_store(frame, reward, done, prev_obs, obs_out, net_obs=None, reward_o
                   done_out=None):
     """obs_out = stack(prev_obs[:, 1:], frame) (reset-filled where done), plus reward/done rows.
 
-    frame [N, D] f32|u8; prev_obs/obs_out [N, W, D] f32|bf16|u8; net_obs [N, W, D] f32.
+    frame [N, D] f32|u8; prev_obs/obs_out [N, W, D] f32|bf16|u8; net_obs [N, W, D] f32, or a
+    channels_last [N, W, H, X] f32 tensor (written in NHWC order).
     """
     N, D = frame.shape[0], frame[0].numel()
     W = obs_out.shape[1]
@@ -308,12 +325,12 @@ def rollout_store(frame, reward, done, prev_obs, obs_out, net_obs=None, reward_o
     if frame.dtype not in (torch.float32, torch.uint8) or obs_out.dtype not in _DTYPE_CODE:
         raise ValueError(f"unsupported dtypes frame={frame.dtype} obs={obs_out.dtype}")
     f = torch.float32
+    net, layout = _net_obs(net_obs, N, W, D, dev)
     call("ocppo_rollout_store", _stream(dev), _check(frame, "frame", None, dev),
          _DTYPE_CODE[frame.dtype], _check(reward, "reward", f, dev, N),
          _check(done, "done", f, dev, N), N, W, D, _check(prev_obs, "prev_obs", None, dev),
-         _check(obs_out, "obs_out", None, dev), _DTYPE_CODE[obs_out.dtype],
-         _opt(net_obs, "net_obs", f, dev, N * W * D), _opt(reward_out, "reward_out", f, dev, N),
-         _opt(done_out, "done_out", f, dev, N))
+         _check(obs_out, "obs_out", None, dev), _DTYPE_CODE[obs_out.dtype], net,
+         _opt(reward_out, "reward_out", f, dev, N), _opt(done_out, "done_out", f, dev, N), layout)
 
 
 def rollout_store_vecnorm(frame, reward, done, prev_obs, obs_out, net_obs, done_out, ret_state,
@@ -327,15 +344,16 @@ def rollout_store_vecnorm(frame, reward, done, prev_obs, obs_out, net_obs, done_
     if tuple(obs_out.shape[:2]) != (N, W) or obs_out[0, 0].numel() != D:
         raise ValueError(f"obs_out {tuple(obs_out.shape)} does not match frame {tuple(frame.shape)}")
     f = torch.float32
+    net, layout = _net_obs(net_obs, N, W, D, dev)
     call("ocppo_rollout_store_vecnorm", _stream(dev), _check(frame, "frame", None, dev),
          _DTYPE_CODE[frame.dtype], _check(reward, "reward", f, dev, N),
          _check(done, "done", f, dev, N), N, W, D, _check(prev_obs, "prev_obs", None, dev),
-         _check(obs_out, "obs_out", None, dev), _DTYPE_CODE[obs_out.dtype],
-         _opt(net_obs, "net_obs", f, dev, N * W * D), _opt(done_out, "done_out", f, dev, N),
+         _check(obs_out, "obs_out", None, dev), _DTYPE_CODE[obs_out.dtype], net,
+         _opt(done_out, "done_out", f, dev, N),
          float(gamma), float(epsilon), float(clip_reward),
          _check(ret_state, "ret_state", torch.float64, dev, N),
          _check(rms_state, "rms_state", torch.float64, dev, 3),
-         _check(reward_out, "reward_out", f, dev, N))
+         _check(reward_out, "reward_out", f, dev, N), layout)
 
 
 def obs_reset(frame, obs_out, net_obs=None):
@@ -344,9 +362,10 @@ def obs_reset(frame, obs_out, net_obs=None):
     dev = frame.device
     if obs_out.numel() != N * W * D:
         raise ValueError("obs_out does not match frame")
+    net, layout = _net_obs(net_obs, N, W, D, dev)
     call("ocppo_obs_reset", _stream(dev), _check(frame, "frame", None, dev),
          _DTYPE_CODE[frame.dtype], N, W, D, _check(obs_out, "obs_out", None, dev),
-         _DTYPE_CODE[obs_out.dtype], _opt(net_obs, "net_obs", torch.float32, dev, N * W * D))
+         _DTYPE_CODE[obs_out.dtype], net, layout)
 
 
 def linear_act(x, weight, bias=None, relu: bool = False, out=None):
@@ -455,7 +474,8 @@ def frame_cache_shift(enc, fresh, done=None):
 
 
 def gather_rows(src, idx, out=None):
-    """out[i] = float32(src[idx[i]]) for src [B, ...] f32|bf16|u8 → out [M, ...] f32."""
+    """out[i] = float32(src[idx[i]]) for src [B, ...] f32|bf16|u8 → out [M, ...] f32. A
+    channels_last `out` [M, C, H, X] gets the rows in NHWC order (ocppo_gather_rows_cl)."""
     dev = src.device
     M = idx.numel()
     R = src[0].numel() if src.shape[0] else 0
@@ -463,6 +483,16 @@ def gather_rows(src, idx, out=None):
         out = torch.empty((M,) + tuple(src.shape[1:]), dtype=torch.float32, device=dev)
     if src.dtype not in _DTYPE_CODE:
         raise ValueError(f"unsupported src dtype {src.dtype}")
+    if not out.is_contiguous():
+        if not (out.dim() == 4 and out.is_contiguous(memory_format=torch.channels_last) and
+                tuple(out.shape[1:]) == tuple(src.shape[1:]) and out.shape[0] == M and
+                out.dtype == torch.float32 and out.device == dev):
+            raise ValueError("out must be contiguous or a channels_last [M, C, H, X] f32 tensor")
+        C = src.shape[1]
+        call("ocppo_gather_rows_cl", _stream(dev), _check(src, "src", None, dev),
+             _DTYPE_CODE[src.dtype], _check(idx, "idx", torch.int64, dev, M), M, C, R // C,
+             out.data_ptr())
+        return out
     call("ocppo_gather_rows", _stream(dev), _check(src, "src", None, dev), _DTYPE_CODE[src.dtype],
          _check(idx, "idx", torch.int64, dev, M), M, R,
          _check(out, "out", torch.float32, dev, M * R))
@@ -544,9 +574,11 @@ class FlatAdam:
             k = p.numel()
             if p.dtype != torch.float32:
                 raise ValueError("FlatAdam needs f32 parameters")
-            self.params[off:off + k].copy_(p.detach().reshape(-1))
-            p.data = self.params[off:off + k].view_as(p)
-            p.grad = self.grads[off:off + k].view_as(p)
+            # same strides as the parameter (e.g. channels_last conv weights keep their layout)
+            view = self.params[off:off + k].as_strided(p.shape, p.stride())
+            view.copy_(p.detach())
+            p.data = view
+            p.grad = self.grads[off:off + k].as_strided(p.shape, p.stride())
             p._ocppo_direct_grad = True  # agents.py's autograd Functions write grads in place
         self.param_list = params
         self.exp_avg = torch.zeros_like(self.params)

@@ -58,7 +58,7 @@ class FlatGrads:
         dev = self.params[0].device
         self.buf = torch.zeros(n, dtype=torch.float32, device=dev)
         for p, off in zip(self.params, offs):
-            p.grad = self.buf[off:off + p.numel()].view_as(p)
+            p.grad = self.buf[off:off + p.numel()].as_strided(p.shape, p.stride())
         self.numel = n
 
     def zero(self):
@@ -152,6 +152,13 @@ class PPOTrainer:
         self.obs_shape = self.env.single_obs_shape
         self.agent = make_agent(a.architecture, self.obs_shape, self.A, self.dev, a.encoder_dims,
                                 a.decoder_dims).to(self.dev)
+        # NatureCNN in channels_last: MIOpen runs its NHWC kernels without transposing every
+        # activation; the HIP store/gather kernels write the network input in NHWC directly
+        self.channels_last = (a.conv_channels_last and self.pixels and len(self.obs_shape) == 3
+                              and any(isinstance(m, nn.Conv2d) for m in self.agent.modules()))
+        self.net_format = torch.channels_last if self.channels_last else torch.contiguous_format
+        if self.channels_last:
+            self.agent = self.agent.to(memory_format=torch.channels_last)
         torch.manual_seed(self.seed)
         self.fused_head = isinstance(self.agent.actor, nn.Linear) and \
             isinstance(self.agent.critic, nn.Linear)
@@ -184,7 +191,8 @@ class PPOTrainer:
         dev = self.dev
         self.obs_dtype = storage_dtype(a, self.pixels)
         self.obs = torch.zeros((T + 1, N) + self.obs_shape, dtype=self.obs_dtype, device=dev)
-        self.net_obs = torch.zeros((N,) + self.obs_shape, dtype=f32, device=dev)
+        self.net_obs = torch.empty((N,) + self.obs_shape, dtype=f32, device=dev,
+                                   memory_format=self.net_format).zero_()
         self.actions = torch.zeros((T, N), dtype=torch.int64, device=dev)
         self.logprobs = torch.zeros((T, N), dtype=f32, device=dev)
         self.rewards = torch.zeros((T, N), dtype=f32, device=dev)
@@ -227,7 +235,8 @@ class PPOTrainer:
                    **{k: torch.zeros(nmbt * self.M, dtype=f32, device=dev)
                       for k in ("logprobs", "advantages", "returns", "values")},
                    "adv_stats": torch.zeros((nmbt, 2), dtype=f32, device=dev)}
-        self.mb_obs = torch.zeros((self.M,) + self.obs_shape, dtype=f32, device=dev)
+        self.mb_obs = torch.empty((self.M,) + self.obs_shape, dtype=f32, device=dev,
+                                  memory_format=self.net_format).zero_()
         self.dlogits = torch.zeros((self.M, self.A), dtype=f32, device=dev)
         self.dvalue = torch.zeros(self.M, dtype=f32, device=dev)
         self.stats = torch.zeros((self.E * self.nmb, len(ops.STAT_NAMES)), dtype=f32, device=dev)

@@ -656,3 +656,57 @@ def test_clip_adam_abi_scalar_tail(ops, dev):
                                                grad_scale=0.5)
     np.testing.assert_allclose(float(sc[1]), total, rtol=1e-5)
     np.testing.assert_allclose(p.cpu().numpy(), ep, rtol=1e-6, atol=1e-9)
+
+
+# ---------------------------------------------------------------------------------------------
+# channels-last (NHWC) network input for the NatureCNN: same values, NHWC memory order
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("W,H,X", [(4, 84, 84), (4, 3, 5), (3, 4, 4), (1, 2, 6)])
+@pytest.mark.parametrize("vecnorm", [False, True])
+def test_store_channels_last_net_equals_plain(ops, dev, W, H, X, vecnorm):
+    rng = np.random.default_rng(H * X + W)
+    N, D = 9, H * X
+    frame = T(rng.integers(0, 256, (N, D)).astype(np.uint8), dev)
+    prev = T(rng.integers(0, 256, (N, W, D)).astype(np.uint8), dev)
+    done = T((rng.random(N) < 0.3).astype(np.float32), dev)
+    rew = T(rng.standard_normal(N).astype(np.float32), dev)
+    res = []
+    for cl in (False, True):
+        o = torch.empty_like(prev)
+        net = torch.empty((N, W, H, X), device=dev,
+                          memory_format=torch.channels_last if cl else torch.contiguous_format)
+        net.fill_(-1.0)
+        dout, rout = torch.empty(N, device=dev), torch.empty(N, device=dev)
+        if vecnorm:
+            ret = torch.zeros(N, dtype=torch.float64, device=dev)
+            rms = torch.tensor([0.0, 1.0, 1e-4], dtype=torch.float64, device=dev)
+            ops.rollout_store_vecnorm(frame, rew, done, prev, o, net, dout, ret, rms, rout)
+        else:
+            ops.rollout_store(frame, rew, done, prev, o, net, rout, dout)
+        res.append((o, net, dout, rout))
+    assert res[1][1].is_contiguous(memory_format=torch.channels_last) or W == 1
+    for x, y in zip(*res):
+        assert torch.equal(x, y)
+    exp = O.rollout_store(frame.cpu().numpy().astype(np.float32), done.cpu().numpy(),
+                          prev.cpu().numpy().astype(np.float32), "u8")
+    assert np.array_equal(res[1][1].cpu().numpy().reshape(N, W, D), exp)
+
+
+def test_obs_reset_channels_last(ops, dev):
+    frame = torch.randint(0, 256, (5, 84 * 84), dtype=torch.uint8, device=dev)
+    out = torch.empty(5, 4, 84 * 84, dtype=torch.uint8, device=dev)
+    net = torch.empty(5, 4, 84, 84, device=dev, memory_format=torch.channels_last)
+    ops.obs_reset(frame, out, net)
+    assert torch.equal(net, frame.float().view(5, 1, 84, 84).expand(5, 4, 84, 84))
+
+
+@pytest.mark.parametrize("src_dt", ["u8", "bf16", "f32"])
+@pytest.mark.parametrize("B,shape,M", [(300, (4, 84, 84), 64), (50, (3, 5, 7), 77), (20, (4, 2, 2), 5)])
+def test_gather_rows_channels_last(ops, dev, src_dt, B, shape, M):
+    rng = np.random.default_rng(B * M)
+    src = rng.integers(0, 256, (B,) + shape).astype(np.float32)
+    idx = rng.integers(0, B, M).astype(np.int64)
+    out = torch.empty((M,) + shape, device=dev, memory_format=torch.channels_last).fill_(-1.0)
+    ops.gather_rows(T(src, dev).to(STORE_DT[src_dt]), T(idx, dev), out)
+    assert out.is_contiguous(memory_format=torch.channels_last)
+    assert np.array_equal(out.cpu().numpy(), src[idx])

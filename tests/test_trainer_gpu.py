@@ -42,6 +42,34 @@ def test_pixel_natureccn_iteration(dev):
     tr, ms = run_iters(args, 2, dev)
     assert tr.obs.dtype == torch.uint8 and tr.obs.shape[2:] == (4, 84, 84)
     assert np.isfinite(ms[-1]["losses/loss"])
+    assert tr.channels_last and tr.net_obs.is_contiguous(memory_format=torch.channels_last)
+
+
+def test_pixel_channels_last_matches_nchw(dev):
+    """The NHWC NatureCNN path (channels_last agent, NHWC store/gather) computes the same network
+    as the plain NCHW one: same initial weights and network input, same logits up to the conv
+    kernels' summation order; both train."""
+    from oc_cleanrl_amd.trainer import PPOTrainer
+
+    trs = []
+    for cl in (False, True):
+        args = small_args(env_id="ALE/Breakout-v5", obs_mode="dqn", architecture="PPO",
+                          num_envs=8, num_steps=8, update_epochs=1, torch_deterministic=False,
+                          conv_channels_last=cl, cuda_graphs=False)
+        trs.append(PPOTrainer(args, dev))
+    a, b = trs
+    assert not a.channels_last and b.channels_last
+    for (ka, pa), (kb, pb) in zip(a.agent.state_dict().items(), b.agent.state_dict().items()):
+        assert ka == kb and torch.equal(pa, pb)
+    assert torch.equal(a.net_obs, b.net_obs)
+    with torch.no_grad():
+        la, va = a.agent.logits_and_value(a.net_obs)
+        lb, vb = b.agent.logits_and_value(b.net_obs)
+    torch.testing.assert_close(la, lb, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(va, vb, rtol=1e-4, atol=1e-4)
+    for tr in trs:
+        m = tr.train_iteration()
+        assert np.isfinite(m["losses/loss"])
 
 
 def test_rollout_buffers_are_consistent(dev):
