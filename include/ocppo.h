@@ -253,6 +253,21 @@ OCPPO_API int ocppo_linear_act(ocppo_stream_t stream, const float* x, int64_t ld
                      int relu);
 
 /* ---------------------------------------------------------------------------------------------
+ * Linear(+ReLU) backward, elementwise part, in one pass — replaces the threshold_backward + bias
+ * `sum(0)` pair autograd runs inside `loss.backward()` (ppo_atari_oc.py:605) for every
+ * nn.Linear -> nn.ReLU of architectures/ppo.py:60-84 / :44-46:
+ *   gp[r, n] = out[r, n] <= 0 ? 0 : g[r, n]   (out = the layer's ReLU output; out == NULL: no
+ *                                             ReLU, gp unused and may be NULL)
+ *   db[n]    = sum_r gp[r, n]                 (deterministic fixed-order reduction)
+ * g/out/gp [R, N] f32 row-major, 16-B aligned, N % 4 == 0, N <= 16384; workspace 256-B aligned,
+ * >= ocppo_relu_bias_grad_workspace_bytes(R, N), ZEROED before its first use (its tickets re-arm).
+ * ------------------------------------------------------------------------------------------- */
+OCPPO_API size_t ocppo_relu_bias_grad_workspace_bytes(int64_t R, int64_t N);
+OCPPO_API int ocppo_relu_bias_grad(ocppo_stream_t stream, const float* g, const float* out,
+                         float* gp, float* db, int64_t R, int64_t N, void* workspace,
+                         size_t workspace_bytes);
+
+/* ---------------------------------------------------------------------------------------------
  * Frame-deduplicated PPObj minibatch encoder — replaces the per-slot encoder work inside
  * `agent.get_action_and_value(b_obs[mb_inds], ...)` of ppo_atari_oc.py:566 for the PPObj network
  * (architectures/ppo.py:60-84: Linear on the last dim of every stacked frame). Slot k of the

@@ -55,7 +55,9 @@ def _splitk(rows: int, k: int, n: int) -> int:
     row chunks + a sum restores 100+ TFLOP/s (tools/exp_gemm_shapes.py, gfx950)."""
     if rows < 8192:
         return 8 if k * n <= 16384 and rows % 8 == 0 else 1
-    if k * n <= 16384:
+    if k * n <= 4096:
+        s = 8  # [12288 x 12] x [12288 x 256]: 13.3 us at 8 vs 22.8 at 16 (exp_update_gemms.py)
+    elif k * n <= 16384:
         s = 16
     elif k * n <= 131072:
         s = 4
@@ -100,20 +102,33 @@ class _LinearAct(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         x, w, out = ctx.saved_tensors
-        gp = torch.ops.aten.threshold_backward(g, out, 0) if ctx.relu else g.contiguous()
+        db = None
+        bias_done = False
+        g = g.contiguous()
+        if FUSED_RELU_BIAS_GRAD and ctx.needs_input_grad[2] and _direct(ctx.b) and \
+                ops.relu_bias_grad_ok(g):
+            # threshold_backward + bias sum in one HIP pass, bias grad written in place
+            gp, _ = ops.relu_bias_grad(g, out if ctx.relu else None, db=ctx.b.grad)
+            bias_done = True
+        else:
+            gp = torch.ops.aten.threshold_backward(g, out, 0) if ctx.relu else g
         dx = gp.mm(w) if ctx.needs_input_grad[0] else None
-        dw = db = None
+        dw = None
         if ctx.needs_input_grad[1]:
             if _direct(ctx.w):
                 _weight_grad(gp, x, out=ctx.w.grad)
             else:
                 dw = _weight_grad(gp, x)
-        if ctx.needs_input_grad[2]:
+        if ctx.needs_input_grad[2] and not bias_done:
             if _direct(ctx.b):
                 torch.sum(gp, 0, out=ctx.b.grad)
             else:
                 db = gp.sum(0)
         return dx, dw, db, None
+
+
+# One-pass HIP ReLU-backward + bias gradient (ops.relu_bias_grad) for FlatAdam-owned biases.
+FUSED_RELU_BIAS_GRAD = True
 
 
 # Rollout-sized inference batches (no autograd) of the shapes where the HIP f32-MFMA kernel beats

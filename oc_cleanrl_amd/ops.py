@@ -395,6 +395,48 @@ def linear_act(x, weight, bias=None, relu: bool = False, out=None):
 
 
 # ---------------------------------------------------------------------------------------------
+# Linear(+ReLU) backward, elementwise part: threshold_backward + bias sum in one pass
+# (autograd of architectures/ppo.py:60-84 inside ppo_atari_oc.py:605)
+# ---------------------------------------------------------------------------------------------
+_RB_WS: dict = {}
+
+
+def _relu_bias_ws(R: int, N: int, dev):
+    """Per-shape workspace (tickets zeroed once, then self re-arming); never reallocated, so
+    captured graphs keep valid pointers."""
+    key = (dev, R, N)
+    ws = _RB_WS.get(key)
+    if ws is None:
+        nb = int(_lib.LIB.ocppo_relu_bias_grad_workspace_bytes(R, N))
+        ws = _RB_WS[key] = torch.zeros(nb, dtype=torch.uint8, device=dev)
+    return ws
+
+
+def relu_bias_grad_ok(g) -> bool:
+    return (g.is_cuda and g.dtype == torch.float32 and g.dim() == 2 and g.shape[1] % 4 == 0
+            and 4 <= g.shape[1] <= 16384 and g.is_contiguous() and g.data_ptr() % 16 == 0)
+
+
+def relu_bias_grad(g, out=None, db=None, gp=None):
+    """(gp, db): gp = threshold_backward(g, out, 0) (g itself when out is None), db = gp.sum(0),
+    in one pass over g [R, N] f32 (N % 4 == 0). Deterministic."""
+    if g.dim() != 2:
+        raise ValueError(f"g must be [R, N], got {tuple(g.shape)}")
+    R, N = g.shape
+    dev = g.device
+    f = torch.float32
+    if db is None:
+        db = torch.empty(N, dtype=f, device=dev)
+    if out is not None and gp is None:
+        gp = torch.empty_like(g)
+    ws = _relu_bias_ws(R, N, dev)
+    call("ocppo_relu_bias_grad", _stream(dev), _check(g, "g", f, dev),
+         _opt(out, "out", f, dev, R * N), _opt(gp, "gp", f, dev, R * N),
+         _check(db, "db", f, dev, N), R, N, ws.data_ptr(), ws.numel())
+    return (gp if out is not None else g), db
+
+
+# ---------------------------------------------------------------------------------------------
 # Frame-deduplicated PPObj minibatch encoder (ppo_atari_oc.py:566 through architectures/ppo.py:60-84)
 # ---------------------------------------------------------------------------------------------
 def _obs_TNWF(obs):

@@ -710,3 +710,49 @@ def test_gather_rows_channels_last(ops, dev, src_dt, B, shape, M):
     ops.gather_rows(T(src, dev).to(STORE_DT[src_dt]), T(idx, dev), out)
     assert out.is_contiguous(memory_format=torch.channels_last)
     assert np.array_equal(out.cpu().numpy(), src[idx])
+
+
+# ---------------------------------------------------------------------------------------------
+# fused ReLU backward + bias gradient (autograd of Linear -> ReLU inside loss.backward())
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("R,N", [(12288, 1024), (4096, 512), (12288, 256), (7, 4), (33, 260),
+                                 (100000, 12), (1, 16384)])
+@pytest.mark.parametrize("relu", [True, False])
+def test_relu_bias_grad_vs_torch(ops, dev, R, N, relu):
+    g = torch.randn(R, N, device=dev)
+    out = torch.relu(torch.randn(R, N, device=dev)) if relu else None
+    if relu:
+        out[::3, ::5] = 0.0  # exact zeros: threshold_backward's `<= 0` boundary
+    gp, db = ops.relu_bias_grad(g, out)
+    want = torch.ops.aten.threshold_backward(g, out, 0) if relu else g
+    assert torch.equal(gp, want)
+    ref = want.double().sum(0)
+    scale = want.double().abs().sum(0).clamp_min(1e-30)
+    assert ((db.double() - ref).abs() / scale).max().item() < 1e-6
+    gp2, db2 = ops.relu_bias_grad(g, out)  # deterministic; tickets re-armed
+    assert torch.equal(db, db2) and torch.equal(gp, gp2)
+
+
+def test_relu_bias_grad_graph_replay(ops, dev):
+    g = torch.randn(3000, 512, device=dev)
+    out = torch.relu(torch.randn(3000, 512, device=dev))
+    gp = torch.empty_like(g)
+    db = torch.empty(512, device=dev)
+    ops.relu_bias_grad(g, out, db=db, gp=gp)
+    ref = db.clone()
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        ops.relu_bias_grad(g, out, db=db, gp=gp)
+    db.zero_()
+    for _ in range(3):
+        graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(db, ref)
+
+
+def test_relu_bias_grad_rejects_bad_shapes(ops, dev):
+    from oc_cleanrl_amd._lib import OcppoError
+
+    with pytest.raises(OcppoError, match="bad sizes"):
+        ops.relu_bias_grad(torch.randn(8, 6, device=dev))
