@@ -35,9 +35,9 @@ sys.path.insert(0, str(ROOT))
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
 # HBM bytes per launch from rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE, separate passes) of
 # the same launch shapes: tools/profile_round.sh -> tools/summarize_profiles.py
-PMC_SUMMARY = ROOT / "profiles" / "r01b" / "pmc_summary.json"
+PMC_SUMMARY = ROOT / "profiles" / "r01c" / "pmc_summary.json"
 PMC_KEYS = {"action_head": "policy_head_config", "gae": "gae_config",
-            "ppo_loss": "ppo_loss_prepared_config"}
+            "ppo_loss": "ppo_loss_prepared_config", "relu_bias_grad": "relu_bias_grad_config"}
 
 
 def pmc_traffic(key):
@@ -54,7 +54,7 @@ def kernel_bytes(tr) -> dict:
     W, D = tr.obs_shape[0], int(torch.tensor(tr.obs_shape[1:]).prod())
     sb = tr.obs.element_size()
     fb = tr.env.frame.element_size()
-    return {
+    kb = {
         # read r, v, d [T,N] + next v/d [N]; write adv, ret [T,N]
         "gae": 20 * T * N + 8 * N,
         # logits 4A + value 4 + action 8 + old logprob/adv/return/value 16 in (contiguous,
@@ -76,6 +76,24 @@ def kernel_bytes(tr) -> dict:
         "frame_cache": (N * (4 + 4 * tr.enc_cache.shape[2] * (2 * tr.enc_cache.shape[1]))
                         if tr.enc_cache is not None else None),
     }
+    if tr.frame_dedup:
+        C, E = tr.planner.cap, tr.agent.encoding_dim
+        F = D
+        # frame id 4 + f32 row out (storage-dtype row in)
+        kb["frames_gather"] = C * (4 + F * (sb + 4))
+        # perm 8 + W x (dones 4 + pos_of 4) per sample; W encoded rows in, W rows out
+        kb["frames_expand"] = M * (8 + 8 * W + 8 * W * E)
+        # dh rows in, one row out per distinct frame
+        kb["frames_scatter"] = 4 * M * W * E + C * (4 + 4 * E)
+    return kb
+
+
+def relu_bias_grad_bytes(name: str):
+    """relu_bias_grad_{R}x{N}[_norelu]: g (+ out in, gp out) f32 [R, N] + db [N] out."""
+    spec = name[len("relu_bias_grad_"):]
+    relu = not spec.endswith("_norelu")
+    R, N = (int(v) for v in spec.replace("_norelu", "").split("x"))
+    return R * N * (12 if relu else 4) + 4 * N
 
 
 def main():
@@ -155,11 +173,25 @@ def main():
     if not opt.no_kernel_timing:
         for name, us in tr.timer.measure().items():
             n = tr.timer.per_iter.get(name, 0)
-            nbytes = kb.get(name)
+            nbytes = kb.get(name) or (relu_bias_grad_bytes(name)
+                                      if name.startswith("relu_bias_grad_") else None)
             kernels[name] = {"mean_us": round(us, 3), "launches_per_iter": n,
                              "us_per_iter": round(us * n, 2)}
             if nbytes:
                 kernels[name].update(bytes=nbytes, GBps=round(nbytes / (us * 1e-6) / 1e9, 2))
+    # one kernel, several launch shapes per minibatch: aggregate them (average bytes per launch
+    # over average launch duration = total bytes / total time)
+    parts = [k for k in kernels if k.startswith("relu_bias_grad_") and "bytes" in kernels[k]]
+    if parts:
+        n = sum(kernels[k]["launches_per_iter"] for k in parts)
+        t = sum(kernels[k]["us_per_iter"] for k in parts)
+        b = sum(kernels[k]["bytes"] * kernels[k]["launches_per_iter"] for k in parts)
+        kernels["relu_bias_grad"] = {"mean_us": round(t / n, 3), "launches_per_iter": n,
+                                     "us_per_iter": round(t, 2), "bytes": round(b / n),
+                                     "GBps": round(b / (t * 1e-6) / 1e9, 2),
+                                     "shapes": sorted(k[len("relu_bias_grad_"):] for k in parts)}
+        for k in parts:
+            kernels[k].pop("GBps", None)  # counted in the aggregate
     timed = [k for k in kernels if "GBps" in kernels[k]]
     dom = max(timed, key=lambda k: kernels[k]["us_per_iter"]) if timed else None
     roofline = None
@@ -168,7 +200,7 @@ def main():
         traffic, src = pmc_traffic(PMC_KEYS.get(dom, ""))
         roofline = {"kernel": dom, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5),
-                    "traffic": traffic, "traffic_source": src, "bytes_per_launch": kb[dom],
+                    "traffic": traffic, "traffic_source": src, "bytes_per_launch": kernels[dom]["bytes"],
                     "mean_launch_us": kernels[dom]["mean_us"]}
 
     scaled = None
@@ -176,7 +208,7 @@ def main():
         from tools.kernel_bench import run_case
 
         scaled = {}
-        for name in ("gae", "ppo_loss_prepared", "policy_head"):
+        for name in ("gae", "ppo_loss_prepared", "policy_head", "relu_bias_grad"):
             r = run_case(name, "scaled", device, reps=10, rounds=5)
             traffic, _ = pmc_traffic(f"{name}_scaled")
             scaled[name] = {"params": r["params"], "mean_us": r["mean_us"], "bytes": r["bytes"],

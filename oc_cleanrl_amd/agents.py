@@ -108,7 +108,10 @@ class _LinearAct(torch.autograd.Function):
         if FUSED_RELU_BIAS_GRAD and ctx.needs_input_grad[2] and _direct(ctx.b) and \
                 ops.relu_bias_grad_ok(g):
             # threshold_backward + bias sum in one HIP pass, bias grad written in place
-            gp, _ = ops.relu_bias_grad(g, out if ctx.relu else None, db=ctx.b.grad)
+            o, db_out = out if ctx.relu else None, ctx.b.grad
+            gp, _ = ops.timed(f"relu_bias_grad_{g.shape[0]}x{g.shape[1]}" +
+                              ("" if ctx.relu else "_norelu"),
+                              lambda: ops.relu_bias_grad(g, o, db=db_out))
             bias_done = True
         else:
             gp = torch.ops.aten.threshold_backward(g, out, 0) if ctx.relu else g

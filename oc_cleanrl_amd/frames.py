@@ -111,13 +111,16 @@ class _FramesExpand(torch.autograd.Function):
     def forward(ctx, enc, pos_of, perm, dones, uniq, inv, mb, T, N, W):
         ctx.save_for_backward(uniq, inv, dones)
         ctx.geom = (int(mb), T, N, W, perm.numel())
-        return ops.frames_expand(enc, pos_of, perm, dones, T, N, W)
+        return ops.timed("frames_expand", lambda: ops.frames_expand(enc, pos_of, perm, dones,
+                                                                    T, N, W))
 
     @staticmethod
     def backward(ctx, dh):
         uniq, inv, dones = ctx.saved_tensors
         mb, T, N, W, M = ctx.geom
-        denc = ops.frames_scatter(dh.contiguous().view(M, W, -1), uniq, inv, mb, dones, T, N, W)
+        dh = dh.contiguous().view(M, W, -1)
+        denc = ops.timed("frames_scatter", lambda: ops.frames_scatter(dh, uniq, inv, mb, dones,
+                                                                      T, N, W))
         return denc, None, None, None, None, None, None, None, None, None
 
 
@@ -127,7 +130,7 @@ def minibatch_hidden(agent, obs, dones, uniq, pos_of, inv, perm, mb: int):
     `mb` is the minibatch's index within its epoch (inv is that epoch's inverse permutation)."""
     T1, N, W, _ = obs.shape
     T = T1 - 1
-    x = ops.frames_gather(obs, uniq)
+    x = ops.timed("frames_gather", lambda: ops.frames_gather(obs, uniq))
     enc = agent.encode(x)
     h = _FramesExpand.apply(enc.contiguous(), pos_of, perm, dones, uniq, inv, mb, T, N, W)
     return agent.decode(h)

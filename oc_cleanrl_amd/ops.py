@@ -54,6 +54,15 @@ def _net_obs(net_obs, N: int, W: int, D: int, device):
     raise ValueError("net_obs must be contiguous [N, W, ...] or channels_last [N, W, H, X]")
 
 
+# Optional per-launch timer for launch sites inside autograd (the trainer's KernelTimer when
+# kernel timing is on): timed(name, fn) runs fn and lets the timer keep its first eager launch.
+TIMER = None
+
+
+def timed(name: str, fn):
+    return TIMER.bracket(name, fn) if TIMER is not None else fn()
+
+
 def _stream(device: torch.device) -> int:
     if device.type != "cuda":
         raise ValueError(f"HIP kernels need GPU tensors, got device {device} (no CPU fallback)")

@@ -249,6 +249,8 @@ class PPOTrainer:
         # is noise anyway); the rollout is still captured.
         self.graph_update = a.cuda_graphs and not self.pixels
         self.timer = KernelTimer(kernel_timing)
+        if kernel_timing:
+            ops.TIMER = self.timer  # launch sites inside autograd (relu_bias_grad, frames_*)
         self.graphs_ready = False
         self.g_rollout = None
         self.g_update: list = []

@@ -38,7 +38,17 @@ SIZES = {
     "mb_prepare": {"config": dict(M=4096, nmb=16, B=16384), "scaled": dict(M=16384, nmb=256, B=1 << 20)},
     "ppo_loss_prepared": {"config": dict(M=4096, A=6), "scaled": dict(M=4 * 1024 * 1024, A=6)},
     "policy_head": {"config": dict(N=128, H=512, A=6), "scaled": dict(N=262144, H=512, A=6)},
+    # the five Linear->ReLU backward launches of one config-2 minibatch (dedup capacity 12288
+    # encoder rows: layers 256/512/1024/512, decoder 4096 x 512), and one streaming-size launch
+    "relu_bias_grad": {"config": dict(shapes=((4096, 512), (12288, 512), (12288, 1024),
+                                              (12288, 512), (12288, 256))),
+                       "scaled": dict(shapes=((262144, 1024),))},
 }
+
+
+def relu_bias_grad_bytes(shapes):
+    """g + out in, gp out (f32 [R, N]) + db out, summed over the launches."""
+    return sum(R * N * 12 + 4 * N for R, N in shapes)
 
 
 def make_case(name: str, p: dict, dev):
@@ -141,6 +151,17 @@ def make_case(name: str, p: dict, dev):
         vo = torch.empty(N, device=dev)
         fn = lambda: ops.policy_head_sample(hid, wa, ba, wc, bc, noise, act, lp, vo)  # noqa: E731
         return fn, N * (4 * H + 4 * A + 16) + 4 * (A + 1) * (H + 1)
+    if name == "relu_bias_grad":
+        bufs = []
+        for R, N in p["shapes"]:
+            gg = torch.randn(R, N, device=dev, generator=g)
+            out = torch.relu(torch.randn(R, N, device=dev, generator=g))
+            bufs.append((gg, out, torch.empty_like(gg), torch.empty(N, device=dev)))
+
+        def fn():
+            for gg, out, gp, db in bufs:
+                ops.relu_bias_grad(gg, out, db=db, gp=gp)
+        return fn, relu_bias_grad_bytes(p["shapes"])
     raise KeyError(name)
 
 
@@ -164,6 +185,8 @@ def time_case(fn, reps=20, rounds=5) -> float:
 def run_case(name, size, dev, reps=20, rounds=5) -> dict:
     fn, nbytes = make_case(name, SIZES[name][size], dev)
     us = time_case(fn, reps, rounds)
+    launches = len(SIZES[name][size].get("shapes", (None,)))
+    us, nbytes = us / launches, nbytes / launches  # per launch (average over the launch mix)
     gbs = nbytes / (us * 1e-6) / 1e9
     return {"kernel": name, "size": size, "params": SIZES[name][size], "mean_us": round(us, 3),
             "bytes": nbytes, "GBps": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}

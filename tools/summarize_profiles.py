@@ -21,9 +21,10 @@ from tools.kernel_bench import SIZES, make_case  # noqa: E402,F401
 KERNEL_SUBSTR = {
     "policy_head": "policy_head_fast_kernel",
     "gae": "gae_kernel",
-    "ppo_loss_prepared": "ppo_loss_kernel",
+    "ppo_loss_prepared": "ocppo::ppo_loss",  # _small / _vec / tile forms by size
     "rollout_store": "rollout_store_kernel",
     "gather": "gather_rows_kernel",
+    "relu_bias_grad": "relu_bias_grad_kernel",
 }
 
 
@@ -40,6 +41,8 @@ def algorithmic_bytes(name, size):
         return p["N"] * ((p["W"] - 1) * p["D"] * 2 + p["D"] * 4 + p["W"] * p["D"] * 6 + 16)
     if name == "gather":
         return p["M"] * (8 + p["R"] * 6)
+    if name == "relu_bias_grad":  # average over the launch mix
+        return sum(R * N * 12 + 4 * N for R, N in p["shapes"]) / len(p["shapes"])
     return None
 
 
