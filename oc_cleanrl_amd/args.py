@@ -119,6 +119,7 @@ class Args:
     rollout_frame_cache: bool = True  # PPO_OBJ rollout: encode only the newest frame per step
     update_frame_dedup: bool = True  # PPO_OBJ update: encode each distinct frame of a minibatch once
     prefetch_shuffle: bool = True  # shuffle (+ frame plan) of the next iteration while the GPU runs
+    dp_overlap: bool = True  # DP: all-reduce the decoder-side gradients during the encoder backward
     conv_channels_last: bool = True  # pixel NatureCNN in NHWC (MIOpen NHWC kernels, no transposes)
     conv_benchmark: bool = False  # cudnn.benchmark (MIOpen Find) for the NatureCNN convolutions
 

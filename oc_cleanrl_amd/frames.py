@@ -124,13 +124,29 @@ class _FramesExpand(torch.autograd.Function):
         return denc, None, None, None, None, None, None, None, None, None
 
 
-def minibatch_hidden(agent, obs, dones, uniq, pos_of, inv, perm, mb: int):
+def minibatch_hidden(agent, obs, dones, uniq, pos_of, inv, perm, mb: int, split: int = 0):
     """Decoder output of PPObj for the samples `perm` (one minibatch) from the rollout obs
     [T+1, N, W, F] with each distinct frame encoded once; autograd flows to every parameter.
-    `mb` is the minibatch's index within its epoch (inv is that epoch's inverse permutation)."""
+    `mb` is the minibatch's index within its epoch (inv is that epoch's inverse permutation).
+
+    split > 0 cuts the autograd graph after agent.network[:split] (a prefix of the encoder) and
+    returns (hidden, (low, low_detached)): a backward from the heads then stops at
+    `low_detached`, and `torch.autograd.backward(low, low_detached.grad)` finishes it -- two
+    phases, so the data-parallel trainer can all-reduce the gradients of the layers above the
+    cut while the layers below it still run their backward."""
+    from .agents import fused_trunk
+
     T1, N, W, _ = obs.shape
     T = T1 - 1
     x = ops.timed("frames_gather", lambda: ops.frames_gather(obs, uniq))
-    enc = agent.encode(x)
+    cut = None
+    if split:
+        low = fused_trunk(agent.network[:split], x)
+        low_d = low.detach().requires_grad_()
+        enc = fused_trunk(agent.network[split:agent._flat], low_d)
+        cut = (low, low_d)
+    else:
+        enc = agent.encode(x)
     h = _FramesExpand.apply(enc.contiguous(), pos_of, perm, dones, uniq, inv, mb, T, N, W)
-    return agent.decode(h)
+    hidden = agent.decode(h)
+    return (hidden, cut) if split else hidden

@@ -7,9 +7,11 @@ One PPO iteration on one GPU (rank):
                    actions/logprobs/values rows) → HIP env step → HIP VecNormalize → HIP store
                    (frame stack + bf16/u8 rollout slot + f32 network input + reward/done rows)]
                    → bootstrap value → HIP GAE → HIP minibatch advantage stats
-  update graph(s): per minibatch: HIP obs gather → agent fwd → HIP fused loss fwd+bwd (dlogits,
-                   dvalue) → autograd backward of the network into a flat grad buffer →
-                   [RCCL all-reduce SUM of the flat buffer, / world] → clip_grad_norm_ → Adam
+  update graph(s): per minibatch: HIP obs gather (PPObj: distinct frames only) → agent fwd →
+                   HIP fused loss fwd+bwd (dlogits, dvalue) → autograd backward of the network
+                   into a flat grad buffer → [RCCL all-reduce SUM of the flat buffer, / world;
+                   PPObj: the decoder-side tail is reduced while the lower encoder layers run
+                   their backward] → clip_grad_norm_ → Adam
 One host sync per iteration (metrics), none per step or per minibatch.
 
 Storage layout (step-major like the reference, :452-459): obs [T+1, N, W, ...] in the rollout
@@ -230,6 +232,16 @@ class PPOTrainer:
         self.planner = (frames.FramePlanner(T, N, W, a.local_minibatch_size, a.update_epochs,
                                             a.num_minibatches) if self.frame_dedup else None)
         self.plan_host = self.plan_stage = self.plan_dev = self.plan = None
+        # DP: cut the backward before the last encoder layer, so the all-reduce of the flat
+        # buffer's tail (last encoder layer + decoder + heads, ~70 % of the bytes for PPObj)
+        # overlaps the backward of the layers below (_exchange)
+        self.split, self.tail_off, self.cuts = 0, 0, {}
+        if world_size > 1 and a.dp_overlap and self.frame_dedup and len(a.encoder_dims) >= 2:
+            self.split = 2 * (len(a.encoder_dims) - 1)  # network[:split] = the layers below
+            first_tail = self.agent.network[self.split].weight
+            offs, _ = ops.flat_offsets(self.params)
+            self.tail_off = next(o for p, o in zip(self.params, offs) if p is first_tail)
+            assert self.grad_buf[self.tail_off:].data_ptr() == first_tail.grad.data_ptr()
         nmbt = self.E * self.nmb
         self.mb = {"actions": torch.zeros(nmbt * self.M, dtype=torch.int64, device=dev),
                    **{k: torch.zeros(nmbt * self.M, dtype=f32, device=dev)
@@ -254,6 +266,7 @@ class PPOTrainer:
         self.graphs_ready = False
         self.g_rollout = None
         self.g_update: list = []
+        self.g_low: list = []
         self.g_opt = None
         self.iteration = 0
         self.global_step = 0
@@ -341,7 +354,9 @@ class PPOTrainer:
             e, k = divmod(j, self.nmb)
             uniq, pos_of, inv = self.plan
             hidden = frames.minibatch_hidden(ag, self.obs, self.dones, uniq[j], pos_of[j], inv[e],
-                                             idx, k)
+                                             idx, k, split=self.split)
+            if self.split:
+                hidden, self.cuts[j] = hidden
             logits, value = ag._head(ag.actor, hidden), ag._head(ag.critic, hidden)
         else:
             self.timer.bracket("gather", lambda: ops.gather_rows(self.b_obs, idx, self.mb_obs))
@@ -360,10 +375,36 @@ class PPOTrainer:
             self.grad_buf.zero_()
         torch.autograd.backward([logits, value], [self.dlogits, self.dvalue.view(-1, 1)])
 
+    def _backward_low(self, j: int):
+        """Second backward phase of a split minibatch: the encoder layers below the cut."""
+        # popped: a cut kept alive past its backward would keep the autograd graph (and its
+        # AccumulateGrad nodes, bound to the stream they were created on) alive into the next
+        # capture, which then syncs with that stream and breaks
+        low, low_d = self.cuts.pop(j)
+        torch.autograd.backward(low, low_d.grad)
+
     def _allreduce(self):
         """DP exchange (ppo_atari_multigpu.py:360-374): ONE in-place RCCL all-reduce of the flat
         grad buffer; the `/ world_size` is folded into the optimizer step (grad_scale)."""
         dist.all_reduce(self.grad_buf, op=dist.ReduceOp.SUM)
+        if not self.args.fused_optimizer:
+            self.grad_buf.div_(self.world)
+
+    def _exchange(self, j: int, replay: bool):
+        """Minibatch j's gradients, all-reduced. Split form: the first backward phase has filled
+        the flat buffer's tail (the last encoder layer, decoder and heads); its all-reduce runs on
+        RCCL's stream while the second phase (the encoder layers below the cut) runs on ours,
+        then the head of the buffer follows. Same SUM of the same bytes as _allreduce."""
+        if not self.split:
+            self._allreduce()
+            return
+        work = dist.all_reduce(self.grad_buf[self.tail_off:], op=dist.ReduceOp.SUM, async_op=True)
+        if replay:
+            self.g_low[j].replay()
+        else:
+            self._backward_low(j)
+        dist.all_reduce(self.grad_buf[:self.tail_off], op=dist.ReduceOp.SUM)
+        work.wait()
         if not self.args.fused_optimizer:
             self.grad_buf.div_(self.world)
 
@@ -376,9 +417,10 @@ class PPOTrainer:
 
     def _update_epoch(self, epoch: int):
         for k in range(self.nmb):
-            self._forward_backward(epoch * self.nmb + k)
+            j = epoch * self.nmb + k
+            self._forward_backward(j)
             if self.world > 1:
-                self._allreduce()
+                self._exchange(j, replay=False)
             self._opt_step()
 
     # ------------------------------------------------------------------------------------------
@@ -408,7 +450,7 @@ class PPOTrainer:
         if self.plan_dev is not None:
             torch.cuda.synchronize(self.dev)
             self.graphs_ready = False
-            self.g_rollout, self.g_update, self.g_opt = None, [], None
+            self.g_rollout, self.g_update, self.g_opt, self.g_low = None, [], None, []
         self.planner.cap = cap
         n = self.planner.size(cap)
         self.plan_host = torch.empty(n, dtype=torch.int32, pin_memory=True)
@@ -447,6 +489,11 @@ class PPOTrainer:
                 with torch.cuda.graph(g, pool=pool):
                     self._forward_backward(j)
                 self.g_update.append(g)
+                if self.split:  # second backward phase: reads the cut tensors of graph j
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, pool=pool):
+                        self._backward_low(j)
+                    self.g_low.append(g)
             self.g_opt = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.g_opt, pool=pool):
                 self._opt_step()
@@ -460,8 +507,9 @@ class PPOTrainer:
                     self.g_update[e].replay()
                 else:
                     for k in range(self.nmb):
-                        self.g_update[e * self.nmb + k].replay()
-                        self._allreduce()
+                        j = e * self.nmb + k
+                        self.g_update[j].replay()
+                        self._exchange(j, replay=True)
                         self.g_opt.replay()
             else:
                 self._update_epoch(e)

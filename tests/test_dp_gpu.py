@@ -19,7 +19,7 @@ def _port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out, fused_opt, graphs):
+def _worker(rank, world, port, out, fused_opt, graphs, overlap=True):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from oc_cleanrl_amd.args import Args, finalize
@@ -29,8 +29,9 @@ def _worker(rank, world, port, out, fused_opt, graphs):
                          num_envs=16 * world, num_steps=16, num_minibatches=2, update_epochs=2,
                          total_timesteps=16 * world * 16 * 10, encoder_dims=(32, 64),
                          decoder_dims=(64,), save_model=False, fused_optimizer=fused_opt,
-                         cuda_graphs=graphs), world)
+                         cuda_graphs=graphs, dp_overlap=overlap), world)
     tr = PPOTrainer(args, torch.device("cuda:0"), rank, world)
+    assert bool(tr.split) == overlap
     for _ in range(3):
         tr.train_iteration()
     torch.cuda.synchronize()
@@ -49,3 +50,16 @@ def test_two_ranks_share_one_gpu_over_gloo(fused_opt, graphs):
     assert torch.equal(p0, p1), "DP replicas diverged"
     assert not torch.equal(a0, a1), "ranks must roll out different env shards"
 
+
+
+@pytest.mark.parametrize("graphs", [True, False])
+def test_overlapped_exchange_equals_single_allreduce(graphs):
+    """dp_overlap (tail all-reduce during the lower layers' backward, then the head) gives the
+    same parameters, bit for bit, as one all-reduce of the whole flat buffer."""
+    res = []
+    for overlap in (False, True):
+        mgr = mp.Manager()
+        out = mgr.dict()
+        mp.spawn(_worker, args=(2, _port(), out, True, graphs, overlap), nprocs=2, join=True)
+        res.append(out[0][0])
+    assert torch.equal(res[0], res[1])
