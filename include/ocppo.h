@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define OCPPO_ABI_VERSION 2
+#define OCPPO_ABI_VERSION 3
 
 /* status codes */
 #define OCPPO_OK 0
@@ -41,6 +41,10 @@ extern "C" {
 #define OCPPO_F32 0
 #define OCPPO_BF16 1
 #define OCPPO_U8 2
+
+/* net_flags of the rollout store / reset / channels-last gather */
+#define OCPPO_NET_CHANNELS_LAST 1
+#define OCPPO_NET_SCALE_255 2
 
 /* layout of the `stats` output of ocppo_ppo_loss_fwd_bwd (all f32) */
 #define OCPPO_STAT_LOSS 0          /* loss = pg - ent_coef*entropy + vf_coef*v_loss   :599-602 */
@@ -207,9 +211,12 @@ OCPPO_API int ocppo_categorical_logprob_entropy_bwd(ocppo_stream_t stream, const
  *   obs_out    : [N, W, D] new stacked obs, dtype obs_dtype (rollout slot t+1)
  *   net_obs    : f32 copy of obs_out for the network forward (may be NULL when net_layout = 0)
  *   reward_out : [N] f32 (&rewards[t*N]);  done_out : [N] f32 (&dones[(t+1)*N]); either may be NULL
- *   net_layout : 0 = net_obs [N, W, D] like obs_out; 1 = channels-last [N, D, W] (the NHWC input
- *                of a channels_last NatureCNN, 16-B aligned; MIOpen's NHWC convolutions then
- *                need no transpose)
+ *   net_flags  : bit 0 (OCPPO_NET_CHANNELS_LAST): net_obs in channels-last order [N, D, W] (the
+ *                NHWC input of a channels_last NatureCNN, 16-B aligned; MIOpen's NHWC
+ *                convolutions then need no transpose), else [N, W, D] like obs_out;
+ *                bit 1 (OCPPO_NET_SCALE_255): net_obs = value / 255 as ATen computes it
+ *                (x * (1.0f / 255.0f)) -- the NatureCNN's NormalizeImg (architectures/common.py:19-22)
+ *                folded into the store
  * Stacking: obs_out[n] = prev_obs[n][1:] ++ frame[n]; on done[n] every slot is frame[n] (the
  * gymnasium FrameStack reset fill). Conversion to bf16 is round-to-nearest-even and exact for
  * the integer-valued obs of both modes (|x| <= 256).
@@ -217,13 +224,13 @@ OCPPO_API int ocppo_categorical_logprob_entropy_bwd(ocppo_stream_t stream, const
 OCPPO_API int ocppo_rollout_store(ocppo_stream_t stream, const void* frame, int frame_dtype,
                         const float* reward, const float* done, int64_t N, int64_t W, int64_t D,
                         const void* prev_obs, void* obs_out, int obs_dtype, float* net_obs,
-                        float* reward_out, float* done_out, int net_layout);
+                        float* reward_out, float* done_out, int net_flags);
 
 /* Fill a whole stacked-obs slot from one frame per env (env reset, ppo_atari_oc.py:464-465);
- * net_layout as in ocppo_rollout_store. */
+ * net_flags as in ocppo_rollout_store. */
 OCPPO_API int ocppo_obs_reset(ocppo_stream_t stream, const void* frame, int frame_dtype, int64_t N,
                     int64_t W, int64_t D, void* obs_out, int obs_dtype, float* net_obs,
-                    int net_layout);
+                    int net_flags);
 
 /* ---------------------------------------------------------------------------------------------
  * Frame-encoding cache of the rollout forward (PPObj, architectures/ppo.py:60-84, whose encoder
@@ -299,10 +306,12 @@ OCPPO_API int ocppo_gather_rows(ocppo_stream_t stream, const void* src, int src_
                       int64_t M, int64_t R, float* dst);
 
 /* The same gather into channels-last rows (the NHWC input of a channels_last NatureCNN):
- *   dst[i, p, c] = f32(src[idx[i], c, p]),  src [B, C, P] (C stacked frames of P pixels),
- *   dst [M, P, C] f32, 16-B aligned. */
+ *   dst[i, p, c] = f32(src[idx[i], c, p]) (/ 255 with OCPPO_NET_SCALE_255 in net_flags, as in
+ *   ocppo_rollout_store),  src [B, C, P] (C stacked frames of P pixels), dst [M, P, C] f32,
+ *   16-B aligned. */
 OCPPO_API int ocppo_gather_rows_cl(ocppo_stream_t stream, const void* src, int src_dtype,
-                         const int64_t* idx, int64_t M, int64_t C, int64_t P, float* dst);
+                         const int64_t* idx, int64_t M, int64_t C, int64_t P, float* dst,
+                         int net_flags);
 
 /* ---------------------------------------------------------------------------------------------
  * Reward normalisation of SB3 VecNormalize(norm_obs=False, norm_reward=True) as wrapped at
@@ -324,7 +333,7 @@ OCPPO_API int ocppo_rollout_store_vecnorm(ocppo_stream_t stream, const void* fra
                                           int64_t W, int64_t D, const void* prev_obs, void* obs_out,
                                           int obs_dtype, float* net_obs, float* done_out,
                                           double gamma, double epsilon, double clip_reward,
-                                          double* ret_state, double* rms_state, float* reward_out, int net_layout);
+                                          double* ret_state, double* rms_state, float* reward_out, int net_flags);
 
 /* ---------------------------------------------------------------------------------------------
  * DQN (config 5, dqn_atari_oc.py) — HBM replay buffer with stable-baselines3 2.0.0

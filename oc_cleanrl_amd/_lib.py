@@ -22,7 +22,7 @@ LIB_PATH = Path(os.environ.get("OCPPO_LIB", PKG / "lib" / "libocppo_hip.so"))
 HEADER = PKG.parent / "include" / "ocppo.h"
 
 # constants mirrored from include/ocppo.h (checked against the header by tests/test_abi.py)
-OCPPO_ABI_VERSION = 2
+OCPPO_ABI_VERSION = 3
 OCPPO_OK, OCPPO_E_INVALID, OCPPO_E_LAUNCH, OCPPO_E_WORKSPACE = 0, 1, 2, 3
 OCPPO_F32, OCPPO_BF16, OCPPO_U8 = 0, 1, 2
 STAT_NAMES = ("loss", "pg_loss", "v_loss", "entropy", "old_approx_kl", "approx_kl", "clipfrac",
@@ -50,7 +50,7 @@ SIGNATURES: dict[str, tuple[type, list]] = {
     "ocppo_rollout_store": (I, [P, P, I, P, P, I64, I64, I64, P, P, I, P, P, P, I]),
     "ocppo_obs_reset": (I, [P, P, I, I64, I64, I64, P, I, P, I]),
     "ocppo_gather_rows": (I, [P, P, I, P, I64, I64, P]),
-    "ocppo_gather_rows_cl": (I, [P, P, I, P, I64, I64, I64, P]),
+    "ocppo_gather_rows_cl": (I, [P, P, I, P, I64, I64, I64, P, I]),
     "ocppo_frame_cache_shift": (I, [P, P, P, I64, P, I64, I64, I64]),
     "ocppo_linear_act": (I, [P, P, I64, P, P, P, I64, I64, I64, I64, I]),
     "ocppo_relu_bias_grad_workspace_bytes": (SZ, [I64, I64]),

@@ -187,9 +187,15 @@ def fused_trunk(seq: nn.Sequential, x):
 class _ActorCritic(Predictor):
     """Shared interface: network → (actor logits, critic value)."""
 
-    def trunk(self, x):
-        return fused_trunk(self.network, x) if isinstance(self.network, nn.Sequential) \
-            else self.network(x)
+    def trunk(self, x, prescaled: bool = False):
+        """Shared network output. prescaled: x already holds obs / 255 (the HIP store / gather
+        fold NormalizeImg in, bit-identical to it), so a leading NormalizeImg is skipped."""
+        net = self.network
+        if not isinstance(net, nn.Sequential):
+            return net(x)
+        if prescaled and len(net) and isinstance(net[0], NormalizeImg):
+            net = net[1:]
+        return fused_trunk(net, x)
 
     def _head(self, lin, h):
         if isinstance(lin, nn.Linear) and lin.bias is not None and h.is_cuda and \
@@ -197,11 +203,11 @@ class _ActorCritic(Predictor):
             return linear_act(h, lin, False)
         return lin(h)
 
-    def get_value(self, x):
-        return self._head(self.critic, self.trunk(x))
+    def get_value(self, x, prescaled: bool = False):
+        return self._head(self.critic, self.trunk(x, prescaled))
 
-    def logits_and_value(self, x):
-        hidden = self.trunk(x)
+    def logits_and_value(self, x, prescaled: bool = False):
+        hidden = self.trunk(x, prescaled)
         return self._head(self.actor, hidden), self._head(self.critic, hidden)
 
     def get_action_and_value(self, x, action=None):

@@ -19,7 +19,7 @@ __device__ __forceinline__ void store_groups(int64_t blk, int64_t nblk, const vo
                                              int64_t D, const void* __restrict__ prev,
                                              void* __restrict__ out, float* __restrict__ net,
                                              float* __restrict__ reward_out,
-                                             float* __restrict__ done_out) {
+                                             float* __restrict__ done_out, float net_scale) {
   const int64_t DG = D / VEC;
   const int64_t groups = N * W * DG;
   const int64_t stride = nblk * blockDim.x;
@@ -38,7 +38,7 @@ __device__ __forceinline__ void store_groups(int64_t blk, int64_t nblk, const vo
     if (net) {  // the network sees exactly what the rollout buffer holds
       float back[VEC];
 #pragma unroll
-      for (int q = 0; q < VEC; ++q) back[q] = Elem<ODT>::roundtrip(v[q]);
+      for (int q = 0; q < VEC; ++q) back[q] = Elem<ODT>::roundtrip(v[q]) * net_scale;
       VecIO<OCPPO_F32, VEC>::store(net, o, back);
     }
     if (g < N) {
@@ -60,7 +60,7 @@ __device__ __forceinline__ void store_groups_cl(int64_t blk, int64_t nblk,
                                                 int64_t D, const void* __restrict__ prev,
                                                 void* __restrict__ out, float* __restrict__ net,
                                                 float* __restrict__ reward_out,
-                                                float* __restrict__ done_out) {
+                                                float* __restrict__ done_out, float net_scale) {
   const int64_t DG = D / VEC;
   const int64_t groups = N * DG;
   const int64_t stride = nblk * blockDim.x;
@@ -81,8 +81,10 @@ __device__ __forceinline__ void store_groups_cl(int64_t blk, int64_t nblk,
       }
 #pragma unroll
       for (int q = 0; q < VEC; ++q) {
-        float px[4] = {Elem<ODT>::roundtrip(v[0][q]), Elem<ODT>::roundtrip(v[1][q]),
-                       Elem<ODT>::roundtrip(v[2][q]), Elem<ODT>::roundtrip(v[3][q])};
+        float px[4] = {Elem<ODT>::roundtrip(v[0][q]) * net_scale,
+                       Elem<ODT>::roundtrip(v[1][q]) * net_scale,
+                       Elem<ODT>::roundtrip(v[2][q]) * net_scale,
+                       Elem<ODT>::roundtrip(v[3][q]) * net_scale};
         VecIO<OCPPO_F32, 4>::store(dst, 4 * q, px);  // net is 16-B aligned (host check)
       }
     } else {
@@ -94,7 +96,7 @@ __device__ __forceinline__ void store_groups_cl(int64_t blk, int64_t nblk,
           VecIO<ODT, VEC>::load(prev, (n * W + w + 1) * D + k, v);
         VecIO<ODT, VEC>::store(out, (n * W + w) * D + k, v);
 #pragma unroll
-        for (int q = 0; q < VEC; ++q) dst[q * W + w] = Elem<ODT>::roundtrip(v[q]);
+        for (int q = 0; q < VEC; ++q) dst[q * W + w] = Elem<ODT>::roundtrip(v[q]) * net_scale;
       }
     }
     if (g < N) {
@@ -109,19 +111,19 @@ __global__ __launch_bounds__(256) void rollout_store_kernel(
     const void* __restrict__ frame, const float* __restrict__ reward,
     const float* __restrict__ done, int64_t N, int W, int64_t D, const void* __restrict__ prev,
     void* __restrict__ out, float* __restrict__ net, float* __restrict__ reward_out,
-    float* __restrict__ done_out) {
+    float* __restrict__ done_out, float net_scale) {
   if (CL)
     store_groups_cl<FDT, ODT, VEC>(blockIdx.x, gridDim.x, frame, reward, done, N, W, D, prev, out,
-                                   net, reward_out, done_out);
+                                   net, reward_out, done_out, net_scale);
   else
     store_groups<FDT, ODT, VEC>(blockIdx.x, gridDim.x, frame, reward, done, N, W, D, prev, out,
-                                net, reward_out, done_out);
+                                net, reward_out, done_out, net_scale);
 }
 
 template <int FDT, int ODT, int VEC, bool CL>
 __global__ __launch_bounds__(256) void obs_reset_kernel(const void* __restrict__ frame, int64_t N,
                                                         int W, int64_t D, void* __restrict__ out,
-                                                        float* __restrict__ net) {
+                                                        float* __restrict__ net, float net_scale) {
   const int64_t DG = D / VEC;
   const int64_t groups = N * W * DG;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
@@ -138,7 +140,7 @@ __global__ __launch_bounds__(256) void obs_reset_kernel(const void* __restrict__
     if (net) {
       float back[VEC];
 #pragma unroll
-      for (int q = 0; q < VEC; ++q) back[q] = Elem<ODT>::roundtrip(v[q]);
+      for (int q = 0; q < VEC; ++q) back[q] = Elem<ODT>::roundtrip(v[q]) * net_scale;
       if (CL) {
 #pragma unroll
         for (int q = 0; q < VEC; ++q) net[(n * D + k + q) * W + w] = back[q];
@@ -177,7 +179,8 @@ template <int SDT, int VEC>
 __global__ __launch_bounds__(256) void gather_rows_cl_kernel(const void* __restrict__ src,
                                                              const int64_t* __restrict__ idx,
                                                              int64_t M, int C, int64_t P,
-                                                             float* __restrict__ dst) {
+                                                             float* __restrict__ dst,
+                                                             float scale) {
   const int64_t PG = P / VEC;
   const int64_t groups = M * PG;
   const int64_t R = C * P;
@@ -194,7 +197,7 @@ __global__ __launch_bounds__(256) void gather_rows_cl_kernel(const void* __restr
       for (int c = 0; c < 4; ++c) VecIO<SDT, VEC>::load(src, row * R + c * P + k, v[c]);
 #pragma unroll
       for (int q = 0; q < VEC; ++q) {
-        float px[4] = {v[0][q], v[1][q], v[2][q], v[3][q]};
+        float px[4] = {v[0][q] * scale, v[1][q] * scale, v[2][q] * scale, v[3][q] * scale};
         VecIO<OCPPO_F32, 4>::store(out, 4 * q, px);  // dst is 16-B aligned (host check)
       }
     } else {
@@ -202,7 +205,7 @@ __global__ __launch_bounds__(256) void gather_rows_cl_kernel(const void* __restr
         float v[VEC];
         VecIO<SDT, VEC>::load(src, row * R + c * P + k, v);
 #pragma unroll
-        for (int q = 0; q < VEC; ++q) out[q * C + c] = v[q];
+        for (int q = 0; q < VEC; ++q) out[q * C + c] = v[q] * scale;
       }
     }
   }
@@ -274,17 +277,17 @@ __global__ __launch_bounds__(256) void store_vecnorm_kernel(
     const float* __restrict__ done, int64_t N, int W, int64_t D, const void* __restrict__ prev,
     void* __restrict__ out, float* __restrict__ net, float* __restrict__ done_out, double gamma,
     double eps, double clip, double* __restrict__ ret, double* __restrict__ rms,
-    float* __restrict__ reward_out) {
+    float* __restrict__ reward_out, float net_scale) {
   if (blockIdx.x == 0) {
     vecnorm_block(reward, done, N, gamma, eps, clip, ret, rms, reward_out);
     return;
   }
   if (CL)
     store_groups_cl<FDT, ODT, VEC>(blockIdx.x - 1, gridDim.x - 1, frame, reward, done, N, W, D,
-                                   prev, out, net, nullptr, done_out);
+                                   prev, out, net, nullptr, done_out, net_scale);
   else
     store_groups<FDT, ODT, VEC>(blockIdx.x - 1, gridDim.x - 1, frame, reward, done, N, W, D, prev,
-                                out, net, nullptr, done_out);
+                                out, net, nullptr, done_out, net_scale);
 }
 
 // ---- synthetic env ------------------------------------------------------------------------------
@@ -363,15 +366,15 @@ inline int64_t store_groups_count(int64_t N, int64_t W, int64_t D, int vec, bool
 template <int FDT, int ODT, bool CL>
 int launch_store(hipStream_t s, const void* frame, const float* reward, const float* done,
                  int64_t N, int64_t W, int64_t D, const void* prev, void* out, float* net,
-                 float* rout, float* dout) {
+                 float* rout, float* dout, float sc) {
   if (D % 4 == 0)
     hipLaunchKernelGGL((rollout_store_kernel<FDT, ODT, 4, CL>),
                        dim3(grid_for(store_groups_count(N, W, D, 4, CL), 256)), dim3(256), 0, s,
-                       frame, reward, done, N, (int)W, D, prev, out, net, rout, dout);
+                       frame, reward, done, N, (int)W, D, prev, out, net, rout, dout, sc);
   else
     hipLaunchKernelGGL((rollout_store_kernel<FDT, ODT, 1, CL>),
                        dim3(grid_for(store_groups_count(N, W, D, 1, CL), 256)), dim3(256), 0, s,
-                       frame, reward, done, N, (int)W, D, prev, out, net, rout, dout);
+                       frame, reward, done, N, (int)W, D, prev, out, net, rout, dout, sc);
   return check_launch("ocppo_rollout_store");
 }
 
@@ -380,6 +383,7 @@ struct VecNormArgs {
   double* ret;
   double* rms;
   float* reward_out;
+  float net_scale;
 };
 
 template <int FDT, int ODT, bool CL>
@@ -390,26 +394,26 @@ int launch_store_vecnorm(hipStream_t s, const void* frame, const float* reward, 
     hipLaunchKernelGGL((store_vecnorm_kernel<FDT, ODT, 4, CL>),
                        dim3(1 + grid_for(store_groups_count(N, W, D, 4, CL), 256)), dim3(256), 0,
                        s, frame, reward, done, N, (int)W, D, prev, out, net, dout, vn.gamma,
-                       vn.eps, vn.clip, vn.ret, vn.rms, vn.reward_out);
+                       vn.eps, vn.clip, vn.ret, vn.rms, vn.reward_out, vn.net_scale);
   else
     hipLaunchKernelGGL((store_vecnorm_kernel<FDT, ODT, 1, CL>),
                        dim3(1 + grid_for(store_groups_count(N, W, D, 1, CL), 256)), dim3(256), 0,
                        s, frame, reward, done, N, (int)W, D, prev, out, net, dout, vn.gamma,
-                       vn.eps, vn.clip, vn.ret, vn.rms, vn.reward_out);
+                       vn.eps, vn.clip, vn.ret, vn.rms, vn.reward_out, vn.net_scale);
   return check_launch("ocppo_rollout_store_vecnorm");
 }
 
 template <int FDT, int ODT, bool CL>
 int launch_reset(hipStream_t s, const void* frame, int64_t N, int64_t W, int64_t D, void* out,
-                 float* net) {
+                 float* net, float sc) {
   if (D % 4 == 0) {
     const int64_t groups = N * W * (D / 4);
     hipLaunchKernelGGL((obs_reset_kernel<FDT, ODT, 4, CL>), dim3(grid_for(groups, 256)), dim3(256),
-                       0, s, frame, N, (int)W, D, out, net);
+                       0, s, frame, N, (int)W, D, out, net, sc);
   } else {
     const int64_t groups = N * W * D;
     hipLaunchKernelGGL((obs_reset_kernel<FDT, ODT, 1, CL>), dim3(grid_for(groups, 256)), dim3(256),
-                       0, s, frame, N, (int)W, D, out, net);
+                       0, s, frame, N, (int)W, D, out, net, sc);
   }
   return check_launch("ocppo_obs_reset");
 }
@@ -431,17 +435,21 @@ int launch_gather(hipStream_t s, const void* src, const int64_t* idx, int64_t M,
 
 template <int SDT>
 int launch_gather_cl(hipStream_t s, const void* src, const int64_t* idx, int64_t M, int64_t C,
-                     int64_t P, float* dst) {
+                     int64_t P, float* dst, float sc) {
   if (P % 4 == 0)
     hipLaunchKernelGGL((gather_rows_cl_kernel<SDT, 4>), dim3(grid_for(M * (P / 4), 256)), dim3(256),
-                       0, s, src, idx, M, (int)C, P, dst);
+                       0, s, src, idx, M, (int)C, P, dst, sc);
   else
     hipLaunchKernelGGL((gather_rows_cl_kernel<SDT, 1>), dim3(grid_for(M * P, 256)), dim3(256), 0,
-                       s, src, idx, M, (int)C, P, dst);
+                       s, src, idx, M, (int)C, P, dst, sc);
   return check_launch("ocppo_gather_rows_cl");
 }
 
 static bool aligned16(const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; }
+
+// x / 255 as ATen computes it for a float tensor and a CPU scalar: x * (1.0f / 255.0f)
+// (div_true_kernel_cuda multiplies by the scalar's reciprocal); 1.0f leaves values untouched
+inline float net_scale_of(int flags) { return (flags & OCPPO_NET_SCALE_255) ? 1.0f / 255.0f : 1.0f; }
 
 // ---- frame-encoding cache of the rollout (PPObj: the encoder acts on each frame alone) ---------
 // enc[n, w, :] = done[n] != 0 || w == W-1 ? fresh[n, :] : enc[n, w+1, :]   (in place)
@@ -488,10 +496,14 @@ extern "C" int ocppo_rollout_store(ocppo_stream_t stream, const void* frame, int
                                    const float* reward, const float* done, int64_t N, int64_t W,
                                    int64_t D, const void* prev_obs, void* obs_out, int obs_dtype,
                                    float* net_obs, float* reward_out, float* done_out,
-                                   int net_layout) {
+                                   int net_flags) {
   OCPPO_REQUIRE(N >= 0 && W >= 1 && D >= 1 && W <= 64, "ocppo_rollout_store: bad sizes");
-  OCPPO_REQUIRE(net_layout == 0 || (net_layout == 1 && net_obs && aligned16(net_obs)),
-                "ocppo_rollout_store: net_layout must be 0, or 1 with a 16-B aligned net_obs");
+  OCPPO_REQUIRE((net_flags & ~3) == 0 &&
+                    (!(net_flags & OCPPO_NET_CHANNELS_LAST) || (net_obs && aligned16(net_obs))),
+                "ocppo_rollout_store: bad net_flags %d (channels-last needs a 16-B aligned net_obs)",
+                net_flags);
+  const bool net_layout = net_flags & OCPPO_NET_CHANNELS_LAST;
+  const float sc = net_scale_of(net_flags);
   OCPPO_REQUIRE(frame_dtype == OCPPO_F32 || frame_dtype == OCPPO_U8,
                 "ocppo_rollout_store: frame dtype must be OCPPO_F32 or OCPPO_U8");
   OCPPO_REQUIRE(valid_dtype(obs_dtype), "ocppo_rollout_store: bad obs dtype %d", obs_dtype);
@@ -503,9 +515,9 @@ extern "C" int ocppo_rollout_store(ocppo_stream_t stream, const void* frame, int
 #define OCPPO_STORE(F, O)                                                                     \
   if (frame_dtype == F && obs_dtype == O)                                                     \
     return net_layout ? launch_store<F, O, true>(s, frame, reward, done, N, W, D, prev_obs,   \
-                                                 obs_out, net_obs, reward_out, done_out)      \
+                                                 obs_out, net_obs, reward_out, done_out, sc)  \
                       : launch_store<F, O, false>(s, frame, reward, done, N, W, D, prev_obs,  \
-                                                  obs_out, net_obs, reward_out, done_out);
+                                                  obs_out, net_obs, reward_out, done_out, sc);
   OCPPO_STORE(OCPPO_F32, OCPPO_F32)
   OCPPO_STORE(OCPPO_F32, OCPPO_BF16)
   OCPPO_STORE(OCPPO_F32, OCPPO_U8)
@@ -518,9 +530,11 @@ extern "C" int ocppo_rollout_store(ocppo_stream_t stream, const void* frame, int
 
 extern "C" int ocppo_obs_reset(ocppo_stream_t stream, const void* frame, int frame_dtype, int64_t N,
                                int64_t W, int64_t D, void* obs_out, int obs_dtype, float* net_obs,
-                               int net_layout) {
+                               int net_flags) {
   OCPPO_REQUIRE(N >= 0 && W >= 1 && D >= 1 && W <= 64, "ocppo_obs_reset: bad sizes");
-  OCPPO_REQUIRE(net_layout == 0 || net_layout == 1, "ocppo_obs_reset: bad net_layout");
+  OCPPO_REQUIRE((net_flags & ~3) == 0, "ocppo_obs_reset: bad net_flags %d", net_flags);
+  const bool net_layout = net_flags & OCPPO_NET_CHANNELS_LAST;
+  const float sc = net_scale_of(net_flags);
   OCPPO_REQUIRE(frame_dtype == OCPPO_F32 || frame_dtype == OCPPO_U8,
                 "ocppo_obs_reset: frame dtype must be OCPPO_F32 or OCPPO_U8");
   OCPPO_REQUIRE(valid_dtype(obs_dtype), "ocppo_obs_reset: bad obs dtype %d", obs_dtype);
@@ -530,8 +544,8 @@ extern "C" int ocppo_obs_reset(ocppo_stream_t stream, const void* frame, int fra
   hipStream_t s = as_stream(stream);
 #define OCPPO_RESET(F, O)                                                                 \
   if (frame_dtype == F && obs_dtype == O)                                                 \
-    return net_layout ? launch_reset<F, O, true>(s, frame, N, W, D, obs_out, net_obs)     \
-                      : launch_reset<F, O, false>(s, frame, N, W, D, obs_out, net_obs);
+    return net_layout ? launch_reset<F, O, true>(s, frame, N, W, D, obs_out, net_obs, sc)  \
+                      : launch_reset<F, O, false>(s, frame, N, W, D, obs_out, net_obs, sc);
   OCPPO_RESET(OCPPO_F32, OCPPO_F32)
   OCPPO_RESET(OCPPO_F32, OCPPO_BF16)
   OCPPO_RESET(OCPPO_F32, OCPPO_U8)
@@ -557,7 +571,9 @@ extern "C" int ocppo_gather_rows(ocppo_stream_t stream, const void* src, int src
 
 extern "C" int ocppo_gather_rows_cl(ocppo_stream_t stream, const void* src, int src_dtype,
                                     const int64_t* idx, int64_t M, int64_t C, int64_t P,
-                                    float* dst) {
+                                    float* dst, int net_flags) {
+  OCPPO_REQUIRE((net_flags & ~3) == 0, "ocppo_gather_rows_cl: bad net_flags %d", net_flags);
+  const float sc = net_scale_of(net_flags);
   OCPPO_REQUIRE(M >= 0 && C >= 1 && C <= 64 && P >= 1, "ocppo_gather_rows_cl: bad sizes");
   OCPPO_REQUIRE(valid_dtype(src_dtype), "ocppo_gather_rows_cl: bad dtype %d", src_dtype);
   if (M == 0) return OCPPO_OK;
@@ -565,9 +581,9 @@ extern "C" int ocppo_gather_rows_cl(ocppo_stream_t stream, const void* src, int 
   OCPPO_REQUIRE(aligned16(dst), "ocppo_gather_rows_cl: dst must be 16-B aligned");
   clear_stale_error();
   hipStream_t s = as_stream(stream);
-  if (src_dtype == OCPPO_F32) return launch_gather_cl<OCPPO_F32>(s, src, idx, M, C, P, dst);
-  if (src_dtype == OCPPO_BF16) return launch_gather_cl<OCPPO_BF16>(s, src, idx, M, C, P, dst);
-  return launch_gather_cl<OCPPO_U8>(s, src, idx, M, C, P, dst);
+  if (src_dtype == OCPPO_F32) return launch_gather_cl<OCPPO_F32>(s, src, idx, M, C, P, dst, sc);
+  if (src_dtype == OCPPO_BF16) return launch_gather_cl<OCPPO_BF16>(s, src, idx, M, C, P, dst, sc);
+  return launch_gather_cl<OCPPO_U8>(s, src, idx, M, C, P, dst, sc);
 }
 
 extern "C" int ocppo_vecnorm_reward(ocppo_stream_t stream, const float* reward, const float* done,
@@ -609,10 +625,13 @@ extern "C" int ocppo_rollout_store_vecnorm(ocppo_stream_t stream, const void* fr
                                            void* obs_out, int obs_dtype, float* net_obs,
                                            float* done_out, double gamma, double epsilon,
                                            double clip_reward, double* ret_state,
-                                           double* rms_state, float* reward_out, int net_layout) {
+                                           double* rms_state, float* reward_out, int net_flags) {
   OCPPO_REQUIRE(N >= 1 && W >= 1 && D >= 1 && W <= 64, "ocppo_rollout_store_vecnorm: bad sizes");
-  OCPPO_REQUIRE(net_layout == 0 || (net_layout == 1 && net_obs && aligned16(net_obs)),
-                "ocppo_rollout_store_vecnorm: net_layout must be 0, or 1 with a 16-B aligned net_obs");
+  OCPPO_REQUIRE((net_flags & ~3) == 0 &&
+                    (!(net_flags & OCPPO_NET_CHANNELS_LAST) || (net_obs && aligned16(net_obs))),
+                "ocppo_rollout_store_vecnorm: bad net_flags %d (channels-last needs a 16-B aligned "
+                "net_obs)", net_flags);
+  const bool net_layout = net_flags & OCPPO_NET_CHANNELS_LAST;
   OCPPO_REQUIRE(frame_dtype == OCPPO_F32 || frame_dtype == OCPPO_U8,
                 "ocppo_rollout_store_vecnorm: frame dtype must be OCPPO_F32 or OCPPO_U8");
   OCPPO_REQUIRE(valid_dtype(obs_dtype), "ocppo_rollout_store_vecnorm: bad obs dtype %d", obs_dtype);
@@ -621,7 +640,8 @@ extern "C" int ocppo_rollout_store_vecnorm(ocppo_stream_t stream, const void* fr
                 "ocppo_rollout_store_vecnorm: null pointer");
   OCPPO_REQUIRE(prev_obs != obs_out, "ocppo_rollout_store_vecnorm: prev_obs must not alias obs_out");
   OCPPO_REQUIRE(reward_out != reward, "ocppo_rollout_store_vecnorm: reward_out must not alias reward");
-  const VecNormArgs vn{gamma, epsilon, clip_reward, ret_state, rms_state, reward_out};
+  const VecNormArgs vn{gamma,     epsilon,    clip_reward,
+                       ret_state, rms_state,  reward_out, net_scale_of(net_flags)};
   clear_stale_error();
   hipStream_t s = as_stream(stream);
 #define OCPPO_SV(F, O)                                                                        \

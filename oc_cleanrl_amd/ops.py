@@ -318,11 +318,12 @@ def categorical_logprob_entropy(logits, actions):
 # rollout store / reset (ppo_atari_oc.py:502-503, 512-514), minibatch gather (:566-567)
 # ---------------------------------------------------------------------------------------------
 def rollout_store(frame, reward, done, prev_obs, obs_out, net_obs=None, reward_out=None,
-                  done_out=None):
+                  done_out=None, scale255: bool = False):
     """obs_out = stack(prev_obs[:, 1:], frame) (reset-filled where done), plus reward/done rows.
 
     frame [N, D] f32|u8; prev_obs/obs_out [N, W, D] f32|bf16|u8; net_obs [N, W, D] f32, or a
-    channels_last [N, W, H, X] f32 tensor (written in NHWC order).
+    channels_last [N, W, H, X] f32 tensor (written in NHWC order). scale255: net_obs holds
+    value / 255 exactly as the NatureCNN's NormalizeImg computes it on the GPU.
     """
     N, D = frame.shape[0], frame[0].numel()
     W = obs_out.shape[1]
@@ -339,11 +340,13 @@ def rollout_store(frame, reward, done, prev_obs, obs_out, net_obs=None, reward_o
          _DTYPE_CODE[frame.dtype], _check(reward, "reward", f, dev, N),
          _check(done, "done", f, dev, N), N, W, D, _check(prev_obs, "prev_obs", None, dev),
          _check(obs_out, "obs_out", None, dev), _DTYPE_CODE[obs_out.dtype], net,
-         _opt(reward_out, "reward_out", f, dev, N), _opt(done_out, "done_out", f, dev, N), layout)
+         _opt(reward_out, "reward_out", f, dev, N), _opt(done_out, "done_out", f, dev, N),
+         layout | (2 if scale255 else 0))
 
 
 def rollout_store_vecnorm(frame, reward, done, prev_obs, obs_out, net_obs, done_out, ret_state,
-                          rms_state, reward_out, gamma=0.99, epsilon=1e-8, clip_reward=10.0):
+                          rms_state, reward_out, gamma=0.99, epsilon=1e-8, clip_reward=10.0,
+                          scale255: bool = False):
     """rollout_store + vecnorm_reward in one launch (reward_out gets the normalised reward)."""
     N, D = frame.shape[0], frame[0].numel()
     W = obs_out.shape[1]
@@ -362,10 +365,10 @@ def rollout_store_vecnorm(frame, reward, done, prev_obs, obs_out, net_obs, done_
          float(gamma), float(epsilon), float(clip_reward),
          _check(ret_state, "ret_state", torch.float64, dev, N),
          _check(rms_state, "rms_state", torch.float64, dev, 3),
-         _check(reward_out, "reward_out", f, dev, N), layout)
+         _check(reward_out, "reward_out", f, dev, N), layout | (2 if scale255 else 0))
 
 
-def obs_reset(frame, obs_out, net_obs=None):
+def obs_reset(frame, obs_out, net_obs=None, scale255: bool = False):
     N, D = frame.shape[0], frame[0].numel()
     W = obs_out.shape[1]
     dev = frame.device
@@ -374,7 +377,7 @@ def obs_reset(frame, obs_out, net_obs=None):
     net, layout = _net_obs(net_obs, N, W, D, dev)
     call("ocppo_obs_reset", _stream(dev), _check(frame, "frame", None, dev),
          _DTYPE_CODE[frame.dtype], N, W, D, _check(obs_out, "obs_out", None, dev),
-         _DTYPE_CODE[obs_out.dtype], net, layout)
+         _DTYPE_CODE[obs_out.dtype], net, layout | (2 if scale255 else 0))
 
 
 def linear_act(x, weight, bias=None, relu: bool = False, out=None):
@@ -524,9 +527,10 @@ def frame_cache_shift(enc, fresh, done=None):
     return enc
 
 
-def gather_rows(src, idx, out=None):
+def gather_rows(src, idx, out=None, scale255: bool = False):
     """out[i] = float32(src[idx[i]]) for src [B, ...] f32|bf16|u8 → out [M, ...] f32. A
-    channels_last `out` [M, C, H, X] gets the rows in NHWC order (ocppo_gather_rows_cl)."""
+    channels_last `out` [M, C, H, X] gets the rows in NHWC order (ocppo_gather_rows_cl), divided
+    by 255 as NormalizeImg does when scale255."""
     dev = src.device
     M = idx.numel()
     R = src[0].numel() if src.shape[0] else 0
@@ -542,8 +546,10 @@ def gather_rows(src, idx, out=None):
         C = src.shape[1]
         call("ocppo_gather_rows_cl", _stream(dev), _check(src, "src", None, dev),
              _DTYPE_CODE[src.dtype], _check(idx, "idx", torch.int64, dev, M), M, C, R // C,
-             out.data_ptr())
+             out.data_ptr(), 2 if scale255 else 0)
         return out
+    if scale255:
+        raise ValueError("scale255 needs a channels_last out (ocppo_gather_rows_cl)")
     call("ocppo_gather_rows", _stream(dev), _check(src, "src", None, dev), _DTYPE_CODE[src.dtype],
          _check(idx, "idx", torch.int64, dev, M), M, R,
          _check(out, "out", torch.float32, dev, M * R))

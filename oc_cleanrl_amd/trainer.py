@@ -33,7 +33,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from . import frames, ops
-from .agents import PPObj, make_agent
+from .agents import NormalizeImg, PPObj, make_agent
 from .args import Args
 from .envs import SyntheticAtariEnv
 
@@ -161,6 +161,9 @@ class PPOTrainer:
         self.net_format = torch.channels_last if self.channels_last else torch.contiguous_format
         if self.channels_last:
             self.agent = self.agent.to(memory_format=torch.channels_last)
+        # ... and its NormalizeImg (x / 255) folded into those HIP writes
+        net0 = self.agent.network[0] if isinstance(self.agent.network, nn.Sequential) else None
+        self.prescale = self.channels_last and isinstance(net0, NormalizeImg)
         torch.manual_seed(self.seed)
         self.fused_head = isinstance(self.agent.actor, nn.Linear) and \
             isinstance(self.agent.critic, nn.Linear)
@@ -276,7 +279,7 @@ class PPOTrainer:
     # ------------------------------------------------------------------------------------------
     def _reset_env(self):
         frame = self.env.reset()
-        ops.obs_reset(frame, self.obs[self.T], self.net_obs)
+        ops.obs_reset(frame, self.obs[self.T], self.net_obs, scale255=self.prescale)
         self.dones[self.T].zero_()
 
     def _policy_hidden(self, t: int):
@@ -285,7 +288,7 @@ class PPOTrainer:
         later steps encode only the newest frame and shift the cache with done row t."""
         ag = self.agent
         if not self.frame_cache:
-            return ag.trunk(self.net_obs)
+            return ag.trunk(self.net_obs, self.prescale)
         if t == 0:
             self.enc_cache.copy_(ag.encode(self.net_obs))
         else:
@@ -306,7 +309,7 @@ class PPOTrainer:
                 hidden, ag.actor.weight, ag.actor.bias, ag.critic.weight, ag.critic.bias,
                 self.noise[t], self.actions[t], self.logprobs[t], self.values[t]))
         else:
-            logits, value = ag.logits_and_value(self.net_obs)
+            logits, value = ag.logits_and_value(self.net_obs, self.prescale)
             self.timer.bracket("action_head", lambda: ops.categorical_sample(
                 logits, self.noise[t], self.actions[t], self.logprobs[t], None, value.view(-1),
                 self.values[t]))
@@ -314,11 +317,12 @@ class PPOTrainer:
         if a.vecnorm_reward:
             self.timer.bracket("rollout_store", lambda: ops.rollout_store_vecnorm(
                 self.env.frame, self.env.reward, self.env.done, self.obs[t], self.obs[t + 1],
-                self.net_obs, self.dones[t + 1], self.ret_state, self.rms_state, self.rewards[t]))
+                self.net_obs, self.dones[t + 1], self.ret_state, self.rms_state, self.rewards[t],
+                scale255=self.prescale))
         else:
             self.timer.bracket("rollout_store", lambda: ops.rollout_store(
                 self.env.frame, self.env.reward, self.env.done, self.obs[t], self.obs[t + 1],
-                self.net_obs, self.rewards[t], self.dones[t + 1]))
+                self.net_obs, self.rewards[t], self.dones[t + 1], scale255=self.prescale))
 
     def _rollout(self):
         """Rollout (:500-530) + bootstrap + GAE (:533-547) + minibatch adv stats (:577-579)."""
@@ -335,7 +339,7 @@ class PPOTrainer:
                 self.values[T].copy_(self.agent._head(self.agent.critic,
                                                       self._policy_hidden(T)).view(-1))
             else:
-                self.values[T].copy_(self.agent.get_value(self.net_obs).view(-1))
+                self.values[T].copy_(self.agent.get_value(self.net_obs, self.prescale).view(-1))
             self.timer.bracket("gae", lambda: ops.gae(
                 self.rewards, self.values[:T], self.dones[:T], self.values[T], self.dones[T],
                 a.gamma, a.gae_lambda, self.advantages, self.returns))
@@ -359,8 +363,9 @@ class PPOTrainer:
                 hidden, self.cuts[j] = hidden
             logits, value = ag._head(ag.actor, hidden), ag._head(ag.critic, hidden)
         else:
-            self.timer.bracket("gather", lambda: ops.gather_rows(self.b_obs, idx, self.mb_obs))
-            logits, value = ag.logits_and_value(self.mb_obs)
+            self.timer.bracket("gather", lambda: ops.gather_rows(self.b_obs, idx, self.mb_obs,
+                                                                 scale255=self.prescale))
+            logits, value = ag.logits_and_value(self.mb_obs, self.prescale)
         lg, vv = logits.detach(), value.detach().view(-1)  # the timer's closure must not hold
         sl = slice(j * self.M, (j + 1) * self.M)
         mb = self.mb

@@ -756,3 +756,36 @@ def test_relu_bias_grad_rejects_bad_shapes(ops, dev):
 
     with pytest.raises(OcppoError, match="bad sizes"):
         ops.relu_bias_grad(torch.randn(8, 6, device=dev))
+
+
+@pytest.mark.parametrize("cl", [False, True])
+def test_store_and_gather_scale255_equal_torch_division(ops, dev, cl):
+    """OCPPO_NET_SCALE_255: the network copy holds exactly what NormalizeImg (x / 255.0 on the
+    GPU, architectures/common.py:19-22) computes from the plain copy."""
+    rng = np.random.default_rng(5)
+    N, W, H, X = 6, 4, 84, 84
+    D = H * X
+    frame = T(rng.integers(0, 256, (N, D)).astype(np.uint8), dev)
+    prev = T(rng.integers(0, 256, (N, W, D)).astype(np.uint8), dev)
+    done = T((rng.random(N) < 0.3).astype(np.float32), dev)
+    rew = torch.zeros(N, device=dev)
+    fmt = torch.channels_last if cl else torch.contiguous_format
+    nets = []
+    for sc in (False, True):
+        net = torch.empty((N, W, H, X), device=dev, memory_format=fmt)
+        ops.rollout_store(frame, rew, done, prev, torch.empty_like(prev), net, scale255=sc)
+        nets.append(net)
+    assert torch.equal(nets[0] / 255.0, nets[1])
+    r0 = torch.empty((N, W, H, X), device=dev, memory_format=fmt)
+    r1 = torch.empty((N, W, H, X), device=dev, memory_format=fmt)
+    ops.obs_reset(frame, torch.empty_like(prev), r0)
+    ops.obs_reset(frame, torch.empty_like(prev), r1, scale255=True)
+    assert torch.equal(r0 / 255.0, r1)
+    if cl:
+        src = prev.view(N, W, H, X)
+        idx = torch.tensor([5, 0, 3, 3], device=dev)
+        g0 = torch.empty((4, W, H, X), device=dev, memory_format=fmt)
+        g1 = torch.empty((4, W, H, X), device=dev, memory_format=fmt)
+        ops.gather_rows(src, idx, g0)
+        ops.gather_rows(src, idx, g1, scale255=True)
+        assert torch.equal(g0 / 255.0, g1)

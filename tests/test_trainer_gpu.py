@@ -61,10 +61,11 @@ def test_pixel_channels_last_matches_nchw(dev):
     assert not a.channels_last and b.channels_last
     for (ka, pa), (kb, pb) in zip(a.agent.state_dict().items(), b.agent.state_dict().items()):
         assert ka == kb and torch.equal(pa, pb)
-    assert torch.equal(a.net_obs, b.net_obs)
+    assert b.prescale and not a.prescale
+    assert torch.equal(a.net_obs / 255.0, b.net_obs)  # NormalizeImg folded in, bit-exact
     with torch.no_grad():
         la, va = a.agent.logits_and_value(a.net_obs)
-        lb, vb = b.agent.logits_and_value(b.net_obs)
+        lb, vb = b.agent.logits_and_value(b.net_obs, prescaled=True)
     torch.testing.assert_close(la, lb, rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(va, vb, rtol=1e-4, atol=1e-4)
     for tr in trs:
