@@ -269,6 +269,12 @@ OCPPO_API int ocppo_linear_act(ocppo_stream_t stream, const float* x, int64_t ld
  * g/out/gp [R, N] f32 row-major, 16-B aligned, N % 4 == 0, N <= 16384; workspace 256-B aligned,
  * >= ocppo_relu_bias_grad_workspace_bytes(R, N), ZEROED before its first use (its tickets re-arm).
  * ------------------------------------------------------------------------------------------- */
+/* Forward epilogue of a bias-less convolution / GEMM in NHWC / row-major layout, in place:
+ *   y[r, n] = act(y[r, n] + b[n])   (act = ReLU when relu != 0; torch's conv + bias then ReLU,
+ *                                    one f32 rounding for the add, architectures/ppo.py:20-31)
+ * y [R, N] f32, b [N] f32, both 16-B aligned, N % 4 == 0. */
+OCPPO_API int ocppo_bias_act(ocppo_stream_t stream, float* y, const float* b, int64_t R, int64_t N,
+                   int relu);
 OCPPO_API size_t ocppo_relu_bias_grad_workspace_bytes(int64_t R, int64_t N);
 OCPPO_API int ocppo_relu_bias_grad(ocppo_stream_t stream, const float* g, const float* out,
                          float* gp, float* db, int64_t R, int64_t N, void* workspace,

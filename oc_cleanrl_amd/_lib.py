@@ -55,6 +55,7 @@ SIGNATURES: dict[str, tuple[type, list]] = {
     "ocppo_linear_act": (I, [P, P, I64, P, P, P, I64, I64, I64, I64, I]),
     "ocppo_relu_bias_grad_workspace_bytes": (SZ, [I64, I64]),
     "ocppo_relu_bias_grad": (I, [P, P, P, P, P, I64, I64, P, SZ]),
+    "ocppo_bias_act": (I, [P, P, P, I64, I64, I]),
     "ocppo_frames_gather": (I, [P, P, I, I64, I64, I64, I64, P, I64, P]),
     "ocppo_frames_expand": (I, [P, P, I64, I64, P, P, I64, P, I64, I64, I64, P]),
     "ocppo_frames_scatter": (I, [P, P, I64, I64, P, I64, P, I64, P, I64, I64, I64, P]),

@@ -134,6 +134,60 @@ class _LinearAct(torch.autograd.Function):
 FUSED_RELU_BIAS_GRAD = True
 
 
+class _ConvAct(torch.autograd.Function):
+    """y = act(conv2d(x, w) + b) for a channels_last (NHWC) input: MIOpen's bias-less NHWC
+    convolution, then ONE HIP pass for bias + ReLU (ATen runs them as two); backward: ONE HIP pass
+    for ReLU-backward + bias gradient over the NHWC gradient viewed [B*H*W, C]
+    (ops.relu_bias_grad), then aten.convolution_backward for dX / dW. Same arithmetic as
+    nn.Conv2d + nn.ReLU up to the bias-gradient summation order (architectures/ppo.py:20-31)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, stride, padding, relu: bool):
+        y = torch.ops.aten.convolution(x, w, None, stride, padding, (1, 1), False, (0, 0), 1)
+        y = y.contiguous(memory_format=torch.channels_last)
+        C = y.shape[1]
+        ops.timed("bias_act", lambda: ops.bias_act(y.permute(0, 2, 3, 1).reshape(-1, C), b, relu))
+        ctx.conv = (stride, padding, relu)
+        ctx.b = b
+        ctx.save_for_backward(x, w, y if relu else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w, y = ctx.saved_tensors
+        stride, padding, relu = ctx.conv
+        g = g.contiguous(memory_format=torch.channels_last)
+        C = g.shape[1]
+        g2 = g.permute(0, 2, 3, 1).reshape(-1, C)
+        b = ctx.b
+        direct_b = _direct(b)
+        db_out = b.grad if direct_b else torch.empty_like(b)
+        o2 = y.permute(0, 2, 3, 1).reshape(-1, C) if relu else None
+        gp2, _ = ops.timed(f"relu_bias_grad_{g2.shape[0]}x{C}" + ("" if relu else "_norelu"),
+                           lambda: ops.relu_bias_grad(g2, o2, db=db_out))
+        gp = gp2.view(g.shape[0], g.shape[2], g.shape[3], C).permute(0, 3, 1, 2)
+        dx, dw, _ = torch.ops.aten.convolution_backward(
+            gp, x, w, None, stride, padding, (1, 1), False, (0, 0), 1,
+            (ctx.needs_input_grad[0], ctx.needs_input_grad[1], False))
+        if dw is not None and _direct(w):
+            w.grad.copy_(dw)
+            dw = None
+        return dx, dw, (None if direct_b else db_out), None, None, None
+
+
+def _conv_act_ok(x, conv) -> bool:
+    return (FUSED_CONV_ACT and isinstance(conv, nn.Conv2d) and conv.bias is not None and x.is_cuda
+            and x.dtype == torch.float32 and x.dim() == 4 and conv.groups == 1
+            and conv.dilation == (1, 1) and conv.padding_mode == "zeros"
+            and isinstance(conv.padding, tuple) and conv.out_channels % 4 == 0
+            and x.is_contiguous(memory_format=torch.channels_last)
+            and conv.weight.is_contiguous(memory_format=torch.channels_last))
+
+
+# NHWC conv + one-pass HIP bias/ReLU forward and ReLU-backward/bias-grad backward (_ConvAct).
+FUSED_CONV_ACT = True
+
+
 # Rollout-sized inference batches (no autograd) of the shapes where the HIP f32-MFMA kernel beats
 # the BLAS library's (tools/exp_rollout_linear.py on MI355X: K <= 64 at up to 512 rows, K <= 256 at
 # up to 128 rows); everything else, and every autograd forward, stays on hipBLASLt.
@@ -172,7 +226,11 @@ def fused_trunk(seq: nn.Sequential, x):
         m = mods[i]
         fusable = (isinstance(m, nn.Linear) and m.bias is not None and x.is_cuda
                    and x.dtype == torch.float32)
-        if fusable and i + 1 < len(mods) and isinstance(mods[i + 1], nn.ReLU):
+        if _conv_act_ok(x, m):
+            relu = i + 1 < len(mods) and isinstance(mods[i + 1], nn.ReLU)
+            x = _ConvAct.apply(x, m.weight, m.bias, m.stride, m.padding, relu)
+            i += 2 if relu else 1
+        elif fusable and i + 1 < len(mods) and isinstance(mods[i + 1], nn.ReLU):
             x = linear_relu(x, m)
             i += 2
         elif fusable:

@@ -23,16 +23,36 @@ namespace ocppo {
 
 constexpr int kRbStripeCols = 256;  // columns per workgroup (64 lanes x 4)
 constexpr int kRbMaxStripes = 64;   // N <= 16384
-constexpr int kRbMaxChunks = 128;
+constexpr int kRbMaxChunks = 512;
 constexpr size_t kRbTicketBytes = kRbMaxStripes * 128;
 
-inline int rb_chunks(int64_t R, int64_t stripes) {
-  // >= ~512 workgroups when the rows allow it, >= 32 rows per chunk, <= kRbMaxChunks
-  int64_t c = 512 / stripes;
-  if (c > kRbMaxChunks) c = kRbMaxChunks;
-  const int64_t by_rows = (R + 31) / 32;
-  if (c > by_rows) c = by_rows;
+inline int rb_chunks(int64_t R, int64_t N) {
+  const int64_t stripes = (N + kRbStripeCols - 1) / kRbStripeCols;
+  int64_t c;
+  if (N >= kRbStripeCols) {
+    // >= ~512 workgroups when the rows allow it, >= 32 rows and <= 128 chunks per stripe (the
+    // last arriver's chunk-order sum stays short)
+    c = 512 / stripes;
+    if (c > 128) c = 128;
+    const int64_t by_rows = (R + 31) / 32;
+    if (c > by_rows) c = by_rows;
+  } else {
+    // one stripe: ~64K elements per workgroup (tall NHWC convolution outputs), <= 512 chunks
+    c = (R * N + 65535) / 65536;
+    if (c > kRbMaxChunks) c = kRbMaxChunks;
+    const int64_t by_rows = (R + 31) / 32;
+    if (c > by_rows) c = by_rows;
+    if (c < 128 && by_rows >= 128) c = by_rows < 128 ? by_rows : 128;
+  }
   return static_cast<int>(c < 1 ? 1 : c);
+}
+
+// Lanes per row: 64 lanes x 4 columns cover a 256-column stripe; a narrower N whose N/4 divides
+// 64 (conv channel counts 32 / 64 of an NHWC output, N = 128) packs 64 / (N/4) rows into every
+// wave instruction instead of idling lanes.
+__host__ __device__ inline int rb_lanes_per_row(int64_t N) {
+  const int64_t q = N / 4;
+  return (q < 64 && 64 % q == 0) ? static_cast<int>(q) : 64;
 }
 
 template <bool RELU>
@@ -43,38 +63,42 @@ __global__ __launch_bounds__(256) void relu_bias_grad_kernel(const float* __rest
                                                              int64_t N, int chunks,
                                                              unsigned* __restrict__ tickets,
                                                              float* __restrict__ partials) {
-  __shared__ float red[4][kRbStripeCols];
+  __shared__ float4 red[4][64];
   __shared__ int s_last;
-  const int stripe = blockIdx.x % (static_cast<int>((N + kRbStripeCols - 1) / kRbStripeCols));
-  const int chunk = blockIdx.x / (static_cast<int>((N + kRbStripeCols - 1) / kRbStripeCols));
+  const int nstripes = static_cast<int>((N + kRbStripeCols - 1) / kRbStripeCols);
+  const int stripe = blockIdx.x % nstripes;
+  const int chunk = blockIdx.x / nstripes;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t c0 = static_cast<int64_t>(stripe) * kRbStripeCols + 4 * lane;
+  const int L = rb_lanes_per_row(N), RP = 64 / L;
+  const int lrow = lane / L, lcol = lane - lrow * L;
+  const int64_t c0 = static_cast<int64_t>(stripe) * kRbStripeCols + 4 * lcol;
   const bool live = c0 < N;  // N % 4 == 0: a lane's 4 columns are all live or all dead
   const int64_t rows_per = (R + chunks - 1) / chunks;
   const int64_t r0 = chunk * rows_per;
   const int64_t r1 = r0 + rows_per < R ? r0 + rows_per : R;
+  const int64_t step = 4 * RP;  // rows per block-wide sweep (4 waves x RP rows)
 
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   if (live) {
-    int64_t r = r0 + wv;
-    // two rows in flight per wave iteration
-    for (; r + 4 < r1; r += 8) {
+    int64_t r = r0 + wv * RP + lrow;
+    // two rows in flight per lane and iteration
+    for (; r + step < r1; r += 2 * step) {
       float4 a = *reinterpret_cast<const float4*>(g + r * N + c0);
-      float4 b = *reinterpret_cast<const float4*>(g + (r + 4) * N + c0);
+      float4 b = *reinterpret_cast<const float4*>(g + (r + step) * N + c0);
       if (RELU) {
         const float4 oa = *reinterpret_cast<const float4*>(out + r * N + c0);
-        const float4 ob = *reinterpret_cast<const float4*>(out + (r + 4) * N + c0);
+        const float4 ob = *reinterpret_cast<const float4*>(out + (r + step) * N + c0);
         a.x = oa.x <= 0.f ? 0.f : a.x; a.y = oa.y <= 0.f ? 0.f : a.y;
         a.z = oa.z <= 0.f ? 0.f : a.z; a.w = oa.w <= 0.f ? 0.f : a.w;
         b.x = ob.x <= 0.f ? 0.f : b.x; b.y = ob.y <= 0.f ? 0.f : b.y;
         b.z = ob.z <= 0.f ? 0.f : b.z; b.w = ob.w <= 0.f ? 0.f : b.w;
         *reinterpret_cast<float4*>(gp + r * N + c0) = a;
-        *reinterpret_cast<float4*>(gp + (r + 4) * N + c0) = b;
+        *reinterpret_cast<float4*>(gp + (r + step) * N + c0) = b;
       }
       acc.x += a.x; acc.y += a.y; acc.z += a.z; acc.w += a.w;
       acc.x += b.x; acc.y += b.y; acc.z += b.z; acc.w += b.w;
     }
-    for (; r < r1; r += 4) {
+    for (; r < r1; r += step) {
       float4 a = *reinterpret_cast<const float4*>(g + r * N + c0);
       if (RELU) {
         const float4 oa = *reinterpret_cast<const float4*>(out + r * N + c0);
@@ -85,15 +109,19 @@ __global__ __launch_bounds__(256) void relu_bias_grad_kernel(const float* __rest
       acc.x += a.x; acc.y += a.y; acc.z += a.z; acc.w += a.w;
     }
   }
-  red[wv][4 * lane + 0] = acc.x;
-  red[wv][4 * lane + 1] = acc.y;
-  red[wv][4 * lane + 2] = acc.z;
-  red[wv][4 * lane + 3] = acc.w;
+  red[wv][lane] = acc;
   __syncthreads();
-  const int j = threadIdx.x;  // one column of the stripe per thread
+  // column j of the stripe: waves in order, then the RP row-lanes of its lane column in order
+  const int j = threadIdx.x;
   const int64_t col = static_cast<int64_t>(stripe) * kRbStripeCols + j;
-  if (col < N) {
-    const float s = ((red[0][j] + red[1][j]) + red[2][j]) + red[3][j];
+  if (col < N && j < 4 * L) {
+    const int jc = j >> 2, comp = j & 3;
+    float s = 0.f;
+    for (int w = 0; w < 4; ++w)
+      for (int q = 0; q < RP; ++q) {
+        const float4 v = red[w][q * L + jc];
+        s += comp == 0 ? v.x : comp == 1 ? v.y : comp == 2 ? v.z : v.w;
+      }
     __hip_atomic_store(&partials[static_cast<int64_t>(chunk) * N + col], s, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -107,7 +135,7 @@ __global__ __launch_bounds__(256) void relu_bias_grad_kernel(const float* __rest
   }
   __syncthreads();
   if (!s_last) return;
-  if (col < N) {
+  if (col < N && j < 4 * L) {
     float s = 0.f;
 #pragma unroll 16
     for (int c = 0; c < chunks; ++c)
@@ -124,8 +152,7 @@ using namespace ocppo;
 
 extern "C" size_t ocppo_relu_bias_grad_workspace_bytes(int64_t R, int64_t N) {
   if (R < 1 || N < 1) return kRbTicketBytes;
-  const int64_t stripes = (N + kRbStripeCols - 1) / kRbStripeCols;
-  return kRbTicketBytes + static_cast<size_t>(rb_chunks(R, stripes)) * N * sizeof(float);
+  return kRbTicketBytes + static_cast<size_t>(rb_chunks(R, N)) * N * sizeof(float);
 }
 
 extern "C" int ocppo_relu_bias_grad(ocppo_stream_t stream, const float* g, const float* out,
@@ -150,7 +177,7 @@ extern "C" int ocppo_relu_bias_grad(ocppo_stream_t stream, const float* g, const
     return check_launch("ocppo_relu_bias_grad");
   }
   const int64_t stripes = (N + kRbStripeCols - 1) / kRbStripeCols;
-  const int chunks = rb_chunks(R, stripes);
+  const int chunks = rb_chunks(R, N);
   unsigned* tickets = static_cast<unsigned*>(workspace);
   float* partials = reinterpret_cast<float*>(static_cast<char*>(workspace) + kRbTicketBytes);
   const dim3 grid(static_cast<unsigned>(stripes * chunks)), block(256);
@@ -161,4 +188,44 @@ extern "C" int ocppo_relu_bias_grad(ocppo_stream_t stream, const float* g, const
     hipLaunchKernelGGL(relu_bias_grad_kernel<false>, grid, block, 0, s, g, out, gp, db, R, N,
                        chunks, tickets, partials);
   return check_launch("ocppo_relu_bias_grad");
+}
+
+// ---- forward epilogue: y = act(y + b) in place over [R, N] rows (e.g. an NHWC convolution
+// output, N = channels), the bias add + ReLU ATen runs as two passes after a bias-less conv.
+namespace ocppo {
+template <bool RELU>
+__global__ __launch_bounds__(256) void bias_act_kernel(float* __restrict__ y,
+                                                       const float* __restrict__ b, int64_t R,
+                                                       int64_t N) {
+  const int64_t groups = R * (N / 4);
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t q = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; q < groups;
+       q += stride) {
+    const int64_t c = (q % (N / 4)) * 4;
+    float4 v = reinterpret_cast<float4*>(y)[q];
+    const float4 bb = *reinterpret_cast<const float4*>(b + c);
+    v.x = v.x + bb.x; v.y = v.y + bb.y; v.z = v.z + bb.z; v.w = v.w + bb.w;
+    if (RELU) {
+      v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+    }
+    reinterpret_cast<float4*>(y)[q] = v;
+  }
+}
+}  // namespace ocppo
+
+extern "C" int ocppo_bias_act(ocppo_stream_t stream, float* y, const float* b, int64_t R,
+                              int64_t N, int relu) {
+  OCPPO_REQUIRE(R >= 0 && N >= 4 && N % 4 == 0, "ocppo_bias_act: bad sizes R=%lld N=%lld",
+                (long long)R, (long long)N);
+  if (R == 0) return OCPPO_OK;
+  OCPPO_REQUIRE(y && b, "ocppo_bias_act: null pointer");
+  OCPPO_REQUIRE(reinterpret_cast<uintptr_t>(y) % 16 == 0 && reinterpret_cast<uintptr_t>(b) % 16 == 0,
+                "ocppo_bias_act: y and b must be 16-B aligned");
+  clear_stale_error();
+  const dim3 grid(grid_for(R * (N / 4), 256)), block(256);
+  if (relu)
+    hipLaunchKernelGGL(bias_act_kernel<true>, grid, block, 0, as_stream(stream), y, b, R, N);
+  else
+    hipLaunchKernelGGL(bias_act_kernel<false>, grid, block, 0, as_stream(stream), y, b, R, N);
+  return check_launch("ocppo_bias_act");
 }

@@ -448,6 +448,18 @@ def relu_bias_grad(g, out=None, db=None, gp=None):
     return (gp if out is not None else g), db
 
 
+def bias_act(y, b, relu: bool = True):
+    """In place: y = act(y + b) over the rows of y [R, N] f32 (N % 4 == 0): the bias add + ReLU
+    after a bias-less convolution (NHWC output viewed [B*H*W, C]) in one pass."""
+    if y.dim() != 2:
+        raise ValueError(f"y must be [R, N], got {tuple(y.shape)}")
+    R, N = y.shape
+    dev = y.device
+    call("ocppo_bias_act", _stream(dev), _check(y, "y", torch.float32, dev),
+         _check(b, "b", torch.float32, dev, N), R, N, int(bool(relu)))
+    return y
+
+
 # ---------------------------------------------------------------------------------------------
 # Frame-deduplicated PPObj minibatch encoder (ppo_atari_oc.py:566 through architectures/ppo.py:60-84)
 # ---------------------------------------------------------------------------------------------

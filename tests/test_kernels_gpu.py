@@ -789,3 +789,25 @@ def test_store_and_gather_scale255_equal_torch_division(ops, dev, cl):
         ops.gather_rows(src, idx, g0)
         ops.gather_rows(src, idx, g1, scale255=True)
         assert torch.equal(g0 / 255.0, g1)
+
+
+@pytest.mark.parametrize("R,N", [(3276800, 32), (401408, 64), (100, 16), (7, 8), (5000, 128)])
+def test_relu_bias_grad_narrow_rows_packed(ops, dev, R, N):
+    """N/4 < 64 lanes per row: several rows per wave instruction (NHWC conv outputs)."""
+    g = torch.randn(R, N, device=dev)
+    out = torch.relu(torch.randn(R, N, device=dev))
+    gp, db = ops.relu_bias_grad(g, out)
+    want = torch.ops.aten.threshold_backward(g, out, 0)
+    assert torch.equal(gp, want)
+    ref = want.double().sum(0)
+    scale = want.double().abs().sum(0).clamp_min(1e-30)
+    assert ((db.double() - ref).abs() / scale).max().item() < 1e-6
+
+
+@pytest.mark.parametrize("relu", [True, False])
+def test_bias_act_equals_torch(ops, dev, relu):
+    y = torch.randn(50000, 64, device=dev)
+    b = torch.randn(64, device=dev)
+    want = torch.relu(y + b) if relu else y + b
+    ops.bias_act(y, b, relu)
+    assert torch.equal(y, want)

@@ -182,3 +182,25 @@ def test_rollout_frame_cache_matches_full_trunk(dev):
     assert not b.frame_cache and c.frame_cache
     same = (c.actions == b.actions).float().mean().item()
     assert same > 0.99, same
+
+
+def test_nhwc_conv_act_matches_module_forward_and_grads(dev):
+    """NatureCNN in channels_last through _ConvAct (bias-less NHWC conv + HIP bias/ReLU forward,
+    HIP ReLU-backward/bias-grad backward) == nn.Conv2d/nn.ReLU autograd, and the HIP path runs."""
+    from oc_cleanrl_amd import agents
+    from oc_cleanrl_amd.agents import make_agent
+
+    torch.manual_seed(0)
+    ag = make_agent("PPO", (4, 84, 84), 4, dev).to(dev).to(memory_format=torch.channels_last)
+    x = torch.randint(0, 256, (16, 4, 84, 84), device=dev).float()
+    x = x.contiguous(memory_format=torch.channels_last)
+    assert agents._conv_act_ok(x, ag.network[1])
+    h1 = ag.network(x)
+    h2 = ag.trunk(x)
+    torch.testing.assert_close(h2, h1, rtol=1e-5, atol=1e-5)
+    g = torch.randn_like(h1)
+    ps = list(ag.network.parameters())
+    gr1 = torch.autograd.grad(h1, ps, g)
+    gr2 = torch.autograd.grad(h2, ps, g)
+    for a, b in zip(gr1, gr2):
+        torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-5 * float(a.abs().max()))
