@@ -8,11 +8,13 @@
 // that runs at ~2 TB/s on [12288, 1024]); here g and out are read once, gp written once.
 //
 // Deterministic column reduction without atomics on data: the rows are cut into `chunks` equal
-// ranges; workgroup (stripe, chunk) owns 256 columns x one row range (4 waves split the rows,
-// each lane 4 adjacent columns, 16-B accesses), sums its rows in a fixed order, combines the 4
-// waves through LDS in wave order and publishes its 256 partial sums with write-through (sc1)
-// stores; the last workgroup of a stripe to arrive on the stripe's ticket (one 128-B line per
-// stripe) sums the `chunks` partials of each column in chunk order. Hand-off per
+// ranges; workgroup (stripe, chunk) owns a stripe of 4L columns x one row range (L lanes per row,
+// 4 adjacent columns per lane, 16-B accesses, 64/L rows per wave instruction; 4 waves split the
+// rows), sums its rows in a fixed order, combines waves and row-lanes through LDS in a fixed
+// order and publishes its partial column sums with write-through (sc1) stores; the last
+// workgroup of a stripe to arrive on the stripe's ticket (one 128-B line per stripe) sums the
+// `chunks` partials of each column in chunk order (32 loads in flight). rb_plan picks L, the
+// stripes and the chunks so a launch has >= 256 workgroups where the rows allow it. Hand-off per
 // MI355X_MICROARCH.md "Valid forms" row 1 (sc1 stores, every storing wave's vmcnt(0), barrier,
 // one agent-scope atomic add; the last arriver reads with sc1 loads). Tickets re-arm themselves.
 // Roofline: HBM / Infinity-Cache stream, 12 B per element (relu) or 4 B (no relu) + 4 B per
@@ -21,38 +23,44 @@
 
 namespace ocppo {
 
-constexpr int kRbStripeCols = 256;  // columns per workgroup (64 lanes x 4)
-constexpr int kRbMaxStripes = 64;   // N <= 16384
+constexpr int kRbMaxStripes = 64;
 constexpr int kRbMaxChunks = 512;
 constexpr size_t kRbTicketBytes = kRbMaxStripes * 128;
 
-inline int rb_chunks(int64_t R, int64_t N) {
-  const int64_t stripes = (N + kRbStripeCols - 1) / kRbStripeCols;
-  int64_t c;
-  if (N >= kRbStripeCols) {
-    // >= ~512 workgroups when the rows allow it, >= 32 rows and <= 128 chunks per stripe (the
-    // last arriver's chunk-order sum stays short)
-    c = 512 / stripes;
-    if (c > 128) c = 128;
-    const int64_t by_rows = (R + 31) / 32;
-    if (c > by_rows) c = by_rows;
-  } else {
-    // one stripe: ~64K elements per workgroup (tall NHWC convolution outputs), <= 512 chunks
-    c = (R * N + 65535) / 65536;
-    if (c > kRbMaxChunks) c = kRbMaxChunks;
-    const int64_t by_rows = (R + 31) / 32;
-    if (c > by_rows) c = by_rows;
-    if (c < 128 && by_rows >= 128) c = by_rows < 128 ? by_rows : 128;
-  }
-  return static_cast<int>(c < 1 ? 1 : c);
-}
+// Launch plan: L lanes per row (4 columns each: a stripe is 4L columns, 64/L rows per wave
+// instruction), `stripes` column stripes x `chunks` row chunks workgroups.
+struct RbPlan {
+  int L, stripes, chunks;
+};
 
-// Lanes per row: 64 lanes x 4 columns cover a 256-column stripe; a narrower N whose N/4 divides
-// 64 (conv channel counts 32 / 64 of an NHWC output, N = 128) packs 64 / (N/4) rows into every
-// wave instruction instead of idling lanes.
-__host__ __device__ inline int rb_lanes_per_row(int64_t N) {
+inline RbPlan rb_plan(int64_t R, int64_t N) {
   const int64_t q = N / 4;
-  return (q < 64 && 64 % q == 0) ? static_cast<int>(q) : 64;
+  RbPlan p;
+  // narrow N (N/4 divides 64, e.g. conv channels 32 / 64): several rows per wave instruction
+  p.L = (q < 64 && 64 % q == 0) ? static_cast<int>(q) : 64;
+  p.stripes = static_cast<int>((N + 4 * p.L - 1) / (4 * p.L));
+  const int64_t by_rows = (R + 31) / 32;  // >= 32 rows per chunk
+  if (p.stripes == 1 && p.L < 64) {
+    // tall narrow (NHWC conv outputs): ~64K elements per workgroup, 128..512 chunks
+    int64_t c = (R * N + 65535) / 65536;
+    if (c < 128) c = 128;
+    if (c > kRbMaxChunks) c = kRbMaxChunks;
+    if (c > by_rows) c = by_rows;
+    p.chunks = static_cast<int>(c < 1 ? 1 : c);
+    return p;
+  }
+  // <= 128 chunks per stripe (the last arriver's chunk-order sum stays short); narrower stripes
+  // until the launch has >= 256 workgroups (one per CU) when the rows allow it
+  const int64_t c = by_rows < 128 ? by_rows : 128;
+  while (static_cast<int64_t>(p.stripes) * c < 256 && p.L > 16) {
+    const int L2 = p.L / 2;
+    const int s2 = static_cast<int>((N + 4 * L2 - 1) / (4 * L2));
+    if (s2 > kRbMaxStripes) break;
+    p.L = L2;
+    p.stripes = s2;
+  }
+  p.chunks = static_cast<int>(c < 1 ? 1 : c);
+  return p;
 }
 
 template <bool RELU>
@@ -60,18 +68,19 @@ __global__ __launch_bounds__(256) void relu_bias_grad_kernel(const float* __rest
                                                              const float* __restrict__ out,
                                                              float* __restrict__ gp,
                                                              float* __restrict__ db, int64_t R,
-                                                             int64_t N, int chunks,
+                                                             int64_t N, int L, int chunks,
                                                              unsigned* __restrict__ tickets,
                                                              float* __restrict__ partials) {
   __shared__ float4 red[4][64];
   __shared__ int s_last;
-  const int nstripes = static_cast<int>((N + kRbStripeCols - 1) / kRbStripeCols);
+  const int SW = 4 * L;  // columns per stripe
+  const int nstripes = static_cast<int>((N + SW - 1) / SW);
   const int stripe = blockIdx.x % nstripes;
   const int chunk = blockIdx.x / nstripes;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int L = rb_lanes_per_row(N), RP = 64 / L;
+  const int RP = 64 / L;
   const int lrow = lane / L, lcol = lane - lrow * L;
-  const int64_t c0 = static_cast<int64_t>(stripe) * kRbStripeCols + 4 * lcol;
+  const int64_t c0 = static_cast<int64_t>(stripe) * SW + 4 * lcol;
   const bool live = c0 < N;  // N % 4 == 0: a lane's 4 columns are all live or all dead
   const int64_t rows_per = (R + chunks - 1) / chunks;
   const int64_t r0 = chunk * rows_per;
@@ -113,8 +122,9 @@ __global__ __launch_bounds__(256) void relu_bias_grad_kernel(const float* __rest
   __syncthreads();
   // column j of the stripe: waves in order, then the RP row-lanes of its lane column in order
   const int j = threadIdx.x;
-  const int64_t col = static_cast<int64_t>(stripe) * kRbStripeCols + j;
-  if (col < N && j < 4 * L) {
+  const int64_t col = static_cast<int64_t>(stripe) * SW + j;
+  const bool mine = j < SW && col < N;
+  if (mine) {
     const int jc = j >> 2, comp = j & 3;
     float s = 0.f;
     for (int w = 0; w < 4; ++w)
@@ -135,10 +145,20 @@ __global__ __launch_bounds__(256) void relu_bias_grad_kernel(const float* __rest
   }
   __syncthreads();
   if (!s_last) return;
-  if (col < N && j < 4 * L) {
+  if (mine) {
+    // chunk order; 32 loads in flight per batch (one round trip each), summed in order
     float s = 0.f;
-#pragma unroll 16
-    for (int c = 0; c < chunks; ++c)
+    int c = 0;
+    for (; c + 32 <= chunks; c += 32) {
+      float v[32];
+#pragma unroll
+      for (int k = 0; k < 32; ++k)
+        v[k] = __hip_atomic_load(&partials[static_cast<int64_t>(c + k) * N + col],
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int k = 0; k < 32; ++k) s += v[k];
+    }
+    for (; c < chunks; ++c)
       s += __hip_atomic_load(&partials[static_cast<int64_t>(c) * N + col], __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
     db[col] = s;
@@ -152,13 +172,13 @@ using namespace ocppo;
 
 extern "C" size_t ocppo_relu_bias_grad_workspace_bytes(int64_t R, int64_t N) {
   if (R < 1 || N < 1) return kRbTicketBytes;
-  return kRbTicketBytes + static_cast<size_t>(rb_chunks(R, N)) * N * sizeof(float);
+  return kRbTicketBytes + static_cast<size_t>(rb_plan(R, N).chunks) * N * sizeof(float);
 }
 
 extern "C" int ocppo_relu_bias_grad(ocppo_stream_t stream, const float* g, const float* out,
                                     float* gp, float* db, int64_t R, int64_t N, void* workspace,
                                     size_t workspace_bytes) {
-  OCPPO_REQUIRE(R >= 0 && N >= 4 && N % 4 == 0 && N <= kRbMaxStripes * kRbStripeCols,
+  OCPPO_REQUIRE(R >= 0 && N >= 4 && N % 4 == 0 && N <= kRbMaxStripes * 256,
                 "ocppo_relu_bias_grad: bad sizes R=%lld N=%lld (N %% 4 == 0, 4 <= N <= 16384)",
                 (long long)R, (long long)N);
   OCPPO_REQUIRE(g && db && workspace && (!out || gp), "ocppo_relu_bias_grad: null pointer");
@@ -176,17 +196,16 @@ extern "C" int ocppo_relu_bias_grad(ocppo_stream_t stream, const float* g, const
     (void)hipMemsetAsync(db, 0, N * sizeof(float), s);
     return check_launch("ocppo_relu_bias_grad");
   }
-  const int64_t stripes = (N + kRbStripeCols - 1) / kRbStripeCols;
-  const int chunks = rb_chunks(R, N);
+  const RbPlan p = rb_plan(R, N);
   unsigned* tickets = static_cast<unsigned*>(workspace);
   float* partials = reinterpret_cast<float*>(static_cast<char*>(workspace) + kRbTicketBytes);
-  const dim3 grid(static_cast<unsigned>(stripes * chunks)), block(256);
+  const dim3 grid(static_cast<unsigned>(p.stripes * p.chunks)), block(256);
   if (out)
     hipLaunchKernelGGL(relu_bias_grad_kernel<true>, grid, block, 0, s, g, out, gp, db, R, N,
-                       chunks, tickets, partials);
+                       p.L, p.chunks, tickets, partials);
   else
     hipLaunchKernelGGL(relu_bias_grad_kernel<false>, grid, block, 0, s, g, out, gp, db, R, N,
-                       chunks, tickets, partials);
+                       p.L, p.chunks, tickets, partials);
   return check_launch("ocppo_relu_bias_grad");
 }
 
