@@ -118,6 +118,60 @@ __global__ __launch_bounds__(256) void gae_kernel(const float* __restrict__ rew,
   }
 }
 
+// Streaming form for wide rollouts (N >= 64K envs): one thread per env walks t = T-1 .. 0 with
+// the rows in registers, U rows of r/v/d loaded per batch before the U dependent steps run
+// (256 B per wave instruction: consecutive lanes = consecutive envs of a time row), advantages
+// and returns stored per batch. No LDS and no barriers, so every wave streams independently and
+// the occupancy (16 waves per CU at N = 262144) hides the latency; same arithmetic as gae_kernel,
+// op by op. T=128, N=262144 on MI355X: U = 1/2/4/8/16/32 -> 121/120/123/128/133/146 us, the LDS
+// form 143 us (tools/kernel_bench.py gae scaled).
+template <int U>
+__global__ __launch_bounds__(256) void gae_stream_kernel(const float* __restrict__ rew,
+                                                         const float* __restrict__ val,
+                                                         const float* __restrict__ don,
+                                                         const float* __restrict__ next_val,
+                                                         const float* __restrict__ next_done,
+                                                         int T, int64_t N, float g, float gl,
+                                                         float* __restrict__ adv,
+                                                         float* __restrict__ ret) {
+  const int64_t n = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float last = 0.f, carry_v = next_val[n], carry_d = next_done[n];
+  for (int t_hi = T; t_hi > 0; t_hi -= U) {
+    const int rows = t_hi < U ? t_hi : U;
+    float r[U], v[U], d[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      if (k < rows) {
+        const size_t gi = static_cast<size_t>(t_hi - 1 - k) * N + n;
+        r[k] = rew[gi];
+        v[k] = val[gi];
+        d[k] = don[gi];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      if (k < rows) {
+        const float nnt = 1.0f - carry_d;
+        float delta = r[k] + (g * carry_v) * nnt;
+        delta = delta - v[k];
+        last = delta + (gl * nnt) * last;
+        r[k] = last;
+        carry_v = v[k];
+        carry_d = d[k];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      if (k < rows) {
+        const size_t gi = static_cast<size_t>(t_hi - 1 - k) * N + n;
+        adv[gi] = r[k];
+        ret[gi] = r[k] + v[k];
+      }
+    }
+  }
+}
+
 }  // namespace ocppo
 
 using namespace ocppo;
@@ -138,11 +192,8 @@ extern "C" int ocppo_gae(ocppo_stream_t stream, const float* rewards, const floa
   clear_stale_error();
   hipStream_t s = as_stream(stream);
   if (N >= 64 * 1024) {
-    constexpr int TILE = 256;
-    const int TC = 16;
-    const size_t lds = 3 * sizeof(float) * TC * TILE;
-    hipLaunchKernelGGL(gae_kernel<TILE>, dim3(ceil_div(N, TILE)), dim3(256), lds, s, rewards,
-                       values, dones, next_value, next_done, (int)T, N, TC, g, gl, advantages,
+    hipLaunchKernelGGL(gae_stream_kernel<2>, dim3(ceil_div(N, 256)), dim3(256), 0, s, rewards,
+                       values, dones, next_value, next_done, (int)T, N, g, gl, advantages,
                        returns);
   } else {
     constexpr int TILE = 64;
