@@ -121,6 +121,7 @@ class Args:
     prefetch_shuffle: bool = True  # shuffle (+ frame plan) of the next iteration while the GPU runs
     dp_overlap: bool = True  # DP: all-reduce the decoder-side gradients during the encoder backward
     conv_channels_last: bool = True  # pixel NatureCNN in NHWC (MIOpen NHWC kernels, no transposes)
+    eval_episodes: int = 0  # after training: evaluate() episodes (the reference runs 10 when tracking)
     conv_benchmark: bool = False  # cudnn.benchmark (MIOpen Find) for the NatureCNN convolutions
 
 

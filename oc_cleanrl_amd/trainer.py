@@ -618,6 +618,19 @@ def run(args: Args, device=None, rank: int = 0, world_size: int = 1) -> PPOTrain
     if rank == 0 and args.save_model:
         torch.save({"model_weights": _own_tensors(tr.agent.state_dict()), "args": asdict(args)},
                    run_dir / f"{args.exp_name}_final.cleanrl_model")
+    if rank == 0 and args.eval_episodes > 0:  # ppo_atari_oc.py:687-695 (FinalReward_* summary)
+        from .evals import evaluate, make_env
+
+        rewards = evaluate(tr.agent, make_env, args.eval_episodes, tr.dev, env_id=args.env_id,
+                           obs_mode=args.obs_mode, num_features=args.num_features,
+                           seed=args.seed + 10_000)
+        summ = {"eval/FinalReward_mean": float(np.mean(rewards)),
+                "eval/FinalReward_median": float(np.median(rewards)),
+                "eval/FinalReward_min": float(np.min(rewards)),
+                "eval/FinalReward_max": float(np.max(rewards)), "eval/returns": rewards}
+        tr.last_metrics.update({k: v for k, v in summ.items() if k != "eval/returns"})
+        if writer:
+            writer.write(json.dumps(summ) + "\n")
     if writer:
         writer.close()
     return tr

@@ -204,3 +204,24 @@ def test_nhwc_conv_act_matches_module_forward_and_grads(dev):
     gr2 = torch.autograd.grad(h2, ps, g)
     for a, b in zip(gr1, gr2):
         torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-5 * float(a.abs().max()))
+
+
+def test_eval_harness_generic_eval_semantics(dev):
+    """evaluate(agent, make_env, n, device) (generic_eval.py:7-29): n finished episodes'
+    returns, equal to a hand-rolled loop over the same env and the same sampling stream."""
+    from oc_cleanrl_amd.agents import make_agent
+    from oc_cleanrl_amd.evals import EvalEnv, evaluate, make_env
+
+    torch.manual_seed(0)
+    ag = make_agent("PPO_OBJ", (4, 12), 6, dev, (32, 64), (64,)).to(dev)
+    torch.manual_seed(1)
+    rets = evaluate(ag, make_env, 2, dev, env_id="ALE/Pong-v5", seed=3)
+    assert len(rets) == 2 and all(np.isfinite(r) for r in rets)
+    torch.manual_seed(1)
+    env = EvalEnv("ALE/Pong-v5", seed=3, device=dev)
+    obs, mine = env.reset(), []
+    with torch.no_grad():
+        while len(mine) < 2:
+            obs, fin = env.step(ag.get_action_and_value(obs)[0])
+            mine += fin
+    assert mine == rets
