@@ -280,6 +280,15 @@ OCPPO_API int ocppo_relu_bias_grad(ocppo_stream_t stream, const float* g, const 
                          float* gp, float* db, int64_t R, int64_t N, void* workspace,
                          size_t workspace_bytes);
 
+/* Two rollout Linear(+ReLU) layers in one launch (the PPObj encoder's first two layers on the
+ * newest frame of every env, architectures/ppo.py:60-84, under torch.no_grad()):
+ *   y[M, N2] = act2(act1(x[M, K1] @ w1[N1, K1]^T + b1) @ w2[N2, N1]^T + b2)
+ * K1 <= 64, N1 % 16 == 0 and N1 <= 512; x row stride ldx (>= K1), y row stride ldy (>= N2);
+ * w2 16-B aligned; b1 / b2 may be NULL. Same f32-MFMA arithmetic as ocppo_linear_act per layer. */
+OCPPO_API int ocppo_linear2_act(ocppo_stream_t stream, const float* x, int64_t ldx, const float* w1,
+                      const float* b1, const float* w2, const float* b2, float* y, int64_t ldy,
+                      int64_t M, int64_t N1, int64_t N2, int64_t K1, int relu1, int relu2);
+
 /* ---------------------------------------------------------------------------------------------
  * Frame-deduplicated PPObj minibatch encoder — replaces the per-slot encoder work inside
  * `agent.get_action_and_value(b_obs[mb_inds], ...)` of ppo_atari_oc.py:566 for the PPObj network

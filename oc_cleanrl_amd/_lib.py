@@ -53,6 +53,7 @@ SIGNATURES: dict[str, tuple[type, list]] = {
     "ocppo_gather_rows_cl": (I, [P, P, I, P, I64, I64, I64, P, I]),
     "ocppo_frame_cache_shift": (I, [P, P, P, I64, P, I64, I64, I64]),
     "ocppo_linear_act": (I, [P, P, I64, P, P, P, I64, I64, I64, I64, I]),
+    "ocppo_linear2_act": (I, [P, P, I64, P, P, P, P, P, I64, I64, I64, I64, I64, I, I]),
     "ocppo_relu_bias_grad_workspace_bytes": (SZ, [I64, I64]),
     "ocppo_relu_bias_grad": (I, [P, P, P, P, P, I64, I64, P, SZ]),
     "ocppo_bias_act": (I, [P, P, P, I64, I64, I]),

@@ -216,6 +216,28 @@ def linear_relu(x, lin: nn.Linear):
     return linear_act(x, lin, True)
 
 
+# The first two Linear->ReLU layers of a rollout-sized inference batch as ONE HIP launch
+# (ops.linear2_act): the first layer's K <= 64 makes recomputing its rows per output tile free.
+HIP_ROLLOUT_LINEAR2 = True
+
+
+def _pair_ok(x, l1: nn.Linear, l2: nn.Linear) -> bool:
+    if not (HIP_ROLLOUT_LINEAR2 and HIP_ROLLOUT_LINEAR) or torch.is_grad_enabled() or \
+            not x.is_cuda or x.dtype != torch.float32 or l1.bias is None or l2.bias is None:
+        return False
+    x2 = x.reshape(-1, x.shape[-1])
+    M, K = x2.shape
+    N1 = l1.out_features
+    return (M <= 256 and K <= 64 and N1 % 16 == 0 and N1 <= 512 and
+            (M == 1 or x2.stride(1) == 1) and l2.weight.data_ptr() % 16 == 0)
+
+
+def linear2_relu(x, l1: nn.Linear, l2: nn.Linear):
+    lead = x.shape[:-1]
+    y = ops.linear2_act(x.reshape(-1, x.shape[-1]), l1.weight, l1.bias, l2.weight, l2.bias)
+    return y.view(*lead, y.shape[-1])
+
+
 def fused_trunk(seq: nn.Sequential, x):
     """Run `seq` with every Linear→ReLU pair as one fused GEMM (same math, fewer launches) and
     every other biased Linear through the same path (so FlatAdam-owned grads are written in place,
@@ -226,7 +248,12 @@ def fused_trunk(seq: nn.Sequential, x):
         m = mods[i]
         fusable = (isinstance(m, nn.Linear) and m.bias is not None and x.is_cuda
                    and x.dtype == torch.float32)
-        if _conv_act_ok(x, m):
+        if (isinstance(m, nn.Linear) and i + 3 < len(mods) and isinstance(mods[i + 1], nn.ReLU)
+                and isinstance(mods[i + 2], nn.Linear) and isinstance(mods[i + 3], nn.ReLU)
+                and _pair_ok(x, m, mods[i + 2])):
+            x = linear2_relu(x, m, mods[i + 2])
+            i += 4
+        elif _conv_act_ok(x, m):
             relu = i + 1 < len(mods) and isinstance(mods[i + 1], nn.ReLU)
             x = _ConvAct.apply(x, m.weight, m.bias, m.stride, m.padding, relu)
             i += 2 if relu else 1

@@ -182,3 +182,174 @@ extern "C" int ocppo_linear_act(ocppo_stream_t stream, const float* x, int64_t l
     launch_linear<false>(s, vec, x, ldx, w, b, y, ldy, (int)M, (int)N, (int)K);
   return check_launch("ocppo_linear_act");
 }
+
+// ---- two Linear(+ReLU) layers in one launch: y = act2(act1(x W1^T + b1) W2^T + b2) ---------------
+// The first two PPObj encoder layers of the rollout's newest-frame encode (architectures/ppo.py:
+// 60-84: F -> 256 -> 512 at 128 rows per step): the first layer is tiny (K1 = F <= 64), so every
+// workgroup recomputes the 16 hidden rows its output tile needs (16 x N1 values, K1 MACs each) into
+// LDS instead of waiting for a second launch, then runs the second layer's 16x16 tile from LDS
+// (A operand, rows padded to N1 + 4 floats: conflict-free 16-B reads) and global W2 (B operand),
+// K = N1 split over the S waves and combined through LDS in wave order. One launch instead of
+// two on the rollout's dependent chain; same v_mfma_f32_16x16x4_f32 arithmetic as linear_rows.
+namespace ocppo {
+
+constexpr int kLin2MaxK1 = 64;
+constexpr int kLin2MaxN1 = 512;
+
+template <int S, bool RELU1, bool RELU2>
+__global__ __launch_bounds__(64 * S) void linear2_rows_kernel(
+    const float* __restrict__ x, int64_t ldx, const float* __restrict__ w1,
+    const float* __restrict__ b1, const float* __restrict__ w2, const float* __restrict__ b2,
+    float* __restrict__ y, int64_t ldy, int M, int N1, int N2, int K1, int ntm, int tiles) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int ldh = N1 + 4;
+  float* h1 = smem;                                                    // [16][ldh]
+  floatx4* red = reinterpret_cast<floatx4*>(smem + 16 * ldh);          // [S-1][64]
+  const int b = blockIdx.x;
+  const int per_xcd = (tiles + 7) / 8;
+  const int t = (b % 8) * per_xcd + b / 8;  // XCD-contiguous tile ranges (as linear_rows)
+  if (t >= tiles) return;
+  const int tm = t % ntm, tn = t / ntm;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int g = lane >> 4, c16 = lane & 15;
+  const int row = tm * 16 + c16;
+  const bool rok = row < M;
+  const float* xr = x + static_cast<int64_t>(rok ? row : 0) * ldx;
+
+  // every global operand of both phases is loaded up front (one round trip of latency): the x
+  // chunks, this wave's W1 rows (phase-1 tiles ct = wv, wv + S, ...) and its W2 K-chunks
+  const int nkc = (K1 + 15) / 16;
+  const int nct = N1 / 16;
+  const int col2 = tn * 16 + c16;
+  const bool cok = col2 < N2;
+  const float* w2r = w2 + static_cast<int64_t>(cok ? col2 : 0) * N1;
+  const int cpw = (nct + S - 1) / S;
+  const int c0 = wv * cpw;
+  const int c1 = c0 + cpw < nct ? c0 + cpw : nct;
+  constexpr int kMaxT = kLin2MaxN1 / 16 / S;  // phase-1 tiles and phase-2 chunks per wave
+  float4 a1[kLin2MaxK1 / 16];
+#pragma unroll
+  for (int kc = 0; kc < kLin2MaxK1 / 16; ++kc) {
+    const int k = kc * 16 + 4 * g;
+    a1[kc].x = (kc < nkc && rok && k + 0 < K1) ? xr[k + 0] : 0.f;
+    a1[kc].y = (kc < nkc && rok && k + 1 < K1) ? xr[k + 1] : 0.f;
+    a1[kc].z = (kc < nkc && rok && k + 2 < K1) ? xr[k + 2] : 0.f;
+    a1[kc].w = (kc < nkc && rok && k + 3 < K1) ? xr[k + 3] : 0.f;
+  }
+  float4 b2v[kMaxT];
+#pragma unroll
+  for (int q = 0; q < kMaxT; ++q) {
+    const int c = c0 + q;
+    b2v[q] = (c < c1 && cok) ? *reinterpret_cast<const float4*>(w2r + c * 16 + 4 * g)
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  // phase 1: h1[16][N1] = act1(x[16 rows] W1^T + b1)
+#pragma unroll
+  for (int q = 0; q < kMaxT; ++q) {
+    const int ct = wv + q * S;
+    if (ct < nct) {
+      const int col = ct * 16 + c16;  // W1 row of this lane's B operand
+      const float* wr = w1 + static_cast<int64_t>(col) * K1;
+      floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kc = 0; kc < kLin2MaxK1 / 16; ++kc) {
+        if (kc < nkc) {
+          const int k = kc * 16 + 4 * g;
+          float4 bb;
+          bb.x = k + 0 < K1 ? wr[k + 0] : 0.f;
+          bb.y = k + 1 < K1 ? wr[k + 1] : 0.f;
+          bb.z = k + 2 < K1 ? wr[k + 2] : 0.f;
+          bb.w = k + 3 < K1 ? wr[k + 3] : 0.f;
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[kc].x, bb.x, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[kc].y, bb.y, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[kc].z, bb.z, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[kc].w, bb.w, acc, 0, 0, 0);
+        }
+      }
+      const float bv = b1 ? b1[col] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = acc[r] + bv;
+        if (RELU1) v = fmaxf(v, 0.f);
+        h1[(4 * g + r) * ldh + col] = v;  // C layout: column lane & 15, rows 4 * (lane >> 4) + r
+      }
+    }
+  }
+  __syncthreads();
+
+  // phase 2: the 16x16 tile of y; K = N1 in 16-wide chunks split over the S waves
+  floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int q = 0; q < kMaxT; ++q) {
+    const int c = c0 + q;
+    if (c < c1) {
+      const float4 a = *reinterpret_cast<const float4*>(h1 + c16 * ldh + c * 16 + 4 * g);
+      const float4 bb = b2v[q];
+      floatx4& acc = (q & 1) ? acc1 : acc0;
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, bb.x, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, bb.y, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, bb.z, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, bb.w, acc, 0, 0, 0);
+    }
+  }
+  floatx4 acc = acc0 + acc1;
+  if (S > 1) {
+    if (wv > 0) red[(wv - 1) * 64 + lane] = acc;
+    __syncthreads();
+    if (wv > 0) return;
+#pragma unroll
+    for (int q = 0; q < S - 1; ++q) acc += red[q * 64 + lane];
+  }
+  if (!cok) return;
+  const float bv2 = b2 ? b2[col2] : 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int orow = tm * 16 + 4 * g + r;
+    if (orow < M) {
+      float v = acc[r] + bv2;
+      if (RELU2) v = fmaxf(v, 0.f);
+      y[static_cast<int64_t>(orow) * ldy + col2] = v;
+    }
+  }
+}
+
+template <bool R1, bool R2>
+static void launch_linear2(hipStream_t s, const float* x, int64_t ldx, const float* w1,
+                           const float* b1, const float* w2, const float* b2, float* y,
+                           int64_t ldy, int M, int N1, int N2, int K1) {
+  constexpr int S = 4;
+  const int ntm = (M + 15) / 16, ntn = (N2 + 15) / 16, tiles = ntm * ntn;
+  const size_t lds = sizeof(float) * 16 * (N1 + 4) + sizeof(floatx4) * 64 * (S - 1);
+  hipLaunchKernelGGL((linear2_rows_kernel<S, R1, R2>), dim3(8 * ((tiles + 7) / 8)), dim3(64 * S),
+                     lds, s, x, ldx, w1, b1, w2, b2, y, ldy, M, N1, N2, K1, ntm, tiles);
+}
+
+}  // namespace ocppo
+
+extern "C" int ocppo_linear2_act(ocppo_stream_t stream, const float* x, int64_t ldx,
+                                 const float* w1, const float* b1, const float* w2,
+                                 const float* b2, float* y, int64_t ldy, int64_t M, int64_t N1,
+                                 int64_t N2, int64_t K1, int relu1, int relu2) {
+  OCPPO_REQUIRE(M >= 0 && K1 >= 1 && K1 <= kLin2MaxK1 && N1 >= 16 && N1 % 16 == 0 &&
+                    N1 <= kLin2MaxN1 && N2 >= 1 && N2 <= INT32_MAX && M <= INT32_MAX,
+                "ocppo_linear2_act: bad sizes M=%lld K1=%lld N1=%lld N2=%lld (K1 <= 64, N1 %% 16 "
+                "== 0, N1 <= 512)", (long long)M, (long long)K1, (long long)N1, (long long)N2);
+  OCPPO_REQUIRE(ldx >= K1 && ldy >= N2, "ocppo_linear2_act: leading dimensions ldx=%lld ldy=%lld",
+                (long long)ldx, (long long)ldy);
+  if (M == 0) return OCPPO_OK;
+  OCPPO_REQUIRE(x && w1 && w2 && y, "ocppo_linear2_act: null pointer");
+  OCPPO_REQUIRE(reinterpret_cast<uintptr_t>(w2) % 16 == 0,
+                "ocppo_linear2_act: w2 must be 16-B aligned");
+  clear_stale_error();
+  hipStream_t s = as_stream(stream);
+  const int m = (int)M, n1 = (int)N1, n2 = (int)N2, k1 = (int)K1;
+  if (relu1 && relu2)
+    launch_linear2<true, true>(s, x, ldx, w1, b1, w2, b2, y, ldy, m, n1, n2, k1);
+  else if (relu1)
+    launch_linear2<true, false>(s, x, ldx, w1, b1, w2, b2, y, ldy, m, n1, n2, k1);
+  else if (relu2)
+    launch_linear2<false, true>(s, x, ldx, w1, b1, w2, b2, y, ldy, m, n1, n2, k1);
+  else
+    launch_linear2<false, false>(s, x, ldx, w1, b1, w2, b2, y, ldy, m, n1, n2, k1);
+  return check_launch("ocppo_linear2_act");
+}

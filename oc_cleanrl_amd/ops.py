@@ -406,6 +406,29 @@ def linear_act(x, weight, bias=None, relu: bool = False, out=None):
     return out
 
 
+def linear2_act(x, w1, b1, w2, b2, relu1: bool = True, relu2: bool = True, out=None):
+    """y = act2(act1(x @ w1.T + b1) @ w2.T + b2) in ONE launch for rollout-sized batches (no
+    autograd): x [M, K1] f32 (unit column stride, K1 <= 64), w1 [N1, K1], w2 [N2, N1]
+    (N1 % 16 == 0, N1 <= 512)."""
+    if x.dim() != 2 or x.stride(1) != 1:
+        raise ValueError("x must be [M, K1] with unit column stride")
+    M, K1 = x.shape
+    N1, N2 = w1.shape[0], w2.shape[0]
+    if w1.shape[1] != K1 or w2.shape[1] != N1:
+        raise ValueError(f"shapes: x {tuple(x.shape)}, w1 {tuple(w1.shape)}, w2 {tuple(w2.shape)}")
+    dev = x.device
+    f = torch.float32
+    if out is None:
+        out = torch.empty((M, N2), dtype=f, device=dev)
+    if x.dtype != f or x.device.type != "cuda":
+        raise ValueError("x must be a float32 GPU tensor")
+    call("ocppo_linear2_act", _stream(dev), x.data_ptr(), x.stride(0) if M > 1 else K1,
+         _check(w1, "w1", f, dev), _opt(b1, "b1", f, dev, N1), _check(w2, "w2", f, dev),
+         _opt(b2, "b2", f, dev, N2), _check(out, "out", f, dev, M * N2), N2, M, N1, N2, K1,
+         int(bool(relu1)), int(bool(relu2)))
+    return out
+
+
 # ---------------------------------------------------------------------------------------------
 # Linear(+ReLU) backward, elementwise part: threshold_backward + bias sum in one pass
 # (autograd of architectures/ppo.py:60-84 inside ppo_atari_oc.py:605)

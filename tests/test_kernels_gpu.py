@@ -811,3 +811,23 @@ def test_bias_act_equals_torch(ops, dev, relu):
     want = torch.relu(y + b) if relu else y + b
     ops.bias_act(y, b, relu)
     assert torch.equal(y, want)
+
+
+@pytest.mark.parametrize("M,K1,N1,N2,ldx", [(128, 12, 256, 512, 48), (128, 6, 256, 512, 6),
+                                           (7, 12, 64, 33, 12), (256, 64, 512, 1024, 64),
+                                           (1, 5, 16, 7, 5)])
+def test_linear2_act_vs_torch(ops, dev, M, K1, N1, N2, ldx):
+    """Two Linear+ReLU layers in one launch == the two layers in f64, to f32 rounding."""
+    torch.manual_seed(M + K1)
+    xb = torch.randint(0, 200, (M, ldx), device=dev).float()
+    x = xb[:, :K1]
+    w1, b1 = torch.randn(N1, K1, device=dev) * 0.1, torch.randn(N1, device=dev) * 0.1
+    w2, b2 = torch.randn(N2, N1, device=dev) * 0.05, torch.randn(N2, device=dev) * 0.1
+    y = ops.linear2_act(x, w1, b1, w2, b2)
+    h = torch.relu(x.double() @ w1.double().t() + b1.double())
+    ref = torch.relu(h @ w2.double().t() + b2.double())
+    scale = (torch.relu(x.double().abs() @ w1.double().abs().t() + b1.double().abs())
+             @ w2.double().abs().t()).max().item() + 1.0
+    assert (y.double() - ref).abs().max().item() <= 1e-5 * scale
+    y2 = ops.linear2_act(x, w1, b1, w2, b2)
+    assert torch.equal(y, y2)  # deterministic

@@ -51,3 +51,19 @@ for B in (256, 8192):
         g, xs, ws, None, (1, 1), (0, 0), (1, 1), False, (0, 0), 1, (False, True, False)))
     print(f"B={B}: fwd 8x8/s4 {t1:8.1f} us  s2d 2x2/s1 {t2:8.1f} us  (rel diff {err:.1e});"
           f"  dW {tw1:8.1f} vs {tw2:8.1f} us", flush=True)
+
+# conv1 at the rollout batch: eager launches vs the same launch replayed from a hipGraph
+x = (torch.randint(0, 256, (256, 4, 84, 84), device=dev).float() / 255).contiguous(memory_format=CL)
+f = lambda: torch.ops.aten.convolution(x, wc, None, (4, 4), (0, 0), (1, 1), False, (0, 0), 1)  # noqa: E731
+t_eager = timeit(f, 50)
+s = torch.cuda.Stream()
+s.wait_stream(torch.cuda.current_stream())
+with torch.cuda.stream(s):
+    f()
+torch.cuda.current_stream().wait_stream(s)
+gr = torch.cuda.CUDAGraph()
+with torch.cuda.graph(gr):
+    for _ in range(20):
+        f()
+t_graph = timeit(gr.replay, 5) / 20
+print(f"rollout conv1 B=256: eager {t_eager:.1f} us, graph-replayed {t_graph:.1f} us", flush=True)
