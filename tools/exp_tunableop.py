@@ -36,6 +36,9 @@ def timeit(fn, reps=20):
 
 
 tag = "tunable" if os.environ.get("PYTORCH_TUNABLEOP_ENABLED") == "1" else "default"
+if os.environ.get("OCPPO_BLAS"):  # "cublas" = rocBLAS, "cublaslt" = hipBLASLt on ROCm
+    torch.backends.cuda.preferred_blas_library(os.environ["OCPPO_BLAS"])
+    tag = os.environ["OCPPO_BLAS"]
 total = 0.0
 # rollout (M = 128 envs): fwd only, 128 steps per iteration
 for M, K, N, per_iter in [(128, 512, 1024, 128), (128, 1024, 512, 129), (128, 2048, 512, 129)]:
