@@ -20,7 +20,7 @@ from tools.kernel_bench import SIZES, make_case  # noqa: E402,F401
 
 KERNEL_SUBSTR = {
     "policy_head": "policy_head_fast_kernel",
-    "gae": "gae_kernel",
+    "gae": "ocppo::gae",  # gae_kernel (LDS) / gae_stream_kernel by width
     "ppo_loss_prepared": "ocppo::ppo_loss",  # _small / _vec / tile forms by size
     "rollout_store": "rollout_store_kernel",
     "gather": "gather_rows_kernel",
