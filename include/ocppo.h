@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define OCPPO_ABI_VERSION 3
+#define OCPPO_ABI_VERSION 4
 
 /* status codes */
 #define OCPPO_OK 0
@@ -372,11 +372,12 @@ OCPPO_API int ocppo_replay_sample(ocppo_stream_t stream, uint64_t seed, int64_t*
                                   const float* rb_rewards, const float* rb_dones, int64_t B,
                                   float* obs_out, float* next_obs_out, int64_t* actions_out,
                                   float* rewards_out, float* dones_out, int64_t* indices_out);
-/* step : device i64 global step; epsilon_out : device f32 or NULL */
+/* global step t = *step + step_offset (step : device i64, so a captured chunk of env steps
+ * reads one counter advanced once per chunk); epsilon_out : device f32 or NULL */
 OCPPO_API int ocppo_epsilon_greedy(ocppo_stream_t stream, const float* q, int64_t E, int64_t A,
-                                   uint64_t seed, const int64_t* step, double start_e,
-                                   double end_e, double duration, int64_t* actions,
-                                   float* epsilon_out);
+                                   uint64_t seed, const int64_t* step, int64_t step_offset,
+                                   double start_e, double end_e, double duration,
+                                   int64_t* actions, float* epsilon_out);
 /* q, q_next : [B, A] f32 (q_network(obs), target_network(next_obs)); dq : [B, A] = d loss / d q;
  * stats : [2] = {td_loss, mean(old_val)} (losses/td_loss, losses/q_values of :385-386)
  *   td = r + (f32(gamma) * max_a q_next) * (1 - d);  old = q[b, a_b];  loss = mean((td - old)^2) */

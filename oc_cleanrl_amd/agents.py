@@ -199,7 +199,9 @@ def _hip_linear_ok(x2, lin: nn.Linear) -> bool:
             x2.dtype != torch.float32 or (x2.shape[0] > 1 and x2.stride(1) != 1):
         return False
     M, K = x2.shape
-    return (K <= 64 and M <= 512) or (K <= 256 and M <= 128)
+    # M <= 8 (single-env acting, e.g. the DQN learner's epsilon-greedy forward): the library
+    # takes a copy-bias + GEMV + separate ReLU path there (3 launches)
+    return (K <= 64 and M <= 512) or (K <= 256 and M <= 128) or M <= 8
 
 
 def linear_act(x, lin: nn.Linear, relu: bool):

@@ -117,9 +117,9 @@ __global__ void counter_add_kernel(int64_t* counter, int64_t n) { counter[0] += 
 // envs; random actions uniform in [0, A), else argmax_j q[e, j] (first maximum, like torch).
 __global__ __launch_bounds__(256) void epsilon_greedy_kernel(
     const float* __restrict__ q, int64_t E, int A, uint64_t seed, const int64_t* __restrict__ step,
-    double start_e, double end_e, double duration, int64_t* __restrict__ actions,
-    float* __restrict__ eps_out) {
-  const int64_t t = step[0];
+    int64_t step_offset, double start_e, double end_e, double duration,
+    int64_t* __restrict__ actions, float* __restrict__ eps_out) {
+  const int64_t t = step[0] + step_offset;
   const double slope = (end_e - start_e) / duration;
   double eps = slope * static_cast<double>(t) + start_e;
   eps = eps > end_e ? eps : end_e;
@@ -273,9 +273,9 @@ extern "C" int ocppo_td_loss_fwd_bwd(ocppo_stream_t stream, const float* q, cons
 }
 
 extern "C" int ocppo_epsilon_greedy(ocppo_stream_t stream, const float* q, int64_t E, int64_t A,
-                                    uint64_t seed, const int64_t* step, double start_e,
-                                    double end_e, double duration, int64_t* actions,
-                                    float* epsilon_out) {
+                                    uint64_t seed, const int64_t* step, int64_t step_offset,
+                                    double start_e, double end_e, double duration,
+                                    int64_t* actions, float* epsilon_out) {
   OCPPO_REQUIRE(E >= 1 && A >= 1 && A <= INT32_MAX && duration > 0,
                 "ocppo_epsilon_greedy: bad sizes");
   OCPPO_REQUIRE(q && step && actions, "ocppo_epsilon_greedy: null pointer");
@@ -283,6 +283,6 @@ extern "C" int ocppo_epsilon_greedy(ocppo_stream_t stream, const float* q, int64
   int64_t g = ceil_div(E, 256);
   g = g < 1024 ? g : 1024;
   hipLaunchKernelGGL(epsilon_greedy_kernel, dim3(g), dim3(256), 0, as_stream(stream), q, E, (int)A,
-                     seed, step, start_e, end_e, duration, actions, epsilon_out);
+                     seed, step, step_offset, start_e, end_e, duration, actions, epsilon_out);
   return check_launch("ocppo_epsilon_greedy");
 }

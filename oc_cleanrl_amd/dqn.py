@@ -245,11 +245,11 @@ class DQNTrainer:
         """One global step (:345-372): act, step, store + VecNormalize, replay add."""
         a = self.args
         prev, nxt = self.stacks[self.cur], self.stacks[1 - self.cur]
-        self.step_dev.add_(1)
         with torch.no_grad():
             q = _q_forward(self.q, self.net_obs)
+        # global step = chunk base (step_dev, advanced once per chunk) + k + 1
         ops.epsilon_greedy(q, a.seed, self.step_dev, a.start_e, a.end_e, self.duration,
-                           self.actions, self.epsilon)
+                           self.actions, self.epsilon, step_offset=k + 1)
         self.env.step(self.actions, k)
         if a.vecnorm_reward:
             ops.rollout_store_vecnorm(self.env.frame, self.env.reward, self.env.done, prev, nxt,
@@ -286,6 +286,7 @@ class DQNTrainer:
         for k in range(tf):
             self._env_step(k)
         self.env.advance(tf)
+        self.step_dev.add_(tf)
         if train:
             self._train_step()
 
@@ -332,6 +333,7 @@ class DQNTrainer:
             self.global_step += 1
             self._env_step(0)
             self.env.advance(1)
+            self.step_dev.add_(1)
             gs = self.global_step
             if gs > a.learning_starts:
                 if gs % tf == 0:

@@ -757,13 +757,14 @@ class ReplayBuffer:
 
 
 def epsilon_greedy(q, seed: int, step, start_e: float, end_e: float, duration: float,
-                   actions_out=None, epsilon_out=None):
+                   actions_out=None, epsilon_out=None, step_offset: int = 0):
     E, A = q.shape
     dev = q.device
     if actions_out is None:
         actions_out = torch.empty(E, dtype=torch.int64, device=dev)
     call("ocppo_epsilon_greedy", _stream(dev), _check(q, "q", torch.float32, dev), E, A,
-         int(seed) & 0xFFFFFFFFFFFFFFFF, _check(step, "step", torch.int64, dev, 1), float(start_e),
+         int(seed) & 0xFFFFFFFFFFFFFFFF, _check(step, "step", torch.int64, dev, 1),
+         int(step_offset), float(start_e),
          float(end_e), float(duration), _check(actions_out, "actions", torch.int64, dev, E),
          _opt(epsilon_out, "epsilon_out", torch.float32, dev, 1))
     return actions_out
