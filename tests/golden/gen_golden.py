@@ -19,6 +19,9 @@ Fixtures:
   td_{name}.npz       dqn_atari_oc.py:378-382 (TD target, gathered Q, MSE loss) exec'd with stub
                       Q / target networks, plus d loss / d q by autograd
   ppobj_small.npz     a small PPObj's state_dict + input + reference outputs
+  update_2mb.npz      two consecutive minibatch updates of the reference block :566-610 (forward,
+                      loss, backward, clip_grad_norm_, Adam) on a small PPObj: the state_dict
+                      before, after the first and after the second update, and both grad norms
   init_{name}.json    per-parameter checksums of seeded default-size agents + outputs on a fixed
                       input (pins layer order, state-dict keys and orthogonal init order)
 
@@ -242,6 +245,47 @@ def gen_td(name, B, A, seed):
                         q_values=ns["old_val"].mean().item(), dq=q.grad.numpy())
 
 
+def gen_update(B=512, M=256, F=6, A=6, seed=21):
+    """Two minibatch updates (one epoch of 2 minibatches) through the reference's update block,
+    with its Adam (lr 2.5e-4, eps 1e-5) and clip_grad_norm_(0.5): the whole learner step."""
+    torch.manual_seed(seed)
+    rng = np.random.default_rng(seed)
+    agent = PPObj(Envs((4, F), A), "cpu", (32, 64), (32,))
+    b_obs = torch.from_numpy(rng.integers(0, 160, (B, 4, F)).astype(np.float32))
+    with torch.no_grad():
+        hid = agent.network(b_obs)
+        dist = torch.distributions.Categorical(logits=agent.actor(hid))
+        b_actions = dist.sample()
+        lp = dist.log_prob(b_actions)
+        val = agent.critic(hid).view(-1)
+    b_logprobs = lp + torch.from_numpy((rng.standard_normal(B) * 0.15).astype(np.float32))
+    b_values = val + torch.from_numpy((rng.standard_normal(B) * 0.3).astype(np.float32))
+    b_returns = val + torch.from_numpy((rng.standard_normal(B) * 1.0).astype(np.float32))
+    b_advantages = torch.from_numpy((rng.standard_normal(B) * 2.0).astype(np.float32))
+    perm = rng.permutation(B)
+    args = types.SimpleNamespace(clip_coef=0.1, norm_adv=True, clip_vloss=True, ent_coef=0.01,
+                                 vf_coef=0.5, max_grad_norm=0.5, track=False, minibatch_size=M)
+    optimizer = optim.Adam(agent.parameters(), lr=2.5e-4, eps=1e-5)
+    sds = [{k: v.detach().clone().numpy() for k, v in agent.state_dict().items()}]
+    gns = []
+    for start in (0, M):
+        ns = dict(torch=torch, nn=nn, np=np, agent=agent, args=args, optimizer=optimizer,
+                  b_obs=b_obs, b_actions=b_actions, b_logprobs=b_logprobs,
+                  b_advantages=b_advantages, b_returns=b_returns, b_values=b_values,
+                  mb_inds=perm[start:start + M], clipfracs=[], start=start)
+        exec(UPDATE_CODE, ns)
+        gns.append(float(ns["gn"]))
+        sds.append({k: v.detach().clone().numpy() for k, v in agent.state_dict().items()})
+    out = dict(b_obs=b_obs.numpy(), b_actions=b_actions.numpy().astype(np.int64),
+               b_logprobs=b_logprobs.numpy(), b_values=b_values.numpy(),
+               b_returns=b_returns.numpy(), b_advantages=b_advantages.numpy(),
+               perm=perm.astype(np.int64), M=M, grad_norms=np.array(gns, np.float64))
+    for i, sd in enumerate(sds):
+        for k, v in sd.items():
+            out[f"sd{i}::{k}"] = v
+    np.savez_compressed(OUT / "update_2mb.npz", **out)
+
+
 def main():
     torch.set_num_threads(8)
     gen_gae(16, 8, "synthetic", 1)
@@ -261,6 +305,7 @@ def main():
     gen_td("b32_a6", 32, 6, 11)
     gen_td("b256_a18", 256, 18, 12)
     gen_ppobj_small()
+    gen_update()
     gen_init("ppobj_f12_a6", lambda e: PPObj(e, "cpu", (256, 512, 1024, 512), (512,)), (4, 12), 6,
              1, 160.0)
     gen_init("ppodefault_a4", lambda e: PPODefault(e, "cpu"), (4, 84, 84), 4, 1, 255.0)

@@ -123,3 +123,45 @@ def test_td_loss_matches_reference(name):
     assert np.array_equal(td.view(np.uint32), z["td_target"].view(np.uint32))  # bit-exact
     np.testing.assert_allclose(stats, [z["loss"], z["q_values"]], rtol=1e-6)
     assert np.array_equal(dq.view(np.uint32), z["dq"].view(np.uint32))  # bit-exact
+
+
+def test_oracle_update_step_matches_reference_update_block():
+    """The oracle's loss backward + clip_grad_norm_ + Adam restatement, driving the same small
+    PPObj through autograd on CPU, reproduces two consecutive updates of the reference's own
+    update block (ppo_atari_oc.py:566-610; tests/golden/update_2mb.npz)."""
+    import torch
+
+    from oc_cleanrl_amd.agents import make_agent
+
+    z = golden("update_2mb.npz")
+    ag = make_agent("PPO_OBJ", (4, 6), 6, None, (32, 64), (32,))
+    sd = lambda i: {k.split("::", 1)[1]: torch.from_numpy(z[k]) for k in z  # noqa: E731
+                    if k.startswith(f"sd{i}::")}
+    ag.load_state_dict(sd(0))
+    params = list(ag.parameters())
+    n = sum(p.numel() for p in params)
+    m, v, step = np.zeros(n, np.float32), np.zeros(n, np.float32), 0
+    M = int(z["M"])
+    for i, start in enumerate((0, M)):
+        idx = z["perm"][start:start + M]
+        x = torch.from_numpy(z["b_obs"][idx])
+        logits, value = ag.actor(ag.network(x)), ag.critic(ag.network(x))
+        _, dl, dv = O.ppo_loss_fwd_bwd(logits.detach().numpy(), value.detach().numpy(),
+                                       z["b_actions"], z["b_logprobs"], z["b_advantages"],
+                                       z["b_returns"], z["b_values"], idx, clip_coef=0.1,
+                                       ent_coef=0.01, vf_coef=0.5, norm_adv=True, clip_vloss=True)
+        for p in params:
+            p.grad = None
+        torch.autograd.backward([logits, value],
+                                [torch.from_numpy(dl), torch.from_numpy(dv).view(-1, 1)])
+        flat_p = np.concatenate([p.detach().numpy().ravel() for p in params])
+        flat_g = np.concatenate([p.grad.numpy().ravel() for p in params])
+        flat_p, m, v, step, total = O.clip_adam_step(flat_p, flat_g, m, v, step, 2.5e-4)
+        np.testing.assert_allclose(total, z["grad_norms"][i], rtol=1e-5)
+        off = 0
+        with torch.no_grad():
+            for p in params:
+                p.copy_(torch.from_numpy(flat_p[off:off + p.numel()]).view_as(p))
+                off += p.numel()
+        for k, ref in sd(i + 1).items():
+            np.testing.assert_allclose(ag.state_dict()[k].numpy(), ref.numpy(), rtol=0, atol=2e-7)

@@ -225,3 +225,43 @@ def test_eval_harness_generic_eval_semantics(dev):
             obs, fin = env.step(ag.get_action_and_value(obs)[0])
             mine += fin
     assert mine == rets
+
+
+def test_two_minibatch_updates_match_reference_golden(dev):
+    """The whole learner step against the reference's own update block (ppo_atari_oc.py:566-610,
+    exec'd with a real PPObj, torch Adam and clip_grad_norm_; tests/golden/update_2mb.npz): our
+    fused-trunk forward, HIP fused loss, autograd into the flat buffer and HIP clip + Adam give
+    the reference's parameters after each of two consecutive minibatch updates."""
+    from conftest import golden
+    from oc_cleanrl_amd import ops
+    from oc_cleanrl_amd.agents import make_agent
+
+    z = golden("update_2mb.npz")
+    ag = make_agent("PPO_OBJ", (4, 6), 6, dev, (32, 64), (32,)).to(dev)
+    sd = lambda i: {k.split("::", 1)[1]: torch.from_numpy(z[k]) for k in z  # noqa: E731
+                    if k.startswith(f"sd{i}::")}
+    ag.load_state_dict(sd(0))
+    opt = ops.FlatAdam(ag.parameters(), lr=2.5e-4, eps=1e-5, max_grad_norm=0.5)
+    T = lambda k, dt=None: torch.from_numpy(z[k]).to(dev) if dt is None else \
+        torch.from_numpy(z[k]).to(dev, dt)  # noqa: E731
+    b_obs, acts = T("b_obs"), T("b_actions")
+    lp, adv, ret, val = T("b_logprobs"), T("b_advantages"), T("b_returns"), T("b_values")
+    perm, M = T("perm"), int(z["M"])
+    for i, start in enumerate((0, M)):
+        idx = perm[start:start + M].contiguous()
+        logits, value = ag.logits_and_value(ops.gather_rows(b_obs, idx))
+        _, dl, dv = ops.ppo_loss_fwd_bwd(logits.detach(), value.detach().view(-1), acts, lp, adv,
+                                         ret, val, mb_inds=idx, clip_coef=0.1, ent_coef=0.01,
+                                         vf_coef=0.5, norm_adv=True, clip_vloss=True)
+        torch.autograd.backward([logits, value], [dl, dv.view(-1, 1)])
+        gn = float(torch.linalg.vector_norm(opt.grads.double()))
+        assert abs(gn - z["grad_norms"][i]) <= 1e-5 * z["grad_norms"][i]
+        opt.step()
+        # Adam normalises each gradient element (m / (sqrt(v) + eps)): where |g| is near eps the
+        # step is sensitive to the f32 summation order of g (MFMA / split-K vs the reference's
+        # CPU GEMMs), so the bound is 1 % of one step (lr), and almost every element is exact
+        # to 2e-7
+        for k, ref in sd(i + 1).items():
+            got = ag.state_dict()[k].cpu()
+            torch.testing.assert_close(got, ref, rtol=0, atol=0.01 * 2.5e-4)
+            assert float(((got - ref).abs() > 2e-7).float().mean()) < 0.01
