@@ -19,7 +19,7 @@ Fixtures:
   td_{name}.npz       dqn_atari_oc.py:378-382 (TD target, gathered Q, MSE loss) exec'd with stub
                       Q / target networks, plus d loss / d q by autograd
   ppobj_small.npz     a small PPObj's state_dict + input + reference outputs
-  update_2mb.npz      two consecutive minibatch updates of the reference block :566-610 (forward,
+  update_2mb[_cnn].npz two consecutive minibatch updates of the reference block :566-610 (forward,
                       loss, backward, clip_grad_norm_, Adam) on a small PPObj: the state_dict
                       before, after the first and after the second update, and both grad norms
   init_{name}.json    per-parameter checksums of seeded default-size agents + outputs on a fixed
@@ -245,13 +245,18 @@ def gen_td(name, B, A, seed):
                         q_values=ns["old_val"].mean().item(), dq=q.grad.numpy())
 
 
-def gen_update(B=512, M=256, F=6, A=6, seed=21):
+def gen_update(B=512, M=256, F=6, A=6, seed=21, pixels=False, name="update_2mb"):
     """Two minibatch updates (one epoch of 2 minibatches) through the reference's update block,
-    with its Adam (lr 2.5e-4, eps 1e-5) and clip_grad_norm_(0.5): the whole learner step."""
+    with its Adam (lr 2.5e-4, eps 1e-5) and clip_grad_norm_(0.5): the whole learner step.
+    pixels: the NatureCNN (PPODefault) on u8-valued 4x84x84 stacks instead of a small PPObj."""
     torch.manual_seed(seed)
     rng = np.random.default_rng(seed)
-    agent = PPObj(Envs((4, F), A), "cpu", (32, 64), (32,))
-    b_obs = torch.from_numpy(rng.integers(0, 160, (B, 4, F)).astype(np.float32))
+    if pixels:
+        agent = PPODefault(Envs((4, 84, 84), A), "cpu")
+        b_obs = torch.from_numpy(rng.integers(0, 256, (B, 4, 84, 84)).astype(np.float32))
+    else:
+        agent = PPObj(Envs((4, F), A), "cpu", (32, 64), (32,))
+        b_obs = torch.from_numpy(rng.integers(0, 160, (B, 4, F)).astype(np.float32))
     with torch.no_grad():
         hid = agent.network(b_obs)
         dist = torch.distributions.Categorical(logits=agent.actor(hid))
@@ -280,10 +285,24 @@ def gen_update(B=512, M=256, F=6, A=6, seed=21):
                b_logprobs=b_logprobs.numpy(), b_values=b_values.numpy(),
                b_returns=b_returns.numpy(), b_advantages=b_advantages.numpy(),
                perm=perm.astype(np.int64), M=M, grad_norms=np.array(gns, np.float64))
+    big = 1 << 16  # parameters above this size: a fixed sample of elements (keeps the file small)
+    pick = {}
     for i, sd in enumerate(sds):
         for k, v in sd.items():
-            out[f"sd{i}::{k}"] = v
-    np.savez_compressed(OUT / "update_2mb.npz", **out)
+            if pixels and i == 0:  # sd0 is the seeded init: checksums only (the test re-creates it)
+                out[f"sum0::{k}"] = np.array([v.astype(np.float64).sum(),
+                                              (v.astype(np.float64) ** 2).sum()])
+                continue
+            if v.size > big:
+                if k not in pick:
+                    pick[k] = np.sort(rng.choice(v.size, 4096, replace=False)).astype(np.int64)
+                    out[f"pick::{k}"] = pick[k]
+                out[f"sd{i}::{k}"] = v.reshape(-1)[pick[k]]
+            else:
+                out[f"sd{i}::{k}"] = v
+    if pixels:
+        out["b_obs"] = b_obs.numpy().astype(np.uint8)  # exact: integer pixel values
+    np.savez_compressed(OUT / f"{name}.npz", **out)
 
 
 def main():
@@ -306,6 +325,7 @@ def main():
     gen_td("b256_a18", 256, 18, 12)
     gen_ppobj_small()
     gen_update()
+    gen_update(B=32, M=16, A=4, seed=22, pixels=True, name="update_2mb_cnn")
     gen_init("ppobj_f12_a6", lambda e: PPObj(e, "cpu", (256, 512, 1024, 512), (512,)), (4, 12), 6,
              1, 160.0)
     gen_init("ppodefault_a4", lambda e: PPODefault(e, "cpu"), (4, 84, 84), 4, 1, 255.0)

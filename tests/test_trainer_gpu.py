@@ -265,3 +265,49 @@ def test_two_minibatch_updates_match_reference_golden(dev):
             got = ag.state_dict()[k].cpu()
             torch.testing.assert_close(got, ref, rtol=0, atol=0.01 * 2.5e-4)
             assert float(((got - ref).abs() > 2e-7).float().mean()) < 0.01
+
+
+def test_two_minibatch_updates_match_reference_golden_naturecnn(dev):
+    """The NatureCNN learner step (channels_last agent, NHWC u8 gather with NormalizeImg folded
+    in, _ConvAct convolutions, HIP loss, clip + Adam) against two updates of the reference's
+    update block with PPODefault (tests/golden/update_2mb_cnn.npz; the 3136->512 weight is
+    compared on a fixed sample of 4096 elements)."""
+    from conftest import golden
+    from oc_cleanrl_amd import ops
+    from oc_cleanrl_amd.agents import make_agent
+
+    z = golden("update_2mb_cnn.npz")
+    torch.manual_seed(22)  # the fixture's seeded reference init, re-created (pinned by checksums)
+    ag = make_agent("PPO", (4, 84, 84), 4).to(dev)
+    for k, v in ag.state_dict().items():
+        s = z[f"sum0::{k}"]
+        vd = v.double()
+        # init runs on the host CPU: its LAPACK QR (orthogonal_) differs from the fixture
+        # machine's in the last bits, hence the same tolerance as test_models_cpu's init check
+        np.testing.assert_allclose(float(vd.sum()), s[0], rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(float((vd ** 2).sum()), s[1], rtol=1e-6)
+    ag = ag.to(memory_format=torch.channels_last)
+    opt = ops.FlatAdam(ag.parameters(), lr=2.5e-4, eps=1e-5, max_grad_norm=0.5)
+    T = lambda k: torch.from_numpy(z[k]).to(dev)  # noqa: E731
+    b_obs, acts = T("b_obs"), T("b_actions")
+    lp, adv, ret, val = T("b_logprobs"), T("b_advantages"), T("b_returns"), T("b_values")
+    perm, M = T("perm"), int(z["M"])
+    for i, start in enumerate((0, M)):
+        idx = perm[start:start + M].contiguous()
+        x = torch.empty((M, 4, 84, 84), device=dev, memory_format=torch.channels_last)
+        ops.gather_rows(b_obs, idx, x, scale255=True)
+        logits, value = ag.logits_and_value(x, prescaled=True)
+        _, dl, dv = ops.ppo_loss_fwd_bwd(logits.detach(), value.detach().view(-1), acts, lp, adv,
+                                         ret, val, mb_inds=idx, clip_coef=0.1, ent_coef=0.01,
+                                         vf_coef=0.5, norm_adv=True, clip_vloss=True)
+        opt.zero_grad()  # conv grads are accumulated by autograd (not written in place)
+        torch.autograd.backward([logits, value], [dl, dv.view(-1, 1)])
+        gn = float(torch.linalg.vector_norm(opt.grads.double()))
+        assert abs(gn - z["grad_norms"][i]) <= 1e-4 * z["grad_norms"][i]
+        opt.step()
+        for k, v in ag.state_dict().items():
+            got = v.detach().cpu().contiguous().view(-1)
+            ref = torch.from_numpy(z[f"sd{i + 1}::{k}"]).view(-1)
+            if f"pick::{k}" in z:
+                got = got[torch.from_numpy(z[f"pick::{k}"])]
+            torch.testing.assert_close(got, ref, rtol=0, atol=0.01 * 2.5e-4)

@@ -21,9 +21,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--set", action="append", default=[])
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--config", type=int, default=2, choices=(2, 3))
     o = ap.parse_args()
-    args = Args(env_id="ALE/Pong-v5", obs_mode="obj", architecture="PPO_OBJ", num_envs=128,
-                num_steps=128, num_features=12, total_timesteps=10_000_000, save_model=False)
+    if o.config == 3:
+        args = Args(env_id="ALE/Breakout-v5", obs_mode="dqn", architecture="PPO", num_envs=256,
+                    num_steps=128, total_timesteps=10_000_000, save_model=False,
+                    torch_deterministic=False)
+    else:
+        args = Args(env_id="ALE/Pong-v5", obs_mode="obj", architecture="PPO_OBJ", num_envs=128,
+                    num_steps=128, num_features=12, total_timesteps=10_000_000, save_model=False)
     for kv in o.set:
         k, v = kv.split("=", 1)
         cur = getattr(args, k)
