@@ -13,8 +13,10 @@
 // rows), sums its rows in a fixed order, combines waves and row-lanes through LDS in a fixed
 // order and publishes its partial column sums with write-through (sc1) stores; the last
 // workgroup of a stripe to arrive on the stripe's ticket (one 128-B line per stripe) sums the
-// `chunks` partials of each column in chunk order (32 loads in flight). rb_plan picks L, the
-// stripes and the chunks so a launch has >= 256 workgroups where the rows allow it. Hand-off per
+// `chunks` partials of each column: the 256 threads split the chunks into 256/(4L) ordered groups
+// per column (32 loads in flight each), then add the group sums in group order. rb_plan picks L,
+// the stripes and the chunks (<= 64 for wide N) so a launch has >= 512 workgroups where the rows
+// allow it (tools/exp_relu_bias.py: chunk caps 16 / 32 / 64 / 128 measured, 64 best). Hand-off per
 // MI355X_MICROARCH.md "Valid forms" row 1 (sc1 stores, every storing wave's vmcnt(0), barrier,
 // one agent-scope atomic add; the last arriver reads with sc1 loads). Tickets re-arm themselves.
 // Roofline: HBM / Infinity-Cache stream, 12 B per element (relu) or 4 B (no relu) + 4 B per
@@ -25,6 +27,10 @@ namespace ocppo {
 
 constexpr int kRbMaxStripes = 64;
 constexpr int kRbMaxChunks = 512;
+#ifndef OCPPO_RB_CHUNKS
+#define OCPPO_RB_CHUNKS 64
+#endif
+constexpr int kRbChunks = OCPPO_RB_CHUNKS;  // wide-N chunk cap
 constexpr size_t kRbTicketBytes = kRbMaxStripes * 128;
 
 // Launch plan: L lanes per row (4 columns each: a stripe is 4L columns, 64/L rows per wave
@@ -49,10 +55,11 @@ inline RbPlan rb_plan(int64_t R, int64_t N) {
     p.chunks = static_cast<int>(c < 1 ? 1 : c);
     return p;
   }
-  // <= 128 chunks per stripe (the last arriver's chunk-order sum stays short); narrower stripes
-  // until the launch has >= 256 workgroups (one per CU) when the rows allow it
-  const int64_t c = by_rows < 128 ? by_rows : 128;
-  while (static_cast<int64_t>(p.stripes) * c < 256 && p.L > 16) {
+  // <= kRbChunks chunks per stripe (the last arriver's loads of a column are ONE batch in flight
+  // per thread group); narrower stripes (down to 8 lanes = 32 columns, 128-B row pieces) until the
+  // launch has >= 512 workgroups (two per CU) when the rows allow it
+  const int64_t c = by_rows < kRbChunks ? by_rows : kRbChunks;
+  while (static_cast<int64_t>(p.stripes) * c < 512 && p.L > 8) {
     const int L2 = p.L / 2;
     const int s2 = static_cast<int>((N + 4 * L2 - 1) / (4 * L2));
     if (s2 > kRbMaxStripes) break;
@@ -72,6 +79,7 @@ __global__ __launch_bounds__(256) void relu_bias_grad_kernel(const float* __rest
                                                              unsigned* __restrict__ tickets,
                                                              float* __restrict__ partials) {
   __shared__ float4 red[4][64];
+  __shared__ float tail[256];
   __shared__ int s_last;
   const int SW = 4 * L;  // columns per stripe
   const int nstripes = static_cast<int>((N + SW - 1) / SW);
@@ -145,23 +153,36 @@ __global__ __launch_bounds__(256) void relu_bias_grad_kernel(const float* __rest
   }
   __syncthreads();
   if (!s_last) return;
-  if (mine) {
-    // chunk order; 32 loads in flight per batch (one round trip each), summed in order
+  // the 256 threads as 256/SW groups of the stripe's SW columns: group gi sums chunks
+  // [gi*cpg, (gi+1)*cpg) of its column in chunk order (32 loads in flight per batch), then the
+  // groups' sums are added in group order -- a fixed order, so db is deterministic
+  {
+    const int NG = 256 / SW;
+    const int jj = threadIdx.x % SW, gi = threadIdx.x / SW;
+    const int64_t colj = static_cast<int64_t>(stripe) * SW + jj;
+    const int cpg = (chunks + NG - 1) / NG;
+    const int cb = gi * cpg;
+    const int ce = cb + cpg < chunks ? cb + cpg : chunks;
     float s = 0.f;
-    int c = 0;
-    for (; c + 32 <= chunks; c += 32) {
-      float v[32];
+    if (colj < N) {
+      for (int c = cb; c < ce; c += 32) {
+        float v[32];
 #pragma unroll
-      for (int k = 0; k < 32; ++k)
-        v[k] = __hip_atomic_load(&partials[static_cast<int64_t>(c + k) * N + col],
-                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int k = 0; k < 32; ++k)
+          v[k] = c + k < ce ? __hip_atomic_load(&partials[static_cast<int64_t>(c + k) * N + colj],
+                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                            : 0.f;
 #pragma unroll
-      for (int k = 0; k < 32; ++k) s += v[k];
+        for (int k = 0; k < 32; ++k) s += v[k];
+      }
     }
-    for (; c < chunks; ++c)
-      s += __hip_atomic_load(&partials[static_cast<int64_t>(c) * N + col], __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-    db[col] = s;
+    tail[threadIdx.x] = s;
+    __syncthreads();
+    if (gi == 0 && colj < N) {
+      float t = tail[jj];
+      for (int g2 = 1; g2 < NG; ++g2) t += tail[g2 * SW + jj];
+      db[colj] = t;
+    }
   }
   if (threadIdx.x == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
