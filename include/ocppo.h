@@ -275,6 +275,17 @@ OCPPO_API int ocppo_linear_act(ocppo_stream_t stream, const float* x, int64_t ld
  * y [R, N] f32, b [N] f32, both 16-B aligned, N % 4 == 0. */
 OCPPO_API int ocppo_bias_act(ocppo_stream_t stream, float* y, const float* b, int64_t R, int64_t N,
                    int relu);
+
+/* ---------------------------------------------------------------------------------------------
+ * Split-K combine of a weight gradient — replaces ATen's `sum(0)` after the batched (split-K)
+ * weight-gradient GEMM dW = g'^T x the build runs inside `loss.backward()` (ppo_atari_oc.py:605)
+ * for the Linear layers of architectures/ppo.py:60-84:
+ *   out[i] = part[0*n + i] + part[1*n + i] + ... + part[(S-1)*n + i]   (left fold, split order)
+ * part [S, n] f32, out [n] f32 (e.g. the parameter's view in the flat grad buffer); both 16-B
+ * aligned, n % 4 == 0, S in {1, 2, 4, 8, 16}. Deterministic.
+ * ------------------------------------------------------------------------------------------- */
+OCPPO_API int ocppo_sum_splits(ocppo_stream_t stream, const float* part, int64_t S, int64_t n,
+                     float* out);
 OCPPO_API size_t ocppo_relu_bias_grad_workspace_bytes(int64_t R, int64_t N);
 OCPPO_API int ocppo_relu_bias_grad(ocppo_stream_t stream, const float* g, const float* out,
                          float* gp, float* db, int64_t R, int64_t N, void* workspace,

@@ -57,6 +57,7 @@ SIGNATURES: dict[str, tuple[type, list]] = {
     "ocppo_relu_bias_grad_workspace_bytes": (SZ, [I64, I64]),
     "ocppo_relu_bias_grad": (I, [P, P, P, P, P, I64, I64, P, SZ]),
     "ocppo_bias_act": (I, [P, P, P, I64, I64, I]),
+    "ocppo_sum_splits": (I, [P, P, I64, I64, P]),
     "ocppo_frames_gather": (I, [P, P, I, I64, I64, I64, I64, P, I64, P]),
     "ocppo_frames_expand": (I, [P, P, I64, I64, P, P, I64, P, I64, I64, I64, P]),
     "ocppo_frames_scatter": (I, [P, P, I64, I64, P, I64, P, I64, P, I64, I64, I64, P]),

@@ -76,7 +76,13 @@ def _weight_grad(g, x, out=None):
     if s == 1:
         return torch.mm(g.t(), x, out=out) if out is not None else g.t().mm(x)
     part = torch.bmm(g.view(s, rows // s, n).transpose(1, 2), x.view(s, rows // s, k))
+    if out is not None and HIP_SUM_SPLITS and ops.sum_splits_ok(part, out):
+        return ops.timed(f"sum_splits_{s}x{n}x{k}", lambda: ops.sum_splits(part, out))
     return torch.sum(part, 0, out=out) if out is not None else part.sum(0)
+
+
+# Split-K partials of FlatAdam-owned weight gradients summed by one HIP pass (ops.sum_splits).
+HIP_SUM_SPLITS = True
 
 
 def _direct(p) -> bool:

@@ -483,6 +483,25 @@ def bias_act(y, b, relu: bool = True):
     return y
 
 
+def sum_splits_ok(part, out) -> bool:
+    return (part.is_cuda and part.dtype == torch.float32 and part.is_contiguous() and
+            out.is_contiguous() and out.dtype == torch.float32 and part.shape[0] in (1, 2, 4, 8, 16)
+            and part[0].numel() % 4 == 0 and part.data_ptr() % 16 == 0 and out.data_ptr() % 16 == 0)
+
+
+def sum_splits(part, out=None):
+    """out = part.sum(0) over the S split-K partial blocks of a weight gradient, in split order,
+    in one streaming pass (part [S, ...] f32 contiguous, S in {1, 2, 4, 8, 16})."""
+    S = part.shape[0]
+    dev = part.device
+    if out is None:
+        out = torch.empty(part.shape[1:], dtype=torch.float32, device=dev)
+    n = part[0].numel()
+    call("ocppo_sum_splits", _stream(dev), _check(part, "part", torch.float32, dev), S, n,
+         _check(out, "out", torch.float32, dev, n))
+    return out
+
+
 # ---------------------------------------------------------------------------------------------
 # Frame-deduplicated PPObj minibatch encoder (ppo_atari_oc.py:566 through architectures/ppo.py:60-84)
 # ---------------------------------------------------------------------------------------------

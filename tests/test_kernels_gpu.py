@@ -377,6 +377,22 @@ def test_linear_act_deterministic(ops, dev):
     assert torch.equal(y1, y2)
 
 
+@pytest.mark.parametrize("S,shape", [(8, (1024, 512)), (4, (512, 256)), (16, (256, 12)),
+                                     (8, (6, 512)), (1, (4, 4)), (2, (3, 4))])
+def test_sum_splits_is_the_split_order_fold(ops, dev, S, shape):
+    """Split-K combine: bit-identical to ((p0 + p1) + p2) + ... in f32, written into a view."""
+    g = torch.Generator(device=dev).manual_seed(S * 1000 + shape[0])
+    part = torch.randn((S,) + shape, device=dev, generator=g)
+    ref = part[0].clone()
+    for s in range(1, S):
+        ref = ref + part[s]
+    flat = torch.full((shape[0] * shape[1] + 8,), 5.0, device=dev)
+    out = flat[4:4 + shape[0] * shape[1]].view(shape)
+    ops.sum_splits(part, out)
+    assert torch.equal(out, ref)
+    assert torch.all(flat[:4] == 5.0) and torch.all(flat[-4:] == 5.0)
+
+
 def test_obs_reset(ops, dev):
     frame = torch.randint(0, 256, (9, 7056), dtype=torch.uint8, device=dev)
     out = torch.empty(9, 4, 7056, dtype=torch.bfloat16, device=dev)

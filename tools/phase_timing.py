@@ -32,8 +32,12 @@ def main():
                     num_steps=128, num_features=12, total_timesteps=10_000_000, save_model=False)
     for kv in o.set:
         k, v = kv.split("=", 1)
-        cur = getattr(args, k)
-        setattr(args, k, (v.lower() in ("1", "true", "yes")) if isinstance(cur, bool) else type(cur)(v))
+        obj = args
+        if k.startswith("agents."):  # a module switch, e.g. agents.HIP_SUM_SPLITS=0
+            from oc_cleanrl_amd import agents as obj
+            k = k.split(".", 1)[1]
+        cur = getattr(obj, k)
+        setattr(obj, k, (v.lower() in ("1", "true", "yes")) if isinstance(cur, bool) else type(cur)(v))
     args = finalize(args, 1)
     dev = torch.device("cuda:0")
     tr = PPOTrainer(args, dev, log=False)
