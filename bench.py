@@ -110,6 +110,11 @@ def main():
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--no-scaled", action="store_true", help="skip roofline_scaled")
+    ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
+                    help="torch.distributed backend for N > 1 (nccl = RCCL; gloo only for the "
+                         "N = 2 rehearsal with ranks sharing one GPU)")
+    ap.add_argument("--device-index", type=int, default=None,
+                    help="GPU of this rank (default LOCAL_RANK; 0 for the shared-GPU rehearsal)")
     ap.add_argument("--set", action="append", default=[], metavar="FIELD=VALUE",
                     help="override an Args field (experiments; e.g. --set rollout_frame_cache=0)")
     opt = ap.parse_args()
@@ -123,10 +128,13 @@ def main():
     if world != opt.gpus:
         if world == 1 and opt.gpus > 1:
             raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run")
-    device = torch.device(f"cuda:{local_rank}")
+    device = torch.device(f"cuda:{local_rank if opt.device_index is None else opt.device_index}")
     torch.cuda.set_device(device)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if opt.backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group("gloo")
 
     if opt.config == 3:
         envs = opt.envs_per_gpu or 256
