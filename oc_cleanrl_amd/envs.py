@@ -12,6 +12,7 @@ kernel (ops.rollout_store).
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 
 from . import ops
@@ -63,4 +64,131 @@ class SyntheticAtariEnv:
         """(sum of finished-episode returns, sum of lengths, count) since the last call."""
         s = self.ep_state[:, 2:5].sum(0, dtype=torch.float64).tolist()
         self.ep_state[:, 2:5].zero_()
+        return s
+
+
+class HostVecEnv:
+    """Host (CPU) vector env → the device rollout path: the env-step boundary of
+    cleanrl/ppo_atari_oc.py:506-514 for real emulators (OCAtari / ALE through
+    gymnasium's vector API, which this image lacks).
+
+    `envs` is any gymnasium-style vector env WITHOUT VecNormalize (reward normalisation runs on
+    the device, fused into the store kernel) and with the reference's frame stack:
+      reset(seed=...) -> (obs [N, W, *frame], info)
+      step(actions np.int64 [N]) -> (obs, reward [N], terminated [N], truncated [N], info)
+    Only the NEWEST frame obs[:, -1] crosses PCIe (the device store kernel rebuilds the stack,
+    and fills it with the first frame after a reset, which is what FrameStack returns then).
+
+    Per step: actions D2H into pinned memory (one stream sync: the env needs them), env.step on
+    the host, newest frame / reward / done (= terminated | truncated, :514) written into pinned
+    staging, then ONE async H2D copy of the staging block on the current stream, ordered before
+    the store kernel that consumes .frame / .reward / .done. The trainer captures the device work
+    between two host steps (upload + store of step t-1, act of step t, action copy) as one
+    hipGraph per step, so a rollout step costs one graph launch + one sync + the env's own step. RecordEpisodeStatistics-style
+    return/length counters run on the host over the raw rewards.
+    """
+
+    def __init__(self, envs, env_id: str, obs_mode: str, num_envs: int, seed: int, device,
+                 window: int = 4):
+        self.envs = envs
+        self.env_id = env_id
+        self.pixels = obs_mode == "dqn"
+        self.num_envs = N = int(num_envs)
+        self.n_actions = ACTION_COUNTS.get(env_id, 6)
+        na = getattr(getattr(envs, "single_action_space", None), "n", None)
+        if na is not None:
+            self.n_actions = int(na)
+        self.window = window
+        self.seed = int(seed)
+        self.device = torch.device(device)
+        self.frame_dtype = torch.uint8 if self.pixels else torch.float32
+        self._frame_shape = None
+        self.single_obs_shape = None
+        pin = self.device.type == "cuda"
+        self._act_host = torch.empty(N, dtype=torch.int64, pin_memory=pin)
+        self._run_ret = np.zeros(N, np.float64)
+        self._run_len = np.zeros(N, np.int64)
+        self._fin = [0.0, 0.0, 0.0]
+        self._pin = pin
+        self.frame = self.reward = self.done = None
+
+    def _alloc(self, obs):
+        obs = np.asarray(obs)
+        if obs.shape[0] != self.num_envs or obs.ndim < 3:
+            raise ValueError(f"host env obs must be [N={self.num_envs}, W, *frame], got {obs.shape}")
+        self.single_obs_shape = tuple(obs.shape[1:])
+        self._frame_shape = tuple(obs.shape[2:])
+        fe = int(np.prod(self._frame_shape))
+        self.frame_elems = fe
+        N = self.num_envs
+        # one pinned staging block: [frame bytes | reward f32 | done f32], one H2D per step
+        fb = N * fe * (1 if self.pixels else 4)
+        self._off_r = (fb + 255) // 256 * 256
+        self._off_d = self._off_r + 4 * N
+        nbytes = self._off_d + 4 * N
+        self._stage_host = torch.empty(nbytes, dtype=torch.uint8, pin_memory=self._pin)
+        self._stage_dev = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+
+        def views(buf):
+            fr = buf[:fb].view(self.frame_dtype).view(N, fe)
+            rw = buf[self._off_r:self._off_r + 4 * N].view(torch.float32)
+            dn = buf[self._off_d:self._off_d + 4 * N].view(torch.float32)
+            return fr, rw, dn
+
+        self._h_frame, self._h_reward, self._h_done = views(self._stage_host)
+        self.frame, self.reward, self.done = views(self._stage_dev)
+
+    def _stage(self, obs, reward, done):
+        obs = np.asarray(obs)
+        newest = obs.reshape(self.num_envs, obs.shape[1], -1)[:, -1]
+        np.copyto(self._h_frame.numpy(), newest, casting="unsafe")
+        np.copyto(self._h_reward.numpy(), np.asarray(reward, dtype=np.float64), casting="unsafe")
+        np.copyto(self._h_done.numpy(), np.asarray(done), casting="unsafe")
+
+    def upload(self):
+        """Staging block → device, async on the current stream (graph-capturable)."""
+        self._stage_dev.copy_(self._stage_host, non_blocking=True)
+
+    def fetch_actions(self, actions):
+        """Actions → pinned host memory, async on the current stream (graph-capturable)."""
+        self._act_host.copy_(actions, non_blocking=True)
+
+    def reset(self):
+        obs, _ = self.envs.reset(seed=self.seed)
+        if self.frame is None:
+            self._alloc(obs)
+        self._stage(obs, np.zeros(self.num_envs), np.zeros(self.num_envs))
+        self.upload()
+        return self.frame
+
+    def host_step(self):
+        """Wait for the queued action copy, step the host env, fill the staging block. The wait
+        also drains the previous upload (same stream, queued earlier), so the block is free."""
+        if self._pin:
+            torch.cuda.current_stream(self.device).synchronize()
+        act = self._act_host.numpy().copy()
+        obs, reward, term, trunc, _ = self.envs.step(act)
+        done = np.logical_or(term, trunc)
+        r = np.asarray(reward, dtype=np.float64)
+        self._run_ret += r
+        self._run_len += 1
+        if done.any():
+            self._fin[0] += float(self._run_ret[done].sum())
+            self._fin[1] += float(self._run_len[done].sum())
+            self._fin[2] += float(done.sum())
+            self._run_ret[done] = 0.0
+            self._run_len[done] = 0
+        self._stage(obs, r, done)
+
+    def step(self, actions, step_offset: int = 0):
+        """Eager form of one env step: fetch_actions + host_step + upload."""
+        self.fetch_actions(actions)
+        self.host_step()
+        self.upload()
+
+    def advance(self, n: int):
+        pass
+
+    def pop_episode_stats(self):
+        s, self._fin = self._fin, [0.0, 0.0, 0.0]
         return s

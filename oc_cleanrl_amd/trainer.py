@@ -35,7 +35,7 @@ import torch.nn as nn
 from . import frames, ops
 from .agents import NormalizeImg, PPObj, make_agent
 from .args import Args
-from .envs import SyntheticAtariEnv
+from .envs import HostVecEnv, SyntheticAtariEnv
 
 
 def storage_dtype(args: Args, pixels: bool) -> torch.dtype:
@@ -123,13 +123,15 @@ class KernelTimer:
 
 class PPOTrainer:
     def __init__(self, args: Args, device, rank: int = 0, world_size: int = 1,
-                 kernel_timing: bool = False, log: bool = True):
+                 kernel_timing: bool = False, log: bool = True, envs=None):
+        """envs: optional host (CPU) gymnasium-style vector env of this rank's local_num_envs
+        (envs.HostVecEnv documents the contract); None = the device-resident synthetic env."""
         self.args = args
         self.dev = torch.device(device)
         self.rank, self.world = rank, world_size
         self.log_enabled = log and rank == 0
         a = args
-        if a.backend != "Synthetic":
+        if envs is None and a.backend != "Synthetic":
             raise NotImplementedError(f"env backend {a.backend!r} needs ALE/OCAtari (not available);"
                                       " use --backend Synthetic")
         torch.use_deterministic_algorithms(a.torch_deterministic)
@@ -147,8 +149,14 @@ class PPOTrainer:
 
         self.N = a.local_num_envs
         self.T = a.num_steps
-        self.env = SyntheticAtariEnv(a.env_id, a.obs_mode, self.N, a.num_features, self.seed,
-                                     self.dev, a.buffer_window_size)
+        self.host_env = envs is not None
+        if self.host_env:
+            self.env = HostVecEnv(envs, a.env_id, a.obs_mode, self.N, self.seed, self.dev,
+                                  a.buffer_window_size)
+            self.env.reset()  # the obs shape comes from the env
+        else:
+            self.env = SyntheticAtariEnv(a.env_id, a.obs_mode, self.N, a.num_features, self.seed,
+                                         self.dev, a.buffer_window_size)
         self.pixels = self.env.pixels
         self.A = self.env.n_actions
         self.obs_shape = self.env.single_obs_shape
@@ -270,6 +278,7 @@ class PPOTrainer:
         self.g_rollout = None
         self.g_update: list = []
         self.g_low: list = []
+        self.g_host: list = []
         self.g_opt = None
         self.iteration = 0
         self.global_step = 0
@@ -278,7 +287,7 @@ class PPOTrainer:
 
     # ------------------------------------------------------------------------------------------
     def _reset_env(self):
-        frame = self.env.reset()
+        frame = self.env.frame if self.host_env else self.env.reset()
         ops.obs_reset(frame, self.obs[self.T], self.net_obs, scale255=self.prescale)
         self.dones[self.T].zero_()
 
@@ -301,7 +310,11 @@ class PPOTrainer:
         """One env step of the rollout (:500-514): network trunk (PyTorch) → fused HIP policy
         head (actor+critic GEMVs + Categorical sample, writes actions/logprobs/values rows) →
         env → fused HIP store (+ VecNormalize) of the next obs slot and reward/done rows."""
-        a = self.args
+        self._act(t)
+        self.timer.bracket("env_step", lambda: self.env.step(self.actions[t], t))
+        self._store(t)
+
+    def _act(self, t: int):
         ag = self.agent
         if self.fused_head:
             hidden = self._policy_hidden(t)
@@ -313,7 +326,9 @@ class PPOTrainer:
             self.timer.bracket("action_head", lambda: ops.categorical_sample(
                 logits, self.noise[t], self.actions[t], self.logprobs[t], None, value.view(-1),
                 self.values[t]))
-        self.timer.bracket("env_step", lambda: self.env.step(self.actions[t], t))
+
+    def _store(self, t: int):
+        a = self.args
         if a.vecnorm_reward:
             self.timer.bracket("rollout_store", lambda: ops.rollout_store_vecnorm(
                 self.env.frame, self.env.reward, self.env.done, self.obs[t], self.obs[t + 1],
@@ -324,30 +339,63 @@ class PPOTrainer:
                 self.env.frame, self.env.reward, self.env.done, self.obs[t], self.obs[t + 1],
                 self.net_obs, self.rewards[t], self.dones[t + 1], scale255=self.prescale))
 
-    def _rollout(self):
-        """Rollout (:500-530) + bootstrap + GAE (:533-547) + minibatch adv stats (:577-579)."""
+    def _rollout_begin(self):
+        T = self.T
+        self.obs[0].copy_(self.obs[T])
+        self.dones[0].copy_(self.dones[T])
+        self.noise.exponential_()
+
+    def _rollout_end(self):
+        """Bootstrap + GAE (:533-547) + minibatch adv stats (:577-579)."""
         a = self.args
         T = self.T
+        if self.frame_cache:
+            self.values[T].copy_(self.agent._head(self.agent.critic,
+                                                  self._policy_hidden(T)).view(-1))
+        else:
+            self.values[T].copy_(self.agent.get_value(self.net_obs, self.prescale).view(-1))
+        self.timer.bracket("gae", lambda: ops.gae(
+            self.rewards, self.values[:T], self.dones[:T], self.values[T], self.dones[T],
+            a.gamma, a.gae_lambda, self.advantages, self.returns))
+        # every minibatch's per-sample records in minibatch order + its adv (mean, std)
+        self.timer.bracket("mb_prepare", lambda: ops.minibatch_prepare(
+            self.perm_dev, self.M, self.actions.view(-1), self.logprobs.view(-1),
+            self.advantages.view(-1), self.returns.view(-1), self.values[:T].reshape(-1),
+            out=self.mb, with_stats=a.norm_adv))
+
+    def _rollout(self):
+        """Rollout (:500-530) + bootstrap + GAE (:533-547) + minibatch adv stats (:577-579)."""
         with torch.no_grad():
-            self.obs[0].copy_(self.obs[T])
-            self.dones[0].copy_(self.dones[T])
-            self.noise.exponential_()
-            for t in range(T):
+            self._rollout_begin()
+            for t in range(self.T):
                 self._rollout_step(t)
-            self.env.advance(T)
-            if self.frame_cache:
-                self.values[T].copy_(self.agent._head(self.agent.critic,
-                                                      self._policy_hidden(T)).view(-1))
+            self.env.advance(self.T)
+            self._rollout_end()
+
+    def _host_part(self, k: int):
+        """Device work between two host env steps (host env): part k uploads env step k-1's
+        staging block and stores it, then acts for step k and queues its actions' D2H copy; part
+        T ends the rollout. Each part is one hipGraph once captured."""
+        with torch.no_grad():
+            if k == 0:
+                self._rollout_begin()
             else:
-                self.values[T].copy_(self.agent.get_value(self.net_obs, self.prescale).view(-1))
-            self.timer.bracket("gae", lambda: ops.gae(
-                self.rewards, self.values[:T], self.dones[:T], self.values[T], self.dones[T],
-                a.gamma, a.gae_lambda, self.advantages, self.returns))
-            # every minibatch's per-sample records in minibatch order + its adv (mean, std)
-            self.timer.bracket("mb_prepare", lambda: ops.minibatch_prepare(
-                self.perm_dev, self.M, self.actions.view(-1), self.logprobs.view(-1),
-                self.advantages.view(-1), self.returns.view(-1), self.values[:T].reshape(-1),
-                out=self.mb, with_stats=a.norm_adv))
+                self.env.upload()
+                self._store(k - 1)
+            if k < self.T:
+                self._act(k)
+                self.env.fetch_actions(self.actions[k])
+            else:
+                self._rollout_end()
+
+    def _rollout_host(self):
+        for k in range(self.T + 1):
+            if self.g_host:
+                self.g_host[k].replay()
+            else:
+                self._host_part(k)
+            if k < self.T:
+                self.env.host_step()  # waits for part k's action copy, steps the CPU env
 
     def _forward_backward(self, j: int):
         """Minibatch j: gather, forward, fused loss, backward into the flat grad buffer."""
@@ -456,6 +504,7 @@ class PPOTrainer:
             torch.cuda.synchronize(self.dev)
             self.graphs_ready = False
             self.g_rollout, self.g_update, self.g_opt, self.g_low = None, [], None, []
+            self.g_host = []
         self.planner.cap = cap
         n = self.planner.size(cap)
         self.plan_host = torch.empty(n, dtype=torch.int32, pin_memory=True)
@@ -476,10 +525,20 @@ class PPOTrainer:
         """Capture the rollout and the update into hipGraphs (after one eager warm-up iteration,
         which has also created the Adam state)."""
         torch.cuda.synchronize(self.dev)
-        self.g_rollout = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_rollout):
-            self._rollout()
-        pool = self.g_rollout.pool()
+        self.g_rollout = None
+        pool = None
+        if not self.host_env:
+            self.g_rollout = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.g_rollout):
+                self._rollout()
+            pool = self.g_rollout.pool()
+        else:  # a host env steps between the parts: one graph per part
+            for k in range(self.T + 1):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=pool):
+                    self._host_part(k)
+                pool = pool if pool is not None else g.pool()
+                self.g_host.append(g)
         if not self.graph_update:
             pass
         elif self.world == 1:
@@ -488,12 +547,14 @@ class PPOTrainer:
                 with torch.cuda.graph(g, pool=pool):
                     self._update_epoch(e)
                 self.g_update.append(g)
+                pool = pool if pool is not None else g.pool()
         else:
             for j in range(self.E * self.nmb):
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, pool=pool):
                     self._forward_backward(j)
                 self.g_update.append(g)
+                pool = pool if pool is not None else g.pool()
                 if self.split:  # second backward phase: reads the cut tensors of graph j
                     g = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(g, pool=pool):
@@ -535,7 +596,9 @@ class PPOTrainer:
         use_graphs = a.cuda_graphs and self.iteration > 1
         if use_graphs and not self.graphs_ready:
             self._capture()
-        if self.graphs_ready:
+        if self.host_env:
+            self._rollout_host()
+        elif self.graphs_ready:
             self.g_rollout.replay()
         else:
             self._rollout()
