@@ -72,10 +72,14 @@ class HostVecEnv:
     cleanrl/ppo_atari_oc.py:506-514 for real emulators (OCAtari / ALE through
     gymnasium's vector API, which this image lacks).
 
-    `envs` is any gymnasium-style vector env WITHOUT VecNormalize (reward normalisation runs on
-    the device, fused into the store kernel) and with the reference's frame stack:
-      reset(seed=...) -> (obs [N, W, *frame], info)
-      step(actions np.int64 [N]) -> (obs, reward [N], terminated [N], truncated [N], info)
+    `envs` is the reference's SubprocVecEnv of make_env thunks (:411-413) WITHOUT the VecNormalize
+    of :414 (reward normalisation runs on the device, fused into the store kernel; a
+    reward-normalising wrapper is rejected), or any gymnasium vector env with the same frame
+    stack. Both APIs are accepted:
+      SB3 VecEnv (the reference's): reset() -> obs [N, W, *frame];
+        step(actions np.int64 [N]) -> (obs, reward [N], done [N], infos)   (:511)
+      gymnasium: reset(seed=...) -> (obs, info);
+        step(actions) -> (obs, reward, terminated, truncated, info)
     Only the NEWEST frame obs[:, -1] crosses PCIe (the device store kernel rebuilds the stack,
     and fills it with the first frame after a reset, which is what FrameStack returns then).
 
@@ -90,6 +94,9 @@ class HostVecEnv:
 
     def __init__(self, envs, env_id: str, obs_mode: str, num_envs: int, seed: int, device,
                  window: int = 4):
+        if getattr(envs, "norm_reward", False):
+            raise ValueError("pass the vector env without VecNormalize(norm_reward=True): the "
+                             "device store kernel applies the reward normalisation (:414)")
         self.envs = envs
         self.env_id = env_id
         self.pixels = obs_mode == "dqn"
@@ -154,7 +161,11 @@ class HostVecEnv:
         self._act_host.copy_(actions, non_blocking=True)
 
     def reset(self):
-        obs, _ = self.envs.reset(seed=self.seed)
+        try:
+            r = self.envs.reset(seed=self.seed)
+        except TypeError:  # SB3 VecEnv: reset() takes no seed (seeded per worker, :412)
+            r = self.envs.reset()
+        obs = r[0] if isinstance(r, tuple) and len(r) == 2 and isinstance(r[1], dict) else r
         if self.frame is None:
             self._alloc(obs)
         self._stage(obs, np.zeros(self.num_envs), np.zeros(self.num_envs))
@@ -167,8 +178,13 @@ class HostVecEnv:
         if self._pin:
             torch.cuda.current_stream(self.device).synchronize()
         act = self._act_host.numpy().copy()
-        obs, reward, term, trunc, _ = self.envs.step(act)
-        done = np.logical_or(term, trunc)
+        out = self.envs.step(act)
+        if len(out) == 5:  # gymnasium: terminated | truncated (:514)
+            obs, reward, term, trunc, _ = out
+            done = np.logical_or(term, trunc)
+        else:  # SB3 VecEnv: done already folds both, the env auto-resets
+            obs, reward, done, _ = out
+            done = np.asarray(done, dtype=bool)
         r = np.asarray(reward, dtype=np.float64)
         self._run_ret += r
         self._run_len += 1

@@ -64,3 +64,31 @@ def test_host_env_pixels_u8():
     fr = env.reset()
     assert fr.dtype == torch.uint8 and fr.shape == (N, 84 * 84)
     assert int(fr[1, 3 * 84 + 5]) == 7 and int(fr.sum()) == 14
+
+
+def test_host_env_sb3_api_and_vecnormalize_rejected():
+    """The reference's SubprocVecEnv API (:464, :511): reset() -> obs, step -> 4-tuple."""
+    import pytest
+
+    N, W, F = 2, 4, 3
+
+    class SB3Like:
+        def reset(self):
+            return np.ones((N, W, F), np.float32)
+
+        def step(self, actions):
+            return (np.full((N, W, F), 2, np.float32), np.array([1.0, -1.0]),
+                    np.array([True, False]), [{}, {}])
+
+    env = HostVecEnv(SB3Like(), "ALE/Pong-v5", "obj", N, 0, "cpu", W)
+    assert float(env.reset().sum()) == N * F
+    env.step(torch.tensor([0, 1]))
+    np.testing.assert_array_equal(env.done.numpy(), [1, 0])
+    np.testing.assert_array_equal(env.reward.numpy(), [1, -1])
+    assert env.pop_episode_stats() == [1.0, 1.0, 1.0]
+
+    class Normed(SB3Like):
+        norm_reward = True
+
+    with pytest.raises(ValueError, match="VecNormalize"):
+        HostVecEnv(Normed(), "ALE/Pong-v5", "obj", N, 0, "cpu", W)
