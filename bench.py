@@ -96,6 +96,12 @@ def relu_bias_grad_bytes(name: str):
     return R * N * (12 if relu else 4) + 4 * N
 
 
+def relu_bias_wgrad_bytes(name: str):
+    """relu_bias_wgrad_{R}x{N}x{K}: g + out f32 [R, N] and x f32 [R, K] in, dw [N, K] + db out."""
+    R, N, K = (int(v) for v in name[len("relu_bias_wgrad_"):].split("x"))
+    return R * N * 8 + R * K * 4 + N * (K + 1) * 4
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -182,7 +188,9 @@ def main():
         for name, us in tr.timer.measure().items():
             n = tr.timer.per_iter.get(name, 0)
             nbytes = kb.get(name) or (relu_bias_grad_bytes(name)
-                                      if name.startswith("relu_bias_grad_") else None)
+                                      if name.startswith("relu_bias_grad_") else
+                                      relu_bias_wgrad_bytes(name)
+                                      if name.startswith("relu_bias_wgrad_") else None)
             kernels[name] = {"mean_us": round(us, 3), "launches_per_iter": n,
                              "us_per_iter": round(us * n, 2)}
             if nbytes:

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define OCPPO_ABI_VERSION 4
+#define OCPPO_ABI_VERSION 5
 
 /* status codes */
 #define OCPPO_OK 0
@@ -290,6 +290,23 @@ OCPPO_API size_t ocppo_relu_bias_grad_workspace_bytes(int64_t R, int64_t N);
 OCPPO_API int ocppo_relu_bias_grad(ocppo_stream_t stream, const float* g, const float* out,
                          float* gp, float* db, int64_t R, int64_t N, void* workspace,
                          size_t workspace_bytes);
+
+/* ---------------------------------------------------------------------------------------------
+ * First-layer backward in ONE pass — replaces threshold_backward + the split-K weight-gradient
+ * GEMM + the bias sum autograd runs inside `loss.backward()` (ppo_atari_oc.py:605) for a
+ * Linear(+ReLU) layer whose input needs no gradient and has K <= 16 features (the PPObj
+ * encoder's first layer on the object frames, architectures/ppo.py:60-84):
+ *   gp[r, n] = out[r, n] <= 0 ? 0 : g[r, n]   (g itself when out == NULL; gp is not written)
+ *   db[n]    = sum_r gp[r, n]
+ *   dw[n, k] = sum_r gp[r, n] * x[r, k]        (dw [N, K] row-major, nn.Linear.weight layout)
+ * g/out [R, N] f32 row-major 16-B aligned, N % 4 == 0, N <= 16384; x [R, K] f32, row stride ldx;
+ * 1 <= K <= 16. Workspace 256-B aligned, >= ocppo_relu_bias_wgrad_workspace_bytes(R, N, K),
+ * ZEROED before its first use (tickets re-arm). Deterministic (fixed-order sums, f32 fma).
+ * ------------------------------------------------------------------------------------------- */
+OCPPO_API size_t ocppo_relu_bias_wgrad_workspace_bytes(int64_t R, int64_t N, int64_t K);
+OCPPO_API int ocppo_relu_bias_wgrad(ocppo_stream_t stream, const float* g, const float* out,
+                          const float* x, int64_t ldx, float* dw, float* db, int64_t R,
+                          int64_t N, int64_t K, void* workspace, size_t workspace_bytes);
 
 /* Two rollout Linear(+ReLU) layers in one launch (the PPObj encoder's first two layers on the
  * newest frame of every env, architectures/ppo.py:60-84, under torch.no_grad()):

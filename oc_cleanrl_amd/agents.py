@@ -111,6 +111,14 @@ class _LinearAct(torch.autograd.Function):
         db = None
         bias_done = False
         g = g.contiguous()
+        if FUSED_FIRST_LAYER_BWD and not ctx.needs_input_grad[0] and ctx.needs_input_grad[1] \
+                and ctx.needs_input_grad[2] and _direct(ctx.w) and _direct(ctx.b) and \
+                ops.relu_bias_wgrad_ok(g, x):
+            # input layer (no dX): ReLU-backward + bias grad + weight grad in one HIP pass
+            o = out if ctx.relu else None
+            ops.timed(f"relu_bias_wgrad_{g.shape[0]}x{g.shape[1]}x{x.shape[1]}",
+                      lambda: ops.relu_bias_wgrad(g, o, x, dw=ctx.w.grad, db=ctx.b.grad))
+            return None, None, None, None
         if FUSED_RELU_BIAS_GRAD and ctx.needs_input_grad[2] and _direct(ctx.b) and \
                 ops.relu_bias_grad_ok(g):
             # threshold_backward + bias sum in one HIP pass, bias grad written in place
@@ -138,6 +146,9 @@ class _LinearAct(torch.autograd.Function):
 
 # One-pass HIP ReLU-backward + bias gradient (ops.relu_bias_grad) for FlatAdam-owned biases.
 FUSED_RELU_BIAS_GRAD = True
+# Input layers with K <= 16 features (PPObj's first encoder layer): ReLU-backward, bias and
+# weight gradient in one HIP pass (ops.relu_bias_wgrad), gp never materialised.
+FUSED_FIRST_LAYER_BWD = True
 
 
 class _ConvAct(torch.autograd.Function):

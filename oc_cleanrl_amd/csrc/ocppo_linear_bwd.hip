@@ -322,3 +322,209 @@ extern "C" int ocppo_sum_splits(ocppo_stream_t stream, const float* part, int64_
   }
   return check_launch("ocppo_sum_splits");
 }
+
+// ---- first-layer backward in ONE pass: ReLU-backward + bias gradient + weight gradient -----------
+// For a Linear(+ReLU) layer whose input needs no gradient and has few features (the PPObj
+// encoder's first layer on the object frames, F = 6 / 12 -> 256, architectures/ppo.py:60-84,
+// inside loss.backward() of ppo_atari_oc.py:605) the elementwise pass and the weight-gradient GEMM
+// read the same rows, and gp is consumed by nothing else:
+//   gp[r, n] = out[r, n] <= 0 ? 0 : g[r, n]      (never written)
+//   db[n]    = sum_r gp[r, n]
+//   dw[n, k] = sum_r gp[r, n] * x[r, k]           (k < K <= 16)
+// Autograd runs threshold_backward (writes gp), a split-K GEMM over gp (a long K = R reduction
+// into a tiny [N, K] output: ~3 TFLOP/s) and a sum: 3 launches, gp written and read back. Here a
+// workgroup (stripe, chunk) owns 4L columns x a row range, each lane keeps 4 columns x (K + 1)
+// running sums (fmaf, rows in a fixed order), waves and row-lanes are combined through LDS in a
+// fixed order, partials published with sc1 stores, and the stripe's last arriver (ticket per
+// stripe, re-arming) sums the chunks in chunk order: deterministic, no data atomics.
+// Roofline: HBM stream, 8 B (relu; 4 B without) per element of g + 4K B per row of x.
+namespace ocppo {
+
+constexpr int kWgL = 4;             // lanes per row: 16-column stripes, 16 rows per wave instruction
+constexpr int kWgMaxChunks = 64;
+constexpr int kWgMaxStripes = 1024;  // N <= 16384
+constexpr size_t kWgTicketBytes = kWgMaxStripes * 128;
+
+inline int wg_chunks(int64_t R, int64_t N) {
+  const int64_t stripes = (N + 4 * kWgL - 1) / (4 * kWgL);
+  int64_t c = (512 + stripes - 1) / stripes;  // ~512 workgroups
+  if (c > kWgMaxChunks) c = kWgMaxChunks;
+  const int64_t by_rows = (R + 63) / 64;      // >= 64 rows per chunk
+  if (c > by_rows) c = by_rows;
+  return static_cast<int>(c < 1 ? 1 : c);
+}
+
+template <bool RELU, int KP>
+__global__ __launch_bounds__(256) void relu_bias_wgrad_kernel(
+    const float* __restrict__ g, const float* __restrict__ out, const float* __restrict__ x,
+    int64_t ldx, float* __restrict__ dw, float* __restrict__ db, int64_t R, int64_t N, int K,
+    int chunks, unsigned* __restrict__ tickets, float* __restrict__ partials) {
+  constexpr int L = kWgL, RP = 64 / L, SW = 4 * L, NV = KP + 1;
+  __shared__ float red[4 * RP][SW][NV + 1];  // [wave * RP + row-lane][column][value], padded
+  __shared__ int s_last;
+  const int nstripes = static_cast<int>((N + SW - 1) / SW);
+  const int stripe = blockIdx.x % nstripes;
+  const int chunk = blockIdx.x / nstripes;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int lrow = lane / L, lcol = lane - lrow * L;
+  const int64_t c0 = static_cast<int64_t>(stripe) * SW + 4 * lcol;
+  const bool live = c0 < N;
+  const int64_t rows_per = (R + chunks - 1) / chunks;
+  const int64_t r0 = chunk * rows_per;
+  const int64_t r1 = r0 + rows_per < R ? r0 + rows_per : R;
+  const int64_t step = 4 * RP;
+  const int NK = K + 1;  // values per column in the partials (layout of the workspace)
+
+  float sb[4] = {0.f, 0.f, 0.f, 0.f};
+  float sw[4][KP];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int k = 0; k < KP; ++k) sw[j][k] = 0.f;
+  if (live) {
+    // U rows in flight per lane: every load of a batch is issued before its FMAs
+    constexpr int U = 3;
+    for (int64_t rb = r0 + wv * RP + lrow; rb < r1; rb += U * step) {
+      float4 a[U];
+      float xv[U][KP];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t r = rb + u * step;
+        const bool ok = r < r1;
+        const int64_t rr = ok ? r : r0;
+        a[u] = *reinterpret_cast<const float4*>(g + rr * N + c0);
+        if (RELU || !ok) {
+          const float4 o = RELU ? *reinterpret_cast<const float4*>(out + rr * N + c0)
+                                : make_float4(1.f, 1.f, 1.f, 1.f);
+          a[u].x = (!ok || o.x <= 0.f) ? 0.f : a[u].x; a[u].y = (!ok || o.y <= 0.f) ? 0.f : a[u].y;
+          a[u].z = (!ok || o.z <= 0.f) ? 0.f : a[u].z; a[u].w = (!ok || o.w <= 0.f) ? 0.f : a[u].w;
+        }
+#pragma unroll
+        for (int k = 0; k < KP; ++k) xv[u][k] = k < K ? x[rr * ldx + k] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const float av[4] = {a[u].x, a[u].y, a[u].z, a[u].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          sb[j] += av[j];
+#pragma unroll
+          for (int k = 0; k < KP; ++k) sw[j][k] = fmaf(av[j], xv[u][k], sw[j][k]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    red[wv * RP + lrow][4 * lcol + j][0] = sb[j];
+#pragma unroll
+    for (int k = 0; k < KP; ++k) red[wv * RP + lrow][4 * lcol + j][1 + k] = sw[j][k];
+  }
+  __syncthreads();
+  // value (column j, v) of the stripe: waves in order, row-lanes in order
+  for (int q = threadIdx.x; q < SW * NV; q += 256) {
+    const int j = q / NV, v = q - j * NV;
+    const int64_t col = static_cast<int64_t>(stripe) * SW + j;
+    if (col < N && (v == 0 || v - 1 < K)) {
+      float s = 0.f;
+      for (int w = 0; w < 4 * RP; ++w) s += red[w][j][v];
+      __hip_atomic_store(&partials[(static_cast<int64_t>(chunk) * N + col) * NK + v], s,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  unsigned* ticket = tickets + stripe * 32;
+  if (threadIdx.x == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+    s_last = prev == static_cast<unsigned>(chunks - 1);
+  }
+  __syncthreads();
+  if (!s_last) return;
+  // last arriver: every (column, value) of the stripe summed over the chunks in chunk order
+  for (int q = threadIdx.x; q < SW * NV; q += 256) {
+    const int j = q / NV, v = q - j * NV;
+    const int64_t col = static_cast<int64_t>(stripe) * SW + j;
+    if (col >= N || (v > 0 && v - 1 >= K)) continue;
+    float s = 0.f;
+    for (int c = 0; c < chunks; c += 32) {  // <= 32 chunks per stripe at N >= 256: one batch
+      float t[32];
+#pragma unroll
+      for (int u = 0; u < 32; ++u)
+        t[u] = c + u < chunks
+                   ? __hip_atomic_load(&partials[(static_cast<int64_t>(c + u) * N + col) * NK + v],
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                   : 0.f;
+#pragma unroll
+      for (int u = 0; u < 32; ++u) s += t[u];
+    }
+    if (v == 0)
+      db[col] = s;
+    else
+      dw[col * K + (v - 1)] = s;
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <bool RELU>
+static void launch_wgrad(hipStream_t s, int K, dim3 grid, const float* g, const float* out,
+                         const float* x, int64_t ldx, float* dw, float* db, int64_t R, int64_t N,
+                         int chunks, unsigned* tickets, float* partials) {
+  if (K <= 4)
+    hipLaunchKernelGGL((relu_bias_wgrad_kernel<RELU, 4>), grid, dim3(256), 0, s, g, out, x, ldx,
+                       dw, db, R, N, K, chunks, tickets, partials);
+  else if (K <= 8)
+    hipLaunchKernelGGL((relu_bias_wgrad_kernel<RELU, 8>), grid, dim3(256), 0, s, g, out, x, ldx,
+                       dw, db, R, N, K, chunks, tickets, partials);
+  else if (K <= 12)
+    hipLaunchKernelGGL((relu_bias_wgrad_kernel<RELU, 12>), grid, dim3(256), 0, s, g, out, x, ldx,
+                       dw, db, R, N, K, chunks, tickets, partials);
+  else
+    hipLaunchKernelGGL((relu_bias_wgrad_kernel<RELU, 16>), grid, dim3(256), 0, s, g, out, x, ldx,
+                       dw, db, R, N, K, chunks, tickets, partials);
+}
+
+}  // namespace ocppo
+
+extern "C" size_t ocppo_relu_bias_wgrad_workspace_bytes(int64_t R, int64_t N, int64_t K) {
+  if (R < 1 || N < 1 || K < 1) return kWgTicketBytes;
+  return kWgTicketBytes + static_cast<size_t>(wg_chunks(R, N)) * N * (K + 1) * sizeof(float);
+}
+
+extern "C" int ocppo_relu_bias_wgrad(ocppo_stream_t stream, const float* g, const float* out,
+                                     const float* x, int64_t ldx, float* dw, float* db, int64_t R,
+                                     int64_t N, int64_t K, void* workspace,
+                                     size_t workspace_bytes) {
+  OCPPO_REQUIRE(R >= 0 && N >= 4 && N % 4 == 0 && N <= kWgMaxStripes * 4 * kWgL && K >= 1 &&
+                    K <= 16 && ldx >= K,
+                "ocppo_relu_bias_wgrad: bad sizes R=%lld N=%lld K=%lld ldx=%lld (N %% 4 == 0, "
+                "N <= 16384, 1 <= K <= 16, ldx >= K)", (long long)R, (long long)N, (long long)K,
+                (long long)ldx);
+  OCPPO_REQUIRE(dw && db && workspace, "ocppo_relu_bias_wgrad: null pointer");
+  clear_stale_error();
+  hipStream_t s = as_stream(stream);
+  if (R == 0) {  // empty batch: zero gradients (g / out / x may be NULL)
+    (void)hipMemsetAsync(db, 0, N * sizeof(float), s);
+    (void)hipMemsetAsync(dw, 0, N * K * sizeof(float), s);
+    return check_launch("ocppo_relu_bias_wgrad");
+  }
+  OCPPO_REQUIRE(g && x, "ocppo_relu_bias_wgrad: null pointer");
+  OCPPO_REQUIRE(reinterpret_cast<uintptr_t>(g) % 16 == 0 &&
+                    (!out || reinterpret_cast<uintptr_t>(out) % 16 == 0) &&
+                    reinterpret_cast<uintptr_t>(workspace) % 256 == 0,
+                "ocppo_relu_bias_wgrad: g/out must be 16-B aligned, workspace 256-B aligned");
+  OCPPO_REQUIRE(workspace_bytes >= ocppo_relu_bias_wgrad_workspace_bytes(R, N, K),
+                "ocppo_relu_bias_wgrad: workspace too small (%zu < %zu)", workspace_bytes,
+                ocppo_relu_bias_wgrad_workspace_bytes(R, N, K));
+  const int chunks = wg_chunks(R, N);
+  const int64_t stripes = (N + 4 * kWgL - 1) / (4 * kWgL);
+  unsigned* tickets = static_cast<unsigned*>(workspace);
+  float* partials = reinterpret_cast<float*>(static_cast<char*>(workspace) + kWgTicketBytes);
+  const dim3 grid(static_cast<unsigned>(stripes * chunks));
+  if (out)
+    launch_wgrad<true>(s, (int)K, grid, g, out, x, ldx, dw, db, R, N, chunks, tickets, partials);
+  else
+    launch_wgrad<false>(s, (int)K, grid, g, out, x, ldx, dw, db, R, N, chunks, tickets, partials);
+  return check_launch("ocppo_relu_bias_wgrad");
+}

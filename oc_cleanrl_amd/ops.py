@@ -471,6 +471,43 @@ def relu_bias_grad(g, out=None, db=None, gp=None):
     return (gp if out is not None else g), db
 
 
+def relu_bias_wgrad_ok(g, x) -> bool:
+    return (relu_bias_grad_ok(g) and x.is_cuda and x.dtype == torch.float32 and x.dim() == 2
+            and 1 <= x.shape[1] <= 16 and x.shape[0] == g.shape[0] and x.stride(1) == 1)
+
+
+def relu_bias_wgrad(g, out, x, dw=None, db=None):
+    """(dw, db) of a Linear(+ReLU) layer whose input needs no gradient, in one pass:
+    gp = threshold_backward(g, out, 0) (g when out is None, never materialised),
+    db = gp.sum(0), dw = gp^T x. g [R, N] f32 (N % 4 == 0), x [R, K] f32 (K <= 16)."""
+    if g.dim() != 2 or x.dim() != 2 or x.shape[0] != g.shape[0]:
+        raise ValueError(f"g [R, N] and x [R, K] expected, got {tuple(g.shape)}, {tuple(x.shape)}")
+    R, N = g.shape
+    K = x.shape[1]
+    dev = g.device
+    f = torch.float32
+    if x.stride(1) != 1 and R > 0:
+        raise ValueError("x must have unit column stride")
+    ldx = x.stride(0) if R > 1 else K
+    if dw is None:
+        dw = torch.empty((N, K), dtype=f, device=dev)
+    if db is None:
+        db = torch.empty(N, dtype=f, device=dev)
+    if tuple(dw.shape) != (N, K) or not dw.is_contiguous():
+        raise ValueError(f"dw must be a contiguous [{N}, {K}] tensor")
+    key = (dev, "wg", R, N, K)
+    ws = _RB_WS.get(key)
+    if ws is None:
+        nb = int(_lib.LIB.ocppo_relu_bias_wgrad_workspace_bytes(R, N, K))
+        ws = _RB_WS[key] = torch.zeros(nb, dtype=torch.uint8, device=dev)
+    call("ocppo_relu_bias_wgrad", _stream(dev), _check(g, "g", f, dev),
+         _opt(out, "out", f, dev, R * N),
+         _check(x, "x", f, dev) if x.is_contiguous() else x.data_ptr(), ldx,
+         _check(dw, "dw", f, dev, N * K), _check(db, "db", f, dev, N), R, N, K, ws.data_ptr(),
+         ws.numel())
+    return dw, db
+
+
 def bias_act(y, b, relu: bool = True):
     """In place: y = act(y + b) over the rows of y [R, N] f32 (N % 4 == 0): the bias add + ReLU
     after a bias-less convolution (NHWC output viewed [B*H*W, C]) in one pass."""

@@ -847,3 +847,49 @@ def test_linear2_act_vs_torch(ops, dev, M, K1, N1, N2, ldx):
     assert (y.double() - ref).abs().max().item() <= 1e-5 * scale
     y2 = ops.linear2_act(x, w1, b1, w2, b2)
     assert torch.equal(y, y2)  # deterministic
+
+
+@pytest.mark.parametrize("R,N,K", [(12288, 256, 12), (12288, 256, 6), (4096, 32, 12), (7, 4, 1),
+                                   (33, 260, 16), (100000, 64, 3), (1, 16384, 5)])
+@pytest.mark.parametrize("relu", [True, False])
+def test_relu_bias_wgrad_vs_torch(ops, dev, R, N, K, relu):
+    """First-layer backward in one pass vs autograd's threshold_backward + g'^T x + sum (f64)."""
+    g = torch.randn(R, N, device=dev)
+    out = torch.relu(torch.randn(R, N, device=dev)) if relu else None
+    if relu:
+        out[::3, ::5] = 0.0
+    xs = torch.randn(R, K + 3, device=dev)
+    x = xs[:, 1:K + 1]  # row stride K + 3: the kernel takes ldx
+    dw, db = ops.relu_bias_wgrad(g, out, x)
+    gp = (torch.ops.aten.threshold_backward(g, out, 0) if relu else g).double()
+    ref_w, ref_b = gp.t() @ x.double(), gp.sum(0)
+    sw = gp.abs().t() @ x.double().abs()
+    assert ((dw.double() - ref_w).abs() / sw.clamp_min(1e-30)).max().item() < 1e-6
+    sb = gp.abs().sum(0).clamp_min(1e-30)
+    assert ((db.double() - ref_b).abs() / sb).max().item() < 1e-6
+    dw2, db2 = ops.relu_bias_wgrad(g, out, x)  # deterministic; tickets re-armed
+    assert torch.equal(dw, dw2) and torch.equal(db, db2)
+
+
+def test_relu_bias_wgrad_graph_replay_and_zero_rows(ops, dev):
+    g = torch.randn(3000, 256, device=dev)
+    out = torch.relu(torch.randn(3000, 256, device=dev))
+    x = torch.randn(3000, 12, device=dev)
+    dw, db = torch.empty(256, 12, device=dev), torch.empty(256, device=dev)
+    ops.relu_bias_wgrad(g, out, x, dw, db)
+    torch.cuda.synchronize()
+    want_w, want_b = dw.clone(), db.clone()
+    dw.zero_(); db.zero_()
+    gr = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gr):
+        ops.relu_bias_wgrad(g, out, x, dw, db)
+    for _ in range(3):
+        gr.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(dw, want_w) and torch.equal(db, want_b)
+    e = torch.empty(0, 8, device=dev)
+    w0, b0 = ops.relu_bias_wgrad(e, e, torch.empty(0, 3, device=dev))
+    torch.cuda.synchronize()
+    assert not w0.any() and not b0.any()
+    with pytest.raises(RuntimeError, match="bad sizes"):
+        ops.relu_bias_wgrad(g, None, torch.randn(3000, 17, device=dev))  # K > 16

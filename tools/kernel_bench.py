@@ -38,11 +38,14 @@ SIZES = {
     "mb_prepare": {"config": dict(M=4096, nmb=16, B=16384), "scaled": dict(M=16384, nmb=256, B=1 << 20)},
     "ppo_loss_prepared": {"config": dict(M=4096, A=6), "scaled": dict(M=4 * 1024 * 1024, A=6)},
     "policy_head": {"config": dict(N=128, H=512, A=6), "scaled": dict(N=262144, H=512, A=6)},
-    # the five Linear->ReLU backward launches of one config-2 minibatch (dedup capacity 12288
-    # encoder rows: layers 256/512/1024/512, decoder 4096 x 512), and one streaming-size launch
+    # the four Linear->ReLU backward launches of one config-2 minibatch (dedup capacity 12288
+    # encoder rows: layers 512/1024/512 -- the first layer (256) runs relu_bias_wgrad -- decoder
+    # 4096 x 512), and one streaming-size launch
     "relu_bias_grad": {"config": dict(shapes=((4096, 512), (12288, 512), (12288, 1024),
-                                              (12288, 512), (12288, 256))),
+                                              (12288, 512))),
                        "scaled": dict(shapes=((262144, 1024),))},
+    # the first encoder layer's fused ReLU-backward + bias + weight gradient (F = 12 -> 256)
+    "relu_bias_wgrad": {"config": dict(R=12288, N=256, K=12), "scaled": dict(R=262144, N=256, K=12)},
 }
 
 
@@ -162,6 +165,14 @@ def make_case(name: str, p: dict, dev):
             for gg, out, gp, db in bufs:
                 ops.relu_bias_grad(gg, out, db=db, gp=gp)
         return fn, relu_bias_grad_bytes(p["shapes"])
+    if name == "relu_bias_wgrad":
+        R, N, K = p["R"], p["N"], p["K"]
+        gg = torch.randn(R, N, device=dev, generator=g)
+        out = torch.relu(torch.randn(R, N, device=dev, generator=g))
+        x = torch.randn(R, K, device=dev, generator=g)
+        dw, db = torch.empty(N, K, device=dev), torch.empty(N, device=dev)
+        fn = lambda: ops.relu_bias_wgrad(gg, out, x, dw, db)  # noqa: E731
+        return fn, R * N * 8 + R * K * 4 + N * (K + 1) * 4
     raise KeyError(name)
 
 

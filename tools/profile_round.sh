@@ -16,7 +16,8 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/
 echo "bench trace done"
 for case in "policy_head config" "gae config" "ppo_loss_prepared config" \
             "gae scaled" "ppo_loss_prepared scaled" "policy_head scaled" "rollout_store scaled" \
-            "gather scaled" "relu_bias_grad config" "relu_bias_grad scaled"; do
+            "gather scaled" "relu_bias_grad config" "relu_bias_grad scaled" \
+            "relu_bias_wgrad config"; do
   set -- $case
   for ctr in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 240 rocprofv3 --pmc "$ctr" --kernel-trace --output-format csv \

@@ -25,6 +25,7 @@ KERNEL_SUBSTR = {
     "rollout_store": "rollout_store_kernel",
     "gather": "gather_rows_kernel",
     "relu_bias_grad": "relu_bias_grad_kernel",
+    "relu_bias_wgrad": "relu_bias_wgrad_kernel",
 }
 
 
@@ -43,6 +44,8 @@ def algorithmic_bytes(name, size):
         return p["M"] * (8 + p["R"] * 6)
     if name == "relu_bias_grad":  # average over the launch mix
         return sum(R * N * 12 + 4 * N for R, N in p["shapes"]) / len(p["shapes"])
+    if name == "relu_bias_wgrad":
+        return p["R"] * p["N"] * 8 + p["R"] * p["K"] * 4 + p["N"] * (p["K"] + 1) * 4
     return None
 
 
