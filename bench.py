@@ -35,7 +35,7 @@ sys.path.insert(0, str(ROOT))
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
 # HBM bytes per launch from rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE, separate passes) of
 # the same launch shapes: tools/profile_round.sh -> tools/summarize_profiles.py
-PMC_SUMMARY = ROOT / "profiles" / "r01e" / "pmc_summary.json"
+PMC_SUMMARY = ROOT / "profiles" / "r01f" / "pmc_summary.json"
 PMC_KEYS = {"action_head": "policy_head_config", "gae": "gae_config",
             "ppo_loss": "ppo_loss_prepared_config", "relu_bias_grad": "relu_bias_grad_config"}
 
@@ -213,7 +213,8 @@ def main():
     roofline = None
     if dom:
         ach = kernels[dom]["GBps"]
-        traffic, src = pmc_traffic(PMC_KEYS.get(dom, ""))
+        # the PMC passes replay config 2's launch shapes: no traffic figure for other configs
+        traffic, src = pmc_traffic(PMC_KEYS.get(dom, "")) if opt.config == 2 else (None, None)
         roofline = {"kernel": dom, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5),
                     "traffic": traffic, "traffic_source": src, "bytes_per_launch": kernels[dom]["bytes"],

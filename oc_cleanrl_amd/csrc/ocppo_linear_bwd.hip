@@ -340,9 +340,9 @@ extern "C" int ocppo_sum_splits(ocppo_stream_t stream, const float* part, int64_
 // Roofline: HBM stream, 8 B (relu; 4 B without) per element of g + 4K B per row of x.
 namespace ocppo {
 
-constexpr int kWgL = 4;             // lanes per row: 16-column stripes, 16 rows per wave instruction
+constexpr int kWgL = 8;  // lanes per row: 32-column stripes (whole 128-B lines), 8 rows per instruction
 constexpr int kWgMaxChunks = 64;
-constexpr int kWgMaxStripes = 1024;  // N <= 16384
+constexpr int kWgMaxStripes = 512;  // N <= 16384
 constexpr size_t kWgTicketBytes = kWgMaxStripes * 128;
 
 inline int wg_chunks(int64_t R, int64_t N) {
