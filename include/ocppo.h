@@ -308,6 +308,25 @@ OCPPO_API int ocppo_relu_bias_wgrad(ocppo_stream_t stream, const float* g, const
                           const float* x, int64_t ldx, float* dw, float* db, int64_t R,
                           int64_t N, int64_t K, void* workspace, size_t workspace_bytes);
 
+/* ---------------------------------------------------------------------------------------------
+ * Policy heads + decoder ReLU backward in ONE pass — replaces, inside `loss.backward()`
+ * (ppo_atari_oc.py:605), the actor / critic heads' dX, dW and db (architectures/ppo.py:81-84)
+ * and the ReLU-backward + bias grad of the decoder layer feeding them. With
+ * c[m] = (dlogits[m, 0..A), dvalue[m]) and W = [wa; wc] ([A+1, H]):
+ *   dh[m, j] = sum_k c[m, k] W[k, j];  gp[m, j] = relu && h[m, j] <= 0 ? 0 : dh[m, j]
+ *   db_h[j]  = sum_m gp[m, j]   (skipped when db_h == NULL)
+ *   dwa[a, j] = sum_m dlogits[m, a] h[m, j];  dwc[j] = sum_m dvalue[m] h[m, j]
+ *   dba[a] = sum_m dlogits[m, a];  dbc[0] = sum_m dvalue[m]
+ * h / gp [M, H] f32 row-major 16-B aligned, H % 4 == 0, H <= 16384; dlogits [M, A] and dvalue
+ * [M] contiguous, 1 <= A <= 7; wa [A, H], wc [H]. Workspace 256-B aligned, >=
+ * ocppo_heads_bwd_workspace_bytes(M, H, A), ZEROED before first use. Deterministic.
+ * ------------------------------------------------------------------------------------------- */
+OCPPO_API size_t ocppo_heads_bwd_workspace_bytes(int64_t M, int64_t H, int64_t A);
+OCPPO_API int ocppo_heads_bwd(ocppo_stream_t stream, const float* h, const float* dlogits,
+                    const float* dvalue, const float* wa, const float* wc, float* gp,
+                    float* db_h, float* dwa, float* dwc, float* dba, float* dbc, int64_t M,
+                    int64_t H, int64_t A, int relu, void* workspace, size_t workspace_bytes);
+
 /* Two rollout Linear(+ReLU) layers in one launch (the PPObj encoder's first two layers on the
  * newest frame of every env, architectures/ppo.py:60-84, under torch.no_grad()):
  *   y[M, N2] = act2(act1(x[M, K1] @ w1[N1, K1]^T + b1) @ w2[N2, N1]^T + b2)

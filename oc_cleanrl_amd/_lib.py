@@ -58,6 +58,8 @@ SIGNATURES: dict[str, tuple[type, list]] = {
     "ocppo_relu_bias_grad": (I, [P, P, P, P, P, I64, I64, P, SZ]),
     "ocppo_relu_bias_wgrad_workspace_bytes": (SZ, [I64, I64, I64]),
     "ocppo_relu_bias_wgrad": (I, [P, P, P, P, I64, P, P, I64, I64, I64, P, SZ]),
+    "ocppo_heads_bwd_workspace_bytes": (SZ, [I64, I64, I64]),
+    "ocppo_heads_bwd": (I, [P, P, P, P, P, P, P, P, P, P, P, P, I64, I64, I64, I, P, SZ]),
     "ocppo_bias_act": (I, [P, P, P, I64, I64, I]),
     "ocppo_sum_splits": (I, [P, P, I64, I64, P]),
     "ocppo_frames_gather": (I, [P, P, I, I64, I64, I64, I64, P, I64, P]),

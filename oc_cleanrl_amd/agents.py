@@ -97,12 +97,13 @@ class _LinearAct(torch.autograd.Function):
     for FlatAdam-owned parameters dW/db are written straight into the flat grad buffer."""
 
     @staticmethod
-    def forward(ctx, x, w, b, relu: bool):
+    def forward(ctx, x, w, b, relu: bool, box=None):
         out = torch._addmm_activation(b, x, w.t(), use_gelu=False) if relu else \
             torch.addmm(b, x, w.t())
         ctx.relu = relu
         ctx.save_for_backward(x, w, out if relu else None)
         ctx.w, ctx.b = w, b
+        ctx.box = box  # _Heads sets box["premasked"]: g arrives masked, bias grad already written
         return out
 
     @staticmethod
@@ -111,6 +112,12 @@ class _LinearAct(torch.autograd.Function):
         db = None
         bias_done = False
         g = g.contiguous()
+        if ctx.box is not None and ctx.box["premasked"]:
+            # the fused heads backward (_Heads) already applied this layer's ReLU mask and wrote
+            # its bias gradient: only dX and dW remain
+            dx = g.mm(w) if ctx.needs_input_grad[0] else None
+            _weight_grad(g, x, out=ctx.w.grad)
+            return dx, None, None, None, None
         if FUSED_FIRST_LAYER_BWD and not ctx.needs_input_grad[0] and ctx.needs_input_grad[1] \
                 and ctx.needs_input_grad[2] and _direct(ctx.w) and _direct(ctx.b) and \
                 ops.relu_bias_wgrad_ok(g, x):
@@ -118,7 +125,7 @@ class _LinearAct(torch.autograd.Function):
             o = out if ctx.relu else None
             ops.timed(f"relu_bias_wgrad_{g.shape[0]}x{g.shape[1]}x{x.shape[1]}",
                       lambda: ops.relu_bias_wgrad(g, o, x, dw=ctx.w.grad, db=ctx.b.grad))
-            return None, None, None, None
+            return None, None, None, None, None
         if FUSED_RELU_BIAS_GRAD and ctx.needs_input_grad[2] and _direct(ctx.b) and \
                 ops.relu_bias_grad_ok(g):
             # threshold_backward + bias sum in one HIP pass, bias grad written in place
@@ -141,7 +148,57 @@ class _LinearAct(torch.autograd.Function):
                 torch.sum(gp, 0, out=ctx.b.grad)
             else:
                 db = gp.sum(0)
-        return dx, dw, db, None
+        return dx, dw, db, None, None
+
+
+class _Heads(torch.autograd.Function):
+    """logits = h Wa^T + ba, value = h Wc^T + bc (architectures/ppo.py:81-84, the two head
+    Linears on the decoder output h). Backward = ONE HIP pass (ops.heads_bwd): dh from both heads,
+    the dW / db of both heads and, when h is the ReLU output of a Linear whose grads are written in
+    place (box), that layer's ReLU mask and bias gradient too (its _LinearAct backward then only
+    runs dX / dW). Same formulas as autograd's, fixed summation orders."""
+
+    @staticmethod
+    def forward(ctx, h, wa, ba, wc, bc, box):
+        logits = torch.addmm(ba, h, wa.t())
+        value = torch.addmm(bc, h, wc.t())
+        ctx.save_for_backward(h, wa, wc)
+        ctx.params = (wa, ba, wc, bc)
+        ctx.box = box
+        if box is not None:
+            box["premasked"] = True
+        return logits, value
+
+    @staticmethod
+    def backward(ctx, g_logits, g_value):
+        h, wa, wc = ctx.saved_tensors
+        pa, pba, pc, pbc = ctx.params
+        M, A = h.shape[0], wa.shape[0]
+        if g_logits is None:
+            g_logits = torch.zeros(M, A, dtype=h.dtype, device=h.device)
+        if g_value is None:
+            g_value = torch.zeros(M, 1, dtype=h.dtype, device=h.device)
+        box = ctx.box
+        db_h = box["bias"].grad if box is not None else None
+        outs = [p.grad if _direct(p) else None for p in (pa, pc, pba, pbc)]
+        gp, _, dwa, dwc, dba, dbc = ops.timed(
+            "heads_bwd", lambda: ops.heads_bwd(
+                h, g_logits.contiguous(), g_value.reshape(-1).contiguous(), wa, wc.reshape(-1),
+                relu=box is not None, db_h=db_h, dwa=outs[0], dwc=outs[1], dba=outs[2],
+                dbc=outs[3]))
+        ret = [None if outs[i] is not None else t for i, t in enumerate((dwa, dwc, dba, dbc))]
+        return gp, ret[0], ret[2], ret[1], ret[3], None
+
+
+# Actor + critic backward (and the decoder's ReLU mask + bias grad) as one HIP pass (_Heads).
+FUSED_HEADS_BWD = True
+
+
+def heads_ok(h, actor, critic) -> bool:
+    return (FUSED_HEADS_BWD and torch.is_grad_enabled() and h.requires_grad and h.is_cuda and
+            h.dtype == torch.float32 and h.dim() == 2 and isinstance(actor, nn.Linear) and
+            isinstance(critic, nn.Linear) and actor.bias is not None and critic.bias is not None
+            and critic.out_features == 1 and ops.heads_bwd_ok(h, actor.out_features))
 
 
 # One-pass HIP ReLU-backward + bias gradient (ops.relu_bias_grad) for FlatAdam-owned biases.
@@ -226,9 +283,16 @@ def linear_act(x, lin: nn.Linear, relu: bool):
     x2 = x.reshape(-1, x.shape[-1])
     if _hip_linear_ok(x2, lin):
         y = ops.linear_act(x2, lin.weight, lin.bias, relu)
-    else:
-        y = _LinearAct.apply(x2, lin.weight, lin.bias, relu)
-    return y.view(*lead, y.shape[-1])
+        return y.view(*lead, y.shape[-1])
+    box = None
+    if relu and FUSED_HEADS_BWD and torch.is_grad_enabled() and _direct(lin.weight) and \
+            _direct(lin.bias):
+        box = {"premasked": False, "bias": lin.bias}
+    y = _LinearAct.apply(x2, lin.weight, lin.bias, relu, box)
+    y = y.view(*lead, y.shape[-1])
+    if box is not None:
+        y._ocppo_box = box
+    return y
 
 
 def linear_relu(x, lin: nn.Linear):
@@ -310,9 +374,17 @@ class _ActorCritic(Predictor):
     def get_value(self, x, prescaled: bool = False):
         return self._head(self.critic, self.trunk(x, prescaled))
 
-    def logits_and_value(self, x, prescaled: bool = False):
-        hidden = self.trunk(x, prescaled)
+    def heads(self, hidden):
+        """(actor logits, critic value) from the trunk output; under autograd on the GPU one
+        _Heads function (fused HIP backward), else the two head Linears."""
+        if heads_ok(hidden, self.actor, self.critic):
+            box = getattr(hidden, "_ocppo_box", None)
+            return _Heads.apply(hidden, self.actor.weight, self.actor.bias, self.critic.weight,
+                                self.critic.bias, box)
         return self._head(self.actor, hidden), self._head(self.critic, hidden)
+
+    def logits_and_value(self, x, prescaled: bool = False):
+        return self.heads(self.trunk(x, prescaled))
 
     def get_action_and_value(self, x, action=None):
         """(action [B] i64, log_prob [B], entropy [B], value [B, 1]) like the reference."""

@@ -528,3 +528,226 @@ extern "C" int ocppo_relu_bias_wgrad(ocppo_stream_t stream, const float* g, cons
     launch_wgrad<false>(s, (int)K, grid, g, out, x, ldx, dw, db, R, N, chunks, tickets, partials);
   return check_launch("ocppo_relu_bias_wgrad");
 }
+
+// ---- policy heads + decoder ReLU backward in ONE pass ---------------------------------------------
+// The actor / critic heads (architectures/ppo.py:81-84: Linear(H, A), Linear(H, 1) on the decoder
+// output h = relu(z)) get d loss / d logits [M, A] and d loss / d value [M] from the fused loss
+// (ppo_atari_oc.py:581-605). Autograd then runs per head a dX GEMM (K = A), a split-K dW GEMM and
+// a bias sum, adds the two dX, and the decoder's ReLU-backward + bias-grad pass: ~9 launches, dh
+// written and read back. Here, with c[m] = (dlogits[m, 0..A), dv[m]) and W = [Wa; Wc] ([A+1, H]):
+//   dh[m, j]  = sum_k c[m, k] W[k, j]                   (k order, fmaf)
+//   gp[m, j]  = relu ? (h[m, j] <= 0 ? 0 : dh[m, j]) : dh[m, j]      (written once)
+//   db_h[j]   = sum_m gp[m, j]                          (the decoder bias grad; optional)
+//   dW[k, j]  = sum_m c[m, k] h[m, j]                   (dWa rows k < A, dWc row A)
+//   dbk[k]    = sum_m c[m, k]                           (dba, dbc)
+// Same launch structure as relu_bias_wgrad (32-column stripes x row chunks, fixed-order LDS
+// combine, chunk-order tail by the stripe's last arriver); stripe 0 also carries dbk.
+// Roofline: HBM stream, 8 B per element of h (h in, gp out) + 4(A+1) B per row.
+namespace ocppo {
+
+constexpr int kHbKP = 8;  // A + 1 <= 8
+
+inline size_t hb_partials_per_chunk(int64_t H, int K) { return H * (K + 1) + K; }
+
+template <bool RELU>
+__global__ __launch_bounds__(256) void heads_bwd_kernel(
+    const float* __restrict__ h, const float* __restrict__ dl, const float* __restrict__ dv,
+    const float* __restrict__ wa, const float* __restrict__ wc, float* __restrict__ gp,
+    float* __restrict__ dbh, float* __restrict__ dwa, float* __restrict__ dwc,
+    float* __restrict__ dba, float* __restrict__ dbc, int64_t M, int64_t H, int A, int chunks,
+    unsigned* __restrict__ tickets, float* __restrict__ partials) {
+  constexpr int L = kWgL, RP = 64 / L, SW = 4 * L, KP = kHbKP, NV = KP + 1;
+  __shared__ float red[4 * RP][SW][NV + 1];
+  __shared__ float redc[4 * RP][KP];
+  __shared__ int s_last;
+  const int K = A + 1;
+  const int nstripes = static_cast<int>((H + SW - 1) / SW);
+  const int stripe = blockIdx.x % nstripes;
+  const int chunk = blockIdx.x / nstripes;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int lrow = lane / L, lcol = lane - lrow * L;
+  const int64_t c0 = static_cast<int64_t>(stripe) * SW + 4 * lcol;
+  const bool live = c0 < H;
+  const int64_t rows_per = (M + chunks - 1) / chunks;
+  const int64_t r0 = chunk * rows_per;
+  const int64_t r1 = r0 + rows_per < M ? r0 + rows_per : M;
+  const int64_t step = 4 * RP;
+  const int64_t ppc = static_cast<int64_t>(H) * (K + 1) + K;  // partials per chunk
+
+  // this lane's 4 columns of W = [Wa; Wc]
+  float wk[KP][4];
+#pragma unroll
+  for (int k = 0; k < KP; ++k) {
+    const float* wr = k < A ? wa + static_cast<int64_t>(k) * H : wc;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) wk[k][j] = (live && k < K) ? wr[c0 + j] : 0.f;
+  }
+  float sb[4] = {0.f, 0.f, 0.f, 0.f};
+  float sw[4][KP];
+  float sc[KP];
+#pragma unroll
+  for (int k = 0; k < KP; ++k) {
+    sc[k] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) sw[j][k] = 0.f;
+  }
+  if (live) {
+    constexpr int U = 3;
+    for (int64_t rb = r0 + wv * RP + lrow; rb < r1; rb += U * step) {
+      float4 hv[U];
+      float cv[U][KP];
+      bool ok[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t r = rb + u * step;
+        ok[u] = r < r1;
+        const int64_t rr = ok[u] ? r : r0;
+        hv[u] = *reinterpret_cast<const float4*>(h + rr * H + c0);
+#pragma unroll
+        for (int k = 0; k < KP; ++k)
+          cv[u][k] = !ok[u] || k >= K ? 0.f : (k < A ? dl[rr * A + k] : dv[rr]);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const float hj[4] = {hv[u].x, hv[u].y, hv[u].z, hv[u].w};
+        float g4[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float d = 0.f;
+#pragma unroll
+          for (int k = 0; k < KP; ++k) d = fmaf(cv[u][k], wk[k][j], d);
+          g4[j] = (RELU && hj[j] <= 0.f) ? 0.f : d;
+          sb[j] += g4[j];
+#pragma unroll
+          for (int k = 0; k < KP; ++k) sw[j][k] = fmaf(cv[u][k], hj[j], sw[j][k]);
+        }
+#pragma unroll
+        for (int k = 0; k < KP; ++k) sc[k] += cv[u][k];
+        if (ok[u])
+          *reinterpret_cast<float4*>(gp + (rb + u * step) * H + c0) =
+              make_float4(g4[0], g4[1], g4[2], g4[3]);
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    red[wv * RP + lrow][4 * lcol + j][0] = sb[j];
+#pragma unroll
+    for (int k = 0; k < KP; ++k) red[wv * RP + lrow][4 * lcol + j][1 + k] = sw[j][k];
+  }
+  if (lcol == 0) {
+#pragma unroll
+    for (int k = 0; k < KP; ++k) redc[wv * RP + lrow][k] = live ? sc[k] : 0.f;
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < SW * NV; q += 256) {
+    const int j = q / NV, v = q - j * NV;
+    const int64_t col = static_cast<int64_t>(stripe) * SW + j;
+    if (col < H && v < K + 1) {
+      float s = 0.f;
+#pragma unroll 8
+      for (int w = 0; w < 4 * RP; ++w) s += red[w][j][v];
+      __hip_atomic_store(&partials[chunk * ppc + col * (K + 1) + v], s, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  if (stripe == 0 && threadIdx.x < K) {
+    float s = 0.f;
+    for (int w = 0; w < 4 * RP; ++w) s += redc[w][threadIdx.x];
+    __hip_atomic_store(&partials[chunk * ppc + H * (K + 1) + threadIdx.x], s, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  unsigned* ticket = tickets + stripe * 32;
+  if (threadIdx.x == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+    s_last = prev == static_cast<unsigned>(chunks - 1);
+  }
+  __syncthreads();
+  if (!s_last) return;
+  const int nq = SW * (K + 1) + (stripe == 0 ? K : 0);
+  for (int q = threadIdx.x; q < nq; q += 256) {
+    int64_t idx;
+    int j = 0, v = 0;
+    const bool colv = q < SW * (K + 1);
+    if (colv) {
+      j = q / (K + 1);
+      v = q - j * (K + 1);
+      const int64_t col = static_cast<int64_t>(stripe) * SW + j;
+      if (col >= H) continue;
+      idx = col * (K + 1) + v;
+    } else {
+      idx = static_cast<int64_t>(H) * (K + 1) + (q - SW * (K + 1));
+    }
+    float s = 0.f;
+    for (int c = 0; c < chunks; c += 32) {
+      float t[32];
+#pragma unroll
+      for (int u = 0; u < 32; ++u)
+        t[u] = c + u < chunks ? __hip_atomic_load(&partials[(c + u) * ppc + idx], __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT)
+                              : 0.f;
+#pragma unroll
+      for (int u = 0; u < 32; ++u) s += t[u];
+    }
+    if (colv) {
+      const int64_t col = static_cast<int64_t>(stripe) * SW + j;
+      if (v == 0) {
+        if (dbh) dbh[col] = s;
+      } else if (v - 1 < A) {
+        dwa[static_cast<int64_t>(v - 1) * H + col] = s;
+      } else {
+        dwc[col] = s;
+      }
+    } else {
+      const int k = q - SW * (K + 1);
+      if (k < A) dba[k] = s;
+      else dbc[0] = s;
+    }
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+}  // namespace ocppo
+
+extern "C" size_t ocppo_heads_bwd_workspace_bytes(int64_t M, int64_t H, int64_t A) {
+  if (M < 1 || H < 1 || A < 1) return kWgTicketBytes;
+  return kWgTicketBytes +
+         static_cast<size_t>(wg_chunks(M, H)) * hb_partials_per_chunk(H, (int)A + 1) * sizeof(float);
+}
+
+extern "C" int ocppo_heads_bwd(ocppo_stream_t stream, const float* h, const float* dlogits,
+                               const float* dvalue, const float* wa, const float* wc, float* gp,
+                               float* db_h, float* dwa, float* dwc, float* dba, float* dbc,
+                               int64_t M, int64_t H, int64_t A, int relu, void* workspace,
+                               size_t workspace_bytes) {
+  OCPPO_REQUIRE(M >= 1 && H >= 4 && H % 4 == 0 && H <= kWgMaxStripes * 4 * kWgL && A >= 1 &&
+                    A + 1 <= kHbKP,
+                "ocppo_heads_bwd: bad sizes M=%lld H=%lld A=%lld (M >= 1, H %% 4 == 0, "
+                "H <= 16384, 1 <= A <= 7)", (long long)M, (long long)H, (long long)A);
+  OCPPO_REQUIRE(h && dlogits && dvalue && wa && wc && gp && dwa && dwc && dba && dbc && workspace,
+                "ocppo_heads_bwd: null pointer");
+  OCPPO_REQUIRE(reinterpret_cast<uintptr_t>(h) % 16 == 0 &&
+                    reinterpret_cast<uintptr_t>(gp) % 16 == 0 &&
+                    reinterpret_cast<uintptr_t>(workspace) % 256 == 0,
+                "ocppo_heads_bwd: h/gp must be 16-B aligned, workspace 256-B aligned");
+  OCPPO_REQUIRE(workspace_bytes >= ocppo_heads_bwd_workspace_bytes(M, H, A),
+                "ocppo_heads_bwd: workspace too small (%zu < %zu)", workspace_bytes,
+                ocppo_heads_bwd_workspace_bytes(M, H, A));
+  clear_stale_error();
+  hipStream_t s = as_stream(stream);
+  const int chunks = wg_chunks(M, H);
+  const int64_t stripes = (H + 4 * kWgL - 1) / (4 * kWgL);
+  unsigned* tickets = static_cast<unsigned*>(workspace);
+  float* partials = reinterpret_cast<float*>(static_cast<char*>(workspace) + kWgTicketBytes);
+  const dim3 grid(static_cast<unsigned>(stripes * chunks)), block(256);
+  if (relu)
+    hipLaunchKernelGGL(heads_bwd_kernel<true>, grid, block, 0, s, h, dlogits, dvalue, wa, wc, gp,
+                       db_h, dwa, dwc, dba, dbc, M, H, (int)A, chunks, tickets, partials);
+  else
+    hipLaunchKernelGGL(heads_bwd_kernel<false>, grid, block, 0, s, h, dlogits, dvalue, wa, wc, gp,
+                       db_h, dwa, dwc, dba, dbc, M, H, (int)A, chunks, tickets, partials);
+  return check_launch("ocppo_heads_bwd");
+}

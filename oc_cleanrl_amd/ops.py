@@ -508,6 +508,41 @@ def relu_bias_wgrad(g, out, x, dw=None, db=None):
     return dw, db
 
 
+def heads_bwd_ok(h, A: int) -> bool:
+    return (h.is_cuda and h.dtype == torch.float32 and h.dim() == 2 and h.shape[0] >= 1 and
+            h.shape[1] % 4 == 0 and 4 <= h.shape[1] <= 16384 and 1 <= A <= 7 and
+            h.is_contiguous() and h.data_ptr() % 16 == 0)
+
+
+def heads_bwd(h, dlogits, dvalue, wa, wc, relu: bool = True, gp=None, db_h=None, dwa=None,
+              dwc=None, dba=None, dbc=None):
+    """Actor/critic heads' backward + the producing layer's ReLU backward in one pass (see
+    include/ocppo.h). h [M, H] (the heads' input = decoder ReLU output), dlogits [M, A],
+    dvalue [M]; returns (gp, db_h, dwa, dwc, dba, dbc); db_h None skips the decoder bias."""
+    M, H = h.shape
+    A = dlogits.shape[1]
+    dev = h.device
+    f = torch.float32
+    gp = torch.empty_like(h) if gp is None else gp
+    dwa = torch.empty(A, H, dtype=f, device=dev) if dwa is None else dwa
+    dwc = torch.empty(1, H, dtype=f, device=dev) if dwc is None else dwc
+    dba = torch.empty(A, dtype=f, device=dev) if dba is None else dba
+    dbc = torch.empty(1, dtype=f, device=dev) if dbc is None else dbc
+    key = (dev, "hb", M, H, A)
+    ws = _RB_WS.get(key)
+    if ws is None:
+        nb = int(_lib.LIB.ocppo_heads_bwd_workspace_bytes(M, H, A))
+        ws = _RB_WS[key] = torch.zeros(nb, dtype=torch.uint8, device=dev)
+    call("ocppo_heads_bwd", _stream(dev), _check(h, "h", f, dev, M * H),
+         _check(dlogits, "dlogits", f, dev, M * A), _check(dvalue, "dvalue", f, dev, M),
+         _check(wa, "wa", f, dev, A * H), _check(wc, "wc", f, dev, H),
+         _check(gp, "gp", f, dev, M * H), _opt(db_h, "db_h", f, dev, H),
+         _check(dwa, "dwa", f, dev, A * H), _check(dwc, "dwc", f, dev, H),
+         _check(dba, "dba", f, dev, A), _check(dbc, "dbc", f, dev, 1), M, H, A,
+         1 if relu else 0, ws.data_ptr(), ws.numel())
+    return gp, db_h, dwa, dwc, dba, dbc
+
+
 def bias_act(y, b, relu: bool = True):
     """In place: y = act(y + b) over the rows of y [R, N] f32 (N % 4 == 0): the bias add + ReLU
     after a bias-less convolution (NHWC output viewed [B*H*W, C]) in one pass."""

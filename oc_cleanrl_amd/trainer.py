@@ -409,7 +409,7 @@ class PPOTrainer:
                                              idx, k, split=self.split)
             if self.split:
                 hidden, self.cuts[j] = hidden
-            logits, value = ag._head(ag.actor, hidden), ag._head(ag.critic, hidden)
+            logits, value = ag.heads(hidden)
         else:
             self.timer.bracket("gather", lambda: ops.gather_rows(self.b_obs, idx, self.mb_obs,
                                                                  scale255=self.prescale))

@@ -893,3 +893,66 @@ def test_relu_bias_wgrad_graph_replay_and_zero_rows(ops, dev):
     assert not w0.any() and not b0.any()
     with pytest.raises(RuntimeError, match="bad sizes"):
         ops.relu_bias_wgrad(g, None, torch.randn(3000, 17, device=dev))  # K > 16
+
+
+@pytest.mark.parametrize("M,H,A", [(4096, 512, 6), (8192, 512, 4), (33, 12, 7), (1, 4, 1),
+                                   (5000, 64, 3)])
+@pytest.mark.parametrize("relu", [True, False])
+def test_heads_bwd_vs_autograd(ops, dev, M, H, A, relu):
+    """Heads + producing-ReLU backward in one pass vs autograd of relu -> two Linears (f64)."""
+    z = torch.randn(M, H, device=dev, dtype=torch.float64)
+    z[::4, ::3] = 0.0
+    hd = (torch.relu(z) if relu else z).requires_grad_(True)
+    wa = torch.randn(A, H, device=dev, dtype=torch.float64, requires_grad=True)
+    ba = torch.randn(A, device=dev, dtype=torch.float64, requires_grad=True)
+    wc = torch.randn(1, H, device=dev, dtype=torch.float64, requires_grad=True)
+    bc = torch.randn(1, device=dev, dtype=torch.float64, requires_grad=True)
+    dl = torch.randn(M, A, device=dev, dtype=torch.float64)
+    dv = torch.randn(M, device=dev, dtype=torch.float64)
+    logits, value = hd @ wa.t() + ba, hd @ wc.t() + bc
+    torch.autograd.backward([logits, value], [dl, dv.view(-1, 1)])
+    gh = hd.grad * (z > 0) if relu else hd.grad
+    f = torch.float32
+    gp, db_h, dwa, dwc, dba, dbc = ops.heads_bwd(
+        hd.detach().to(f).contiguous(), dl.to(f), dv.to(f), wa.detach().to(f), wc.detach().to(f).reshape(-1),
+        relu=relu, db_h=torch.empty(H, device=dev))
+    def close(got, want, scale, tol=1e-5):
+        assert ((got.double() - want).abs() / scale.clamp_min(1e-30)).max().item() < tol
+    h32 = hd.detach().abs()
+    close(gp, gh, dl.abs() @ wa.detach().abs() + dv.abs().view(-1, 1) * wc.detach().abs())
+    close(db_h, gh.sum(0), gh.abs().sum(0))
+    close(dwa, wa.grad, dl.abs().t() @ h32)
+    close(dwc, wc.grad, dv.abs().view(1, -1) @ h32)
+    close(dba, ba.grad, dl.abs().sum(0))
+    close(dbc, bc.grad, dv.abs().sum().view(1))
+    again = ops.heads_bwd(hd.detach().to(f).contiguous(), dl.to(f), dv.to(f), wa.detach().to(f),
+                          wc.detach().to(f).reshape(-1), relu=relu, db_h=torch.empty(H, device=dev))
+    for x, y in zip((gp, db_h, dwa, dwc, dba, dbc), again):
+        assert torch.equal(x, y)  # deterministic; tickets re-armed
+
+
+def test_heads_function_matches_module_autograd(dev):
+    """agents._Heads (with the decoder's premasked box) == plain decoder ReLU + two Linears."""
+    from oc_cleanrl_amd import agents, ops as O
+
+    torch.manual_seed(0)
+    M, K, H, A = 700, 64, 128, 6
+    dec, act, cri = (torch.nn.Linear(K, H).to(dev), torch.nn.Linear(H, A).to(dev),
+                     torch.nn.Linear(H, 1).to(dev))
+    x = torch.randn(M, K, device=dev)
+    dl, dv = torch.randn(M, A, device=dev), torch.randn(M, 1, device=dev)
+    h = torch.relu(dec(x))
+    torch.autograd.backward([act(h), cri(h)], [dl, dv])
+    want = [p.grad.clone() for p in (dec.weight, dec.bias, act.weight, act.bias, cri.weight,
+                                     cri.bias)]
+    params = [dec.weight, dec.bias, act.weight, act.bias, cri.weight, cri.bias]
+    for p in params:  # FlatAdam-style in-place grads
+        p.grad = torch.zeros_like(p)
+        p._ocppo_direct_grad = True
+    h2 = agents.linear_act(x, dec, True)
+    assert getattr(h2, "_ocppo_box", None) is not None
+    logits, value = agents._Heads.apply(h2, act.weight, act.bias, cri.weight, cri.bias,
+                                        h2._ocppo_box)
+    torch.autograd.backward([logits, value], [dl, dv])
+    for p, w in zip(params, want):
+        torch.testing.assert_close(p.grad, w, rtol=1e-4, atol=1e-5)
