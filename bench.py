@@ -35,7 +35,7 @@ sys.path.insert(0, str(ROOT))
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
 # HBM bytes per launch from rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE, separate passes) of
 # the same launch shapes: tools/profile_round.sh -> tools/summarize_profiles.py
-PMC_SUMMARY = ROOT / "profiles" / "r01f" / "pmc_summary.json"
+PMC_SUMMARY = ROOT / "profiles" / "r01g" / "pmc_summary.json"
 PMC_KEYS = {"action_head": "policy_head_config", "gae": "gae_config",
             "ppo_loss": "ppo_loss_prepared_config", "relu_bias_grad": "relu_bias_grad_config"}
 
@@ -76,6 +76,9 @@ def kernel_bytes(tr) -> dict:
         "frame_cache": (N * (4 + 4 * tr.enc_cache.shape[2] * (2 * tr.enc_cache.shape[1]))
                         if tr.enc_cache is not None else None),
     }
+    Hh = tr.agent.actor.in_features
+    # heads' input h in + masked dh out [M, H]; dlogits + dv in; [Wa; Wc] in, dW + db out
+    kb["heads_bwd"] = M * Hh * 8 + M * (A + 1) * 4 + 2 * (A + 1) * Hh * 4 + Hh * 4 + (A + 1) * 4
     if tr.frame_dedup:
         C, E = tr.planner.cap, tr.agent.encoding_dim
         F = D

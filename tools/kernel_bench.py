@@ -38,14 +38,15 @@ SIZES = {
     "mb_prepare": {"config": dict(M=4096, nmb=16, B=16384), "scaled": dict(M=16384, nmb=256, B=1 << 20)},
     "ppo_loss_prepared": {"config": dict(M=4096, A=6), "scaled": dict(M=4 * 1024 * 1024, A=6)},
     "policy_head": {"config": dict(N=128, H=512, A=6), "scaled": dict(N=262144, H=512, A=6)},
-    # the four Linear->ReLU backward launches of one config-2 minibatch (dedup capacity 12288
-    # encoder rows: layers 512/1024/512 -- the first layer (256) runs relu_bias_wgrad -- decoder
-    # 4096 x 512), and one streaming-size launch
-    "relu_bias_grad": {"config": dict(shapes=((4096, 512), (12288, 512), (12288, 1024),
-                                              (12288, 512))),
+    # the three Linear->ReLU backward launches of one config-2 minibatch (dedup capacity 12288
+    # encoder rows: layers 512/1024/512 -- the first layer (256) runs relu_bias_wgrad, the decoder
+    # (4096 x 512) heads_bwd), and one streaming-size launch
+    "relu_bias_grad": {"config": dict(shapes=((12288, 512), (12288, 1024), (12288, 512))),
                        "scaled": dict(shapes=((262144, 1024),))},
     # the first encoder layer's fused ReLU-backward + bias + weight gradient (F = 12 -> 256)
     "relu_bias_wgrad": {"config": dict(R=12288, N=256, K=12), "scaled": dict(R=262144, N=256, K=12)},
+    # actor + critic heads' backward with the decoder's ReLU mask + bias grad (M = 4096, H = 512)
+    "heads_bwd": {"config": dict(M=4096, H=512, A=6), "scaled": dict(M=262144, H=512, A=6)},
 }
 
 
@@ -165,6 +166,16 @@ def make_case(name: str, p: dict, dev):
             for gg, out, gp, db in bufs:
                 ops.relu_bias_grad(gg, out, db=db, gp=gp)
         return fn, relu_bias_grad_bytes(p["shapes"])
+    if name == "heads_bwd":
+        M, H, A = p["M"], p["H"], p["A"]
+        hh = torch.relu(torch.randn(M, H, device=dev, generator=g))
+        dl, dv = torch.randn(M, A, device=dev, generator=g), torch.randn(M, device=dev, generator=g)
+        wa, wc = torch.randn(A, H, device=dev, generator=g), torch.randn(H, device=dev, generator=g)
+        gp, dbh = torch.empty_like(hh), torch.empty(H, device=dev)
+        dwa, dwc = torch.empty(A, H, device=dev), torch.empty(1, H, device=dev)
+        dba, dbc = torch.empty(A, device=dev), torch.empty(1, device=dev)
+        fn = lambda: ops.heads_bwd(hh, dl, dv, wa, wc, True, gp, dbh, dwa, dwc, dba, dbc)  # noqa: E731
+        return fn, M * H * 8 + M * (A + 1) * 4 + 2 * (A + 1) * H * 4 + H * 4 + (A + 1) * 4
     if name == "relu_bias_wgrad":
         R, N, K = p["R"], p["N"], p["K"]
         gg = torch.randn(R, N, device=dev, generator=g)

@@ -17,7 +17,7 @@ echo "bench trace done"
 for case in "policy_head config" "gae config" "ppo_loss_prepared config" \
             "gae scaled" "ppo_loss_prepared scaled" "policy_head scaled" "rollout_store scaled" \
             "gather scaled" "relu_bias_grad config" "relu_bias_grad scaled" \
-            "relu_bias_wgrad config"; do
+            "relu_bias_wgrad config" "heads_bwd config"; do
   set -- $case
   for ctr in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 240 rocprofv3 --pmc "$ctr" --kernel-trace --output-format csv \

@@ -26,6 +26,7 @@ KERNEL_SUBSTR = {
     "gather": "gather_rows_kernel",
     "relu_bias_grad": "relu_bias_grad_kernel",
     "relu_bias_wgrad": "relu_bias_wgrad_kernel",
+    "heads_bwd": "heads_bwd_kernel",
 }
 
 
@@ -44,6 +45,9 @@ def algorithmic_bytes(name, size):
         return p["M"] * (8 + p["R"] * 6)
     if name == "relu_bias_grad":  # average over the launch mix
         return sum(R * N * 12 + 4 * N for R, N in p["shapes"]) / len(p["shapes"])
+    if name == "heads_bwd":
+        M, H, A = p["M"], p["H"], p["A"]
+        return M * H * 8 + M * (A + 1) * 4 + 2 * (A + 1) * H * 4 + H * 4 + (A + 1) * 4
     if name == "relu_bias_wgrad":
         return p["R"] * p["N"] * 8 + p["R"] * p["K"] * 4 + p["N"] * (p["K"] + 1) * 4
     return None
