@@ -376,7 +376,11 @@ class _ActorCritic(Predictor):
 
     def heads(self, hidden):
         """(actor logits, critic value) from the trunk output; under autograd on the GPU one
-        _Heads function (fused HIP backward), else the two head Linears."""
+        _Heads function (fused HIP backward), else the two head Linears. With the fused path
+        the trunk layer that produced `hidden` leaves its ReLU mask and bias gradient to _Heads,
+        so `hidden` must feed nothing but these two heads in the graph being differentiated
+        (true for the PPO loss of ppo_atari_oc.py:566-605; set FUSED_HEADS_BWD = False for
+        extra losses on the trunk output)."""
         if heads_ok(hidden, self.actor, self.critic):
             box = getattr(hidden, "_ocppo_box", None)
             return _Heads.apply(hidden, self.actor.weight, self.actor.bias, self.critic.weight,
