@@ -318,7 +318,9 @@ OCPPO_API int ocppo_relu_bias_wgrad(ocppo_stream_t stream, const float* g, const
  *   dwa[a, j] = sum_m dlogits[m, a] h[m, j];  dwc[j] = sum_m dvalue[m] h[m, j]
  *   dba[a] = sum_m dlogits[m, a];  dbc[0] = sum_m dvalue[m]
  * h / gp [M, H] f32 row-major 16-B aligned, H % 4 == 0, H <= 16384; dlogits [M, A] and dvalue
- * [M] contiguous, 1 <= A <= 7; wa [A, H], wc [H]. Workspace 256-B aligned, >=
+ * [M] contiguous, 1 <= A <= 7; wa [A, H], wc [H]. wc, dvalue, dwc and dbc may all be NULL: one
+ * head only (K = A rows of W; e.g. the DQN Q head of dqn_atari_oc.py:378-392). Workspace 256-B
+ * aligned, >=
  * ocppo_heads_bwd_workspace_bytes(M, H, A), ZEROED before first use. Deterministic.
  * ------------------------------------------------------------------------------------------- */
 OCPPO_API size_t ocppo_heads_bwd_workspace_bytes(int64_t M, int64_t H, int64_t A);

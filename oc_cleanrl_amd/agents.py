@@ -190,6 +190,42 @@ class _Heads(torch.autograd.Function):
         return gp, ret[0], ret[2], ret[1], ret[3], None
 
 
+class _QHead(torch.autograd.Function):
+    """q = h Wq^T + bq, a single head (the DQN Q head, architectures/dqn.py:14-25 and the obj
+    Q-network's last Linear): backward = ops.heads_bwd without a critic row, with the producing
+    layer's ReLU mask + bias grad when `box` says so (as _Heads)."""
+
+    @staticmethod
+    def forward(ctx, h, wq, bq, box):
+        ctx.save_for_backward(h, wq)
+        ctx.params = (wq, bq)
+        ctx.box = box
+        if box is not None:
+            box["premasked"] = True
+        return torch.addmm(bq, h, wq.t())
+
+    @staticmethod
+    def backward(ctx, g):
+        h, wq = ctx.saved_tensors
+        pw, pb = ctx.params
+        box = ctx.box
+        db_h = box["bias"].grad if box is not None else None
+        ow, ob = (pw.grad if _direct(pw) else None), (pb.grad if _direct(pb) else None)
+        gp, _, dw, _, db, _ = ops.timed("heads_bwd", lambda: ops.heads_bwd(
+            h, g.contiguous(), None, wq, None, relu=box is not None, db_h=db_h, dwa=ow, dba=ob))
+        return gp, (None if ow is not None else dw), (None if ob is not None else db), None
+
+
+def q_head(hidden, lin: nn.Linear):
+    """lin(hidden) for the last Linear of a Q-network; the fused single-head backward under
+    autograd on the GPU (same single-consumer contract as _ActorCritic.heads)."""
+    if (FUSED_HEADS_BWD and torch.is_grad_enabled() and hidden.requires_grad and hidden.is_cuda
+            and hidden.dtype == torch.float32 and hidden.dim() == 2 and lin.bias is not None
+            and ops.heads_bwd_ok(hidden, lin.out_features)):
+        return _QHead.apply(hidden, lin.weight, lin.bias, getattr(hidden, "_ocppo_box", None))
+    return linear_act(hidden, lin, False) if hidden.is_cuda else lin(hidden)
+
+
 # Actor + critic backward (and the decoder's ReLU mask + bias grad) as one HIP pass (_Heads).
 FUSED_HEADS_BWD = True
 

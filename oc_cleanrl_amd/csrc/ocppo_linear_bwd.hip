@@ -554,13 +554,13 @@ __global__ __launch_bounds__(256) void heads_bwd_kernel(
     const float* __restrict__ h, const float* __restrict__ dl, const float* __restrict__ dv,
     const float* __restrict__ wa, const float* __restrict__ wc, float* __restrict__ gp,
     float* __restrict__ dbh, float* __restrict__ dwa, float* __restrict__ dwc,
-    float* __restrict__ dba, float* __restrict__ dbc, int64_t M, int64_t H, int A, int chunks,
+    float* __restrict__ dba, float* __restrict__ dbc, int64_t M, int64_t H, int A, int K, int chunks,
     unsigned* __restrict__ tickets, float* __restrict__ partials) {
   constexpr int L = kWgL, RP = 64 / L, SW = 4 * L, KP = kHbKP, NV = KP + 1;
   __shared__ float red[4 * RP][SW][NV + 1];
   __shared__ float redc[4 * RP][KP];
   __shared__ int s_last;
-  const int K = A + 1;
+  // K = A + 1 with a critic row (dv, wc), K = A without (a single head, e.g. the DQN Q head)
   const int nstripes = static_cast<int>((H + SW - 1) / SW);
   const int stripe = blockIdx.x % nstripes;
   const int chunk = blockIdx.x / nstripes;
@@ -727,8 +727,9 @@ extern "C" int ocppo_heads_bwd(ocppo_stream_t stream, const float* h, const floa
                     A + 1 <= kHbKP,
                 "ocppo_heads_bwd: bad sizes M=%lld H=%lld A=%lld (M >= 1, H %% 4 == 0, "
                 "H <= 16384, 1 <= A <= 7)", (long long)M, (long long)H, (long long)A);
-  OCPPO_REQUIRE(h && dlogits && dvalue && wa && wc && gp && dwa && dwc && dba && dbc && workspace,
-                "ocppo_heads_bwd: null pointer");
+  OCPPO_REQUIRE(h && dlogits && wa && gp && dwa && dba && workspace &&
+                    (wc ? (dvalue && dwc && dbc) : (!dvalue && !dwc && !dbc)),
+                "ocppo_heads_bwd: null pointer (wc, dvalue, dwc, dbc: all set or all NULL)");
   OCPPO_REQUIRE(reinterpret_cast<uintptr_t>(h) % 16 == 0 &&
                     reinterpret_cast<uintptr_t>(gp) % 16 == 0 &&
                     reinterpret_cast<uintptr_t>(workspace) % 256 == 0,
@@ -739,15 +740,16 @@ extern "C" int ocppo_heads_bwd(ocppo_stream_t stream, const float* h, const floa
   clear_stale_error();
   hipStream_t s = as_stream(stream);
   const int chunks = wg_chunks(M, H);
+  const int K = static_cast<int>(A) + (wc ? 1 : 0);
   const int64_t stripes = (H + 4 * kWgL - 1) / (4 * kWgL);
   unsigned* tickets = static_cast<unsigned*>(workspace);
   float* partials = reinterpret_cast<float*>(static_cast<char*>(workspace) + kWgTicketBytes);
   const dim3 grid(static_cast<unsigned>(stripes * chunks)), block(256);
   if (relu)
     hipLaunchKernelGGL(heads_bwd_kernel<true>, grid, block, 0, s, h, dlogits, dvalue, wa, wc, gp,
-                       db_h, dwa, dwc, dba, dbc, M, H, (int)A, chunks, tickets, partials);
+                       db_h, dwa, dwc, dba, dbc, M, H, (int)A, K, chunks, tickets, partials);
   else
     hipLaunchKernelGGL(heads_bwd_kernel<false>, grid, block, 0, s, h, dlogits, dvalue, wa, wc, gp,
-                       db_h, dwa, dwc, dba, dbc, M, H, (int)A, chunks, tickets, partials);
+                       db_h, dwa, dwc, dba, dbc, M, H, (int)A, K, chunks, tickets, partials);
   return check_launch("ocppo_heads_bwd");
 }

@@ -38,7 +38,7 @@ import torch
 import torch.nn as nn
 
 from . import ops
-from .agents import Predictor, fused_trunk
+from .agents import Predictor, fused_trunk, q_head
 from .args import OBS_MODES, parse_dataclass
 from .envs import SyntheticAtariEnv
 
@@ -111,7 +111,7 @@ class QNetwork(Predictor):
         return self.network(x / 255.0)
 
     def q_values(self, x):
-        return fused_trunk(self.network, x / 255.0)
+        return q_head(fused_trunk(self.network[:-1], x / 255.0), self.network[-1])
 
     def get_action_and_value(self, x):
         """architectures/dqn.py:28-31 (greedy action; the eval harness uses element 0)."""
@@ -148,7 +148,7 @@ class QNetworkObj(Predictor):
         return self.network(x)
 
     def q_values(self, x):
-        return fused_trunk(self.network, x)
+        return q_head(fused_trunk(self.network[:-1], x), self.network[-1])
 
     get_action_and_value = QNetwork.get_action_and_value
     predict = QNetwork.predict

@@ -518,27 +518,34 @@ def heads_bwd(h, dlogits, dvalue, wa, wc, relu: bool = True, gp=None, db_h=None,
               dwc=None, dba=None, dbc=None):
     """Actor/critic heads' backward + the producing layer's ReLU backward in one pass (see
     include/ocppo.h). h [M, H] (the heads' input = decoder ReLU output), dlogits [M, A],
-    dvalue [M]; returns (gp, db_h, dwa, dwc, dba, dbc); db_h None skips the decoder bias."""
+    dvalue [M]; returns (gp, db_h, dwa, dwc, dba, dbc); db_h None skips the decoder bias.
+    dvalue = wc = None: a single head (dwc, dbc returned as None)."""
     M, H = h.shape
     A = dlogits.shape[1]
     dev = h.device
     f = torch.float32
+    critic = wc is not None
+    if critic != (dvalue is not None):
+        raise ValueError("dvalue and wc: both or neither")
     gp = torch.empty_like(h) if gp is None else gp
     dwa = torch.empty(A, H, dtype=f, device=dev) if dwa is None else dwa
-    dwc = torch.empty(1, H, dtype=f, device=dev) if dwc is None else dwc
     dba = torch.empty(A, dtype=f, device=dev) if dba is None else dba
-    dbc = torch.empty(1, dtype=f, device=dev) if dbc is None else dbc
+    if critic:
+        dwc = torch.empty(1, H, dtype=f, device=dev) if dwc is None else dwc
+        dbc = torch.empty(1, dtype=f, device=dev) if dbc is None else dbc
+    else:
+        dwc = dbc = None
     key = (dev, "hb", M, H, A)
     ws = _RB_WS.get(key)
     if ws is None:
         nb = int(_lib.LIB.ocppo_heads_bwd_workspace_bytes(M, H, A))
         ws = _RB_WS[key] = torch.zeros(nb, dtype=torch.uint8, device=dev)
     call("ocppo_heads_bwd", _stream(dev), _check(h, "h", f, dev, M * H),
-         _check(dlogits, "dlogits", f, dev, M * A), _check(dvalue, "dvalue", f, dev, M),
-         _check(wa, "wa", f, dev, A * H), _check(wc, "wc", f, dev, H),
+         _check(dlogits, "dlogits", f, dev, M * A), _opt(dvalue, "dvalue", f, dev, M),
+         _check(wa, "wa", f, dev, A * H), _opt(wc, "wc", f, dev, H),
          _check(gp, "gp", f, dev, M * H), _opt(db_h, "db_h", f, dev, H),
-         _check(dwa, "dwa", f, dev, A * H), _check(dwc, "dwc", f, dev, H),
-         _check(dba, "dba", f, dev, A), _check(dbc, "dbc", f, dev, 1), M, H, A,
+         _check(dwa, "dwa", f, dev, A * H), _opt(dwc, "dwc", f, dev, H),
+         _check(dba, "dba", f, dev, A), _opt(dbc, "dbc", f, dev, 1), M, H, A,
          1 if relu else 0, ws.data_ptr(), ws.numel())
     return gp, db_h, dwa, dwc, dba, dbc
 

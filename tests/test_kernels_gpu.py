@@ -956,3 +956,46 @@ def test_heads_function_matches_module_autograd(dev):
     torch.autograd.backward([logits, value], [dl, dv])
     for p, w in zip(params, want):
         torch.testing.assert_close(p.grad, w, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("M,H,A", [(32, 512, 6), (300, 64, 7), (5, 8, 2)])
+def test_heads_bwd_single_head(ops, dev, M, H, A):
+    """No critic row (wc = dvalue = None): the DQN Q head + producing ReLU, vs autograd (f64)."""
+    z = torch.randn(M, H, device=dev, dtype=torch.float64)
+    hd = torch.relu(z).requires_grad_(True)
+    wq = torch.randn(A, H, device=dev, dtype=torch.float64, requires_grad=True)
+    bq = torch.randn(A, device=dev, dtype=torch.float64, requires_grad=True)
+    g = torch.randn(M, A, device=dev, dtype=torch.float64)
+    (hd @ wq.t() + bq).backward(g)
+    gh = hd.grad * (z > 0)
+    f = torch.float32
+    gp, db_h, dw, dwc, db, dbc = ops.heads_bwd(hd.detach().to(f).contiguous(), g.to(f), None,
+                                               wq.detach().to(f), None, relu=True,
+                                               db_h=torch.empty(H, device=dev))
+    assert dwc is None and dbc is None
+    h32 = hd.detach().abs()
+    for got, want, scale in ((gp, gh, g.abs() @ wq.detach().abs()), (db_h, gh.sum(0), gh.abs().sum(0)),
+                             (dw, wq.grad, g.abs().t() @ h32), (db, bq.grad, g.abs().sum(0))):
+        assert ((got.double() - want).abs() / scale.clamp_min(1e-30)).max().item() < 1e-5
+
+
+def test_q_head_matches_module_autograd(dev):
+    """agents.q_head (fused single-head backward, premasked decoder) == ReLU Linear + Linear."""
+    from oc_cleanrl_amd import agents
+
+    torch.manual_seed(1)
+    M, K, H, A = 32, 48, 512, 6
+    dec, qh = torch.nn.Linear(K, H).to(dev), torch.nn.Linear(H, A).to(dev)
+    x, g = torch.randn(M, K, device=dev), torch.randn(M, A, device=dev)
+    qh(torch.relu(dec(x))).backward(g)
+    params = [dec.weight, dec.bias, qh.weight, qh.bias]
+    want = [p.grad.clone() for p in params]
+    for p in params:
+        p.grad = torch.zeros_like(p)
+        p._ocppo_direct_grad = True
+    h = agents.linear_act(x, dec, True)
+    q = agents.q_head(h, qh)
+    assert q.grad_fn is not None and "QHead" in type(q.grad_fn).__name__
+    q.backward(g)
+    for p, w in zip(params, want):
+        torch.testing.assert_close(p.grad, w, rtol=1e-4, atol=1e-5)
