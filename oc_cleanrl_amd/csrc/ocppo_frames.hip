@@ -98,43 +98,46 @@ __global__ __launch_bounds__(128) void frames_scatter_kernel(
     const float* __restrict__ dh, int64_t M, int64_t E, const int32_t* __restrict__ uniq,
     int64_t C, const int32_t* __restrict__ inv, int64_t mb, const float* __restrict__ dones,
     int64_t T, int64_t N, int W, float* __restrict__ denc) {
+  // slot i * W + k: the use of this frame by sample t = s + i at stack slot k (-1: none); thread
+  // i < W resolves sample t = s + i (its inv entry and latest reset) in parallel with the others
   __shared__ int64_t uses[kFramesMaxW * kFramesMaxW];
-  __shared__ int n_uses;
   const int64_t groups = E / VEC;
+  const int WW = W * W;
   for (int64_t c = blockIdx.x; c < C; c += gridDim.x) {
-    __syncthreads();  // the previous row's use list is no longer read
-    if (threadIdx.x == 0) {
-      int cnt = 0;
-      const int32_t u = uniq[c];
-      if (u >= 0) {
-        const int s = static_cast<int>(u / N) - (W - 1);
-        const int64_t n = u - (s + W - 1) * N;
-        const int t_hi = s + W - 1 < T - 1 ? s + W - 1 : static_cast<int>(T - 1);
-        for (int t = s > 0 ? s : 0; t <= t_hi; ++t) {
-          const int32_t p = inv[t * N + n];
-          if (p / M != mb) continue;
+    __syncthreads();  // the previous row's use slots are no longer read
+    for (int q = threadIdx.x; q < WW; q += blockDim.x) uses[q] = -1;
+    __syncthreads();
+    const int32_t u = uniq[c];
+    if (u >= 0 && static_cast<int>(threadIdx.x) < W) {
+      const int i = static_cast<int>(threadIdx.x);
+      const int s = static_cast<int>(u / N) - (W - 1);
+      const int64_t n = u - (s + W - 1) * N;
+      const int t = s + i;
+      if (t >= 0 && t <= T - 1) {
+        const int32_t p = inv[t * N + n];
+        if (p / M == mb) {
           const int64_t row = p - mb * M;
           const int r = latest_reset(dones, t, n, N, W);
           for (int k = 0; k < W; ++k) {
             int sk = t - (W - 1) + k;
             sk = sk > r ? sk : r;
-            if (sk == s) uses[cnt++] = row * W + k;
+            if (sk == s) uses[i * W + k] = row * W + k;
           }
         }
       }
-      n_uses = cnt;
     }
     __syncthreads();
-    const int cnt = n_uses;
     float* dst = denc + c * E;
     for (int64_t q = threadIdx.x; q < groups; q += blockDim.x) {
       const int64_t e = q * VEC;
       float acc[VEC];
 #pragma unroll
       for (int v = 0; v < VEC; ++v) acc[v] = 0.f;
-      for (int j = 0; j < cnt; ++j) {
+      for (int j = 0; j < WW; ++j) {  // (t ascending, k ascending): the fixed summation order
+        const int64_t us = uses[j];
+        if (us < 0) continue;
         float x[VEC];
-        VecIO<OCPPO_F32, VEC>::load(dh, uses[j] * E + e, x);
+        VecIO<OCPPO_F32, VEC>::load(dh, us * E + e, x);
 #pragma unroll
         for (int v = 0; v < VEC; ++v) acc[v] += x[v];
       }
