@@ -120,6 +120,8 @@ class Args:
     update_frame_dedup: bool = True  # PPO_OBJ update: encode each distinct frame of a minibatch once
     prefetch_shuffle: bool = True  # shuffle (+ frame plan) of the next iteration while the GPU runs
     dp_overlap: bool = True  # DP: all-reduce the decoder-side gradients during the encoder backward
+    dp_exchange: bool = False  # run the DP exchange path (per-minibatch graphs + all-reduce) even
+                               # at world size 1, over an initialised 1-rank process group
     conv_channels_last: bool = True  # pixel NatureCNN in NHWC (MIOpen NHWC kernels, no transposes)
     eval_episodes: int = 0  # after training: evaluate() episodes (the reference runs 10 when tracking)
     conv_benchmark: bool = False  # cudnn.benchmark (MIOpen Find) for the NatureCNN convolutions

@@ -252,9 +252,11 @@ class DQNTrainer:
                            self.actions, self.epsilon, step_offset=k + 1)
         self.env.step(self.actions, k)
         if a.vecnorm_reward:
+            # VecNormalize(envs, norm_obs=False, norm_reward=True) (:298) keeps SB3's default
+            # gamma = 0.99 whatever --gamma says (ops' default)
             ops.rollout_store_vecnorm(self.env.frame, self.env.reward, self.env.done, prev, nxt,
                                       self.net_obs, self.done_out, self.ret_state,
-                                      self.rms_state, self.rew_out, gamma=a.gamma)
+                                      self.rms_state, self.rew_out)
         else:
             ops.rollout_store(self.env.frame, self.env.reward, self.env.done, prev, nxt,
                               self.net_obs, self.rew_out, self.done_out)

@@ -38,14 +38,16 @@ from .args import Args
 from .envs import HostVecEnv, SyntheticAtariEnv
 
 
-def storage_dtype(args: Args, pixels: bool) -> torch.dtype:
-    """Rollout obs dtype. `auto` picks the narrowest EXACT type: u8 for ALE pixels, bf16 for
-    integer object coordinates (|x| <= 256), f32 when detection noise makes them fractional."""
+def storage_dtype(args: Args, pixels: bool, host_env: bool = False) -> torch.dtype:
+    """Rollout obs dtype. `auto` picks the narrowest EXACT type: u8 for ALE pixels, bf16 for the
+    synthetic env's integer object coordinates (|x| <= 256), f32 when detection noise makes them
+    fractional and for host envs, whose feature ranges nothing here pins (OCAtari is
+    un-vendored): pass obs_storage="bf16" for a host env known to emit integers |x| <= 256."""
     choice = args.obs_storage
     if choice == "auto":
         if pixels:
             return torch.uint8
-        return torch.bfloat16 if args.noise_std == 0.0 else torch.float32
+        return torch.bfloat16 if args.noise_std == 0.0 and not host_env else torch.float32
     return {"f32": torch.float32, "bf16": torch.bfloat16, "u8": torch.uint8}[choice]
 
 
@@ -129,6 +131,10 @@ class PPOTrainer:
         self.args = args
         self.dev = torch.device(device)
         self.rank, self.world = rank, world_size
+        # the DP exchange path (per-minibatch graphs around an all-reduce of the flat grad buffer);
+        # at world size 1 only on request (dp_exchange), over an initialised 1-rank group
+        self.dp = world_size > 1 or (args.dp_exchange and dist.is_available()
+                                     and dist.is_initialized())
         self.log_enabled = log and rank == 0
         a = args
         if envs is None and a.backend != "Synthetic":
@@ -202,7 +208,7 @@ class PPOTrainer:
         T, N = self.T, self.N
         f32 = torch.float32
         dev = self.dev
-        self.obs_dtype = storage_dtype(a, self.pixels)
+        self.obs_dtype = storage_dtype(a, self.pixels, self.host_env)
         self.obs = torch.zeros((T + 1, N) + self.obs_shape, dtype=self.obs_dtype, device=dev)
         self.net_obs = torch.empty((N,) + self.obs_shape, dtype=f32, device=dev,
                                    memory_format=self.net_format).zero_()
@@ -233,6 +239,8 @@ class PPOTrainer:
         # in perm_stage and is moved into perm_dev (which the graphs read) at iteration start
         self.perm_stage = torch.zeros_like(self.perm_dev)
         self.staged = False
+        self.staged_rng_state = self.current_rng_state = None
+        self.executed_mb = self.E * self.nmb  # minibatches the last update ran (target_kl)
         self.perm_event = torch.cuda.Event()
         self.perm_event.record()
         # PPObj update with every distinct frame of a minibatch encoded once (frames.py)
@@ -247,7 +255,7 @@ class PPOTrainer:
         # buffer's tail (last encoder layer + decoder + heads, ~70 % of the bytes for PPObj)
         # overlaps the backward of the layers below (_exchange)
         self.split, self.tail_off, self.cuts = 0, 0, {}
-        if world_size > 1 and a.dp_overlap and self.frame_dedup and len(a.encoder_dims) >= 2:
+        if self.dp and a.dp_overlap and self.frame_dedup and len(a.encoder_dims) >= 2:
             self.split = 2 * (len(a.encoder_dims) - 1)  # network[:split] = the layers below
             first_tail = self.agent.network[self.split].weight
             offs, _ = ops.flat_offsets(self.params)
@@ -472,7 +480,7 @@ class PPOTrainer:
         for k in range(self.nmb):
             j = epoch * self.nmb + k
             self._forward_backward(j)
-            if self.world > 1:
+            if self.dp:
                 self._exchange(j, replay=False)
             self._opt_step()
 
@@ -483,6 +491,8 @@ class PPOTrainer:
         for iteration i+1 while the GPU executes iteration i (same RNG stream order)."""
         self.perm_event.synchronize()  # the previous async copies out of the host buffers are done
         out = self.perm_host.numpy()
+        self.staged_rng_state = self.np_rng.get_state()
+        self.b_inds = np.arange(self.B)  # b_inds = np.arange(batch_size) every iteration (:558)
         for e in range(self.E):
             self.np_rng.shuffle(self.b_inds)
             out[e * self.B:(e + 1) * self.B] = self.b_inds
@@ -496,6 +506,14 @@ class PPOTrainer:
         self.perm_stage.copy_(self.perm_host, non_blocking=True)
         self.perm_event.record()
         self.staged = True
+
+    def _rewind_shuffle(self, epochs: int):
+        """target_kl stopped the update after `epochs` epochs: the reference drew only that many
+        shuffles this iteration (:561), so put the np RNG where those draws leave it."""
+        self.np_rng.set_state(self.current_rng_state)
+        b = np.arange(self.B)
+        for _ in range(epochs):
+            self.np_rng.shuffle(b)
 
     def _alloc_plan(self, cap: int):
         """(Re)size the frame-plan buffers for `cap` distinct frames per minibatch. A resize
@@ -516,6 +534,7 @@ class PPOTrainer:
         """Move the staged shuffle / frame plan into the buffers the graphs read."""
         if not self.staged:
             self._shuffle()
+        self.current_rng_state = self.staged_rng_state
         self.perm_dev.copy_(self.perm_stage)
         if self.frame_dedup:
             self.plan_dev.copy_(self.plan_stage)
@@ -541,7 +560,7 @@ class PPOTrainer:
                 self.g_host.append(g)
         if not self.graph_update:
             pass
-        elif self.world == 1:
+        elif not self.dp:
             for e in range(self.E):
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, pool=pool):
@@ -566,10 +585,13 @@ class PPOTrainer:
         self.graphs_ready = True
 
     def _run_update(self):
+        """update_epochs x num_minibatches updates (:560-617); with target_kl, the epoch loop
+        stops after the first epoch whose last minibatch's approx_kl exceeds it (:616-617)."""
         a = self.args
+        self.executed_mb = 0
         for e in range(self.E):
             if self.graphs_ready and self.graph_update:
-                if self.world == 1:
+                if not self.dp:
                     self.g_update[e].replay()
                 else:
                     for k in range(self.nmb):
@@ -579,9 +601,12 @@ class PPOTrainer:
                         self.g_opt.replay()
             else:
                 self._update_epoch(e)
+            self.executed_mb += self.nmb
             if a.target_kl is not None:
                 kl = float(self.stats[e * self.nmb + self.nmb - 1, 5])
                 if kl > a.target_kl:
+                    if e + 1 < self.E:
+                        self._rewind_shuffle(e + 1)
                     break
 
     # ------------------------------------------------------------------------------------------
@@ -619,7 +644,9 @@ class PPOTrainer:
         y_pred = self.values[:self.T].double().reshape(-1)
         var_y = torch.var(y_true, unbiased=False)
         ev = 1 - torch.var(y_true - y_pred, unbiased=False) / var_y
-        stats = self.stats.cpu().numpy()  # sync point
+        # rows of the minibatches this iteration executed (target_kl may stop early): the scalars
+        # of the last executed one, clipfrac averaged over the executed ones (:616-638)
+        stats = self.stats[:self.executed_mb].cpu().numpy()  # sync point
         ep_ret, ep_len, ep_n = self.env.pop_episode_stats()
         last = stats[-1]
         m = {

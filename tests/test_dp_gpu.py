@@ -52,6 +52,57 @@ def test_two_ranks_share_one_gpu_over_gloo(fused_opt, graphs):
 
 
 
+def _rccl_worker(rank, world, port, out, overlap, graphs):
+    """The RCCL exchange path at world size 1: nccl (= RCCL) process group bound to cuda:0,
+    per-minibatch graphs, the async tail all-reduce overlapped with the g_low replay, the head
+    all-reduce, g_opt -- against the plain single-GPU trainer in the same process."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    from oc_cleanrl_amd.args import Args, finalize
+    from oc_cleanrl_amd.trainer import PPOTrainer
+
+    def args(dp):
+        return finalize(Args(env_id="ALE/Pong-v5", obs_mode="obj", architecture="PPO_OBJ",
+                             num_envs=32, num_steps=16, num_minibatches=4, update_epochs=2,
+                             total_timesteps=32 * 16 * 10, encoder_dims=(32, 64, 48),
+                             decoder_dims=(64,), save_model=False, cuda_graphs=graphs,
+                             dp_overlap=overlap, dp_exchange=dp), 1)
+
+    plain = PPOTrainer(args(False), dev)
+    for _ in range(3):
+        plain.train_iteration()
+    torch.cuda.synchronize()
+    assert not plain.dp
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    assert dist.get_backend() == "nccl"
+    tr = PPOTrainer(args(True), dev)
+    assert tr.dp and bool(tr.split) == overlap
+    for _ in range(3):
+        tr.train_iteration()
+    torch.cuda.synchronize()
+    if graphs:
+        assert tr.graphs_ready and len(tr.g_update) == tr.E * tr.nmb and tr.g_opt is not None
+        assert len(tr.g_low) == (tr.E * tr.nmb if overlap else 0)
+    flat = lambda t: torch.cat([p.detach().flatten() for p in t.agent.parameters()]).cpu()  # noqa
+    out["plain"], out["dp"] = flat(plain), flat(tr)
+    out["same_actions"] = bool(torch.equal(plain.actions, tr.actions))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("overlap,graphs", [(True, True), (False, True), (True, False)])
+def test_rccl_exchange_one_rank_matches_single_gpu(overlap, graphs):
+    """ppo_atari_multigpu.py:174-183, 360-377 over RCCL on the one-GPU box: the DP flow with a
+    1-rank nccl group leaves parameters bit-identical to the single-GPU trainer after 3
+    iterations (SUM over one rank, /1 folded into Adam)."""
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_rccl_worker, args=(1, _port(), out, overlap, graphs), nprocs=1, join=True)
+    assert out["same_actions"]
+    assert torch.equal(out["plain"], out["dp"]), \
+        float((out["plain"] - out["dp"]).abs().max())
+
+
 @pytest.mark.parametrize("graphs", [True, False])
 def test_overlapped_exchange_equals_single_allreduce(graphs):
     """dp_overlap (tail all-reduce during the lower layers' backward, then the head) gives the

@@ -27,7 +27,8 @@ def test_host_env_matches_device_env(dev, pixels):
 
     kw = dict(env_id="ALE/Breakout-v5", obs_mode="dqn", architecture="PPO", num_envs=8,
               num_steps=8, update_epochs=1) if pixels else {}
-    a = _args(**kw)
+    # the synthetic frames are integers <= 210: bf16 storage is exact (host envs default to f32)
+    a = _args(obs_storage="bf16", **kw)
     names = ("obs", "rewards", "dones", "actions", "logprobs", "values", "advantages", "returns")
     # one learner after the other: both draw their sampling noise from torch's global generator,
     # which each PPOTrainer re-seeds at construction

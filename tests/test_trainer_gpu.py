@@ -311,3 +311,57 @@ def test_two_minibatch_updates_match_reference_golden_naturecnn(dev):
             if f"pick::{k}" in z:
                 got = got[torch.from_numpy(z[f"pick::{k}"])]
             torch.testing.assert_close(got, ref, rtol=0, atol=0.01 * 2.5e-4)
+
+
+def _reference_perms(seed, B, E, iterations, epochs_run=None):
+    """The reference's shuffle stream (ppo_atari_oc.py:558-561): b_inds = arange every
+    iteration, one np.random.shuffle per executed epoch, legacy global RNG seeded with `seed`."""
+    rng = np.random.RandomState(seed)
+    out = []
+    for _ in range(iterations):
+        b = np.arange(B)
+        perms = []
+        for _ in range(E if epochs_run is None else epochs_run):
+            rng.shuffle(b)
+            perms.append(b.copy())
+        out.append(np.concatenate(perms))
+    return out
+
+
+def test_shuffle_stream_matches_reference(dev):
+    from oc_cleanrl_amd.trainer import PPOTrainer
+
+    a = small_args()
+    tr = PPOTrainer(a, dev)
+    ref = _reference_perms(a.seed, a.local_batch_size, a.update_epochs, 3)
+    for it in range(3):
+        tr.train_iteration()
+        assert np.array_equal(tr.perm_dev.cpu().numpy(), ref[it]), it
+
+
+@pytest.mark.parametrize("graphs", [True, False])
+def test_target_kl_early_stop(dev, graphs):
+    """target_kl (:616-617): approx_kl >= 0 always exceeds -1, so every iteration stops after its
+    first epoch. Metrics come from the executed minibatches only (no stale rows of skipped ones),
+    and the np RNG advances by one shuffle per executed epoch, as the reference's does."""
+    from oc_cleanrl_amd.trainer import PPOTrainer
+
+    a = small_args(target_kl=-1.0, cuda_graphs=graphs)
+    tr = PPOTrainer(a, dev)
+    ref = _reference_perms(a.seed, a.local_batch_size, a.update_epochs, 3, epochs_run=1)
+    B = a.local_batch_size
+    for it in range(3):
+        tr.stats.fill_(float("nan"))  # rows a skipped minibatch would leave stale
+        m = tr.train_iteration()
+        assert tr.executed_mb == a.num_minibatches
+        assert np.array_equal(tr.perm_dev[:B].cpu().numpy(), ref[it]), it
+        st = tr.stats.cpu().numpy()
+        n = a.num_minibatches
+        assert np.isfinite(st[:n]).all() and np.isnan(st[n:]).all()
+        assert m["losses/loss"] == float(st[n - 1, 0])
+        assert m["losses/approx_kl"] == float(st[n - 1, 5])
+        assert abs(m["losses/clipfrac"] - float(np.mean(st[:n, 6]))) < 1e-7
+    # without target_kl every epoch runs
+    tr2 = PPOTrainer(small_args(cuda_graphs=graphs), dev)
+    tr2.train_iteration()
+    assert tr2.executed_mb == a.update_epochs * a.num_minibatches
