@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define OCPPO_ABI_VERSION 5
+#define OCPPO_ABI_VERSION 7
 
 /* status codes */
 #define OCPPO_OK 0
@@ -217,14 +217,19 @@ OCPPO_API int ocppo_categorical_logprob_entropy_bwd(ocppo_stream_t stream, const
  *                bit 1 (OCPPO_NET_SCALE_255): net_obs = value / 255 as ATen computes it
  *                (x * (1.0f / 255.0f)) -- the NatureCNN's NormalizeImg (architectures/common.py:19-22)
  *                folded into the store
- * Stacking: obs_out[n] = prev_obs[n][1:] ++ frame[n]; on done[n] every slot is frame[n] (the
- * gymnasium FrameStack reset fill). Conversion to bf16 is round-to-nearest-even and exact for
- * the integer-valued obs of both modes (|x| <= 256).
+ *   reset_prev : [N, W-1, D] frame_dtype or NULL: the older W-1 frames of the observation the env
+ *                itself returned on a done (read for done rows only)
+ * Stacking: obs_out[n] = prev_obs[n][1:] ++ frame[n]; on done[n] the older W-1 slots are
+ * reset_prev[n] when given (a host env whose reset stack holds distinct frames: the reference's
+ * NoopResetEnv/FireResetEnv step after reset, EpisodicLifeEnv signals done on a life loss without
+ * resetting the stack, ppo_atari_oc.py:278-282), else frame[n] (the gymnasium FrameStack reset
+ * fill). Conversion to bf16 is round-to-nearest-even and exact for the integer-valued obs of both
+ * modes (|x| <= 256).
  * ------------------------------------------------------------------------------------------- */
 OCPPO_API int ocppo_rollout_store(ocppo_stream_t stream, const void* frame, int frame_dtype,
                         const float* reward, const float* done, int64_t N, int64_t W, int64_t D,
                         const void* prev_obs, void* obs_out, int obs_dtype, float* net_obs,
-                        float* reward_out, float* done_out, int net_flags);
+                        float* reward_out, float* done_out, int net_flags, const void* reset_prev);
 
 /* Fill a whole stacked-obs slot from one frame per env (env reset, ppo_atari_oc.py:464-465);
  * net_flags as in ocppo_rollout_store. */
@@ -397,7 +402,8 @@ OCPPO_API int ocppo_rollout_store_vecnorm(ocppo_stream_t stream, const void* fra
                                           int64_t W, int64_t D, const void* prev_obs, void* obs_out,
                                           int obs_dtype, float* net_obs, float* done_out,
                                           double gamma, double epsilon, double clip_reward,
-                                          double* ret_state, double* rms_state, float* reward_out, int net_flags);
+                                          double* ret_state, double* rms_state, float* reward_out, int net_flags,
+                                          const void* reset_prev);
 
 /* ---------------------------------------------------------------------------------------------
  * DQN (config 5, dqn_atari_oc.py) — HBM replay buffer with stable-baselines3 2.0.0
@@ -451,6 +457,22 @@ OCPPO_API int ocppo_td_loss_fwd_bwd(ocppo_stream_t stream, const float* q, const
 OCPPO_API int ocppo_synth_env_step(ocppo_stream_t stream, uint64_t seed, const int64_t* step_base,
                          int64_t step_offset, const int64_t* actions, int64_t N, int64_t D, int pixel_mode,
                          void* frame_out, float* reward_out, float* done_out, float* ep_state);
+
+/* ---------------------------------------------------------------------------------------------
+ * CartPole-v1 vector env (config 1: cleanrl/ppo.py:81-91, 162 -- SyncVectorEnv of
+ * RecordEpisodeStatistics(gym.make("CartPole-v1"))), device-resident. gymnasium 0.28.1
+ * cartpole.py dynamics in f64 (Euler, same constants and op order), reward 1 per step,
+ * TimeLimit 500, same-step auto-reset (obs of a done env = its reset obs), obs = f32(state).
+ * Reset states ~ U(-0.05, 0.05)^4 from a counter-based stream of (seed, env, episode index).
+ *   actions  : [N] i64 (0 = push left, 1 = push right), or NULL = reset every env
+ *   state    : [N, 4] f64 (x, x_dot, theta, theta_dot), in/out
+ *   counters : [N, 2] i64 = {elapsed steps, episodes started}, in/out (zero-initialised)
+ *   obs_out  : [N, 4] f32;  reward_out, done_out : [N] f32 (may be NULL on reset)
+ *   ep_state : [N, 5] f32 RecordEpisodeStatistics counters as in ocppo_synth_env_step, or NULL
+ * ------------------------------------------------------------------------------------------- */
+OCPPO_API int ocppo_cartpole_step(ocppo_stream_t stream, uint64_t seed, const int64_t* actions,
+                                  int64_t N, double* state, int64_t* counters, float* obs_out,
+                                  float* reward_out, float* done_out, float* ep_state);
 
 #ifdef __cplusplus
 }

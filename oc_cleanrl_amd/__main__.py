@@ -11,8 +11,8 @@ from .args import env_rank, finalize, parse_args
 from .trainer import run
 
 
-def main(argv=None):
-    args = parse_args(argv)
+def main(argv=None, defaults: dict | None = None):
+    args = parse_args(argv, defaults)
     rank, local_rank, world = env_rank()
     args = finalize(args, world)
     if args.device_ids:
@@ -31,6 +31,7 @@ def main(argv=None):
     finally:
         if world > 1:
             dist.destroy_process_group()
+    return tr
 
 
 if __name__ == "__main__":

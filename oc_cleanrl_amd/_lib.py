@@ -22,7 +22,7 @@ LIB_PATH = Path(os.environ.get("OCPPO_LIB", PKG / "lib" / "libocppo_hip.so"))
 HEADER = PKG.parent / "include" / "ocppo.h"
 
 # constants mirrored from include/ocppo.h (checked against the header by tests/test_abi.py)
-OCPPO_ABI_VERSION = 5
+OCPPO_ABI_VERSION = 7
 OCPPO_OK, OCPPO_E_INVALID, OCPPO_E_LAUNCH, OCPPO_E_WORKSPACE = 0, 1, 2, 3
 OCPPO_F32, OCPPO_BF16, OCPPO_U8 = 0, 1, 2
 STAT_NAMES = ("loss", "pg_loss", "v_loss", "entropy", "old_approx_kl", "approx_kl", "clipfrac",
@@ -47,7 +47,7 @@ SIGNATURES: dict[str, tuple[type, list]] = {
     "ocppo_policy_head_sample": (I, [P, P, I64, I64, P, P, P, P, P, I64, P, P, P, P, P]),
     "ocppo_categorical_logprob_entropy": (I, [P, P, P, I64, I64, P, P]),
     "ocppo_categorical_logprob_entropy_bwd": (I, [P, P, P, P, P, I64, I64, P]),
-    "ocppo_rollout_store": (I, [P, P, I, P, P, I64, I64, I64, P, P, I, P, P, P, I]),
+    "ocppo_rollout_store": (I, [P, P, I, P, P, I64, I64, I64, P, P, I, P, P, P, I, P]),
     "ocppo_obs_reset": (I, [P, P, I, I64, I64, I64, P, I, P, I]),
     "ocppo_gather_rows": (I, [P, P, I, P, I64, I64, P]),
     "ocppo_gather_rows_cl": (I, [P, P, I, P, I64, I64, I64, P, I]),
@@ -67,7 +67,7 @@ SIGNATURES: dict[str, tuple[type, list]] = {
     "ocppo_frames_scatter": (I, [P, P, I64, I64, P, I64, P, I64, P, I64, I64, I64, P]),
     "ocppo_vecnorm_reward": (I, [P, P, P, I64, D, D, D, P, P, P]),
     "ocppo_rollout_store_vecnorm": (I, [P, P, I, P, P, I64, I64, I64, P, P, I, P, P, D, D, D, P,
-                                        P, P, I]),
+                                        P, P, I, P]),
     "ocppo_replay_workspace_bytes": (SZ, []),
     "ocppo_replay_add": (I, [P, P, P, I, P, P, P, I64, I64, P, I64, P, I, P, P, P, P]),
     "ocppo_replay_sample": (I, [P, U64, P, P, I64, I64, I64, P, I, P, P, P, I64, P, P, P, P, P,
@@ -75,6 +75,7 @@ SIGNATURES: dict[str, tuple[type, list]] = {
     "ocppo_epsilon_greedy": (I, [P, P, I64, I64, U64, P, I64, D, D, D, P, P]),
     "ocppo_td_loss_fwd_bwd": (I, [P, P, P, P, P, P, I64, I64, D, P, P]),
     "ocppo_synth_env_step": (I, [P, U64, P, I64, P, I64, I64, I, P, P, P, P]),
+    "ocppo_cartpole_step": (I, [P, U64, P, I64, P, P, P, P, P, P]),
 }
 
 

@@ -528,6 +528,10 @@ class CartPoleAgent(_ActorCritic):
             layer_init(nn.Linear(64, envs.action_space.n), std=0.01))
         self.network = nn.Identity()
 
+    def trunk(self, x, prescaled: bool = False):
+        """The raw observation, flattened per sample ([B, 4] from the rollout's [B, 1, 4])."""
+        return x.reshape(x.shape[0], -1)
+
 
 class Space:
     """Minimal gym-like space (shape / n) for constructing agents without gymnasium."""

@@ -198,7 +198,7 @@ def finalize(args: Args, world_size: int = 1) -> Args:
     if "masked" in args.obs_mode:
         raise NotImplementedError("masked_* observation modes need the un-vendored ocatari_wrappers"
                                   " (out of scope); use obs_mode dqn or obj")
-    if args.obs_mode == "obj" and args.architecture != "PPO_OBJ":
+    if args.obs_mode == "obj" and args.architecture not in ("PPO_OBJ", "CARTPOLE_MLP"):
         raise AssertionError('"obj" observations only work with "PPO_OBJ" architecture!')
     if args.local_batch_size % args.num_minibatches:
         raise ValueError("local batch size must be divisible by num_minibatches")

@@ -10,7 +10,10 @@
 namespace ocppo {
 
 // ---- rollout store ----------------------------------------------------------------------------
-// obs_out[n, w, :] = done[n] || w == W-1 ? frame[n, :] : prev_obs[n, w+1, :]
+// obs_out[n, w, :] = w == W-1 ? frame[n, :] : done[n] ? R(n, w) : prev_obs[n, w+1, :]
+// R(n, w) = reset_prev[n, w, :] when the caller passes the older W-1 frames of the env's own reset
+// observation (host envs whose reset stack is not W copies of one frame: NoopReset/EpisodicLife
+// steps), else frame[n, :] (FrameStack's fill of a fresh episode).
 // Work split over `nblk` workgroups starting at workgroup `blk` (grid-stride).
 template <int FDT, int ODT, int VEC>
 __device__ __forceinline__ void store_groups(int64_t blk, int64_t nblk, const void* __restrict__ frame,
@@ -19,7 +22,8 @@ __device__ __forceinline__ void store_groups(int64_t blk, int64_t nblk, const vo
                                              int64_t D, const void* __restrict__ prev,
                                              void* __restrict__ out, float* __restrict__ net,
                                              float* __restrict__ reward_out,
-                                             float* __restrict__ done_out, float net_scale) {
+                                             float* __restrict__ done_out, float net_scale,
+                                             const void* __restrict__ reset_prev) {
   const int64_t DG = D / VEC;
   const int64_t groups = N * W * DG;
   const int64_t stride = nblk * blockDim.x;
@@ -29,8 +33,11 @@ __device__ __forceinline__ void store_groups(int64_t blk, int64_t nblk, const vo
     const int w = static_cast<int>(rem / DG);
     const int64_t k = (rem - static_cast<int64_t>(w) * DG) * VEC;
     float v[VEC];
-    if (w == W - 1 || done[n] != 0.f)
+    if (w == W - 1)
       VecIO<FDT, VEC>::load(frame, n * D + k, v);
+    else if (done[n] != 0.f)
+      VecIO<FDT, VEC>::load(reset_prev ? reset_prev : frame,
+                            reset_prev ? (n * (W - 1) + w) * D + k : n * D + k, v);
     else
       VecIO<ODT, VEC>::load(prev, (n * W + w + 1) * D + k, v);
     const int64_t o = (n * W + w) * D + k;
@@ -60,7 +67,8 @@ __device__ __forceinline__ void store_groups_cl(int64_t blk, int64_t nblk,
                                                 int64_t D, const void* __restrict__ prev,
                                                 void* __restrict__ out, float* __restrict__ net,
                                                 float* __restrict__ reward_out,
-                                                float* __restrict__ done_out, float net_scale) {
+                                                float* __restrict__ done_out, float net_scale,
+                                                const void* __restrict__ reset_prev) {
   const int64_t DG = D / VEC;
   const int64_t groups = N * DG;
   const int64_t stride = nblk * blockDim.x;
@@ -73,8 +81,10 @@ __device__ __forceinline__ void store_groups_cl(int64_t blk, int64_t nblk,
       float v[4][VEC];
 #pragma unroll
       for (int w = 0; w < 4; ++w) {
-        if (w == 3 || reset)
+        if (w == 3 || (reset && !reset_prev))
           VecIO<FDT, VEC>::load(frame, n * D + k, v[w]);
+        else if (reset)
+          VecIO<FDT, VEC>::load(reset_prev, (n * 3 + w) * D + k, v[w]);
         else
           VecIO<ODT, VEC>::load(prev, (n * 4 + w + 1) * D + k, v[w]);
         VecIO<ODT, VEC>::store(out, (n * 4 + w) * D + k, v[w]);
@@ -90,8 +100,10 @@ __device__ __forceinline__ void store_groups_cl(int64_t blk, int64_t nblk,
     } else {
       for (int w = 0; w < W; ++w) {
         float v[VEC];
-        if (w == W - 1 || reset)
+        if (w == W - 1 || (reset && !reset_prev))
           VecIO<FDT, VEC>::load(frame, n * D + k, v);
+        else if (reset)
+          VecIO<FDT, VEC>::load(reset_prev, (n * (W - 1) + w) * D + k, v);
         else
           VecIO<ODT, VEC>::load(prev, (n * W + w + 1) * D + k, v);
         VecIO<ODT, VEC>::store(out, (n * W + w) * D + k, v);
@@ -111,13 +123,13 @@ __global__ __launch_bounds__(256) void rollout_store_kernel(
     const void* __restrict__ frame, const float* __restrict__ reward,
     const float* __restrict__ done, int64_t N, int W, int64_t D, const void* __restrict__ prev,
     void* __restrict__ out, float* __restrict__ net, float* __restrict__ reward_out,
-    float* __restrict__ done_out, float net_scale) {
+    float* __restrict__ done_out, float net_scale, const void* __restrict__ reset_prev) {
   if (CL)
     store_groups_cl<FDT, ODT, VEC>(blockIdx.x, gridDim.x, frame, reward, done, N, W, D, prev, out,
-                                   net, reward_out, done_out, net_scale);
+                                   net, reward_out, done_out, net_scale, reset_prev);
   else
     store_groups<FDT, ODT, VEC>(blockIdx.x, gridDim.x, frame, reward, done, N, W, D, prev, out,
-                                net, reward_out, done_out, net_scale);
+                                net, reward_out, done_out, net_scale, reset_prev);
 }
 
 template <int FDT, int ODT, int VEC, bool CL>
@@ -277,17 +289,17 @@ __global__ __launch_bounds__(256) void store_vecnorm_kernel(
     const float* __restrict__ done, int64_t N, int W, int64_t D, const void* __restrict__ prev,
     void* __restrict__ out, float* __restrict__ net, float* __restrict__ done_out, double gamma,
     double eps, double clip, double* __restrict__ ret, double* __restrict__ rms,
-    float* __restrict__ reward_out, float net_scale) {
+    float* __restrict__ reward_out, float net_scale, const void* __restrict__ reset_prev) {
   if (blockIdx.x == 0) {
     vecnorm_block(reward, done, N, gamma, eps, clip, ret, rms, reward_out);
     return;
   }
   if (CL)
     store_groups_cl<FDT, ODT, VEC>(blockIdx.x - 1, gridDim.x - 1, frame, reward, done, N, W, D,
-                                   prev, out, net, nullptr, done_out, net_scale);
+                                   prev, out, net, nullptr, done_out, net_scale, reset_prev);
   else
     store_groups<FDT, ODT, VEC>(blockIdx.x - 1, gridDim.x - 1, frame, reward, done, N, W, D, prev,
-                                out, net, nullptr, done_out, net_scale);
+                                out, net, nullptr, done_out, net_scale, reset_prev);
 }
 
 // ---- synthetic env ------------------------------------------------------------------------------
@@ -366,15 +378,15 @@ inline int64_t store_groups_count(int64_t N, int64_t W, int64_t D, int vec, bool
 template <int FDT, int ODT, bool CL>
 int launch_store(hipStream_t s, const void* frame, const float* reward, const float* done,
                  int64_t N, int64_t W, int64_t D, const void* prev, void* out, float* net,
-                 float* rout, float* dout, float sc) {
+                 float* rout, float* dout, float sc, const void* rp) {
   if (D % 4 == 0)
     hipLaunchKernelGGL((rollout_store_kernel<FDT, ODT, 4, CL>),
                        dim3(grid_for(store_groups_count(N, W, D, 4, CL), 256)), dim3(256), 0, s,
-                       frame, reward, done, N, (int)W, D, prev, out, net, rout, dout, sc);
+                       frame, reward, done, N, (int)W, D, prev, out, net, rout, dout, sc, rp);
   else
     hipLaunchKernelGGL((rollout_store_kernel<FDT, ODT, 1, CL>),
                        dim3(grid_for(store_groups_count(N, W, D, 1, CL), 256)), dim3(256), 0, s,
-                       frame, reward, done, N, (int)W, D, prev, out, net, rout, dout, sc);
+                       frame, reward, done, N, (int)W, D, prev, out, net, rout, dout, sc, rp);
   return check_launch("ocppo_rollout_store");
 }
 
@@ -384,6 +396,7 @@ struct VecNormArgs {
   double* rms;
   float* reward_out;
   float net_scale;
+  const void* reset_prev;
 };
 
 template <int FDT, int ODT, bool CL>
@@ -394,12 +407,14 @@ int launch_store_vecnorm(hipStream_t s, const void* frame, const float* reward, 
     hipLaunchKernelGGL((store_vecnorm_kernel<FDT, ODT, 4, CL>),
                        dim3(1 + grid_for(store_groups_count(N, W, D, 4, CL), 256)), dim3(256), 0,
                        s, frame, reward, done, N, (int)W, D, prev, out, net, dout, vn.gamma,
-                       vn.eps, vn.clip, vn.ret, vn.rms, vn.reward_out, vn.net_scale);
+                       vn.eps, vn.clip, vn.ret, vn.rms, vn.reward_out, vn.net_scale,
+                       vn.reset_prev);
   else
     hipLaunchKernelGGL((store_vecnorm_kernel<FDT, ODT, 1, CL>),
                        dim3(1 + grid_for(store_groups_count(N, W, D, 1, CL), 256)), dim3(256), 0,
                        s, frame, reward, done, N, (int)W, D, prev, out, net, dout, vn.gamma,
-                       vn.eps, vn.clip, vn.ret, vn.rms, vn.reward_out, vn.net_scale);
+                       vn.eps, vn.clip, vn.ret, vn.rms, vn.reward_out, vn.net_scale,
+                       vn.reset_prev);
   return check_launch("ocppo_rollout_store_vecnorm");
 }
 
@@ -496,7 +511,7 @@ extern "C" int ocppo_rollout_store(ocppo_stream_t stream, const void* frame, int
                                    const float* reward, const float* done, int64_t N, int64_t W,
                                    int64_t D, const void* prev_obs, void* obs_out, int obs_dtype,
                                    float* net_obs, float* reward_out, float* done_out,
-                                   int net_flags) {
+                                   int net_flags, const void* reset_prev) {
   OCPPO_REQUIRE(N >= 0 && W >= 1 && D >= 1 && W <= 64, "ocppo_rollout_store: bad sizes");
   OCPPO_REQUIRE((net_flags & ~3) == 0 &&
                     (!(net_flags & OCPPO_NET_CHANNELS_LAST) || (net_obs && aligned16(net_obs))),
@@ -514,10 +529,11 @@ extern "C" int ocppo_rollout_store(ocppo_stream_t stream, const void* frame, int
   hipStream_t s = as_stream(stream);
 #define OCPPO_STORE(F, O)                                                                     \
   if (frame_dtype == F && obs_dtype == O)                                                     \
-    return net_layout ? launch_store<F, O, true>(s, frame, reward, done, N, W, D, prev_obs,   \
-                                                 obs_out, net_obs, reward_out, done_out, sc)  \
-                      : launch_store<F, O, false>(s, frame, reward, done, N, W, D, prev_obs,  \
-                                                  obs_out, net_obs, reward_out, done_out, sc);
+    return net_layout                                                                        \
+               ? launch_store<F, O, true>(s, frame, reward, done, N, W, D, prev_obs, obs_out,  \
+                                          net_obs, reward_out, done_out, sc, reset_prev)       \
+               : launch_store<F, O, false>(s, frame, reward, done, N, W, D, prev_obs, obs_out, \
+                                           net_obs, reward_out, done_out, sc, reset_prev);
   OCPPO_STORE(OCPPO_F32, OCPPO_F32)
   OCPPO_STORE(OCPPO_F32, OCPPO_BF16)
   OCPPO_STORE(OCPPO_F32, OCPPO_U8)
@@ -625,7 +641,8 @@ extern "C" int ocppo_rollout_store_vecnorm(ocppo_stream_t stream, const void* fr
                                            void* obs_out, int obs_dtype, float* net_obs,
                                            float* done_out, double gamma, double epsilon,
                                            double clip_reward, double* ret_state,
-                                           double* rms_state, float* reward_out, int net_flags) {
+                                           double* rms_state, float* reward_out, int net_flags,
+                                           const void* reset_prev) {
   OCPPO_REQUIRE(N >= 1 && W >= 1 && D >= 1 && W <= 64, "ocppo_rollout_store_vecnorm: bad sizes");
   OCPPO_REQUIRE((net_flags & ~3) == 0 &&
                     (!(net_flags & OCPPO_NET_CHANNELS_LAST) || (net_obs && aligned16(net_obs))),
@@ -641,7 +658,8 @@ extern "C" int ocppo_rollout_store_vecnorm(ocppo_stream_t stream, const void* fr
   OCPPO_REQUIRE(prev_obs != obs_out, "ocppo_rollout_store_vecnorm: prev_obs must not alias obs_out");
   OCPPO_REQUIRE(reward_out != reward, "ocppo_rollout_store_vecnorm: reward_out must not alias reward");
   const VecNormArgs vn{gamma,     epsilon,    clip_reward,
-                       ret_state, rms_state,  reward_out, net_scale_of(net_flags)};
+                       ret_state, rms_state,  reward_out, net_scale_of(net_flags),
+                       reset_prev};
   clear_stale_error();
   hipStream_t s = as_stream(stream);
 #define OCPPO_SV(F, O)                                                                        \

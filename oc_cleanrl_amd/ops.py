@@ -317,13 +317,23 @@ def categorical_logprob_entropy(logits, actions):
 # ---------------------------------------------------------------------------------------------
 # rollout store / reset (ppo_atari_oc.py:502-503, 512-514), minibatch gather (:566-567)
 # ---------------------------------------------------------------------------------------------
+def _reset_prev(reset_prev, frame, N: int, W: int, D: int, dev):
+    if reset_prev is None:
+        return None
+    if reset_prev.dtype != frame.dtype:
+        raise ValueError(f"reset_prev dtype {reset_prev.dtype} != frame dtype {frame.dtype}")
+    return _check(reset_prev, "reset_prev", None, dev, N * (W - 1) * D)
+
+
 def rollout_store(frame, reward, done, prev_obs, obs_out, net_obs=None, reward_out=None,
-                  done_out=None, scale255: bool = False):
+                  done_out=None, scale255: bool = False, reset_prev=None):
     """obs_out = stack(prev_obs[:, 1:], frame) (reset-filled where done), plus reward/done rows.
 
     frame [N, D] f32|u8; prev_obs/obs_out [N, W, D] f32|bf16|u8; net_obs [N, W, D] f32, or a
     channels_last [N, W, H, X] f32 tensor (written in NHWC order). scale255: net_obs holds
-    value / 255 exactly as the NatureCNN's NormalizeImg computes it on the GPU.
+    value / 255 exactly as the NatureCNN's NormalizeImg computes it on the GPU. reset_prev
+    [N, W-1, D] (frame dtype): the older frames of the env's own reset observation for done rows
+    (None: FrameStack's fill with the newest frame).
     """
     N, D = frame.shape[0], frame[0].numel()
     W = obs_out.shape[1]
@@ -341,12 +351,12 @@ def rollout_store(frame, reward, done, prev_obs, obs_out, net_obs=None, reward_o
          _check(done, "done", f, dev, N), N, W, D, _check(prev_obs, "prev_obs", None, dev),
          _check(obs_out, "obs_out", None, dev), _DTYPE_CODE[obs_out.dtype], net,
          _opt(reward_out, "reward_out", f, dev, N), _opt(done_out, "done_out", f, dev, N),
-         layout | (2 if scale255 else 0))
+         layout | (2 if scale255 else 0), _reset_prev(reset_prev, frame, N, W, D, dev))
 
 
 def rollout_store_vecnorm(frame, reward, done, prev_obs, obs_out, net_obs, done_out, ret_state,
                           rms_state, reward_out, gamma=0.99, epsilon=1e-8, clip_reward=10.0,
-                          scale255: bool = False):
+                          scale255: bool = False, reset_prev=None):
     """rollout_store + vecnorm_reward in one launch (reward_out gets the normalised reward)."""
     N, D = frame.shape[0], frame[0].numel()
     W = obs_out.shape[1]
@@ -365,7 +375,8 @@ def rollout_store_vecnorm(frame, reward, done, prev_obs, obs_out, net_obs, done_
          float(gamma), float(epsilon), float(clip_reward),
          _check(ret_state, "ret_state", torch.float64, dev, N),
          _check(rms_state, "rms_state", torch.float64, dev, 3),
-         _check(reward_out, "reward_out", f, dev, N), layout | (2 if scale255 else 0))
+         _check(reward_out, "reward_out", f, dev, N), layout | (2 if scale255 else 0),
+         _reset_prev(reset_prev, frame, N, W, D, dev))
 
 
 def obs_reset(frame, obs_out, net_obs=None, scale255: bool = False):
@@ -723,6 +734,22 @@ def synth_env_step(seed: int, step_base, step_offset: int, actions, frame_out, r
          _check(reward_out, "reward_out", torch.float32, dev, N),
          _check(done_out, "done_out", torch.float32, dev, N),
          _opt(ep_state, "ep_state", torch.float32, dev, N * 5))
+
+
+def cartpole_step(seed: int, actions, state, counters, obs_out, reward_out=None, done_out=None,
+                  ep_state=None):
+    """One step (actions [N] i64) or, with actions None, a reset of N device CartPole-v1 envs
+    (gymnasium 0.28.1 dynamics, TimeLimit 500, same-step auto-reset): state [N, 4] f64 and
+    counters [N, 2] i64 in/out, obs_out [N, 4] f32, reward_out / done_out [N] f32."""
+    N = obs_out.shape[0]
+    dev = obs_out.device
+    f = torch.float32
+    call("ocppo_cartpole_step", _stream(dev), int(seed) & 0xFFFFFFFFFFFFFFFF,
+         _opt(actions, "actions", torch.int64, dev, N), N,
+         _check(state, "state", torch.float64, dev, 4 * N),
+         _check(counters, "counters", torch.int64, dev, 2 * N),
+         _check(obs_out, "obs_out", f, dev, 4 * N), _opt(reward_out, "reward_out", f, dev, N),
+         _opt(done_out, "done_out", f, dev, N), _opt(ep_state, "ep_state", f, dev, 5 * N))
 
 
 # ---------------------------------------------------------------------------------------------

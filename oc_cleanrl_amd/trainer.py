@@ -35,19 +35,20 @@ import torch.nn as nn
 from . import frames, ops
 from .agents import NormalizeImg, PPObj, make_agent
 from .args import Args
-from .envs import HostVecEnv, SyntheticAtariEnv
+from .envs import HostVecEnv, make_device_env
 
 
-def storage_dtype(args: Args, pixels: bool, host_env: bool = False) -> torch.dtype:
+def storage_dtype(args: Args, pixels: bool, integer_obs: bool = True) -> torch.dtype:
     """Rollout obs dtype. `auto` picks the narrowest EXACT type: u8 for ALE pixels, bf16 for the
     synthetic env's integer object coordinates (|x| <= 256), f32 when detection noise makes them
-    fractional and for host envs, whose feature ranges nothing here pins (OCAtari is
-    un-vendored): pass obs_storage="bf16" for a host env known to emit integers |x| <= 256."""
+    fractional, for CartPole's state and for host envs, whose feature ranges nothing here pins
+    (OCAtari is un-vendored): pass obs_storage="bf16" for a host env known to emit integers
+    |x| <= 256."""
     choice = args.obs_storage
     if choice == "auto":
         if pixels:
             return torch.uint8
-        return torch.bfloat16 if args.noise_std == 0.0 and not host_env else torch.float32
+        return torch.bfloat16 if args.noise_std == 0.0 and integer_obs else torch.float32
     return {"f32": torch.float32, "bf16": torch.bfloat16, "u8": torch.uint8}[choice]
 
 
@@ -161,9 +162,13 @@ class PPOTrainer:
                                   a.buffer_window_size)
             self.env.reset()  # the obs shape comes from the env
         else:
-            self.env = SyntheticAtariEnv(a.env_id, a.obs_mode, self.N, a.num_features, self.seed,
-                                         self.dev, a.buffer_window_size)
+            self.env = make_device_env(a.env_id, a.obs_mode, self.N, a.num_features, self.seed,
+                                       self.dev, a.buffer_window_size)
         self.pixels = self.env.pixels
+        # a host env's reset observations are its own stacks (envs.HostVecEnv): the stored obs no
+        # longer follow the frame-stack fill rule the rollout frame cache and the update's frame
+        # dedup rely on, so both use the plain (every slot encoded) path then
+        self.reset_stacks = self.host_env and self.env.reset_stacks
         self.A = self.env.n_actions
         self.obs_shape = self.env.single_obs_shape
         self.agent = make_agent(a.architecture, self.obs_shape, self.A, self.dev, a.encoder_dims,
@@ -184,7 +189,7 @@ class PPOTrainer:
         self.H = self.agent.actor.in_features if self.fused_head else 0
         # PPObj's encoder sees one frame at a time: the rollout keeps the W frame encodings of
         # every env in a cache and encodes only the newest frame per step
-        self.frame_cache = (a.rollout_frame_cache and self.fused_head and
+        self.frame_cache = (a.rollout_frame_cache and self.fused_head and not self.reset_stacks and
                             isinstance(self.agent, PPObj) and len(a.encoder_dims) > 0)
         # every parameter's grad is written in place by agents._LinearAct (no zero-fill needed)
         # when the agent is a Linear/ReLU stack owned by the fused optimizer
@@ -208,7 +213,8 @@ class PPOTrainer:
         T, N = self.T, self.N
         f32 = torch.float32
         dev = self.dev
-        self.obs_dtype = storage_dtype(a, self.pixels, self.host_env)
+        self.obs_dtype = storage_dtype(a, self.pixels, not self.host_env and
+                                       getattr(self.env, "integer_obs", False))
         self.obs = torch.zeros((T + 1, N) + self.obs_shape, dtype=self.obs_dtype, device=dev)
         self.net_obs = torch.empty((N,) + self.obs_shape, dtype=f32, device=dev,
                                    memory_format=self.net_format).zero_()
@@ -246,6 +252,7 @@ class PPOTrainer:
         # PPObj update with every distinct frame of a minibatch encoded once (frames.py)
         W = self.obs_shape[0]
         self.frame_dedup = (a.update_frame_dedup and isinstance(self.agent, PPObj) and
+                            not self.reset_stacks and
                             not self.pixels and len(self.obs_shape) == 2 and
                             len(a.encoder_dims) > 0 and 1 <= W <= 16)
         self.planner = (frames.FramePlanner(T, N, W, a.local_minibatch_size, a.update_epochs,
@@ -296,7 +303,12 @@ class PPOTrainer:
     # ------------------------------------------------------------------------------------------
     def _reset_env(self):
         frame = self.env.frame if self.host_env else self.env.reset()
-        ops.obs_reset(frame, self.obs[self.T], self.net_obs, scale255=self.prescale)
+        if self.reset_stacks:  # the env's own initial stack (envs.HostVecEnv.reset)
+            ones = torch.ones(self.N, dtype=torch.float32, device=self.dev)
+            ops.rollout_store(frame, ones, ones, self.obs[0], self.obs[self.T], self.net_obs,
+                              scale255=self.prescale, reset_prev=self.env.reset_prev)
+        else:
+            ops.obs_reset(frame, self.obs[self.T], self.net_obs, scale255=self.prescale)
         self.dones[self.T].zero_()
 
     def _policy_hidden(self, t: int):
@@ -337,15 +349,17 @@ class PPOTrainer:
 
     def _store(self, t: int):
         a = self.args
+        rp = self.env.reset_prev if self.reset_stacks else None
         if a.vecnorm_reward:
             self.timer.bracket("rollout_store", lambda: ops.rollout_store_vecnorm(
                 self.env.frame, self.env.reward, self.env.done, self.obs[t], self.obs[t + 1],
                 self.net_obs, self.dones[t + 1], self.ret_state, self.rms_state, self.rewards[t],
-                scale255=self.prescale))
+                scale255=self.prescale, reset_prev=rp))
         else:
             self.timer.bracket("rollout_store", lambda: ops.rollout_store(
                 self.env.frame, self.env.reward, self.env.done, self.obs[t], self.obs[t + 1],
-                self.net_obs, self.rewards[t], self.dones[t + 1], scale255=self.prescale))
+                self.net_obs, self.rewards[t], self.dones[t + 1], scale255=self.prescale,
+                reset_prev=rp))
 
     def _rollout_begin(self):
         T = self.T
@@ -398,6 +412,8 @@ class PPOTrainer:
 
     def _rollout_host(self):
         for k in range(self.T + 1):
+            if k > 0:  # eager, ordered before part k's store of step k-1
+                self.env.upload_resets()
             if self.g_host:
                 self.g_host[k].replay()
             else:

@@ -47,6 +47,9 @@ GAE_LINES = (533, 547)
 UPDATE_LINES = (566, 610)
 DQN_SCRIPT = REF / "cleanrl" / "dqn_atari_oc.py"
 TD_LINES = (378, 382)
+PPO_SCRIPT = REF / "cleanrl" / "ppo.py"
+PPO_AGENT_LINES = (94, 126)   # layer_init + Agent (tanh-MLP actor / critic)
+PPO_UPDATE_LINES = (250, 290)  # minibatch forward, loss, zero_grad, backward, clip, Adam
 
 sys.dont_write_bytecode = True
 sys.path.insert(0, str(REF / "cleanrl"))
@@ -61,6 +64,8 @@ def block(lines, script=SCRIPT):
 GAE_CODE = block(GAE_LINES)
 UPDATE_CODE = block(UPDATE_LINES)
 TD_CODE = block(TD_LINES, DQN_SCRIPT)
+PPO_AGENT_CODE = block(PPO_AGENT_LINES, PPO_SCRIPT)
+PPO_UPDATE_CODE = block(PPO_UPDATE_LINES, PPO_SCRIPT)
 
 
 class Space:
@@ -305,6 +310,53 @@ def gen_update(B=512, M=256, F=6, A=6, seed=21, pixels=False, name="update_2mb")
     np.savez_compressed(OUT / f"{name}.npz", **out)
 
 
+def gen_update_cartpole(B=512, M=128, seed=23, name="update_cartpole"):
+    """Config 1: two minibatch updates of cleanrl/ppo.py's own update block (:250-290, clip 0.2)
+    on its own Agent class (:94-126, exec'd), the whole learner step of ppo.py on CartPole-shaped
+    observations."""
+    from torch.distributions.categorical import Categorical
+
+    ns_agent = dict(torch=torch, nn=nn, np=np, Categorical=Categorical)
+    exec(PPO_AGENT_CODE, ns_agent)
+    envs = types.SimpleNamespace(single_observation_space=Space(shape=(4,)),
+                                 single_action_space=Space(shape=(), n=2))
+    torch.manual_seed(seed)
+    rng = np.random.default_rng(seed)
+    agent = ns_agent["Agent"](envs)
+    b_obs = torch.from_numpy((rng.uniform(-1, 1, (B, 4)) * [2.0, 1.5, 0.2, 1.5]).astype(np.float32))
+    with torch.no_grad():
+        b_actions, lp, _, val = agent.get_action_and_value(b_obs)
+        val = val.view(-1)
+    b_logprobs = lp + torch.from_numpy((rng.standard_normal(B) * 0.1).astype(np.float32))
+    b_values = val + torch.from_numpy((rng.standard_normal(B) * 0.3).astype(np.float32))
+    b_returns = val + torch.from_numpy((rng.standard_normal(B) * 2.0).astype(np.float32))
+    b_advantages = torch.from_numpy((rng.standard_normal(B) * 1.5).astype(np.float32))
+    perm = rng.permutation(B)
+    args = types.SimpleNamespace(clip_coef=0.2, norm_adv=True, clip_vloss=True, ent_coef=0.01,
+                                 vf_coef=0.5, max_grad_norm=0.5)
+    optimizer = optim.Adam(agent.parameters(), lr=2.5e-4, eps=1e-5)
+    sds = [{k: v.detach().clone().numpy() for k, v in agent.state_dict().items()}]
+    stats = []
+    for start in (0, M):
+        ns = dict(torch=torch, nn=nn, np=np, agent=agent, args=args, optimizer=optimizer,
+                  b_obs=b_obs, b_actions=b_actions.float(), b_logprobs=b_logprobs,
+                  b_advantages=b_advantages, b_returns=b_returns, b_values=b_values,
+                  mb_inds=perm[start:start + M], clipfracs=[])
+        exec(PPO_UPDATE_CODE, ns)
+        stats.append([ns["loss"].item(), ns["pg_loss"].item(), ns["v_loss"].item(),
+                      ns["entropy_loss"].item(), ns["old_approx_kl"].item(),
+                      ns["approx_kl"].item(), ns["clipfracs"][-1]])
+        sds.append({k: v.detach().clone().numpy() for k, v in agent.state_dict().items()})
+    out = dict(b_obs=b_obs.numpy(), b_actions=b_actions.numpy().astype(np.int64),
+               b_logprobs=b_logprobs.numpy(), b_values=b_values.numpy(),
+               b_returns=b_returns.numpy(), b_advantages=b_advantages.numpy(),
+               perm=perm.astype(np.int64), M=M, stats=np.array(stats, np.float32))
+    for i, sd in enumerate(sds):
+        for k, v in sd.items():
+            out[f"sd{i}::{k}"] = v
+    np.savez_compressed(OUT / f"{name}.npz", **out)
+
+
 def main():
     torch.set_num_threads(8)
     gen_gae(16, 8, "synthetic", 1)
@@ -326,6 +378,7 @@ def main():
     gen_ppobj_small()
     gen_update()
     gen_update(B=32, M=16, A=4, seed=22, pixels=True, name="update_2mb_cnn")
+    gen_update_cartpole()
     gen_init("ppobj_f12_a6", lambda e: PPObj(e, "cpu", (256, 512, 1024, 512), (512,)), (4, 12), 6,
              1, 160.0)
     gen_init("ppodefault_a4", lambda e: PPODefault(e, "cpu"), (4, 84, 84), 4, 1, 255.0)

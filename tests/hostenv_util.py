@@ -12,6 +12,8 @@ import torch
 
 
 class DeviceEnvAsHost:
+    frame_stack_fill_rule = True  # reset stacks are W copies of the first frame (FrameStack)
+
     def __init__(self, env_id, obs_mode, num_envs, num_features, seed, device, window=4):
         from oc_cleanrl_amd.envs import SyntheticAtariEnv
 
@@ -49,6 +51,8 @@ class NumpyObjVecEnv:
     """N object-vector envs on the host: F = 12 integer coordinates per frame, ±1 rewards with
     p = 0.005 each, episode ends with p = 1/3500, FrameStack(W)."""
 
+    frame_stack_fill_rule = True
+
     def __init__(self, num_envs, num_features=12, window=4, seed=0):
         self.N, self.F, self.W = num_envs, num_features, window
         self.rng = np.random.default_rng(seed)
@@ -71,3 +75,50 @@ class NumpyObjVecEnv:
         self.stack[:, -1] = f
         self.stack[d] = f[d][:, None]
         return self.stack.copy(), r, d, np.zeros_like(d), {}
+
+
+class AtariLikeVecEnv:
+    """SB3-VecEnv-shaped stand-in for the reference's wrapper chain (ppo_atari_oc.py:278-282):
+    RecordEpisodeStatistics -> NoopResetEnv -> EpisodicLifeEnv -> FireResetEnv over a FrameStack.
+    A done is a life loss (p_life; the stack is NOT reset and the game goes on) or a game over
+    (p_game; the auto-reset stack holds W distinct frames, as the no-op / FIRE steps after reset
+    leave it). info["episode"] = {"r", "l"} of the whole game is reported on game over only.
+    Every returned stack is recorded in `history` (index 0 = the reset obs)."""
+
+    def __init__(self, num_envs, num_features=12, window=4, seed=0, p_life=0.03, p_game=0.02):
+        self.N, self.F, self.W = num_envs, num_features, window
+        self.rng = np.random.default_rng(seed)
+        self.p_life, self.p_game = p_life, p_game
+        self.stack = np.zeros((num_envs, window, num_features), np.float32)
+        self.game_ret = np.zeros(num_envs)
+        self.game_len = np.zeros(num_envs, np.int64)
+        self.history = []
+        self.games = []  # (return, length) of every finished game
+
+    def _frames(self, *lead):
+        return self.rng.integers(0, 210, lead + (self.F,)).astype(np.float32)
+
+    def reset(self):
+        self.stack[:] = self._frames(self.N, self.W)
+        self.history = [self.stack.copy()]
+        return self.stack.copy()
+
+    def step(self, actions):
+        assert len(actions) == self.N
+        r = self.rng.choice([-1.0, 0.0, 0.0, 0.0, 1.0], self.N)
+        u = self.rng.random(self.N)
+        life = u < self.p_life
+        game = (u >= self.p_life) & (u < self.p_life + self.p_game)
+        self.stack[:, :-1] = self.stack[:, 1:]
+        self.stack[:, -1] = self._frames(self.N)
+        self.game_ret += r
+        self.game_len += 1
+        infos = [{} for _ in range(self.N)]
+        for n in np.flatnonzero(game):
+            infos[n]["episode"] = {"r": float(self.game_ret[n]), "l": int(self.game_len[n])}
+            self.games.append((float(self.game_ret[n]), int(self.game_len[n])))
+            self.game_ret[n] = 0.0
+            self.game_len[n] = 0
+            self.stack[n] = self._frames(self.W)  # auto-reset: distinct no-op frames
+        self.history.append(self.stack.copy())
+        return self.stack.copy(), r, life | game, infos

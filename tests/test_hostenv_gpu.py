@@ -3,6 +3,7 @@ cleanrl/ppo_atari_oc.py:506-514): fed with the device synthetic env seen through
 vector API (tests/hostenv_util.DeviceEnvAsHost), the learner must produce exactly what the
 device-env learner produces -- same obs / rewards / dones / actions / advantages bit for bit and
 the same weights -- so the staging (actions D2H, newest frame + reward + done H2D) is exact."""
+import numpy as np
 import pytest
 import torch
 
@@ -62,3 +63,37 @@ def test_numpy_host_env_trains(dev):
     # the newest frame of every stored obs slot is an integer coordinate frame from the host
     last = tr.obs[:, :, -1].float()
     assert torch.equal(last, last.floor()) and float(last.max()) < 210
+
+
+@pytest.mark.parametrize("graphs", [True, False])
+def test_host_env_reset_stacks_and_episode_infos(dev, graphs):
+    """A host env whose reset stacks are NOT the FrameStack fill (no-op steps after reset,
+    life-loss dones without a stack reset): every stored obs slot is exactly the stack the env
+    returned, and the episodic scalars are whole games from info["episode"] (:516-529), not
+    per-life sums."""
+    from oc_cleanrl_amd.trainer import PPOTrainer
+    from tests.hostenv_util import AtariLikeVecEnv
+
+    a = _args(cuda_graphs=graphs, num_envs=16, num_steps=16)
+    env = AtariLikeVecEnv(a.local_num_envs, a.num_features, seed=5)
+    tr = PPOTrainer(a, dev, envs=env)
+    assert tr.reset_stacks and not tr.frame_cache and not tr.frame_dedup
+    assert tr.obs.dtype == torch.float32  # host envs: f32 storage by default
+    T = a.num_steps
+    games_seen = 0
+    for it in range(3):
+        m = tr.train_iteration()
+        torch.cuda.synchronize()
+        got = tr.obs.cpu().numpy()
+        for t in range(T + 1):
+            exp = env.history[it * T + t]
+            assert np.array_equal(got[t], exp), (it, t)
+        new = env.games[games_seen:]
+        games_seen = len(env.games)
+        if new:
+            assert m["charts/Episodic_Original_Reward"] == pytest.approx(
+                sum(g[0] for g in new) / len(new))
+            assert m["charts/Episodic_Length"] == pytest.approx(sum(g[1] for g in new) / len(new))
+        else:
+            assert "charts/Episodic_Original_Reward" not in m
+    assert games_seen > 0

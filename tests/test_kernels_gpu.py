@@ -295,6 +295,51 @@ def test_rollout_store_bitwise(ops, dev, obs_dt, pixel, N, D):
     assert torch.equal(dout.cpu(), torch.from_numpy(done))
 
 
+@pytest.mark.parametrize("layout", ["plain", "cl", "vecnorm"])
+@pytest.mark.parametrize("pixel,N,W,D", [(False, 64, 4, 12), (False, 9, 3, 6), (True, 8, 4, 7056),
+                                         (True, 5, 3, 36)])
+def test_rollout_store_reset_stack_bitwise(ops, dev, layout, pixel, N, W, D):
+    """Done rows take the env's own reset observation (reset_prev ++ frame) instead of the
+    FrameStack fill -- a host env whose reset stack holds distinct frames (NoopReset/FireReset
+    steps, EpisodicLifeEnv's life-loss dones, ppo_atari_oc.py:278-282)."""
+    rng = np.random.default_rng(N * D + W)
+    hi = 256 if pixel else 210
+    npdt = np.uint8 if pixel else np.float32
+    prev = rng.integers(0, hi, (N, W, D)).astype(np.float32)
+    frame = rng.integers(0, hi, (N, D)).astype(npdt)
+    rp = rng.integers(0, hi, (N, W - 1, D)).astype(npdt)
+    done = (rng.random(N) < 0.4).astype(np.float32)
+    done[0] = 1.0
+    reward = rng.standard_normal(N).astype(np.float32)
+    dt = torch.uint8 if pixel else torch.bfloat16
+    prev_t = T(prev, dev).to(dt)
+    out = torch.empty_like(prev_t)
+    exp = O.rollout_store(frame.astype(np.float32), done, prev, "u8" if pixel else "bf16",
+                          reset_prev=rp)
+    args = (T(frame, dev), T(reward, dev), T(done, dev), prev_t, out)
+    if layout == "cl":
+        if not pixel:
+            pytest.skip("channels-last network input is a pixel-stack layout")
+        side = int(round(D ** 0.5))
+        net = torch.empty((N, W, side, side), device=dev, memory_format=torch.channels_last)
+        ops.rollout_store(*args, net, reset_prev=T(rp, dev))
+        got_net = net.contiguous().cpu().numpy().reshape(N, W, D)
+    elif layout == "vecnorm":
+        net = torch.empty(N, W, D, device=dev)
+        ret = torch.zeros(N, dtype=torch.float64, device=dev)
+        rms = torch.tensor([0.0, 1.0, 1e-4], dtype=torch.float64, device=dev)
+        rout = torch.empty(N, device=dev)
+        ops.rollout_store_vecnorm(*args, net, torch.empty(N, device=dev), ret, rms, rout,
+                                  reset_prev=T(rp, dev))
+        got_net = net.cpu().numpy()
+    else:
+        net = torch.empty(N, W, D, device=dev)
+        ops.rollout_store(*args, net, reset_prev=T(rp, dev))
+        got_net = net.cpu().numpy()
+    assert np.array_equal(out.float().cpu().numpy(), exp)
+    assert np.array_equal(got_net, exp)
+
+
 def test_bf16_conversion_rounds_to_nearest_even(ops, dev):
     x = torch.tensor([[1.0 + 2 ** -8, 1.0 + 3 * 2 ** -8, 300.5, -0.0]], device=dev)
     prev = torch.zeros(1, 1, 4, dtype=torch.bfloat16, device=dev)

@@ -165,3 +165,62 @@ def test_oracle_update_step_matches_reference_update_block():
                 off += p.numel()
         for k, ref in sd(i + 1).items():
             np.testing.assert_allclose(ag.state_dict()[k].numpy(), ref.numpy(), rtol=0, atol=2e-7)
+
+
+def test_cartpole_update_golden_on_cpu():
+    """Config 1 learner step on the host: agents.CartPoleAgent (cleanrl/ppo.py:100-126 layout,
+    state-dict keys), the oracle's loss gradient (clip 0.2) fed to autograd, torch clip + Adam
+    -- the parameters ppo.py's own update block (:250-290) produced (update_cartpole.npz)."""
+    import torch
+
+    from oc_cleanrl_amd.agents import make_agent
+
+    z = golden("update_cartpole.npz")
+    ag = make_agent("CARTPOLE_MLP", (4,), 2)
+    sd = lambda i: {k.split("::", 1)[1]: torch.from_numpy(z[k]) for k in z  # noqa: E731
+                    if k.startswith(f"sd{i}::")}
+    ag.load_state_dict(sd(0))
+    opt = torch.optim.Adam(ag.parameters(), lr=2.5e-4, eps=1e-5)
+    M = int(z["M"])
+    for i, start in enumerate((0, M)):
+        idx = z["perm"][start:start + M]
+        logits, value = ag.logits_and_value(torch.from_numpy(z["b_obs"][idx]))
+        st, dl, dv = O.ppo_loss_fwd_bwd(
+            logits.detach().numpy(), value.detach().numpy().reshape(-1), z["b_actions"],
+            z["b_logprobs"], z["b_advantages"], z["b_returns"], z["b_values"], idx,
+            clip_coef=0.2, ent_coef=0.01, vf_coef=0.5)
+        np.testing.assert_allclose(st[:7], z["stats"][i], rtol=2e-6, atol=1e-8)
+        opt.zero_grad()
+        torch.autograd.backward([logits, value], [torch.from_numpy(dl),
+                                                  torch.from_numpy(dv).view(-1, 1)])
+        torch.nn.utils.clip_grad_norm_(ag.parameters(), 0.5)
+        opt.step()
+        for k, ref in sd(i + 1).items():
+            torch.testing.assert_close(ag.state_dict()[k], ref, rtol=0, atol=0.01 * 2.5e-4)
+
+
+def test_cartpole_oracle_dynamics_invariants():
+    """The CartPole restatement (gymnasium 0.28.1 cartpole.py): constants, reset range, one
+    hand-checked Euler step, termination and the 500-step TimeLimit with auto-reset."""
+    import math
+
+    env = O.CartPoleOracle(3, seed=11)
+    o = env.reset()
+    assert o.shape == (3, 4) and np.all(np.abs(o) < 0.05)
+    env.state[0] = [0.0, 0.0, 0.0, 0.0]
+    o, r, d = env.step([1, 0, 1])
+    # push right from rest: xacc = force/total_mass - ... with theta = 0: temp = 10/1.1,
+    # thetaacc = -temp / (0.5 * (4/3 - 0.1/1.1)); x_dot' = tau * xacc, theta_dot' = tau*thetaacc
+    temp = 10.0 / 1.1
+    thetaacc = (0.0 - 1.0 * temp) / (0.5 * (4.0 / 3.0 - 0.1 * 1.0 / 1.1))
+    xacc = temp - 0.05 * thetaacc * 1.0 / 1.1
+    assert env.state[0] == [0.0, 0.02 * xacc, 0.0, 0.02 * thetaacc]
+    assert r.tolist() == [1.0] * 3 and d.tolist() == [0.0] * 3
+    env.state[1] = [2.45, 0.0, 0.0, 0.0]  # beyond x_threshold after the step -> terminated
+    _, _, d = env.step([1, 1, 1])
+    assert d[1] == 1 and env.elapsed[1] == 0 and abs(env.state[1][0]) < 0.05
+    assert env.theta_threshold_radians == 12 * 2 * math.pi / 360
+    env.elapsed[2] = 499
+    env.state[2] = [0.0, 0.0, 0.0, 0.0]
+    _, _, d = env.step([0, 0, 1])
+    assert d[2] == 1  # TimeLimit(500) truncation
