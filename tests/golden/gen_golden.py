@@ -50,6 +50,8 @@ TD_LINES = (378, 382)
 PPO_SCRIPT = REF / "cleanrl" / "ppo.py"
 PPO_AGENT_LINES = (94, 126)   # layer_init + Agent (tanh-MLP actor / critic)
 PPO_UPDATE_LINES = (250, 290)  # minibatch forward, loss, zero_grad, backward, clip, Adam
+BUFFERS = REF / "cleanrl_utils" / "buffers.py"
+REPLAY_METHOD_LINES = (379, 431)  # ReplayBuffer.add / sample / _get_samples (SB3 restatement)
 
 sys.dont_write_bytecode = True
 sys.path.insert(0, str(REF / "cleanrl"))
@@ -357,6 +359,84 @@ def gen_update_cartpole(B=512, M=128, seed=23, name="update_cartpole"):
     np.savez_compressed(OUT / f"{name}.npz", **out)
 
 
+def gen_replay(size=7, obs_shape=(4, 5), adds=10, seed=31, name="replay_sb3"):
+    """SB3 ReplayBuffer(optimize_memory_usage=True) as the reference holds it
+    (cleanrl_utils/buffers.py:379-431: add, sample, _get_samples), exec'd as the body of a class
+    over a stub base that provides the state __init__ would build (:337-363; the module itself
+    imports gym / SB3, absent here). Records the buffer after every add (wrap-around included),
+    _get_samples for every slot, and the index support of sample() at a not-full and a full
+    state (sample's own np.random.randint law, :412-415)."""
+    import collections
+    from typing import Optional
+
+    lines = BUFFERS.read_text().splitlines()[REPLAY_METHOD_LINES[0] - 1:REPLAY_METHOD_LINES[1]]
+    src = "class RB(Base):\n" + "\n".join(lines)
+
+    class Base:
+        def __init__(self, buffer_size, obs_shape, n_envs=1):
+            self.buffer_size, self.n_envs, self.pos, self.full = buffer_size, n_envs, 0, False
+            self.optimize_memory_usage = True
+            self.observations = np.zeros((buffer_size, n_envs) + obs_shape, np.uint8)
+            self.next_observations = None
+            self.actions = np.zeros((buffer_size, n_envs, 1), np.int64)
+            self.rewards = np.zeros((buffer_size, n_envs), np.float32)
+            self.dones = np.zeros((buffer_size, n_envs), np.float32)
+
+        @staticmethod
+        def _normalize_obs(obs, env=None):
+            return obs
+
+        @staticmethod
+        def _normalize_reward(reward, env=None):
+            return reward
+
+        def to_torch(self, array, copy=True):
+            return np.array(array)
+
+    Samples = collections.namedtuple("ReplayBufferSamples", "observations actions "
+                                     "next_observations dones rewards")
+    ns = dict(np=np, Optional=Optional, VecNormalize=object, ReplayBufferSamples=Samples,
+              Base=Base)
+    exec(compile(src, f"{BUFFERS}:{REPLAY_METHOD_LINES[0]}-{REPLAY_METHOD_LINES[1]}", "exec"), ns)
+    rb = ns["RB"](size, obs_shape)
+    rng = np.random.default_rng(seed)
+    out = {"size": size}
+    ins = {k: [] for k in ("obs", "next_obs", "action", "reward", "done")}
+    snaps = {k: [] for k in ("pos", "full", "observations", "actions", "rewards", "dones")}
+    support = {}
+    for t in range(adds):
+        o = rng.integers(0, 256, (1,) + obs_shape).astype(np.uint8)
+        no = rng.integers(0, 256, (1,) + obs_shape).astype(np.uint8)
+        a = rng.integers(0, 6, (1, 1))
+        r = rng.standard_normal(1).astype(np.float32)
+        d = (rng.random(1) < 0.3).astype(np.float32)
+        rb.add(o, no, a, r, d)
+        for k, v in zip(ins, (o, no, a, r, d)):
+            ins[k].append(v)
+        snaps["pos"].append(rb.pos)
+        snaps["full"].append(rb.full)
+        for k in ("observations", "actions", "rewards", "dones"):
+            snaps[k].append(getattr(rb, k).copy())
+        if t in (2, adds - 1):  # not full (pos = 3), full (pos = adds - size)
+            get = rb._get_samples
+            rb._get_samples = lambda inds, env=None: inds  # sample() returns its batch_inds
+            np.random.seed(seed + t)
+            inds = rb.sample(20000)
+            del rb._get_samples
+            assert get is not None
+            support[t] = np.unique(inds)
+    every = rb._get_samples(np.arange(size))
+    for k, v in ins.items():
+        out[f"in_{k}"] = np.stack(v)
+    for k, v in snaps.items():
+        out[f"after_{k}"] = np.array(v)
+    for k in Samples._fields:
+        out[f"get_{k}"] = getattr(every, k)
+    for t, v in support.items():
+        out[f"support_{t}"] = v
+    np.savez_compressed(OUT / f"{name}.npz", **out)
+
+
 def main():
     torch.set_num_threads(8)
     gen_gae(16, 8, "synthetic", 1)
@@ -379,6 +459,7 @@ def main():
     gen_update()
     gen_update(B=32, M=16, A=4, seed=22, pixels=True, name="update_2mb_cnn")
     gen_update_cartpole()
+    gen_replay()
     gen_init("ppobj_f12_a6", lambda e: PPObj(e, "cpu", (256, 512, 1024, 512), (512,)), (4, 12), 6,
              1, 160.0)
     gen_init("ppodefault_a4", lambda e: PPODefault(e, "cpu"), (4, 84, 84), 4, 1, 255.0)

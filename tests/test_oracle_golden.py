@@ -224,3 +224,14 @@ def test_cartpole_oracle_dynamics_invariants():
     env.state[2] = [0.0, 0.0, 0.0, 0.0]
     _, _, d = env.step([0, 0, 1])
     assert d[2] == 1  # TimeLimit(500) truncation
+
+
+def test_replay_sample_law_matches_reference_support():
+    """The oracle's SB3 sample support ([0, pos) / every slot but pos once full) equals what the
+    reference's own sample() (cleanrl_utils/buffers.py:412-415, exec'd) drew in 20000 tries."""
+    z = golden("replay_sb3.npz")
+    size = int(z["size"])
+    for k in (k for k in z if k.startswith("support_")):
+        t = int(k.split("_")[1])
+        pos, full = int(z["after_pos"][t]), bool(z["after_full"][t])
+        assert O.replay_sample_law(pos, full, size, 0) == set(z[k].tolist()), k
