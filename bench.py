@@ -116,6 +116,8 @@ def main():
     ap.add_argument("--envs-per-gpu", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-iterations", type=int, default=3)
+    ap.add_argument("--no-cpu-blocks", action="store_true",
+                    help="skip the per-block CPU timings (GAE, minibatch update, config-3 estimate)")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--no-scaled", action="store_true", help="skip roofline_scaled")
@@ -238,16 +240,21 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not opt.no_cpu_baseline and opt.config == 2:
-        from oracle.cpu_learner import time_cpu_baseline  # CPU baseline leg (oracle port)
+        # CPU baseline leg (the oracle's port of the reference loop), on every host core this
+        # process may use (its CPU affinity capped by the cgroup quota)
+        from oracle.cpu_learner import host_info, time_cpu_baseline, time_cpu_blocks, usable_threads
 
-        threads = min(16, os.cpu_count() or 1)
+        threads = usable_threads()
         r = time_cpu_baseline(iterations=opt.cpu_iterations, threads=threads, num_envs=128,
                               num_steps=128)
         cpu = {"value": round(r["sps"], 1), "unit": "env steps/s", "cores": threads,
                "kind": "port",
                "updates_per_sec": round(r["updates_per_sec"], 3),
                "sample": f"{opt.cpu_iterations} PPO iterations of config 2 (128 envs x 128 steps, "
-                         f"16 minibatch updates of 4096) on CPU torch, {r['seconds']:.1f} s"}
+                         f"16 minibatch updates of 4096) on CPU torch, {r['seconds']:.1f} s",
+               "host": host_info()}
+        if not opt.no_cpu_blocks:
+            cpu["blocks"] = time_cpu_blocks(threads)
 
     if rank == 0:
         sps = env_steps / dt

@@ -55,26 +55,89 @@ class CpuPPObj(nn.Module):
         return action, probs.log_prob(action), probs.entropy(), self.critic(h)
 
 
+class CpuNatureCNN(nn.Module):
+    """PPODefault (cleanrl/architectures/ppo.py:15-57): x/255, 3 convs, Linear(3136, 512)."""
+
+    def __init__(self, n_actions, window=4):
+        super().__init__()
+        self.network = nn.Sequential(
+            _init(nn.Conv2d(window, 32, 8, stride=4)), nn.ReLU(),
+            _init(nn.Conv2d(32, 64, 4, stride=2)), nn.ReLU(),
+            _init(nn.Conv2d(64, 64, 3, stride=1)), nn.ReLU(), nn.Flatten(),
+            _init(nn.Linear(64 * 7 * 7, 512)), nn.ReLU())
+        self.actor = _init(nn.Linear(512, n_actions), 0.01)
+        self.critic = _init(nn.Linear(512, 1), 1)
+
+    def get_value(self, x):
+        return self.critic(self.network(x / 255.0))
+
+    def get_action_and_value(self, x, action=None):
+        h = self.network(x / 255.0)
+        probs = Categorical(logits=self.actor(h))
+        if action is None:
+            action = probs.sample()
+        return action, probs.log_prob(action), probs.entropy(), self.critic(h)
+
+
 class CpuLearner:
-    """One process, `num_envs` synthetic Pong-obj envs, reference hyper-parameters."""
+    """One process, `num_envs` synthetic envs (Pong obj vectors, or 84x84 pixel stacks with the
+    NatureCNN when pixels=True), reference hyper-parameters."""
 
     def __init__(self, num_envs=128, num_steps=128, num_features=12, n_actions=6, seed=42,
-                 num_minibatches=4, update_epochs=4, window=4):
+                 num_minibatches=4, update_epochs=4, window=4, pixels=False):
         torch.manual_seed(seed)
         np.random.seed(seed)
+        self.pixels = pixels
+        if pixels:
+            num_features = 84 * 84
         self.N, self.T, self.F, self.A, self.W = num_envs, num_steps, num_features, n_actions, window
-        self.obs_shape = (window, num_features)
-        self.agent = CpuPPObj(self.obs_shape, n_actions)
+        self.obs_shape = (window, 84, 84) if pixels else (window, num_features)
+        self.agent = CpuNatureCNN(n_actions, window) if pixels else \
+            CpuPPObj(self.obs_shape, n_actions)
         self.opt = torch.optim.Adam(self.agent.parameters(), lr=2.5e-4, eps=1e-5)
         self.nmb, self.E = num_minibatches, update_epochs
         self.seed = seed
         self.step_id = 0
-        f, _, _ = O.synth_env_step(seed, self.step_id, None, self.N, self.F, False)
+        f, _, _ = O.synth_env_step(seed, self.step_id, None, self.N, self.F, pixels)
         self.step_id += 1
         self.stack = np.repeat(f[:, None, :], window, 1)
         self.ret, self.rms = np.zeros(self.N), (0.0, 1.0, 1e-4)
-        self.next_obs = torch.tensor(self.stack, dtype=torch.float32)
+        self.next_obs = self._obs_tensor()
         self.next_done = torch.zeros(self.N)
+
+    def _obs_tensor(self):
+        return torch.tensor(self.stack, dtype=torch.float32).view((self.N,) + self.obs_shape)
+
+    def rollout_step(self, next_obs):
+        """Act + env step + VecNormalize + frame stack of one rollout step (:502-514)."""
+        with torch.no_grad():
+            action, logprob, _, value = self.agent.get_action_and_value(next_obs)
+        a = action.cpu().numpy()
+        frame, r, d = O.synth_env_step(self.seed, self.step_id, a, self.N, self.F, self.pixels)
+        self.step_id += 1
+        r, self.ret, self.rms = O.vecnorm_reward(r, d, self.ret, self.rms)
+        self.stack = np.concatenate([self.stack[:, 1:], frame[:, None]], 1)
+        self.stack[d != 0] = frame[d != 0][:, None]
+        return action, logprob, value, r, d
+
+    def minibatch_update(self, b_obs, b_actions, b_logprobs, b_adv, b_ret, b_val, mb):
+        """One minibatch of :566-610 (forward, loss, backward, clip_grad_norm_, Adam)."""
+        _, newlp, ent, newv = self.agent.get_action_and_value(b_obs[mb], b_actions[mb])
+        logratio = newlp - b_logprobs[mb]
+        ratio = logratio.exp()
+        mba = b_adv[mb]
+        mba = (mba - mba.mean()) / (mba.std() + 1e-8)
+        pg = torch.max(-mba * ratio, -mba * torch.clamp(ratio, 0.9, 1.1)).mean()
+        newv = newv.view(-1)
+        vu = (newv - b_ret[mb]) ** 2
+        vc = (b_val[mb] + torch.clamp(newv - b_val[mb], -0.1, 0.1) - b_ret[mb]) ** 2
+        v_loss = 0.5 * torch.max(vu, vc).mean()
+        loss = pg - 0.01 * ent.mean() + v_loss * 0.5
+        for p in self.agent.parameters():
+            p.grad = None
+        loss.backward()
+        nn.utils.clip_grad_norm_(self.agent.parameters(), 0.5)
+        self.opt.step()
 
     def iteration(self):
         T, N = self.T, self.N
@@ -86,33 +149,16 @@ class CpuLearner:
         for step in range(T):
             obs[step] = next_obs
             dones[step] = next_done
-            with torch.no_grad():
-                action, logprob, _, value = self.agent.get_action_and_value(next_obs)
-                values[step] = value.flatten()
+            action, logprob, value, r, d = self.rollout_step(next_obs)
+            values[step] = value.flatten()
             actions[step] = action
             logprobs[step] = logprob
-            a = action.cpu().numpy()
-            frame, r, d = O.synth_env_step(self.seed, self.step_id, a, N, self.F, False)
-            self.step_id += 1
-            r, self.ret, self.rms = O.vecnorm_reward(r, d, self.ret, self.rms)
-            self.stack = np.concatenate([self.stack[:, 1:], frame[:, None]], 1)
-            self.stack[d != 0] = frame[d != 0][:, None]
             rewards[step] = torch.tensor(r, dtype=torch.float32).view(-1)
-            next_obs = torch.tensor(self.stack, dtype=torch.float32)
+            next_obs = self._obs_tensor()
             next_done = torch.tensor(d, dtype=torch.float32)
         with torch.no_grad():  # GAE, ppo_atari_oc.py:533-547
             next_value = self.agent.get_value(next_obs).reshape(1, -1)
-            advantages = torch.zeros_like(rewards)
-            lastgaelam = 0.0
-            for t in reversed(range(T)):
-                if t == T - 1:
-                    nnt, nv = 1.0 - next_done, next_value
-                else:
-                    nnt, nv = 1.0 - dones[t + 1], values[t + 1]
-                delta = rewards[t] + 0.99 * nv * nnt - values[t]
-                lastgaelam = delta + 0.99 * 0.95 * nnt * lastgaelam
-                advantages[t] = lastgaelam
-            returns = advantages + values
+            advantages, returns = gae_torch(rewards, values, dones, next_value, next_done)
         self.next_obs, self.next_done = next_obs, next_done
         B = T * N
         M = B // self.nmb
@@ -123,24 +169,106 @@ class CpuLearner:
         for _ in range(self.E):  # ppo_atari_oc.py:559-610
             np.random.shuffle(b_inds)
             for start in range(0, B, M):
-                mb = b_inds[start:start + M]
-                _, newlp, ent, newv = self.agent.get_action_and_value(b_obs[mb], b_actions[mb])
-                logratio = newlp - b_logprobs[mb]
-                ratio = logratio.exp()
-                mba = b_adv[mb]
-                mba = (mba - mba.mean()) / (mba.std() + 1e-8)
-                pg = torch.max(-mba * ratio, -mba * torch.clamp(ratio, 0.9, 1.1)).mean()
-                newv = newv.view(-1)
-                vu = (newv - b_ret[mb]) ** 2
-                vc = (b_val[mb] + torch.clamp(newv - b_val[mb], -0.1, 0.1) - b_ret[mb]) ** 2
-                v_loss = 0.5 * torch.max(vu, vc).mean()
-                loss = pg - 0.01 * ent.mean() + v_loss * 0.5
-                for p in self.agent.parameters():
-                    p.grad = None
-                loss.backward()
-                nn.utils.clip_grad_norm_(self.agent.parameters(), 0.5)
-                self.opt.step()
+                self.minibatch_update(b_obs, b_actions, b_logprobs, b_adv, b_ret, b_val,
+                                      b_inds[start:start + M])
         return T * N
+
+
+def gae_torch(rewards, values, dones, next_value, next_done, gamma=0.99, gae_lambda=0.95):
+    """The reference's reverse GAE loop (ppo_atari_oc.py:533-547) on CPU torch tensors."""
+    T = rewards.shape[0]
+    advantages = torch.zeros_like(rewards)
+    lastgaelam = 0.0
+    for t in reversed(range(T)):
+        if t == T - 1:
+            nnt, nv = 1.0 - next_done, next_value
+        else:
+            nnt, nv = 1.0 - dones[t + 1], values[t + 1]
+        delta = rewards[t] + gamma * nv * nnt - values[t]
+        lastgaelam = delta + gamma * gae_lambda * nnt * lastgaelam
+        advantages[t] = lastgaelam
+    return advantages, advantages + values
+
+
+def host_info() -> dict:
+    """CPU model, logical CPUs, the CPUs this process may run on and the cgroup CPU quota."""
+    import os
+
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = float(q) / float(period)
+    except (OSError, ValueError):
+        pass
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    return {"cpu_model": model, "cpu_count": os.cpu_count(), "affinity_cpus": aff,
+            "cgroup_cpu_quota": quota, "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+
+
+def usable_threads() -> int:
+    """All host cores this process may use: its CPU affinity, capped by the cgroup quota."""
+    h = host_info()
+    n = h["affinity_cpus"] or 1
+    if h["cgroup_cpu_quota"]:
+        n = min(n, max(1, int(h["cgroup_cpu_quota"])))
+    return n
+
+
+def _best(fn, reps):
+    best = float("inf")
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        best = min(best, time.perf_counter() - t0)
+    return best
+
+
+def time_cpu_blocks(threads: int, c3: bool = True) -> dict:
+    """Per-block CPU timings of the reference's own op sequences: GAE at T=128 for
+    N in {128, 1024}; one PPObj minibatch forward + loss + backward + clip + Adam at M=4096;
+    and a config-3 (NatureCNN, 256 pixel envs, minibatch 8192) iteration extrapolated from timed
+    rollout steps and minibatch updates (128 x step + 16 x update)."""
+    torch.set_num_threads(threads)
+    g = torch.Generator().manual_seed(0)
+    out = {}
+    for N in (128, 1024):
+        r = torch.randn(128, N, generator=g)
+        v = torch.randn(128, N, generator=g)
+        d = (torch.rand(128, N, generator=g) < 0.01).float()
+        nv, nd = torch.randn(1, N, generator=g), torch.zeros(N)
+        out[f"gae_T128_N{N}_ms"] = round(1e3 * _best(lambda: gae_torch(r, v, d, nv, nd), 5), 3)
+    lr = CpuLearner(num_envs=32, num_steps=128)
+    B, M = 4096 * 4, 4096
+    b_obs = torch.randint(0, 160, (B,) + lr.obs_shape, generator=g).float()
+    b_act = torch.randint(0, 6, (B,), generator=g)
+    b_lp, b_adv, b_ret, b_val = (torch.randn(B, generator=g) for _ in range(4))
+    mb = np.random.RandomState(0).permutation(B)[:M]
+    out["ppobj_minibatch_update_M4096_ms"] = round(1e3 * _best(
+        lambda: lr.minibatch_update(b_obs, b_act, b_lp, b_adv, b_ret, b_val, mb), 3), 1)
+    if c3:
+        cl = CpuLearner(num_envs=256, num_steps=128, n_actions=4, pixels=True)
+        x = cl._obs_tensor()
+        step_s = _best(lambda: cl.rollout_step(x), 3)
+        Bc, Mc = 256 * 128, 8192
+        bo = torch.randint(0, 256, (Mc,) + cl.obs_shape, generator=g).float()
+        ba = torch.randint(0, 4, (Mc,), generator=g)
+        bl, bd, br, bv = (torch.randn(Mc, generator=g) for _ in range(4))
+        upd_s = _best(lambda: cl.minibatch_update(bo, ba, bl, bd, br, bv, np.arange(Mc)), 1)
+        it_s = 128 * step_s + 16 * upd_s
+        out["c3_rollout_step_ms"] = round(1e3 * step_s, 1)
+        out["c3_minibatch_update_M8192_ms"] = round(1e3 * upd_s, 1)
+        out["c3_iteration_s_extrapolated"] = round(it_s, 2)
+        out["c3_sps_extrapolated"] = round(Bc / it_s, 1)
+    return out
 
 
 def time_cpu_baseline(iterations=2, threads=16, **kw) -> dict:

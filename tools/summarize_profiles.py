@@ -36,7 +36,7 @@ def algorithmic_bytes(name, size):
     if name == "gae":
         return 20 * p["T"] * p["N"] + 8 * p["N"]
     if name == "ppo_loss_prepared":
-        return (8 * p["A"] + 28) * p["M"]
+        return (8 * p["A"] + 32) * p["M"]
     if name == "policy_head":
         return p["N"] * (4 * p["H"] + 4 * p["A"] + 16) + 4 * (p["A"] + 1) * (p["H"] + 1)
     if name == "rollout_store":
