@@ -33,11 +33,15 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
+MFMA_F32_PEAK_TFLOPS = 157.3  # dense f32 MFMA (MI355X_MICROARCH.md; no xf32 on gfx950)
+RIDGE = MFMA_F32_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9)  # flop/B where the two bounds meet
 # HBM bytes per launch from rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE, separate passes) of
 # the same launch shapes: tools/profile_round.sh -> tools/summarize_profiles.py
 PMC_SUMMARY = ROOT / "profiles" / "r01g" / "pmc_summary.json"
 PMC_KEYS = {"action_head": "policy_head_config", "gae": "gae_config",
-            "ppo_loss": "ppo_loss_prepared_config", "relu_bias_grad": "relu_bias_grad_config"}
+            "ppo_loss": "ppo_loss_prepared_config", "relu_bias_grad": "relu_bias_grad_config",
+            "cache_linear": "cache_linear_config", "store_encode": "store_encode_config",
+            "heads_bwd": "heads_bwd_config", "relu_bias_wgrad": "relu_bias_wgrad_config"}
 
 
 def pmc_traffic(key):
@@ -76,6 +80,14 @@ def kernel_bytes(tr) -> dict:
         "frame_cache": (N * (4 + 4 * tr.enc_cache.shape[2] * (2 * tr.enc_cache.shape[1]))
                         if tr.enc_cache is not None else None),
     }
+    if tr.rollout_fusion:
+        lins = [m for m in tr.agent.network[:tr.agent._flat] if isinstance(m, torch.nn.Linear)]
+        N1, N2 = lins[0].out_features, lins[1].out_features
+        E, Kl = lins[-1].out_features, lins[-1].in_features
+        # store (as rollout_store) + linear2: W1, W2 in, y [N, N2] out (the frame is counted once)
+        kb["store_encode"] = kb["rollout_store"] + 4 * (N1 * (D + 1) + N2 * (N1 + 1)) + 4 * N * N2
+        # x [N, K] + W [E, K] in; cache: W-1 slots read, W slots written, done row
+        kb["cache_linear"] = 4 * (N * Kl + E * (Kl + 1)) + 4 * N * E * (2 * W - 1) + 4 * N
     Hh = tr.agent.actor.in_features
     # heads' input h in + masked dh out [M, H]; dlogits + dv in; [Wa; Wc] in, dW + db out
     kb["heads_bwd"] = M * Hh * 8 + M * (A + 1) * 4 + 2 * (A + 1) * Hh * 4 + Hh * 4 + (A + 1) * 4
@@ -89,6 +101,34 @@ def kernel_bytes(tr) -> dict:
         # dh rows in, one row out per distinct frame
         kb["frames_scatter"] = 4 * M * W * E + C * (4 + 4 * E)
     return kb
+
+
+def kernel_flops(tr) -> dict:
+    """Useful flops per launch of the MFMA kernels (2 per multiply-add)."""
+    fl = {}
+    if tr.rollout_fusion:
+        lins = [m for m in tr.agent.network[:tr.agent._flat] if isinstance(m, torch.nn.Linear)]
+        fl["store_encode"] = 2 * tr.N * (lins[0].in_features * lins[0].out_features +
+                                         lins[1].in_features * lins[1].out_features)
+        fl["cache_linear"] = 2 * tr.N * lins[-1].in_features * lins[-1].out_features
+    return fl
+
+
+def roofline_of(name, k, flops, traffic, src):
+    """The roofline record of one timed kernel: MFMA-bound when its arithmetic intensity (useful
+    flops / algorithmic bytes) is above the ridge point, else HBM-bound."""
+    rec = {"kernel": name, "bytes_per_launch": k["bytes"], "mean_launch_us": k["mean_us"],
+           "traffic": traffic, "traffic_source": src}
+    if flops and flops / k["bytes"] > RIDGE:
+        ach = flops / (k["mean_us"] * 1e-6) / 1e12
+        rec.update(bound="mfma", achieved=round(ach, 2), peak=MFMA_F32_PEAK_TFLOPS,
+                   unit="TFLOP/s", frac=round(ach / MFMA_F32_PEAK_TFLOPS, 5),
+                   flops_per_launch=flops)
+    else:
+        ach = k["GBps"]
+        rec.update(bound="hbm", achieved=ach, peak=HBM_PEAK_GBS, unit="GB/s",
+                   frac=round(ach / HBM_PEAK_GBS, 5))
+    return rec
 
 
 def relu_bias_grad_bytes(name: str):
@@ -214,16 +254,16 @@ def main():
         for k in parts:
             kernels[k].pop("GBps", None)  # counted in the aggregate
     timed = [k for k in kernels if "GBps" in kernels[k]]
-    dom = max(timed, key=lambda k: kernels[k]["us_per_iter"]) if timed else None
-    roofline = None
-    if dom:
-        ach = kernels[dom]["GBps"]
+    kf = kernel_flops(tr)
+    recs = []
+    for name in sorted(timed, key=lambda k: -kernels[k]["us_per_iter"]):
         # the PMC passes replay config 2's launch shapes: no traffic figure for other configs
-        traffic, src = pmc_traffic(PMC_KEYS.get(dom, "")) if opt.config == 2 else (None, None)
-        roofline = {"kernel": dom, "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5),
-                    "traffic": traffic, "traffic_source": src, "bytes_per_launch": kernels[dom]["bytes"],
-                    "mean_launch_us": kernels[dom]["mean_us"]}
+        traffic, src = pmc_traffic(PMC_KEYS.get(name, "")) if opt.config == 2 else (None, None)
+        recs.append(roofline_of(name, kernels[name], kf.get(name), traffic, src))
+    # the dominant kernel of this package by device time per iteration; also the dominant
+    # HBM-bound one when that is a different kernel
+    roofline = recs[0] if recs else None
+    roofline_hbm = next((r for r in recs if r["bound"] == "hbm"), None)
 
     scaled = None
     if rank == 0 and world == 1 and not opt.no_scaled and opt.config == 2:
@@ -288,6 +328,8 @@ def main():
                        "parallelism": f"dp{world}"},
             "updates_per_sec": round(updates / dt, 2),
             "roofline": roofline,
+            "roofline_hbm": roofline_hbm if roofline_hbm is not roofline else None,
+            "rooflines_top": recs[:6],
             "roofline_scaled": scaled,
             "kernels": kernels,
             "cpu_baseline": cpu,

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define OCPPO_ABI_VERSION 7
+#define OCPPO_ABI_VERSION 9
 
 /* status codes */
 #define OCPPO_OK 0
@@ -308,6 +308,18 @@ OCPPO_API int ocppo_relu_bias_grad(ocppo_stream_t stream, const float* g, const 
  * 1 <= K <= 16. Workspace 256-B aligned, >= ocppo_relu_bias_wgrad_workspace_bytes(R, N, K),
  * ZEROED before its first use (tickets re-arm). Deterministic (fixed-order sums, f32 fma).
  * ------------------------------------------------------------------------------------------- */
+/* Deferred form: gp as above, db left as per-chunk column partials partials[chunks, N]
+ * (chunks = ocppo_relu_bias_grad_chunks(R, N)), summed later in chunk order by
+ * ocppo_sum_splits_db in the launch that combines the layer's split-K weight gradient: no
+ * cross-workgroup hand-off inside this launch. */
+OCPPO_API int64_t ocppo_relu_bias_grad_chunks(int64_t R, int64_t N);
+OCPPO_API int ocppo_relu_bias_grad_partial(ocppo_stream_t stream, const float* g, const float* out,
+                                           float* gp, float* partials, int64_t R, int64_t N);
+/* ocppo_sum_splits (out = sum of the S split-K blocks) + db[j] = sum_c db_partials[c, j] (chunk
+ * order) in one launch; n, N multiples of 4, all pointers 16-B aligned. */
+OCPPO_API int ocppo_sum_splits_db(ocppo_stream_t stream, const float* part, int64_t S, int64_t n,
+                                  float* out, const float* db_partials, int64_t chunks, int64_t N,
+                                  float* db);
 OCPPO_API size_t ocppo_relu_bias_wgrad_workspace_bytes(int64_t R, int64_t N, int64_t K);
 OCPPO_API int ocppo_relu_bias_wgrad(ocppo_stream_t stream, const float* g, const float* out,
                           const float* x, int64_t ldx, float* dw, float* db, int64_t R,
@@ -457,6 +469,35 @@ OCPPO_API int ocppo_td_loss_fwd_bwd(ocppo_stream_t stream, const float* q, const
 OCPPO_API int ocppo_synth_env_step(ocppo_stream_t stream, uint64_t seed, const int64_t* step_base,
                          int64_t step_offset, const int64_t* actions, int64_t N, int64_t D, int pixel_mode,
                          void* frame_out, float* reward_out, float* done_out, float* ep_state);
+
+/* ---------------------------------------------------------------------------------------------
+ * Rollout fusions of the PPObj frame-encoding cache path (ppo_atari_oc.py:502-514 + :506 with
+ * architectures/ppo.py:60-95): per env step the launches are [store of step t-1 + the first two
+ * encoder layers of the newest frame] -> middle encoder layers -> [last encoder layer + cache
+ * shift] -> decoder -> fused policy head.
+ *
+ * ocppo_linear_cache_shift: fresh = act(x W^T + b) (as ocppo_linear_act, x [M, K], W [N, K]) is
+ *   not stored; instead enc [M, W, N] (the frame-encoding cache) is shifted with it:
+ *   enc[m, w] = done[m] != 0 || w == W-1 ? fresh[m] : enc[m, w+1]  (ocppo_frame_cache_shift's rule;
+ *   done [M] f32 or NULL).
+ * ocppo_store_linear2: ocppo_rollout_store (vecnorm = 0; reward_out = the raw reward row) or
+ *   ocppo_rollout_store_vecnorm (vecnorm = 1) of frame [N, D] f32 into obs_out / net_obs /
+ *   reward_out / done_out, AND y [N, N2] (row stride ldy) = relu(relu(f W1^T + b1) W2^T + b2) of
+ *   the newest frames f = frame seen through obs_dtype (OCPPO_F32 or OCPPO_BF16 round trip), as
+ *   ocppo_linear2_act (D <= 64, N1 % 16 == 0, N1 <= 512, W2 16-B aligned), in one launch.
+ * ------------------------------------------------------------------------------------------- */
+OCPPO_API int ocppo_linear_cache_shift(ocppo_stream_t stream, const float* x, int64_t ldx,
+                                       const float* w, const float* b, float* enc,
+                                       const float* done, int64_t M, int64_t N, int64_t K,
+                                       int64_t W, int relu);
+OCPPO_API int ocppo_store_linear2(ocppo_stream_t stream, const float* frame, const float* reward,
+                                  const float* done, int64_t N, int64_t W, int64_t D,
+                                  const void* prev_obs, void* obs_out, int obs_dtype,
+                                  float* net_obs, float* reward_out, float* done_out, int vecnorm,
+                                  double gamma, double epsilon, double clip_reward,
+                                  double* ret_state, double* rms_state, const float* w1,
+                                  const float* b1, const float* w2, const float* b2, float* y,
+                                  int64_t ldy, int64_t N1, int64_t N2);
 
 /* ---------------------------------------------------------------------------------------------
  * CartPole-v1 vector env (config 1: cleanrl/ppo.py:81-91, 162 -- SyncVectorEnv of

@@ -68,17 +68,36 @@ def _splitk(rows: int, k: int, n: int) -> int:
     return max(s, 1)
 
 
-def _weight_grad(g, x, out=None):
-    """dW = g^T x (g [rows, n], x [rows, k]) with the split-K rule; written into `out` if given."""
+def _weight_grad(g, x, out=None, db=None):
+    """dW = g^T x (g [rows, n], x [rows, k]) with the split-K rule; written into `out` if given.
+    db = (partials of ops.relu_bias_grad_partial, bias grad): the bias gradient is finished in
+    the same launch as the split-K combine (only when _defer_db_ok said so)."""
     rows, n = g.shape
     k = x.shape[1]
     s = _splitk(rows, k, n)
     if s == 1:
         return torch.mm(g.t(), x, out=out) if out is not None else g.t().mm(x)
     part = torch.bmm(g.view(s, rows // s, n).transpose(1, 2), x.view(s, rows // s, k))
+    if db is not None:
+        return ops.timed(f"sum_splits_db_{s}x{n}x{k}", lambda: ops.sum_splits_db(part, out, *db))
     if out is not None and HIP_SUM_SPLITS and ops.sum_splits_ok(part, out):
         return ops.timed(f"sum_splits_{s}x{n}x{k}", lambda: ops.sum_splits(part, out))
     return torch.sum(part, 0, out=out) if out is not None else part.sum(0)
+
+
+def _defer_db_ok(g, x, w, b) -> bool:
+    """The bias gradient can ride in the split-K combine of the weight gradient (HIP sum_splits
+    path, FlatAdam-owned aligned grads)."""
+    rows, n = g.shape
+    k = x.shape[1]
+    return (DEFER_BIAS_GRAD and HIP_SUM_SPLITS and _splitk(rows, k, n) > 1 and (n * k) % 4 == 0
+            and n % 4 == 0 and w.grad.data_ptr() % 16 == 0 and b.grad.data_ptr() % 16 == 0
+            and w.grad.is_contiguous())
+
+
+# relu_bias_grad without its last-arriver tail: bias-gradient chunk sums finished by the weight
+# gradient's split-K combine (ops.relu_bias_grad_partial + ops.sum_splits_db).
+DEFER_BIAS_GRAD = True
 
 
 # Split-K partials of FlatAdam-owned weight gradients summed by one HIP pass (ops.sum_splits).
@@ -126,6 +145,17 @@ class _LinearAct(torch.autograd.Function):
             ops.timed(f"relu_bias_wgrad_{g.shape[0]}x{g.shape[1]}x{x.shape[1]}",
                       lambda: ops.relu_bias_wgrad(g, o, x, dw=ctx.w.grad, db=ctx.b.grad))
             return None, None, None, None, None
+        if FUSED_RELU_BIAS_GRAD and ctx.needs_input_grad[2] and _direct(ctx.b) and \
+                ops.relu_bias_grad_ok(g) and ctx.needs_input_grad[1] and _direct(ctx.w) and \
+                _defer_db_ok(g, x, ctx.w, ctx.b):
+            # ReLU-backward in one pass, bias grad finished with the split-K weight-grad combine
+            o = out if ctx.relu else None
+            gp, dbp = ops.timed(f"relu_bias_grad_{g.shape[0]}x{g.shape[1]}" +
+                                ("" if ctx.relu else "_norelu"),
+                                lambda: ops.relu_bias_grad_partial(g, o))
+            dx = gp.mm(w) if ctx.needs_input_grad[0] else None
+            _weight_grad(gp, x, out=ctx.w.grad, db=(dbp, ctx.b.grad))
+            return dx, None, None, None, None
         if FUSED_RELU_BIAS_GRAD and ctx.needs_input_grad[2] and _direct(ctx.b) and \
                 ops.relu_bias_grad_ok(g):
             # threshold_backward + bias sum in one HIP pass, bias grad written in place

@@ -117,6 +117,8 @@ class Args:
     save_model: bool = True
     metrics_every: int = 1     # read the device-side metrics every N iterations
     rollout_frame_cache: bool = True  # PPO_OBJ rollout: encode only the newest frame per step
+    rollout_fusion: bool = True  # PPO_OBJ rollout: store + first encoder layers in one launch,
+                                 # cache shift in the last encoder layer's epilogue
     update_frame_dedup: bool = True  # PPO_OBJ update: encode each distinct frame of a minibatch once
     prefetch_shuffle: bool = True  # shuffle (+ frame plan) of the next iteration while the GPU runs
     dp_overlap: bool = True  # DP: all-reduce the decoder-side gradients during the encoder backward

@@ -67,12 +67,26 @@ __device__ __forceinline__ void linear_wave_chunks(const float* xr, const float*
   }
 }
 
+// Frame-encoding cache epilogue (PPObj rollout, the last encoder layer): the layer's output row
+// m is env m's fresh frame encoding; instead of storing it to y, shift env m's cache enc[m, W, N]
+// like the frame stack (ocppo_frame_cache_shift's rule) with the fresh row in slot W-1:
+//   enc[m, w] = done[m] != 0 || w == W-1 ? fresh[m] : enc[m, w+1]
+// Each (row, column) of the cache is read and written by the one lane that owns that output
+// element, slots in increasing w, so the shift needs no second launch.
+struct CacheOut {
+  float* enc;         // [M, W, N]
+  const float* done;  // [M] or NULL
+  int W;
+};
+constexpr int kCacheMaxW = 8;
+
 // VEC: x / W rows are 16-B aligned with K % 4 == 0 (float4 operand loads); else scalar loads.
-template <int S, int CH, bool RELU, bool VEC>
+// CACHE: the output goes through the frame-cache epilogue above (y / ldy unused).
+template <int S, int CH, bool RELU, bool VEC, bool CACHE = false>
 __global__ __launch_bounds__(64 * S) void linear_rows_kernel(
     const float* __restrict__ x, int64_t ldx, const float* __restrict__ w,
     const float* __restrict__ bias, float* __restrict__ y, int64_t ldy, int M, int N, int K,
-    int ntm, int tiles) {
+    int ntm, int tiles, CacheOut cache = CacheOut{nullptr, nullptr, 0}) {
   __shared__ floatx4 red[S > 1 ? S - 1 : 1][64];
   const int b = blockIdx.x;
   const int per_xcd = (tiles + 7) / 8;
@@ -91,6 +105,24 @@ __global__ __launch_bounds__(64 * S) void linear_rows_kernel(
   const int cpw = (nch + S - 1) / S;
   const int c0 = wv * cpw;
   const int c1 = c0 + cpw < nch ? c0 + cpw : nch;
+  // cache epilogue: wave 0 loads the old slots and done flags of its 4 x 1 outputs before the
+  // MFMA loop, so their latency hides behind it (W <= kCacheMaxW; else loaded in the epilogue)
+  float old[4][kCacheMaxW - 1];
+  bool dn[4] = {false, false, false, false};
+  const bool pre = CACHE && wv == 0 && cache.W <= kCacheMaxW && tn * 16 + c16 < N;
+  if (pre) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int orow = tm * 16 + 4 * g + r;
+      if (orow < M) {
+        const float* e = cache.enc + static_cast<int64_t>(orow) * cache.W * N + tn * 16 + c16;
+        dn[r] = cache.done != nullptr && cache.done[orow] != 0.f;
+#pragma unroll
+        for (int q = 0; q < kCacheMaxW - 1; ++q)
+          old[r][q] = q + 1 < cache.W ? e[static_cast<int64_t>(q + 1) * N] : 0.f;
+      }
+    }
+  }
   floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
   linear_wave_chunks<CH, VEC>(xr, wr, rok, cok, K, g, c0, c1, acc0, acc1);
   floatx4 acc = acc0 + acc1;
@@ -111,49 +143,67 @@ __global__ __launch_bounds__(64 * S) void linear_rows_kernel(
     if (orow < M) {
       float v = acc[r] + bv;
       if (RELU) v = fmaxf(v, 0.f);
-      y[static_cast<int64_t>(orow) * ldy + ocol] = v;
+      if (CACHE) {
+        const int W = cache.W;
+        float* e = cache.enc + static_cast<int64_t>(orow) * W * N + ocol;
+        if (pre) {
+#pragma unroll
+          for (int q = 0; q < kCacheMaxW - 1; ++q)
+            if (q + 1 < W) e[static_cast<int64_t>(q) * N] = dn[r] ? v : old[r][q];
+          e[static_cast<int64_t>(W - 1) * N] = v;
+        } else if (cache.done != nullptr && cache.done[orow] != 0.f) {
+          for (int q = 0; q < W; ++q) e[static_cast<int64_t>(q) * N] = v;
+        } else {
+          for (int q = 0; q + 1 < W; ++q) e[static_cast<int64_t>(q) * N] = e[static_cast<int64_t>(q + 1) * N];
+          e[static_cast<int64_t>(W - 1) * N] = v;
+        }
+      } else {
+        y[static_cast<int64_t>(orow) * ldy + ocol] = v;
+      }
     }
   }
 }
 
-template <int S, int CH, bool RELU>
+template <int S, int CH, bool RELU, bool CACHE>
 static void launch_linear_sc(hipStream_t s, bool vec, const float* x, int64_t ldx, const float* w,
-                             const float* b, float* y, int64_t ldy, int M, int N, int K) {
+                             const float* b, float* y, int64_t ldy, int M, int N, int K,
+                             CacheOut c) {
   const int ntm = (M + 15) / 16, ntn = (N + 15) / 16, tiles = ntm * ntn;
   const dim3 grid(8 * ((tiles + 7) / 8)), block(64 * S);
   if (vec)
-    hipLaunchKernelGGL((linear_rows_kernel<S, CH, RELU, true>), grid, block, 0, s, x, ldx, w, b,
-                       y, ldy, M, N, K, ntm, tiles);
+    hipLaunchKernelGGL((linear_rows_kernel<S, CH, RELU, true, CACHE>), grid, block, 0, s, x, ldx,
+                       w, b, y, ldy, M, N, K, ntm, tiles, c);
   else
-    hipLaunchKernelGGL((linear_rows_kernel<S, CH, RELU, false>), grid, block, 0, s, x, ldx, w, b,
-                       y, ldy, M, N, K, ntm, tiles);
+    hipLaunchKernelGGL((linear_rows_kernel<S, CH, RELU, false, CACHE>), grid, block, 0, s, x, ldx,
+                       w, b, y, ldy, M, N, K, ntm, tiles, c);
 }
 
-template <int S, bool RELU>
+template <int S, bool RELU, bool CACHE>
 static void launch_linear_s(hipStream_t s, int cpw, bool vec, const float* x, int64_t ldx,
                             const float* w, const float* b, float* y, int64_t ldy, int M, int N,
-                            int K) {
+                            int K, CacheOut c) {
   if (cpw <= 2)
-    launch_linear_sc<S, 2, RELU>(s, vec, x, ldx, w, b, y, ldy, M, N, K);
+    launch_linear_sc<S, 2, RELU, CACHE>(s, vec, x, ldx, w, b, y, ldy, M, N, K, c);
   else if (cpw <= 4)
-    launch_linear_sc<S, 4, RELU>(s, vec, x, ldx, w, b, y, ldy, M, N, K);
+    launch_linear_sc<S, 4, RELU, CACHE>(s, vec, x, ldx, w, b, y, ldy, M, N, K, c);
   else
-    launch_linear_sc<S, 8, RELU>(s, vec, x, ldx, w, b, y, ldy, M, N, K);
+    launch_linear_sc<S, 8, RELU, CACHE>(s, vec, x, ldx, w, b, y, ldy, M, N, K, c);
 }
 
-template <bool RELU>
+template <bool RELU, bool CACHE = false>
 static void launch_linear(hipStream_t s, bool vec, const float* x, int64_t ldx, const float* w,
-                          const float* b, float* y, int64_t ldy, int M, int N, int K) {
+                          const float* b, float* y, int64_t ldy, int M, int N, int K,
+                          CacheOut c = CacheOut{nullptr, nullptr, 0}) {
   const int64_t tiles = static_cast<int64_t>((M + 15) / 16) * ((N + 15) / 16);
   const int nch = (K + 15) / 16;
   int S = 1;  // K split: >= ~4096 waves (4 per SIMD), >= 2 chunks per wave
   while (S < kLinMaxWaves && tiles * S < 4096 && nch >= 2 * S * 2) S *= 2;
   const int cpw = (nch + S - 1) / S;
   switch (S) {
-    case 1: launch_linear_s<1, RELU>(s, cpw, vec, x, ldx, w, b, y, ldy, M, N, K); break;
-    case 2: launch_linear_s<2, RELU>(s, cpw, vec, x, ldx, w, b, y, ldy, M, N, K); break;
-    case 4: launch_linear_s<4, RELU>(s, cpw, vec, x, ldx, w, b, y, ldy, M, N, K); break;
-    default: launch_linear_s<8, RELU>(s, cpw, vec, x, ldx, w, b, y, ldy, M, N, K); break;
+    case 1: launch_linear_s<1, RELU, CACHE>(s, cpw, vec, x, ldx, w, b, y, ldy, M, N, K, c); break;
+    case 2: launch_linear_s<2, RELU, CACHE>(s, cpw, vec, x, ldx, w, b, y, ldy, M, N, K, c); break;
+    case 4: launch_linear_s<4, RELU, CACHE>(s, cpw, vec, x, ldx, w, b, y, ldy, M, N, K, c); break;
+    default: launch_linear_s<8, RELU, CACHE>(s, cpw, vec, x, ldx, w, b, y, ldy, M, N, K, c); break;
   }
 }
 
@@ -183,6 +233,31 @@ extern "C" int ocppo_linear_act(ocppo_stream_t stream, const float* x, int64_t l
   return check_launch("ocppo_linear_act");
 }
 
+extern "C" int ocppo_linear_cache_shift(ocppo_stream_t stream, const float* x, int64_t ldx,
+                                        const float* w, const float* b, float* enc,
+                                        const float* done, int64_t M, int64_t N, int64_t K,
+                                        int64_t W, int relu) {
+  OCPPO_REQUIRE(M >= 0 && N >= 1 && K >= 1 && W >= 1 && W <= 64 && M <= INT32_MAX &&
+                    N <= INT32_MAX && K <= INT32_MAX,
+                "ocppo_linear_cache_shift: bad sizes M=%lld N=%lld K=%lld W=%lld", (long long)M,
+                (long long)N, (long long)K, (long long)W);
+  OCPPO_REQUIRE(ldx >= K, "ocppo_linear_cache_shift: ldx=%lld < K", (long long)ldx);
+  if (M == 0) return OCPPO_OK;
+  OCPPO_REQUIRE(x && w && enc, "ocppo_linear_cache_shift: null pointer");
+  OCPPO_REQUIRE((M + 15) / 16 * ((N + 15) / 16) <= INT32_MAX / 8,
+                "ocppo_linear_cache_shift: too large");
+  const bool vec = K % 4 == 0 && ldx % 4 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0 &&
+                   reinterpret_cast<uintptr_t>(w) % 16 == 0;
+  const CacheOut c{enc, done, static_cast<int>(W)};
+  clear_stale_error();
+  hipStream_t s = as_stream(stream);
+  if (relu)
+    launch_linear<true, true>(s, vec, x, ldx, w, b, nullptr, 0, (int)M, (int)N, (int)K, c);
+  else
+    launch_linear<false, true>(s, vec, x, ldx, w, b, nullptr, 0, (int)M, (int)N, (int)K, c);
+  return check_launch("ocppo_linear_cache_shift");
+}
+
 // ---- two Linear(+ReLU) layers in one launch: y = act2(act1(x W1^T + b1) W2^T + b2) ---------------
 // The first two PPObj encoder layers of the rollout's newest-frame encode (architectures/ppo.py:
 // 60-84: F -> 256 -> 512 at 128 rows per step): the first layer is tiny (K1 = F <= 64), so every
@@ -196,16 +271,17 @@ namespace ocppo {
 constexpr int kLin2MaxK1 = 64;
 constexpr int kLin2MaxN1 = 512;
 
-template <int S, bool RELU1, bool RELU2>
-__global__ __launch_bounds__(64 * S) void linear2_rows_kernel(
-    const float* __restrict__ x, int64_t ldx, const float* __restrict__ w1,
+// One workgroup's output tile. XDT: x is an f32 frame seen through the rollout storage dtype
+// (the network reads what the rollout buffer holds: bf16 round trip for object vectors stored in
+// bf16, identity for f32).
+template <int S, bool RELU1, bool RELU2, int XDT>
+__device__ __forceinline__ void linear2_tile(
+    int b, float* smem, const float* __restrict__ x, int64_t ldx, const float* __restrict__ w1,
     const float* __restrict__ b1, const float* __restrict__ w2, const float* __restrict__ b2,
     float* __restrict__ y, int64_t ldy, int M, int N1, int N2, int K1, int ntm, int tiles) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
   const int ldh = N1 + 4;
   float* h1 = smem;                                                    // [16][ldh]
   floatx4* red = reinterpret_cast<floatx4*>(smem + 16 * ldh);          // [S-1][64]
-  const int b = blockIdx.x;
   const int per_xcd = (tiles + 7) / 8;
   const int t = (b % 8) * per_xcd + b / 8;  // XCD-contiguous tile ranges (as linear_rows)
   if (t >= tiles) return;
@@ -231,10 +307,10 @@ __global__ __launch_bounds__(64 * S) void linear2_rows_kernel(
 #pragma unroll
   for (int kc = 0; kc < kLin2MaxK1 / 16; ++kc) {
     const int k = kc * 16 + 4 * g;
-    a1[kc].x = (kc < nkc && rok && k + 0 < K1) ? xr[k + 0] : 0.f;
-    a1[kc].y = (kc < nkc && rok && k + 1 < K1) ? xr[k + 1] : 0.f;
-    a1[kc].z = (kc < nkc && rok && k + 2 < K1) ? xr[k + 2] : 0.f;
-    a1[kc].w = (kc < nkc && rok && k + 3 < K1) ? xr[k + 3] : 0.f;
+    a1[kc].x = (kc < nkc && rok && k + 0 < K1) ? Elem<XDT>::roundtrip(xr[k + 0]) : 0.f;
+    a1[kc].y = (kc < nkc && rok && k + 1 < K1) ? Elem<XDT>::roundtrip(xr[k + 1]) : 0.f;
+    a1[kc].z = (kc < nkc && rok && k + 2 < K1) ? Elem<XDT>::roundtrip(xr[k + 2]) : 0.f;
+    a1[kc].w = (kc < nkc && rok && k + 3 < K1) ? Elem<XDT>::roundtrip(xr[k + 3]) : 0.f;
   }
   float4 b2v[kMaxT];
 #pragma unroll
@@ -313,6 +389,16 @@ __global__ __launch_bounds__(64 * S) void linear2_rows_kernel(
   }
 }
 
+template <int S, bool RELU1, bool RELU2>
+__global__ __launch_bounds__(64 * S) void linear2_rows_kernel(
+    const float* __restrict__ x, int64_t ldx, const float* __restrict__ w1,
+    const float* __restrict__ b1, const float* __restrict__ w2, const float* __restrict__ b2,
+    float* __restrict__ y, int64_t ldy, int M, int N1, int N2, int K1, int ntm, int tiles) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  linear2_tile<S, RELU1, RELU2, OCPPO_F32>(blockIdx.x, smem, x, ldx, w1, b1, w2, b2, y, ldy, M,
+                                           N1, N2, K1, ntm, tiles);
+}
+
 template <bool R1, bool R2>
 static void launch_linear2(hipStream_t s, const float* x, int64_t ldx, const float* w1,
                            const float* b1, const float* w2, const float* b2, float* y,
@@ -352,4 +438,124 @@ extern "C" int ocppo_linear2_act(ocppo_stream_t stream, const float* x, int64_t 
   else
     launch_linear2<false, false>(s, x, ldx, w1, b1, w2, b2, y, ldy, m, n1, n2, k1);
   return check_launch("ocppo_linear2_act");
+}
+
+// ---- rollout store of step t-1 + the first two encoder layers of step t in ONE launch -----------
+// The PPObj rollout with the frame-encoding cache (ocppo_frame_cache_shift): each step stores the
+// env's output (ocppo_rollout_store[_vecnorm]: frame stack into rollout slot t, f32 network copy,
+// reward / done rows, VecNormalize) and then encodes ONLY the newest frame, whose first two
+// Linear+ReLU layers are ocppo_linear2_act over those N frames. Neither half reads what the other
+// writes (the encoder takes the newest frame straight from the env output, seen through the
+// storage dtype exactly as the stored slot holds it), so they share a launch: workgroups
+// [0, lin) run linear2 tiles, workgroup lin the VecNormalize reduction (when asked), the rest the
+// store groups. Same arithmetic as the two launches it replaces (ppo_atari_oc.py:502-514 and the
+// encoder half of :506).
+#include "ocppo_store.h"
+
+namespace ocppo {
+
+struct StoreLin2Args {
+  // store
+  const float* frame;
+  const float* reward;
+  const float* done;
+  int64_t N, D;
+  int W;
+  const void* prev;
+  void* out;
+  float* net;
+  float* reward_out;
+  float* done_out;
+  double gamma, eps, clip;
+  double* ret;
+  double* rms;
+  // linear2
+  const float* w1;
+  const float* b1;
+  const float* w2;
+  const float* b2;
+  float* y;
+  int64_t ldy;
+  int N1, N2, ntm, tiles, lin_blocks;
+};
+
+template <int ODT, int VEC, bool VN>
+__global__ __launch_bounds__(256) void store_linear2_kernel(StoreLin2Args a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int b = blockIdx.x;
+  if (b < a.lin_blocks) {
+    // the newest frame of slot t+1 is frame[n] itself (slot W-1, reset fill or not)
+    linear2_tile<4, true, true, ODT>(b, smem, a.frame, a.D, a.w1, a.b1, a.w2, a.b2, a.y, a.ldy,
+                                     static_cast<int>(a.N), a.N1, a.N2, static_cast<int>(a.D),
+                                     a.ntm, a.tiles);
+    return;
+  }
+  if (VN && b == a.lin_blocks) {
+    vecnorm_block(a.reward, a.done, a.N, a.gamma, a.eps, a.clip, a.ret, a.rms, a.reward_out);
+    return;
+  }
+  const int s0 = a.lin_blocks + (VN ? 1 : 0);
+  store_groups<OCPPO_F32, ODT, VEC>(b - s0, gridDim.x - s0, a.frame, a.reward, a.done, a.N, a.W,
+                                    a.D, a.prev, a.out, a.net, VN ? nullptr : a.reward_out,
+                                    a.done_out, 1.0f, nullptr);
+}
+
+template <int ODT, bool VN>
+static void launch_store_linear2(hipStream_t s, const StoreLin2Args& a) {
+  const size_t lds = sizeof(float) * 16 * (a.N1 + 4) + sizeof(floatx4) * 64 * 3;
+  const int vec = a.D % 4 == 0 ? 4 : 1;
+  const int64_t groups = a.N * a.W * (a.D / vec);
+  const int sg = grid_for(groups, 256);
+  const dim3 grid(a.lin_blocks + (VN ? 1 : 0) + sg);
+  if (vec == 4)
+    hipLaunchKernelGGL((store_linear2_kernel<ODT, 4, VN>), grid, dim3(256), lds, s, a);
+  else
+    hipLaunchKernelGGL((store_linear2_kernel<ODT, 1, VN>), grid, dim3(256), lds, s, a);
+}
+
+}  // namespace ocppo
+
+extern "C" int ocppo_store_linear2(ocppo_stream_t stream, const float* frame, const float* reward,
+                                   const float* done, int64_t N, int64_t W, int64_t D,
+                                   const void* prev_obs, void* obs_out, int obs_dtype,
+                                   float* net_obs, float* reward_out, float* done_out,
+                                   int vecnorm, double gamma, double epsilon, double clip_reward,
+                                   double* ret_state, double* rms_state, const float* w1,
+                                   const float* b1, const float* w2, const float* b2, float* y,
+                                   int64_t ldy, int64_t N1, int64_t N2) {
+  OCPPO_REQUIRE(N >= 1 && N <= INT32_MAX && W >= 1 && W <= 64 && D >= 1 && D <= kLin2MaxK1 &&
+                    N1 >= 16 && N1 % 16 == 0 && N1 <= kLin2MaxN1 && N2 >= 1 && N2 <= INT32_MAX &&
+                    ldy >= N2,
+                "ocppo_store_linear2: bad sizes N=%lld W=%lld D=%lld N1=%lld N2=%lld (D <= 64, "
+                "N1 %% 16 == 0, N1 <= 512)", (long long)N, (long long)W, (long long)D,
+                (long long)N1, (long long)N2);
+  OCPPO_REQUIRE(obs_dtype == OCPPO_F32 || obs_dtype == OCPPO_BF16,
+                "ocppo_store_linear2: obs dtype must be OCPPO_F32 or OCPPO_BF16 (object vectors)");
+  OCPPO_REQUIRE(frame && reward && done && prev_obs && obs_out && w1 && w2 && y,
+                "ocppo_store_linear2: null pointer");
+  OCPPO_REQUIRE(prev_obs != obs_out, "ocppo_store_linear2: prev_obs must not alias obs_out");
+  OCPPO_REQUIRE(!vecnorm || (ret_state && rms_state && reward_out && reward_out != reward),
+                "ocppo_store_linear2: VecNormalize needs ret/rms state and a separate reward_out");
+  OCPPO_REQUIRE(reinterpret_cast<uintptr_t>(w2) % 16 == 0,
+                "ocppo_store_linear2: w2 must be 16-B aligned");
+  StoreLin2Args a;
+  a.frame = frame; a.reward = reward; a.done = done; a.N = N; a.D = D; a.W = (int)W;
+  a.prev = prev_obs; a.out = obs_out; a.net = net_obs; a.reward_out = reward_out;
+  a.done_out = done_out; a.gamma = gamma; a.eps = epsilon; a.clip = clip_reward;
+  a.ret = ret_state; a.rms = rms_state;
+  a.w1 = w1; a.b1 = b1; a.w2 = w2; a.b2 = b2; a.y = y; a.ldy = ldy;
+  a.N1 = (int)N1; a.N2 = (int)N2;
+  a.ntm = (int)((N + 15) / 16);
+  a.tiles = a.ntm * (int)((N2 + 15) / 16);
+  a.lin_blocks = 8 * ((a.tiles + 7) / 8);
+  clear_stale_error();
+  hipStream_t s = as_stream(stream);
+  if (obs_dtype == OCPPO_BF16) {
+    if (vecnorm) launch_store_linear2<OCPPO_BF16, true>(s, a);
+    else launch_store_linear2<OCPPO_BF16, false>(s, a);
+  } else {
+    if (vecnorm) launch_store_linear2<OCPPO_F32, true>(s, a);
+    else launch_store_linear2<OCPPO_F32, false>(s, a);
+  }
+  return check_launch("ocppo_store_linear2");
 }

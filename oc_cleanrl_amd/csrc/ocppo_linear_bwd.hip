@@ -70,7 +70,10 @@ inline RbPlan rb_plan(int64_t R, int64_t N) {
   return p;
 }
 
-template <bool RELU>
+// TAIL = false: every workgroup stores its partial column sums (plain stores) and is done; the
+// chunk sums are left to a later kernel of the same stream (ocppo_sum_splits_db, which runs after
+// the layer's split-K weight gradient anyway): no ticket, no last-arriver tail on this launch.
+template <bool RELU, bool TAIL = true>
 __global__ __launch_bounds__(256) void relu_bias_grad_kernel(const float* __restrict__ g,
                                                              const float* __restrict__ out,
                                                              float* __restrict__ gp,
@@ -140,9 +143,13 @@ __global__ __launch_bounds__(256) void relu_bias_grad_kernel(const float* __rest
         const float4 v = red[w][q * L + jc];
         s += comp == 0 ? v.x : comp == 1 ? v.y : comp == 2 ? v.z : v.w;
       }
-    __hip_atomic_store(&partials[static_cast<int64_t>(chunk) * N + col], s, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
+    if (TAIL)
+      __hip_atomic_store(&partials[static_cast<int64_t>(chunk) * N + col], s, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    else
+      partials[static_cast<int64_t>(chunk) * N + col] = s;
   }
+  if (!TAIL) return;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   unsigned* ticket = tickets + stripe * 32;
@@ -230,6 +237,35 @@ extern "C" int ocppo_relu_bias_grad(ocppo_stream_t stream, const float* g, const
   return check_launch("ocppo_relu_bias_grad");
 }
 
+extern "C" int64_t ocppo_relu_bias_grad_chunks(int64_t R, int64_t N) {
+  if (R < 1 || N < 4) return 1;
+  return rb_plan(R, N).chunks;
+}
+
+extern "C" int ocppo_relu_bias_grad_partial(ocppo_stream_t stream, const float* g,
+                                            const float* out, float* gp, float* partials,
+                                            int64_t R, int64_t N) {
+  OCPPO_REQUIRE(R >= 1 && N >= 4 && N % 4 == 0 && N <= kRbMaxStripes * 256,
+                "ocppo_relu_bias_grad_partial: bad sizes R=%lld N=%lld (R >= 1, N %% 4 == 0, "
+                "4 <= N <= 16384)", (long long)R, (long long)N);
+  OCPPO_REQUIRE(g && partials && (!out || gp), "ocppo_relu_bias_grad_partial: null pointer");
+  OCPPO_REQUIRE(reinterpret_cast<uintptr_t>(g) % 16 == 0 &&
+                    (!out || (reinterpret_cast<uintptr_t>(out) % 16 == 0 &&
+                              reinterpret_cast<uintptr_t>(gp) % 16 == 0)),
+                "ocppo_relu_bias_grad_partial: g/out/gp must be 16-B aligned");
+  clear_stale_error();
+  hipStream_t s = as_stream(stream);
+  const RbPlan p = rb_plan(R, N);
+  const dim3 grid(static_cast<unsigned>(p.stripes * p.chunks)), block(256);
+  if (out)
+    hipLaunchKernelGGL((relu_bias_grad_kernel<true, false>), grid, block, 0, s, g, out, gp,
+                       nullptr, R, N, p.L, p.chunks, nullptr, partials);
+  else
+    hipLaunchKernelGGL((relu_bias_grad_kernel<false, false>), grid, block, 0, s, g, out, gp,
+                       nullptr, R, N, p.L, p.chunks, nullptr, partials);
+  return check_launch("ocppo_relu_bias_grad_partial");
+}
+
 // ---- forward epilogue: y = act(y + b) in place over [R, N] rows (e.g. an NHWC convolution
 // output, N = channels), the bias add + ReLU ATen runs as two passes after a bias-less conv.
 namespace ocppo {
@@ -296,6 +332,97 @@ __global__ __launch_bounds__(256) void sum_splits_kernel(const float4* __restric
   }
 }
 }  // namespace ocppo
+
+// The deferred bias gradient of ocppo_relu_bias_grad_partial, summed in the same launch as the
+// weight gradient's split-K combine: blocks [0, nsb) combine the weight splits, blocks
+// [nsb, nsb + ceil(N / 64)) each own 64 columns of db: 16 column quads x 16 chunk groups, each
+// thread summing its chunks in order, then the 16 group sums in group order (LDS): one pass,
+// deterministic.
+template <int S>
+__global__ __launch_bounds__(256) void sum_splits_db_kernel(const float4* __restrict__ part,
+                                                            int64_t n4, float4* __restrict__ out,
+                                                            int nsb, const float* __restrict__ dbp,
+                                                            int chunks, int64_t N,
+                                                            float* __restrict__ db) {
+  if (static_cast<int>(blockIdx.x) < nsb) {
+    const int64_t stride = static_cast<int64_t>(nsb) * blockDim.x;
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n4;
+         i += stride) {
+      float4 v[S];
+#pragma unroll
+      for (int s = 0; s < S; ++s) v[s] = part[s * n4 + i];
+      float4 a = v[0];
+#pragma unroll
+      for (int s = 1; s < S; ++s) {
+        a.x += v[s].x; a.y += v[s].y; a.z += v[s].z; a.w += v[s].w;
+      }
+      out[i] = a;
+    }
+    return;
+  }
+  __shared__ float4 red[16][16];
+  const int cb = blockIdx.x - nsb;
+  const int q = threadIdx.x & 15, gi = threadIdx.x >> 4;  // column quad, chunk group
+  const int64_t col = static_cast<int64_t>(cb) * 64 + 4 * q;
+  const int cpg = (chunks + 15) / 16;
+  const int c0 = gi * cpg, c1 = c0 + cpg < chunks ? c0 + cpg : chunks;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (col < N) {
+    for (int c = c0; c < c1; c += 8) {
+      float4 v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        v[k] = c + k < c1 ? *reinterpret_cast<const float4*>(dbp + (c + k) * N + col)
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        acc.x += v[k].x; acc.y += v[k].y; acc.z += v[k].z; acc.w += v[k].w;
+      }
+    }
+  }
+  red[gi][q] = acc;
+  __syncthreads();
+  if (gi == 0 && col < N) {
+    float4 t = red[0][q];
+    for (int k = 1; k < 16; ++k) {
+      const float4 v = red[k][q];
+      t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+    }
+    *reinterpret_cast<float4*>(db + col) = t;
+  }
+}
+
+extern "C" int ocppo_sum_splits_db(ocppo_stream_t stream, const float* part, int64_t S, int64_t n,
+                                   float* out, const float* db_partials, int64_t chunks, int64_t N,
+                                   float* db) {
+  OCPPO_REQUIRE(n >= 4 && n % 4 == 0 && (S == 1 || S == 2 || S == 4 || S == 8 || S == 16) &&
+                    N >= 4 && N % 4 == 0 && chunks >= 1,
+                "ocppo_sum_splits_db: bad sizes S=%lld n=%lld N=%lld chunks=%lld", (long long)S,
+                (long long)n, (long long)N, (long long)chunks);
+  OCPPO_REQUIRE(part && out && db_partials && db, "ocppo_sum_splits_db: null pointer");
+  OCPPO_REQUIRE(reinterpret_cast<uintptr_t>(part) % 16 == 0 &&
+                    reinterpret_cast<uintptr_t>(out) % 16 == 0 &&
+                    reinterpret_cast<uintptr_t>(db_partials) % 16 == 0 &&
+                    reinterpret_cast<uintptr_t>(db) % 16 == 0,
+                "ocppo_sum_splits_db: pointers must be 16-B aligned");
+  clear_stale_error();
+  const int64_t n4 = n / 4;
+  const int nsb = grid_for(n4, 256);
+  const int ndb = static_cast<int>((N + 63) / 64);
+  const dim3 grid(nsb + ndb), block(256);
+  hipStream_t s = as_stream(stream);
+  const float4* p4 = reinterpret_cast<const float4*>(part);
+  float4* o4 = reinterpret_cast<float4*>(out);
+  const int c = static_cast<int>(chunks);
+  switch (S) {
+    case 1: hipLaunchKernelGGL(sum_splits_db_kernel<1>, grid, block, 0, s, p4, n4, o4, nsb, db_partials, c, N, db); break;
+    case 2: hipLaunchKernelGGL(sum_splits_db_kernel<2>, grid, block, 0, s, p4, n4, o4, nsb, db_partials, c, N, db); break;
+    case 4: hipLaunchKernelGGL(sum_splits_db_kernel<4>, grid, block, 0, s, p4, n4, o4, nsb, db_partials, c, N, db); break;
+    case 8: hipLaunchKernelGGL(sum_splits_db_kernel<8>, grid, block, 0, s, p4, n4, o4, nsb, db_partials, c, N, db); break;
+    default: hipLaunchKernelGGL(sum_splits_db_kernel<16>, grid, block, 0, s, p4, n4, o4, nsb, db_partials, c, N, db); break;
+  }
+  return check_launch("ocppo_sum_splits_db");
+}
 
 extern "C" int ocppo_sum_splits(ocppo_stream_t stream, const float* part, int64_t S, int64_t n,
                                 float* out) {

@@ -440,6 +440,64 @@ def linear2_act(x, w1, b1, w2, b2, relu1: bool = True, relu2: bool = True, out=N
     return out
 
 
+def linear_cache_shift(x, weight, bias, enc, done=None, relu: bool = True):
+    """The rollout's last encoder layer and the frame-encoding cache shift in one launch:
+    fresh = act(x @ weight.T + bias) (x [M, K] f32, unit column stride; weight [E, K]) shifts
+    enc [M, W, E] like ops.frame_cache_shift(enc, fresh, done) without storing fresh."""
+    if x.dim() != 2 or weight.dim() != 2 or enc.dim() != 3:
+        raise ValueError(f"x [M, K], weight [E, K], enc [M, W, E] expected, got {tuple(x.shape)}, "
+                         f"{tuple(weight.shape)}, {tuple(enc.shape)}")
+    M, K = x.shape
+    E = weight.shape[0]
+    dev = x.device
+    if weight.shape[1] != K or enc.shape[0] != M or enc.shape[2] != E:
+        raise ValueError(f"shapes: x {tuple(x.shape)}, weight {tuple(weight.shape)}, "
+                         f"enc {tuple(enc.shape)}")
+    if x.dtype != torch.float32 or (M > 1 and x.stride(1) != 1) or x.device.type != "cuda":
+        raise ValueError("x must be an f32 GPU tensor with unit column stride")
+    call("ocppo_linear_cache_shift", _stream(dev), x.data_ptr(), x.stride(0) if M > 1 else K,
+         _check(weight, "weight", torch.float32, dev), _opt(bias, "bias", torch.float32, dev, E),
+         _check(enc, "enc", torch.float32, dev), _opt(done, "done", torch.float32, dev, M), M, E,
+         K, enc.shape[1], 1 if relu else 0)
+    return enc
+
+
+def store_linear2(frame, reward, done, prev_obs, obs_out, net_obs, done_out, reward_out, w1, b1,
+                  w2, b2, y, vecnorm_state=None, gamma=0.99, epsilon=1e-8, clip_reward=10.0):
+    """ONE launch: the rollout store of the previous step (ops.rollout_store, or
+    ops.rollout_store_vecnorm when vecnorm_state = (ret_state, rms_state)) and
+    y = relu(relu(f @ w1.T + b1) @ w2.T + b2) of the newest frames f (frame seen through the
+    storage dtype of obs_out, f32 or bf16). frame [N, D] f32, obs [N, W, D], net_obs [N, W, D]
+    f32, y [N, N2] f32 (row stride may exceed N2)."""
+    N, D = frame.shape
+    W = obs_out.shape[1]
+    dev = frame.device
+    f = torch.float32
+    if frame.dtype != f:
+        raise ValueError("store_linear2: object frames only (f32)")
+    if prev_obs.shape != obs_out.shape or prev_obs.dtype != obs_out.dtype or \
+            tuple(obs_out.shape) != (N, W, D) or obs_out.dtype not in (torch.float32, torch.bfloat16):
+        raise ValueError(f"obs slots must be [N, W, D] f32|bf16, got {tuple(obs_out.shape)} "
+                         f"{obs_out.dtype}")
+    N1, N2 = w1.shape[0], w2.shape[0]
+    if tuple(w1.shape) != (N1, D) or tuple(w2.shape) != (N2, N1) or y.shape[0] != N or \
+            y.shape[1] != N2 or y.stride(1) != 1 or y.dtype != f:
+        raise ValueError(f"shapes: frame {tuple(frame.shape)}, w1 {tuple(w1.shape)}, "
+                         f"w2 {tuple(w2.shape)}, y {tuple(y.shape)}")
+    vn = vecnorm_state is not None
+    ret, rms = vecnorm_state if vn else (None, None)
+    call("ocppo_store_linear2", _stream(dev), _check(frame, "frame", f, dev),
+         _check(reward, "reward", f, dev, N), _check(done, "done", f, dev, N), N, W, D,
+         _check(prev_obs, "prev_obs", None, dev), _check(obs_out, "obs_out", None, dev),
+         _DTYPE_CODE[obs_out.dtype], _opt(net_obs, "net_obs", f, dev, N * W * D),
+         _check(reward_out, "reward_out", f, dev, N), _opt(done_out, "done_out", f, dev, N),
+         int(vn), float(gamma), float(epsilon), float(clip_reward),
+         _opt(ret, "ret_state", torch.float64, dev, N), _opt(rms, "rms_state", torch.float64, dev, 3),
+         _check(w1, "w1", f, dev), _opt(b1, "b1", f, dev, N1), _check(w2, "w2", f, dev),
+         _opt(b2, "b2", f, dev, N2), y.data_ptr(), y.stride(0) if N > 1 else N2, N1, N2)
+    return y
+
+
 # ---------------------------------------------------------------------------------------------
 # Linear(+ReLU) backward, elementwise part: threshold_backward + bias sum in one pass
 # (autograd of architectures/ppo.py:60-84 inside ppo_atari_oc.py:605)
@@ -480,6 +538,43 @@ def relu_bias_grad(g, out=None, db=None, gp=None):
          _opt(out, "out", f, dev, R * N), _opt(gp, "gp", f, dev, R * N),
          _check(db, "db", f, dev, N), R, N, ws.data_ptr(), ws.numel())
     return (gp if out is not None else g), db
+
+
+_RB_PART: dict = {}
+
+
+def relu_bias_grad_partial(g, out=None, gp=None):
+    """(gp, (partials, chunks)): relu_bias_grad with the bias-gradient chunk sums left for
+    sum_splits_db (deferred to the launch that combines the layer's split-K weight gradient).
+    partials [chunks, N] f32 is a per-shape persistent buffer (graph-safe)."""
+    R, N = g.shape
+    dev = g.device
+    f = torch.float32
+    if out is not None and gp is None:
+        gp = torch.empty_like(g)
+    key = (dev, R, N)
+    buf = _RB_PART.get(key)
+    if buf is None:
+        chunks = int(_lib.LIB.ocppo_relu_bias_grad_chunks(R, N))
+        buf = _RB_PART[key] = (torch.zeros((chunks, N), dtype=f, device=dev), chunks)
+    call("ocppo_relu_bias_grad_partial", _stream(dev), _check(g, "g", f, dev),
+         _opt(out, "out", f, dev, R * N), _opt(gp, "gp", f, dev, R * N), buf[0].data_ptr(), R, N)
+    return (gp if out is not None else g), buf
+
+
+def sum_splits_db(part, out, db_part, db):
+    """sum_splits(part, out) and db = db_part[0].sum(0) in chunk order, one launch
+    (db_part = the (partials, chunks) of relu_bias_grad_partial)."""
+    S = part.shape[0]
+    dev = part.device
+    f = torch.float32
+    parts, chunks = db_part
+    N = parts.shape[1]
+    n = part[0].numel()
+    call("ocppo_sum_splits_db", _stream(dev), _check(part, "part", f, dev), S, n,
+         _check(out, "out", f, dev, n), _check(parts, "db_partials", f, dev, chunks * N), chunks,
+         N, _check(db, "db", f, dev, N))
+    return out, db
 
 
 def relu_bias_wgrad_ok(g, x) -> bool:

@@ -33,7 +33,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from . import frames, ops
-from .agents import NormalizeImg, PPObj, make_agent
+from .agents import NormalizeImg, PPObj, linear_relu, make_agent
 from .args import Args
 from .envs import HostVecEnv, make_device_env
 
@@ -230,6 +230,11 @@ class PPOTrainer:
         self.noise = torch.zeros((T, N, self.A), dtype=f32, device=dev)
         self.enc_cache = (torch.zeros((N, self.obs_shape[0], self.agent.encoding_dim), dtype=f32,
                                       device=dev) if self.frame_cache else None)
+        # frame cache + fusions: the store of step t-1 rides in the launch of step t's first two
+        # encoder layers, the last encoder layer shifts the cache in its epilogue
+        self.rollout_fusion = self.frame_cache and a.rollout_fusion and self._fusable_encoder()
+        self.enc_pair = (torch.zeros((N, self.agent.network[2].out_features), dtype=f32, device=dev)
+                         if self.rollout_fusion else None)
         self.ret_state = torch.zeros(N, dtype=torch.float64, device=dev)
         self.rms_state = torch.tensor([0.0, 1.0, 1e-4], dtype=torch.float64, device=dev)
 
@@ -300,6 +305,21 @@ class PPOTrainer:
         self.last_metrics: dict = {}
         self._reset_env()
 
+    def _fusable_encoder(self) -> bool:
+        """PPObj encoder shapes the fused rollout kernels take: >= 3 Linear+ReLU layers, the first
+        two within ocppo_store_linear2's limits, f32 object frames, f32 / bf16 storage."""
+        net = self.agent.network
+        lins = [m for m in net[:self.agent._flat] if isinstance(m, nn.Linear)]
+        if len(lins) < 3 or self.pixels or self.env.frame_dtype != torch.float32 or \
+                self.obs_dtype not in (torch.float32, torch.bfloat16) or self.channels_last:
+            return False
+        acts = list(net[:self.agent._flat])
+        if not all(isinstance(acts[i], nn.ReLU) for i in range(1, len(acts), 2)):
+            return False
+        l1, l2 = lins[0], lins[1]
+        return (l1.in_features <= 64 and l1.out_features % 16 == 0 and l1.out_features <= 512
+                and l2.weight.data_ptr() % 16 == 0 and all(m.bias is not None for m in lins))
+
     # ------------------------------------------------------------------------------------------
     def _reset_env(self):
         frame = self.env.frame if self.host_env else self.env.reset()
@@ -320,11 +340,30 @@ class PPOTrainer:
             return ag.trunk(self.net_obs, self.prescale)
         if t == 0:
             self.enc_cache.copy_(ag.encode(self.net_obs))
+        elif self.rollout_fusion:
+            self._store_encode(t)
         else:
             fresh = ag.encode(self.net_obs[:, -1])
             self.timer.bracket("frame_cache", lambda: ops.frame_cache_shift(
                 self.enc_cache, fresh, self.dones[t]))
         return ag.decode(self.enc_cache)
+
+    def _store_encode(self, t: int):
+        """Store of step t-1 + encode of step t's newest frame into the cache, in 2 + (encoder
+        depth - 3) launches (ops.store_linear2, middle layers, ops.linear_cache_shift)."""
+        a, env, net = self.args, self.env, self.agent.network
+        lins = [m for m in net[:self.agent._flat] if isinstance(m, nn.Linear)]
+        vn = (self.ret_state, self.rms_state) if a.vecnorm_reward else None
+        self.timer.bracket("store_encode", lambda: ops.store_linear2(
+            env.frame, env.reward, env.done, self.obs[t - 1], self.obs[t], self.net_obs,
+            self.dones[t], self.rewards[t - 1], lins[0].weight, lins[0].bias, lins[1].weight,
+            lins[1].bias, self.enc_pair, vecnorm_state=vn))
+        x = self.enc_pair
+        for lin in lins[2:-1]:
+            x = linear_relu(x, lin)
+        last = lins[-1]
+        self.timer.bracket("cache_linear", lambda: ops.linear_cache_shift(
+            x, last.weight, last.bias, self.enc_cache, self.dones[t]))
 
     def _rollout_step(self, t: int):
         """One env step of the rollout (:500-514): network trunk (PyTorch) → fused HIP policy
@@ -332,7 +371,8 @@ class PPOTrainer:
         env → fused HIP store (+ VecNormalize) of the next obs slot and reward/done rows."""
         self._act(t)
         self.timer.bracket("env_step", lambda: self.env.step(self.actions[t], t))
-        self._store(t)
+        if not self.rollout_fusion:  # else the store rides in step t+1's encoder launch
+            self._store(t)
 
     def _act(self, t: int):
         ag = self.agent
@@ -403,7 +443,8 @@ class PPOTrainer:
                 self._rollout_begin()
             else:
                 self.env.upload()
-                self._store(k - 1)
+                if not self.rollout_fusion:
+                    self._store(k - 1)
             if k < self.T:
                 self._act(k)
                 self.env.fetch_actions(self.actions[k])

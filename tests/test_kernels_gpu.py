@@ -794,6 +794,34 @@ def test_relu_bias_grad_vs_torch(ops, dev, R, N, relu):
     assert torch.equal(db, db2) and torch.equal(gp, gp2)
 
 
+@pytest.mark.parametrize("R,N,K,S", [(12288, 512, 256, 4), (12288, 1024, 512, 8),
+                                     (12288, 512, 1024, 8), (1000, 20, 8, 2)])
+@pytest.mark.parametrize("relu", [True, False])
+def test_relu_bias_grad_deferred_db(ops, dev, R, N, K, S, relu):
+    """relu_bias_grad_partial + sum_splits_db (the bias gradient finished in the launch that
+    combines the split-K weight gradient): gp bit-identical to threshold_backward, the weight
+    gradient bit-identical to sum_splits, db to 1e-6 of sum |gp| per column."""
+    g = torch.randn(R, N, device=dev)
+    out = torch.relu(torch.randn(R, N, device=dev)) if relu else None
+    if relu:
+        out[::3, ::5] = 0.0
+    x = torch.randn(R, K, device=dev)
+    gp, dbp = ops.relu_bias_grad_partial(g, out)
+    want = torch.ops.aten.threshold_backward(g, out, 0) if relu else g
+    assert torch.equal(gp, want)
+    part = torch.bmm(gp.view(S, R // S, N).transpose(1, 2), x.view(S, R // S, K))
+    dw, db = torch.empty(N, K, device=dev), torch.empty(N, device=dev)
+    ops.sum_splits_db(part, dw, dbp, db)
+    assert torch.equal(dw, ops.sum_splits(part))
+    ref = want.double().sum(0)
+    scale = want.double().abs().sum(0).clamp_min(1e-30)
+    assert ((db.double() - ref).abs() / scale).max().item() < 1e-6
+    db2 = torch.empty_like(db)
+    ops.relu_bias_grad_partial(g, out)
+    ops.sum_splits_db(part, dw, dbp, db2)
+    assert torch.equal(db, db2)  # deterministic
+
+
 def test_relu_bias_grad_graph_replay(ops, dev):
     g = torch.randn(3000, 512, device=dev)
     out = torch.relu(torch.randn(3000, 512, device=dev))
@@ -1044,3 +1072,60 @@ def test_q_head_matches_module_autograd(dev):
     q.backward(g)
     for p, w in zip(params, want):
         torch.testing.assert_close(p.grad, w, rtol=1e-4, atol=1e-5)
+
+
+# ---------------------------------------------------------------------------------------------
+# rollout fusions (PPObj frame-cache path): bit-identical to the launches they replace
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("obs_dt,vecnorm", [("bf16", True), ("f32", False), ("bf16", False)])
+@pytest.mark.parametrize("N,F,N1,N2", [(128, 12, 256, 512), (37, 6, 64, 96)])
+def test_store_linear2_equals_store_then_linear2(ops, dev, obs_dt, vecnorm, N, F, N1, N2):
+    rng = np.random.default_rng(N + F)
+    W = 4
+    dt = STORE_DT[obs_dt]
+    frame = T(rng.integers(0, 210, (N, F)).astype(np.float32) + (0.3 if obs_dt == "f32" else 0), dev)
+    reward = T(rng.choice([-1.0, 0.0, 1.0], N).astype(np.float32), dev)
+    done = T((rng.random(N) < 0.2).astype(np.float32), dev)
+    prev = T(rng.integers(0, 210, (N, W, F)).astype(np.float32), dev).to(dt)
+    w1 = torch.randn(N1, F, device=dev) * 0.1
+    b1 = torch.randn(N1, device=dev) * 0.1
+    w2 = torch.randn(N2, N1, device=dev) * 0.05
+    b2 = torch.randn(N2, device=dev) * 0.1
+    outs = []
+    for fused in (False, True):
+        out = torch.empty_like(prev)
+        net = torch.empty(N, W, F, device=dev)
+        rew = torch.full((N,), 7.0, device=dev)
+        dn = torch.empty(N, device=dev)
+        ret = torch.linspace(-1, 1, N, dtype=torch.float64, device=dev)
+        rms = torch.tensor([0.1, 2.0, 50.0], dtype=torch.float64, device=dev)
+        y = torch.empty(N, N2 + 8, device=dev)[:, :N2]  # row stride > N2
+        vn = (ret, rms) if vecnorm else None
+        if fused:
+            ops.store_linear2(frame, reward, done, prev, out, net, dn, rew, w1, b1, w2, b2, y,
+                              vecnorm_state=vn)
+        else:
+            if vecnorm:
+                ops.rollout_store_vecnorm(frame, reward, done, prev, out, net, dn, ret, rms, rew)
+            else:
+                ops.rollout_store(frame, reward, done, prev, out, net, rew, dn)
+            y.copy_(ops.linear2_act(net[:, -1], w1, b1, w2, b2))
+        outs.append([out.float(), net, rew, dn, ret, rms, y])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("M,K,E,W", [(128, 1024, 512, 4), (50, 96, 40, 3), (128, 512, 256, 1)])
+def test_linear_cache_shift_equals_linear_then_shift(ops, dev, M, K, E, W):
+    x = torch.randn(M, K, device=dev)
+    w = torch.randn(E, K, device=dev) * K ** -0.5
+    b = torch.randn(E, device=dev)
+    enc0 = torch.randn(M, W, E, device=dev)
+    done = (torch.rand(M, device=dev) < 0.3).float()
+    a = enc0.clone()
+    fresh = ops.linear_act(x, w, b, relu=True)
+    ops.frame_cache_shift(a, fresh, done)
+    c = ops.linear_cache_shift(x, w, b, enc0.clone(), done)
+    assert torch.equal(a, c)
+    d = ops.linear_cache_shift(x, w, b, enc0.clone(), None)  # no resets: a pure shift
+    assert torch.equal(d[:, :-1], enc0[:, 1:]) and torch.equal(d[:, -1], fresh)

@@ -365,3 +365,27 @@ def test_target_kl_early_stop(dev, graphs):
     tr2 = PPOTrainer(small_args(cuda_graphs=graphs), dev)
     tr2.train_iteration()
     assert tr2.executed_mb == a.update_epochs * a.num_minibatches
+
+
+def test_rollout_fusion_matches_unfused_rollout(dev):
+    """store + first encoder layers in one launch and the cache shift in the last encoder layer's
+    epilogue: same rollout buffers (obs, rewards, dones bit for bit; the last layer runs on the HIP
+    MFMA kernel instead of hipBLASLt, so values / logprobs agree to f32 summation order)."""
+    runs = []
+    for fusion in (False, True):
+        tr, _ = run_iters(small_args(encoder_dims=(32, 64, 48, 40), decoder_dims=(64,),
+                                     rollout_fusion=fusion), 1, dev)
+        with torch.no_grad():
+            tr._rollout()  # a rollout under the same weights (after one identical update)
+        torch.cuda.synchronize()
+        assert tr.rollout_fusion == fusion
+        runs.append(tr)
+    a, b = runs
+    # sampled actions steer the synthetic env, so a rare flipped sample (logits differ ~1e-6)
+    # changes that env's later frames: compare by fraction
+    same = (a.actions == b.actions).float().mean().item()
+    assert same > 0.99, same
+    same_obs = (a.obs == b.obs).flatten(2).all(-1).float().mean().item()
+    assert same_obs > 0.99, same_obs
+    close = ((a.values - b.values).abs() <= 1e-4 + 1e-4 * a.values.abs()).float().mean().item()
+    assert close > 0.99, close

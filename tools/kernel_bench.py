@@ -25,6 +25,7 @@ sys.path.insert(0, str(ROOT))
 from oc_cleanrl_amd import ops  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0
+MFMA_F32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense f32 MFMA (= the f32 vector rate)
 
 SIZES = {
     # name: {size: params}
@@ -47,6 +48,21 @@ SIZES = {
     "relu_bias_wgrad": {"config": dict(R=12288, N=256, K=12), "scaled": dict(R=262144, N=256, K=12)},
     # actor + critic heads' backward with the decoder's ReLU mask + bias grad (M = 4096, H = 512)
     "heads_bwd": {"config": dict(M=4096, H=512, A=6), "scaled": dict(M=262144, H=512, A=6)},
+    # relu_bias_grad with its in-launch last-arriver bias-gradient tail (conv layers; the
+    # Linear layers at config run the deferred form above, ops.relu_bias_grad_partial)
+    "relu_bias_grad_tail": {"config": dict(shapes=((12288, 512), (12288, 1024), (12288, 512))),
+                            "scaled": dict(shapes=((262144, 1024),))},
+    # the rollout's last encoder layer + frame-cache shift (M = 128 envs, 1024 -> 512, W = 4)
+    "cache_linear": {"config": dict(M=128, K=1024, E=512, W=4), "scaled": dict(M=8192, K=1024, E=512, W=4)},
+    # the rollout store of step t-1 + the first two encoder layers of step t (F=12 -> 256 -> 512)
+    "store_encode": {"config": dict(N=128, W=4, F=12, N1=256, N2=512),
+                     "scaled": dict(N=8192, W=4, F=12, N1=256, N2=512)},
+}
+
+# useful flops per launch of the MFMA kernels (2 per multiply-add)
+FLOPS = {
+    "cache_linear": lambda p: 2 * p["M"] * p["K"] * p["E"],
+    "store_encode": lambda p: 2 * p["N"] * (p["F"] * p["N1"] + p["N1"] * p["N2"]),
 }
 
 
@@ -155,7 +171,7 @@ def make_case(name: str, p: dict, dev):
         vo = torch.empty(N, device=dev)
         fn = lambda: ops.policy_head_sample(hid, wa, ba, wc, bc, noise, act, lp, vo)  # noqa: E731
         return fn, N * (4 * H + 4 * A + 16) + 4 * (A + 1) * (H + 1)
-    if name == "relu_bias_grad":
+    if name in ("relu_bias_grad", "relu_bias_grad_tail"):
         bufs = []
         for R, N in p["shapes"]:
             gg = torch.randn(R, N, device=dev, generator=g)
@@ -164,8 +180,38 @@ def make_case(name: str, p: dict, dev):
 
         def fn():
             for gg, out, gp, db in bufs:
-                ops.relu_bias_grad(gg, out, db=db, gp=gp)
+                if name == "relu_bias_grad":
+                    ops.relu_bias_grad_partial(gg, out, gp=gp)
+                else:
+                    ops.relu_bias_grad(gg, out, db=db, gp=gp)
         return fn, relu_bias_grad_bytes(p["shapes"])
+    if name == "cache_linear":
+        M, K, E, W = p["M"], p["K"], p["E"], p["W"]
+        x = torch.relu(torch.randn(M, K, device=dev, generator=g))
+        w = torch.randn(E, K, device=dev, generator=g) * K ** -0.5
+        b = torch.randn(E, device=dev, generator=g)
+        enc = torch.randn(M, W, E, device=dev, generator=g)
+        done = (torch.rand(M, device=dev, generator=g) < 1 / 3500).float()
+        fn = lambda: ops.linear_cache_shift(x, w, b, enc, done)  # noqa: E731
+        return fn, 4 * (M * K + E * (K + 1)) + 4 * M * E * (2 * W - 1) + 4 * M
+    if name == "store_encode":
+        N, W, F, N1, N2 = p["N"], p["W"], p["F"], p["N1"], p["N2"]
+        frame = torch.randint(0, 210, (N, F), device=dev, generator=g).float()
+        reward = torch.zeros(N, device=dev)
+        done = (torch.rand(N, device=dev, generator=g) < 1 / 3500).float()
+        prev = torch.zeros(N, W, F, dtype=torch.bfloat16, device=dev)
+        out = torch.empty_like(prev)
+        net = torch.empty(N, W, F, device=dev)
+        dn, rw = torch.empty(N, device=dev), torch.empty(N, device=dev)
+        ret = torch.zeros(N, dtype=torch.float64, device=dev)
+        rms = torch.tensor([0.0, 1.0, 1e-4], dtype=torch.float64, device=dev)
+        w1, b1 = torch.randn(N1, F, device=dev, generator=g) * 0.1, torch.zeros(N1, device=dev)
+        w2, b2 = torch.randn(N2, N1, device=dev, generator=g) * 0.05, torch.zeros(N2, device=dev)
+        y = torch.empty(N, N2, device=dev)
+        fn = lambda: ops.store_linear2(frame, reward, done, prev, out, net, dn, rw, w1, b1, w2, b2,  # noqa: E731
+                                       y, vecnorm_state=(ret, rms))
+        store = N * ((W - 1) * F * 2 + F * 4 + W * F * 6 + 8 + 4 + 24 + 4)
+        return fn, store + 4 * (N1 * (F + 1) + N2 * (N1 + 1)) + 4 * N * N2
     if name == "heads_bwd":
         M, H, A = p["M"], p["H"], p["A"]
         hh = torch.relu(torch.randn(M, H, device=dev, generator=g))
@@ -210,8 +256,13 @@ def run_case(name, size, dev, reps=20, rounds=5) -> dict:
     launches = len(SIZES[name][size].get("shapes", (None,)))
     us, nbytes = us / launches, nbytes / launches  # per launch (average over the launch mix)
     gbs = nbytes / (us * 1e-6) / 1e9
-    return {"kernel": name, "size": size, "params": SIZES[name][size], "mean_us": round(us, 3),
-            "bytes": nbytes, "GBps": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
+    r = {"kernel": name, "size": size, "params": SIZES[name][size], "mean_us": round(us, 3),
+         "bytes": nbytes, "GBps": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
+    if name in FLOPS:
+        fl = FLOPS[name](SIZES[name][size])
+        r.update(flops=fl, TFLOPs=round(fl / (us * 1e-6) / 1e12, 2),
+                 mfma_frac=round(fl / (us * 1e-6) / 1e12 / MFMA_F32_PEAK_TFLOPS, 4))
+    return r
 
 
 def main():
