@@ -41,7 +41,8 @@ PMC_SUMMARY = ROOT / "profiles" / "r01g" / "pmc_summary.json"
 PMC_KEYS = {"action_head": "policy_head_config", "gae": "gae_config",
             "ppo_loss": "ppo_loss_prepared_config", "relu_bias_grad": "relu_bias_grad_config",
             "cache_linear": "cache_linear_config", "store_encode": "store_encode_config",
-            "heads_bwd": "heads_bwd_config", "relu_bias_wgrad": "relu_bias_wgrad_config"}
+            "heads_bwd": "heads_bwd_config", "relu_bias_wgrad": "relu_bias_wgrad_config",
+            "heads_loss": "heads_loss_config"}
 
 
 def pmc_traffic(key):
@@ -88,6 +89,10 @@ def kernel_bytes(tr) -> dict:
         kb["store_encode"] = kb["rollout_store"] + 4 * (N1 * (D + 1) + N2 * (N1 + 1)) + 4 * N * N2
         # x [N, K] + W [E, K] in; cache: W-1 slots read, W slots written, done row
         kb["cache_linear"] = 4 * (N * Kl + E * (Kl + 1)) + 4 * N * E * (2 * W - 1) + 4 * N
+    if tr.fused_heads_loss:
+        Hh, A1 = tr.H, tr.A + 1
+        kb["heads_loss"] = (M * Hh * 8 + M * 24 + 4 * A1 * (Hh + 1) + 4 * (A1 * (Hh + 1) + Hh)
+                            + 36)
     Hh = tr.agent.actor.in_features
     # heads' input h in + masked dh out [M, H]; dlogits + dv in; [Wa; Wc] in, dW + db out
     kb["heads_bwd"] = M * Hh * 8 + M * (A + 1) * 4 + 2 * (A + 1) * Hh * 4 + Hh * 4 + (A + 1) * 4

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define OCPPO_ABI_VERSION 9
+#define OCPPO_ABI_VERSION 10
 
 /* status codes */
 #define OCPPO_OK 0
@@ -469,6 +469,32 @@ OCPPO_API int ocppo_td_loss_fwd_bwd(ocppo_stream_t stream, const float* q, const
 OCPPO_API int ocppo_synth_env_step(ocppo_stream_t stream, uint64_t seed, const int64_t* step_base,
                          int64_t step_offset, const int64_t* actions, int64_t N, int64_t D, int pixel_mode,
                          void* frame_out, float* reward_out, float* done_out, float* ep_state);
+
+/* ---------------------------------------------------------------------------------------------
+ * Policy heads forward + fused PPO loss + heads backward in one pass over the decoder output
+ * (ppo_atari_oc.py:566-605 from h = relu(z) on; architectures/ppo.py:81-84):
+ *   logits = h Wa^T + ba, value = h Wc^T + bc; the loss of ocppo_ppo_loss_fwd_bwd on the prepared
+ *   (minibatch-order, contiguous) records mb_* [M] with adv_stats [2] (required when norm_adv);
+ *   c = (d loss / d logits, d loss / d value);  gp [M, H] = (h <= 0 ? 0 : c W), W = [Wa; Wc];
+ *   db_h [H] = sum_m gp (the decoder bias grad, may be NULL); dwa [A, H], dwc [H], dba [A],
+ *   dbc [1] the heads' grads; stats [9] as ocppo_ppo_loss_fwd_bwd; dlogits [M, A] / dvalue [M]
+ *   optional (both NULL or both set).
+ * H % 64 == 0, 64 <= H <= 512, 1 <= A <= 7; h, gp, Wa, Wc 16-B aligned. Two launches (rows, then
+ * the workgroups' partial records in order): deterministic; workspace =
+ * ocppo_heads_loss_workspace_bytes(M, H, A), needs no zeroing.
+ * ------------------------------------------------------------------------------------------- */
+OCPPO_API size_t ocppo_heads_loss_workspace_bytes(int64_t M, int64_t H, int64_t A);
+OCPPO_API int ocppo_heads_loss_fwd_bwd(ocppo_stream_t stream, const float* h, int64_t M, int64_t H,
+                                       const float* w_actor, const float* b_actor,
+                                       const float* w_critic, const float* b_critic, int64_t A,
+                                       const int64_t* mb_actions, const float* mb_logprobs,
+                                       const float* mb_advantages, const float* mb_returns,
+                                       const float* mb_values, const float* adv_stats,
+                                       double clip_coef, double ent_coef, double vf_coef,
+                                       int norm_adv, int clip_vloss, float* gp, float* db_h,
+                                       float* dwa, float* dwc, float* dba, float* dbc,
+                                       float* stats, float* dlogits, float* dvalue,
+                                       void* workspace, size_t workspace_bytes);
 
 /* ---------------------------------------------------------------------------------------------
  * Rollout fusions of the PPObj frame-encoding cache path (ppo_atari_oc.py:502-514 + :506 with

@@ -121,6 +121,7 @@ class Args:
                                  # cache shift in the last encoder layer's epilogue
     update_frame_dedup: bool = True  # PPO_OBJ update: encode each distinct frame of a minibatch once
     prefetch_shuffle: bool = True  # shuffle (+ frame plan) of the next iteration while the GPU runs
+    fused_heads_loss: bool = True  # update: policy heads fwd + PPO loss + heads bwd in one HIP op
     dp_overlap: bool = True  # DP: all-reduce the decoder-side gradients during the encoder backward
     dp_exchange: bool = False  # run the DP exchange path (per-minibatch graphs + all-reduce) even
                                # at world size 1, over an initialised 1-rank process group

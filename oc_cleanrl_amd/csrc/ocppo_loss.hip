@@ -1272,3 +1272,363 @@ extern "C" int ocppo_minibatch_prepare(ocppo_stream_t stream, const int64_t* per
 #undef OCPPO_PREP
   return check_launch("ocppo_minibatch_prepare");
 }
+
+namespace ocppo {
+
+// ---- policy heads forward + fused PPO loss + heads backward in ONE pass over h ---------------------
+// The minibatch update's tail (ppo_atari_oc.py:566-605 from the decoder output h = relu(z) on):
+// logits = h Wa^T + ba and value = h Wc^T + bc (architectures/ppo.py:81-84), the fused loss of
+// loss_element (its per-row gradient needs only the prepared records, the minibatch's adv
+// (mean, std) and 1/M), and the heads' whole backward with the decoder's ReLU mask:
+//   c[m] = (d loss / d logits[m, 0..A), d loss / d value[m])
+//   gp[m, j] = h[m, j] <= 0 ? 0 : sum_k c[m, k] W[k, j]        (W = [Wa; Wc], k order, fmaf)
+//   db_h[j] = sum_m gp[m, j];  dW[k, j] = sum_m c[m, k] h[m, j];  db[k] = sum_m c[m, k]
+// Row-major: one wave per row (lane = CPL = H / 64 adjacent columns), the A + 1 head dot products
+// reduced by the wave's xor butterfly (bitwise the same in every lane), the loss computed by every
+// lane alike, gp written once. Each workgroup sums its rows (waves, then LDS in wave order) into
+// ONE partial record [H (K + 1) + K + 6]; heads_loss_finish_kernel adds the records in workgroup
+// order (deterministic) and forms the loss statistics. Replaces two head GEMMs, the loss launch
+// and ocppo_heads_bwd (logits / dlogits / value / dvalue never touch HBM).
+struct HeadsLossParams {
+  LossParams L;  // records (prepared, contiguous), adv_stats, coefficients, upstream grads
+  const float* h;
+  int64_t H;
+  const float* wa;
+  const float* ba;
+  const float* wc;
+  const float* bc;
+  float* gp;
+  float* partials;  // [gridDim.x][npw]
+  int64_t npw;
+  int rows_per_wg;
+};
+
+template <int AMAX, bool EXACT, int CPL>
+__global__ __launch_bounds__(256) void heads_loss_kernel(HeadsLossParams P) {
+  constexpr int KMAX = AMAX + 1;
+  extern __shared__ __attribute__((aligned(16))) float hl_red[];  // [4 waves][64 lanes][CPL*(KMAX+1)]
+  __shared__ float s_misc[4][KMAX + kNumPartials];
+  const LossParams& L = P.L;
+  const int A = EXACT ? AMAX : L.A;
+  const int K = A + 1;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t H = P.H;
+  const int c0 = lane * CPL;
+  float w[KMAX][CPL], bk[KMAX];
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) {
+    bk[k] = k < A ? P.ba[k] : (k == A ? P.bc[0] : 0.f);
+#pragma unroll
+    for (int c = 0; c < CPL; ++c)
+      w[k][c] = k < A ? P.wa[k * H + c0 + c] : (k == A ? P.wc[c0 + c] : 0.f);
+  }
+  float sb[CPL], sw[KMAX][CPL], sc[KMAX], part[kNumPartials];
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) sb[c] = 0.f;
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) {
+    sc[k] = 0.f;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) sw[k][c] = 0.f;
+  }
+#pragma unroll
+  for (int q = 0; q < kNumPartials; ++q) part[q] = 0.f;
+  const float adv_mean = L.norm_adv ? L.adv_stats[0] : 0.f;
+  const float adv_den = L.norm_adv ? L.adv_stats[1] + 1e-8f : 1.f;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * P.rows_per_wg;
+  const int64_t r1 = r0 + P.rows_per_wg < L.M ? r0 + P.rows_per_wg : L.M;
+
+  // software pipeline: the next row's h and records are in flight while this row computes
+  float hn[CPL];
+  int64_t an = 0;
+  float lpn = 0.f, advn = 0.f, Rn = 0.f, von = 0.f;
+  auto load_row = [&](int64_t r) {
+    if (r < r1) {
+      const float* hr = P.h + r * H + c0;
+#pragma unroll
+      for (int c = 0; c < CPL; c += 4) {
+        if (CPL >= 4) {
+          const float4 v = *reinterpret_cast<const float4*>(hr + c);
+          hn[c] = v.x; hn[c + 1] = v.y; hn[c + 2] = v.z; hn[c + 3] = v.w;
+        } else {
+#pragma unroll
+          for (int q = 0; q < CPL; ++q) hn[q] = hr[q];
+        }
+      }
+      an = L.b_actions[r];
+      lpn = L.b_logprobs[r];
+      advn = L.b_adv[r];
+      Rn = L.b_ret[r];
+      von = L.b_val[r];
+    }
+  };
+  load_row(r0 + wv);
+  for (int64_t r = r0 + wv; r < r1; r += 4) {
+    float hv[CPL];
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) hv[c] = hn[c];
+    const int64_t a = an;
+    const float old_lp = lpn, adv = advn, R = Rn, v_old = von;
+    load_row(r + 4);
+    // head forward: the A + 1 dot products, lane-local in column order, then the butterfly
+    float t[KMAX];
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      float s = 0.f;
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) s = fmaf(hv[c], w[k][c], s);
+      t[k] = wave_sum(s);
+    }
+    float l[AMAX];
+#pragma unroll
+    for (int k = 0; k < AMAX; ++k) l[k] = t[k] + bk[k];
+    float vnew = 0.f;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k)
+      if (k == A) vnew = t[k] + bk[k];
+    float dl[AMAX], dv;
+    loss_element<AMAX>(L, A, l, a, old_lp, adv, R, v_old, vnew, adv_mean, adv_den, part, dl, dv);
+    if (L.dlogits != nullptr && lane == 0) {
+#pragma unroll
+      for (int k = 0; k < AMAX; ++k)
+        if (k < A) L.dlogits[r * A + k] = dl[k];
+      L.dvalue[r] = dv;
+    }
+    float cv[KMAX];
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) cv[k] = k < A ? dl[k < AMAX ? k : 0] : (k == A ? dv : 0.f);
+    float g[CPL];
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      float d = 0.f;
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k) d = fmaf(cv[k], w[k][c], d);
+      g[c] = hv[c] <= 0.f ? 0.f : d;
+      sb[c] += g[c];
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k) sw[k][c] = fmaf(cv[k], hv[c], sw[k][c]);
+    }
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) sc[k] += cv[k];
+    float* gr = P.gp + r * H + c0;
+#pragma unroll
+    for (int c = 0; c < CPL; c += 4) {
+      if (CPL >= 4)
+        *reinterpret_cast<float4*>(gr + c) = make_float4(g[c], g[c + 1], g[c + 2], g[c + 3]);
+      else
+#pragma unroll
+        for (int q = 0; q < CPL; ++q) gr[q] = g[q];
+    }
+  }
+  // workgroup combine: per lane CPL x (1 + K) values through LDS, waves in order
+  constexpr int NV = KMAX + 1;
+  float* mine = hl_red + (static_cast<int64_t>(wv) * 64 + lane) * CPL * NV;
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    mine[c * NV] = sb[c];
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) mine[c * NV + 1 + k] = sw[k][c];
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) s_misc[wv][k] = sc[k];
+#pragma unroll
+    for (int q = 0; q < kNumPartials; ++q) s_misc[wv][KMAX + q] = part[q];
+  }
+  __syncthreads();
+  float* out = P.partials + static_cast<int64_t>(blockIdx.x) * P.npw;
+  const int64_t nvals = H * (K + 1);
+  const int64_t lane_stride = static_cast<int64_t>(CPL) * NV;
+  for (int64_t q = threadIdx.x; q < nvals; q += blockDim.x) {
+    const int64_t col = q / (K + 1);
+    const int v = static_cast<int>(q - col * (K + 1));
+    const int ln = static_cast<int>(col / CPL), c = static_cast<int>(col - ln * CPL);
+    const int64_t off = ln * lane_stride + c * NV + v;
+    float s = hl_red[off];
+#pragma unroll
+    for (int wq = 1; wq < 4; ++wq) s += hl_red[wq * 64 * lane_stride + off];
+    out[q] = s;
+  }
+  if (threadIdx.x < K + kNumPartials) {
+    const int i = threadIdx.x;
+    const int slot = i < K ? i : KMAX + (i - K);
+    float s = s_misc[0][slot];
+    for (int wq = 1; wq < 4; ++wq) s += s_misc[wq][slot];
+    out[i < K ? nvals + i : P.npw - kNumPartials + (i - K)] = s;
+  }
+}
+
+// Adds the workgroups' partial records in workgroup order: 16 outputs x 16 workgroup groups per
+// block (each thread sums its group's records in order, then the 16 group sums in group order).
+// The record ends with the 6 loss partials at `ls` (a multiple of 16), so one block holds all of
+// them and forms the loss statistics (loss_finish's formulas).
+__global__ __launch_bounds__(256) void heads_loss_finish_kernel(
+    const float* __restrict__ partials, int G, int64_t npw, int64_t ls, int64_t H, int A, int K,
+    float* __restrict__ db_h, float* __restrict__ dwa, float* __restrict__ dwc,
+    float* __restrict__ dba, float* __restrict__ dbc, LossParams L) {
+  __shared__ float red[16][17];
+  __shared__ float tot[16];
+  const int o = threadIdx.x & 15, gi = threadIdx.x >> 4;
+  const int64_t idx = static_cast<int64_t>(blockIdx.x) * 16 + o;
+  const int cpg = (G + 15) / 16;
+  const int g0 = gi * cpg, g1 = g0 + cpg < G ? g0 + cpg : G;
+  float s = 0.f;
+  if (idx < npw) {
+    for (int g = g0; g < g1; g += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = g + u < g1 ? partials[(g + u) * npw + idx] : 0.f;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+  }
+  red[gi][o] = s;
+  __syncthreads();
+  const int64_t nvals = H * (K + 1);
+  if (gi == 0) {
+    float t = red[0][o];
+    for (int q = 1; q < 16; ++q) t += red[q][o];
+    tot[o] = t;
+    if (idx < nvals) {
+      const int64_t col = idx / (K + 1);
+      const int v = static_cast<int>(idx - col * (K + 1));
+      if (v == 0) {
+        if (db_h) db_h[col] = t;
+      } else if (v - 1 < A) {
+        dwa[static_cast<int64_t>(v - 1) * H + col] = t;
+      } else {
+        dwc[col] = t;
+      }
+    } else if (idx < nvals + K) {
+      const int k = static_cast<int>(idx - nvals);
+      if (k < A) dba[k] = t;
+      else dbc[0] = t;
+    }
+  }
+  __syncthreads();
+  if (static_cast<int64_t>(blockIdx.x) * 16 == ls && threadIdx.x == 0) {
+    const float pg_loss = tot[0] * L.inv_m;
+    const float v_loss = 0.5f * (tot[1] * L.inv_m);
+    const float ent = tot[2] * L.inv_m;
+    const float loss = (pg_loss - L.ent_coef * ent) + v_loss * L.vf_coef;
+    L.stats[OCPPO_STAT_LOSS] = loss;
+    L.stats[OCPPO_STAT_PG_LOSS] = pg_loss;
+    L.stats[OCPPO_STAT_V_LOSS] = v_loss;
+    L.stats[OCPPO_STAT_ENTROPY] = ent;
+    L.stats[OCPPO_STAT_OLD_APPROX_KL] = tot[3] * L.inv_m;
+    L.stats[OCPPO_STAT_APPROX_KL] = tot[4] * L.inv_m;
+    L.stats[OCPPO_STAT_CLIPFRAC] = tot[5] * L.inv_m;
+    L.stats[OCPPO_STAT_ADV_MEAN] = L.norm_adv ? L.adv_stats[0] : 0.f;
+    L.stats[OCPPO_STAT_ADV_STD] = L.norm_adv ? L.adv_stats[1] : 0.f;
+  }
+}
+
+constexpr int kHlRowsPerWg = 32;  // 8 rows per wave
+
+inline int64_t hl_layout(int64_t M, int64_t H, int64_t A, int64_t& G, int64_t& ls) {
+  const int64_t K = A + 1;
+  G = (M + kHlRowsPerWg - 1) / kHlRowsPerWg;
+  ls = (H * (K + 1) + K + 15) / 16 * 16;
+  return ls + kNumPartials;  // npw
+}
+
+template <int AMAX, bool EXACT>
+static void launch_heads_loss(hipStream_t s, const HeadsLossParams& P, int G, int cpl) {
+  const size_t lds = sizeof(float) * 4 * 64 * cpl * (AMAX + 2);
+  const dim3 g(G), b(256);
+  switch (cpl) {
+    case 1: hipLaunchKernelGGL((heads_loss_kernel<AMAX, EXACT, 1>), g, b, lds, s, P); break;
+    case 2: hipLaunchKernelGGL((heads_loss_kernel<AMAX, EXACT, 2>), g, b, lds, s, P); break;
+    case 4: hipLaunchKernelGGL((heads_loss_kernel<AMAX, EXACT, 4>), g, b, lds, s, P); break;
+    default: hipLaunchKernelGGL((heads_loss_kernel<AMAX, EXACT, 8>), g, b, lds, s, P); break;
+  }
+}
+
+}  // namespace ocppo
+
+extern "C" size_t ocppo_heads_loss_workspace_bytes(int64_t M, int64_t H, int64_t A) {
+  if (M < 1 || H < 1 || A < 1) return 0;
+  int64_t G, ls;
+  const int64_t npw = ocppo::hl_layout(M, H, A, G, ls);
+  return static_cast<size_t>(G * npw) * sizeof(float);
+}
+
+extern "C" int ocppo_heads_loss_fwd_bwd(
+    ocppo_stream_t stream, const float* h, int64_t M, int64_t H, const float* w_actor,
+    const float* b_actor, const float* w_critic, const float* b_critic, int64_t A,
+    const int64_t* mb_actions, const float* mb_logprobs, const float* mb_advantages,
+    const float* mb_returns, const float* mb_values, const float* adv_stats, double clip_coef,
+    double ent_coef, double vf_coef, int norm_adv, int clip_vloss, float* gp, float* db_h,
+    float* dwa, float* dwc, float* dba, float* dbc, float* stats, float* dlogits, float* dvalue,
+    void* workspace, size_t workspace_bytes) {
+  OCPPO_REQUIRE(M >= 1 && M <= INT32_MAX && H >= 64 && H % 64 == 0 && H <= 512 && A >= 1 &&
+                    A <= 7,
+                "ocppo_heads_loss_fwd_bwd: bad sizes M=%lld H=%lld A=%lld (H %% 64 == 0, "
+                "64 <= H <= 512, 1 <= A <= 7)", (long long)M, (long long)H, (long long)A);
+  OCPPO_REQUIRE(h && w_actor && b_actor && w_critic && b_critic && mb_actions && mb_logprobs &&
+                    mb_advantages && mb_returns && mb_values && gp && dwa && dwc && dba && dbc &&
+                    stats && (!norm_adv || adv_stats) && (!dlogits == !dvalue),
+                "ocppo_heads_loss_fwd_bwd: null pointer");
+  OCPPO_REQUIRE(aligned16(h) && aligned16(gp) && aligned16(w_actor) && aligned16(w_critic),
+                "ocppo_heads_loss_fwd_bwd: h / gp / weights must be 16-B aligned");
+  if (!workspace || workspace_bytes < ocppo_heads_loss_workspace_bytes(M, H, A))
+    return fail(OCPPO_E_WORKSPACE, "ocppo_heads_loss_fwd_bwd: workspace needs %zu bytes, got %zu",
+                ocppo_heads_loss_workspace_bytes(M, H, A), workspace_bytes);
+  int64_t G, ls;
+  const int64_t npw = hl_layout(M, H, A, G, ls);
+  HeadsLossParams P;
+  LossParams& L = P.L;
+  L.logits = nullptr;
+  L.new_value = nullptr;
+  L.mb_inds = nullptr;
+  L.b_actions = mb_actions;
+  L.b_logprobs = mb_logprobs;
+  L.b_adv = mb_advantages;
+  L.b_ret = mb_returns;
+  L.b_val = mb_values;
+  L.adv_stats = adv_stats;
+  L.dlogits = dlogits;
+  L.dvalue = dvalue;
+  L.stats = stats;
+  L.ticket = nullptr;
+  L.partials = nullptr;
+  L.gpartials = nullptr;
+  L.M = M;
+  L.A = static_cast<int>(A);
+  L.norm_adv = norm_adv ? 1 : 0;
+  L.clip_vloss = clip_vloss ? 1 : 0;
+  L.clip = static_cast<float>(clip_coef);
+  L.clip_lo = static_cast<float>(1.0 - clip_coef);
+  L.clip_hi = static_cast<float>(1.0 + clip_coef);
+  L.ent_coef = static_cast<float>(ent_coef);
+  L.vf_coef = static_cast<float>(vf_coef);
+  const float fm = static_cast<float>(M);
+  L.g_pg = 1.0f / fm;  // the upstream grads of ocppo_ppo_loss_fwd_bwd (mean() backward)
+  L.g_h = (-1.0f * L.ent_coef) / fm;
+  L.g_v = (L.vf_coef * 0.5f) / fm;
+  L.inv_m = 1.0f / fm;
+  P.h = h;
+  P.H = H;
+  P.wa = w_actor;
+  P.ba = b_actor;
+  P.wc = w_critic;
+  P.bc = b_critic;
+  P.gp = gp;
+  P.partials = static_cast<float*>(workspace);
+  P.npw = npw;
+  P.rows_per_wg = kHlRowsPerWg;
+  clear_stale_error();
+  hipStream_t s = as_stream(stream);
+  const int cpl = static_cast<int>(H / 64);
+  switch (A) {
+    case 4: launch_heads_loss<4, true>(s, P, (int)G, cpl); break;
+    case 6: launch_heads_loss<6, true>(s, P, (int)G, cpl); break;
+    default: launch_heads_loss<7, false>(s, P, (int)G, cpl); break;
+  }
+  if (int rc = check_launch("ocppo_heads_loss_fwd_bwd")) return rc;
+  const int K = static_cast<int>(A) + 1;
+  hipLaunchKernelGGL(heads_loss_finish_kernel, dim3((npw + 15) / 16), dim3(256), 0, s,
+                     static_cast<const float*>(workspace), (int)G, npw, ls, H, (int)A, K, db_h,
+                     dwa, dwc, dba, dbc, L);
+  return check_launch("ocppo_heads_loss_fwd_bwd/finish");
+}

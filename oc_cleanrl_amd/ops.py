@@ -201,6 +201,53 @@ def ppo_loss_fwd_bwd(logits, new_value, b_actions, b_logprobs, b_advantages, b_r
     return stats, dlogits, dvalue
 
 
+_HL_WS: dict = {}
+
+
+def heads_loss_ok(h, A: int) -> bool:
+    H = h.shape[-1]
+    return (h.is_cuda and h.dtype == torch.float32 and h.dim() == 2 and h.is_contiguous() and
+            H % 64 == 0 and 64 <= H <= 512 and 1 <= A <= 7 and h.data_ptr() % 16 == 0)
+
+
+def heads_loss_fwd_bwd(h, wa, ba, wc, bc, mb_actions, mb_logprobs, mb_advantages, mb_returns,
+                       mb_values, *, adv_stats, clip_coef, ent_coef, vf_coef, norm_adv: bool,
+                       clip_vloss: bool, gp=None, db_h=None, dwa=None, dwc=None, dba=None,
+                       dbc=None, stats=None, dlogits=None, dvalue=None):
+    """The policy heads' forward, the fused PPO loss and the heads' backward with the decoder's
+    ReLU mask, from the decoder output h [M, H] (include/ocppo.h ocppo_heads_loss_fwd_bwd).
+    mb_* are the minibatch's prepared records [M]. Returns (gp, db_h, dwa, dwc, dba, dbc, stats)."""
+    M, H = h.shape
+    A = wa.shape[0]
+    dev = h.device
+    f = torch.float32
+    gp = torch.empty_like(h) if gp is None else gp
+    dwa = torch.empty(A, H, dtype=f, device=dev) if dwa is None else dwa
+    dwc = torch.empty(1, H, dtype=f, device=dev) if dwc is None else dwc
+    dba = torch.empty(A, dtype=f, device=dev) if dba is None else dba
+    dbc = torch.empty(1, dtype=f, device=dev) if dbc is None else dbc
+    stats = torch.empty(len(STAT_NAMES), dtype=f, device=dev) if stats is None else stats
+    key = (dev, M, H, A)
+    ws = _HL_WS.get(key)
+    if ws is None:
+        nb = int(_lib.LIB.ocppo_heads_loss_workspace_bytes(M, H, A))
+        ws = _HL_WS[key] = torch.zeros(nb // 4, dtype=f, device=dev)
+    call("ocppo_heads_loss_fwd_bwd", _stream(dev), _check(h, "h", f, dev, M * H), M, H,
+         _check(wa, "wa", f, dev, A * H), _check(ba, "ba", f, dev, A), _check(wc, "wc", f, dev, H),
+         _check(bc, "bc", f, dev, 1), A, _check(mb_actions, "mb_actions", torch.int64, dev, M),
+         _check(mb_logprobs, "mb_logprobs", f, dev, M),
+         _check(mb_advantages, "mb_advantages", f, dev, M),
+         _check(mb_returns, "mb_returns", f, dev, M), _check(mb_values, "mb_values", f, dev, M),
+         _opt(adv_stats, "adv_stats", f, dev, 2) if norm_adv else None, float(clip_coef),
+         float(ent_coef), float(vf_coef), int(bool(norm_adv)), int(bool(clip_vloss)),
+         _check(gp, "gp", f, dev, M * H), _opt(db_h, "db_h", f, dev, H),
+         _check(dwa, "dwa", f, dev, A * H), _check(dwc, "dwc", f, dev, H),
+         _check(dba, "dba", f, dev, A), _check(dbc, "dbc", f, dev, 1),
+         _check(stats, "stats", f, dev, len(STAT_NAMES)), _opt(dlogits, "dlogits", f, dev, M * A),
+         _opt(dvalue, "dvalue", f, dev, M), ws.data_ptr(), ws.numel() * 4)
+    return gp, db_h, dwa, dwc, dba, dbc, stats
+
+
 class _PPOLoss(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, new_value, b_actions, b_logprobs, b_advantages, b_returns, b_values,

@@ -284,6 +284,12 @@ class PPOTrainer:
         self.dvalue = torch.zeros(self.M, dtype=f32, device=dev)
         self.stats = torch.zeros((self.E * self.nmb, len(ops.STAT_NAMES)), dtype=f32, device=dev)
         self.loss_ws = ops.LossWorkspace(self.M, self.A, dev)
+        # heads forward + loss + heads backward fused on the decoder output (needs the in-place
+        # grads of FlatAdam and the decoder's ReLU box; see _fused_tail)
+        self.fused_heads_loss = (a.fused_heads_loss and self.direct_grads and self.fused_head and
+                                 self.H % 64 == 0 and 64 <= self.H <= 512 and self.A <= 7)
+        self.gp_tail = (torch.empty((self.M, self.H), dtype=f32, device=dev)
+                        if self.fused_heads_loss else None)
         self.b_obs = self.obs[:T].view((T * N,) + self.obs_shape)
 
         # The update of the NatureCNN agent runs eagerly: capturing its MIOpen convolution
@@ -474,11 +480,16 @@ class PPOTrainer:
                                              idx, k, split=self.split)
             if self.split:
                 hidden, self.cuts[j] = hidden
+            if self._fused_tail(j, hidden):
+                return
             logits, value = ag.heads(hidden)
         else:
             self.timer.bracket("gather", lambda: ops.gather_rows(self.b_obs, idx, self.mb_obs,
                                                                  scale255=self.prescale))
-            logits, value = ag.logits_and_value(self.mb_obs, self.prescale)
+            hidden = ag.trunk(self.mb_obs, self.prescale)
+            if self._fused_tail(j, hidden):
+                return
+            logits, value = ag.heads(hidden)
         lg, vv = logits.detach(), value.detach().view(-1)  # the timer's closure must not hold
         sl = slice(j * self.M, (j + 1) * self.M)
         mb = self.mb
@@ -492,6 +503,30 @@ class PPOTrainer:
         if not self.direct_grads:
             self.grad_buf.zero_()
         torch.autograd.backward([logits, value], [self.dlogits, self.dvalue.view(-1, 1)])
+
+    def _fused_tail(self, j: int, hidden) -> bool:
+        """Heads forward + fused loss + heads backward (with the decoder's ReLU mask and bias grad)
+        as ONE HIP op on the decoder output (ops.heads_loss_fwd_bwd), then autograd from the
+        decoder down. Taken when the head / decoder grads are written in place (FlatAdam)."""
+        if hidden is None or not self.fused_heads_loss:
+            return False
+        box = getattr(hidden, "_ocppo_box", None)
+        if box is None or not ops.heads_loss_ok(hidden, self.A):
+            return False
+        a, ag, mb = self.args, self.agent, self.mb
+        sl = slice(j * self.M, (j + 1) * self.M)
+        box["premasked"] = True  # the decoder's _LinearAct backward gets gp with its mask applied
+        h = hidden.detach()
+        self.timer.bracket("heads_loss", lambda: ops.heads_loss_fwd_bwd(
+            h, ag.actor.weight, ag.actor.bias, ag.critic.weight, ag.critic.bias,
+            mb["actions"][sl], mb["logprobs"][sl], mb["advantages"][sl], mb["returns"][sl],
+            mb["values"][sl], adv_stats=mb["adv_stats"][j] if a.norm_adv else None,
+            clip_coef=a.clip_coef, ent_coef=a.ent_coef, vf_coef=a.vf_coef, norm_adv=a.norm_adv,
+            clip_vloss=a.clip_vloss, gp=self.gp_tail, db_h=box["bias"].grad,
+            dwa=ag.actor.weight.grad, dwc=ag.critic.weight.grad, dba=ag.actor.bias.grad,
+            dbc=ag.critic.bias.grad, stats=self.stats[j]))
+        torch.autograd.backward(hidden, self.gp_tail)
+        return True
 
     def _backward_low(self, j: int):
         """Second backward phase of a split minibatch: the encoder layers below the cut."""

@@ -252,7 +252,8 @@ def gen_td(name, B, A, seed):
                         q_values=ns["old_val"].mean().item(), dq=q.grad.numpy())
 
 
-def gen_update(B=512, M=256, F=6, A=6, seed=21, pixels=False, name="update_2mb"):
+def gen_update(B=512, M=256, F=6, A=6, seed=21, pixels=False, name="update_2mb", enc=(32, 64),
+               dec=(32,)):
     """Two minibatch updates (one epoch of 2 minibatches) through the reference's update block,
     with its Adam (lr 2.5e-4, eps 1e-5) and clip_grad_norm_(0.5): the whole learner step.
     pixels: the NatureCNN (PPODefault) on u8-valued 4x84x84 stacks instead of a small PPObj."""
@@ -262,7 +263,7 @@ def gen_update(B=512, M=256, F=6, A=6, seed=21, pixels=False, name="update_2mb")
         agent = PPODefault(Envs((4, 84, 84), A), "cpu")
         b_obs = torch.from_numpy(rng.integers(0, 256, (B, 4, 84, 84)).astype(np.float32))
     else:
-        agent = PPObj(Envs((4, F), A), "cpu", (32, 64), (32,))
+        agent = PPObj(Envs((4, F), A), "cpu", enc, dec)
         b_obs = torch.from_numpy(rng.integers(0, 160, (B, 4, F)).astype(np.float32))
     with torch.no_grad():
         hid = agent.network(b_obs)
@@ -460,6 +461,8 @@ def main():
     gen_update(B=32, M=16, A=4, seed=22, pixels=True, name="update_2mb_cnn")
     gen_update_cartpole()
     gen_replay()
+    # decoder width 64: the fused heads + loss + heads-backward kernel's shapes (H % 64 == 0)
+    gen_update(seed=24, name="update_2mb_h64", enc=(32, 64), dec=(64,))
     gen_init("ppobj_f12_a6", lambda e: PPObj(e, "cpu", (256, 512, 1024, 512), (512,)), (4, 12), 6,
              1, 160.0)
     gen_init("ppodefault_a4", lambda e: PPODefault(e, "cpu"), (4, 84, 84), 4, 1, 255.0)

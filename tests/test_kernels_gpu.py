@@ -1129,3 +1129,49 @@ def test_linear_cache_shift_equals_linear_then_shift(ops, dev, M, K, E, W):
     assert torch.equal(a, c)
     d = ops.linear_cache_shift(x, w, b, enc0.clone(), None)  # no resets: a pure shift
     assert torch.equal(d[:, :-1], enc0[:, 1:]) and torch.equal(d[:, -1], fresh)
+
+
+# ---------------------------------------------------------------------------------------------
+# policy heads forward + fused PPO loss + heads backward in one pass (ocppo_heads_loss_fwd_bwd)
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("M,H,A", [(4096, 512, 6), (1000, 256, 4), (77, 64, 7), (300, 128, 3)])
+@pytest.mark.parametrize("norm_adv,clip_vloss", [(True, True), (False, False)])
+def test_heads_loss_equals_heads_then_loss_then_heads_bwd(ops, dev, M, H, A, norm_adv, clip_vloss):
+    g = torch.Generator(device=dev).manual_seed(M + H)
+    h = torch.relu(torch.randn(M, H, device=dev, generator=g))
+    h[::7, ::3] = 0.0
+    wa = torch.randn(A, H, device=dev, generator=g) * 0.05
+    ba = torch.randn(A, device=dev, generator=g) * 0.1
+    wc = torch.randn(1, H, device=dev, generator=g) * 0.05
+    bc = torch.randn(1, device=dev, generator=g)
+    logits = torch.addmm(ba, h, wa.t())
+    value = torch.addmm(bc, h, wc.t()).view(-1)
+    acts = torch.randint(0, A, (M,), device=dev, generator=g)
+    with torch.no_grad():
+        lp_now = torch.log_softmax(logits, -1).gather(1, acts.view(-1, 1)).view(-1)
+    old_lp = lp_now + 0.2 * torch.randn(M, device=dev, generator=g)
+    old_lp[: M // 5] = lp_now[: M // 5]  # ratio 1: max() ties
+    adv = 2.0 * torch.randn(M, device=dev, generator=g)
+    ret = value + torch.randn(M, device=dev, generator=g)
+    val = value + 0.3 * torch.randn(M, device=dev, generator=g)
+    st = ops.minibatch_adv_stats(adv, torch.arange(M, device=dev), M)[0]
+    cfg = dict(clip_coef=0.1, ent_coef=0.01, vf_coef=0.5, norm_adv=norm_adv, clip_vloss=clip_vloss)
+    s_ref, dl_ref, dv_ref = ops.ppo_loss_fwd_bwd(logits, value, acts, old_lp, adv, ret, val,
+                                                 adv_stats=st if norm_adv else None, **cfg)
+    gp_ref, dbh_ref, dwa_ref, dwc_ref, dba_ref, dbc_ref = ops.heads_bwd(
+        h, dl_ref, dv_ref, wa, wc.reshape(-1), relu=True, db_h=torch.empty(H, device=dev))
+    dl, dv = torch.empty(M, A, device=dev), torch.empty(M, device=dev)
+    gp, dbh, dwa, dwc, dba, dbc, stats = ops.heads_loss_fwd_bwd(
+        h, wa, ba, wc, bc, acts, old_lp, adv, ret, val, adv_stats=st if norm_adv else None,
+        db_h=torch.empty(H, device=dev), dlogits=dl, dvalue=dv, **cfg)
+    # the head dot products run in another order than the GEMM: f32 rounding differences only
+    torch.testing.assert_close(stats, s_ref, rtol=2e-5, atol=1e-7)
+    scale = lambda t: float(t.abs().max()) + 1e-30  # noqa: E731
+    for got, ref in ((dl, dl_ref), (dv, dv_ref), (gp, gp_ref), (dbh, dbh_ref), (dwa, dwa_ref),
+                     (dwc.view(-1), dwc_ref.view(-1)), (dba, dba_ref), (dbc, dbc_ref)):
+        assert float((got - ref).abs().max()) <= 2e-5 * scale(ref), (got, ref)
+    again = ops.heads_loss_fwd_bwd(h, wa, ba, wc, bc, acts, old_lp, adv, ret, val,
+                                   adv_stats=st if norm_adv else None,
+                                   db_h=torch.empty(H, device=dev), **cfg)
+    for x, y in zip((gp, dbh, dwa, dwc, dba, dbc, stats), again):
+        assert torch.equal(x, y)  # deterministic

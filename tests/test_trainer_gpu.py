@@ -389,3 +389,58 @@ def test_rollout_fusion_matches_unfused_rollout(dev):
     assert same_obs > 0.99, same_obs
     close = ((a.values - b.values).abs() <= 1e-4 + 1e-4 * a.values.abs()).float().mean().item()
     assert close > 0.99, close
+
+
+def test_fused_heads_loss_updates_match_reference_golden(dev):
+    """The update tail as ONE HIP op (heads forward + PPO loss + heads backward with the decoder's
+    ReLU mask): two minibatch updates against the reference's own update block
+    (ppo_atari_oc.py:566-610 exec'd on a PPObj with a 64-wide decoder, update_2mb_h64.npz)."""
+    from conftest import golden
+    from oc_cleanrl_amd import ops
+    from oc_cleanrl_amd.agents import make_agent
+
+    z = golden("update_2mb_h64.npz")
+    ag = make_agent("PPO_OBJ", (4, 6), 6, dev, (32, 64), (64,)).to(dev)
+    sd = lambda i: {k.split("::", 1)[1]: torch.from_numpy(z[k]) for k in z  # noqa: E731
+                    if k.startswith(f"sd{i}::")}
+    ag.load_state_dict(sd(0))
+    opt = ops.FlatAdam(ag.parameters(), lr=2.5e-4, eps=1e-5, max_grad_norm=0.5)
+    T = lambda k: torch.from_numpy(z[k]).to(dev)  # noqa: E731
+    b_obs, acts = T("b_obs"), T("b_actions")
+    lp, adv, ret, val = T("b_logprobs"), T("b_advantages"), T("b_returns"), T("b_values")
+    perm, M = T("perm"), int(z["M"])
+    for i, start in enumerate((0, M)):
+        idx = perm[start:start + M].contiguous()
+        hidden = ag.trunk(ops.gather_rows(b_obs, idx))
+        box = hidden._ocppo_box
+        box["premasked"] = True
+        gp, *_ = ops.heads_loss_fwd_bwd(
+            hidden.detach(), ag.actor.weight, ag.actor.bias, ag.critic.weight, ag.critic.bias,
+            acts[idx], lp[idx], adv[idx], ret[idx], val[idx],
+            adv_stats=ops.minibatch_adv_stats(adv, idx, M)[0], clip_coef=0.1, ent_coef=0.01,
+            vf_coef=0.5, norm_adv=True, clip_vloss=True, db_h=box["bias"].grad,
+            dwa=ag.actor.weight.grad, dwc=ag.critic.weight.grad, dba=ag.actor.bias.grad,
+            dbc=ag.critic.bias.grad)
+        torch.autograd.backward(hidden, gp)
+        gn = float(torch.linalg.vector_norm(opt.grads.double()))
+        assert abs(gn - z["grad_norms"][i]) <= 1e-5 * z["grad_norms"][i]
+        opt.step()
+        for k, ref in sd(i + 1).items():
+            got = ag.state_dict()[k].cpu()
+            torch.testing.assert_close(got, ref, rtol=0, atol=0.01 * 2.5e-4)
+            assert float(((got - ref).abs() > 2e-7).float().mean()) < 0.01
+
+
+def test_fused_heads_loss_trainer_matches_unfused(dev):
+    """Trainer with and without the fused update tail: same minibatch stats and parameters up to
+    f32 reduction order after two iterations (64-wide decoder)."""
+    runs = []
+    for fused in (False, True):
+        tr, ms = run_iters(small_args(decoder_dims=(64,), fused_heads_loss=fused), 2, dev)
+        assert tr.fused_heads_loss == fused
+        runs.append((tr, ms))
+    (a, ma), (b, mb) = runs
+    for k in ("losses/value_loss", "losses/policy_loss", "losses/entropy", "losses/approx_kl"):
+        assert ma[0][k] == pytest.approx(mb[0][k], rel=1e-4, abs=1e-6), k
+    for p, q in zip(a.agent.parameters(), b.agent.parameters()):
+        torch.testing.assert_close(p, q, rtol=1e-3, atol=2e-5)

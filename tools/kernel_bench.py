@@ -48,6 +48,8 @@ SIZES = {
     "relu_bias_wgrad": {"config": dict(R=12288, N=256, K=12), "scaled": dict(R=262144, N=256, K=12)},
     # actor + critic heads' backward with the decoder's ReLU mask + bias grad (M = 4096, H = 512)
     "heads_bwd": {"config": dict(M=4096, H=512, A=6), "scaled": dict(M=262144, H=512, A=6)},
+    # policy heads forward + fused PPO loss + heads backward (both launches: rows, then records)
+    "heads_loss": {"config": dict(M=4096, H=512, A=6), "scaled": dict(M=262144, H=512, A=6)},
     # relu_bias_grad with its in-launch last-arriver bias-gradient tail (conv layers; the
     # Linear layers at config run the deferred form above, ops.relu_bias_grad_partial)
     "relu_bias_grad_tail": {"config": dict(shapes=((12288, 512), (12288, 1024), (12288, 512))),
@@ -185,6 +187,23 @@ def make_case(name: str, p: dict, dev):
                 else:
                     ops.relu_bias_grad(gg, out, db=db, gp=gp)
         return fn, relu_bias_grad_bytes(p["shapes"])
+    if name == "heads_loss":
+        M, H, A = p["M"], p["H"], p["A"]
+        hh = torch.relu(torch.randn(M, H, device=dev, generator=g))
+        wa, ba = torch.randn(A, H, device=dev, generator=g) * 0.05, torch.zeros(A, device=dev)
+        wc, bc = torch.randn(1, H, device=dev, generator=g) * 0.05, torch.zeros(1, device=dev)
+        acts = torch.randint(0, A, (M,), device=dev, generator=g)
+        lp, adv, ret, val = (torch.randn(M, device=dev, generator=g) for _ in range(4))
+        st = torch.tensor([0.0, 1.0], device=dev)
+        gp, dbh = torch.empty_like(hh), torch.empty(H, device=dev)
+        dwa, dwc = torch.empty(A, H, device=dev), torch.empty(1, H, device=dev)
+        dba, dbc, stats = torch.empty(A, device=dev), torch.empty(1, device=dev), torch.empty(9, device=dev)
+        fn = lambda: ops.heads_loss_fwd_bwd(  # noqa: E731
+            hh, wa, ba, wc, bc, acts, lp, adv, ret, val, adv_stats=st, clip_coef=0.1,
+            ent_coef=0.01, vf_coef=0.5, norm_adv=True, clip_vloss=True, gp=gp, db_h=dbh, dwa=dwa,
+            dwc=dwc, dba=dba, dbc=dbc, stats=stats)
+        # h in + gp out; records (action 8 + 4 x 4) in; [Wa; Wc] + biases in; head grads out
+        return fn, M * H * 8 + M * 24 + 4 * (A + 1) * (H + 1) + 4 * ((A + 1) * (H + 1) + H) + 36
     if name == "cache_linear":
         M, K, E, W = p["M"], p["K"], p["E"], p["W"]
         x = torch.relu(torch.randn(M, K, device=dev, generator=g))
