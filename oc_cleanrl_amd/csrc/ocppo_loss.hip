@@ -16,6 +16,7 @@
 // (logits 4A + value 4 + index 8 + action 8 + old logprob/adv/return/value 16 in; dlogits 4A + dv 4
 // out). At the configs (M = 4096) one launch moves 344 KB and is launch/latency bound.
 #include <cfloat>
+#include <cstdlib>
 
 #include "ocppo_common.h"
 
@@ -1303,33 +1304,106 @@ struct HeadsLossParams {
   int rows_per_wg;
 };
 
+// Lane layout of a row: CPL columns per lane, interleaved so that every load of the wave is one
+// contiguous run: CPL >= 4 -> float4 chunk q4 at columns 4 (q4 * 64 + lane) .. +3 (the policy
+// head's layout); CPL < 4 -> column q * 64 + lane.
+template <int CPL>
+__device__ __forceinline__ int hl_col(int lane, int q) {
+  return CPL >= 4 ? 4 * ((q >> 2) * kWave + lane) + (q & 3) : q * kWave + lane;
+}
+
+template <int CPL>
+__device__ __forceinline__ void hl_load(const float* __restrict__ row, int lane, float (&x)[CPL]) {
+  if (CPL >= 4) {
+    const float4* r4 = reinterpret_cast<const float4*>(row);
+#pragma unroll
+    for (int q4 = 0; q4 < CPL / 4; ++q4) {
+      const float4 v = r4[q4 * kWave + lane];
+      x[4 * q4] = v.x; x[4 * q4 + 1] = v.y; x[4 * q4 + 2] = v.z; x[4 * q4 + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < CPL; ++q) x[q] = row[q * kWave + lane];
+  }
+}
+
+template <int CPL>
+__device__ __forceinline__ void hl_store(float* __restrict__ row, int lane, const float (&x)[CPL]) {
+  if (CPL >= 4) {
+    float4* r4 = reinterpret_cast<float4*>(row);
+#pragma unroll
+    for (int q4 = 0; q4 < CPL / 4; ++q4)
+      r4[q4 * kWave + lane] = make_float4(x[4 * q4], x[4 * q4 + 1], x[4 * q4 + 2], x[4 * q4 + 3]);
+  } else {
+#pragma unroll
+    for (int q = 0; q < CPL; ++q) row[q * kWave + lane] = x[q];
+  }
+}
+
+// The 8 (A logits + value, zero-padded) dot products of one row, reduce-scattered (xor 32 / 16 / 8
+// halve the values each lane carries, xor 4 / 2 / 1 finish one value per 8-lane group: 10
+// cross-lane steps instead of 48) and broadcast: out[j] = lane 8j's sum, wave-uniform.
+template <int CPL>
+__device__ __forceinline__ void hl_dots(const float (&x)[CPL], const float (&w)[8][CPL], int lane,
+                                        float (&out)[8]) {
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < CPL; ++q) s = fmaf(x[q], w[j][q], s);
+    acc[j] = s;
+  }
+  const bool b5 = lane & 32, b4 = lane & 16, b3 = lane & 8;
+  float s4[4], s2[2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float send = b5 ? acc[i] : acc[i + 4];
+    s4[i] = (b5 ? acc[i + 4] : acc[i]) + __shfl_xor(send, 32);
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const float send = b4 ? s4[i] : s4[i + 2];
+    s2[i] = (b4 ? s4[i + 2] : s4[i]) + __shfl_xor(send, 16);
+  }
+  float t = (b3 ? s2[1] : s2[0]) + __shfl_xor(b3 ? s2[0] : s2[1], 8);
+  t += __shfl_xor(t, 4);
+  t += __shfl_xor(t, 2);
+  t += __shfl_xor(t, 1);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) out[j] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t), 8 * j));
+}
+
+// Two rows per wave step: the rows' dependent chains (dots, loss, backward) are independent, so
+// the compiler interleaves them.
 template <int AMAX, bool EXACT, int CPL>
 __global__ __launch_bounds__(256) void heads_loss_kernel(HeadsLossParams P) {
-  constexpr int KMAX = AMAX + 1;
-  extern __shared__ __attribute__((aligned(16))) float hl_red[];  // [4 waves][64 lanes][CPL*(KMAX+1)]
-  __shared__ float s_misc[4][KMAX + kNumPartials];
+  static_assert(AMAX <= 7, "A logits + the value in 8 lanes-groups");
+  constexpr int NV = 9;  // per column: db_h, then dW rows 0..7 (j < A: actor, 7: critic)
+  extern __shared__ __attribute__((aligned(16))) float hl_red[];  // [4][64][CPL * NV]
+  __shared__ float s_misc[4][8 + kNumPartials];
   const LossParams& L = P.L;
   const int A = EXACT ? AMAX : L.A;
-  const int K = A + 1;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t H = P.H;
-  const int c0 = lane * CPL;
-  float w[KMAX][CPL], bk[KMAX];
+  float w[8][CPL], bk[8];
 #pragma unroll
-  for (int k = 0; k < KMAX; ++k) {
-    bk[k] = k < A ? P.ba[k] : (k == A ? P.bc[0] : 0.f);
+  for (int j = 0; j < 8; ++j) {
+    bk[j] = j < A ? P.ba[j] : (j == 7 ? P.bc[0] : 0.f);
+    const float* wr = j == 7 ? P.wc : P.wa + static_cast<int64_t>(j < A ? j : 0) * H;
+    float t[CPL];
+    hl_load<CPL>(wr, lane, t);
 #pragma unroll
-    for (int c = 0; c < CPL; ++c)
-      w[k][c] = k < A ? P.wa[k * H + c0 + c] : (k == A ? P.wc[c0 + c] : 0.f);
+    for (int q = 0; q < CPL; ++q) w[j][q] = (j < A || j == 7) ? t[q] : 0.f;
   }
-  float sb[CPL], sw[KMAX][CPL], sc[KMAX], part[kNumPartials];
+  float sb[CPL], sw[8][CPL], sc[8], part[kNumPartials];
 #pragma unroll
-  for (int c = 0; c < CPL; ++c) sb[c] = 0.f;
+  for (int q = 0; q < CPL; ++q) sb[q] = 0.f;
 #pragma unroll
-  for (int k = 0; k < KMAX; ++k) {
-    sc[k] = 0.f;
+  for (int j = 0; j < 8; ++j) {
+    sc[j] = 0.f;
 #pragma unroll
-    for (int c = 0; c < CPL; ++c) sw[k][c] = 0.f;
+    for (int q = 0; q < CPL; ++q) sw[j][q] = 0.f;
   }
 #pragma unroll
   for (int q = 0; q < kNumPartials; ++q) part[q] = 0.f;
@@ -1338,123 +1412,96 @@ __global__ __launch_bounds__(256) void heads_loss_kernel(HeadsLossParams P) {
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * P.rows_per_wg;
   const int64_t r1 = r0 + P.rows_per_wg < L.M ? r0 + P.rows_per_wg : L.M;
 
-  // software pipeline: the next row's h and records are in flight while this row computes
-  float hn[CPL];
-  int64_t an = 0;
-  float lpn = 0.f, advn = 0.f, Rn = 0.f, von = 0.f;
-  auto load_row = [&](int64_t r) {
-    if (r < r1) {
-      const float* hr = P.h + r * H + c0;
+  for (int64_t rb = r0 + wv; rb < r1; rb += 8) {
+    float x[2][CPL], t[2][8];
+    bool ok[2];
+    int64_t a[2];
+    float old_lp[2], adv[2], R[2], v_old[2];
 #pragma unroll
-      for (int c = 0; c < CPL; c += 4) {
-        if (CPL >= 4) {
-          const float4 v = *reinterpret_cast<const float4*>(hr + c);
-          hn[c] = v.x; hn[c + 1] = v.y; hn[c + 2] = v.z; hn[c + 3] = v.w;
-        } else {
+    for (int u = 0; u < 2; ++u) {
+      const int64_t r = rb + 4 * u;
+      ok[u] = r < r1;
+      const int64_t rr = ok[u] ? r : rb;
+      hl_load<CPL>(P.h + rr * H, lane, x[u]);
+      a[u] = L.b_actions[rr];
+      old_lp[u] = L.b_logprobs[rr];
+      adv[u] = L.b_adv[rr];
+      R[u] = L.b_ret[rr];
+      v_old[u] = L.b_val[rr];
+    }
 #pragma unroll
-          for (int q = 0; q < CPL; ++q) hn[q] = hr[q];
-        }
+    for (int u = 0; u < 2; ++u) hl_dots<CPL>(x[u], w, lane, t[u]);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int64_t r = rb + 4 * u;
+      float l[AMAX];
+#pragma unroll
+      for (int k = 0; k < AMAX; ++k) l[k] = t[u][k] + bk[k];
+      const float vnew = t[u][7] + bk[7];
+      float dl[AMAX], dv;
+      float pr[kNumPartials] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      loss_element<AMAX>(L, A, l, a[u], old_lp[u], adv[u], R[u], v_old[u], vnew, adv_mean,
+                         adv_den, pr, dl, dv);
+      if (!ok[u]) continue;  // wave-uniform
+#pragma unroll
+      for (int q = 0; q < kNumPartials; ++q) part[q] += pr[q];
+      if (L.dlogits != nullptr && lane == 0) {
+#pragma unroll
+        for (int k = 0; k < AMAX; ++k)
+          if (k < A) L.dlogits[r * A + k] = dl[k];
+        L.dvalue[r] = dv;
       }
-      an = L.b_actions[r];
-      lpn = L.b_logprobs[r];
-      advn = L.b_adv[r];
-      Rn = L.b_ret[r];
-      von = L.b_val[r];
-    }
-  };
-  load_row(r0 + wv);
-  for (int64_t r = r0 + wv; r < r1; r += 4) {
-    float hv[CPL];
+      float cv[8];
 #pragma unroll
-    for (int c = 0; c < CPL; ++c) hv[c] = hn[c];
-    const int64_t a = an;
-    const float old_lp = lpn, adv = advn, R = Rn, v_old = von;
-    load_row(r + 4);
-    // head forward: the A + 1 dot products, lane-local in column order, then the butterfly
-    float t[KMAX];
+      for (int k = 0; k < 8; ++k) cv[k] = k < A ? dl[k < AMAX ? k : 0] : (k == 7 ? dv : 0.f);
+      float g[CPL];
 #pragma unroll
-    for (int k = 0; k < KMAX; ++k) {
-      float s = 0.f;
+      for (int q = 0; q < CPL; ++q) {
+        float d = 0.f;
 #pragma unroll
-      for (int c = 0; c < CPL; ++c) s = fmaf(hv[c], w[k][c], s);
-      t[k] = wave_sum(s);
-    }
-    float l[AMAX];
+        for (int k = 0; k < 8; ++k) d = fmaf(cv[k], w[k][q], d);
+        g[q] = x[u][q] <= 0.f ? 0.f : d;
+        sb[q] += g[q];
 #pragma unroll
-    for (int k = 0; k < AMAX; ++k) l[k] = t[k] + bk[k];
-    float vnew = 0.f;
+        for (int k = 0; k < 8; ++k) sw[k][q] = fmaf(cv[k], x[u][q], sw[k][q]);
+      }
 #pragma unroll
-    for (int k = 0; k < KMAX; ++k)
-      if (k == A) vnew = t[k] + bk[k];
-    float dl[AMAX], dv;
-    loss_element<AMAX>(L, A, l, a, old_lp, adv, R, v_old, vnew, adv_mean, adv_den, part, dl, dv);
-    if (L.dlogits != nullptr && lane == 0) {
-#pragma unroll
-      for (int k = 0; k < AMAX; ++k)
-        if (k < A) L.dlogits[r * A + k] = dl[k];
-      L.dvalue[r] = dv;
-    }
-    float cv[KMAX];
-#pragma unroll
-    for (int k = 0; k < KMAX; ++k) cv[k] = k < A ? dl[k < AMAX ? k : 0] : (k == A ? dv : 0.f);
-    float g[CPL];
-#pragma unroll
-    for (int c = 0; c < CPL; ++c) {
-      float d = 0.f;
-#pragma unroll
-      for (int k = 0; k < KMAX; ++k) d = fmaf(cv[k], w[k][c], d);
-      g[c] = hv[c] <= 0.f ? 0.f : d;
-      sb[c] += g[c];
-#pragma unroll
-      for (int k = 0; k < KMAX; ++k) sw[k][c] = fmaf(cv[k], hv[c], sw[k][c]);
-    }
-#pragma unroll
-    for (int k = 0; k < KMAX; ++k) sc[k] += cv[k];
-    float* gr = P.gp + r * H + c0;
-#pragma unroll
-    for (int c = 0; c < CPL; c += 4) {
-      if (CPL >= 4)
-        *reinterpret_cast<float4*>(gr + c) = make_float4(g[c], g[c + 1], g[c + 2], g[c + 3]);
-      else
-#pragma unroll
-        for (int q = 0; q < CPL; ++q) gr[q] = g[q];
+      for (int k = 0; k < 8; ++k) sc[k] += cv[k];
+      hl_store<CPL>(P.gp + r * H, lane, g);
     }
   }
-  // workgroup combine: per lane CPL x (1 + K) values through LDS, waves in order
-  constexpr int NV = KMAX + 1;
+  // workgroup combine: per lane CPL x NV values through LDS, waves in order
   float* mine = hl_red + (static_cast<int64_t>(wv) * 64 + lane) * CPL * NV;
 #pragma unroll
-  for (int c = 0; c < CPL; ++c) {
-    mine[c * NV] = sb[c];
+  for (int q = 0; q < CPL; ++q) {
+    mine[q * NV] = sb[q];
 #pragma unroll
-    for (int k = 0; k < KMAX; ++k) mine[c * NV + 1 + k] = sw[k][c];
+    for (int k = 0; k < 8; ++k) mine[q * NV + 1 + k] = sw[k][q];
   }
   if (lane == 0) {
 #pragma unroll
-    for (int k = 0; k < KMAX; ++k) s_misc[wv][k] = sc[k];
+    for (int k = 0; k < 8; ++k) s_misc[wv][k] = sc[k];
 #pragma unroll
-    for (int q = 0; q < kNumPartials; ++q) s_misc[wv][KMAX + q] = part[q];
+    for (int q = 0; q < kNumPartials; ++q) s_misc[wv][8 + q] = part[q];
   }
   __syncthreads();
+  // record layout = the wave's LDS layout [lane][q][slot] (64 * CPL * 9 values: slot 0 db_h,
+  // 1..7 actor rows, 8 critic), then 8 head-bias sums (7 = critic), then the 6 loss partials at
+  // npw - 6: the waves are added in order with contiguous LDS reads and coalesced stores
   float* out = P.partials + static_cast<int64_t>(blockIdx.x) * P.npw;
-  const int64_t nvals = H * (K + 1);
-  const int64_t lane_stride = static_cast<int64_t>(CPL) * NV;
-  for (int64_t q = threadIdx.x; q < nvals; q += blockDim.x) {
-    const int64_t col = q / (K + 1);
-    const int v = static_cast<int>(q - col * (K + 1));
-    const int ln = static_cast<int>(col / CPL), c = static_cast<int>(col - ln * CPL);
-    const int64_t off = ln * lane_stride + c * NV + v;
-    float s = hl_red[off];
+  constexpr int nvals = 64 * CPL * NV;
+  constexpr int wstride = 64 * CPL * NV;
+  for (int i = threadIdx.x; i < nvals; i += 256) {
+    float sacc = hl_red[i];
 #pragma unroll
-    for (int wq = 1; wq < 4; ++wq) s += hl_red[wq * 64 * lane_stride + off];
-    out[q] = s;
+    for (int wq = 1; wq < 4; ++wq) sacc += hl_red[wq * wstride + i];
+    out[i] = sacc;
   }
-  if (threadIdx.x < K + kNumPartials) {
+  if (threadIdx.x < 8 + kNumPartials) {
     const int i = threadIdx.x;
-    const int slot = i < K ? i : KMAX + (i - K);
-    float s = s_misc[0][slot];
-    for (int wq = 1; wq < 4; ++wq) s += s_misc[wq][slot];
-    out[i < K ? nvals + i : P.npw - kNumPartials + (i - K)] = s;
+    float sacc = s_misc[0][i];
+    for (int wq = 1; wq < 4; ++wq) sacc += s_misc[wq][i];
+    out[i < 8 ? nvals + i : P.npw - kNumPartials + (i - 8)] = sacc;
   }
 }
 
@@ -1463,7 +1510,7 @@ __global__ __launch_bounds__(256) void heads_loss_kernel(HeadsLossParams P) {
 // The record ends with the 6 loss partials at `ls` (a multiple of 16), so one block holds all of
 // them and forms the loss statistics (loss_finish's formulas).
 __global__ __launch_bounds__(256) void heads_loss_finish_kernel(
-    const float* __restrict__ partials, int G, int64_t npw, int64_t ls, int64_t H, int A, int K,
+    const float* __restrict__ partials, int G, int64_t npw, int64_t ls, int64_t H, int A, int cpl,
     float* __restrict__ db_h, float* __restrict__ dwa, float* __restrict__ dwc,
     float* __restrict__ dba, float* __restrict__ dbc, LossParams L) {
   __shared__ float red[16][17];
@@ -1484,25 +1531,27 @@ __global__ __launch_bounds__(256) void heads_loss_finish_kernel(
   }
   red[gi][o] = s;
   __syncthreads();
-  const int64_t nvals = H * (K + 1);
+  const int64_t nvals = 64 * cpl * 9;
   if (gi == 0) {
     float t = red[0][o];
     for (int q = 1; q < 16; ++q) t += red[q][o];
     tot[o] = t;
-    if (idx < nvals) {
-      const int64_t col = idx / (K + 1);
-      const int v = static_cast<int>(idx - col * (K + 1));
-      if (v == 0) {
+    if (idx < nvals) {  // [lane][q][slot] -> column of hl_col
+      const int slot = static_cast<int>(idx % 9);
+      const int lq = static_cast<int>(idx / 9);
+      const int ln = lq / cpl, q = lq - ln * cpl;
+      const int64_t col = cpl >= 4 ? 4 * ((q >> 2) * kWave + ln) + (q & 3) : q * kWave + ln;
+      if (slot == 0) {
         if (db_h) db_h[col] = t;
-      } else if (v - 1 < A) {
-        dwa[static_cast<int64_t>(v - 1) * H + col] = t;
-      } else {
+      } else if (slot == 8) {
         dwc[col] = t;
+      } else if (slot - 1 < A) {
+        dwa[static_cast<int64_t>(slot - 1) * H + col] = t;
       }
-    } else if (idx < nvals + K) {
+    } else if (idx < nvals + 8) {
       const int k = static_cast<int>(idx - nvals);
       if (k < A) dba[k] = t;
-      else dbc[0] = t;
+      else if (k == 7) dbc[0] = t;
     }
   }
   __syncthreads();
@@ -1523,18 +1572,27 @@ __global__ __launch_bounds__(256) void heads_loss_finish_kernel(
   }
 }
 
-constexpr int kHlRowsPerWg = 32;  // 8 rows per wave
+// rows per workgroup (4 waves): OCPPO_HL_ROWS overrides it for experiments (tools/)
+inline int hl_rows_per_wg() {
+  static const int r = [] {
+    const char* e = getenv("OCPPO_HL_ROWS");
+    const int v = e ? atoi(e) : 16;
+    return v >= 4 && v <= 256 ? v : 16;
+  }();
+  return r;
+}
 
 inline int64_t hl_layout(int64_t M, int64_t H, int64_t A, int64_t& G, int64_t& ls) {
-  const int64_t K = A + 1;
-  G = (M + kHlRowsPerWg - 1) / kHlRowsPerWg;
-  ls = (H * (K + 1) + K + 15) / 16 * 16;
+  (void)A;
+  const int rows = hl_rows_per_wg();
+  G = (M + rows - 1) / rows;
+  ls = (H * 9 + 8 + 15) / 16 * 16;  // 64 lanes x (H / 64) columns x 9 slots, 8 bias sums
   return ls + kNumPartials;  // npw
 }
 
 template <int AMAX, bool EXACT>
 static void launch_heads_loss(hipStream_t s, const HeadsLossParams& P, int G, int cpl) {
-  const size_t lds = sizeof(float) * 4 * 64 * cpl * (AMAX + 2);
+  const size_t lds = sizeof(float) * 4 * 64 * cpl * 9;
   const dim3 g(G), b(256);
   switch (cpl) {
     case 1: hipLaunchKernelGGL((heads_loss_kernel<AMAX, EXACT, 1>), g, b, lds, s, P); break;
@@ -1616,7 +1674,7 @@ extern "C" int ocppo_heads_loss_fwd_bwd(
   P.gp = gp;
   P.partials = static_cast<float*>(workspace);
   P.npw = npw;
-  P.rows_per_wg = kHlRowsPerWg;
+  P.rows_per_wg = hl_rows_per_wg();
   clear_stale_error();
   hipStream_t s = as_stream(stream);
   const int cpl = static_cast<int>(H / 64);
@@ -1626,9 +1684,8 @@ extern "C" int ocppo_heads_loss_fwd_bwd(
     default: launch_heads_loss<7, false>(s, P, (int)G, cpl); break;
   }
   if (int rc = check_launch("ocppo_heads_loss_fwd_bwd")) return rc;
-  const int K = static_cast<int>(A) + 1;
   hipLaunchKernelGGL(heads_loss_finish_kernel, dim3((npw + 15) / 16), dim3(256), 0, s,
-                     static_cast<const float*>(workspace), (int)G, npw, ls, H, (int)A, K, db_h,
+                     static_cast<const float*>(workspace), (int)G, npw, ls, H, (int)A, cpl, db_h,
                      dwa, dwc, dba, dbc, L);
   return check_launch("ocppo_heads_loss_fwd_bwd/finish");
 }
