@@ -330,6 +330,11 @@ def main():
                        "obs_storage": str(tr.obs_dtype).replace("torch.", ""),
                        "cuda_graphs": args.cuda_graphs,
                        "torch_deterministic": args.torch_deterministic,
+                       **({"deviation": "torch_deterministic=False (reference default True): "
+                           "MIOpen's deterministic convolution algorithms are naive kernels on "
+                           "gfx950, 83x slower (1875 vs 22.5 ms per iteration at 16 envs, "
+                           "profiles/r02/c3_capture.log); this package's own HIP kernels are "
+                           "deterministic either way"} if opt.config == 3 else {}),
                        "parallelism": f"dp{world}"},
             "updates_per_sec": round(updates / dt, 2),
             "roofline": roofline,

@@ -292,11 +292,11 @@ class PPOTrainer:
                         if self.fused_heads_loss else None)
         self.b_obs = self.obs[:T].view((T * N,) + self.obs_shape)
 
-        # The update of the NatureCNN agent runs eagerly: capturing its MIOpen convolution
-        # backward at Atari minibatch sizes (8192 x 4 x 84 x 84) segfaults inside hipGraph
-        # capture_end on ROCm 7.0 / torch 2.10 (its kernels are large enough that launch overhead
-        # is noise anyway); the rollout is still captured.
-        self.graph_update = a.cuda_graphs and not self.pixels
+        # Every update is captured, the NatureCNN's MIOpen convolutions included (round 1 ran that
+        # one eagerly after a capture_end crash that no longer reproduces: tools/exp_c3_capture.py
+        # captures and replays it at 16 and 256 envs, deterministic or not, NHWC or NCHW,
+        # profiles/r02/c3_capture.log)
+        self.graph_update = a.cuda_graphs
         self.timer = KernelTimer(kernel_timing)
         if kernel_timing:
             ops.TIMER = self.timer  # launch sites inside autograd (relu_bias_grad, frames_*)

@@ -45,6 +45,23 @@ def test_pixel_natureccn_iteration(dev):
     assert tr.channels_last and tr.net_obs.is_contiguous(memory_format=torch.channels_last)
 
 
+def test_pixel_update_graph_replay_matches_eager(dev):
+    """The NatureCNN update captured into hipGraphs (MIOpen convolutions inside the capture)
+    computes what the eager update computes: same rollout, parameters to conv-algorithm order."""
+    runs = []
+    for graphs in (False, True):
+        args = small_args(env_id="ALE/Breakout-v5", obs_mode="dqn", architecture="PPO",
+                          num_envs=8, num_steps=8, update_epochs=1, torch_deterministic=False,
+                          cuda_graphs=graphs)
+        tr, ms = run_iters(args, 2, dev)  # iteration 2: the update captured and replayed
+        assert tr.graphs_ready == graphs and (len(tr.g_update) > 0) == graphs
+        runs.append(tr)
+    a, b = runs
+    assert torch.equal(a.obs, b.obs) and torch.equal(a.actions, b.actions)
+    for p, q in zip(a.agent.parameters(), b.agent.parameters()):
+        torch.testing.assert_close(p, q, rtol=1e-4, atol=1e-5)
+
+
 def test_pixel_channels_last_matches_nchw(dev):
     """The NHWC NatureCNN path (channels_last agent, NHWC store/gather) computes the same network
     as the plain NCHW one: same initial weights and network input, same logits up to the conv
