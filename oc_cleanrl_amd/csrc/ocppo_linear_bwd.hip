@@ -481,150 +481,165 @@ inline int wg_chunks(int64_t R, int64_t N) {
   return static_cast<int>(c < 1 ? 1 : c);
 }
 
-template <bool RELU, int KP>
-__global__ __launch_bounds__(256) void relu_bias_wgrad_kernel(
-    const float* __restrict__ g, const float* __restrict__ out, const float* __restrict__ x,
-    int64_t ldx, float* __restrict__ dw, float* __restrict__ db, int64_t R, int64_t N, int K,
-    int chunks, unsigned* __restrict__ tickets, float* __restrict__ partials) {
-  constexpr int L = kWgL, RP = 64 / L, SW = 4 * L, NV = KP + 1;
-  __shared__ float red[4 * RP][SW][NV + 1];  // [wave * RP + row-lane][column][value], padded
-  __shared__ int s_last;
-  const int nstripes = static_cast<int>((N + SW - 1) / SW);
-  const int stripe = blockIdx.x % nstripes;
-  const int chunk = blockIdx.x / nstripes;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int lrow = lane / L, lcol = lane - lrow * L;
-  const int64_t c0 = static_cast<int64_t>(stripe) * SW + 4 * lcol;
-  const bool live = c0 < N;
-  const int64_t rows_per = (R + chunks - 1) / chunks;
-  const int64_t r0 = chunk * rows_per;
-  const int64_t r1 = r0 + rows_per < R ? r0 + rows_per : R;
-  const int64_t step = 4 * RP;
-  const int NK = K + 1;  // values per column in the partials (layout of the workspace)
+// Row-major form (round 2): a workgroup owns a range of rows x 256 columns (lane = 4 adjacent
+// columns, 16-B loads; the 4 waves take every 4th row), so every row of x is read once per
+// column group, by scalar loads (the row index is wave-uniform): x is no longer re-read by 8
+// column stripes. Each lane keeps 4 columns x (K + 1) running sums (fmaf, rows in order); the
+// waves are combined through LDS in wave order into ONE record per workgroup, and a second small
+// launch adds the records in workgroup order (16 outputs x 16 workgroup groups per block): no
+// ticket, no last-arriver tail, deterministic.
+constexpr int kWrRowsPerWg = 64;  // 8 rows per wave: 192 workgroups at R = 12288
+constexpr int kWrCols = 256;       // columns per workgroup (64 lanes x 4)
+constexpr int kWrWaves = 8;        // 2 waves per SIMD: enough loads in flight per CU
+constexpr int kWrU = 8;            // rows in flight per wave
 
+template <bool RELU, int KP>
+__global__ __launch_bounds__(64 * kWrWaves) void relu_bias_wgrad_rows_kernel(
+    const float* __restrict__ g, const float* __restrict__ out, const float* __restrict__ x,
+    int64_t ldx, int64_t R, int64_t N, int K, float* __restrict__ partials) {
+  constexpr int NV = KP + 1;
+  extern __shared__ __attribute__((aligned(16))) float wr_red[];  // [waves][256][NV]
+  __shared__ float xs[kWrRowsPerWg][KP];                           // this chunk's rows of x
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int cg = blockIdx.y;
+  const int64_t c0 = static_cast<int64_t>(cg) * kWrCols + 4 * lane;
+  const bool live = c0 < N;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * kWrRowsPerWg;
+  const int64_t r1 = r0 + kWrRowsPerWg < R ? r0 + kWrRowsPerWg : R;
+  // x rows of the chunk -> LDS once (each row read once per column group)
+  for (int i = threadIdx.x; i < kWrRowsPerWg * KP; i += 64 * kWrWaves) {
+    const int rr = i / KP, k = i - rr * KP;
+    xs[rr][k] = (r0 + rr < r1 && k < K) ? x[(r0 + rr) * ldx + k] : 0.f;
+  }
   float sb[4] = {0.f, 0.f, 0.f, 0.f};
   float sw[4][KP];
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
     for (int k = 0; k < KP; ++k) sw[j][k] = 0.f;
-  if (live) {
-    // U rows in flight per lane: every load of a batch is issued before its FMAs
-    constexpr int U = 3;
-    for (int64_t rb = r0 + wv * RP + lrow; rb < r1; rb += U * step) {
-      float4 a[U];
-      float xv[U][KP];
+  __syncthreads();
+  for (int64_t rb = r0 + wv; rb < r1; rb += kWrWaves * kWrU) {
+    float4 a[kWrU];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int64_t r = rb + u * step;
-        const bool ok = r < r1;
-        const int64_t rr = ok ? r : r0;
-        a[u] = *reinterpret_cast<const float4*>(g + rr * N + c0);
-        if (RELU || !ok) {
-          const float4 o = RELU ? *reinterpret_cast<const float4*>(out + rr * N + c0)
-                                : make_float4(1.f, 1.f, 1.f, 1.f);
-          a[u].x = (!ok || o.x <= 0.f) ? 0.f : a[u].x; a[u].y = (!ok || o.y <= 0.f) ? 0.f : a[u].y;
-          a[u].z = (!ok || o.z <= 0.f) ? 0.f : a[u].z; a[u].w = (!ok || o.w <= 0.f) ? 0.f : a[u].w;
-        }
+    for (int u = 0; u < kWrU; ++u) {
+      const int64_t r = rb + kWrWaves * u;
+      const bool ok = r < r1 && live;
+      a[u] = ok ? *reinterpret_cast<const float4*>(g + r * N + c0) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if (RELU) {
 #pragma unroll
-        for (int k = 0; k < KP; ++k) xv[u][k] = k < K ? x[rr * ldx + k] : 0.f;
+      for (int u = 0; u < kWrU; ++u) {
+        const int64_t r = rb + kWrWaves * u;
+        const float4 o = (r < r1 && live) ? *reinterpret_cast<const float4*>(out + r * N + c0)
+                                          : make_float4(0.f, 0.f, 0.f, 0.f);
+        a[u].x = o.x <= 0.f ? 0.f : a[u].x; a[u].y = o.y <= 0.f ? 0.f : a[u].y;
+        a[u].z = o.z <= 0.f ? 0.f : a[u].z; a[u].w = o.w <= 0.f ? 0.f : a[u].w;
       }
+    }
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const float av[4] = {a[u].x, a[u].y, a[u].z, a[u].w};
+    for (int u = 0; u < kWrU; ++u) {
+      const int64_t r = rb + kWrWaves * u;
+      if (r >= r1) break;  // wave-uniform; rows past the chunk carry zeros anyway
+      const float* xr = xs[r - r0];
+      const float av[4] = {a[u].x, a[u].y, a[u].z, a[u].w};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          sb[j] += av[j];
+      for (int j = 0; j < 4; ++j) {
+        sb[j] += av[j];
 #pragma unroll
-          for (int k = 0; k < KP; ++k) sw[j][k] = fmaf(av[j], xv[u][k], sw[j][k]);
-        }
+        for (int k = 0; k < KP; ++k) sw[j][k] = fmaf(av[j], xr[k], sw[j][k]);
       }
     }
   }
+  float* mine = wr_red + (static_cast<int64_t>(wv) * kWrCols + 4 * lane) * NV;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    red[wv * RP + lrow][4 * lcol + j][0] = sb[j];
+    mine[j * NV] = sb[j];
 #pragma unroll
-    for (int k = 0; k < KP; ++k) red[wv * RP + lrow][4 * lcol + j][1 + k] = sw[j][k];
+    for (int k = 0; k < KP; ++k) mine[j * NV + 1 + k] = sw[j][k];
   }
   __syncthreads();
-  // value (column j, v) of the stripe: waves in order, row-lanes in order
-  for (int q = threadIdx.x; q < SW * NV; q += 256) {
-    const int j = q / NV, v = q - j * NV;
-    const int64_t col = static_cast<int64_t>(stripe) * SW + j;
-    if (col < N && (v == 0 || v - 1 < K)) {
-      float s = 0.f;
-      for (int w = 0; w < 4 * RP; ++w) s += red[w][j][v];
-      __hip_atomic_store(&partials[(static_cast<int64_t>(chunk) * N + col) * NK + v], s,
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  constexpr int nrec = kWrCols * NV;
+  float* rec = partials + (static_cast<int64_t>(blockIdx.x) * gridDim.y + cg) * nrec;
+  for (int i = threadIdx.x; i < nrec; i += 64 * kWrWaves) {
+    float t = wr_red[i];
+#pragma unroll
+    for (int q = 1; q < kWrWaves; ++q) t += wr_red[q * nrec + i];
+    rec[i] = t;
+  }
+}
+
+// Adds the workgroup records in order; output o = (column group, column, value).
+// 8 outputs x 32 workgroup groups per block: every thread's loads are one batch in flight.
+__global__ __launch_bounds__(256) void relu_bias_wgrad_finish_kernel(
+    const float* __restrict__ partials, int G, int64_t npw, int NV, int64_t N, int K,
+    float* __restrict__ dw, float* __restrict__ db) {
+  __shared__ float red[32][9];
+  const int o = threadIdx.x & 7, gi = threadIdx.x >> 3;
+  const int64_t idx = static_cast<int64_t>(blockIdx.x) * 8 + o;
+  const int cpg = (G + 31) / 32;
+  const int g0 = gi * cpg, g1 = g0 + cpg < G ? g0 + cpg : G;
+  float s = 0.f;
+  if (idx < npw) {
+    for (int gg = g0; gg < g1; gg += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = gg + u < g1 ? partials[(gg + u) * npw + idx] : 0.f;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  red[gi][o] = s;
   __syncthreads();
-  unsigned* ticket = tickets + stripe * 32;
-  if (threadIdx.x == 0) {
-    const unsigned prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-    s_last = prev == static_cast<unsigned>(chunks - 1);
-  }
-  __syncthreads();
-  if (!s_last) return;
-  // last arriver: every (column, value) of the stripe summed over the chunks in chunk order
-  for (int q = threadIdx.x; q < SW * NV; q += 256) {
-    const int j = q / NV, v = q - j * NV;
-    const int64_t col = static_cast<int64_t>(stripe) * SW + j;
-    if (col >= N || (v > 0 && v - 1 >= K)) continue;
-    float s = 0.f;
-    for (int c = 0; c < chunks; c += 32) {  // <= 32 chunks per stripe at N >= 256: one batch
-      float t[32];
-#pragma unroll
-      for (int u = 0; u < 32; ++u)
-        t[u] = c + u < chunks
-                   ? __hip_atomic_load(&partials[(static_cast<int64_t>(c + u) * N + col) * NK + v],
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                   : 0.f;
-#pragma unroll
-      for (int u = 0; u < 32; ++u) s += t[u];
-    }
-    if (v == 0)
-      db[col] = s;
-    else
-      dw[col * K + (v - 1)] = s;
-  }
-  if (threadIdx.x == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (gi != 0 || idx >= npw) return;
+  float t = red[0][o];
+  for (int q = 1; q < 32; ++q) t += red[q][o];
+  const int64_t per = static_cast<int64_t>(kWrCols) * NV;
+  const int64_t cgi = idx / per, rem = idx - cgi * per;
+  const int64_t col = cgi * kWrCols + rem / NV;
+  const int v = static_cast<int>(rem % NV);
+  if (col >= N) return;
+  if (v == 0) db[col] = t;
+  else if (v - 1 < K) dw[col * K + (v - 1)] = t;
 }
 
 template <bool RELU>
-static void launch_wgrad(hipStream_t s, int K, dim3 grid, const float* g, const float* out,
-                         const float* x, int64_t ldx, float* dw, float* db, int64_t R, int64_t N,
-                         int chunks, unsigned* tickets, float* partials) {
-  if (K <= 4)
-    hipLaunchKernelGGL((relu_bias_wgrad_kernel<RELU, 4>), grid, dim3(256), 0, s, g, out, x, ldx,
-                       dw, db, R, N, K, chunks, tickets, partials);
-  else if (K <= 8)
-    hipLaunchKernelGGL((relu_bias_wgrad_kernel<RELU, 8>), grid, dim3(256), 0, s, g, out, x, ldx,
-                       dw, db, R, N, K, chunks, tickets, partials);
-  else if (K <= 12)
-    hipLaunchKernelGGL((relu_bias_wgrad_kernel<RELU, 12>), grid, dim3(256), 0, s, g, out, x, ldx,
-                       dw, db, R, N, K, chunks, tickets, partials);
+static void launch_wgrad_rows(hipStream_t s, int K, const float* g, const float* out,
+                              const float* x, int64_t ldx, float* dw, float* db, int64_t R,
+                              int64_t N, float* partials) {
+  const int G = static_cast<int>((R + kWrRowsPerWg - 1) / kWrRowsPerWg);
+  const int ncg = static_cast<int>((N + kWrCols - 1) / kWrCols);
+  const dim3 grid(G, ncg), block(64 * kWrWaves);
+  int KP = K <= 4 ? 4 : K <= 8 ? 8 : K <= 12 ? 12 : 16;
+  const size_t lds = sizeof(float) * kWrWaves * kWrCols * (KP + 1);
+  if (KP == 4)
+    hipLaunchKernelGGL((relu_bias_wgrad_rows_kernel<RELU, 4>), grid, block, lds, s, g, out, x, ldx, R, N, K, partials);
+  else if (KP == 8)
+    hipLaunchKernelGGL((relu_bias_wgrad_rows_kernel<RELU, 8>), grid, block, lds, s, g, out, x, ldx, R, N, K, partials);
+  else if (KP == 12)
+    hipLaunchKernelGGL((relu_bias_wgrad_rows_kernel<RELU, 12>), grid, block, lds, s, g, out, x, ldx, R, N, K, partials);
   else
-    hipLaunchKernelGGL((relu_bias_wgrad_kernel<RELU, 16>), grid, dim3(256), 0, s, g, out, x, ldx,
-                       dw, db, R, N, K, chunks, tickets, partials);
+    hipLaunchKernelGGL((relu_bias_wgrad_rows_kernel<RELU, 16>), grid, block, lds, s, g, out, x, ldx, R, N, K, partials);
+  const int64_t npw = static_cast<int64_t>(ncg) * kWrCols * (KP + 1);
+  hipLaunchKernelGGL(relu_bias_wgrad_finish_kernel, dim3((npw + 7) / 8), dim3(256), 0, s,
+                     partials, G, npw, KP + 1, N, K, dw, db);
 }
+
+inline int wg_kp(int64_t K) { return K <= 4 ? 4 : K <= 8 ? 8 : K <= 12 ? 12 : 16; }
 
 }  // namespace ocppo
 
 extern "C" size_t ocppo_relu_bias_wgrad_workspace_bytes(int64_t R, int64_t N, int64_t K) {
-  if (R < 1 || N < 1 || K < 1) return kWgTicketBytes;
-  return kWgTicketBytes + static_cast<size_t>(wg_chunks(R, N)) * N * (K + 1) * sizeof(float);
+  if (R < 1 || N < 1 || K < 1) return 256;
+  const int64_t G = (R + ocppo::kWrRowsPerWg - 1) / ocppo::kWrRowsPerWg;
+  const int64_t ncg = (N + ocppo::kWrCols - 1) / ocppo::kWrCols;
+  return static_cast<size_t>(G * ncg * ocppo::kWrCols * (ocppo::wg_kp(K) + 1)) * sizeof(float);
 }
 
 extern "C" int ocppo_relu_bias_wgrad(ocppo_stream_t stream, const float* g, const float* out,
                                      const float* x, int64_t ldx, float* dw, float* db, int64_t R,
                                      int64_t N, int64_t K, void* workspace,
                                      size_t workspace_bytes) {
-  OCPPO_REQUIRE(R >= 0 && N >= 4 && N % 4 == 0 && N <= kWgMaxStripes * 4 * kWgL && K >= 1 &&
-                    K <= 16 && ldx >= K,
+  OCPPO_REQUIRE(R >= 0 && N >= 4 && N % 4 == 0 && N <= 16384 && K >= 1 && K <= 16 && ldx >= K,
                 "ocppo_relu_bias_wgrad: bad sizes R=%lld N=%lld K=%lld ldx=%lld (N %% 4 == 0, "
                 "N <= 16384, 1 <= K <= 16, ldx >= K)", (long long)R, (long long)N, (long long)K,
                 (long long)ldx);
@@ -639,20 +654,16 @@ extern "C" int ocppo_relu_bias_wgrad(ocppo_stream_t stream, const float* g, cons
   OCPPO_REQUIRE(g && x, "ocppo_relu_bias_wgrad: null pointer");
   OCPPO_REQUIRE(reinterpret_cast<uintptr_t>(g) % 16 == 0 &&
                     (!out || reinterpret_cast<uintptr_t>(out) % 16 == 0) &&
-                    reinterpret_cast<uintptr_t>(workspace) % 256 == 0,
-                "ocppo_relu_bias_wgrad: g/out must be 16-B aligned, workspace 256-B aligned");
+                    reinterpret_cast<uintptr_t>(workspace) % 16 == 0,
+                "ocppo_relu_bias_wgrad: g/out/workspace must be 16-B aligned");
   OCPPO_REQUIRE(workspace_bytes >= ocppo_relu_bias_wgrad_workspace_bytes(R, N, K),
                 "ocppo_relu_bias_wgrad: workspace too small (%zu < %zu)", workspace_bytes,
                 ocppo_relu_bias_wgrad_workspace_bytes(R, N, K));
-  const int chunks = wg_chunks(R, N);
-  const int64_t stripes = (N + 4 * kWgL - 1) / (4 * kWgL);
-  unsigned* tickets = static_cast<unsigned*>(workspace);
-  float* partials = reinterpret_cast<float*>(static_cast<char*>(workspace) + kWgTicketBytes);
-  const dim3 grid(static_cast<unsigned>(stripes * chunks));
+  float* partials = static_cast<float*>(workspace);
   if (out)
-    launch_wgrad<true>(s, (int)K, grid, g, out, x, ldx, dw, db, R, N, chunks, tickets, partials);
+    launch_wgrad_rows<true>(s, (int)K, g, out, x, ldx, dw, db, R, N, partials);
   else
-    launch_wgrad<false>(s, (int)K, grid, g, out, x, ldx, dw, db, R, N, chunks, tickets, partials);
+    launch_wgrad_rows<false>(s, (int)K, g, out, x, ldx, dw, db, R, N, partials);
   return check_launch("ocppo_relu_bias_wgrad");
 }
 
