@@ -121,6 +121,8 @@ class Args:
                                  # cache shift in the last encoder layer's epilogue
     update_frame_dedup: bool = True  # PPO_OBJ update: encode each distinct frame of a minibatch once
     prefetch_shuffle: bool = True  # shuffle (+ frame plan) of the next iteration while the GPU runs
+    per_step_noise: bool = False  # rollout sampling noise drawn per step ([N, A], the reference's
+                                  # generator stream) instead of once per rollout ([T, N, A])
     fused_heads_loss: bool = True  # update: policy heads fwd + PPO loss + heads bwd in one HIP op
     dp_overlap: bool = True  # DP: all-reduce the decoder-side gradients during the encoder backward
     dp_exchange: bool = False  # run the DP exchange path (per-minibatch graphs + all-reduce) even

@@ -31,10 +31,22 @@ __global__ __launch_bounds__(kOptThreads) void grad_norm_kernel(
   float acc = 0.f;
   const int64_t P4 = P / 4;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kOptThreads;
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kOptThreads + threadIdx.x; i < P4; i += stride) {
-    const float4 x = reinterpret_cast<const float4*>(g)[i];
-    const float a = x.x * grad_scale, b = x.y * grad_scale, c = x.z * grad_scale, d = x.w * grad_scale;
-    acc += a * a + b * b + c * c + d * d;
+  // kNormU grid-strided float4 loads in flight per thread, then accumulated in index order
+  constexpr int kNormU = 8;
+  for (int64_t i0 = static_cast<int64_t>(blockIdx.x) * kOptThreads + threadIdx.x; i0 < P4;
+       i0 += kNormU * stride) {
+    float4 x[kNormU];
+#pragma unroll
+    for (int u = 0; u < kNormU; ++u) {
+      const int64_t i = i0 + u * stride;
+      x[u] = i < P4 ? reinterpret_cast<const float4*>(g)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < kNormU; ++u) {
+      const float a = x[u].x * grad_scale, b = x[u].y * grad_scale, c = x[u].z * grad_scale,
+                  d = x[u].w * grad_scale;
+      acc += a * a + b * b + c * c + d * d;
+    }
   }
   if (blockIdx.x == 0)
     for (int64_t i = 4 * P4 + threadIdx.x; i < P; i += kOptThreads) {

@@ -289,9 +289,56 @@ int launch_gather(hipStream_t s, const void* src, const int64_t* idx, int64_t M,
   return check_launch("ocppo_gather_rows");
 }
 
+// The pixel case (u8 stacks of C = 4 frames, NatureCNN input): a workgroup owns 1024 pixels of
+// one row. Load phase: thread t reads pixels [4t, 4t+4) of each frame plane (one dword, 256 B per
+// wave instruction) into LDS; store phase: thread t writes pixel j = t + 256 i as ONE float4
+// (its 4 channels), so consecutive lanes write consecutive 16 B: every wave store instruction is
+// a contiguous 1 KB run (the direct form's lanes wrote 16 B pieces 64 B apart).
+constexpr int kClTile = 1024;  // pixels per workgroup
+
+__global__ __launch_bounds__(256) void gather_rows_cl4_u8_kernel(const uint8_t* __restrict__ src,
+                                                                 const int64_t* __restrict__ idx,
+                                                                 int64_t M, int64_t P,
+                                                                 float* __restrict__ dst,
+                                                                 float scale, int tiles) {
+  __shared__ uint32_t s[4][kClTile / 4];
+  const int64_t i = blockIdx.x / tiles;
+  const int tile = blockIdx.x - static_cast<int>(i * tiles);
+  const int64_t p0 = static_cast<int64_t>(tile) * kClTile;
+  const int64_t row = idx[i];
+  const uint8_t* sr = src + row * 4 * P;
+  const int t = threadIdx.x;
+  const int64_t pl = p0 + 4 * t;
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+    s[c][t] = pl + 3 < P ? *reinterpret_cast<const uint32_t*>(sr + c * P + pl) : 0u;
+  __syncthreads();
+  float* out = dst + (i * P + p0) * 4;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int j = t + 256 * k;
+    if (p0 + j < P) {
+      const int w = j >> 2, sh = 8 * (j & 3);
+      const float4 v = make_float4(static_cast<float>((s[0][w] >> sh) & 0xFFu) * scale,
+                                   static_cast<float>((s[1][w] >> sh) & 0xFFu) * scale,
+                                   static_cast<float>((s[2][w] >> sh) & 0xFFu) * scale,
+                                   static_cast<float>((s[3][w] >> sh) & 0xFFu) * scale);
+      *reinterpret_cast<float4*>(out + 4 * j) = v;
+    }
+  }
+}
+
 template <int SDT>
 int launch_gather_cl(hipStream_t s, const void* src, const int64_t* idx, int64_t M, int64_t C,
                      int64_t P, float* dst, float sc) {
+  if (SDT == OCPPO_U8 && C == 4 && P % 4 == 0 &&
+      reinterpret_cast<uintptr_t>(src) % 4 == 0) {
+    const int tiles = static_cast<int>((P + kClTile - 1) / kClTile);
+    hipLaunchKernelGGL(gather_rows_cl4_u8_kernel, dim3(static_cast<unsigned>(M * tiles)),
+                       dim3(256), 0, s, static_cast<const uint8_t*>(src), idx, M, P, dst, sc,
+                       tiles);
+    return check_launch("ocppo_gather_rows_cl");
+  }
   if (P % 4 == 0)
     hipLaunchKernelGGL((gather_rows_cl_kernel<SDT, 4>), dim3(grid_for(M * (P / 4), 256)), dim3(256),
                        0, s, src, idx, M, (int)C, P, dst, sc);

@@ -382,6 +382,10 @@ class PPOTrainer:
 
     def _act(self, t: int):
         ag = self.agent
+        if self.args.per_step_noise:
+            # the reference's stream: one Exp(1) draw of [N, A] per step (Categorical.sample at
+            # ppo_atari_oc.py:506), from the same device generator
+            self.noise[t].exponential_()
         if self.fused_head:
             hidden = self._policy_hidden(t)
             self.timer.bracket("action_head", lambda: ops.policy_head_sample(
@@ -411,7 +415,8 @@ class PPOTrainer:
         T = self.T
         self.obs[0].copy_(self.obs[T])
         self.dones[0].copy_(self.dones[T])
-        self.noise.exponential_()
+        if not self.args.per_step_noise:
+            self.noise.exponential_()  # the whole rollout's Exp(1) draws in one generator call
 
     def _rollout_end(self):
         """Bootstrap + GAE (:533-547) + minibatch adv stats (:577-579)."""

@@ -461,3 +461,24 @@ def test_fused_heads_loss_trainer_matches_unfused(dev):
         assert ma[0][k] == pytest.approx(mb[0][k], rel=1e-4, abs=1e-6), k
     for p, q in zip(a.agent.parameters(), b.agent.parameters()):
         torch.testing.assert_close(p, q, rtol=1e-3, atol=2e-5)
+
+
+@pytest.mark.parametrize("graphs", [True, False])
+def test_per_step_noise_is_the_reference_sampling_stream(dev, graphs):
+    """per_step_noise: the rollout's Exp(1) draws are exactly the [N, A] draws the reference's
+    Categorical.sample makes step after step (ppo_atari_oc.py:506) from the device generator
+    seeded like the trainer -- eager and graph-replayed iterations alike."""
+    from oc_cleanrl_amd.trainer import PPOTrainer
+
+    a = small_args(per_step_noise=True, cuda_graphs=graphs)
+    tr = PPOTrainer(a, dev)
+    got = []
+    for _ in range(3):
+        tr.train_iteration()
+        got.append(tr.noise.clone())
+    torch.cuda.synchronize()
+    torch.manual_seed(tr.seed)
+    for it in range(3):
+        for t in range(a.num_steps):
+            ref = torch.empty(a.local_num_envs, tr.A, device=dev).exponential_()
+            assert torch.equal(got[it][t], ref), (it, t)

@@ -32,6 +32,8 @@ SIZES = {
     "gae": {"config": dict(T=128, N=128), "scaled": dict(T=128, N=262144)},
     "ppo_loss": {"config": dict(M=4096, A=6, B=16384), "scaled": dict(M=4 * 1024 * 1024, A=6, B=4 * 1024 * 1024)},
     "gather": {"config": dict(M=4096, B=16384, R=48), "scaled": dict(M=1 << 20, B=1 << 20, R=48)},
+    # config-3 minibatch gather: u8 frame stacks -> f32 NHWC (NatureCNN input, 8192 rows)
+    "gather_pixels": {"config": dict(M=8192, B=16384), "scaled": dict(M=16384, B=32768)},
     "rollout_store": {"config": dict(N=128, W=4, D=12), "scaled": dict(N=1 << 20, W=4, D=12)},
     "action_head": {"config": dict(N=128, A=6), "scaled": dict(N=4 * 1024 * 1024, A=6)},
     "env_step": {"config": dict(N=128, D=12), "scaled": dict(N=4 * 1024 * 1024, D=12)},
@@ -106,6 +108,12 @@ def make_case(name: str, p: dict, dev):
         idx = torch.randperm(B, device=dev, generator=g)[:M]
         out = torch.empty(M, R, device=dev)
         return (lambda: ops.gather_rows(src, idx, out)), M * (8 + R * 6)
+    if name == "gather_pixels":
+        M, B = p["M"], p["B"]
+        src = torch.randint(0, 256, (B, 4, 84, 84), device=dev, generator=g).to(torch.uint8)
+        idx = torch.randperm(B, device=dev, generator=g)[:M]
+        out = torch.empty(M, 4, 84, 84, device=dev, memory_format=torch.channels_last)
+        return (lambda: ops.gather_rows(src, idx, out)), M * (8 + 4 * 7056 * 5)
     if name == "rollout_store":
         N, W, D = p["N"], p["W"], p["D"]
         frame = torch.randint(0, 200, (N, D), device=dev, generator=g).float()
