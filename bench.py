@@ -37,7 +37,7 @@ MFMA_F32_PEAK_TFLOPS = 157.3  # dense f32 MFMA (MI355X_MICROARCH.md; no xf32 on 
 RIDGE = MFMA_F32_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9)  # flop/B where the two bounds meet
 # HBM bytes per launch from rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE, separate passes) of
 # the same launch shapes: tools/profile_round.sh -> tools/summarize_profiles.py
-PMC_SUMMARY = ROOT / "profiles" / "r01g" / "pmc_summary.json"
+PMC_SUMMARY = ROOT / "profiles" / "r02" / "pmc_summary.json"
 PMC_KEYS = {"action_head": "policy_head_config", "gae": "gae_config",
             "ppo_loss": "ppo_loss_prepared_config", "relu_bias_grad": "relu_bias_grad_config",
             "cache_linear": "cache_linear_config", "store_encode": "store_encode_config",

@@ -329,8 +329,10 @@ FUSED_CONV_ACT = True
 
 
 # Rollout-sized inference batches (no autograd) of the shapes where the HIP f32-MFMA kernel beats
-# the BLAS library's (tools/exp_rollout_linear.py on MI355X: K <= 64 at up to 512 rows, K <= 256 at
-# up to 128 rows); everything else, and every autograd forward, stays on hipBLASLt.
+# the BLAS library's (tools/exp_rollout_linear.py on MI355X: K <= 256 at up to 512 rows; at up to
+# 128 rows every K <= 2048 with K % 16 == 0 -- the LDS-staged form: 4.7 vs 6.1 us at 512 -> 1024,
+# 4.7 vs 5.6 at 1024 -> 512, 6.8 vs 7.0 at 2048 -> 512); everything else, and every autograd
+# forward, stays on hipBLASLt.
 HIP_ROLLOUT_LINEAR = True
 
 
@@ -341,7 +343,8 @@ def _hip_linear_ok(x2, lin: nn.Linear) -> bool:
     M, K = x2.shape
     # M <= 8 (single-env acting, e.g. the DQN learner's epsilon-greedy forward): the library
     # takes a copy-bias + GEMV + separate ReLU path there (3 launches)
-    return (K <= 64 and M <= 512) or (K <= 256 and M <= 128) or M <= 8
+    return ((K <= 256 and M <= 512 and K % 16 == 0) or (K <= 64 and M <= 512) or
+            (M <= 128 and (K <= 256 or (K <= 2048 and K % 16 == 0))) or M <= 8)
 
 
 def linear_act(x, lin: nn.Linear, relu: bool):

@@ -10,10 +10,14 @@
 //     launch has >= ~2048 waves, i.e. >= 2 per SIMD), partial tiles summed through LDS in wave
 //     order (deterministic);
 //   * v_mfma_f32_16x16x4_f32 (exact f32 products, one rounding per product, f32 accumulation);
-//     operands come straight from global memory as one 16-B load per lane per 16-wide K chunk for
-//     both x (row-major [M, K]) and W (nn.Linear's [N, K]) -- MFMA j of a chunk takes element j
-//     of every lane's float4, so the 4 MFMAs of a chunk together cover its 16 k values, the same
-//     permutation on A and B;
+//     a lane's fragment of a 16-wide K chunk is one float4 for both x (row-major [M, K]) and W
+//     (nn.Linear's [N, K]) -- MFMA j of a chunk takes element j of every lane's float4, so the
+//     4 MFMAs of a chunk together cover its 16 k values, the same permutation on A and B;
+//   * K % 16 == 0: operands go through a wave-private LDS image loaded in whole 128-B lines (8
+//     lines per wave instruction), fragments read back from LDS, the next 32-k group's loads in
+//     flight during this group's MFMAs -- fragment-shaped global loads (16 rows x 64 B per
+//     instruction) cost the address units twice the work per byte: 6.4 -> 4.7 us at
+//     128 x 512 -> 1024, 11.2 -> 6.8 us at 128 x 2048 -> 512 (tools/exp_rollout_linear.py);
 //   * XCD-aware tile order: workgroups b and b+8 share an XCD (round-robin dispatch), and each
 //     XCD gets a contiguous range of output-column tiles, so it streams 1/8 of W through its L2;
 //   * bias + ReLU fused in the epilogue (torch._addmm_activation's order: acc + b, then max(., 0)).
@@ -67,6 +71,87 @@ __device__ __forceinline__ void linear_wave_chunks(const float* xr, const float*
   }
 }
 
+// Full-line staged form (VEC, K % 16 == 0): the fragment-shaped loads above touch 16 rows x 64 B
+// per wave instruction (half of each 128-B line, twice the address-unit work per byte); here each
+// wave instruction loads 8 whole 128-B lines (lane = one 16-B piece) of the wave's 16-row x
+// 16*CH-column slice of x and of W into a wave-private LDS image (rows padded by 4 floats:
+// conflict-free 16-B fragment reads), and the MFMA fragments come from LDS. Same products in the
+// same order as the direct form.
+template <int CH>
+struct LinStage {
+  static constexpr int kRow = 16 * CH + 4;  // floats per LDS row
+  float a[16 * kRow];
+  float b[16 * kRow];
+};
+
+// one group's global loads: instruction i covers lines [8i, 8i+8) of the 16 x 16CH slice
+template <int CH>
+__device__ __forceinline__ void lin_stage_load(const float* x, int64_t ldx, const float* w, int K,
+                                               int row0, int col0, int M, int N, int lane, int cb,
+                                               int c1, float4 (&va)[CH], float4 (&vb)[CH]) {
+  constexpr int LPR = CH / 2;  // 128-B lines per row slice
+  const int piece = lane & 7, lsub = lane >> 3;
+#pragma unroll
+  for (int i = 0; i < CH; ++i) {
+    const int L = i * 8 + lsub;  // row L / LPR, line L % LPR
+    const int r = L / LPR, li = L - r * LPR;
+    const int kk = cb * 16 + li * 32 + piece * 4;
+    const bool kok = kk < c1 * 16;
+    const int ar = row0 + r, bc = col0 + r;
+    va[i] = (kok && ar < M) ? *reinterpret_cast<const float4*>(x + static_cast<int64_t>(ar) * ldx + kk)
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
+    vb[i] = (kok && bc < N) ? *reinterpret_cast<const float4*>(w + static_cast<int64_t>(bc) * K + kk)
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+// one group: the staged lines -> LDS, fragments back, CH x 4 MFMAs
+template <int CH>
+__device__ __forceinline__ void lin_stage_mfma(LinStage<CH>& st, int lane, const float4 (&va)[CH],
+                                               const float4 (&vb)[CH], floatx4& acc0,
+                                               floatx4& acc1) {
+  constexpr int LPR = CH / 2;
+  constexpr int kRow = LinStage<CH>::kRow;
+  const int g = lane >> 4, c16 = lane & 15;
+  const int piece = lane & 7, lsub = lane >> 3;
+#pragma unroll
+  for (int i = 0; i < CH; ++i) {
+    const int L = i * 8 + lsub;
+    const int r = L / LPR, li = L - r * LPR;
+    *reinterpret_cast<float4*>(&st.a[r * kRow + li * 32 + piece * 4]) = va[i];
+    *reinterpret_cast<float4*>(&st.b[r * kRow + li * 32 + piece * 4]) = vb[i];
+  }
+#pragma unroll
+  for (int q = 0; q < CH; ++q) {
+    const float4 fa = *reinterpret_cast<const float4*>(&st.a[c16 * kRow + q * 16 + 4 * g]);
+    const float4 fb = *reinterpret_cast<const float4*>(&st.b[c16 * kRow + q * 16 + 4 * g]);
+    floatx4& acc = (q & 1) ? acc1 : acc0;
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(fa.x, fb.x, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(fa.y, fb.y, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(fa.z, fb.z, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(fa.w, fb.w, acc, 0, 0, 0);
+  }
+}
+
+// The next group's global loads are issued before this group's LDS pass and MFMAs (two register
+// sets, loop unrolled by two).
+template <int CH>
+__device__ __forceinline__ void linear_wave_chunks_lds(const float* x, int64_t ldx, const float* w,
+                                                       int K, int row0, int col0, int M, int N,
+                                                       int lane, int c0, int c1, LinStage<CH>& st,
+                                                       floatx4& acc0, floatx4& acc1) {
+  if (c0 >= c1) return;
+  float4 a0[CH], b0[CH], a1[CH], b1[CH];
+  lin_stage_load<CH>(x, ldx, w, K, row0, col0, M, N, lane, c0, c1, a0, b0);
+  for (int cb = c0; cb < c1; cb += 2 * CH) {
+    const bool has1 = cb + CH < c1, has2 = cb + 2 * CH < c1;  // wave-uniform
+    if (has1) lin_stage_load<CH>(x, ldx, w, K, row0, col0, M, N, lane, cb + CH, c1, a1, b1);
+    lin_stage_mfma<CH>(st, lane, a0, b0, acc0, acc1);
+    if (has2) lin_stage_load<CH>(x, ldx, w, K, row0, col0, M, N, lane, cb + 2 * CH, c1, a0, b0);
+    if (has1) lin_stage_mfma<CH>(st, lane, a1, b1, acc0, acc1);
+  }
+}
+
 // Frame-encoding cache epilogue (PPObj rollout, the last encoder layer): the layer's output row
 // m is env m's fresh frame encoding; instead of storing it to y, shift env m's cache enc[m, W, N]
 // like the frame stack (ocppo_frame_cache_shift's rule) with the fresh row in slot W-1:
@@ -82,7 +167,7 @@ constexpr int kCacheMaxW = 8;
 
 // VEC: x / W rows are 16-B aligned with K % 4 == 0 (float4 operand loads); else scalar loads.
 // CACHE: the output goes through the frame-cache epilogue above (y / ldy unused).
-template <int S, int CH, bool RELU, bool VEC, bool CACHE = false>
+template <int S, int CH, bool RELU, bool VEC, bool CACHE = false, bool STAGE = false>
 __global__ __launch_bounds__(64 * S) void linear_rows_kernel(
     const float* __restrict__ x, int64_t ldx, const float* __restrict__ w,
     const float* __restrict__ bias, float* __restrict__ y, int64_t ldy, int M, int N, int K,
@@ -124,7 +209,14 @@ __global__ __launch_bounds__(64 * S) void linear_rows_kernel(
     }
   }
   floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-  linear_wave_chunks<CH, VEC>(xr, wr, rok, cok, K, g, c0, c1, acc0, acc1);
+  if constexpr (STAGE) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lin_stage_raw[];
+    LinStage<CH>* st = reinterpret_cast<LinStage<CH>*>(lin_stage_raw) + wv;
+    linear_wave_chunks_lds<CH>(x, ldx, w, K, tm * 16, tn * 16, M, N, lane, c0, c1, *st,
+                                     acc0, acc1);
+  } else {
+    linear_wave_chunks<CH, VEC>(xr, wr, rok, cok, K, g, c0, c1, acc0, acc1);
+  }
   floatx4 acc = acc0 + acc1;
   if (S > 1) {
     if (wv > 0) red[wv - 1][lane] = acc;
@@ -170,7 +262,10 @@ static void launch_linear_sc(hipStream_t s, bool vec, const float* x, int64_t ld
                              CacheOut c) {
   const int ntm = (M + 15) / 16, ntn = (N + 15) / 16, tiles = ntm * ntn;
   const dim3 grid(8 * ((tiles + 7) / 8)), block(64 * S);
-  if (vec)
+  if (vec && K % 16 == 0)  // full-line staged, pipelined in groups of 2 chunks (32 k values)
+    hipLaunchKernelGGL((linear_rows_kernel<S, 2, RELU, true, CACHE, true>), grid, block,
+                       sizeof(LinStage<2>) * S, s, x, ldx, w, b, y, ldy, M, N, K, ntm, tiles, c);
+  else if (vec)
     hipLaunchKernelGGL((linear_rows_kernel<S, CH, RELU, true, CACHE>), grid, block, 0, s, x, ldx,
                        w, b, y, ldy, M, N, K, ntm, tiles, c);
   else

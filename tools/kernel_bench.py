@@ -75,6 +75,57 @@ def relu_bias_grad_bytes(shapes):
     return sum(R * N * 12 + 4 * N for R, N in shapes)
 
 
+def case_bytes(name: str, p: dict) -> float:
+    """Algorithmic bytes per launch of a case (the DESIGN.md §4 figures; no GPU needed, so
+    tools/summarize_profiles.py prices the PMC passes with the same numbers). ppo_loss gathers its
+    records through the minibatch indices (8A+32 B per element + the 4-B index); the prepared
+    form reads them contiguous (8A+32)."""
+    if name == "gae":
+        return 20 * p["T"] * p["N"] + 8 * p["N"]
+    if name == "ppo_loss":
+        return (8 * p["A"] + 36) * p["M"]
+    if name == "ppo_loss_prepared":
+        return (8 * p["A"] + 32) * p["M"]
+    if name == "gather":
+        return p["M"] * (8 + p["R"] * 6)
+    if name == "gather_pixels":
+        return p["M"] * (8 + 4 * 7056 * 5)
+    if name == "rollout_store":
+        N, W, D = p["N"], p["W"], p["D"]
+        return N * ((W - 1) * D * 2 + D * 4 + W * D * 6 + 16)
+    if name == "action_head":
+        return p["N"] * (8 * p["A"] + 8 + 4 + 8)
+    if name == "env_step":
+        return p["N"] * (8 + p["D"] * 4 + 8 + 2 * 20)
+    if name == "adv_stats":
+        return 2 * p["nmb"] * p["M"] * 12
+    if name == "mb_prepare":
+        return p["nmb"] * p["M"] * (8 + 2 * (8 + 16))
+    if name == "policy_head":
+        N, H, A = p["N"], p["H"], p["A"]
+        return N * (4 * H + 4 * A + 16) + 4 * (A + 1) * (H + 1)
+    if name in ("relu_bias_grad", "relu_bias_grad_tail"):
+        return relu_bias_grad_bytes(p["shapes"])
+    if name == "heads_loss":
+        # h in + gp out; records (action 8 + 4 x 4) in; [Wa; Wc] + biases in; head grads out
+        M, H, A = p["M"], p["H"], p["A"]
+        return M * H * 8 + M * 24 + 4 * (A + 1) * (H + 1) + 4 * ((A + 1) * (H + 1) + H) + 36
+    if name == "cache_linear":
+        M, K, E, W = p["M"], p["K"], p["E"], p["W"]
+        return 4 * (M * K + E * (K + 1)) + 4 * M * E * (2 * W - 1) + 4 * M
+    if name == "store_encode":
+        N, W, F, N1, N2 = p["N"], p["W"], p["F"], p["N1"], p["N2"]
+        store = N * ((W - 1) * F * 2 + F * 4 + W * F * 6 + 8 + 4 + 24 + 4)
+        return store + 4 * (N1 * (F + 1) + N2 * (N1 + 1)) + 4 * N * N2
+    if name == "heads_bwd":
+        M, H, A = p["M"], p["H"], p["A"]
+        return M * H * 8 + M * (A + 1) * 4 + 2 * (A + 1) * H * 4 + H * 4 + (A + 1) * 4
+    if name == "relu_bias_wgrad":
+        R, N, K = p["R"], p["N"], p["K"]
+        return R * N * 8 + R * K * 4 + N * (K + 1) * 4
+    raise KeyError(name)
+
+
 def make_case(name: str, p: dict, dev):
     """Returns (launch closure, algorithmic bytes per launch)."""
     g = torch.Generator(device=dev).manual_seed(0)
@@ -279,6 +330,7 @@ def time_case(fn, reps=20, rounds=5) -> float:
 
 def run_case(name, size, dev, reps=20, rounds=5) -> dict:
     fn, nbytes = make_case(name, SIZES[name][size], dev)
+    assert nbytes == case_bytes(name, SIZES[name][size]), name
     us = time_case(fn, reps, rounds)
     launches = len(SIZES[name][size].get("shapes", (None,)))
     us, nbytes = us / launches, nbytes / launches  # per launch (average over the launch mix)

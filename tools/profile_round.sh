@@ -5,7 +5,7 @@
 #      kernels at config and scaled sizes, one kernel_bench case per run.
 # Outputs under gpurun_out/prof_<tag>/; copy the summaries into profiles/ afterwards.
 set -euo pipefail
-TAG=${1:-r01b}
+TAG=${1:-r02}
 OUT="$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG"
 REPO="$GRAFT_REPO_ROOT"
 mkdir -p "$OUT"
@@ -17,7 +17,8 @@ echo "bench trace done"
 for case in "policy_head config" "gae config" "ppo_loss_prepared config" \
             "gae scaled" "ppo_loss_prepared scaled" "policy_head scaled" "rollout_store scaled" \
             "gather scaled" "relu_bias_grad config" "relu_bias_grad scaled" \
-            "relu_bias_wgrad config" "heads_bwd config"; do
+            "relu_bias_wgrad config" "heads_bwd config" "heads_loss config" "heads_loss scaled" \
+            "cache_linear config" "store_encode config" "gather_pixels config"; do
   set -- $case
   for ctr in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 240 rocprofv3 --pmc "$ctr" --kernel-trace --output-format csv \

@@ -16,49 +16,46 @@ from pathlib import Path
 
 csv.field_size_limit(1 << 30)
 sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
-from tools.kernel_bench import SIZES, make_case  # noqa: E402,F401
+from tools.kernel_bench import SIZES  # noqa: E402
 
+from tools.kernel_bench import case_bytes  # noqa: E402
+
+# kernels of each case (name substrings); a case's counters are summed over them per launch
 KERNEL_SUBSTR = {
-    "policy_head": "policy_head_fast_kernel",
-    "gae": "ocppo::gae",  # gae_kernel (LDS) / gae_stream_kernel by width
-    "ppo_loss_prepared": "ocppo::ppo_loss",  # _small / _vec / tile forms by size
-    "rollout_store": "rollout_store_kernel",
-    "gather": "gather_rows_kernel",
-    "relu_bias_grad": "relu_bias_grad_kernel",
-    "relu_bias_wgrad": "relu_bias_wgrad_kernel",
-    "heads_bwd": "heads_bwd_kernel",
+    "policy_head": ("policy_head_fast_kernel",),
+    "gae": ("ocppo::gae",),  # gae_kernel (LDS) / gae_stream_kernel by width
+    "ppo_loss_prepared": ("ocppo::ppo_loss",),  # _small / _vec / tile forms by size
+    "rollout_store": ("rollout_store_kernel",),
+    "gather": ("gather_rows_kernel",),
+    "gather_pixels": ("gather_rows_cl4_u8_kernel",),
+    "relu_bias_grad": ("relu_bias_grad_kernel",),
+    "relu_bias_grad_tail": ("relu_bias_grad_kernel",),
+    "relu_bias_wgrad": ("relu_bias_wgrad_rows_kernel", "relu_bias_wgrad_finish_kernel"),
+    "heads_bwd": ("heads_bwd_kernel",),
+    "heads_loss": ("heads_loss_kernel", "heads_loss_finish_kernel"),
+    "cache_linear": ("linear_rows_kernel",),
+    "store_encode": ("store_linear2_kernel",),
 }
 
 
 def algorithmic_bytes(name, size):
-    """Algorithmic bytes per launch: the kernel_bench formulas (needs no GPU for these)."""
+    """Algorithmic bytes per launch: kernel_bench's formulas (needs no GPU); a multi-shape case
+    (relu_bias_grad) is averaged over its launch mix like kernel_bench's per-launch figures."""
     p = SIZES[name][size]
-    if name == "gae":
-        return 20 * p["T"] * p["N"] + 8 * p["N"]
-    if name == "ppo_loss_prepared":
-        return (8 * p["A"] + 32) * p["M"]
-    if name == "policy_head":
-        return p["N"] * (4 * p["H"] + 4 * p["A"] + 16) + 4 * (p["A"] + 1) * (p["H"] + 1)
-    if name == "rollout_store":
-        return p["N"] * ((p["W"] - 1) * p["D"] * 2 + p["D"] * 4 + p["W"] * p["D"] * 6 + 16)
-    if name == "gather":
-        return p["M"] * (8 + p["R"] * 6)
-    if name == "relu_bias_grad":  # average over the launch mix
-        return sum(R * N * 12 + 4 * N for R, N in p["shapes"]) / len(p["shapes"])
-    if name == "heads_bwd":
-        M, H, A = p["M"], p["H"], p["A"]
-        return M * H * 8 + M * (A + 1) * 4 + 2 * (A + 1) * H * 4 + H * 4 + (A + 1) * 4
-    if name == "relu_bias_wgrad":
-        return p["R"] * p["N"] * 8 + p["R"] * p["K"] * 4 + p["N"] * (p["K"] + 1) * 4
-    return None
+    return case_bytes(name, p) / len(p.get("shapes", (None,)))
 
 
-def mean_counter(path: Path, substr: str):
-    vals = []
-    for row in csv.DictReader(open(path)):
-        if substr in row["Kernel_Name"]:
-            vals.append(float(row["Counter_Value"]))
-    return (sum(vals) / len(vals), len(vals)) if vals else (None, 0)
+def mean_counter(path: Path, substrs):
+    """Per-launch counter: the mean over dispatches of each kernel, summed over the kernels."""
+    rows = list(csv.DictReader(open(path)))
+    total, n = 0.0, []
+    for sub in substrs:
+        vals = [float(r["Counter_Value"]) for r in rows if sub in r["Kernel_Name"]]
+        if not vals:
+            return None, 0
+        total += sum(vals) / len(vals)
+        n.append(len(vals))
+    return total, n
 
 
 def main(src, dst):
