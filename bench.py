@@ -87,8 +87,10 @@ def kernel_bytes(tr) -> dict:
         E, Kl = lins[-1].out_features, lins[-1].in_features
         # store (as rollout_store) + linear2: W1, W2 in, y [N, N2] out (the frame is counted once)
         kb["store_encode"] = kb["rollout_store"] + 4 * (N1 * (D + 1) + N2 * (N1 + 1)) + 4 * N * N2
-        # x [N, K] + W [E, K] in; cache: W-1 slots read, W slots written, done row
-        kb["cache_linear"] = 4 * (N * Kl + E * (Kl + 1)) + 4 * N * E * (2 * W - 1) + 4 * N
+        # x [N, K] + W [E, K] in; done row; ring: the fresh row into one slot (shift form: W-1
+        # slots read, W written)
+        kb["cache_linear"] = (4 * (N * Kl + E * (Kl + 1)) + 4 * N +
+                              (4 * N * E if tr.cache_ring else 4 * N * E * (2 * W - 1)))
     if tr.fused_heads_loss:
         Hh, A1 = tr.H, tr.A + 1
         kb["heads_loss"] = (M * Hh * 8 + M * 24 + 4 * A1 * (Hh + 1) + 4 * (A1 * (Hh + 1) + Hh)

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define OCPPO_ABI_VERSION 10
+#define OCPPO_ABI_VERSION 11
 
 /* status codes */
 #define OCPPO_OK 0
@@ -516,6 +516,26 @@ OCPPO_API int ocppo_linear_cache_shift(ocppo_stream_t stream, const float* x, in
                                        const float* w, const float* b, float* enc,
                                        const float* done, int64_t M, int64_t N, int64_t K,
                                        int64_t W, int relu);
+/* Ring form of the frame-encoding cache (no shift): the W physical slots of enc [M, W, N] hold the
+ * W logical frames (oldest .. newest) rotated by a per-step offset r, logical slot w at physical
+ * (w + r) mod W.
+ * ocppo_linear_cache_ring: fresh = act(x W^T + b) overwrites physical slot `slot` only (the
+ *   oldest frame's: at rollout step t the newest frame goes to slot (t - 1) mod W), or every
+ *   slot of env m when done[m] != 0 (a reset fills the stack with the new frame). No old slot is
+ *   read. done [M] f32 or NULL.
+ * ocppo_linear_act_ring: ocppo_linear_act whose x rows are W = K / seg segments of seg floats
+ *   stored rotated: logical segment s at physical segment (s + rot) mod W (seg % 32 == 0,
+ *   K % seg == 0, x / w 16-B aligned, ldx % 4 == 0). Products and summation order are those of
+ *   the logical layout: the decoder (architectures/ppo.py:74-78: Flatten + Linear over the W
+ *   frame encodings) on the ring gives bit for bit what it gives on the shifted cache. */
+OCPPO_API int ocppo_linear_cache_ring(ocppo_stream_t stream, const float* x, int64_t ldx,
+                                      const float* w, const float* b, float* enc,
+                                      const float* done, int64_t M, int64_t N, int64_t K,
+                                      int64_t W, int64_t slot, int relu);
+OCPPO_API int ocppo_linear_act_ring(ocppo_stream_t stream, const float* x, int64_t ldx,
+                                    const float* w, const float* b, float* y, int64_t ldy,
+                                    int64_t M, int64_t N, int64_t K, int64_t seg, int64_t rot,
+                                    int relu);
 OCPPO_API int ocppo_store_linear2(ocppo_stream_t stream, const float* frame, const float* reward,
                                   const float* done, int64_t N, int64_t W, int64_t D,
                                   const void* prev_obs, void* obs_out, int obs_dtype,

@@ -85,10 +85,19 @@ struct LinStage {
 };
 
 // one group's global loads: instruction i covers lines [8i, 8i+8) of the 16 x 16CH slice
+// Ring (seg > 0): x's K dimension is K / seg segments; logical segment s of a row is stored at
+// physical segment (s + rot) mod (K / seg) (the rollout's frame-encoding ring, seg % 32 == 0, so a
+// 32-float group never straddles a segment). Only the x addresses move: products and their order
+// are those of the logical layout.
+struct XRing {
+  int seg, rot, nseg;
+};
+
 template <int CH>
 __device__ __forceinline__ void lin_stage_load(const float* x, int64_t ldx, const float* w, int K,
                                                int row0, int col0, int M, int N, int lane, int cb,
-                                               int c1, float4 (&va)[CH], float4 (&vb)[CH]) {
+                                               int c1, float4 (&va)[CH], float4 (&vb)[CH],
+                                               XRing ring) {
   constexpr int LPR = CH / 2;  // 128-B lines per row slice
   const int piece = lane & 7, lsub = lane >> 3;
 #pragma unroll
@@ -98,7 +107,14 @@ __device__ __forceinline__ void lin_stage_load(const float* x, int64_t ldx, cons
     const int kk = cb * 16 + li * 32 + piece * 4;
     const bool kok = kk < c1 * 16;
     const int ar = row0 + r, bc = col0 + r;
-    va[i] = (kok && ar < M) ? *reinterpret_cast<const float4*>(x + static_cast<int64_t>(ar) * ldx + kk)
+    int kx = kk;
+    if (ring.seg) {
+      const int sg = kk / ring.seg;
+      int ps = sg + ring.rot;
+      ps = ps >= ring.nseg ? ps - ring.nseg : ps;
+      kx = ps * ring.seg + (kk - sg * ring.seg);
+    }
+    va[i] = (kok && ar < M) ? *reinterpret_cast<const float4*>(x + static_cast<int64_t>(ar) * ldx + kx)
                             : make_float4(0.f, 0.f, 0.f, 0.f);
     vb[i] = (kok && bc < N) ? *reinterpret_cast<const float4*>(w + static_cast<int64_t>(bc) * K + kk)
                             : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -139,15 +155,15 @@ template <int CH>
 __device__ __forceinline__ void linear_wave_chunks_lds(const float* x, int64_t ldx, const float* w,
                                                        int K, int row0, int col0, int M, int N,
                                                        int lane, int c0, int c1, LinStage<CH>& st,
-                                                       floatx4& acc0, floatx4& acc1) {
+                                                       floatx4& acc0, floatx4& acc1, XRing ring) {
   if (c0 >= c1) return;
   float4 a0[CH], b0[CH], a1[CH], b1[CH];
-  lin_stage_load<CH>(x, ldx, w, K, row0, col0, M, N, lane, c0, c1, a0, b0);
+  lin_stage_load<CH>(x, ldx, w, K, row0, col0, M, N, lane, c0, c1, a0, b0, ring);
   for (int cb = c0; cb < c1; cb += 2 * CH) {
     const bool has1 = cb + CH < c1, has2 = cb + 2 * CH < c1;  // wave-uniform
-    if (has1) lin_stage_load<CH>(x, ldx, w, K, row0, col0, M, N, lane, cb + CH, c1, a1, b1);
+    if (has1) lin_stage_load<CH>(x, ldx, w, K, row0, col0, M, N, lane, cb + CH, c1, a1, b1, ring);
     lin_stage_mfma<CH>(st, lane, a0, b0, acc0, acc1);
-    if (has2) lin_stage_load<CH>(x, ldx, w, K, row0, col0, M, N, lane, cb + 2 * CH, c1, a0, b0);
+    if (has2) lin_stage_load<CH>(x, ldx, w, K, row0, col0, M, N, lane, cb + 2 * CH, c1, a0, b0, ring);
     if (has1) lin_stage_mfma<CH>(st, lane, a1, b1, acc0, acc1);
   }
 }
@@ -158,10 +174,14 @@ __device__ __forceinline__ void linear_wave_chunks_lds(const float* x, int64_t l
 //   enc[m, w] = done[m] != 0 || w == W-1 ? fresh[m] : enc[m, w+1]
 // Each (row, column) of the cache is read and written by the one lane that owns that output
 // element, slots in increasing w, so the shift needs no second launch.
+// Ring form (slot >= 0): the cache is a ring over its W physical slots (XRing above, read by the
+// decoder with rot = the oldest frame's slot); the fresh row only overwrites physical slot `slot`
+// (the oldest frame's), or every slot of an env that was just reset -- no old slot is read.
 struct CacheOut {
   float* enc;         // [M, W, N]
   const float* done;  // [M] or NULL
   int W;
+  int slot;           // -1: shift form
 };
 constexpr int kCacheMaxW = 8;
 
@@ -171,7 +191,8 @@ template <int S, int CH, bool RELU, bool VEC, bool CACHE = false, bool STAGE = f
 __global__ __launch_bounds__(64 * S) void linear_rows_kernel(
     const float* __restrict__ x, int64_t ldx, const float* __restrict__ w,
     const float* __restrict__ bias, float* __restrict__ y, int64_t ldy, int M, int N, int K,
-    int ntm, int tiles, CacheOut cache = CacheOut{nullptr, nullptr, 0}) {
+    int ntm, int tiles, CacheOut cache = CacheOut{nullptr, nullptr, 0, -1},
+    XRing ring = XRing{0, 0, 1}) {
   __shared__ floatx4 red[S > 1 ? S - 1 : 1][64];
   const int b = blockIdx.x;
   const int per_xcd = (tiles + 7) / 8;
@@ -194,7 +215,8 @@ __global__ __launch_bounds__(64 * S) void linear_rows_kernel(
   // MFMA loop, so their latency hides behind it (W <= kCacheMaxW; else loaded in the epilogue)
   float old[4][kCacheMaxW - 1];
   bool dn[4] = {false, false, false, false};
-  const bool pre = CACHE && wv == 0 && cache.W <= kCacheMaxW && tn * 16 + c16 < N;
+  const bool pre = CACHE && cache.slot < 0 && wv == 0 && cache.W <= kCacheMaxW &&
+                   tn * 16 + c16 < N;
   if (pre) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -213,7 +235,7 @@ __global__ __launch_bounds__(64 * S) void linear_rows_kernel(
     extern __shared__ __attribute__((aligned(16))) unsigned char lin_stage_raw[];
     LinStage<CH>* st = reinterpret_cast<LinStage<CH>*>(lin_stage_raw) + wv;
     linear_wave_chunks_lds<CH>(x, ldx, w, K, tm * 16, tn * 16, M, N, lane, c0, c1, *st,
-                                     acc0, acc1);
+                               acc0, acc1, ring);
   } else {
     linear_wave_chunks<CH, VEC>(xr, wr, rok, cok, K, g, c0, c1, acc0, acc1);
   }
@@ -238,7 +260,13 @@ __global__ __launch_bounds__(64 * S) void linear_rows_kernel(
       if (CACHE) {
         const int W = cache.W;
         float* e = cache.enc + static_cast<int64_t>(orow) * W * N + ocol;
-        if (pre) {
+        if (cache.slot >= 0) {
+          if (cache.done != nullptr && cache.done[orow] != 0.f) {
+            for (int q = 0; q < W; ++q) e[static_cast<int64_t>(q) * N] = v;
+          } else {
+            e[static_cast<int64_t>(cache.slot) * N] = v;
+          }
+        } else if (pre) {
 #pragma unroll
           for (int q = 0; q < kCacheMaxW - 1; ++q)
             if (q + 1 < W) e[static_cast<int64_t>(q) * N] = dn[r] ? v : old[r][q];
@@ -259,12 +287,13 @@ __global__ __launch_bounds__(64 * S) void linear_rows_kernel(
 template <int S, int CH, bool RELU, bool CACHE>
 static void launch_linear_sc(hipStream_t s, bool vec, const float* x, int64_t ldx, const float* w,
                              const float* b, float* y, int64_t ldy, int M, int N, int K,
-                             CacheOut c) {
+                             CacheOut c, XRing ring) {
   const int ntm = (M + 15) / 16, ntn = (N + 15) / 16, tiles = ntm * ntn;
   const dim3 grid(8 * ((tiles + 7) / 8)), block(64 * S);
   if (vec && K % 16 == 0)  // full-line staged, pipelined in groups of 2 chunks (32 k values)
     hipLaunchKernelGGL((linear_rows_kernel<S, 2, RELU, true, CACHE, true>), grid, block,
-                       sizeof(LinStage<2>) * S, s, x, ldx, w, b, y, ldy, M, N, K, ntm, tiles, c);
+                       sizeof(LinStage<2>) * S, s, x, ldx, w, b, y, ldy, M, N, K, ntm, tiles, c,
+                       ring);
   else if (vec)
     hipLaunchKernelGGL((linear_rows_kernel<S, CH, RELU, true, CACHE>), grid, block, 0, s, x, ldx,
                        w, b, y, ldy, M, N, K, ntm, tiles, c);
@@ -276,29 +305,30 @@ static void launch_linear_sc(hipStream_t s, bool vec, const float* x, int64_t ld
 template <int S, bool RELU, bool CACHE>
 static void launch_linear_s(hipStream_t s, int cpw, bool vec, const float* x, int64_t ldx,
                             const float* w, const float* b, float* y, int64_t ldy, int M, int N,
-                            int K, CacheOut c) {
+                            int K, CacheOut c, XRing ring) {
   if (cpw <= 2)
-    launch_linear_sc<S, 2, RELU, CACHE>(s, vec, x, ldx, w, b, y, ldy, M, N, K, c);
+    launch_linear_sc<S, 2, RELU, CACHE>(s, vec, x, ldx, w, b, y, ldy, M, N, K, c, ring);
   else if (cpw <= 4)
-    launch_linear_sc<S, 4, RELU, CACHE>(s, vec, x, ldx, w, b, y, ldy, M, N, K, c);
+    launch_linear_sc<S, 4, RELU, CACHE>(s, vec, x, ldx, w, b, y, ldy, M, N, K, c, ring);
   else
-    launch_linear_sc<S, 8, RELU, CACHE>(s, vec, x, ldx, w, b, y, ldy, M, N, K, c);
+    launch_linear_sc<S, 8, RELU, CACHE>(s, vec, x, ldx, w, b, y, ldy, M, N, K, c, ring);
 }
 
 template <bool RELU, bool CACHE = false>
 static void launch_linear(hipStream_t s, bool vec, const float* x, int64_t ldx, const float* w,
                           const float* b, float* y, int64_t ldy, int M, int N, int K,
-                          CacheOut c = CacheOut{nullptr, nullptr, 0}) {
+                          CacheOut c = CacheOut{nullptr, nullptr, 0, -1},
+                          XRing ring = XRing{0, 0, 1}) {
   const int64_t tiles = static_cast<int64_t>((M + 15) / 16) * ((N + 15) / 16);
   const int nch = (K + 15) / 16;
   int S = 1;  // K split: >= ~4096 waves (4 per SIMD), >= 2 chunks per wave
   while (S < kLinMaxWaves && tiles * S < 4096 && nch >= 2 * S * 2) S *= 2;
   const int cpw = (nch + S - 1) / S;
   switch (S) {
-    case 1: launch_linear_s<1, RELU, CACHE>(s, cpw, vec, x, ldx, w, b, y, ldy, M, N, K, c); break;
-    case 2: launch_linear_s<2, RELU, CACHE>(s, cpw, vec, x, ldx, w, b, y, ldy, M, N, K, c); break;
-    case 4: launch_linear_s<4, RELU, CACHE>(s, cpw, vec, x, ldx, w, b, y, ldy, M, N, K, c); break;
-    default: launch_linear_s<8, RELU, CACHE>(s, cpw, vec, x, ldx, w, b, y, ldy, M, N, K, c); break;
+    case 1: launch_linear_s<1, RELU, CACHE>(s, cpw, vec, x, ldx, w, b, y, ldy, M, N, K, c, ring); break;
+    case 2: launch_linear_s<2, RELU, CACHE>(s, cpw, vec, x, ldx, w, b, y, ldy, M, N, K, c, ring); break;
+    case 4: launch_linear_s<4, RELU, CACHE>(s, cpw, vec, x, ldx, w, b, y, ldy, M, N, K, c, ring); break;
+    default: launch_linear_s<8, RELU, CACHE>(s, cpw, vec, x, ldx, w, b, y, ldy, M, N, K, c, ring); break;
   }
 }
 
@@ -343,7 +373,7 @@ extern "C" int ocppo_linear_cache_shift(ocppo_stream_t stream, const float* x, i
                 "ocppo_linear_cache_shift: too large");
   const bool vec = K % 4 == 0 && ldx % 4 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0 &&
                    reinterpret_cast<uintptr_t>(w) % 16 == 0;
-  const CacheOut c{enc, done, static_cast<int>(W)};
+  const CacheOut c{enc, done, static_cast<int>(W), -1};
   clear_stale_error();
   hipStream_t s = as_stream(stream);
   if (relu)
@@ -351,6 +381,61 @@ extern "C" int ocppo_linear_cache_shift(ocppo_stream_t stream, const float* x, i
   else
     launch_linear<false, true>(s, vec, x, ldx, w, b, nullptr, 0, (int)M, (int)N, (int)K, c);
   return check_launch("ocppo_linear_cache_shift");
+}
+
+extern "C" int ocppo_linear_act_ring(ocppo_stream_t stream, const float* x, int64_t ldx,
+                                     const float* w, const float* b, float* y, int64_t ldy,
+                                     int64_t M, int64_t N, int64_t K, int64_t seg, int64_t rot,
+                                     int relu) {
+  OCPPO_REQUIRE(M >= 0 && N >= 1 && K >= 1 && M <= INT32_MAX && N <= INT32_MAX && K <= INT32_MAX,
+                "ocppo_linear_act_ring: bad sizes M=%lld N=%lld K=%lld", (long long)M, (long long)N,
+                (long long)K);
+  OCPPO_REQUIRE(seg >= 32 && seg % 32 == 0 && K % seg == 0 && rot >= 0 && rot < K / seg,
+                "ocppo_linear_act_ring: seg=%lld rot=%lld (seg %% 32 == 0, K %% seg == 0, "
+                "0 <= rot < K / seg)", (long long)seg, (long long)rot);
+  OCPPO_REQUIRE(ldx >= K && ldy >= N && ldx % 4 == 0,
+                "ocppo_linear_act_ring: leading dimensions ldx=%lld ldy=%lld", (long long)ldx,
+                (long long)ldy);
+  if (M == 0) return OCPPO_OK;
+  OCPPO_REQUIRE(x && w && y, "ocppo_linear_act_ring: null pointer");
+  OCPPO_REQUIRE(reinterpret_cast<uintptr_t>(x) % 16 == 0 && reinterpret_cast<uintptr_t>(w) % 16 == 0,
+                "ocppo_linear_act_ring: x and w must be 16-B aligned");
+  OCPPO_REQUIRE((M + 15) / 16 * ((N + 15) / 16) <= INT32_MAX / 8, "ocppo_linear_act_ring: too large");
+  const XRing ring{static_cast<int>(seg), static_cast<int>(rot), static_cast<int>(K / seg)};
+  clear_stale_error();
+  hipStream_t s = as_stream(stream);
+  if (relu)
+    launch_linear<true>(s, true, x, ldx, w, b, y, ldy, (int)M, (int)N, (int)K,
+                        CacheOut{nullptr, nullptr, 0, -1}, ring);
+  else
+    launch_linear<false>(s, true, x, ldx, w, b, y, ldy, (int)M, (int)N, (int)K,
+                         CacheOut{nullptr, nullptr, 0, -1}, ring);
+  return check_launch("ocppo_linear_act_ring");
+}
+
+extern "C" int ocppo_linear_cache_ring(ocppo_stream_t stream, const float* x, int64_t ldx,
+                                       const float* w, const float* b, float* enc,
+                                       const float* done, int64_t M, int64_t N, int64_t K,
+                                       int64_t W, int64_t slot, int relu) {
+  OCPPO_REQUIRE(M >= 0 && N >= 1 && K >= 1 && W >= 1 && W <= 64 && M <= INT32_MAX &&
+                    N <= INT32_MAX && K <= INT32_MAX && slot >= 0 && slot < W,
+                "ocppo_linear_cache_ring: bad sizes M=%lld N=%lld K=%lld W=%lld slot=%lld",
+                (long long)M, (long long)N, (long long)K, (long long)W, (long long)slot);
+  OCPPO_REQUIRE(ldx >= K, "ocppo_linear_cache_ring: ldx=%lld < K", (long long)ldx);
+  if (M == 0) return OCPPO_OK;
+  OCPPO_REQUIRE(x && w && enc, "ocppo_linear_cache_ring: null pointer");
+  OCPPO_REQUIRE((M + 15) / 16 * ((N + 15) / 16) <= INT32_MAX / 8,
+                "ocppo_linear_cache_ring: too large");
+  const bool vec = K % 4 == 0 && ldx % 4 == 0 && reinterpret_cast<uintptr_t>(x) % 16 == 0 &&
+                   reinterpret_cast<uintptr_t>(w) % 16 == 0;
+  const CacheOut c{enc, done, static_cast<int>(W), static_cast<int>(slot)};
+  clear_stale_error();
+  hipStream_t s = as_stream(stream);
+  if (relu)
+    launch_linear<true, true>(s, vec, x, ldx, w, b, nullptr, 0, (int)M, (int)N, (int)K, c);
+  else
+    launch_linear<false, true>(s, vec, x, ldx, w, b, nullptr, 0, (int)M, (int)N, (int)K, c);
+  return check_launch("ocppo_linear_cache_ring");
 }
 
 // ---- two Linear(+ReLU) layers in one launch: y = act2(act1(x W1^T + b1) W2^T + b2) ---------------

@@ -41,13 +41,14 @@ class FramePlanner:
     """
 
     def __init__(self, T: int, N: int, W: int, M: int, epochs: int, num_minibatches: int,
-                 cap: int | None = None, headroom: float = 1.05, align: int = 2048):
+                 cap: int | None = None, margin: int = 64, align: int = 2048,
+                 extra_caps: tuple = (11520,)):
         self.T, self.N, self.W, self.M = T, N, W, M
         self.E, self.nmb = epochs, num_minibatches
         self.J = epochs * num_minibatches
         self.B = T * N
         self.U = (T + W - 1) * N
-        self.headroom, self.align = headroom, align
+        self.margin, self.align, self.extra_caps = margin, align, tuple(extra_caps)
         self.cap = cap
         self.counts = np.zeros(self.J, np.int64)
 
@@ -63,11 +64,17 @@ class FramePlanner:
         return uniq, pos_of, inv
 
     def cap_for(self, counts) -> int:
-        """Capacity for the largest minibatch + headroom, rounded up to `align` rows: hipBLASLt's
-        f32 tiles quantise badly between multiples of 2048 rows on gfx950 (encoder fwd+bwd at
-        [10240, 12032, 12288, 16384] rows: 802, 1002, 896, 1088 us; tools/exp_dedup_rows.py)."""
-        c = int(np.ceil(int(counts.max()) * self.headroom / self.align) * self.align)
-        return min(max(c, self.align), self.M * self.W)
+        """Capacity for the largest minibatch + `margin` rows: the smallest multiple of `align`
+        or entry of `extra_caps` that holds it. hipBLASLt's f32 tiles quantise the encoder's
+        fwd+bwd time in rows on gfx950 (tools/exp_dedup_rows.py, encoder 12->256->512->1024->512:
+        10240 / 11264 / 11520 / 11776 / 12032 / 12288 rows -> 710 / 837 / 781 / 905 / 906 / 800 us),
+        so between the multiples of 2048 only 11520 pays. At config 2 the largest of an
+        iteration's 16 minibatches is 11357 +- 40 distinct frames (max 11470 over 300 iterations),
+        so 11520 holds it; a later overflow re-sizes the plan (trainer._alloc_plan)."""
+        need = int(counts.max()) + self.margin
+        cands = sorted({c for c in self.extra_caps if c >= need} |
+                       {-(-need // self.align) * self.align})
+        return min(max(cands[0], self.align), self.M * self.W)
 
     def plan(self, perm: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
         """perm [E*B] (the epochs' shuffles, ppo_atari_oc.py:561) -> (used [J, U] bool,

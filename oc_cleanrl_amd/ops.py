@@ -438,10 +438,12 @@ def obs_reset(frame, obs_out, net_obs=None, scale255: bool = False):
          _DTYPE_CODE[obs_out.dtype], net, layout | (2 if scale255 else 0))
 
 
-def linear_act(x, weight, bias=None, relu: bool = False, out=None):
+def linear_act(x, weight, bias=None, relu: bool = False, out=None, ring=None):
     """y = act(x @ weight.T + bias) on the f32 matrix cores, for rollout-sized batches (no
     autograd). x [M, K] f32 with unit column stride (row stride may exceed K, e.g. a frame slice
-    of the stacked obs); weight [N, K] contiguous (nn.Linear.weight); bias [N] or None."""
+    of the stacked obs); weight [N, K] contiguous (nn.Linear.weight); bias [N] or None.
+    ring = (seg, rot): x's rows are K / seg segments stored rotated, logical segment s at
+    physical (s + rot) mod (K / seg) (the frame-encoding ring, ocppo_linear_act_ring)."""
     if x.dim() != 2 or weight.dim() != 2:
         raise ValueError(f"x must be [M, K] and weight [N, K], got {tuple(x.shape)}, "
                          f"{tuple(weight.shape)}")
@@ -458,6 +460,12 @@ def linear_act(x, weight, bias=None, relu: bool = False, out=None):
     if tuple(out.shape) != (M, N) or (M > 1 and out.stride(1) != 1) or out.dtype != torch.float32:
         raise ValueError("out must be an f32 [M, N] tensor with unit column stride")
     ldy = out.stride(0) if M > 1 else N
+    if ring is not None:
+        seg, rot = (int(v) for v in ring)
+        call("ocppo_linear_act_ring", _stream(dev), x.data_ptr(), ldx,
+             _check(weight, "weight", torch.float32, dev), _opt(bias, "bias", torch.float32, dev, N),
+             out.data_ptr(), ldy, M, N, K, seg, rot, 1 if relu else 0)
+        return out
     call("ocppo_linear_act", _stream(dev), x.data_ptr(), ldx,
          _check(weight, "weight", torch.float32, dev), _opt(bias, "bias", torch.float32, dev, N),
          out.data_ptr(), ldy, M, N, K, 1 if relu else 0)
@@ -506,6 +514,29 @@ def linear_cache_shift(x, weight, bias, enc, done=None, relu: bool = True):
          _check(weight, "weight", torch.float32, dev), _opt(bias, "bias", torch.float32, dev, E),
          _check(enc, "enc", torch.float32, dev), _opt(done, "done", torch.float32, dev, M), M, E,
          K, enc.shape[1], 1 if relu else 0)
+    return enc
+
+
+def linear_cache_ring(x, weight, bias, enc, slot: int, done=None, relu: bool = True):
+    """The rollout's last encoder layer writing the frame-encoding RING: fresh = act(x @ weight.T
+    + bias) overwrites physical slot `slot` of enc [M, W, E] (every slot of an env with
+    done != 0); nothing is shifted (ocppo_linear_cache_ring; read back with
+    linear_act(..., ring=(E, rot)))."""
+    if x.dim() != 2 or weight.dim() != 2 or enc.dim() != 3:
+        raise ValueError(f"x [M, K], weight [E, K], enc [M, W, E] expected, got {tuple(x.shape)}, "
+                         f"{tuple(weight.shape)}, {tuple(enc.shape)}")
+    M, K = x.shape
+    E = weight.shape[0]
+    dev = x.device
+    if weight.shape[1] != K or enc.shape[0] != M or enc.shape[2] != E:
+        raise ValueError(f"shapes: x {tuple(x.shape)}, weight {tuple(weight.shape)}, "
+                         f"enc {tuple(enc.shape)}")
+    if x.dtype != torch.float32 or (M > 1 and x.stride(1) != 1) or x.device.type != "cuda":
+        raise ValueError("x must be an f32 GPU tensor with unit column stride")
+    call("ocppo_linear_cache_ring", _stream(dev), x.data_ptr(), x.stride(0) if M > 1 else K,
+         _check(weight, "weight", torch.float32, dev), _opt(bias, "bias", torch.float32, dev, E),
+         _check(enc, "enc", torch.float32, dev), _opt(done, "done", torch.float32, dev, M), M, E,
+         K, enc.shape[1], int(slot), 1 if relu else 0)
     return enc
 
 

@@ -33,7 +33,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from . import frames, ops
-from .agents import NormalizeImg, PPObj, linear_relu, make_agent
+from .agents import NormalizeImg, PPObj, fused_trunk, linear_relu, make_agent
 from .args import Args
 from .envs import HostVecEnv, make_device_env
 
@@ -235,6 +235,10 @@ class PPOTrainer:
         self.rollout_fusion = self.frame_cache and a.rollout_fusion and self._fusable_encoder()
         self.enc_pair = (torch.zeros((N, self.agent.network[2].out_features), dtype=f32, device=dev)
                          if self.rollout_fusion else None)
+        # ... and the cache is a ring (no shift): step t writes the newest encoding over the oldest
+        # (physical slot (t-1) mod W) and the decoder's first layer reads the slots rotated by
+        # t mod W (ocppo_linear_cache_ring / ocppo_linear_act_ring), bit-identical to the shift
+        self.cache_ring = self.rollout_fusion and a.rollout_cache_ring and self._ring_decoder()
         self.ret_state = torch.zeros(N, dtype=torch.float64, device=dev)
         self.rms_state = torch.tensor([0.0, 1.0, 1e-4], dtype=torch.float64, device=dev)
 
@@ -326,6 +330,35 @@ class PPOTrainer:
         return (l1.in_features <= 64 and l1.out_features % 16 == 0 and l1.out_features <= 512
                 and l2.weight.data_ptr() % 16 == 0 and all(m.bias is not None for m in lins))
 
+    def _ring_decoder(self) -> bool:
+        """The decoder's first layer (after the Flatten) is a biased Linear+ReLU that the ring
+        kernel takes (K = W*E, E % 32 == 0) at a batch where it runs on the HIP path anyway."""
+        net, f = self.agent.network, self.agent._flat
+        if len(net) < f + 3 or not isinstance(net[f + 1], nn.Linear) or \
+                not isinstance(net[f + 2], nn.ReLU) or net[f + 1].bias is None:
+            return False
+        E, K = self.agent.encoding_dim, net[f + 1].in_features
+        return E % 32 == 0 and K == self.obs_shape[0] * E and self.N <= 128 and K <= 2048
+
+    def _decode_cache(self, t: int):
+        """Decoder output on the frame-encoding cache at rollout step t."""
+        ag = self.agent
+        if not self.cache_ring:
+            return ag.decode(self.enc_cache)
+        net, f = ag.network, ag._flat
+        W, E = self.enc_cache.shape[1], self.enc_cache.shape[2]
+        lin = net[f + 1]
+        h = ops.linear_act(self.enc_cache.view(self.N, W * E), lin.weight, lin.bias, True,
+                           ring=(E, t % W))
+        rest = net[f + 3:]
+        return fused_trunk(rest, h) if len(rest) else h
+
+    def cache_logical(self, t: int):
+        """The cache in logical slot order (oldest .. newest) at rollout step t (tests)."""
+        if not self.cache_ring:
+            return self.enc_cache
+        return torch.roll(self.enc_cache, -(t % self.enc_cache.shape[1]), dims=1)
+
     # ------------------------------------------------------------------------------------------
     def _reset_env(self):
         frame = self.env.frame if self.host_env else self.env.reset()
@@ -345,14 +378,14 @@ class PPOTrainer:
         if not self.frame_cache:
             return ag.trunk(self.net_obs, self.prescale)
         if t == 0:
-            self.enc_cache.copy_(ag.encode(self.net_obs))
+            self.enc_cache.copy_(ag.encode(self.net_obs))  # logical order: ring offset 0
         elif self.rollout_fusion:
             self._store_encode(t)
         else:
             fresh = ag.encode(self.net_obs[:, -1])
             self.timer.bracket("frame_cache", lambda: ops.frame_cache_shift(
                 self.enc_cache, fresh, self.dones[t]))
-        return ag.decode(self.enc_cache)
+        return self._decode_cache(t)
 
     def _store_encode(self, t: int):
         """Store of step t-1 + encode of step t's newest frame into the cache, in 2 + (encoder
@@ -368,8 +401,13 @@ class PPOTrainer:
         for lin in lins[2:-1]:
             x = linear_relu(x, lin)
         last = lins[-1]
-        self.timer.bracket("cache_linear", lambda: ops.linear_cache_shift(
-            x, last.weight, last.bias, self.enc_cache, self.dones[t]))
+        if self.cache_ring:
+            W = self.enc_cache.shape[1]
+            self.timer.bracket("cache_linear", lambda: ops.linear_cache_ring(
+                x, last.weight, last.bias, self.enc_cache, (t - 1) % W, self.dones[t]))
+        else:
+            self.timer.bracket("cache_linear", lambda: ops.linear_cache_shift(
+                x, last.weight, last.bias, self.enc_cache, self.dones[t]))
 
     def _rollout_step(self, t: int):
         """One env step of the rollout (:500-514): network trunk (PyTorch) → fused HIP policy

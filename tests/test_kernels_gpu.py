@@ -1131,6 +1131,37 @@ def test_linear_cache_shift_equals_linear_then_shift(ops, dev, M, K, E, W):
     assert torch.equal(d[:, :-1], enc0[:, 1:]) and torch.equal(d[:, -1], fresh)
 
 
+@pytest.mark.parametrize("M,K,E,W", [(128, 1024, 512, 4), (50, 96, 64, 3), (128, 512, 32, 1)])
+def test_linear_cache_ring_is_the_shift_rotated(ops, dev, M, K, E, W):
+    """Ring form of the cache: after every step t, the ring rolled by t mod W equals the shifted
+    cache bit for bit (resets included)."""
+    w = torch.randn(E, K, device=dev) * K ** -0.5
+    b = torch.randn(E, device=dev)
+    enc0 = torch.randn(M, W, E, device=dev)
+    shift, ring = enc0.clone(), enc0.clone()
+    for t in range(1, 2 * W + 3):
+        x = torch.relu(torch.randn(M, K, device=dev))
+        done = (torch.rand(M, device=dev) < 0.2).float()
+        ops.linear_cache_shift(x, w, b, shift, done)
+        ops.linear_cache_ring(x, w, b, ring, (t - 1) % W, done)
+        assert torch.equal(torch.roll(ring, -(t % W), dims=1), shift), t
+
+
+@pytest.mark.parametrize("M,W,E,N", [(128, 4, 512, 512), (50, 3, 64, 40), (128, 4, 64, 64),
+                                     (7, 2, 32, 16)])
+def test_linear_act_ring_equals_linear_on_logical_order(ops, dev, M, W, E, N):
+    x = torch.randn(M, W, E, device=dev)
+    w = torch.randn(N, W * E, device=dev) * (W * E) ** -0.5
+    b = torch.randn(N, device=dev)
+    want = ops.linear_act(x.view(M, W * E), w, b, relu=True)
+    for rot in range(W):
+        phys = torch.roll(x, rot, dims=1).contiguous()  # logical s at physical (s + rot) mod W
+        got = ops.linear_act(phys.view(M, W * E), w, b, relu=True, ring=(E, rot))
+        assert torch.equal(got, want), rot
+    with pytest.raises(RuntimeError, match="seg"):
+        ops.linear_act(x.view(M, W * E), w, b, relu=True, ring=(E + 1, 0))
+
+
 # ---------------------------------------------------------------------------------------------
 # policy heads forward + fused PPO loss + heads backward in one pass (ocppo_heads_loss_fwd_bwd)
 # ---------------------------------------------------------------------------------------------

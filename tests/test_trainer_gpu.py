@@ -183,7 +183,7 @@ def test_rollout_frame_cache_matches_full_trunk(dev):
         a._rollout()  # a rollout under fixed weights, no update after it
         torch.cuda.synchronize()
         # the cache holds the encodings of the bootstrap obs (step T)
-        torch.testing.assert_close(a.agent.decode(a.enc_cache), a.agent.trunk(a.net_obs),
+        torch.testing.assert_close(a.agent.decode(a.cache_logical(a.T)), a.agent.trunk(a.net_obs),
                                    rtol=1e-5, atol=1e-5)
         # every step's stored value = the critic on the full stacked obs of that step. The two
         # paths run different f32 GEMM kernels (the rollout's HIP MFMA kernel at N rows vs
@@ -406,6 +406,25 @@ def test_rollout_fusion_matches_unfused_rollout(dev):
     assert same_obs > 0.99, same_obs
     close = ((a.values - b.values).abs() <= 1e-4 + 1e-4 * a.values.abs()).float().mean().item()
     assert close > 0.99, close
+
+
+def test_rollout_cache_ring_is_bitwise_the_shifted_cache(dev):
+    """The frame-encoding cache as a ring (newest encoding over the oldest slot, the decoder reading
+    the slots rotated) gives bit for bit the rollout of the shifted cache: same kernels, same
+    products in the same order, only addresses differ."""
+    runs = []
+    for ring in (False, True):
+        tr, _ = run_iters(small_args(encoder_dims=(32, 64, 48, 64), decoder_dims=(64,),
+                                     rollout_cache_ring=ring, num_steps=18), 2, dev)
+        torch.cuda.synchronize()
+        assert tr.rollout_fusion and tr.cache_ring == ring
+        runs.append(tr)
+    a, b = runs
+    for k in ("obs", "actions", "logprobs", "values", "rewards", "dones", "advantages"):
+        assert torch.equal(getattr(a, k), getattr(b, k)), k
+    assert torch.equal(a.cache_logical(a.T), b.cache_logical(b.T))
+    for p, q in zip(a.agent.parameters(), b.agent.parameters()):
+        assert torch.equal(p, q)
 
 
 def test_fused_heads_loss_updates_match_reference_golden(dev):

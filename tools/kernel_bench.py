@@ -56,7 +56,7 @@ SIZES = {
     # Linear layers at config run the deferred form above, ops.relu_bias_grad_partial)
     "relu_bias_grad_tail": {"config": dict(shapes=((12288, 512), (12288, 1024), (12288, 512))),
                             "scaled": dict(shapes=((262144, 1024),))},
-    # the rollout's last encoder layer + frame-cache shift (M = 128 envs, 1024 -> 512, W = 4)
+    # the rollout's last encoder layer writing the frame-encoding ring (M = 128 envs, 1024 -> 512)
     "cache_linear": {"config": dict(M=128, K=1024, E=512, W=4), "scaled": dict(M=8192, K=1024, E=512, W=4)},
     # the rollout store of step t-1 + the first two encoder layers of step t (F=12 -> 256 -> 512)
     "store_encode": {"config": dict(N=128, W=4, F=12, N1=256, N2=512),
@@ -110,9 +110,9 @@ def case_bytes(name: str, p: dict) -> float:
         # h in + gp out; records (action 8 + 4 x 4) in; [Wa; Wc] + biases in; head grads out
         M, H, A = p["M"], p["H"], p["A"]
         return M * H * 8 + M * 24 + 4 * (A + 1) * (H + 1) + 4 * ((A + 1) * (H + 1) + H) + 36
-    if name == "cache_linear":
-        M, K, E, W = p["M"], p["K"], p["E"], p["W"]
-        return 4 * (M * K + E * (K + 1)) + 4 * M * E * (2 * W - 1) + 4 * M
+    if name == "cache_linear":  # ring form: x + W in, the fresh row written into one slot
+        M, K, E = p["M"], p["K"], p["E"]
+        return 4 * (M * K + E * (K + 1)) + 4 * M * E + 4 * M
     if name == "store_encode":
         N, W, F, N1, N2 = p["N"], p["W"], p["F"], p["N1"], p["N2"]
         store = N * ((W - 1) * F * 2 + F * 4 + W * F * 6 + 8 + 4 + 24 + 4)
@@ -270,8 +270,8 @@ def make_case(name: str, p: dict, dev):
         b = torch.randn(E, device=dev, generator=g)
         enc = torch.randn(M, W, E, device=dev, generator=g)
         done = (torch.rand(M, device=dev, generator=g) < 1 / 3500).float()
-        fn = lambda: ops.linear_cache_shift(x, w, b, enc, done)  # noqa: E731
-        return fn, 4 * (M * K + E * (K + 1)) + 4 * M * E * (2 * W - 1) + 4 * M
+        fn = lambda: ops.linear_cache_ring(x, w, b, enc, 1, done)  # noqa: E731
+        return fn, 4 * (M * K + E * (K + 1)) + 4 * M * E + 4 * M
     if name == "store_encode":
         N, W, F, N1, N2 = p["N"], p["W"], p["F"], p["N1"], p["N2"]
         frame = torch.randint(0, 210, (N, F), device=dev, generator=g).float()
