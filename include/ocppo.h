@@ -524,7 +524,7 @@ OCPPO_API int ocppo_linear_cache_shift(ocppo_stream_t stream, const float* x, in
  *   slot of env m when done[m] != 0 (a reset fills the stack with the new frame). No old slot is
  *   read. done [M] f32 or NULL.
  * ocppo_linear_act_ring: ocppo_linear_act whose x rows are W = K / seg segments of seg floats
- *   stored rotated: logical segment s at physical segment (s + rot) mod W (seg % 32 == 0,
+ *   stored rotated: logical segment s at physical segment (s + rot) mod W (seg a power of two >= 32,
  *   K % seg == 0, x / w 16-B aligned, ldx % 4 == 0). Products and summation order are those of
  *   the logical layout: the decoder (architectures/ppo.py:74-78: Flatten + Linear over the W
  *   frame encodings) on the ring gives bit for bit what it gives on the shifted cache. */

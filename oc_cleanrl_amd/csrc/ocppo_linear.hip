@@ -85,12 +85,13 @@ struct LinStage {
 };
 
 // one group's global loads: instruction i covers lines [8i, 8i+8) of the 16 x 16CH slice
-// Ring (seg > 0): x's K dimension is K / seg segments; logical segment s of a row is stored at
-// physical segment (s + rot) mod (K / seg) (the rollout's frame-encoding ring, seg % 32 == 0, so a
-// 32-float group never straddles a segment). Only the x addresses move: products and their order
+// Ring: x's K dimension is K / seg segments; logical segment s of a row is stored at physical
+// segment (s + rot) mod (K / seg) (the rollout's frame-encoding ring; seg a power of two >= 32, so
+// a 32-float group never straddles a segment). Only the x addresses move: products and their order
 // are those of the logical layout.
 struct XRing {
-  int seg, rot, nseg;
+  int seg_shift;  // log2(seg); 0: no ring (the remap is a shift and a mask: no integer division,
+  int rot, nseg;  // which cost 1.1 us per launch at 128 x 2048 -> 512)
 };
 
 template <int CH>
@@ -108,11 +109,11 @@ __device__ __forceinline__ void lin_stage_load(const float* x, int64_t ldx, cons
     const bool kok = kk < c1 * 16;
     const int ar = row0 + r, bc = col0 + r;
     int kx = kk;
-    if (ring.seg) {
-      const int sg = kk / ring.seg;
+    if (ring.seg_shift) {
+      const int sg = kk >> ring.seg_shift;
       int ps = sg + ring.rot;
       ps = ps >= ring.nseg ? ps - ring.nseg : ps;
-      kx = ps * ring.seg + (kk - sg * ring.seg);
+      kx = (ps << ring.seg_shift) | (kk & ((1 << ring.seg_shift) - 1));
     }
     va[i] = (kok && ar < M) ? *reinterpret_cast<const float4*>(x + static_cast<int64_t>(ar) * ldx + kx)
                             : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -390,9 +391,9 @@ extern "C" int ocppo_linear_act_ring(ocppo_stream_t stream, const float* x, int6
   OCPPO_REQUIRE(M >= 0 && N >= 1 && K >= 1 && M <= INT32_MAX && N <= INT32_MAX && K <= INT32_MAX,
                 "ocppo_linear_act_ring: bad sizes M=%lld N=%lld K=%lld", (long long)M, (long long)N,
                 (long long)K);
-  OCPPO_REQUIRE(seg >= 32 && seg % 32 == 0 && K % seg == 0 && rot >= 0 && rot < K / seg,
-                "ocppo_linear_act_ring: seg=%lld rot=%lld (seg %% 32 == 0, K %% seg == 0, "
-                "0 <= rot < K / seg)", (long long)seg, (long long)rot);
+  OCPPO_REQUIRE(seg >= 32 && (seg & (seg - 1)) == 0 && K % seg == 0 && rot >= 0 && rot < K / seg,
+                "ocppo_linear_act_ring: seg=%lld rot=%lld (seg a power of two >= 32, K %% seg == "
+                "0, 0 <= rot < K / seg)", (long long)seg, (long long)rot);
   OCPPO_REQUIRE(ldx >= K && ldy >= N && ldx % 4 == 0,
                 "ocppo_linear_act_ring: leading dimensions ldx=%lld ldy=%lld", (long long)ldx,
                 (long long)ldy);
@@ -401,7 +402,8 @@ extern "C" int ocppo_linear_act_ring(ocppo_stream_t stream, const float* x, int6
   OCPPO_REQUIRE(reinterpret_cast<uintptr_t>(x) % 16 == 0 && reinterpret_cast<uintptr_t>(w) % 16 == 0,
                 "ocppo_linear_act_ring: x and w must be 16-B aligned");
   OCPPO_REQUIRE((M + 15) / 16 * ((N + 15) / 16) <= INT32_MAX / 8, "ocppo_linear_act_ring: too large");
-  const XRing ring{static_cast<int>(seg), static_cast<int>(rot), static_cast<int>(K / seg)};
+  const XRing ring{__builtin_ctzll(static_cast<unsigned long long>(seg)), static_cast<int>(rot),
+                   static_cast<int>(K / seg)};
   clear_stale_error();
   hipStream_t s = as_stream(stream);
   if (relu)

@@ -332,13 +332,15 @@ class PPOTrainer:
 
     def _ring_decoder(self) -> bool:
         """The decoder's first layer (after the Flatten) is a biased Linear+ReLU that the ring
-        kernel takes (K = W*E, E % 32 == 0) at a batch where it runs on the HIP path anyway."""
+        kernel takes (K = W*E, E a power of two >= 32) at a batch where it runs on the HIP path
+        anyway."""
         net, f = self.agent.network, self.agent._flat
         if len(net) < f + 3 or not isinstance(net[f + 1], nn.Linear) or \
                 not isinstance(net[f + 2], nn.ReLU) or net[f + 1].bias is None:
             return False
         E, K = self.agent.encoding_dim, net[f + 1].in_features
-        return E % 32 == 0 and K == self.obs_shape[0] * E and self.N <= 128 and K <= 2048
+        return (E >= 32 and E & (E - 1) == 0 and K == self.obs_shape[0] * E and self.N <= 128
+                and K <= 2048)
 
     def _decode_cache(self, t: int):
         """Decoder output on the frame-encoding cache at rollout step t."""

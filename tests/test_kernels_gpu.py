@@ -1160,6 +1160,12 @@ def test_linear_act_ring_equals_linear_on_logical_order(ops, dev, M, W, E, N):
         assert torch.equal(got, want), rot
     with pytest.raises(RuntimeError, match="seg"):
         ops.linear_act(x.view(M, W * E), w, b, relu=True, ring=(E + 1, 0))
+    with pytest.raises(RuntimeError, match="seg"):  # not a power of two
+        ops.linear_act(torch.zeros(4, 192, device=dev), torch.zeros(8, 192, device=dev), None,
+                       ring=(96, 1))
+    with pytest.raises(RuntimeError, match="seg"):  # not a power of two
+        ops.linear_act(torch.zeros(4, 96 * 2, device=dev), torch.zeros(8, 192, device=dev), None,
+                       ring=(96, 1))
 
 
 # ---------------------------------------------------------------------------------------------
