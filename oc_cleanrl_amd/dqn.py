@@ -309,7 +309,7 @@ class DQNTrainer:
             torch.cuda.synchronize(self.dev)
             g = torch.cuda.CUDAGraph()
             cur = self.cur
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 self._chunk(train)
             # capture recorded the work without running it: restore the host-side stack parity
             self.cur = cur

@@ -108,7 +108,7 @@ class KernelTimer:
             fn()
             torch.cuda.synchronize()
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with _graph_capture(g):
                 for _ in range(reps):
                     fn()
             g.replay()
@@ -122,6 +122,14 @@ class KernelTimer:
             self.mean_us[name] = 1e3 * a.elapsed_time(b) / (reps * rounds)
             del g
         return self.mean_us
+
+
+def _graph_capture(graph, pool=None):
+    """hipGraph capture in thread-local mode: the RCCL process group's watchdog thread polls its
+    work events (hipEventQuery) while this thread captures, which global-mode capture turns into
+    hipErrorStreamCaptureUnsupported and a process abort (seen once in 3 runs of the 1-rank nccl
+    test, tests/test_dp_gpu.py). Only this thread's calls are restricted, as they must be."""
+    return torch.cuda.graph(graph, pool=pool, capture_error_mode="thread_local")
 
 
 class PPOTrainer:
@@ -685,13 +693,13 @@ class PPOTrainer:
         pool = None
         if not self.host_env:
             self.g_rollout = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.g_rollout):
+            with _graph_capture(self.g_rollout):
                 self._rollout()
             pool = self.g_rollout.pool()
         else:  # a host env steps between the parts: one graph per part
             for k in range(self.T + 1):
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, pool=pool):
+                with _graph_capture(g, pool):
                     self._host_part(k)
                 pool = pool if pool is not None else g.pool()
                 self.g_host.append(g)
@@ -700,24 +708,24 @@ class PPOTrainer:
         elif not self.dp:
             for e in range(self.E):
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, pool=pool):
+                with _graph_capture(g, pool):
                     self._update_epoch(e)
                 self.g_update.append(g)
                 pool = pool if pool is not None else g.pool()
         else:
             for j in range(self.E * self.nmb):
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, pool=pool):
+                with _graph_capture(g, pool):
                     self._forward_backward(j)
                 self.g_update.append(g)
                 pool = pool if pool is not None else g.pool()
                 if self.split:  # second backward phase: reads the cut tensors of graph j
                     g = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g, pool=pool):
+                    with _graph_capture(g, pool):
                         self._backward_low(j)
                     self.g_low.append(g)
             self.g_opt = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.g_opt, pool=pool):
+            with _graph_capture(self.g_opt, pool):
                 self._opt_step()
         self.graphs_ready = True
 
