@@ -42,7 +42,8 @@ PMC_KEYS = {"action_head": "policy_head_config", "gae": "gae_config",
             "ppo_loss": "ppo_loss_prepared_config", "relu_bias_grad": "relu_bias_grad_config",
             "cache_linear": "cache_linear_config", "store_encode": "store_encode_config",
             "heads_bwd": "heads_bwd_config", "relu_bias_wgrad": "relu_bias_wgrad_config",
-            "heads_loss": "heads_loss_config"}
+            "heads_loss": "heads_loss_config", "decoder": "decoder_config",
+            "encoder_mid": "encoder_mid_config"}
 
 
 def pmc_traffic(key):
@@ -91,6 +92,14 @@ def kernel_bytes(tr) -> dict:
         # slots read, W written)
         kb["cache_linear"] = (4 * (N * Kl + E * (Kl + 1)) + 4 * N +
                               (4 * N * E if tr.cache_ring else 4 * N * E * (2 * W - 1)))
+    if tr.rollout_fusion and len(lins) > 3:
+        mid = lins[2]  # the first middle encoder layer, x [N, K] + W + b in, y out
+        kb["encoder_mid"] = 4 * (N * mid.in_features + mid.out_features * (mid.in_features + 1) +
+                                 N * mid.out_features)
+    if tr.cache_ring:
+        dec = tr.agent.network[tr.agent._flat + 1]
+        kb["decoder"] = 4 * (N * dec.in_features + dec.out_features * (dec.in_features + 1) +
+                             N * dec.out_features)
     if tr.fused_heads_loss:
         Hh, A1 = tr.H, tr.A + 1
         kb["heads_loss"] = (M * Hh * 8 + M * 24 + 4 * A1 * (Hh + 1) + 4 * (A1 * (Hh + 1) + Hh)
@@ -118,6 +127,11 @@ def kernel_flops(tr) -> dict:
         fl["store_encode"] = 2 * tr.N * (lins[0].in_features * lins[0].out_features +
                                          lins[1].in_features * lins[1].out_features)
         fl["cache_linear"] = 2 * tr.N * lins[-1].in_features * lins[-1].out_features
+        if len(lins) > 3:
+            fl["encoder_mid"] = 2 * tr.N * lins[2].in_features * lins[2].out_features
+    if tr.cache_ring:
+        dec = tr.agent.network[tr.agent._flat + 1]
+        fl["decoder"] = 2 * tr.N * dec.in_features * dec.out_features
     return fl
 
 

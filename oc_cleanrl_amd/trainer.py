@@ -358,8 +358,8 @@ class PPOTrainer:
         net, f = ag.network, ag._flat
         W, E = self.enc_cache.shape[1], self.enc_cache.shape[2]
         lin = net[f + 1]
-        h = ops.linear_act(self.enc_cache.view(self.N, W * E), lin.weight, lin.bias, True,
-                           ring=(E, t % W))
+        h = self.timer.bracket("decoder", lambda: ops.linear_act(
+            self.enc_cache.view(self.N, W * E), lin.weight, lin.bias, True, ring=(E, t % W)))
         rest = net[f + 3:]
         return fused_trunk(rest, h) if len(rest) else h
 
@@ -408,8 +408,9 @@ class PPOTrainer:
             self.dones[t], self.rewards[t - 1], lins[0].weight, lins[0].bias, lins[1].weight,
             lins[1].bias, self.enc_pair, vecnorm_state=vn))
         x = self.enc_pair
-        for lin in lins[2:-1]:
-            x = linear_relu(x, lin)
+        for i, lin in enumerate(lins[2:-1]):
+            x = self.timer.bracket("encoder_mid" if i == 0 else f"encoder_mid{i}",
+                                   lambda x=x, lin=lin: linear_relu(x, lin))
         last = lins[-1]
         if self.cache_ring:
             W = self.enc_cache.shape[1]

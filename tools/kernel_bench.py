@@ -41,13 +41,13 @@ SIZES = {
     "mb_prepare": {"config": dict(M=4096, nmb=16, B=16384), "scaled": dict(M=16384, nmb=256, B=1 << 20)},
     "ppo_loss_prepared": {"config": dict(M=4096, A=6), "scaled": dict(M=4 * 1024 * 1024, A=6)},
     "policy_head": {"config": dict(N=128, H=512, A=6), "scaled": dict(N=262144, H=512, A=6)},
-    # the three Linear->ReLU backward launches of one config-2 minibatch (dedup capacity 12288
+    # the three Linear->ReLU backward launches of one config-2 minibatch (dedup capacity 11520
     # encoder rows: layers 512/1024/512 -- the first layer (256) runs relu_bias_wgrad, the decoder
-    # (4096 x 512) heads_bwd), and one streaming-size launch
-    "relu_bias_grad": {"config": dict(shapes=((12288, 512), (12288, 1024), (12288, 512))),
+    # (4096 x 512) heads_loss), and one streaming-size launch
+    "relu_bias_grad": {"config": dict(shapes=((11520, 512), (11520, 1024), (11520, 512))),
                        "scaled": dict(shapes=((262144, 1024),))},
     # the first encoder layer's fused ReLU-backward + bias + weight gradient (F = 12 -> 256)
-    "relu_bias_wgrad": {"config": dict(R=12288, N=256, K=12), "scaled": dict(R=262144, N=256, K=12)},
+    "relu_bias_wgrad": {"config": dict(R=11520, N=256, K=12), "scaled": dict(R=262144, N=256, K=12)},
     # actor + critic heads' backward with the decoder's ReLU mask + bias grad (M = 4096, H = 512)
     "heads_bwd": {"config": dict(M=4096, H=512, A=6), "scaled": dict(M=262144, H=512, A=6)},
     # policy heads forward + fused PPO loss + heads backward (both launches: rows, then records)
@@ -58,6 +58,10 @@ SIZES = {
                             "scaled": dict(shapes=((262144, 1024),))},
     # the rollout's last encoder layer writing the frame-encoding ring (M = 128 envs, 1024 -> 512)
     "cache_linear": {"config": dict(M=128, K=1024, E=512, W=4), "scaled": dict(M=8192, K=1024, E=512, W=4)},
+    # the rollout decoder on the frame-encoding ring (128 envs, W*E = 4*512 -> 512, rot 1) and the
+    # middle encoder layer (512 -> 1024): the LDS-staged f32-MFMA Linear kernel
+    "decoder": {"config": dict(M=128, K=2048, N=512, seg=512), "scaled": dict(M=8192, K=2048, N=512, seg=512)},
+    "encoder_mid": {"config": dict(M=128, K=512, N=1024), "scaled": dict(M=8192, K=512, N=1024)},
     # the rollout store of step t-1 + the first two encoder layers of step t (F=12 -> 256 -> 512)
     "store_encode": {"config": dict(N=128, W=4, F=12, N1=256, N2=512),
                      "scaled": dict(N=8192, W=4, F=12, N1=256, N2=512)},
@@ -66,6 +70,8 @@ SIZES = {
 # useful flops per launch of the MFMA kernels (2 per multiply-add)
 FLOPS = {
     "cache_linear": lambda p: 2 * p["M"] * p["K"] * p["E"],
+    "decoder": lambda p: 2 * p["M"] * p["K"] * p["N"],
+    "encoder_mid": lambda p: 2 * p["M"] * p["K"] * p["N"],
     "store_encode": lambda p: 2 * p["N"] * (p["F"] * p["N1"] + p["N1"] * p["N2"]),
 }
 
@@ -113,6 +119,9 @@ def case_bytes(name: str, p: dict) -> float:
     if name == "cache_linear":  # ring form: x + W in, the fresh row written into one slot
         M, K, E = p["M"], p["K"], p["E"]
         return 4 * (M * K + E * (K + 1)) + 4 * M * E + 4 * M
+    if name in ("decoder", "encoder_mid"):  # x + W + b in, y out
+        M, K, N = p["M"], p["K"], p["N"]
+        return 4 * (M * K + N * (K + 1) + M * N)
     if name == "store_encode":
         N, W, F, N1, N2 = p["N"], p["W"], p["F"], p["N1"], p["N2"]
         store = N * ((W - 1) * F * 2 + F * 4 + W * F * 6 + 8 + 4 + 24 + 4)
@@ -272,6 +281,15 @@ def make_case(name: str, p: dict, dev):
         done = (torch.rand(M, device=dev, generator=g) < 1 / 3500).float()
         fn = lambda: ops.linear_cache_ring(x, w, b, enc, 1, done)  # noqa: E731
         return fn, 4 * (M * K + E * (K + 1)) + 4 * M * E + 4 * M
+    if name in ("decoder", "encoder_mid"):
+        M, K, N = p["M"], p["K"], p["N"]
+        x = torch.relu(torch.randn(M, K, device=dev, generator=g))
+        w = torch.randn(N, K, device=dev, generator=g) * K ** -0.5
+        b = torch.randn(N, device=dev, generator=g)
+        y = torch.empty(M, N, device=dev)
+        ring = (p["seg"], 1) if "seg" in p else None
+        fn = lambda: ops.linear_act(x, w, b, True, out=y, ring=ring)  # noqa: E731
+        return fn, case_bytes(name, p)
     if name == "store_encode":
         N, W, F, N1, N2 = p["N"], p["W"], p["F"], p["N1"], p["N2"]
         frame = torch.randint(0, 210, (N, F), device=dev, generator=g).float()

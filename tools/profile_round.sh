@@ -18,7 +18,8 @@ for case in "policy_head config" "gae config" "ppo_loss_prepared config" \
             "gae scaled" "ppo_loss_prepared scaled" "policy_head scaled" "rollout_store scaled" \
             "gather scaled" "relu_bias_grad config" "relu_bias_grad scaled" \
             "relu_bias_wgrad config" "heads_bwd config" "heads_loss config" "heads_loss scaled" \
-            "cache_linear config" "store_encode config" "gather_pixels config"; do
+            "cache_linear config" "store_encode config" "gather_pixels config" \
+            "decoder config" "encoder_mid config"; do
   set -- $case
   for ctr in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 240 rocprofv3 --pmc "$ctr" --kernel-trace --output-format csv \

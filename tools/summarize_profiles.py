@@ -35,6 +35,8 @@ KERNEL_SUBSTR = {
     "heads_loss": ("heads_loss_kernel", "heads_loss_finish_kernel"),
     "cache_linear": ("linear_rows_kernel",),
     "store_encode": ("store_linear2_kernel",),
+    "decoder": ("linear_rows_kernel",),
+    "encoder_mid": ("linear_rows_kernel",),
 }
 
 
