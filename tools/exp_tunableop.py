@@ -47,8 +47,8 @@ for M, K, N, per_iter in [(128, 512, 1024, 128), (128, 1024, 512, 129), (128, 20
     t = timeit(lambda: torch._addmm_activation(b, x, w.t(), use_gelu=False))
     total += t * per_iter
     print(f"[{tag}] rollout M={M} K={K} N={N} fwd {t:7.2f} us", flush=True)
-# update: 16 minibatches; encoder rows 12288, decoder rows 4096
-for M, K, N in [(12288, 256, 512), (12288, 512, 1024), (12288, 1024, 512), (4096, 2048, 512)]:
+# update: 16 minibatches; encoder rows 11520 (dedup capacity), decoder rows 4096
+for M, K, N in [(11520, 256, 512), (11520, 512, 1024), (11520, 1024, 512), (4096, 2048, 512)]:
     x, w, b = (torch.randn(M, K, device=dev), torch.randn(N, K, device=dev),
                torch.randn(N, device=dev))
     gp = torch.randn(M, N, device=dev)
