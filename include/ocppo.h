@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define OCPPO_ABI_VERSION 12
+#define OCPPO_ABI_VERSION 11
 
 /* status codes */
 #define OCPPO_OK 0
@@ -57,12 +57,6 @@ extern "C" {
 #define OCPPO_STAT_ADV_MEAN 7      /* minibatch advantage mean used by the norm      :577-579 */
 #define OCPPO_STAT_ADV_STD 8       /* minibatch advantage std (unbiased)             :577-579 */
 #define OCPPO_NUM_STATS 9
-
-/* epilogues of ocppo_gemm */
-#define OCPPO_GEMM_STORE 0     /* C = acc */
-#define OCPPO_GEMM_BIAS 1      /* C = acc + bias[n] */
-#define OCPPO_GEMM_BIAS_RELU 2 /* C = max(acc + bias[n], 0) (torch._addmm_activation's order) */
-#define OCPPO_GEMM_MASK_DB 3   /* C = mask[m, n] > 0 ? acc : 0, dbp[m / BM, n] = column sums */
 
 typedef void* ocppo_stream_t; /* hipStream_t */
 
@@ -566,29 +560,6 @@ OCPPO_API int ocppo_store_linear2(ocppo_stream_t stream, const float* frame, con
 OCPPO_API int ocppo_cartpole_step(ocppo_stream_t stream, uint64_t seed, const int64_t* actions,
                                   int64_t N, double* state, int64_t* counters, float* obs_out,
                                   float* reward_out, float* done_out, float* ep_state);
-
-/* ---------------------------------------------------------------------------------------------
- * Update-phase GEMM on the f32 matrix cores (the minibatch forward / backward of the Linear
- * layers, ppo_atari_oc.py:566-606 through architectures/ppo.py:60-84; replaces the BLAS calls
- * torch makes for F.linear / addmm / mm there):
- *   C_s[m, n] = epilogue( sum_{k in split s} A(m, k) B(n, k) ),  s = 0 .. splits-1
- *   A(m, k) = a[m * sam + k * sak], B(n, k) = b[n * sbn + k * sbk]: for each operand one stride
- *   is 1 and the other a multiple of 4; a, b 16-B aligned. Split s reduces over
- *   k in [s K / splits, (s+1) K / splits) into C_s = c + s * split_stride_c (plain store only).
- *   C[m, n] = c[m * ldc + n]. M, N multiples of the tile (64 or 128), K % (32 splits) == 0.
- *   epilogue: OCPPO_GEMM_*; bias [N] for the bias forms; MASK_DB: mask [M, ldmask] (the ReLU
- *   output whose backward this fuses), dbp [M / BM, N] receives the per-row-tile column sums of
- *   C (BM = 32 * (tile / 10)).
- *   tile: 0 = automatic (ocppo_gemm_tile), or 44 / 42 / 24 / 22 = (BM / 32) * 10 + BN / 32.
- * Deterministic (fixed per-tile summation order, no atomics). Graph-capturable.
- * ------------------------------------------------------------------------------------------- */
-OCPPO_API int ocppo_gemm(ocppo_stream_t stream, int64_t M, int64_t N, int64_t K, const float* a,
-                         int64_t sam, int64_t sak, const float* b, int64_t sbn, int64_t sbk,
-                         float* c, int64_t ldc, int64_t splits, int64_t split_stride_c,
-                         int epilogue, const float* bias, const float* mask, int64_t ldmask,
-                         float* dbp, int tile);
-/* the tile ocppo_gemm picks for tile = 0 (0 if none fits) */
-OCPPO_API int ocppo_gemm_tile(int64_t M, int64_t N, int64_t splits);
 
 #ifdef __cplusplus
 }

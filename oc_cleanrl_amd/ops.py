@@ -768,69 +768,6 @@ def sum_splits(part, out=None):
 # ---------------------------------------------------------------------------------------------
 # Frame-deduplicated PPObj minibatch encoder (ppo_atari_oc.py:566 through architectures/ppo.py:60-84)
 # ---------------------------------------------------------------------------------------------
-GEMM_STORE, GEMM_BIAS, GEMM_BIAS_RELU, GEMM_MASK_DB = 0, 1, 2, 3
-
-
-def gemm_tile(M: int, N: int, splits: int = 1) -> int:
-    """The tile ocppo_gemm picks by itself (0: none fits): (BM / 32) * 10 + BN / 32."""
-    return int(_lib.LIB.ocppo_gemm_tile(M, N, splits))
-
-
-def gemm_ok(M: int, N: int, K: int, splits: int = 1) -> bool:
-    """Shapes the f32-MFMA GEMM takes: M, N multiples of 64 (a tile fits), K % (32 splits) == 0."""
-    return M > 0 and N > 0 and K > 0 and K % (32 * splits) == 0 and gemm_tile(M, N, splits) != 0
-
-
-def linear_fwd(x, w, b=None, relu: bool = False, out=None, tile: int = 0):
-    """y = act(x W^T + b) for x [M, K], W [N, K] (the update forward of a Linear(+ReLU),
-    architectures/ppo.py:60-84), one ocppo_gemm launch with the bias / ReLU epilogue."""
-    M, K = x.shape
-    N = w.shape[0]
-    dev = x.device
-    f = torch.float32
-    if out is None:
-        out = torch.empty((M, N), dtype=f, device=dev)
-    epi = GEMM_STORE if b is None else (GEMM_BIAS_RELU if relu else GEMM_BIAS)
-    if b is None and relu:
-        raise ValueError("linear_fwd: ReLU without a bias is not an epilogue of ocppo_gemm")
-    call("ocppo_gemm", _stream(dev), M, N, K, _check(x, "x", f, dev), K, 1,
-         _check(w, "w", f, dev, N * K), K, 1, _check(out, "out", f, dev, M * N), N, 1, 0, epi,
-         _opt(b, "b", f, dev, N), None, 0, None, tile)
-    return out
-
-
-def linear_dx(g, w, out=None, mask=None, dbp=None, tile: int = 0):
-    """dx = g W for g [M, N] (the gradient at a Linear's output, ReLU mask applied), W [N, K].
-    With mask (the ReLU output of the layer BELOW, [M, K]): dx = mask > 0 ? g W : 0 and dbp
-    [M / BM, K] receives its per-row-tile column sums (that layer's bias-gradient partials)."""
-    M, N = g.shape
-    K = w.shape[1]
-    dev = g.device
-    f = torch.float32
-    if out is None:
-        out = torch.empty((M, K), dtype=f, device=dev)
-    epi = GEMM_STORE if mask is None else GEMM_MASK_DB
-    call("ocppo_gemm", _stream(dev), M, K, N, _check(g, "g", f, dev), N, 1,
-         _check(w, "w", f, dev, N * K), 1, K, _check(out, "out", f, dev, M * K), K, 1, 0, epi,
-         None, _opt(mask, "mask", f, dev, M * K), K, _opt(dbp, "dbp", f, dev), tile)
-    return out
-
-
-def linear_dw(g, x, splits: int, out=None, tile: int = 0):
-    """Split-K partials of dW = g^T x for g [R, N], x [R, K]: out [splits, N, K], split s the
-    rows [s R / splits, (s + 1) R / splits) (summed by sum_splits / sum_splits_db)."""
-    R, N = g.shape
-    K = x.shape[1]
-    dev = g.device
-    f = torch.float32
-    if out is None:
-        out = torch.empty((splits, N, K), dtype=f, device=dev)
-    call("ocppo_gemm", _stream(dev), N, K, R, _check(g, "g", f, dev), 1, N,
-         _check(x, "x", f, dev, R * K), 1, K, _check(out, "out", f, dev, splits * N * K), K,
-         splits, N * K, GEMM_STORE, None, None, 0, None, tile)
-    return out
-
-
 def _obs_TNWF(obs):
     if obs.dim() != 4:
         raise ValueError(f"obs must be [T+1, N, W, F], got {tuple(obs.shape)}")
