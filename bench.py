@@ -43,7 +43,6 @@ PMC_KEYS = {"action_head": "policy_head_config", "gae": "gae_config",
             "cache_linear": "cache_linear_config", "store_encode": "store_encode_config",
             "heads_bwd": "heads_bwd_config", "relu_bias_wgrad": "relu_bias_wgrad_config",
             "heads_loss": "heads_loss_config", "decoder": "decoder_config",
-            "decoder_head": "decoder_head_config",
             "encoder_mid": "encoder_mid_config"}
 
 
@@ -101,11 +100,6 @@ def kernel_bytes(tr) -> dict:
         dec = tr.agent.network[tr.agent._flat + 1]
         kb["decoder"] = 4 * (N * dec.in_features + dec.out_features * (dec.in_features + 1) +
                              N * dec.out_features)
-    if tr.dec_head:  # x + W + b + head weights + noise in; action, log-prob, value out
-        dec = tr.agent.network[tr.agent._flat + 1]
-        Kd, Nd = dec.in_features, dec.out_features
-        kb["decoder_head"] = (4 * (N * Kd + Nd * (Kd + 1) + (A + 1) * (Nd + 1) + N * A) +
-                              16 * N)
     if tr.fused_heads_loss:
         Hh, A1 = tr.H, tr.A + 1
         kb["heads_loss"] = (M * Hh * 8 + M * 24 + 4 * A1 * (Hh + 1) + 4 * (A1 * (Hh + 1) + Hh)
@@ -138,8 +132,6 @@ def kernel_flops(tr) -> dict:
     if tr.cache_ring:
         dec = tr.agent.network[tr.agent._flat + 1]
         fl["decoder"] = 2 * tr.N * dec.in_features * dec.out_features
-        if tr.dec_head:
-            fl["decoder_head"] = 2 * tr.N * dec.out_features * (dec.in_features + tr.A + 1)
     return fl
 
 

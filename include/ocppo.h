@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define OCPPO_ABI_VERSION 12
+#define OCPPO_ABI_VERSION 11
 
 /* status codes */
 #define OCPPO_OK 0
@@ -536,30 +536,6 @@ OCPPO_API int ocppo_linear_act_ring(ocppo_stream_t stream, const float* x, int64
                                     const float* w, const float* b, float* y, int64_t ldy,
                                     int64_t M, int64_t N, int64_t K, int64_t seg, int64_t rot,
                                     int relu);
-/* ---------------------------------------------------------------------------------------------
- * The rollout step's last trunk layer and its policy heads in ONE launch (ppo_atari_oc.py:506
- * `agent.get_action_and_value(next_obs)`: architectures/ppo.py:81-95 on the PPObj decoder):
- *   h = relu(x W^T + b)   x [M, K] read through the frame-encoding ring as ocppo_linear_act_ring
- *                         (seg = 0: plain x), W [N, K], b [N] or NULL -- h is not stored
- *   then exactly ocppo_policy_head_sample(h, ...): actor logits + critic value, Categorical
- *   sample with the given Exp(1) noise [M, A], log-prob, entropy (entropy_out / logits_out may
- *   be NULL). K % 16 == 0, A <= 7, x / w 16-B aligned, ldx % 4 == 0.
- * Each 16 x 16 tile of h contributes partial head dot products (its 16 columns, in order); the
- * last of a row tile's column workgroups (one counter per row tile, agent-scope release /
- * acquire) sums them in column-tile order and samples. Workspace 256-B aligned, >=
- * ocppo_linear_head_workspace_bytes(M, N), ZEROED before first use (counters re-arm). The head
- * sums run in a different order than ocppo_policy_head_sample's (logits agree to f32 rounding);
- * the sampling tail is the same code. Deterministic.
- * ------------------------------------------------------------------------------------------- */
-OCPPO_API size_t ocppo_linear_head_workspace_bytes(int64_t M, int64_t N);
-OCPPO_API int ocppo_linear_head_ring(ocppo_stream_t stream, const float* x, int64_t ldx,
-                                     const float* w, const float* b, int64_t M, int64_t N,
-                                     int64_t K, int64_t seg, int64_t rot, const float* w_actor,
-                                     const float* b_actor, const float* w_critic,
-                                     const float* b_critic, const float* noise, int64_t A,
-                                     int64_t* action_out, float* logprob_out, float* entropy_out,
-                                     float* value_out, float* logits_out, void* workspace,
-                                     size_t workspace_bytes);
 OCPPO_API int ocppo_store_linear2(ocppo_stream_t stream, const float* frame, const float* reward,
                                   const float* done, int64_t N, int64_t W, int64_t D,
                                   const void* prev_obs, void* obs_out, int obs_dtype,

@@ -120,7 +120,6 @@ class Args:
     rollout_fusion: bool = True  # PPO_OBJ rollout: store + first encoder layers in one launch,
                                  # cache shift in the last encoder layer's epilogue
     rollout_cache_ring: bool = True  # ... the cache as a ring the decoder reads rotated (no shift)
-    rollout_decoder_head: bool = False  # ... the decoder + policy heads + sample in one launch
     update_frame_dedup: bool = True  # PPO_OBJ update: encode each distinct frame of a minibatch once
     prefetch_shuffle: bool = True  # shuffle (+ frame plan) of the next iteration while the GPU runs
     per_step_noise: bool = False  # rollout sampling noise drawn per step ([N, A], the reference's

@@ -23,7 +23,6 @@
 //   * bias + ReLU fused in the epilogue (torch._addmm_activation's order: acc + b, then max(., 0)).
 // Roofline: MFMA-bound in principle (2*M*N*K flops), latency-bound at these sizes.
 #include "ocppo_common.h"
-#include "ocppo_categorical.h"
 
 namespace ocppo {
 
@@ -414,230 +413,6 @@ extern "C" int ocppo_linear_act_ring(ocppo_stream_t stream, const float* x, int6
     launch_linear<false>(s, true, x, ldx, w, b, y, ldy, (int)M, (int)N, (int)K,
                          CacheOut{nullptr, nullptr, 0, -1}, ring);
   return check_launch("ocppo_linear_act_ring");
-}
-
-namespace ocppo {
-
-// ---- the rollout decoder + policy heads + Categorical sample in ONE launch ----------------------
-// The last trunk layer of the rollout step (the PPObj decoder on the frame-encoding ring, M = N
-// envs <= a few hundred rows) followed by ocppo_policy_head_sample's work (architectures/ppo.py:
-// 81-95 at ppo_atari_oc.py:506): h = relu(x W^T + b) is never stored. Each workgroup's 16 x 16
-// tile of h (linear_rows' staged MFMA path) is turned into partial head dot products -- its 16
-// rows against the A actor rows and the critic row over its 16 columns, summed in column order --
-// written to the workspace with write-through (sc1) stores; the last of the row tile's ntn column
-// workgroups to arrive (one counter per row tile; sc1 loads of the partials, so neither a release
-// nor an acquire fence: MI355X guide §6 Guideline 16, "Valid forms") adds
-// the ntn partials in column-tile order, adds the biases and runs the Categorical tail of the
-// head kernel (same helpers, same noise) for the tile's 16 envs. Deterministic; one kernel
-// boundary and the h round trip fewer per env step.
-struct HeadArgs {
-  const float* wa;  // [A, N]
-  const float* ba;  // [A]
-  const float* wc;  // [N]
-  const float* bc;  // [1]
-  const float* noise;  // [M, A] Exp(1)
-  int A;
-  int64_t* action;
-  float* logprob;
-  float* entropy;  // may be NULL
-  float* value;
-  float* logits;   // may be NULL
-  float* part;     // [ntn][mpad][8]
-  unsigned* cnt;   // [ntm] x 32 (one 128-B line per row tile), zero between launches
-  int ntn, mpad;
-};
-constexpr int kHeadCntStride = 32;
-
-template <int S>
-__global__ __launch_bounds__(64 * S) void linear_head_kernel(
-    const float* __restrict__ x, int64_t ldx, const float* __restrict__ w,
-    const float* __restrict__ bias, int M, int N, int K, int ntm, int tiles, XRing ring,
-    HeadArgs h) {
-  __shared__ floatx4 red[S > 1 ? S - 1 : 1][64];
-  __shared__ float hs[16][17];
-  __shared__ float ls[16][9];
-  extern __shared__ __attribute__((aligned(16))) unsigned char lin_stage_raw[];
-  const int b = blockIdx.x;
-  const int per_xcd = (tiles + 7) / 8;
-  const int t = (b % 8) * per_xcd + b / 8;  // XCD-contiguous tile ranges (as linear_rows)
-  if (t >= tiles) return;
-  const int tm = t % ntm, tn = t / ntm;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int g = lane >> 4, c16 = lane & 15;
-  const int nch = K / 16;
-  const int cpw = (nch + S - 1) / S;
-  const int c0 = wv * cpw;
-  const int c1 = c0 + cpw < nch ? c0 + cpw : nch;
-  // wave 0's epilogue operands, loaded before the K loop so that their latency hides behind it:
-  // this lane's (row, two head outputs) weights over the tile's 16 columns, their biases, the
-  // decoder bias of its column and (lanes < 16) the noise row of the env it may sample
-  const int row = lane >> 2;
-  const int ocol = tn * 16 + c16;
-  float hw[2][16], hb[2], nz[7], bv = 0.f;
-  if (wv == 0) {
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int o = (lane & 3) * 2 + q;
-      const float* wr = o < h.A ? h.wa + static_cast<int64_t>(o) * N : (o == 7 ? h.wc : nullptr);
-#pragma unroll
-      for (int c = 0; c < 16; ++c) hw[q][c] = (wr && tn * 16 + c < N) ? wr[tn * 16 + c] : 0.f;
-      hb[q] = o < h.A ? h.ba[o] : (o == 7 ? h.bc[0] : 0.f);
-    }
-    const int64_t n = static_cast<int64_t>(tm) * 16 + lane;
-#pragma unroll
-    for (int j = 0; j < 7; ++j) nz[j] = (lane < 16 && n < M && j < h.A) ? h.noise[n * h.A + j] : 1.f;
-    bv = (ocol < N && bias) ? bias[ocol] : 0.f;
-  }
-  floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-  LinStage<2>* st = reinterpret_cast<LinStage<2>*>(lin_stage_raw) + wv;
-  linear_wave_chunks_lds<2>(x, ldx, w, K, tm * 16, tn * 16, M, N, lane, c0, c1, *st, acc0, acc1,
-                            ring);
-  floatx4 acc = acc0 + acc1;
-  if (S > 1) {
-    if (wv > 0) red[wv - 1][lane] = acc;
-    __syncthreads();
-    if (wv > 0) return;
-#pragma unroll
-    for (int q = 0; q < S - 1; ++q) acc += red[q][lane];
-  }
-  // wave 0 from here: the tile of h into LDS (C layout: column lane & 15, rows 4 (lane >> 4) + r)
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int orow = tm * 16 + 4 * g + r;
-    hs[4 * g + r][c16] = (orow < M && ocol < N) ? fmaxf(acc[r] + bv, 0.f) : 0.f;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  // lane = (row, pair of head outputs): the tile's partial dot products, columns in order
-  float* prow = h.part + (static_cast<int64_t>(tn) * h.mpad + tm * 16 + row) * 8;
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int o = (lane & 3) * 2 + q;
-    float s = 0.f;
-#pragma unroll
-    for (int c = 0; c < 16; ++c) s += hs[row][c] * hw[q][c];
-    // write-through (sc1) store: visible to every XCD once drained, no release fence
-    __hip_atomic_store(prow + o, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  // publish: this wave (the only storing one) drains its stores, then the row tile's counter
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  unsigned prev = 0;
-  if (lane == 0)
-    prev = __hip_atomic_fetch_add(h.cnt + tm * kHeadCntStride, 1u, __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_AGENT);
-  prev = __shfl(prev, 0, kWave);
-  if (prev != static_cast<unsigned>(h.ntn - 1)) return;  // wave-uniform
-  // every load of the handed-off partials below is an sc1 load (bypasses this CU's L1), so no
-  // acquire fence: the wavefront fence only keeps the compiler from hoisting them
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  // the row tile's logits: the ntn partials in column-tile order, then the biases
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int o = (lane & 3) * 2 + q;
-    float* pp = h.part + static_cast<int64_t>(tm * 16 + row) * 8 + o;
-    const int64_t stride = static_cast<int64_t>(h.mpad) * 8;
-    float s = 0.f;
-    for (int t0 = 0; t0 < h.ntn; t0 += 16) {  // 16 loads in flight, then the ordered sum
-      float v[16];
-#pragma unroll
-      for (int u = 0; u < 16; ++u)
-        v[u] = t0 + u < h.ntn ? __hip_atomic_load(pp + (t0 + u) * stride, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT)
-                              : 0.f;
-#pragma unroll
-      for (int u = 0; u < 16; ++u) s += v[u];
-    }
-    ls[row][o] = s + hb[q];
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  if (lane < 16) {
-    const int64_t n = static_cast<int64_t>(tm) * 16 + lane;
-    if (n < M) {
-      float l[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) l[j] = ls[lane][j];
-      head_tail(l, nz, h.A, n, h.action, h.logprob, h.entropy, h.value, h.logits, true);
-    }
-  }
-  if (lane == 0)  // re-arm for the next launch (stream order puts it after this one)
-    __hip_atomic_store(h.cnt + tm * kHeadCntStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-static int head_waves(int64_t tiles, int nch) {
-  int S = 1;  // K split as launch_linear: >= ~4096 waves, >= 2 chunks per wave
-  while (S < kLinMaxWaves && tiles * S < 4096 && nch >= 2 * S * 2) S *= 2;
-  return S;
-}
-
-static size_t head_cnt_bytes(int64_t ntm) {
-  return static_cast<size_t>((ntm * kHeadCntStride * sizeof(unsigned) + 255) / 256 * 256);
-}
-
-}  // namespace ocppo
-
-extern "C" size_t ocppo_linear_head_workspace_bytes(int64_t M, int64_t N) {
-  if (M < 1 || N < 1) return 256;
-  const int64_t ntm = (M + 15) / 16, ntn = (N + 15) / 16;
-  return head_cnt_bytes(ntm) + static_cast<size_t>(ntn * ntm * 16 * 8) * sizeof(float);
-}
-
-extern "C" int ocppo_linear_head_ring(ocppo_stream_t stream, const float* x, int64_t ldx,
-                                      const float* w, const float* b, int64_t M, int64_t N,
-                                      int64_t K, int64_t seg, int64_t rot, const float* w_actor,
-                                      const float* b_actor, const float* w_critic,
-                                      const float* b_critic, const float* noise, int64_t A,
-                                      int64_t* action_out, float* logprob_out,
-                                      float* entropy_out, float* value_out, float* logits_out,
-                                      void* workspace, size_t workspace_bytes) {
-  OCPPO_REQUIRE(M >= 0 && M <= 65536 && N >= 1 && N <= 65536 && K >= 16 && K % 16 == 0 &&
-                    K <= INT32_MAX && A >= 1 && A <= 7,
-                "ocppo_linear_head_ring: bad sizes M=%lld N=%lld K=%lld A=%lld (M, N <= 65536, "
-                "K %% 16 == 0, A <= 7)", (long long)M, (long long)N, (long long)K, (long long)A);
-  OCPPO_REQUIRE(seg == 0 || (seg >= 32 && (seg & (seg - 1)) == 0 && K % seg == 0 && rot >= 0 &&
-                             rot < K / seg),
-                "ocppo_linear_head_ring: seg=%lld rot=%lld (0, or a power of two >= 32 dividing "
-                "K with 0 <= rot < K / seg)", (long long)seg, (long long)rot);
-  OCPPO_REQUIRE(ldx >= K && ldx % 4 == 0, "ocppo_linear_head_ring: ldx=%lld", (long long)ldx);
-  if (M == 0) return OCPPO_OK;
-  OCPPO_REQUIRE(x && w && w_actor && b_actor && w_critic && b_critic && noise && action_out &&
-                    logprob_out && value_out && workspace,
-                "ocppo_linear_head_ring: null pointer");
-  OCPPO_REQUIRE(reinterpret_cast<uintptr_t>(x) % 16 == 0 && reinterpret_cast<uintptr_t>(w) % 16 == 0 &&
-                    reinterpret_cast<uintptr_t>(workspace) % 256 == 0,
-                "ocppo_linear_head_ring: x, w 16-B and the workspace 256-B aligned");
-  OCPPO_REQUIRE(workspace_bytes >= ocppo_linear_head_workspace_bytes(M, N),
-                "ocppo_linear_head_ring: workspace too small (%zu < %zu)", workspace_bytes,
-                ocppo_linear_head_workspace_bytes(M, N));
-  const int ntm = static_cast<int>((M + 15) / 16), ntn = static_cast<int>((N + 15) / 16);
-  const int tiles = ntm * ntn;
-  const XRing ring = seg ? XRing{__builtin_ctzll(static_cast<unsigned long long>(seg)),
-                                 static_cast<int>(rot), static_cast<int>(K / seg)}
-                         : XRing{0, 0, 1};
-  HeadArgs h;
-  h.wa = w_actor; h.ba = b_actor; h.wc = w_critic; h.bc = b_critic; h.noise = noise;
-  h.A = static_cast<int>(A);
-  h.action = action_out; h.logprob = logprob_out; h.entropy = entropy_out; h.value = value_out;
-  h.logits = logits_out;
-  h.cnt = static_cast<unsigned*>(workspace);
-  h.part = reinterpret_cast<float*>(static_cast<char*>(workspace) + head_cnt_bytes(ntm));
-  h.ntn = ntn;
-  h.mpad = ntm * 16;
-  const int S = head_waves(tiles, static_cast<int>(K / 16));
-  const dim3 grid(8 * ((tiles + 7) / 8)), block(64 * S);
-  const size_t lds = sizeof(LinStage<2>) * S;
-  clear_stale_error();
-  hipStream_t s = as_stream(stream);
-  const int m = (int)M, n = (int)N, k = (int)K;
-  switch (S) {
-    case 1: hipLaunchKernelGGL(linear_head_kernel<1>, grid, block, lds, s, x, ldx, w, b, m, n, k, ntm, tiles, ring, h); break;
-    case 2: hipLaunchKernelGGL(linear_head_kernel<2>, grid, block, lds, s, x, ldx, w, b, m, n, k, ntm, tiles, ring, h); break;
-    case 4: hipLaunchKernelGGL(linear_head_kernel<4>, grid, block, lds, s, x, ldx, w, b, m, n, k, ntm, tiles, ring, h); break;
-    default: hipLaunchKernelGGL(linear_head_kernel<8>, grid, block, lds, s, x, ldx, w, b, m, n, k, ntm, tiles, ring, h); break;
-  }
-  return check_launch("ocppo_linear_head_ring");
 }
 
 extern "C" int ocppo_linear_cache_ring(ocppo_stream_t stream, const float* x, int64_t ldx,

@@ -472,49 +472,6 @@ def linear_act(x, weight, bias=None, relu: bool = False, out=None, ring=None):
     return out
 
 
-_HEAD_WS: dict = {}
-
-
-def linear_head_workspace(M: int, N: int, dev):
-    """The zeroed workspace of ocppo_linear_head_ring for [M, N] (per device and shape, kept:
-    its row-tile counters re-arm themselves, so graph replays reuse it)."""
-    key = (dev, M, N)
-    ws = _HEAD_WS.get(key)
-    if ws is None:
-        nbytes = int(_lib.LIB.ocppo_linear_head_workspace_bytes(M, N))
-        ws = _HEAD_WS[key] = torch.zeros((nbytes + 255) // 256 * 64, dtype=torch.float32,
-                                         device=dev)
-    return ws
-
-
-def linear_head_sample(x, weight, bias, w_actor, b_actor, w_critic, b_critic, noise,
-                       action_out, logprob_out, value_out, entropy_out=None, logits_out=None,
-                       ring=None):
-    """h = relu(x W^T + b) and policy_head_sample(h, ...) in one launch, h never stored
-    (ocppo_linear_head_ring); x is read through the frame-encoding ring when ring = (seg, rot)."""
-    M, K = x.shape
-    N = weight.shape[0]
-    A = w_actor.shape[0]
-    dev = x.device
-    f = torch.float32
-    if x.dtype != f or (M > 1 and x.stride(1) != 1) or x.device.type != "cuda":
-        raise ValueError("x must be an f32 GPU tensor with unit column stride")
-    if tuple(weight.shape) != (N, K) or tuple(w_actor.shape) != (A, N) or w_critic.numel() != N:
-        raise ValueError("decoder / head weights do not match x")
-    seg, rot = (int(v) for v in ring) if ring is not None else (0, 0)
-    ws = linear_head_workspace(M, N, dev)
-    call("ocppo_linear_head_ring", _stream(dev), x.data_ptr(), x.stride(0) if M > 1 else K,
-         _check(weight, "weight", f, dev), _opt(bias, "bias", f, dev, N), M, N, K, seg, rot,
-         _check(w_actor, "w_actor", f, dev), _check(b_actor, "b_actor", f, dev, A),
-         _check(w_critic, "w_critic", f, dev, N), _check(b_critic, "b_critic", f, dev, 1),
-         _check(noise, "noise", f, dev, M * A), A,
-         _check(action_out, "action_out", torch.int64, dev, M),
-         _check(logprob_out, "logprob_out", f, dev, M), _opt(entropy_out, "entropy_out", f, dev, M),
-         _check(value_out, "value_out", f, dev, M), _opt(logits_out, "logits_out", f, dev, M * A),
-         ws.data_ptr(), ws.numel() * 4)
-    return action_out, logprob_out, value_out
-
-
 def linear2_act(x, w1, b1, w2, b2, relu1: bool = True, relu2: bool = True, out=None):
     """y = act2(act1(x @ w1.T + b1) @ w2.T + b2) in ONE launch for rollout-sized batches (no
     autograd): x [M, K1] f32 (unit column stride, K1 <= 64), w1 [N1, K1], w2 [N2, N1]

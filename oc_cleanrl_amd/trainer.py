@@ -247,9 +247,6 @@ class PPOTrainer:
         # (physical slot (t-1) mod W) and the decoder's first layer reads the slots rotated by
         # t mod W (ocppo_linear_cache_ring / ocppo_linear_act_ring), bit-identical to the shift
         self.cache_ring = self.rollout_fusion and a.rollout_cache_ring and self._ring_decoder()
-        # ... and the decoder, both policy heads and the sample are one launch, the decoder
-        # output never stored (ocppo_linear_head_ring)
-        self.dec_head = self.cache_ring and a.rollout_decoder_head and self._decoder_head_ok()
         self.ret_state = torch.zeros(N, dtype=torch.float64, device=dev)
         self.rms_state = torch.tensor([0.0, 1.0, 1e-4], dtype=torch.float64, device=dev)
 
@@ -353,24 +350,6 @@ class PPOTrainer:
         return (E >= 32 and E & (E - 1) == 0 and K == self.obs_shape[0] * E and self.N <= 128
                 and K <= 2048)
 
-    def _decoder_head_ok(self) -> bool:
-        """The decoder is the trunk's last layer and feeds the heads the fused kernel takes."""
-        net, f = self.agent.network, self.agent._flat
-        return (self.fused_head and len(net) == f + 3 and self.A <= 7 and
-                net[f + 1].in_features % 16 == 0 and self.agent.critic.out_features == 1 and
-                self.agent.actor.bias is not None and self.agent.critic.bias is not None)
-
-    def _decode_head(self, t: int):
-        """Decoder on the ring + actor / critic heads + Categorical sample of rollout step t in
-        one launch (ops.linear_head_sample): actions / logprobs / values rows of step t."""
-        ag, net, f = self.agent, self.agent.network, self.agent._flat
-        W, E = self.enc_cache.shape[1], self.enc_cache.shape[2]
-        dec = net[f + 1]
-        self.timer.bracket("decoder_head", lambda: ops.linear_head_sample(
-            self.enc_cache.view(self.N, W * E), dec.weight, dec.bias, ag.actor.weight,
-            ag.actor.bias, ag.critic.weight, ag.critic.bias, self.noise[t], self.actions[t],
-            self.logprobs[t], self.values[t], ring=(E, t % W)))
-
     def _decode_cache(self, t: int):
         """Decoder output on the frame-encoding cache at rollout step t."""
         ag = self.agent
@@ -460,10 +439,7 @@ class PPOTrainer:
             # the reference's stream: one Exp(1) draw of [N, A] per step (Categorical.sample at
             # ppo_atari_oc.py:506), from the same device generator
             self.noise[t].exponential_()
-        if self.dec_head:
-            self._policy_encode(t)
-            self._decode_head(t)
-        elif self.fused_head:
+        if self.fused_head:
             hidden = self._policy_hidden(t)
             self.timer.bracket("action_head", lambda: ops.policy_head_sample(
                 hidden, ag.actor.weight, ag.actor.bias, ag.critic.weight, ag.critic.bias,

@@ -1168,81 +1168,6 @@ def test_linear_act_ring_equals_linear_on_logical_order(ops, dev, M, W, E, N):
                        ring=(96, 1))
 
 
-@pytest.mark.parametrize("M,W,E,N,A", [(128, 4, 512, 512, 6), (100, 4, 64, 64, 6),
-                                       (7, 2, 32, 48, 3), (200, 3, 32, 80, 7)])
-def test_linear_head_ring_equals_decoder_then_policy_head(ops, dev, M, W, E, N, A):
-    """Decoder on the ring + heads + sample in one launch (ocppo_linear_head_ring) vs the decoder
-    launch followed by ocppo_policy_head_sample: logits / values to f32 summation order, and the
-    sampler on the fused kernel's own logits bit for bit; repeated launches and a graph replay
-    bitwise identical (the row-tile counters re-arm)."""
-    g = torch.Generator(device=dev).manual_seed(M + N + A)
-    x = torch.randn(M, W, E, device=dev, generator=g)
-    w = torch.randn(N, W * E, device=dev, generator=g) * (W * E) ** -0.5
-    b = torch.randn(N, device=dev, generator=g) * 0.1
-    wa = torch.randn(A, N, device=dev, generator=g) * 0.05
-    ba = torch.randn(A, device=dev, generator=g) * 0.1
-    wc = torch.randn(1, N, device=dev, generator=g) * 0.1
-    bc = torch.randn(1, device=dev, generator=g)
-    noise = torch.empty(M, A, device=dev).exponential_(generator=g)
-    for rot in range(W):
-        phys = torch.roll(x, rot, dims=1).contiguous()
-        h = ops.linear_act(x.view(M, W * E), w, b, relu=True)
-        ref = h.double() @ wa.double().t() + ba.double()
-        ref_v = (h.double() @ wc.double().t() + bc.double()).view(-1)
-        outs = []
-        for _ in range(2):
-            act = torch.empty(M, dtype=torch.int64, device=dev)
-            lp, val, ent = (torch.empty(M, device=dev) for _ in range(3))
-            logits = torch.empty(M, A, device=dev)
-            ops.linear_head_sample(phys.view(M, W * E), w, b, wa, ba, wc, bc, noise, act, lp,
-                                   val, entropy_out=ent, logits_out=logits, ring=(E, rot))
-            outs.append((act, lp, val, ent, logits))
-        for u, v in zip(*outs):
-            assert torch.equal(u, v)
-        act, lp, val, ent, logits = outs[0]
-        torch.testing.assert_close(logits.double(), ref, rtol=1e-5, atol=1e-5)
-        torch.testing.assert_close(val.double(), ref_v, rtol=1e-5, atol=1e-5)
-        a2, lp2, e2 = ops.categorical_sample(logits, noise, entropy_out=torch.empty(M, device=dev))
-        assert torch.equal(act, a2) and torch.equal(lp, lp2) and torch.equal(ent, e2)
-        # against the unfused pair: the same action wherever the logits are not a near tie
-        a3, _, v3 = ops.policy_head_sample(h, wa, ba, wc, bc, noise)
-        assert (a3 == act).float().mean().item() > 0.97
-        torch.testing.assert_close(v3, val, rtol=1e-5, atol=1e-5)
-    # graph capture / replay
-    act = torch.empty(M, dtype=torch.int64, device=dev)
-    lp, val = torch.empty(M, device=dev), torch.empty(M, device=dev)
-    run = lambda: ops.linear_head_sample(x.view(M, W * E), w, b, wa, ba, wc, bc, noise,  # noqa: E731
-                                         act, lp, val, ring=(E, 0))
-    run()
-    torch.cuda.synchronize()
-    want = (act.clone(), lp.clone(), val.clone())
-    s = torch.cuda.Stream()
-    s.wait_stream(torch.cuda.current_stream())
-    graph = torch.cuda.CUDAGraph()
-    with torch.cuda.stream(s), torch.cuda.graph(graph, stream=s):
-        run()
-    act.zero_(), lp.zero_(), val.zero_()
-    for _ in range(3):
-        graph.replay()
-    torch.cuda.synchronize()
-    assert torch.equal(act, want[0]) and torch.equal(lp, want[1]) and torch.equal(val, want[2])
-
-
-def test_linear_head_ring_rejects_bad_shapes(ops, dev):
-    x = torch.zeros(4, 64, device=dev)
-    w = torch.zeros(32, 64, device=dev)
-    wa, wc = torch.zeros(8, 32, device=dev), torch.zeros(1, 32, device=dev)
-    one = torch.zeros(8, device=dev)
-    act = torch.zeros(4, dtype=torch.int64, device=dev)
-    f = torch.zeros(4, device=dev)
-    with pytest.raises(RuntimeError, match="A <= 7"):
-        ops.linear_head_sample(x, w, None, wa, one, wc, one[:1], torch.ones(4, 8, device=dev),
-                               act, f, f)
-    with pytest.raises(RuntimeError, match="seg"):
-        ops.linear_head_sample(x, w, None, wa[:6], one[:6], wc, one[:1],
-                               torch.ones(4, 6, device=dev), act, f, f, ring=(48, 0))
-
-
 # ---------------------------------------------------------------------------------------------
 # policy heads forward + fused PPO loss + heads backward in one pass (ocppo_heads_loss_fwd_bwd)
 # ---------------------------------------------------------------------------------------------

@@ -62,9 +62,6 @@ SIZES = {
     # middle encoder layer (512 -> 1024): the LDS-staged f32-MFMA Linear kernel
     "decoder": {"config": dict(M=128, K=2048, N=512, seg=512), "scaled": dict(M=8192, K=2048, N=512, seg=512)},
     "encoder_mid": {"config": dict(M=128, K=512, N=1024), "scaled": dict(M=8192, K=512, N=1024)},
-    # the decoder on the ring + both policy heads + the sample in one launch (h never stored)
-    "decoder_head": {"config": dict(M=128, K=2048, N=512, seg=512, A=6),
-                     "scaled": dict(M=8192, K=2048, N=512, seg=512, A=6)},
     # the rollout store of step t-1 + the first two encoder layers of step t (F=12 -> 256 -> 512)
     "store_encode": {"config": dict(N=128, W=4, F=12, N1=256, N2=512),
                      "scaled": dict(N=8192, W=4, F=12, N1=256, N2=512)},
@@ -75,7 +72,6 @@ FLOPS = {
     "cache_linear": lambda p: 2 * p["M"] * p["K"] * p["E"],
     "decoder": lambda p: 2 * p["M"] * p["K"] * p["N"],
     "encoder_mid": lambda p: 2 * p["M"] * p["K"] * p["N"],
-    "decoder_head": lambda p: 2 * p["M"] * p["N"] * (p["K"] + p["A"] + 1),
     "store_encode": lambda p: 2 * p["N"] * (p["F"] * p["N1"] + p["N1"] * p["N2"]),
 }
 
@@ -126,9 +122,6 @@ def case_bytes(name: str, p: dict) -> float:
     if name in ("decoder", "encoder_mid"):  # x + W + b in, y out
         M, K, N = p["M"], p["K"], p["N"]
         return 4 * (M * K + N * (K + 1) + M * N)
-    if name == "decoder_head":  # x + W + b + head weights + noise in; action, log-prob, value out
-        M, K, N, A = p["M"], p["K"], p["N"], p["A"]
-        return 4 * (M * K + N * (K + 1) + (A + 1) * (N + 1) + M * A) + 16 * M
     if name == "store_encode":
         N, W, F, N1, N2 = p["N"], p["W"], p["F"], p["N1"], p["N2"]
         store = N * ((W - 1) * F * 2 + F * 4 + W * F * 6 + 8 + 4 + 24 + 4)
@@ -296,21 +289,6 @@ def make_case(name: str, p: dict, dev):
         y = torch.empty(M, N, device=dev)
         ring = (p["seg"], 1) if "seg" in p else None
         fn = lambda: ops.linear_act(x, w, b, True, out=y, ring=ring)  # noqa: E731
-        return fn, case_bytes(name, p)
-    if name == "decoder_head":
-        M, K, N, A = p["M"], p["K"], p["N"], p["A"]
-        x = torch.relu(torch.randn(M, K, device=dev, generator=g))
-        w = torch.randn(N, K, device=dev, generator=g) * K ** -0.5
-        b = torch.randn(N, device=dev, generator=g)
-        wa = torch.randn(A, N, device=dev, generator=g) * 0.01
-        ba = torch.zeros(A, device=dev)
-        wc = torch.randn(1, N, device=dev, generator=g)
-        bc = torch.zeros(1, device=dev)
-        noise = torch.empty(M, A, device=dev).exponential_(generator=g)
-        act = torch.empty(M, dtype=torch.int64, device=dev)
-        lp, val = torch.empty(M, device=dev), torch.empty(M, device=dev)
-        fn = lambda: ops.linear_head_sample(x, w, b, wa, ba, wc, bc, noise, act, lp, val,  # noqa: E731
-                                            ring=(p["seg"], 1))
         return fn, case_bytes(name, p)
     if name == "store_encode":
         N, W, F, N1, N2 = p["N"], p["W"], p["F"], p["N1"], p["N2"]

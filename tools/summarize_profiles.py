@@ -37,7 +37,6 @@ KERNEL_SUBSTR = {
     "store_encode": ("store_linear2_kernel",),
     "decoder": ("linear_rows_kernel",),
     "encoder_mid": ("linear_rows_kernel",),
-    "decoder_head": ("linear_head_kernel",),
 }
 
 
