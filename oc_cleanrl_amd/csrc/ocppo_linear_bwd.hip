@@ -488,9 +488,15 @@ inline int wg_chunks(int64_t R, int64_t N) {
 // waves are combined through LDS in wave order into ONE record per workgroup, and a second small
 // launch adds the records in workgroup order (16 outputs x 16 workgroup groups per block): no
 // ticket, no last-arriver tail, deterministic.
-constexpr int kWrRowsPerWg = 64;  // 8 rows per wave: 192 workgroups at R = 12288
+#ifndef OCPPO_WR_ROWS  // experiments (tools/build_variant.py) move these
+#define OCPPO_WR_ROWS 64
+#endif
+#ifndef OCPPO_WR_WAVES
+#define OCPPO_WR_WAVES 8
+#endif
+constexpr int kWrRowsPerWg = OCPPO_WR_ROWS;  // 8 rows per wave: 192 workgroups at R = 12288
 constexpr int kWrCols = 256;       // columns per workgroup (64 lanes x 4)
-constexpr int kWrWaves = 8;        // 2 waves per SIMD: enough loads in flight per CU
+constexpr int kWrWaves = OCPPO_WR_WAVES;  // 2 waves per SIMD: enough loads in flight per CU
 constexpr int kWrU = 8;            // rows in flight per wave
 
 template <bool RELU, int KP>
