@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define OCPPO_ABI_VERSION 11
+#define OCPPO_ABI_VERSION 12
 
 /* status codes */
 #define OCPPO_OK 0
@@ -536,6 +536,19 @@ OCPPO_API int ocppo_linear_act_ring(ocppo_stream_t stream, const float* x, int64
                                     const float* w, const float* b, float* y, int64_t ldy,
                                     int64_t M, int64_t N, int64_t K, int64_t seg, int64_t rot,
                                     int relu);
+/* ---------------------------------------------------------------------------------------------
+ * NHWC Conv2d (no padding, no dilation, groups 1) + bias + optional ReLU for the rollout
+ * forward of the NatureCNN trunk (architectures/ppo.py:20-31 at ppo_atari_oc.py:506):
+ *   y[b, oy, ox, co] = act(bias[co] + sum_{ky,kx,ci} x[b, oy*s+ky, ox*s+kx, ci] w[co, ky, kx, ci])
+ * x [B, H, W, Cin] f32 (a channels_last NCHW tensor's memory), w [Cout, KH, KW, Cin] (a
+ * channels_last conv weight's memory), bias [Cout] or NULL, y [B, OH, OW, Cout] f32, OH =
+ * (H - KH) / s + 1. Cin a power of two >= 4, KH*KW*Cin % 16 == 0, x / w 16-B aligned.
+ * Implicit GEMM on v_mfma_f32_16x16x4_f32 (exact f32 products, f32 accumulation).
+ * ------------------------------------------------------------------------------------------- */
+OCPPO_API int ocppo_conv2d_act(ocppo_stream_t stream, const float* x, int64_t B, int64_t H,
+                               int64_t W, int64_t Cin, const float* w, const float* b,
+                               int64_t Cout, int64_t KH, int64_t KW, int64_t stride, float* y,
+                               int relu);
 OCPPO_API int ocppo_store_linear2(ocppo_stream_t stream, const float* frame, const float* reward,
                                   const float* done, int64_t N, int64_t W, int64_t D,
                                   const void* prev_obs, void* obs_out, int obs_dtype,

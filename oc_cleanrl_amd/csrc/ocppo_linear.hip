@@ -415,6 +415,164 @@ extern "C" int ocppo_linear_act_ring(ocppo_stream_t stream, const float* x, int6
   return check_launch("ocppo_linear_act_ring");
 }
 
+namespace ocppo {
+
+// ---- NHWC convolution (no padding) + bias + ReLU for rollout-sized batches ----------------------
+// The NatureCNN trunk of the rollout forward (architectures/ppo.py:20-31 at ppo_atari_oc.py:506,
+// Conv2d 4->32 8x8/4, 32->64 4x4/2, 64->64 3x3/1 on 256 envs' channels-last frames) as an
+// implicit GEMM on the f32 matrix cores: rows = output pixels (b, oy, ox), columns = output
+// channels, k = (ky, kx, ci) -- the order of the channels_last weight [Cout, KH, KW, Cin], so W is
+// the same k-contiguous B operand as a Linear's, and a 16-k chunk of a row is 4 float4 loads of
+// the NHWC input (Cin = 4: one tap's 4 channels each; Cin >= 16: 16 channels of one tap). Tiles,
+// K split and epilogue are linear_rows_kernel's (one workgroup per 16 x 16 output tile, waves
+// combined through LDS in wave order, bias then ReLU as torch's conv + relu). MIOpen at this
+// batch runs an implicit GEMM per layer plus a zero-fill, an NCHW->NHWC copy and our bias/ReLU
+// pass (tools/exp_conv_rollout.py).
+#ifndef OCPPO_CONV_WAVES  // experiments (tools/build_variant.py) move the K-split target
+#define OCPPO_CONV_WAVES 4096
+#endif
+constexpr int64_t kConvWaves = OCPPO_CONV_WAVES;
+
+struct ConvGeom {
+  int H, W, Cin, KW, stride, OH, OW;
+  int cin_shift;  // log2(Cin)
+  int kw_magic;   // ceil(2^16 / KW): tap / KW = (tap * kw_magic) >> 16 for tap < 2^10
+};
+
+template <int S, int CH, bool RELU>
+__global__ __launch_bounds__(64 * S) void conv_rows_kernel(
+    const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
+    float* __restrict__ y, int M, int N, int K, int ntm, int tiles, ConvGeom cg) {
+  __shared__ floatx4 red[S > 1 ? S - 1 : 1][64];
+  const int b = blockIdx.x;
+  const int per_xcd = (tiles + 7) / 8;
+  const int t = (b % 8) * per_xcd + b / 8;  // XCD-contiguous tile ranges (as linear_rows)
+  if (t >= tiles) return;
+  const int tm = t % ntm, tn = t / ntm;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int g = lane >> 4, c16 = lane & 15;
+  const int row = tm * 16 + c16, col = tn * 16 + c16;
+  const bool rok = row < M, cok = col < N;
+  // this lane's output pixel -> the first input element of its receptive field
+  const int pix = rok ? row : 0;
+  const int ohw = cg.OH * cg.OW;
+  const int bi = pix / ohw, r2 = pix - bi * ohw;
+  const int oy = r2 / cg.OW, ox = r2 - oy * cg.OW;
+  const float* xr = x + (static_cast<int64_t>(bi * cg.H + oy * cg.stride) * cg.W +
+                         ox * cg.stride) * cg.Cin;
+  const float* wr = w + static_cast<int64_t>(cok ? col : 0) * K;
+  const int nch = K / 16;
+  const int cpw = (nch + S - 1) / S;
+  const int c0 = wv * cpw;
+  const int c1 = c0 + cpw < nch ? c0 + cpw : nch;
+  floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  for (int cb = c0; cb < c1; cb += CH) {
+    float4 a[CH], bb[CH];
+#pragma unroll
+    for (int q = 0; q < CH; ++q) {
+      const int k = (cb + q) * 16 + 4 * g;
+      const bool live = cb + q < c1;
+      const int tap = k >> cg.cin_shift, ci = k & (cg.Cin - 1);
+      const int ky = (tap * cg.kw_magic) >> 16, kx = tap - ky * cg.KW;
+      const int off = (ky * cg.W + kx) * cg.Cin + ci;
+      a[q] = (live && rok) ? *reinterpret_cast<const float4*>(xr + off) : make_float4(0.f, 0.f, 0.f, 0.f);
+      bb[q] = (live && cok) ? *reinterpret_cast<const float4*>(wr + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int q = 0; q < CH; ++q) {  // same MFMA order as linear_wave_chunks
+      floatx4& acc = (q & 1) ? acc1 : acc0;
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[q].x, bb[q].x, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[q].y, bb[q].y, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[q].z, bb[q].z, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[q].w, bb[q].w, acc, 0, 0, 0);
+    }
+  }
+  floatx4 acc = acc0 + acc1;
+  if (S > 1) {
+    if (wv > 0) red[wv - 1][lane] = acc;
+    __syncthreads();
+    if (wv > 0) return;
+#pragma unroll
+    for (int q = 0; q < S - 1; ++q) acc += red[q][lane];
+  }
+  if (!cok) return;
+  const float bv = bias ? bias[col] : 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int orow = tm * 16 + 4 * g + r;
+    if (orow < M) {
+      float v = acc[r] + bv;
+      if (RELU) v = fmaxf(v, 0.f);
+      y[static_cast<int64_t>(orow) * N + col] = v;
+    }
+  }
+}
+
+template <int S, bool RELU>
+static void launch_conv_s(hipStream_t s, int cpw, const float* x, const float* w, const float* b,
+                          float* y, int M, int N, int K, ConvGeom cg) {
+  const int ntm = (M + 15) / 16, ntn = (N + 15) / 16, tiles = ntm * ntn;
+  const dim3 grid(8 * ((tiles + 7) / 8)), block(64 * S);
+  if (cpw <= 2)
+    hipLaunchKernelGGL((conv_rows_kernel<S, 2, RELU>), grid, block, 0, s, x, w, b, y, M, N, K, ntm, tiles, cg);
+  else if (cpw <= 4)
+    hipLaunchKernelGGL((conv_rows_kernel<S, 4, RELU>), grid, block, 0, s, x, w, b, y, M, N, K, ntm, tiles, cg);
+  else
+    hipLaunchKernelGGL((conv_rows_kernel<S, 8, RELU>), grid, block, 0, s, x, w, b, y, M, N, K, ntm, tiles, cg);
+}
+
+template <bool RELU>
+static void launch_conv(hipStream_t s, const float* x, const float* w, const float* b, float* y,
+                        int M, int N, int K, ConvGeom cg) {
+  const int64_t tiles = static_cast<int64_t>((M + 15) / 16) * ((N + 15) / 16);
+  const int nch = K / 16;
+  int S = 1;  // K split as launch_linear: >= ~kConvWaves waves, >= 2 chunks per wave
+  while (S < kLinMaxWaves && tiles * S < kConvWaves && nch >= 2 * S * 2) S *= 2;
+  const int cpw = (nch + S - 1) / S;
+  switch (S) {
+    case 1: launch_conv_s<1, RELU>(s, cpw, x, w, b, y, M, N, K, cg); break;
+    case 2: launch_conv_s<2, RELU>(s, cpw, x, w, b, y, M, N, K, cg); break;
+    case 4: launch_conv_s<4, RELU>(s, cpw, x, w, b, y, M, N, K, cg); break;
+    default: launch_conv_s<8, RELU>(s, cpw, x, w, b, y, M, N, K, cg); break;
+  }
+}
+
+}  // namespace ocppo
+
+extern "C" int ocppo_conv2d_act(ocppo_stream_t stream, const float* x, int64_t B, int64_t H,
+                                int64_t W, int64_t Cin, const float* w, const float* b,
+                                int64_t Cout, int64_t KH, int64_t KW, int64_t stride, float* y,
+                                int relu) {
+  OCPPO_REQUIRE(B >= 0 && H >= 1 && W >= 1 && Cin >= 4 && (Cin & (Cin - 1)) == 0 &&
+                    Cout >= 1 && KH >= 1 && KW >= 1 && KW <= 64 && KH <= H && KW <= W &&
+                    stride >= 1 && (KH * KW * Cin) % 16 == 0 && KH * KW <= 1024,
+                "ocppo_conv2d_act: bad sizes B=%lld H=%lld W=%lld Cin=%lld Cout=%lld K=%lldx%lld "
+                "stride=%lld (Cin a power of two >= 4, KH*KW*Cin %% 16 == 0)", (long long)B,
+                (long long)H, (long long)W, (long long)Cin, (long long)Cout, (long long)KH,
+                (long long)KW, (long long)stride);
+  const int64_t OH = (H - KH) / stride + 1, OW = (W - KW) / stride + 1;
+  const int64_t M = B * OH * OW, K = KH * KW * Cin;
+  OCPPO_REQUIRE(B * H * W * Cin <= INT32_MAX && M <= INT32_MAX && Cout * K <= INT32_MAX &&
+                    (M + 15) / 16 * ((Cout + 15) / 16) <= INT32_MAX / 8,
+                "ocppo_conv2d_act: too large");
+  if (B == 0) return OCPPO_OK;
+  OCPPO_REQUIRE(x && w && y, "ocppo_conv2d_act: null pointer");
+  OCPPO_REQUIRE(reinterpret_cast<uintptr_t>(x) % 16 == 0 && reinterpret_cast<uintptr_t>(w) % 16 == 0,
+                "ocppo_conv2d_act: x and w must be 16-B aligned");
+  ConvGeom cg;
+  cg.H = (int)H; cg.W = (int)W; cg.Cin = (int)Cin; cg.KW = (int)KW; cg.stride = (int)stride;
+  cg.OH = (int)OH; cg.OW = (int)OW;
+  cg.cin_shift = __builtin_ctzll(static_cast<unsigned long long>(Cin));
+  cg.kw_magic = static_cast<int>((65536 + KW - 1) / KW);
+  clear_stale_error();
+  hipStream_t s = as_stream(stream);
+  if (relu)
+    launch_conv<true>(s, x, w, b, y, (int)M, (int)Cout, (int)K, cg);
+  else
+    launch_conv<false>(s, x, w, b, y, (int)M, (int)Cout, (int)K, cg);
+  return check_launch("ocppo_conv2d_act");
+}
+
 extern "C" int ocppo_linear_cache_ring(ocppo_stream_t stream, const float* x, int64_t ldx,
                                        const float* w, const float* b, float* enc,
                                        const float* done, int64_t M, int64_t N, int64_t K,

@@ -472,6 +472,30 @@ def linear_act(x, weight, bias=None, relu: bool = False, out=None, ring=None):
     return out
 
 
+def conv2d_act(x, weight, bias=None, stride: int = 1, relu: bool = True, out=None):
+    """act(conv2d(x, weight, bias, stride)) on the f32 matrix cores (ocppo_conv2d_act) for
+    channels_last tensors: x [B, Cin, H, W] and weight [Cout, Cin, KH, KW] both in
+    torch.channels_last memory format; no padding / dilation / groups. Returns [B, Cout, OH, OW]
+    in channels_last (no autograd: the rollout forward)."""
+    B, Cin, H, W = x.shape
+    Cout, Cw, KH, KW = weight.shape
+    dev = x.device
+    f = torch.float32
+    cl = torch.channels_last
+    if Cw != Cin or x.dtype != f or weight.dtype != f or x.device.type != "cuda":
+        raise ValueError("conv2d_act: f32 GPU x [B, Cin, H, W] and weight [Cout, Cin, KH, KW]")
+    if not (x.is_contiguous(memory_format=cl) and weight.is_contiguous(memory_format=cl)):
+        raise ValueError("conv2d_act: x and weight must be channels_last")
+    OH, OW = (H - KH) // stride + 1, (W - KW) // stride + 1
+    if out is None:
+        out = torch.empty((B, Cout, OH, OW), dtype=f, device=dev, memory_format=cl)
+    if tuple(out.shape) != (B, Cout, OH, OW) or not out.is_contiguous(memory_format=cl):
+        raise ValueError("conv2d_act: out must be a channels_last [B, Cout, OH, OW] tensor")
+    call("ocppo_conv2d_act", _stream(dev), x.data_ptr(), B, H, W, Cin, weight.data_ptr(),
+         _opt(bias, "bias", f, dev, Cout), Cout, KH, KW, stride, out.data_ptr(), int(bool(relu)))
+    return out
+
+
 def linear2_act(x, w1, b1, w2, b2, relu1: bool = True, relu2: bool = True, out=None):
     """y = act2(act1(x @ w1.T + b1) @ w2.T + b2) in ONE launch for rollout-sized batches (no
     autograd): x [M, K1] f32 (unit column stride, K1 <= 64), w1 [N1, K1], w2 [N2, N1]

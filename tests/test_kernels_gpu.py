@@ -1168,6 +1168,53 @@ def test_linear_act_ring_equals_linear_on_logical_order(ops, dev, M, W, E, N):
                        ring=(96, 1))
 
 
+@pytest.mark.parametrize("B,Cin,H,W,Cout,k,s,relu", [
+    (256, 4, 84, 84, 32, 8, 4, True),    # NatureCNN conv1 at the rollout batch
+    (37, 32, 20, 20, 64, 4, 2, True),    # conv2, ragged batch
+    (5, 64, 9, 9, 64, 3, 1, False),      # conv3, no ReLU
+    (3, 4, 11, 13, 20, 4, 3, True),      # non-square input, Cout not a multiple of 16
+    (0, 4, 84, 84, 32, 8, 4, True)])     # empty batch
+def test_conv2d_act_vs_torch(ops, dev, B, Cin, H, W, Cout, k, s, relu):
+    """NHWC implicit-GEMM conv + bias (+ ReLU) vs torch's conv2d in f64 (tolerance: f32 rounding
+    of a K = k*k*Cin sum)."""
+    import torch.nn.functional as F
+    g = torch.Generator(device=dev).manual_seed(B + Cin + k)
+    cl = torch.channels_last
+    x = torch.rand(B, Cin, H, W, device=dev, generator=g).contiguous(memory_format=cl)
+    w = (torch.randn(Cout, Cin, k, k, device=dev, generator=g) * (Cin * k * k) ** -0.5
+         ).contiguous(memory_format=cl)
+    b = torch.randn(Cout, device=dev, generator=g) * 0.1
+    y = ops.conv2d_act(x, w, b, s, relu)
+    assert y.shape == (B, Cout, (H - k) // s + 1, (W - k) // s + 1)
+    assert y.is_contiguous(memory_format=cl)
+    if B == 0:
+        return
+    ref = F.conv2d(x.double(), w.double(), b.double(), stride=s)
+    ref = F.relu(ref) if relu else ref
+    torch.testing.assert_close(y.double(), ref, rtol=1e-5, atol=1e-5 * float(ref.abs().max()))
+    assert torch.equal(y, ops.conv2d_act(x, w, b, s, relu))  # deterministic
+    with pytest.raises(ValueError, match="channels_last"):
+        ops.conv2d_act(x.contiguous(), w, b, s, relu)
+
+
+def test_rollout_conv_trunk_matches_miopen(ops, dev):
+    """The NatureCNN trunk under no_grad with the HIP input convolution vs the MIOpen path."""
+    from oc_cleanrl_amd import agents
+    from oc_cleanrl_amd.agents import make_agent
+
+    ag = make_agent("PPO", (4, 84, 84), 4, dev).to(dev).to(memory_format=torch.channels_last)
+    x = (torch.randint(0, 256, (64, 4, 84, 84), device=dev).float() / 255).contiguous(
+        memory_format=torch.channels_last)
+    with torch.no_grad():
+        agents.HIP_ROLLOUT_CONV = False
+        try:
+            want = ag.trunk(x, prescaled=True)
+        finally:
+            agents.HIP_ROLLOUT_CONV = True
+        got = ag.trunk(x, prescaled=True)
+    torch.testing.assert_close(got, want, rtol=1e-5, atol=1e-5)
+
+
 # ---------------------------------------------------------------------------------------------
 # policy heads forward + fused PPO loss + heads backward in one pass (ocppo_heads_loss_fwd_bwd)
 # ---------------------------------------------------------------------------------------------
