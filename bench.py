@@ -212,10 +212,12 @@ def main():
         envs = opt.envs_per_gpu or 256
         # MIOpen's deterministic convolution algorithms (use_deterministic_algorithms(True), the
         # reference default) are naive kernels on gfx950, ~30x slower for NatureCNN: config 3 is
-        # measured with torch_deterministic=False (our own HIP kernels are deterministic anyway)
+        # measured with torch_deterministic=False (our own HIP kernels are deterministic anyway),
+        # and with MIOpen's Find choosing the convolution solutions (cudnn.benchmark)
         args = Args(env_id="ALE/Breakout-v5", obs_mode="dqn", architecture="PPO",
                     num_envs=envs * world, num_steps=128, total_timesteps=10_000_000,
-                    cuda_graphs=not opt.no_graphs, save_model=False, torch_deterministic=False)
+                    cuda_graphs=not opt.no_graphs, save_model=False, torch_deterministic=False,
+                    conv_benchmark=True)
     else:
         envs = opt.envs_per_gpu or 128
         args = Args(env_id="ALE/Pong-v5", obs_mode="obj", architecture="PPO_OBJ",
@@ -350,7 +352,11 @@ def main():
                            "MIOpen's deterministic convolution algorithms are naive kernels on "
                            "gfx950, 83x slower (1875 vs 22.5 ms per iteration at 16 envs, "
                            "profiles/r02/c3_capture.log); this package's own HIP kernels are "
-                           "deterministic either way"} if opt.config == 3 else {}),
+                           "deterministic either way. MIOpen's Find picks the convolution "
+                           "solutions (cudnn.benchmark, conv_benchmark=True: 283k -> 319k env "
+                           "steps/s; a few seconds of search in the warm-up)"}
+                          if opt.config == 3 else {}),
+                       "conv_benchmark": args.conv_benchmark,
                        "parallelism": f"dp{world}"},
             "updates_per_sec": round(updates / dt, 2),
             "roofline": roofline,

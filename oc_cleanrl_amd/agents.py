@@ -329,13 +329,16 @@ FUSED_CONV_ACT = True
 
 # Rollout-sized inference batches (no autograd) of the input convolution (Cin <= 4, e.g. the
 # NatureCNN's 8x8/4 on the 4-frame stack) on the HIP implicit-GEMM kernel (ops.conv2d_act, bias
-# and ReLU fused): 44 vs 60 us at 256 envs for MIOpen's convolution + layout copy + bias/ReLU;
-# the deeper layers stay on MIOpen, which is faster there (tools/exp_conv_rollout.py).
+# and ReLU fused): 44 vs 60 us at 256 envs for MIOpen's default solution + layout copy +
+# bias/ReLU; the deeper layers stay on MIOpen, which is faster there. With MIOpen's Find
+# (cudnn.benchmark, Args.conv_benchmark) its conv1 solution is faster (38.5 us), so the kernel
+# only stands in for MIOpen's immediate-mode choice (tools/exp_conv_rollout.py).
 HIP_ROLLOUT_CONV = True
 
 
 def _hip_conv_ok(x, conv) -> bool:
-    return (HIP_ROLLOUT_CONV and not torch.is_grad_enabled() and _conv_act_ok(x, conv) and
+    return (HIP_ROLLOUT_CONV and not torch.is_grad_enabled() and
+            not torch.backends.cudnn.benchmark and _conv_act_ok(x, conv) and
             conv.in_channels <= 4 and conv.in_channels & (conv.in_channels - 1) == 0 and
             conv.padding == (0, 0) and conv.stride[0] == conv.stride[1] and x.shape[0] <= 1024
             and (conv.kernel_size[0] * conv.kernel_size[1] * conv.in_channels) % 16 == 0)

@@ -1205,6 +1205,7 @@ def test_rollout_conv_trunk_matches_miopen(ops, dev):
     ag = make_agent("PPO", (4, 84, 84), 4, dev).to(dev).to(memory_format=torch.channels_last)
     x = (torch.randint(0, 256, (64, 4, 84, 84), device=dev).float() / 255).contiguous(
         memory_format=torch.channels_last)
+    torch.backends.cudnn.benchmark = False
     with torch.no_grad():
         agents.HIP_ROLLOUT_CONV = False
         try:

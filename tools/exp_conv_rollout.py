@@ -6,6 +6,7 @@ back-to-back launches; correctness vs an f64 conv.
     python tools/exp_conv_rollout.py [B ...]
 """
 import json
+import os
 import sys
 
 import torch
@@ -17,6 +18,7 @@ from oc_cleanrl_amd import ops  # noqa: E402
 dev = torch.device("cuda:0")
 torch.manual_seed(0)
 torch.backends.cudnn.deterministic = False
+torch.backends.cudnn.benchmark = os.environ.get("CONV_BENCHMARK", "0") == "1"  # MIOpen Find
 CL = torch.channels_last
 LAYERS = [(4, 32, 8, 4, 84), (32, 64, 4, 2, 20), (64, 64, 3, 1, 9)]  # Cin, Cout, k, stride, H
 
