@@ -116,6 +116,8 @@ def kernel_bytes(tr) -> dict:
         kb["frames_expand"] = M * (8 + 8 * W + 8 * W * E)
         # dh rows in, one row out per distinct frame
         kb["frames_scatter"] = 4 * M * W * E + C * (4 + 4 * E)
+        # ... with the last encoder layer's ReLU backward: its output rows in as the mask
+        kb["frames_scatter_relu"] = 4 * M * W * E + C * (4 + 8 * E)
     return kb
 
 

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define OCPPO_ABI_VERSION 12
+#define OCPPO_ABI_VERSION 13
 
 /* status codes */
 #define OCPPO_OK 0
@@ -378,6 +378,19 @@ OCPPO_API int ocppo_frames_expand(ocppo_stream_t stream, const float* enc, int64
 OCPPO_API int ocppo_frames_scatter(ocppo_stream_t stream, const float* dh, int64_t M, int64_t E,
                          const int32_t* uniq, int64_t C, const int32_t* inv, int64_t mb,
                          const float* dones, int64_t T, int64_t N, int64_t W, float* denc_out);
+/* frames_scatter with the encoder's last ReLU backward fused in (the update's `loss.backward()`
+ * through architectures/ppo.py:60-84's last Linear->ReLU, ppo_atari_oc.py:605):
+ *   gp_out[c, :] = out[c, :] <= 0 ? 0 : denc[c, :]   (out = that layer's ReLU output [C, E];
+ *                                                     NULL: no mask, gp_out = denc)
+ *   dbp[g, :] = sum of gp_out rows of chunk g (ocppo_frames_scatter_chunks(C) chunks of 16 frames,
+ *               summed later in chunk order by ocppo_sum_splits_db); NULL: not written.
+ * E % 4 == 0, dh / out / gp_out / dbp 16-B aligned. Same per-frame sums as frames_scatter. */
+OCPPO_API int64_t ocppo_frames_scatter_chunks(int64_t C);
+OCPPO_API int ocppo_frames_scatter_relu(ocppo_stream_t stream, const float* dh, int64_t M,
+                                        int64_t E, const int32_t* uniq, int64_t C,
+                                        const int32_t* inv, int64_t mb, const float* dones,
+                                        int64_t T, int64_t N, int64_t W, const float* out,
+                                        float* gp_out, float* dbp);
 
 /* ---------------------------------------------------------------------------------------------
  * Minibatch gather — replaces `b_obs[mb_inds]` of ppo_atari_oc.py:566-567:

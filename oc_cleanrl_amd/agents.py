@@ -132,10 +132,18 @@ class _LinearAct(torch.autograd.Function):
         bias_done = False
         g = g.contiguous()
         if ctx.box is not None and ctx.box["premasked"]:
-            # the fused heads backward (_Heads) already applied this layer's ReLU mask and wrote
-            # its bias gradient: only dX and dW remain
+            # the consumer already applied this layer's ReLU mask: the fused heads backward
+            # (_Heads) also wrote its bias gradient; the frame scatter (frames._FramesExpand)
+            # left the bias-gradient partials in the box ("dbp"). Only dX and dW remain.
             dx = g.mm(w) if ctx.needs_input_grad[0] else None
-            _weight_grad(g, x, out=ctx.w.grad)
+            dbp = ctx.box.get("dbp")
+            if dbp is None:
+                _weight_grad(g, x, out=ctx.w.grad)
+            elif _defer_db_ok(g, x, ctx.w, ctx.b):
+                _weight_grad(g, x, out=ctx.w.grad, db=(dbp, ctx.b.grad))
+            else:
+                _weight_grad(g, x, out=ctx.w.grad)
+                torch.sum(dbp[0], 0, out=ctx.b.grad)
             return dx, None, None, None, None
         if FUSED_FIRST_LAYER_BWD and not ctx.needs_input_grad[0] and ctx.needs_input_grad[1] \
                 and ctx.needs_input_grad[2] and _direct(ctx.w) and _direct(ctx.b) and \

@@ -146,6 +146,108 @@ __global__ __launch_bounds__(128) void frames_scatter_kernel(
   }
 }
 
+// The same sum with the ReLU backward of the encoder's last layer fused in (its output `out`
+// [C, E] is the frames' encodings): gp[c, :] = out[c, :] <= 0 ? 0 : denc[c, :] -- what
+// relu_bias_grad would do next -- and the per-workgroup column sums of gp (the layer's
+// bias-gradient partials, dbp [chunks, E], summed in chunk order by ocppo_sum_splits_db).
+// Workgroup = kScatterFrames frames: their uses are resolved in parallel (one thread per
+// (frame, candidate sample)), compacted per frame in (t, k) order, and the data pass keeps two
+// frames in flight per thread pair with the first two uses of every frame loaded before any is
+// summed (almost every frame has one or two uses; further ones are added in order afterwards).
+constexpr int kScatterFrames = 16;
+
+__global__ __launch_bounds__(256) void frames_scatter_relu_kernel(
+    const float* __restrict__ dh, int64_t M, int64_t E, const int32_t* __restrict__ uniq,
+    int64_t C, const int32_t* __restrict__ inv, int64_t mb, const float* __restrict__ dones,
+    int64_t T, int64_t N, int W, const float* __restrict__ out, float* __restrict__ gp,
+    float* __restrict__ dbp) {
+  constexpr int F = kScatterFrames;
+  __shared__ int32_t uses[F][kFramesMaxW * kFramesMaxW];
+  __shared__ int32_t list[F][kFramesMaxW * kFramesMaxW];
+  __shared__ int cnt[F];
+  __shared__ float4 half1[128];
+  const int WW = W * W;
+  const int tid = threadIdx.x;
+  const int64_t c0 = static_cast<int64_t>(blockIdx.x) * F;
+  for (int q = tid; q < F * WW; q += blockDim.x) uses[q / WW][q % WW] = -1;
+  __syncthreads();
+  if (tid < F * W) {  // (frame j, candidate sample t = s + i)
+    const int j = tid / W, i = tid - j * W;
+    const int64_t c = c0 + j;
+    const int32_t u = c < C ? uniq[c] : -1;
+    if (u >= 0) {
+      const int s = static_cast<int>(u / N) - (W - 1);
+      const int64_t n = u - (s + W - 1) * N;
+      const int t = s + i;
+      if (t >= 0 && t <= T - 1) {
+        const int32_t p = inv[t * N + n];
+        if (p / M == mb) {
+          const int32_t row = static_cast<int32_t>(p - mb * M);
+          const int r = latest_reset(dones, t, n, N, W);
+          for (int k = 0; k < W; ++k) {
+            int sk = t - (W - 1) + k;
+            sk = sk > r ? sk : r;
+            if (sk == s) uses[j][i * W + k] = row * W + k;
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (tid < F) {  // compact each frame's uses, keeping the (t ascending, k ascending) order
+    int m = 0;
+    for (int q = 0; q < WW; ++q)
+      if (uses[tid][q] >= 0) list[tid][m++] = uses[tid][q];
+    cnt[tid] = m;
+  }
+  __syncthreads();
+  // data pass: thread = (frame parity h, float4 column group q); frames j = 2 p + h
+  const int h = tid >> 7, qg = tid & 127;
+  float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int64_t e = static_cast<int64_t>(qg) * 4; e < E; e += 128 * 4) {
+    float4 v0[F / 2], v1[F / 2], mk[F / 2];
+#pragma unroll
+    for (int p = 0; p < F / 2; ++p) {  // first two uses + the mask of every frame, in flight
+      const int j = 2 * p + h;
+      const int n = cnt[j];
+      const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+      v0[p] = n > 0 ? *reinterpret_cast<const float4*>(dh + static_cast<int64_t>(list[j][0]) * E + e) : z;
+      v1[p] = n > 1 ? *reinterpret_cast<const float4*>(dh + static_cast<int64_t>(list[j][1]) * E + e) : z;
+      mk[p] = (out && c0 + j < C) ? *reinterpret_cast<const float4*>(out + (c0 + j) * E + e)
+                                  : make_float4(1.f, 1.f, 1.f, 1.f);
+    }
+#pragma unroll
+    for (int p = 0; p < F / 2; ++p) {
+      const int j = 2 * p + h;
+      const int64_t c = c0 + j;
+      if (c >= C) continue;
+      const int n = cnt[j];
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (n > 0) { a.x += v0[p].x; a.y += v0[p].y; a.z += v0[p].z; a.w += v0[p].w; }
+      if (n > 1) { a.x += v1[p].x; a.y += v1[p].y; a.z += v1[p].z; a.w += v1[p].w; }
+      for (int m = 2; m < n; ++m) {
+        const float4 x = *reinterpret_cast<const float4*>(dh + static_cast<int64_t>(list[j][m]) * E + e);
+        a.x += x.x; a.y += x.y; a.z += x.z; a.w += x.w;
+      }
+      a.x = mk[p].x <= 0.f ? 0.f : a.x; a.y = mk[p].y <= 0.f ? 0.f : a.y;
+      a.z = mk[p].z <= 0.f ? 0.f : a.z; a.w = mk[p].w <= 0.f ? 0.f : a.w;
+      *reinterpret_cast<float4*>(gp + c * E + e) = a;
+      cs.x += a.x; cs.y += a.y; cs.z += a.z; cs.w += a.w;
+    }
+    if (dbp) {  // the two frame parities of this column group, in h order
+      if (h == 1) half1[qg] = cs;
+      __syncthreads();
+      if (h == 0) {
+        const float4 o = half1[qg];
+        *reinterpret_cast<float4*>(dbp + static_cast<int64_t>(blockIdx.x) * E + e) =
+            make_float4(cs.x + o.x, cs.y + o.y, cs.z + o.z, cs.w + o.w);
+      }
+      __syncthreads();
+    }
+    cs = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
 static bool aligned16(const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; }
 
 }  // namespace ocppo
@@ -222,4 +324,31 @@ extern "C" int ocppo_frames_scatter(ocppo_stream_t stream, const float* dh, int6
     hipLaunchKernelGGL(frames_scatter_kernel<1>, dim3(g), dim3(128), 0, s, dh, M, E, uniq, C, inv,
                        mb, dones, T, N, (int)W, denc_out);
   return check_launch("ocppo_frames_scatter");
+}
+
+extern "C" int64_t ocppo_frames_scatter_chunks(int64_t C) {
+  return C < 1 ? 1 : (C + ocppo::kScatterFrames - 1) / ocppo::kScatterFrames;
+}
+
+extern "C" int ocppo_frames_scatter_relu(ocppo_stream_t stream, const float* dh, int64_t M,
+                                         int64_t E, const int32_t* uniq, int64_t C,
+                                         const int32_t* inv, int64_t mb, const float* dones,
+                                         int64_t T, int64_t N, int64_t W, const float* out,
+                                         float* gp_out, float* dbp) {
+  OCPPO_REQUIRE(M >= 1 && E >= 4 && E % 4 == 0 && C >= 0 && mb >= 0 && T >= 1 && N >= 1 &&
+                    W >= 1 && W <= kFramesMaxW && (T + W - 1) * N < INT32_MAX &&
+                    T * N < INT32_MAX && M * W < INT32_MAX,
+                "ocppo_frames_scatter_relu: bad sizes (E %% 4 == 0, W <= %d)", kFramesMaxW);
+  if (C == 0) return OCPPO_OK;
+  OCPPO_REQUIRE(dh && uniq && inv && dones && gp_out, "ocppo_frames_scatter_relu: null pointer");
+  OCPPO_REQUIRE(aligned16(dh) && aligned16(gp_out) && (!out || aligned16(out)) &&
+                    (!dbp || aligned16(dbp)),
+                "ocppo_frames_scatter_relu: dh / out / gp / dbp must be 16-B aligned");
+  clear_stale_error();
+  const int64_t g = ocppo_frames_scatter_chunks(C);
+  OCPPO_REQUIRE(g <= INT32_MAX, "ocppo_frames_scatter_relu: too large");
+  hipLaunchKernelGGL(frames_scatter_relu_kernel, dim3(static_cast<unsigned>(g)), dim3(256), 0,
+                     as_stream(stream), dh, M, E, uniq, C, inv, mb, dones, T, N, (int)W, out,
+                     gp_out, dbp);
+  return check_launch("ocppo_frames_scatter_relu");
 }

@@ -335,9 +335,12 @@ __global__ __launch_bounds__(256) void sum_splits_kernel(const float4* __restric
 
 // The deferred bias gradient of ocppo_relu_bias_grad_partial, summed in the same launch as the
 // weight gradient's split-K combine: blocks [0, nsb) combine the weight splits, blocks
-// [nsb, nsb + ceil(N / 64)) each own 64 columns of db: 16 column quads x 16 chunk groups, each
-// thread summing its chunks in order, then the 16 group sums in group order (LDS): one pass,
-// deterministic.
+// [nsb, nsb + ceil(N / 16)) each own 16 columns of db: 4 column quads x 64 chunk groups, each
+// thread summing its chunks in order, then the 64 group sums in group order (LDS): one pass,
+// deterministic. (16 columns per block: the frame scatter's 720 chunk partials at [11520 x 512]
+// take two load batches per thread instead of six.)
+constexpr int kDbQuads = 4;
+constexpr int kDbGroups = 64;
 template <int S>
 __global__ __launch_bounds__(256) void sum_splits_db_kernel(const float4* __restrict__ part,
                                                             int64_t n4, float4* __restrict__ out,
@@ -360,11 +363,11 @@ __global__ __launch_bounds__(256) void sum_splits_db_kernel(const float4* __rest
     }
     return;
   }
-  __shared__ float4 red[16][16];
+  __shared__ float4 red[kDbGroups][kDbQuads];
   const int cb = blockIdx.x - nsb;
-  const int q = threadIdx.x & 15, gi = threadIdx.x >> 4;  // column quad, chunk group
-  const int64_t col = static_cast<int64_t>(cb) * 64 + 4 * q;
-  const int cpg = (chunks + 15) / 16;
+  const int q = threadIdx.x % kDbQuads, gi = threadIdx.x / kDbQuads;  // column quad, chunk group
+  const int64_t col = static_cast<int64_t>(cb) * (4 * kDbQuads) + 4 * q;
+  const int cpg = (chunks + kDbGroups - 1) / kDbGroups;
   const int c0 = gi * cpg, c1 = c0 + cpg < chunks ? c0 + cpg : chunks;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   if (col < N) {
@@ -384,7 +387,7 @@ __global__ __launch_bounds__(256) void sum_splits_db_kernel(const float4* __rest
   __syncthreads();
   if (gi == 0 && col < N) {
     float4 t = red[0][q];
-    for (int k = 1; k < 16; ++k) {
+    for (int k = 1; k < kDbGroups; ++k) {
       const float4 v = red[k][q];
       t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
     }
@@ -408,7 +411,7 @@ extern "C" int ocppo_sum_splits_db(ocppo_stream_t stream, const float* part, int
   clear_stale_error();
   const int64_t n4 = n / 4;
   const int nsb = grid_for(n4, 256);
-  const int ndb = static_cast<int>((N + 63) / 64);
+  const int ndb = static_cast<int>((N + 4 * kDbQuads - 1) / (4 * kDbQuads));
   const dim3 grid(nsb + ndb), block(256);
   hipStream_t s = as_stream(stream);
   const float4* p4 = reinterpret_cast<const float4*>(part);

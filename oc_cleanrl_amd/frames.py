@@ -111,24 +111,47 @@ class FramePlanner:
         iv[...] = inv
 
 
+# The encoder's last ReLU backward (and its bias-gradient partials) inside the frame scatter
+# (ops.frames_scatter_relu) when enc is the ReLU output of an in-place-grad Linear (its box).
+FUSED_SCATTER_RELU = True
+
+
 class _FramesExpand(torch.autograd.Function):
-    """h [M, W, E] = enc[pos_of[slot frame ids]]; backward = deterministic per-frame slot sum."""
+    """h [M, W, E] = enc[pos_of[slot frame ids]]; backward = deterministic per-frame slot sum.
+    When enc carries the producing _LinearAct's box (agents.linear_act: ReLU output, grads in
+    place), the backward also applies that layer's ReLU mask and leaves its bias-gradient
+    partials in the box: the layer's own backward then runs only dX / dW (single consumer: enc
+    feeds nothing but this expand)."""
 
     @staticmethod
-    def forward(ctx, enc, pos_of, perm, dones, uniq, inv, mb, T, N, W):
-        ctx.save_for_backward(uniq, inv, dones)
+    def forward(ctx, enc, pos_of, perm, dones, uniq, inv, mb, T, N, W, box=None):
+        fuse = (FUSED_SCATTER_RELU and box is not None and not box["premasked"] and
+                enc.shape[-1] % 4 == 0)
+        if fuse:
+            box["premasked"] = True
+            ctx.save_for_backward(uniq, inv, dones, enc)
+        else:
+            ctx.save_for_backward(uniq, inv, dones)
+        ctx.box = box if fuse else None
         ctx.geom = (int(mb), T, N, W, perm.numel())
         return ops.timed("frames_expand", lambda: ops.frames_expand(enc, pos_of, perm, dones,
                                                                     T, N, W))
 
     @staticmethod
     def backward(ctx, dh):
-        uniq, inv, dones = ctx.saved_tensors
         mb, T, N, W, M = ctx.geom
         dh = dh.contiguous().view(M, W, -1)
+        if ctx.box is not None:
+            uniq, inv, dones, enc = ctx.saved_tensors
+            box = ctx.box
+            gp, part = ops.timed("frames_scatter_relu", lambda: ops.frames_scatter_relu(
+                dh, uniq, inv, mb, dones, T, N, W, out=enc))
+            box["dbp"] = part
+            return gp, None, None, None, None, None, None, None, None, None, None
+        uniq, inv, dones = ctx.saved_tensors
         denc = ops.timed("frames_scatter", lambda: ops.frames_scatter(dh, uniq, inv, mb, dones,
                                                                       T, N, W))
-        return denc, None, None, None, None, None, None, None, None, None
+        return denc, None, None, None, None, None, None, None, None, None, None
 
 
 def minibatch_hidden(agent, obs, dones, uniq, pos_of, inv, perm, mb: int, split: int = 0):
@@ -154,6 +177,7 @@ def minibatch_hidden(agent, obs, dones, uniq, pos_of, inv, perm, mb: int, split:
         cut = (low, low_d)
     else:
         enc = agent.encode(x)
-    h = _FramesExpand.apply(enc.contiguous(), pos_of, perm, dones, uniq, inv, mb, T, N, W)
+    h = _FramesExpand.apply(enc.contiguous(), pos_of, perm, dones, uniq, inv, mb, T, N, W,
+                            getattr(enc, "_ocppo_box", None))
     hidden = agent.decode(h)
     return (hidden, cut) if split else hidden

@@ -848,6 +848,39 @@ def frames_scatter(dh, uniq, inv, mb: int, dones, T: int, N: int, W: int, out=No
     return out
 
 
+_SCATTER_DBP: dict = {}
+
+
+def frames_scatter_relu(dh, uniq, inv, mb: int, dones, T: int, N: int, W: int, out=None,
+                        gp=None, with_db: bool = True):
+    """frames_scatter with the ReLU backward of the layer whose output `out` [C, E] encoded the
+    frames: gp = out <= 0 ? 0 : denc (ocppo_frames_scatter_relu). Returns (gp, (partials,
+    chunks)): the bias-gradient chunk sums (16 frames per chunk; a per-shape persistent buffer,
+    graph-safe) for sum_splits_db, or (gp, None) without with_db."""
+    M = dh.shape[0]
+    E = dh.shape[-1]
+    if dh.numel() != M * W * E:
+        raise ValueError(f"dh must be [M, W, E] with W={W}, got {tuple(dh.shape)}")
+    C = uniq.numel()
+    dev = dh.device
+    f = torch.float32
+    if gp is None:
+        gp = torch.empty((C, E), dtype=f, device=dev)
+    part = None
+    if with_db:
+        key = (dev, C, E)
+        part = _SCATTER_DBP.get(key)
+        if part is None:
+            chunks = int(_lib.LIB.ocppo_frames_scatter_chunks(C))
+            part = _SCATTER_DBP[key] = (torch.zeros((chunks, E), dtype=f, device=dev), chunks)
+    call("ocppo_frames_scatter_relu", _stream(dev), _check(dh, "dh", f, dev), M, E,
+         _check(uniq, "uniq", torch.int32, dev), C, _check(inv, "inv", torch.int32, dev, T * N),
+         int(mb), _check(dones, "dones", f, dev, (T + 1) * N), T, N, W,
+         _opt(out, "out", f, dev, C * E), _check(gp, "gp", f, dev, C * E),
+         part[0].data_ptr() if part is not None else None)
+    return gp, part
+
+
 def frame_cache_shift(enc, fresh, done=None):
     """In-place shift of the rollout's frame-encoding cache (PPObj): enc [N, W, E] f32,
     fresh [N, E] f32 (row stride may exceed E), done [N] f32 or None:

@@ -56,6 +56,39 @@ def test_frames_kernels_match_oracle(dev, T, N, W, F, M, E, nmb, p_done):
         assert np.array_equal(denc.cpu().numpy(), want)  # same summation order: bit-exact
 
 
+@pytest.mark.parametrize("T,N,W,M,E,nmb,p_done,Ed", [
+    (16, 8, 4, 32, 2, 4, 0.2, 20),      # resets in every window
+    (9, 5, 3, 15, 1, 3, 0.5, 8),        # ragged sizes, odd W
+    (24, 7, 4, 42, 1, 4, 0.0, 64),      # no resets
+    (10, 3, 16, 10, 1, 3, 0.1, 12),     # W = 16 (the kernels' maximum)
+])
+def test_frames_scatter_relu_is_scatter_then_relu_backward(dev, T, N, W, M, E, nmb, p_done, Ed):
+    """ocppo_frames_scatter_relu: gp = out <= 0 ? 0 : frames_scatter(...) bit for bit (same
+    per-frame summation order as the oracle), the bias-gradient chunk partials summing to the
+    column sums of gp, and out = None the plain scatter."""
+    s = _setup(T, N, W, 12, M, E, nmb, p_done, 13, dev)
+    uniq, pos_of, inv = s["plan"]
+    du, dp, di = s["d_plan"]
+    rng = np.random.default_rng(6)
+    for j in range(E * nmb):
+        e, k = divmod(j, nmb)
+        dh = rng.standard_normal((M, W, Ed)).astype(np.float32)
+        out = np.maximum(rng.standard_normal((s["cap"], Ed)), 0).astype(np.float32)
+        want = O.frames_scatter(dh, uniq[j], inv[e], k, s["dones"], T, N, W)
+        want = np.where(out <= 0, 0, want).astype(np.float32)
+        gp, (part, chunks) = ops.frames_scatter_relu(torch.from_numpy(dh).to(dev), du[j], di[e], k,
+                                                     s["d_dones"], T, N, W,
+                                                     out=torch.from_numpy(out).to(dev))
+        assert np.array_equal(gp.cpu().numpy(), want)
+        assert chunks == -(-s["cap"] // 16)
+        torch.testing.assert_close(part.sum(0).double(), gp.double().sum(0), rtol=1e-5, atol=1e-5)
+        plain, none = ops.frames_scatter_relu(torch.from_numpy(dh).to(dev), du[j], di[e], k,
+                                              s["d_dones"], T, N, W, with_db=False)
+        assert none is None
+        assert np.array_equal(plain.cpu().numpy(), O.frames_scatter(dh, uniq[j], inv[e], k,
+                                                                     s["dones"], T, N, W))
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32, torch.uint8])
 def test_frames_at_config_size_reproduce_the_minibatch(dev, dtype):
     """Config 2 sizes (T=128, N=128, W=4, F=12, 4 x 4 minibatches of 4096): the deduplicated
