@@ -41,10 +41,11 @@ SIZES = {
     "mb_prepare": {"config": dict(M=4096, nmb=16, B=16384), "scaled": dict(M=16384, nmb=256, B=1 << 20)},
     "ppo_loss_prepared": {"config": dict(M=4096, A=6), "scaled": dict(M=4 * 1024 * 1024, A=6)},
     "policy_head": {"config": dict(N=128, H=512, A=6), "scaled": dict(N=262144, H=512, A=6)},
-    # the three Linear->ReLU backward launches of one config-2 minibatch (dedup capacity 11520
-    # encoder rows: layers 512/1024/512 -- the first layer (256) runs relu_bias_wgrad, the decoder
-    # (4096 x 512) heads_loss), and one streaming-size launch
-    "relu_bias_grad": {"config": dict(shapes=((11520, 512), (11520, 1024), (11520, 512))),
+    # the two Linear->ReLU backward launches of one config-2 minibatch (dedup capacity 11520
+    # encoder rows: layers 1024/512 -- the first layer (256) runs relu_bias_wgrad, the last
+    # encoder layer's mask rides in frames_scatter_relu, the decoder's in heads_loss), and one
+    # streaming-size launch
+    "relu_bias_grad": {"config": dict(shapes=((11520, 1024), (11520, 512))),
                        "scaled": dict(shapes=((262144, 1024),))},
     # the first encoder layer's fused ReLU-backward + bias + weight gradient (F = 12 -> 256)
     "relu_bias_wgrad": {"config": dict(R=11520, N=256, K=12), "scaled": dict(R=262144, N=256, K=12)},
