@@ -85,6 +85,21 @@ def _weight_grad(g, x, out=None, db=None):
     return torch.sum(part, 0, out=out) if out is not None else part.sum(0)
 
 
+# dX = g W for a few hundred rows and <= 256 output columns: hipBLASLt's kernel for
+# [128 x 512] x [512 x 256] (the DQN train step's second encoder layer) takes ~60 us; the HIP
+# rollout Linear kernel on W^T takes 4.0 us + 2.9 us for the transpose (tools/exp_dqn_gemms.py).
+HIP_SMALL_DX = True
+
+
+def _dx(g, w):
+    M, N = g.shape
+    K = w.shape[1]
+    if (HIP_SMALL_DX and g.is_cuda and M <= 256 and K <= 256 and N >= 256 and N % 16 == 0 and
+            g.dtype == torch.float32 and g.is_contiguous()):
+        return ops.linear_act(g, w.t().contiguous())
+    return g.mm(w)
+
+
 def _defer_db_ok(g, x, w, b) -> bool:
     """The bias gradient can ride in the split-K combine of the weight gradient (HIP sum_splits
     path, FlatAdam-owned aligned grads)."""
@@ -135,7 +150,7 @@ class _LinearAct(torch.autograd.Function):
             # the consumer already applied this layer's ReLU mask: the fused heads backward
             # (_Heads) also wrote its bias gradient; the frame scatter (frames._FramesExpand)
             # left the bias-gradient partials in the box ("dbp"). Only dX and dW remain.
-            dx = g.mm(w) if ctx.needs_input_grad[0] else None
+            dx = _dx(g, w) if ctx.needs_input_grad[0] else None
             dbp = ctx.box.get("dbp")
             if dbp is None:
                 _weight_grad(g, x, out=ctx.w.grad)
@@ -161,7 +176,7 @@ class _LinearAct(torch.autograd.Function):
             gp, dbp = ops.timed(f"relu_bias_grad_{g.shape[0]}x{g.shape[1]}" +
                                 ("" if ctx.relu else "_norelu"),
                                 lambda: ops.relu_bias_grad_partial(g, o))
-            dx = gp.mm(w) if ctx.needs_input_grad[0] else None
+            dx = _dx(gp, w) if ctx.needs_input_grad[0] else None
             _weight_grad(gp, x, out=ctx.w.grad, db=(dbp, ctx.b.grad))
             return dx, None, None, None, None
         if FUSED_RELU_BIAS_GRAD and ctx.needs_input_grad[2] and _direct(ctx.b) and \
@@ -174,7 +189,7 @@ class _LinearAct(torch.autograd.Function):
             bias_done = True
         else:
             gp = torch.ops.aten.threshold_backward(g, out, 0) if ctx.relu else g
-        dx = gp.mm(w) if ctx.needs_input_grad[0] else None
+        dx = _dx(gp, w) if ctx.needs_input_grad[0] else None
         dw = None
         if ctx.needs_input_grad[1]:
             if _direct(ctx.w):
