@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define OCPPO_ABI_VERSION 13
+#define OCPPO_ABI_VERSION 14
 
 /* status codes */
 #define OCPPO_OK 0
@@ -454,6 +454,14 @@ OCPPO_API int ocppo_replay_sample(ocppo_stream_t stream, uint64_t seed, int64_t*
                                   float* rewards_out, float* dones_out, int64_t* indices_out);
 /* global step t = *step + step_offset (step : device i64, so a captured chunk of env steps
  * reads one counter advanced once per chunk); epsilon_out : device f32 or NULL */
+/* the Q head (q = hidden Wq^T + bq, hidden [E, H] H a multiple of 256 <= 1024, wq [A, H], A <= 8)
+ * and ocppo_epsilon_greedy on it in one launch (same coin, argmax rule and random action);
+ * q_out [E, A] or NULL */
+OCPPO_API int ocppo_q_head_epsilon_greedy(ocppo_stream_t stream, const float* hidden, int64_t E,
+                                          int64_t H, const float* wq, const float* bq, int64_t A,
+                                          uint64_t seed, const int64_t* step, int64_t step_offset,
+                                          double start_e, double end_e, double duration,
+                                          int64_t* actions, float* epsilon_out, float* q_out);
 OCPPO_API int ocppo_epsilon_greedy(ocppo_stream_t stream, const float* q, int64_t E, int64_t A,
                                    uint64_t seed, const int64_t* step, int64_t step_offset,
                                    double start_e, double end_e, double duration,

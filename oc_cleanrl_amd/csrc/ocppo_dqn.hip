@@ -11,6 +11,7 @@
 // so sampling is graph-replayable; the law is SB3's, the bits are not numpy's (parity of the
 // sampler is by distribution, the TD math is bit-level).
 #include "ocppo_common.h"
+#include "ocppo_categorical.h"
 
 namespace ocppo {
 
@@ -146,6 +147,62 @@ __global__ __launch_bounds__(256) void epsilon_greedy_kernel(
     actions[e] = a;
   }
   if (eps_out && blockIdx.x == 0 && threadIdx.x == 0) eps_out[0] = static_cast<float>(eps);
+}
+
+// The acting step's Q head and epsilon-greedy choice in one launch (dqn_atari_oc.py:345-352:
+// `q_values = q_network(obs); actions = argmax(q_values)` or a uniform random action with
+// probability epsilon): one wave per env, the head's A <= 8 weight rows in registers, the A dot
+// products of the hidden row by the policy head's reduce-scatter butterfly, then exactly
+// epsilon_greedy_kernel's coin, argmax rule and random action on those values.
+template <int CH>
+__global__ __launch_bounds__(256) void q_head_eps_kernel(
+    const float* __restrict__ hidden, int64_t E, const float* __restrict__ wq,
+    const float* __restrict__ bq, int A, uint64_t seed, const int64_t* __restrict__ step,
+    int64_t step_offset, double start_e, double end_e, double duration,
+    int64_t* __restrict__ actions, float* __restrict__ eps_out, float* __restrict__ q_out) {
+  constexpr int H = 256 * CH;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t e = static_cast<int64_t>(blockIdx.x) * 4 + wv;
+  if (e >= E) return;  // wave-uniform
+  const int jo = lane >> 3;
+  const float bias = jo < A ? bq[jo] : 0.f;
+  float4 w[8][CH];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+      w[j][c] = j < A ? reinterpret_cast<const float4*>(wq + static_cast<int64_t>(j) * H)[c * kWave + lane]
+                      : make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 x[CH];
+  head_load_row<CH>(hidden, e, lane, x);
+  const float t = head_dots<CH>(x, w, lane) + bias;
+  const int64_t ts = step[0] + step_offset;
+  const double slope = (end_e - start_e) / duration;
+  double eps = slope * static_cast<double>(ts) + start_e;
+  eps = eps > end_e ? eps : end_e;
+  const uint64_t hh = mix64(mix64(seed ^ 0xA0761D6478BD642Full) + static_cast<uint64_t>(ts));
+  const double coin = static_cast<double>(hh >> 11) * (1.0 / 9007199254740992.0);  // [0, 1)
+  float q[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) q[j] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t), 8 * j));
+  int64_t a;
+  if (coin < eps) {
+    a = static_cast<int64_t>(mix64(hh + static_cast<uint64_t>(e) + 1) % static_cast<uint64_t>(A));
+  } else {
+    int best = 0;
+    float bqv = q[0];
+#pragma unroll
+    for (int j = 1; j < 8; ++j)
+      if (j < A && (q[j] > bqv || (q[j] != q[j] && bqv == bqv))) {
+        bqv = q[j];
+        best = j;
+      }
+    a = best;
+  }
+  if (lane == 0) actions[e] = a;
+  const float mine = __shfl(t, 8 * (lane & 7), kWave);  // all lanes take part in the permute
+  if (q_out && lane < A) q_out[e * A + lane] = mine;
+  if (eps_out && e == 0 && lane == 0) eps_out[0] = static_cast<float>(eps);
 }
 
 // Fused TD target + MSE loss, forward and backward w.r.t. q (dqn_atari_oc.py:378-382):
@@ -285,4 +342,32 @@ extern "C" int ocppo_epsilon_greedy(ocppo_stream_t stream, const float* q, int64
   hipLaunchKernelGGL(epsilon_greedy_kernel, dim3(g), dim3(256), 0, as_stream(stream), q, E, (int)A,
                      seed, step, step_offset, start_e, end_e, duration, actions, epsilon_out);
   return check_launch("ocppo_epsilon_greedy");
+}
+
+extern "C" int ocppo_q_head_epsilon_greedy(ocppo_stream_t stream, const float* hidden, int64_t E,
+                                          int64_t H, const float* wq, const float* bq, int64_t A,
+                                          uint64_t seed, const int64_t* step, int64_t step_offset,
+                                          double start_e, double end_e, double duration,
+                                          int64_t* actions, float* epsilon_out, float* q_out) {
+  OCPPO_REQUIRE(E >= 1 && A >= 1 && A <= 8 && H >= 256 && H % 256 == 0 && H <= 1024 &&
+                    duration > 0 && E <= INT32_MAX,
+                "ocppo_q_head_epsilon_greedy: bad sizes E=%lld H=%lld A=%lld (A <= 8, H a "
+                "multiple of 256 <= 1024)", (long long)E, (long long)H, (long long)A);
+  OCPPO_REQUIRE(hidden && wq && bq && step && actions, "ocppo_q_head_epsilon_greedy: null pointer");
+  OCPPO_REQUIRE(((reinterpret_cast<uintptr_t>(hidden) | reinterpret_cast<uintptr_t>(wq)) & 15) == 0,
+                "ocppo_q_head_epsilon_greedy: hidden and wq must be 16-B aligned");
+  clear_stale_error();
+  const dim3 grid(static_cast<unsigned>(ceil_div(E, 4))), block(256);
+  hipStream_t s = as_stream(stream);
+#define OCPPO_QH(CH)                                                                            \
+  hipLaunchKernelGGL(q_head_eps_kernel<CH>, grid, block, 0, s, hidden, E, wq, bq, (int)A, seed, \
+                     step, step_offset, start_e, end_e, duration, actions, epsilon_out, q_out)
+  switch (H / 256) {
+    case 1: OCPPO_QH(1); break;
+    case 2: OCPPO_QH(2); break;
+    case 3: OCPPO_QH(3); break;
+    default: OCPPO_QH(4); break;
+  }
+#undef OCPPO_QH
+  return check_launch("ocppo_q_head_epsilon_greedy");
 }

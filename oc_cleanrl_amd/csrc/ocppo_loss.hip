@@ -792,46 +792,6 @@ __global__ __launch_bounds__(256) void policy_head_sample_kernel(
 constexpr int kHeadWavesPerBlock = 4;
 
 template <int CH>
-__device__ __forceinline__ void head_load_row(const float* __restrict__ hidden, int64_t n, int lane,
-                                              float4 (&x)[CH]) {
-  const float4* h4 = reinterpret_cast<const float4*>(hidden + n * (256 * CH));
-#pragma unroll
-  for (int c = 0; c < CH; ++c) x[c] = h4[c * kWave + lane];
-}
-
-// The A+1 (padded to 8) dot products of one hidden row against the register-resident weights,
-// reduce-scattered so that lane 8j ends with value j (see above).
-template <int CH>
-__device__ __forceinline__ float head_dots(const float4 (&x)[CH], const float4 (&w)[8][CH],
-                                           int lane) {
-  float acc[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    acc[j] = 0.f;
-#pragma unroll
-    for (int c = 0; c < CH; ++c)
-      acc[j] += x[c].x * w[j][c].x + x[c].y * w[j][c].y + x[c].z * w[j][c].z + x[c].w * w[j][c].w;
-  }
-  const bool b5 = lane & 32, b4 = lane & 16, b3 = lane & 8;
-  float s4[4], s2[2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const float send = b5 ? acc[i] : acc[i + 4];
-    s4[i] = (b5 ? acc[i + 4] : acc[i]) + __shfl_xor(send, 32);
-  }
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const float send = b4 ? s4[i] : s4[i + 2];
-    s2[i] = (b4 ? s4[i + 2] : s4[i]) + __shfl_xor(send, 16);
-  }
-  float t = (b3 ? s2[1] : s2[0]) + __shfl_xor(b3 ? s2[0] : s2[1], 8);
-  t += __shfl_xor(t, 4);
-  t += __shfl_xor(t, 2);
-  t += __shfl_xor(t, 1);
-  return t;
-}
-
-template <int CH>
 __global__ __launch_bounds__(256) void policy_head_fast_kernel(
     const float* __restrict__ hidden, int64_t N, int E, const float* __restrict__ wa,
     const float* __restrict__ ba, const float* __restrict__ wc, const float* __restrict__ bc,

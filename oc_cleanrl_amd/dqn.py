@@ -154,6 +154,10 @@ class QNetworkObj(Predictor):
     predict = QNetwork.predict
 
 
+# The acting step's Q head + epsilon-greedy choice as one HIP launch (ops.q_head_epsilon_greedy).
+FUSED_ACT = True
+
+
 def make_qnet(args: DQNArgs, obs_shape, n_actions) -> nn.Module:
     if args.obs_mode == "obj":
         return QNetworkObj(obs_shape, n_actions, args.encoder_dims, args.decoder_dims)
@@ -232,6 +236,11 @@ class DQNTrainer:
         self.dq = torch.zeros((B, self.A), dtype=f32, device=dev)
         self.td_stats = torch.zeros(2, dtype=f32, device=dev)
         self.duration = a.exploration_fraction * a.total_timesteps
+        # acting: the Q head and the epsilon-greedy choice in one launch
+        head = self.q.network[-1]
+        self.fused_act = (FUSED_ACT and isinstance(head, nn.Linear) and head.bias is not None and
+                          self.A <= 8 and head.in_features % 256 == 0 and
+                          head.in_features <= 1024)
         self.cur = 0  # index of the stack holding the current obs
         self.global_step = 0
         self.log_enabled = log
@@ -245,11 +254,19 @@ class DQNTrainer:
         """One global step (:345-372): act, step, store + VecNormalize, replay add."""
         a = self.args
         prev, nxt = self.stacks[self.cur], self.stacks[1 - self.cur]
-        with torch.no_grad():
-            q = _q_forward(self.q, self.net_obs)
         # global step = chunk base (step_dev, advanced once per chunk) + k + 1
-        ops.epsilon_greedy(q, a.seed, self.step_dev, a.start_e, a.end_e, self.duration,
-                           self.actions, self.epsilon, step_offset=k + 1)
+        with torch.no_grad():
+            if self.fused_act:
+                net = self.q.network
+                x = self.net_obs / 255.0 if self.pixels else self.net_obs
+                h = fused_trunk(net[:-1], x)
+                ops.q_head_epsilon_greedy(h, net[-1].weight, net[-1].bias, a.seed, self.step_dev,
+                                          a.start_e, a.end_e, self.duration, self.actions,
+                                          self.epsilon, step_offset=k + 1)
+            else:
+                q = _q_forward(self.q, self.net_obs)
+                ops.epsilon_greedy(q, a.seed, self.step_dev, a.start_e, a.end_e, self.duration,
+                                   self.actions, self.epsilon, step_offset=k + 1)
         self.env.step(self.actions, k)
         if a.vecnorm_reward:
             # VecNormalize(envs, norm_obs=False, norm_reward=True) (:298) keeps SB3's default

@@ -1125,6 +1125,25 @@ def epsilon_greedy(q, seed: int, step, start_e: float, end_e: float, duration: f
     return actions_out
 
 
+def q_head_epsilon_greedy(hidden, wq, bq, seed: int, step, start_e: float, end_e: float,
+                          duration: float, actions_out=None, epsilon_out=None,
+                          step_offset: int = 0, q_out=None):
+    """epsilon_greedy(hidden @ wq.T + bq, ...) in one launch (ocppo_q_head_epsilon_greedy)."""
+    E, H = hidden.shape
+    A = wq.shape[0]
+    dev = hidden.device
+    f = torch.float32
+    if actions_out is None:
+        actions_out = torch.empty(E, dtype=torch.int64, device=dev)
+    call("ocppo_q_head_epsilon_greedy", _stream(dev), _check(hidden, "hidden", f, dev), E, H,
+         _check(wq, "wq", f, dev, A * H), _check(bq, "bq", f, dev, A), A,
+         int(seed) & 0xFFFFFFFFFFFFFFFF, _check(step, "step", torch.int64, dev, 1),
+         int(step_offset), float(start_e), float(end_e), float(duration),
+         _check(actions_out, "actions", torch.int64, dev, E),
+         _opt(epsilon_out, "epsilon_out", f, dev, 1), _opt(q_out, "q_out", f, dev, E * A))
+    return actions_out
+
+
 def td_loss_fwd_bwd(q, q_next, actions, rewards, dones, gamma: float, dq=None, stats=None):
     """(stats [2] = {td_loss, mean q(s,a)}, dq [B, A] = d loss / d q)."""
     B, A = q.shape

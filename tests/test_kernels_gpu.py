@@ -670,6 +670,31 @@ def test_epsilon_greedy(ops, dev):
     assert seen.min() > 0.1 * seen.mean()
 
 
+@pytest.mark.parametrize("E,H,A", [(1, 512, 6), (37, 256, 8), (5, 1024, 3)])
+def test_q_head_epsilon_greedy(ops, dev, E, H, A):
+    """Q head + epsilon-greedy in one launch: q to f32 rounding of F.linear, and the action is
+    exactly ocppo_epsilon_greedy's on the kernel's own q, greedy (epsilon = 0), random (1) and
+    mixed."""
+    g = torch.Generator(device=dev).manual_seed(E + H + A)
+    h = torch.relu(torch.randn(E, H, device=dev, generator=g))
+    wq = torch.randn(A, H, device=dev, generator=g) * H ** -0.5
+    bq = torch.randn(A, device=dev, generator=g) * 0.1
+    step = torch.zeros(1, dtype=torch.int64, device=dev)
+    for start_e, end_e, dur in ((0.0, 0.0, 10.0), (1.0, 1.0, 10.0), (1.0, 0.05, 50.0)):
+        for t in (0, 7, 30, 100):
+            step.fill_(t)
+            q = torch.empty(E, A, device=dev)
+            eps = torch.empty(1, device=dev)
+            a = ops.q_head_epsilon_greedy(h, wq, bq, 3, step, start_e, end_e, dur,
+                                          epsilon_out=eps, step_offset=1, q_out=q)
+            torch.testing.assert_close(q, torch.nn.functional.linear(h, wq, bq), rtol=1e-5,
+                                       atol=1e-5)
+            eps2 = torch.empty(1, device=dev)
+            a2 = ops.epsilon_greedy(q, 3, step, start_e, end_e, dur, epsilon_out=eps2,
+                                    step_offset=1)
+            assert torch.equal(a, a2) and torch.equal(eps, eps2)
+
+
 @pytest.mark.parametrize("dt", [torch.uint8, torch.bfloat16])
 def test_replay_buffer_semantics(ops, dev, dt):
     from oracle import ocppo_oracle as O
