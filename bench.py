@@ -194,6 +194,7 @@ def main():
     opt = ap.parse_args()
 
     from oc_cleanrl_amd.args import Args, finalize
+    from oc_cleanrl_amd import gemm_table
     from oc_cleanrl_amd.trainer import PPOTrainer
 
     rank = int(os.environ.get("RANK", "0"))
@@ -350,6 +351,8 @@ def main():
                        "obs_storage": str(tr.obs_dtype).replace("torch.", ""),
                        "cuda_graphs": args.cuda_graphs,
                        "torch_deterministic": args.torch_deterministic,
+                       "gemm_table": (str(gemm_table.TABLE.relative_to(ROOT))
+                                      if tr.gemm_table else None),
                        **({"deviation": "torch_deterministic=False (reference default True): "
                            "MIOpen's deterministic convolution algorithms are naive kernels on "
                            "gfx950, 83x slower (1875 vs 22.5 ms per iteration at 16 envs, "

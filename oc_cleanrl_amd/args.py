@@ -131,6 +131,7 @@ class Args:
     conv_channels_last: bool = True  # pixel NatureCNN in NHWC (MIOpen NHWC kernels, no transposes)
     eval_episodes: int = 0  # after training: evaluate() episodes (the reference runs 10 when tracking)
     conv_benchmark: bool = False  # cudnn.benchmark (MIOpen Find) for the NatureCNN convolutions
+    gemm_table: bool = True  # the shipped hipBLASLt solution table for the update GEMMs
 
 
 def _flag_names(name: str) -> list[str]:

@@ -37,7 +37,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from . import ops
+from . import gemm_table, ops
 from .agents import Predictor, fused_trunk, q_head
 from .args import OBS_MODES, parse_dataclass
 from .envs import SyntheticAtariEnv
@@ -89,6 +89,7 @@ class DQNArgs:
     encoder_dims: tuple = (256, 512, 1024, 512)  # QNetworkObj (obs_mode obj)
     decoder_dims: tuple = (512,)
     cuda_graphs: bool = True
+    gemm_table: bool = False  # the shipped hipBLASLt solution table (gemm_table.py): no gain measured here
     vecnorm_reward: bool = True  # VecNormalize(norm_reward=True) of dqn_atari_oc.py:286
     log_dir: str = "runs"
     save_model: bool = True
@@ -184,6 +185,7 @@ class DQNTrainer:
         torch.utils.deterministic.fill_uninitialized_memory = False
         torch.backends.cudnn.deterministic = a.torch_deterministic
         torch.backends.cudnn.benchmark = False
+        self.gemm_table = a.gemm_table and gemm_table.use(device)
         torch.manual_seed(a.seed)
         self.E = a.num_envs
         self.env = SyntheticAtariEnv(a.env_id, a.obs_mode, self.E, a.num_features, a.seed,

@@ -32,7 +32,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
-from . import frames, ops
+from . import frames, gemm_table, ops
 from .agents import NormalizeImg, PPObj, fused_trunk, linear_relu, make_agent
 from .args import Args
 from .envs import HostVecEnv, make_device_env
@@ -155,6 +155,7 @@ class PPOTrainer:
         torch.utils.deterministic.fill_uninitialized_memory = False
         torch.backends.cudnn.deterministic = a.torch_deterministic
         torch.backends.cudnn.benchmark = a.conv_benchmark
+        self.gemm_table = a.gemm_table and gemm_table.use(device)
 
         # seeding as ppo_atari_multigpu.py:208-212, 230-231: identical init on every rank, then
         # rank-dependent sampling / env / shuffle streams

@@ -48,6 +48,7 @@ def main():
                    "replay_obs_dtype": str(tr.obs_dtype).replace("torch.", ""),
                    "replay_bytes": tr.rb.obs.numel() * tr.rb.obs.element_size(),
                    "batch_size": args.batch_size, "train_frequency": args.train_frequency,
+                   "gemm_table": tr.gemm_table,
                    "cuda_graphs": tr._graphable()},
         "td_loss": m["losses/td_loss"], "data": "synthetic device env, random-init Q-network"}))
 
