@@ -88,3 +88,35 @@ def test_predict_greedy():
     with torch.no_grad():
         ref = ag.actor(ag.network(torch.from_numpy(x))).argmax(1).numpy()
     assert np.array_equal(a, ref)
+
+
+def test_gemm_table_file_is_a_tunableop_table():
+    """The shipped hipBLASLt solution table (gemm_table.py): TunableOp's CSV with its validators
+    (PyTorch version of this image, gfx950) and one solution per GEMM signature, hipBLASLt
+    solutions or the default only (no rocBLAS entries: those lose under hipGraph replay)."""
+    import csv
+
+    import torch
+
+    from oc_cleanrl_amd import gemm_table
+
+    rows = list(csv.reader(open(gemm_table.TABLE)))
+    val = {r[1]: r[2] for r in rows if r[0] == "Validator"}
+    assert val["PT_VERSION"] == torch.__version__.split("+")[0]
+    assert val["GCN_ARCH_NAME"].startswith("gfx950")
+    entries = [r for r in rows if r[0] != "Validator"]
+    assert len(entries) == len({(r[0], r[1]) for r in entries}) > 0
+    assert all(r[2] == "Default" or r[2].startswith("Gemm_Hipblaslt_") for r in entries)
+    # config 2's encoder / decoder GEMM shapes are in it
+    sigs = {r[1] for r in entries}
+    assert "tn_1024_11520_512_ld_512_512_1024" in sigs and "nn_2048_4096_512_ld_2048_512_2048" in sigs
+
+
+def test_gemm_table_not_used_off_gpu():
+    from oc_cleanrl_amd import gemm_table
+
+    gemm_table._state.clear()
+    try:
+        assert gemm_table.use("cpu") is False
+    finally:
+        gemm_table._state.clear()
