@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define OCPPO_ABI_VERSION 14
+#define OCPPO_ABI_VERSION 15
 
 /* status codes */
 #define OCPPO_OK 0
@@ -391,6 +391,16 @@ OCPPO_API int ocppo_frames_scatter_relu(ocppo_stream_t stream, const float* dh, 
                                         const int32_t* inv, int64_t mb, const float* dones,
                                         int64_t T, int64_t N, int64_t W, const float* out,
                                         float* gp_out, float* dbp);
+/* frames_gather + the encoder's first Linear(+ReLU) in one pass (the update's first encoder layer
+ * over the distinct frames, architectures/ppo.py:60-84 on b_obs[mb_inds], ppo_atari_oc.py:566) (F <= 16, N1 % 4 == 0,
+ * N1 <= 1024): x_out [C, F] = the gathered frames (as frames_gather),
+ * h_out [C, N1] = act(x W^T + b)
+ * (w [N1, F], b [N1] or NULL; products summed over f in order, then + b, then ReLU if relu). */
+OCPPO_API int ocppo_frames_gather_linear(ocppo_stream_t stream, const void* obs, int obs_dtype,
+                                         int64_t T, int64_t N, int64_t W, int64_t F,
+                                         const int32_t* uniq, int64_t C, const float* w,
+                                         const float* b, int64_t N1, int relu, float* x_out,
+                                         float* h_out);
 
 /* ---------------------------------------------------------------------------------------------
  * Minibatch gather — replaces `b_obs[mb_inds]` of ppo_atari_oc.py:566-567:

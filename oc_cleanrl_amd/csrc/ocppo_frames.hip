@@ -59,6 +59,82 @@ __global__ __launch_bounds__(256) void frames_gather_kernel(const void* __restri
   }
 }
 
+// frames_gather + the encoder's first Linear(+ReLU) (F <= 16 inputs): the update's first layer
+// over the C distinct frames, x written for its backward (ocppo_relu_bias_wgrad) and
+// h = act(x W^T + b) in the same pass -- one launch instead of the gather and a K = F BLAS GEMM
+// whose 11.8 MB output dominates. Workgroup = 16 frames; W and b staged in LDS; thread = (frame,
+// 4-column group), products summed over f in order with fmaf, then + b, then ReLU.
+constexpr int kGlRows = 32;  // two rows per thread (r, r + 16) share every W read
+constexpr int kGlCols = 64;  // columns per workgroup (16 float4 groups): grid.y = N1 / 64
+constexpr int kGlMaxF = 16;
+constexpr int kGlMaxN = 1024;
+
+// Workgroup = 32 frames x 64 columns, thread = 2 frames x one float4 column group. LDS: the
+// workgroup's W^T slice [F][64] (float4 reads by consecutive column groups: conflict-free), its
+// b slice, the 32 gathered rows (the column-block-0 workgroups also write x_out).
+template <int DT, bool RELU>
+__global__ __launch_bounds__(256) void frames_gather_linear_kernel(
+    const void* __restrict__ obs, int64_t N, int W, int F, const int32_t* __restrict__ uniq,
+    int64_t C, const float* __restrict__ w, const float* __restrict__ b, int N1,
+    float* __restrict__ x_out, float* __restrict__ h_out) {
+  __shared__ float4 wt4[kGlMaxF * kGlCols / 4];
+  __shared__ float4 bs4[kGlCols / 4];
+  __shared__ float xs[kGlRows][kGlMaxF];
+  float* wt = reinterpret_cast<float*>(wt4);
+  float* bs = reinterpret_cast<float*>(bs4);
+  const int tid = threadIdx.x;
+  const int n0 = blockIdx.y * kGlCols;
+  for (int i = tid; i < kGlCols * F; i += 256) {
+    const int f = i / kGlCols, n = i - f * kGlCols;
+    wt[i] = n0 + n < N1 ? w[(n0 + n) * F + f] : 0.f;
+  }
+  if (tid < kGlCols) bs[tid] = (b && n0 + tid < N1) ? b[n0 + tid] : 0.f;
+  const int64_t c0 = static_cast<int64_t>(blockIdx.x) * kGlRows;
+  for (int i = tid; i < kGlRows * F; i += 256) {
+    const int r = i / F, f = i - r * F;
+    const int64_t c = c0 + r;
+    float v = 0.f;
+    if (c < C) {
+      const int32_t u = uniq[c];
+      if (u >= 0) {
+        const int64_t sidx = u / N - (W - 1);
+        const int64_t n = u - (sidx + W - 1) * N;
+        const int64_t src = sidx >= 0 ? ((sidx * N + n) * W + (W - 1)) * F + f
+                                      : ((n * W) + (W - 1 + sidx)) * F + f;
+        v = Elem<DT>::load(static_cast<const typename Elem<DT>::T*>(obs), src);
+      }
+      if (blockIdx.y == 0) x_out[c * F + f] = v;
+    }
+    xs[r][f] = v;
+  }
+  __syncthreads();
+  const int r = tid >> 4, q = tid & 15;
+  const int64_t ca = c0 + r, cb = c0 + r + 16;
+  const int col = n0 + 4 * q;
+  if (ca >= C || col >= N1) return;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f), bb = a;
+#pragma unroll
+  for (int f = 0; f < kGlMaxF; ++f) {
+    if (f < F) {
+      const float xa = xs[r][f], xb = xs[r + 16][f];
+      const float4 wv = wt4[f * (kGlCols / 4) + q];
+      a.x = fmaf(xa, wv.x, a.x); a.y = fmaf(xa, wv.y, a.y);
+      a.z = fmaf(xa, wv.z, a.z); a.w = fmaf(xa, wv.w, a.w);
+      bb.x = fmaf(xb, wv.x, bb.x); bb.y = fmaf(xb, wv.y, bb.y);
+      bb.z = fmaf(xb, wv.z, bb.z); bb.w = fmaf(xb, wv.w, bb.w);
+    }
+  }
+  const float4 bv = bs4[q];
+  a.x += bv.x; a.y += bv.y; a.z += bv.z; a.w += bv.w;
+  bb.x += bv.x; bb.y += bv.y; bb.z += bv.z; bb.w += bv.w;
+  if (RELU) {
+    a = make_float4(fmaxf(a.x, 0.f), fmaxf(a.y, 0.f), fmaxf(a.z, 0.f), fmaxf(a.w, 0.f));
+    bb = make_float4(fmaxf(bb.x, 0.f), fmaxf(bb.y, 0.f), fmaxf(bb.z, 0.f), fmaxf(bb.w, 0.f));
+  }
+  *reinterpret_cast<float4*>(h_out + ca * N1 + col) = a;
+  if (cb < C) *reinterpret_cast<float4*>(h_out + cb * N1 + col) = bb;
+}
+
 // h[i, k, :] = enc[pos_of[u(i, k)], :] for the M samples perm[0..M) (b = t*N + n)
 template <int VEC>
 __global__ __launch_bounds__(256) void frames_expand_kernel(
@@ -351,4 +427,42 @@ extern "C" int ocppo_frames_scatter_relu(ocppo_stream_t stream, const float* dh,
                      as_stream(stream), dh, M, E, uniq, C, inv, mb, dones, T, N, (int)W, out,
                      gp_out, dbp);
   return check_launch("ocppo_frames_scatter_relu");
+}
+
+extern "C" int ocppo_frames_gather_linear(ocppo_stream_t stream, const void* obs, int obs_dtype,
+                                          int64_t T, int64_t N, int64_t W, int64_t F,
+                                          const int32_t* uniq, int64_t C, const float* w,
+                                          const float* b, int64_t N1, int relu, float* x_out,
+                                          float* h_out) {
+  OCPPO_REQUIRE(T >= 1 && N >= 1 && W >= 1 && W <= kFramesMaxW && F >= 1 && F <= kGlMaxF &&
+                    N1 >= 4 && N1 % 4 == 0 && N1 <= kGlMaxN && C >= 0 &&
+                    (T + W - 1) * N < INT32_MAX,
+                "ocppo_frames_gather_linear: bad sizes (F <= %d, N1 %% 4 == 0, N1 <= %d)",
+                kGlMaxF, kGlMaxN);
+  if (C == 0) return OCPPO_OK;
+  OCPPO_REQUIRE(obs && uniq && w && x_out && h_out, "ocppo_frames_gather_linear: null pointer");
+  OCPPO_REQUIRE(aligned16(h_out), "ocppo_frames_gather_linear: h_out must be 16-B aligned");
+  clear_stale_error();
+  hipStream_t s = as_stream(stream);
+  const int64_t g = (C + kGlRows - 1) / kGlRows;
+  OCPPO_REQUIRE(g <= INT32_MAX, "ocppo_frames_gather_linear: too large");
+  const dim3 grid(static_cast<unsigned>(g), static_cast<unsigned>((N1 + kGlCols - 1) / kGlCols));
+  const dim3 block(256);
+#define OCPPO_GL(DT)                                                                              \
+  do {                                                                                            \
+    if (relu)                                                                                     \
+      hipLaunchKernelGGL((frames_gather_linear_kernel<DT, true>), grid, block, 0, s, obs, N,      \
+                         (int)W, (int)F, uniq, C, w, b, (int)N1, x_out, h_out);                   \
+    else                                                                                          \
+      hipLaunchKernelGGL((frames_gather_linear_kernel<DT, false>), grid, block, 0, s, obs, N,     \
+                         (int)W, (int)F, uniq, C, w, b, (int)N1, x_out, h_out);                   \
+  } while (0)
+  switch (obs_dtype) {
+    case OCPPO_F32: OCPPO_GL(OCPPO_F32); break;
+    case OCPPO_BF16: OCPPO_GL(OCPPO_BF16); break;
+    case OCPPO_U8: OCPPO_GL(OCPPO_U8); break;
+    default: return fail(OCPPO_E_INVALID, "ocppo_frames_gather_linear: bad obs dtype %d", obs_dtype);
+  }
+#undef OCPPO_GL
+  return check_launch("ocppo_frames_gather_linear");
 }

@@ -154,6 +154,49 @@ class _FramesExpand(torch.autograd.Function):
         return denc, None, None, None, None, None, None, None, None, None, None
 
 
+# The frame gather and the encoder's first Linear(+ReLU) as one HIP launch
+# (ops.frames_gather_linear) when that layer has <= 16 inputs and FlatAdam-owned grads; its
+# backward is the one-pass ReLU-backward + bias + weight gradient (ops.relu_bias_wgrad).
+FUSED_GATHER_L1 = True
+
+
+class _GatherLinear1(torch.autograd.Function):
+    """h1 = relu(frames_gather(obs, uniq) @ W1^T + b1); backward = dW1 / db1 only (the frames
+    need no gradient), written into the FlatAdam-owned grads."""
+
+    @staticmethod
+    def forward(ctx, w, b, obs, uniq):
+        x, h1 = ops.timed("frames_gather_linear",
+                          lambda: ops.frames_gather_linear(obs, uniq, w, b, relu=True))
+        ctx.save_for_backward(x, h1)
+        ctx.params = (w, b)
+        return h1
+
+    @staticmethod
+    def backward(ctx, g):
+        x, h1 = ctx.saved_tensors
+        w, b = ctx.params
+        g = g.contiguous()
+        ops.timed(f"relu_bias_wgrad_{g.shape[0]}x{g.shape[1]}x{x.shape[1]}",
+                  lambda: ops.relu_bias_wgrad(g, h1, x, dw=w.grad, db=b.grad))
+        return None, None, None, None
+
+
+def _gather_l1_ok(agent, obs, split: int) -> bool:
+    from .agents import _direct
+
+    net = agent.network
+    flat = getattr(agent, "_flat", 0)
+    if not (FUSED_GATHER_L1 and torch.is_grad_enabled() and obs.is_cuda and flat >= 4
+            and (split == 0 or split >= 2) and isinstance(net[0], torch.nn.Linear)
+            and isinstance(net[1], torch.nn.ReLU) and net[0].bias is not None):
+        return False
+    l1 = net[0]
+    return (l1.in_features == obs.shape[-1] <= 16 and l1.out_features % 4 == 0
+            and l1.out_features <= 1024 and _direct(l1.weight) and _direct(l1.bias)
+            and l1.weight.is_contiguous())
+
+
 def minibatch_hidden(agent, obs, dones, uniq, pos_of, inv, perm, mb: int, split: int = 0):
     """Decoder output of PPObj for the samples `perm` (one minibatch) from the rollout obs
     [T+1, N, W, F] with each distinct frame encoded once; autograd flows to every parameter.
@@ -168,8 +211,22 @@ def minibatch_hidden(agent, obs, dones, uniq, pos_of, inv, perm, mb: int, split:
 
     T1, N, W, _ = obs.shape
     T = T1 - 1
-    x = ops.timed("frames_gather", lambda: ops.frames_gather(obs, uniq))
     cut = None
+    if _gather_l1_ok(agent, obs, split):
+        l1 = agent.network[0]
+        h1 = _GatherLinear1.apply(l1.weight, l1.bias, obs, uniq)
+        if split:
+            low = fused_trunk(agent.network[2:split], h1)
+            low_d = low.detach().requires_grad_()
+            enc = fused_trunk(agent.network[split:agent._flat], low_d)
+            cut = (low, low_d)
+        else:
+            enc = fused_trunk(agent.network[2:agent._flat], h1)
+        h = _FramesExpand.apply(enc.contiguous(), pos_of, perm, dones, uniq, inv, mb, T, N, W,
+                                getattr(enc, "_ocppo_box", None))
+        hidden = agent.decode(h)
+        return (hidden, cut) if split else hidden
+    x = ops.timed("frames_gather", lambda: ops.frames_gather(obs, uniq))
     if split:
         low = fused_trunk(agent.network[:split], x)
         low_d = low.detach().requires_grad_()

@@ -813,6 +813,27 @@ def frames_gather(obs, uniq, out=None):
     return out
 
 
+def frames_gather_linear(obs, uniq, weight, bias=None, relu: bool = True, x_out=None,
+                         h_out=None):
+    """(x, h): frames_gather(obs, uniq) and act(x @ weight.T + bias) in one launch
+    (ocppo_frames_gather_linear: the update's first encoder layer over the distinct frames)."""
+    T, N, W, F = _obs_TNWF(obs)
+    dev = obs.device
+    C = uniq.numel()
+    N1 = weight.shape[0]
+    f = torch.float32
+    if x_out is None:
+        x_out = torch.empty((C, F), dtype=f, device=dev)
+    if h_out is None:
+        h_out = torch.empty((C, N1), dtype=f, device=dev)
+    call("ocppo_frames_gather_linear", _stream(dev), _check(obs, "obs", None, dev),
+         _DTYPE_CODE[obs.dtype], T, N, W, F, _check(uniq, "uniq", torch.int32, dev), C,
+         _check(weight, "weight", f, dev, N1 * F), _opt(bias, "bias", f, dev, N1), N1,
+         int(bool(relu)), _check(x_out, "x_out", f, dev, C * F),
+         _check(h_out, "h_out", f, dev, C * N1))
+    return x_out, h_out
+
+
 def frames_expand(enc, pos_of, perm, dones, T: int, N: int, W: int, out=None):
     """h[i, k, :] = enc[pos_of[timeline id of slot k of sample perm[i]]] -> [M, W, E] f32.
     enc [C, E] f32, pos_of [(T+W-1)*N] int32, perm [M] int64, dones [T+1, N] f32."""

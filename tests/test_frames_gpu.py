@@ -90,6 +90,36 @@ def test_frames_scatter_relu_is_scatter_then_relu_backward(dev, T, N, W, M, E, n
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32, torch.uint8])
+@pytest.mark.parametrize("T,N,W,F,N1,p_done,bias,relu", [
+    (16, 8, 4, 12, 256, 0.2, True, True),    # PPObj's first encoder layer shape
+    (9, 5, 3, 6, 20, 0.5, False, True),      # ragged sizes, no bias
+    (10, 3, 16, 16, 1024, 0.1, True, False),  # F = 16, N1 = 1024 (the maxima), identity
+    (12, 4, 4, 3, 100, 0.2, True, True),     # N1 not a multiple of the 64-column block
+])
+def test_frames_gather_linear_is_gather_then_linear(dev, dtype, T, N, W, F, N1, p_done, bias,
+                                                    relu):
+    """ocppo_frames_gather_linear: x is frames_gather bit for bit (the oracle), and h = act(x W^T
+    + b) to f32 rounding of an f64 product (padding rows -1 give x = 0, h = act(b))."""
+    s = _setup(T, N, W, F, 2 * N, 1, max(T // 2, 1), p_done, 21, dev, dtype)
+    uniq, _, _ = s["plan"]
+    du, _, _ = s["d_plan"]
+    g = torch.Generator(device=dev).manual_seed(1)
+    w = torch.randn((N1, F), device=dev, generator=g) * F ** -0.5
+    b = torch.randn(N1, device=dev, generator=g) if bias else None
+    for j in range(du.shape[0]):
+        x, h = ops.frames_gather_linear(s["d_obs"], du[j], w, b, relu=relu)
+        want_x = O.frames_gather(s["obs"], uniq[j])
+        if dtype != torch.float32:  # the device obs are stored rounded
+            want_x = ops.frames_gather(s["d_obs"], du[j]).cpu().numpy()
+        assert np.array_equal(x.cpu().numpy(), want_x)
+        ref = x.double() @ w.double().t() + (b.double() if bias else 0)
+        ref = ref.clamp_min(0) if relu else ref
+        # f32 fma chain over F terms + bias: |err| <= (F + 1) u sum |x_f w_f| + |b| (u = 2^-24)
+        scale = x.double().abs() @ w.double().abs().t() + (b.double().abs() if bias else 0)
+        assert bool(((h.double() - ref).abs() <= (F + 2) * 2.0 ** -24 * scale + 1e-30).all())
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32, torch.uint8])
 def test_frames_at_config_size_reproduce_the_minibatch(dev, dtype):
     """Config 2 sizes (T=128, N=128, W=4, F=12, 4 x 4 minibatches of 4096): the deduplicated
     frames, expanded, ARE b_obs[mb_inds] bit for bit; scatter is expand's adjoint."""
