@@ -112,6 +112,9 @@ def kernel_bytes(tr) -> dict:
         F = D
         # frame id 4 + f32 row out (storage-dtype row in)
         kb["frames_gather"] = C * (4 + F * (sb + 4))
+        # ... fused with the first encoder Linear+ReLU: + the f32 [C, N1] output (W1 from L2)
+        N1 = tr.agent.network[0].out_features if hasattr(tr.agent, "network") else 0
+        kb["frames_gather_linear"] = C * (4 + F * (sb + 4) + 4 * N1)
         # perm 8 + W x (dones 4 + pos_of 4) per sample; W encoded rows in, W rows out
         kb["frames_expand"] = M * (8 + 8 * W + 8 * W * E)
         # dh rows in, one row out per distinct frame
