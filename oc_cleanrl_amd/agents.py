@@ -100,14 +100,30 @@ def _dx(g, w):
     return g.mm(w)
 
 
-def _defer_db_ok(g, x, w, b) -> bool:
+def _defer_db_ok(g, x, wgrad, b) -> bool:
     """The bias gradient can ride in the split-K combine of the weight gradient (HIP sum_splits
-    path, FlatAdam-owned aligned grads)."""
+    path, FlatAdam-owned aligned grads; wgrad = where the weight gradient is written)."""
     rows, n = g.shape
     k = x.shape[1]
     return (DEFER_BIAS_GRAD and HIP_SUM_SPLITS and _splitk(rows, k, n) > 1 and (n * k) % 4 == 0
-            and n % 4 == 0 and w.grad.data_ptr() % 16 == 0 and b.grad.data_ptr() % 16 == 0
-            and w.grad.is_contiguous())
+            and n % 4 == 0 and wgrad.data_ptr() % 16 == 0 and b.grad.data_ptr() % 16 == 0
+            and wgrad.is_contiguous())
+
+
+def _cols_to_nhwc(w, chw):
+    """Linear weight [O, C*H*W] (columns in nn.Flatten's NCHW order) -> [O, H*W*C] (a copy)."""
+    C, H, W = chw
+    return w.view(w.shape[0], C, H, W).permute(0, 2, 3, 1).reshape(w.shape[0], H * W * C)
+
+
+def _cols_from_nhwc(w_nhwc, chw, out=None):
+    """Inverse of _cols_to_nhwc, written into `out` when given."""
+    C, H, W = chw
+    v = w_nhwc.view(w_nhwc.shape[0], H, W, C).permute(0, 3, 1, 2)
+    if out is not None:
+        out.view(out.shape[0], C, H, W).copy_(v)
+        return out
+    return v.reshape(w_nhwc.shape[0], C * H * W)
 
 
 # relu_bias_grad without its last-arriver tail: bias-gradient chunk sums finished by the weight
@@ -131,18 +147,39 @@ class _LinearAct(torch.autograd.Function):
     for FlatAdam-owned parameters dW/db are written straight into the flat grad buffer."""
 
     @staticmethod
-    def forward(ctx, x, w, b, relu: bool, box=None):
-        out = torch._addmm_activation(b, x, w.t(), use_gelu=False) if relu else \
-            torch.addmm(b, x, w.t())
+    def forward(ctx, x, w, b, relu: bool, box=None, chw=None):
+        # chw = (C, H, W): x is a channels_last activation flattened in its memory (H, W, C)
+        # order, so the weight's columns are permuted to match instead (linear_act_nhwc)
+        wm = _cols_to_nhwc(w, chw) if chw is not None else w
+        out = torch._addmm_activation(b, x, wm.t(), use_gelu=False) if relu else \
+            torch.addmm(b, x, wm.t())
         ctx.relu = relu
         ctx.save_for_backward(x, w, out if relu else None)
         ctx.w, ctx.b = w, b
+        ctx.chw, ctx.wm = chw, (wm if chw is not None else None)
         ctx.box = box  # _Heads sets box["premasked"]: g arrives masked, bias grad already written
         return out
 
     @staticmethod
     def backward(ctx, g):
+        chw = ctx.chw
+        if chw is None:
+            return _LinearAct._backward(ctx, g, ctx.w.grad)
+        # permuted columns: weight gradient formed in the NHWC column order, then put back
+        direct = _direct(ctx.w)
+        wgrad = torch.empty_like(ctx.wm) if direct else None
+        dx, dw, db, _, _, _ = _LinearAct._backward(ctx, g, wgrad)
+        if direct and ctx.needs_input_grad[1]:
+            _cols_from_nhwc(wgrad, chw, out=ctx.w.grad)
+        if dw is not None:
+            dw = _cols_from_nhwc(dw, chw)
+        return dx, dw, db, None, None, None
+
+    @staticmethod
+    def _backward(ctx, g, wgrad):
         x, w, out = ctx.saved_tensors
+        if ctx.wm is not None:
+            w = ctx.wm
         db = None
         bias_done = False
         g = g.contiguous()
@@ -153,32 +190,32 @@ class _LinearAct(torch.autograd.Function):
             dx = _dx(g, w) if ctx.needs_input_grad[0] else None
             dbp = ctx.box.get("dbp")
             if dbp is None:
-                _weight_grad(g, x, out=ctx.w.grad)
-            elif _defer_db_ok(g, x, ctx.w, ctx.b):
-                _weight_grad(g, x, out=ctx.w.grad, db=(dbp, ctx.b.grad))
+                _weight_grad(g, x, out=wgrad)
+            elif _defer_db_ok(g, x, wgrad, ctx.b):
+                _weight_grad(g, x, out=wgrad, db=(dbp, ctx.b.grad))
             else:
-                _weight_grad(g, x, out=ctx.w.grad)
+                _weight_grad(g, x, out=wgrad)
                 torch.sum(dbp[0], 0, out=ctx.b.grad)
-            return dx, None, None, None, None
+            return dx, None, None, None, None, None
         if FUSED_FIRST_LAYER_BWD and not ctx.needs_input_grad[0] and ctx.needs_input_grad[1] \
                 and ctx.needs_input_grad[2] and _direct(ctx.w) and _direct(ctx.b) and \
                 ops.relu_bias_wgrad_ok(g, x):
             # input layer (no dX): ReLU-backward + bias grad + weight grad in one HIP pass
             o = out if ctx.relu else None
             ops.timed(f"relu_bias_wgrad_{g.shape[0]}x{g.shape[1]}x{x.shape[1]}",
-                      lambda: ops.relu_bias_wgrad(g, o, x, dw=ctx.w.grad, db=ctx.b.grad))
-            return None, None, None, None, None
+                      lambda: ops.relu_bias_wgrad(g, o, x, dw=wgrad, db=ctx.b.grad))
+            return None, None, None, None, None, None
         if FUSED_RELU_BIAS_GRAD and ctx.needs_input_grad[2] and _direct(ctx.b) and \
                 ops.relu_bias_grad_ok(g) and ctx.needs_input_grad[1] and _direct(ctx.w) and \
-                _defer_db_ok(g, x, ctx.w, ctx.b):
+                _defer_db_ok(g, x, wgrad, ctx.b):
             # ReLU-backward in one pass, bias grad finished with the split-K weight-grad combine
             o = out if ctx.relu else None
             gp, dbp = ops.timed(f"relu_bias_grad_{g.shape[0]}x{g.shape[1]}" +
                                 ("" if ctx.relu else "_norelu"),
                                 lambda: ops.relu_bias_grad_partial(g, o))
             dx = _dx(gp, w) if ctx.needs_input_grad[0] else None
-            _weight_grad(gp, x, out=ctx.w.grad, db=(dbp, ctx.b.grad))
-            return dx, None, None, None, None
+            _weight_grad(gp, x, out=wgrad, db=(dbp, ctx.b.grad))
+            return dx, None, None, None, None, None
         if FUSED_RELU_BIAS_GRAD and ctx.needs_input_grad[2] and _direct(ctx.b) and \
                 ops.relu_bias_grad_ok(g):
             # threshold_backward + bias sum in one HIP pass, bias grad written in place
@@ -193,7 +230,7 @@ class _LinearAct(torch.autograd.Function):
         dw = None
         if ctx.needs_input_grad[1]:
             if _direct(ctx.w):
-                _weight_grad(gp, x, out=ctx.w.grad)
+                _weight_grad(gp, x, out=wgrad)
             else:
                 dw = _weight_grad(gp, x)
         if ctx.needs_input_grad[2] and not bias_done:
@@ -201,7 +238,7 @@ class _LinearAct(torch.autograd.Function):
                 torch.sum(gp, 0, out=ctx.b.grad)
             else:
                 db = gp.sum(0)
-        return dx, dw, db, None, None
+        return dx, dw, db, None, None, None
 
 
 class _Heads(torch.autograd.Function):
@@ -386,21 +423,44 @@ def _hip_linear_ok(x2, lin: nn.Linear) -> bool:
             (M <= 128 and (K <= 256 or (K <= 2048 and K % 16 == 0))) or M <= 8)
 
 
-def linear_act(x, lin: nn.Linear, relu: bool):
+def linear_act(x, lin: nn.Linear, relu: bool, chw=None):
     lead = x.shape[:-1]
     x2 = x.reshape(-1, x.shape[-1])
-    if _hip_linear_ok(x2, lin):
+    if chw is None and _hip_linear_ok(x2, lin):
         y = ops.linear_act(x2, lin.weight, lin.bias, relu)
         return y.view(*lead, y.shape[-1])
     box = None
     if relu and FUSED_HEADS_BWD and torch.is_grad_enabled() and _direct(lin.weight) and \
             _direct(lin.bias):
         box = {"premasked": False, "bias": lin.bias}
-    y = _LinearAct.apply(x2, lin.weight, lin.bias, relu, box)
+    y = _LinearAct.apply(x2, lin.weight, lin.bias, relu, box, chw)
     y = y.view(*lead, y.shape[-1])
     if box is not None:
         y._ocppo_box = box
     return y
+
+
+# nn.Flatten -> nn.Linear on a channels_last activation under autograd (the NatureCNN's
+# 3136 -> 512 layer in the update): the Linear reads the activation in its memory order with the
+# weight's columns permuted to match (a 6.4 MB copy) instead of nn.Flatten's NCHW-order copy of the
+# activation and the channels_last copy of its gradient (2 x 103 MB per minibatch of 8192).
+FLAT_NHWC_LINEAR = True
+
+
+def _flat_nhwc_ok(x, flat, lin) -> bool:
+    return (FLAT_NHWC_LINEAR and torch.is_grad_enabled() and isinstance(flat, nn.Flatten)
+            and isinstance(lin, nn.Linear) and lin.bias is not None and x.is_cuda
+            and x.dtype == torch.float32 and x.dim() == 4 and flat.start_dim == 1
+            and flat.end_dim in (-1, 3) and x.is_contiguous(memory_format=torch.channels_last)
+            and not x.is_contiguous() and lin.in_features == x[0].numel())
+
+
+def linear_act_nhwc(x, lin: nn.Linear, relu: bool):
+    """act(lin(flatten(x))) for a channels_last x [B, C, H, W], without materialising the
+    NCHW-order flatten: same products and sums as the reference layer, columns visited in (H, W,
+    C) order (the f32 GEMM's summation order over K differs accordingly)."""
+    B, C, H, W = x.shape
+    return linear_act(x.permute(0, 2, 3, 1).reshape(B, H * W * C), lin, relu, (C, H, W))
 
 
 def linear_relu(x, lin: nn.Linear):
@@ -452,6 +512,10 @@ def fused_trunk(seq: nn.Sequential, x):
             relu = i + 1 < len(mods) and isinstance(mods[i + 1], nn.ReLU)
             x = _ConvAct.apply(x, m.weight, m.bias, m.stride, m.padding, relu)
             i += 2 if relu else 1
+        elif i + 1 < len(mods) and _flat_nhwc_ok(x, m, mods[i + 1]):
+            relu = i + 2 < len(mods) and isinstance(mods[i + 2], nn.ReLU)
+            x = linear_act_nhwc(x, mods[i + 1], relu)
+            i += 3 if relu else 2
         elif fusable and i + 1 < len(mods) and isinstance(mods[i + 1], nn.ReLU):
             x = linear_relu(x, m)
             i += 2

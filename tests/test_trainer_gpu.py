@@ -212,6 +212,8 @@ def test_nhwc_conv_act_matches_module_forward_and_grads(dev):
     x = torch.randint(0, 256, (16, 4, 84, 84), device=dev).float()
     x = x.contiguous(memory_format=torch.channels_last)
     assert agents._conv_act_ok(x, ag.network[1])
+    feat = ag.network[:7](x)  # the last conv's ReLU output: flatten + Linear read it as NHWC
+    assert agents._flat_nhwc_ok(feat, ag.network[7], ag.network[8])
     h1 = ag.network(x)
     h2 = ag.trunk(x)
     torch.testing.assert_close(h2, h1, rtol=1e-5, atol=1e-5)
