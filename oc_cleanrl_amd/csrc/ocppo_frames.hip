@@ -96,9 +96,10 @@ __global__ __launch_bounds__(256) void frames_gather_linear_kernel(
     float v = 0.f;
     if (c < C) {
       const int32_t u = uniq[c];
-      if (u >= 0) {
-        const int64_t sidx = u / N - (W - 1);
-        const int64_t n = u - (sidx + W - 1) * N;
+      if (u >= 0) {  // u < (T + W - 1) * N < 2^31 (checked on the host): 32-bit division
+        const int32_t n32 = static_cast<int32_t>(N), q = u / n32;
+        const int64_t sidx = q - (W - 1);
+        const int64_t n = u - q * n32;
         const int64_t src = sidx >= 0 ? ((sidx * N + n) * W + (W - 1)) * F + f
                                       : ((n * W) + (W - 1 + sidx)) * F + f;
         v = Elem<DT>::load(static_cast<const typename Elem<DT>::T*>(obs), src);
