@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define OCPPO_ABI_VERSION 15
+#define OCPPO_ABI_VERSION 16
 
 /* status codes */
 #define OCPPO_OK 0
@@ -280,6 +280,11 @@ OCPPO_API int ocppo_linear_act(ocppo_stream_t stream, const float* x, int64_t ld
  * y [R, N] f32, b [N] f32, both 16-B aligned, N % 4 == 0. */
 OCPPO_API int ocppo_bias_act(ocppo_stream_t stream, float* y, const float* b, int64_t R, int64_t N,
                    int relu);
+/* The same epilogue with the output in NCHW order (the rollout's last NatureCNN convolution, whose
+ * nn.Flatten reads NCHW, architectures/ppo.py:20-31): out[b, c, p] = act(y[b, p, c] + bias[c]),
+ * y [B, P, C] NHWC f32 (P = H*W), out [B, C, P] f32 (not aliasing y), P * (C + 1) <= 12288. */
+OCPPO_API int ocppo_bias_act_nchw(ocppo_stream_t stream, const float* y, const float* b, int64_t B,
+                                  int64_t P, int64_t C, int relu, float* out);
 
 /* ---------------------------------------------------------------------------------------------
  * Split-K combine of a weight gradient — replaces ATen's `sum(0)` after the batched (split-K)

@@ -22,7 +22,7 @@ LIB_PATH = Path(os.environ.get("OCPPO_LIB", PKG / "lib" / "libocppo_hip.so"))
 HEADER = PKG.parent / "include" / "ocppo.h"
 
 # constants mirrored from include/ocppo.h (checked against the header by tests/test_abi.py)
-OCPPO_ABI_VERSION = 15
+OCPPO_ABI_VERSION = 16
 OCPPO_OK, OCPPO_E_INVALID, OCPPO_E_LAUNCH, OCPPO_E_WORKSPACE = 0, 1, 2, 3
 OCPPO_F32, OCPPO_BF16, OCPPO_U8 = 0, 1, 2
 STAT_NAMES = ("loss", "pg_loss", "v_loss", "entropy", "old_approx_kl", "approx_kl", "clipfrac",
@@ -64,6 +64,7 @@ SIGNATURES: dict[str, tuple[type, list]] = {
     "ocppo_heads_bwd_workspace_bytes": (SZ, [I64, I64, I64]),
     "ocppo_heads_bwd": (I, [P, P, P, P, P, P, P, P, P, P, P, P, I64, I64, I64, I, P, SZ]),
     "ocppo_bias_act": (I, [P, P, P, I64, I64, I]),
+    "ocppo_bias_act_nchw": (I, [P, P, P, I64, I64, I64, I, P]),
     "ocppo_sum_splits": (I, [P, P, I64, I64, P]),
     "ocppo_frames_gather": (I, [P, P, I, I64, I64, I64, I64, P, I64, P]),
     "ocppo_frames_expand": (I, [P, P, I64, I64, P, P, I64, P, I64, I64, I64, P]),

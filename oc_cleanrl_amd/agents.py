@@ -440,6 +440,24 @@ def linear_act(x, lin: nn.Linear, relu: bool, chw=None):
     return y
 
 
+# Inference (the rollout): the last convolution's bias + ReLU pass writes its output in NCHW order
+# (ops.bias_act_nchw) when an nn.Flatten follows, instead of the in-place NHWC pass and the
+# Flatten's layout copy (3.2 MB per step at 256 envs).
+CONV_NCHW_OUT = True
+
+
+def _conv_nchw_out_ok(x, conv, nxt) -> bool:
+    if not (CONV_NCHW_OUT and not torch.is_grad_enabled() and len(nxt) == 2 and
+            isinstance(nxt[0], nn.ReLU) and isinstance(nxt[1], nn.Flatten) and
+            nxt[1].start_dim == 1 and _conv_act_ok(x, conv) and x.shape[0] > 0):
+        return False
+    kh, kw = conv.kernel_size
+    (sh, sw), (ph, pw) = conv.stride, conv.padding
+    oh = (x.shape[2] + 2 * ph - kh) // sh + 1
+    ow = (x.shape[3] + 2 * pw - kw) // sw + 1
+    return oh * ow * (conv.out_channels + 1) <= 12288
+
+
 # nn.Flatten -> nn.Linear on a channels_last activation under autograd (the NatureCNN's
 # 3136 -> 512 layer in the update): the Linear reads the activation in its memory order with the
 # weight's columns permuted to match (a 6.4 MB copy) instead of nn.Flatten's NCHW-order copy of the
@@ -508,6 +526,13 @@ def fused_trunk(seq: nn.Sequential, x):
             relu = i + 1 < len(mods) and isinstance(mods[i + 1], nn.ReLU)
             x = ops.conv2d_act(x, m.weight, m.bias, m.stride[0], relu)
             i += 2 if relu else 1
+        elif _conv_nchw_out_ok(x, m, mods[i + 1:i + 3]):
+            # inference: the bias/ReLU pass writes NCHW, so the nn.Flatten after it is a view
+            y = torch.ops.aten.convolution(x, m.weight, None, m.stride, m.padding, (1, 1), False,
+                                           (0, 0), 1).contiguous(memory_format=torch.channels_last)
+            x = ops.timed("bias_act_nchw",
+                          lambda y=y, b=m.bias: ops.bias_act_nchw(y, b, True))  # bound now
+            i += 2
         elif _conv_act_ok(x, m):
             relu = i + 1 < len(mods) and isinstance(mods[i + 1], nn.ReLU)
             x = _ConvAct.apply(x, m.weight, m.bias, m.stride, m.padding, relu)

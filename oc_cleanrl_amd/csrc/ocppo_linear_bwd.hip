@@ -306,6 +306,58 @@ extern "C" int ocppo_bias_act(ocppo_stream_t stream, float* y, const float* b, i
   return check_launch("ocppo_bias_act");
 }
 
+// ---- the same epilogue written out in NCHW order: out[b, c, p] = act(y[b, p, c] + bias[c]) for an
+// NHWC convolution output y [B, P, C] (P = H*W) whose consumer flattens in NCHW order (nn.Flatten
+// before a Linear): one image per workgroup through LDS (row stride C + 1: conflict-free reads
+// down a channel), coalesced reads of y and writes of out -- the layout copy rides in the pass.
+namespace ocppo {
+constexpr int kBaNchwMaxElems = 12288;  // P * (C + 1) floats of LDS (48 KB)
+
+template <bool RELU>
+__global__ __launch_bounds__(256) void bias_act_nchw_kernel(const float* __restrict__ y,
+                                                            const float* __restrict__ bias,
+                                                            int P, int C,
+                                                            float* __restrict__ out) {
+  extern __shared__ float tile[];
+  const int64_t img = blockIdx.x;
+  const float* src = y + img * P * C;
+  float* dst = out + img * P * C;
+  const int ld = C + 1;
+  for (int i = threadIdx.x; i < P * C; i += 256) {
+    const int p = i / C, c = i - p * C;
+    tile[p * ld + c] = src[i];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < P * C; i += 256) {
+    const int c = i / P, p = i - c * P;
+    float v = tile[p * ld + c] + bias[c];
+    if (RELU) v = fmaxf(v, 0.f);
+    dst[i] = v;
+  }
+}
+}  // namespace ocppo
+
+extern "C" int ocppo_bias_act_nchw(ocppo_stream_t stream, const float* y, const float* b,
+                                   int64_t B, int64_t P, int64_t C, int relu, float* out) {
+  OCPPO_REQUIRE(B >= 0 && P >= 1 && C >= 1 && P * (C + 1) <= ocppo::kBaNchwMaxElems &&
+                    B <= INT32_MAX,
+                "ocppo_bias_act_nchw: bad sizes B=%lld P=%lld C=%lld (P * (C + 1) <= %d)",
+                (long long)B, (long long)P, (long long)C, ocppo::kBaNchwMaxElems);
+  if (B == 0) return OCPPO_OK;
+  OCPPO_REQUIRE(y && b && out, "ocppo_bias_act_nchw: null pointer");
+  OCPPO_REQUIRE(y != out, "ocppo_bias_act_nchw: out must not alias y");
+  clear_stale_error();
+  const dim3 grid(static_cast<unsigned>(B)), block(256);
+  const size_t lds = static_cast<size_t>(P) * (C + 1) * sizeof(float);
+  if (relu)
+    hipLaunchKernelGGL(ocppo::bias_act_nchw_kernel<true>, grid, block, lds, as_stream(stream), y,
+                       b, (int)P, (int)C, out);
+  else
+    hipLaunchKernelGGL(ocppo::bias_act_nchw_kernel<false>, grid, block, lds, as_stream(stream),
+                       y, b, (int)P, (int)C, out);
+  return check_launch("ocppo_bias_act_nchw");
+}
+
 // ---- split-K combine of a weight gradient: out[i] = part[0][i] + part[1][i] + ... (split order)
 // The update's tall-skinny weight-gradient GEMMs dW = g'^T x (inside loss.backward(),
 // ppo_atari_oc.py:605, for the PPObj Linear layers of architectures/ppo.py:60-84) run as a

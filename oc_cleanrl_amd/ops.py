@@ -770,6 +770,24 @@ def bias_act(y, b, relu: bool = True):
     return y
 
 
+def bias_act_nchw(y, b, relu: bool = True, out=None):
+    """act(y + b) of a channels_last conv output y [B, C, H, W] (bias-less), returned as an
+    NCHW-contiguous tensor (so an nn.Flatten after it is a view): one pass, layout copy included."""
+    if y.dim() != 4 or not y.is_contiguous(memory_format=torch.channels_last):
+        raise ValueError("y must be a channels_last [B, C, H, W] tensor")
+    B, C, H, W = y.shape
+    dev = y.device
+    f = torch.float32
+    if out is None:
+        out = torch.empty((B, C, H, W), dtype=f, device=dev)
+    if not out.is_contiguous() or tuple(out.shape) != (B, C, H, W):
+        raise ValueError("out must be a contiguous (NCHW) [B, C, H, W] tensor")
+    call("ocppo_bias_act_nchw", _stream(dev), _check(y.permute(0, 2, 3, 1), "y", f, dev),
+         _check(b, "b", f, dev, C),
+         B, H * W, C, int(bool(relu)), _check(out, "out", f, dev, B * C * H * W))
+    return out
+
+
 def sum_splits_ok(part, out) -> bool:
     return (part.is_cuda and part.dtype == torch.float32 and part.is_contiguous() and
             out.is_contiguous() and out.dtype == torch.float32 and part.shape[0] in (1, 2, 4, 8, 16)

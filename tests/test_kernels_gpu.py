@@ -1241,6 +1241,50 @@ def test_rollout_conv_trunk_matches_miopen(ops, dev):
     torch.testing.assert_close(got, want, rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("B,C,H,W,relu", [(256, 64, 7, 7, True), (3, 20, 5, 9, False),
+                                           (1, 1, 1, 1, True), (0, 64, 7, 7, True),
+                                           (5, 96, 8, 16, True)])  # P * (C + 1) = 12416 > max
+def test_bias_act_nchw(ops, dev, B, C, H, W, relu):
+    """ocppo_bias_act_nchw: act(y + b) of a channels_last tensor written NCHW-contiguous, bit for
+    bit torch's (y + b).relu() (one f32 add, then max)."""
+    g = torch.Generator(device=dev).manual_seed(C + H)
+    y = torch.randn(B, C, H, W, device=dev, generator=g).contiguous(
+        memory_format=torch.channels_last)
+    b = torch.randn(C, device=dev, generator=g)
+    if H * W * (C + 1) > 12288:
+        with pytest.raises(RuntimeError, match="bad sizes"):
+            ops.bias_act_nchw(y, b, relu)
+        return
+    out = ops.bias_act_nchw(y, b, relu)
+    assert out.is_contiguous() and out.shape == y.shape
+    want = y + b.view(1, C, 1, 1)
+    want = want.relu() if relu else want
+    assert torch.equal(out, want.contiguous())
+
+
+def test_rollout_trunk_nchw_flatten_matches_module(ops, dev):
+    """The NatureCNN trunk under no_grad (the last conv's bias/ReLU pass writing NCHW for the
+    Flatten) == the module's own forward; the path is taken."""
+    from oc_cleanrl_amd import agents
+    from oc_cleanrl_amd.agents import make_agent
+
+    ag = make_agent("PPO", (4, 84, 84), 4, dev).to(dev).to(memory_format=torch.channels_last)
+    x = (torch.randint(0, 256, (32, 4, 84, 84), device=dev).float() / 255).contiguous(
+        memory_format=torch.channels_last)
+    with torch.no_grad():
+        feat = ag.network[1:5](x)
+        assert agents._conv_nchw_out_ok(feat, ag.network[5], list(ag.network)[6:8])
+        got = ag.trunk(x, prescaled=True)
+        agents.CONV_NCHW_OUT = False
+        try:
+            want = ag.trunk(x, prescaled=True)
+        finally:
+            agents.CONV_NCHW_OUT = True
+        ref = ag.network[1:](x)
+    assert torch.equal(got, want)
+    torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-5)
+
+
 # ---------------------------------------------------------------------------------------------
 # policy heads forward + fused PPO loss + heads backward in one pass (ocppo_heads_loss_fwd_bwd)
 # ---------------------------------------------------------------------------------------------
