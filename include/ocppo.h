@@ -94,8 +94,10 @@ OCPPO_API int ocppo_minibatch_adv_stats(ocppo_stream_t stream, const float* b_ad
 /* Minibatch prepare: the statistics above AND the per-sample records of every minibatch gathered
  * into minibatch order, mb_*[k*M + i] = b_*[perm[k*M + i]] (SoA), so that each
  * ocppo_ppo_loss_fwd_bwd launch can take the already-gathered arrays (mb_inds = NULL) instead of
- * five scattered loads per element (ppo_atari_oc.py:569-593 index b_* by mb_inds).
- *   M <= 16384; adv_stats : [num_mb, 2] or NULL (statistics skipped). */
+ * five scattered loads per element (ppo_atari_oc.py:569-593 index b_* by mb_inds). Two launches:
+ * the gather over all num_mb*M elements on a chip-filling grid, then the statistics over the
+ * gathered advantages (one workgroup per minibatch; the same figures as
+ * ocppo_minibatch_adv_stats). adv_stats : [num_mb, 2] or NULL (statistics skipped). */
 OCPPO_API int ocppo_minibatch_prepare(ocppo_stream_t stream, const int64_t* perm, int64_t M,
                                       int64_t num_mb, const int64_t* b_actions,
                                       const float* b_logprobs, const float* b_advantages,
@@ -515,8 +517,9 @@ OCPPO_API int ocppo_synth_env_step(ocppo_stream_t stream, uint64_t seed, const i
  *   db_h [H] = sum_m gp (the decoder bias grad, may be NULL); dwa [A, H], dwc [H], dba [A],
  *   dbc [1] the heads' grads; stats [9] as ocppo_ppo_loss_fwd_bwd; dlogits [M, A] / dvalue [M]
  *   optional (both NULL or both set).
- * H % 64 == 0, 64 <= H <= 512, 1 <= A <= 7; h, gp, Wa, Wc 16-B aligned. Two launches (rows, then
- * the workgroups' partial records in order): deterministic; workspace =
+ * H in {64, 128, 256, 512} (else OCPPO_E_INVALID), 1 <= A <= 7; h, gp, Wa, Wc 16-B aligned. Two
+ * launches: a fixed grid of at most 512 workgroups, each owning a contiguous row range and writing
+ * ONE partial record, then a fixed-shape tree over the records: deterministic; workspace =
  * ocppo_heads_loss_workspace_bytes(M, H, A), needs no zeroing.
  * ------------------------------------------------------------------------------------------- */
 OCPPO_API size_t ocppo_heads_loss_workspace_bytes(int64_t M, int64_t H, int64_t A);

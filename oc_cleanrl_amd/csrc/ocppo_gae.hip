@@ -2,115 +2,142 @@
 // ppo.py:218-231 and ppo_atari_multigpu.py:288-301).
 //
 // Layout: rewards/values/dones/advantages/returns are [T, N] f32, step-major, so one time row of
-// an env tile is contiguous. A workgroup owns ENV_TILE envs and walks the rollout from t = T-1
-// down in chunks of TC rows:
-//   1. all 256 threads stage the chunk's r, v, d rows into LDS with 16-B loads (coalesced);
-//   2. one lane per env runs the sequential recurrence out of LDS and overwrites r with A;
-//   3. all threads stream A and R = A + v back out with 16-B stores.
-// The recurrence is carried in registers across chunks. The arithmetic is the reference's, op by
-// op, in f32 without contraction (build flag -ffp-contract=off):
-//   nnt = 1 - d';  delta = (r + (f32(gamma) * v') * nnt) - v;  A = delta + (f32(gamma*lambda) * nnt) * A'
-// so advantages and returns are bit-identical to the PyTorch loop.
-// Roofline: HBM-bound, 20 B per (t, n) element + 8 B per env (next_value, next_done).
+// an env tile is contiguous.
+//
+// The recurrence A_t = delta_t + c_t * A_{t+1} is the only serial part, and it is two dependent
+// f32 ops per step; everything else is parallel over (t, n). gae_tile_kernel therefore spreads a
+// rollout over many small workgroups (E envs each, E chosen so that the grid has >= 64
+// workgroups) and splits the work into phases:
+//   1. all 256 threads stage the chunk's r, v, d rows into LDS (16-B loads when E % 4 == 0);
+//   2. all threads form, per (t, n), delta = (r + (f32(gamma) * v') * nnt) - v and
+//      c = f32(gamma*lambda) * nnt with nnt = 1 - d' (v', d' = the next row, or next_value /
+//      next_done / the later chunk's first row at the chunk boundary);
+//   3. one lane per env runs A = delta + c * A over the chunk (LDS operands loaded 8 rows ahead);
+//   4. all threads store A and R = A + v.
+// Every value is the reference's op for op, in f32 without contraction (-ffp-contract=off), so
+// advantages and returns are bit-identical to the PyTorch loop (ppo_atari_oc.py:533-547): only
+// WHERE each op runs changed, not the ops or their order along the recurrence.
+// Roofline: HBM-bound, 20 B per (t, n) element + 8 B per env (next_value, next_done); at config
+// sizes (128 x 128, 328 KB) it is latency-bound, hence the small tiles.
 #include "ocppo_common.h"
 
 namespace ocppo {
 
-template <int ENV_TILE>
-__global__ __launch_bounds__(256) void gae_kernel(const float* __restrict__ rew,
-                                                  const float* __restrict__ val,
-                                                  const float* __restrict__ don,
-                                                  const float* __restrict__ next_val,
-                                                  const float* __restrict__ next_done, int T,
-                                                  int64_t N, int TC, float g, float gl,
-                                                  float* __restrict__ adv, float* __restrict__ ret) {
+template <int E>
+__global__ __launch_bounds__(256) void gae_tile_kernel(const float* __restrict__ rew,
+                                                       const float* __restrict__ val,
+                                                       const float* __restrict__ don,
+                                                       const float* __restrict__ next_val,
+                                                       const float* __restrict__ next_done, int T,
+                                                       int64_t N, int TC, float g, float gl,
+                                                       float* __restrict__ adv,
+                                                       float* __restrict__ ret) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* sr = smem;                  // [TC][ENV_TILE]  rewards in, advantages out
-  float* sv = smem + TC * ENV_TILE;  // [TC][ENV_TILE]  values
-  float* sd = sv + TC * ENV_TILE;    // [TC][ENV_TILE]  dones
+  float* sa = smem;           // [TC][E]  rewards in -> delta -> advantages
+  float* sv = sa + TC * E;    // [TC][E]  values
+  float* sd = sv + TC * E;    // [TC][E]  dones
+  float* sc = sd + TC * E;    // [TC][E]  c = f32(gamma * lambda) * nnt
+  __shared__ float s_cv[E], s_cd[E];  // per env: the value / done of the row after the chunk
 
-  const int64_t n0 = static_cast<int64_t>(blockIdx.x) * ENV_TILE;
+  const int64_t n0 = static_cast<int64_t>(blockIdx.x) * E;
   const int tid = threadIdx.x;
-  const bool vec = (N & 3) == 0;  // every row start is 16-B aligned
-  const bool active = tid < ENV_TILE && n0 + tid < N;
-
-  float last = 0.f, carry_v = 0.f, carry_d = 0.f;
-  if (active) {
-    carry_v = next_val[n0 + tid];
-    carry_d = next_done[n0 + tid];
+  const bool vec = (E % 4) == 0 && (N & 3) == 0;  // every tile row is 16-B aligned
+  const bool chain = tid < E && n0 + tid < N;
+  if (tid < E) {
+    s_cv[tid] = n0 + tid < N ? next_val[n0 + tid] : 0.f;
+    s_cd[tid] = n0 + tid < N ? next_done[n0 + tid] : 0.f;
   }
+  float last = 0.f;
 
   for (int t_hi = T; t_hi > 0; t_hi -= TC) {
     const int t_lo = t_hi > TC ? t_hi - TC : 0;
     const int rows = t_hi - t_lo;
-
     // 1. stage
     if (vec) {
-      constexpr int C4 = ENV_TILE / 4;
-      for (int e = tid; e < rows * C4; e += blockDim.x) {
+      constexpr int C4 = E / 4;
+      for (int e = tid; e < rows * C4; e += 256) {
         const int row = e / C4, c4 = e - row * C4;
         const int64_t col = n0 + 4 * c4;
         if (col < N) {
           const size_t gi = static_cast<size_t>(t_lo + row) * N + col;
-          const int li = row * ENV_TILE + 4 * c4;
-          *reinterpret_cast<float4*>(sr + li) = *reinterpret_cast<const float4*>(rew + gi);
+          const int li = row * E + 4 * c4;
+          *reinterpret_cast<float4*>(sa + li) = *reinterpret_cast<const float4*>(rew + gi);
           *reinterpret_cast<float4*>(sv + li) = *reinterpret_cast<const float4*>(val + gi);
           *reinterpret_cast<float4*>(sd + li) = *reinterpret_cast<const float4*>(don + gi);
         }
       }
     } else {
-      for (int e = tid; e < rows * ENV_TILE; e += blockDim.x) {
-        const int row = e / ENV_TILE, c = e - row * ENV_TILE;
+      for (int e = tid; e < rows * E; e += 256) {
+        const int row = e / E, c = e - row * E;
         const int64_t col = n0 + c;
         if (col < N) {
           const size_t gi = static_cast<size_t>(t_lo + row) * N + col;
-          sr[e] = rew[gi];
+          sa[e] = rew[gi];
           sv[e] = val[gi];
           sd[e] = don[gi];
         }
       }
     }
     __syncthreads();
-
-    // 2. sequential recurrence, one lane per env
-    if (active) {
-      for (int row = rows - 1; row >= 0; --row) {
-        const int li = row * ENV_TILE + tid;
-        const float r = sr[li], v = sv[li], d = sd[li];
-        const float nnt = 1.0f - carry_d;
-        float delta = r + (g * carry_v) * nnt;
-        delta = delta - v;
-        last = delta + (gl * nnt) * last;
-        sr[li] = last;
-        carry_v = v;
-        carry_d = d;
+    // 2. delta and c of every (t, n) of the chunk
+    for (int e = tid; e < rows * E; e += 256) {
+      const int row = e / E, c = e - row * E;
+      const float nv = row + 1 < rows ? sv[e + E] : s_cv[c];
+      const float nd = row + 1 < rows ? sd[e + E] : s_cd[c];
+      const float nnt = 1.0f - nd;
+      float delta = sa[e] + (g * nv) * nnt;
+      sa[e] = delta - sv[e];
+      sc[e] = gl * nnt;
+    }
+    __syncthreads();
+    if (tid < E) {  // the next (earlier) chunk's boundary row
+      s_cv[tid] = sv[tid];
+      s_cd[tid] = sd[tid];
+    }
+    // 3. the recurrence, one lane per env, operands fetched 8 rows ahead of the chain
+    if (chain) {
+      for (int r0 = rows - 1; r0 >= 0; r0 -= 8) {
+        float dl[8], cc[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int r = r0 - k >= 0 ? r0 - k : 0;
+          dl[k] = sa[r * E + tid];
+          cc[k] = sc[r * E + tid];
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          if (r0 - k >= 0) {
+            last = dl[k] + cc[k] * last;
+            sa[(r0 - k) * E + tid] = last;
+          }
+        }
       }
     }
     __syncthreads();
-
-    // 3. write back advantages and returns
+    // 4. advantages and returns
     if (vec) {
-      constexpr int C4 = ENV_TILE / 4;
-      for (int e = tid; e < rows * C4; e += blockDim.x) {
+      constexpr int C4 = E / 4;
+      for (int e = tid; e < rows * C4; e += 256) {
         const int row = e / C4, c4 = e - row * C4;
         const int64_t col = n0 + 4 * c4;
         if (col < N) {
           const size_t gi = static_cast<size_t>(t_lo + row) * N + col;
-          const int li = row * ENV_TILE + 4 * c4;
-          const float4 a = *reinterpret_cast<const float4*>(sr + li);
+          const int li = row * E + 4 * c4;
+          const float4 a = *reinterpret_cast<const float4*>(sa + li);
           const float4 v = *reinterpret_cast<const float4*>(sv + li);
           *reinterpret_cast<float4*>(adv + gi) = a;
-          *reinterpret_cast<float4*>(ret + gi) = make_float4(a.x + v.x, a.y + v.y, a.z + v.z, a.w + v.w);
+          *reinterpret_cast<float4*>(ret + gi) =
+              make_float4(a.x + v.x, a.y + v.y, a.z + v.z, a.w + v.w);
         }
       }
     } else {
-      for (int e = tid; e < rows * ENV_TILE; e += blockDim.x) {
-        const int row = e / ENV_TILE, c = e - row * ENV_TILE;
+      for (int e = tid; e < rows * E; e += 256) {
+        const int row = e / E, c = e - row * E;
         const int64_t col = n0 + c;
         if (col < N) {
           const size_t gi = static_cast<size_t>(t_lo + row) * N + col;
-          adv[gi] = sr[e];
-          ret[gi] = sr[e] + sv[e];
+          adv[gi] = sa[e];
+          ret[gi] = sa[e] + sv[e];
         }
       }
     }
@@ -122,7 +149,7 @@ __global__ __launch_bounds__(256) void gae_kernel(const float* __restrict__ rew,
 // the rows in registers, U rows of r/v/d loaded per batch before the U dependent steps run
 // (256 B per wave instruction: consecutive lanes = consecutive envs of a time row), advantages
 // and returns stored per batch. No LDS and no barriers, so every wave streams independently and
-// the occupancy (16 waves per CU at N = 262144) hides the latency; same arithmetic as gae_kernel,
+// the occupancy (16 waves per CU at N = 262144) hides the latency; same arithmetic as gae_tile_kernel,
 // op by op. T=128, N=262144 on MI355X: U = 1/2/4/8/16/32 -> 121/120/123/128/133/146 us, the LDS
 // form 143 us (tools/kernel_bench.py gae scaled).
 template <int U>
@@ -196,12 +223,16 @@ extern "C" int ocppo_gae(ocppo_stream_t stream, const float* rewards, const floa
                        values, dones, next_value, next_done, (int)T, N, g, gl, advantages,
                        returns);
   } else {
-    constexpr int TILE = 64;
-    const int TC = 64;
-    const size_t lds = 3 * sizeof(float) * TC * TILE;
-    hipLaunchKernelGGL(gae_kernel<TILE>, dim3(ceil_div(N, TILE)), dim3(256), lds, s, rewards,
-                       values, dones, next_value, next_done, (int)T, N, TC, g, gl, advantages,
-                       returns);
+    // >= 64 workgroups where N allows it: E = 4 envs per workgroup up to N = 256, then wider
+    const int TC = T < 128 ? (int)T : 128;
+#define OCPPO_GAE_TILE(E)                                                                          \
+  hipLaunchKernelGGL(gae_tile_kernel<E>, dim3(ceil_div(N, E)), dim3(256),                         \
+                     4 * sizeof(float) * TC * (E), s, rewards, values, dones, next_value,          \
+                     next_done, (int)T, N, TC, g, gl, advantages, returns)
+    if (N <= 256) OCPPO_GAE_TILE(4);
+    else if (N <= 1024) OCPPO_GAE_TILE(16);
+    else OCPPO_GAE_TILE(64);
+#undef OCPPO_GAE_TILE
   }
   return check_launch("ocppo_gae");
 }

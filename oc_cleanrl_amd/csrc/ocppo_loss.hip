@@ -152,58 +152,46 @@ __global__ __launch_bounds__(kStatsThreads) void adv_stats_kernel(const float* _
   }
 }
 
-// Minibatch prepare: adv_stats_kernel<VPT> plus the per-sample records of every minibatch gathered
-// into minibatch order (SoA), so that each loss launch reads contiguous arrays (no index, no
-// scattered 4-8 B loads). One workgroup per minibatch; all gathers of a thread are in flight
-// together.
+// Minibatch prepare, part 1: the per-sample records of every minibatch gathered into minibatch
+// order (SoA), so that each loss launch reads contiguous arrays (no index, no scattered 4-8 B
+// loads). The permutation of all minibatches is one flat index space, so this is a plain
+// elementwise gather over num_mb * M elements on a grid that fills the chip (VPT elements per
+// thread, all index loads, then all gathers, then all stores in flight). Part 2 is
+// adv_stats_kernel over the gathered (now contiguous) advantages, one workgroup per minibatch.
 template <int VPT>
-__global__ __launch_bounds__(kStatsThreads) void minibatch_prepare_kernel(
-    const int64_t* __restrict__ perm, int64_t M, const int64_t* __restrict__ b_act,
+__global__ __launch_bounds__(256) void minibatch_gather_kernel(
+    const int64_t* __restrict__ perm, int64_t n, const int64_t* __restrict__ b_act,
     const float* __restrict__ b_lp, const float* __restrict__ b_adv, const float* __restrict__ b_ret,
     const float* __restrict__ b_val, int64_t* __restrict__ mb_act, float* __restrict__ mb_lp,
-    float* __restrict__ mb_adv, float* __restrict__ mb_ret, float* __restrict__ mb_val,
-    float* __restrict__ stats) {
-  __shared__ float scratch[kStatsThreads / kWave];
-  const int64_t base = static_cast<int64_t>(blockIdx.x) * M;
+    float* __restrict__ mb_adv, float* __restrict__ mb_ret, float* __restrict__ mb_val) {
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * 256 * VPT + threadIdx.x;
   int64_t idx[VPT];
-  float x[VPT];
 #pragma unroll
   for (int k = 0; k < VPT; ++k) {
-    const int64_t i = threadIdx.x + static_cast<int64_t>(k) * kStatsThreads;
-    idx[k] = i < M ? perm[base + i] : -1;
+    const int64_t i = base + k * 256;
+    idx[k] = i < n ? perm[i] : -1;
+  }
+  int64_t a[VPT];
+  float lp[VPT], ad[VPT], rt[VPT], vl[VPT];
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int64_t b = idx[k] >= 0 ? idx[k] : 0;
+    a[k] = b_act[b];
+    lp[k] = b_lp[b];
+    ad[k] = b_adv[b];
+    rt[k] = b_ret[b];
+    vl[k] = b_val[b];
   }
 #pragma unroll
   for (int k = 0; k < VPT; ++k) {
-    const int64_t i = base + threadIdx.x + static_cast<int64_t>(k) * kStatsThreads;
+    const int64_t i = base + k * 256;
     if (idx[k] >= 0) {
-      const int64_t b = idx[k];
-      x[k] = b_adv[b];
-      mb_act[i] = b_act[b];
-      mb_lp[i] = b_lp[b];
-      mb_ret[i] = b_ret[b];
-      mb_val[i] = b_val[b];
-      mb_adv[i] = x[k];
-    } else {
-      x[k] = 0.f;
+      mb_act[i] = a[k];
+      mb_lp[i] = lp[k];
+      mb_adv[i] = ad[k];
+      mb_ret[i] = rt[k];
+      mb_val[i] = vl[k];
     }
-  }
-  if (!stats) return;
-  float s = 0.f;
-#pragma unroll
-  for (int k = 0; k < VPT; ++k) s += x[k];
-  s = block_sum(s, scratch);
-  const float mean = s / static_cast<float>(M);
-  float q = 0.f;
-#pragma unroll
-  for (int k = 0; k < VPT; ++k)
-    if (idx[k] >= 0) {
-      const float d = x[k] - mean;
-      q += d * d;
-    }
-  q = block_sum(q, scratch);
-  if (threadIdx.x == 0) {
-    stats[2 * blockIdx.x + 0] = mean;
-    stats[2 * blockIdx.x + 1] = sqrtf(q / static_cast<float>(M - 1));
   }
 }
 
@@ -1130,27 +1118,25 @@ extern "C" int ocppo_minibatch_prepare(ocppo_stream_t stream, const int64_t* per
                                        int64_t* mb_actions, float* mb_logprobs,
                                        float* mb_advantages, float* mb_returns, float* mb_values,
                                        float* adv_stats) {
-  OCPPO_REQUIRE(M > 0 && num_mb > 0 && num_mb <= INT32_MAX && M <= 16 * kStatsThreads,
-                "ocppo_minibatch_prepare: bad sizes M=%lld num_mb=%lld (M <= %d)", (long long)M,
-                (long long)num_mb, 16 * kStatsThreads);
+  OCPPO_REQUIRE(M > 0 && num_mb > 0 && num_mb <= INT32_MAX && M <= INT64_MAX / num_mb,
+                "ocppo_minibatch_prepare: bad sizes M=%lld num_mb=%lld", (long long)M,
+                (long long)num_mb);
   OCPPO_REQUIRE(perm && b_actions && b_logprobs && b_advantages && b_returns && b_values &&
                     mb_actions && mb_logprobs && mb_advantages && mb_returns && mb_values,
                 "ocppo_minibatch_prepare: null pointer");
   clear_stale_error();
   hipStream_t s = as_stream(stream);
-  const dim3 grid(static_cast<unsigned>(num_mb)), block(kStatsThreads);
-#define OCPPO_PREP(V)                                                                            \
-  hipLaunchKernelGGL(minibatch_prepare_kernel<V>, grid, block, 0, s, perm, M, b_actions,         \
-                     b_logprobs, b_advantages, b_returns, b_values, mb_actions, mb_logprobs,     \
-                     mb_advantages, mb_returns, mb_values, adv_stats)
-  if (M <= kStatsThreads)
-    OCPPO_PREP(1);
-  else if (M <= 4 * kStatsThreads)
-    OCPPO_PREP(4);
-  else
-    OCPPO_PREP(16);
-#undef OCPPO_PREP
-  return check_launch("ocppo_minibatch_prepare");
+  constexpr int VPT = 2;
+  const int64_t n = M * num_mb;
+  hipLaunchKernelGGL(minibatch_gather_kernel<VPT>, dim3(static_cast<unsigned>(ceil_div(n, 256 * VPT))),
+                     dim3(256), 0, s, perm, n, b_actions, b_logprobs, b_advantages, b_returns,
+                     b_values, mb_actions, mb_logprobs, mb_advantages, mb_returns, mb_values);
+  if (int rc = check_launch("ocppo_minibatch_prepare")) return rc;
+  if (!adv_stats) return OCPPO_OK;
+  // mean / unbiased std of each minibatch's (contiguous) advantages: the reduction order of
+  // ocppo_minibatch_adv_stats over the same values, so the figures are identical
+  launch_adv_stats(s, mb_advantages, nullptr, M, num_mb, adv_stats);
+  return check_launch("ocppo_minibatch_prepare/stats");
 }
 
 namespace ocppo {
@@ -1253,188 +1239,331 @@ __device__ __forceinline__ void hl_dots(const float (&x)[CPL], const float (&w)[
   for (int j = 0; j < 8; ++j) out[j] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t), 8 * j));
 }
 
-// Two rows per wave step: the rows' dependent chains (dots, loss, backward) are independent, so
-// the compiler interleaves them.
-template <int AMAX, bool EXACT, int CPL>
+// ---- heads_loss rows kernel -----------------------------------------------------------------------
+// A wave walks its rows U at a time. Lane layout of a row: CPL = H / 64 columns per lane
+// (hl_col). Per step:
+//   1. the U rows' h chunks were loaded one step ahead (ping-pong register sets); lane u < U also
+//      loads row u's records (action, old log-prob, advantage, return, old value);
+//   2. per lane the U x NK partial dot products (NK = AMAX actor logits + the value), then ONE
+//      reduce-scatter over the wave for all of them (xor 32 .. 2: each lane keeps half of its
+//      values and adds its partner's other half), so value (u, k) ends in lanes 2(8u + k) and
+//      2(8u + k) + 1 (U = 4) or lane 8u + k (U = 8);
+//   3. lane u gathers row u's NK sums and runs the fused loss for row u: the loss arithmetic runs
+//      once per U rows, not once per row in every lane;
+//   4. each row's NK gradients c are broadcast (readlane) and the heads' backward runs per row:
+//      gp = (h > 0) * sum_k c_k W_k (written once), db_h += gp, dW_k += c_k h (registers).
+// Lanes accumulate c (head db) and the loss partials for their own rows; the workgroup adds its
+// waves through LDS in wave order and writes ONE record.
+template <int CPL, int U>
+struct HlRows {
+  float x[U][CPL];
+  int64_t a;                    // lane u < U: row u's record
+  float old_lp, adv, R, v_old;
+};
+
+template <int CPL, int U>
+__device__ __forceinline__ void hl_rows_load(const HeadsLossParams& P, int64_t rb, int64_t r1,
+                                             int lane, HlRows<CPL, U>& s) {
+  const LossParams& L = P.L;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t r = rb + u < r1 ? rb + u : rb;
+    hl_load<CPL>(P.h + r * P.H, lane, s.x[u]);
+  }
+  const int64_t rl = rb + (lane & (U - 1)) < r1 ? rb + (lane & (U - 1)) : rb;
+  s.a = L.b_actions[rl];
+  s.old_lp = L.b_logprobs[rl];
+  s.adv = L.b_adv[rl];
+  s.R = L.b_ret[rl];
+  s.v_old = L.b_val[rl];
+}
+
+template <int CPL, int NK>
+struct HlAcc {
+  float sb[CPL], sw[NK][CPL];
+  float sc[NK], part[kNumPartials];  // per lane: the rows this lane ran the loss for
+};
+
+// One reduce-scatter step over N values: partner lane = lane ^ M; the lane with bit M set keeps
+// the upper half of its values and receives the partner's upper half (the other lane the lower
+// halves), so the N / 2 values left are sums over both lanes.
+template <int N, int M>
+__device__ __forceinline__ void hl_rs_step(float* v, int lane) {
+  const bool hi = lane & M;
+#pragma unroll
+  for (int i = 0; i < N / 2; ++i) {
+    const float send = hi ? v[i] : v[i + N / 2];
+    const float keep = hi ? v[i + N / 2] : v[i];
+    v[i] = keep + __shfl_xor(send, M);
+  }
+}
+
+// Reduce-scatter of the 8U values over the wave (masks 32, 16, ... halving the values each step);
+// returns the wave sum of value lane >> 1 (U = 4, after a last xor-1 add) or of value lane (U = 8).
+template <int U>
+__device__ __forceinline__ float hl_reduce_scatter(float (&v)[8 * U], int lane) {
+  if constexpr (U == 8) {
+    hl_rs_step<64, 32>(v, lane);
+    hl_rs_step<32, 16>(v, lane);
+    hl_rs_step<16, 8>(v, lane);
+    hl_rs_step<8, 4>(v, lane);
+    hl_rs_step<4, 2>(v, lane);
+    hl_rs_step<2, 1>(v, lane);
+    return v[0];
+  } else {
+    hl_rs_step<32, 32>(v, lane);
+    hl_rs_step<16, 16>(v, lane);
+    hl_rs_step<8, 8>(v, lane);
+    hl_rs_step<4, 4>(v, lane);
+    hl_rs_step<2, 2>(v, lane);
+    return v[0] + __shfl_xor(v[0], 1);
+  }
+}
+
+template <int AMAX, bool EXACT, int CPL, int U>
+__device__ __forceinline__ void hl_rows_compute(const HeadsLossParams& P, int A,
+                                                const float (&w)[AMAX + 1][CPL],
+                                                const float (&bk)[AMAX + 1], float adv_mean,
+                                                float adv_den, int64_t rb, int64_t r1, int lane,
+                                                const HlRows<CPL, U>& s,
+                                                HlAcc<CPL, AMAX + 1>& acc) {
+  constexpr int NK = AMAX + 1;
+  const LossParams& L = P.L;
+  // 2. partial dots, slot (u, k) at u * 8 + k (k = NK..7 padding)
+  float v[8 * U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float d = 0.f;
+      if (k < NK) {
+#pragma unroll
+        for (int q = 0; q < CPL; ++q) d = fmaf(s.x[u][q], w[k][q], d);
+      }
+      v[u * 8 + k] = d;
+    }
+  }
+  const float red = hl_reduce_scatter<U>(v, lane);
+  // 3. the loss of row `lane` (lanes < U)
+  const int lu = lane & (U - 1);
+  float l[AMAX], vnew = 0.f;
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    const int src = U == 4 ? 2 * (8 * lu + k) : 8 * lu + k;
+    const float t = __shfl(red, src);
+    if (k < AMAX) l[k] = t + bk[k];
+    else vnew = t + bk[k];
+  }
+  float dl[AMAX], dv;
+  float pr[kNumPartials] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  loss_element<AMAX>(L, A, l, s.a, s.old_lp, s.adv, s.R, s.v_old, vnew, adv_mean, adv_den, pr,
+                     dl, dv);
+  const bool mine = lane < U && rb + lane < r1;
+  float cl[NK];
+#pragma unroll
+  for (int k = 0; k < NK; ++k) cl[k] = mine ? (k < AMAX ? (k < A ? dl[k] : 0.f) : dv) : 0.f;
+#pragma unroll
+  for (int k = 0; k < NK; ++k) acc.sc[k] += cl[k];
+#pragma unroll
+  for (int q = 0; q < kNumPartials; ++q) acc.part[q] += mine ? pr[q] : 0.f;
+  if (L.dlogits != nullptr && mine) {
+    const int64_t r = rb + lane;
+#pragma unroll
+    for (int k = 0; k < AMAX; ++k)
+      if (k < A) L.dlogits[r * A + k] = dl[k];
+    L.dvalue[r] = dv;
+  }
+  // 4. the heads' backward per row
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (rb + u >= r1) break;  // wave-uniform
+    float c[NK];
+#pragma unroll
+    for (int k = 0; k < NK; ++k)
+      c[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cl[k]), u));
+    float g[CPL];
+#pragma unroll
+    for (int q = 0; q < CPL; ++q) {
+      float d = 0.f;
+#pragma unroll
+      for (int k = 0; k < NK; ++k) d = fmaf(c[k], w[k][q], d);
+      g[q] = s.x[u][q] <= 0.f ? 0.f : d;
+      acc.sb[q] += g[q];
+#pragma unroll
+      for (int k = 0; k < NK; ++k) acc.sw[k][q] = fmaf(c[k], s.x[u][q], acc.sw[k][q]);
+    }
+    hl_store<CPL>(P.gp + (rb + u) * P.H, lane, g);
+  }
+}
+
+// Fixed grid (hl_layout): workgroup g owns rows [g * rows_per_wg, ...) and walks them in steps
+// of U rows per wave (4 waves: 4U rows per step), the next step's loads issued before this step's
+// arithmetic (two register sets, ping-pong). The workgroup's sums leave as ONE record
+// [64 lanes][CPL][NV] (NV = AMAX + 2 slots: db_h, AMAX actor dW rows, critic dW), NK head-bias
+// sums, the 6 loss partials at npw - 6: record traffic is O(grid), not O(M).
+template <int AMAX, bool EXACT, int CPL, int U>
 __global__ __launch_bounds__(256) void heads_loss_kernel(HeadsLossParams P) {
-  static_assert(AMAX <= 7, "A logits + the value in 8 lanes-groups");
-  constexpr int NV = 9;  // per column: db_h, then dW rows 0..7 (j < A: actor, 7: critic)
+  static_assert(AMAX <= 7, "A logits + the value in 8 slots");
+  static_assert(U == 4 || U == 8, "reduce-scatter layouts");
+  constexpr int NK = AMAX + 1, NV = AMAX + 2;
   extern __shared__ __attribute__((aligned(16))) float hl_red[];  // [4][64][CPL * NV]
   __shared__ float s_misc[4][8 + kNumPartials];
   const LossParams& L = P.L;
   const int A = EXACT ? AMAX : L.A;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t H = P.H;
-  float w[8][CPL], bk[8];
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * P.rows_per_wg;
+  const int64_t r1 = r0 + P.rows_per_wg < L.M ? r0 + P.rows_per_wg : L.M;
+  int64_t rb = r0 + wv * U;
+  HlRows<CPL, U> sa, sbuf;
+  if (rb < r1) hl_rows_load<CPL, U>(P, rb, r1, lane, sa);
+  float w[NK][CPL], bk[NK];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    bk[j] = j < A ? P.ba[j] : (j == 7 ? P.bc[0] : 0.f);
-    const float* wr = j == 7 ? P.wc : P.wa + static_cast<int64_t>(j < A ? j : 0) * H;
+  for (int k = 0; k < NK; ++k) {
+    const bool critic = k == AMAX;
+    bk[k] = critic ? P.bc[0] : (k < A ? P.ba[k] : 0.f);
+    const float* wr = critic ? P.wc : P.wa + static_cast<int64_t>(k < A ? k : 0) * H;
     float t[CPL];
     hl_load<CPL>(wr, lane, t);
 #pragma unroll
-    for (int q = 0; q < CPL; ++q) w[j][q] = (j < A || j == 7) ? t[q] : 0.f;
+    for (int q = 0; q < CPL; ++q) w[k][q] = (critic || k < A) ? t[q] : 0.f;
   }
-  float sb[CPL], sw[8][CPL], sc[8], part[kNumPartials];
+  HlAcc<CPL, NK> acc;
 #pragma unroll
-  for (int q = 0; q < CPL; ++q) sb[q] = 0.f;
+  for (int q = 0; q < CPL; ++q) acc.sb[q] = 0.f;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    sc[j] = 0.f;
+  for (int k = 0; k < NK; ++k) {
+    acc.sc[k] = 0.f;
 #pragma unroll
-    for (int q = 0; q < CPL; ++q) sw[j][q] = 0.f;
+    for (int q = 0; q < CPL; ++q) acc.sw[k][q] = 0.f;
   }
 #pragma unroll
-  for (int q = 0; q < kNumPartials; ++q) part[q] = 0.f;
+  for (int q = 0; q < kNumPartials; ++q) acc.part[q] = 0.f;
   const float adv_mean = L.norm_adv ? L.adv_stats[0] : 0.f;
   const float adv_den = L.norm_adv ? L.adv_stats[1] + 1e-8f : 1.f;
-  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * P.rows_per_wg;
-  const int64_t r1 = r0 + P.rows_per_wg < L.M ? r0 + P.rows_per_wg : L.M;
-
-  for (int64_t rb = r0 + wv; rb < r1; rb += 8) {
-    float x[2][CPL], t[2][8];
-    bool ok[2];
-    int64_t a[2];
-    float old_lp[2], adv[2], R[2], v_old[2];
+  constexpr int kStep = 4 * U;
+  while (rb < r1) {
+    if (rb + kStep < r1) hl_rows_load<CPL, U>(P, rb + kStep, r1, lane, sbuf);
+    hl_rows_compute<AMAX, EXACT, CPL, U>(P, A, w, bk, adv_mean, adv_den, rb, r1, lane, sa, acc);
+    rb += kStep;
+    if (rb >= r1) break;
+    if (rb + kStep < r1) hl_rows_load<CPL, U>(P, rb + kStep, r1, lane, sa);
+    hl_rows_compute<AMAX, EXACT, CPL, U>(P, A, w, bk, adv_mean, adv_den, rb, r1, lane, sbuf,
+                                         acc);
+    rb += kStep;
+  }
+  // the lanes' head-bias and loss sums (lanes < U hold them): wave sum in lane order
+  float misc[NK + kNumPartials];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int64_t r = rb + 4 * u;
-      ok[u] = r < r1;
-      const int64_t rr = ok[u] ? r : rb;
-      hl_load<CPL>(P.h + rr * H, lane, x[u]);
-      a[u] = L.b_actions[rr];
-      old_lp[u] = L.b_logprobs[rr];
-      adv[u] = L.b_adv[rr];
-      R[u] = L.b_ret[rr];
-      v_old[u] = L.b_val[rr];
-    }
+  for (int k = 0; k < NK; ++k) misc[k] = acc.sc[k];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) hl_dots<CPL>(x[u], w, lane, t[u]);
+  for (int q = 0; q < kNumPartials; ++q) misc[NK + q] = acc.part[q];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int64_t r = rb + 4 * u;
-      float l[AMAX];
+  for (int i = 0; i < NK + kNumPartials; ++i) {
+    float t = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(misc[i]), 0));
 #pragma unroll
-      for (int k = 0; k < AMAX; ++k) l[k] = t[u][k] + bk[k];
-      const float vnew = t[u][7] + bk[7];
-      float dl[AMAX], dv;
-      float pr[kNumPartials] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      loss_element<AMAX>(L, A, l, a[u], old_lp[u], adv[u], R[u], v_old[u], vnew, adv_mean,
-                         adv_den, pr, dl, dv);
-      if (!ok[u]) continue;  // wave-uniform
-#pragma unroll
-      for (int q = 0; q < kNumPartials; ++q) part[q] += pr[q];
-      if (L.dlogits != nullptr && lane == 0) {
-#pragma unroll
-        for (int k = 0; k < AMAX; ++k)
-          if (k < A) L.dlogits[r * A + k] = dl[k];
-        L.dvalue[r] = dv;
-      }
-      float cv[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) cv[k] = k < A ? dl[k < AMAX ? k : 0] : (k == 7 ? dv : 0.f);
-      float g[CPL];
-#pragma unroll
-      for (int q = 0; q < CPL; ++q) {
-        float d = 0.f;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) d = fmaf(cv[k], w[k][q], d);
-        g[q] = x[u][q] <= 0.f ? 0.f : d;
-        sb[q] += g[q];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) sw[k][q] = fmaf(cv[k], x[u][q], sw[k][q]);
-      }
-#pragma unroll
-      for (int k = 0; k < 8; ++k) sc[k] += cv[k];
-      hl_store<CPL>(P.gp + r * H, lane, g);
-    }
+    for (int u = 1; u < U; ++u)
+      t += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(misc[i]), u));
+    misc[i] = t;
   }
   // workgroup combine: per lane CPL x NV values through LDS, waves in order
   float* mine = hl_red + (static_cast<int64_t>(wv) * 64 + lane) * CPL * NV;
 #pragma unroll
   for (int q = 0; q < CPL; ++q) {
-    mine[q * NV] = sb[q];
+    mine[q * NV] = acc.sb[q];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) mine[q * NV + 1 + k] = sw[k][q];
+    for (int k = 0; k < NK; ++k) mine[q * NV + 1 + k] = acc.sw[k][q];
   }
   if (lane == 0) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) s_misc[wv][k] = sc[k];
+    for (int k = 0; k < NK; ++k) s_misc[wv][k] = misc[k];
 #pragma unroll
-    for (int q = 0; q < kNumPartials; ++q) s_misc[wv][8 + q] = part[q];
+    for (int q = 0; q < kNumPartials; ++q) s_misc[wv][8 + q] = misc[NK + q];
   }
   __syncthreads();
-  // record layout = the wave's LDS layout [lane][q][slot] (64 * CPL * 9 values: slot 0 db_h,
-  // 1..7 actor rows, 8 critic), then 8 head-bias sums (7 = critic), then the 6 loss partials at
-  // npw - 6: the waves are added in order with contiguous LDS reads and coalesced stores
   float* out = P.partials + static_cast<int64_t>(blockIdx.x) * P.npw;
   constexpr int nvals = 64 * CPL * NV;
-  constexpr int wstride = 64 * CPL * NV;
   for (int i = threadIdx.x; i < nvals; i += 256) {
     float sacc = hl_red[i];
 #pragma unroll
-    for (int wq = 1; wq < 4; ++wq) sacc += hl_red[wq * wstride + i];
+    for (int wq = 1; wq < 4; ++wq) sacc += hl_red[wq * nvals + i];
     out[i] = sacc;
   }
-  if (threadIdx.x < 8 + kNumPartials) {
+  if (threadIdx.x < NK) {
     const int i = threadIdx.x;
     float sacc = s_misc[0][i];
     for (int wq = 1; wq < 4; ++wq) sacc += s_misc[wq][i];
-    out[i < 8 ? nvals + i : P.npw - kNumPartials + (i - 8)] = sacc;
+    out[nvals + i] = sacc;
+  } else if (threadIdx.x >= 64 && threadIdx.x < 64 + kNumPartials) {
+    const int i = threadIdx.x - 64;
+    float sacc = s_misc[0][8 + i];
+    for (int wq = 1; wq < 4; ++wq) sacc += s_misc[wq][8 + i];
+    out[P.npw - kNumPartials + i] = sacc;
   }
 }
 
-// Adds the workgroups' partial records in workgroup order: 16 outputs x 16 workgroup groups per
-// block (each thread sums its group's records in order, then the 16 group sums in group order).
-// The record ends with the 6 loss partials at `ls` (a multiple of 16), so one block holds all of
-// them and forms the loss statistics (loss_finish's formulas).
+// Adds the G workgroup records with a fixed-shape tree: a block owns 16 record entries (outputs)
+// x 16 record groups; group gi takes records gi, gi + 16, gi + 32, ... in batches of 16 loads in
+// flight, each batch summed pairwise (8 / 4 / 2 / 1), batch sums added in batch order, then the
+// 16 group sums pairwise through LDS. The same shape for every G: deterministic. The record ends
+// with the 6 loss partials at `ls` (a multiple of 16), so one block holds all of them and forms
+// the loss statistics (loss_finish's formulas).
+constexpr int kHlFinOut = 16, kHlFinGroups = 16, kHlFinBatch = 16;
 __global__ __launch_bounds__(256) void heads_loss_finish_kernel(
-    const float* __restrict__ partials, int G, int64_t npw, int64_t ls, int64_t H, int A, int cpl,
-    float* __restrict__ db_h, float* __restrict__ dwa, float* __restrict__ dwc,
+    const float* __restrict__ partials, int G, int64_t npw, int64_t ls, int64_t H, int A, int amax,
+    int cpl, float* __restrict__ db_h, float* __restrict__ dwa, float* __restrict__ dwc,
     float* __restrict__ dba, float* __restrict__ dbc, LossParams L) {
-  __shared__ float red[16][17];
-  __shared__ float tot[16];
-  const int o = threadIdx.x & 15, gi = threadIdx.x >> 4;
-  const int64_t idx = static_cast<int64_t>(blockIdx.x) * 16 + o;
-  const int cpg = (G + 15) / 16;
-  const int g0 = gi * cpg, g1 = g0 + cpg < G ? g0 + cpg : G;
+  __shared__ float red[kHlFinGroups][kHlFinOut + 1];
+  __shared__ float tot[kHlFinOut];
+  const int o = threadIdx.x % kHlFinOut, gi = threadIdx.x / kHlFinOut;
+  const int64_t idx = static_cast<int64_t>(blockIdx.x) * kHlFinOut + o;
   float s = 0.f;
   if (idx < npw) {
-    for (int g = g0; g < g1; g += 8) {
-      float v[8];
+    for (int g0 = gi; g0 < G; g0 += kHlFinGroups * kHlFinBatch) {
+      float v[kHlFinBatch];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = g + u < g1 ? partials[(g + u) * npw + idx] : 0.f;
+      for (int u = 0; u < kHlFinBatch; ++u) {
+        const int g = g0 + u * kHlFinGroups;
+        v[u] = g < G ? partials[static_cast<int64_t>(g) * npw + idx] : 0.f;
+      }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) s += v[u];
+      for (int wdt = kHlFinBatch / 2; wdt >= 1; wdt /= 2)
+#pragma unroll
+        for (int u = 0; u < wdt; ++u) v[u] += v[u + wdt];
+      s += v[0];
     }
   }
   red[gi][o] = s;
   __syncthreads();
-  const int64_t nvals = 64 * cpl * 9;
+  for (int wdt = kHlFinGroups / 2; wdt >= 1; wdt /= 2) {
+    if (gi < wdt) red[gi][o] += red[gi + wdt][o];
+    __syncthreads();
+  }
+  const int nv = amax + 2;
+  const int64_t nvals = 64 * cpl * nv;
   if (gi == 0) {
-    float t = red[0][o];
-    for (int q = 1; q < 16; ++q) t += red[q][o];
+    const float t = red[0][o];
     tot[o] = t;
     if (idx < nvals) {  // [lane][q][slot] -> column of hl_col
-      const int slot = static_cast<int>(idx % 9);
-      const int lq = static_cast<int>(idx / 9);
+      const int slot = static_cast<int>(idx % nv);
+      const int lq = static_cast<int>(idx / nv);
       const int ln = lq / cpl, q = lq - ln * cpl;
       const int64_t col = cpl >= 4 ? 4 * ((q >> 2) * kWave + ln) + (q & 3) : q * kWave + ln;
       if (slot == 0) {
         if (db_h) db_h[col] = t;
-      } else if (slot == 8) {
+      } else if (slot == nv - 1) {
         dwc[col] = t;
       } else if (slot - 1 < A) {
         dwa[static_cast<int64_t>(slot - 1) * H + col] = t;
       }
-    } else if (idx < nvals + 8) {
+    } else if (idx < nvals + amax + 1) {
       const int k = static_cast<int>(idx - nvals);
       if (k < A) dba[k] = t;
-      else if (k == 7) dbc[0] = t;
+      else if (k == amax) dbc[0] = t;
     }
   }
   __syncthreads();
-  if (static_cast<int64_t>(blockIdx.x) * 16 == ls && threadIdx.x == 0) {
+  if (static_cast<int64_t>(blockIdx.x) * kHlFinOut == ls && threadIdx.x == 0) {
     const float pg_loss = tot[0] * L.inv_m;
     const float v_loss = 0.5f * (tot[1] * L.inv_m);
     const float ent = tot[2] * L.inv_m;
@@ -1451,33 +1580,53 @@ __global__ __launch_bounds__(256) void heads_loss_finish_kernel(
   }
 }
 
-// rows per workgroup (4 waves): OCPPO_HL_ROWS overrides it for experiments (tools/)
-inline int hl_rows_per_wg() {
-  static const int r = [] {
-    const char* e = getenv("OCPPO_HL_ROWS");
-    const int v = e ? atoi(e) : 16;
-    return v >= 4 && v <= 256 ? v : 16;
-  }();
-  return r;
+// Grid of the rows launch: G = min(ceil(M / rows_min), grid_cap) workgroups of rows_per_wg rows
+// (a multiple of the 16-row step of 4 waves x U = 4 rows). rows_min = 16 keeps a config-size
+// minibatch (4096 rows) on 256 workgroups, one per CU, every wave's 4 rows loaded at once;
+// grid_cap = 256 (one per CU: ~300 VGPRs, one wave per SIMD, 64 KB of h in flight per CU with the
+// ping-pong) bounds the records at streaming sizes.
+// OCPPO_HL_ROWS / OCPPO_HL_GRID override them for experiments (tools/).
+inline int hl_env(const char* name, int dflt, int lo, int hi) {
+  const char* e = getenv(name);
+  const int v = e ? atoi(e) : dflt;
+  return v >= lo && v <= hi ? v : dflt;
 }
 
-inline int64_t hl_layout(int64_t M, int64_t H, int64_t A, int64_t& G, int64_t& ls) {
-  (void)A;
-  const int rows = hl_rows_per_wg();
-  G = (M + rows - 1) / rows;
-  ls = (H * 9 + 8 + 15) / 16 * 16;  // 64 lanes x (H / 64) columns x 9 slots, 8 bias sums
+// the action count the rows kernel is instantiated with: exact for 4 (Breakout) and 6 (Pong,
+// SpaceInvaders), else the 7-wide generic form
+inline int hl_amax(int64_t A) { return A == 4 || A == 6 ? static_cast<int>(A) : 7; }
+
+inline int64_t hl_layout(int64_t M, int64_t H, int64_t A, int64_t& G, int64_t& ls,
+                         int64_t* rows_per_wg = nullptr) {
+  static const int rows_min = hl_env("OCPPO_HL_ROWS", 16, 16, 65536);
+  static const int grid_cap = hl_env("OCPPO_HL_GRID", 256, 1, 65536);
+  G = (M + rows_min - 1) / rows_min;
+  if (G > grid_cap) G = grid_cap;
+  int64_t rpw = (M + G - 1) / G;
+  rpw = (rpw + 15) / 16 * 16;
+  G = (M + rpw - 1) / rpw;
+  if (rows_per_wg) *rows_per_wg = rpw;
+  const int64_t amax = hl_amax(A);
+  // 64 lanes x (H / 64) columns x (amax + 2) slots, amax + 1 head-bias sums
+  ls = (H * (amax + 2) + amax + 1 + 15) / 16 * 16;
   return ls + kNumPartials;  // npw
+}
+
+// the decoder widths the rows kernel is instantiated for: H / 64 columns per lane in {1, 2, 4, 8}
+inline bool hl_width_ok(int64_t H) {
+  return H == 64 || H == 128 || H == 256 || H == 512;
 }
 
 template <int AMAX, bool EXACT>
 static void launch_heads_loss(hipStream_t s, const HeadsLossParams& P, int G, int cpl) {
-  const size_t lds = sizeof(float) * 4 * 64 * cpl * 9;
+  const size_t lds = sizeof(float) * 4 * 64 * cpl * (AMAX + 2);
   const dim3 g(G), b(256);
   switch (cpl) {
-    case 1: hipLaunchKernelGGL((heads_loss_kernel<AMAX, EXACT, 1>), g, b, lds, s, P); break;
-    case 2: hipLaunchKernelGGL((heads_loss_kernel<AMAX, EXACT, 2>), g, b, lds, s, P); break;
-    case 4: hipLaunchKernelGGL((heads_loss_kernel<AMAX, EXACT, 4>), g, b, lds, s, P); break;
-    default: hipLaunchKernelGGL((heads_loss_kernel<AMAX, EXACT, 8>), g, b, lds, s, P); break;
+    case 1: hipLaunchKernelGGL((heads_loss_kernel<AMAX, EXACT, 1, 4>), g, b, lds, s, P); break;
+    case 2: hipLaunchKernelGGL((heads_loss_kernel<AMAX, EXACT, 2, 4>), g, b, lds, s, P); break;
+    case 4: hipLaunchKernelGGL((heads_loss_kernel<AMAX, EXACT, 4, 4>), g, b, lds, s, P); break;
+    case 8: hipLaunchKernelGGL((heads_loss_kernel<AMAX, EXACT, 8, 4>), g, b, lds, s, P); break;
+    default: break;  // rejected by hl_width_ok before the launch
   }
 }
 
@@ -1498,10 +1647,9 @@ extern "C" int ocppo_heads_loss_fwd_bwd(
     double ent_coef, double vf_coef, int norm_adv, int clip_vloss, float* gp, float* db_h,
     float* dwa, float* dwc, float* dba, float* dbc, float* stats, float* dlogits, float* dvalue,
     void* workspace, size_t workspace_bytes) {
-  OCPPO_REQUIRE(M >= 1 && M <= INT32_MAX && H >= 64 && H % 64 == 0 && H <= 512 && A >= 1 &&
-                    A <= 7,
-                "ocppo_heads_loss_fwd_bwd: bad sizes M=%lld H=%lld A=%lld (H %% 64 == 0, "
-                "64 <= H <= 512, 1 <= A <= 7)", (long long)M, (long long)H, (long long)A);
+  OCPPO_REQUIRE(M >= 1 && M <= INT32_MAX && hl_width_ok(H) && A >= 1 && A <= 7,
+                "ocppo_heads_loss_fwd_bwd: bad sizes M=%lld H=%lld A=%lld (H in {64, 128, 256, "
+                "512}, 1 <= A <= 7)", (long long)M, (long long)H, (long long)A);
   OCPPO_REQUIRE(h && w_actor && b_actor && w_critic && b_critic && mb_actions && mb_logprobs &&
                     mb_advantages && mb_returns && mb_values && gp && dwa && dwc && dba && dbc &&
                     stats && (!norm_adv || adv_stats) && (!dlogits == !dvalue),
@@ -1511,8 +1659,8 @@ extern "C" int ocppo_heads_loss_fwd_bwd(
   if (!workspace || workspace_bytes < ocppo_heads_loss_workspace_bytes(M, H, A))
     return fail(OCPPO_E_WORKSPACE, "ocppo_heads_loss_fwd_bwd: workspace needs %zu bytes, got %zu",
                 ocppo_heads_loss_workspace_bytes(M, H, A), workspace_bytes);
-  int64_t G, ls;
-  const int64_t npw = hl_layout(M, H, A, G, ls);
+  int64_t G, ls, rpw;
+  const int64_t npw = hl_layout(M, H, A, G, ls, &rpw);
   HeadsLossParams P;
   LossParams& L = P.L;
   L.logits = nullptr;
@@ -1553,7 +1701,7 @@ extern "C" int ocppo_heads_loss_fwd_bwd(
   P.gp = gp;
   P.partials = static_cast<float*>(workspace);
   P.npw = npw;
-  P.rows_per_wg = hl_rows_per_wg();
+  P.rows_per_wg = static_cast<int>(rpw);
   clear_stale_error();
   hipStream_t s = as_stream(stream);
   const int cpl = static_cast<int>(H / 64);
@@ -1563,8 +1711,8 @@ extern "C" int ocppo_heads_loss_fwd_bwd(
     default: launch_heads_loss<7, false>(s, P, (int)G, cpl); break;
   }
   if (int rc = check_launch("ocppo_heads_loss_fwd_bwd")) return rc;
-  hipLaunchKernelGGL(heads_loss_finish_kernel, dim3((npw + 15) / 16), dim3(256), 0, s,
-                     static_cast<const float*>(workspace), (int)G, npw, ls, H, (int)A, cpl, db_h,
-                     dwa, dwc, dba, dbc, L);
+  hipLaunchKernelGGL(heads_loss_finish_kernel, dim3((npw + kHlFinOut - 1) / kHlFinOut),
+                     dim3(256), 0, s, static_cast<const float*>(workspace), (int)G, npw, ls, H,
+                     (int)A, hl_amax(A), cpl, db_h, dwa, dwc, dba, dbc, L);
   return check_launch("ocppo_heads_loss_fwd_bwd/finish");
 }

@@ -204,10 +204,14 @@ def ppo_loss_fwd_bwd(logits, new_value, b_actions, b_logprobs, b_advantages, b_r
 _HL_WS: dict = {}
 
 
+# decoder widths ocppo_heads_loss_fwd_bwd is instantiated for (H / 64 columns per lane: 1, 2, 4, 8)
+HEADS_LOSS_WIDTHS = (64, 128, 256, 512)
+
+
 def heads_loss_ok(h, A: int) -> bool:
     H = h.shape[-1]
     return (h.is_cuda and h.dtype == torch.float32 and h.dim() == 2 and h.is_contiguous() and
-            H % 64 == 0 and 64 <= H <= 512 and 1 <= A <= 7 and h.data_ptr() % 16 == 0)
+            H in HEADS_LOSS_WIDTHS and 1 <= A <= 7 and h.data_ptr() % 16 == 0)
 
 
 def heads_loss_fwd_bwd(h, wa, ba, wc, bc, mb_actions, mb_logprobs, mb_advantages, mb_returns,

@@ -300,7 +300,7 @@ class PPOTrainer:
         # heads forward + loss + heads backward fused on the decoder output (needs the in-place
         # grads of FlatAdam and the decoder's ReLU box; see _fused_tail)
         self.fused_heads_loss = (a.fused_heads_loss and self.direct_grads and self.fused_head and
-                                 self.H % 64 == 0 and 64 <= self.H <= 512 and self.A <= 7)
+                                 self.H in ops.HEADS_LOSS_WIDTHS and self.A <= 7)
         self.gp_tail = (torch.empty((self.M, self.H), dtype=f32, device=dev)
                         if self.fused_heads_loss else None)
         self.b_obs = self.obs[:T].view((T * N,) + self.obs_shape)
@@ -484,11 +484,16 @@ class PPOTrainer:
         self.timer.bracket("gae", lambda: ops.gae(
             self.rewards, self.values[:T], self.dones[:T], self.values[T], self.dones[T],
             a.gamma, a.gae_lambda, self.advantages, self.returns))
-        # every minibatch's per-sample records in minibatch order + its adv (mean, std)
+        self._prepare_minibatches()
+
+    def _prepare_minibatches(self):
+        """Every minibatch's per-sample records in minibatch order + its adv (mean, std)
+        (:566-579: b_*[mb_inds] and the minibatch advantage statistics)."""
+        T = self.T
         self.timer.bracket("mb_prepare", lambda: ops.minibatch_prepare(
             self.perm_dev, self.M, self.actions.view(-1), self.logprobs.view(-1),
             self.advantages.view(-1), self.returns.view(-1), self.values[:T].reshape(-1),
-            out=self.mb, with_stats=a.norm_adv))
+            out=self.mb, with_stats=self.args.norm_adv))
 
     def _rollout(self):
         """Rollout (:500-530) + bootstrap + GAE (:533-547) + minibatch adv stats (:577-579)."""
@@ -647,6 +652,11 @@ class PPOTrainer:
         for e in range(self.E):
             self.np_rng.shuffle(self.b_inds)
             out[e * self.B:(e + 1) * self.B] = self.b_inds
+        self._stage(out)
+
+    def _stage(self, out: np.ndarray):
+        """Stage the epochs' permutations `out` (a view of perm_host) and, with frame dedup,
+        their frame plan: one async copy each into the staging buffers."""
         if self.frame_dedup:
             used, inv = self.planner.plan(out)
             cap = self.planner.cap
@@ -657,6 +667,20 @@ class PPOTrainer:
         self.perm_stage.copy_(self.perm_host, non_blocking=True)
         self.perm_event.record()
         self.staged = True
+
+    def load_permutation(self, perm) -> None:
+        """Use `perm` [E*B] (the epochs' shuffles) as the current iteration's minibatch order,
+        with its frame plan, in place of the np.random stream (tests: a reference fixture's
+        permutation through the trainer's own update path)."""
+        perm = np.asarray(perm, np.int64)
+        if perm.shape != (self.E * self.B,):
+            raise ValueError(f"perm must have {self.E * self.B} entries, got {perm.shape}")
+        self.perm_event.synchronize()
+        out = self.perm_host.numpy()
+        out[:] = perm
+        self.staged_rng_state = self.np_rng.get_state()
+        self._stage(out)
+        self._load_staged()
 
     def _rewind_shuffle(self, epochs: int):
         """target_kl stopped the update after `epochs` epochs: the reference drew only that many

@@ -313,6 +313,130 @@ def gen_update(B=512, M=256, F=6, A=6, seed=21, pixels=False, name="update_2mb",
     np.savez_compressed(OUT / f"{name}.npz", **out)
 
 
+def config2_weights(agent, seed):
+    """Seeded PPObj parameters from numpy's PCG64 stream (platform-independent, so the GPU test
+    re-creates them bit for bit without shipping 9 MB of weights; a CPU orthogonal_ init would
+    differ in the last bits between LAPACK builds): weight [out, in] ~ N(0, 1) * gain / sqrt(in)
+    with layer_init's gains (sqrt 2 network, 0.01 actor, 1 critic), bias ~ N(0, 1) * 0.05, in
+    state_dict order. The update block does not care how the weights were made."""
+    rng = np.random.default_rng(seed)
+    sd = {}
+    for k, v in agent.state_dict().items():
+        if k.endswith("weight"):
+            gain = 0.01 if k.startswith("actor") else 1.0 if k.startswith("critic") else 2 ** 0.5
+            w = rng.standard_normal(tuple(v.shape)) * (gain / np.sqrt(v.shape[1]))
+        else:
+            w = rng.standard_normal(tuple(v.shape)) * 0.05
+        sd[k] = torch.from_numpy(w.astype(np.float32))
+    return sd
+
+
+def gen_update_config2(T=128, N=128, F=12, A=6, W=4, seed=25, name="update_config2"):
+    """BASELINE config 2 at the network's real size: PPObj(encoder (256, 512, 1024, 512),
+    decoder (512,)) on a rollout-structured batch of T x N = 128 x 128 Pong-obj samples, and two
+    minibatch updates of 4096 through the reference's update block (ppo_atari_oc.py:566-610).
+
+    The rollout obeys the frame-stack rule the trainer's frame dedup relies on: obs [T+1, N, W, F]
+    with obs[t] = obs[t-1] shifted by env n's frame of step t, or W copies of it where
+    dones[t, n] (FrameStack's reset fill; obs[0] likewise where dones[0, n]). Features: x U{0..159},
+    y U{0..209}, w, h U{1..16} (integers: exact in bf16 storage). Actions and log-probs
+    are the reference agent's own samples, values its critic (+ noise), rewards sparse +-1, and
+    advantages / returns come from the reference's GAE block (:533-547) with bootstrap
+    V(obs[T]). Stored: inputs, the 2 x 4096 permutation, per-minibatch loss scalars and grad
+    norms, the parameters after each update (tensors above 64K elements as 4096 fixed samples)
+    and checksums of the seeded initial ones (config2_weights)."""
+    rng = np.random.default_rng(seed)
+    hi = np.array([160, 210, 17, 17] * (F // 4))
+    lo = np.array([0, 0, 1, 1] * (F // 4))
+
+    def frames(n):
+        return rng.integers(lo, hi, (n, F)).astype(np.float32)
+
+    dones = (rng.random((T + 1, N)) < 0.02).astype(np.float32)
+    obs = np.zeros((T + 1, N, W, F), np.float32)
+    obs[0] = rng.integers(lo, hi, (N, W, F))
+    obs[0][dones[0] != 0] = obs[0][dones[0] != 0][:, -1:, :]
+    for t in range(1, T + 1):
+        f = frames(N)
+        obs[t] = np.concatenate([obs[t - 1][:, 1:], f[:, None]], 1)
+        d = dones[t] != 0
+        obs[t][d] = f[d][:, None, :]
+    agent = PPObj(Envs((W, F), A), "cpu", (256, 512, 1024, 512), (512,))
+    sd0 = config2_weights(agent, seed)
+    agent.load_state_dict(sd0)
+    b_obs = torch.from_numpy(obs[:T].reshape(T * N, W, F))
+    torch.manual_seed(seed)
+    with torch.no_grad():
+        hid = agent.network(b_obs)
+        dist = torch.distributions.Categorical(logits=agent.actor(hid))
+        b_actions = dist.sample()
+        lp = dist.log_prob(b_actions)
+        val = agent.critic(hid).view(-1)
+        next_value = agent.critic(agent.network(torch.from_numpy(obs[T]))).view(-1)
+    u = rng.random((T, N))
+    rewards = np.where(u < 0.005, 1.0, np.where(u < 0.01, -1.0, 0.0)).astype(np.float32)
+    values = (val + torch.from_numpy((rng.standard_normal(T * N) * 0.3).astype(np.float32)))
+    values = values.view(T, N).contiguous()
+    nv = next_value.reshape(N)
+    ns = dict(torch=torch, agent=types.SimpleNamespace(get_value=lambda x: nv.reshape(1, N)),
+              args=types.SimpleNamespace(num_steps=T, gamma=0.99, gae_lambda=0.95),
+              device="cpu", next_obs=None, rewards=torch.from_numpy(rewards), values=values,
+              dones=torch.from_numpy(dones[:T]), next_done=torch.from_numpy(dones[T]))
+    exec(GAE_CODE, ns)
+    b_advantages = ns["advantages"].reshape(-1)
+    b_returns = ns["returns"].reshape(-1)
+    b_values = values.reshape(-1)
+    b_logprobs = lp + torch.from_numpy((rng.standard_normal(T * N) * 0.15).astype(np.float32))
+    B, M = T * N, T * N // 4
+    perm = rng.permutation(B)
+    args = types.SimpleNamespace(clip_coef=0.1, norm_adv=True, clip_vloss=True, ent_coef=0.01,
+                                 vf_coef=0.5, max_grad_norm=0.5, track=False, minibatch_size=M)
+    optimizer = optim.Adam(agent.parameters(), lr=2.5e-4, eps=1e-5)
+    sds = [{k: v.detach().clone().numpy() for k, v in agent.state_dict().items()}]
+    gns, stats, grads = [], [], []
+    for start in (0, M):
+        mb_inds = perm[start:start + M]
+        ns = dict(torch=torch, nn=nn, np=np, agent=agent, args=args, optimizer=optimizer,
+                  b_obs=b_obs, b_actions=b_actions, b_logprobs=b_logprobs,
+                  b_advantages=b_advantages, b_returns=b_returns, b_values=b_values,
+                  mb_inds=mb_inds, clipfracs=[], start=start)
+        exec(UPDATE_CODE, ns)
+        gns.append(float(ns["gn"]))
+        # the gradients the optimizer saw (after clip_grad_norm_): per-tensor norms + samples
+        grads.append({k: p.grad.detach().clone().numpy() for k, p in agent.named_parameters()})
+        mba = b_advantages[mb_inds]
+        stats.append([ns["loss"].item(), ns["pg_loss"].item(), ns["v_loss"].item(),
+                      ns["entropy_loss"].item(), ns["old_approx_kl"].item(),
+                      ns["approx_kl"].item(), ns["clipfracs"][-1], mba.mean().item(),
+                      mba.std().item()])
+        sds.append({k: v.detach().clone().numpy() for k, v in agent.state_dict().items()})
+    out = dict(obs=obs.astype(np.uint8), dones=dones, actions=b_actions.numpy().astype(np.int64),
+               logprobs=b_logprobs.numpy(), values=b_values.numpy(), rewards=rewards,
+               next_value=nv.numpy(), advantages=b_advantages.numpy(),
+               returns=b_returns.numpy(), perm=perm[:2 * M].astype(np.int64), M=M, seed=seed,
+               grad_norms=np.array(gns, np.float64), stats=np.array(stats, np.float32))
+    assert np.array_equal(out["obs"].astype(np.float32), obs)
+    pick_rng = np.random.default_rng(seed + 1)
+    for k, v in sds[0].items():
+        v64 = v.astype(np.float64)
+        out[f"sum0::{k}"] = np.array([v64.sum(), (v64 ** 2).sum()])
+    for i, sd in enumerate(sds[1:], 1):
+        for k, v in sd.items():
+            if v.size > (1 << 16):
+                if f"pick::{k}" not in out:
+                    out[f"pick::{k}"] = np.sort(pick_rng.choice(v.size, 4096, replace=False))
+                out[f"sd{i}::{k}"] = v.reshape(-1)[out[f"pick::{k}"]]
+            else:
+                out[f"sd{i}::{k}"] = v
+    for i, gd in enumerate(grads):
+        for k, v in gd.items():
+            out[f"gnorm{i}::{k}"] = np.array([np.linalg.norm(v.astype(np.float64)),
+                                             np.abs(v).max()])
+            out[f"grad{i}::{k}"] = (v.reshape(-1)[out[f"pick::{k}"]] if f"pick::{k}" in out
+                                   else v)
+    np.savez_compressed(OUT / f"{name}.npz", **out)
+
+
 def gen_update_cartpole(B=512, M=128, seed=23, name="update_cartpole"):
     """Config 1: two minibatch updates of cleanrl/ppo.py's own update block (:250-290, clip 0.2)
     on its own Agent class (:94-126, exec'd), the whole learner step of ppo.py on CartPole-shaped
@@ -466,6 +590,8 @@ def main():
     gen_init("ppobj_f12_a6", lambda e: PPObj(e, "cpu", (256, 512, 1024, 512), (512,)), (4, 12), 6,
              1, 160.0)
     gen_init("ppodefault_a4", lambda e: PPODefault(e, "cpu"), (4, 84, 84), 4, 1, 255.0)
+    # config 2 at the real network dims, rollout-structured (the bench's update chain)
+    gen_update_config2()
     print("fixtures written to", OUT)
 
 

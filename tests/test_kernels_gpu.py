@@ -643,6 +643,22 @@ def test_minibatch_prepare_then_loss_equals_indexed_loss(ops, dev):
         assert torch.equal(x, y)
 
 
+@pytest.mark.parametrize("M,nmb,B", [(1, 3, 5), (333, 7, 1000), (20000, 3, 30011)])
+def test_minibatch_prepare_shapes(ops, dev, M, nmb, B):
+    """The gather runs over all nmb * M elements on one grid (ragged tails) and the statistics
+    are ocppo_minibatch_adv_stats' over the same values (bitwise), for any M."""
+    rng = np.random.default_rng(M + nmb)
+    b_act = T(rng.integers(0, 6, B).astype(np.int64), dev)
+    b_lp, b_adv, b_ret, b_val = (T(rng.standard_normal(B).astype(np.float32), dev) for _ in range(4))
+    perm = T(rng.integers(0, B, nmb * M).astype(np.int64), dev)
+    mb = ops.minibatch_prepare(perm, M, b_act, b_lp, b_adv, b_ret, b_val)
+    for k, src in (("actions", b_act), ("logprobs", b_lp), ("advantages", b_adv),
+                   ("returns", b_ret), ("values", b_val)):
+        assert torch.equal(mb[k], src[perm]), k
+    if M > 1:
+        assert torch.equal(mb["adv_stats"], ops.minibatch_adv_stats(b_adv, perm, M))
+
+
 # ---------------------------------------------------------------------------------------------
 # DQN: fused TD loss, epsilon-greedy, HBM replay buffer
 # ---------------------------------------------------------------------------------------------
@@ -1288,7 +1304,8 @@ def test_rollout_trunk_nchw_flatten_matches_module(ops, dev):
 # ---------------------------------------------------------------------------------------------
 # policy heads forward + fused PPO loss + heads backward in one pass (ocppo_heads_loss_fwd_bwd)
 # ---------------------------------------------------------------------------------------------
-@pytest.mark.parametrize("M,H,A", [(4096, 512, 6), (1000, 256, 4), (77, 64, 7), (300, 128, 3)])
+@pytest.mark.parametrize("M,H,A", [(4096, 512, 6), (1000, 256, 4), (77, 64, 7), (300, 128, 3),
+                                   (20000, 512, 6), (70001, 128, 6)])
 @pytest.mark.parametrize("norm_adv,clip_vloss", [(True, True), (False, False)])
 def test_heads_loss_equals_heads_then_loss_then_heads_bwd(ops, dev, M, H, A, norm_adv, clip_vloss):
     g = torch.Generator(device=dev).manual_seed(M + H)
@@ -1329,3 +1346,28 @@ def test_heads_loss_equals_heads_then_loss_then_heads_bwd(ops, dev, M, H, A, nor
                                    db_h=torch.empty(H, device=dev), **cfg)
     for x, y in zip((gp, dbh, dwa, dwc, dba, dbc, stats), again):
         assert torch.equal(x, y)  # deterministic
+
+
+@pytest.mark.parametrize("H", [192, 320, 384, 448, 576])
+def test_heads_loss_rejects_uninstantiated_widths(ops, dev, H):
+    """Only H / 64 in {1, 2, 4, 8} has a rows kernel: other widths are refused by every gate
+    (the C entry point, ops.heads_loss_ok and the trainer's fused_heads_loss) instead of running
+    the 8-column instance past the end of each row."""
+    from oc_cleanrl_amd._lib import OcppoError
+
+    M, A = 64, 6
+    h = torch.relu(torch.randn(M, H, device=dev))
+    assert not ops.heads_loss_ok(h, A)
+    wa, ba = torch.zeros(A, H, device=dev), torch.zeros(A, device=dev)
+    wc, bc = torch.zeros(1, H, device=dev), torch.zeros(1, device=dev)
+    acts = torch.zeros(M, dtype=torch.int64, device=dev)
+    z = torch.zeros(M, device=dev)
+    with pytest.raises(OcppoError, match="bad sizes"):
+        ops.heads_loss_fwd_bwd(h, wa, ba, wc, bc, acts, z, z, z, z, adv_stats=None,
+                               clip_coef=0.1, ent_coef=0.01, vf_coef=0.5, norm_adv=False,
+                               clip_vloss=True)
+    from test_trainer_gpu import small_args
+    from oc_cleanrl_amd.trainer import PPOTrainer
+
+    tr = PPOTrainer(small_args(decoder_dims=(H,)), dev)
+    assert not tr.fused_heads_loss

@@ -235,3 +235,26 @@ def test_replay_sample_law_matches_reference_support():
         t = int(k.split("_")[1])
         pos, full = int(z["after_pos"][t]), bool(z["after_full"][t])
         assert O.replay_sample_law(pos, full, size, 0) == set(z[k].tolist()), k
+
+
+def test_config2_fixture_is_rollout_structured():
+    """update_config2.npz (the reference's GAE + update blocks at config 2) obeys the frame-stack
+    rule the frame-dedup update relies on: every stored slot is the frame slot_frame_ids names
+    (the newest slot of obs[s], or an older slot of obs[0]); and the oracle's GAE reproduces the
+    reference's advantages / returns bit for bit on it."""
+    z = golden("update_config2.npz")
+    obs = z["obs"].astype(np.float32)
+    T1, N, W, F = obs.shape
+    T = T1 - 1
+    samples = np.arange(T * N)
+    ids = O.slot_frame_ids(samples, z["dones"], N, W)
+    frames = O.frames_gather(obs, ids.reshape(-1)).reshape(T * N, W, F)
+    assert np.array_equal(frames, obs[:T].reshape(T * N, W, F))
+    adv, ret = O.gae(z["rewards"], z["values"].reshape(T, N), z["dones"][:T], z["next_value"],
+                     z["dones"][T], 0.99, 0.95)
+    assert np.array_equal(adv.reshape(-1), z["advantages"])
+    assert np.array_equal(ret.reshape(-1), z["returns"])
+    # distinct frames per minibatch: what the dedup plan sizes (11.3k of 16384 slots)
+    for j in range(2):
+        u = np.unique(ids[z["perm"][j * 4096:(j + 1) * 4096]])
+        assert 10000 < len(u) < 11520, len(u)
