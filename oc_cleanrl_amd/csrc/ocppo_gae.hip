@@ -12,7 +12,7 @@
 //   2. all threads form, per (t, n), delta = (r + (f32(gamma) * v') * nnt) - v and
 //      c = f32(gamma*lambda) * nnt with nnt = 1 - d' (v', d' = the next row, or next_value /
 //      next_done / the later chunk's first row at the chunk boundary);
-//   3. one lane per env runs A = delta + c * A over the chunk (LDS operands loaded 8 rows ahead);
+//   3. one lane per env runs A = delta + c * A over the chunk (16 rows of operands per LDS batch);
 //   4. all threads store A and R = A + v.
 // Every value is the reference's op for op, in f32 without contraction (-ffp-contract=off), so
 // advantages and returns are bit-identical to the PyTorch loop (ppo_atari_oc.py:533-547): only
@@ -22,6 +22,34 @@
 #include "ocppo_common.h"
 
 namespace ocppo {
+
+// The recurrence over rows rows-1 .. 0 of env column `tid` of an E-wide LDS tile (delta in sa,
+// c in sc; A written over delta): whole groups of 16 rows with no per-step branch (a uniform
+// branch per step costs more than the two dependent ops it guards), then the remainder.
+template <int E>
+__device__ __forceinline__ void gae_chain(float* sa, const float* sc, int rows, int tid,
+                                          float& last) {
+  int r0 = rows - 1;
+  for (int grp = rows / 16; grp > 0; --grp, r0 -= 16) {
+    float d[16], c[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      d[k] = sa[(r0 - k) * E + tid];
+      c[k] = sc[(r0 - k) * E + tid];
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      last = d[k] + c[k] * last;
+      d[k] = last;
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) sa[(r0 - k) * E + tid] = d[k];
+  }
+  for (; r0 >= 0; --r0) {
+    last = sa[r0 * E + tid] + sc[r0 * E + tid] * last;
+    sa[r0 * E + tid] = last;
+  }
+}
 
 template <int E>
 __global__ __launch_bounds__(256) void gae_tile_kernel(const float* __restrict__ rew,
@@ -94,24 +122,13 @@ __global__ __launch_bounds__(256) void gae_tile_kernel(const float* __restrict__
       s_cv[tid] = sv[tid];
       s_cd[tid] = sd[tid];
     }
-    // 3. the recurrence, one lane per env, operands fetched 8 rows ahead of the chain
+    // 3. the recurrence, one lane per env
+#ifndef OCPPO_GAE_NOCHAIN  // probe variant (tools/): every phase but the recurrence
     if (chain) {
-      for (int r0 = rows - 1; r0 >= 0; r0 -= 8) {
-        float dl[8], cc[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const int r = r0 - k >= 0 ? r0 - k : 0;
-          dl[k] = sa[r * E + tid];
-          cc[k] = sc[r * E + tid];
-        }
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          if (r0 - k >= 0) {
-            last = dl[k] + cc[k] * last;
-            sa[(r0 - k) * E + tid] = last;
-          }
-        }
-      }
+#else
+    if (chain && T < 0) {
+#endif
+      gae_chain<E>(sa, sc, rows, tid, last);
     }
     __syncthreads();
     // 4. advantages and returns
@@ -229,6 +246,10 @@ extern "C" int ocppo_gae(ocppo_stream_t stream, const float* rewards, const floa
   hipLaunchKernelGGL(gae_tile_kernel<E>, dim3(ceil_div(N, E)), dim3(256),                         \
                      4 * sizeof(float) * TC * (E), s, rewards, values, dones, next_value,          \
                      next_done, (int)T, N, TC, g, gl, advantages, returns)
+#ifdef OCPPO_GAE_E  // tile-width variants (tools/)
+    if (N <= 1024) OCPPO_GAE_TILE(OCPPO_GAE_E);
+    else
+#endif
     if (N <= 256) OCPPO_GAE_TILE(4);
     else if (N <= 1024) OCPPO_GAE_TILE(16);
     else OCPPO_GAE_TILE(64);

@@ -1254,9 +1254,50 @@ __device__ __forceinline__ void hl_dots(const float (&x)[CPL], const float (&w)[
 //      gp = (h > 0) * sum_k c_k W_k (written once), db_h += gp, dW_k += c_k h (registers).
 // Lanes accumulate c (head db) and the loss partials for their own rows; the workgroup adds its
 // waves through LDS in wave order and writes ONE record.
+// Packed f32 pairs (v_pk_fma_f32 / v_pk_add_f32: two f32 lanes per instruction). A lane's CPL
+// columns are held as CP = max(CPL / 2, 1) pairs (q = 2p, 2p + 1 of hl_col's order; CPL = 1 pads
+// the second half with zeros).
+typedef float hl_f2 __attribute__((ext_vector_type(2)));
+
+template <int CPL>
+__device__ __forceinline__ void hl_load2(const float* __restrict__ row, int lane,
+                                         hl_f2 (&x)[CPL >= 2 ? CPL / 2 : 1]) {
+  if constexpr (CPL >= 4) {
+    const float4* r4 = reinterpret_cast<const float4*>(row);
+#pragma unroll
+    for (int q4 = 0; q4 < CPL / 4; ++q4) {
+      const float4 v = r4[q4 * kWave + lane];
+      x[2 * q4] = hl_f2{v.x, v.y};
+      x[2 * q4 + 1] = hl_f2{v.z, v.w};
+    }
+  } else if constexpr (CPL == 2) {
+    x[0] = hl_f2{row[lane], row[kWave + lane]};
+  } else {
+    x[0] = hl_f2{row[lane], 0.f};
+  }
+}
+
+template <int CPL>
+__device__ __forceinline__ void hl_store2(float* __restrict__ row, int lane,
+                                          const hl_f2 (&x)[CPL >= 2 ? CPL / 2 : 1]) {
+  if constexpr (CPL >= 4) {
+    float4* r4 = reinterpret_cast<float4*>(row);
+#pragma unroll
+    for (int q4 = 0; q4 < CPL / 4; ++q4)
+      r4[q4 * kWave + lane] = make_float4(x[2 * q4].x, x[2 * q4].y, x[2 * q4 + 1].x,
+                                          x[2 * q4 + 1].y);
+  } else if constexpr (CPL == 2) {
+    row[lane] = x[0].x;
+    row[kWave + lane] = x[0].y;
+  } else {
+    row[lane] = x[0].x;
+  }
+}
+
 template <int CPL, int U>
 struct HlRows {
-  float x[U][CPL];
+  static constexpr int CP = CPL >= 2 ? CPL / 2 : 1;
+  hl_f2 x[U][CP];
   int64_t a;                    // lane u < U: row u's record
   float old_lp, adv, R, v_old;
 };
@@ -1268,7 +1309,7 @@ __device__ __forceinline__ void hl_rows_load(const HeadsLossParams& P, int64_t r
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int64_t r = rb + u < r1 ? rb + u : rb;
-    hl_load<CPL>(P.h + r * P.H, lane, s.x[u]);
+    hl_load2<CPL>(P.h + r * P.H, lane, s.x[u]);
   }
   const int64_t rl = rb + (lane & (U - 1)) < r1 ? rb + (lane & (U - 1)) : rb;
   s.a = L.b_actions[rl];
@@ -1280,7 +1321,8 @@ __device__ __forceinline__ void hl_rows_load(const HeadsLossParams& P, int64_t r
 
 template <int CPL, int NK>
 struct HlAcc {
-  float sb[CPL], sw[NK][CPL];
+  static constexpr int CP = CPL >= 2 ? CPL / 2 : 1;
+  hl_f2 sb[CP], sw[NK][CP];
   float sc[NK], part[kNumPartials];  // per lane: the rows this lane ran the loss for
 };
 
@@ -1322,26 +1364,27 @@ __device__ __forceinline__ float hl_reduce_scatter(float (&v)[8 * U], int lane) 
 
 template <int AMAX, bool EXACT, int CPL, int U>
 __device__ __forceinline__ void hl_rows_compute(const HeadsLossParams& P, int A,
-                                                const float (&w)[AMAX + 1][CPL],
+                                                const hl_f2 (&w)[AMAX + 1][CPL >= 2 ? CPL / 2 : 1],
                                                 const float (&bk)[AMAX + 1], float adv_mean,
                                                 float adv_den, int64_t rb, int64_t r1, int lane,
                                                 const HlRows<CPL, U>& s,
                                                 HlAcc<CPL, AMAX + 1>& acc) {
-  constexpr int NK = AMAX + 1;
+  constexpr int NK = AMAX + 1, CP = CPL >= 2 ? CPL / 2 : 1;
   const LossParams& L = P.L;
-  // 2. partial dots, slot (u, k) at u * 8 + k (k = NK..7 padding)
+  // 2. partial dots (even / odd columns in the two halves of a packed accumulator), slot (u, k)
+  //    at u * 8 + k (k = NK..7 padding)
   float v[8 * U];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
+    hl_f2 d[NK];  // NK independent chains interleaved (no back-to-back dependent pk_fma)
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      float d = 0.f;
-      if (k < NK) {
+    for (int k = 0; k < NK; ++k) d[k] = hl_f2{0.f, 0.f};
 #pragma unroll
-        for (int q = 0; q < CPL; ++q) d = fmaf(s.x[u][q], w[k][q], d);
-      }
-      v[u * 8 + k] = d;
-    }
+    for (int p = 0; p < CP; ++p)
+#pragma unroll
+      for (int k = 0; k < NK; ++k) d[k] = __builtin_elementwise_fma(s.x[u][p], w[k][p], d[k]);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[u * 8 + k] = k < NK ? d[k].x + d[k].y : 0.f;
   }
   const float red = hl_reduce_scatter<U>(v, lane);
   // 3. the loss of row `lane` (lanes < U)
@@ -1381,18 +1424,26 @@ __device__ __forceinline__ void hl_rows_compute(const HeadsLossParams& P, int A,
 #pragma unroll
     for (int k = 0; k < NK; ++k)
       c[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cl[k]), u));
-    float g[CPL];
+    hl_f2 d[CP], g[CP];  // CP independent chains interleaved
 #pragma unroll
-    for (int q = 0; q < CPL; ++q) {
-      float d = 0.f;
+    for (int p = 0; p < CP; ++p) d[p] = hl_f2{0.f, 0.f};
 #pragma unroll
-      for (int k = 0; k < NK; ++k) d = fmaf(c[k], w[k][q], d);
-      g[q] = s.x[u][q] <= 0.f ? 0.f : d;
-      acc.sb[q] += g[q];
+    for (int k = 0; k < NK; ++k)
 #pragma unroll
-      for (int k = 0; k < NK; ++k) acc.sw[k][q] = fmaf(c[k], s.x[u][q], acc.sw[k][q]);
+      for (int p = 0; p < CP; ++p)
+        d[p] = __builtin_elementwise_fma(hl_f2{c[k], c[k]}, w[k][p], d[p]);
+#pragma unroll
+    for (int k = 0; k < NK; ++k)
+#pragma unroll
+      for (int p = 0; p < CP; ++p)
+        acc.sw[k][p] = __builtin_elementwise_fma(hl_f2{c[k], c[k]}, s.x[u][p], acc.sw[k][p]);
+#pragma unroll
+    for (int p = 0; p < CP; ++p) {
+      const hl_f2 xv = s.x[u][p];
+      g[p] = hl_f2{xv.x <= 0.f ? 0.f : d[p].x, xv.y <= 0.f ? 0.f : d[p].y};
+      acc.sb[p] += g[p];
     }
-    hl_store<CPL>(P.gp + (rb + u) * P.H, lane, g);
+    hl_store2<CPL>(P.gp + (rb + u) * P.H, lane, g);
   }
 }
 
@@ -1415,27 +1466,30 @@ __global__ __launch_bounds__(256) void heads_loss_kernel(HeadsLossParams P) {
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * P.rows_per_wg;
   const int64_t r1 = r0 + P.rows_per_wg < L.M ? r0 + P.rows_per_wg : L.M;
   int64_t rb = r0 + wv * U;
+  constexpr int CP = CPL >= 2 ? CPL / 2 : 1;
   HlRows<CPL, U> sa, sbuf;
   if (rb < r1) hl_rows_load<CPL, U>(P, rb, r1, lane, sa);
-  float w[NK][CPL], bk[NK];
+  hl_f2 w[NK][CP];
+  float bk[NK];
 #pragma unroll
   for (int k = 0; k < NK; ++k) {
     const bool critic = k == AMAX;
     bk[k] = critic ? P.bc[0] : (k < A ? P.ba[k] : 0.f);
     const float* wr = critic ? P.wc : P.wa + static_cast<int64_t>(k < A ? k : 0) * H;
-    float t[CPL];
-    hl_load<CPL>(wr, lane, t);
+    hl_load2<CPL>(wr, lane, w[k]);
+    if (!(critic || k < A)) {
 #pragma unroll
-    for (int q = 0; q < CPL; ++q) w[k][q] = (critic || k < A) ? t[q] : 0.f;
+      for (int p = 0; p < CP; ++p) w[k][p] = hl_f2{0.f, 0.f};
+    }
   }
   HlAcc<CPL, NK> acc;
 #pragma unroll
-  for (int q = 0; q < CPL; ++q) acc.sb[q] = 0.f;
+  for (int p = 0; p < CP; ++p) acc.sb[p] = hl_f2{0.f, 0.f};
 #pragma unroll
   for (int k = 0; k < NK; ++k) {
     acc.sc[k] = 0.f;
 #pragma unroll
-    for (int q = 0; q < CPL; ++q) acc.sw[k][q] = 0.f;
+    for (int p = 0; p < CP; ++p) acc.sw[k][p] = hl_f2{0.f, 0.f};
   }
 #pragma unroll
   for (int q = 0; q < kNumPartials; ++q) acc.part[q] = 0.f;
@@ -1470,9 +1524,10 @@ __global__ __launch_bounds__(256) void heads_loss_kernel(HeadsLossParams P) {
   float* mine = hl_red + (static_cast<int64_t>(wv) * 64 + lane) * CPL * NV;
 #pragma unroll
   for (int q = 0; q < CPL; ++q) {
-    mine[q * NV] = acc.sb[q];
+    const int p = q >> 1;
+    mine[q * NV] = (q & 1) ? acc.sb[p].y : acc.sb[p].x;
 #pragma unroll
-    for (int k = 0; k < NK; ++k) mine[q * NV + 1 + k] = acc.sw[k][q];
+    for (int k = 0; k < NK; ++k) mine[q * NV + 1 + k] = (q & 1) ? acc.sw[k][p].y : acc.sw[k][p].x;
   }
   if (lane == 0) {
 #pragma unroll
@@ -1508,7 +1563,10 @@ __global__ __launch_bounds__(256) void heads_loss_kernel(HeadsLossParams P) {
 // 16 group sums pairwise through LDS. The same shape for every G: deterministic. The record ends
 // with the 6 loss partials at `ls` (a multiple of 16), so one block holds all of them and forms
 // the loss statistics (loss_finish's formulas).
-constexpr int kHlFinOut = 16, kHlFinGroups = 16, kHlFinBatch = 16;
+#ifndef OCPPO_HLFIN_OUT  // finish geometry (outputs x record groups per block); tools/ variants
+#define OCPPO_HLFIN_OUT 32
+#endif
+constexpr int kHlFinOut = OCPPO_HLFIN_OUT, kHlFinGroups = 256 / kHlFinOut, kHlFinBatch = 16;
 __global__ __launch_bounds__(256) void heads_loss_finish_kernel(
     const float* __restrict__ partials, int G, int64_t npw, int64_t ls, int64_t H, int A, int amax,
     int cpl, float* __restrict__ db_h, float* __restrict__ dwa, float* __restrict__ dwc,
@@ -1608,7 +1666,7 @@ inline int64_t hl_layout(int64_t M, int64_t H, int64_t A, int64_t& G, int64_t& l
   if (rows_per_wg) *rows_per_wg = rpw;
   const int64_t amax = hl_amax(A);
   // 64 lanes x (H / 64) columns x (amax + 2) slots, amax + 1 head-bias sums
-  ls = (H * (amax + 2) + amax + 1 + 15) / 16 * 16;
+  ls = (H * (amax + 2) + amax + 1 + kHlFinOut - 1) / kHlFinOut * kHlFinOut;
   return ls + kNumPartials;  // npw
 }
 
