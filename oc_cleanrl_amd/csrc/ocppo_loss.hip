@@ -1344,6 +1344,9 @@ __device__ __forceinline__ void hl_rs_step(float* v, int lane) {
 // returns the wave sum of value lane >> 1 (U = 4, after a last xor-1 add) or of value lane (U = 8).
 template <int U>
 __device__ __forceinline__ float hl_reduce_scatter(float (&v)[8 * U], int lane) {
+#ifdef OCPPO_HL_NORED  // probe variant (tools/): no cross-lane reduction
+  return v[lane & (8 * U - 1)];
+#endif
   if constexpr (U == 8) {
     hl_rs_step<64, 32>(v, lane);
     hl_rs_step<32, 16>(v, lane);
@@ -1443,14 +1446,18 @@ __device__ __forceinline__ void hl_rows_compute(const HeadsLossParams& P, int A,
       g[p] = hl_f2{xv.x <= 0.f ? 0.f : d[p].x, xv.y <= 0.f ? 0.f : d[p].y};
       acc.sb[p] += g[p];
     }
+#ifndef OCPPO_HL_NOSTORE  // probe variant (tools/)
     hl_store2<CPL>(P.gp + (rb + u) * P.H, lane, g);
+#else
+    if (g[0].x == 12345.f) hl_store2<CPL>(P.gp + (rb + u) * P.H, lane, g);
+#endif
   }
 }
 
 // Fixed grid (hl_layout): workgroup g owns rows [g * rows_per_wg, ...) and walks them in steps
 // of U rows per wave (4 waves: 4U rows per step), the next step's loads issued before this step's
 // arithmetic (two register sets, ping-pong). The workgroup's sums leave as ONE record
-// [64 lanes][CPL][NV] (NV = AMAX + 2 slots: db_h, AMAX actor dW rows, critic dW), NK head-bias
+// [CPL][NV][64 lanes] (NV = AMAX + 2 slots: db_h, AMAX actor dW rows, critic dW), NK head-bias
 // sums, the 6 loss partials at npw - 6: record traffic is O(grid), not O(M).
 template <int AMAX, bool EXACT, int CPL, int U>
 __global__ __launch_bounds__(256) void heads_loss_kernel(HeadsLossParams P) {
@@ -1463,6 +1470,9 @@ __global__ __launch_bounds__(256) void heads_loss_kernel(HeadsLossParams P) {
   const int A = EXACT ? AMAX : L.A;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t H = P.H;
+#ifdef OCPPO_HL_PHASES  // probe variant (tools/exp_hl_phases.py): shader-clock phase stamps
+  const uint64_t t0 = __builtin_readcyclecounter();
+#endif
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * P.rows_per_wg;
   const int64_t r1 = r0 + P.rows_per_wg < L.M ? r0 + P.rows_per_wg : L.M;
   int64_t rb = r0 + wv * U;
@@ -1506,6 +1516,9 @@ __global__ __launch_bounds__(256) void heads_loss_kernel(HeadsLossParams P) {
                                          acc);
     rb += kStep;
   }
+#ifdef OCPPO_HL_PHASES
+  const uint64_t t1 = __builtin_readcyclecounter();
+#endif
   // the lanes' head-bias and loss sums (lanes < U hold them): wave sum in lane order
   float misc[NK + kNumPartials];
 #pragma unroll
@@ -1520,14 +1533,25 @@ __global__ __launch_bounds__(256) void heads_loss_kernel(HeadsLossParams P) {
       t += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(misc[i]), u));
     misc[i] = t;
   }
-  // workgroup combine: per lane CPL x NV values through LDS, waves in order
-  float* mine = hl_red + (static_cast<int64_t>(wv) * 64 + lane) * CPL * NV;
+#ifdef OCPPO_HL_NOREC  // probe variant (tools/): no workgroup combine, no record
+  if (acc.sb[0].x != 12345.f) return;
+#endif
+  // workgroup combine: per lane CPL x NV values (+ padding to JP) through LDS as float4s,
+  // waves in order. Image of a wave: [JP / 4][64 lanes][4] (consecutive lanes, consecutive
+  // 16 B: conflict-free ds_write_b128 / ds_read_b128); the record keeps that layout.
+  constexpr int JP = (CPL * NV + 3) / 4 * 4;
+  float4* mine = reinterpret_cast<float4*>(hl_red) + static_cast<int64_t>(wv) * 16 * JP + lane;
 #pragma unroll
-  for (int q = 0; q < CPL; ++q) {
-    const int p = q >> 1;
-    mine[q * NV] = (q & 1) ? acc.sb[p].y : acc.sb[p].x;
+  for (int c4 = 0; c4 < JP / 4; ++c4) {
+    float e[4];
 #pragma unroll
-    for (int k = 0; k < NK; ++k) mine[q * NV + 1 + k] = (q & 1) ? acc.sw[k][p].y : acc.sw[k][p].x;
+    for (int i = 0; i < 4; ++i) {
+      const int j = 4 * c4 + i, q = j / NV, slot = j - q * NV, p = q >> 1;
+      e[i] = j >= CPL * NV ? 0.f
+             : slot == 0   ? ((q & 1) ? acc.sb[p].y : acc.sb[p].x)
+                           : ((q & 1) ? acc.sw[slot - 1][p].y : acc.sw[slot - 1][p].x);
+    }
+    mine[c4 * 64] = make_float4(e[0], e[1], e[2], e[3]);
   }
   if (lane == 0) {
 #pragma unroll
@@ -1536,13 +1560,23 @@ __global__ __launch_bounds__(256) void heads_loss_kernel(HeadsLossParams P) {
     for (int q = 0; q < kNumPartials; ++q) s_misc[wv][8 + q] = misc[NK + q];
   }
   __syncthreads();
+#ifdef OCPPO_HL_PHASES
+  const uint64_t t2 = __builtin_readcyclecounter();
+#endif
   float* out = P.partials + static_cast<int64_t>(blockIdx.x) * P.npw;
-  constexpr int nvals = 64 * CPL * NV;
-  for (int i = threadIdx.x; i < nvals; i += 256) {
-    float sacc = hl_red[i];
+  constexpr int nvals = 64 * JP;
+  {
+    const float4* img = reinterpret_cast<const float4*>(hl_red);
+    float4* out4 = reinterpret_cast<float4*>(out);
+    for (int c = threadIdx.x; c < nvals / 4; c += 256) {
+      float4 a = img[c];
 #pragma unroll
-    for (int wq = 1; wq < 4; ++wq) sacc += hl_red[wq * nvals + i];
-    out[i] = sacc;
+      for (int wq = 1; wq < 4; ++wq) {
+        const float4 b = img[wq * (nvals / 4) + c];
+        a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+      }
+      out4[c] = a;
+    }
   }
   if (threadIdx.x < NK) {
     const int i = threadIdx.x;
@@ -1553,8 +1587,19 @@ __global__ __launch_bounds__(256) void heads_loss_kernel(HeadsLossParams P) {
     const int i = threadIdx.x - 64;
     float sacc = s_misc[0][8 + i];
     for (int wq = 1; wq < 4; ++wq) sacc += s_misc[wq][8 + i];
-    out[P.npw - kNumPartials + i] = sacc;
+    out[P.npw - 8 + i] = sacc;  // at ls (npw = ls + 8)
   }
+#ifdef OCPPO_HL_PHASES
+  const uint64_t t3 = __builtin_readcyclecounter();
+  __syncthreads();
+  if (lane == 0) {  // per wave: rows done, LDS image synced, record issued (cycles after start)
+    float* dbg = P.gp + (static_cast<int64_t>(blockIdx.x) * 4 + wv) * 4;
+    dbg[0] = static_cast<float>(t1 - t0);
+    dbg[1] = static_cast<float>(t2 - t0);
+    dbg[2] = static_cast<float>(t3 - t0);
+    dbg[3] = static_cast<float>(t0 & 0xFFFFFF);
+  }
+#endif
 }
 
 // Adds the G workgroup records with a fixed-shape tree: a block owns 16 record entries (outputs)
@@ -1598,16 +1643,18 @@ __global__ __launch_bounds__(256) void heads_loss_finish_kernel(
     __syncthreads();
   }
   const int nv = amax + 2;
-  const int64_t nvals = 64 * cpl * nv;
+  const int jp = (cpl * nv + 3) / 4 * 4;
+  const int64_t nvals = 64 * jp;
   if (gi == 0) {
     const float t = red[0][o];
     tot[o] = t;
-    if (idx < nvals) {  // [lane][q][slot] -> column of hl_col
-      const int slot = static_cast<int>(idx % nv);
-      const int lq = static_cast<int>(idx / nv);
-      const int ln = lq / cpl, q = lq - ln * cpl;
+    const int ln = static_cast<int>((idx >> 2) & 63);
+    const int j = static_cast<int>((idx >> 8) * 4 + (idx & 3));
+    if (idx < nvals) {  // [j / 4][lane][j % 4], j = q * nv + slot (j >= cpl * nv: padding)
+      const int q = j / nv, slot = j - q * nv;
       const int64_t col = cpl >= 4 ? 4 * ((q >> 2) * kWave + ln) + (q & 3) : q * kWave + ln;
-      if (slot == 0) {
+      if (j >= cpl * nv) {
+      } else if (slot == 0) {
         if (db_h) db_h[col] = t;
       } else if (slot == nv - 1) {
         dwc[col] = t;
@@ -1665,9 +1712,11 @@ inline int64_t hl_layout(int64_t M, int64_t H, int64_t A, int64_t& G, int64_t& l
   G = (M + rpw - 1) / rpw;
   if (rows_per_wg) *rows_per_wg = rpw;
   const int64_t amax = hl_amax(A);
-  // 64 lanes x (H / 64) columns x (amax + 2) slots, amax + 1 head-bias sums
-  ls = (H * (amax + 2) + amax + 1 + kHlFinOut - 1) / kHlFinOut * kHlFinOut;
-  return ls + kNumPartials;  // npw
+  // 64 lanes x (H / 64) columns x (amax + 2) slots (padded to a multiple of 4 per lane),
+  // amax + 1 head-bias sums; the 6 loss partials at ls (npw = ls + 8 keeps records 16-B aligned)
+  const int64_t jp = ((H / 64) * (amax + 2) + 3) / 4 * 4;
+  ls = (64 * jp + amax + 1 + kHlFinOut - 1) / kHlFinOut * kHlFinOut;
+  return ls + 8;  // npw
 }
 
 // the decoder widths the rows kernel is instantiated for: H / 64 columns per lane in {1, 2, 4, 8}
@@ -1677,7 +1726,7 @@ inline bool hl_width_ok(int64_t H) {
 
 template <int AMAX, bool EXACT>
 static void launch_heads_loss(hipStream_t s, const HeadsLossParams& P, int G, int cpl) {
-  const size_t lds = sizeof(float) * 4 * 64 * cpl * (AMAX + 2);
+  const size_t lds = sizeof(float) * 4 * 64 * ((cpl * (AMAX + 2) + 3) / 4 * 4);
   const dim3 g(G), b(256);
   switch (cpl) {
     case 1: hipLaunchKernelGGL((heads_loss_kernel<AMAX, EXACT, 1, 4>), g, b, lds, s, P); break;

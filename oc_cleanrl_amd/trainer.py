@@ -75,6 +75,44 @@ class FlatGrads:
         self.buf.div_(ws)
 
 
+class GradExchange:
+    """The data-parallel gradient exchange of ppo_atari_multigpu.py:360-374 on ONE persistent flat
+    grad buffer (every parameter's .grad is a view of it): all_reduce(SUM), then / world -- the
+    division either here or folded into the optimizer step (FlatAdam's grad_scale), identical on
+    every rank.
+
+    split(): the buffer's tail [tail_off:] (the gradients the first backward phase has already
+    written) is reduced asynchronously while `lower_backward()` fills the head [:tail_off], then
+    the head is reduced and the tail's work awaited. The same SUM of the same bytes as
+    whole(); ranks end with identical buffers."""
+
+    def __init__(self, buf, tail_off: int, world: int, scale_in_optimizer: bool, group=None):
+        self.buf, self.tail_off, self.world = buf, tail_off, world
+        self.scale_in_optimizer, self.group = scale_in_optimizer, group
+
+    def _finish(self):
+        if not self.scale_in_optimizer:
+            self.buf.div_(self.world)
+
+    def whole(self):
+        dist.all_reduce(self.buf, op=dist.ReduceOp.SUM, group=self.group)
+        self._finish()
+
+    def split(self, lower_backward):
+        work = dist.all_reduce(self.buf[self.tail_off:], op=dist.ReduceOp.SUM, group=self.group,
+                               async_op=True)
+        lower_backward()
+        dist.all_reduce(self.buf[:self.tail_off], op=dist.ReduceOp.SUM, group=self.group)
+        work.wait()
+        self._finish()
+
+
+def rank_seeds(seed: int, rank: int) -> tuple[int, int]:
+    """(init seed, stream seed) of ppo_atari_multigpu.py:208-212, 230-231: every rank builds the
+    network from the same seed, then draws its env / sampling / shuffle streams from seed + rank."""
+    return seed, seed + rank
+
+
 class KernelTimer:
     """Per-launch device durations of this package's HIP kernels.
 
@@ -159,9 +197,9 @@ class PPOTrainer:
 
         # seeding as ppo_atari_multigpu.py:208-212, 230-231: identical init on every rank, then
         # rank-dependent sampling / env / shuffle streams
-        self.seed = a.seed + rank
+        init_seed, self.seed = rank_seeds(a.seed, rank)
         self.np_rng = np.random.RandomState(self.seed)  # np.random.shuffle stream of :561
-        torch.manual_seed(a.seed)
+        torch.manual_seed(init_seed)
 
         self.N = a.local_num_envs
         self.T = a.num_steps
@@ -600,30 +638,19 @@ class PPOTrainer:
         low, low_d = self.cuts.pop(j)
         torch.autograd.backward(low, low_d.grad)
 
-    def _allreduce(self):
-        """DP exchange (ppo_atari_multigpu.py:360-374): ONE in-place RCCL all-reduce of the flat
-        grad buffer; the `/ world_size` is folded into the optimizer step (grad_scale)."""
-        dist.all_reduce(self.grad_buf, op=dist.ReduceOp.SUM)
-        if not self.args.fused_optimizer:
-            self.grad_buf.div_(self.world)
-
     def _exchange(self, j: int, replay: bool):
-        """Minibatch j's gradients, all-reduced. Split form: the first backward phase has filled
-        the flat buffer's tail (the last encoder layer, decoder and heads); its all-reduce runs on
-        RCCL's stream while the second phase (the encoder layers below the cut) runs on ours,
-        then the head of the buffer follows. Same SUM of the same bytes as _allreduce."""
+        """Minibatch j's gradients, all-reduced (GradExchange; the `/ world_size` is folded into
+        the fused optimizer step). Split form: the first backward phase has filled the flat
+        buffer's tail (the last encoder layer, decoder and heads); its all-reduce runs on RCCL's
+        stream while the second phase (the encoder layers below the cut) runs on ours, then the
+        head of the buffer follows."""
+        ex = GradExchange(self.grad_buf, self.tail_off, self.world, self.args.fused_optimizer)
         if not self.split:
-            self._allreduce()
-            return
-        work = dist.all_reduce(self.grad_buf[self.tail_off:], op=dist.ReduceOp.SUM, async_op=True)
-        if replay:
-            self.g_low[j].replay()
+            ex.whole()
+        elif replay:
+            ex.split(self.g_low[j].replay)
         else:
-            self._backward_low(j)
-        dist.all_reduce(self.grad_buf[:self.tail_off], op=dist.ReduceOp.SUM)
-        work.wait()
-        if not self.args.fused_optimizer:
-            self.grad_buf.div_(self.world)
+            ex.split(lambda: self._backward_low(j))
 
     def _opt_step(self):
         if self.args.fused_optimizer:
