@@ -12,9 +12,10 @@ value = env steps of all ranks / max-over-ranks wall time of the K timed iterati
 
 Rank 0 prints ONE JSON line. Extra fields: `roofline` (dominant HIP kernel of this package, live
 HIP-event timing over the timed region), `kernels` (every HIP kernel's mean launch duration and
-algorithmic GB/s), `roofline_scaled` (N=1: the north-star kernels -- GAE, fused PPO loss -- and the
-rollout head re-timed at streaming sizes, where HBM rather than launch latency bounds them; same
-algorithmic-byte formulas, tools/kernel_bench.py cases), `cpu_baseline` (the oracle's CPU port of
+algorithmic GB/s), `roofline_scaled` (N=1: the north-star kernels the timed path runs -- GAE, minibatch
+prepare, the fused heads + loss pair -- and the rollout head and ReLU backward re-timed cold at
+streaming sizes, where HBM rather than launch latency bounds them; same algorithmic-byte formulas,
+tools/kernel_bench.py cases), `cpu_baseline` (the oracle's CPU port of
 the same loop timed on this host, N=1).
 """
 from __future__ import annotations
@@ -37,13 +38,13 @@ MFMA_F32_PEAK_TFLOPS = 157.3  # dense f32 MFMA (MI355X_MICROARCH.md; no xf32 on 
 RIDGE = MFMA_F32_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9)  # flop/B where the two bounds meet
 # HBM bytes per launch from rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE, separate passes) of
 # the same launch shapes: tools/profile_round.sh -> tools/summarize_profiles.py
-PMC_SUMMARY = ROOT / "profiles" / "r02" / "pmc_summary.json"
+PMC_SUMMARY = ROOT / "profiles" / "r03" / "pmc_summary.json"
 PMC_KEYS = {"action_head": "policy_head_config", "gae": "gae_config",
             "ppo_loss": "ppo_loss_prepared_config", "relu_bias_grad": "relu_bias_grad_config",
             "cache_linear": "cache_linear_config", "store_encode": "store_encode_config",
             "heads_bwd": "heads_bwd_config", "relu_bias_wgrad": "relu_bias_wgrad_config",
             "heads_loss": "heads_loss_config", "decoder": "decoder_config",
-            "encoder_mid": "encoder_mid_config"}
+            "encoder_mid": "encoder_mid_config", "mb_prepare": "mb_prepare_config"}
 
 
 def pmc_traffic(key):
@@ -140,20 +141,29 @@ def kernel_flops(tr) -> dict:
     return fl
 
 
+def mfma_bound(flops, nbytes) -> bool:
+    """Arithmetic intensity (useful flops / algorithmic bytes) above the ridge point."""
+    return bool(flops) and flops / nbytes > RIDGE
+
+
 def roofline_of(name, k, flops, traffic, src):
-    """The roofline record of one timed kernel: MFMA-bound when its arithmetic intensity (useful
-    flops / algorithmic bytes) is above the ridge point, else HBM-bound."""
-    rec = {"kernel": name, "bytes_per_launch": k["bytes"], "mean_launch_us": k["mean_us"],
-           "traffic": traffic, "traffic_source": src}
-    if flops and flops / k["bytes"] > RIDGE:
+    """The roofline record of one timed kernel: MFMA-bound when its arithmetic intensity is above
+    the ridge point (timed warm: its operands are cache-resident in the iteration too), else
+    HBM-bound, timed cold (an L3 scrub before every replayed launch: the operands come from HBM,
+    never from Infinity-Cache hits; trainer.replay_time_us)."""
+    rec = {"kernel": name, "bytes_per_launch": k["bytes"], "traffic": traffic,
+           "traffic_source": src}
+    if mfma_bound(flops, k["bytes"]):
         ach = flops / (k["mean_us"] * 1e-6) / 1e12
-        rec.update(bound="mfma", achieved=round(ach, 2), peak=MFMA_F32_PEAK_TFLOPS,
-                   unit="TFLOP/s", frac=round(ach / MFMA_F32_PEAK_TFLOPS, 5),
-                   flops_per_launch=flops)
+        rec.update(bound="mfma", mean_launch_us=k["mean_us"], cache="warm",
+                   achieved=round(ach, 2), peak=MFMA_F32_PEAK_TFLOPS, unit="TFLOP/s",
+                   frac=round(ach / MFMA_F32_PEAK_TFLOPS, 5), flops_per_launch=flops)
     else:
-        ach = k["GBps"]
-        rec.update(bound="hbm", achieved=ach, peak=HBM_PEAK_GBS, unit="GB/s",
-                   frac=round(ach / HBM_PEAK_GBS, 5))
+        us = k.get("cold_us", k["mean_us"])
+        ach = round(k["bytes"] / (us * 1e-6) / 1e9, 2)
+        rec.update(bound="hbm", mean_launch_us=us, warm_launch_us=k["mean_us"],
+                   cache="cold" if "cold_us" in k else "warm", achieved=ach, peak=HBM_PEAK_GBS,
+                   unit="GB/s", frac=round(ach / HBM_PEAK_GBS, 5))
     return rec
 
 
@@ -176,9 +186,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, default=2, choices=(2, 3),
+    ap.add_argument("--config", type=int, default=2, choices=(1, 2, 3),
                     help="BASELINE config: 2 = Pong obj PPO_OBJ (the headline; 4 = 2 per GPU), "
-                         "3 = Breakout dqn-pixels NatureCNN, 256 envs")
+                         "3 = Breakout dqn-pixels NatureCNN, 256 envs, 1 = ppo.py CartPole-v1 "
+                         "(4 envs; its CPU leg is the reference's own CPU path)")
     ap.add_argument("--envs-per-gpu", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-iterations", type=int, default=3)
@@ -214,7 +225,14 @@ def main():
         else:
             dist.init_process_group("gloo")
 
-    if opt.config == 3:
+    if opt.config == 1:
+        from oc_cleanrl_amd.ppo import PPO_DEFAULTS
+
+        envs = opt.envs_per_gpu or 4
+        args = Args(**{**PPO_DEFAULTS, "num_envs": envs * world, "cuda_graphs": not opt.no_graphs,
+                       "save_model": False})
+        opt.no_kernel_timing = True
+    elif opt.config == 3:
         envs = opt.envs_per_gpu or 256
         # MIOpen's deterministic convolution algorithms (use_deterministic_algorithms(True), the
         # reference default) are naive kernels on gfx950, ~30x slower for NatureCNN: config 3 is
@@ -256,10 +274,14 @@ def main():
 
     env_steps = opt.steps * args.num_steps * args.local_num_envs * world
     updates = opt.steps * args.update_epochs * args.num_minibatches
-    kb = kernel_bytes(tr)
+    kb = kernel_bytes(tr) if opt.config != 1 else {}
+    kf = kernel_flops(tr) if opt.config != 1 else {}
     kernels = {}
     if not opt.no_kernel_timing:
-        for name, us in tr.timer.measure().items():
+        # HBM-bound sites (no flops, or below the ridge) are also timed cold
+        cold = {n for n in tr.timer.sites
+                if not mfma_bound(kf.get(n), kb.get(n) or 1)}
+        for name, us in tr.timer.measure(cold=cold).items():
             n = tr.timer.per_iter.get(name, 0)
             nbytes = kb.get(name) or (relu_bias_grad_bytes(name)
                                       if name.startswith("relu_bias_grad_") else
@@ -267,8 +289,13 @@ def main():
                                       if name.startswith("relu_bias_wgrad_") else None)
             kernels[name] = {"mean_us": round(us, 3), "launches_per_iter": n,
                              "us_per_iter": round(us * n, 2)}
+            if name in tr.timer.cold_us:
+                kernels[name]["cold_us"] = round(tr.timer.cold_us[name], 3)
             if nbytes:
                 kernels[name].update(bytes=nbytes, GBps=round(nbytes / (us * 1e-6) / 1e9, 2))
+                if "cold_us" in kernels[name]:
+                    kernels[name]["GBps_cold"] = round(
+                        nbytes / (kernels[name]["cold_us"] * 1e-6) / 1e9, 2)
     # one kernel, several launch shapes per minibatch: aggregate them (average bytes per launch
     # over average launch duration = total bytes / total time)
     parts = [k for k in kernels if k.startswith("relu_bias_grad_") and "bytes" in kernels[k]]
@@ -280,10 +307,14 @@ def main():
                                      "us_per_iter": round(t, 2), "bytes": round(b / n),
                                      "GBps": round(b / (t * 1e-6) / 1e9, 2),
                                      "shapes": sorted(k[len("relu_bias_grad_"):] for k in parts)}
+        if all("cold_us" in kernels[k] for k in parts):
+            tc = sum(kernels[k]["cold_us"] * kernels[k]["launches_per_iter"] for k in parts)
+            kernels["relu_bias_grad"].update(cold_us=round(tc / n, 3),
+                                             GBps_cold=round(b / (tc * 1e-6) / 1e9, 2))
         for k in parts:
             kernels[k].pop("GBps", None)  # counted in the aggregate
+            kernels[k].pop("GBps_cold", None)
     timed = [k for k in kernels if "GBps" in kernels[k]]
-    kf = kernel_flops(tr)
     recs = []
     for name in sorted(timed, key=lambda k: -kernels[k]["us_per_iter"]):
         # the PMC passes replay config 2's launch shapes: no traffic figure for other configs
@@ -298,16 +329,30 @@ def main():
     if rank == 0 and world == 1 and not opt.no_scaled and opt.config == 2:
         from tools.kernel_bench import run_case
 
+        # the north-star kernels the timed path runs (GAE, minibatch prepare = adv-norm stats,
+        # the fused heads + loss pair) and the largest HBM streams of the iteration, at streaming
+        # sizes, every launch after an L3 scrub (cold)
         scaled = {}
-        for name in ("gae", "ppo_loss_prepared", "policy_head", "relu_bias_grad"):
-            r = run_case(name, "scaled", device, reps=10, rounds=5)
+        for name in ("gae", "heads_loss", "mb_prepare", "policy_head", "relu_bias_grad"):
+            r = run_case(name, "scaled", device, reps=10, rounds=5, cold=True)
             traffic, _ = pmc_traffic(f"{name}_scaled")
-            scaled[name] = {"params": r["params"], "mean_us": r["mean_us"], "bytes": r["bytes"],
-                            "achieved": r["GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                            "frac": r["frac"], "traffic": traffic}
+            scaled[name] = {"params": r["params"], "mean_us": r["mean_us"], "cache": r["cache"],
+                            "bytes": r["bytes"], "achieved": r["GBps"], "peak": HBM_PEAK_GBS,
+                            "unit": "GB/s", "frac": r["frac"], "traffic": traffic}
             torch.cuda.empty_cache()
 
     cpu = None
+    if rank == 0 and world == 1 and not opt.no_cpu_baseline and opt.config == 1:
+        # config 1 is the reference's CPU path: its loop on this host (oracle CartPole dynamics)
+        from oracle.cpu_learner import host_info, time_cpu_cartpole
+
+        r = time_cpu_cartpole(iterations=opt.cpu_iterations * 20, threads=1)
+        cpu = {"value": round(r["sps"], 1), "unit": "env steps/s", "cores": 1, "kind": "port",
+               "updates_per_sec": round(r["updates_per_sec"], 2),
+               "sample": f"{r['iterations']} iterations of cleanrl/ppo.py's loop (4 CartPole-v1 "
+                         f"envs x 128 steps, 16 minibatch updates of 128) on CPU torch, 1 thread, "
+                         f"{r['seconds']:.1f} s",
+               "host": host_info()}
     if rank == 0 and world == 1 and not opt.no_cpu_baseline and opt.config == 2:
         # CPU baseline leg (the oracle's port of the reference loop), on every host core this
         # process may use (its CPU affinity capped by the cgroup quota)
@@ -330,7 +375,9 @@ def main():
         line = {
             "metric": "env steps/sec (SPS) + PPO updates/sec, ALE/Pong-v5 obj-mode, 1/2/4/8 MI355X"
                       if opt.config == 2 else
-                      "env steps/sec (SPS) + PPO updates/sec, ALE/Breakout-v5 dqn pixels, 1 MI355X",
+                      "env steps/sec (SPS) + PPO updates/sec, ALE/Breakout-v5 dqn pixels, 1 MI355X"
+                      if opt.config == 3 else
+                      "env steps/sec (SPS) + PPO updates/sec, CartPole-v1 (ppo.py), 1 MI355X",
             "value": round(sps, 1),
             "unit": "env steps/s",
             "n_gpus": world,
@@ -342,10 +389,13 @@ def main():
             "vs_baseline": None,
             "dtype": "fp32",
             "data": "synthetic (device-resident Pong-obj env; random-init PPObj)" if opt.config == 2
-                    else "synthetic (device-resident 84x84 u8 frames; random-init NatureCNN)",
+                    else "synthetic (device-resident 84x84 u8 frames; random-init NatureCNN)"
+                    if opt.config == 3 else
+                    "device CartPole-v1 env (gymnasium 0.28.1 dynamics restated); random-init agent",
             "config": {"workload": "ppo_atari_oc.py Pong-v5 obj PPO_OBJ (BASELINE config 2 per GPU)"
                        if opt.config == 2 else
-                       "ppo_atari_oc.py Breakout-v5 dqn NatureCNN (BASELINE config 3)",
+                       "ppo_atari_oc.py Breakout-v5 dqn NatureCNN (BASELINE config 3)"
+                       if opt.config == 3 else "ppo.py CartPole-v1, 4 envs (BASELINE config 1)",
                        "local_num_envs": args.local_num_envs, "num_envs": args.num_envs,
                        "num_steps": args.num_steps, "num_features": args.num_features,
                        "minibatch_size": args.local_minibatch_size,

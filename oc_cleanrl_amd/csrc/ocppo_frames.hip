@@ -281,23 +281,28 @@ __global__ __launch_bounds__(256) void frames_scatter_relu_kernel(
   // data pass: thread = (frame parity h, float4 column group q); frames j = 2 p + h
   const int h = tid >> 7, qg = tid & 127;
   float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int64_t e = static_cast<int64_t>(qg) * 4; e < E; e += 128 * 4) {
+  // block-uniform trip count (the barriers below are reached by every thread); lanes past E
+  // load and store nothing
+  for (int64_t e0 = 0; e0 < E; e0 += 128 * 4) {
+    const int64_t e = e0 + static_cast<int64_t>(qg) * 4;
+    const bool live = e < E;
     float4 v0[F / 2], v1[F / 2], mk[F / 2];
 #pragma unroll
     for (int p = 0; p < F / 2; ++p) {  // first two uses + the mask of every frame, in flight
       const int j = 2 * p + h;
-      const int n = cnt[j];
+      const int n = live ? cnt[j] : 0;
       const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
       v0[p] = n > 0 ? *reinterpret_cast<const float4*>(dh + static_cast<int64_t>(list[j][0]) * E + e) : z;
       v1[p] = n > 1 ? *reinterpret_cast<const float4*>(dh + static_cast<int64_t>(list[j][1]) * E + e) : z;
-      mk[p] = (out && c0 + j < C) ? *reinterpret_cast<const float4*>(out + (c0 + j) * E + e)
-                                  : make_float4(1.f, 1.f, 1.f, 1.f);
+      mk[p] = (live && out && c0 + j < C)
+                  ? *reinterpret_cast<const float4*>(out + (c0 + j) * E + e)
+                  : make_float4(1.f, 1.f, 1.f, 1.f);
     }
 #pragma unroll
     for (int p = 0; p < F / 2; ++p) {
       const int j = 2 * p + h;
       const int64_t c = c0 + j;
-      if (c >= C) continue;
+      if (c >= C || !live) continue;
       const int n = cnt[j];
       float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
       if (n > 0) { a.x += v0[p].x; a.y += v0[p].y; a.z += v0[p].z; a.w += v0[p].w; }
@@ -314,7 +319,7 @@ __global__ __launch_bounds__(256) void frames_scatter_relu_kernel(
     if (dbp) {  // the two frame parities of this column group, in h order
       if (h == 1) half1[qg] = cs;
       __syncthreads();
-      if (h == 0) {
+      if (h == 0 && live) {
         const float4 o = half1[qg];
         *reinterpret_cast<float4*>(dbp + static_cast<int64_t>(blockIdx.x) * E + e) =
             make_float4(cs.x + o.x, cs.y + o.y, cs.z + o.z, cs.w + o.w);

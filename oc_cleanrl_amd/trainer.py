@@ -113,6 +113,68 @@ def rank_seeds(seed: int, rank: int) -> tuple[int, int]:
     return seed, seed + rank
 
 
+_SCRUB: dict = {}
+
+
+def l3_scrub(device, mib: int = 640):
+    """A launch that streams `mib` MiB through the caches (a sum over a resident buffer, 2.5x the
+    256 MiB Infinity Cache): whatever a kernel read before it is no longer cached after it."""
+    key = (str(device), mib)
+    if key not in _SCRUB:
+        _SCRUB[key] = torch.ones(mib << 18, dtype=torch.float32, device=device)
+    buf = _SCRUB[key]
+    return lambda: buf.sum()
+
+
+def replay_time_us(fn, reps: int = 64, rounds: int = 5, cold: bool = False) -> float:
+    """Mean device time of one launch of the closure `fn`: `reps` back-to-back copies captured
+    into one hipGraph, timed with HIP events over `rounds` replays (includes the ~1 us graph-node
+    gap per launch). cold=True puts an L3 scrub (l3_scrub) before every copy and subtracts the
+    same graph of scrubs alone (min over rounds of each), so every launch reads its operands
+    from HBM: the figure an HBM roofline fraction may be quoted on."""
+    def graph_of(body):
+        g = torch.cuda.CUDAGraph()
+        with _graph_capture(g):
+            for _ in range(reps):
+                body()
+        g.replay()
+        return g
+
+    def timed(g):
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record()
+        g.replay()
+        b.record()
+        torch.cuda.synchronize()
+        return a.elapsed_time(b)
+
+    fn()
+    torch.cuda.synchronize()
+    if not cold:
+        g = graph_of(fn)
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(rounds):
+            g.replay()
+        b.record()
+        torch.cuda.synchronize()
+        return 1e3 * a.elapsed_time(b) / (reps * rounds)
+    scrub = l3_scrub(torch.device("cuda", torch.cuda.current_device()))
+
+    def both():
+        scrub()
+        fn()
+
+    g1, g0 = graph_of(both), graph_of(scrub)
+    t1, t0 = [], []
+    for _ in range(rounds):
+        t1.append(timed(g1))
+        t0.append(timed(g0))
+    return 1e3 * max(min(t1) - min(t0), 0.0) / reps
+
+
 class KernelTimer:
     """Per-launch device durations of this package's HIP kernels.
 
@@ -120,9 +182,10 @@ class KernelTimer:
     hipEventRecordWithFlags(.., hipEventRecordExternal) returns hipErrorInvalidValue during
     capture), so the timed region itself cannot be bracketed per kernel. Instead every bracketed
     launch site keeps the closure of its first eager launch (same buffers, same stream) and
-    `measure()` replays `reps` back-to-back copies of exactly that launch as one hipGraph between
-    two HIP events: mean launch duration = elapsed / reps (includes the ~1 us graph-node gap;
-    cross-checked against rocprofv3 --kernel-trace in profiles/)."""
+    `measure()` replays copies of exactly that launch (replay_time_us): warm (back to back, the
+    operands cache-resident) for every site, and cold (an L3 scrub before every copy) for the
+    sites named in `cold` -- the HBM-bound kernels, whose roofline fraction must not be quoted on
+    Infinity-Cache hits. Cross-checked against rocprofv3 --kernel-trace in profiles/."""
 
     def __init__(self, enabled: bool):
         self.enabled = enabled
@@ -130,9 +193,11 @@ class KernelTimer:
         self.per_iter: dict = {}
         self._counting = True
         self.mean_us: dict = {}
+        self.cold_us: dict = {}
 
     def bracket(self, name, fn):
-        if self.enabled and not torch.cuda.is_current_stream_capturing():
+        if self.enabled and not (torch.cuda.is_available() and
+                                 torch.cuda.is_current_stream_capturing()):
             self.sites.setdefault(name, fn)
             if self._counting:
                 self.per_iter[name] = self.per_iter.get(name, 0) + 1
@@ -141,24 +206,11 @@ class KernelTimer:
     def end_iteration(self):
         self._counting = False
 
-    def measure(self, reps: int = 64, rounds: int = 5) -> dict:
+    def measure(self, reps: int = 64, rounds: int = 5, cold=()) -> dict:
         for name, fn in self.sites.items():
-            fn()
-            torch.cuda.synchronize()
-            g = torch.cuda.CUDAGraph()
-            with _graph_capture(g):
-                for _ in range(reps):
-                    fn()
-            g.replay()
-            a = torch.cuda.Event(enable_timing=True)
-            b = torch.cuda.Event(enable_timing=True)
-            a.record()
-            for _ in range(rounds):
-                g.replay()
-            b.record()
-            torch.cuda.synchronize()
-            self.mean_us[name] = 1e3 * a.elapsed_time(b) / (reps * rounds)
-            del g
+            self.mean_us[name] = replay_time_us(fn, reps, rounds)
+            if name in cold:
+                self.cold_us[name] = replay_time_us(fn, 16, rounds, cold=True)
         return self.mean_us
 
 

@@ -271,6 +271,97 @@ def time_cpu_blocks(threads: int, c3: bool = True) -> dict:
     return out
 
 
+class CpuCartPoleAgent(nn.Module):
+    """cleanrl/ppo.py:100-126 restated: separate tanh-MLP critic / actor (64-64), orthogonal init
+    (critic out std 1, actor out std 0.01)."""
+
+    def __init__(self, obs_dim=4, n_actions=2):
+        super().__init__()
+        self.critic = nn.Sequential(_init(nn.Linear(obs_dim, 64)), nn.Tanh(),
+                                    _init(nn.Linear(64, 64)), nn.Tanh(),
+                                    _init(nn.Linear(64, 1), std=1.0))
+        self.actor = nn.Sequential(_init(nn.Linear(obs_dim, 64)), nn.Tanh(),
+                                   _init(nn.Linear(64, 64)), nn.Tanh(),
+                                   _init(nn.Linear(64, n_actions), std=0.01))
+
+    def get_value(self, x):
+        return self.critic(x)
+
+    def get_action_and_value(self, x, action=None):
+        dist = torch.distributions.Categorical(logits=self.actor(x))
+        if action is None:
+            action = dist.sample()
+        return action, dist.log_prob(action), dist.entropy(), self.critic(x)
+
+
+def time_cpu_cartpole(iterations=20, threads=1, num_envs=4, num_steps=128, seed=1) -> dict:
+    """BASELINE config 1 on the host: cleanrl/ppo.py's loop (:185-309; 4 CartPole-v1 envs,
+    128 steps, 4 epochs x 4 minibatches of 128, clip 0.2, lr 2.5e-4 annealed off) with the
+    oracle's CartPole dynamics (CartPoleOracle, gymnasium 0.28.1 restated) and the reference's
+    agent on CPU torch with `threads` threads (ppo.py sets no thread count; 1 is its per-process
+    share on a loaded host). Returns env steps/s and PPO updates/s over `iterations`."""
+    torch.set_num_threads(threads)
+    torch.manual_seed(seed)
+    np.random.seed(seed)
+    env = O.CartPoleOracle(num_envs, seed)
+    agent = CpuCartPoleAgent()
+    opt = torch.optim.Adam(agent.parameters(), lr=2.5e-4, eps=1e-5)
+    T, N, nmb, E = num_steps, num_envs, 4, 4
+    B, M = T * N, T * N // nmb
+    next_obs = torch.tensor(env.reset())
+    next_done = torch.zeros(N)
+
+    def iteration(next_obs, next_done):
+        obs = torch.zeros((T, N, 4))
+        actions = torch.zeros((T, N), dtype=torch.long)
+        logprobs, rewards = torch.zeros((T, N)), torch.zeros((T, N))
+        dones, values = torch.zeros((T, N)), torch.zeros((T, N))
+        for step in range(T):
+            obs[step] = next_obs
+            dones[step] = next_done
+            with torch.no_grad():
+                action, logprob, _, value = agent.get_action_and_value(next_obs)
+            values[step] = value.flatten()
+            actions[step] = action
+            logprobs[step] = logprob
+            o, r, d = env.step(action.numpy())
+            rewards[step] = torch.tensor(r)
+            next_obs, next_done = torch.tensor(o), torch.tensor(d)
+        with torch.no_grad():
+            nv = agent.get_value(next_obs).reshape(1, -1)
+            adv, ret = gae_torch(rewards, values, dones, nv, next_done)
+        b_obs, b_lp, b_act = obs.reshape(-1, 4), logprobs.reshape(-1), actions.reshape(-1)
+        b_adv, b_ret, b_val = adv.reshape(-1), ret.reshape(-1), values.reshape(-1)
+        b_inds = np.arange(B)
+        for _ in range(E):
+            np.random.shuffle(b_inds)
+            for start in range(0, B, M):
+                mb = b_inds[start:start + M]
+                _, newlp, ent, newv = agent.get_action_and_value(b_obs[mb], b_act[mb])
+                logratio = newlp - b_lp[mb]
+                ratio = logratio.exp()
+                mba = b_adv[mb]
+                mba = (mba - mba.mean()) / (mba.std() + 1e-8)
+                pg = torch.max(-mba * ratio, -mba * torch.clamp(ratio, 0.8, 1.2)).mean()
+                newv = newv.view(-1)
+                vu = (newv - b_ret[mb]) ** 2
+                vc = (b_val[mb] + torch.clamp(newv - b_val[mb], -0.2, 0.2) - b_ret[mb]) ** 2
+                loss = pg - 0.01 * ent.mean() + 0.5 * torch.max(vu, vc).mean() * 0.5
+                opt.zero_grad()
+                loss.backward()
+                nn.utils.clip_grad_norm_(agent.parameters(), 0.5)
+                opt.step()
+        return next_obs, next_done
+
+    next_obs, next_done = iteration(next_obs, next_done)  # warm-up
+    t0 = time.perf_counter()
+    for _ in range(iterations):
+        next_obs, next_done = iteration(next_obs, next_done)
+    dt = time.perf_counter() - t0
+    return {"sps": iterations * B / dt, "updates_per_sec": iterations * E * nmb / dt,
+            "seconds": dt, "iterations": iterations, "threads": threads}
+
+
 def time_cpu_baseline(iterations=2, threads=16, **kw) -> dict:
     """Time `iterations` CPU PPO iterations (after one untimed warm-up step of the network)."""
     torch.set_num_threads(threads)

@@ -61,6 +61,7 @@ def test_frames_kernels_match_oracle(dev, T, N, W, F, M, E, nmb, p_done):
     (9, 5, 3, 15, 1, 3, 0.5, 8),        # ragged sizes, odd W
     (24, 7, 4, 42, 1, 4, 0.0, 64),      # no resets
     (10, 3, 16, 10, 1, 3, 0.1, 12),     # W = 16 (the kernels' maximum)
+    (12, 6, 4, 24, 1, 4, 0.1, 516),     # E not a multiple of 512: a partial column pass
 ])
 def test_frames_scatter_relu_is_scatter_then_relu_backward(dev, T, N, W, M, E, nmb, p_done, Ed):
     """ocppo_frames_scatter_relu: gp = out <= 0 ? 0 : frames_scatter(...) bit for bit (same

@@ -503,3 +503,42 @@ def test_per_step_noise_is_the_reference_sampling_stream(dev, graphs):
         for t in range(a.num_steps):
             ref = torch.empty(a.local_num_envs, tr.A, device=dev).exponential_()
             assert torch.equal(got[it][t], ref), (it, t)
+
+
+_GEMM_CHILD = r"""
+import sys, torch
+sys.path.insert(0, {root!r})
+from oc_cleanrl_amd.args import Args, finalize
+from oc_cleanrl_amd.trainer import PPOTrainer
+a = finalize(Args(env_id="ALE/Pong-v5", obs_mode="obj", architecture="PPO_OBJ", num_envs=128,
+                  num_steps=128, num_features=12, save_model=False, total_timesteps=10_000_000), 1)
+tr = PPOTrainer(a, torch.device("cuda:0"), log=False)
+for _ in range(2):
+    tr.train_iteration()
+torch.cuda.synchronize()
+assert tr.gemm_table == {on}, tr.gemm_table
+torch.save(torch.cat([p.detach().flatten() for p in tr.agent.parameters()]).cpu(), {out!r})
+"""
+
+
+def test_gemm_table_is_deterministic_and_matches_default(tmp_path):
+    """The shipped hipBLASLt solution table (gemm_table.py, TunableOp read-only) under the default
+    torch_deterministic=True: two config-2 runs with the table are bitwise identical, and a run
+    with the default heuristic (OCPPO_GEMM_TABLE=0) agrees to f32 GEMM summation order. One child
+    process per run: TunableOp's state is process-wide."""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = str(Path(__file__).resolve().parent.parent)
+    outs = []
+    for i, on in enumerate((True, True, False)):
+        out = str(tmp_path / f"p{i}.pt")
+        env = dict(os.environ, OCPPO_GEMM_TABLE="1" if on else "0")
+        r = subprocess.run([sys.executable, "-c", _GEMM_CHILD.format(root=root, on=on, out=out)],
+                           env=env, capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs.append(torch.load(out, weights_only=True))
+    assert torch.equal(outs[0], outs[1]), "the table's picks are not run-to-run deterministic"
+    torch.testing.assert_close(outs[0], outs[2], rtol=1e-3, atol=2e-5)

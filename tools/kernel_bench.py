@@ -23,6 +23,7 @@ ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
 
 from oc_cleanrl_amd import ops  # noqa: E402
+from oc_cleanrl_amd.trainer import replay_time_us  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0
 MFMA_F32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense f32 MFMA (= the f32 vector rate)
@@ -330,31 +331,21 @@ def make_case(name: str, p: dict, dev):
     raise KeyError(name)
 
 
-def time_case(fn, reps=20, rounds=5) -> float:
-    fn()
-    torch.cuda.synchronize()
-    gr = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(gr):
-        for _ in range(reps):
-            fn()
-    gr.replay()
-    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    a.record()
-    for _ in range(rounds):
-        gr.replay()
-    b.record()
-    torch.cuda.synchronize()
-    return 1e3 * a.elapsed_time(b) / (reps * rounds)
+def time_case(fn, reps=20, rounds=5, cold=False) -> float:
+    """Mean launch duration (us): trainer.replay_time_us (cold = an L3 scrub before every
+    launch, subtracted)."""
+    return replay_time_us(fn, reps, rounds, cold=cold)
 
 
-def run_case(name, size, dev, reps=20, rounds=5) -> dict:
+def run_case(name, size, dev, reps=20, rounds=5, cold=False) -> dict:
     fn, nbytes = make_case(name, SIZES[name][size], dev)
     assert nbytes == case_bytes(name, SIZES[name][size]), name
-    us = time_case(fn, reps, rounds)
+    us = time_case(fn, reps, rounds, cold)
     launches = len(SIZES[name][size].get("shapes", (None,)))
     us, nbytes = us / launches, nbytes / launches  # per launch (average over the launch mix)
     gbs = nbytes / (us * 1e-6) / 1e9
-    r = {"kernel": name, "size": size, "params": SIZES[name][size], "mean_us": round(us, 3),
+    r = {"kernel": name, "size": size, "cache": "cold" if cold else "warm",
+         "params": SIZES[name][size], "mean_us": round(us, 3),
          "bytes": nbytes, "GBps": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
     if name in FLOPS:
         fl = FLOPS[name](SIZES[name][size])
@@ -369,13 +360,14 @@ def main():
     ap.add_argument("--size", default="all", choices=["all", "config", "scaled"])
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--cold", action="store_true", help="L3 scrub before every launch")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     names = list(SIZES) if a.kernel == "all" else [a.kernel]
     sizes = ["config", "scaled"] if a.size == "all" else [a.size]
     for n in names:
         for s in sizes:
-            print(json.dumps(run_case(n, s, dev, a.reps, a.rounds)), flush=True)
+            print(json.dumps(run_case(n, s, dev, a.reps, a.rounds, a.cold)), flush=True)
             torch.cuda.empty_cache()
 
 
