@@ -536,128 +536,155 @@ inline int wg_chunks(int64_t R, int64_t N) {
   return static_cast<int>(c < 1 ? 1 : c);
 }
 
-// Row-major form (round 2): a workgroup owns a range of rows x 256 columns (lane = 4 adjacent
-// columns, 16-B loads; the 4 waves take every 4th row), so every row of x is read once per
-// column group, by scalar loads (the row index is wave-uniform): x is no longer re-read by 8
-// column stripes. Each lane keeps 4 columns x (K + 1) running sums (fmaf, rows in order); the
-// waves are combined through LDS in wave order into ONE record per workgroup, and a second small
-// launch adds the records in workgroup order (16 outputs x 16 workgroup groups per block): no
-// ticket, no last-arriver tail, deterministic.
-#ifndef OCPPO_WR_ROWS  // experiments (tools/build_variant.py) move these
-#define OCPPO_WR_ROWS 64
-#endif
-#ifndef OCPPO_WR_WAVES
+// Row-major form: a workgroup owns a contiguous range of rows x 256 columns (lane = 4 adjacent
+// columns, 16-B loads; the waves take every kWrWaves-th row), so every row of x is read once per
+// column group, out of LDS (staged kWrStage rows at a time). Each lane keeps 4 columns x (K + 1)
+// running sums (fmaf, rows in order). Fixed grid (round 3): wr_layout picks about 128 row
+// ranges per column group, so the records -- ONE per workgroup, the waves combined through LDS
+// in wave order -- are O(grid), not O(R / 64); a second launch adds them with a fixed-shape tree
+// (relu_bias_wgrad_finish_kernel). Deterministic, no atomics.
+#ifndef OCPPO_WR_WAVES  // experiments (tools/build_variant.py) move these
 #define OCPPO_WR_WAVES 8
 #endif
-constexpr int kWrRowsPerWg = OCPPO_WR_ROWS;  // 8 rows per wave: 192 workgroups at R = 12288
+#ifndef OCPPO_WR_GRID
+#define OCPPO_WR_GRID 256
+#endif
 constexpr int kWrCols = 256;       // columns per workgroup (64 lanes x 4)
 constexpr int kWrWaves = OCPPO_WR_WAVES;  // 2 waves per SIMD: enough loads in flight per CU
 constexpr int kWrU = 8;            // rows in flight per wave
+constexpr int kWrStage = 128;      // rows of x staged in LDS at a time
+constexpr int kWrGrid = OCPPO_WR_GRID;  // row ranges per column group (at most)
+
+// rows per workgroup: a multiple of the wave count, >= 32
+inline int64_t wr_rows_per_wg(int64_t R) {
+  int64_t rpw = (R + kWrGrid - 1) / kWrGrid;
+  if (rpw < 32) rpw = 32;
+  return (rpw + kWrWaves - 1) / kWrWaves * kWrWaves;
+}
 
 template <bool RELU, int KP>
 __global__ __launch_bounds__(64 * kWrWaves) void relu_bias_wgrad_rows_kernel(
     const float* __restrict__ g, const float* __restrict__ out, const float* __restrict__ x,
-    int64_t ldx, int64_t R, int64_t N, int K, float* __restrict__ partials) {
+    int64_t ldx, int64_t R, int64_t N, int K, int64_t rows_per_wg, float* __restrict__ partials) {
   constexpr int NV = KP + 1;
-  extern __shared__ __attribute__((aligned(16))) float wr_red[];  // [waves][256][NV]
-  __shared__ float xs[kWrRowsPerWg][KP];                           // this chunk's rows of x
+  // per wave an image [NV][256 columns]: a lane's 4 columns of one value are one float4, so
+  // consecutive lanes store / load consecutive 16 B (no bank conflicts)
+  extern __shared__ __attribute__((aligned(16))) float wr_red[];  // [waves][NV][256]
+  __shared__ float xs[kWrStage][KP];                               // staged rows of x
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int cg = blockIdx.y;
   const int64_t c0 = static_cast<int64_t>(cg) * kWrCols + 4 * lane;
   const bool live = c0 < N;
-  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * kWrRowsPerWg;
-  const int64_t r1 = r0 + kWrRowsPerWg < R ? r0 + kWrRowsPerWg : R;
-  // x rows of the chunk -> LDS once (each row read once per column group)
-  for (int i = threadIdx.x; i < kWrRowsPerWg * KP; i += 64 * kWrWaves) {
-    const int rr = i / KP, k = i - rr * KP;
-    xs[rr][k] = (r0 + rr < r1 && k < K) ? x[(r0 + rr) * ldx + k] : 0.f;
-  }
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_wg;
+  const int64_t r1 = r0 + rows_per_wg < R ? r0 + rows_per_wg : R;
   float sb[4] = {0.f, 0.f, 0.f, 0.f};
   float sw[4][KP];
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
     for (int k = 0; k < KP; ++k) sw[j][k] = 0.f;
-  __syncthreads();
-  for (int64_t rb = r0 + wv; rb < r1; rb += kWrWaves * kWrU) {
-    float4 a[kWrU];
-#pragma unroll
-    for (int u = 0; u < kWrU; ++u) {
-      const int64_t r = rb + kWrWaves * u;
-      const bool ok = r < r1 && live;
-      a[u] = ok ? *reinterpret_cast<const float4*>(g + r * N + c0) : make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int64_t s0 = r0; s0 < r1; s0 += kWrStage) {  // block-uniform trip count
+    const int64_t s1 = s0 + kWrStage < r1 ? s0 + kWrStage : r1;
+    __syncthreads();  // the previous stage's rows are consumed
+    for (int i = threadIdx.x; i < kWrStage * KP; i += 64 * kWrWaves) {
+      const int rr = i / KP, k = i - rr * KP;
+      xs[rr][k] = (s0 + rr < s1 && k < K) ? x[(s0 + rr) * ldx + k] : 0.f;
     }
-    if (RELU) {
+    __syncthreads();
+    for (int64_t rb = s0 + wv; rb < s1; rb += kWrWaves * kWrU) {
+      float4 a[kWrU];
 #pragma unroll
       for (int u = 0; u < kWrU; ++u) {
         const int64_t r = rb + kWrWaves * u;
-        const float4 o = (r < r1 && live) ? *reinterpret_cast<const float4*>(out + r * N + c0)
-                                          : make_float4(0.f, 0.f, 0.f, 0.f);
-        a[u].x = o.x <= 0.f ? 0.f : a[u].x; a[u].y = o.y <= 0.f ? 0.f : a[u].y;
-        a[u].z = o.z <= 0.f ? 0.f : a[u].z; a[u].w = o.w <= 0.f ? 0.f : a[u].w;
+        const bool ok = r < s1 && live;
+        a[u] = ok ? *reinterpret_cast<const float4*>(g + r * N + c0)
+                  : make_float4(0.f, 0.f, 0.f, 0.f);
       }
-    }
+      if (RELU) {
 #pragma unroll
-    for (int u = 0; u < kWrU; ++u) {
-      const int64_t r = rb + kWrWaves * u;
-      if (r >= r1) break;  // wave-uniform; rows past the chunk carry zeros anyway
-      const float* xr = xs[r - r0];
-      const float av[4] = {a[u].x, a[u].y, a[u].z, a[u].w};
+        for (int u = 0; u < kWrU; ++u) {
+          const int64_t r = rb + kWrWaves * u;
+          const float4 o = (r < s1 && live) ? *reinterpret_cast<const float4*>(out + r * N + c0)
+                                            : make_float4(0.f, 0.f, 0.f, 0.f);
+          a[u].x = o.x <= 0.f ? 0.f : a[u].x; a[u].y = o.y <= 0.f ? 0.f : a[u].y;
+          a[u].z = o.z <= 0.f ? 0.f : a[u].z; a[u].w = o.w <= 0.f ? 0.f : a[u].w;
+        }
+      }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        sb[j] += av[j];
+      for (int u = 0; u < kWrU; ++u) {
+        const int64_t r = rb + kWrWaves * u;
+        if (r >= s1) break;  // wave-uniform; rows past the stage carry zeros anyway
+        const float* xr = xs[r - s0];
+        const float av[4] = {a[u].x, a[u].y, a[u].z, a[u].w};
 #pragma unroll
-        for (int k = 0; k < KP; ++k) sw[j][k] = fmaf(av[j], xr[k], sw[j][k]);
+        for (int j = 0; j < 4; ++j) {
+          sb[j] += av[j];
+#pragma unroll
+          for (int k = 0; k < KP; ++k) sw[j][k] = fmaf(av[j], xr[k], sw[j][k]);
+        }
       }
     }
   }
-  float* mine = wr_red + (static_cast<int64_t>(wv) * kWrCols + 4 * lane) * NV;
+  float4* mine = reinterpret_cast<float4*>(wr_red) + static_cast<int64_t>(wv) * NV * 64 + lane;
+  mine[0] = make_float4(sb[0], sb[1], sb[2], sb[3]);
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    mine[j * NV] = sb[j];
-#pragma unroll
-    for (int k = 0; k < KP; ++k) mine[j * NV + 1 + k] = sw[j][k];
-  }
+  for (int k = 0; k < KP; ++k) mine[(1 + k) * 64] = make_float4(sw[0][k], sw[1][k], sw[2][k], sw[3][k]);
   __syncthreads();
-  constexpr int nrec = kWrCols * NV;
-  float* rec = partials + (static_cast<int64_t>(blockIdx.x) * gridDim.y + cg) * nrec;
-  for (int i = threadIdx.x; i < nrec; i += 64 * kWrWaves) {
-    float t = wr_red[i];
+  // record [NV][256 columns] of this (row range, column group), waves added in order
+  constexpr int nrec4 = NV * 64;
+  const float4* img = reinterpret_cast<const float4*>(wr_red);
+  float4* rec = reinterpret_cast<float4*>(partials) +
+                (static_cast<int64_t>(blockIdx.x) * gridDim.y + cg) * nrec4;
+  for (int i = threadIdx.x; i < nrec4; i += 64 * kWrWaves) {
+    float4 t = img[i];
 #pragma unroll
-    for (int q = 1; q < kWrWaves; ++q) t += wr_red[q * nrec + i];
+    for (int q = 1; q < kWrWaves; ++q) {
+      const float4 b = img[q * nrec4 + i];
+      t.x += b.x; t.y += b.y; t.z += b.z; t.w += b.w;
+    }
     rec[i] = t;
   }
 }
 
-// Adds the workgroup records in order; output o = (column group, column, value).
-// 8 outputs x 32 workgroup groups per block: every thread's loads are one batch in flight.
+// Adds the G records of every column group with a fixed-shape tree: a block owns 32 record
+// entries x 8 record groups; group gi takes records gi, gi + 8, ... in batches of 32 loads in
+// flight, each batch summed pairwise, then the 8 group sums pairwise through LDS.
+// Output o = (column group, value v, column): v = 0 the bias gradient, 1..K the weight columns.
+constexpr int kWfOut = 32, kWfGroups = 8, kWfBatch = 32;
 __global__ __launch_bounds__(256) void relu_bias_wgrad_finish_kernel(
     const float* __restrict__ partials, int G, int64_t npw, int NV, int64_t N, int K,
     float* __restrict__ dw, float* __restrict__ db) {
-  __shared__ float red[32][9];
-  const int o = threadIdx.x & 7, gi = threadIdx.x >> 3;
-  const int64_t idx = static_cast<int64_t>(blockIdx.x) * 8 + o;
-  const int cpg = (G + 31) / 32;
-  const int g0 = gi * cpg, g1 = g0 + cpg < G ? g0 + cpg : G;
+  __shared__ float red[kWfGroups][kWfOut + 1];
+  const int o = threadIdx.x % kWfOut, gi = threadIdx.x / kWfOut;
+  const int64_t idx = static_cast<int64_t>(blockIdx.x) * kWfOut + o;
   float s = 0.f;
   if (idx < npw) {
-    for (int gg = g0; gg < g1; gg += 8) {
-      float v[8];
+    for (int g0 = gi; g0 < G; g0 += kWfGroups * kWfBatch) {
+      float v[kWfBatch];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = gg + u < g1 ? partials[(gg + u) * npw + idx] : 0.f;
+      for (int u = 0; u < kWfBatch; ++u) {
+        const int gg = g0 + u * kWfGroups;
+        v[u] = gg < G ? partials[static_cast<int64_t>(gg) * npw + idx] : 0.f;
+      }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) s += v[u];
+      for (int wdt = kWfBatch / 2; wdt >= 1; wdt /= 2)
+#pragma unroll
+        for (int u = 0; u < wdt; ++u) v[u] += v[u + wdt];
+      s += v[0];
     }
   }
   red[gi][o] = s;
   __syncthreads();
+  for (int wdt = kWfGroups / 2; wdt >= 1; wdt /= 2) {
+    if (gi < wdt) red[gi][o] += red[gi + wdt][o];
+    __syncthreads();
+  }
   if (gi != 0 || idx >= npw) return;
-  float t = red[0][o];
-  for (int q = 1; q < 32; ++q) t += red[q][o];
+  const float t = red[0][o];
   const int64_t per = static_cast<int64_t>(kWrCols) * NV;
   const int64_t cgi = idx / per, rem = idx - cgi * per;
-  const int64_t col = cgi * kWrCols + rem / NV;
-  const int v = static_cast<int>(rem % NV);
+  const int v = static_cast<int>(rem / kWrCols);
+  const int64_t col = cgi * kWrCols + (rem - static_cast<int64_t>(v) * kWrCols);
   if (col >= N) return;
   if (v == 0) db[col] = t;
   else if (v - 1 < K) dw[col * K + (v - 1)] = t;
@@ -667,22 +694,23 @@ template <bool RELU>
 static void launch_wgrad_rows(hipStream_t s, int K, const float* g, const float* out,
                               const float* x, int64_t ldx, float* dw, float* db, int64_t R,
                               int64_t N, float* partials) {
-  const int G = static_cast<int>((R + kWrRowsPerWg - 1) / kWrRowsPerWg);
+  const int64_t rpw = wr_rows_per_wg(R);
+  const int G = static_cast<int>((R + rpw - 1) / rpw);
   const int ncg = static_cast<int>((N + kWrCols - 1) / kWrCols);
   const dim3 grid(G, ncg), block(64 * kWrWaves);
   int KP = K <= 4 ? 4 : K <= 8 ? 8 : K <= 12 ? 12 : 16;
   const size_t lds = sizeof(float) * kWrWaves * kWrCols * (KP + 1);
-  if (KP == 4)
-    hipLaunchKernelGGL((relu_bias_wgrad_rows_kernel<RELU, 4>), grid, block, lds, s, g, out, x, ldx, R, N, K, partials);
-  else if (KP == 8)
-    hipLaunchKernelGGL((relu_bias_wgrad_rows_kernel<RELU, 8>), grid, block, lds, s, g, out, x, ldx, R, N, K, partials);
-  else if (KP == 12)
-    hipLaunchKernelGGL((relu_bias_wgrad_rows_kernel<RELU, 12>), grid, block, lds, s, g, out, x, ldx, R, N, K, partials);
-  else
-    hipLaunchKernelGGL((relu_bias_wgrad_rows_kernel<RELU, 16>), grid, block, lds, s, g, out, x, ldx, R, N, K, partials);
+#define OCPPO_WR(KP_)                                                                            \
+  hipLaunchKernelGGL((relu_bias_wgrad_rows_kernel<RELU, KP_>), grid, block, lds, s, g, out, x,   \
+                     ldx, R, N, K, rpw, partials)
+  if (KP == 4) OCPPO_WR(4);
+  else if (KP == 8) OCPPO_WR(8);
+  else if (KP == 12) OCPPO_WR(12);
+  else OCPPO_WR(16);
+#undef OCPPO_WR
   const int64_t npw = static_cast<int64_t>(ncg) * kWrCols * (KP + 1);
-  hipLaunchKernelGGL(relu_bias_wgrad_finish_kernel, dim3((npw + 7) / 8), dim3(256), 0, s,
-                     partials, G, npw, KP + 1, N, K, dw, db);
+  hipLaunchKernelGGL(relu_bias_wgrad_finish_kernel, dim3((npw + kWfOut - 1) / kWfOut), dim3(256),
+                     0, s, partials, G, npw, KP + 1, N, K, dw, db);
 }
 
 inline int wg_kp(int64_t K) { return K <= 4 ? 4 : K <= 8 ? 8 : K <= 12 ? 12 : 16; }
@@ -691,7 +719,8 @@ inline int wg_kp(int64_t K) { return K <= 4 ? 4 : K <= 8 ? 8 : K <= 12 ? 12 : 16
 
 extern "C" size_t ocppo_relu_bias_wgrad_workspace_bytes(int64_t R, int64_t N, int64_t K) {
   if (R < 1 || N < 1 || K < 1) return 256;
-  const int64_t G = (R + ocppo::kWrRowsPerWg - 1) / ocppo::kWrRowsPerWg;
+  const int64_t rpw = ocppo::wr_rows_per_wg(R);
+  const int64_t G = (R + rpw - 1) / rpw;
   const int64_t ncg = (N + ocppo::kWrCols - 1) / ocppo::kWrCols;
   return static_cast<size_t>(G * ncg * ocppo::kWrCols * (ocppo::wg_kp(K) + 1)) * sizeof(float);
 }

@@ -1602,16 +1602,16 @@ __global__ __launch_bounds__(256) void heads_loss_kernel(HeadsLossParams P) {
 #endif
 }
 
-// Adds the G workgroup records with a fixed-shape tree: a block owns 16 record entries (outputs)
-// x 16 record groups; group gi takes records gi, gi + 16, gi + 32, ... in batches of 16 loads in
-// flight, each batch summed pairwise (8 / 4 / 2 / 1), batch sums added in batch order, then the
-// 16 group sums pairwise through LDS. The same shape for every G: deterministic. The record ends
-// with the 6 loss partials at `ls` (a multiple of 16), so one block holds all of them and forms
-// the loss statistics (loss_finish's formulas).
+// Adds the G workgroup records with a fixed-shape tree: a block owns 32 record entries (outputs)
+// x 8 record groups; group gi takes records gi, gi + 8, gi + 16, ... in batches of 32 loads in
+// flight (one batch for G <= 256), each batch summed pairwise (16 / 8 / 4 / 2 / 1), batch sums
+// added in batch order, then the 8 group sums pairwise through LDS. The same shape for every G:
+// deterministic. The record holds the 6 loss partials at `ls` (a multiple of 32), so one block
+// holds all of them and forms the loss statistics (loss_finish's formulas).
 #ifndef OCPPO_HLFIN_OUT  // finish geometry (outputs x record groups per block); tools/ variants
 #define OCPPO_HLFIN_OUT 32
 #endif
-constexpr int kHlFinOut = OCPPO_HLFIN_OUT, kHlFinGroups = 256 / kHlFinOut, kHlFinBatch = 16;
+constexpr int kHlFinOut = OCPPO_HLFIN_OUT, kHlFinGroups = 256 / kHlFinOut, kHlFinBatch = 32;
 __global__ __launch_bounds__(256) void heads_loss_finish_kernel(
     const float* __restrict__ partials, int G, int64_t npw, int64_t ls, int64_t H, int A, int amax,
     int cpl, float* __restrict__ db_h, float* __restrict__ dwa, float* __restrict__ dwc,
