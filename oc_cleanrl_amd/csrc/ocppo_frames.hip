@@ -330,6 +330,85 @@ __global__ __launch_bounds__(256) void frames_scatter_relu_kernel(
   }
 }
 
+// Wide form for N1 <= 256 (PPObj's first encoder layer, 12 -> 256): a workgroup owns RW frames x
+// ALL N1 columns, so every frame is gathered once (not once per 64-column block) and the W^T
+// [F][N1] image is staged once per workgroup from contiguous reads of W. Thread = one float4
+// column group (q = tid % 64) x RW / 4 frames (r = tid / 64 + 4 i): a wave stores whole 1-KB
+// rows of h (one 256-column row per store instruction), and reads W^T as one float4 per f,
+// reused for all its frames. Same products in the same order as the narrow form (fmaf over f,
+// + b, ReLU): bit-identical outputs.
+#ifndef OCPPO_GW_ROWS  // experiments (tools/build_variant.py)
+#define OCPPO_GW_ROWS 16
+#endif
+constexpr int kGwRows = OCPPO_GW_ROWS;
+constexpr int kGwCols = 256;
+template <int DT, bool RELU>
+__global__ __launch_bounds__(256) void frames_gather_linear_wide_kernel(
+    const void* __restrict__ obs, int64_t N, int W, int F, const int32_t* __restrict__ uniq,
+    int64_t C, const float* __restrict__ w, const float* __restrict__ b, int N1,
+    float* __restrict__ x_out, float* __restrict__ h_out) {
+  __shared__ float4 wt4[kGlMaxF * kGwCols / 4];
+  __shared__ float4 bs4[kGwCols / 4];
+  __shared__ float xs[kGwRows][kGlMaxF];
+  float* wt = reinterpret_cast<float*>(wt4);
+  float* bs = reinterpret_cast<float*>(bs4);
+  const int tid = threadIdx.x;
+  const int64_t c0 = static_cast<int64_t>(blockIdx.x) * kGwRows;
+  for (int i = tid; i < kGwRows * F; i += 256) {  // the gather first: its loads go out early
+    const int r = i / F, f = i - r * F;
+    const int64_t c = c0 + r;
+    float v = 0.f;
+    if (c < C) {
+      const int32_t u = uniq[c];
+      if (u >= 0) {  // u < (T + W - 1) * N < 2^31 (checked on the host): 32-bit division
+        const int32_t n32 = static_cast<int32_t>(N), q = u / n32;
+        const int64_t sidx = q - (W - 1);
+        const int64_t n = u - q * n32;
+        const int64_t src = sidx >= 0 ? ((sidx * N + n) * W + (W - 1)) * F + f
+                                      : ((n * W) + (W - 1 + sidx)) * F + f;
+        v = Elem<DT>::load(static_cast<const typename Elem<DT>::T*>(obs), src);
+      }
+      x_out[c * F + f] = v;
+    }
+    xs[r][f] = v;
+  }
+  for (int i = tid; i < N1 * F; i += 256) {  // W [N1][F] read contiguously, stored transposed
+    const int n = i / F, f = i - n * F;
+    wt[f * kGwCols + n] = w[i];
+  }
+  if (tid < kGwCols) bs[tid] = (b && tid < N1) ? b[tid] : 0.f;
+  __syncthreads();
+  const int q = tid & 63, r0 = tid >> 6;
+  const int col = 4 * q;
+  if (col >= N1) return;
+  constexpr int RPT = kGwRows / 4;
+  float4 acc[RPT];
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) acc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int f = 0; f < kGlMaxF; ++f) {
+    if (f < F) {
+      const float4 wv = wt4[f * (kGwCols / 4) + q];
+#pragma unroll
+      for (int i = 0; i < RPT; ++i) {
+        const float xa = xs[r0 + 4 * i][f];
+        acc[i].x = fmaf(xa, wv.x, acc[i].x); acc[i].y = fmaf(xa, wv.y, acc[i].y);
+        acc[i].z = fmaf(xa, wv.z, acc[i].z); acc[i].w = fmaf(xa, wv.w, acc[i].w);
+      }
+    }
+  }
+  const float4 bv = bs4[q];
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
+    const int64_t c = c0 + r0 + 4 * i;
+    if (c >= C) break;
+    float4 a = acc[i];
+    a.x += bv.x; a.y += bv.y; a.z += bv.z; a.w += bv.w;
+    if (RELU) a = make_float4(fmaxf(a.x, 0.f), fmaxf(a.y, 0.f), fmaxf(a.z, 0.f), fmaxf(a.w, 0.f));
+    *reinterpret_cast<float4*>(h_out + c * N1 + col) = a;
+  }
+}
+
 static bool aligned16(const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; }
 
 }  // namespace ocppo
@@ -450,18 +529,25 @@ extern "C" int ocppo_frames_gather_linear(ocppo_stream_t stream, const void* obs
   OCPPO_REQUIRE(aligned16(h_out), "ocppo_frames_gather_linear: h_out must be 16-B aligned");
   clear_stale_error();
   hipStream_t s = as_stream(stream);
-  const int64_t g = (C + kGlRows - 1) / kGlRows;
+  const bool wide = N1 <= kGwCols;
+  const int64_t g = (C + (wide ? kGwRows : kGlRows) - 1) / (wide ? kGwRows : kGlRows);
   OCPPO_REQUIRE(g <= INT32_MAX, "ocppo_frames_gather_linear: too large");
-  const dim3 grid(static_cast<unsigned>(g), static_cast<unsigned>((N1 + kGlCols - 1) / kGlCols));
+  const dim3 grid(static_cast<unsigned>(g),
+                  wide ? 1u : static_cast<unsigned>((N1 + kGlCols - 1) / kGlCols));
   const dim3 block(256);
-#define OCPPO_GL(DT)                                                                              \
+#define OCPPO_GL_K(KERN, DT)                                                                      \
   do {                                                                                            \
     if (relu)                                                                                     \
-      hipLaunchKernelGGL((frames_gather_linear_kernel<DT, true>), grid, block, 0, s, obs, N,      \
-                         (int)W, (int)F, uniq, C, w, b, (int)N1, x_out, h_out);                   \
+      hipLaunchKernelGGL((KERN<DT, true>), grid, block, 0, s, obs, N, (int)W, (int)F, uniq, C, w, \
+                         b, (int)N1, x_out, h_out);                                               \
     else                                                                                          \
-      hipLaunchKernelGGL((frames_gather_linear_kernel<DT, false>), grid, block, 0, s, obs, N,     \
-                         (int)W, (int)F, uniq, C, w, b, (int)N1, x_out, h_out);                   \
+      hipLaunchKernelGGL((KERN<DT, false>), grid, block, 0, s, obs, N, (int)W, (int)F, uniq, C,   \
+                         w, b, (int)N1, x_out, h_out);                                            \
+  } while (0)
+#define OCPPO_GL(DT)                                                                              \
+  do {                                                                                            \
+    if (wide) OCPPO_GL_K(frames_gather_linear_wide_kernel, DT);                                   \
+    else OCPPO_GL_K(frames_gather_linear_kernel, DT);                                             \
   } while (0)
   switch (obs_dtype) {
     case OCPPO_F32: OCPPO_GL(OCPPO_F32); break;
@@ -470,5 +556,6 @@ extern "C" int ocppo_frames_gather_linear(ocppo_stream_t stream, const void* obs
     default: return fail(OCPPO_E_INVALID, "ocppo_frames_gather_linear: bad obs dtype %d", obs_dtype);
   }
 #undef OCPPO_GL
+#undef OCPPO_GL_K
   return check_launch("ocppo_frames_gather_linear");
 }

@@ -54,6 +54,10 @@ SIZES = {
     "heads_bwd": {"config": dict(M=4096, H=512, A=6), "scaled": dict(M=262144, H=512, A=6)},
     # policy heads forward + fused PPO loss + heads backward (both launches: rows, then records)
     "heads_loss": {"config": dict(M=4096, H=512, A=6), "scaled": dict(M=262144, H=512, A=6)},
+    # the dedup update's frame gather fused with the first encoder Linear+ReLU (F=12 -> 256) at
+    # the frame capacity of config 2 (11520 distinct frames of a [129, 128, 4, 12] bf16 rollout)
+    "frames_gather_linear": {"config": dict(T=128, N=128, W=4, F=12, C=11520, N1=256),
+                             "scaled": dict(T=128, N=2048, W=4, F=12, C=184320, N1=256)},
     # relu_bias_grad with its in-launch last-arriver bias-gradient tail (conv layers; the
     # Linear layers at config run the deferred form above, ops.relu_bias_grad_partial)
     "relu_bias_grad_tail": {"config": dict(shapes=((12288, 512), (12288, 1024), (12288, 512))),
@@ -118,6 +122,8 @@ def case_bytes(name: str, p: dict) -> float:
         # h in + gp out; records (action 8 + 4 x 4) in; [Wa; Wc] + biases in; head grads out
         M, H, A = p["M"], p["H"], p["A"]
         return M * H * 8 + M * 24 + 4 * (A + 1) * (H + 1) + 4 * ((A + 1) * (H + 1) + H) + 36
+    if name == "frames_gather_linear":  # frame id 4 + bf16 row in + f32 row out + f32 h out
+        return p["C"] * (4 + p["F"] * (2 + 4) + 4 * p["N1"])
     if name == "cache_linear":  # ring form: x + W in, the fresh row written into one slot
         M, K, E = p["M"], p["K"], p["E"]
         return 4 * (M * K + E * (K + 1)) + 4 * M * E + 4 * M
@@ -274,6 +280,16 @@ def make_case(name: str, p: dict, dev):
             dwc=dwc, dba=dba, dbc=dbc, stats=stats)
         # h in + gp out; records (action 8 + 4 x 4) in; [Wa; Wc] + biases in; head grads out
         return fn, M * H * 8 + M * 24 + 4 * (A + 1) * (H + 1) + 4 * ((A + 1) * (H + 1) + H) + 36
+    if name == "frames_gather_linear":
+        T, N, W, F, C, N1 = p["T"], p["N"], p["W"], p["F"], p["C"], p["N1"]
+        obs = torch.randint(0, 200, (T + 1, N, W, F), device=dev, generator=g).to(torch.bfloat16)
+        U = (T + W - 1) * N
+        uniq = torch.randperm(U, device=dev, generator=g)[:C].sort().values.to(torch.int32)
+        w = torch.randn(N1, F, device=dev, generator=g) * F ** -0.5
+        b = torch.randn(N1, device=dev, generator=g)
+        x, h = torch.empty(C, F, device=dev), torch.empty(C, N1, device=dev)
+        fn = lambda: ops.frames_gather_linear(obs, uniq, w, b, relu=True, x_out=x, h_out=h)  # noqa: E731
+        return fn, case_bytes(name, p)
     if name == "cache_linear":
         M, K, E, W = p["M"], p["K"], p["E"], p["W"]
         x = torch.relu(torch.randn(M, K, device=dev, generator=g))
