@@ -94,10 +94,10 @@ OCPPO_API int ocppo_minibatch_adv_stats(ocppo_stream_t stream, const float* b_ad
 /* Minibatch prepare: the statistics above AND the per-sample records of every minibatch gathered
  * into minibatch order, mb_*[k*M + i] = b_*[perm[k*M + i]] (SoA), so that each
  * ocppo_ppo_loss_fwd_bwd launch can take the already-gathered arrays (mb_inds = NULL) instead of
- * five scattered loads per element (ppo_atari_oc.py:569-593 index b_* by mb_inds). Two launches:
- * the gather over all num_mb*M elements on a chip-filling grid, then the statistics over the
- * gathered advantages (one workgroup per minibatch; the same figures as
- * ocppo_minibatch_adv_stats). adv_stats : [num_mb, 2] or NULL (statistics skipped). */
+ * five scattered loads per element (ppo_atari_oc.py:569-593 index b_* by mb_inds). One launch:
+ * gather blocks over all num_mb*M elements on a chip-filling grid beside one statistics block
+ * per minibatch (bitwise the figures of ocppo_minibatch_adv_stats).
+ * adv_stats : [num_mb, 2] or NULL (statistics skipped). */
 OCPPO_API int ocppo_minibatch_prepare(ocppo_stream_t stream, const int64_t* perm, int64_t M,
                                       int64_t num_mb, const int64_t* b_actions,
                                       const float* b_logprobs, const float* b_advantages,

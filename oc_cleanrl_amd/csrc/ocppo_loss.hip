@@ -114,16 +114,19 @@ __device__ __forceinline__ void categorical_backward_loss(const float (&ln)[AMAX
 }
 
 // ---- minibatch advantage statistics ------------------------------------------------------------
-// grid = num_mb, one 1024-thread workgroup per minibatch. Each thread first issues all of its
-// index loads, then all of its gathered loads (VPT in flight instead of a dependent chain), keeps
-// the values in registers, and runs the two passes (mean, then squared deviations) from there.
-constexpr int kStatsThreads = 1024;
+// One 256-thread block per minibatch. Each thread first issues all of its index loads, then all
+// of its gathered loads (VPT in flight instead of a dependent chain), keeps the values in
+// registers, and runs the two passes (mean, then squared deviations) from there -- torch's
+// mean() / std() (unbiased) of ppo_atari_oc.py:579 in f32. The same block body serves
+// ocppo_minibatch_adv_stats and the statistics blocks of ocppo_minibatch_prepare, so the two
+// give bitwise-identical figures.
+constexpr int kStatsThreads = 256;
 template <int VPT>
-__global__ __launch_bounds__(kStatsThreads) void adv_stats_kernel(const float* __restrict__ adv,
-                                                                  const int64_t* __restrict__ perm,
-                                                                  int64_t M, float* __restrict__ out) {
-  __shared__ float scratch[kStatsThreads / kWave];
-  const int64_t base = static_cast<int64_t>(blockIdx.x) * M;
+__device__ __forceinline__ void adv_stats_block(const float* __restrict__ adv,
+                                                const int64_t* __restrict__ perm, int64_t M,
+                                                int64_t mb, float* __restrict__ out,
+                                                float* scratch) {
+  const int64_t base = mb * M;
   int64_t idx[VPT];
   float x[VPT];
 #pragma unroll
@@ -147,24 +150,93 @@ __global__ __launch_bounds__(kStatsThreads) void adv_stats_kernel(const float* _
     }
   q = block_sum(q, scratch);
   if (threadIdx.x == 0) {
-    out[2 * blockIdx.x + 0] = mean;
-    out[2 * blockIdx.x + 1] = sqrtf(q / static_cast<float>(M - 1));  // unbiased, torch.std()
+    out[2 * mb + 0] = mean;
+    out[2 * mb + 1] = sqrtf(q / static_cast<float>(M - 1));  // unbiased, torch.std()
   }
 }
 
-// Minibatch prepare, part 1: the per-sample records of every minibatch gathered into minibatch
-// order (SoA), so that each loss launch reads contiguous arrays (no index, no scattered 4-8 B
-// loads). The permutation of all minibatches is one flat index space, so this is a plain
-// elementwise gather over num_mb * M elements on a grid that fills the chip (VPT elements per
-// thread, all index loads, then all gathers, then all stores in flight). Part 2 is
-// adv_stats_kernel over the gathered (now contiguous) advantages, one workgroup per minibatch.
+// Any M: strided loops, values re-gathered for the second pass.
+__device__ __forceinline__ void adv_stats_block_any(const float* __restrict__ adv,
+                                                    const int64_t* __restrict__ perm, int64_t M,
+                                                    int64_t mb, float* __restrict__ out,
+                                                    float* scratch) {
+  const int64_t base = mb * M;
+  float s = 0.f;
+  for (int64_t i = threadIdx.x; i < M; i += kStatsThreads) s += adv[perm ? perm[base + i] : base + i];
+  s = block_sum(s, scratch);
+  const float mean = s / static_cast<float>(M);
+  float q = 0.f;
+  for (int64_t i = threadIdx.x; i < M; i += kStatsThreads) {
+    const float d = adv[perm ? perm[base + i] : base + i] - mean;
+    q += d * d;
+  }
+  q = block_sum(q, scratch);
+  if (threadIdx.x == 0) {
+    out[2 * mb + 0] = mean;
+    out[2 * mb + 1] = sqrtf(q / static_cast<float>(M - 1));
+  }
+}
+
+// VPT = 0: the strided form
 template <int VPT>
-__global__ __launch_bounds__(256) void minibatch_gather_kernel(
-    const int64_t* __restrict__ perm, int64_t n, const int64_t* __restrict__ b_act,
-    const float* __restrict__ b_lp, const float* __restrict__ b_adv, const float* __restrict__ b_ret,
+__device__ __forceinline__ void adv_stats_any_vpt(const float* adv, const int64_t* perm,
+                                                  int64_t M, int64_t mb, float* out,
+                                                  float* scratch) {
+  if constexpr (VPT == 0)
+    adv_stats_block_any(adv, perm, M, mb, out, scratch);
+  else
+    adv_stats_block<VPT>(adv, perm, M, mb, out, scratch);
+}
+
+inline int adv_stats_vpt(int64_t M) {
+  return M <= kStatsThreads ? 1 : M <= 4 * kStatsThreads ? 4 : M <= 16 * kStatsThreads ? 16
+       : M <= 64 * kStatsThreads ? 64 : 0;
+}
+
+template <int VPT>
+__global__ __launch_bounds__(kStatsThreads) void adv_stats_kernel(const float* __restrict__ adv,
+                                                                  const int64_t* __restrict__ perm,
+                                                                  int64_t M, float* __restrict__ out) {
+  __shared__ float scratch[kStatsThreads / kWave];
+  adv_stats_any_vpt<VPT>(adv, perm, M, blockIdx.x, out, scratch);
+}
+
+static void launch_adv_stats(hipStream_t s, const float* adv, const int64_t* perm, int64_t M,
+                             int64_t num_mb, float* out) {
+  const dim3 grid(static_cast<unsigned>(num_mb)), block(kStatsThreads);
+  switch (adv_stats_vpt(M)) {
+    case 1: hipLaunchKernelGGL(adv_stats_kernel<1>, grid, block, 0, s, adv, perm, M, out); break;
+    case 4: hipLaunchKernelGGL(adv_stats_kernel<4>, grid, block, 0, s, adv, perm, M, out); break;
+    case 16: hipLaunchKernelGGL(adv_stats_kernel<16>, grid, block, 0, s, adv, perm, M, out); break;
+    case 64: hipLaunchKernelGGL(adv_stats_kernel<64>, grid, block, 0, s, adv, perm, M, out); break;
+    default: hipLaunchKernelGGL(adv_stats_kernel<0>, grid, block, 0, s, adv, perm, M, out); break;
+  }
+}
+
+// Minibatch prepare: the per-sample records of every minibatch gathered into minibatch order
+// (SoA), so that each loss launch reads contiguous arrays (no index, no scattered 4-8 B loads),
+// AND each minibatch's advantage statistics, in ONE launch: num_mb statistics blocks, each running
+// adv_stats_block for one minibatch (its own gathers of b_adv through perm: the figures of
+// ocppo_minibatch_adv_stats, bit for bit), then gather_blocks blocks running a plain elementwise
+// gather over the flat num_mb * M index space (VPT elements per thread, all index loads, then
+// all gathers, then all stores in flight).
+template <int VPT, int SVPT>
+__global__ __launch_bounds__(256) void minibatch_prepare_kernel(
+    const int64_t* __restrict__ perm, int64_t n, int gather_blocks, int64_t M,
+    const int64_t* __restrict__ b_act, const float* __restrict__ b_lp,
+    const float* __restrict__ b_adv, const float* __restrict__ b_ret,
     const float* __restrict__ b_val, int64_t* __restrict__ mb_act, float* __restrict__ mb_lp,
-    float* __restrict__ mb_adv, float* __restrict__ mb_ret, float* __restrict__ mb_val) {
-  const int64_t base = static_cast<int64_t>(blockIdx.x) * 256 * VPT + threadIdx.x;
+    float* __restrict__ mb_adv, float* __restrict__ mb_ret, float* __restrict__ mb_val,
+    float* __restrict__ stats) {
+  // the statistics blocks come first (they gather a whole minibatch each: started early, they
+  // overlap the elementwise gather blocks behind them)
+  const int nstat = stats ? static_cast<int>(gridDim.x) - gather_blocks : 0;
+  if (static_cast<int>(blockIdx.x) < nstat) {  // statistics block of minibatch blockIdx.x
+    __shared__ float scratch[kStatsThreads / kWave];
+    adv_stats_any_vpt<SVPT>(b_adv, perm, M, blockIdx.x, stats, scratch);
+    return;
+  }
+  const int64_t base = static_cast<int64_t>(blockIdx.x - nstat) * 256 * VPT + threadIdx.x;
   int64_t idx[VPT];
 #pragma unroll
   for (int k = 0; k < VPT; ++k) {
@@ -193,41 +265,6 @@ __global__ __launch_bounds__(256) void minibatch_gather_kernel(
       mb_val[i] = vl[k];
     }
   }
-}
-
-// Any M: strided loops, values re-gathered for the second pass.
-__global__ __launch_bounds__(kStatsThreads) void adv_stats_kernel_any(
-    const float* __restrict__ adv, const int64_t* __restrict__ perm, int64_t M,
-    float* __restrict__ out) {
-  __shared__ float scratch[kStatsThreads / kWave];
-  const int64_t base = static_cast<int64_t>(blockIdx.x) * M;
-  float s = 0.f;
-  for (int64_t i = threadIdx.x; i < M; i += kStatsThreads) s += adv[perm ? perm[base + i] : base + i];
-  s = block_sum(s, scratch);
-  const float mean = s / static_cast<float>(M);
-  float q = 0.f;
-  for (int64_t i = threadIdx.x; i < M; i += kStatsThreads) {
-    const float d = adv[perm ? perm[base + i] : base + i] - mean;
-    q += d * d;
-  }
-  q = block_sum(q, scratch);
-  if (threadIdx.x == 0) {
-    out[2 * blockIdx.x + 0] = mean;
-    out[2 * blockIdx.x + 1] = sqrtf(q / static_cast<float>(M - 1));
-  }
-}
-
-static void launch_adv_stats(hipStream_t s, const float* adv, const int64_t* perm, int64_t M,
-                             int64_t num_mb, float* out) {
-  const dim3 grid(static_cast<unsigned>(num_mb)), block(kStatsThreads);
-  if (M <= 1 * kStatsThreads)
-    hipLaunchKernelGGL(adv_stats_kernel<1>, grid, block, 0, s, adv, perm, M, out);
-  else if (M <= 4 * kStatsThreads)
-    hipLaunchKernelGGL(adv_stats_kernel<4>, grid, block, 0, s, adv, perm, M, out);
-  else if (M <= 16 * kStatsThreads)
-    hipLaunchKernelGGL(adv_stats_kernel<16>, grid, block, 0, s, adv, perm, M, out);
-  else
-    hipLaunchKernelGGL(adv_stats_kernel_any, grid, block, 0, s, adv, perm, M, out);
 }
 
 // ---- fused loss ----------------------------------------------------------------------------------
@@ -1128,15 +1165,22 @@ extern "C" int ocppo_minibatch_prepare(ocppo_stream_t stream, const int64_t* per
   hipStream_t s = as_stream(stream);
   constexpr int VPT = 2;
   const int64_t n = M * num_mb;
-  hipLaunchKernelGGL(minibatch_gather_kernel<VPT>, dim3(static_cast<unsigned>(ceil_div(n, 256 * VPT))),
-                     dim3(256), 0, s, perm, n, b_actions, b_logprobs, b_advantages, b_returns,
-                     b_values, mb_actions, mb_logprobs, mb_advantages, mb_returns, mb_values);
-  if (int rc = check_launch("ocppo_minibatch_prepare")) return rc;
-  if (!adv_stats) return OCPPO_OK;
-  // mean / unbiased std of each minibatch's (contiguous) advantages: the reduction order of
-  // ocppo_minibatch_adv_stats over the same values, so the figures are identical
-  launch_adv_stats(s, mb_advantages, nullptr, M, num_mb, adv_stats);
-  return check_launch("ocppo_minibatch_prepare/stats");
+  const int64_t gb = ceil_div(n, 256 * VPT);
+  OCPPO_REQUIRE(gb + num_mb <= INT32_MAX, "ocppo_minibatch_prepare: too large");
+  const dim3 grid(static_cast<unsigned>(gb + (adv_stats ? num_mb : 0))), block(256);
+#define OCPPO_PREP(SV)                                                                           \
+  hipLaunchKernelGGL((minibatch_prepare_kernel<VPT, SV>), grid, block, 0, s, perm, n, (int)gb, M, \
+                     b_actions, b_logprobs, b_advantages, b_returns, b_values, mb_actions,       \
+                     mb_logprobs, mb_advantages, mb_returns, mb_values, adv_stats)
+  switch (adv_stats_vpt(M)) {
+    case 1: OCPPO_PREP(1); break;
+    case 4: OCPPO_PREP(4); break;
+    case 16: OCPPO_PREP(16); break;
+    case 64: OCPPO_PREP(64); break;
+    default: OCPPO_PREP(0); break;
+  }
+#undef OCPPO_PREP
+  return check_launch("ocppo_minibatch_prepare");
 }
 
 namespace ocppo {

@@ -2,7 +2,8 @@
 replay, which crash. Each variant runs in its own child process (a crash ends only that child).
 
     python tools/exp_c3_capture.py            # all variants
-    python tools/exp_c3_capture.py child ENVS DET CL   # one variant (used by the parent)
+    python tools/exp_c3_capture.py only ENVS DET CL TIMED   # one variant, in a child process
+    python tools/exp_c3_capture.py child ENVS DET CL TIMED  # (used by the parent)
 """
 import json
 import subprocess
@@ -14,7 +15,7 @@ ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
 
 
-def child(envs: int, det: int, cl: int):
+def child(envs: int, det: int, cl: int, timed: int = 3):
     import torch
 
     from oc_cleanrl_amd.args import Args, finalize
@@ -33,21 +34,24 @@ def child(envs: int, det: int, cl: int):
     torch.cuda.synchronize()
     print("captured:", tr.graphs_ready, len(tr.g_update), flush=True)
     t0 = time.perf_counter()
-    for _ in range(3):
+    for _ in range(timed):
         tr.train_iteration()
     torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / 3
+    dt = (time.perf_counter() - t0) / timed
     print(json.dumps({"envs": envs, "det": det, "cl": cl, "ms_per_iter": round(1e3 * dt, 2),
                       "sps": round(envs * 128 / dt, 1)}), flush=True)
 
 
 def main():
     if len(sys.argv) > 1 and sys.argv[1] == "child":
-        child(*map(int, sys.argv[2:5]))
+        child(*map(int, sys.argv[2:6]))
         return
-    for envs, det, cl in ((16, 0, 1), (16, 1, 1), (16, 0, 0), (256, 0, 1)):
-        r = subprocess.run([sys.executable, __file__, "child", str(envs), str(det), str(cl)],
-                           capture_output=True, text=True, timeout=400)
+    variants = ((16, 0, 1, 3), (16, 1, 1, 3), (16, 0, 0, 3), (256, 0, 1, 3))
+    if len(sys.argv) > 1 and sys.argv[1] == "only":  # e.g. `only 256 1 1 1` (envs det cl timed)
+        variants = (tuple(map(int, sys.argv[2:6])),)
+    for envs, det, cl, timed in variants:
+        r = subprocess.run([sys.executable, __file__, "child", str(envs), str(det), str(cl),
+                            str(timed)], capture_output=True, text=True, timeout=560)
         print(f"--- envs={envs} det={det} cl={cl}: rc={r.returncode}")
         print(r.stdout[-1500:])
         print(r.stderr[-2500:])

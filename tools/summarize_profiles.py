@@ -33,7 +33,7 @@ KERNEL_SUBSTR = {
     "relu_bias_wgrad": ("relu_bias_wgrad_rows_kernel", "relu_bias_wgrad_finish_kernel"),
     "heads_bwd": ("heads_bwd_kernel",),
     "heads_loss": ("heads_loss_kernel", "heads_loss_finish_kernel"),
-    "mb_prepare": ("minibatch_gather_kernel", "adv_stats_kernel"),
+    "mb_prepare": ("minibatch_prepare_kernel",),
     "cache_linear": ("linear_rows_kernel",),
     "store_encode": ("store_linear2_kernel",),
     "decoder": ("linear_rows_kernel",),
