@@ -285,16 +285,21 @@ __global__ __launch_bounds__(64 * S) void linear_rows_kernel(
   }
 }
 
+#ifndef OCPPO_LIN_STAGE_CH  // chunks of 16 k per staged group (experiments: tools/)
+#define OCPPO_LIN_STAGE_CH 2
+#endif
+constexpr int kLinStageCH = OCPPO_LIN_STAGE_CH;
+
 template <int S, int CH, bool RELU, bool CACHE>
 static void launch_linear_sc(hipStream_t s, bool vec, const float* x, int64_t ldx, const float* w,
                              const float* b, float* y, int64_t ldy, int M, int N, int K,
                              CacheOut c, XRing ring) {
   const int ntm = (M + 15) / 16, ntn = (N + 15) / 16, tiles = ntm * ntn;
   const dim3 grid(8 * ((tiles + 7) / 8)), block(64 * S);
-  if (vec && K % 16 == 0)  // full-line staged, pipelined in groups of 2 chunks (32 k values)
-    hipLaunchKernelGGL((linear_rows_kernel<S, 2, RELU, true, CACHE, true>), grid, block,
-                       sizeof(LinStage<2>) * S, s, x, ldx, w, b, y, ldy, M, N, K, ntm, tiles, c,
-                       ring);
+  if (vec && K % 16 == 0)  // full-line staged, pipelined in groups of kLinStageCH chunks
+    hipLaunchKernelGGL((linear_rows_kernel<S, kLinStageCH, RELU, true, CACHE, true>), grid, block,
+                       sizeof(LinStage<kLinStageCH>) * S, s, x, ldx, w, b, y, ldy, M, N, K, ntm,
+                       tiles, c, ring);
   else if (vec)
     hipLaunchKernelGGL((linear_rows_kernel<S, CH, RELU, true, CACHE>), grid, block, 0, s, x, ldx,
                        w, b, y, ldy, M, N, K, ntm, tiles, c);
