@@ -359,7 +359,9 @@ def run_case(name, size, dev, reps=20, rounds=5, cold=False) -> dict:
     us = time_case(fn, reps, rounds, cold)
     launches = len(SIZES[name][size].get("shapes", (None,)))
     us, nbytes = us / launches, nbytes / launches  # per launch (average over the launch mix)
-    gbs = nbytes / (us * 1e-6) / 1e9
+    # (a cold figure is a difference of two timings: under a profiler with one round it can
+    # come out <= 0; only the profile's counters matter there)
+    gbs = nbytes / (us * 1e-6) / 1e9 if us > 0 else float("nan")
     r = {"kernel": name, "size": size, "cache": "cold" if cold else "warm",
          "params": SIZES[name][size], "mean_us": round(us, 3),
          "bytes": nbytes, "GBps": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
