@@ -415,6 +415,13 @@ def main():
                            "steps/s; a few seconds of search in the warm-up)"}
                           if opt.config == 3 else {}),
                        "conv_benchmark": args.conv_benchmark,
+                       "sampling_noise": ("per step: one Exp(1) draw of [N, A] per rollout step "
+                                          "(the reference's Categorical.sample stream)"
+                                          if args.per_step_noise else
+                                          "per rollout: one Exp(1) draw of [T, N, A] (the "
+                                          "reference's stream is --set per_step_noise=1: "
+                                          "770.7k vs 779.9k env steps/s, -1.2 %, "
+                                          "profiles/r03/noise_ab.json)"),
                        "parallelism": f"dp{world}"},
             "updates_per_sec": round(updates / dt, 2),
             "roofline": roofline,
