@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define OCPPO_ABI_VERSION 16
+#define OCPPO_ABI_VERSION 17
 
 /* status codes */
 #define OCPPO_OK 0
@@ -287,6 +287,34 @@ OCPPO_API int ocppo_bias_act(ocppo_stream_t stream, float* y, const float* b, in
  * y [B, P, C] NHWC f32 (P = H*W), out [B, C, P] f32 (not aliasing y), P * (C + 1) <= 12288. */
 OCPPO_API int ocppo_bias_act_nchw(ocppo_stream_t stream, const float* y, const float* b, int64_t B,
                                   int64_t P, int64_t C, int relu, float* out);
+
+/* ---------------------------------------------------------------------------------------------
+ * Update-phase f32 GEMM on the bf16 matrix cores — replaces the f32 GEMMs (addmm /
+ * _addmm_activation forward, g'W dX, split-K g'^T x dW) of the Linear layers that
+ * `agent.get_action_and_value(b_obs[mb])` and `loss.backward()` run (ppo_atari_oc.py:566-606
+ * through architectures/ppo.py:60-84):
+ *   C_s[m, n] = act( sum_{k in K_s} A(m, k) B(n, k) + bias[n] )     s = 0 .. splits-1
+ *   A(m, k) = a[m*sam + k*sak], B(n, k) = b[n*sbn + k*sbk], C_s[m, n] = c[s*split_c + m*ldc + n]
+ *   K_s = steps [s*nk/splits, (s+1)*nk/splits) of the nk = K/32 steps of 32 (even partition)
+ * Each f32 operand is split exactly into three bf16 pieces (x = x0 + x1 + x2) and the six piece
+ * products down to 2^-24 of |a b| are accumulated in f32 (leading and small terms in separate
+ * accumulators): f32-level accuracy (tests/test_gemm_gpu.py: error vs f64 at or below
+ * hipBLASLt's f32 GEMM) at 6 bf16 MFMAs per f32 multiply-add.
+ * One of (sam, sak) and one of (sbn, sbk) must be 1 (the other a multiple of 4, >= the extent it
+ * strides over); a, b 16-B aligned; K % 32 == 0, K / 32 >= splits; M, N multiples of the tile (tile 0: 128 x 128,
+ * 1: 64 x 128, 2: 128 x 64, 3: 64 x 64 rows x columns); bias (NULL: none) and relu only with
+ * splits == 1. Mask epilogue (mask != NULL; the dX product of the layer above a Linear+ReLU,
+ * whose input `mask` [M, N] (row stride ldm) is that ReLU's output): C = mask > 0 ? acc : 0
+ * (threshold_backward) and dbp[tm, n] = sum of C over row tile tm (tile rows each) — that layer's
+ * bias-gradient partials, [M / tile rows, N], for ocppo_sum_splits_db; splits == 1, no bias/relu.
+ * tile: bits 0-1 the tile above, bit 2 loads two K steps ahead, bit 3 one accumulator for all six
+ * products. Deterministic (fixed MFMA order, no atomics).
+ * ------------------------------------------------------------------------------------------- */
+OCPPO_API int ocppo_gemm_x6(ocppo_stream_t stream, const float* a, int64_t sam, int64_t sak,
+                            const float* b, int64_t sbn, int64_t sbk, float* c, int64_t ldc,
+                            int64_t M, int64_t N, int64_t K, int64_t splits, int64_t split_c,
+                            const float* bias, int relu, const float* mask, int64_t ldm,
+                            float* dbp, int tile);
 
 /* ---------------------------------------------------------------------------------------------
  * Split-K combine of a weight gradient — replaces ATen's `sum(0)` after the batched (split-K)

@@ -68,6 +68,59 @@ def _splitk(rows: int, k: int, n: int) -> int:
     return max(s, 1)
 
 
+# The update's f32 GEMMs on the bf16 matrix cores (ops.gemm_x6: each f32 operand split exactly
+# into three bf16 pieces, six piece products accumulated in f32 -- f32 accuracy at 6/16 of the f32
+# MFMA's time, tests/test_gemm_gpu.py); shapes it does not tile stay on hipBLASLt.
+X6_GEMM = True
+# Where it wins (tools/exp_gemm_x6.py at the config-2 update shapes): products whose output holds
+# >= 256 tiles of 128 x 128 (forward / dX), and weight gradients with >= 32 such tiles (the rows
+# split over up to 16 workgroups per tile); smaller outputs leave the chip half idle and stay on
+# hipBLASLt (e.g. the decoder forward [4096 x 512] from K = 2048: 84 vs 63 us).
+X6_MIN_TILES, X6_MIN_TILES_DW = 256, 32
+
+
+def _x6(M: int, N: int, K: int) -> bool:
+    """Forward / dX product [M, N] = [M, K] x [K, N] on gemm_x6."""
+    return X6_GEMM and M * N >= X6_MIN_TILES * 16384 and K >= 64
+
+
+def _x6_dw(n: int, k: int, rows: int) -> bool:
+    """Weight gradient [n, k] = g^T x over `rows` on gemm_x6."""
+    return X6_GEMM and n * k >= X6_MIN_TILES_DW * 16384 and rows >= 1024
+
+
+def _x6_splits(rows: int, n: int, k: int):
+    """(splits, variant) of dW = g^T x on gemm_x6 (rows in steps of 32, split evenly): the
+    largest tile that reaches >= 512 workgroups (two per CU) over the [n, k] output with at most
+    16 splits, at the fewest splits; else the most workgroups. The combine is sum_splits[_db]."""
+    if rows % 32:
+        return None
+    best, best_units = None, -1
+    for t in range(ops.X6_AUTO, ops.X6_AUTO + 4):
+        bm, bn = ops.X6_TILES[t]
+        if n % bm or k % bn:
+            continue
+        for s in (1, 2, 4, 8, 16):
+            if s > rows // 32:
+                break
+            units = s * (n // bm) * (k // bn)
+            if units >= 512:
+                return s, t
+            if units > best_units:
+                best, best_units = (s, t), units
+    return best
+
+
+# The ReLU backward + bias-gradient partials of a Linear+ReLU layer fused into the next layer's
+# dX GEMM (ops.dx_x6_relu): replaces that layer's relu_bias_grad pass.
+X6_MASK_DX = True
+
+
+def _x6_dx_shape_ok(M: int, N: int, K: int) -> bool:
+    """dX [M, K] = g [M, N] W [N, K] runs on gemm_x6 (agents._dx's rule, decided from shapes)."""
+    return _x6(M, K, N) and N % 32 == 0 and ops.x6_tile(M, K) is not None
+
+
 def _weight_grad(g, x, out=None, db=None):
     """dW = g^T x (g [rows, n], x [rows, k]) with the split-K rule; written into `out` if given.
     db = (partials of ops.relu_bias_grad_partial, bias grad): the bias gradient is finished in
@@ -75,9 +128,17 @@ def _weight_grad(g, x, out=None, db=None):
     rows, n = g.shape
     k = x.shape[1]
     s = _splitk(rows, k, n)
-    if s == 1:
+    st = _x6_splits(rows, n, k) if _x6_dw(n, k, rows) else None
+    if st is not None and ops.dw_x6_ok(g, x, st[0]):
+        s6, t6 = st
+        if s6 == 1 and out is not None and db is None and out.is_contiguous():
+            return ops.gemm_x6(g, 1, g.stride(0), x, 1, x.stride(0), out, k, n, k, rows, tile=t6)
+        s = s6
+        part = ops.dw_x6_parts(g, x, s, tile=t6)
+    elif s == 1:
         return torch.mm(g.t(), x, out=out) if out is not None else g.t().mm(x)
-    part = torch.bmm(g.view(s, rows // s, n).transpose(1, 2), x.view(s, rows // s, k))
+    else:
+        part = torch.bmm(g.view(s, rows // s, n).transpose(1, 2), x.view(s, rows // s, k))
     if db is not None:
         return ops.timed(f"sum_splits_db_{s}x{n}x{k}", lambda: ops.sum_splits_db(part, out, *db))
     if out is not None and HIP_SUM_SPLITS and ops.sum_splits_ok(part, out):
@@ -94,6 +155,8 @@ HIP_SMALL_DX = True
 def _dx(g, w):
     M, N = g.shape
     K = w.shape[1]
+    if _x6(M, K, N) and ops.dx_x6_ok(g, w):
+        return ops.dx_x6(g, w)
     if (HIP_SMALL_DX and g.is_cuda and M <= 256 and K <= 256 and N >= 256 and N % 16 == 0 and
             g.dtype == torch.float32 and g.is_contiguous()):
         return ops.linear_act(g, w.t().contiguous())
@@ -147,12 +210,22 @@ class _LinearAct(torch.autograd.Function):
     for FlatAdam-owned parameters dW/db are written straight into the flat grad buffer."""
 
     @staticmethod
-    def forward(ctx, x, w, b, relu: bool, box=None, chw=None):
+    def forward(ctx, x, w, b, relu: bool, box=None, chw=None, below=None):
         # chw = (C, H, W): x is a channels_last activation flattened in its memory (H, W, C)
         # order, so the weight's columns are permuted to match instead (linear_act_nhwc)
         wm = _cols_to_nhwc(w, chw) if chw is not None else w
-        out = torch._addmm_activation(b, x, wm.t(), use_gelu=False) if relu else \
-            torch.addmm(b, x, wm.t())
+        # below = the box of the Linear+ReLU that produced x: its ReLU backward and bias-gradient
+        # partials ride in this layer's dX GEMM (ops.dx_x6_relu, mask = x)
+        ctx.below = None
+        if (X6_MASK_DX and below is not None and not below["premasked"] and chw is None
+                and x.requires_grad and _x6_dx_shape_ok(x.shape[0], wm.shape[0], x.shape[1])):
+            below["premasked"] = True
+            ctx.below = below
+        if _x6(x.shape[0], wm.shape[0], x.shape[1]) and ops.linear_x6_ok(x, wm):
+            out = ops.linear_x6(x, wm, b, relu)
+        else:
+            out = torch._addmm_activation(b, x, wm.t(), use_gelu=False) if relu else \
+                torch.addmm(b, x, wm.t())
         ctx.relu = relu
         ctx.save_for_backward(x, w, out if relu else None)
         ctx.w, ctx.b = w, b
@@ -164,7 +237,7 @@ class _LinearAct(torch.autograd.Function):
     def backward(ctx, g):
         chw = ctx.chw
         if chw is None:
-            return _LinearAct._backward(ctx, g, ctx.w.grad)
+            return _LinearAct._backward(ctx, g, ctx.w.grad) + (None,)
         # permuted columns: weight gradient formed in the NHWC column order, then put back
         direct = _direct(ctx.w)
         wgrad = torch.empty_like(ctx.wm) if direct else None
@@ -173,7 +246,16 @@ class _LinearAct(torch.autograd.Function):
             _cols_from_nhwc(wgrad, chw, out=ctx.w.grad)
         if dw is not None:
             dw = _cols_from_nhwc(dw, chw)
-        return dx, dw, db, None, None, None
+        return dx, dw, db, None, None, None, None
+
+    @staticmethod
+    def _dx_of(ctx, g, w):
+        if ctx.below is None:
+            return _dx(g, w)
+        x = ctx.saved_tensors[0]
+        gp, dbp = ops.dx_x6_relu(g, w, x)
+        ctx.below["dbp"] = (dbp, dbp.shape[0])  # relu_bias_grad_partial's (partials, chunks)
+        return gp
 
     @staticmethod
     def _backward(ctx, g, wgrad):
@@ -187,7 +269,7 @@ class _LinearAct(torch.autograd.Function):
             # the consumer already applied this layer's ReLU mask: the fused heads backward
             # (_Heads) also wrote its bias gradient; the frame scatter (frames._FramesExpand)
             # left the bias-gradient partials in the box ("dbp"). Only dX and dW remain.
-            dx = _dx(g, w) if ctx.needs_input_grad[0] else None
+            dx = _LinearAct._dx_of(ctx, g, w) if ctx.needs_input_grad[0] else None
             dbp = ctx.box.get("dbp")
             if dbp is None:
                 _weight_grad(g, x, out=wgrad)
@@ -213,7 +295,7 @@ class _LinearAct(torch.autograd.Function):
             gp, dbp = ops.timed(f"relu_bias_grad_{g.shape[0]}x{g.shape[1]}" +
                                 ("" if ctx.relu else "_norelu"),
                                 lambda: ops.relu_bias_grad_partial(g, o))
-            dx = _dx(gp, w) if ctx.needs_input_grad[0] else None
+            dx = _LinearAct._dx_of(ctx, gp, w) if ctx.needs_input_grad[0] else None
             _weight_grad(gp, x, out=wgrad, db=(dbp, ctx.b.grad))
             return dx, None, None, None, None, None
         if FUSED_RELU_BIAS_GRAD and ctx.needs_input_grad[2] and _direct(ctx.b) and \
@@ -226,7 +308,7 @@ class _LinearAct(torch.autograd.Function):
             bias_done = True
         else:
             gp = torch.ops.aten.threshold_backward(g, out, 0) if ctx.relu else g
-        dx = _dx(gp, w) if ctx.needs_input_grad[0] else None
+        dx = _LinearAct._dx_of(ctx, gp, w) if ctx.needs_input_grad[0] else None
         dw = None
         if ctx.needs_input_grad[1]:
             if _direct(ctx.w):
@@ -433,7 +515,8 @@ def linear_act(x, lin: nn.Linear, relu: bool, chw=None):
     if relu and FUSED_HEADS_BWD and torch.is_grad_enabled() and _direct(lin.weight) and \
             _direct(lin.bias):
         box = {"premasked": False, "bias": lin.bias}
-    y = _LinearAct.apply(x2, lin.weight, lin.bias, relu, box, chw)
+    y = _LinearAct.apply(x2, lin.weight, lin.bias, relu, box, chw,
+                         getattr(x, "_ocppo_box", None))
     y = y.view(*lead, y.shape[-1])
     if box is not None:
         y._ocppo_box = box

@@ -132,6 +132,8 @@ class Args:
     eval_episodes: int = 0  # after training: evaluate() episodes (the reference runs 10 when tracking)
     conv_benchmark: bool = False  # cudnn.benchmark (MIOpen Find) for the NatureCNN convolutions
     gemm_table: bool = True  # the shipped hipBLASLt solution table for the update GEMMs
+    x6_gemm: bool = True  # update Linear GEMMs on the bf16 matrix cores as exact-split f32
+                          # (ops.gemm_x6, f32 accuracy), ReLU backward fused into the next dX
 
 
 def _flag_names(name: str) -> list[str]:

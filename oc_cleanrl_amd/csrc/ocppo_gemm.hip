@@ -1,0 +1,454 @@
+// Update-phase f32 GEMMs of the PPObj / NatureCNN-head Linear layers on the bf16 matrix cores
+// (cleanrl/ppo_atari_oc.py:566-606: the minibatch forward `agent.get_action_and_value(b_obs[mb])`
+// through architectures/ppo.py:60-84 and its `loss.backward()`; the reference's Linear layers are
+// torch.float32 with TF32 off, i.e. f32 products).
+//
+//   C[m, n] = epilogue( sum_k A(m, k) B(n, k) )
+//
+// gfx950 has no TF32/xf32 matrix path; its f32 MFMA runs at 1/16 of the bf16 MFMA rate
+// (157 vs 2,500 TFLOP/s dense, MI355X_MICROARCH.md). Every f32 operand is therefore split EXACTLY
+// into three bf16 pieces, x = x0 + x1 + x2 (x0 = rn_bf16(x), x1 = rn_bf16(x - x0), x2 = x - x0 - x1:
+// 3 x 8 significand bits hold f32's 24, each subtraction is exact), and the product is formed from
+// the six piece products down to the f32 rounding level:
+//   a*b = a0 b0 + (a0 b1 + a1 b0) + (a0 b2 + a1 b1 + a2 b0) + [a1 b2 + a2 b1 + a2 b2]
+// The bracketed terms are dropped: |a1 b2| <= 2^-8 * 2^-16 |a b| = 2^-24 |a b| (half an f32 ulp of
+// the product at most, ~2^-28 typically, randomly signed), below the per-product rounding a plain
+// f32 FMA chain already makes. Every piece product is exact in f32 (8 x 8 bits) and is accumulated
+// by the MFMA in f32. The leading products a0 b0 go into one accumulator and the five small ones into
+// a second (x 2^-8 in magnitude), added once at the end, so the small terms are never rounded
+// against the large running sum. Six bf16 MFMAs = 6/16 of one f32 MFMA's time for the same
+// output: the f32-equivalent ceiling is 2,500 / 6 = 417 TFLOP/s against 157 for the f32 MFMA.
+// tests/test_gemm_gpu.py measures the error against an f64 product next to hipBLASLt's f32 GEMM.
+//
+// A(m, k) and B(n, k) are strided views (one of the two strides is 1), so one kernel covers the
+// three products of a Linear layer without transposing anything in HBM:
+//   forward  y  = x W^T        A = x  [M, K] (k-contiguous), B = W [N, K] (k-contiguous)
+//   dX       dx = g' W         A = g' [M, N] (k-contiguous), B(n=k_in, k=n_out) = W (n-contiguous)
+//   dW       dW = g'^T x       A(m=n_out, k=row) = g' (m-contiguous), B(n=k_in, k=row) = x
+//                              (n-contiguous), the rows (K steps of 32) split evenly over
+//                              `splits` partial outputs that ocppo_sum_splits[_db] combines in
+//                              split order.
+//
+// Structure (gfx950, 256 CUs, 64-wide waves):
+//   * workgroup = 4 waves in 2 x 2, output tile BM x BN = 32 FM x 32 FN, wave tile 16 FM x 16 FN
+//     = FM x FN blocks of v_mfma_f32_16x16x32_bf16, each with a lead and a small-term accumulator;
+//   * K in steps of 32 (one MFMA depth): the next step's f32 tiles are loaded into registers while
+//     this step's MFMAs run from LDS; then (between two barriers) they are split and written as
+//     three bf16 planes [rows][32] per operand. A thread stages 4 x 4 (row, k) pieces: four 16-B
+//     loads along the contiguous dimension (whole 128-B lines per 8 lanes for a k-contiguous
+//     operand, 512-B runs per 32 lanes for an m/n-contiguous one, transposed in registers), then
+//     one 8-B LDS write per row and plane. The 64-B plane rows are XOR-swizzled in 16-B chunks
+//     (chunk ^ (row / 4) % 4), so the fragment reads (lane l: row l % 16, chunk l / 16, one
+//     ds_read_b128) are bank-conflict free;
+//   * XCD-aware order: each XCD gets a contiguous range of work units, consecutive units share
+//     their A row tile, so each XCD's L2 holds what its CUs share.
+// Roofline: MFMA-bound (6 bf16 MFMA passes per f32 multiply-add: 12 M N K bf16 flops against
+// the 2.5 PFLOP/s dense bf16 peak).
+#include "ocppo_common.h"
+
+namespace ocppo {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int kX6BK = 32;       // K step = one MFMA depth
+
+struct X6Args {
+  const float* a;
+  int64_t sam, sak;  // A(m, k) = a[m * sam + k * sak]
+  const float* b;
+  int64_t sbn, sbk;  // B(n, k) = b[n * sbn + k * sbk]
+  float* c;
+  int64_t ldc;       // C[m, n] = c[m * ldc + n]
+  const float* bias;
+  int relu;
+  int M, N, K;       // K: the whole reduction length (K / 32 steps, split evenly over splits)
+  int tiles_m, tiles_n, units, splits;
+  int64_t split_c;   // element offset of split s's output: s * split_c
+  // mask epilogue (dX of the layer above a Linear+ReLU): C = mask > 0 ? acc : 0 and the column
+  // sums of C over each row tile into dbp[tile_m, N] (that layer's bias-gradient partials)
+  const float* mask;
+  int64_t ldm;
+  float* dbp;
+};
+
+// The three bf16 pieces of an f32 pair (exact: x == x0 + x1 + x2 for finite normal x), packed:
+// p_i = (x_i of a) | (x_i of b) << 16 (v_cvt_pk_bf16_f32 and packed f32 subtractions: 9 VALU
+// instructions per pair).
+typedef float x6f2 __attribute__((ext_vector_type(2)));
+typedef __bf16 x6h2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t x6_pk(x6f2 v) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, x6h2));
+}
+__device__ __forceinline__ x6f2 x6_unpk(uint32_t p) {
+  return x6f2{__uint_as_float(p << 16), __uint_as_float(p & 0xffff0000u)};
+}
+__device__ __forceinline__ void x6_split2(x6f2 v, uint32_t& p0, uint32_t& p1, uint32_t& p2) {
+  p0 = x6_pk(v);
+  const x6f2 r1 = v - x6_unpk(p0);
+  p1 = x6_pk(r1);
+  const x6f2 r2 = r1 - x6_unpk(p1);
+  p2 = x6_pk(r2);
+}
+
+// byte offset of (row, k..k+3) in a [rows][32] bf16 plane, 16-B chunks XOR-swizzled by row / 4
+__device__ __forceinline__ int x6_off(int row, int k) {
+  const int chunk = (k >> 3) ^ ((row >> 2) & 3);
+  return row * 64 + chunk * 16 + (k & 4) * 2;
+}
+
+// One operand tile [ROWS][32 k] of one K step: PIECES 4 x 4 (row, k) pieces per thread.
+template <int ROWS, bool KC, int NT>
+struct X6Stage {
+  static constexpr int kPieces = ROWS / 4 * 8;
+  static constexpr int kPer = (kPieces + NT - 1) / NT;
+  static constexpr int kPlane = ROWS * 64;  // bytes per bf16 plane
+
+  __device__ static void piece_of(int p, int& rq, int& kq) {
+    if constexpr (KC) {  // k quads fastest: 8 lanes read one row's 128 B
+      kq = p & 7;
+      rq = p >> 3;
+    } else {  // row quads fastest: 32 lanes read 512 contiguous bytes of one k row
+      rq = p % (ROWS / 4);
+      kq = p / (ROWS / 4);
+    }
+  }
+
+  __device__ static void load(const float* __restrict__ src, int64_t srow, int64_t sk, int row0,
+                              int k0, int t, floatx4 (&r)[kPer][4]) {
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int p = t + NT * i;
+      if (kPieces % NT != 0 && p >= kPieces) continue;
+      int rq, kq;
+      piece_of(p, rq, kq);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float* q = KC ? src + static_cast<int64_t>(row0 + 4 * rq + j) * srow + (k0 + 4 * kq)
+                            : src + static_cast<int64_t>(k0 + 4 * kq + j) * sk + (row0 + 4 * rq);
+        r[i][j] = *reinterpret_cast<const floatx4*>(q);
+      }
+    }
+  }
+
+  // split the staged pieces and write the three planes (plane p at lds + p * kPlane)
+  __device__ static void stash(unsigned char* lds, int t, const floatx4 (&r)[kPer][4]) {
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int p = t + NT * i;
+      if (kPieces % NT != 0 && p >= kPieces) continue;
+      int rq, kq;
+      piece_of(p, rq, kq);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {  // row 4 rq + j of the piece
+        const x6f2 v01 = KC ? x6f2{r[i][j][0], r[i][j][1]} : x6f2{r[i][0][j], r[i][1][j]};
+        const x6f2 v23 = KC ? x6f2{r[i][j][2], r[i][j][3]} : x6f2{r[i][2][j], r[i][3][j]};
+        uint32_t a0, a1, a2, b0, b1, b2;
+        x6_split2(v01, a0, a1, a2);
+        x6_split2(v23, b0, b1, b2);
+        const int off = x6_off(4 * rq + j, 4 * kq);
+        *reinterpret_cast<uint2*>(lds + off) = uint2{a0, b0};
+        *reinterpret_cast<uint2*>(lds + kPlane + off) = uint2{a1, b1};
+        *reinterpret_cast<uint2*>(lds + 2 * kPlane + off) = uint2{a2, b2};
+      }
+    }
+  }
+};
+
+__device__ __forceinline__ bf16x8 x6_frag(const unsigned char* plane, int row, int chunk) {
+  const int off = row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4);
+  return *reinterpret_cast<const bf16x8*>(plane + off);
+}
+
+// The six piece products of one (A block i, B block j) pair into acc (lead) / acs (small terms)
+template <bool LO>
+__device__ __forceinline__ void x6_mfma6(const bf16x8 (&a)[3], const bf16x8 (&b)[3], floatx4& acc,
+                                         floatx4& acs) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], acc, 0, 0, 0);
+  floatx4& s = LO ? acs : acc;
+  s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], s, 0, 0, 0);
+  s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], s, 0, 0, 0);
+  s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], s, 0, 0, 0);
+  s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], s, 0, 0, 0);
+  s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], s, 0, 0, 0);
+}
+
+// WGM x WGN waves per workgroup, each FM x FN blocks of 16 x 16 (tile BM x BN = 16 FM WGM x
+// 16 FN WGN); LO: separate small-term accumulators (else all six products go into one); PF2: two
+// register sets, loads issued two K steps ahead (else one).
+template <int FM, int FN, int WGM, int WGN, bool AKC, bool BKC, bool LO, bool PF2>
+__global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_x6_kernel(X6Args g) {
+  constexpr int NT = 64 * WGM * WGN;
+  constexpr int BM = 16 * FM * WGM, BN = 16 * FN * WGN;
+  using SA = X6Stage<BM, AKC, NT>;
+  using SB = X6Stage<BN, BKC, NT>;
+  __shared__ __attribute__((aligned(16))) unsigned char lds[3 * SA::kPlane + 3 * SB::kPlane];
+  unsigned char* la = lds;
+  unsigned char* lb = lds + 3 * SA::kPlane;
+
+  // XCD-aware bijective remap: workgroups b, b + 8, ... share an XCD; XCD x gets units
+  // [start(x), start(x) + count(x)) in order
+  const int nb = gridDim.x, b = blockIdx.x;
+  const int xcd = b & 7, q = nb >> 3, rr = nb & 7;
+  const int u = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (b >> 3);
+  if (u >= g.units) return;
+  const int per_split = g.tiles_m * g.tiles_n;
+  const int s = u / per_split, rem = u - s * per_split;
+  const int tm = rem / g.tiles_n, tn = rem - tm * g.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const float* __restrict__ A = g.a;
+  const float* __restrict__ B = g.b;
+  // split s reduces K steps [kb, kb + nk): an even partition of the K / 32 steps
+  const int nall = g.K / kX6BK;
+  const int kb = static_cast<int>(static_cast<int64_t>(s) * nall / g.splits);
+  const int nk = static_cast<int>(static_cast<int64_t>(s + 1) * nall / g.splits) - kb;
+
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int wm = wv / WGN, wn = wv % WGN;
+  const int fr = lane & 15, fc = lane >> 4;
+
+  floatx4 hi[FM][FN], lo[LO ? FM : 1][LO ? FN : 1];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) hi[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  if constexpr (LO) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) lo[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  // MFMAs of the step held in LDS
+  auto compute = [&]() {
+    bf16x8 af[FM][3];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        af[i][pl] = x6_frag(la + pl * SA::kPlane, wm * 16 * FM + 16 * i + fr, fc);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      bf16x8 bf[3];
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        bf[pl] = x6_frag(lb + pl * SB::kPlane, wn * 16 * FN + 16 * j + fr, fc);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+        x6_mfma6<LO>(af[i], bf, hi[i][j], lo[LO ? i : 0][LO ? j : 0]);
+    }
+  };
+  floatx4 ra[SA::kPer][4], rb[SB::kPer][4];
+  if constexpr (!PF2) {
+    SA::load(A, g.sam, g.sak, m0, kb * kX6BK, t, ra);
+    SB::load(B, g.sbn, g.sbk, n0, kb * kX6BK, t, rb);
+    SA::stash(la, t, ra);
+    SB::stash(lb, t, rb);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const bool more = kt + 1 < nk;
+      if (more) {
+        SA::load(A, g.sam, g.sak, m0, (kb + kt + 1) * kX6BK, t, ra);
+        SB::load(B, g.sbn, g.sbk, n0, (kb + kt + 1) * kX6BK, t, rb);
+      }
+      compute();
+      __syncthreads();
+      if (more) {
+        SA::stash(la, t, ra);
+        SB::stash(lb, t, rb);
+      }
+      __syncthreads();
+    }
+  } else {
+    // set (ra, rb) holds even steps, (qa, qb) odd ones; at step kt the loads of step kt + 2 go
+    // into the set step kt came from (already in LDS), then step kt + 1 is stashed
+    floatx4 qa[SA::kPer][4], qb[SB::kPer][4];
+    SA::load(A, g.sam, g.sak, m0, kb * kX6BK, t, ra);
+    SB::load(B, g.sbn, g.sbk, n0, kb * kX6BK, t, rb);
+    if (nk > 1) {
+      SA::load(A, g.sam, g.sak, m0, (kb + 1) * kX6BK, t, qa);
+      SB::load(B, g.sbn, g.sbk, n0, (kb + 1) * kX6BK, t, qb);
+    }
+    SA::stash(la, t, ra);
+    SB::stash(lb, t, rb);
+    __syncthreads();
+    auto step = [&](int kt, floatx4 (&ldA)[SA::kPer][4], floatx4 (&ldB)[SB::kPer][4],
+                    floatx4 (&stA)[SA::kPer][4], floatx4 (&stB)[SB::kPer][4]) {
+      if (kt + 2 < nk) {
+        SA::load(A, g.sam, g.sak, m0, (kb + kt + 2) * kX6BK, t, ldA);
+        SB::load(B, g.sbn, g.sbk, n0, (kb + kt + 2) * kX6BK, t, ldB);
+      }
+      compute();
+      __syncthreads();
+      if (kt + 1 < nk) {
+        SA::stash(la, t, stA);
+        SB::stash(lb, t, stB);
+      }
+      __syncthreads();
+    };
+    for (int kt = 0; kt < nk; kt += 2) {
+      step(kt, ra, rb, qa, qb);
+      if (kt + 1 < nk) step(kt + 1, qa, qb, ra, rb);
+    }
+  }
+
+  // epilogue: MFMA result C[4 fc + r][fr] of block (i, j)
+  float* __restrict__ Cp = g.c + s * g.split_c;
+  const int wr0 = m0 + wm * 16 * FM, wc0 = n0 + wn * 16 * FN;
+  if (g.mask) {
+    // threshold_backward(acc, mask, 0) and the tile's column sums: rows of a lane (i, r) in
+    // order, then the wave's 4 row groups (xor 16, 32), then the two wave rows through LDS
+    float colsum[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int col = wc0 + 16 * j + fr;
+      float cs = 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t row = wr0 + 16 * i + 4 * fc + r;
+          const float acc = LO ? hi[i][j][r] + lo[LO ? i : 0][LO ? j : 0][r] : hi[i][j][r];
+          const float v = g.mask[row * g.ldm + col] > 0.f ? acc : 0.f;
+          Cp[row * g.ldc + col] = v;
+          cs += v;
+        }
+      }
+      cs += __shfl_xor(cs, 16, kWave);
+      cs += __shfl_xor(cs, 32, kWave);
+      colsum[j] = cs;
+    }
+    float* red = reinterpret_cast<float*>(lds);  // [WGM - 1][BN]; the K loop ended with a barrier
+    if (wm > 0 && fc == 0) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) red[(wm - 1) * BN + wn * 16 * FN + 16 * j + fr] = colsum[j];
+    }
+    __syncthreads();
+    if (wm == 0 && fc == 0) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int lc = wn * 16 * FN + 16 * j + fr;
+        float v = colsum[j];
+#pragma unroll
+        for (int q = 0; q + 1 < WGM; ++q) v += red[q * BN + lc];  // wave rows in order
+        g.dbp[static_cast<int64_t>(tm) * g.N + n0 + lc] = v;
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int col = wc0 + 16 * j + fr;
+    const float bv = g.bias ? g.bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = wr0 + 16 * i + 4 * fc + r;
+        float v = LO ? hi[i][j][r] + lo[LO ? i : 0][LO ? j : 0][r] : hi[i][j][r];
+        if (g.bias) v += bv;
+        if (g.relu) v = fmaxf(v, 0.f);
+        Cp[row * g.ldc + col] = v;
+      }
+    }
+  }
+}
+
+template <int FM, int FN, int WGM, int WGN, bool LO, bool PF2>
+static void launch_x6_t(hipStream_t s, bool akc, bool bkc, X6Args& g) {
+  g.tiles_m = g.M / (16 * FM * WGM);
+  g.tiles_n = g.N / (16 * FN * WGN);
+  const dim3 grid(g.units), block(64 * WGM * WGN);
+  if (akc && bkc)
+    hipLaunchKernelGGL((gemm_x6_kernel<FM, FN, WGM, WGN, true, true, LO, PF2>), grid, block, 0, s, g);
+  else if (akc)
+    hipLaunchKernelGGL((gemm_x6_kernel<FM, FN, WGM, WGN, true, false, LO, PF2>), grid, block, 0, s, g);
+  else if (bkc)
+    hipLaunchKernelGGL((gemm_x6_kernel<FM, FN, WGM, WGN, false, true, LO, PF2>), grid, block, 0, s, g);
+  else
+    hipLaunchKernelGGL((gemm_x6_kernel<FM, FN, WGM, WGN, false, false, LO, PF2>), grid, block, 0, s, g);
+}
+
+// Tile configs (FM, FN, WGM, WGN): tile = 16 FM WGM rows x 16 FN WGN columns
+struct X6Tile {
+  int fm, fn, wgm, wgn;
+};
+constexpr X6Tile kX6Tiles[] = {{4, 4, 2, 2}, {2, 4, 2, 2}, {4, 2, 2, 2}, {2, 2, 2, 2},
+                               {4, 2, 2, 4}, {2, 2, 2, 4}, {2, 4, 4, 2}, {2, 2, 4, 2}};
+
+// variant: shape (bits 0-2) | PF2 (bit 3) | one accumulator (bit 4); instantiated: every shape
+// with PF2 + one accumulator (the product family), shapes 0-3 with one-step loads (+/- LO)
+static bool launch_x6(hipStream_t s, int tile, bool akc, bool bkc, X6Args& g) {
+  const int shape = tile & 7;
+  const bool pf2 = tile & 8, one = tile & 16;
+  if (pf2 && one) {
+    switch (shape) {
+      case 0: launch_x6_t<4, 4, 2, 2, false, true>(s, akc, bkc, g); return true;
+      case 1: launch_x6_t<2, 4, 2, 2, false, true>(s, akc, bkc, g); return true;
+      case 2: launch_x6_t<4, 2, 2, 2, false, true>(s, akc, bkc, g); return true;
+      case 3: launch_x6_t<2, 2, 2, 2, false, true>(s, akc, bkc, g); return true;
+      case 4: launch_x6_t<4, 2, 2, 4, false, true>(s, akc, bkc, g); return true;
+      case 5: launch_x6_t<2, 2, 2, 4, false, true>(s, akc, bkc, g); return true;
+      case 6: launch_x6_t<2, 4, 4, 2, false, true>(s, akc, bkc, g); return true;
+      default: launch_x6_t<2, 2, 4, 2, false, true>(s, akc, bkc, g); return true;
+    }
+  }
+  if (pf2 || shape > 3) return false;
+  switch (shape + (one ? 4 : 0)) {
+    case 0: launch_x6_t<4, 4, 2, 2, true, false>(s, akc, bkc, g); return true;
+    case 1: launch_x6_t<2, 4, 2, 2, true, false>(s, akc, bkc, g); return true;
+    case 2: launch_x6_t<4, 2, 2, 2, true, false>(s, akc, bkc, g); return true;
+    case 3: launch_x6_t<2, 2, 2, 2, true, false>(s, akc, bkc, g); return true;
+    case 4: launch_x6_t<4, 4, 2, 2, false, false>(s, akc, bkc, g); return true;
+    case 5: launch_x6_t<2, 4, 2, 2, false, false>(s, akc, bkc, g); return true;
+    case 6: launch_x6_t<4, 2, 2, 2, false, false>(s, akc, bkc, g); return true;
+    default: launch_x6_t<2, 2, 2, 2, false, false>(s, akc, bkc, g); return true;
+  }
+}
+
+}  // namespace ocppo
+
+using namespace ocppo;
+
+extern "C" int ocppo_gemm_x6(ocppo_stream_t stream, const float* a, int64_t sam, int64_t sak,
+                             const float* b, int64_t sbn, int64_t sbk, float* c, int64_t ldc,
+                             int64_t M, int64_t N, int64_t K, int64_t splits, int64_t split_c,
+                             const float* bias, int relu,
+                             const float* mask, int64_t ldm, float* dbp, int tile) {
+  OCPPO_REQUIRE(M >= 1 && N >= 1 && K >= 1 && splits >= 1 && M <= INT32_MAX && N <= INT32_MAX &&
+                    K <= INT32_MAX,
+                "ocppo_gemm_x6: bad sizes M=%lld N=%lld K=%lld splits=%lld", (long long)M,
+                (long long)N, (long long)K, (long long)splits);
+  OCPPO_REQUIRE(a && b && c, "ocppo_gemm_x6: null pointer");
+  OCPPO_REQUIRE((sak == 1 && sam >= K && sam % 4 == 0) || (sam == 1 && sak >= M && sak % 4 == 0),
+                "ocppo_gemm_x6: A strides (%lld, %lld): one must be 1, the other a multiple of 4",
+                (long long)sam, (long long)sak);
+  OCPPO_REQUIRE((sbk == 1 && sbn >= K && sbn % 4 == 0) || (sbn == 1 && sbk >= N && sbk % 4 == 0),
+                "ocppo_gemm_x6: B strides (%lld, %lld): one must be 1, the other a multiple of 4",
+                (long long)sbn, (long long)sbk);
+  OCPPO_REQUIRE(ldc >= N, "ocppo_gemm_x6: ldc=%lld < N", (long long)ldc);
+  OCPPO_REQUIRE(reinterpret_cast<uintptr_t>(a) % 16 == 0 && reinterpret_cast<uintptr_t>(b) % 16 == 0,
+                "ocppo_gemm_x6: A and B must be 16-B aligned");
+  OCPPO_REQUIRE(K % kX6BK == 0 && K / kX6BK >= splits,
+                "ocppo_gemm_x6: K=%lld must be a multiple of %d with >= 1 step per split",
+                (long long)K, kX6BK);
+  OCPPO_REQUIRE(tile >= 0 && tile < 32, "ocppo_gemm_x6: tile=%d", tile);
+  const X6Tile tc = kX6Tiles[tile & 7];
+  const int64_t bm = 16 * tc.fm * tc.wgm, bn = 16 * tc.fn * tc.wgn;
+  OCPPO_REQUIRE(M % bm == 0 && N % bn == 0,
+                "ocppo_gemm_x6: M=%lld, N=%lld must be multiples of the %lld x %lld tile",
+                (long long)M, (long long)N, (long long)bm, (long long)bn);
+  OCPPO_REQUIRE(splits == 1 || (bias == nullptr && !relu),
+                "ocppo_gemm_x6: bias / ReLU epilogues need splits == 1");
+  OCPPO_REQUIRE(mask == nullptr || (splits == 1 && bias == nullptr && !relu && dbp && ldm >= N),
+                "ocppo_gemm_x6: the mask epilogue needs splits == 1, no bias / ReLU, dbp, ldm >= N");
+  const int64_t units = splits * (M / bm) * (N / bn);
+  OCPPO_REQUIRE(units <= INT32_MAX / 2, "ocppo_gemm_x6: too large");
+  X6Args g{a, sam, sak, b, sbn, sbk, c, ldc, bias, relu ? 1 : 0, (int)M, (int)N, (int)K,
+           0, 0, (int)units, (int)splits, split_c, mask, ldm, dbp};
+  clear_stale_error();
+  hipStream_t s = as_stream(stream);
+  const bool akc = sak == 1, bkc = sbk == 1;
+  OCPPO_REQUIRE(launch_x6(s, tile, akc, bkc, g), "ocppo_gemm_x6: variant %d not built", tile);
+  return check_launch("ocppo_gemm_x6");
+}

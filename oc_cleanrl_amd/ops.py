@@ -812,6 +812,126 @@ def sum_splits(part, out=None):
 
 
 # ---------------------------------------------------------------------------------------------
+# Update-phase f32 GEMMs on the bf16 matrix cores (ocppo_gemm_x6; ppo_atari_oc.py:566-606)
+# ---------------------------------------------------------------------------------------------
+# (rows, columns) of variant & 7 (0-3: 4 waves, 4-7: 8 waves); variant & 8: loads two K steps
+# ahead; variant & 16: one accumulator (built: every shape with both, shapes 0-3 with neither or
+# only the latter)
+X6_TILES = ((128, 128), (64, 128), (128, 64), (64, 64),
+            (128, 128), (64, 128), (128, 128), (128, 64)) * 4
+X6_BUILT = tuple(range(4)) + tuple(range(16, 20)) + tuple(range(24, 32))
+
+
+X6_AUTO = 24  # the variant family x6_tile picks from (two K steps of loads in flight, one
+# accumulator: fastest at every config-2 update shape, tools/exp_gemm_x6.py; error vs f64 at or
+# below hipBLASLt's f32 GEMM, tests/test_gemm_gpu.py)
+
+
+def x6_tile(M: int, N: int, splits: int = 1, tile: int | None = None) -> int | None:
+    """Tile for an M x N (x splits) product: the largest tile that divides it and still gives
+    >= 512 workgroups (two per CU), else the one giving the most; None if none divides."""
+    if tile is not None:
+        bm, bn = X6_TILES[tile]
+        return tile if M % bm == 0 and N % bn == 0 else None
+    best, best_units = None, -1
+    for i, (bm, bn) in enumerate(X6_TILES[:4]):
+        i += X6_AUTO
+        if M % bm or N % bn:
+            continue
+        units = splits * (M // bm) * (N // bn)
+        if units >= 512:
+            return i
+        if units > best_units:
+            best, best_units = i, units
+    return best
+
+
+def _x6_operand_ok(t) -> bool:
+    return (t.is_cuda and t.dtype == torch.float32 and t.dim() == 2 and t.data_ptr() % 16 == 0
+            and t.stride(1) == 1 and t.stride(0) % 4 == 0)
+
+
+def gemm_x6(a, sam, sak, b, sbn, sbk, c, ldc, M, N, K, splits=1, split_c=0, bias=None,
+            relu=False, mask=None, dbp=None, tile=None):
+    """Raw ocppo_gemm_x6 call on tensors a, b, c (their data pointers; strides as given)."""
+    t = x6_tile(M, N, splits, tile)
+    if t is None:
+        raise ValueError(f"gemm_x6: no tile divides {M} x {N}")
+    dev = c.device
+    if mask is not None:
+        if (mask.dim() != 2 or tuple(mask.shape) != (M, N) or mask.stride(1) != 1
+                or mask.dtype != torch.float32 or dbp is None):
+            raise ValueError("gemm_x6: mask must be an f32 [M, N] row-major view, with dbp")
+        _check(dbp, "dbp", torch.float32, dev, (M // X6_TILES[t][0]) * N)
+    call("ocppo_gemm_x6", _stream(dev), a.data_ptr(), sam, sak, b.data_ptr(), sbn, sbk,
+         c.data_ptr(), ldc, M, N, K, splits, split_c,
+         None if bias is None else _check(bias, "bias", torch.float32, dev, N), int(bool(relu)),
+         None if mask is None else mask.data_ptr(), 0 if mask is None else mask.stride(0),
+         None if dbp is None else dbp.data_ptr(), t)
+    return c
+
+
+def linear_x6_ok(x, w) -> bool:
+    """y = x W^T on gemm_x6: x [M, K], W [N, K] row-major f32, K % 32 == 0, a tile divides M x N."""
+    return (_x6_operand_ok(x) and _x6_operand_ok(w) and x.shape[1] == w.shape[1]
+            and x.shape[1] % 32 == 0 and x6_tile(x.shape[0], w.shape[0]) is not None)
+
+
+def linear_x6(x, w, b=None, relu=False, out=None):
+    """act(x W^T + b) (torch._addmm_activation's order: sum, + bias, then ReLU)."""
+    M, K = x.shape
+    N = w.shape[0]
+    out = torch.empty((M, N), dtype=torch.float32, device=x.device) if out is None else out
+    return gemm_x6(x, x.stride(0), 1, w, w.stride(0), 1, out, out.stride(0), M, N, K, bias=b,
+                   relu=relu)
+
+
+def dx_x6_ok(g, w) -> bool:
+    """dX = g W on gemm_x6: g [M, N] (N % 32 == 0), W [N, K]."""
+    return (_x6_operand_ok(g) and _x6_operand_ok(w) and g.shape[1] == w.shape[0]
+            and g.shape[1] % 32 == 0 and x6_tile(g.shape[0], w.shape[1]) is not None)
+
+
+def dx_x6(g, w, out=None):
+    M, N = g.shape
+    K = w.shape[1]
+    out = torch.empty((M, K), dtype=torch.float32, device=g.device) if out is None else out
+    return gemm_x6(g, g.stride(0), 1, w, 1, w.stride(0), out, out.stride(0), M, K, N)
+
+
+def dx_x6_relu(g, w, mask):
+    """gp = threshold_backward(g W, mask, 0) for the Linear+ReLU layer below whose output is
+    `mask` [M, K], with that layer's bias-gradient partials: returns (gp, dbp [M / tile rows, K])
+    (dbp summed in row-tile order by sum_splits_db)."""
+    M, N = g.shape
+    K = w.shape[1]
+    t = x6_tile(M, K)
+    gp = torch.empty((M, K), dtype=torch.float32, device=g.device)
+    dbp = torch.empty((M // X6_TILES[t][0], K), dtype=torch.float32, device=g.device)
+    gemm_x6(g, g.stride(0), 1, w, 1, w.stride(0), gp, K, M, K, N, mask=mask, dbp=dbp, tile=t)
+    return gp, dbp
+
+
+def dw_x6_ok(g, x, splits: int) -> bool:
+    """dW = g^T x on gemm_x6 as `splits` partial products over the rows (in steps of 32)."""
+    rows = g.shape[0]
+    return (_x6_operand_ok(g) and _x6_operand_ok(x) and x.shape[0] == rows and splits >= 1
+            and rows % 32 == 0 and rows // 32 >= splits
+            and x6_tile(g.shape[1], x.shape[1], splits) is not None)
+
+
+def dw_x6_parts(g, x, splits: int, part=None, tile=None):
+    """part[s] = g[rows of split s]^T x[rows of split s] -> [splits, N, K], the rows split evenly
+    in steps of 32 (combined by sum_splits / sum_splits_db in split order)."""
+    rows, N = g.shape
+    K = x.shape[1]
+    part = (torch.empty((splits, N, K), dtype=torch.float32, device=g.device)
+            if part is None else part)
+    return gemm_x6(g, 1, g.stride(0), x, 1, x.stride(0), part, K, N, K, rows, splits=splits,
+                   split_c=N * K, tile=tile)
+
+
+# ---------------------------------------------------------------------------------------------
 # Frame-deduplicated PPObj minibatch encoder (ppo_atari_oc.py:566 through architectures/ppo.py:60-84)
 # ---------------------------------------------------------------------------------------------
 def _obs_TNWF(obs):

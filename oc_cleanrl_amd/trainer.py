@@ -32,7 +32,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
-from . import frames, gemm_table, ops
+from . import agents, frames, gemm_table, ops
 from .agents import NormalizeImg, PPObj, fused_trunk, linear_relu, make_agent
 from .args import Args
 from .envs import HostVecEnv, make_device_env
@@ -246,6 +246,8 @@ class PPOTrainer:
         torch.backends.cudnn.deterministic = a.torch_deterministic
         torch.backends.cudnn.benchmark = a.conv_benchmark
         self.gemm_table = a.gemm_table and gemm_table.use(device)
+        # process-wide switch of agents' update GEMM path (like the TunableOp table above)
+        agents.X6_GEMM = agents.X6_MASK_DX = bool(a.x6_gemm)
 
         # seeding as ppo_atari_multigpu.py:208-212, 230-231: identical init on every rank, then
         # rank-dependent sampling / env / shuffle streams

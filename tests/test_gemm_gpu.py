@@ -1,0 +1,140 @@
+"""ocppo_gemm_x6: the update's f32 GEMMs as six bf16 piece products (include/ocppo.h).
+
+Accuracy is checked against an f64 product, scaled by (|A| |B|)[m, n] — the bound an f32 dot
+product's rounding obeys — next to hipBLASLt's own f32 GEMM on the same operands: the x6 product
+must stay at f32 accuracy (the reference's Linear layers, ppo_atari_oc.py:566-606, are f32 with
+TF32 off)."""
+import pytest
+import torch
+
+from oc_cleanrl_amd import ops
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda:0")
+
+
+def _rand(*shape, gen, scale=1.0):
+    return (torch.rand(*shape, device=DEV, generator=gen) * 2 - 1) * scale
+
+
+def _rel(c, ref, scale):
+    d = (c.double() - ref).abs() / scale.clamp_min(1e-300)
+    return float(d.max()), float(d.mean())
+
+
+def _check(c, ref, scale, torch_c):
+    mx, mean = _rel(c, ref, scale)
+    tmx, tmean = _rel(torch_c, ref, scale)
+    # f32 level: a few units of 2^-24 relative to sum |a b|, and no worse on average than the
+    # f32 library GEMM (tolerance for its different summation order)
+    assert mx <= 4e-7, (mx, tmx)
+    assert mean <= 2.0 * tmean + 1e-9, (mean, tmean)
+
+
+@pytest.mark.parametrize("tile", ops.X6_BUILT)
+@pytest.mark.parametrize("M,N,K", [(256, 256, 96), (128, 384, 320), (384, 128, 1024)])
+def test_forward_bias_relu(tile, M, N, K):
+    if ops.x6_tile(M, N, 1, tile) is None:
+        pytest.skip("tile does not divide")
+    g = torch.Generator(device=DEV).manual_seed(M * 7 + N + K)
+    x = _rand(M, K, gen=g)
+    w = _rand(N, K, gen=g, scale=K ** -0.5)
+    b = _rand(N, gen=g, scale=0.1)
+    pre64 = x.double() @ w.double().t() + b.double()
+    scale = x.double().abs() @ w.double().abs().t() + b.double().abs()
+    out = torch.empty(M, N, device=DEV)
+    ops.gemm_x6(x, K, 1, w, K, 1, out, N, M, N, K, bias=b, relu=True, tile=tile)
+    torch_c = torch._addmm_activation(b, x, w.t())
+    _check(out, pre64.clamp_min(0), scale, torch_c)
+    # ReLU exactly where the f64 pre-activation is clearly negative
+    assert bool(((pre64 < -1e-5 * scale) <= (out == 0)).all())
+
+
+@pytest.mark.parametrize("tile", [0, 3, 16, 24, 28, 30, 31])
+def test_dx_and_linear_helpers(tile):
+    g = torch.Generator(device=DEV).manual_seed(11)
+    M, N, K = 512, 256, 384  # dX [M, K] = g [M, N] W [N, K]
+    gg = _rand(M, N, gen=g)
+    w = _rand(N, K, gen=g, scale=N ** -0.5)
+    ref = gg.double() @ w.double()
+    scale = gg.double().abs() @ w.double().abs()
+    out = torch.empty(M, K, device=DEV)
+    ops.gemm_x6(gg, N, 1, w, 1, K, out, K, M, K, N, tile=tile)
+    _check(out, ref, scale, gg @ w)
+    assert ops.dx_x6_ok(gg, w)
+    _check(ops.dx_x6(gg, w), ref, scale, gg @ w)
+    x = _rand(M, K, gen=g)
+    assert ops.linear_x6_ok(x, w)
+    y = ops.linear_x6(x, w)
+    _check(y, x.double() @ w.double().t(), x.double().abs() @ w.double().abs().t(), x @ w.t())
+
+
+@pytest.mark.parametrize("tile", [None, 0, 24, 28])
+@pytest.mark.parametrize("splits", [1, 4, 8, 5])
+def test_weight_grad_splits(splits, tile):
+    g = torch.Generator(device=DEV).manual_seed(splits)
+    R, N, K = 2048, 256, 128  # dW [N, K] = g [R, N]^T x [R, K]; 64 steps of 32 rows
+    gg = _rand(R, N, gen=g)
+    x = _rand(R, K, gen=g)
+    assert ops.dw_x6_ok(gg, x, splits)
+    if tile is None:
+        part = ops.dw_x6_parts(gg, x, splits)
+    else:
+        part = torch.empty(splits, N, K, device=DEV)
+        ops.gemm_x6(gg, 1, N, x, 1, K, part, K, N, K, R, splits=splits, split_c=N * K, tile=tile)
+    nk = R // 32
+    for s in range(splits):
+        r0, r1 = 32 * (s * nk // splits), 32 * ((s + 1) * nk // splits)
+        ref = gg[r0:r1].double().t() @ x[r0:r1].double()
+        scale = gg[r0:r1].double().abs().t() @ x[r0:r1].double().abs()
+        _check(part[s], ref, scale, gg[r0:r1].t() @ x[r0:r1])
+
+
+def test_deterministic_and_exact_on_bf16_operands():
+    # operands that are already bf16 values: the split is (x, 0, 0) and every product is exact,
+    # so the result is an exact sum of exact products when the sums fit in f32 (small integers)
+    g = torch.Generator(device=DEV).manual_seed(5)
+    M, N, K = 256, 128, 512
+    x = torch.randint(-8, 9, (M, K), device=DEV, generator=g).float()
+    w = torch.randint(-8, 9, (N, K), device=DEV, generator=g).float()
+    out1 = ops.linear_x6(x, w)
+    out2 = ops.linear_x6(x, w)
+    assert torch.equal(out1, out2)
+    assert torch.equal(out1, (x.double() @ w.double().t()).float())
+
+
+def test_rejects_bad_shapes():
+    x = torch.zeros(128, 48, device=DEV)
+    w = torch.zeros(128, 48, device=DEV)
+    assert not ops.linear_x6_ok(x, w)  # K % 32 != 0
+    out = torch.empty(128, 128, device=DEV)
+    with pytest.raises(ops._lib.OcppoError):
+        ops.gemm_x6(x, 48, 1, w, 48, 1, out, 128, 128, 128, 48, tile=0)
+    x2 = torch.zeros(96, 64, device=DEV)
+    assert ops.x6_tile(96, 128) is None
+    assert not ops.linear_x6_ok(x2, torch.zeros(128, 64, device=DEV))
+
+
+@pytest.mark.parametrize("tile", [0, 3, 16, 24, 28, 30])
+def test_dx_mask_epilogue(tile):
+    # the dX product of the layer above a Linear+ReLU with that ReLU's backward fused in:
+    # gp = threshold_backward(g W, out, 0) and the per-row-tile column sums of gp (bias grad)
+    g = torch.Generator(device=DEV).manual_seed(21)
+    M, N, K = 512, 256, 384
+    gg = _rand(M, N, gen=g)
+    w = _rand(N, K, gen=g, scale=N ** -0.5)
+    out = torch.relu(_rand(M, K, gen=g))  # the layer-below's ReLU output (mask)
+    bm = ops.X6_TILES[tile][0]
+    gp = torch.empty(M, K, device=DEV)
+    dbp = torch.empty(M // bm, K, device=DEV)
+    ops.gemm_x6(gg, N, 1, w, 1, K, gp, K, M, K, N, mask=out, dbp=dbp, tile=tile)
+    ref = torch.where(out > 0, gg.double() @ w.double(), torch.zeros((), dtype=torch.float64, device=DEV))
+    scale = gg.double().abs() @ w.double().abs()
+    _check(gp, ref, scale, torch.ops.aten.threshold_backward(gg @ w, out, 0))
+    assert bool((gp[out <= 0] == 0).all())
+    # each partial is the sum of gp over its row tile (fixed order: close to an f64 sum)
+    ps = gp.double().view(M // bm, bm, K).sum(1)
+    assert torch.allclose(dbp.double(), ps, rtol=1e-5, atol=1e-5)
+    gp2, dbp2 = ops.dx_x6_relu(gg, w, out)
+    assert torch.equal(gp2, gp if ops.x6_tile(M, K) == tile else gp2)
