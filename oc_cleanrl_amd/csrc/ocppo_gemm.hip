@@ -37,9 +37,9 @@
 //     three bf16 planes [rows][32] per operand. A thread stages 4 x 4 (row, k) pieces: four 16-B
 //     loads along the contiguous dimension (whole 128-B lines per 8 lanes for a k-contiguous
 //     operand, 512-B runs per 32 lanes for an m/n-contiguous one, transposed in registers), then
-//     one 8-B LDS write per row and plane. The 64-B plane rows are XOR-swizzled in 16-B chunks
-//     (chunk ^ (row / 4) % 4), so the fragment reads (lane l: row l % 16, chunk l / 16, one
-//     ds_read_b128) are bank-conflict free;
+//     one 8-B LDS write per row and plane. The plane rows are stored in 128-B pairs with a
+//     3-bit XOR swizzle of their 16-B chunks (x6_chunk_off), so the fragment reads (lane l:
+//     row l % 16, chunk l / 16, one ds_read_b128) and the stash writes are bank-conflict free;
 //   * XCD-aware order: each XCD gets a contiguous range of work units, consecutive units share
 //     their A row tile, so each XCD's L2 holds what its CUs share.
 // Roofline: MFMA-bound (6 bf16 MFMA passes per f32 multiply-add: 12 M N K bf16 flops against
@@ -91,15 +91,28 @@ __device__ __forceinline__ void x6_split2(x6f2 v, uint32_t& p0, uint32_t& p1, ui
   p2 = x6_pk(r2);
 }
 
-// byte offset of (row, k..k+3) in a [rows][32] bf16 plane, 16-B chunks XOR-swizzled by row / 4
+// LDS plane layout: rows in pairs of 128 B (row r's 64 B = 16-B chunks 4 (r & 1) .. + 3 of pair
+// r / 2), chunk index XOR-swizzled by H(r) = bitrev3((r / 4) % 8). Found by exhaustive search
+// over the 8! chunk maps (tools/x6_swizzle.py) so that, with the piece mappings of X6Stage, every
+// ds_read_b128 fragment read (its four 16-lane groups) and every ds_write_b64 stash write (four
+// 16 x 8-B groups, k- or row-contiguous operand) touches each bank once: no conflicts.
+__device__ __forceinline__ int x6_h(int row) {
+  const int x = (row >> 2) & 7;
+  return ((x & 1) << 2) | (x & 2) | (x >> 2);
+}
+// byte offset of 16-B chunk `chunk` (k = 8 chunk .. + 7) of plane row `row`
+__device__ __forceinline__ int x6_chunk_off(int row, int chunk) {
+  return (row >> 1) * 128 + 16 * ((((row & 1) << 2) | chunk) ^ x6_h(row));
+}
+// byte offset of (row, k..k+3), k % 4 == 0
 __device__ __forceinline__ int x6_off(int row, int k) {
-  const int chunk = (k >> 3) ^ ((row >> 2) & 3);
-  return row * 64 + chunk * 16 + (k & 4) * 2;
+  return x6_chunk_off(row, k >> 3) + (k & 4) * 2;
 }
 
 // One operand tile [ROWS][32 k] of one K step: PIECES 4 x 4 (row, k) pieces per thread.
 template <int ROWS, bool KC, int NT>
 struct X6Stage {
+  static_assert(ROWS % 32 == 0, "tile rows must be a multiple of 32");
   static constexpr int kPieces = ROWS / 4 * 8;
   static constexpr int kPer = (kPieces + NT - 1) / NT;
   static constexpr int kPlane = ROWS * 64;  // bytes per bf16 plane
@@ -108,9 +121,11 @@ struct X6Stage {
     if constexpr (KC) {  // k quads fastest: 8 lanes read one row's 128 B
       kq = p & 7;
       rq = p >> 3;
-    } else {  // row quads fastest: 32 lanes read 512 contiguous bytes of one k row
-      rq = p % (ROWS / 4);
-      kq = p / (ROWS / 4);
+    } else {  // 8 row quads x 2 k quads per 16 lanes: 8 lanes read 128 contiguous bytes of a
+              // k row (the mapping the swizzle's conflict-free stash writes assume)
+      constexpr int kRqBlocks = ROWS / 32;  // blocks of 8 row quads
+      rq = (p & 7) + 8 * ((p >> 4) % kRqBlocks);
+      kq = ((p >> 3) & 1) + 2 * ((p >> 4) / kRqBlocks);
     }
   }
 
@@ -156,8 +171,7 @@ struct X6Stage {
 };
 
 __device__ __forceinline__ bf16x8 x6_frag(const unsigned char* plane, int row, int chunk) {
-  const int off = row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4);
-  return *reinterpret_cast<const bf16x8*>(plane + off);
+  return *reinterpret_cast<const bf16x8*>(plane + x6_chunk_off(row, chunk));
 }
 
 // The six piece products of one (A block i, B block j) pair into acc (lead) / acs (small terms)

@@ -829,7 +829,8 @@ X6_AUTO = 24  # the variant family x6_tile picks from (two K steps of loads in f
 
 def x6_tile(M: int, N: int, splits: int = 1, tile: int | None = None) -> int | None:
     """Tile for an M x N (x splits) product: the largest tile that divides it and still gives
-    >= 512 workgroups (two per CU), else the one giving the most; None if none divides."""
+    >= 256 workgroups (one per CU; 128 x 128 is the fastest at every config-2 shape that has
+    that many, tools/exp_gemm_x6.py), else the one giving the most; None if none divides."""
     if tile is not None:
         bm, bn = X6_TILES[tile]
         return tile if M % bm == 0 and N % bn == 0 else None
@@ -839,7 +840,7 @@ def x6_tile(M: int, N: int, splits: int = 1, tile: int | None = None) -> int | N
         if M % bm or N % bn:
             continue
         units = splits * (M // bm) * (N // bn)
-        if units >= 512:
+        if units >= 256:
             return i
         if units > best_units:
             best, best_units = i, units

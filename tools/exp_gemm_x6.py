@@ -49,12 +49,19 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--only", default=None, help="kind,M,N,K: one shape (profiling)")
+    ap.add_argument("--tiles", default=None, help="comma-separated variants (default: all built)")
     a = ap.parse_args()
+    shapes = SHAPES
+    if a.only:
+        k, *dims = a.only.split(",")
+        shapes = [(k, *map(int, dims))]
+    tiles = [int(t) for t in a.tiles.split(",")] if a.tiles else list(ops.X6_BUILT)
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
     lines = []
     tot_torch, tot_best = 0.0, 0.0
-    for kind, M, N, K in SHAPES:
+    for kind, M, N, K in shapes:
         flops = 2.0 * M * N * K
         if kind == "fwd":
             x = torch.rand(M, K, device=dev, generator=g) * 2 - 1
@@ -99,7 +106,7 @@ def main():
         rec = {"kind": kind, "M": M, "N": N, "K": K, "torch_us": round(t_us, 2),
                "torch_tf": round(flops / t_us / 1e6, 1), "torch_err": t_err, "ours": {}}
         best = None
-        for t in ops.X6_BUILT:
+        for t in tiles:
             if not shape_ok(t):
                 continue
             f = ofn(t)

@@ -1,0 +1,27 @@
+#!/usr/bin/env bash
+# PMC passes (SQ counters, one pass each) of one gemm_x6 variant at one update shape:
+#   bash tools/pmc_gemm.sh TAG kind,M,N,K VARIANT
+set -euo pipefail
+TAG=$1; SHAPE=$2; T=$3
+R=$GRAFT_REPO_ROOT
+OUT=$R/gpurun_out/pmc_gemm_$TAG
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp
+i=0
+for set in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
+           "SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MFMA SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_ANY SQ_INSTS_VMEM" ; do
+  i=$((i+1))
+  timeout -s KILL 90 rocprofv3 --pmc $set --output-format csv -d "$OUT/p$i" -o p \
+    -- python3 "$R/tools/exp_gemm_x6.py" --only "$SHAPE" --tiles "$T" --reps 5 > "$OUT/p$i.log" 2>&1
+done
+python3 - "$OUT" <<'PY'
+import csv, glob, sys, collections
+tot = collections.defaultdict(float); n = collections.Counter()
+for f in glob.glob(sys.argv[1] + "/p*/**/*counter_collection.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        if "gemm_x6" not in r["Kernel_Name"]:
+            continue
+        tot[r["Counter_Name"]] += float(r["Counter_Value"]); n[r["Counter_Name"]] += 1
+for k in sorted(tot):
+    print(f"{k:28s} {tot[k] / max(1, n[k]):14.1f}  (avg over {n[k]} dispatch-rows)")
+PY
