@@ -35,6 +35,7 @@ sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
 MFMA_F32_PEAK_TFLOPS = 157.3  # dense f32 MFMA (MI355X_MICROARCH.md; no xf32 on gfx950)
+MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (the matrix rate ocppo_gemm_x6 runs on)
 RIDGE = MFMA_F32_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9)  # flop/B where the two bounds meet
 # HBM bytes per launch from rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE, separate passes) of
 # the same launch shapes: tools/profile_round.sh -> tools/summarize_profiles.py
@@ -141,6 +142,21 @@ def kernel_flops(tr) -> dict:
     return fl
 
 
+def gemm_x6_shape(name: str):
+    """(M, N, K, splits, masked) of an ops.gemm_x6 timer site `gemm_x6_{M}x{N}x{K}s{S}[m]`."""
+    spec = name[len("gemm_x6_"):]
+    masked = spec.endswith("m")
+    dims, S = spec.rstrip("m").split("s")
+    M, N, K = (int(v) for v in dims.split("x"))
+    return M, N, K, int(S), masked
+
+
+def gemm_x6_bytes(name: str) -> int:
+    """A [M, K] + B [N, K] f32 in, C [splits, M, N] f32 out (+ the [M, N] mask read)."""
+    M, N, K, S, masked = gemm_x6_shape(name)
+    return 4 * (M * K + N * K + S * M * N + (M * N if masked else 0))
+
+
 def mfma_bound(flops, nbytes) -> bool:
     """Arithmetic intensity (useful flops / algorithmic bytes) above the ridge point."""
     return bool(flops) and flops / nbytes > RIDGE
@@ -153,7 +169,16 @@ def roofline_of(name, k, flops, traffic, src):
     never from Infinity-Cache hits; trainer.replay_time_us)."""
     rec = {"kernel": name, "bytes_per_launch": k["bytes"], "traffic": traffic,
            "traffic_source": src}
-    if mfma_bound(flops, k["bytes"]):
+    if name == "gemm_x6":
+        # f32 products as six bf16 piece products on the bf16 matrix cores: the MFMA work issued
+        # is 6 x the f32-equivalent flops, against the dense bf16 peak
+        f32e = flops / (k["mean_us"] * 1e-6) / 1e12
+        rec.update(bound="mfma", mean_launch_us=k["mean_us"], cache="warm",
+                   achieved=round(6 * f32e, 2), peak=MFMA_BF16_PEAK_TFLOPS, unit="TFLOP/s",
+                   frac=round(6 * f32e / MFMA_BF16_PEAK_TFLOPS, 5), flops_per_launch=6 * flops,
+                   f32_equivalent_tflops=round(f32e, 2), launches_per_iter=k["launches_per_iter"],
+                   shapes=k.get("shapes"))
+    elif mfma_bound(flops, k["bytes"]):
         ach = flops / (k["mean_us"] * 1e-6) / 1e12
         rec.update(bound="mfma", mean_launch_us=k["mean_us"], cache="warm",
                    achieved=round(ach, 2), peak=MFMA_F32_PEAK_TFLOPS, unit="TFLOP/s",
@@ -280,13 +305,14 @@ def main():
     if not opt.no_kernel_timing:
         # HBM-bound sites (no flops, or below the ridge) are also timed cold
         cold = {n for n in tr.timer.sites
-                if not mfma_bound(kf.get(n), kb.get(n) or 1)}
+                if not n.startswith("gemm_x6_") and not mfma_bound(kf.get(n), kb.get(n) or 1)}
         for name, us in tr.timer.measure(cold=cold).items():
             n = tr.timer.per_iter.get(name, 0)
             nbytes = kb.get(name) or (relu_bias_grad_bytes(name)
                                       if name.startswith("relu_bias_grad_") else
                                       relu_bias_wgrad_bytes(name)
-                                      if name.startswith("relu_bias_wgrad_") else None)
+                                      if name.startswith("relu_bias_wgrad_") else
+                                      gemm_x6_bytes(name) if name.startswith("gemm_x6_") else None)
             kernels[name] = {"mean_us": round(us, 3), "launches_per_iter": n,
                              "us_per_iter": round(us * n, 2)}
             if name in tr.timer.cold_us:
@@ -314,6 +340,24 @@ def main():
         for k in parts:
             kernels[k].pop("GBps", None)  # counted in the aggregate
             kernels[k].pop("GBps_cold", None)
+    # the update GEMMs on ocppo_gemm_x6: one kernel, a dozen launch shapes per minibatch ->
+    # total f32-equivalent flops over total time (the bf16 MFMA work issued is 6x that)
+    parts = [k for k in kernels if k.startswith("gemm_x6_") and "bytes" in kernels[k]]
+    if parts:
+        n = sum(kernels[k]["launches_per_iter"] for k in parts)
+        t = sum(kernels[k]["us_per_iter"] for k in parts)
+        b = sum(kernels[k]["bytes"] * kernels[k]["launches_per_iter"] for k in parts)
+        fl = 0
+        for k in parts:
+            M, N, K, _, _ = gemm_x6_shape(k)
+            fl += 2 * M * N * K * kernels[k]["launches_per_iter"]
+        kernels["gemm_x6"] = {"mean_us": round(t / n, 3), "launches_per_iter": n,
+                              "us_per_iter": round(t, 2), "bytes": round(b / n),
+                              "GBps": round(b / (t * 1e-6) / 1e9, 2),
+                              "shapes": sorted(k[len("gemm_x6_"):] for k in parts)}
+        kf["gemm_x6"] = fl / n
+        for k in parts:
+            kernels[k].pop("GBps", None)  # counted in the aggregate
     timed = [k for k in kernels if "GBps" in kernels[k]]
     recs = []
     for name in sorted(timed, key=lambda k: -kernels[k]["us_per_iter"]):

@@ -129,6 +129,10 @@ struct X6Stage {
     }
   }
 
+  // every wave issues the same number of loads (a counted vmcnt is per wave)
+  static constexpr bool kUniform = kPieces % NT == 0;
+
+  template <bool ASM = false>
   __device__ static void load(const float* __restrict__ src, int64_t srow, int64_t sk, int row0,
                               int k0, int t, floatx4 (&r)[kPer][4]) {
 #pragma unroll
@@ -141,7 +145,10 @@ struct X6Stage {
       for (int j = 0; j < 4; ++j) {
         const float* q = KC ? src + static_cast<int64_t>(row0 + 4 * rq + j) * srow + (k0 + 4 * kq)
                             : src + static_cast<int64_t>(k0 + 4 * kq + j) * sk + (row0 + 4 * rq);
-        r[i][j] = *reinterpret_cast<const floatx4*>(q);
+        if constexpr (ASM)  // invisible to the compiler's wait insertion: waited by x6_vmwait
+          asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r[i][j]) : "v"(q) : "memory");
+        else
+          r[i][j] = *reinterpret_cast<const floatx4*>(q);
       }
     }
   }
@@ -170,6 +177,21 @@ struct X6Stage {
   }
 };
 
+// Counted wait for inline-asm loads: vmcnt(N) (N newer loads may stay in flight), then every
+// register of the consumed set is passed through an empty asm so no use of it can be scheduled
+// before the wait.
+template <int N, int P>
+__device__ __forceinline__ void x6_vmwait(floatx4 (&r)[P][4]) {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else static_assert(N == 0 || N == 4 || N == 8, "unsupported count");
+#pragma unroll
+  for (int i = 0; i < P; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(r[i][j]));
+}
+
 __device__ __forceinline__ bf16x8 x6_frag(const unsigned char* plane, int row, int chunk) {
   return *reinterpret_cast<const bf16x8*>(plane + x6_chunk_off(row, chunk));
 }
@@ -190,8 +212,11 @@ __device__ __forceinline__ void x6_mfma6(const bf16x8 (&a)[3], const bf16x8 (&b)
 // WGM x WGN waves per workgroup, each FM x FN blocks of 16 x 16 (tile BM x BN = 16 FM WGM x
 // 16 FN WGN); LO: separate small-term accumulators (else all six products go into one); PF2: two
 // register sets, loads issued two K steps ahead (else one).
+#ifndef OCPPO_X6_OCC  // waves per SIMD the kernel is register-budgeted for (experiments)
+#define OCPPO_X6_OCC 2
+#endif
 template <int FM, int FN, int WGM, int WGN, bool AKC, bool BKC, bool LO, bool PF2>
-__global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_x6_kernel(X6Args g) {
+__global__ __launch_bounds__(64 * WGM * WGN, OCPPO_X6_OCC) void gemm_x6_kernel(X6Args g) {
   constexpr int NT = 64 * WGM * WGN;
   constexpr int BM = 16 * FM * WGM, BN = 16 * FN * WGN;
   using SA = X6Stage<BM, AKC, NT>;
@@ -276,37 +301,74 @@ __global__ __launch_bounds__(64 * WGM * WGN, 2) void gemm_x6_kernel(X6Args g) {
   } else {
     // set (ra, rb) holds even steps, (qa, qb) odd ones; at step kt the loads of step kt + 2 go
     // into the set step kt came from (already in LDS), then step kt + 1 is stashed
+    // OCPPO_X6_ASMLD: the operand loads as inline asm with counted waits (the compiler's own
+    // wait insertion loses the order of loads carried around the loop and drains the newer set
+    // at every step); measured no faster (tools/exp_gemm_x6.py), so off by default
+#ifdef OCPPO_X6_ASMLD
+    constexpr bool ASM = SA::kUniform && SB::kUniform;
+#else
+    constexpr bool ASM = false;
+#endif
+    constexpr int kLoads = 4 * (SA::kPer + SB::kPer);  // loads per step per thread
+    static_assert(!ASM || kLoads == 8, "x6_vmwait counts assume 8 loads per step");
     floatx4 qa[SA::kPer][4], qb[SB::kPer][4];
-    SA::load(A, g.sam, g.sak, m0, kb * kX6BK, t, ra);
-    SB::load(B, g.sbn, g.sbk, n0, kb * kX6BK, t, rb);
+    SA::template load<ASM>(A, g.sam, g.sak, m0, kb * kX6BK, t, ra);
+    SB::template load<ASM>(B, g.sbn, g.sbk, n0, kb * kX6BK, t, rb);
     if (nk > 1) {
-      SA::load(A, g.sam, g.sak, m0, (kb + 1) * kX6BK, t, qa);
-      SB::load(B, g.sbn, g.sbk, n0, (kb + 1) * kX6BK, t, qb);
+      SA::template load<ASM>(A, g.sam, g.sak, m0, (kb + 1) * kX6BK, t, qa);
+      SB::template load<ASM>(B, g.sbn, g.sbk, n0, (kb + 1) * kX6BK, t, qb);
+    }
+    if constexpr (ASM) {
+      if (nk > 1) {
+        x6_vmwait<8>(ra);
+        x6_vmwait<8>(rb);
+      } else {
+        x6_vmwait<0>(ra);
+        x6_vmwait<0>(rb);
+      }
     }
     SA::stash(la, t, ra);
     SB::stash(lb, t, rb);
     __syncthreads();
     auto step = [&](int kt, floatx4 (&ldA)[SA::kPer][4], floatx4 (&ldB)[SB::kPer][4],
                     floatx4 (&stA)[SA::kPer][4], floatx4 (&stB)[SB::kPer][4]) {
-      if (kt + 2 < nk) {
-        SA::load(A, g.sam, g.sak, m0, (kb + kt + 2) * kX6BK, t, ldA);
-        SB::load(B, g.sbn, g.sbk, n0, (kb + kt + 2) * kX6BK, t, ldB);
+      const bool issue = kt + 2 < nk;
+      if (issue) {
+        SA::template load<ASM>(A, g.sam, g.sak, m0, (kb + kt + 2) * kX6BK, t, ldA);
+        SB::template load<ASM>(B, g.sbn, g.sbk, n0, (kb + kt + 2) * kX6BK, t, ldB);
       }
       compute();
       __syncthreads();
       if (kt + 1 < nk) {
+        if constexpr (ASM) {  // step kt + 1's loads are older than the ones just issued
+          if (issue) {
+            x6_vmwait<8>(stA);
+            x6_vmwait<8>(stB);
+          } else {
+            x6_vmwait<0>(stA);
+            x6_vmwait<0>(stB);
+          }
+        }
         SA::stash(la, t, stA);
         SB::stash(lb, t, stB);
       }
       __syncthreads();
     };
-    for (int kt = 0; kt < nk; kt += 2) {
+    // both steps of a pair in one loop body with no branch between them (a conditional second
+    // step let the compiler fold the pair into one step with register copies, which put a
+    // vmcnt(0) before every step's loads: one step of prefetch, not two)
+    int kt = 0;
+    for (; kt + 1 < nk; kt += 2) {
       step(kt, ra, rb, qa, qb);
-      if (kt + 1 < nk) step(kt + 1, qa, qb, ra, rb);
+      step(kt + 1, qa, qb, ra, rb);
     }
+    if (kt < nk) step(kt, ra, rb, qa, qb);
   }
 
   // epilogue: MFMA result C[4 fc + r][fr] of block (i, j)
+#ifdef OCPPO_X6_ASMLD
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no inline-asm load left in flight
+#endif
   float* __restrict__ Cp = g.c + s * g.split_c;
   const int wr0 = m0 + wm * 16 * FM, wc0 = n0 + wn * 16 * FN;
   if (g.mask) {

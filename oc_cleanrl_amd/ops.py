@@ -864,11 +864,15 @@ def gemm_x6(a, sam, sak, b, sbn, sbk, c, ldc, M, N, K, splits=1, split_c=0, bias
                 or mask.dtype != torch.float32 or dbp is None):
             raise ValueError("gemm_x6: mask must be an f32 [M, N] row-major view, with dbp")
         _check(dbp, "dbp", torch.float32, dev, (M // X6_TILES[t][0]) * N)
-    call("ocppo_gemm_x6", _stream(dev), a.data_ptr(), sam, sak, b.data_ptr(), sbn, sbk,
-         c.data_ptr(), ldc, M, N, K, splits, split_c,
-         None if bias is None else _check(bias, "bias", torch.float32, dev, N), int(bool(relu)),
-         None if mask is None else mask.data_ptr(), 0 if mask is None else mask.stride(0),
-         None if dbp is None else dbp.data_ptr(), t)
+    bp = None if bias is None else _check(bias, "bias", torch.float32, dev, N)
+    args = (a.data_ptr(), sam, sak, b.data_ptr(), sbn, sbk, c.data_ptr(), ldc, M, N, K, splits,
+            split_c, bp, int(bool(relu)), None if mask is None else mask.data_ptr(),
+            0 if mask is None else mask.stride(0), None if dbp is None else dbp.data_ptr(), t)
+    # timer site name: the product's shape (bench.py's gemm_x6 roofline parses it); the closure
+    # keeps the operand tensors alive for the timer's replays
+    name = f"gemm_x6_{M}x{N}x{K}s{splits}{'m' if mask is not None else ''}"
+    keep = (a, b, c, bias, mask, dbp)
+    timed(name, lambda: call("ocppo_gemm_x6", _stream(dev), *args) or keep)
     return c
 
 
