@@ -18,4 +18,5 @@ timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeou
 echo "gpu tests done"
 timeout -k 10 300 python3 bench.py > gpurun_out/bench_line.json 2> gpurun_out/bench_line.err
 timeout -k 10 300 python3 bench.py --config 3 > gpurun_out/bench_line_config3.json 2> gpurun_out/bench_line_config3.err
+timeout -k 10 300 python3 bench.py --config 1 > gpurun_out/bench_line_config1.json 2> gpurun_out/bench_line_config1.err
 echo "bench lines done"
