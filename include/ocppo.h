@@ -307,14 +307,20 @@ OCPPO_API int ocppo_bias_act_nchw(ocppo_stream_t stream, const float* y, const f
  * whose input `mask` [M, N] (row stride ldm) is that ReLU's output): C = mask > 0 ? acc : 0
  * (threshold_backward) and dbp[tm, n] = sum of C over row tile tm (tile rows each) — that layer's
  * bias-gradient partials, [M / tile rows, N], for ocppo_sum_splits_db; splits == 1, no bias/relu.
- * tile: bits 0-1 the tile above, bit 2 loads two K steps ahead, bit 3 one accumulator for all six
- * products. Deterministic (fixed MFMA order, no atomics).
+ * ReLU bitmask (mbits: (M / tile rows) x (N / tile columns) x threads per workgroup (256, or 512
+ * for the 8-wave shapes) 64-bit words): a forward with relu writes, per tile and thread, one word
+ * of (output > 0) bits in the MFMA fragment order (mbits_out); the mask
+ * epilogue of a later dX over the same [M, N] with the same tile reads them (mbits_in, mask may
+ * then be NULL) instead of the f32 mask. tile: bits 0-2 the tile shape (0: 128 x 128, 1: 64 x
+ * 128, 2: 128 x 64, 3: 64 x 64 with 4 waves; 4-7: 8-wave forms), bit 3 loads two K steps ahead,
+ * bit 4 one accumulator for all six products. Deterministic (fixed MFMA order, no atomics).
  * ------------------------------------------------------------------------------------------- */
 OCPPO_API int ocppo_gemm_x6(ocppo_stream_t stream, const float* a, int64_t sam, int64_t sak,
                             const float* b, int64_t sbn, int64_t sbk, float* c, int64_t ldc,
                             int64_t M, int64_t N, int64_t K, int64_t splits, int64_t split_c,
                             const float* bias, int relu, const float* mask, int64_t ldm,
-                            float* dbp, int tile);
+                            float* dbp, uint64_t* mbits_out, const uint64_t* mbits_in,
+                            int tile);
 
 /* ---------------------------------------------------------------------------------------------
  * Split-K combine of a weight gradient — replaces ATen's `sum(0)` after the batched (split-K)

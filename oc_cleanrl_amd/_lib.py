@@ -92,7 +92,7 @@ SIGNATURES: dict[str, tuple[type, list]] = {
     "ocppo_q_head_epsilon_greedy": (I, [P, P, I64, I64, P, P, I64, U64, P, I64, D, D, D, P, P, P]),
     "ocppo_frames_scatter_relu": (I, [P, P, I64, I64, P, I64, P, I64, P, I64, I64, I64, P, P, P]),
     "ocppo_gemm_x6": (I, [P, P, I64, I64, P, I64, I64, P, I64, I64, I64, I64, I64, I64, P, I, P,
-                          I64, P, I]),
+                          I64, P, P, P, I]),
     "ocppo_store_linear2": (I, [P, P, P, P, I64, I64, I64, P, P, I, P, P, P, I, D, D, D, P, P, P,
                                 P, P, P, P, I64, I64, I64]),
 }

@@ -222,7 +222,11 @@ class _LinearAct(torch.autograd.Function):
             below["premasked"] = True
             ctx.below = below
         if _x6(x.shape[0], wm.shape[0], x.shape[1]) and ops.linear_x6_ok(x, wm):
-            out = ops.linear_x6(x, wm, b, relu)
+            if relu and box is not None and X6_MASK_DX:
+                # the ReLU bitmask for the next layer's fused dX epilogue (box consumer)
+                out, box["mbits"] = ops.linear_x6(x, wm, b, relu, mbits=True)
+            else:
+                out = ops.linear_x6(x, wm, b, relu)
         else:
             out = torch._addmm_activation(b, x, wm.t(), use_gelu=False) if relu else \
                 torch.addmm(b, x, wm.t())
@@ -253,7 +257,7 @@ class _LinearAct(torch.autograd.Function):
         if ctx.below is None:
             return _dx(g, w)
         x = ctx.saved_tensors[0]
-        gp, dbp = ops.dx_x6_relu(g, w, x)
+        gp, dbp = ops.dx_x6_relu(g, w, x, mbits=ctx.below.get("mbits"))
         ctx.below["dbp"] = (dbp, dbp.shape[0])  # relu_bias_grad_partial's (partials, chunks)
         return gp
 

@@ -70,6 +70,12 @@ struct X6Args {
   const float* mask;
   int64_t ldm;
   float* dbp;
+  // ReLU bitmasks in the MFMA fragment layout: bit (i FN + j) 4 + r of word [tile][thread] is
+  // element (block i, j; register r) of that thread's accumulators, > 0. A forward with a ReLU
+  // epilogue writes them (mbits_out); the next layer's dX, the same tile shape over the same
+  // [M, N], reads them (mbits_in) instead of the f32 mask: 1 bit instead of 4 B per element.
+  uint64_t* mbits_out;
+  const uint64_t* mbits_in;
 };
 
 // The three bf16 pieces of an f32 pair (exact: x == x0 + x1 + x2 for finite normal x), packed:
@@ -371,9 +377,11 @@ __global__ __launch_bounds__(64 * WGM * WGN, OCPPO_X6_OCC) void gemm_x6_kernel(X
 #endif
   float* __restrict__ Cp = g.c + s * g.split_c;
   const int wr0 = m0 + wm * 16 * FM, wc0 = n0 + wn * 16 * FN;
-  if (g.mask) {
+  const int64_t tile_id = static_cast<int64_t>(tm) * g.tiles_n + tn;
+  if (g.mask || g.mbits_in) {
     // threshold_backward(acc, mask, 0) and the tile's column sums: rows of a lane (i, r) in
     // order, then the wave's 4 row groups (xor 16, 32), then the two wave rows through LDS
+    const uint64_t bits = g.mbits_in ? g.mbits_in[tile_id * NT + t] : 0;
     float colsum[FN];
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
@@ -385,7 +393,9 @@ __global__ __launch_bounds__(64 * WGM * WGN, OCPPO_X6_OCC) void gemm_x6_kernel(X
         for (int r = 0; r < 4; ++r) {
           const int64_t row = wr0 + 16 * i + 4 * fc + r;
           const float acc = LO ? hi[i][j][r] + lo[LO ? i : 0][LO ? j : 0][r] : hi[i][j][r];
-          const float v = g.mask[row * g.ldm + col] > 0.f ? acc : 0.f;
+          const bool on = g.mbits_in ? ((bits >> ((i * FN + j) * 4 + r)) & 1) != 0
+                                     : g.mask[row * g.ldm + col] > 0.f;
+          const float v = on ? acc : 0.f;
           Cp[row * g.ldc + col] = v;
           cs += v;
         }
@@ -412,6 +422,8 @@ __global__ __launch_bounds__(64 * WGM * WGN, OCPPO_X6_OCC) void gemm_x6_kernel(X
     }
     return;
   }
+  static_assert(FM * FN * 4 <= 64, "one 64-bit mask word per thread and tile");
+  uint64_t bits = 0;
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
     const int col = wc0 + 16 * j + fr;
@@ -425,9 +437,11 @@ __global__ __launch_bounds__(64 * WGM * WGN, OCPPO_X6_OCC) void gemm_x6_kernel(X
         if (g.bias) v += bv;
         if (g.relu) v = fmaxf(v, 0.f);
         Cp[row * g.ldc + col] = v;
+        bits |= static_cast<uint64_t>(v > 0.f) << ((i * FN + j) * 4 + r);
       }
     }
   }
+  if (g.mbits_out) g.mbits_out[tile_id * NT + t] = bits;
 }
 
 template <int FM, int FN, int WGM, int WGN, bool LO, bool PF2>
@@ -490,7 +504,8 @@ extern "C" int ocppo_gemm_x6(ocppo_stream_t stream, const float* a, int64_t sam,
                              const float* b, int64_t sbn, int64_t sbk, float* c, int64_t ldc,
                              int64_t M, int64_t N, int64_t K, int64_t splits, int64_t split_c,
                              const float* bias, int relu,
-                             const float* mask, int64_t ldm, float* dbp, int tile) {
+                             const float* mask, int64_t ldm, float* dbp, uint64_t* mbits_out,
+                             const uint64_t* mbits_in, int tile) {
   OCPPO_REQUIRE(M >= 1 && N >= 1 && K >= 1 && splits >= 1 && M <= INT32_MAX && N <= INT32_MAX &&
                     K <= INT32_MAX,
                 "ocppo_gemm_x6: bad sizes M=%lld N=%lld K=%lld splits=%lld", (long long)M,
@@ -516,12 +531,16 @@ extern "C" int ocppo_gemm_x6(ocppo_stream_t stream, const float* a, int64_t sam,
                 (long long)M, (long long)N, (long long)bm, (long long)bn);
   OCPPO_REQUIRE(splits == 1 || (bias == nullptr && !relu),
                 "ocppo_gemm_x6: bias / ReLU epilogues need splits == 1");
-  OCPPO_REQUIRE(mask == nullptr || (splits == 1 && bias == nullptr && !relu && dbp && ldm >= N),
+  OCPPO_REQUIRE((mask == nullptr && mbits_in == nullptr) ||
+                    (splits == 1 && bias == nullptr && !relu && dbp &&
+                     (mbits_in != nullptr || ldm >= N)),
                 "ocppo_gemm_x6: the mask epilogue needs splits == 1, no bias / ReLU, dbp, ldm >= N");
+  OCPPO_REQUIRE(mbits_out == nullptr || (splits == 1 && mask == nullptr && mbits_in == nullptr),
+                "ocppo_gemm_x6: mbits_out needs splits == 1 and no mask epilogue");
   const int64_t units = splits * (M / bm) * (N / bn);
   OCPPO_REQUIRE(units <= INT32_MAX / 2, "ocppo_gemm_x6: too large");
   X6Args g{a, sam, sak, b, sbn, sbk, c, ldc, bias, relu ? 1 : 0, (int)M, (int)N, (int)K,
-           0, 0, (int)units, (int)splits, split_c, mask, ldm, dbp};
+           0, 0, (int)units, (int)splits, split_c, mask, ldm, dbp, mbits_out, mbits_in};
   clear_stale_error();
   hipStream_t s = as_stream(stream);
   const bool akc = sak == 1, bkc = sbk == 1;

@@ -852,8 +852,14 @@ def _x6_operand_ok(t) -> bool:
             and t.stride(1) == 1 and t.stride(0) % 4 == 0)
 
 
+def x6_mbits_words(M: int, N: int, tile: int) -> int:
+    """64-bit words of a gemm_x6 ReLU bitmask over an [M, N] output with `tile`."""
+    bm, bn = X6_TILES[tile]
+    return (M // bm) * (N // bn) * (512 if (tile & 7) >= 4 else 256)
+
+
 def gemm_x6(a, sam, sak, b, sbn, sbk, c, ldc, M, N, K, splits=1, split_c=0, bias=None,
-            relu=False, mask=None, dbp=None, tile=None):
+            relu=False, mask=None, dbp=None, tile=None, mbits_out=None, mbits_in=None):
     """Raw ocppo_gemm_x6 call on tensors a, b, c (their data pointers; strides as given)."""
     t = x6_tile(M, N, splits, tile)
     if t is None:
@@ -863,15 +869,22 @@ def gemm_x6(a, sam, sak, b, sbn, sbk, c, ldc, M, N, K, splits=1, split_c=0, bias
         if (mask.dim() != 2 or tuple(mask.shape) != (M, N) or mask.stride(1) != 1
                 or mask.dtype != torch.float32 or dbp is None):
             raise ValueError("gemm_x6: mask must be an f32 [M, N] row-major view, with dbp")
+    if mask is not None or mbits_in is not None:
         _check(dbp, "dbp", torch.float32, dev, (M // X6_TILES[t][0]) * N)
+    for mb in (mbits_out, mbits_in):
+        if mb is not None:
+            _check(mb, "mbits", torch.int64, dev, x6_mbits_words(M, N, t))
     bp = None if bias is None else _check(bias, "bias", torch.float32, dev, N)
     args = (a.data_ptr(), sam, sak, b.data_ptr(), sbn, sbk, c.data_ptr(), ldc, M, N, K, splits,
             split_c, bp, int(bool(relu)), None if mask is None else mask.data_ptr(),
-            0 if mask is None else mask.stride(0), None if dbp is None else dbp.data_ptr(), t)
+            0 if mask is None else mask.stride(0), None if dbp is None else dbp.data_ptr(),
+            None if mbits_out is None else mbits_out.data_ptr(),
+            None if mbits_in is None else mbits_in.data_ptr(), t)
     # timer site name: the product's shape (bench.py's gemm_x6 roofline parses it); the closure
     # keeps the operand tensors alive for the timer's replays
-    name = f"gemm_x6_{M}x{N}x{K}s{splits}{'m' if mask is not None else ''}"
-    keep = (a, b, c, bias, mask, dbp)
+    masked = mask is not None or mbits_in is not None
+    name = f"gemm_x6_{M}x{N}x{K}s{splits}{'m' if masked else ''}"
+    keep = (a, b, c, bias, mask, dbp, mbits_out, mbits_in)
     timed(name, lambda: call("ocppo_gemm_x6", _stream(dev), *args) or keep)
     return c
 
@@ -882,13 +895,20 @@ def linear_x6_ok(x, w) -> bool:
             and x.shape[1] % 32 == 0 and x6_tile(x.shape[0], w.shape[0]) is not None)
 
 
-def linear_x6(x, w, b=None, relu=False, out=None):
-    """act(x W^T + b) (torch._addmm_activation's order: sum, + bias, then ReLU)."""
+def linear_x6(x, w, b=None, relu=False, out=None, mbits=False):
+    """act(x W^T + b) (torch._addmm_activation's order: sum, + bias, then ReLU). mbits=True
+    (with relu) also returns the output's ReLU bitmask (tensor, tile) for dx_x6_relu."""
     M, K = x.shape
     N = w.shape[0]
     out = torch.empty((M, N), dtype=torch.float32, device=x.device) if out is None else out
-    return gemm_x6(x, x.stride(0), 1, w, w.stride(0), 1, out, out.stride(0), M, N, K, bias=b,
-                   relu=relu)
+    if not mbits:
+        return gemm_x6(x, x.stride(0), 1, w, w.stride(0), 1, out, out.stride(0), M, N, K, bias=b,
+                       relu=relu)
+    t = x6_tile(M, N)
+    bits = torch.empty(x6_mbits_words(M, N, t), dtype=torch.int64, device=x.device)
+    gemm_x6(x, x.stride(0), 1, w, w.stride(0), 1, out, out.stride(0), M, N, K, bias=b,
+            relu=relu, tile=t, mbits_out=bits)
+    return out, (bits, t)
 
 
 def dx_x6_ok(g, w) -> bool:
@@ -904,16 +924,21 @@ def dx_x6(g, w, out=None):
     return gemm_x6(g, g.stride(0), 1, w, 1, w.stride(0), out, out.stride(0), M, K, N)
 
 
-def dx_x6_relu(g, w, mask):
+def dx_x6_relu(g, w, mask, mbits=None):
     """gp = threshold_backward(g W, mask, 0) for the Linear+ReLU layer below whose output is
     `mask` [M, K], with that layer's bias-gradient partials: returns (gp, dbp [M / tile rows, K])
-    (dbp summed in row-tile order by sum_splits_db)."""
+    (dbp summed in row-tile order by sum_splits_db). mbits = (bitmask, tile) from that layer's
+    linear_x6(..., mbits=True): read instead of the f32 mask when this product has the same tile."""
     M, N = g.shape
     K = w.shape[1]
     t = x6_tile(M, K)
     gp = torch.empty((M, K), dtype=torch.float32, device=g.device)
     dbp = torch.empty((M // X6_TILES[t][0], K), dtype=torch.float32, device=g.device)
-    gemm_x6(g, g.stride(0), 1, w, 1, w.stride(0), gp, K, M, K, N, mask=mask, dbp=dbp, tile=t)
+    if mbits is not None and mbits[1] == t:
+        gemm_x6(g, g.stride(0), 1, w, 1, w.stride(0), gp, K, M, K, N, dbp=dbp, tile=t,
+                mbits_in=mbits[0])
+    else:
+        gemm_x6(g, g.stride(0), 1, w, 1, w.stride(0), gp, K, M, K, N, mask=mask, dbp=dbp, tile=t)
     return gp, dbp
 
 

@@ -138,3 +138,35 @@ def test_dx_mask_epilogue(tile):
     assert torch.allclose(dbp.double(), ps, rtol=1e-5, atol=1e-5)
     gp2, dbp2 = ops.dx_x6_relu(gg, w, out)
     assert torch.equal(gp2, gp if ops.x6_tile(M, K) == tile else gp2)
+
+
+@pytest.mark.parametrize("tile", [24, 25, 0])
+def test_relu_bitmask_roundtrip(tile):
+    # forward with ReLU writes the fragment-order bitmask; the dX mask epilogue over the same
+    # [M, N] with the same tile reads it: identical to the f32-mask epilogue
+    g = torch.Generator(device=DEV).manual_seed(33)
+    M, K0, N, N2 = 512, 256, 256, 128  # layer L: x [M, K0] -> h [M, N]; layer L+1: N -> N2
+    x = _rand(M, K0, gen=g)
+    w = _rand(N, K0, gen=g, scale=K0 ** -0.5)
+    b = _rand(N, gen=g, scale=0.1)
+    h = torch.empty(M, N, device=DEV)
+    bits = torch.empty(ops.x6_mbits_words(M, N, tile), dtype=torch.int64, device=DEV)
+    ops.gemm_x6(x, K0, 1, w, K0, 1, h, N, M, N, K0, bias=b, relu=True, tile=tile, mbits_out=bits)
+    h_ref = torch.empty_like(h)
+    ops.gemm_x6(x, K0, 1, w, K0, 1, h_ref, N, M, N, K0, bias=b, relu=True, tile=tile)
+    assert torch.equal(h, h_ref)
+    gg = _rand(M, N2, gen=g)
+    w2 = _rand(N2, N, gen=g, scale=N2 ** -0.5)
+    bm = ops.X6_TILES[tile][0]
+    gp_f, dbp_f = torch.empty(M, N, device=DEV), torch.empty(M // bm, N, device=DEV)
+    gp_b, dbp_b = torch.empty(M, N, device=DEV), torch.empty(M // bm, N, device=DEV)
+    ops.gemm_x6(gg, N2, 1, w2, 1, N, gp_f, N, M, N, N2, mask=h, dbp=dbp_f, tile=tile)
+    ops.gemm_x6(gg, N2, 1, w2, 1, N, gp_b, N, M, N, N2, dbp=dbp_b, tile=tile, mbits_in=bits)
+    assert torch.equal(gp_f, gp_b) and torch.equal(dbp_f, dbp_b)
+    assert bool((gp_b[h <= 0] == 0).all())
+    # the helpers: linear_x6(mbits=True) -> dx_x6_relu(mbits=...)
+    y, mb = ops.linear_x6(x, w, b, relu=True, mbits=True)
+    assert torch.equal(y, h_ref if mb[1] == tile else y)
+    gp2, _ = ops.dx_x6_relu(gg, w2, y, mbits=mb)
+    gp3, _ = ops.dx_x6_relu(gg, w2, y)
+    assert torch.equal(gp2, gp3)

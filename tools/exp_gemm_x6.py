@@ -103,8 +103,15 @@ def main():
         torch.cuda.synchronize()
         t_err = err(ct, ref, scale)
         t_us = dev_time_us(tfn, a.reps)
+        # the library's own bf16 GEMM of the same shape (one product, bf16 out): the efficiency
+        # a plain bf16 GEMM reaches here, x6 issues six of them
+        xa = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+        xb = torch.randn(N, K, device=dev, dtype=torch.bfloat16)
+        b16_us = dev_time_us(lambda: torch.mm(xa, xb.t()), a.reps)
         rec = {"kind": kind, "M": M, "N": N, "K": K, "torch_us": round(t_us, 2),
-               "torch_tf": round(flops / t_us / 1e6, 1), "torch_err": t_err, "ours": {}}
+               "torch_tf": round(flops / t_us / 1e6, 1), "torch_err": t_err,
+               "bf16_lib_us": round(b16_us, 2), "bf16_lib_tf": round(flops / b16_us / 1e6, 1),
+               "ours": {}}
         best = None
         for t in tiles:
             if not shape_ok(t):
