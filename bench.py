@@ -152,9 +152,10 @@ def gemm_x6_shape(name: str):
 
 
 def gemm_x6_bytes(name: str) -> int:
-    """A [M, K] + B [N, K] f32 in, C [splits, M, N] f32 out (+ the [M, N] mask read)."""
+    """A [M, K] + B [N, K] f32 in, C [splits, M, N] f32 out (+ the [M, N] ReLU bitmask read,
+    1 bit per element, and the bias-gradient partials written, in the masked dX form)."""
     M, N, K, S, masked = gemm_x6_shape(name)
-    return 4 * (M * K + N * K + S * M * N + (M * N if masked else 0))
+    return 4 * (M * K + N * K + S * M * N) + ((M * N) // 8 + 4 * N * (M // 128) if masked else 0)
 
 
 def mfma_bound(flops, nbytes) -> bool:

@@ -1,0 +1,57 @@
+"""Host-side choices of the update GEMM path (no GPU): which config-2 products run on
+ocppo_gemm_x6, with which tile and row split (agents._x6 / _x6_dw / _x6_splits, ops.x6_tile), and
+the bench's parsing of the gemm_x6 timer sites. The measurements behind the rules are
+profiles/r03/exp_gemm_x6*.jsonl."""
+import bench
+from oc_cleanrl_amd import agents, ops
+
+# config 2's update products per minibatch: encoder at the dedup capacity (11520 frames),
+# decoder at the minibatch (4096); (M, N_out, K_in) of each Linear
+LAYERS = {"L2": (11520, 512, 256), "L3": (11520, 1024, 512), "L4": (11520, 512, 1024),
+          "dec": (4096, 512, 2048)}
+
+
+def test_forward_and_dx_gating_matches_the_measurements():
+    on = {k: agents._x6(M, N, K) for k, (M, N, K) in LAYERS.items()}
+    # forward [M, N]: the decoder's 128 tiles of 128 x 128 stay on hipBLASLt (79 vs 62 us)
+    assert on == {"L2": True, "L3": True, "L4": True, "dec": False}
+    # dX [M, K] = g [M, N] W: the second layer's [11520 x 256] stays on hipBLASLt
+    dx = {k: agents._x6(M, K, N) for k, (M, N, K) in LAYERS.items()}
+    assert dx == {"L2": False, "L3": True, "L4": True, "dec": True}
+
+
+def test_weight_grad_gating_and_split():
+    dw = {k: agents._x6_dw(N, K, M) for k, (M, N, K) in LAYERS.items()}
+    assert dw == {"L2": False, "L3": True, "L4": True, "dec": True}
+    # 128 x 128 tiles (variant 24) with the fewest splits reaching two workgroups per CU
+    assert agents._x6_splits(11520, 1024, 512) == (16, 24)
+    assert agents._x6_splits(11520, 512, 1024) == (16, 24)
+    assert agents._x6_splits(4096, 512, 2048) == (8, 24)
+    assert agents._x6_splits(100, 512, 512) is None  # rows not a multiple of 32
+
+
+def test_tile_choice():
+    assert ops.X6_AUTO == 24 and ops.X6_TILES[24] == (128, 128)
+    assert ops.x6_tile(11520, 1024) == 24  # 720 tiles
+    assert ops.x6_tile(11520, 512) == 24  # 360 >= 256
+    assert ops.x6_tile(4096, 512) == 25  # 128 tiles of 128 x 128 -> 64 x 128 (256)
+    assert ops.x6_tile(96, 128) is None
+    assert ops.x6_tile(512, 1024, 16) == 24
+    assert ops.x6_tile(128, 128, 1, 3) == 3 and ops.x6_tile(96, 128, 1, 3) is None
+    for t in ops.X6_BUILT:
+        assert 0 <= t < 32
+
+
+def test_mbits_words():
+    # one 64-bit word per thread and tile: 720 tiles x 256 threads at [11520 x 1024]
+    assert ops.x6_mbits_words(11520, 1024, 24) == 720 * 256
+    assert ops.x6_mbits_words(128, 128, 28) == 512  # 8-wave shape: 512 threads
+
+
+def test_bench_parses_gemm_sites():
+    assert bench.gemm_x6_shape("gemm_x6_11520x1024x512s1m") == (11520, 1024, 512, 1, True)
+    assert bench.gemm_x6_shape("gemm_x6_512x1024x11520s16") == (512, 1024, 11520, 16, False)
+    M, N, K = 11520, 1024, 512
+    assert bench.gemm_x6_bytes("gemm_x6_11520x1024x512s1") == 4 * (M * K + N * K + M * N)
+    assert bench.gemm_x6_bytes("gemm_x6_11520x1024x512s1m") == (
+        4 * (M * K + N * K + M * N) + M * N // 8 + 4 * N * (M // 128))
