@@ -71,6 +71,10 @@ SIZES = {
     # the rollout store of step t-1 + the first two encoder layers of step t (F=12 -> 256 -> 512)
     "store_encode": {"config": dict(N=128, W=4, F=12, N1=256, N2=512),
                      "scaled": dict(N=8192, W=4, F=12, N1=256, N2=512)},
+    # the update GEMM on the bf16 matrix cores (exact-split f32): the middle encoder layer's
+    # forward at the dedup capacity (x [11520, 512] -> [11520, 1024], bias + ReLU) and a large
+    # square-ish product
+    "gemm_x6": {"config": dict(M=11520, N=1024, K=512), "scaled": dict(M=8192, N=8192, K=4096)},
 }
 
 # useful flops per launch of the MFMA kernels (2 per multiply-add)
@@ -78,6 +82,8 @@ FLOPS = {
     "cache_linear": lambda p: 2 * p["M"] * p["K"] * p["E"],
     "decoder": lambda p: 2 * p["M"] * p["K"] * p["N"],
     "encoder_mid": lambda p: 2 * p["M"] * p["K"] * p["N"],
+    # f32-equivalent flops (the bf16 MFMA work issued is 6x)
+    "gemm_x6": lambda p: 2 * p["M"] * p["K"] * p["N"],
     "store_encode": lambda p: 2 * p["N"] * (p["F"] * p["N1"] + p["N1"] * p["N2"]),
 }
 
@@ -140,6 +146,9 @@ def case_bytes(name: str, p: dict) -> float:
     if name == "relu_bias_wgrad":
         R, N, K = p["R"], p["N"], p["K"]
         return R * N * 8 + R * K * 4 + N * (K + 1) * 4
+    if name == "gemm_x6":  # x, W (+ bias) in, y out
+        M, N, K = p["M"], p["N"], p["K"]
+        return 4 * (M * K + N * (K + 1) + M * N)
     raise KeyError(name)
 
 
@@ -344,6 +353,14 @@ def make_case(name: str, p: dict, dev):
         dw, db = torch.empty(N, K, device=dev), torch.empty(N, device=dev)
         fn = lambda: ops.relu_bias_wgrad(gg, out, x, dw, db)  # noqa: E731
         return fn, R * N * 8 + R * K * 4 + N * (K + 1) * 4
+    if name == "gemm_x6":
+        M, N, K = p["M"], p["N"], p["K"]
+        x = torch.rand(M, K, device=dev, generator=g) * 2 - 1
+        w = (torch.rand(N, K, device=dev, generator=g) * 2 - 1) / K ** 0.5
+        b = torch.randn(N, device=dev, generator=g) * 0.1
+        y = torch.empty(M, N, device=dev)
+        fn = lambda: ops.linear_x6(x, w, b, relu=True, out=y)  # noqa: E731
+        return fn, case_bytes(name, p)
     raise KeyError(name)
 
 

@@ -38,6 +38,7 @@ KERNEL_SUBSTR = {
     "store_encode": ("store_linear2_kernel",),
     "decoder": ("linear_rows_kernel",),
     "encoder_mid": ("linear_rows_kernel",),
+    "gemm_x6": ("gemm_x6_kernel",),
 }
 
 
