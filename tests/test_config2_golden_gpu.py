@@ -4,9 +4,11 @@ tests/golden/update_config2.npz is the reference's GAE block (ppo_atari_oc.py:53
 minibatch updates of 4096 through its update block (:566-610) on PPObj(encoder (256, 512, 1024,
 512), decoder (512,)) over a rollout-structured 128 x 128 Pong-obj batch (gen_golden.py
 gen_update_config2). Here the fixture is loaded into PPOTrainer's own HBM buffers and run through
-exactly the path bench.py times: frame-dedup gather fused with the first encoder layer, hipBLASLt
-under the shipped solution table, frame scatter with the last encoder ReLU, deferred bias grads,
-heads forward + loss + heads backward in one HIP op at H = 512, FlatAdam (clip + Adam).
+exactly the path bench.py times: frame-dedup gather fused with the first encoder layer, the
+update GEMMs on the bf16 matrix cores as exact-split f32 (ocppo_gemm_x6, the ReLU backward of the
+layer below fused into each dX) and hipBLASLt under the shipped solution table for the rest (and,
+with x6_gemm off, for all of them), frame scatter with the last encoder ReLU, deferred bias
+grads, heads forward + loss + heads backward in one HIP op at H = 512, FlatAdam (clip + Adam).
 """
 import numpy as np
 import pytest
@@ -87,14 +89,18 @@ def test_config2_gae_matches_reference(dev, fixture):
     assert np.array_equal(tr.returns.cpu().numpy().reshape(-1), z["returns"])
 
 
-def test_config2_update_chain_matches_reference(dev, fixture):
+@pytest.mark.parametrize("x6", [True, False])
+def test_config2_update_chain_matches_reference(dev, fixture, x6):
     """Two minibatch updates of the bench's chain vs the reference's update block at config 2:
     grad norms to 1e-5, loss scalars to 1e-4, and every parameter (4096 fixed samples of the
     large ones) within 1 % of one Adam step (lr) -- Adam's m / (sqrt(v) + eps) is sensitive to
     the f32 summation order of a gradient element only where |g| ~ eps. (Graph replay of this
     chain is bitwise the eager run: test_trainer_gpu.py::test_graph_replay_matches_eager.)"""
+    from oc_cleanrl_amd import ops
+    from oc_cleanrl_amd.trainer import KernelTimer
+
     z = fixture
-    tr = config2_trainer(dev, z)
+    tr = config2_trainer(dev, z, x6_gemm=x6)
     assert tr.frame_dedup and tr.fused_heads_loss and tr.direct_grads and tr.H == 512
     assert tr.gemm_table and tr.args.gemm_table
     tr.advantages.view(-1).copy_(torch.from_numpy(z["advantages"]).to(dev))
@@ -104,36 +110,51 @@ def test_config2_update_chain_matches_reference(dev, fixture):
     M = int(z["M"])
     assert tr.M == M
     params = dict(tr.agent.named_parameters())
-    for j in range(2):
-        tr._forward_backward(j)
-        gn = float(torch.linalg.vector_norm(tr.grad_buf.double()))
-        # the gradients the reference's Adam saw (after clip_grad_norm_: x max_norm / (norm +
-        # 1e-6)), per tensor, at the fixture's sample points, relative to the tensor's largest
-        coef = min(1.0, 0.5 / (gn + 1e-6))
-        gerr = {}
-        for k, p in params.items():
-            g = p.grad.detach().double().cpu().reshape(-1) * coef
-            if f"pick::{k}" in z:
-                g = g[torch.from_numpy(z[f"pick::{k}"])]
-            ref = torch.from_numpy(z[f"grad{j}::{k}"]).double().reshape(-1)
-            gerr[k] = float((g - ref).abs().max()) / float(z[f"gnorm{j}::{k}"][1])
-        print(f"minibatch {j}: grad norm {gn:.7g} vs {z['grad_norms'][j]:.7g}; worst relative "
-              f"grad error per tensor: " + ", ".join(f"{k} {e:.2g}" for k, e in gerr.items()))
-        tr._opt_step()
-        torch.cuda.synchronize()
-        st = tr.stats[j].cpu().numpy()
-        ref = z["stats"][j]
-        np.testing.assert_allclose(st, ref, rtol=1e-4, atol=1e-6, err_msg=f"stats mb {j}")
-        assert abs(gn - z["grad_norms"][j]) <= 1e-4 * z["grad_norms"][j], (j, gn)
-        assert max(gerr.values()) <= 1e-3, gerr
-        worst = 0.0
-        for k, p in params.items():
-            got = p.detach().cpu().reshape(-1)
-            if f"pick::{k}" in z:
-                got = got[torch.from_numpy(z[f"pick::{k}"])]
-            ref = torch.from_numpy(z[f"sd{j + 1}::{k}"]).reshape(-1)
-            err = (got - ref).abs()
-            worst = max(worst, float(err.max()))
-            assert float(err.max()) <= 0.01 * LR, (j, k, float(err.max()))
-            assert float((err > 2e-7).float().mean()) < 0.01, (j, k)
-        print(f"minibatch {j}: worst |param - ref| = {worst:.3g} ({worst / LR:.3g} lr)")
+    timer = KernelTimer(enabled=True)  # records which launch sites the chain runs
+    ops.TIMER = timer
+    try:
+        for j in range(2):
+            _minibatch(tr, z, j, params)
+    finally:
+        ops.TIMER = None
+        from oc_cleanrl_amd import agents
+        agents.X6_GEMM = agents.X6_MASK_DX = True  # the trainer set the process-wide default
+    x6_sites = sorted(n for n in timer.sites if n.startswith("gemm_x6_"))
+    # on: the nine x6 products of config 2 (forward, masked / plain dX, split-K dW); off: none
+    assert (len(x6_sites) >= 8) if x6 else not x6_sites, x6_sites
+
+
+def _minibatch(tr, z, j, params):
+    """One minibatch of the chain against the fixture's grads, stats and parameters."""
+    tr._forward_backward(j)
+    gn = float(torch.linalg.vector_norm(tr.grad_buf.double()))
+    # the gradients the reference's Adam saw (after clip_grad_norm_: x max_norm / (norm +
+    # 1e-6)), per tensor, at the fixture's sample points, relative to the tensor's largest
+    coef = min(1.0, 0.5 / (gn + 1e-6))
+    gerr = {}
+    for k, p in params.items():
+        g = p.grad.detach().double().cpu().reshape(-1) * coef
+        if f"pick::{k}" in z:
+            g = g[torch.from_numpy(z[f"pick::{k}"])]
+        ref = torch.from_numpy(z[f"grad{j}::{k}"]).double().reshape(-1)
+        gerr[k] = float((g - ref).abs().max()) / float(z[f"gnorm{j}::{k}"][1])
+    print(f"minibatch {j}: grad norm {gn:.7g} vs {z['grad_norms'][j]:.7g}; worst relative "
+          f"grad error per tensor: " + ", ".join(f"{k} {e:.2g}" for k, e in gerr.items()))
+    tr._opt_step()
+    torch.cuda.synchronize()
+    st = tr.stats[j].cpu().numpy()
+    ref = z["stats"][j]
+    np.testing.assert_allclose(st, ref, rtol=1e-4, atol=1e-6, err_msg=f"stats mb {j}")
+    assert abs(gn - z["grad_norms"][j]) <= 1e-4 * z["grad_norms"][j], (j, gn)
+    assert max(gerr.values()) <= 1e-3, gerr
+    worst = 0.0
+    for k, p in params.items():
+        got = p.detach().cpu().reshape(-1)
+        if f"pick::{k}" in z:
+            got = got[torch.from_numpy(z[f"pick::{k}"])]
+        ref = torch.from_numpy(z[f"sd{j + 1}::{k}"]).reshape(-1)
+        err = (got - ref).abs()
+        worst = max(worst, float(err.max()))
+        assert float(err.max()) <= 0.01 * LR, (j, k, float(err.max()))
+        assert float((err > 2e-7).float().mean()) < 0.01, (j, k)
+    print(f"minibatch {j}: worst |param - ref| = {worst:.3g} ({worst / LR:.3g} lr)")
