@@ -451,6 +451,12 @@ def main():
                        "torch_deterministic": args.torch_deterministic,
                        "gemm_table": (str(gemm_table.TABLE.relative_to(ROOT))
                                       if tr.gemm_table else None),
+                       "update_gemm": ("ocppo_gemm_x6: f32 operands split exactly into three "
+                                       "bf16 pieces, six piece products accumulated in f32 on "
+                                       "the bf16 matrix cores (error vs f64 at or below "
+                                       "hipBLASLt's f32 GEMM, tests/test_gemm_gpu.py); "
+                                       "products it does not tile on hipBLASLt f32"
+                                       if args.x6_gemm else "hipBLASLt f32"),
                        **({"deviation": "torch_deterministic=False (reference default True): "
                            "MIOpen's deterministic convolution algorithms are naive kernels on "
                            "gfx950, 83x slower (1875 vs 22.5 ms per iteration at 16 envs, "
