@@ -313,7 +313,12 @@ OCPPO_API int ocppo_bias_act_nchw(ocppo_stream_t stream, const float* y, const f
  * epilogue of a later dX over the same [M, N] with the same tile reads them (mbits_in, mask may
  * then be NULL) instead of the f32 mask. tile: bits 0-2 the tile shape (0: 128 x 128, 1: 64 x
  * 128, 2: 128 x 64, 3: 64 x 64 with 4 waves; 4-7: 8-wave forms), bit 3 loads two K steps ahead,
- * bit 4 one accumulator for all six products. Deterministic (fixed MFMA order, no atomics).
+ * bit 4 one accumulator for all six products. tile 56 (bit 5: mixed tiles; splits == 1): rows
+ * [0, mbig) in 128 x 128 tiles dispatched first, rows [mbig, M) in 64 x 128 tiles — mbig chosen
+ * by the library (one 128 x 128 tile per CU when the output holds 257..384 of them, else all of
+ * M); M, N multiples of 64 x 128, and dbp rows / mbits words counted as for 64 x 128 (a 128-row
+ * tile's dbp partial sits in the first of its two rows, the second is written as zeros).
+ * Deterministic (fixed MFMA order, no atomics).
  * ------------------------------------------------------------------------------------------- */
 OCPPO_API int ocppo_gemm_x6(ocppo_stream_t stream, const float* a, int64_t sam, int64_t sak,
                             const float* b, int64_t sbn, int64_t sbk, float* c, int64_t ldc,

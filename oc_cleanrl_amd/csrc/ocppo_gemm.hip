@@ -44,6 +44,9 @@
 //     their A row tile, so each XCD's L2 holds what its CUs share.
 // Roofline: MFMA-bound (6 bf16 MFMA passes per f32 multiply-add: 12 M N K bf16 flops against
 // the 2.5 PFLOP/s dense bf16 peak).
+#include <algorithm>
+#include <cstdlib>
+
 #include "ocppo_common.h"
 
 namespace ocppo {
@@ -76,6 +79,17 @@ struct X6Args {
   // [M, N], reads them (mbits_in) instead of the f32 mask: 1 bit instead of 4 B per element.
   uint64_t* mbits_out;
   const uint64_t* mbits_in;
+  // mixed tiles (variant bit 5): rows [0, mbig) in 128 x 128 tiles, dispatched first, the rest
+  // in 64 x 128 tiles; dbp rows and mask words are then counted in 64-row tiles
+  int mbig;
+};
+
+// Where one tile's outputs go: its row tiles start at row0_base, its dbp partial row is
+// db_base + db_mult tm (db_mult 2: the second of the two 64-row partials is written as zeros),
+// its mask words at (id_base + tile id) x threads
+struct X6Place {
+  int tiles_m, row0_base, db_base, db_mult;
+  int64_t id_base;
 };
 
 // The three bf16 pieces of an f32 pair (exact: x == x0 + x1 + x2 for finite normal x), packed:
@@ -221,26 +235,32 @@ __device__ __forceinline__ void x6_mfma6(const bf16x8 (&a)[3], const bf16x8 (&b)
 #ifndef OCPPO_X6_OCC  // waves per SIMD the kernel is register-budgeted for (experiments)
 #define OCPPO_X6_OCC 2
 #endif
+template <int FM, int FN, int WGM, int WGN, bool AKC, bool BKC>
+constexpr int x6_lds_bytes() {
+  return 3 * X6Stage<16 * FM * WGM, AKC, 64 * WGM * WGN>::kPlane +
+         3 * X6Stage<16 * FN * WGN, BKC, 64 * WGM * WGN>::kPlane;
+}
+
+// XCD-aware bijective remap of workgroups [0, nb): workgroups b, b + 8, ... share an XCD; XCD x
+// gets units [start(x), start(x) + count(x)) in order
+__device__ __forceinline__ int x6_remap(int b, int nb) {
+  const int xcd = b & 7, q = nb >> 3, rr = nb & 7;
+  return (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (b >> 3);
+}
+
+// One output tile (unit u: split u / (tiles_m tiles_n), then row-major tiles) of the product
 template <int FM, int FN, int WGM, int WGN, bool AKC, bool BKC, bool LO, bool PF2>
-__global__ __launch_bounds__(64 * WGM * WGN, OCPPO_X6_OCC) void gemm_x6_kernel(X6Args g) {
+__device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int u, X6Place pl_) {
   constexpr int NT = 64 * WGM * WGN;
   constexpr int BM = 16 * FM * WGM, BN = 16 * FN * WGN;
   using SA = X6Stage<BM, AKC, NT>;
   using SB = X6Stage<BN, BKC, NT>;
-  __shared__ __attribute__((aligned(16))) unsigned char lds[3 * SA::kPlane + 3 * SB::kPlane];
   unsigned char* la = lds;
   unsigned char* lb = lds + 3 * SA::kPlane;
-
-  // XCD-aware bijective remap: workgroups b, b + 8, ... share an XCD; XCD x gets units
-  // [start(x), start(x) + count(x)) in order
-  const int nb = gridDim.x, b = blockIdx.x;
-  const int xcd = b & 7, q = nb >> 3, rr = nb & 7;
-  const int u = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (b >> 3);
-  if (u >= g.units) return;
-  const int per_split = g.tiles_m * g.tiles_n;
+  const int per_split = pl_.tiles_m * g.tiles_n;
   const int s = u / per_split, rem = u - s * per_split;
   const int tm = rem / g.tiles_n, tn = rem - tm * g.tiles_n;
-  const int m0 = tm * BM, n0 = tn * BN;
+  const int m0 = pl_.row0_base + tm * BM, n0 = tn * BN;
   const float* __restrict__ A = g.a;
   const float* __restrict__ B = g.b;
   // split s reduces K steps [kb, kb + nk): an even partition of the K / 32 steps
@@ -377,7 +397,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, OCPPO_X6_OCC) void gemm_x6_kernel(X
 #endif
   float* __restrict__ Cp = g.c + s * g.split_c;
   const int wr0 = m0 + wm * 16 * FM, wc0 = n0 + wn * 16 * FN;
-  const int64_t tile_id = static_cast<int64_t>(tm) * g.tiles_n + tn;
+  const int64_t tile_id = pl_.id_base + static_cast<int64_t>(tm) * g.tiles_n + tn;
   if (g.mask || g.mbits_in) {
     // threshold_backward(acc, mask, 0) and the tile's column sums: rows of a lane (i, r) in
     // order, then the wave's 4 row groups (xor 16, 32), then the two wave rows through LDS
@@ -417,7 +437,9 @@ __global__ __launch_bounds__(64 * WGM * WGN, OCPPO_X6_OCC) void gemm_x6_kernel(X
         float v = colsum[j];
 #pragma unroll
         for (int q = 0; q + 1 < WGM; ++q) v += red[q * BN + lc];  // wave rows in order
-        g.dbp[static_cast<int64_t>(tm) * g.N + n0 + lc] = v;
+        const int64_t dr = pl_.db_base + static_cast<int64_t>(pl_.db_mult) * tm;
+        g.dbp[dr * g.N + n0 + lc] = v;
+        if (pl_.db_mult == 2) g.dbp[(dr + 1) * g.N + n0 + lc] = 0.f;
       }
     }
     return;
@@ -442,6 +464,53 @@ __global__ __launch_bounds__(64 * WGM * WGN, OCPPO_X6_OCC) void gemm_x6_kernel(X
     }
   }
   if (g.mbits_out) g.mbits_out[tile_id * NT + t] = bits;
+}
+
+template <int FM, int FN, int WGM, int WGN, bool AKC, bool BKC, bool LO, bool PF2>
+__global__ __launch_bounds__(64 * WGM * WGN, OCPPO_X6_OCC) void gemm_x6_kernel(X6Args g) {
+  __shared__ __attribute__((aligned(16)))
+  unsigned char lds[x6_lds_bytes<FM, FN, WGM, WGN, AKC, BKC>()];
+  const int u = x6_remap(blockIdx.x, gridDim.x);
+  if (u >= g.units) return;
+  x6_unit<FM, FN, WGM, WGN, AKC, BKC, LO, PF2>(g, lds, u, X6Place{g.tiles_m, 0, 0, 1, 0});
+}
+
+// Mixed tiles: workgroups [0, nbig) take the 128 x 128 tiles of rows [0, mbig) (dispatched
+// first, the longest units), the rest the 64 x 128 tiles of rows [mbig, M) as slots free up;
+// each range keeps its own XCD remap (nbig is a multiple of 8, so XCD b & 7 is the same in both)
+template <bool AKC, bool BKC>
+__global__ __launch_bounds__(256, OCPPO_X6_OCC) void gemm_x6_mixed_kernel(X6Args g) {
+  __shared__ __attribute__((aligned(16))) unsigned char lds[x6_lds_bytes<4, 4, 2, 2, AKC, BKC>()];
+  const int nbig = (g.mbig / 128) * g.tiles_n;
+  const int b = blockIdx.x;
+  if (b < nbig) {
+    x6_unit<4, 4, 2, 2, AKC, BKC, false, true>(g, lds, x6_remap(b, nbig),
+                                               X6Place{g.mbig / 128, 0, 0, 2, 0});
+  } else {
+    const int small = (g.M - g.mbig) / 64;
+    const int u = x6_remap(b - nbig, gridDim.x - nbig);
+    if (u >= small * g.tiles_n) return;
+    x6_unit<2, 4, 2, 2, AKC, BKC, false, true>(
+        g, lds, u, X6Place{small, g.mbig, g.mbig / 64, 1, static_cast<int64_t>(nbig)});
+  }
+}
+
+template <bool AKC, bool BKC>
+static void launch_x6_mixed1(hipStream_t s, X6Args& g) {
+  hipLaunchKernelGGL((gemm_x6_mixed_kernel<AKC, BKC>), dim3(g.units), dim3(256), 0, s, g);
+}
+
+// Rows in 128-row tiles for an [M x N] mixed product. With 256 < T <= 384 tiles of 128 x 128
+// (T / 256 CUs: some CUs run two, the rest one), 256 of them — one per CU — and the rest as
+// 2 (T - 256) tiles of 64 x 128 that fill the second slot of every CU: one wave of <= 512
+// workgroups with no CU holding two big tiles (tools/exp_gemm_x6.py --mbig: [11520 x 512] from
+// K = 1024 80.4 -> 70.3 us); otherwise every row in 128-row tiles (at 720 tiles no split beat it).
+// OCPPO_X6_MBIG overrides (experiments and tests).
+static int x6_mixed_mbig(int M, int N) {
+  if (const char* e = getenv("OCPPO_X6_MBIG")) return atoi(e);
+  const int tn = N / 128, tiles = (M / 128) * tn;
+  if (tiles > 256 && tiles <= 384 && 256 % tn == 0) return (256 / tn) * 128;
+  return (M / 128) * 128 == M && tiles % 8 == 0 ? M : 0;
 }
 
 template <int FM, int FN, int WGM, int WGN, bool LO, bool PF2>
@@ -470,6 +539,18 @@ constexpr X6Tile kX6Tiles[] = {{4, 4, 2, 2}, {2, 4, 2, 2}, {4, 2, 2, 2}, {2, 2, 
 // with PF2 + one accumulator (the product family), shapes 0-3 with one-step loads (+/- LO)
 static bool launch_x6(hipStream_t s, int tile, bool akc, bool bkc, X6Args& g) {
   const int shape = tile & 7;
+  if (tile & 32) {  // mixed 128 x 128 / 64 x 128 tiles (variant 56 only)
+    if (tile != 56) return false;
+    g.tiles_n = g.N / 128;
+    g.tiles_m = 0;
+    const int nbig = (g.mbig / 128) * g.tiles_n;
+    g.units = nbig + ((g.M - g.mbig) / 64) * g.tiles_n;
+    if (akc && bkc) launch_x6_mixed1<true, true>(s, g);
+    else if (akc) launch_x6_mixed1<true, false>(s, g);
+    else if (bkc) launch_x6_mixed1<false, true>(s, g);
+    else launch_x6_mixed1<false, false>(s, g);
+    return true;
+  }
   const bool pf2 = tile & 8, one = tile & 16;
   if (pf2 && one) {
     switch (shape) {
@@ -523,8 +604,9 @@ extern "C" int ocppo_gemm_x6(ocppo_stream_t stream, const float* a, int64_t sam,
   OCPPO_REQUIRE(K % kX6BK == 0 && K / kX6BK >= splits,
                 "ocppo_gemm_x6: K=%lld must be a multiple of %d with >= 1 step per split",
                 (long long)K, kX6BK);
-  OCPPO_REQUIRE(tile >= 0 && tile < 32, "ocppo_gemm_x6: tile=%d", tile);
-  const X6Tile tc = kX6Tiles[tile & 7];
+  OCPPO_REQUIRE(tile >= 0 && tile < 64, "ocppo_gemm_x6: tile=%d", tile);
+  OCPPO_REQUIRE(!(tile & 32) || splits == 1, "ocppo_gemm_x6: mixed tiles need splits == 1");
+  const X6Tile tc = kX6Tiles[(tile & 32) ? 1 : (tile & 7)];  // mixed: divisibility of 64 x 128
   const int64_t bm = 16 * tc.fm * tc.wgm, bn = 16 * tc.fn * tc.wgn;
   OCPPO_REQUIRE(M % bm == 0 && N % bn == 0,
                 "ocppo_gemm_x6: M=%lld, N=%lld must be multiples of the %lld x %lld tile",
@@ -540,7 +622,12 @@ extern "C" int ocppo_gemm_x6(ocppo_stream_t stream, const float* a, int64_t sam,
   const int64_t units = splits * (M / bm) * (N / bn);
   OCPPO_REQUIRE(units <= INT32_MAX / 2, "ocppo_gemm_x6: too large");
   X6Args g{a, sam, sak, b, sbn, sbk, c, ldc, bias, relu ? 1 : 0, (int)M, (int)N, (int)K,
-           0, 0, (int)units, (int)splits, split_c, mask, ldm, dbp, mbits_out, mbits_in};
+           0, 0, (int)units, (int)splits, split_c, mask, ldm, dbp, mbits_out, mbits_in, 0};
+  if (tile & 32) {
+    g.mbig = x6_mixed_mbig((int)M, (int)N);
+    OCPPO_REQUIRE(g.mbig >= 0 && g.mbig <= M && g.mbig % 128 == 0 && ((g.mbig / 128) * (N / 128)) % 8 == 0,
+                  "ocppo_gemm_x6: mixed split at row %d", g.mbig);
+  }
   clear_stale_error();
   hipStream_t s = as_stream(stream);
   const bool akc = sak == 1, bkc = sbk == 1;

@@ -816,10 +816,13 @@ def sum_splits(part, out=None):
 # ---------------------------------------------------------------------------------------------
 # (rows, columns) of variant & 7 (0-3: 4 waves, 4-7: 8 waves); variant & 8: loads two K steps
 # ahead; variant & 16: one accumulator (built: every shape with both, shapes 0-3 with neither or
-# only the latter)
+# only the latter). Variant 56: mixed tiles — rows [0, mbig) in 128 x 128 tiles dispatched first,
+# the rest in 64 x 128 (mbig chosen in the library, include/ocppo.h); it divides, and counts its
+# dbp rows and mask words, like 64 x 128
 X6_TILES = ((128, 128), (64, 128), (128, 64), (64, 64),
-            (128, 128), (64, 128), (128, 128), (128, 64)) * 4
-X6_BUILT = tuple(range(4)) + tuple(range(16, 20)) + tuple(range(24, 32))
+            (128, 128), (64, 128), (128, 128), (128, 64)) * 7 + ((64, 128),) + ((0, 0),) * 7
+X6_BUILT = tuple(range(4)) + tuple(range(16, 20)) + tuple(range(24, 32)) + (56,)
+X6_MIXED = 56
 
 
 X6_AUTO = 24  # the variant family x6_tile picks from (two K steps of loads in flight, one
@@ -833,7 +836,16 @@ def x6_tile(M: int, N: int, splits: int = 1, tile: int | None = None) -> int | N
     that many, tools/exp_gemm_x6.py), else the one giving the most; None if none divides."""
     if tile is not None:
         bm, bn = X6_TILES[tile]
+        if tile == X6_MIXED and splits != 1:
+            return None
         return tile if M % bm == 0 and N % bn == 0 else None
+    # 256 < tiles of 128 x 128 <= 384 (more than one per CU, fewer than two): the mixed variant,
+    # one 128 x 128 tile per CU and the rest in 64 x 128 tiles beside them (tools/exp_gemm_x6.py
+    # --mbig; the split itself is chosen in the library)
+    t128 = (M // 128) * (N // 128)
+    if (splits == 1 and M % 128 == 0 and N % 128 == 0 and 256 < t128 <= 384
+            and 256 % (N // 128) == 0):
+        return X6_MIXED
     best, best_units = None, -1
     for i, (bm, bn) in enumerate(X6_TILES[:4]):
         i += X6_AUTO

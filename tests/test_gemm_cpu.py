@@ -33,13 +33,14 @@ def test_weight_grad_gating_and_split():
 def test_tile_choice():
     assert ops.X6_AUTO == 24 and ops.X6_TILES[24] == (128, 128)
     assert ops.x6_tile(11520, 1024) == 24  # 720 tiles
-    assert ops.x6_tile(11520, 512) == 24  # 360 >= 256
+    assert ops.x6_tile(11520, 512) == ops.X6_MIXED == 56  # 360 tiles: 256 of 128 x 128 + 208 x 2
+    assert ops.X6_TILES[56] == (64, 128) and ops.x6_tile(11520, 512, 2) == 24
     assert ops.x6_tile(4096, 512) == 25  # 128 tiles of 128 x 128 -> 64 x 128 (256)
     assert ops.x6_tile(96, 128) is None
     assert ops.x6_tile(512, 1024, 16) == 24
     assert ops.x6_tile(128, 128, 1, 3) == 3 and ops.x6_tile(96, 128, 1, 3) is None
     for t in ops.X6_BUILT:
-        assert 0 <= t < 32
+        assert 0 <= t < 64
 
 
 def test_mbits_words():

@@ -51,7 +51,12 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--only", default=None, help="kind,M,N,K: one shape (profiling)")
     ap.add_argument("--tiles", default=None, help="comma-separated variants (default: all built)")
+    ap.add_argument("--mbig", type=int, default=None,
+                    help="rows in 128 x 128 tiles for the mixed variant (OCPPO_X6_MBIG)")
     a = ap.parse_args()
+    if a.mbig is not None:
+        import os
+        os.environ["OCPPO_X6_MBIG"] = str(a.mbig)
     shapes = SHAPES
     if a.only:
         k, *dims = a.only.split(",")
@@ -99,6 +104,11 @@ def main():
                     ops.sum_splits(part, out)
                 return f
             shape_ok = lambda t: ops.x6_tile(N, K, S, t) is not None  # noqa: E731
+        if a.mbig is not None:  # the mixed split must fit the output [rows, cols]
+            rows, cols = (M, N) if kind == "fwd" else (M, K)
+            if (not shape_ok(ops.X6_MIXED) or a.mbig > rows
+                    or (a.mbig // 128) * (cols // 128) % 8):
+                continue
         ct = tfn()
         torch.cuda.synchronize()
         t_err = err(ct, ref, scale)
