@@ -271,6 +271,9 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int wm = wv / WGN, wn = wv % WGN;
   const int fr = lane & 15, fc = lane >> 4;
+  const int64_t tile_id = pl_.id_base + static_cast<int64_t>(tm) * g.tiles_n + tn;
+  // the mask epilogue's bitmask word, fetched before the K loop (off the epilogue's critical path)
+  const uint64_t bits_in = g.mbits_in ? g.mbits_in[tile_id * NT + t] : 0;
 
   floatx4 hi[FM][FN], lo[LO ? FM : 1][LO ? FN : 1];
 #pragma unroll
@@ -397,11 +400,10 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
 #endif
   float* __restrict__ Cp = g.c + s * g.split_c;
   const int wr0 = m0 + wm * 16 * FM, wc0 = n0 + wn * 16 * FN;
-  const int64_t tile_id = pl_.id_base + static_cast<int64_t>(tm) * g.tiles_n + tn;
   if (g.mask || g.mbits_in) {
     // threshold_backward(acc, mask, 0) and the tile's column sums: rows of a lane (i, r) in
     // order, then the wave's 4 row groups (xor 16, 32), then the two wave rows through LDS
-    const uint64_t bits = g.mbits_in ? g.mbits_in[tile_id * NT + t] : 0;
+    const uint64_t bits = bits_in;
     float colsum[FN];
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
