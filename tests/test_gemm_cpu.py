@@ -39,6 +39,7 @@ def test_tile_choice():
     assert ops.x6_tile(96, 128) is None
     assert ops.x6_tile(512, 1024, 16) == 24
     assert ops.x6_tile(128, 128, 1, 3) == 3 and ops.x6_tile(96, 128, 1, 3) is None
+    assert ops.x6_tile(128, 128, 1, 57) is None and ops.x6_tile(128, 128, 1, 64) is None
     for t in ops.X6_BUILT:
         assert 0 <= t < 64
 
