@@ -207,6 +207,53 @@ def relu_bias_wgrad_bytes(name: str):
     return R * N * 8 + R * K * 4 + N * (K + 1) * 4
 
 
+def free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launcher_cmd(argv, gpus: int, port: int, script=None) -> list:
+    """The torch.distributed.run command that starts `gpus` ranks of this script with the same
+    arguments (one process per GPU; the ranks read RANK / LOCAL_RANK / WORLD_SIZE from the env,
+    as under the driver's own launch)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            f"--nproc-per-node={gpus}", "--master-addr", "127.0.0.1", "--master-port", str(port),
+            str(script or ROOT / "bench.py"), *argv]
+
+
+def needs_launch(gpus: int, env=os.environ) -> bool:
+    """--gpus N > 1 outside a torch.distributed launch: start the ranks as a child."""
+    return gpus > 1 and "WORLD_SIZE" not in env
+
+
+def launch(argv, gpus: int, script=None) -> int:
+    """Run the N ranks as ONE child process tree (not an exec), before this process makes any GPU
+    call; the child's stdout is this process's (rank 0 prints the line). Returns its exit code."""
+    import subprocess
+
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(launcher_cmd(argv, gpus, free_port(), script), env=env).returncode
+
+
+def replica_check(tr, world: int, device) -> dict:
+    """Every rank's parameter checksum after the timed iterations, gathered on every rank and
+    asserted equal: the replica invariant of ppo_atari_multigpu.py:360-377 (identical init, the
+    same all-reduced gradient, the same Adam step)."""
+    mine = tr.param_checksum()
+    sums = [mine]
+    if world > 1:
+        sums = [None] * world
+        dist.all_gather_object(sums, mine)
+    equal = all(s == sums[0] for s in sums)
+    if not equal:
+        raise SystemExit(f"DP replicas diverged: parameter checksums {sums}")
+    return {"param_checksums": [f"{s:016x}" for s in sums], "equal": equal}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -232,6 +279,9 @@ def main():
     ap.add_argument("--set", action="append", default=[], metavar="FIELD=VALUE",
                     help="override an Args field (experiments; e.g. --set rollout_frame_cache=0)")
     opt = ap.parse_args()
+    if needs_launch(opt.gpus):
+        # nothing has touched the GPU yet in this process
+        raise SystemExit(launch(sys.argv[1:], opt.gpus))
 
     from oc_cleanrl_amd.args import Args, finalize
     from oc_cleanrl_amd import gemm_table
@@ -241,8 +291,7 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != opt.gpus:
-        if world == 1 and opt.gpus > 1:
-            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run")
+        raise SystemExit(f"--gpus {opt.gpus} under a launch of WORLD_SIZE={world}")
     device = torch.device(f"cuda:{local_rank if opt.device_index is None else opt.device_index}")
     torch.cuda.set_device(device)
     if world > 1:
@@ -297,6 +346,7 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t)
+    replicas = replica_check(tr, world, device)
 
     env_steps = opt.steps * args.num_steps * args.local_num_envs * world
     updates = opt.steps * args.update_epochs * args.num_minibatches
@@ -473,7 +523,9 @@ def main():
                                           "reference's stream is --set per_step_noise=1: "
                                           "770.7k vs 779.9k env steps/s, -1.2 %, "
                                           "profiles/r03/noise_ab.json)"),
-                       "parallelism": f"dp{world}"},
+                       "parallelism": f"dp{world}",
+                       **({"dist_backend": opt.backend} if world > 1 else {})},
+            "replicas": replicas,
             "updates_per_sec": round(updates / dt, 2),
             "roofline": roofline,
             "roofline_hbm": roofline_hbm if roofline_hbm is not roofline else None,

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define OCPPO_ABI_VERSION 17
+#define OCPPO_ABI_VERSION 18
 
 /* status codes */
 #define OCPPO_OK 0
@@ -297,8 +297,9 @@ OCPPO_API int ocppo_bias_act_nchw(ocppo_stream_t stream, const float* y, const f
  *   A(m, k) = a[m*sam + k*sak], B(n, k) = b[n*sbn + k*sbk], C_s[m, n] = c[s*split_c + m*ldc + n]
  *   K_s = steps [s*nk/splits, (s+1)*nk/splits) of the nk = K/32 steps of 32 (even partition)
  * Each f32 operand is split exactly into three bf16 pieces (x = x0 + x1 + x2) and the six piece
- * products down to 2^-24 of |a b| are accumulated in f32 (leading and small terms in separate
- * accumulators): f32-level accuracy (tests/test_gemm_gpu.py: error vs f64 at or below
+ * products down to 2^-24 of |a b| are accumulated in f32 (one accumulator per output with tile
+ * bit 4 and the mixed tiles, the shipped forms; the small terms in a second one otherwise):
+ * f32-level accuracy (tests/test_gemm_gpu.py: error vs f64 at or below
  * hipBLASLt's f32 GEMM) at 6 bf16 MFMAs per f32 multiply-add.
  * One of (sam, sak) and one of (sbn, sbk) must be 1 (the other a multiple of 4, >= the extent it
  * strides over); a, b 16-B aligned; K % 32 == 0, K / 32 >= splits; M, N multiples of the tile (tile 0: 128 x 128,
@@ -316,8 +317,9 @@ OCPPO_API int ocppo_bias_act_nchw(ocppo_stream_t stream, const float* y, const f
  * bit 4 one accumulator for all six products. tile 56 (bit 5: mixed tiles; splits == 1): rows
  * [0, mbig) in 128 x 128 tiles dispatched first, rows [mbig, M) in 64 x 128 tiles — mbig chosen
  * by the library (one 128 x 128 tile per CU when the output holds 257..384 of them, else all of
- * M); M, N multiples of 64 x 128, and dbp rows / mbits words counted as for 64 x 128 (a 128-row
- * tile's dbp partial sits in the first of its two rows, the second is written as zeros).
+ * M) when mbig is -1; mbig >= 0 imposes the split (a multiple of 128, (mbig / 128)(N / 128) a
+ * multiple of 8; experiments and tests); mbig must be -1 for every other tile. M, N multiples of
+ * 64 x 128, and dbp rows / mbits words counted as for 64 x 128 (a 128-row tile's dbp partial sits in the first of its two rows, the second is written as zeros).
  * Deterministic (fixed MFMA order, no atomics).
  * ------------------------------------------------------------------------------------------- */
 OCPPO_API int ocppo_gemm_x6(ocppo_stream_t stream, const float* a, int64_t sam, int64_t sak,
@@ -325,7 +327,7 @@ OCPPO_API int ocppo_gemm_x6(ocppo_stream_t stream, const float* a, int64_t sam, 
                             int64_t M, int64_t N, int64_t K, int64_t splits, int64_t split_c,
                             const float* bias, int relu, const float* mask, int64_t ldm,
                             float* dbp, uint64_t* mbits_out, const uint64_t* mbits_in,
-                            int tile);
+                            int tile, int mbig);
 
 /* ---------------------------------------------------------------------------------------------
  * Split-K combine of a weight gradient — replaces ATen's `sum(0)` after the batched (split-K)

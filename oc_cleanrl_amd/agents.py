@@ -70,8 +70,10 @@ def _splitk(rows: int, k: int, n: int) -> int:
 
 # The update's f32 GEMMs on the bf16 matrix cores (ops.gemm_x6: each f32 operand split exactly
 # into three bf16 pieces, six piece products accumulated in f32 -- f32 accuracy at 6/16 of the f32
-# MFMA's time, tests/test_gemm_gpu.py); shapes it does not tile stay on hipBLASLt.
-X6_GEMM = True
+# MFMA's time, tests/test_gemm_gpu.py); shapes it does not tile stay on hipBLASLt. The route is
+# per parameter: a Linear whose weight carries `_ocppo_x6` (set_update_gemm, done by each
+# PPOTrainer for its own agent from Args.x6_gemm) uses that; any other weight uses this default.
+X6_GEMM_DEFAULT = True
 # Where it wins (tools/exp_gemm_x6.py at the config-2 update shapes): products whose output holds
 # >= 256 tiles of 128 x 128 (forward / dX), and weight gradients with >= 32 such tiles (the rows
 # split over up to 16 workgroups per tile); smaller outputs leave the chip half idle and stay on
@@ -79,14 +81,28 @@ X6_GEMM = True
 X6_MIN_TILES, X6_MIN_TILES_DW = 256, 32
 
 
-def _x6(M: int, N: int, K: int) -> bool:
+def x6_route(w) -> bool:
+    """The update-GEMM route of the Linear owning weight `w` (gemm_x6 or hipBLASLt)."""
+    return bool(getattr(w, "_ocppo_x6", X6_GEMM_DEFAULT))
+
+
+def set_update_gemm(module: nn.Module, x6: bool) -> None:
+    """Route every Linear of `module` (forward, dX, dW and the fused ReLU-backward dX epilogue)
+    through gemm_x6 (x6) or hipBLASLt: per-agent state, so two trainers in one process with
+    different Args.x6_gemm do not interfere."""
+    for m in module.modules():
+        if isinstance(m, nn.Linear):
+            m.weight._ocppo_x6 = bool(x6)
+
+
+def _x6(M: int, N: int, K: int, on: bool = True) -> bool:
     """Forward / dX product [M, N] = [M, K] x [K, N] on gemm_x6."""
-    return X6_GEMM and M * N >= X6_MIN_TILES * 16384 and K >= 64
+    return on and M * N >= X6_MIN_TILES * 16384 and K >= 64
 
 
-def _x6_dw(n: int, k: int, rows: int) -> bool:
+def _x6_dw(n: int, k: int, rows: int, on: bool = True) -> bool:
     """Weight gradient [n, k] = g^T x over `rows` on gemm_x6."""
-    return X6_GEMM and n * k >= X6_MIN_TILES_DW * 16384 and rows >= 1024
+    return on and n * k >= X6_MIN_TILES_DW * 16384 and rows >= 1024
 
 
 def _x6_splits(rows: int, n: int, k: int):
@@ -112,23 +128,22 @@ def _x6_splits(rows: int, n: int, k: int):
 
 
 # The ReLU backward + bias-gradient partials of a Linear+ReLU layer fused into the next layer's
-# dX GEMM (ops.dx_x6_relu): replaces that layer's relu_bias_grad pass.
-X6_MASK_DX = True
+# dX GEMM (ops.dx_x6_relu) on the gemm_x6 route: replaces that layer's relu_bias_grad pass.
 
 
-def _x6_dx_shape_ok(M: int, N: int, K: int) -> bool:
+def _x6_dx_shape_ok(M: int, N: int, K: int, on: bool = True) -> bool:
     """dX [M, K] = g [M, N] W [N, K] runs on gemm_x6 (agents._dx's rule, decided from shapes)."""
-    return _x6(M, K, N) and N % 32 == 0 and ops.x6_tile(M, K) is not None
+    return _x6(M, K, N, on) and N % 32 == 0 and ops.x6_tile(M, K) is not None
 
 
-def _weight_grad(g, x, out=None, db=None):
+def _weight_grad(g, x, out=None, db=None, x6: bool = True):
     """dW = g^T x (g [rows, n], x [rows, k]) with the split-K rule; written into `out` if given.
     db = (partials of ops.relu_bias_grad_partial, bias grad): the bias gradient is finished in
     the same launch as the split-K combine (only when _defer_db_ok said so)."""
     rows, n = g.shape
     k = x.shape[1]
     s = _splitk(rows, k, n)
-    st = _x6_splits(rows, n, k) if _x6_dw(n, k, rows) else None
+    st = _x6_splits(rows, n, k) if _x6_dw(n, k, rows, x6) else None
     if st is not None and ops.dw_x6_ok(g, x, st[0]):
         s6, t6 = st
         if s6 == 1 and out is not None and db is None and out.is_contiguous():
@@ -152,10 +167,10 @@ def _weight_grad(g, x, out=None, db=None):
 HIP_SMALL_DX = True
 
 
-def _dx(g, w):
+def _dx(g, w, x6: bool = True):
     M, N = g.shape
     K = w.shape[1]
-    if _x6(M, K, N) and ops.dx_x6_ok(g, w):
+    if _x6(M, K, N, x6) and ops.dx_x6_ok(g, w):
         return ops.dx_x6(g, w)
     if (HIP_SMALL_DX and g.is_cuda and M <= 256 and K <= 256 and N >= 256 and N % 16 == 0 and
             g.dtype == torch.float32 and g.is_contiguous()):
@@ -214,15 +229,16 @@ class _LinearAct(torch.autograd.Function):
         # chw = (C, H, W): x is a channels_last activation flattened in its memory (H, W, C)
         # order, so the weight's columns are permuted to match instead (linear_act_nhwc)
         wm = _cols_to_nhwc(w, chw) if chw is not None else w
+        x6 = ctx.x6 = x6_route(w)
         # below = the box of the Linear+ReLU that produced x: its ReLU backward and bias-gradient
         # partials ride in this layer's dX GEMM (ops.dx_x6_relu, mask = x)
         ctx.below = None
-        if (X6_MASK_DX and below is not None and not below["premasked"] and chw is None
+        if (x6 and below is not None and not below["premasked"] and chw is None
                 and x.requires_grad and _x6_dx_shape_ok(x.shape[0], wm.shape[0], x.shape[1])):
             below["premasked"] = True
             ctx.below = below
-        if _x6(x.shape[0], wm.shape[0], x.shape[1]) and ops.linear_x6_ok(x, wm):
-            if relu and box is not None and X6_MASK_DX:
+        if _x6(x.shape[0], wm.shape[0], x.shape[1], x6) and ops.linear_x6_ok(x, wm):
+            if relu and box is not None:
                 # the ReLU bitmask for the next layer's fused dX epilogue (box consumer)
                 out, box["mbits"] = ops.linear_x6(x, wm, b, relu, mbits=True)
             else:
@@ -254,11 +270,24 @@ class _LinearAct(torch.autograd.Function):
 
     @staticmethod
     def _dx_of(ctx, g, w):
+        """dX of this layer; when the forward claimed the layer below's ReLU backward (ctx.below:
+        x is that layer's ReLU output, consumed by this layer alone — fused_trunk's chains), the
+        mask and the below layer's bias-gradient partials come with it. Operands the fused C
+        entry refuses (layout, alignment) take the plain dX plus the same two results, so the
+        claim always holds."""
         if ctx.below is None:
-            return _dx(g, w)
+            return _dx(g, w, ctx.x6)
         x = ctx.saved_tensors[0]
-        gp, dbp = ops.dx_x6_relu(g, w, x, mbits=ctx.below.get("mbits"))
-        ctx.below["dbp"] = (dbp, dbp.shape[0])  # relu_bias_grad_partial's (partials, chunks)
+        if ops.dx_x6_ok(g, w):
+            gp, dbp = ops.dx_x6_relu(g, w, x, mbits=ctx.below.get("mbits"))
+            ctx.below["dbp"] = (dbp, dbp.shape[0])  # relu_bias_grad_partial's (partials, chunks)
+            return gp
+        dx = _dx(g, w, ctx.x6).contiguous()
+        if ops.relu_bias_grad_ok(dx):
+            gp, ctx.below["dbp"] = ops.relu_bias_grad_partial(dx, x.contiguous())
+        else:
+            gp = torch.ops.aten.threshold_backward(dx, x, 0)
+            ctx.below["dbp"] = (gp.sum(0, keepdim=True), 1)
         return gp
 
     @staticmethod
@@ -276,11 +305,11 @@ class _LinearAct(torch.autograd.Function):
             dx = _LinearAct._dx_of(ctx, g, w) if ctx.needs_input_grad[0] else None
             dbp = ctx.box.get("dbp")
             if dbp is None:
-                _weight_grad(g, x, out=wgrad)
+                _weight_grad(g, x, out=wgrad, x6=ctx.x6)
             elif _defer_db_ok(g, x, wgrad, ctx.b):
-                _weight_grad(g, x, out=wgrad, db=(dbp, ctx.b.grad))
+                _weight_grad(g, x, out=wgrad, db=(dbp, ctx.b.grad), x6=ctx.x6)
             else:
-                _weight_grad(g, x, out=wgrad)
+                _weight_grad(g, x, out=wgrad, x6=ctx.x6)
                 torch.sum(dbp[0], 0, out=ctx.b.grad)
             return dx, None, None, None, None, None
         if FUSED_FIRST_LAYER_BWD and not ctx.needs_input_grad[0] and ctx.needs_input_grad[1] \
@@ -300,7 +329,7 @@ class _LinearAct(torch.autograd.Function):
                                 ("" if ctx.relu else "_norelu"),
                                 lambda: ops.relu_bias_grad_partial(g, o))
             dx = _LinearAct._dx_of(ctx, gp, w) if ctx.needs_input_grad[0] else None
-            _weight_grad(gp, x, out=wgrad, db=(dbp, ctx.b.grad))
+            _weight_grad(gp, x, out=wgrad, db=(dbp, ctx.b.grad), x6=ctx.x6)
             return dx, None, None, None, None, None
         if FUSED_RELU_BIAS_GRAD and ctx.needs_input_grad[2] and _direct(ctx.b) and \
                 ops.relu_bias_grad_ok(g):
@@ -316,9 +345,9 @@ class _LinearAct(torch.autograd.Function):
         dw = None
         if ctx.needs_input_grad[1]:
             if _direct(ctx.w):
-                _weight_grad(gp, x, out=wgrad)
+                _weight_grad(gp, x, out=wgrad, x6=ctx.x6)
             else:
-                dw = _weight_grad(gp, x)
+                dw = _weight_grad(gp, x, x6=ctx.x6)
         if ctx.needs_input_grad[2] and not bias_done:
             if _direct(ctx.b):
                 torch.sum(gp, 0, out=ctx.b.grad)

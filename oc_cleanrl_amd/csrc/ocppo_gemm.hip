@@ -14,9 +14,12 @@
 // The bracketed terms are dropped: |a1 b2| <= 2^-8 * 2^-16 |a b| = 2^-24 |a b| (half an f32 ulp of
 // the product at most, ~2^-28 typically, randomly signed), below the per-product rounding a plain
 // f32 FMA chain already makes. Every piece product is exact in f32 (8 x 8 bits) and is accumulated
-// by the MFMA in f32. The leading products a0 b0 go into one accumulator and the five small ones into
-// a second (x 2^-8 in magnitude), added once at the end, so the small terms are never rounded
-// against the large running sum. Six bf16 MFMAs = 6/16 of one f32 MFMA's time for the same
+// by the MFMA in f32. The shipped variants (tile bit 4, and the mixed tiles) accumulate all six
+// products into ONE f32 accumulator per output (small terms issued before the lead one in each K
+// step): the accumulation then rounds like an f32 FMA chain over 6 K terms per k, measured at or
+// below hipBLASLt's f32 GEMM error vs f64 up to K = 4096 (tests/test_gemm_gpu.py). The two-
+// accumulator variants (bit 4 clear) keep the five small products in a second accumulator
+// (x 2^-8 in magnitude), added once at the end: 3x more accurate, 0-5 % slower. Six bf16 MFMAs = 6/16 of one f32 MFMA's time for the same
 // output: the f32-equivalent ceiling is 2,500 / 6 = 417 TFLOP/s against 157 for the f32 MFMA.
 // tests/test_gemm_gpu.py measures the error against an f64 product next to hipBLASLt's f32 GEMM.
 //
@@ -45,7 +48,6 @@
 // Roofline: MFMA-bound (6 bf16 MFMA passes per f32 multiply-add: 12 M N K bf16 flops against
 // the 2.5 PFLOP/s dense bf16 peak).
 #include <algorithm>
-#include <cstdlib>
 
 #include "ocppo_common.h"
 
@@ -507,9 +509,8 @@ static void launch_x6_mixed1(hipStream_t s, X6Args& g) {
 // 2 (T - 256) tiles of 64 x 128 that fill the second slot of every CU: one wave of <= 512
 // workgroups with no CU holding two big tiles (tools/exp_gemm_x6.py --mbig: [11520 x 512] from
 // K = 1024 80.4 -> 70.3 us); otherwise every row in 128-row tiles (at 720 tiles no split beat it).
-// OCPPO_X6_MBIG overrides (experiments and tests).
+// The caller may pass its own split (the mbig argument, >= 0: experiments and tests).
 static int x6_mixed_mbig(int M, int N) {
-  if (const char* e = getenv("OCPPO_X6_MBIG")) return atoi(e);
   const int tn = N / 128, tiles = (M / 128) * tn;
   if (tiles > 256 && tiles <= 384 && 256 % tn == 0) return (256 / tn) * 128;
   return (M / 128) * 128 == M && tiles % 8 == 0 ? M : 0;
@@ -588,7 +589,7 @@ extern "C" int ocppo_gemm_x6(ocppo_stream_t stream, const float* a, int64_t sam,
                              int64_t M, int64_t N, int64_t K, int64_t splits, int64_t split_c,
                              const float* bias, int relu,
                              const float* mask, int64_t ldm, float* dbp, uint64_t* mbits_out,
-                             const uint64_t* mbits_in, int tile) {
+                             const uint64_t* mbits_in, int tile, int mbig) {
   OCPPO_REQUIRE(M >= 1 && N >= 1 && K >= 1 && splits >= 1 && M <= INT32_MAX && N <= INT32_MAX &&
                     K <= INT32_MAX,
                 "ocppo_gemm_x6: bad sizes M=%lld N=%lld K=%lld splits=%lld", (long long)M,
@@ -608,6 +609,8 @@ extern "C" int ocppo_gemm_x6(ocppo_stream_t stream, const float* a, int64_t sam,
                 (long long)K, kX6BK);
   OCPPO_REQUIRE(tile >= 0 && tile < 64, "ocppo_gemm_x6: tile=%d", tile);
   OCPPO_REQUIRE(!(tile & 32) || splits == 1, "ocppo_gemm_x6: mixed tiles need splits == 1");
+  OCPPO_REQUIRE(mbig == -1 || ((tile & 32) && mbig >= 0),
+                "ocppo_gemm_x6: mbig=%d (-1, or a split of the mixed tile)", mbig);
   const X6Tile tc = kX6Tiles[(tile & 32) ? 1 : (tile & 7)];  // mixed: divisibility of 64 x 128
   const int64_t bm = 16 * tc.fm * tc.wgm, bn = 16 * tc.fn * tc.wgn;
   OCPPO_REQUIRE(M % bm == 0 && N % bn == 0,
@@ -626,7 +629,7 @@ extern "C" int ocppo_gemm_x6(ocppo_stream_t stream, const float* a, int64_t sam,
   X6Args g{a, sam, sak, b, sbn, sbk, c, ldc, bias, relu ? 1 : 0, (int)M, (int)N, (int)K,
            0, 0, (int)units, (int)splits, split_c, mask, ldm, dbp, mbits_out, mbits_in, 0};
   if (tile & 32) {
-    g.mbig = x6_mixed_mbig((int)M, (int)N);
+    g.mbig = mbig >= 0 ? mbig : x6_mixed_mbig((int)M, (int)N);
     OCPPO_REQUIRE(g.mbig >= 0 && g.mbig <= M && g.mbig % 128 == 0 && ((g.mbig / 128) * (N / 128)) % 8 == 0,
                   "ocppo_gemm_x6: mixed split at row %d", g.mbig);
   }

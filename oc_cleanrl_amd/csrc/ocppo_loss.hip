@@ -1734,12 +1734,17 @@ __global__ __launch_bounds__(256) void heads_loss_finish_kernel(
 // minibatch (4096 rows) on 256 workgroups, one per CU, every wave's 4 rows loaded at once;
 // grid_cap = 256 (one per CU: ~300 VGPRs, one wave per SIMD, 64 KB of h in flight per CU with the
 // ping-pong) bounds the records at streaming sizes.
-// OCPPO_HL_ROWS / OCPPO_HL_GRID override them for experiments (tools/).
-inline int hl_env(const char* name, int dflt, int lo, int hi) {
-  const char* e = getenv(name);
-  const int v = e ? atoi(e) : dflt;
-  return v >= lo && v <= hi ? v : dflt;
-}
+// Compile-time only (-DOCPPO_HL_ROWS=... / -DOCPPO_HL_GRID=..., tools/build_variant.py): the
+// grid fixes the records' summation order, so the shipped library has one geometry, independent
+// of the environment.
+#ifndef OCPPO_HL_ROWS
+#define OCPPO_HL_ROWS 16
+#endif
+#ifndef OCPPO_HL_GRID
+#define OCPPO_HL_GRID 256
+#endif
+static_assert(OCPPO_HL_ROWS >= 16 && OCPPO_HL_ROWS % 16 == 0 && OCPPO_HL_GRID >= 1,
+              "heads_loss geometry");
 
 // the action count the rows kernel is instantiated with: exact for 4 (Breakout) and 6 (Pong,
 // SpaceInvaders), else the 7-wide generic form
@@ -1747,8 +1752,8 @@ inline int hl_amax(int64_t A) { return A == 4 || A == 6 ? static_cast<int>(A) : 
 
 inline int64_t hl_layout(int64_t M, int64_t H, int64_t A, int64_t& G, int64_t& ls,
                          int64_t* rows_per_wg = nullptr) {
-  static const int rows_min = hl_env("OCPPO_HL_ROWS", 16, 16, 65536);
-  static const int grid_cap = hl_env("OCPPO_HL_GRID", 256, 1, 65536);
+  constexpr int rows_min = OCPPO_HL_ROWS;
+  constexpr int grid_cap = OCPPO_HL_GRID;
   G = (M + rows_min - 1) / rows_min;
   if (G > grid_cap) G = grid_cap;
   int64_t rpw = (M + G - 1) / G;

@@ -873,8 +873,9 @@ def x6_mbits_words(M: int, N: int, tile: int) -> int:
 
 
 def gemm_x6(a, sam, sak, b, sbn, sbk, c, ldc, M, N, K, splits=1, split_c=0, bias=None,
-            relu=False, mask=None, dbp=None, tile=None, mbits_out=None, mbits_in=None):
-    """Raw ocppo_gemm_x6 call on tensors a, b, c (their data pointers; strides as given)."""
+            relu=False, mask=None, dbp=None, tile=None, mbits_out=None, mbits_in=None, mbig=None):
+    """Raw ocppo_gemm_x6 call on tensors a, b, c (their data pointers; strides as given).
+    mbig: rows in 128 x 128 tiles for the mixed variant (None: the library's choice)."""
     t = x6_tile(M, N, splits, tile)
     if t is None:
         raise ValueError(f"gemm_x6: no tile divides {M} x {N}")
@@ -893,7 +894,7 @@ def gemm_x6(a, sam, sak, b, sbn, sbk, c, ldc, M, N, K, splits=1, split_c=0, bias
             split_c, bp, int(bool(relu)), None if mask is None else mask.data_ptr(),
             0 if mask is None else mask.stride(0), None if dbp is None else dbp.data_ptr(),
             None if mbits_out is None else mbits_out.data_ptr(),
-            None if mbits_in is None else mbits_in.data_ptr(), t)
+            None if mbits_in is None else mbits_in.data_ptr(), t, -1 if mbig is None else int(mbig))
     # timer site name: the product's shape (bench.py's gemm_x6 roofline parses it); the closure
     # keeps the operand tensors alive for the timer's replays
     masked = mask is not None or mbits_in is not None

@@ -246,8 +246,6 @@ class PPOTrainer:
         torch.backends.cudnn.deterministic = a.torch_deterministic
         torch.backends.cudnn.benchmark = a.conv_benchmark
         self.gemm_table = a.gemm_table and gemm_table.use(device)
-        # process-wide switch of agents' update GEMM path (like the TunableOp table above)
-        agents.X6_GEMM = agents.X6_MASK_DX = bool(a.x6_gemm)
 
         # seeding as ppo_atari_multigpu.py:208-212, 230-231: identical init on every rank, then
         # rank-dependent sampling / env / shuffle streams
@@ -274,6 +272,8 @@ class PPOTrainer:
         self.obs_shape = self.env.single_obs_shape
         self.agent = make_agent(a.architecture, self.obs_shape, self.A, self.dev, a.encoder_dims,
                                 a.decoder_dims).to(self.dev)
+        # this agent's update-GEMM route (gemm_x6 or hipBLASLt): per-agent state, not a global
+        agents.set_update_gemm(self.agent, a.x6_gemm)
         # NatureCNN in channels_last: MIOpen runs its NHWC kernels without transposing every
         # activation; the HIP store/gather kernels write the network input in NHWC directly
         self.channels_last = (a.conv_channels_last and self.pixels and len(self.obs_shape) == 3
@@ -930,6 +930,17 @@ class PPOTrainer:
 
     def save(self, path):
         torch.save(self.state_dict_checkpoint(), path)
+
+    def param_checksum(self) -> int:
+        """An exact, order-sensitive checksum of every parameter's f32 bit pattern (int64 sum of
+        bits × (position mod 65521 + 1)). The DP replicas of ppo_atari_multigpu.py:360-377 start
+        from one init and apply the same all-reduced step, so this is equal on every rank."""
+        total = 0
+        for p in self.params:
+            bits = p.detach().contiguous().view(-1).view(torch.int32).to(torch.int64)
+            w = torch.arange(bits.numel(), dtype=torch.int64, device=bits.device) % 65521 + 1
+            total = (total * 1_000_003 + int((bits * w).sum())) % (1 << 61)
+        return total
 
 
 def _own_tensors(sd: dict) -> dict:

@@ -70,3 +70,25 @@ def test_zero_sized_calls_are_noops(lib):
 def test_workspace_size_is_host_only(lib):
     n = lib.LIB.ocppo_ppo_loss_workspace_bytes(4096, 6)
     assert n >= 256 + 16 * 6 * 4 and n % 16 == 0
+
+
+def test_library_reads_no_environment():
+    """No tiling, grid or workspace choice of the shipped library depends on the environment:
+    it imports no getenv (the geometry knobs of experiments are compile-time -D flags for
+    tools/build_variant.py, or explicit ABI arguments such as ocppo_gemm_x6's mbig)."""
+    import subprocess
+
+    out = subprocess.run(["nm", "-D", "--undefined-only",
+                          str(ROOT / "oc_cleanrl_amd" / "lib" / "libocppo_hip.so")],
+                         capture_output=True, text=True, check=True).stdout
+    assert not [l for l in out.splitlines() if "getenv" in l]
+    for src in (ROOT / "oc_cleanrl_amd" / "csrc").glob("*.hip"):
+        assert "getenv" not in src.read_text(), src.name
+
+
+def test_gemm_x6_mbig_only_for_the_mixed_tile(lib):
+    dummy = ctypes.c_void_p(256)
+    args = [None, dummy, 64, 1, dummy, 64, 1, dummy, 128, 128, 128, 64, 1, 0, None, 0, None, 0,
+            None, None, None]
+    assert lib.LIB.ocppo_gemm_x6(*args, 24, 512) == lib.OCPPO_E_INVALID
+    assert b"mbig" in lib.LIB.ocppo_last_error()

@@ -1,0 +1,109 @@
+"""bench.py --gpus N > 1 outside a torch.distributed launch starts its N ranks as a child
+`torch.distributed.run` (ppo_atari_multigpu.py:162-175 is launched the same way: one process per
+GPU, RANK / LOCAL_RANK / WORLD_SIZE from the env) and forwards every argument verbatim; the ranks'
+parameter checksums are gathered and compared (the replica invariant of
+ppo_atari_multigpu.py:360-377). CPU only: the child here is a probe script, not the trainer."""
+import json
+import os
+import socket
+import sys
+import types
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import bench
+from oc_cleanrl_amd.trainer import PPOTrainer
+
+PROBE = """
+import json, os, sys
+if os.environ["RANK"] == "0":
+    print(json.dumps({"argv": sys.argv[1:], "world": os.environ["WORLD_SIZE"],
+                      "local_rank": os.environ["LOCAL_RANK"],
+                      "ipc": os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY")}), flush=True)
+sys.exit(int(os.environ.get("PROBE_RC", "0")))
+"""
+
+
+def test_needs_launch():
+    assert bench.needs_launch(2, {})
+    assert bench.needs_launch(8, {"RANK": "0"})
+    assert not bench.needs_launch(1, {})
+    assert not bench.needs_launch(2, {"WORLD_SIZE": "2"})
+
+
+def test_launcher_cmd_forwards_arguments():
+    argv = ["--gpus", "2", "--steps", "7", "--backend", "gloo", "--device-index", "0",
+            "--set", "x6_gemm=0"]
+    cmd = bench.launcher_cmd(argv, 2, 29511)
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nproc-per-node=2" in cmd and "--nnodes=1" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[cmd.index("--master-port") + 1] == "29511"
+    script = cmd.index(str(bench.ROOT / "bench.py"))
+    assert cmd[script + 1:] == argv
+
+
+def test_launch_runs_ranks_and_forwards_rank0_line(tmp_path, capfd):
+    probe = tmp_path / "probe.py"
+    probe.write_text(PROBE)
+    argv = ["--gpus", "2", "--steps", "3", "--warmup", "1"]
+    rc = bench.launch(argv, 2, script=probe)
+    assert rc == 0
+    out = [json.loads(l) for l in capfd.readouterr().out.splitlines() if l.startswith("{")]
+    assert len(out) == 1  # rank 0 only
+    assert out[0]["argv"] == argv and out[0]["world"] == "2" and out[0]["local_rank"] == "0"
+    assert out[0]["ipc"] == "0"
+
+
+def test_launch_returns_child_exit_code(tmp_path, monkeypatch):
+    probe = tmp_path / "probe.py"
+    probe.write_text(PROBE)
+    monkeypatch.setenv("PROBE_RC", "3")
+    assert bench.launch(["--gpus", "2"], 2, script=probe) != 0
+
+
+def _fake_trainer(seed):
+    g = torch.Generator().manual_seed(seed)
+    return types.SimpleNamespace(params=[torch.randn(5, 3, generator=g), torch.randn(7, generator=g)])
+
+
+def test_param_checksum_is_exact_and_order_sensitive():
+    a = _fake_trainer(0)
+    s = PPOTrainer.param_checksum(a)
+    assert s == PPOTrainer.param_checksum(_fake_trainer(0))
+    b = _fake_trainer(0)
+    b.params[1][3] = torch.nextafter(b.params[1][3], torch.tensor(10.0))  # one ulp
+    assert PPOTrainer.param_checksum(b) != s
+    c = _fake_trainer(0)
+    c.params[0] = c.params[0].flip(0)
+    assert PPOTrainer.param_checksum(c) != s
+
+
+def _replica_worker(rank, world, port, diverge, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    tr = _fake_trainer(0)
+    tr.param_checksum = lambda: PPOTrainer.param_checksum(tr)
+    if diverge and rank == 1:
+        tr.params[0][0, 0] += 1.0
+    try:
+        out[rank] = bench.replica_check(tr, world, torch.device("cpu"))
+    except SystemExit as e:
+        out[rank] = str(e)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("diverge", [False, True])
+def test_replica_check_gloo_world2(diverge):
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out = mp.Manager().dict()
+    mp.spawn(_replica_worker, args=(2, port, diverge, out), nprocs=2, join=True)
+    if diverge:
+        assert all("diverged" in out[r] for r in range(2))
+    else:
+        assert out[0] == out[1] and out[0]["equal"] and len(out[0]["param_checksums"]) == 2

@@ -117,8 +117,6 @@ def test_config2_update_chain_matches_reference(dev, fixture, x6):
             _minibatch(tr, z, j, params)
     finally:
         ops.TIMER = None
-        from oc_cleanrl_amd import agents
-        agents.X6_GEMM = agents.X6_MASK_DX = True  # the trainer set the process-wide default
     x6_sites = sorted(n for n in timer.sites if n.startswith("gemm_x6_"))
     # on: the nine x6 products of config 2 (forward, masked / plain dX, split-K dW); off: none
     assert (len(x6_sites) >= 8) if x6 else not x6_sites, x6_sites

@@ -57,3 +57,22 @@ def test_bench_parses_gemm_sites():
     assert bench.gemm_x6_bytes("gemm_x6_11520x1024x512s1") == 4 * (M * K + N * K + M * N)
     assert bench.gemm_x6_bytes("gemm_x6_11520x1024x512s1m") == (
         4 * (M * K + N * K + M * N) + M * N // 8 + 4 * N * (M // 128))
+
+
+def test_update_gemm_route_is_per_agent():
+    """Two agents in one process keep their own update-GEMM route (Args.x6_gemm per trainer):
+    agents.set_update_gemm marks each Linear's weight, nothing process-wide changes."""
+    import torch.nn as nn
+
+    from oc_cleanrl_amd import agents
+
+    a = agents.make_agent("PPO_OBJ", (4, 12), 6)
+    b = agents.make_agent("PPO_OBJ", (4, 12), 6)
+    agents.set_update_gemm(a, False)
+    agents.set_update_gemm(b, True)
+    lins_a = [m for m in a.modules() if isinstance(m, nn.Linear)]
+    lins_b = [m for m in b.modules() if isinstance(m, nn.Linear)]
+    assert lins_a and all(not agents.x6_route(m.weight) for m in lins_a)
+    assert all(agents.x6_route(m.weight) for m in lins_b)
+    assert agents.x6_route(nn.Linear(4, 4).weight) == agents.X6_GEMM_DEFAULT
+    assert not hasattr(agents, "X6_GEMM") and not hasattr(agents, "X6_MASK_DX")

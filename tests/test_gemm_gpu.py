@@ -173,11 +173,9 @@ def test_relu_bitmask_roundtrip(tile):
 
 
 @pytest.mark.parametrize("mbig", [0, 512, 1024, None])
-def test_mixed_tiles(mbig, monkeypatch):
+def test_mixed_tiles(mbig):
     # variant 56: rows [0, mbig) in 128 x 128 tiles, the rest in 64 x 128 (None: the library's
     # own split); forward with bias + ReLU + bitmask, then the masked dX reading that bitmask
-    if mbig is not None:
-        monkeypatch.setenv("OCPPO_X6_MBIG", str(mbig))
     t = ops.X6_MIXED
     g = torch.Generator(device=DEV).manual_seed(57)
     M, K0, N, N2 = 1024, 256, 256, 128  # x [M, K0] -> h [M, N] -> [M, N2]
@@ -186,7 +184,7 @@ def test_mixed_tiles(mbig, monkeypatch):
     b = _rand(N, gen=g, scale=0.1)
     h = torch.empty(M, N, device=DEV)
     bits = torch.empty(ops.x6_mbits_words(M, N, t), dtype=torch.int64, device=DEV)
-    ops.gemm_x6(x, K0, 1, w, K0, 1, h, N, M, N, K0, bias=b, relu=True, tile=t, mbits_out=bits)
+    ops.gemm_x6(x, K0, 1, w, K0, 1, h, N, M, N, K0, bias=b, relu=True, tile=t, mbits_out=bits, mbig=mbig)
     pre64 = x.double() @ w.double().t() + b.double()
     scale = x.double().abs() @ w.double().abs().t() + b.double().abs()
     _check(h, pre64.clamp_min(0), scale, torch._addmm_activation(b, x, w.t()))
@@ -194,8 +192,8 @@ def test_mixed_tiles(mbig, monkeypatch):
     w2 = _rand(N2, N, gen=g, scale=N2 ** -0.5)
     gp_f, dbp_f = torch.empty(M, N, device=DEV), torch.full((M // 64, N), 7.0, device=DEV)
     gp_b, dbp_b = torch.empty(M, N, device=DEV), torch.full((M // 64, N), 7.0, device=DEV)
-    ops.gemm_x6(gg, N2, 1, w2, 1, N, gp_f, N, M, N, N2, mask=h, dbp=dbp_f, tile=t)
-    ops.gemm_x6(gg, N2, 1, w2, 1, N, gp_b, N, M, N, N2, dbp=dbp_b, tile=t, mbits_in=bits)
+    ops.gemm_x6(gg, N2, 1, w2, 1, N, gp_f, N, M, N, N2, mask=h, dbp=dbp_f, tile=t, mbig=mbig)
+    ops.gemm_x6(gg, N2, 1, w2, 1, N, gp_b, N, M, N, N2, dbp=dbp_b, tile=t, mbits_in=bits, mbig=mbig)
     assert torch.equal(gp_f, gp_b) and torch.equal(dbp_f, dbp_b)
     ref = torch.where(h > 0, gg.double() @ w2.double(), torch.zeros((), dtype=torch.float64, device=DEV))
     _check(gp_f, ref, gg.double().abs() @ w2.double().abs(), torch.ops.aten.threshold_backward(gg @ w2, h, 0))

@@ -43,7 +43,8 @@ def test_gae_golden_bitwise(ops, dev, name):
 
 
 @pytest.mark.parametrize("T_,N", [(1, 1), (128, 1), (7, 5), (128, 128), (200, 130), (64, 1001),
-                                  (128, 1024), (128, 65536), (16, 65540), (33, 262144)])
+                                  (128, 1024), (33, 1030), (200, 2048), (128, 4096), (300, 8192),
+                                  (129, 65535), (128, 65536), (16, 65540), (33, 262144)])
 def test_gae_random_bitwise_vs_oracle(ops, dev, T_, N):
     rng = np.random.default_rng(T_ * 7919 + N)
     r = rng.standard_normal((T_, N)).astype(np.float32)

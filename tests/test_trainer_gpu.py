@@ -552,3 +552,29 @@ def test_gemm_table_is_deterministic_and_matches_default(tmp_path):
     # within 2 % of each other; almost every element is identical
     torch.testing.assert_close(outs[0], outs[2], rtol=0, atol=0.02 * 2.5e-4)
     assert float(((outs[0] - outs[2]).abs() > 2e-7).float().mean()) < 0.01
+
+
+def test_two_trainers_keep_their_own_update_gemm_route(dev):
+    """Args.x6_gemm is per-trainer state (agents.set_update_gemm on its own agent): a trainer
+    built with x6 off and one built after it with x6 on run their own routes, in either order,
+    at config-2 sizes (the x6 products need >= 256 output tiles)."""
+    from oc_cleanrl_amd import ops
+    from oc_cleanrl_amd.trainer import KernelTimer, PPOTrainer
+
+    def sites(tr):
+        timer = KernelTimer(enabled=True)
+        ops.TIMER = timer
+        try:
+            tr.train_iteration(collect_metrics=False)
+            torch.cuda.synchronize()
+        finally:
+            ops.TIMER = None
+        return sorted(n for n in timer.sites if n.startswith("gemm_x6_"))
+
+    kw = dict(num_envs=128, num_steps=128, encoder_dims=(256, 512, 1024, 512),
+              decoder_dims=(512,), update_epochs=1, cuda_graphs=False)
+    off = PPOTrainer(small_args(x6_gemm=False, **kw), dev)
+    on = PPOTrainer(small_args(x6_gemm=True, **kw), dev)
+    assert len(sites(on)) >= 8
+    assert sites(off) == []
+    assert len(sites(on)) >= 8

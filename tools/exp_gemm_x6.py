@@ -52,11 +52,17 @@ def main():
     ap.add_argument("--only", default=None, help="kind,M,N,K: one shape (profiling)")
     ap.add_argument("--tiles", default=None, help="comma-separated variants (default: all built)")
     ap.add_argument("--mbig", type=int, default=None,
-                    help="rows in 128 x 128 tiles for the mixed variant (OCPPO_X6_MBIG)")
+                    help="rows in 128 x 128 tiles for the mixed variant (ocppo_gemm_x6's mbig)")
     a = ap.parse_args()
     if a.mbig is not None:
-        import os
-        os.environ["OCPPO_X6_MBIG"] = str(a.mbig)
+        # every mixed-variant ops.gemm_x6 call of this run with the given split
+        _gemm_x6 = ops.gemm_x6
+
+        def _with_mbig(*args, **kw):
+            if kw.get("tile") == ops.X6_MIXED:
+                kw["mbig"] = a.mbig
+            return _gemm_x6(*args, **kw)
+        ops.gemm_x6 = _with_mbig
     shapes = SHAPES
     if a.only:
         k, *dims = a.only.split(",")
