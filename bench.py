@@ -231,12 +231,19 @@ def needs_launch(gpus: int, env=os.environ) -> bool:
 
 def launch(argv, gpus: int, script=None) -> int:
     """Run the N ranks as ONE child process tree (not an exec), before this process makes any GPU
-    call; the child's stdout is this process's (rank 0 prints the line). Returns its exit code."""
+    call. Rank 0's JSON line is forwarded to stdout as it arrives; anything else the ranks print
+    on stdout (gloo's connection chatter) goes to stderr, so stdout holds the line alone.
+    Returns the child's exit code."""
     import subprocess
 
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    return subprocess.run(launcher_cmd(argv, gpus, free_port(), script), env=env).returncode
+    p = subprocess.Popen(launcher_cmd(argv, gpus, free_port(), script), env=env,
+                         stdout=subprocess.PIPE, text=True, bufsize=1)
+    for line in p.stdout:
+        (sys.stdout if line.startswith("{") else sys.stderr).write(line)
+        (sys.stdout if line.startswith("{") else sys.stderr).flush()
+    return p.wait()
 
 
 def replica_check(tr, world: int, device) -> dict:

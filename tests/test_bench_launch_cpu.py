@@ -19,6 +19,7 @@ from oc_cleanrl_amd.trainer import PPOTrainer
 
 PROBE = """
 import json, os, sys
+print("[Gloo] Rank", os.environ["RANK"], "chatter", flush=True)
 if os.environ["RANK"] == "0":
     print(json.dumps({"argv": sys.argv[1:], "world": os.environ["WORLD_SIZE"],
                       "local_rank": os.environ["LOCAL_RANK"],
@@ -52,8 +53,11 @@ def test_launch_runs_ranks_and_forwards_rank0_line(tmp_path, capfd):
     argv = ["--gpus", "2", "--steps", "3", "--warmup", "1"]
     rc = bench.launch(argv, 2, script=probe)
     assert rc == 0
-    out = [json.loads(l) for l in capfd.readouterr().out.splitlines() if l.startswith("{")]
-    assert len(out) == 1  # rank 0 only
+    cap = capfd.readouterr()
+    lines = cap.out.splitlines()
+    assert len(lines) == 1  # rank 0's line only; the ranks' other stdout went to stderr
+    out = [json.loads(lines[0])]
+    assert cap.err.count("chatter") == 2
     assert out[0]["argv"] == argv and out[0]["world"] == "2" and out[0]["local_rank"] == "0"
     assert out[0]["ipc"] == "0"
 
