@@ -25,7 +25,7 @@ Fixtures:
   init_{name}.json    per-parameter checksums of seeded default-size agents + outputs on a fixed
                       input (pins layer order, state-dict keys and orthogonal init order)
 
-    python tests/golden/gen_golden.py
+    python tests/golden/gen_golden.py [update_config2]
 """
 from __future__ import annotations
 
@@ -393,11 +393,11 @@ def gen_update_config2(T=128, N=128, F=12, A=6, W=4, seed=25, name="update_confi
                                  vf_coef=0.5, max_grad_norm=0.5, track=False, minibatch_size=M)
     optimizer = optim.Adam(agent.parameters(), lr=2.5e-4, eps=1e-5)
     sds = [{k: v.detach().clone().numpy() for k, v in agent.state_dict().items()}]
-    gns, stats, grads = [], [], []
+    gns, stats, grads, pre32 = [], [], [], []
     for start in (0, M):
         mb_inds = perm[start:start + M]
-        ns = dict(torch=torch, nn=nn, np=np, agent=agent, args=args, optimizer=optimizer,
-                  b_obs=b_obs, b_actions=b_actions, b_logprobs=b_logprobs,
+        ns = dict(torch=torch, nn=_recording_nn(agent, pre32), np=np, agent=agent, args=args,
+                  optimizer=optimizer, b_obs=b_obs, b_actions=b_actions, b_logprobs=b_logprobs,
                   b_advantages=b_advantages, b_returns=b_returns, b_values=b_values,
                   mb_inds=mb_inds, clipfracs=[], start=start)
         exec(UPDATE_CODE, ns)
@@ -434,7 +434,41 @@ def gen_update_config2(T=128, N=128, F=12, A=6, W=4, seed=25, name="update_confi
                                              np.abs(v).max()])
             out[f"grad{i}::{k}"] = (v.reshape(-1)[out[f"pick::{k}"]] if f"pick::{k}" in out
                                    else v)
+    # f64 twin: the same update block on the same inputs in float64, at the reference's own f32
+    # parameters before each minibatch (so minibatch 1 is evaluated where the f32 reference
+    # evaluated it); stored are the PRE-clip gradients of both runs (the f32 reference's own,
+    # recorded as clip_grad_norm_ received them) and the f64 grad norms. The gap f32 -> f64 is
+    # the reference's own rounding, the yardstick of the GPU chain's per-tensor check.
+    agent64 = PPObj(Envs((W, F), A), "cpu", (256, 512, 1024, 512), (512,)).double()
+    f64 = lambda t: t.double()  # noqa: E731
+    for i, start in enumerate((0, M)):
+        agent64.load_state_dict({k: torch.from_numpy(v).double() for k, v in sds[i].items()})
+        pre64 = []
+        ns = dict(torch=torch, nn=_recording_nn(agent64, pre64), np=np, agent=agent64, args=args,
+                  optimizer=optim.Adam(agent64.parameters(), lr=2.5e-4, eps=1e-5),
+                  b_obs=f64(b_obs), b_actions=b_actions, b_logprobs=f64(b_logprobs),
+                  b_advantages=f64(b_advantages), b_returns=f64(b_returns),
+                  b_values=f64(b_values), mb_inds=perm[start:start + M], clipfracs=[],
+                  start=start)
+        exec(UPDATE_CODE, ns)
+        out[f"grad_norm64_{i}"] = np.array(float(ns["gn"]))
+        for k, v in pre64[0].items():
+            out[f"gnorm64pre{i}::{k}"] = np.array([np.linalg.norm(v), np.abs(v).max()])
+            pk = out.get(f"pick::{k}")
+            out[f"grad64pre{i}::{k}"] = v.reshape(-1)[pk] if pk is not None else v
+            v32 = pre32[i][k]
+            out[f"gradpre{i}::{k}"] = v32.reshape(-1)[pk] if pk is not None else v32
     np.savez_compressed(OUT / f"{name}.npz", **out)
+
+
+def _recording_nn(agent, record):
+    """`nn` for an exec'd update block whose clip_grad_norm_ first records every parameter's
+    gradient as it stands (pre-clip), then runs torch's own clip: numerics untouched."""
+    def clip_grad_norm_(params, max_norm, *a, **kw):
+        record.append({k: p.grad.detach().clone().numpy() for k, p in agent.named_parameters()})
+        return nn.utils.clip_grad_norm_(params, max_norm, *a, **kw)
+
+    return types.SimpleNamespace(utils=types.SimpleNamespace(clip_grad_norm_=clip_grad_norm_))
 
 
 def gen_update_cartpole(B=512, M=128, seed=23, name="update_cartpole"):
@@ -564,6 +598,9 @@ def gen_replay(size=7, obs_shape=(4, 5), adds=10, seed=31, name="replay_sb3"):
 
 def main():
     torch.set_num_threads(8)
+    if sys.argv[1:] == ["update_config2"]:  # just the config-2 fixture (it takes a minute)
+        gen_update_config2()
+        return
     gen_gae(16, 8, "synthetic", 1)
     gen_gae(123, 7, "jaxtest", 42)
     gen_gae(128, 128, "synthetic", 2)

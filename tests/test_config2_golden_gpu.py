@@ -122,10 +122,30 @@ def test_config2_update_chain_matches_reference(dev, fixture, x6):
     assert (len(x6_sites) >= 8) if x6 else not x6_sites, x6_sites
 
 
+def f64_errors(z, j, params):
+    """Per tensor, the PRE-clip gradient error against the fixture's float64 twin of the same
+    update block (gen_golden: the same inputs in f64 at the f32 reference's parameters), relative
+    to the tensor's largest f64 element: (ours, the f32 reference's own)."""
+    out = {}
+    for k, p in params.items():
+        g = p.grad.detach().double().cpu().reshape(-1)
+        if f"pick::{k}" in z:
+            g = g[torch.from_numpy(z[f"pick::{k}"])]
+        g64 = torch.from_numpy(z[f"grad64pre{j}::{k}"]).reshape(-1)
+        g32 = torch.from_numpy(z[f"gradpre{j}::{k}"]).double().reshape(-1)
+        mx = float(z[f"gnorm64pre{j}::{k}"][1])
+        out[k] = (float((g - g64).abs().max()) / mx, float((g32 - g64).abs().max()) / mx)
+    return out
+
+
 def _minibatch(tr, z, j, params):
     """One minibatch of the chain against the fixture's grads, stats and parameters."""
     tr._forward_backward(j)
     gn = float(torch.linalg.vector_norm(tr.grad_buf.double()))
+    e64 = f64_errors(z, j, params)
+    print(f"minibatch {j}: grad norm {gn:.10g}, f64 {float(z[f'grad_norm64_{j}']):.10g}, f32 ref "
+          f"{z['grad_norms'][j]:.10g}; pre-clip error vs f64 per tensor (ours / reference f32): "
+          + ", ".join(f"{k} {a:.2g}/{b:.2g}" for k, (a, b) in e64.items()))
     # the gradients the reference's Adam saw (after clip_grad_norm_: x max_norm / (norm +
     # 1e-6)), per tensor, at the fixture's sample points, relative to the tensor's largest
     coef = min(1.0, 0.5 / (gn + 1e-6))
