@@ -390,9 +390,16 @@ __global__ __launch_bounds__(256) void sum_splits_kernel(const float4* __restric
 // [nsb, nsb + ceil(N / 16)) each own 16 columns of db: 4 column quads x 64 chunk groups, each
 // thread summing its chunks in order, then the 64 group sums in group order (LDS): one pass,
 // deterministic. (16 columns per block: the frame scatter's 720 chunk partials at [11520 x 512]
-// take two load batches per thread instead of six.)
+// take two load batches per thread instead of six.) Both folds add in float64 and round once:
+// a bias gradient is a column sum over ~10^4 rows with heavy cancellation, and a left fold of
+// 90-720 f32 partials rounded at every step cost it up to 1.6e-4 of its largest element against
+// the reference's own 2e-5 (tests/test_config2_golden_gpu.py, against the f64 twin); the split
+// combine of the weight gradient likewise (S <= 16 adds per element; HBM-bound either way).
 constexpr int kDbQuads = 4;
 constexpr int kDbGroups = 64;
+struct d4 {
+  double x, y, z, w;
+};
 template <int S>
 __global__ __launch_bounds__(256) void sum_splits_db_kernel(const float4* __restrict__ part,
                                                             int64_t n4, float4* __restrict__ out,
@@ -406,22 +413,23 @@ __global__ __launch_bounds__(256) void sum_splits_db_kernel(const float4* __rest
       float4 v[S];
 #pragma unroll
       for (int s = 0; s < S; ++s) v[s] = part[s * n4 + i];
-      float4 a = v[0];
+      double ax = v[0].x, ay = v[0].y, az = v[0].z, aw = v[0].w;
 #pragma unroll
       for (int s = 1; s < S; ++s) {
-        a.x += v[s].x; a.y += v[s].y; a.z += v[s].z; a.w += v[s].w;
+        ax += v[s].x; ay += v[s].y; az += v[s].z; aw += v[s].w;
       }
-      out[i] = a;
+      out[i] = make_float4(static_cast<float>(ax), static_cast<float>(ay),
+                           static_cast<float>(az), static_cast<float>(aw));
     }
     return;
   }
-  __shared__ float4 red[kDbGroups][kDbQuads];
+  __shared__ d4 red[kDbGroups][kDbQuads];
   const int cb = blockIdx.x - nsb;
   const int q = threadIdx.x % kDbQuads, gi = threadIdx.x / kDbQuads;  // column quad, chunk group
   const int64_t col = static_cast<int64_t>(cb) * (4 * kDbQuads) + 4 * q;
   const int cpg = (chunks + kDbGroups - 1) / kDbGroups;
   const int c0 = gi * cpg, c1 = c0 + cpg < chunks ? c0 + cpg : chunks;
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  d4 acc{0.0, 0.0, 0.0, 0.0};
   if (col < N) {
     for (int c = c0; c < c1; c += 8) {
       float4 v[8];
@@ -438,12 +446,14 @@ __global__ __launch_bounds__(256) void sum_splits_db_kernel(const float4* __rest
   red[gi][q] = acc;
   __syncthreads();
   if (gi == 0 && col < N) {
-    float4 t = red[0][q];
+    d4 t = red[0][q];
     for (int k = 1; k < kDbGroups; ++k) {
-      const float4 v = red[k][q];
+      const d4 v = red[k][q];
       t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
     }
-    *reinterpret_cast<float4*>(db + col) = t;
+    *reinterpret_cast<float4*>(db + col) =
+        make_float4(static_cast<float>(t.x), static_cast<float>(t.y), static_cast<float>(t.z),
+                    static_cast<float>(t.w));
   }
 }
 

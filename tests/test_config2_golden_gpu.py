@@ -91,11 +91,16 @@ def test_config2_gae_matches_reference(dev, fixture):
 
 @pytest.mark.parametrize("x6", [True, False])
 def test_config2_update_chain_matches_reference(dev, fixture, x6):
-    """Two minibatch updates of the bench's chain vs the reference's update block at config 2:
-    grad norms to 1e-5, loss scalars to 1e-4, and every parameter (4096 fixed samples of the
-    large ones) within 1 % of one Adam step (lr) -- Adam's m / (sqrt(v) + eps) is sensitive to
-    the f32 summation order of a gradient element only where |g| ~ eps. (Graph replay of this
-    chain is bitwise the eager run: test_trainer_gpu.py::test_graph_replay_matches_eager.)"""
+    """Two minibatch updates of the bench's chain vs the reference's update block at config 2.
+    Against the fixture's float64 twin (same inputs, same parameters): the grad norm within 1e-5
+    (the f32 reference's own is 2.2e-5 off), every tensor's pre-clip gradient within 3e-4 of its
+    largest element -- an end-to-end figure dominated by ReLU decisions of pre-activations
+    within rounding distance of 0 (measured <= 1.6e-4; the arithmetic alone is checked to f32
+    level by test_config2_chain_matches_f64_under_its_own_relu_decisions). Against the f32
+    reference: loss scalars to 1e-4, and every parameter (4096 fixed samples of the large ones)
+    within 1 % of one Adam step (lr) -- Adam's m / (sqrt(v) + eps) is sensitive to the f32
+    summation order of a gradient element only where |g| ~ eps. (Graph replay of this chain is
+    bitwise the eager run: test_trainer_gpu.py::test_graph_replay_matches_eager.)"""
     from oc_cleanrl_amd import ops
     from oc_cleanrl_amd.trainer import KernelTimer
 
@@ -139,32 +144,21 @@ def f64_errors(z, j, params):
 
 
 def _minibatch(tr, z, j, params):
-    """One minibatch of the chain against the fixture's grads, stats and parameters."""
+    """One minibatch of the chain against the fixture's f64 twin, stats and parameters."""
     tr._forward_backward(j)
     gn = float(torch.linalg.vector_norm(tr.grad_buf.double()))
+    gn64 = float(z[f"grad_norm64_{j}"])
     e64 = f64_errors(z, j, params)
-    print(f"minibatch {j}: grad norm {gn:.10g}, f64 {float(z[f'grad_norm64_{j}']):.10g}, f32 ref "
+    print(f"minibatch {j}: grad norm {gn:.10g}, f64 {gn64:.10g}, f32 ref "
           f"{z['grad_norms'][j]:.10g}; pre-clip error vs f64 per tensor (ours / reference f32): "
           + ", ".join(f"{k} {a:.2g}/{b:.2g}" for k, (a, b) in e64.items()))
-    # the gradients the reference's Adam saw (after clip_grad_norm_: x max_norm / (norm +
-    # 1e-6)), per tensor, at the fixture's sample points, relative to the tensor's largest
-    coef = min(1.0, 0.5 / (gn + 1e-6))
-    gerr = {}
-    for k, p in params.items():
-        g = p.grad.detach().double().cpu().reshape(-1) * coef
-        if f"pick::{k}" in z:
-            g = g[torch.from_numpy(z[f"pick::{k}"])]
-        ref = torch.from_numpy(z[f"grad{j}::{k}"]).double().reshape(-1)
-        gerr[k] = float((g - ref).abs().max()) / float(z[f"gnorm{j}::{k}"][1])
-    print(f"minibatch {j}: grad norm {gn:.7g} vs {z['grad_norms'][j]:.7g}; worst relative "
-          f"grad error per tensor: " + ", ".join(f"{k} {e:.2g}" for k, e in gerr.items()))
     tr._opt_step()
     torch.cuda.synchronize()
     st = tr.stats[j].cpu().numpy()
     ref = z["stats"][j]
     np.testing.assert_allclose(st, ref, rtol=1e-4, atol=1e-6, err_msg=f"stats mb {j}")
-    assert abs(gn - z["grad_norms"][j]) <= 1e-4 * z["grad_norms"][j], (j, gn)
-    assert max(gerr.values()) <= 1e-3, gerr
+    assert abs(gn - gn64) <= 1e-5 * gn64, (j, gn, gn64)
+    assert max(a for a, _ in e64.values()) <= 3e-4, e64
     worst = 0.0
     for k, p in params.items():
         got = p.detach().cpu().reshape(-1)
@@ -176,3 +170,113 @@ def _minibatch(tr, z, j, params):
         assert float(err.max()) <= 0.01 * LR, (j, k, float(err.max()))
         assert float((err > 2e-7).float().mean()) < 0.01, (j, k)
     print(f"minibatch {j}: worst |param - ref| = {worst:.3g} ({worst / LR:.3g} lr)")
+
+
+def _row_hash(t):
+    """An exact per-row fingerprint of an f32 matrix (its bit patterns, position-weighted)."""
+    bits = t.contiguous().view(torch.int32).to(torch.int64)
+    w = torch.arange(1, t.shape[1] + 1, device=t.device, dtype=torch.int64) * 2654435761
+    return (bits * w).sum(1)
+
+
+def _f64_under_decisions(tr, j, saved):
+    """Float64 gradients of minibatch j's loss (the reference's update block, ppo_atari_oc.py:
+    566-602, in f64) through the same network at the chain's current parameters, with every
+    ReLU taking the decision the chain's own f32 forward took. saved = the tensors the chain's
+    forward saved for backward: the distinct frames' features and ReLU outputs [cap, .] and the
+    decoder's input / output [M, .]."""
+    ag = tr.agent
+    M, cap = tr.M, tr.plan[0].shape[1]
+    uniq = []
+    for t in saved:  # distinct f32 [cap, *] / [M, *] tensors in save order
+        if (t.dtype == torch.float32 and t.dim() == 2 and t.shape[0] in (cap, M)
+                and all(t.data_ptr() != u.data_ptr() for u in uniq)):
+            uniq.append(t)
+    frames_ = [t for t in uniq if t.shape[0] == cap]
+    dec = [t for t in uniq if t.shape[0] == M]
+    x0, relu_outs = frames_[0], frames_[1:]
+    dec_in, h5 = dec[0], dec[1]
+    lins = [m for m in ag.network if isinstance(m, torch.nn.Linear)]
+    assert [t.shape[1] for t in relu_outs] == [m.out_features for m in lins[:4]]
+    P = {n: p.detach().double().clone().requires_grad_(True) for n, p in ag.named_parameters()}
+    x = x0.double()
+    own = x0.double()  # the f64 forward with its own ReLU decisions: the flips of the chain's
+    flips = []
+    with torch.no_grad():
+        zs = []
+        for i in range(len(relu_outs)):
+            zo = own @ P[f"network.{2 * i}.weight"].t() + P[f"network.{2 * i}.bias"]
+            zs.append(zo)
+            own = torch.relu(zo)
+    for i, h in enumerate(relu_outs):
+        x = (x @ P[f"network.{2 * i}.weight"].t() + P[f"network.{2 * i}.bias"]) * (h > 0)
+        # padding rows (id -1) are all-zero frames no sample reads
+        flips.append(int(((h > 0) != (zs[i] > 0))[:int((tr.plan[0][j] >= 0).sum())].sum()))
+    enc = relu_outs[-1]
+    # which encoding row each decoder-input slot holds (exact bit match)
+    he, order = torch.sort(_row_hash(enc))
+    chunks = dec_in.reshape(M * tr.obs_shape[0], enc.shape[1])
+    pos = order[torch.searchsorted(he, _row_hash(chunks))]
+    assert torch.equal(enc[pos], chunks)
+    d = x[pos].reshape(M, -1)
+    dn = tr.agent._flat + 1
+    with torch.no_grad():
+        zo = own[pos].reshape(M, -1) @ P[f"network.{dn}.weight"].t() + P[f"network.{dn}.bias"]
+        flips.append(int(((h5 > 0) != (zo > 0)).sum()))
+    h = (d @ P[f"network.{dn}.weight"].t() + P[f"network.{dn}.bias"]) * (h5 > 0)
+    logits = h @ P["actor.weight"].t() + P["actor.bias"]
+    value = (h @ P["critic.weight"].t() + P["critic.bias"]).view(-1)
+    sl = slice(j * M, (j + 1) * M)
+    mb = {k: v[sl] for k, v in tr.mb.items() if k != "adv_stats"}
+    logp = torch.log_softmax(logits, 1)
+    newlp = logp.gather(1, mb["actions"].view(-1, 1)).view(-1)
+    ent = -(logp.exp() * logp).sum(1)
+    ratio = (newlp - mb["logprobs"].double()).exp()
+    adv = mb["advantages"].double()
+    adv = (adv - adv.mean()) / (adv.std() + 1e-8)
+    pg = torch.max(-adv * ratio, -adv * torch.clamp(ratio, 1 - 0.1, 1 + 0.1)).mean()
+    ret, vold = mb["returns"].double(), mb["values"].double()
+    vc = vold + torch.clamp(value - vold, -0.1, 0.1)
+    vl = 0.5 * torch.max((value - ret) ** 2, (vc - ret) ** 2).mean()
+    loss = pg - 0.01 * ent.mean() + 0.5 * vl
+    loss.backward()
+    return {n: p.grad for n, p in P.items()}, flips
+
+
+@pytest.mark.parametrize("x6", [True, False])
+def test_config2_chain_matches_f64_under_its_own_relu_decisions(dev, fixture, x6):
+    """The chain's gradients equal float64 arithmetic through the same network at the same
+    parameters when every ReLU takes the decision the chain's f32 forward took. This separates
+    the two sources of difference from f64: arithmetic (checked here, per tensor, at f32 GEMM
+    level) and the ReLU decision of pre-activations within rounding distance of 0, which any f32
+    forward (the reference's CPU one included) flips now and then: a flip moves a bias gradient
+    by that element's upstream gradient (tools/exp_chain_accuracy.py counts them per route)."""
+    z = fixture
+    tr = config2_trainer(dev, z, x6_gemm=x6)
+    tr.advantages.view(-1).copy_(torch.from_numpy(z["advantages"]).to(dev))
+    tr.returns.view(-1).copy_(torch.from_numpy(z["returns"]).to(dev))
+    tr.load_permutation(full_permutation(z, tr.E, tr.B))
+    tr._prepare_minibatches()
+    params = dict(tr.agent.named_parameters())
+    ref_err = {k: e_ref for k, (_, e_ref) in f64_errors(z, 0, params).items()}
+    for j in range(2):
+        saved = []
+        with torch.autograd.graph.saved_tensors_hooks(lambda t: saved.append(t) or t,
+                                                      lambda t: t):
+            tr._forward_backward(j)
+        g64, flips = _f64_under_decisions(tr, j, saved)
+        errs = {}
+        for k, p in params.items():
+            mx = float(g64[k].abs().max())
+            errs[k] = float((p.grad.double() - g64[k]).abs().max()) / mx
+        print(f"minibatch {j} (x6={x6}): ReLU decisions unlike f64's per layer {flips}; error vs "
+              "f64 under the chain's decisions: "
+              + ", ".join(f"{k} {e:.2g}" for k, e in errs.items()))
+        # f32 level: within 3x of the f32 reference's own worst per-tensor error against the f64
+        # twin at the same parameters (minibatch 0 of the fixture: 1.7e-6, actor.weight)
+        bound = 3 * max(ref_err.values())
+        assert max(errs.values()) <= bound, (j, errs, bound)
+        # flips: a few per million decisions (pre-activations within rounding distance of 0)
+        assert sum(flips) <= 1e-5 * (tr.plan[0].shape[1] * 2304 + tr.M * 512), flips
+        tr._opt_step()
+        torch.cuda.synchronize()
