@@ -25,7 +25,7 @@ Fixtures:
   init_{name}.json    per-parameter checksums of seeded default-size agents + outputs on a fixed
                       input (pins layer order, state-dict keys and orthogonal init order)
 
-    python tests/golden/gen_golden.py [update_config2]
+    python tests/golden/gen_golden.py [update_config2 update_config3 ...]
 """
 from __future__ import annotations
 
@@ -471,6 +471,147 @@ def _recording_nn(agent, record):
     return types.SimpleNamespace(utils=types.SimpleNamespace(clip_grad_norm_=clip_grad_norm_))
 
 
+def config3_weights(agent, seed):
+    """config2_weights for any layer shape: weight ~ N(0, 1) * gain / sqrt(fan_in), fan_in =
+    in x kh x kw for a convolution (the NatureCNN of config 3), numpy PCG64, state_dict order."""
+    rng = np.random.default_rng(seed)
+    sd = {}
+    for k, v in agent.state_dict().items():
+        if k.endswith("weight"):
+            gain = 0.01 if k.startswith("actor") else 1.0 if k.startswith("critic") else 2 ** 0.5
+            w = rng.standard_normal(tuple(v.shape)) * (gain / np.sqrt(np.prod(v.shape[1:])))
+        else:
+            w = rng.standard_normal(tuple(v.shape)) * 0.05
+        sd[k] = torch.from_numpy(w.astype(np.float32))
+    return sd
+
+
+def breakout_frames(rng, n):
+    """n synthetic 84x84 u8 Breakout-like frames: a brick wall (rows of 6 gray levels, a random
+    subset of bricks knocked out), a paddle and a ball at random places, black elsewhere."""
+    f = np.zeros((n, 84, 84), np.uint8)
+    levels = np.array([200, 180, 160, 140, 120, 100], np.uint8)
+    for r in range(6):
+        keep = rng.random((n, 14)) < 0.8
+        row = np.repeat(np.where(keep, levels[r], 0).astype(np.uint8), 6, axis=1)
+        f[:, 18 + 3 * r:21 + 3 * r, :] = row[:, None, :]
+    px = rng.integers(0, 76, n)
+    bx, by = rng.integers(0, 82, n), rng.integers(30, 76, n)
+    for i in range(n):
+        f[i, 78:80, px[i]:px[i] + 8] = 144
+        f[i, by[i]:by[i] + 2, bx[i]:bx[i] + 2] = 236
+    return f
+
+
+def gen_update_config3(T=16, N=256, A=4, W=4, seed=27, name="update_config3"):
+    """BASELINE config 3's network at its minibatch size: PPODefault (NatureCNN, 84x84x4,
+    NormalizeImg) on a rollout-structured batch of T x N = 16 x 256 synthetic Breakout frame
+    stacks (the frame-stack rule with resets, as in gen_update_config2), and two minibatch
+    updates of 2048 through the reference's update block (ppo_atari_oc.py:566-610). Stored: the
+    distinct frames [T+W, N, 84, 84] u8 and the dones (the test rebuilds the stacks), actions /
+    log-probs / values / rewards, GAE advantages / returns from the reference block (:533-547),
+    the permutation, per-minibatch loss scalars and grad norms, pre-clip gradients of the f32
+    reference and of its float64 twin at the same parameters, and the parameters after each
+    update (tensors above 16K elements as 4096 fixed samples)."""
+    rng = np.random.default_rng(seed)
+    # timeline row s + W - 1 = env n's frame of step s, s in [-(W-1), T]
+    frames = breakout_frames(rng, (T + W) * N).reshape(T + W, N, 84, 84)
+    dones = (rng.random((T + 1, N)) < 0.02).astype(np.float32)
+    obs = np.zeros((T + 1, N, W, 84, 84), np.uint8)
+    # obs[t] slot w = the frame of step t - (W-1) + w (timeline row t + w), clipped to the
+    # latest reset: a reset at step t fills every slot with that step's frame
+    last_reset = np.full(N, -10 ** 9)
+    for t in range(T + 1):
+        last_reset = np.where(dones[t] != 0, t, last_reset)
+        for w in range(W):
+            src = np.maximum(t - (W - 1) + w, last_reset)  # step whose frame fills the slot
+            obs[t, :, w] = frames[src + W - 1, np.arange(N)]
+    agent = PPODefault(Envs((W, 84, 84), A), "cpu")
+    sd0 = config3_weights(agent, seed)
+    agent.load_state_dict(sd0)
+    B, M = T * N, T * N // 2
+    b_obs = torch.from_numpy(obs[:T].reshape(B, W, 84, 84).astype(np.float32))
+    torch.manual_seed(seed)
+    with torch.no_grad():
+        hid = agent.network(b_obs)
+        dist = torch.distributions.Categorical(logits=agent.actor(hid))
+        b_actions = dist.sample()
+        lp = dist.log_prob(b_actions)
+        val = agent.critic(hid).view(-1)
+        next_value = agent.critic(agent.network(torch.from_numpy(
+            obs[T].astype(np.float32)))).view(-1)
+    u = rng.random((T, N))
+    rewards = np.where(u < 0.02, 1.0, 0.0).astype(np.float32)
+    values = (val + torch.from_numpy((rng.standard_normal(B) * 0.3).astype(np.float32)))
+    values = values.view(T, N).contiguous()
+    nv = next_value.reshape(N)
+    ns = dict(torch=torch, agent=types.SimpleNamespace(get_value=lambda x: nv.reshape(1, N)),
+              args=types.SimpleNamespace(num_steps=T, gamma=0.99, gae_lambda=0.95),
+              device="cpu", next_obs=None, rewards=torch.from_numpy(rewards), values=values,
+              dones=torch.from_numpy(dones[:T]), next_done=torch.from_numpy(dones[T]))
+    exec(GAE_CODE, ns)
+    b_advantages = ns["advantages"].reshape(-1)
+    b_returns = ns["returns"].reshape(-1)
+    b_values = values.reshape(-1)
+    b_logprobs = lp + torch.from_numpy((rng.standard_normal(B) * 0.15).astype(np.float32))
+    perm = rng.permutation(B)
+    args = types.SimpleNamespace(clip_coef=0.1, norm_adv=True, clip_vloss=True, ent_coef=0.01,
+                                 vf_coef=0.5, max_grad_norm=0.5, track=False, minibatch_size=M)
+    optimizer = optim.Adam(agent.parameters(), lr=2.5e-4, eps=1e-5)
+    sds = [{k: v.detach().clone().numpy() for k, v in agent.state_dict().items()}]
+    gns, stats, pre32 = [], [], []
+    for start in (0, M):
+        mb_inds = perm[start:start + M]
+        ns = dict(torch=torch, nn=_recording_nn(agent, pre32), np=np, agent=agent, args=args,
+                  optimizer=optimizer, b_obs=b_obs, b_actions=b_actions, b_logprobs=b_logprobs,
+                  b_advantages=b_advantages, b_returns=b_returns, b_values=b_values,
+                  mb_inds=mb_inds, clipfracs=[], start=start)
+        exec(UPDATE_CODE, ns)
+        gns.append(float(ns["gn"]))
+        mba = b_advantages[mb_inds]
+        stats.append([ns["loss"].item(), ns["pg_loss"].item(), ns["v_loss"].item(),
+                      ns["entropy_loss"].item(), ns["old_approx_kl"].item(),
+                      ns["approx_kl"].item(), ns["clipfracs"][-1], mba.mean().item(),
+                      mba.std().item()])
+        sds.append({k: v.detach().clone().numpy() for k, v in agent.state_dict().items()})
+    out = dict(frames=frames, dones=dones, actions=b_actions.numpy().astype(np.int64),
+               logprobs=b_logprobs.numpy(), values=b_values.numpy(), rewards=rewards,
+               next_value=nv.numpy(), advantages=b_advantages.numpy(),
+               returns=b_returns.numpy(), perm=perm.astype(np.int64), M=M, seed=seed,
+               grad_norms=np.array(gns, np.float64), stats=np.array(stats, np.float32),
+               obs_sum=np.array(obs.astype(np.int64).sum()))
+    pick_rng = np.random.default_rng(seed + 1)
+    for k, v in sds[0].items():
+        v64 = v.astype(np.float64)
+        out[f"sum0::{k}"] = np.array([v64.sum(), (v64 ** 2).sum()])
+        if v.size > (1 << 14):
+            out[f"pick::{k}"] = np.sort(pick_rng.choice(v.size, 4096, replace=False))
+    for i, sd in enumerate(sds[1:], 1):
+        for k, v in sd.items():
+            pk = out.get(f"pick::{k}")
+            out[f"sd{i}::{k}"] = v.reshape(-1)[pk] if pk is not None else v
+    agent64 = PPODefault(Envs((W, 84, 84), A), "cpu").double()
+    f64 = lambda t: t.double()  # noqa: E731
+    for i, start in enumerate((0, M)):
+        agent64.load_state_dict({k: torch.from_numpy(v).double() for k, v in sds[i].items()})
+        pre64 = []
+        ns = dict(torch=torch, nn=_recording_nn(agent64, pre64), np=np, agent=agent64, args=args,
+                  optimizer=optim.Adam(agent64.parameters(), lr=2.5e-4, eps=1e-5),
+                  b_obs=f64(b_obs), b_actions=b_actions, b_logprobs=f64(b_logprobs),
+                  b_advantages=f64(b_advantages), b_returns=f64(b_returns),
+                  b_values=f64(b_values), mb_inds=perm[start:start + M], clipfracs=[],
+                  start=start)
+        exec(UPDATE_CODE, ns)
+        out[f"grad_norm64_{i}"] = np.array(float(ns["gn"]))
+        for k, v in pre64[0].items():
+            out[f"gnorm64pre{i}::{k}"] = np.array([np.linalg.norm(v), np.abs(v).max()])
+            pk = out.get(f"pick::{k}")
+            out[f"grad64pre{i}::{k}"] = v.reshape(-1)[pk] if pk is not None else v
+            v32 = pre32[i][k]
+            out[f"gradpre{i}::{k}"] = v32.reshape(-1)[pk] if pk is not None else v32
+    np.savez_compressed(OUT / f"{name}.npz", **out)
+
+
 def gen_update_cartpole(B=512, M=128, seed=23, name="update_cartpole"):
     """Config 1: two minibatch updates of cleanrl/ppo.py's own update block (:250-290, clip 0.2)
     on its own Agent class (:94-126, exec'd), the whole learner step of ppo.py on CartPole-shaped
@@ -598,8 +739,9 @@ def gen_replay(size=7, obs_shape=(4, 5), adds=10, seed=31, name="replay_sb3"):
 
 def main():
     torch.set_num_threads(8)
-    if sys.argv[1:] == ["update_config2"]:  # just the config-2 fixture (it takes a minute)
-        gen_update_config2()
+    if sys.argv[1:]:  # just the named fixtures, e.g. update_config2 update_config3
+        for n in sys.argv[1:]:
+            globals()[f"gen_{n}"]()
         return
     gen_gae(16, 8, "synthetic", 1)
     gen_gae(123, 7, "jaxtest", 42)
@@ -629,6 +771,8 @@ def main():
     gen_init("ppodefault_a4", lambda e: PPODefault(e, "cpu"), (4, 84, 84), 4, 1, 255.0)
     # config 2 at the real network dims, rollout-structured (the bench's update chain)
     gen_update_config2()
+    # config 3's NatureCNN at a real minibatch size (2048), rollout-structured pixel stacks
+    gen_update_config3()
     print("fixtures written to", OUT)
 
 

@@ -1,0 +1,224 @@
+"""BASELINE config 3's network (NatureCNN on 84x84x4 Breakout stacks, architectures/ppo.py:15-57)
+at a real minibatch size, through PPOTrainer's own pixel update.
+
+tests/golden/update_config3.npz (gen_golden.gen_update_config3) is the reference's GAE block
+(ppo_atari_oc.py:533-547) and two minibatch updates of 2048 through its update block (:566-610)
+on PPODefault over a rollout-structured 16 x 256 batch of synthetic Breakout frame stacks (the
+frame-stack rule with resets), with a float64 twin of the update at the f32 reference's
+parameters. The trainer runs exactly the bench's config-3 path: u8 -> f32 NHWC gather with
+NormalizeImg folded in, channels_last convolutions on MIOpen (Find-selected solutions, the bench's
+flags) with HIP bias/ReLU and ReLU-backward/bias-grad passes, the 3136 -> 512 Linear on the
+activation's NHWC memory order, HIP loss, clip + Adam; once eagerly and once as the captured
+hipGraph the bench replays.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+LR = 2.5e-4
+
+
+def config3_weights(agent, seed):
+    """gen_golden.config3_weights (numpy PCG64, fan_in = in x kh x kw), pinned by checksums."""
+    rng = np.random.default_rng(seed)
+    sd = {}
+    for k, v in agent.state_dict().items():
+        if k.endswith("weight"):
+            gain = 0.01 if k.startswith("actor") else 1.0 if k.startswith("critic") else 2 ** 0.5
+            w = rng.standard_normal(tuple(v.shape)) * (gain / np.sqrt(np.prod(v.shape[1:])))
+        else:
+            w = rng.standard_normal(tuple(v.shape)) * 0.05
+        sd[k] = torch.from_numpy(w.astype(np.float32))
+    return sd
+
+
+def stacks(frames, dones, W=4):
+    """The rollout's frame stacks from the distinct frames (gen_golden's rule): obs[t] slot w =
+    env n's frame of step t - (W-1) + w, clipped to its latest reset (timeline row s + W - 1)."""
+    T1, N = dones.shape
+    obs = np.zeros((T1, N, W, 84, 84), np.uint8)
+    last = np.full(N, -10 ** 9)
+    for t in range(T1):
+        last = np.where(dones[t] != 0, t, last)
+        for w in range(W):
+            src = np.maximum(t - (W - 1) + w, last)
+            obs[t, :, w] = frames[src + W - 1, np.arange(N)]
+    return obs
+
+
+@pytest.fixture(scope="module")
+def fixture():
+    from conftest import golden
+
+    z = golden("update_config3.npz")
+    z["obs"] = stacks(z["frames"], z["dones"])
+    assert int(z["obs"].astype(np.int64).sum()) == int(z["obs_sum"])
+    return z
+
+
+def config3_trainer(dev, z):
+    from oc_cleanrl_amd.args import Args, finalize
+    from oc_cleanrl_amd.trainer import PPOTrainer
+
+    T, N = z["dones"].shape[0] - 1, z["dones"].shape[1]
+    args = finalize(Args(env_id="ALE/Breakout-v5", obs_mode="dqn", architecture="PPO",
+                         num_envs=N, num_steps=T, num_minibatches=2, update_epochs=1,
+                         save_model=False, torch_deterministic=False, conv_benchmark=True), 1)
+    tr = PPOTrainer(args, dev)
+    assert tr.channels_last and tr.prescale and tr.M == int(z["M"])
+    sd0 = config3_weights(tr.agent, int(z["seed"]))
+    for k, v in sd0.items():
+        s = z[f"sum0::{k}"]
+        assert float(v.double().sum()) == pytest.approx(s[0], rel=1e-12, abs=1e-9), k
+    with torch.no_grad():
+        for k, p in tr.agent.state_dict().items():
+            p.copy_(sd0[k])
+    D = lambda k: torch.from_numpy(z[k]).to(dev)  # noqa: E731
+    tr.obs.copy_(D("obs"))
+    tr.dones.copy_(D("dones"))
+    tr.actions.copy_(D("actions").view(T, N))
+    tr.logprobs.copy_(D("logprobs").view(T, N))
+    tr.values[:T].copy_(D("values").view(T, N))
+    tr.values[T].copy_(D("next_value"))
+    tr.rewards.copy_(D("rewards").view(T, N))
+    tr.load_permutation(z["perm"])
+    return tr
+
+
+def _grad_errors(z, j, params):
+    """Pre-clip gradient error per tensor vs the f64 twin, relative to its largest element:
+    (ours, the f32 reference's own)."""
+    out = {}
+    for k, p in params.items():
+        g = p.grad.detach().double().cpu().reshape(-1)
+        if f"pick::{k}" in z:
+            g = g[torch.from_numpy(z[f"pick::{k}"])]
+        g64 = torch.from_numpy(z[f"grad64pre{j}::{k}"]).reshape(-1)
+        g32 = torch.from_numpy(z[f"gradpre{j}::{k}"]).double().reshape(-1)
+        mx = float(z[f"gnorm64pre{j}::{k}"][1])
+        out[k] = (float((g - g64).abs().max()) / mx, float((g32 - g64).abs().max()) / mx)
+    return out
+
+
+def _params_vs(tr, z, i):
+    """Worst |param - reference after update i| over every tensor (large ones at the fixture's
+    4096 sample points), and the fraction of elements off by more than 2e-7."""
+    worst, frac = 0.0, 0.0
+    for k, v in tr.agent.state_dict().items():
+        got = v.detach().cpu().contiguous().view(-1)
+        if f"pick::{k}" in z:
+            got = got[torch.from_numpy(z[f"pick::{k}"])]
+        err = (got - torch.from_numpy(z[f"sd{i}::{k}"]).reshape(-1)).abs()
+        worst = max(worst, float(err.max()))
+        frac = max(frac, float((err > 2e-7).float().mean()))
+    return worst, frac
+
+
+def test_config3_gae_matches_reference(dev, fixture):
+    z = fixture
+    from oc_cleanrl_amd import ops
+
+    tr = config3_trainer(dev, z)
+
+    T = tr.T
+    ops.gae(tr.rewards, tr.values[:T], tr.dones[:T], tr.values[T], tr.dones[T], 0.99, 0.95,
+            tr.advantages, tr.returns)
+    torch.cuda.synchronize()
+    assert np.array_equal(tr.advantages.cpu().numpy().reshape(-1), z["advantages"])
+    assert np.array_equal(tr.returns.cpu().numpy().reshape(-1), z["returns"])
+
+
+def test_config3_update_matches_reference_eager_and_captured(dev, fixture):
+    """Two minibatch updates of 2048: eager with per-minibatch checks against the f64 twin and the
+    f32 reference, then the same two updates replayed as the captured hipGraph from the same
+    start (parameters, Adam state) -- within MIOpen's run-to-run reordering of the eager run
+    (its Find-selected convolution kernels need not be bitwise repeatable)."""
+    z = fixture
+    tr = config3_trainer(dev, z)
+    tr.advantages.view(-1).copy_(torch.from_numpy(z["advantages"]).to(dev))
+    tr.returns.view(-1).copy_(torch.from_numpy(z["returns"]).to(dev))
+    tr._prepare_minibatches()
+    opt = tr.optimizer
+    state0 = [t.clone() for t in (opt.params, opt.exp_avg, opt.exp_avg_sq, opt.scalars)]
+    params = dict(tr.agent.named_parameters())
+    for j in range(2):
+        tr._forward_backward(j)
+        gn = float(torch.linalg.vector_norm(tr.grad_buf.double()))
+        gn64 = float(z[f"grad_norm64_{j}"])
+        e = _grad_errors(z, j, params)
+        print(f"minibatch {j}: grad norm {gn:.8g}, f64 {gn64:.8g}, f32 ref {z['grad_norms'][j]:.8g};"
+              " pre-clip error vs f64 per tensor (ours / reference f32): "
+              + ", ".join(f"{k} {a:.2g}/{b:.2g}" for k, (a, b) in e.items()))
+        # end-to-end, ReLU decisions included: the f32 reference's own worst is 4e-4 here
+        assert abs(gn - gn64) <= 1e-4 * gn64, (j, gn, gn64)
+        assert max(a for a, _ in e.values()) <= 2e-3, e
+        tr._opt_step()
+        torch.cuda.synchronize()
+        np.testing.assert_allclose(tr.stats[j].cpu().numpy(), z["stats"][j], rtol=1e-4,
+                                   atol=1e-6, err_msg=f"stats mb {j}")
+        worst, frac = _params_vs(tr, z, j + 1)
+        print(f"minibatch {j}: worst |param - ref| = {worst:.3g} ({worst / LR:.3g} lr), "
+              f"fraction > 2e-7: {frac:.3g}")
+        assert worst <= 0.01 * LR and frac < 0.01, (j, worst, frac)
+    eager = [p.detach().clone() for p in tr.params]
+    # the captured update (as the bench replays it) from the same start
+    for t, s in zip((opt.params, opt.exp_avg, opt.exp_avg_sq, opt.scalars), state0):
+        t.copy_(s)
+    g = torch.cuda.CUDAGraph()
+    torch.cuda.synchronize()
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        tr._update_epoch(0)
+    for t, s in zip((opt.params, opt.exp_avg, opt.exp_avg_sq, opt.scalars), state0):
+        t.copy_(s)
+    g.replay()
+    torch.cuda.synchronize()
+    worst, frac = _params_vs(tr, z, 2)
+    diff = max(float((p - q).abs().max()) for p, q in zip(tr.params, eager))
+    print(f"captured: worst |param - ref| = {worst:.3g} ({worst / LR:.3g} lr); max |captured - "
+          f"eager| = {diff:.3g} ({diff / LR:.3g} lr)")
+    assert worst <= 0.01 * LR and frac < 0.01
+    assert diff <= 0.002 * LR
+
+
+def test_config3_full_size_captured_update_matches_eager(dev):
+    """At config 3's own size (256 envs x 128 steps, minibatches of 8192, the bench's flags): one
+    rollout, then the update epoch eagerly and as the captured hipGraph from the same start. The
+    convolutions are MIOpen's Find-selected solutions (torch_deterministic=False, as the bench
+    line states): the two runs are compared to a tolerance, and whether they are bitwise equal is
+    printed."""
+    from oc_cleanrl_amd.args import Args, finalize
+    from oc_cleanrl_amd.trainer import PPOTrainer
+
+    args = finalize(Args(env_id="ALE/Breakout-v5", obs_mode="dqn", architecture="PPO",
+                         num_envs=256, num_steps=128, update_epochs=1, save_model=False,
+                         torch_deterministic=False, conv_benchmark=True, cuda_graphs=False), 1)
+    tr = PPOTrainer(args, dev)
+    assert tr.M == 8192
+    tr._rollout()
+    tr._prepare_minibatches()
+    opt = tr.optimizer
+    keep = (opt.params, opt.exp_avg, opt.exp_avg_sq, opt.scalars)
+    state0 = [t.clone() for t in keep]
+    tr._update_epoch(0)  # eager (MIOpen's Find runs here)
+    for t, s in zip(keep, state0):
+        t.copy_(s)
+    tr._update_epoch(0)  # eager again, searched: the reference run
+    torch.cuda.synchronize()
+    eager = opt.params.clone()
+    for t, s in zip(keep, state0):
+        t.copy_(s)
+    g = torch.cuda.CUDAGraph()
+    torch.cuda.synchronize()
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        tr._update_epoch(0)
+    for t, s in zip(keep, state0):
+        t.copy_(s)
+    g.replay()
+    torch.cuda.synchronize()
+    diff = float((opt.params - eager).abs().max())
+    step = float((eager - state0[0]).abs().max())
+    print(f"config 3 full size: captured vs eager max |diff| {diff:.3g} (bitwise: "
+          f"{bool(torch.equal(opt.params, eager))}); largest parameter step {step:.3g}")
+    assert step > 0 and diff <= 0.01 * LR
