@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define OCPPO_ABI_VERSION 18
+#define OCPPO_ABI_VERSION 19
 
 /* status codes */
 #define OCPPO_OK 0
@@ -320,6 +320,10 @@ OCPPO_API int ocppo_bias_act_nchw(ocppo_stream_t stream, const float* y, const f
  * M) when mbig is -1; mbig >= 0 imposes the split (a multiple of 128, (mbig / 128)(N / 128) a
  * multiple of 8; experiments and tests); mbig must be -1 for every other tile. M, N multiples of
  * 64 x 128, and dbp rows / mbits words counted as for 64 x 128 (a 128-row tile's dbp partial sits in the first of its two rows, the second is written as zeros).
+ * Pre-split B (b_planes != NULL; b is then ignored and may be NULL): the three bf16 pieces of
+ * B(n, k) at b_planes[p * bp_stride + n * bp_ld + k] (p = 0, 1, 2; ocppo_split_planes wrote them
+ * from the f32 B, so the result is bitwise that of the f32 B): staged by copy, no split in the
+ * K loop. Needs sak == 1, bp_ld % 8 == 0, 16-B aligned planes, tile 24..27 or 56.
  * Deterministic (fixed MFMA order, no atomics).
  * ------------------------------------------------------------------------------------------- */
 OCPPO_API int ocppo_gemm_x6(ocppo_stream_t stream, const float* a, int64_t sam, int64_t sak,
@@ -327,7 +331,20 @@ OCPPO_API int ocppo_gemm_x6(ocppo_stream_t stream, const float* a, int64_t sam, 
                             int64_t M, int64_t N, int64_t K, int64_t splits, int64_t split_c,
                             const float* bias, int relu, const float* mask, int64_t ldm,
                             float* dbp, uint64_t* mbits_out, const uint64_t* mbits_in,
-                            int tile, int mbig);
+                            int tile, int mbig, const void* b_planes, int64_t bp_ld,
+                            int64_t bp_stride);
+
+/* ---------------------------------------------------------------------------------------------
+ * The exact three-piece bf16 split ocppo_gemm_x6 forms in its K loop, done once per matrix: the
+ * update's Linear weights (architectures/ppo.py:60-84) as the B operand of the forward (W [N, K],
+ * trans 0) and of dX (W^T, trans 1), after every optimizer step (ppo_atari_oc.py:606) instead of
+ * once per row tile and K step. Job i: src[i] f32 [rows, cols] (row stride ld) -> dst[i] three
+ * dense bf16 planes [R', C'] (R' x C' = rows x cols, or cols x rows transposed), plane stride
+ * R' C' elements; C' % 8 == 0, dst 16-B aligned; 1 <= n <= 8 jobs, one launch.
+ * ------------------------------------------------------------------------------------------- */
+OCPPO_API int ocppo_split_planes(ocppo_stream_t stream, int n, const float* const* src,
+                                 const int64_t* ld, const int64_t* rows, const int64_t* cols,
+                                 const int* trans, void* const* dst);
 
 /* ---------------------------------------------------------------------------------------------
  * Split-K combine of a weight gradient — replaces ATen's `sum(0)` after the batched (split-K)

@@ -15,6 +15,8 @@ actions are bit-identical to the reference's under the same seed.
 """
 from __future__ import annotations
 
+import threading
+
 import numpy as np
 import torch
 import torch.nn as nn
@@ -95,6 +97,31 @@ def set_update_gemm(module: nn.Module, x6: bool) -> None:
             m.weight._ocppo_x6 = bool(x6)
 
 
+# Pre-split weights (ops.WeightPlanes): the forward's and dX's B operand read as three bf16 planes
+# split once per minibatch instead of in every row tile's K loop (bitwise the same products).
+# Only inside a weight_planes() scope, opened by the owner that refreshed the planes after the
+# last optimizer step (the trainer, per minibatch): outside it a weight's planes may be stale.
+_PLANES = threading.local()
+
+
+class weight_planes:
+    """Scope in which _LinearAct reads its weight's pre-split planes (w._ocppo_planes)."""
+
+    def __enter__(self):
+        _PLANES.live = getattr(_PLANES, "live", 0) + 1
+        return self
+
+    def __exit__(self, *exc):
+        _PLANES.live -= 1
+
+
+def _planes(w, kind: str):
+    if not getattr(_PLANES, "live", 0):
+        return None
+    d = getattr(w, "_ocppo_planes", None)
+    return None if d is None else d.get(kind)
+
+
 def _x6(M: int, N: int, K: int, on: bool = True) -> bool:
     """Forward / dX product [M, N] = [M, K] x [K, N] on gemm_x6."""
     return on and M * N >= X6_MIN_TILES * 16384 and K >= 64
@@ -167,11 +194,11 @@ def _weight_grad(g, x, out=None, db=None, x6: bool = True):
 HIP_SMALL_DX = True
 
 
-def _dx(g, w, x6: bool = True):
+def _dx(g, w, x6: bool = True, planes=None):
     M, N = g.shape
     K = w.shape[1]
     if _x6(M, K, N, x6) and ops.dx_x6_ok(g, w):
-        return ops.dx_x6(g, w)
+        return ops.dx_x6(g, w, planes=planes)
     if (HIP_SMALL_DX and g.is_cuda and M <= 256 and K <= 256 and N >= 256 and N % 16 == 0 and
             g.dtype == torch.float32 and g.is_contiguous()):
         return ops.linear_act(g, w.t().contiguous())
@@ -230,6 +257,7 @@ class _LinearAct(torch.autograd.Function):
         # order, so the weight's columns are permuted to match instead (linear_act_nhwc)
         wm = _cols_to_nhwc(w, chw) if chw is not None else w
         x6 = ctx.x6 = x6_route(w)
+        pf, ctx.pdx = (_planes(w, "fwd"), _planes(w, "dx")) if chw is None else (None, None)
         # below = the box of the Linear+ReLU that produced x: its ReLU backward and bias-gradient
         # partials ride in this layer's dX GEMM (ops.dx_x6_relu, mask = x)
         ctx.below = None
@@ -240,9 +268,9 @@ class _LinearAct(torch.autograd.Function):
         if _x6(x.shape[0], wm.shape[0], x.shape[1], x6) and ops.linear_x6_ok(x, wm):
             if relu and box is not None:
                 # the ReLU bitmask for the next layer's fused dX epilogue (box consumer)
-                out, box["mbits"] = ops.linear_x6(x, wm, b, relu, mbits=True)
+                out, box["mbits"] = ops.linear_x6(x, wm, b, relu, mbits=True, planes=pf)
             else:
-                out = ops.linear_x6(x, wm, b, relu)
+                out = ops.linear_x6(x, wm, b, relu, planes=pf)
         else:
             out = torch._addmm_activation(b, x, wm.t(), use_gelu=False) if relu else \
                 torch.addmm(b, x, wm.t())
@@ -276,13 +304,13 @@ class _LinearAct(torch.autograd.Function):
         entry refuses (layout, alignment) take the plain dX plus the same two results, so the
         claim always holds."""
         if ctx.below is None:
-            return _dx(g, w, ctx.x6)
+            return _dx(g, w, ctx.x6, ctx.pdx)
         x = ctx.saved_tensors[0]
         if ops.dx_x6_ok(g, w):
-            gp, dbp = ops.dx_x6_relu(g, w, x, mbits=ctx.below.get("mbits"))
+            gp, dbp = ops.dx_x6_relu(g, w, x, mbits=ctx.below.get("mbits"), planes=ctx.pdx)
             ctx.below["dbp"] = (dbp, dbp.shape[0])  # relu_bias_grad_partial's (partials, chunks)
             return gp
-        dx = _dx(g, w, ctx.x6).contiguous()
+        dx = _dx(g, w, ctx.x6, ctx.pdx).contiguous()
         if ops.relu_bias_grad_ok(dx):
             gp, ctx.below["dbp"] = ops.relu_bias_grad_partial(dx, x.contiguous())
         else:

@@ -134,6 +134,8 @@ class Args:
     gemm_table: bool = True  # the shipped hipBLASLt solution table for the update GEMMs
     x6_gemm: bool = True  # update Linear GEMMs on the bf16 matrix cores as exact-split f32
                           # (ops.gemm_x6, f32 accuracy), ReLU backward fused into the next dX
+    x6_weight_planes: bool = True  # ... with the weights split into bf16 planes once per
+                                   # minibatch (ops.WeightPlanes; bitwise the same results)
 
 
 def _flag_names(name: str) -> list[str]:

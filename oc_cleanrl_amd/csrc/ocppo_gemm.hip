@@ -55,6 +55,7 @@ namespace ocppo {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kX6BK = 32;       // K step = one MFMA depth
 
@@ -84,6 +85,9 @@ struct X6Args {
   // mixed tiles (variant bit 5): rows [0, mbig) in 128 x 128 tiles, dispatched first, the rest
   // in 64 x 128 tiles; dbp rows and mask words are then counted in 64-row tiles
   int mbig;
+  // B pre-split (ocppo_split_planes): piece p of B(n, k) at bpl[p * bpl_ps + n * bpl_ld + k]
+  const uint16_t* bpl;
+  int64_t bpl_ld, bpl_ps;
 };
 
 // Where one tile's outputs go: its row tiles start at row0_base, its dbp partial row is
@@ -105,7 +109,18 @@ __device__ __forceinline__ uint32_t x6_pk(x6f2 v) {
 __device__ __forceinline__ x6f2 x6_unpk(uint32_t p) {
   return x6f2{__uint_as_float(p << 16), __uint_as_float(p & 0xffff0000u)};
 }
+// PROBE (probe builds only, tools/build_variant.py -DOCPPO_X6_PROBE_NOSPLIT[_B]): the same LDS
+// traffic with 2 VALU per pair instead of 9 -- wrong products, the main loop's cost without the
+// split (of both operands, or of B only)
+template <bool PROBE = false>
 __device__ __forceinline__ void x6_split2(x6f2 v, uint32_t& p0, uint32_t& p1, uint32_t& p2) {
+  if constexpr (PROBE) {
+    const uint32_t ua = __float_as_uint(v.x), ub = __float_as_uint(v.y);
+    p0 = __builtin_amdgcn_perm(ub, ua, 0x07060302u);
+    p1 = __builtin_amdgcn_perm(ub, ua, 0x05040100u);
+    p2 = p1;
+    return;
+  }
   p0 = x6_pk(v);
   const x6f2 r1 = v - x6_unpk(p0);
   p1 = x6_pk(r1);
@@ -176,6 +191,7 @@ struct X6Stage {
   }
 
   // split the staged pieces and write the three planes (plane p at lds + p * kPlane)
+  template <bool PROBE = false>
   __device__ static void stash(unsigned char* lds, int t, const floatx4 (&r)[kPer][4]) {
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
@@ -188,13 +204,53 @@ struct X6Stage {
         const x6f2 v01 = KC ? x6f2{r[i][j][0], r[i][j][1]} : x6f2{r[i][0][j], r[i][1][j]};
         const x6f2 v23 = KC ? x6f2{r[i][j][2], r[i][j][3]} : x6f2{r[i][2][j], r[i][3][j]};
         uint32_t a0, a1, a2, b0, b1, b2;
-        x6_split2(v01, a0, a1, a2);
-        x6_split2(v23, b0, b1, b2);
+        x6_split2<PROBE>(v01, a0, a1, a2);
+        x6_split2<PROBE>(v23, b0, b1, b2);
         const int off = x6_off(4 * rq + j, 4 * kq);
         *reinterpret_cast<uint2*>(lds + off) = uint2{a0, b0};
         *reinterpret_cast<uint2*>(lds + kPlane + off) = uint2{a1, b1};
         *reinterpret_cast<uint2*>(lds + 2 * kPlane + off) = uint2{a2, b2};
       }
+    }
+  }
+};
+
+// The B operand as three bf16 planes already split (k-contiguous, ocppo_split_planes: the layer's
+// weight, split once per minibatch instead of once per row tile and K step): staging is a copy of
+// 16-B chunks (8 k of one row and plane) into the swizzled plane rows -- no split VALU, and one
+// ds_write_b128 per chunk (8 lanes = one 128-B row pair: conflict-free).
+template <int ROWS, int NT>
+struct X6StagePl {
+  static constexpr int kChunks = ROWS * 4 * 3;
+  static constexpr int kPer = (kChunks + NT - 1) / NT;
+  static constexpr int kPlane = ROWS * 64;
+
+  __device__ static void at(int c, int& plane, int& row, int& ch) {
+    plane = c / (ROWS * 4);
+    const int rc = c - plane * (ROWS * 4);
+    row = rc >> 2;
+    ch = rc & 3;
+  }
+  __device__ static void load(const uint16_t* __restrict__ pl, int64_t ld, int64_t ps, int row0,
+                              int k0, int t, u32x4 (&r)[kPer]) {
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int c = t + NT * i;
+      if (kChunks % NT != 0 && c >= kChunks) continue;
+      int plane, row, ch;
+      at(c, plane, row, ch);
+      r[i] = *reinterpret_cast<const u32x4*>(pl + plane * ps + static_cast<int64_t>(row0 + row) * ld +
+                                             k0 + 8 * ch);
+    }
+  }
+  __device__ static void stash(unsigned char* lds, int t, const u32x4 (&r)[kPer]) {
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int c = t + NT * i;
+      if (kChunks % NT != 0 && c >= kChunks) continue;
+      int plane, row, ch;
+      at(c, plane, row, ch);
+      *reinterpret_cast<u32x4*>(lds + plane * kPlane + x6_chunk_off(row, ch)) = r[i];
     }
   }
 };
@@ -213,6 +269,14 @@ __device__ __forceinline__ void x6_vmwait(floatx4 (&r)[P][4]) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(r[i][j]));
 }
+
+#if defined(OCPPO_X6_PROBE_NOSPLIT)
+constexpr bool kProbeA = true, kProbeB = true;
+#elif defined(OCPPO_X6_PROBE_NOSPLIT_B)
+constexpr bool kProbeA = false, kProbeB = true;
+#else
+constexpr bool kProbeA = false, kProbeB = false;
+#endif
 
 __device__ __forceinline__ bf16x8 x6_frag(const unsigned char* plane, int row, int chunk) {
   return *reinterpret_cast<const bf16x8*>(plane + x6_chunk_off(row, chunk));
@@ -251,7 +315,7 @@ __device__ __forceinline__ int x6_remap(int b, int nb) {
 }
 
 // One output tile (unit u: split u / (tiles_m tiles_n), then row-major tiles) of the product
-template <int FM, int FN, int WGM, int WGN, bool AKC, bool BKC, bool LO, bool PF2>
+template <int FM, int FN, int WGM, int WGN, bool AKC, bool BKC, bool LO, bool PF2, bool BPL = false>
 __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int u, X6Place pl_) {
   constexpr int NT = 64 * WGM * WGN;
   constexpr int BM = 16 * FM * WGM, BN = 16 * FN * WGN;
@@ -308,12 +372,46 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
         x6_mfma6<LO>(af[i], bf, hi[i][j], lo[LO ? i : 0][LO ? j : 0]);
     }
   };
-  floatx4 ra[SA::kPer][4], rb[SB::kPer][4];
-  if constexpr (!PF2) {
+  floatx4 ra[SA::kPer][4];
+  if constexpr (BPL) {
+    // A two K steps ahead (register sets ra / qa, as below), the pre-split B one step ahead:
+    // its loads of step kt + 1 are issued before A's of step kt + 2, so the stash of step
+    // kt + 1 waits for them without draining A's
+    static_assert(PF2 && !LO, "the pre-split B path is built for the shipped family");
+    using PB = X6StagePl<BN, NT>;
+    const uint16_t* __restrict__ Bp = g.bpl;
+    u32x4 pb[PB::kPer];
+    floatx4 qa[SA::kPer][4];
+    SA::load(A, g.sam, g.sak, m0, kb * kX6BK, t, ra);
+    PB::load(Bp, g.bpl_ld, g.bpl_ps, n0, kb * kX6BK, t, pb);
+    if (nk > 1) SA::load(A, g.sam, g.sak, m0, (kb + 1) * kX6BK, t, qa);
+    SA::template stash<kProbeA>(la, t, ra);
+    PB::stash(lb, t, pb);
+    __syncthreads();
+    auto step = [&](int kt, floatx4 (&ldA)[SA::kPer][4], floatx4 (&stA)[SA::kPer][4],
+                    u32x4 (&pbr)[PB::kPer]) {
+      if (kt + 1 < nk) PB::load(Bp, g.bpl_ld, g.bpl_ps, n0, (kb + kt + 1) * kX6BK, t, pbr);
+      if (kt + 2 < nk) SA::load(A, g.sam, g.sak, m0, (kb + kt + 2) * kX6BK, t, ldA);
+      compute();
+      __syncthreads();
+      if (kt + 1 < nk) {
+        SA::template stash<kProbeA>(la, t, stA);
+        PB::stash(lb, t, pbr);
+      }
+      __syncthreads();
+    };
+    int kt = 0;
+    for (; kt + 1 < nk; kt += 2) {
+      step(kt, ra, qa, pb);
+      step(kt + 1, qa, ra, pb);
+    }
+    if (kt < nk) step(kt, ra, qa, pb);
+  } else if constexpr (!PF2) {
+    floatx4 rb[SB::kPer][4];
     SA::load(A, g.sam, g.sak, m0, kb * kX6BK, t, ra);
     SB::load(B, g.sbn, g.sbk, n0, kb * kX6BK, t, rb);
-    SA::stash(la, t, ra);
-    SB::stash(lb, t, rb);
+    SA::template stash<kProbeA>(la, t, ra);
+    SB::template stash<kProbeB>(lb, t, rb);
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
       const bool more = kt + 1 < nk;
@@ -324,8 +422,8 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
       compute();
       __syncthreads();
       if (more) {
-        SA::stash(la, t, ra);
-        SB::stash(lb, t, rb);
+        SA::template stash<kProbeA>(la, t, ra);
+        SB::template stash<kProbeB>(lb, t, rb);
       }
       __syncthreads();
     }
@@ -342,7 +440,7 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
 #endif
     constexpr int kLoads = 4 * (SA::kPer + SB::kPer);  // loads per step per thread
     static_assert(!ASM || kLoads == 8, "x6_vmwait counts assume 8 loads per step");
-    floatx4 qa[SA::kPer][4], qb[SB::kPer][4];
+    floatx4 rb[SB::kPer][4], qa[SA::kPer][4], qb[SB::kPer][4];
     SA::template load<ASM>(A, g.sam, g.sak, m0, kb * kX6BK, t, ra);
     SB::template load<ASM>(B, g.sbn, g.sbk, n0, kb * kX6BK, t, rb);
     if (nk > 1) {
@@ -358,8 +456,8 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
         x6_vmwait<0>(rb);
       }
     }
-    SA::stash(la, t, ra);
-    SB::stash(lb, t, rb);
+    SA::template stash<kProbeA>(la, t, ra);
+    SB::template stash<kProbeB>(lb, t, rb);
     __syncthreads();
     auto step = [&](int kt, floatx4 (&ldA)[SA::kPer][4], floatx4 (&ldB)[SB::kPer][4],
                     floatx4 (&stA)[SA::kPer][4], floatx4 (&stB)[SB::kPer][4]) {
@@ -380,8 +478,8 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
             x6_vmwait<0>(stB);
           }
         }
-        SA::stash(la, t, stA);
-        SB::stash(lb, t, stB);
+        SA::template stash<kProbeA>(la, t, stA);
+        SB::template stash<kProbeB>(lb, t, stB);
       }
       __syncthreads();
     };
@@ -470,38 +568,41 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
   if (g.mbits_out) g.mbits_out[tile_id * NT + t] = bits;
 }
 
-template <int FM, int FN, int WGM, int WGN, bool AKC, bool BKC, bool LO, bool PF2>
+template <int FM, int FN, int WGM, int WGN, bool AKC, bool BKC, bool LO, bool PF2, bool BPL = false>
 __global__ __launch_bounds__(64 * WGM * WGN, OCPPO_X6_OCC) void gemm_x6_kernel(X6Args g) {
   __shared__ __attribute__((aligned(16)))
   unsigned char lds[x6_lds_bytes<FM, FN, WGM, WGN, AKC, BKC>()];
   const int u = x6_remap(blockIdx.x, gridDim.x);
   if (u >= g.units) return;
-  x6_unit<FM, FN, WGM, WGN, AKC, BKC, LO, PF2>(g, lds, u, X6Place{g.tiles_m, 0, 0, 1, 0});
+  x6_unit<FM, FN, WGM, WGN, AKC, BKC, LO, PF2, BPL>(g, lds, u, X6Place{g.tiles_m, 0, 0, 1, 0});
 }
 
 // Mixed tiles: workgroups [0, nbig) take the 128 x 128 tiles of rows [0, mbig) (dispatched
 // first, the longest units), the rest the 64 x 128 tiles of rows [mbig, M) as slots free up;
 // each range keeps its own XCD remap (nbig is a multiple of 8, so XCD b & 7 is the same in both)
-template <bool AKC, bool BKC>
+template <bool AKC, bool BKC, bool BPL = false>
 __global__ __launch_bounds__(256, OCPPO_X6_OCC) void gemm_x6_mixed_kernel(X6Args g) {
   __shared__ __attribute__((aligned(16))) unsigned char lds[x6_lds_bytes<4, 4, 2, 2, AKC, BKC>()];
   const int nbig = (g.mbig / 128) * g.tiles_n;
   const int b = blockIdx.x;
   if (b < nbig) {
-    x6_unit<4, 4, 2, 2, AKC, BKC, false, true>(g, lds, x6_remap(b, nbig),
-                                               X6Place{g.mbig / 128, 0, 0, 2, 0});
+    x6_unit<4, 4, 2, 2, AKC, BKC, false, true, BPL>(g, lds, x6_remap(b, nbig),
+                                                    X6Place{g.mbig / 128, 0, 0, 2, 0});
   } else {
     const int small = (g.M - g.mbig) / 64;
     const int u = x6_remap(b - nbig, gridDim.x - nbig);
     if (u >= small * g.tiles_n) return;
-    x6_unit<2, 4, 2, 2, AKC, BKC, false, true>(
+    x6_unit<2, 4, 2, 2, AKC, BKC, false, true, BPL>(
         g, lds, u, X6Place{small, g.mbig, g.mbig / 64, 1, static_cast<int64_t>(nbig)});
   }
 }
 
 template <bool AKC, bool BKC>
 static void launch_x6_mixed1(hipStream_t s, X6Args& g) {
-  hipLaunchKernelGGL((gemm_x6_mixed_kernel<AKC, BKC>), dim3(g.units), dim3(256), 0, s, g);
+  if (g.bpl)
+    hipLaunchKernelGGL((gemm_x6_mixed_kernel<true, true, true>), dim3(g.units), dim3(256), 0, s, g);
+  else
+    hipLaunchKernelGGL((gemm_x6_mixed_kernel<AKC, BKC>), dim3(g.units), dim3(256), 0, s, g);
 }
 
 // Rows in 128-row tiles for an [M x N] mixed product. With 256 < T <= 384 tiles of 128 x 128
@@ -521,6 +622,13 @@ static void launch_x6_t(hipStream_t s, bool akc, bool bkc, X6Args& g) {
   g.tiles_m = g.M / (16 * FM * WGM);
   g.tiles_n = g.N / (16 * FN * WGN);
   const dim3 grid(g.units), block(64 * WGM * WGN);
+  if constexpr (PF2 && !LO && WGM * WGN == 4) {
+    if (g.bpl) {  // pre-split B (the caller checked akc)
+      hipLaunchKernelGGL((gemm_x6_kernel<FM, FN, WGM, WGN, true, true, false, true, true>), grid,
+                         block, 0, s, g);
+      return;
+    }
+  }
   if (akc && bkc)
     hipLaunchKernelGGL((gemm_x6_kernel<FM, FN, WGM, WGN, true, true, LO, PF2>), grid, block, 0, s, g);
   else if (akc)
@@ -580,30 +688,114 @@ static bool launch_x6(hipStream_t s, int tile, bool akc, bool bkc, X6Args& g) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// ocppo_split_planes: an f32 matrix (or its transpose) as the three bf16 planes gemm_x6 stages
+// as its B operand (x6_split2: bitwise the pieces the kernel would form itself). Up to
+// kSplitJobs matrices per launch, each cut into 64 x 64 tiles read as rows of 256 B and written
+// (transposed through LDS when asked) as bf16 pairs.
+constexpr int kSplitJobs = 8;
+struct SplitJob {
+  const float* src;
+  int64_t ld;
+  int R, C, trans, tiles_c, tile0;
+  uint16_t* dst;
+};
+struct SplitJobs {
+  SplitJob j[kSplitJobs];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void split_planes_kernel(SplitJobs J) {
+  const int b = blockIdx.x;
+  int ji = 0;
+  while (ji + 1 < J.n && b >= J.j[ji + 1].tile0) ++ji;
+  const SplitJob jb = J.j[ji];
+  const int tl = b - jb.tile0, tr = tl / jb.tiles_c, tc = tl - tr * jb.tiles_c;
+  const int r0 = 64 * tr, c0 = 64 * tc;
+  __shared__ float tile[64][65];
+  for (int e = threadIdx.x; e < 64 * 64; e += 256) {
+    const int r = e >> 6, c = e & 63;
+    tile[r][c] = r0 + r < jb.R && c0 + c < jb.C ? jb.src[static_cast<int64_t>(r0 + r) * jb.ld + c0 + c]
+                                                  : 0.f;
+  }
+  __syncthreads();
+  const int oR = jb.trans ? jb.C : jb.R, oC = jb.trans ? jb.R : jb.C;
+  const int64_t ps = static_cast<int64_t>(oR) * oC;
+  for (int e = threadIdx.x; e < 64 * 32; e += 256) {
+    const int orow = e >> 5, op = e & 31;
+    const x6f2 v = jb.trans ? x6f2{tile[2 * op][orow], tile[2 * op + 1][orow]}
+                            : x6f2{tile[orow][2 * op], tile[orow][2 * op + 1]};
+    const int gr = (jb.trans ? c0 : r0) + orow, gc = (jb.trans ? r0 : c0) + 2 * op;
+    if (gr >= oR || gc >= oC) continue;
+    uint32_t p0, p1, p2;
+    x6_split2(v, p0, p1, p2);
+    uint32_t* d = reinterpret_cast<uint32_t*>(jb.dst + static_cast<int64_t>(gr) * oC + gc);
+    d[0] = p0;
+    d[ps / 2] = p1;
+    d[ps] = p2;
+  }
+}
+
 }  // namespace ocppo
 
 using namespace ocppo;
+
+extern "C" int ocppo_split_planes(ocppo_stream_t stream, int n, const float* const* src,
+                                  const int64_t* ld, const int64_t* rows, const int64_t* cols,
+                                  const int* trans, void* const* dst) {
+  OCPPO_REQUIRE(n >= 1 && n <= kSplitJobs && src && ld && rows && cols && trans && dst,
+                "ocppo_split_planes: n=%d jobs (1..%d) and every array", n, kSplitJobs);
+  SplitJobs J{};
+  J.n = n;
+  int tiles = 0;
+  for (int i = 0; i < n; ++i) {
+    OCPPO_REQUIRE(src[i] && dst[i] && rows[i] >= 1 && cols[i] >= 1 && ld[i] >= cols[i] &&
+                      rows[i] <= 65536 && cols[i] <= 65536 &&
+                      (trans[i] ? rows[i] : cols[i]) % 8 == 0 &&
+                      reinterpret_cast<uintptr_t>(dst[i]) % 16 == 0,
+                  "ocppo_split_planes: job %d (%lld x %lld, ld %lld, trans %d): the planes' rows "
+                  "must be multiples of 8 elements, 16-B aligned", i, (long long)rows[i],
+                  (long long)cols[i], (long long)ld[i], trans[i]);
+    const int tc = static_cast<int>((cols[i] + 63) / 64), tr = static_cast<int>((rows[i] + 63) / 64);
+    J.j[i] = SplitJob{src[i], ld[i], static_cast<int>(rows[i]), static_cast<int>(cols[i]),
+                      trans[i] ? 1 : 0, tc, tiles, static_cast<uint16_t*>(dst[i])};
+    tiles += tc * tr;
+  }
+  clear_stale_error();
+  hipLaunchKernelGGL(split_planes_kernel, dim3(tiles), dim3(256), 0, as_stream(stream), J);
+  return check_launch("ocppo_split_planes");
+}
 
 extern "C" int ocppo_gemm_x6(ocppo_stream_t stream, const float* a, int64_t sam, int64_t sak,
                              const float* b, int64_t sbn, int64_t sbk, float* c, int64_t ldc,
                              int64_t M, int64_t N, int64_t K, int64_t splits, int64_t split_c,
                              const float* bias, int relu,
                              const float* mask, int64_t ldm, float* dbp, uint64_t* mbits_out,
-                             const uint64_t* mbits_in, int tile, int mbig) {
+                             const uint64_t* mbits_in, int tile, int mbig,
+                             const void* b_planes, int64_t bp_ld, int64_t bp_stride) {
   OCPPO_REQUIRE(M >= 1 && N >= 1 && K >= 1 && splits >= 1 && M <= INT32_MAX && N <= INT32_MAX &&
                     K <= INT32_MAX,
                 "ocppo_gemm_x6: bad sizes M=%lld N=%lld K=%lld splits=%lld", (long long)M,
                 (long long)N, (long long)K, (long long)splits);
-  OCPPO_REQUIRE(a && b && c, "ocppo_gemm_x6: null pointer");
+  OCPPO_REQUIRE(a && (b || b_planes) && c, "ocppo_gemm_x6: null pointer");
   OCPPO_REQUIRE((sak == 1 && sam >= K && sam % 4 == 0) || (sam == 1 && sak >= M && sak % 4 == 0),
                 "ocppo_gemm_x6: A strides (%lld, %lld): one must be 1, the other a multiple of 4",
                 (long long)sam, (long long)sak);
-  OCPPO_REQUIRE((sbk == 1 && sbn >= K && sbn % 4 == 0) || (sbn == 1 && sbk >= N && sbk % 4 == 0),
+  OCPPO_REQUIRE(b_planes != nullptr ||
+                    (sbk == 1 && sbn >= K && sbn % 4 == 0) || (sbn == 1 && sbk >= N && sbk % 4 == 0),
                 "ocppo_gemm_x6: B strides (%lld, %lld): one must be 1, the other a multiple of 4",
                 (long long)sbn, (long long)sbk);
+  OCPPO_REQUIRE(b_planes == nullptr ||
+                    (sak == 1 && bp_ld >= K && bp_ld % 8 == 0 && bp_stride >= bp_ld * N &&
+                     bp_stride % 8 == 0 && reinterpret_cast<uintptr_t>(b_planes) % 16 == 0 &&
+                     ((tile >= 24 && tile < 28) || tile == 56)),
+                "ocppo_gemm_x6: pre-split B needs a k-contiguous A, 16-B aligned k-contiguous "
+                "planes (ld %lld, stride %lld) and a tile of 24..27 or 56", (long long)bp_ld,
+                (long long)bp_stride);
   OCPPO_REQUIRE(ldc >= N, "ocppo_gemm_x6: ldc=%lld < N", (long long)ldc);
   OCPPO_REQUIRE(reinterpret_cast<uintptr_t>(a) % 16 == 0 && reinterpret_cast<uintptr_t>(b) % 16 == 0,
                 "ocppo_gemm_x6: A and B must be 16-B aligned");
+  if (b_planes) b = nullptr;
   OCPPO_REQUIRE(K % kX6BK == 0 && K / kX6BK >= splits,
                 "ocppo_gemm_x6: K=%lld must be a multiple of %d with >= 1 step per split",
                 (long long)K, kX6BK);
@@ -627,7 +819,8 @@ extern "C" int ocppo_gemm_x6(ocppo_stream_t stream, const float* a, int64_t sam,
   const int64_t units = splits * (M / bm) * (N / bn);
   OCPPO_REQUIRE(units <= INT32_MAX / 2, "ocppo_gemm_x6: too large");
   X6Args g{a, sam, sak, b, sbn, sbk, c, ldc, bias, relu ? 1 : 0, (int)M, (int)N, (int)K,
-           0, 0, (int)units, (int)splits, split_c, mask, ldm, dbp, mbits_out, mbits_in, 0};
+           0, 0, (int)units, (int)splits, split_c, mask, ldm, dbp, mbits_out, mbits_in, 0,
+           static_cast<const uint16_t*>(b_planes), bp_ld, bp_stride};
   if (tile & 32) {
     g.mbig = mbig >= 0 ? mbig : x6_mixed_mbig((int)M, (int)N);
     OCPPO_REQUIRE(g.mbig >= 0 && g.mbig <= M && g.mbig % 128 == 0 && ((g.mbig / 128) * (N / 128)) % 8 == 0,

@@ -9,6 +9,8 @@ Reference lines replaced are cited per function (paths relative to the reference
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 
 from . import _lib
@@ -873,13 +875,21 @@ def x6_mbits_words(M: int, N: int, tile: int) -> int:
 
 
 def gemm_x6(a, sam, sak, b, sbn, sbk, c, ldc, M, N, K, splits=1, split_c=0, bias=None,
-            relu=False, mask=None, dbp=None, tile=None, mbits_out=None, mbits_in=None, mbig=None):
+            relu=False, mask=None, dbp=None, tile=None, mbits_out=None, mbits_in=None, mbig=None,
+            b_planes=None):
     """Raw ocppo_gemm_x6 call on tensors a, b, c (their data pointers; strides as given).
-    mbig: rows in 128 x 128 tiles for the mixed variant (None: the library's choice)."""
+    mbig: rows in 128 x 128 tiles for the mixed variant (None: the library's choice).
+    b_planes: B pre-split, bf16 [3, N, K] (split_planes of B); b may then be None."""
     t = x6_tile(M, N, splits, tile)
     if t is None:
         raise ValueError(f"gemm_x6: no tile divides {M} x {N}")
     dev = c.device
+    if b_planes is not None:
+        if (b_planes.dtype != torch.bfloat16 or tuple(b_planes.shape) != (3, N, K)
+                or not b_planes.is_contiguous() or b_planes.device != dev or sak != 1
+                or K % 8 or not (X6_AUTO <= t < X6_AUTO + 4 or t == X6_MIXED)):
+            raise ValueError("gemm_x6: b_planes must be a contiguous bf16 [3, N, K] on the "
+                             "output's device, with a k-contiguous A and a tile of the x6 family")
     if mask is not None:
         if (mask.dim() != 2 or tuple(mask.shape) != (M, N) or mask.stride(1) != 1
                 or mask.dtype != torch.float32 or dbp is None):
@@ -890,16 +900,18 @@ def gemm_x6(a, sam, sak, b, sbn, sbk, c, ldc, M, N, K, splits=1, split_c=0, bias
         if mb is not None:
             _check(mb, "mbits", torch.int64, dev, x6_mbits_words(M, N, t))
     bp = None if bias is None else _check(bias, "bias", torch.float32, dev, N)
-    args = (a.data_ptr(), sam, sak, b.data_ptr(), sbn, sbk, c.data_ptr(), ldc, M, N, K, splits,
+    args = (a.data_ptr(), sam, sak, None if b is None else b.data_ptr(), sbn, sbk, c.data_ptr(),
+            ldc, M, N, K, splits,
             split_c, bp, int(bool(relu)), None if mask is None else mask.data_ptr(),
             0 if mask is None else mask.stride(0), None if dbp is None else dbp.data_ptr(),
             None if mbits_out is None else mbits_out.data_ptr(),
-            None if mbits_in is None else mbits_in.data_ptr(), t, -1 if mbig is None else int(mbig))
+            None if mbits_in is None else mbits_in.data_ptr(), t, -1 if mbig is None else int(mbig),
+            None if b_planes is None else b_planes.data_ptr(), K, N * K)
     # timer site name: the product's shape (bench.py's gemm_x6 roofline parses it); the closure
     # keeps the operand tensors alive for the timer's replays
     masked = mask is not None or mbits_in is not None
     name = f"gemm_x6_{M}x{N}x{K}s{splits}{'m' if masked else ''}"
-    keep = (a, b, c, bias, mask, dbp, mbits_out, mbits_in)
+    keep = (a, b, c, bias, mask, dbp, mbits_out, mbits_in, b_planes)
     timed(name, lambda: call("ocppo_gemm_x6", _stream(dev), *args) or keep)
     return c
 
@@ -910,19 +922,20 @@ def linear_x6_ok(x, w) -> bool:
             and x.shape[1] % 32 == 0 and x6_tile(x.shape[0], w.shape[0]) is not None)
 
 
-def linear_x6(x, w, b=None, relu=False, out=None, mbits=False):
+def linear_x6(x, w, b=None, relu=False, out=None, mbits=False, planes=None):
     """act(x W^T + b) (torch._addmm_activation's order: sum, + bias, then ReLU). mbits=True
-    (with relu) also returns the output's ReLU bitmask (tensor, tile) for dx_x6_relu."""
+    (with relu) also returns the output's ReLU bitmask (tensor, tile) for dx_x6_relu. planes:
+    W's pre-split bf16 [3, N, K] (WeightPlanes; bitwise the same result)."""
     M, K = x.shape
     N = w.shape[0]
     out = torch.empty((M, N), dtype=torch.float32, device=x.device) if out is None else out
     if not mbits:
         return gemm_x6(x, x.stride(0), 1, w, w.stride(0), 1, out, out.stride(0), M, N, K, bias=b,
-                       relu=relu)
+                       relu=relu, b_planes=planes)
     t = x6_tile(M, N)
     bits = torch.empty(x6_mbits_words(M, N, t), dtype=torch.int64, device=x.device)
     gemm_x6(x, x.stride(0), 1, w, w.stride(0), 1, out, out.stride(0), M, N, K, bias=b,
-            relu=relu, tile=t, mbits_out=bits)
+            relu=relu, tile=t, mbits_out=bits, b_planes=planes)
     return out, (bits, t)
 
 
@@ -932,14 +945,16 @@ def dx_x6_ok(g, w) -> bool:
             and g.shape[1] % 32 == 0 and x6_tile(g.shape[0], w.shape[1]) is not None)
 
 
-def dx_x6(g, w, out=None):
+def dx_x6(g, w, out=None, planes=None):
+    """g W; planes: W^T's pre-split bf16 [3, K, N] (WeightPlanes)."""
     M, N = g.shape
     K = w.shape[1]
     out = torch.empty((M, K), dtype=torch.float32, device=g.device) if out is None else out
-    return gemm_x6(g, g.stride(0), 1, w, 1, w.stride(0), out, out.stride(0), M, K, N)
+    return gemm_x6(g, g.stride(0), 1, w, 1, w.stride(0), out, out.stride(0), M, K, N,
+                   b_planes=planes)
 
 
-def dx_x6_relu(g, w, mask, mbits=None):
+def dx_x6_relu(g, w, mask, mbits=None, planes=None):
     """gp = threshold_backward(g W, mask, 0) for the Linear+ReLU layer below whose output is
     `mask` [M, K], with that layer's bias-gradient partials: returns (gp, dbp [M / tile rows, K])
     (dbp summed in row-tile order by sum_splits_db). mbits = (bitmask, tile) from that layer's
@@ -951,10 +966,63 @@ def dx_x6_relu(g, w, mask, mbits=None):
     dbp = torch.empty((M // X6_TILES[t][0], K), dtype=torch.float32, device=g.device)
     if mbits is not None and mbits[1] == t:
         gemm_x6(g, g.stride(0), 1, w, 1, w.stride(0), gp, K, M, K, N, dbp=dbp, tile=t,
-                mbits_in=mbits[0])
+                mbits_in=mbits[0], b_planes=planes)
     else:
-        gemm_x6(g, g.stride(0), 1, w, 1, w.stride(0), gp, K, M, K, N, mask=mask, dbp=dbp, tile=t)
+        gemm_x6(g, g.stride(0), 1, w, 1, w.stride(0), gp, K, M, K, N, mask=mask, dbp=dbp, tile=t,
+                b_planes=planes)
     return gp, dbp
+
+
+class WeightPlanes:
+    """Pre-split bf16 planes of Linear weights for the update GEMMs' B operand (ocppo_gemm_x6 with
+    b_planes): [3, N, K] of W for the forward, [3, K, N] of W^T for dX, written by ONE
+    ocppo_split_planes launch per refresh (after every optimizer step: the trainer refreshes at
+    the start of each minibatch). The parameters are views of a flat buffer at fixed addresses,
+    so the job table is built once. Attaches w._ocppo_planes = {"fwd": ..., "dx": ...}."""
+
+    def __init__(self, fwd=(), dx=()):
+        jobs = []
+        for ws, trans in ((fwd, 0), (dx, 1)):
+            for w in ws:
+                if w.dtype != torch.float32 or w.dim() != 2 or w.stride(1) != 1:
+                    raise ValueError("WeightPlanes: row-major f32 weights")
+                R, C = w.shape
+                shape = (3, C, R) if trans else (3, R, C)
+                if shape[2] % 8:
+                    raise ValueError(f"WeightPlanes: plane rows of {shape[2]} elements")
+                dst = torch.empty(shape, dtype=torch.bfloat16, device=w.device)
+                d = getattr(w, "_ocppo_planes", None) or {}
+                d["dx" if trans else "fwd"] = dst
+                w._ocppo_planes = d
+                jobs.append((w, trans, dst))
+        self.jobs = jobs
+        self.dev = jobs[0][0].device if jobs else None
+        c = ctypes
+        self.calls = []
+        for i in range(0, len(jobs), 8):
+            part = jobs[i:i + 8]
+            n = len(part)
+            arrs = ((c.c_void_p * n)(*[w.data_ptr() for w, _, _ in part]),
+                    (c.c_int64 * n)(*[w.stride(0) for w, _, _ in part]),
+                    (c.c_int64 * n)(*[w.shape[0] for w, _, _ in part]),
+                    (c.c_int64 * n)(*[w.shape[1] for w, _, _ in part]),
+                    (c.c_int * n)(*[t for _, t, _ in part]),
+                    (c.c_void_p * n)(*[d.data_ptr() for _, _, d in part]))
+            self.calls.append((n, arrs))
+
+    def refresh(self):
+        for n, arrs in self.calls:
+            call("ocppo_split_planes", _stream(self.dev), n, *arrs)
+
+
+def split_planes_ref(x):
+    """The exact three-piece bf16 split of an f32 tensor in torch (round to nearest even at each
+    step): the reference ocppo_split_planes / gemm_x6 are checked against (tests)."""
+    x0 = x.to(torch.bfloat16)
+    r1 = x - x0.float()
+    x1 = r1.to(torch.bfloat16)
+    x2 = (r1 - x1.float()).to(torch.bfloat16)
+    return torch.stack([x0, x1, x2])
 
 
 def dw_x6_ok(g, x, splits: int) -> bool:

@@ -396,6 +396,7 @@ class PPOTrainer:
         self.gp_tail = (torch.empty((self.M, self.H), dtype=f32, device=dev)
                         if self.fused_heads_loss else None)
         self.b_obs = self.obs[:T].view((T * N,) + self.obs_shape)
+        self.wplanes = self._weight_planes()
 
         # Every update is captured, the NatureCNN's MIOpen convolutions included (round 1 ran that
         # one eagerly after a capture_end crash that no longer reproduces: tools/exp_c3_capture.py
@@ -415,6 +416,29 @@ class PPOTrainer:
         self.global_step = 0
         self.last_metrics: dict = {}
         self._reset_env()
+
+    def _weight_planes(self):
+        """ops.WeightPlanes of the PPObj Linear weights whose update forward / dX run on gemm_x6
+        (agents._x6 at the rows they see: up to M W frames for the encoder, M for the decoder);
+        None when there are none."""
+        a, ag = self.args, self.agent
+        if not (a.x6_gemm and a.x6_weight_planes and isinstance(ag, PPObj) and self.dev.type == "cuda"):
+            return None
+        # the dedup capacity is sized later (first shuffle); M W rows bound it from above, and
+        # the x6 rules pass at 11520 (config 2's capacity) exactly where they pass at 16384
+        enc_rows = self.M * self.obs_shape[0]
+        fwd, dx = [], []
+        net = ag.network
+        for i, m in enumerate(net):
+            if not isinstance(m, nn.Linear) or i == 0:
+                continue
+            rows = enc_rows if i < ag._flat else self.M
+            N_, K_ = m.out_features, m.in_features
+            if agents._x6(rows, N_, K_) and K_ % 32 == 0 and ops.x6_tile(rows, N_) is not None:
+                fwd.append(m.weight)
+            if agents._x6(rows, K_, N_) and N_ % 32 == 0 and ops.x6_tile(rows, K_) is not None:
+                dx.append(m.weight)
+        return ops.WeightPlanes(fwd, dx) if fwd or dx else None
 
     def _fusable_encoder(self) -> bool:
         """PPObj encoder shapes the fused rollout kernels take: >= 3 Linear+ReLU layers, the first
@@ -625,7 +649,15 @@ class PPOTrainer:
                 self.env.host_step()  # waits for part k's action copy, steps the CPU env
 
     def _forward_backward(self, j: int):
-        """Minibatch j: gather, forward, fused loss, backward into the flat grad buffer."""
+        """Minibatch j: gather, forward, fused loss, backward into the flat grad buffer (the
+        weights' bf16 planes refreshed first: the previous minibatch's step changed them)."""
+        if self.wplanes is None:
+            return self._forward_backward_body(j)
+        self.timer.bracket("split_planes", self.wplanes.refresh)
+        with agents.weight_planes():
+            return self._forward_backward_body(j)
+
+    def _forward_backward_body(self, j: int):
         a = self.args
         idx = self.perm_dev[j * self.M:(j + 1) * self.M]
         ag = self.agent
@@ -690,7 +722,8 @@ class PPOTrainer:
         # AccumulateGrad nodes, bound to the stream they were created on) alive into the next
         # capture, which then syncs with that stream and breaks
         low, low_d = self.cuts.pop(j)
-        torch.autograd.backward(low, low_d.grad)
+        with agents.weight_planes():
+            torch.autograd.backward(low, low_d.grad)
 
     def _exchange(self, j: int, replay: bool):
         """Minibatch j's gradients, all-reduced (GradExchange; the `/ world_size` is folded into

@@ -90,5 +90,5 @@ def test_gemm_x6_mbig_only_for_the_mixed_tile(lib):
     dummy = ctypes.c_void_p(256)
     args = [None, dummy, 64, 1, dummy, 64, 1, dummy, 128, 128, 128, 64, 1, 0, None, 0, None, 0,
             None, None, None]
-    assert lib.LIB.ocppo_gemm_x6(*args, 24, 512) == lib.OCPPO_E_INVALID
+    assert lib.LIB.ocppo_gemm_x6(*args, 24, 512, None, 0, 0) == lib.OCPPO_E_INVALID
     assert b"mbig" in lib.LIB.ocppo_last_error()

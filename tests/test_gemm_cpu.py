@@ -76,3 +76,19 @@ def test_update_gemm_route_is_per_agent():
     assert all(agents.x6_route(m.weight) for m in lins_b)
     assert agents.x6_route(nn.Linear(4, 4).weight) == agents.X6_GEMM_DEFAULT
     assert not hasattr(agents, "X6_GEMM") and not hasattr(agents, "X6_MASK_DX")
+
+
+def test_split_planes_ref_is_exact():
+    """The three round-to-nearest bf16 pieces of an f32 sum back to it exactly (the premise of
+    gemm_x6 and of its pre-split weights)."""
+    import torch
+
+    from oc_cleanrl_amd import ops
+
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(4096, generator=g) * torch.exp(torch.randn(4096, generator=g) * 4)
+    p = ops.split_planes_ref(x)
+    assert p.shape == (3, 4096) and p.dtype == torch.bfloat16
+    assert torch.equal(p[0].double() + p[1].double() + p[2].double(), x.double())
+    # each piece is the nearest bf16 of what remains
+    assert torch.equal(p[0], x.to(torch.bfloat16))

@@ -202,3 +202,58 @@ def test_mixed_tiles(mbig):
     assert not bool((dbp_f == 7.0).any())
     pairs = dbp_f.double().view(M // 128, 2, N).sum(1)
     assert torch.allclose(pairs, gp_f.double().view(M // 128, 128, N).sum(1), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("R,C,trans", [(512, 256, 0), (1024, 512, 1), (100, 136, 0), (136, 96, 1),
+                                       (2048, 512, 1)])
+def test_split_planes_is_the_exact_split(R, C, trans):
+    """ocppo_split_planes writes, bitwise, the three round-to-nearest bf16 pieces of every element
+    (of W or W^T), the pieces gemm_x6 forms in its K loop; x0 + x1 + x2 == x exactly."""
+    g = torch.Generator(device=DEV).manual_seed(R + C + trans)
+    w = torch.randn(R, C, device=DEV, generator=g) * torch.exp(
+        torch.randn(R, C, device=DEV, generator=g) * 3)
+    w[0, :4] = torch.tensor([0.0, -0.0, 1e-30, 3.0e38])
+    src = w.t().contiguous() if trans else w
+    wp = ops.WeightPlanes(fwd=[] if trans else [w], dx=[w] if trans else [])
+    wp.refresh()
+    torch.cuda.synchronize()
+    got = w._ocppo_planes["dx" if trans else "fwd"]
+    ref = ops.split_planes_ref(src)
+    assert torch.equal(got.view(torch.int16), ref.view(torch.int16))
+    tot = got[0].double() + got[1].double() + got[2].double()
+    assert torch.equal(tot, src.double())
+
+
+@pytest.mark.parametrize("tile", [24, 25, 26, 27, 56])
+def test_gemm_x6_presplit_b_is_bitwise_the_f32_b(tile):
+    """The forward (bias + ReLU + bitmask) and the masked dX with B read as pre-split planes
+    (WeightPlanes) give bitwise the outputs, bitmasks and bias-gradient partials of the f32 B."""
+    g = torch.Generator(device=DEV).manual_seed(tile)
+    M, K0, N, N2 = 1024, 256, 256, 128
+    x = _rand(M, K0, gen=g)
+    w = _rand(N, K0, gen=g, scale=K0 ** -0.5)
+    b = _rand(N, gen=g, scale=0.1)
+    w2 = _rand(N2, N, gen=g, scale=N2 ** -0.5)
+    wp = ops.WeightPlanes(fwd=[w], dx=[w2])
+    wp.refresh()
+    if ops.x6_tile(M, N, 1, tile) is None or ops.x6_tile(M, N, 1, tile) != tile:
+        pytest.skip("tile does not divide")
+    t = tile
+    bits_a = torch.empty(ops.x6_mbits_words(M, N, t), dtype=torch.int64, device=DEV)
+    bits_b = torch.empty_like(bits_a)
+    h_a, h_b = torch.empty(M, N, device=DEV), torch.empty(M, N, device=DEV)
+    ops.gemm_x6(x, K0, 1, w, K0, 1, h_a, N, M, N, K0, bias=b, relu=True, tile=t, mbits_out=bits_a)
+    ops.gemm_x6(x, K0, 1, None, K0, 1, h_b, N, M, N, K0, bias=b, relu=True, tile=t,
+                mbits_out=bits_b, b_planes=w._ocppo_planes["fwd"])
+    assert torch.equal(h_a, h_b) and torch.equal(bits_a, bits_b)
+    gg = _rand(M, N2, gen=g)
+    bm = ops.X6_TILES[t][0]
+    gp_a, dbp_a = torch.empty(M, N, device=DEV), torch.empty(M // bm, N, device=DEV)
+    gp_b, dbp_b = torch.empty(M, N, device=DEV), torch.empty(M // bm, N, device=DEV)
+    ops.gemm_x6(gg, N2, 1, w2, 1, N, gp_a, N, M, N, N2, dbp=dbp_a, tile=t, mbits_in=bits_a)
+    ops.gemm_x6(gg, N2, 1, None, 1, N, gp_b, N, M, N, N2, dbp=dbp_b, tile=t, mbits_in=bits_a,
+                b_planes=w2._ocppo_planes["dx"])
+    assert torch.equal(gp_a, gp_b) and torch.equal(dbp_a, dbp_b)
+    # unmasked dX and plain forward through the helpers
+    assert torch.equal(ops.dx_x6(gg, w2), ops.dx_x6(gg, w2, planes=w2._ocppo_planes["dx"]))
+    assert torch.equal(ops.linear_x6(x, w, b), ops.linear_x6(x, w, b, planes=w._ocppo_planes["fwd"]))

@@ -578,3 +578,18 @@ def test_two_trainers_keep_their_own_update_gemm_route(dev):
     assert len(sites(on)) >= 8
     assert sites(off) == []
     assert len(sites(on)) >= 8
+
+
+@pytest.mark.parametrize("graphs", [False, True])
+def test_weight_planes_are_bitwise_the_in_kernel_split(dev, graphs):
+    """The update with the weights split into bf16 planes once per minibatch (Args.
+    x6_weight_planes, ops.WeightPlanes) is bitwise the update with the split in gemm_x6's K loop:
+    same rollouts, same parameters after three iterations at config-2 dims."""
+    kw = dict(num_envs=128, num_steps=128, encoder_dims=(256, 512, 1024, 512),
+              decoder_dims=(512,), update_epochs=1, cuda_graphs=graphs)
+    a, _ = run_iters(small_args(x6_weight_planes=True, **kw), 3, dev)
+    b, _ = run_iters(small_args(x6_weight_planes=False, **kw), 3, dev)
+    assert a.wplanes is not None and b.wplanes is None
+    assert len(a.wplanes.jobs) >= 4
+    for p, q in zip(a.agent.parameters(), b.agent.parameters()):
+        assert torch.equal(p, q)
