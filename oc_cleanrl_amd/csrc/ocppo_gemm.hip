@@ -721,18 +721,25 @@ __global__ __launch_bounds__(256) void split_planes_kernel(SplitJobs J) {
   __syncthreads();
   const int oR = jb.trans ? jb.C : jb.R, oC = jb.trans ? jb.R : jb.C;
   const int64_t ps = static_cast<int64_t>(oR) * oC;
-  for (int e = threadIdx.x; e < 64 * 32; e += 256) {
-    const int orow = e >> 5, op = e & 31;
-    const x6f2 v = jb.trans ? x6f2{tile[2 * op][orow], tile[2 * op + 1][orow]}
-                            : x6f2{tile[orow][2 * op], tile[orow][2 * op + 1]};
-    const int gr = (jb.trans ? c0 : r0) + orow, gc = (jb.trans ? r0 : c0) + 2 * op;
-    if (gr >= oR || gc >= oC) continue;
-    uint32_t p0, p1, p2;
-    x6_split2(v, p0, p1, p2);
-    uint32_t* d = reinterpret_cast<uint32_t*>(jb.dst + static_cast<int64_t>(gr) * oC + gc);
-    d[0] = p0;
-    d[ps / 2] = p1;
-    d[ps] = p2;
+  for (int e = threadIdx.x; e < 64 * 16; e += 256) {  // 4 output elements (8 B per plane) each
+    const int orow = e >> 4, oq = e & 15;
+    x6f2 v01, v23;
+    if (jb.trans) {
+      v01 = x6f2{tile[4 * oq][orow], tile[4 * oq + 1][orow]};
+      v23 = x6f2{tile[4 * oq + 2][orow], tile[4 * oq + 3][orow]};
+    } else {
+      v01 = x6f2{tile[orow][4 * oq], tile[orow][4 * oq + 1]};
+      v23 = x6f2{tile[orow][4 * oq + 2], tile[orow][4 * oq + 3]};
+    }
+    const int gr = (jb.trans ? c0 : r0) + orow, gc = (jb.trans ? r0 : c0) + 4 * oq;
+    if (gr >= oR || gc >= oC) continue;  // oC % 8 == 0: a quad is inside or outside whole
+    uint32_t a0, a1, a2, b0, b1, b2;
+    x6_split2(v01, a0, a1, a2);
+    x6_split2(v23, b0, b1, b2);
+    uint2* d = reinterpret_cast<uint2*>(jb.dst + static_cast<int64_t>(gr) * oC + gc);
+    d[0] = uint2{a0, b0};
+    d[ps / 4] = uint2{a1, b1};
+    d[ps / 2] = uint2{a2, b2};
   }
 }
 

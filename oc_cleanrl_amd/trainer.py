@@ -396,7 +396,7 @@ class PPOTrainer:
         self.gp_tail = (torch.empty((self.M, self.H), dtype=f32, device=dev)
                         if self.fused_heads_loss else None)
         self.b_obs = self.obs[:T].view((T * N,) + self.obs_shape)
-        self.wplanes = self._weight_planes()
+        self.wplanes, self.wplanes_built = None, False  # built at the first minibatch
 
         # Every update is captured, the NatureCNN's MIOpen convolutions included (round 1 ran that
         # one eagerly after a capture_end crash that no longer reproduces: tools/exp_c3_capture.py
@@ -419,24 +419,29 @@ class PPOTrainer:
 
     def _weight_planes(self):
         """ops.WeightPlanes of the PPObj Linear weights whose update forward / dX run on gemm_x6
-        (agents._x6 at the rows they see: up to M W frames for the encoder, M for the decoder);
-        None when there are none."""
+        where the pre-split B pays (measured at config 2, profiles/r04/planes_ab.txt): the mixed
+        128 x 128 / 64 x 128 tiles and the 4096-row decoder dX gain 2-7 us per product, the
+        720-tile [11520 x 1024] products lose 4-7 us (their extra B bytes per step), so those keep
+        the in-kernel split. Built at the first minibatch (the frame-dedup capacity, the rows the
+        encoder sees, is known by then); None when no product qualifies."""
         a, ag = self.args, self.agent
         if not (a.x6_gemm and a.x6_weight_planes and isinstance(ag, PPObj) and self.dev.type == "cuda"):
             return None
-        # the dedup capacity is sized later (first shuffle); M W rows bound it from above, and
-        # the x6 rules pass at 11520 (config 2's capacity) exactly where they pass at 16384
-        enc_rows = self.M * self.obs_shape[0]
+        enc_rows = self.planner.cap if self.frame_dedup else self.M * self.obs_shape[0]
+
+        def pays(rows, n, k):
+            t = ops.x6_tile(rows, n)
+            return (agents._x6(rows, n, k) and k % 32 == 0 and t is not None
+                    and (t == ops.X6_MIXED or rows <= 4096))
+
         fwd, dx = [], []
-        net = ag.network
-        for i, m in enumerate(net):
+        for i, m in enumerate(ag.network):
             if not isinstance(m, nn.Linear) or i == 0:
                 continue
             rows = enc_rows if i < ag._flat else self.M
-            N_, K_ = m.out_features, m.in_features
-            if agents._x6(rows, N_, K_) and K_ % 32 == 0 and ops.x6_tile(rows, N_) is not None:
+            if pays(rows, m.out_features, m.in_features):
                 fwd.append(m.weight)
-            if agents._x6(rows, K_, N_) and N_ % 32 == 0 and ops.x6_tile(rows, K_) is not None:
+            if pays(rows, m.in_features, m.out_features):
                 dx.append(m.weight)
         return ops.WeightPlanes(fwd, dx) if fwd or dx else None
 
@@ -651,6 +656,8 @@ class PPOTrainer:
     def _forward_backward(self, j: int):
         """Minibatch j: gather, forward, fused loss, backward into the flat grad buffer (the
         weights' bf16 planes refreshed first: the previous minibatch's step changed them)."""
+        if not self.wplanes_built:
+            self.wplanes, self.wplanes_built = self._weight_planes(), True
         if self.wplanes is None:
             return self._forward_backward_body(j)
         self.timer.bracket("split_planes", self.wplanes.refresh)

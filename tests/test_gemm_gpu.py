@@ -239,8 +239,9 @@ def test_gemm_x6_presplit_b_is_bitwise_the_f32_b(tile):
     if ops.x6_tile(M, N, 1, tile) is None or ops.x6_tile(M, N, 1, tile) != tile:
         pytest.skip("tile does not divide")
     t = tile
-    bits_a = torch.empty(ops.x6_mbits_words(M, N, t), dtype=torch.int64, device=DEV)
-    bits_b = torch.empty_like(bits_a)
+    # zeros: the mixed tile's 128-row tiles fill half of the 64-row-tile word slots
+    bits_a = torch.zeros(ops.x6_mbits_words(M, N, t), dtype=torch.int64, device=DEV)
+    bits_b = torch.zeros_like(bits_a)
     h_a, h_b = torch.empty(M, N, device=DEV), torch.empty(M, N, device=DEV)
     ops.gemm_x6(x, K0, 1, w, K0, 1, h_a, N, M, N, K0, bias=b, relu=True, tile=t, mbits_out=bits_a)
     ops.gemm_x6(x, K0, 1, None, K0, 1, h_b, N, M, N, K0, bias=b, relu=True, tile=t,

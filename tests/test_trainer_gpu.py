@@ -590,6 +590,6 @@ def test_weight_planes_are_bitwise_the_in_kernel_split(dev, graphs):
     a, _ = run_iters(small_args(x6_weight_planes=True, **kw), 3, dev)
     b, _ = run_iters(small_args(x6_weight_planes=False, **kw), 3, dev)
     assert a.wplanes is not None and b.wplanes is None
-    assert len(a.wplanes.jobs) >= 4
+    assert len(a.wplanes.jobs) >= 3
     for p, q in zip(a.agent.parameters(), b.agent.parameters()):
         assert torch.equal(p, q)
