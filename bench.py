@@ -281,6 +281,8 @@ def main():
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                     help="torch.distributed backend for N > 1 (nccl = RCCL; gloo only for the "
                          "N = 2 rehearsal with ranks sharing one GPU)")
+    ap.add_argument("--dp-exchange", action="store_true",
+                    help="N = 1: run the DP exchange path over a 1-rank group (its structure cost)")
     ap.add_argument("--device-index", type=int, default=None,
                     help="GPU of this rank (default LOCAL_RANK; 0 for the shared-GPU rehearsal)")
     ap.add_argument("--set", action="append", default=[], metavar="FIELD=VALUE",
@@ -306,6 +308,15 @@ def main():
             dist.init_process_group("nccl", device_id=device)
         else:
             dist.init_process_group("gloo")
+    elif opt.dp_exchange:
+        # the data-parallel step structure (per-minibatch graphs around an RCCL all-reduce of the
+        # flat gradient buffer, /world folded into Adam) over a 1-rank group: what N > 1 runs,
+        # minus the xGMI transfer
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(free_port()))
+        dist.init_process_group(opt.backend, rank=0, world_size=1,
+                                **({"device_id": device} if opt.backend == "nccl" else {}))
+        opt.set.append("dp_exchange=1")
 
     if opt.config == 1:
         from oc_cleanrl_amd.ppo import PPO_DEFAULTS
@@ -542,7 +553,7 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 
