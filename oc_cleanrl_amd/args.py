@@ -126,6 +126,9 @@ class Args:
                                   # generator stream) instead of once per rollout ([T, N, A])
     fused_heads_loss: bool = True  # update: policy heads fwd + PPO loss + heads bwd in one HIP op
     dp_overlap: bool = True  # DP: all-reduce the decoder-side gradients during the encoder backward
+    dp_graph_collectives: bool = False  # DP: capture each epoch's minibatches WITH their RCCL
+                                        # all-reduces in one hipGraph (else one graph per phase,
+                                        # the collectives launched eagerly between them)
     dp_exchange: bool = False  # run the DP exchange path (per-minibatch graphs + all-reduce) even
                                # at world size 1, over an initialised 1-rank process group
     conv_channels_last: bool = True  # pixel NatureCNN in NHWC (MIOpen NHWC kernels, no transposes)

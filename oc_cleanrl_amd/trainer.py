@@ -856,7 +856,9 @@ class PPOTrainer:
                 self.g_host.append(g)
         if not self.graph_update:
             pass
-        elif not self.dp:
+        elif not self.dp or self.args.dp_graph_collectives:
+            # (DP: the epoch's all-reduces captured with it; ProcessGroupNCCL records no watchdog
+            # work for collectives issued under capture)
             for e in range(self.E):
                 g = torch.cuda.CUDAGraph()
                 with _graph_capture(g, pool):
@@ -887,7 +889,7 @@ class PPOTrainer:
         self.executed_mb = 0
         for e in range(self.E):
             if self.graphs_ready and self.graph_update:
-                if not self.dp:
+                if not self.dp or a.dp_graph_collectives:
                     self.g_update[e].replay()
                 else:
                     for k in range(self.nmb):

@@ -52,7 +52,7 @@ def test_two_ranks_share_one_gpu_over_gloo(fused_opt, graphs):
 
 
 
-def _rccl_worker(rank, world, port, out, overlap, graphs):
+def _rccl_worker(rank, world, port, out, overlap, graphs, collectives=False):
     """The RCCL exchange path at world size 1: nccl (= RCCL) process group bound to cuda:0,
     per-minibatch graphs, the async tail all-reduce overlapped with the g_low replay, the head
     all-reduce, g_opt -- against the plain single-GPU trainer in the same process."""
@@ -67,7 +67,8 @@ def _rccl_worker(rank, world, port, out, overlap, graphs):
                              num_envs=32, num_steps=16, num_minibatches=4, update_epochs=2,
                              total_timesteps=32 * 16 * 10, encoder_dims=(32, 64, 48),
                              decoder_dims=(64,), save_model=False, cuda_graphs=graphs,
-                             dp_overlap=overlap, dp_exchange=dp), 1)
+                             dp_overlap=overlap, dp_exchange=dp,
+                             dp_graph_collectives=collectives), 1)
 
     plain = PPOTrainer(args(False), dev)
     for _ in range(3):
@@ -81,7 +82,9 @@ def _rccl_worker(rank, world, port, out, overlap, graphs):
     for _ in range(3):
         tr.train_iteration()
     torch.cuda.synchronize()
-    if graphs:
+    if graphs and collectives:
+        assert tr.graphs_ready and len(tr.g_update) == tr.E and tr.g_opt is None
+    elif graphs:
         assert tr.graphs_ready and len(tr.g_update) == tr.E * tr.nmb and tr.g_opt is not None
         assert len(tr.g_low) == (tr.E * tr.nmb if overlap else 0)
     flat = lambda t: torch.cat([p.detach().flatten() for p in t.agent.parameters()]).cpu()  # noqa
@@ -90,14 +93,18 @@ def _rccl_worker(rank, world, port, out, overlap, graphs):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("overlap,graphs", [(True, True), (False, True), (True, False)])
-def test_rccl_exchange_one_rank_matches_single_gpu(overlap, graphs):
+@pytest.mark.parametrize("overlap,graphs,collectives", [(True, True, False), (False, True, False),
+                                                        (True, False, False), (True, True, True),
+                                                        (False, True, True)])
+def test_rccl_exchange_one_rank_matches_single_gpu(overlap, graphs, collectives):
     """ppo_atari_multigpu.py:174-183, 360-377 over RCCL on the one-GPU box: the DP flow with a
     1-rank nccl group leaves parameters bit-identical to the single-GPU trainer after 3
-    iterations (SUM over one rank, /1 folded into Adam)."""
+    iterations (SUM over one rank, /1 folded into Adam); also with each epoch's all-reduces
+    captured inside its hipGraph (dp_graph_collectives)."""
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_rccl_worker, args=(1, _port(), out, overlap, graphs), nprocs=1, join=True)
+    mp.spawn(_rccl_worker, args=(1, _port(), out, overlap, graphs, collectives), nprocs=1,
+             join=True)
     assert out["same_actions"]
     assert torch.equal(out["plain"], out["dp"]), \
         float((out["plain"] - out["dp"]).abs().max())
