@@ -22,7 +22,7 @@ LIB_PATH = Path(os.environ.get("OCPPO_LIB", PKG / "lib" / "libocppo_hip.so"))
 HEADER = PKG.parent / "include" / "ocppo.h"
 
 # constants mirrored from include/ocppo.h (checked against the header by tests/test_abi.py)
-OCPPO_ABI_VERSION = 19
+OCPPO_ABI_VERSION = 20
 OCPPO_OK, OCPPO_E_INVALID, OCPPO_E_LAUNCH, OCPPO_E_WORKSPACE = 0, 1, 2, 3
 OCPPO_F32, OCPPO_BF16, OCPPO_U8 = 0, 1, 2
 STAT_NAMES = ("loss", "pg_loss", "v_loss", "entropy", "old_approx_kl", "approx_kl", "clipfrac",
@@ -94,6 +94,8 @@ SIGNATURES: dict[str, tuple[type, list]] = {
     "ocppo_gemm_x6": (I, [P, P, I64, I64, P, I64, I64, P, I64, I64, I64, I64, I64, I64, P, I, P,
                           I64, P, P, P, I, I, P, I64, I64]),
     "ocppo_split_planes": (I, [P, I, P, P, P, P, P, P]),
+    "ocppo_gae_records": (I, [P, P, P, P, P, P, I64, I64, D, D, P, P, P, P, P]),
+    "ocppo_minibatch_prepare_records": (I, [P, P, I64, I64, P, P, P, P, P, P, P]),
     "ocppo_store_linear2": (I, [P, P, P, P, I64, I64, I64, P, P, I, P, P, P, I, D, D, D, P, P, P,
                                 P, P, P, P, I64, I64, I64]),
 }

@@ -23,6 +23,15 @@
 
 namespace ocppo {
 
+// The per-sample record ocppo_minibatch_prepare_records gathers (ocppo.h OcppoSampleRecord): one
+// 32-B line fragment per sample instead of five scattered 4-8 B values.
+__device__ __forceinline__ void gae_put_record(float4* __restrict__ rec, size_t gi, float lp,
+                                               float a, float r, float v, int64_t act) {
+  rec[2 * gi] = make_float4(lp, a, r, v);
+  rec[2 * gi + 1] = make_float4(__int_as_float(static_cast<int>(act & 0xffffffff)),
+                                __int_as_float(static_cast<int>(act >> 32)), 0.f, 0.f);
+}
+
 // The recurrence over rows rows-1 .. 0 of env column `tid` of an E-wide LDS tile (delta in sa,
 // c in sc; A written over delta): whole groups of 16 rows with no per-step branch (a uniform
 // branch per step costs more than the two dependent ops it guards), then the remainder.
@@ -59,7 +68,10 @@ __global__ __launch_bounds__(256) void gae_tile_kernel(const float* __restrict__
                                                        const float* __restrict__ next_done, int T,
                                                        int64_t N, int TC, float g, float gl,
                                                        float* __restrict__ adv,
-                                                       float* __restrict__ ret) {
+                                                       float* __restrict__ ret,
+                                                       const float* __restrict__ lp,
+                                                       const int64_t* __restrict__ act,
+                                                       float4* __restrict__ rec) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* sa = smem;           // [TC][E]  rewards in -> delta -> advantages
   float* sv = sa + TC * E;    // [TC][E]  values
@@ -142,9 +154,16 @@ __global__ __launch_bounds__(256) void gae_tile_kernel(const float* __restrict__
           const int li = row * E + 4 * c4;
           const float4 a = *reinterpret_cast<const float4*>(sa + li);
           const float4 v = *reinterpret_cast<const float4*>(sv + li);
+          const float4 r = make_float4(a.x + v.x, a.y + v.y, a.z + v.z, a.w + v.w);
           *reinterpret_cast<float4*>(adv + gi) = a;
-          *reinterpret_cast<float4*>(ret + gi) =
-              make_float4(a.x + v.x, a.y + v.y, a.z + v.z, a.w + v.w);
+          *reinterpret_cast<float4*>(ret + gi) = r;
+          if (rec) {
+            const float4 l = *reinterpret_cast<const float4*>(lp + gi);
+            gae_put_record(rec, gi, l.x, a.x, r.x, v.x, act[gi]);
+            gae_put_record(rec, gi + 1, l.y, a.y, r.y, v.y, act[gi + 1]);
+            gae_put_record(rec, gi + 2, l.z, a.z, r.z, v.z, act[gi + 2]);
+            gae_put_record(rec, gi + 3, l.w, a.w, r.w, v.w, act[gi + 3]);
+          }
         }
       }
     } else {
@@ -155,6 +174,7 @@ __global__ __launch_bounds__(256) void gae_tile_kernel(const float* __restrict__
           const size_t gi = static_cast<size_t>(t_lo + row) * N + col;
           adv[gi] = sa[e];
           ret[gi] = sa[e] + sv[e];
+          if (rec) gae_put_record(rec, gi, lp[gi], sa[e], sa[e] + sv[e], sv[e], act[gi]);
         }
       }
     }
@@ -177,7 +197,10 @@ __global__ __launch_bounds__(256) void gae_stream_kernel(const float* __restrict
                                                          const float* __restrict__ next_done,
                                                          int T, int64_t N, float g, float gl,
                                                          float* __restrict__ adv,
-                                                         float* __restrict__ ret) {
+                                                         float* __restrict__ ret,
+                                                         const float* __restrict__ lp,
+                                                         const int64_t* __restrict__ act,
+                                                         float4* __restrict__ rec) {
   const int64_t n = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (n >= N) return;
   float last = 0.f, carry_v = next_val[n], carry_d = next_done[n];
@@ -211,6 +234,7 @@ __global__ __launch_bounds__(256) void gae_stream_kernel(const float* __restrict
         const size_t gi = static_cast<size_t>(t_hi - 1 - k) * N + n;
         adv[gi] = r[k];
         ret[gi] = r[k] + v[k];
+        if (rec) gae_put_record(rec, gi, lp[gi], r[k], r[k] + v[k], v[k], act[gi]);
       }
     }
   }
@@ -220,10 +244,11 @@ __global__ __launch_bounds__(256) void gae_stream_kernel(const float* __restrict
 
 using namespace ocppo;
 
-extern "C" int ocppo_gae(ocppo_stream_t stream, const float* rewards, const float* values,
-                         const float* dones, const float* next_value, const float* next_done,
-                         int64_t T, int64_t N, double gamma, double gae_lambda, float* advantages,
-                         float* returns) {
+static int gae_launch(ocppo_stream_t stream, const float* rewards, const float* values,
+                      const float* dones, const float* next_value, const float* next_done,
+                      int64_t T, int64_t N, double gamma, double gae_lambda, float* advantages,
+                      float* returns, const float* logprobs, const int64_t* actions,
+                      void* records) {
   OCPPO_REQUIRE(T >= 0 && N >= 0 && T <= INT32_MAX, "ocppo_gae: bad sizes T=%lld N=%lld",
                 (long long)T, (long long)N);
   if (T == 0 || N == 0) return OCPPO_OK;
@@ -238,14 +263,15 @@ extern "C" int ocppo_gae(ocppo_stream_t stream, const float* rewards, const floa
   if (N >= 64 * 1024) {
     hipLaunchKernelGGL(gae_stream_kernel<2>, dim3(ceil_div(N, 256)), dim3(256), 0, s, rewards,
                        values, dones, next_value, next_done, (int)T, N, g, gl, advantages,
-                       returns);
+                       returns, logprobs, actions, static_cast<float4*>(records));
   } else {
     // >= 64 workgroups where N allows it: E = 4 envs per workgroup up to N = 256, then wider
     const int TC = T < 128 ? (int)T : 128;
 #define OCPPO_GAE_TILE(E)                                                                          \
   hipLaunchKernelGGL(gae_tile_kernel<E>, dim3(ceil_div(N, E)), dim3(256),                         \
                      4 * sizeof(float) * TC * (E), s, rewards, values, dones, next_value,          \
-                     next_done, (int)T, N, TC, g, gl, advantages, returns)
+                     next_done, (int)T, N, TC, g, gl, advantages, returns, logprobs, actions,      \
+                     static_cast<float4*>(records))
 #ifdef OCPPO_GAE_E  // tile-width variants (tools/)
     if (N <= 1024) OCPPO_GAE_TILE(OCPPO_GAE_E);
     else
@@ -256,4 +282,24 @@ extern "C" int ocppo_gae(ocppo_stream_t stream, const float* rewards, const floa
 #undef OCPPO_GAE_TILE
   }
   return check_launch("ocppo_gae");
+}
+
+extern "C" int ocppo_gae(ocppo_stream_t stream, const float* rewards, const float* values,
+                         const float* dones, const float* next_value, const float* next_done,
+                         int64_t T, int64_t N, double gamma, double gae_lambda, float* advantages,
+                         float* returns) {
+  return gae_launch(stream, rewards, values, dones, next_value, next_done, T, N, gamma,
+                    gae_lambda, advantages, returns, nullptr, nullptr, nullptr);
+}
+
+extern "C" int ocppo_gae_records(ocppo_stream_t stream, const float* rewards, const float* values,
+                                 const float* dones, const float* next_value,
+                                 const float* next_done, int64_t T, int64_t N, double gamma,
+                                 double gae_lambda, float* advantages, float* returns,
+                                 const float* logprobs, const int64_t* actions, void* records) {
+  OCPPO_REQUIRE(logprobs && actions && records && reinterpret_cast<uintptr_t>(records) % 32 == 0 &&
+                    reinterpret_cast<uintptr_t>(logprobs) % 16 == 0,
+                "ocppo_gae_records: logprobs (16-B aligned), actions and 32-B aligned records");
+  return gae_launch(stream, rewards, values, dones, next_value, next_done, T, N, gamma,
+                    gae_lambda, advantages, returns, logprobs, actions, records);
 }

@@ -121,7 +121,9 @@ __device__ __forceinline__ void categorical_backward_loss(const float (&ln)[AMAX
 // ocppo_minibatch_adv_stats and the statistics blocks of ocppo_minibatch_prepare, so the two
 // give bitwise-identical figures.
 constexpr int kStatsThreads = 256;
-template <int VPT>
+// STRIDE: floats between consecutive samples' advantages (1: the b_adv array; 8: the advantage
+// field of the 32-B sample records of ocppo_gae_records)
+template <int VPT, int STRIDE = 1>
 __device__ __forceinline__ void adv_stats_block(const float* __restrict__ adv,
                                                 const int64_t* __restrict__ perm, int64_t M,
                                                 int64_t mb, float* __restrict__ out,
@@ -135,7 +137,7 @@ __device__ __forceinline__ void adv_stats_block(const float* __restrict__ adv,
     idx[k] = i < M ? (perm ? perm[base + i] : base + i) : -1;
   }
 #pragma unroll
-  for (int k = 0; k < VPT; ++k) x[k] = idx[k] >= 0 ? adv[idx[k]] : 0.f;
+  for (int k = 0; k < VPT; ++k) x[k] = idx[k] >= 0 ? adv[idx[k] * STRIDE] : 0.f;
   float s = 0.f;
 #pragma unroll
   for (int k = 0; k < VPT; ++k) s += x[k];
@@ -156,18 +158,20 @@ __device__ __forceinline__ void adv_stats_block(const float* __restrict__ adv,
 }
 
 // Any M: strided loops, values re-gathered for the second pass.
+template <int STRIDE = 1>
 __device__ __forceinline__ void adv_stats_block_any(const float* __restrict__ adv,
                                                     const int64_t* __restrict__ perm, int64_t M,
                                                     int64_t mb, float* __restrict__ out,
                                                     float* scratch) {
   const int64_t base = mb * M;
   float s = 0.f;
-  for (int64_t i = threadIdx.x; i < M; i += kStatsThreads) s += adv[perm ? perm[base + i] : base + i];
+  for (int64_t i = threadIdx.x; i < M; i += kStatsThreads)
+    s += adv[(perm ? perm[base + i] : base + i) * STRIDE];
   s = block_sum(s, scratch);
   const float mean = s / static_cast<float>(M);
   float q = 0.f;
   for (int64_t i = threadIdx.x; i < M; i += kStatsThreads) {
-    const float d = adv[perm ? perm[base + i] : base + i] - mean;
+    const float d = adv[(perm ? perm[base + i] : base + i) * STRIDE] - mean;
     q += d * d;
   }
   q = block_sum(q, scratch);
@@ -178,14 +182,14 @@ __device__ __forceinline__ void adv_stats_block_any(const float* __restrict__ ad
 }
 
 // VPT = 0: the strided form
-template <int VPT>
+template <int VPT, int STRIDE = 1>
 __device__ __forceinline__ void adv_stats_any_vpt(const float* adv, const int64_t* perm,
                                                   int64_t M, int64_t mb, float* out,
                                                   float* scratch) {
   if constexpr (VPT == 0)
-    adv_stats_block_any(adv, perm, M, mb, out, scratch);
+    adv_stats_block_any<STRIDE>(adv, perm, M, mb, out, scratch);
   else
-    adv_stats_block<VPT>(adv, perm, M, mb, out, scratch);
+    adv_stats_block<VPT, STRIDE>(adv, perm, M, mb, out, scratch);
 }
 
 inline int adv_stats_vpt(int64_t M) {
@@ -263,6 +267,51 @@ __global__ __launch_bounds__(256) void minibatch_prepare_kernel(
       mb_adv[i] = ad[k];
       mb_ret[i] = rt[k];
       mb_val[i] = vl[k];
+    }
+  }
+}
+
+// The same from the 32-B sample records of ocppo_gae_records ({log-prob, advantage, return,
+// value, action i64, pad}): one 32-B gather per sample (both halves of it are one 64-B sector)
+// instead of five scattered 4-8 B ones; same values, same order, so the statistics and the SoA
+// outputs are bitwise those of minibatch_prepare_kernel.
+template <int VPT, int SVPT>
+__global__ __launch_bounds__(256) void minibatch_prepare_rec_kernel(
+    const int64_t* __restrict__ perm, int64_t n, int gather_blocks, int64_t M,
+    const float4* __restrict__ rec, int64_t* __restrict__ mb_act, float* __restrict__ mb_lp,
+    float* __restrict__ mb_adv, float* __restrict__ mb_ret, float* __restrict__ mb_val,
+    float* __restrict__ stats) {
+  const int nstat = stats ? static_cast<int>(gridDim.x) - gather_blocks : 0;
+  if (static_cast<int>(blockIdx.x) < nstat) {
+    __shared__ float scratch[kStatsThreads / kWave];
+    adv_stats_any_vpt<SVPT, 8>(reinterpret_cast<const float*>(rec) + 1, perm, M, blockIdx.x,
+                               stats, scratch);
+    return;
+  }
+  const int64_t base = static_cast<int64_t>(blockIdx.x - nstat) * 256 * VPT + threadIdx.x;
+  int64_t idx[VPT];
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int64_t i = base + k * 256;
+    idx[k] = i < n ? perm[i] : -1;
+  }
+  float4 r0[VPT], r1[VPT];
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int64_t b = idx[k] >= 0 ? idx[k] : 0;
+    r0[k] = rec[2 * b];
+    r1[k] = rec[2 * b + 1];
+  }
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int64_t i = base + k * 256;
+    if (idx[k] >= 0) {
+      mb_act[i] = static_cast<int64_t>(static_cast<uint32_t>(__float_as_int(r1[k].x))) |
+                  (static_cast<int64_t>(__float_as_int(r1[k].y)) << 32);
+      mb_lp[i] = r0[k].x;
+      mb_adv[i] = r0[k].y;
+      mb_ret[i] = r0[k].z;
+      mb_val[i] = r0[k].w;
     }
   }
 }
@@ -1181,6 +1230,40 @@ extern "C" int ocppo_minibatch_prepare(ocppo_stream_t stream, const int64_t* per
   }
 #undef OCPPO_PREP
   return check_launch("ocppo_minibatch_prepare");
+}
+
+extern "C" int ocppo_minibatch_prepare_records(ocppo_stream_t stream, const int64_t* perm,
+                                               int64_t M, int64_t num_mb, const void* records,
+                                               int64_t* mb_actions, float* mb_logprobs,
+                                               float* mb_advantages, float* mb_returns,
+                                               float* mb_values, float* adv_stats) {
+  OCPPO_REQUIRE(M > 0 && num_mb > 0 && num_mb <= INT32_MAX && M <= INT64_MAX / num_mb,
+                "ocppo_minibatch_prepare_records: bad sizes M=%lld num_mb=%lld", (long long)M,
+                (long long)num_mb);
+  OCPPO_REQUIRE(perm && records && mb_actions && mb_logprobs && mb_advantages && mb_returns &&
+                    mb_values && reinterpret_cast<uintptr_t>(records) % 32 == 0,
+                "ocppo_minibatch_prepare_records: null pointer or records not 32-B aligned");
+  clear_stale_error();
+  hipStream_t s = as_stream(stream);
+  constexpr int VPT = 4;
+  const int64_t n = M * num_mb;
+  const int64_t gb = ceil_div(n, 256 * VPT);
+  OCPPO_REQUIRE(gb + num_mb <= INT32_MAX, "ocppo_minibatch_prepare_records: too large");
+  const dim3 grid(static_cast<unsigned>(gb + (adv_stats ? num_mb : 0))), block(256);
+  const float4* rec = static_cast<const float4*>(records);
+#define OCPPO_PREP(SV)                                                                           \
+  hipLaunchKernelGGL((minibatch_prepare_rec_kernel<VPT, SV>), grid, block, 0, s, perm, n, (int)gb, \
+                     M, rec, mb_actions, mb_logprobs, mb_advantages, mb_returns, mb_values,      \
+                     adv_stats)
+  switch (adv_stats_vpt(M)) {
+    case 1: OCPPO_PREP(1); break;
+    case 4: OCPPO_PREP(4); break;
+    case 16: OCPPO_PREP(16); break;
+    case 64: OCPPO_PREP(64); break;
+    default: OCPPO_PREP(0); break;
+  }
+#undef OCPPO_PREP
+  return check_launch("ocppo_minibatch_prepare_records");
 }
 
 namespace ocppo {

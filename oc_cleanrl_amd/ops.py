@@ -75,11 +75,13 @@ def _stream(device: torch.device) -> int:
 # GAE (ppo_atari_oc.py:533-547)
 # ---------------------------------------------------------------------------------------------
 def gae(rewards, values, dones, next_value, next_done, gamma: float, gae_lambda: float,
-        advantages=None, returns=None):
+        advantages=None, returns=None, logprobs=None, actions=None, records=None):
     """Advantages and returns of one rollout; [T, N] f32 in, ([T, N], [T, N]) out.
 
     Bit-identical to the reference loop. `next_value` may be [N] or [1, N] (as produced by
-    `agent.get_value(next_obs).reshape(1, -1)`).
+    `agent.get_value(next_obs).reshape(1, -1)`). records (with logprobs [T, N] f32 and actions
+    [T, N] i64): also write each sample's 32-B record (sample_records) for
+    minibatch_prepare(records=...).
     """
     if rewards.dim() != 2:
         raise ValueError(f"rewards must be [T, N], got {tuple(rewards.shape)}")
@@ -90,12 +92,24 @@ def gae(rewards, values, dones, next_value, next_done, gamma: float, gae_lambda:
         advantages = torch.empty_like(rewards)
     if returns is None:
         returns = torch.empty_like(rewards)
-    call("ocppo_gae", _stream(dev), _check(rewards, "rewards", f, dev),
-         _check(values, "values", f, dev, T * N), _check(dones, "dones", f, dev, T * N),
-         _check(next_value, "next_value", f, dev, N), _check(next_done, "next_done", f, dev, N),
-         T, N, float(gamma), float(gae_lambda), _check(advantages, "advantages", f, dev, T * N),
-         _check(returns, "returns", f, dev, T * N))
+    args = (_check(rewards, "rewards", f, dev),
+            _check(values, "values", f, dev, T * N), _check(dones, "dones", f, dev, T * N),
+            _check(next_value, "next_value", f, dev, N), _check(next_done, "next_done", f, dev, N),
+            T, N, float(gamma), float(gae_lambda), _check(advantages, "advantages", f, dev, T * N),
+            _check(returns, "returns", f, dev, T * N))
+    if records is None:
+        call("ocppo_gae", _stream(dev), *args)
+    else:
+        call("ocppo_gae_records", _stream(dev), *args,
+             _check(logprobs, "logprobs", f, dev, T * N),
+             _check(actions, "actions", torch.int64, dev, T * N),
+             _check(records, "records", torch.int64, dev, 4 * T * N))
     return advantages, returns
+
+
+def sample_records(B: int, device):
+    """[B] x 32-B per-sample records (ocppo.h OcppoSampleRecord) as an int64 [B, 4] tensor."""
+    return torch.zeros((B, 4), dtype=torch.int64, device=device)
 
 
 # ---------------------------------------------------------------------------------------------
@@ -117,8 +131,10 @@ def minibatch_adv_stats(b_advantages, perm, minibatch_size: int, out=None):
 
 
 def minibatch_prepare(perm, minibatch_size: int, b_actions, b_logprobs, b_advantages, b_returns,
-                      b_values, out: dict | None = None, with_stats: bool = True):
+                      b_values, out: dict | None = None, with_stats: bool = True, records=None):
     """Gather every minibatch's per-sample arrays into minibatch order (+ adv stats).
+    records: the 32-B per-sample records of gae(records=...) gathered instead of the five b_*
+    arrays (then only their sizes are read; bitwise the same outputs).
 
     Returns dict(actions, logprobs, advantages, returns, values: [num_mb*M], adv_stats [num_mb,2])."""
     dev = perm.device
@@ -129,6 +145,22 @@ def minibatch_prepare(perm, minibatch_size: int, b_actions, b_logprobs, b_advant
     num_mb = n // M
     B = b_logprobs.numel()
     f = torch.float32
+    if records is not None:
+        if out is None:
+            out = {"actions": torch.empty(n, dtype=torch.int64, device=dev),
+                   **{k: torch.empty(n, dtype=f, device=dev)
+                      for k in ("logprobs", "advantages", "returns", "values")},
+                   "adv_stats": torch.empty((num_mb, 2), dtype=f, device=dev)}
+        call("ocppo_minibatch_prepare_records", _stream(dev),
+             _check(perm, "perm", torch.int64, dev), M, num_mb,
+             _check(records, "records", torch.int64, dev, 4 * B),
+             _check(out["actions"], "mb_actions", torch.int64, dev, n),
+             _check(out["logprobs"], "mb_logprobs", f, dev, n),
+             _check(out["advantages"], "mb_advantages", f, dev, n),
+             _check(out["returns"], "mb_returns", f, dev, n),
+             _check(out["values"], "mb_values", f, dev, n),
+             _check(out["adv_stats"], "adv_stats", f, dev, 2 * num_mb) if with_stats else None)
+        return out
     if out is None:
         out = {"actions": torch.empty(n, dtype=torch.int64, device=dev),
                **{k: torch.empty(n, dtype=f, device=dev)

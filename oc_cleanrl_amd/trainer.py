@@ -397,6 +397,8 @@ class PPOTrainer:
                         if self.fused_heads_loss else None)
         self.b_obs = self.obs[:T].view((T * N,) + self.obs_shape)
         self.wplanes, self.wplanes_built = None, False  # built at the first minibatch
+        # GAE's per-sample records for the minibatch gather (ops.sample_records)
+        self.records = ops.sample_records(self.B, dev) if a.sample_records else None
 
         # Every update is captured, the NatureCNN's MIOpen convolutions included (round 1 ran that
         # one eagerly after a capture_end crash that no longer reproduces: tools/exp_c3_capture.py
@@ -602,19 +604,24 @@ class PPOTrainer:
                                                   self._policy_hidden(T)).view(-1))
         else:
             self.values[T].copy_(self.agent.get_value(self.net_obs, self.prescale).view(-1))
+        rec = self.records
         self.timer.bracket("gae", lambda: ops.gae(
             self.rewards, self.values[:T], self.dones[:T], self.values[T], self.dones[T],
-            a.gamma, a.gae_lambda, self.advantages, self.returns))
-        self._prepare_minibatches()
+            a.gamma, a.gae_lambda, self.advantages, self.returns, logprobs=self.logprobs,
+            actions=self.actions, records=rec))
+        self._prepare_minibatches(from_records=rec is not None)
 
-    def _prepare_minibatches(self):
+    def _prepare_minibatches(self, from_records: bool = False):
         """Every minibatch's per-sample records in minibatch order + its adv (mean, std)
-        (:566-579: b_*[mb_inds] and the minibatch advantage statistics)."""
+        (:566-579: b_*[mb_inds] and the minibatch advantage statistics). from_records: gather
+        the 32-B sample records this iteration's GAE wrote (one gather per sample instead of
+        five; bitwise the same outputs)."""
         T = self.T
+        rec = self.records if from_records else None
         self.timer.bracket("mb_prepare", lambda: ops.minibatch_prepare(
             self.perm_dev, self.M, self.actions.view(-1), self.logprobs.view(-1),
             self.advantages.view(-1), self.returns.view(-1), self.values[:T].reshape(-1),
-            out=self.mb, with_stats=self.args.norm_adv))
+            out=self.mb, with_stats=self.args.norm_adv, records=rec))
 
     def _rollout(self):
         """Rollout (:500-530) + bootstrap + GAE (:533-547) + minibatch adv stats (:577-579)."""

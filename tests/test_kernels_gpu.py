@@ -1372,3 +1372,48 @@ def test_heads_loss_rejects_uninstantiated_widths(ops, dev, H):
 
     tr = PPOTrainer(small_args(decoder_dims=(H,)), dev)
     assert not tr.fused_heads_loss
+
+
+@pytest.mark.parametrize("T_,N", [(7, 5), (128, 128), (200, 130), (33, 1030), (128, 4096),
+                                  (16, 65540)])
+def test_gae_records_are_the_arrays(ops, dev, T_, N):
+    """ocppo_gae_records: advantages / returns bitwise those of ocppo_gae (every tile width and
+    the streaming form), and each sample's 32-B record holds exactly its log-prob, advantage,
+    return, value and action."""
+    g = torch.Generator(device=dev).manual_seed(T_ * 31 + N)
+    r = torch.randn(T_, N, device=dev, generator=g)
+    v = torch.randn(T_, N, device=dev, generator=g)
+    d = (torch.rand(T_, N, device=dev, generator=g) < 0.1).float()
+    nv, nd = torch.randn(N, device=dev, generator=g), torch.zeros(N, device=dev)
+    lp = torch.randn(T_, N, device=dev, generator=g)
+    act = torch.randint(-3, 1 << 40, (T_, N), device=dev, generator=g)
+    a0, r0 = ops.gae(r, v, d, nv, nd, 0.99, 0.95)
+    rec = ops.sample_records(T_ * N, dev)
+    a1, r1 = ops.gae(r, v, d, nv, nd, 0.99, 0.95, logprobs=lp, actions=act, records=rec)
+    torch.cuda.synchronize()
+    assert torch.equal(a0, a1) and torch.equal(r0, r1)
+    f = rec.view(torch.float32).view(T_ * N, 8)
+    assert torch.equal(f[:, 0], lp.view(-1)) and torch.equal(f[:, 1], a1.view(-1))
+    assert torch.equal(f[:, 2], r1.view(-1)) and torch.equal(f[:, 3], v.view(-1))
+    assert torch.equal(rec[:, 2], act.view(-1))
+
+
+@pytest.mark.parametrize("M,nmb,B", [(4096, 16, 16384), (100, 7, 700), (16384, 4, 65536)])
+def test_minibatch_prepare_from_records_is_bitwise_the_soa_form(ops, dev, M, nmb, B):
+    g = torch.Generator(device=dev).manual_seed(M + nmb)
+    T_ = 4 if B % 4 == 0 else 1
+    acts = torch.randint(0, 6, (B,), device=dev, generator=g)
+    lp, bv = torch.randn(B, device=dev, generator=g), torch.randn(B, device=dev, generator=g)
+    adv, ret = torch.empty(B, device=dev), torch.empty(B, device=dev)
+    z = torch.zeros(B // T_, device=dev)
+    rec = ops.sample_records(B, dev)
+    ops.gae(torch.randn(T_, B // T_, device=dev, generator=g), bv.view(T_, -1),
+            torch.zeros(T_, B // T_, device=dev), z, z, 0.99, 0.95, adv.view(T_, -1),
+            ret.view(T_, -1), logprobs=lp.view(T_, -1), actions=acts.view(T_, -1), records=rec)
+    reps = (nmb * M + B - 1) // B
+    perm = torch.cat([torch.randperm(B, device=dev, generator=g) for _ in range(reps)])[:nmb * M]
+    a = ops.minibatch_prepare(perm, M, acts, lp, adv, ret, bv)
+    b = ops.minibatch_prepare(perm, M, acts, lp, adv, ret, bv, records=rec)
+    torch.cuda.synchronize()
+    for k in a:
+        assert torch.equal(a[k], b[k]), k

@@ -30,7 +30,10 @@ MFMA_F32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense f32 MFMA (= the f32 v
 
 SIZES = {
     # name: {size: params}
+    # GAE as the trainer runs it: advantages / returns + the 32-B sample records (ops.gae with
+    # records); gae_plain without the records
     "gae": {"config": dict(T=128, N=128), "scaled": dict(T=128, N=262144)},
+    "gae_plain": {"config": dict(T=128, N=128), "scaled": dict(T=128, N=262144)},
     "ppo_loss": {"config": dict(M=4096, A=6, B=16384), "scaled": dict(M=4 * 1024 * 1024, A=6, B=4 * 1024 * 1024)},
     "gather": {"config": dict(M=4096, B=16384, R=48), "scaled": dict(M=1 << 20, B=1 << 20, R=48)},
     # config-3 minibatch gather: u8 frame stacks -> f32 NHWC (NatureCNN input, 8192 rows)
@@ -40,6 +43,8 @@ SIZES = {
     "env_step": {"config": dict(N=128, D=12), "scaled": dict(N=4 * 1024 * 1024, D=12)},
     "adv_stats": {"config": dict(M=4096, nmb=16, B=16384), "scaled": dict(M=16384, nmb=256, B=1 << 20)},
     "mb_prepare": {"config": dict(M=4096, nmb=16, B=16384), "scaled": dict(M=16384, nmb=256, B=1 << 20)},
+    # the same from the five SoA arrays (the form before GAE packed 32-B sample records)
+    "mb_prepare_soa": {"config": dict(M=4096, nmb=16, B=16384), "scaled": dict(M=16384, nmb=256, B=1 << 20)},
     "ppo_loss_prepared": {"config": dict(M=4096, A=6), "scaled": dict(M=4 * 1024 * 1024, A=6)},
     "policy_head": {"config": dict(N=128, H=512, A=6), "scaled": dict(N=262144, H=512, A=6)},
     # the two Linear->ReLU backward launches of one config-2 minibatch (dedup capacity 11520
@@ -98,7 +103,9 @@ def case_bytes(name: str, p: dict) -> float:
     tools/summarize_profiles.py prices the PMC passes with the same numbers). ppo_loss gathers its
     records through the minibatch indices (8A+32 B per element + the 4-B index); the prepared
     form reads them contiguous (8A+32)."""
-    if name == "gae":
+    if name == "gae":  # + log-prob 4 + action 8 in, the 32-B record out
+        return 64 * p["T"] * p["N"] + 8 * p["N"]
+    if name == "gae_plain":
         return 20 * p["T"] * p["N"] + 8 * p["N"]
     if name == "ppo_loss":
         return (8 * p["A"] + 36) * p["M"]
@@ -117,7 +124,7 @@ def case_bytes(name: str, p: dict) -> float:
         return p["N"] * (8 + p["D"] * 4 + 8 + 2 * 20)
     if name == "adv_stats":
         return 2 * p["nmb"] * p["M"] * 12
-    if name == "mb_prepare":
+    if name in ("mb_prepare", "mb_prepare_soa"):
         return p["nmb"] * p["M"] * (8 + 2 * (8 + 16))
     if name == "policy_head":
         N, H, A = p["N"], p["H"], p["A"]
@@ -156,7 +163,7 @@ def make_case(name: str, p: dict, dev):
     """Returns (launch closure, algorithmic bytes per launch)."""
     g = torch.Generator(device=dev).manual_seed(0)
     f32 = torch.float32
-    if name == "gae":
+    if name == "gae_plain":
         T, N = p["T"], p["N"]
         r = torch.randn(T, N, device=dev, generator=g)
         v = torch.randn(T, N, device=dev, generator=g)
@@ -164,6 +171,18 @@ def make_case(name: str, p: dict, dev):
         nv, nd = torch.randn(N, device=dev, generator=g), torch.zeros(N, device=dev)
         adv, ret = torch.empty_like(r), torch.empty_like(r)
         return (lambda: ops.gae(r, v, d, nv, nd, 0.99, 0.95, adv, ret)), 20 * T * N + 8 * N
+    if name == "gae":
+        T, N = p["T"], p["N"]
+        r = torch.randn(T, N, device=dev, generator=g)
+        v = torch.randn(T, N, device=dev, generator=g)
+        d = (torch.rand(T, N, device=dev, generator=g) < 0.01).float()
+        nv, nd = torch.randn(N, device=dev, generator=g), torch.zeros(N, device=dev)
+        lp = torch.randn(T, N, device=dev, generator=g)
+        act = torch.randint(0, 6, (T, N), device=dev, generator=g)
+        rec = ops.sample_records(T * N, dev)
+        adv, ret = torch.empty_like(r), torch.empty_like(r)
+        return (lambda: ops.gae(r, v, d, nv, nd, 0.99, 0.95, adv, ret, logprobs=lp, actions=act,
+                                records=rec)), 64 * T * N + 8 * N
     if name == "ppo_loss":
         M, A, B = p["M"], p["A"], p["B"]
         logits = torch.randn(M, A, device=dev, generator=g)
@@ -225,14 +244,26 @@ def make_case(name: str, p: dict, dev):
         perm = torch.cat([torch.randperm(B, device=dev, generator=g) for _ in range(reps)])[:nmb * M]
         out = torch.empty(nmb, 2, device=dev)
         return (lambda: ops.minibatch_adv_stats(adv, perm, M, out)), 2 * nmb * M * 12
-    if name == "mb_prepare":
+    if name in ("mb_prepare", "mb_prepare_soa"):
+        # mb_prepare: the trainer's form, from GAE's 32-B sample records (the records are made
+        # here by ops.gae on a [T, B / T] rollout of the same arrays)
         M, nmb, B = p["M"], p["nmb"], p["B"]
         reps = (nmb * M + B - 1) // B
         perm = torch.cat([torch.randperm(B, device=dev, generator=g) for _ in range(reps)])[:nmb * M]
         acts = torch.randint(0, 6, (B,), device=dev, generator=g)
         lp, adv, ret, bv = (torch.randn(B, device=dev, generator=g) for _ in range(4))
-        out = ops.minibatch_prepare(perm, M, acts, lp, adv, ret, bv)
-        fn = lambda: ops.minibatch_prepare(perm, M, acts, lp, adv, ret, bv, out=out)  # noqa: E731
+        rec = None
+        if name == "mb_prepare":
+            T = 128
+            rec = ops.sample_records(B, dev)
+            z = torch.zeros(B // T, device=dev)
+            ops.gae(torch.randn(T, B // T, device=dev, generator=g), bv.view(T, -1),
+                    torch.zeros(T, B // T, device=dev), z, z, 0.99, 0.95, adv.view(T, -1),
+                    ret.view(T, -1), logprobs=lp.view(T, -1), actions=acts.view(T, -1),
+                    records=rec)
+        out = ops.minibatch_prepare(perm, M, acts, lp, adv, ret, bv, records=rec)
+        fn = lambda: ops.minibatch_prepare(perm, M, acts, lp, adv, ret, bv, out=out,  # noqa: E731
+                                           records=rec)
         return fn, nmb * M * (8 + 2 * (8 + 16))
     if name == "ppo_loss_prepared":
         M, A = p["M"], p["A"]

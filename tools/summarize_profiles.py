@@ -33,7 +33,9 @@ KERNEL_SUBSTR = {
     "relu_bias_wgrad": ("relu_bias_wgrad_rows_kernel", "relu_bias_wgrad_finish_kernel"),
     "heads_bwd": ("heads_bwd_kernel",),
     "heads_loss": ("heads_loss_kernel", "heads_loss_finish_kernel"),
-    "mb_prepare": ("minibatch_prepare_kernel",),
+    "mb_prepare": ("minibatch_prepare",),  # the records form (minibatch_prepare_rec_kernel)
+    "mb_prepare_soa": ("minibatch_prepare_kernel",),
+    "gae_plain": ("ocppo::gae",),
     "cache_linear": ("linear_rows_kernel",),
     "store_encode": ("store_linear2_kernel",),
     "decoder": ("linear_rows_kernel",),
