@@ -64,8 +64,8 @@ def kernel_bytes(tr) -> dict:
     fb = tr.env.frame.element_size()
     kb = {
         # read r, v, d [T,N] + next v/d [N]; write adv, ret [T,N] (+ with the sample records:
-        # log-prob 4 + action 8 in, the 32-B record out)
-        "gae": (64 if tr.records is not None else 20) * T * N + 8 * N,
+        # log-prob 4 + action 8 in, the 16-B record out)
+        "gae": (48 if tr.records is not None else 20) * T * N + 8 * N,
         # logits 4A + value 4 + action 8 + old logprob/adv/return/value 16 in (contiguous,
         # prepared); dlogits 4A + dv 4 out
         "ppo_loss": (8 * A + 32) * M,

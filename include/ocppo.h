@@ -81,10 +81,10 @@ OCPPO_API const char* ocppo_last_error(void);
 OCPPO_API int ocppo_gae(ocppo_stream_t stream, const float* rewards, const float* values, const float* dones,
               const float* next_value, const float* next_done, int64_t T, int64_t N, double gamma,
               double gae_lambda, float* advantages, float* returns);
-/* GAE that also writes each sample's record (OcppoSampleRecord: log-prob, advantage, return,
- * value, action) in batch order for ocppo_minibatch_prepare_records; advantages / returns as
- * ocppo_gae, bit for bit. logprobs [T, N] f32 16-B aligned, actions [T, N] int64, records [T*N]
- * 32-B aligned. */
+/* GAE that also writes each sample's record (OcppoSampleRecord: log-prob, advantage, value,
+ * action) in batch order for ocppo_minibatch_prepare_records; advantages / returns as ocppo_gae,
+ * bit for bit. logprobs [T, N] f32 16-B aligned, actions [T, N] int64 in [0, 2^31), records
+ * [T*N] 16-B aligned. */
 OCPPO_API int ocppo_gae_records(ocppo_stream_t stream, const float* rewards, const float* values,
                                 const float* dones, const float* next_value,
                                 const float* next_done, int64_t T, int64_t N, double gamma,
@@ -116,15 +116,15 @@ OCPPO_API int ocppo_minibatch_prepare(ocppo_stream_t stream, const int64_t* perm
                                       float* adv_stats);
 
 /* ---------------------------------------------------------------------------------------------
- * The same, from 32-B per-sample records (OcppoSampleRecord, written by ocppo_gae_records): one
- * 32-B gather per sample instead of five scattered 4-8 B ones (the batch arrays of
- * ppo_atari_oc.py:550-555 are the records' fields); outputs and statistics bitwise those of
- * ocppo_minibatch_prepare. records: 32-B aligned, [B].
+ * The same, from 16-B per-sample records (OcppoSampleRecord, written by ocppo_gae_records): one
+ * 16-B gather per sample instead of five scattered 4-8 B ones (the batch arrays of
+ * ppo_atari_oc.py:550-555 are the records' fields; the return is advantage + value, GAE's own f32
+ * add); outputs and statistics bitwise those of ocppo_minibatch_prepare. records: 16-B aligned,
+ * [B]; actions in [0, 2^31).
  * ------------------------------------------------------------------------------------------- */
 typedef struct {
-  float logprob, advantage, ret, value;
-  int64_t action;
-  int64_t pad;
+  float logprob, advantage, value;
+  int32_t action;
 } OcppoSampleRecord;
 OCPPO_API int ocppo_minibatch_prepare_records(ocppo_stream_t stream, const int64_t* perm,
                                               int64_t M, int64_t num_mb, const void* records,

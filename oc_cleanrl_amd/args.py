@@ -126,7 +126,7 @@ class Args:
                                   # generator stream) instead of once per rollout ([T, N, A])
     fused_heads_loss: bool = True  # update: policy heads fwd + PPO loss + heads bwd in one HIP op
     dp_overlap: bool = True  # DP: all-reduce the decoder-side gradients during the encoder backward
-    sample_records: bool = True  # GAE also packs each sample's 32-B record; the minibatch gather
+    sample_records: bool = True  # GAE also packs each sample's 16-B record; the minibatch gather
                                  # reads one record per sample instead of five arrays
     dp_graph_collectives: bool = False  # DP: capture each epoch's minibatches WITH their RCCL
                                         # all-reduces in one hipGraph (else one graph per phase,

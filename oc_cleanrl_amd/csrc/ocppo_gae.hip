@@ -24,12 +24,11 @@
 namespace ocppo {
 
 // The per-sample record ocppo_minibatch_prepare_records gathers (ocppo.h OcppoSampleRecord): one
-// 32-B line fragment per sample instead of five scattered 4-8 B values.
+// 16-B load per sample instead of five scattered 4-8 B values. The return is not stored: it is
+// advantage + value, recomputed by the gather with the same f32 add (bitwise the same).
 __device__ __forceinline__ void gae_put_record(float4* __restrict__ rec, size_t gi, float lp,
-                                               float a, float r, float v, int64_t act) {
-  rec[2 * gi] = make_float4(lp, a, r, v);
-  rec[2 * gi + 1] = make_float4(__int_as_float(static_cast<int>(act & 0xffffffff)),
-                                __int_as_float(static_cast<int>(act >> 32)), 0.f, 0.f);
+                                               float a, float v, int64_t act) {
+  rec[gi] = make_float4(lp, a, v, __int_as_float(static_cast<int>(act)));
 }
 
 // The recurrence over rows rows-1 .. 0 of env column `tid` of an E-wide LDS tile (delta in sa,
@@ -159,10 +158,10 @@ __global__ __launch_bounds__(256) void gae_tile_kernel(const float* __restrict__
           *reinterpret_cast<float4*>(ret + gi) = r;
           if (rec) {
             const float4 l = *reinterpret_cast<const float4*>(lp + gi);
-            gae_put_record(rec, gi, l.x, a.x, r.x, v.x, act[gi]);
-            gae_put_record(rec, gi + 1, l.y, a.y, r.y, v.y, act[gi + 1]);
-            gae_put_record(rec, gi + 2, l.z, a.z, r.z, v.z, act[gi + 2]);
-            gae_put_record(rec, gi + 3, l.w, a.w, r.w, v.w, act[gi + 3]);
+            gae_put_record(rec, gi, l.x, a.x, v.x, act[gi]);
+            gae_put_record(rec, gi + 1, l.y, a.y, v.y, act[gi + 1]);
+            gae_put_record(rec, gi + 2, l.z, a.z, v.z, act[gi + 2]);
+            gae_put_record(rec, gi + 3, l.w, a.w, v.w, act[gi + 3]);
           }
         }
       }
@@ -174,7 +173,7 @@ __global__ __launch_bounds__(256) void gae_tile_kernel(const float* __restrict__
           const size_t gi = static_cast<size_t>(t_lo + row) * N + col;
           adv[gi] = sa[e];
           ret[gi] = sa[e] + sv[e];
-          if (rec) gae_put_record(rec, gi, lp[gi], sa[e], sa[e] + sv[e], sv[e], act[gi]);
+          if (rec) gae_put_record(rec, gi, lp[gi], sa[e], sv[e], act[gi]);
         }
       }
     }
@@ -234,7 +233,7 @@ __global__ __launch_bounds__(256) void gae_stream_kernel(const float* __restrict
         const size_t gi = static_cast<size_t>(t_hi - 1 - k) * N + n;
         adv[gi] = r[k];
         ret[gi] = r[k] + v[k];
-        if (rec) gae_put_record(rec, gi, lp[gi], r[k], r[k] + v[k], v[k], act[gi]);
+        if (rec) gae_put_record(rec, gi, lp[gi], r[k], v[k], act[gi]);
       }
     }
   }
@@ -297,9 +296,9 @@ extern "C" int ocppo_gae_records(ocppo_stream_t stream, const float* rewards, co
                                  const float* next_done, int64_t T, int64_t N, double gamma,
                                  double gae_lambda, float* advantages, float* returns,
                                  const float* logprobs, const int64_t* actions, void* records) {
-  OCPPO_REQUIRE(logprobs && actions && records && reinterpret_cast<uintptr_t>(records) % 32 == 0 &&
+  OCPPO_REQUIRE(logprobs && actions && records && reinterpret_cast<uintptr_t>(records) % 16 == 0 &&
                     reinterpret_cast<uintptr_t>(logprobs) % 16 == 0,
-                "ocppo_gae_records: logprobs (16-B aligned), actions and 32-B aligned records");
+                "ocppo_gae_records: logprobs (16-B aligned), actions and 16-B aligned records");
   return gae_launch(stream, rewards, values, dones, next_value, next_done, T, N, gamma,
                     gae_lambda, advantages, returns, logprobs, actions, records);
 }

@@ -121,8 +121,8 @@ __device__ __forceinline__ void categorical_backward_loss(const float (&ln)[AMAX
 // ocppo_minibatch_adv_stats and the statistics blocks of ocppo_minibatch_prepare, so the two
 // give bitwise-identical figures.
 constexpr int kStatsThreads = 256;
-// STRIDE: floats between consecutive samples' advantages (1: the b_adv array; 8: the advantage
-// field of the 32-B sample records of ocppo_gae_records)
+// STRIDE: floats between consecutive samples' advantages (1: the b_adv array;
+// field of the 16-B sample records of ocppo_gae_records: 4)
 template <int VPT, int STRIDE = 1>
 __device__ __forceinline__ void adv_stats_block(const float* __restrict__ adv,
                                                 const int64_t* __restrict__ perm, int64_t M,
@@ -271,10 +271,10 @@ __global__ __launch_bounds__(256) void minibatch_prepare_kernel(
   }
 }
 
-// The same from the 32-B sample records of ocppo_gae_records ({log-prob, advantage, return,
-// value, action i64, pad}): one 32-B gather per sample (both halves of it are one 64-B sector)
-// instead of five scattered 4-8 B ones; same values, same order, so the statistics and the SoA
-// outputs are bitwise those of minibatch_prepare_kernel.
+// The same from the 16-B sample records of ocppo_gae_records ({log-prob, advantage, value,
+// action i32}): one 16-B gather per sample instead of five scattered 4-8 B ones; the return is
+// advantage + value with GAE's own f32 add, so the statistics and the SoA outputs are bitwise
+// those of minibatch_prepare_kernel.
 template <int VPT, int SVPT>
 __global__ __launch_bounds__(256) void minibatch_prepare_rec_kernel(
     const int64_t* __restrict__ perm, int64_t n, int gather_blocks, int64_t M,
@@ -284,7 +284,7 @@ __global__ __launch_bounds__(256) void minibatch_prepare_rec_kernel(
   const int nstat = stats ? static_cast<int>(gridDim.x) - gather_blocks : 0;
   if (static_cast<int>(blockIdx.x) < nstat) {
     __shared__ float scratch[kStatsThreads / kWave];
-    adv_stats_any_vpt<SVPT, 8>(reinterpret_cast<const float*>(rec) + 1, perm, M, blockIdx.x,
+    adv_stats_any_vpt<SVPT, 4>(reinterpret_cast<const float*>(rec) + 1, perm, M, blockIdx.x,
                                stats, scratch);
     return;
   }
@@ -295,23 +295,18 @@ __global__ __launch_bounds__(256) void minibatch_prepare_rec_kernel(
     const int64_t i = base + k * 256;
     idx[k] = i < n ? perm[i] : -1;
   }
-  float4 r0[VPT], r1[VPT];
+  float4 r0[VPT];
 #pragma unroll
-  for (int k = 0; k < VPT; ++k) {
-    const int64_t b = idx[k] >= 0 ? idx[k] : 0;
-    r0[k] = rec[2 * b];
-    r1[k] = rec[2 * b + 1];
-  }
+  for (int k = 0; k < VPT; ++k) r0[k] = rec[idx[k] >= 0 ? idx[k] : 0];
 #pragma unroll
   for (int k = 0; k < VPT; ++k) {
     const int64_t i = base + k * 256;
     if (idx[k] >= 0) {
-      mb_act[i] = static_cast<int64_t>(static_cast<uint32_t>(__float_as_int(r1[k].x))) |
-                  (static_cast<int64_t>(__float_as_int(r1[k].y)) << 32);
+      mb_act[i] = __float_as_int(r0[k].w);
       mb_lp[i] = r0[k].x;
       mb_adv[i] = r0[k].y;
-      mb_ret[i] = r0[k].z;
-      mb_val[i] = r0[k].w;
+      mb_ret[i] = r0[k].y + r0[k].z;  // GAE's returns = advantages + values, the same f32 add
+      mb_val[i] = r0[k].z;
     }
   }
 }
@@ -1241,8 +1236,8 @@ extern "C" int ocppo_minibatch_prepare_records(ocppo_stream_t stream, const int6
                 "ocppo_minibatch_prepare_records: bad sizes M=%lld num_mb=%lld", (long long)M,
                 (long long)num_mb);
   OCPPO_REQUIRE(perm && records && mb_actions && mb_logprobs && mb_advantages && mb_returns &&
-                    mb_values && reinterpret_cast<uintptr_t>(records) % 32 == 0,
-                "ocppo_minibatch_prepare_records: null pointer or records not 32-B aligned");
+                    mb_values && reinterpret_cast<uintptr_t>(records) % 16 == 0,
+                "ocppo_minibatch_prepare_records: null pointer or records not 16-B aligned");
   clear_stale_error();
   hipStream_t s = as_stream(stream);
   constexpr int VPT = 4;

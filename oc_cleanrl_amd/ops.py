@@ -80,7 +80,7 @@ def gae(rewards, values, dones, next_value, next_done, gamma: float, gae_lambda:
 
     Bit-identical to the reference loop. `next_value` may be [N] or [1, N] (as produced by
     `agent.get_value(next_obs).reshape(1, -1)`). records (with logprobs [T, N] f32 and actions
-    [T, N] i64): also write each sample's 32-B record (sample_records) for
+    [T, N] i64 in [0, 2^31)): also write each sample's 16-B record (sample_records) for
     minibatch_prepare(records=...).
     """
     if rewards.dim() != 2:
@@ -103,13 +103,13 @@ def gae(rewards, values, dones, next_value, next_done, gamma: float, gae_lambda:
         call("ocppo_gae_records", _stream(dev), *args,
              _check(logprobs, "logprobs", f, dev, T * N),
              _check(actions, "actions", torch.int64, dev, T * N),
-             _check(records, "records", torch.int64, dev, 4 * T * N))
+             _check(records, "records", torch.int32, dev, 4 * T * N))
     return advantages, returns
 
 
 def sample_records(B: int, device):
-    """[B] x 32-B per-sample records (ocppo.h OcppoSampleRecord) as an int64 [B, 4] tensor."""
-    return torch.zeros((B, 4), dtype=torch.int64, device=device)
+    """[B] x 16-B per-sample records (ocppo.h OcppoSampleRecord) as an int32 [B, 4] tensor."""
+    return torch.zeros((B, 4), dtype=torch.int32, device=device)
 
 
 # ---------------------------------------------------------------------------------------------
@@ -133,7 +133,7 @@ def minibatch_adv_stats(b_advantages, perm, minibatch_size: int, out=None):
 def minibatch_prepare(perm, minibatch_size: int, b_actions, b_logprobs, b_advantages, b_returns,
                       b_values, out: dict | None = None, with_stats: bool = True, records=None):
     """Gather every minibatch's per-sample arrays into minibatch order (+ adv stats).
-    records: the 32-B per-sample records of gae(records=...) gathered instead of the five b_*
+    records: the 16-B per-sample records of gae(records=...) gathered instead of the five b_*
     arrays (then only their sizes are read; bitwise the same outputs).
 
     Returns dict(actions, logprobs, advantages, returns, values: [num_mb*M], adv_stats [num_mb,2])."""
@@ -153,7 +153,7 @@ def minibatch_prepare(perm, minibatch_size: int, b_actions, b_logprobs, b_advant
                    "adv_stats": torch.empty((num_mb, 2), dtype=f, device=dev)}
         call("ocppo_minibatch_prepare_records", _stream(dev),
              _check(perm, "perm", torch.int64, dev), M, num_mb,
-             _check(records, "records", torch.int64, dev, 4 * B),
+             _check(records, "records", torch.int32, dev, 4 * B),
              _check(out["actions"], "mb_actions", torch.int64, dev, n),
              _check(out["logprobs"], "mb_logprobs", f, dev, n),
              _check(out["advantages"], "mb_advantages", f, dev, n),

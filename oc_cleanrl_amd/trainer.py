@@ -614,7 +614,7 @@ class PPOTrainer:
     def _prepare_minibatches(self, from_records: bool = False):
         """Every minibatch's per-sample records in minibatch order + its adv (mean, std)
         (:566-579: b_*[mb_inds] and the minibatch advantage statistics). from_records: gather
-        the 32-B sample records this iteration's GAE wrote (one gather per sample instead of
+        the 16-B sample records this iteration's GAE wrote (one gather per sample instead of
         five; bitwise the same outputs)."""
         T = self.T
         rec = self.records if from_records else None

@@ -1378,24 +1378,24 @@ def test_heads_loss_rejects_uninstantiated_widths(ops, dev, H):
                                   (16, 65540)])
 def test_gae_records_are_the_arrays(ops, dev, T_, N):
     """ocppo_gae_records: advantages / returns bitwise those of ocppo_gae (every tile width and
-    the streaming form), and each sample's 32-B record holds exactly its log-prob, advantage,
-    return, value and action."""
+    the streaming form), and each sample's 16-B record holds exactly its log-prob, advantage,
+    value and action (advantage + value is its return, bitwise)."""
     g = torch.Generator(device=dev).manual_seed(T_ * 31 + N)
     r = torch.randn(T_, N, device=dev, generator=g)
     v = torch.randn(T_, N, device=dev, generator=g)
     d = (torch.rand(T_, N, device=dev, generator=g) < 0.1).float()
     nv, nd = torch.randn(N, device=dev, generator=g), torch.zeros(N, device=dev)
     lp = torch.randn(T_, N, device=dev, generator=g)
-    act = torch.randint(-3, 1 << 40, (T_, N), device=dev, generator=g)
+    act = torch.randint(0, 1 << 31, (T_, N), device=dev, generator=g)
     a0, r0 = ops.gae(r, v, d, nv, nd, 0.99, 0.95)
     rec = ops.sample_records(T_ * N, dev)
     a1, r1 = ops.gae(r, v, d, nv, nd, 0.99, 0.95, logprobs=lp, actions=act, records=rec)
     torch.cuda.synchronize()
     assert torch.equal(a0, a1) and torch.equal(r0, r1)
-    f = rec.view(torch.float32).view(T_ * N, 8)
+    f = rec.view(torch.float32).view(T_ * N, 4)
     assert torch.equal(f[:, 0], lp.view(-1)) and torch.equal(f[:, 1], a1.view(-1))
-    assert torch.equal(f[:, 2], r1.view(-1)) and torch.equal(f[:, 3], v.view(-1))
-    assert torch.equal(rec[:, 2], act.view(-1))
+    assert torch.equal(f[:, 2], v.view(-1)) and torch.equal(rec[:, 3].long(), act.view(-1))
+    assert torch.equal(f[:, 1] + f[:, 2], r1.view(-1))
 
 
 @pytest.mark.parametrize("M,nmb,B", [(4096, 16, 16384), (100, 7, 700), (16384, 4, 65536)])

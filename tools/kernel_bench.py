@@ -30,7 +30,7 @@ MFMA_F32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense f32 MFMA (= the f32 v
 
 SIZES = {
     # name: {size: params}
-    # GAE as the trainer runs it: advantages / returns + the 32-B sample records (ops.gae with
+    # GAE as the trainer runs it: advantages / returns + the 16-B sample records (ops.gae with
     # records); gae_plain without the records
     "gae": {"config": dict(T=128, N=128), "scaled": dict(T=128, N=262144)},
     "gae_plain": {"config": dict(T=128, N=128), "scaled": dict(T=128, N=262144)},
@@ -43,7 +43,7 @@ SIZES = {
     "env_step": {"config": dict(N=128, D=12), "scaled": dict(N=4 * 1024 * 1024, D=12)},
     "adv_stats": {"config": dict(M=4096, nmb=16, B=16384), "scaled": dict(M=16384, nmb=256, B=1 << 20)},
     "mb_prepare": {"config": dict(M=4096, nmb=16, B=16384), "scaled": dict(M=16384, nmb=256, B=1 << 20)},
-    # the same from the five SoA arrays (the form before GAE packed 32-B sample records)
+    # the same from the five SoA arrays (the form before GAE packed 16-B sample records)
     "mb_prepare_soa": {"config": dict(M=4096, nmb=16, B=16384), "scaled": dict(M=16384, nmb=256, B=1 << 20)},
     "ppo_loss_prepared": {"config": dict(M=4096, A=6), "scaled": dict(M=4 * 1024 * 1024, A=6)},
     "policy_head": {"config": dict(N=128, H=512, A=6), "scaled": dict(N=262144, H=512, A=6)},
@@ -103,8 +103,8 @@ def case_bytes(name: str, p: dict) -> float:
     tools/summarize_profiles.py prices the PMC passes with the same numbers). ppo_loss gathers its
     records through the minibatch indices (8A+32 B per element + the 4-B index); the prepared
     form reads them contiguous (8A+32)."""
-    if name == "gae":  # + log-prob 4 + action 8 in, the 32-B record out
-        return 64 * p["T"] * p["N"] + 8 * p["N"]
+    if name == "gae":  # + log-prob 4 + action 8 in, the 16-B record out
+        return 48 * p["T"] * p["N"] + 8 * p["N"]
     if name == "gae_plain":
         return 20 * p["T"] * p["N"] + 8 * p["N"]
     if name == "ppo_loss":
@@ -182,7 +182,7 @@ def make_case(name: str, p: dict, dev):
         rec = ops.sample_records(T * N, dev)
         adv, ret = torch.empty_like(r), torch.empty_like(r)
         return (lambda: ops.gae(r, v, d, nv, nd, 0.99, 0.95, adv, ret, logprobs=lp, actions=act,
-                                records=rec)), 64 * T * N + 8 * N
+                                records=rec)), 48 * T * N + 8 * N
     if name == "ppo_loss":
         M, A, B = p["M"], p["A"], p["B"]
         logits = torch.randn(M, A, device=dev, generator=g)
@@ -245,7 +245,7 @@ def make_case(name: str, p: dict, dev):
         out = torch.empty(nmb, 2, device=dev)
         return (lambda: ops.minibatch_adv_stats(adv, perm, M, out)), 2 * nmb * M * 12
     if name in ("mb_prepare", "mb_prepare_soa"):
-        # mb_prepare: the trainer's form, from GAE's 32-B sample records (the records are made
+        # mb_prepare: the trainer's form, from GAE's 16-B sample records (the records are made
         # here by ops.gae on a [T, B / T] rollout of the same arrays)
         M, nmb, B = p["M"], p["nmb"], p["B"]
         reps = (nmb * M + B - 1) // B
