@@ -126,8 +126,11 @@ class Args:
                                   # generator stream) instead of once per rollout ([T, N, A])
     fused_heads_loss: bool = True  # update: policy heads fwd + PPO loss + heads bwd in one HIP op
     dp_overlap: bool = True  # DP: all-reduce the decoder-side gradients during the encoder backward
-    sample_records: bool = True  # GAE also packs each sample's 16-B record; the minibatch gather
-                                 # reads one record per sample instead of five arrays
+    sample_records_min: int = 131072  # local batches of at least this many samples: GAE also
+                                      # packs each sample's 16-B record and the minibatch gather
+                                      # reads one record instead of five arrays (-1: never).
+                                      # It pays at scale (1M samples: GAE + prepare 454 -> 427
+                                      # us), not at config 2's 16K (+1-2 us), profiles/r04
     dp_graph_collectives: bool = False  # DP: capture each epoch's minibatches WITH their RCCL
                                         # all-reduces in one hipGraph (else one graph per phase,
                                         # the collectives launched eagerly between them)

@@ -398,7 +398,8 @@ class PPOTrainer:
         self.b_obs = self.obs[:T].view((T * N,) + self.obs_shape)
         self.wplanes, self.wplanes_built = None, False  # built at the first minibatch
         # GAE's per-sample records for the minibatch gather (ops.sample_records)
-        self.records = ops.sample_records(self.B, dev) if a.sample_records else None
+        self.records = (ops.sample_records(self.B, dev)
+                        if 0 <= a.sample_records_min <= self.B else None)
 
         # Every update is captured, the NatureCNN's MIOpen convolutions included (round 1 ran that
         # one eagerly after a capture_end crash that no longer reproduces: tools/exp_c3_capture.py

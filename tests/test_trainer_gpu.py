@@ -598,8 +598,8 @@ def test_weight_planes_are_bitwise_the_in_kernel_split(dev, graphs):
 def test_sample_records_are_bitwise_the_soa_gather(dev):
     """GAE's 16-B sample records feeding the minibatch gather (Args.sample_records) leave the
     training bitwise unchanged: same parameters after three iterations with graphs."""
-    a, _ = run_iters(small_args(sample_records=True, cuda_graphs=True), 3, dev)
-    b, _ = run_iters(small_args(sample_records=False, cuda_graphs=True), 3, dev)
+    a, _ = run_iters(small_args(sample_records_min=0, cuda_graphs=True), 3, dev)
+    b, _ = run_iters(small_args(sample_records_min=-1, cuda_graphs=True), 3, dev)
     assert a.records is not None and b.records is None
     for p, q in zip(a.agent.parameters(), b.agent.parameters()):
         assert torch.equal(p, q)
