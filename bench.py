@@ -39,8 +39,11 @@ MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (the matrix rate ocppo_gemm_x6
 RIDGE = MFMA_F32_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9)  # flop/B where the two bounds meet
 # HBM bytes per launch from rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE, separate passes) of
 # the same launch shapes: tools/profile_round.sh -> tools/summarize_profiles.py
-PMC_SUMMARY = ROOT / "profiles" / "r03" / "pmc_summary.json"
-PMC_KEYS = {"action_head": "policy_head_config", "gae": "gae_config",
+PMC_SUMMARY = ROOT / "profiles" / "r04" / "pmc_summary.json"
+# in-situ HBM bytes of the bench's own gemm_x6 launches (all shapes, mean per dispatch):
+# tools/pmc_bench.sh -> tools/pmc_bench_summary.py
+PMC_BENCH = ROOT / "profiles" / "r04" / "pmc_bench.json"
+PMC_KEYS = {"gemm_x6": "gemm_x6", "action_head": "policy_head_config", "gae": "gae_config",
             "ppo_loss": "ppo_loss_prepared_config", "relu_bias_grad": "relu_bias_grad_config",
             "cache_linear": "cache_linear_config", "store_encode": "store_encode_config",
             "heads_bwd": "heads_bwd_config", "relu_bias_wgrad": "relu_bias_wgrad_config",
@@ -50,6 +53,9 @@ PMC_KEYS = {"action_head": "policy_head_config", "gae": "gae_config",
 
 def pmc_traffic(key):
     try:
+        if key == "gemm_x6":
+            rec = json.loads(PMC_BENCH.read_text())["gemm_x6"]
+            return rec.get("traffic_bytes"), str(PMC_BENCH.relative_to(ROOT))
         rec = json.loads(PMC_SUMMARY.read_text())["kernels"][key]
         return rec.get("traffic_bytes"), str(PMC_SUMMARY.relative_to(ROOT))
     except (OSError, KeyError, ValueError):

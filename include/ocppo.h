@@ -376,7 +376,8 @@ OCPPO_API int ocppo_split_planes(ocppo_stream_t stream, int n, const float* cons
  * Split-K combine of a weight gradient — replaces ATen's `sum(0)` after the batched (split-K)
  * weight-gradient GEMM dW = g'^T x the build runs inside `loss.backward()` (ppo_atari_oc.py:605)
  * for the Linear layers of architectures/ppo.py:60-84:
- *   out[i] = part[0*n + i] + part[1*n + i] + ... + part[(S-1)*n + i]   (left fold, split order)
+ *   out[i] = part[0*n + i] + part[1*n + i] + ... + part[(S-1)*n + i]   (left fold, split order,
+ *            in double, rounded once to float)
  * part [S, n] f32, out [n] f32 (e.g. the parameter's view in the flat grad buffer); both 16-B
  * aligned, n % 4 == 0, S in {1, 2, 4, 8, 16}. Deterministic.
  * ------------------------------------------------------------------------------------------- */
@@ -406,8 +407,9 @@ OCPPO_API int ocppo_relu_bias_grad(ocppo_stream_t stream, const float* g, const 
 OCPPO_API int64_t ocppo_relu_bias_grad_chunks(int64_t R, int64_t N);
 OCPPO_API int ocppo_relu_bias_grad_partial(ocppo_stream_t stream, const float* g, const float* out,
                                            float* gp, float* partials, int64_t R, int64_t N);
-/* ocppo_sum_splits (out = sum of the S split-K blocks) + db[j] = sum_c db_partials[c, j] (chunk
- * order) in one launch; n, N multiples of 4, all pointers 16-B aligned. */
+/* ocppo_sum_splits (out = sum of the S split-K blocks) + db[j] = sum_c db_partials[c, j] (a fixed
+ * order) in one launch, both folds in double, rounded once; n, N multiples of 4, all pointers
+ * 16-B aligned. */
 OCPPO_API int ocppo_sum_splits_db(ocppo_stream_t stream, const float* part, int64_t S, int64_t n,
                                   float* out, const float* db_partials, int64_t chunks, int64_t N,
                                   float* db);

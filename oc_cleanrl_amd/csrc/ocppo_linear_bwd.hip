@@ -358,7 +358,8 @@ extern "C" int ocppo_bias_act_nchw(ocppo_stream_t stream, const float* y, const 
   return check_launch("ocppo_bias_act_nchw");
 }
 
-// ---- split-K combine of a weight gradient: out[i] = part[0][i] + part[1][i] + ... (split order)
+// ---- split-K combine of a weight gradient: out[i] = part[0][i] + part[1][i] + ... (split order,
+// added in float64 and rounded once, as in sum_splits_db_kernel below)
 // The update's tall-skinny weight-gradient GEMMs dW = g'^T x (inside loss.backward(),
 // ppo_atari_oc.py:605, for the PPObj Linear layers of architectures/ppo.py:60-84) run as a
 // batched GEMM over S row chunks; this sums the S partial [n] blocks straight into the
@@ -375,12 +376,13 @@ __global__ __launch_bounds__(256) void sum_splits_kernel(const float4* __restric
     float4 v[S];
 #pragma unroll
     for (int s = 0; s < S; ++s) v[s] = part[s * n4 + i];
-    float4 a = v[0];
+    double ax = v[0].x, ay = v[0].y, az = v[0].z, aw = v[0].w;  // f64 fold, one rounding
 #pragma unroll
     for (int s = 1; s < S; ++s) {
-      a.x += v[s].x; a.y += v[s].y; a.z += v[s].z; a.w += v[s].w;
+      ax += v[s].x; ay += v[s].y; az += v[s].z; aw += v[s].w;
     }
-    out[i] = a;
+    out[i] = make_float4(static_cast<float>(ax), static_cast<float>(ay), static_cast<float>(az),
+                         static_cast<float>(aw));
   }
 }
 }  // namespace ocppo
@@ -388,8 +390,8 @@ __global__ __launch_bounds__(256) void sum_splits_kernel(const float4* __restric
 // The deferred bias gradient of ocppo_relu_bias_grad_partial, summed in the same launch as the
 // weight gradient's split-K combine: blocks [0, nsb) combine the weight splits, blocks
 // [nsb, nsb + ceil(N / 16)) each own 16 columns of db: 4 column quads x 64 chunk groups, each
-// thread summing its chunks in order, then the 64 group sums in group order (LDS): one pass,
-// deterministic. (16 columns per block: the frame scatter's 720 chunk partials at [11520 x 512]
+// thread summing its chunks in order, then the 64 group sums by a fixed butterfly inside each
+// wave and the 4 wave sums in order: one pass, deterministic. (16 columns per block: the frame scatter's 720 chunk partials at [11520 x 512]
 // take two load batches per thread instead of six.) Both folds add in float64 and round once:
 // a bias gradient is a column sum over ~10^4 rows with heavy cancellation, and a left fold of
 // 90-720 f32 partials rounded at every step cost it up to 1.6e-4 of its largest element against
@@ -423,7 +425,7 @@ __global__ __launch_bounds__(256) void sum_splits_db_kernel(const float4* __rest
     }
     return;
   }
-  __shared__ d4 red[kDbGroups][kDbQuads];
+  __shared__ d4 red[256 / kWave][kDbQuads];
   const int cb = blockIdx.x - nsb;
   const int q = threadIdx.x % kDbQuads, gi = threadIdx.x / kDbQuads;  // column quad, chunk group
   const int64_t col = static_cast<int64_t>(cb) * (4 * kDbQuads) + 4 * q;
@@ -443,11 +445,18 @@ __global__ __launch_bounds__(256) void sum_splits_db_kernel(const float4* __rest
       }
     }
   }
-  red[gi][q] = acc;
+  // the 16 chunk groups of a wave (lanes 4 apart) by a butterfly, then the 4 waves in order
+#pragma unroll
+  for (int o = kDbQuads; o < kWave; o *= 2) {
+    acc.x += __shfl_xor(acc.x, o); acc.y += __shfl_xor(acc.y, o);
+    acc.z += __shfl_xor(acc.z, o); acc.w += __shfl_xor(acc.w, o);
+  }
+  const int wid = threadIdx.x / kWave;
+  if ((threadIdx.x & (kWave - 1)) < kDbQuads) red[wid][q] = acc;
   __syncthreads();
-  if (gi == 0 && col < N) {
+  if (threadIdx.x < kDbQuads && col < N) {
     d4 t = red[0][q];
-    for (int k = 1; k < kDbGroups; ++k) {
+    for (int k = 1; k < 256 / kWave; ++k) {
       const d4 v = red[k][q];
       t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
     }

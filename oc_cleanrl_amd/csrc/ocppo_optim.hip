@@ -4,30 +4,33 @@
 // DP all-reduce, ppo_atari_multigpu.py:369-374).
 //
 //   norm kernel : grid-strided partial sums of (g * grad_scale)^2 per workgroup (16-B loads),
-//                 written through (sc1) + one agent-scope ticket; the last workgroup combines the
-//                 partials in workgroup order and prepares the step scalars:
-//                 total_norm, clip = min(max_norm / (total_norm + 1e-6), 1), step += 1,
-//                 step_size = lr / (1 - beta1^step), bc2_sqrt = sqrt(1 - beta2^step)
-//   adam kernel : g = (g * grad_scale) * clip;  m = beta1*m + (1-beta1)*g;
+//                 one plain store per workgroup; workgroup 0 also advances the step counter
+//                 (the only writer of it; the adam kernel, next on the stream, only reads it)
+//   adam kernel : every workgroup first combines the <= 256 partials itself, in workgroup order
+//                 (the same fixed-order sum in every workgroup, so every one derives the same
+//                 total_norm, clip = min(max_norm / (total_norm + 1e-6), 1), step_size =
+//                 lr / (1 - beta1^step), bc2_sqrt = sqrt(1 - beta2^step)), then
+//                 g = (g * grad_scale) * clip;  m = beta1*m + (1-beta1)*g;
 //                 v = beta2*v + (1-beta2)*g*g;  p -= step_size * m / (sqrt(v)/bc2_sqrt + eps)
 //                 (the formula of ATen's fused Adam), 16-B vectors, 28 B of HBM per parameter.
+// No ticket and no last-arriver hand-off: the kernel boundary orders the partials (round 3's
+// ticketed form spent ~7 us of its 11 per minibatch in the 256-way fan-in and the dependent
+// combine at config 2).
 #include "ocppo_common.h"
 
 namespace ocppo {
 
 constexpr int kOptThreads = 256;
-constexpr int kOptBlocks = 256;  // grid-stride cap for the norm pass: one workgroup per CU keeps
-                                 // the ticket fan-in at 256 arrivals (~3-4 us, MI355X "fanin")
+constexpr int kOptBlocks = 256;  // grid-stride cap for the norm pass: one workgroup per CU, at
+                                 // most 256 partials for every adam workgroup to combine
 
 // scalars layout (f32): see include/ocppo.h OCPPO_OPT_*
 enum { S_STEP = 0, S_TOTAL_NORM = 1, S_CLIP = 2, S_STEP_SIZE = 3, S_BC2_SQRT = 4 };
 
 __global__ __launch_bounds__(kOptThreads) void grad_norm_kernel(
-    const float* __restrict__ g, int64_t P, float grad_scale, float max_norm,
-    const float* __restrict__ lr, float beta1, float beta2, float* __restrict__ scalars,
-    float* __restrict__ partials, unsigned* __restrict__ ticket) {
+    const float* __restrict__ g, int64_t P, float grad_scale, float* __restrict__ scalars,
+    float* __restrict__ partials) {
   __shared__ float red[kOptThreads / kWave];
-  __shared__ int s_last;
   float acc = 0.f;
   const int64_t P4 = P / 4;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kOptThreads;
@@ -60,18 +63,26 @@ __global__ __launch_bounds__(kOptThreads) void grad_norm_kernel(
   if (threadIdx.x == 0) {
     float s = red[0];
     for (int k = 1; k < kOptThreads / kWave; ++k) s += red[k];
-    __hip_atomic_store(&partials[blockIdx.x], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = prev == gridDim.x - 1;
+    partials[blockIdx.x] = s;
+    if (blockIdx.x == 0) scalars[S_STEP] = scalars[S_STEP] + 1.f;
   }
-  __syncthreads();
-  if (!s_last) return;
+}
+
+// The step scalars from the norm kernel's partials, in every workgroup alike (fixed order: the
+// partial of workgroup t in thread t, the wave sums, then the 4 waves in order)
+struct AdamScalars {
+  float clip, step_size, bc2_sqrt, total;
+};
+__device__ __forceinline__ AdamScalars adam_scalars(const float* __restrict__ partials, int nb,
+                                                    float max_norm, const float* __restrict__ lr,
+                                                    float beta1, float beta2,
+                                                    const float* __restrict__ scalars) {
+  __shared__ float red[kOptThreads / kWave];
+  __shared__ AdamScalars sc;
   float t = 0.f;
-  for (unsigned b = threadIdx.x; b < gridDim.x; b += kOptThreads)
-    t += __hip_atomic_load(&partials[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int b = threadIdx.x; b < nb; b += kOptThreads) t += partials[b];
   const float tw = wave_sum(t);
-  __syncthreads();
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
   if (lane == 0) red[wid] = tw;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -83,16 +94,12 @@ __global__ __launch_bounds__(kOptThreads) void grad_norm_kernel(
       clip = max_norm / (total + 1e-6f);
       clip = clip < 1.f ? clip : 1.f;
     }
-    const float step = scalars[S_STEP] + 1.f;
-    const float bc1 = 1.f - powf(beta1, step);
-    const float bc2 = 1.f - powf(beta2, step);
-    scalars[S_STEP] = step;
-    scalars[S_TOTAL_NORM] = total;
-    scalars[S_CLIP] = clip;
-    scalars[S_STEP_SIZE] = lr[0] / bc1;
-    scalars[S_BC2_SQRT] = sqrtf(bc2);
-    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+    const float step = scalars[S_STEP];
+    sc = AdamScalars{clip, lr[0] / (1.f - powf(beta1, step)), sqrtf(1.f - powf(beta2, step)),
+                     total};
   }
+  __syncthreads();
+  return sc;
 }
 
 __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, float b1, float b2,
@@ -106,9 +113,16 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
 __global__ __launch_bounds__(kOptThreads) void adam_kernel(
     float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
     float* __restrict__ v, int64_t P, float grad_scale, float b1, float b2, float eps,
-    const float* __restrict__ scalars) {
-  const float clip = scalars[S_CLIP], step_size = scalars[S_STEP_SIZE],
-              bc2_sqrt = scalars[S_BC2_SQRT];
+    float max_norm, const float* __restrict__ lr, const float* __restrict__ partials, int nb,
+    float* __restrict__ scalars) {
+  const AdamScalars sc = adam_scalars(partials, nb, max_norm, lr, b1, b2, scalars);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // the reported figures (read after the step)
+    scalars[S_TOTAL_NORM] = sc.total;
+    scalars[S_CLIP] = sc.clip;
+    scalars[S_STEP_SIZE] = sc.step_size;
+    scalars[S_BC2_SQRT] = sc.bc2_sqrt;
+  }
+  const float clip = sc.clip, step_size = sc.step_size, bc2_sqrt = sc.bc2_sqrt;
   const int64_t P4 = P / 4;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kOptThreads;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * kOptThreads + threadIdx.x; i < P4; i += stride) {
@@ -154,22 +168,20 @@ extern "C" int ocppo_clip_adam_step(ocppo_stream_t stream, float* params, const 
     return fail(OCPPO_E_WORKSPACE, "ocppo_clip_adam_step: workspace needs %zu bytes, got %zu",
                 ocppo_clip_adam_workspace_bytes(P), workspace_bytes);
   char* ws = static_cast<char*>(workspace);
-  unsigned* ticket = reinterpret_cast<unsigned*>(ws);
   float* partials = reinterpret_cast<float*>(ws + 256);
   int64_t nb = ceil_div(P / 4 > 0 ? P / 4 : 1, kOptThreads);
   nb = nb < kOptBlocks ? nb : kOptBlocks;
   clear_stale_error();
   hipStream_t s = as_stream(stream);
   hipLaunchKernelGGL(grad_norm_kernel, dim3(static_cast<unsigned>(nb)), dim3(kOptThreads), 0, s,
-                     grads, P, static_cast<float>(grad_scale), static_cast<float>(max_norm), lr,
-                     static_cast<float>(beta1), static_cast<float>(beta2), scalars, partials,
-                     ticket);
+                     grads, P, static_cast<float>(grad_scale), scalars, partials);
   if (int rc = check_launch("ocppo_clip_adam_step/norm")) return rc;
   int64_t na = ceil_div(P / 4 > 0 ? P / 4 : 1, kOptThreads);
   na = na < 256 * 8 ? na : 256 * 8;
   hipLaunchKernelGGL(adam_kernel, dim3(static_cast<unsigned>(na)), dim3(kOptThreads), 0, s, params,
                      grads, exp_avg, exp_avg_sq, P, static_cast<float>(grad_scale),
                      static_cast<float>(beta1), static_cast<float>(beta2),
-                     static_cast<float>(eps), scalars);
+                     static_cast<float>(eps), static_cast<float>(max_norm), lr, partials,
+                     static_cast<int>(nb), scalars);
   return check_launch("ocppo_clip_adam_step/adam");
 }

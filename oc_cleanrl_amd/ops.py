@@ -703,7 +703,7 @@ def relu_bias_grad_partial(g, out=None, gp=None):
 
 
 def sum_splits_db(part, out, db_part, db):
-    """sum_splits(part, out) and db = db_part[0].sum(0) in chunk order, one launch
+    """sum_splits(part, out) and db = db_part.sum(0) in a fixed order, one launch
     (db_part = the (partials, chunks) of relu_bias_grad_partial)."""
     S = part.shape[0]
     dev = part.device
@@ -833,8 +833,8 @@ def sum_splits_ok(part, out) -> bool:
 
 
 def sum_splits(part, out=None):
-    """out = part.sum(0) over the S split-K partial blocks of a weight gradient, in split order,
-    in one streaming pass (part [S, ...] f32 contiguous, S in {1, 2, 4, 8, 16})."""
+    """out = part.sum(0) over the S split-K partial blocks of a weight gradient, in split order
+    (added in f64, rounded once), in one streaming pass (part [S, ...] f32 contiguous, S in {1, 2, 4, 8, 16})."""
     S = part.shape[0]
     dev = part.device
     if out is None:

@@ -426,12 +426,14 @@ def test_linear_act_deterministic(ops, dev):
 @pytest.mark.parametrize("S,shape", [(8, (1024, 512)), (4, (512, 256)), (16, (256, 12)),
                                      (8, (6, 512)), (1, (4, 4)), (2, (3, 4))])
 def test_sum_splits_is_the_split_order_fold(ops, dev, S, shape):
-    """Split-K combine: bit-identical to ((p0 + p1) + p2) + ... in f32, written into a view."""
+    """Split-K combine: bit-identical to ((p0 + p1) + p2) + ... added in f64 and rounded once to
+    f32, written into a view."""
     g = torch.Generator(device=dev).manual_seed(S * 1000 + shape[0])
     part = torch.randn((S,) + shape, device=dev, generator=g)
-    ref = part[0].clone()
+    ref = part[0].double()
     for s in range(1, S):
-        ref = ref + part[s]
+        ref = ref + part[s].double()
+    ref = ref.float()
     flat = torch.full((shape[0] * shape[1] + 8,), 5.0, device=dev)
     out = flat[4:4 + shape[0] * shape[1]].view(shape)
     ops.sum_splits(part, out)
