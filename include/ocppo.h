@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define OCPPO_ABI_VERSION 20
+#define OCPPO_ABI_VERSION 21
 
 /* status codes */
 #define OCPPO_OK 0
@@ -620,6 +620,31 @@ OCPPO_API int ocppo_heads_loss_fwd_bwd(ocppo_stream_t stream, const float* h, in
                                        float* dwa, float* dwc, float* dba, float* dbc,
                                        float* stats, float* dlogits, float* dvalue,
                                        void* workspace, size_t workspace_bytes);
+/* Deferred form: ocppo_heads_loss_rows launches the rows kernel only and writes the finish (the
+ * tree over the records, which writes db_h, dwa, dwc, dba, dbc and stats) into *finish, a plain
+ * host record; the caller runs it later on the same stream, before anything reads those outputs
+ * and before the workspace is reused: folded into the split-K combine the backward runs next
+ * (ocppo_sum_splits_finish = ocppo_sum_splits, bitwise, plus the finish workgroups in the same
+ * launch) or alone (ocppo_deferred_finish_run). Same results as ocppo_heads_loss_fwd_bwd, bitwise.
+ * The record holds device pointers only; it may be copied and run once per rows launch. */
+typedef struct ocppo_deferred_finish {
+  uint64_t opaque[64];
+} ocppo_deferred_finish_t;
+OCPPO_API int ocppo_heads_loss_rows(ocppo_stream_t stream, const float* h, int64_t M, int64_t H,
+                                    const float* w_actor, const float* b_actor,
+                                    const float* w_critic, const float* b_critic, int64_t A,
+                                    const int64_t* mb_actions, const float* mb_logprobs,
+                                    const float* mb_advantages, const float* mb_returns,
+                                    const float* mb_values, const float* adv_stats,
+                                    double clip_coef, double ent_coef, double vf_coef,
+                                    int norm_adv, int clip_vloss, float* gp, float* db_h,
+                                    float* dwa, float* dwc, float* dba, float* dbc, float* stats,
+                                    float* dlogits, float* dvalue, void* workspace,
+                                    size_t workspace_bytes, ocppo_deferred_finish_t* finish);
+OCPPO_API int ocppo_sum_splits_finish(ocppo_stream_t stream, const float* part, int64_t S,
+                                      int64_t n, float* out, const ocppo_deferred_finish_t* finish);
+OCPPO_API int ocppo_deferred_finish_run(ocppo_stream_t stream,
+                                        const ocppo_deferred_finish_t* finish);
 
 /* ---------------------------------------------------------------------------------------------
  * Rollout fusions of the PPObj frame-encoding cache path (ppo_atari_oc.py:502-514 + :506 with

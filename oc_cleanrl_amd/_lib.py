@@ -22,7 +22,7 @@ LIB_PATH = Path(os.environ.get("OCPPO_LIB", PKG / "lib" / "libocppo_hip.so"))
 HEADER = PKG.parent / "include" / "ocppo.h"
 
 # constants mirrored from include/ocppo.h (checked against the header by tests/test_abi.py)
-OCPPO_ABI_VERSION = 20
+OCPPO_ABI_VERSION = 21
 OCPPO_OK, OCPPO_E_INVALID, OCPPO_E_LAUNCH, OCPPO_E_WORKSPACE = 0, 1, 2, 3
 OCPPO_F32, OCPPO_BF16, OCPPO_U8 = 0, 1, 2
 STAT_NAMES = ("loss", "pg_loss", "v_loss", "entropy", "old_approx_kl", "approx_kl", "clipfrac",
@@ -83,6 +83,10 @@ SIGNATURES: dict[str, tuple[type, list]] = {
     "ocppo_heads_loss_workspace_bytes": (SZ, [I64, I64, I64]),
     "ocppo_heads_loss_fwd_bwd": (I, [P, P, I64, I64, P, P, P, P, I64, P, P, P, P, P, P, D, D, D, I,
                                      I, P, P, P, P, P, P, P, P, P, P, SZ]),
+    "ocppo_heads_loss_rows": (I, [P, P, I64, I64, P, P, P, P, I64, P, P, P, P, P, P, D, D, D, I,
+                                  I, P, P, P, P, P, P, P, P, P, P, SZ, P]),
+    "ocppo_sum_splits_finish": (I, [P, P, I64, I64, P, P]),
+    "ocppo_deferred_finish_run": (I, [P, P]),
     "ocppo_linear_cache_shift": (I, [P, P, I64, P, P, P, P, I64, I64, I64, I64, I]),
     "ocppo_linear_cache_ring": (I, [P, P, I64, P, P, P, P, I64, I64, I64, I64, I64, I]),
     "ocppo_linear_act_ring": (I, [P, P, I64, P, P, P, I64, I64, I64, I64, I64, I64, I]),

@@ -163,10 +163,20 @@ def _x6_dx_shape_ok(M: int, N: int, K: int, on: bool = True) -> bool:
     return _x6(M, K, N, on) and N % 32 == 0 and ops.x6_tile(M, K) is not None
 
 
-def _weight_grad(g, x, out=None, db=None, x6: bool = True):
+def _weight_grad(g, x, out=None, db=None, x6: bool = True, finish=None):
     """dW = g^T x (g [rows, n], x [rows, k]) with the split-K rule; written into `out` if given.
     db = (partials of ops.relu_bias_grad_partial, bias grad): the bias gradient is finished in
-    the same launch as the split-K combine (only when _defer_db_ok said so)."""
+    the same launch as the split-K combine (only when _defer_db_ok said so). finish = a pending
+    ops.DeferredFinish (the heads-loss finish): folded into the split-K combine when there is
+    one, else run right after."""
+    if finish is not None and finish.pending:
+        dw = _weight_grad_core(g, x, out, db, x6, finish)
+        finish.run()  # no-op when the combine took it
+        return dw
+    return _weight_grad_core(g, x, out, db, x6, None)
+
+
+def _weight_grad_core(g, x, out, db, x6, finish):
     rows, n = g.shape
     k = x.shape[1]
     s = _splitk(rows, k, n)
@@ -184,6 +194,9 @@ def _weight_grad(g, x, out=None, db=None, x6: bool = True):
     if db is not None:
         return ops.timed(f"sum_splits_db_{s}x{n}x{k}", lambda: ops.sum_splits_db(part, out, *db))
     if out is not None and HIP_SUM_SPLITS and ops.sum_splits_ok(part, out):
+        if finish is not None:
+            return ops.timed(f"sum_splits_fin_{s}x{n}x{k}",
+                             lambda: ops.sum_splits(part, out, finish=finish))
         return ops.timed(f"sum_splits_{s}x{n}x{k}", lambda: ops.sum_splits(part, out))
     return torch.sum(part, 0, out=out) if out is not None else part.sum(0)
 
@@ -333,7 +346,7 @@ class _LinearAct(torch.autograd.Function):
             dx = _LinearAct._dx_of(ctx, g, w) if ctx.needs_input_grad[0] else None
             dbp = ctx.box.get("dbp")
             if dbp is None:
-                _weight_grad(g, x, out=wgrad, x6=ctx.x6)
+                _weight_grad(g, x, out=wgrad, x6=ctx.x6, finish=ctx.box.get("finish"))
             elif _defer_db_ok(g, x, wgrad, ctx.b):
                 _weight_grad(g, x, out=wgrad, db=(dbp, ctx.b.grad), x6=ctx.x6)
             else:

@@ -28,7 +28,13 @@ namespace ocppo {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
-constexpr int kLinMaxWaves = 8;
+#ifndef OCPPO_LIN_MAX_WAVES  // K-split waves per workgroup cap (experiments: tools/build_variant.py)
+#define OCPPO_LIN_MAX_WAVES 8
+#endif
+#ifndef OCPPO_LIN_WAVE_TARGET  // split K until the launch has this many waves
+#define OCPPO_LIN_WAVE_TARGET 4096
+#endif
+constexpr int kLinMaxWaves = OCPPO_LIN_MAX_WAVES;
 
 // One wave's share of a 16x16 tile: chunks [c0, c1) of 16 k values. All operand loads of a group
 // of up to CH chunks are issued before its MFMAs, so the wave pays one L2 / Infinity-Cache round
@@ -328,13 +334,18 @@ static void launch_linear(hipStream_t s, bool vec, const float* x, int64_t ldx, 
   const int64_t tiles = static_cast<int64_t>((M + 15) / 16) * ((N + 15) / 16);
   const int nch = (K + 15) / 16;
   int S = 1;  // K split: >= ~4096 waves (4 per SIMD), >= 2 chunks per wave
-  while (S < kLinMaxWaves && tiles * S < 4096 && nch >= 2 * S * 2) S *= 2;
+  while (S < kLinMaxWaves && tiles * S < OCPPO_LIN_WAVE_TARGET && nch >= 2 * S * 2) S *= 2;
   const int cpw = (nch + S - 1) / S;
   switch (S) {
     case 1: launch_linear_s<1, RELU, CACHE>(s, cpw, vec, x, ldx, w, b, y, ldy, M, N, K, c, ring); break;
     case 2: launch_linear_s<2, RELU, CACHE>(s, cpw, vec, x, ldx, w, b, y, ldy, M, N, K, c, ring); break;
     case 4: launch_linear_s<4, RELU, CACHE>(s, cpw, vec, x, ldx, w, b, y, ldy, M, N, K, c, ring); break;
+#if OCPPO_LIN_MAX_WAVES > 8
+    case 8: launch_linear_s<8, RELU, CACHE>(s, cpw, vec, x, ldx, w, b, y, ldy, M, N, K, c, ring); break;
+    default: launch_linear_s<16, RELU, CACHE>(s, cpw, vec, x, ldx, w, b, y, ldy, M, N, K, c, ring); break;
+#else
     default: launch_linear_s<8, RELU, CACHE>(s, cpw, vec, x, ldx, w, b, y, ldy, M, N, K, c, ring); break;
+#endif
   }
 }
 
@@ -532,7 +543,7 @@ static void launch_conv(hipStream_t s, const float* x, const float* w, const flo
   const int64_t tiles = static_cast<int64_t>((M + 15) / 16) * ((N + 15) / 16);
   const int nch = K / 16;
   int S = 1;  // K split as launch_linear: >= ~kConvWaves waves, >= 2 chunks per wave
-  while (S < kLinMaxWaves && tiles * S < kConvWaves && nch >= 2 * S * 2) S *= 2;
+  while (S < 8 && tiles * S < kConvWaves && nch >= 2 * S * 2) S *= 2;
   const int cpw = (nch + S - 1) / S;
   switch (S) {
     case 1: launch_conv_s<1, RELU>(s, cpw, x, w, b, y, M, N, K, cg); break;

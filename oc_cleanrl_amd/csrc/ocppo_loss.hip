@@ -17,6 +17,7 @@
 // out). At the configs (M = 4096) one launch moves 344 KB and is launch/latency bound.
 #include <cfloat>
 #include <cstdlib>
+#include <cstring>
 
 #include "ocppo_common.h"
 #include "ocppo_categorical.h"
@@ -1734,22 +1735,34 @@ __global__ __launch_bounds__(256) void heads_loss_kernel(HeadsLossParams P) {
 #define OCPPO_HLFIN_OUT 32
 #endif
 constexpr int kHlFinOut = OCPPO_HLFIN_OUT, kHlFinGroups = 256 / kHlFinOut, kHlFinBatch = 32;
-__global__ __launch_bounds__(256) void heads_loss_finish_kernel(
-    const float* __restrict__ partials, int G, int64_t npw, int64_t ls, int64_t H, int A, int amax,
-    int cpl, float* __restrict__ db_h, float* __restrict__ dwa, float* __restrict__ dwc,
-    float* __restrict__ dba, float* __restrict__ dbc, LossParams L) {
+
+// Everything the finish needs, fixed when the rows kernel is launched (ocppo_heads_loss_rows
+// hands it to the caller as an ocppo_deferred_finish_t, so the finish can ride in a later launch)
+struct HlFinish {
+  const float* partials;
+  int G, A, amax, cpl;
+  int64_t npw, ls, H;
+  float *db_h, *dwa, *dwc, *dba, *dbc;
+  LossParams L;
+  int blocks;  // finish workgroups: ceil(npw / kHlFinOut)
+};
+
+// finish workgroup `blk` of f (256 threads)
+__device__ __forceinline__ void hl_finish_block(const HlFinish& f, int blk) {
   __shared__ float red[kHlFinGroups][kHlFinOut + 1];
   __shared__ float tot[kHlFinOut];
   const int o = threadIdx.x % kHlFinOut, gi = threadIdx.x / kHlFinOut;
-  const int64_t idx = static_cast<int64_t>(blockIdx.x) * kHlFinOut + o;
+  const int64_t idx = static_cast<int64_t>(blk) * kHlFinOut + o;
+  const float* __restrict__ partials = f.partials;
+  const int G = f.G;
   float s = 0.f;
-  if (idx < npw) {
+  if (idx < f.npw) {
     for (int g0 = gi; g0 < G; g0 += kHlFinGroups * kHlFinBatch) {
       float v[kHlFinBatch];
 #pragma unroll
       for (int u = 0; u < kHlFinBatch; ++u) {
         const int g = g0 + u * kHlFinGroups;
-        v[u] = g < G ? partials[static_cast<int64_t>(g) * npw + idx] : 0.f;
+        v[u] = g < G ? partials[static_cast<int64_t>(g) * f.npw + idx] : 0.f;
       }
 #pragma unroll
       for (int wdt = kHlFinBatch / 2; wdt >= 1; wdt /= 2)
@@ -1764,8 +1777,8 @@ __global__ __launch_bounds__(256) void heads_loss_finish_kernel(
     if (gi < wdt) red[gi][o] += red[gi + wdt][o];
     __syncthreads();
   }
-  const int nv = amax + 2;
-  const int jp = (cpl * nv + 3) / 4 * 4;
+  const int nv = f.amax + 2;
+  const int jp = (f.cpl * nv + 3) / 4 * 4;
   const int64_t nvals = 64 * jp;
   if (gi == 0) {
     const float t = red[0][o];
@@ -1774,23 +1787,24 @@ __global__ __launch_bounds__(256) void heads_loss_finish_kernel(
     const int j = static_cast<int>((idx >> 8) * 4 + (idx & 3));
     if (idx < nvals) {  // [j / 4][lane][j % 4], j = q * nv + slot (j >= cpl * nv: padding)
       const int q = j / nv, slot = j - q * nv;
-      const int64_t col = cpl >= 4 ? 4 * ((q >> 2) * kWave + ln) + (q & 3) : q * kWave + ln;
-      if (j >= cpl * nv) {
+      const int64_t col = f.cpl >= 4 ? 4 * ((q >> 2) * kWave + ln) + (q & 3) : q * kWave + ln;
+      if (j >= f.cpl * nv) {
       } else if (slot == 0) {
-        if (db_h) db_h[col] = t;
+        if (f.db_h) f.db_h[col] = t;
       } else if (slot == nv - 1) {
-        dwc[col] = t;
-      } else if (slot - 1 < A) {
-        dwa[static_cast<int64_t>(slot - 1) * H + col] = t;
+        f.dwc[col] = t;
+      } else if (slot - 1 < f.A) {
+        f.dwa[static_cast<int64_t>(slot - 1) * f.H + col] = t;
       }
-    } else if (idx < nvals + amax + 1) {
+    } else if (idx < nvals + f.amax + 1) {
       const int k = static_cast<int>(idx - nvals);
-      if (k < A) dba[k] = t;
-      else if (k == amax) dbc[0] = t;
+      if (k < f.A) f.dba[k] = t;
+      else if (k == f.amax) f.dbc[0] = t;
     }
   }
   __syncthreads();
-  if (static_cast<int64_t>(blockIdx.x) * kHlFinOut == ls && threadIdx.x == 0) {
+  if (static_cast<int64_t>(blk) * kHlFinOut == f.ls && threadIdx.x == 0) {
+    const LossParams& L = f.L;
     const float pg_loss = tot[0] * L.inv_m;
     const float v_loss = 0.5f * (tot[1] * L.inv_m);
     const float ent = tot[2] * L.inv_m;
@@ -1806,6 +1820,48 @@ __global__ __launch_bounds__(256) void heads_loss_finish_kernel(
     L.stats[OCPPO_STAT_ADV_STD] = L.norm_adv ? L.adv_stats[1] : 0.f;
   }
 }
+
+__global__ __launch_bounds__(256) void heads_loss_finish_kernel(HlFinish f) {
+  hl_finish_block(f, blockIdx.x);
+}
+
+// The finish folded into the split-K combine of the decoder's weight gradient, the next
+// combine the backward runs anyway (ppo_atari_oc.py:605): workgroups [0, nsb) sum the S split
+// blocks (float64, split order, one rounding: bitwise ocppo_sum_splits), the rest are finish
+// workgroups. One launch instead of two; the finish's outputs are read by no kernel before the
+// optimizer step.
+template <int S>
+__global__ __launch_bounds__(256) void sum_splits_hlfin_kernel(const float4* __restrict__ part,
+                                                               int64_t n4, float4* __restrict__ out,
+                                                               int nsb, HlFinish f) {
+  if (static_cast<int>(blockIdx.x) >= nsb) {
+    hl_finish_block(f, blockIdx.x - nsb);
+    return;
+  }
+  const int64_t stride = static_cast<int64_t>(nsb) * blockDim.x;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n4;
+       i += stride) {
+    float4 v[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) v[s] = part[s * n4 + i];
+    double ax = v[0].x, ay = v[0].y, az = v[0].z, aw = v[0].w;
+#pragma unroll
+    for (int s = 1; s < S; ++s) {
+      ax += v[s].x; ay += v[s].y; az += v[s].z; aw += v[s].w;
+    }
+    out[i] = make_float4(static_cast<float>(ax), static_cast<float>(ay), static_cast<float>(az),
+                         static_cast<float>(aw));
+  }
+}
+
+// the deferred-finish record behind the C-ABI's opaque ocppo_deferred_finish_t
+constexpr uint64_t kDeferHeads = 0x6f63707068666e31ull;  // tag of a heads-loss finish
+struct DeferredFinish {
+  uint64_t tag;
+  HlFinish f;
+};
+static_assert(sizeof(DeferredFinish) <= sizeof(ocppo_deferred_finish_t),
+              "ocppo_deferred_finish_t too small");
 
 // Grid of the rows launch: G = min(ceil(M / rows_min), grid_cap) workgroups of rows_per_wg rows
 // (a multiple of the 16-row step of 4 waves x U = 4 rows). rows_min = 16 keeps a config-size
@@ -1873,14 +1929,17 @@ extern "C" size_t ocppo_heads_loss_workspace_bytes(int64_t M, int64_t H, int64_t
   return static_cast<size_t>(G * npw) * sizeof(float);
 }
 
-extern "C" int ocppo_heads_loss_fwd_bwd(
-    ocppo_stream_t stream, const float* h, int64_t M, int64_t H, const float* w_actor,
-    const float* b_actor, const float* w_critic, const float* b_critic, int64_t A,
-    const int64_t* mb_actions, const float* mb_logprobs, const float* mb_advantages,
-    const float* mb_returns, const float* mb_values, const float* adv_stats, double clip_coef,
-    double ent_coef, double vf_coef, int norm_adv, int clip_vloss, float* gp, float* db_h,
-    float* dwa, float* dwc, float* dba, float* dbc, float* stats, float* dlogits, float* dvalue,
-    void* workspace, size_t workspace_bytes) {
+// validates, launches the rows kernel and fills the finish record
+static int heads_loss_rows(ocppo_stream_t stream, const float* h, int64_t M, int64_t H,
+                           const float* w_actor, const float* b_actor, const float* w_critic,
+                           const float* b_critic, int64_t A, const int64_t* mb_actions,
+                           const float* mb_logprobs, const float* mb_advantages,
+                           const float* mb_returns, const float* mb_values,
+                           const float* adv_stats, double clip_coef, double ent_coef,
+                           double vf_coef, int norm_adv, int clip_vloss, float* gp, float* db_h,
+                           float* dwa, float* dwc, float* dba, float* dbc, float* stats,
+                           float* dlogits, float* dvalue, void* workspace,
+                           size_t workspace_bytes, HlFinish& fin) {
   OCPPO_REQUIRE(M >= 1 && M <= INT32_MAX && hl_width_ok(H) && A >= 1 && A <= 7,
                 "ocppo_heads_loss_fwd_bwd: bad sizes M=%lld H=%lld A=%lld (H in {64, 128, 256, "
                 "512}, 1 <= A <= 7)", (long long)M, (long long)H, (long long)A);
@@ -1945,8 +2004,97 @@ extern "C" int ocppo_heads_loss_fwd_bwd(
     default: launch_heads_loss<7, false>(s, P, (int)G, cpl); break;
   }
   if (int rc = check_launch("ocppo_heads_loss_fwd_bwd")) return rc;
-  hipLaunchKernelGGL(heads_loss_finish_kernel, dim3((npw + kHlFinOut - 1) / kHlFinOut),
-                     dim3(256), 0, s, static_cast<const float*>(workspace), (int)G, npw, ls, H,
-                     (int)A, hl_amax(A), cpl, db_h, dwa, dwc, dba, dbc, L);
+  fin = HlFinish{static_cast<const float*>(workspace), (int)G, (int)A, hl_amax(A), cpl,
+                 npw, ls, H, db_h, dwa, dwc, dba, dbc, L,
+                 static_cast<int>((npw + kHlFinOut - 1) / kHlFinOut)};
+  return OCPPO_OK;
+}
+
+extern "C" int ocppo_heads_loss_fwd_bwd(
+    ocppo_stream_t stream, const float* h, int64_t M, int64_t H, const float* w_actor,
+    const float* b_actor, const float* w_critic, const float* b_critic, int64_t A,
+    const int64_t* mb_actions, const float* mb_logprobs, const float* mb_advantages,
+    const float* mb_returns, const float* mb_values, const float* adv_stats, double clip_coef,
+    double ent_coef, double vf_coef, int norm_adv, int clip_vloss, float* gp, float* db_h,
+    float* dwa, float* dwc, float* dba, float* dbc, float* stats, float* dlogits, float* dvalue,
+    void* workspace, size_t workspace_bytes) {
+  HlFinish fin;
+  if (int rc = heads_loss_rows(stream, h, M, H, w_actor, b_actor, w_critic, b_critic, A,
+                               mb_actions, mb_logprobs, mb_advantages, mb_returns, mb_values,
+                               adv_stats, clip_coef, ent_coef, vf_coef, norm_adv, clip_vloss, gp,
+                               db_h, dwa, dwc, dba, dbc, stats, dlogits, dvalue, workspace,
+                               workspace_bytes, fin))
+    return rc;
+  hipLaunchKernelGGL(heads_loss_finish_kernel, dim3(fin.blocks), dim3(256), 0, as_stream(stream),
+                     fin);
   return check_launch("ocppo_heads_loss_fwd_bwd/finish");
+}
+
+extern "C" int ocppo_heads_loss_rows(
+    ocppo_stream_t stream, const float* h, int64_t M, int64_t H, const float* w_actor,
+    const float* b_actor, const float* w_critic, const float* b_critic, int64_t A,
+    const int64_t* mb_actions, const float* mb_logprobs, const float* mb_advantages,
+    const float* mb_returns, const float* mb_values, const float* adv_stats, double clip_coef,
+    double ent_coef, double vf_coef, int norm_adv, int clip_vloss, float* gp, float* db_h,
+    float* dwa, float* dwc, float* dba, float* dbc, float* stats, float* dlogits, float* dvalue,
+    void* workspace, size_t workspace_bytes, ocppo_deferred_finish_t* finish) {
+  OCPPO_REQUIRE(finish, "ocppo_heads_loss_rows: null finish record");
+  DeferredFinish d;
+  d.tag = kDeferHeads;
+  if (int rc = heads_loss_rows(stream, h, M, H, w_actor, b_actor, w_critic, b_critic, A,
+                               mb_actions, mb_logprobs, mb_advantages, mb_returns, mb_values,
+                               adv_stats, clip_coef, ent_coef, vf_coef, norm_adv, clip_vloss, gp,
+                               db_h, dwa, dwc, dba, dbc, stats, dlogits, dvalue, workspace,
+                               workspace_bytes, d.f))
+    return rc;
+  memset(finish, 0, sizeof(*finish));
+  memcpy(finish, &d, sizeof(d));
+  return OCPPO_OK;
+}
+
+static int deferred_of(const ocppo_deferred_finish_t* finish, DeferredFinish& d,
+                       const char* who) {
+  OCPPO_REQUIRE(finish, "%s: null finish record", who);
+  memcpy(&d, finish, sizeof(d));
+  OCPPO_REQUIRE(d.tag == kDeferHeads, "%s: not a finish record of ocppo_heads_loss_rows", who);
+  return OCPPO_OK;
+}
+
+extern "C" int ocppo_deferred_finish_run(ocppo_stream_t stream,
+                                         const ocppo_deferred_finish_t* finish) {
+  DeferredFinish d;
+  if (int rc = deferred_of(finish, d, "ocppo_deferred_finish_run")) return rc;
+  clear_stale_error();
+  hipLaunchKernelGGL(heads_loss_finish_kernel, dim3(d.f.blocks), dim3(256), 0, as_stream(stream),
+                     d.f);
+  return check_launch("ocppo_deferred_finish_run");
+}
+
+extern "C" int ocppo_sum_splits_finish(ocppo_stream_t stream, const float* part, int64_t S,
+                                       int64_t n, float* out,
+                                       const ocppo_deferred_finish_t* finish) {
+  OCPPO_REQUIRE(n >= 4 && n % 4 == 0 && (S == 1 || S == 2 || S == 4 || S == 8 || S == 16),
+                "ocppo_sum_splits_finish: bad sizes S=%lld n=%lld (S in {1,2,4,8,16}, n %% 4 == 0)",
+                (long long)S, (long long)n);
+  OCPPO_REQUIRE(part && out, "ocppo_sum_splits_finish: null pointer");
+  OCPPO_REQUIRE(aligned16(part) && aligned16(out),
+                "ocppo_sum_splits_finish: part and out must be 16-B aligned");
+  DeferredFinish d;
+  if (int rc = deferred_of(finish, d, "ocppo_sum_splits_finish")) return rc;
+  clear_stale_error();
+  const int64_t n4 = n / 4;
+  const int nsb = grid_for(n4, 256);
+  const dim3 grid(static_cast<unsigned>(nsb + d.f.blocks)), block(256);
+  const float4* p4 = reinterpret_cast<const float4*>(part);
+  float4* o4 = reinterpret_cast<float4*>(out);
+  const int ns = nsb;
+  hipStream_t s = as_stream(stream);
+  switch (S) {
+    case 1: hipLaunchKernelGGL(sum_splits_hlfin_kernel<1>, grid, block, 0, s, p4, n4, o4, ns, d.f); break;
+    case 2: hipLaunchKernelGGL(sum_splits_hlfin_kernel<2>, grid, block, 0, s, p4, n4, o4, ns, d.f); break;
+    case 4: hipLaunchKernelGGL(sum_splits_hlfin_kernel<4>, grid, block, 0, s, p4, n4, o4, ns, d.f); break;
+    case 8: hipLaunchKernelGGL(sum_splits_hlfin_kernel<8>, grid, block, 0, s, p4, n4, o4, ns, d.f); break;
+    default: hipLaunchKernelGGL(sum_splits_hlfin_kernel<16>, grid, block, 0, s, p4, n4, o4, ns, d.f); break;
+  }
+  return check_launch("ocppo_sum_splits_finish");
 }

@@ -6,7 +6,7 @@
 //   norm kernel : grid-strided partial sums of (g * grad_scale)^2 per workgroup (16-B loads),
 //                 one plain store per workgroup; workgroup 0 also advances the step counter
 //                 (the only writer of it; the adam kernel, next on the stream, only reads it)
-//   adam kernel : every workgroup first combines the <= 256 partials itself, in workgroup order
+//   adam kernel : every workgroup first combines the <= 1024 partials itself, in a fixed order
 //                 (the same fixed-order sum in every workgroup, so every one derives the same
 //                 total_norm, clip = min(max_norm / (total_norm + 1e-6), 1), step_size =
 //                 lr / (1 - beta1^step), bc2_sqrt = sqrt(1 - beta2^step)), then
@@ -21,8 +21,8 @@
 namespace ocppo {
 
 constexpr int kOptThreads = 256;
-constexpr int kOptBlocks = 256;  // grid-stride cap for the norm pass: one workgroup per CU, at
-                                 // most 256 partials for every adam workgroup to combine
+constexpr int kOptBlocks = 1024;  // grid-stride cap for the norm pass (4 workgroups per CU), at
+                                  // most 1024 partials for every adam workgroup to combine
 
 // scalars layout (f32): see include/ocppo.h OCPPO_OPT_*
 enum { S_STEP = 0, S_TOTAL_NORM = 1, S_CLIP = 2, S_STEP_SIZE = 3, S_BC2_SQRT = 4 };
@@ -35,7 +35,7 @@ __global__ __launch_bounds__(kOptThreads) void grad_norm_kernel(
   const int64_t P4 = P / 4;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kOptThreads;
   // kNormU grid-strided float4 loads in flight per thread, then accumulated in index order
-  constexpr int kNormU = 8;
+  constexpr int kNormU = 4;
   for (int64_t i0 = static_cast<int64_t>(blockIdx.x) * kOptThreads + threadIdx.x; i0 < P4;
        i0 += kNormU * stride) {
     float4 x[kNormU];
@@ -115,6 +115,18 @@ __global__ __launch_bounds__(kOptThreads) void adam_kernel(
     float* __restrict__ v, int64_t P, float grad_scale, float b1, float b2, float eps,
     float max_norm, const float* __restrict__ lr, const float* __restrict__ partials, int nb,
     float* __restrict__ scalars) {
+  // the first element group's loads are issued before the scalars are combined: their latency
+  // hides the partials' combine (at config 2 every thread has about one group)
+  const int64_t P4 = P / 4;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kOptThreads;
+  int64_t i = static_cast<int64_t>(blockIdx.x) * kOptThreads + threadIdx.x;
+  float4 pp{}, gg{}, mm{}, vv{};
+  if (i < P4) {
+    pp = reinterpret_cast<float4*>(p)[i];
+    gg = reinterpret_cast<const float4*>(g)[i];
+    mm = reinterpret_cast<float4*>(m)[i];
+    vv = reinterpret_cast<float4*>(v)[i];
+  }
   const AdamScalars sc = adam_scalars(partials, nb, max_norm, lr, b1, b2, scalars);
   if (blockIdx.x == 0 && threadIdx.x == 0) {  // the reported figures (read after the step)
     scalars[S_TOTAL_NORM] = sc.total;
@@ -123,13 +135,7 @@ __global__ __launch_bounds__(kOptThreads) void adam_kernel(
     scalars[S_BC2_SQRT] = sc.bc2_sqrt;
   }
   const float clip = sc.clip, step_size = sc.step_size, bc2_sqrt = sc.bc2_sqrt;
-  const int64_t P4 = P / 4;
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * kOptThreads;
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kOptThreads + threadIdx.x; i < P4; i += stride) {
-    float4 pp = reinterpret_cast<float4*>(p)[i];
-    const float4 gg = reinterpret_cast<const float4*>(g)[i];
-    float4 mm = reinterpret_cast<float4*>(m)[i];
-    float4 vv = reinterpret_cast<float4*>(v)[i];
+  for (; i < P4; i += stride) {
     adam_elem(pp.x, (gg.x * grad_scale) * clip, mm.x, vv.x, b1, b2, step_size, bc2_sqrt, eps);
     adam_elem(pp.y, (gg.y * grad_scale) * clip, mm.y, vv.y, b1, b2, step_size, bc2_sqrt, eps);
     adam_elem(pp.z, (gg.z * grad_scale) * clip, mm.z, vv.z, b1, b2, step_size, bc2_sqrt, eps);
@@ -137,6 +143,12 @@ __global__ __launch_bounds__(kOptThreads) void adam_kernel(
     reinterpret_cast<float4*>(p)[i] = pp;
     reinterpret_cast<float4*>(m)[i] = mm;
     reinterpret_cast<float4*>(v)[i] = vv;
+    if (i + stride < P4) {
+      pp = reinterpret_cast<float4*>(p)[i + stride];
+      gg = reinterpret_cast<const float4*>(g)[i + stride];
+      mm = reinterpret_cast<float4*>(m)[i + stride];
+      vv = reinterpret_cast<float4*>(v)[i + stride];
+    }
   }
   if (blockIdx.x == 0)
     for (int64_t i = 4 * P4 + threadIdx.x; i < P; i += kOptThreads)

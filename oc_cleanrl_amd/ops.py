@@ -248,13 +248,36 @@ def heads_loss_ok(h, A: int) -> bool:
             H in HEADS_LOSS_WIDTHS and 1 <= A <= 7 and h.data_ptr() % 16 == 0)
 
 
+class DeferredFinish:
+    """The finish of ocppo_heads_loss_rows (the tree over the heads-loss records that writes the
+    heads' and decoder-bias gradients and the loss statistics), held as the C-ABI's host record
+    until a later launch on the same stream runs it: sum_splits(..., finish=) folds it into a
+    split-K combine, run() launches it alone. It must run exactly once (pending: not yet)."""
+
+    def __init__(self, device):
+        self.device = device
+        self.rec = (ctypes.c_uint64 * 64)()
+        self.pending = False  # filled by a rows launch, not yet run
+        self.filled = False   # holds a record (a timer replay may run it again: same writes)
+
+    def ptr(self) -> int:
+        return ctypes.addressof(self.rec)
+
+    def run(self):
+        if self.pending:
+            self.pending = False
+            call("ocppo_deferred_finish_run", _stream(self.device), self.ptr())
+
+
 def heads_loss_fwd_bwd(h, wa, ba, wc, bc, mb_actions, mb_logprobs, mb_advantages, mb_returns,
                        mb_values, *, adv_stats, clip_coef, ent_coef, vf_coef, norm_adv: bool,
                        clip_vloss: bool, gp=None, db_h=None, dwa=None, dwc=None, dba=None,
-                       dbc=None, stats=None, dlogits=None, dvalue=None):
+                       dbc=None, stats=None, dlogits=None, dvalue=None, defer=None):
     """The policy heads' forward, the fused PPO loss and the heads' backward with the decoder's
     ReLU mask, from the decoder output h [M, H] (include/ocppo.h ocppo_heads_loss_fwd_bwd).
-    mb_* are the minibatch's prepared records [M]. Returns (gp, db_h, dwa, dwc, dba, dbc, stats)."""
+    mb_* are the minibatch's prepared records [M]. Returns (gp, db_h, dwa, dwc, dba, dbc, stats).
+    defer = a DeferredFinish: only the rows kernel runs now (ocppo_heads_loss_rows); db_h, dwa,
+    dwc, dba, dbc and stats are written when the caller runs the finish."""
     M, H = h.shape
     A = wa.shape[0]
     dev = h.device
@@ -270,7 +293,8 @@ def heads_loss_fwd_bwd(h, wa, ba, wc, bc, mb_actions, mb_logprobs, mb_advantages
     if ws is None:
         nb = int(_lib.LIB.ocppo_heads_loss_workspace_bytes(M, H, A))
         ws = _HL_WS[key] = torch.zeros(nb // 4, dtype=f, device=dev)
-    call("ocppo_heads_loss_fwd_bwd", _stream(dev), _check(h, "h", f, dev, M * H), M, H,
+    call("ocppo_heads_loss_rows" if defer is not None else "ocppo_heads_loss_fwd_bwd",
+         _stream(dev), _check(h, "h", f, dev, M * H), M, H,
          _check(wa, "wa", f, dev, A * H), _check(ba, "ba", f, dev, A), _check(wc, "wc", f, dev, H),
          _check(bc, "bc", f, dev, 1), A, _check(mb_actions, "mb_actions", torch.int64, dev, M),
          _check(mb_logprobs, "mb_logprobs", f, dev, M),
@@ -282,7 +306,10 @@ def heads_loss_fwd_bwd(h, wa, ba, wc, bc, mb_actions, mb_logprobs, mb_advantages
          _check(dwa, "dwa", f, dev, A * H), _check(dwc, "dwc", f, dev, H),
          _check(dba, "dba", f, dev, A), _check(dbc, "dbc", f, dev, 1),
          _check(stats, "stats", f, dev, len(STAT_NAMES)), _opt(dlogits, "dlogits", f, dev, M * A),
-         _opt(dvalue, "dvalue", f, dev, M), ws.data_ptr(), ws.numel() * 4)
+         _opt(dvalue, "dvalue", f, dev, M), ws.data_ptr(), ws.numel() * 4,
+         *((defer.ptr(),) if defer is not None else ()))
+    if defer is not None:
+        defer.pending = defer.filled = True
     return gp, db_h, dwa, dwc, dba, dbc, stats
 
 
@@ -832,14 +859,21 @@ def sum_splits_ok(part, out) -> bool:
             and part[0].numel() % 4 == 0 and part.data_ptr() % 16 == 0 and out.data_ptr() % 16 == 0)
 
 
-def sum_splits(part, out=None):
+def sum_splits(part, out=None, finish=None):
     """out = part.sum(0) over the S split-K partial blocks of a weight gradient, in split order
-    (added in f64, rounded once), in one streaming pass (part [S, ...] f32 contiguous, S in {1, 2, 4, 8, 16})."""
+    (added in f64, rounded once), in one streaming pass (part [S, ...] f32 contiguous, S in {1, 2, 4, 8, 16}).
+    finish = a filled DeferredFinish: run by extra workgroups of the same launch
+    (ocppo_sum_splits_finish; out bitwise the same)."""
     S = part.shape[0]
     dev = part.device
     if out is None:
         out = torch.empty(part.shape[1:], dtype=torch.float32, device=dev)
     n = part[0].numel()
+    if finish is not None and finish.filled:
+        finish.pending = False
+        call("ocppo_sum_splits_finish", _stream(dev), _check(part, "part", torch.float32, dev), S,
+             n, _check(out, "out", torch.float32, dev, n), finish.ptr())
+        return out
     call("ocppo_sum_splits", _stream(dev), _check(part, "part", torch.float32, dev), S, n,
          _check(out, "out", torch.float32, dev, n))
     return out

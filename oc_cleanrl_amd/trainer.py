@@ -395,6 +395,7 @@ class PPOTrainer:
                                  self.H in ops.HEADS_LOSS_WIDTHS and self.A <= 7)
         self.gp_tail = (torch.empty((self.M, self.H), dtype=f32, device=dev)
                         if self.fused_heads_loss else None)
+        self.hl_finish = ops.DeferredFinish(dev) if self.fused_heads_loss else None
         self.b_obs = self.obs[:T].view((T * N,) + self.obs_shape)
         self.wplanes, self.wplanes_built = None, False  # built at the first minibatch
         # GAE's per-sample records for the minibatch gather (ops.sample_records)
@@ -719,6 +720,9 @@ class PPOTrainer:
         a, ag, mb = self.args, self.agent, self.mb
         sl = slice(j * self.M, (j + 1) * self.M)
         box["premasked"] = True  # the decoder's _LinearAct backward gets gp with its mask applied
+        # the heads-loss finish (heads' and decoder-bias grads, loss statistics) rides in the
+        # decoder's split-K weight-gradient combine (agents._weight_grad), or runs alone below
+        box["finish"] = self.hl_finish
         h = hidden.detach()
         self.timer.bracket("heads_loss", lambda: ops.heads_loss_fwd_bwd(
             h, ag.actor.weight, ag.actor.bias, ag.critic.weight, ag.critic.bias,
@@ -727,8 +731,9 @@ class PPOTrainer:
             clip_coef=a.clip_coef, ent_coef=a.ent_coef, vf_coef=a.vf_coef, norm_adv=a.norm_adv,
             clip_vloss=a.clip_vloss, gp=self.gp_tail, db_h=box["bias"].grad,
             dwa=ag.actor.weight.grad, dwc=ag.critic.weight.grad, dba=ag.actor.bias.grad,
-            dbc=ag.critic.bias.grad, stats=self.stats[j]))
+            dbc=ag.critic.bias.grad, stats=self.stats[j], defer=self.hl_finish))
         torch.autograd.backward(hidden, self.gp_tail)
+        self.hl_finish.run()  # no-op when the combine took it
         return True
 
     def _backward_low(self, j: int):

@@ -62,6 +62,24 @@ def test_invalid_arguments_report_errors_without_launch(lib):
         lib.call("ocppo_gather_rows", None, None, 7, None, 4, 4, None)
 
 
+def test_deferred_finish_record_is_checked(lib):
+    """ocppo_deferred_finish_run / ocppo_sum_splits_finish refuse a missing record or one no
+    ocppo_heads_loss_rows call filled, before any launch."""
+    L = lib.LIB
+    assert L.ocppo_deferred_finish_run(None, None) == lib.OCPPO_E_INVALID
+    assert b"null finish record" in L.ocppo_last_error()
+    rec = (ctypes.c_uint64 * 64)()
+    assert L.ocppo_deferred_finish_run(None, ctypes.addressof(rec)) == lib.OCPPO_E_INVALID
+    assert b"not a finish record" in L.ocppo_last_error()
+    dummy = ctypes.c_void_p(256)
+    assert L.ocppo_sum_splits_finish(None, dummy, 8, 1024, dummy,
+                                     ctypes.addressof(rec)) == lib.OCPPO_E_INVALID
+    assert b"not a finish record" in L.ocppo_last_error()
+    assert L.ocppo_sum_splits_finish(None, dummy, 3, 1024, dummy,
+                                     ctypes.addressof(rec)) == lib.OCPPO_E_INVALID
+    assert b"bad sizes" in L.ocppo_last_error()
+
+
 def test_zero_sized_calls_are_noops(lib):
     assert lib.LIB.ocppo_gae(None, None, None, None, None, None, 0, 0, 0.99, 0.95, None, None) == 0
     assert lib.LIB.ocppo_gather_rows(None, None, 0, None, 0, 4, None) == 0

@@ -1349,6 +1349,25 @@ def test_heads_loss_equals_heads_then_loss_then_heads_bwd(ops, dev, M, H, A, nor
                                    db_h=torch.empty(H, device=dev), **cfg)
     for x, y in zip((gp, dbh, dwa, dwc, dba, dbc, stats), again):
         assert torch.equal(x, y)  # deterministic
+    # deferred finish: the rows launch alone, then the finish folded into a split-K combine
+    # (ocppo_sum_splits_finish) or run alone (ocppo_deferred_finish_run): bitwise the same
+    part = torch.randn(8, 512, 2048, device=dev, generator=g)
+    for fold in (True, False):
+        fin = ops.DeferredFinish(dev)
+        outs = [torch.full_like(t, float("nan")) for t in (gp, dbh, dwa, dwc, dba, dbc, stats)]
+        ops.heads_loss_fwd_bwd(h, wa, ba, wc, bc, acts, old_lp, adv, ret, val,
+                               adv_stats=st if norm_adv else None, gp=outs[0], db_h=outs[1],
+                               dwa=outs[2], dwc=outs[3], dba=outs[4], dbc=outs[5], stats=outs[6],
+                               defer=fin, **cfg)
+        assert fin.pending and torch.equal(outs[0], gp)
+        if fold:
+            comb = ops.sum_splits(part, finish=fin)
+            assert torch.equal(comb, ops.sum_splits(part))  # the combine itself unchanged
+        else:
+            fin.run()
+        assert not fin.pending
+        for x, y in zip((gp, dbh, dwa, dwc, dba, dbc, stats), outs):
+            assert torch.equal(x, y)
 
 
 @pytest.mark.parametrize("H", [192, 320, 384, 448, 576])

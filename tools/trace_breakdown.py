@@ -35,6 +35,27 @@ def main():
     busy = sum(v[1] for v in per.values())
     print(f"window: {a.iters} iterations, wall {1e-6 * (t1 - t0) / a.iters:.3f} ms/iter, "
           f"kernel busy {1e-6 * busy / a.iters:.3f} ms/iter")
+    # phase split: the rollout runs from the first launch after an iteration's last Adam launch
+    # to the GAE launch; the update from the GAE launch to the last Adam launch
+    gae = [i for i, r in enumerate(win) if "gae" in r["Kernel_Name"]]
+    adam = [i for i, r in enumerate(win) if "adam_kernel" in r["Kernel_Name"]]
+    roll, upd, rbusy = [], [], []
+    for g in gae:
+        prev = [i for i in adam if i < g]
+        nxt = [i for i in adam if i > g]
+        if not prev or not nxt:
+            continue
+        lo = prev[-1] + 1
+        hi = max(i for i in adam if i < (min(j for j in gae if j > g) if any(j > g for j in gae)
+                                          else len(win)))
+        roll.append(int(win[g]["Start_Timestamp"]) - int(win[lo]["Start_Timestamp"]))
+        rbusy.append(sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in win[lo:g]))
+        upd.append(int(win[hi]["End_Timestamp"]) - int(win[g]["Start_Timestamp"]))
+    if roll:
+        n = len(roll)
+        print(f"phases ({n} whole iterations): rollout {1e-6 * sum(roll) / n:.3f} ms "
+              f"({1e-3 * sum(roll) / n / a.T:.2f} us/step, kernel busy "
+              f"{1e-3 * sum(rbusy) / n / a.T:.2f} us/step), update {1e-6 * sum(upd) / n:.3f} ms")
     for name, (n, d) in sorted(per.items(), key=lambda kv: -kv[1][1]):
         print(f"{1e-6 * d / a.iters:8.3f} ms/it {n / a.iters:8.1f} calls/it {1e-3 * d / n:8.2f} us  {name}")
 
