@@ -214,11 +214,23 @@ class KernelTimer:
         return self.mean_us
 
 
+def _quiesce_rccl():
+    """Wait until the RCCL process group's watchdog holds no work of earlier eager collectives:
+    a captured collective joins RCCL's stream into the capture, and the watchdog's hipEventQuery
+    on an older work's event recorded on that stream then fails with hipErrorCapturedEvent and
+    terminates the process (seen once at world 1 with the epoch's all-reduces captured,
+    tests/test_dp_gpu.py). ProcessGroup._wait_for_pending_works is ProcessGroupNCCL's hook for
+    exactly this; other backends have no watchdog events."""
+    if dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl":
+        dist.distributed_c10d._get_default_group()._wait_for_pending_works()
+
+
 def _graph_capture(graph, pool=None):
     """hipGraph capture in thread-local mode: the RCCL process group's watchdog thread polls its
     work events (hipEventQuery) while this thread captures, which global-mode capture turns into
     hipErrorStreamCaptureUnsupported and a process abort (seen once in 3 runs of the 1-rank nccl
     test, tests/test_dp_gpu.py). Only this thread's calls are restricted, as they must be."""
+    _quiesce_rccl()
     return torch.cuda.graph(graph, pool=pool, capture_error_mode="thread_local")
 
 
