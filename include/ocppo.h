@@ -383,6 +383,13 @@ OCPPO_API int ocppo_split_planes(ocppo_stream_t stream, int n, const float* cons
  * ------------------------------------------------------------------------------------------- */
 OCPPO_API int ocppo_sum_splits(ocppo_stream_t stream, const float* part, int64_t S, int64_t n,
                      float* out);
+/* Split-K combine of a forward product with its epilogue — the decoder forward of the update
+ * (architectures/ppo.py:77-80 inside ppo_atari_oc.py:566) as ocppo_gemm_x6 K splits:
+ *   out[m, n] = act(sum_s part[s, m, n] + bias[n])   (part [S, M, N], out [M, N] f32 row-major;
+ * the splits added in split order in double, rounded once, then + bias, then ReLU if relu —
+ * torch._addmm_activation's order). bias [N] or NULL; 16-B aligned; N % 4 == 0. */
+OCPPO_API int ocppo_sum_splits_act(ocppo_stream_t stream, const float* part, int64_t S, int64_t M,
+                                   int64_t N, const float* bias, int relu, float* out);
 OCPPO_API size_t ocppo_relu_bias_grad_workspace_bytes(int64_t R, int64_t N);
 OCPPO_API int ocppo_relu_bias_grad(ocppo_stream_t stream, const float* g, const float* out,
                          float* gp, float* db, int64_t R, int64_t N, void* workspace,

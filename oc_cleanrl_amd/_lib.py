@@ -86,6 +86,7 @@ SIGNATURES: dict[str, tuple[type, list]] = {
     "ocppo_heads_loss_rows": (I, [P, P, I64, I64, P, P, P, P, I64, P, P, P, P, P, P, D, D, D, I,
                                   I, P, P, P, P, P, P, P, P, P, P, SZ, P]),
     "ocppo_sum_splits_finish": (I, [P, P, I64, I64, P, P]),
+    "ocppo_sum_splits_act": (I, [P, P, I64, I64, I64, P, I, P]),
     "ocppo_deferred_finish_run": (I, [P, P]),
     "ocppo_linear_cache_shift": (I, [P, P, I64, P, P, P, P, I64, I64, I64, I64, I]),
     "ocppo_linear_cache_ring": (I, [P, P, I64, P, P, P, P, I64, I64, I64, I64, I64, I]),

@@ -81,6 +81,9 @@ X6_GEMM_DEFAULT = True
 # split over up to 16 workgroups per tile); smaller outputs leave the chip half idle and stay on
 # hipBLASLt (e.g. the decoder forward [4096 x 512] from K = 2048: 84 vs 63 us).
 X6_MIN_TILES, X6_MIN_TILES_DW = 256, 32
+# Forward products with 32-255 such tiles as K-split gemm_x6 + a combine with the bias / ReLU
+# epilogue (ops.x6_fwd_splits: the decoder forward [4096 x 512] from K = 2048)
+X6_FWD_SPLITK = True
 
 
 def x6_route(w) -> bool:
@@ -278,12 +281,19 @@ class _LinearAct(torch.autograd.Function):
                 and x.requires_grad and _x6_dx_shape_ok(x.shape[0], wm.shape[0], x.shape[1])):
             below["premasked"] = True
             ctx.below = below
+        fs = (ops.x6_fwd_splits(x.shape[0], wm.shape[0], x.shape[1])
+              if x6 and X6_FWD_SPLITK else None)
         if _x6(x.shape[0], wm.shape[0], x.shape[1], x6) and ops.linear_x6_ok(x, wm):
             if relu and box is not None:
                 # the ReLU bitmask for the next layer's fused dX epilogue (box consumer)
                 out, box["mbits"] = ops.linear_x6(x, wm, b, relu, mbits=True, planes=pf)
             else:
                 out = ops.linear_x6(x, wm, b, relu, planes=pf)
+        elif fs is not None and ops._x6_operand_ok(x) and ops._x6_operand_ok(wm) and \
+                (b is None or b.data_ptr() % 16 == 0):
+            # K-split partials + the combine with bias / ReLU (no bitmask: a consumer's fused dX
+            # reads the f32 output as its mask)
+            out = ops.linear_x6_split(x, wm, b, relu, fs, planes=pf)
         else:
             out = torch._addmm_activation(b, x, wm.t(), use_gelu=False) if relu else \
                 torch.addmm(b, x, wm.t())

@@ -524,6 +524,73 @@ extern "C" int ocppo_sum_splits(ocppo_stream_t stream, const float* part, int64_
   return check_launch("ocppo_sum_splits");
 }
 
+// ---- split-K combine of a forward product with its epilogue: out[m, n] = act(sum_s part[s, m, n]
+// + bias[n]) (the S partials added in split order in float64, rounded once, then torch's
+// _addmm_activation order: + bias, then ReLU). The update's decoder forward [4096 x 512] from
+// K = 2048 (architectures/ppo.py:77-80) has 128 output tiles: gemm_x6 runs it as 4 K splits of 128
+// tiles each (512 workgroups) and this pass finishes it. Roofline: HBM stream, (S + 1) * 4 B per
+// output element.
+namespace ocppo {
+template <int S>
+__global__ __launch_bounds__(256) void sum_splits_act_kernel(const float4* __restrict__ part,
+                                                             int64_t n4, int64_t N4,
+                                                             const float4* __restrict__ bias,
+                                                             int relu, float4* __restrict__ out) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n4;
+       i += stride) {
+    float4 v[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) v[s] = part[s * n4 + i];
+    double ax = v[0].x, ay = v[0].y, az = v[0].z, aw = v[0].w;
+#pragma unroll
+    for (int s = 1; s < S; ++s) {
+      ax += v[s].x; ay += v[s].y; az += v[s].z; aw += v[s].w;
+    }
+    float4 r = make_float4(static_cast<float>(ax), static_cast<float>(ay),
+                           static_cast<float>(az), static_cast<float>(aw));
+    if (bias) {
+      const float4 b = bias[i % N4];
+      r.x += b.x; r.y += b.y; r.z += b.z; r.w += b.w;
+    }
+    if (relu) {
+      r.x = fmaxf(r.x, 0.f); r.y = fmaxf(r.y, 0.f); r.z = fmaxf(r.z, 0.f); r.w = fmaxf(r.w, 0.f);
+    }
+    out[i] = r;
+  }
+}
+}  // namespace ocppo
+
+extern "C" int ocppo_sum_splits_act(ocppo_stream_t stream, const float* part, int64_t S,
+                                    int64_t M, int64_t N, const float* bias, int relu,
+                                    float* out) {
+  OCPPO_REQUIRE(M >= 0 && N >= 4 && N % 4 == 0 && (S == 1 || S == 2 || S == 4 || S == 8 || S == 16),
+                "ocppo_sum_splits_act: bad sizes S=%lld M=%lld N=%lld (S in {1,2,4,8,16}, "
+                "N %% 4 == 0)", (long long)S, (long long)M, (long long)N);
+  if (M == 0) return OCPPO_OK;
+  OCPPO_REQUIRE(part && out, "ocppo_sum_splits_act: null pointer");
+  OCPPO_REQUIRE(reinterpret_cast<uintptr_t>(part) % 16 == 0 &&
+                    reinterpret_cast<uintptr_t>(out) % 16 == 0 &&
+                    reinterpret_cast<uintptr_t>(bias) % 16 == 0,
+                "ocppo_sum_splits_act: part, out and bias must be 16-B aligned");
+  clear_stale_error();
+  const int64_t n4 = M * N / 4;
+  const dim3 grid(grid_for(n4, 256)), block(256);
+  hipStream_t s = as_stream(stream);
+  const float4* p4 = reinterpret_cast<const float4*>(part);
+  const float4* b4 = reinterpret_cast<const float4*>(bias);
+  float4* o4 = reinterpret_cast<float4*>(out);
+  const int r = relu ? 1 : 0;
+  switch (S) {
+    case 1: hipLaunchKernelGGL(sum_splits_act_kernel<1>, grid, block, 0, s, p4, n4, N / 4, b4, r, o4); break;
+    case 2: hipLaunchKernelGGL(sum_splits_act_kernel<2>, grid, block, 0, s, p4, n4, N / 4, b4, r, o4); break;
+    case 4: hipLaunchKernelGGL(sum_splits_act_kernel<4>, grid, block, 0, s, p4, n4, N / 4, b4, r, o4); break;
+    case 8: hipLaunchKernelGGL(sum_splits_act_kernel<8>, grid, block, 0, s, p4, n4, N / 4, b4, r, o4); break;
+    default: hipLaunchKernelGGL(sum_splits_act_kernel<16>, grid, block, 0, s, p4, n4, N / 4, b4, r, o4); break;
+  }
+  return check_launch("ocppo_sum_splits_act");
+}
+
 // ---- first-layer backward in ONE pass: ReLU-backward + bias gradient + weight gradient -----------
 // For a Linear(+ReLU) layer whose input needs no gradient and has few features (the PPObj
 // encoder's first layer on the object frames, F = 6 / 12 -> 256, architectures/ppo.py:60-84,

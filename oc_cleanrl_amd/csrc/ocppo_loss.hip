@@ -1826,20 +1826,22 @@ __global__ __launch_bounds__(256) void heads_loss_finish_kernel(HlFinish f) {
 }
 
 // The finish folded into the split-K combine of the decoder's weight gradient, the next
-// combine the backward runs anyway (ppo_atari_oc.py:605): workgroups [0, nsb) sum the S split
-// blocks (float64, split order, one rounding: bitwise ocppo_sum_splits), the rest are finish
-// workgroups. One launch instead of two; the finish's outputs are read by no kernel before the
-// optimizer step.
+// combine the backward runs anyway (ppo_atari_oc.py:605): workgroups [0, f.blocks) are finish
+// workgroups (dispatched first: their dependent load -> tree -> store chain is the launch's
+// latency, the streaming combine fills the CUs beside them), the rest sum the S split blocks
+// (float64, split order, one rounding: bitwise ocppo_sum_splits). One launch instead of two; the
+// finish's outputs are read by no kernel before the optimizer step.
 template <int S>
 __global__ __launch_bounds__(256) void sum_splits_hlfin_kernel(const float4* __restrict__ part,
                                                                int64_t n4, float4* __restrict__ out,
                                                                int nsb, HlFinish f) {
-  if (static_cast<int>(blockIdx.x) >= nsb) {
-    hl_finish_block(f, blockIdx.x - nsb);
+  if (static_cast<int>(blockIdx.x) < f.blocks) {
+    hl_finish_block(f, blockIdx.x);
     return;
   }
+  const int sb = static_cast<int>(blockIdx.x) - f.blocks;
   const int64_t stride = static_cast<int64_t>(nsb) * blockDim.x;
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n4;
+  for (int64_t i = static_cast<int64_t>(sb) * blockDim.x + threadIdx.x; i < n4;
        i += stride) {
     float4 v[S];
 #pragma unroll

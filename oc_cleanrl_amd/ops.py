@@ -1005,6 +1005,41 @@ def linear_x6(x, w, b=None, relu=False, out=None, mbits=False, planes=None):
     return out, (bits, t)
 
 
+def x6_fwd_splits(M: int, N: int, K: int):
+    """K splits for a forward product too small for one wave of 128 x 128 tiles (< 256 of them):
+    the fewest splits reaching >= 512 workgroups (two per CU) with >= 256 k per split, on the
+    128 x 128 tile; None when it does not apply. ([4096 x 512] from K = 2048, the decoder: 4
+    splits, 56.8 vs 71.9 us for hipBLASLt's f32 GEMM + epilogue, tools/exp_decoder_fwd.py.)"""
+    if M % 128 or N % 128 or K % 32:
+        return None
+    tiles = (M // 128) * (N // 128)
+    if tiles >= 256 or tiles < 32:
+        return None
+    for S in (2, 4, 8, 16):
+        if K % (32 * S) == 0 and K // S >= 256 and S * tiles >= 512:
+            return S
+    return None
+
+
+def linear_x6_split(x, w, b, relu, splits, out=None, planes=None):
+    """act(x W^T + b) as `splits` K-split gemm_x6 partials + ocppo_sum_splits_act (the partials
+    added in split order in f64, then + bias, then ReLU)."""
+    M, K = x.shape
+    N = w.shape[0]
+    dev = x.device
+    part = torch.empty((splits, M, N), dtype=torch.float32, device=dev)
+    gemm_x6(x, x.stride(0), 1, w, w.stride(0), 1, part, N, M, N, K, splits=splits, split_c=M * N,
+            tile=X6_AUTO, b_planes=planes)
+    out = torch.empty((M, N), dtype=torch.float32, device=dev) if out is None else out
+    f = torch.float32
+    args = (part.data_ptr(), splits, M, N, _opt(b, "bias", f, dev, N), int(bool(relu)),
+            _check(out, "out", f, dev, M * N))
+    keep = (part, out, b)
+    timed(f"sum_splits_act_{splits}x{M}x{N}",
+          lambda: call("ocppo_sum_splits_act", _stream(dev), *args) or keep)
+    return out
+
+
 def dx_x6_ok(g, w) -> bool:
     """dX = g W on gemm_x6: g [M, N] (N % 32 == 0), W [N, K]."""
     return (_x6_operand_ok(g) and _x6_operand_ok(w) and g.shape[1] == w.shape[0]

@@ -455,7 +455,9 @@ class PPOTrainer:
             if not isinstance(m, nn.Linear) or i == 0:
                 continue
             rows = enc_rows if i < ag._flat else self.M
-            if pays(rows, m.out_features, m.in_features):
+            if pays(rows, m.out_features, m.in_features) or (
+                    agents.X6_FWD_SPLITK and m.in_features % 32 == 0 and
+                    ops.x6_fwd_splits(rows, m.out_features, m.in_features) is not None):
                 fwd.append(m.weight)
             if pays(rows, m.in_features, m.out_features):
                 dx.append(m.weight)

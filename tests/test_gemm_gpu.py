@@ -258,3 +258,36 @@ def test_gemm_x6_presplit_b_is_bitwise_the_f32_b(tile):
     # unmasked dX and plain forward through the helpers
     assert torch.equal(ops.dx_x6(gg, w2), ops.dx_x6(gg, w2, planes=w2._ocppo_planes["dx"]))
     assert torch.equal(ops.linear_x6(x, w, b), ops.linear_x6(x, w, b, planes=w._ocppo_planes["fwd"]))
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 512, 2048), (2048, 1024, 2048), (4096, 256, 4096)])
+@pytest.mark.parametrize("planes", [False, True])
+def test_forward_split_k_with_bias_relu_combine(M, N, K, planes):
+    """The K-split forward (ops.linear_x6_split: gemm_x6 partials + ocppo_sum_splits_act) at
+    f32 accuracy; the combine bitwise = the partials added in split order in f64, rounded once,
+    + bias, then ReLU; pre-split weight planes bitwise the in-kernel split."""
+    S = ops.x6_fwd_splits(M, N, K)
+    assert S is not None and S * (M // 128) * (N // 128) >= 512
+    g = torch.Generator(device=DEV).manual_seed(M + N + K)
+    x = _rand(M, K, gen=g)
+    w = _rand(N, K, gen=g, scale=K ** -0.5)
+    b = _rand(N, gen=g, scale=0.1)
+    pre64 = x.double() @ w.double().t() + b.double()
+    scale = x.double().abs() @ w.double().abs().t() + b.double().abs()
+    pl = None
+    if planes:
+        ops.WeightPlanes(fwd=[w]).refresh()
+        pl = w._ocppo_planes["fwd"]
+    out = ops.linear_x6_split(x, w, b, True, S, planes=pl)
+    _check(out, pre64.clamp_min(0), scale, torch._addmm_activation(b, x, w.t()))
+    # the combine itself, against its definition on the same partials
+    part = torch.empty(S, M, N, device=DEV)
+    ops.gemm_x6(x, K, 1, w, K, 1, part, N, M, N, K, splits=S, split_c=M * N, tile=ops.X6_AUTO)
+    acc = part[0].double()
+    for s in range(1, S):
+        acc = acc + part[s].double()
+    want = torch.relu(acc.float() + b)
+    assert torch.equal(out, want)
+    assert torch.equal(ops.linear_x6_split(x, w, b, True, S, planes=pl), out)  # repeatable
+    nob = ops.linear_x6_split(x, w, None, False, S)
+    assert torch.equal(nob, acc.float())
