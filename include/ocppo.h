@@ -361,6 +361,26 @@ OCPPO_API int ocppo_gemm_x6(ocppo_stream_t stream, const float* a, int64_t sam, 
                             int64_t bp_stride);
 
 /* ---------------------------------------------------------------------------------------------
+ * ocppo_gemm_x6 with one operand's rows read through a row table (the update's decoder on the
+ * Flatten of the stacked frame encodings, architectures/ppo.py:77-80, without materialising the
+ * [M, W * E] input of ppo_atari_oc.py:566's b_obs[mb_inds] forward):
+ *   mode 1: A(m, k) = a[gidx[m * gw + k / gseg] * sam + k % gseg]   (sak == 1, K == gw * gseg,
+ *           every split's K range inside one segment: gseg % (K / splits) == 0)
+ *   mode 2: B(n, k) = b[gidx[k * gw + n / gseg] * sbk + n % gseg]   (sbn == 1, N == gw * gseg,
+ *           gseg % 128 == 0, K / splits <= 1024; A m-contiguous, as a weight gradient's g'^T)
+ * gidx int32 (mode 1: [M, gw], mode 2: [K, gw]; e.g. ocppo_frames_expand_index). The 128 x 128
+ * tile (variant 24), M % 128 == N % 128 == 0, (K / 32) % splits == 0; bias / ReLU only with
+ * splits == 1; b_planes (mode 1) as ocppo_gemm_x6's. Bitwise ocppo_gemm_x6 on the gathered
+ * operand written out.
+ * ------------------------------------------------------------------------------------------- */
+OCPPO_API int ocppo_gemm_x6_gather(ocppo_stream_t stream, const float* a, int64_t sam, int64_t sak,
+                                   const float* b, int64_t sbn, int64_t sbk, float* c, int64_t ldc,
+                                   int64_t M, int64_t N, int64_t K, int64_t splits,
+                                   int64_t split_c, const float* bias, int relu,
+                                   const void* b_planes, const int32_t* gidx, int64_t gw,
+                                   int64_t gseg, int mode);
+
+/* ---------------------------------------------------------------------------------------------
  * The exact three-piece bf16 split ocppo_gemm_x6 forms in its K loop, done once per matrix: the
  * update's Linear weights (architectures/ppo.py:60-84) as the B operand of the forward (W [N, K],
  * trans 0) and of dX (W^T, trans 1), after every optimizer step (ppo_atari_oc.py:606) instead of
@@ -475,6 +495,11 @@ OCPPO_API int ocppo_frames_gather(ocppo_stream_t stream, const void* obs, int ob
 OCPPO_API int ocppo_frames_expand(ocppo_stream_t stream, const float* enc, int64_t C, int64_t E,
                         const int32_t* pos_of, const int64_t* perm, int64_t M, const float* dones,
                         int64_t T, int64_t N, int64_t W, float* h_out);
+/* frames_expand's source rows only: idx[i, k] = pos_of[u(perm[i], k)] ([M, W] int32), the row
+ * table ocppo_gemm_x6's gathered operands read (the decoder's input never materialised). */
+OCPPO_API int ocppo_frames_expand_index(ocppo_stream_t stream, const int32_t* pos_of,
+                                        const int64_t* perm, int64_t M, const float* dones,
+                                        int64_t T, int64_t N, int64_t W, int32_t* idx);
 OCPPO_API int ocppo_frames_scatter(ocppo_stream_t stream, const float* dh, int64_t M, int64_t E,
                          const int32_t* uniq, int64_t C, const int32_t* inv, int64_t mb,
                          const float* dones, int64_t T, int64_t N, int64_t W, float* denc_out);

@@ -87,6 +87,9 @@ SIGNATURES: dict[str, tuple[type, list]] = {
                                   I, P, P, P, P, P, P, P, P, P, P, SZ, P]),
     "ocppo_sum_splits_finish": (I, [P, P, I64, I64, P, P]),
     "ocppo_sum_splits_act": (I, [P, P, I64, I64, I64, P, I, P]),
+    "ocppo_gemm_x6_gather": (I, [P, P, I64, I64, P, I64, I64, P, I64, I64, I64, I64, I64, I64, P,
+                                 I, P, P, I64, I64, I]),
+    "ocppo_frames_expand_index": (I, [P, P, P, I64, P, I64, I64, I64, P]),
     "ocppo_deferred_finish_run": (I, [P, P]),
     "ocppo_linear_cache_shift": (I, [P, P, I64, P, P, P, P, I64, I64, I64, I64, I]),
     "ocppo_linear_cache_ring": (I, [P, P, I64, P, P, P, P, I64, I64, I64, I64, I64, I]),

@@ -168,6 +168,24 @@ __global__ __launch_bounds__(256) void frames_expand_kernel(
   }
 }
 
+// idx[i, k] = pos_of[u(i, k)]: frames_expand's source rows alone (the update's decoder GEMMs
+// gather their operand rows through it instead of reading a materialised [M, W, E] copy)
+__global__ __launch_bounds__(256) void frames_expand_index_kernel(
+    const int32_t* __restrict__ pos_of, const int64_t* __restrict__ perm, int64_t M,
+    const float* __restrict__ dones, int64_t N, int W, int32_t* __restrict__ idx) {
+  const int64_t j = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (j >= M * W) return;
+  const int64_t i = j / W;
+  const int k = static_cast<int>(j - i * W);
+  const int64_t b = perm[i];
+  const int t = static_cast<int>(b / N);
+  const int64_t n = b - t * N;
+  const int r = latest_reset(dones, t, n, N, W);
+  int s = t - (W - 1) + k;
+  s = s > r ? s : r;
+  idx[j] = pos_of[(s + W - 1) * N + n];
+}
+
 // denc[c, :] = sum over the (sample row i, slot k) uses of frame uniq[c] in minibatch `mb` of
 // dh[i, k, :], in the fixed order (t ascending, k ascending); zeros for padding ids.
 template <int VEC>
@@ -464,6 +482,20 @@ extern "C" int ocppo_frames_expand(ocppo_stream_t stream, const float* enc, int6
     hipLaunchKernelGGL(frames_expand_kernel<1>, dim3(g), dim3(256), 0, s, enc, E, pos_of, perm, M,
                        dones, N, (int)W, h_out);
   return check_launch("ocppo_frames_expand");
+}
+
+extern "C" int ocppo_frames_expand_index(ocppo_stream_t stream, const int32_t* pos_of,
+                                         const int64_t* perm, int64_t M, const float* dones,
+                                         int64_t T, int64_t N, int64_t W, int32_t* idx) {
+  OCPPO_REQUIRE(M >= 0 && T >= 1 && N >= 1 && W >= 1 && W <= kFramesMaxW &&
+                    (T + W - 1) * N < INT32_MAX && M * W < INT32_MAX,
+                "ocppo_frames_expand_index: bad sizes");
+  if (M == 0) return OCPPO_OK;
+  OCPPO_REQUIRE(pos_of && perm && dones && idx, "ocppo_frames_expand_index: null pointer");
+  clear_stale_error();
+  hipLaunchKernelGGL(frames_expand_index_kernel, dim3(static_cast<unsigned>(ceil_div(M * W, 256))),
+                     dim3(256), 0, as_stream(stream), pos_of, perm, M, dones, N, (int)W, idx);
+  return check_launch("ocppo_frames_expand_index");
 }
 
 extern "C" int ocppo_frames_scatter(ocppo_stream_t stream, const float* dh, int64_t M, int64_t E,

@@ -88,6 +88,10 @@ struct X6Args {
   // B pre-split (ocppo_split_planes): piece p of B(n, k) at bpl[p * bpl_ps + n * bpl_ld + k]
   const uint16_t* bpl;
   int64_t bpl_ld, bpl_ps;
+  // gathered operand rows (ocppo_gemm_x6_gather): the operand's K (mode 1, A) or N (mode 2, B)
+  // dimension is gw segments of gseg, segment s of row r read from source row gidx[r * gw + s]
+  const int32_t* gidx;
+  int64_t gw, gseg;
 };
 
 // Where one tile's outputs go: its row tiles start at row0_base, its dbp partial row is
@@ -186,6 +190,57 @@ struct X6Stage {
           asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r[i][j]) : "v"(q) : "memory");
         else
           r[i][j] = *reinterpret_cast<const floatx4*>(q);
+      }
+    }
+  }
+
+  // k-contiguous operand with gathered rows: roff[i][j] = element offset of piece row (i, j)
+  // (its source row times the row stride, minus the segment start), fixed for a unit whose K
+  // range lies in one segment
+  __device__ static void gather_rows(const int32_t* __restrict__ gidx, int64_t gw, int seg,
+                                     int64_t gseg, int64_t srow, int row0, int t,
+                                     int64_t (&roff)[kPer][4]) {
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int p = t + NT * i;
+      int rq, kq;
+      piece_of(p < kPieces ? p : 0, rq, kq);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        roff[i][j] = static_cast<int64_t>(gidx[static_cast<int64_t>(row0 + 4 * rq + j) * gw + seg]) *
+                         srow - static_cast<int64_t>(seg) * gseg;
+    }
+  }
+  __device__ static void load_rows(const float* __restrict__ src, const int64_t (&roff)[kPer][4],
+                                   int k0, int t, floatx4 (&r)[kPer][4]) {
+    static_assert(KC, "row-gathered loads are for a k-contiguous operand");
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int p = t + NT * i;
+      if (kPieces % NT != 0 && p >= kPieces) continue;
+      int rq, kq;
+      piece_of(p, rq, kq);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        r[i][j] = *reinterpret_cast<const floatx4*>(src + roff[i][j] + (k0 + 4 * kq));
+    }
+  }
+  // row-contiguous operand whose K index (a sample row) picks a gathered source row:
+  // B(n, k) = src[tbl[k - kbase] * sk + coff + n] (tbl = the unit's rows of gidx, in LDS)
+  __device__ static void load_ktbl(const float* __restrict__ src, int64_t sk,
+                                   const int32_t* tbl, int kbase, int64_t coff, int row0, int k0,
+                                   int t, floatx4 (&r)[kPer][4]) {
+    static_assert(!KC, "K-gathered loads are for a row-contiguous operand");
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int p = t + NT * i;
+      if (kPieces % NT != 0 && p >= kPieces) continue;
+      int rq, kq;
+      piece_of(p, rq, kq);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t sr = tbl[k0 + 4 * kq + j - kbase];
+        r[i][j] = *reinterpret_cast<const floatx4*>(src + sr * sk + coff + (row0 + 4 * rq));
       }
     }
   }
@@ -314,9 +369,17 @@ __device__ __forceinline__ int x6_remap(int b, int nb) {
   return (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (b >> 3);
 }
 
+// rows of the gathered-B table per unit (mode 2: the unit's K range, K / splits)
+constexpr int kX6GTbl = 1024;
+
 // One output tile (unit u: split u / (tiles_m tiles_n), then row-major tiles) of the product
-template <int FM, int FN, int WGM, int WGN, bool AKC, bool BKC, bool LO, bool PF2, bool BPL = false>
-__device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int u, X6Place pl_) {
+// GATH: 0 plain operands; 1 A's rows gathered (k-contiguous A, the unit's K range in one
+// segment); 2 B's K index gathered (row-contiguous B, the tile's N range in one segment; gtbl =
+// kX6GTbl ints of LDS)
+template <int FM, int FN, int WGM, int WGN, bool AKC, bool BKC, bool LO, bool PF2, bool BPL = false,
+          int GATH = 0>
+__device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int u, X6Place pl_,
+                                        int32_t* gtbl = nullptr) {
   constexpr int NT = 64 * WGM * WGN;
   constexpr int BM = 16 * FM * WGM, BN = 16 * FN * WGN;
   using SA = X6Stage<BM, AKC, NT>;
@@ -340,6 +403,29 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
   const int64_t tile_id = pl_.id_base + static_cast<int64_t>(tm) * g.tiles_n + tn;
   // the mask epilogue's bitmask word, fetched before the K loop (off the epilogue's critical path)
   const uint64_t bits_in = g.mbits_in ? g.mbits_in[tile_id * NT + t] : 0;
+
+  // operand loads of K step k0 into a register set (GATH: through the gathered row offsets)
+  static_assert(GATH == 0 || (GATH == 1 && AKC) || (GATH == 2 && !BKC && !BPL), "gather modes");
+  int64_t roffA[GATH == 1 ? SA::kPer : 1][4];
+  int64_t coffB = 0;
+  if constexpr (GATH == 1) {
+    const int seg = static_cast<int>((static_cast<int64_t>(kb) * kX6BK) / g.gseg);
+    SA::gather_rows(g.gidx, g.gw, seg, g.gseg, g.sam, m0, t, roffA);
+  } else if constexpr (GATH == 2) {
+    const int segn = static_cast<int>(n0 / g.gseg);
+    coffB = -static_cast<int64_t>(segn) * g.gseg;
+    for (int r = t; r < nk * kX6BK; r += NT)
+      gtbl[r] = g.gidx[static_cast<int64_t>(kb * kX6BK + r) * g.gw + segn];
+    __syncthreads();
+  }
+  auto loadA = [&](int k0, floatx4 (&r)[SA::kPer][4]) {
+    if constexpr (GATH == 1) SA::load_rows(A, roffA, k0, t, r);
+    else SA::load(A, g.sam, g.sak, m0, k0, t, r);
+  };
+  auto loadB = [&](int k0, floatx4 (&r)[SB::kPer][4]) {
+    if constexpr (GATH == 2) SB::load_ktbl(B, g.sbk, gtbl, kb * kX6BK, coffB, n0, k0, t, r);
+    else SB::load(B, g.sbn, g.sbk, n0, k0, t, r);
+  };
 
   floatx4 hi[FM][FN], lo[LO ? FM : 1][LO ? FN : 1];
 #pragma unroll
@@ -382,16 +468,16 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
     const uint16_t* __restrict__ Bp = g.bpl;
     u32x4 pb[PB::kPer];
     floatx4 qa[SA::kPer][4];
-    SA::load(A, g.sam, g.sak, m0, kb * kX6BK, t, ra);
+    loadA(kb * kX6BK, ra);
     PB::load(Bp, g.bpl_ld, g.bpl_ps, n0, kb * kX6BK, t, pb);
-    if (nk > 1) SA::load(A, g.sam, g.sak, m0, (kb + 1) * kX6BK, t, qa);
+    if (nk > 1) loadA((kb + 1) * kX6BK, qa);
     SA::template stash<kProbeA>(la, t, ra);
     PB::stash(lb, t, pb);
     __syncthreads();
     auto step = [&](int kt, floatx4 (&ldA)[SA::kPer][4], floatx4 (&stA)[SA::kPer][4],
                     u32x4 (&pbr)[PB::kPer]) {
       if (kt + 1 < nk) PB::load(Bp, g.bpl_ld, g.bpl_ps, n0, (kb + kt + 1) * kX6BK, t, pbr);
-      if (kt + 2 < nk) SA::load(A, g.sam, g.sak, m0, (kb + kt + 2) * kX6BK, t, ldA);
+      if (kt + 2 < nk) loadA((kb + kt + 2) * kX6BK, ldA);
       compute();
       __syncthreads();
       if (kt + 1 < nk) {
@@ -441,11 +527,20 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
     constexpr int kLoads = 4 * (SA::kPer + SB::kPer);  // loads per step per thread
     static_assert(!ASM || kLoads == 8, "x6_vmwait counts assume 8 loads per step");
     floatx4 rb[SB::kPer][4], qa[SA::kPer][4], qb[SB::kPer][4];
-    SA::template load<ASM>(A, g.sam, g.sak, m0, kb * kX6BK, t, ra);
-    SB::template load<ASM>(B, g.sbn, g.sbk, n0, kb * kX6BK, t, rb);
-    if (nk > 1) {
-      SA::template load<ASM>(A, g.sam, g.sak, m0, (kb + 1) * kX6BK, t, qa);
-      SB::template load<ASM>(B, g.sbn, g.sbk, n0, (kb + 1) * kX6BK, t, qb);
+    if constexpr (GATH != 0) {
+      loadA(kb * kX6BK, ra);
+      loadB(kb * kX6BK, rb);
+      if (nk > 1) {
+        loadA((kb + 1) * kX6BK, qa);
+        loadB((kb + 1) * kX6BK, qb);
+      }
+    } else {
+      SA::template load<ASM>(A, g.sam, g.sak, m0, kb * kX6BK, t, ra);
+      SB::template load<ASM>(B, g.sbn, g.sbk, n0, kb * kX6BK, t, rb);
+      if (nk > 1) {
+        SA::template load<ASM>(A, g.sam, g.sak, m0, (kb + 1) * kX6BK, t, qa);
+        SB::template load<ASM>(B, g.sbn, g.sbk, n0, (kb + 1) * kX6BK, t, qb);
+      }
     }
     if constexpr (ASM) {
       if (nk > 1) {
@@ -463,8 +558,13 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
                     floatx4 (&stA)[SA::kPer][4], floatx4 (&stB)[SB::kPer][4]) {
       const bool issue = kt + 2 < nk;
       if (issue) {
-        SA::template load<ASM>(A, g.sam, g.sak, m0, (kb + kt + 2) * kX6BK, t, ldA);
-        SB::template load<ASM>(B, g.sbn, g.sbk, n0, (kb + kt + 2) * kX6BK, t, ldB);
+        if constexpr (GATH != 0) {
+          loadA((kb + kt + 2) * kX6BK, ldA);
+          loadB((kb + kt + 2) * kX6BK, ldB);
+        } else {
+          SA::template load<ASM>(A, g.sam, g.sak, m0, (kb + kt + 2) * kX6BK, t, ldA);
+          SB::template load<ASM>(B, g.sbn, g.sbk, n0, (kb + kt + 2) * kX6BK, t, ldB);
+        }
       }
       compute();
       __syncthreads();
@@ -568,13 +668,16 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
   if (g.mbits_out) g.mbits_out[tile_id * NT + t] = bits;
 }
 
-template <int FM, int FN, int WGM, int WGN, bool AKC, bool BKC, bool LO, bool PF2, bool BPL = false>
+template <int FM, int FN, int WGM, int WGN, bool AKC, bool BKC, bool LO, bool PF2, bool BPL = false,
+          int GATH = 0>
 __global__ __launch_bounds__(64 * WGM * WGN, OCPPO_X6_OCC) void gemm_x6_kernel(X6Args g) {
   __shared__ __attribute__((aligned(16)))
   unsigned char lds[x6_lds_bytes<FM, FN, WGM, WGN, AKC, BKC>()];
+  __shared__ int32_t gtbl[GATH == 2 ? kX6GTbl : 1];
   const int u = x6_remap(blockIdx.x, gridDim.x);
   if (u >= g.units) return;
-  x6_unit<FM, FN, WGM, WGN, AKC, BKC, LO, PF2, BPL>(g, lds, u, X6Place{g.tiles_m, 0, 0, 1, 0});
+  x6_unit<FM, FN, WGM, WGN, AKC, BKC, LO, PF2, BPL, GATH>(g, lds, u,
+                                                         X6Place{g.tiles_m, 0, 0, 1, 0}, gtbl);
 }
 
 // Mixed tiles: workgroups [0, nbig) take the 128 x 128 tiles of rows [0, mbig) (dispatched
@@ -686,6 +789,23 @@ static bool launch_x6(hipStream_t s, int tile, bool akc, bool bkc, X6Args& g) {
     case 6: launch_x6_t<4, 2, 2, 2, false, false>(s, akc, bkc, g); return true;
     default: launch_x6_t<2, 2, 2, 2, false, false>(s, akc, bkc, g); return true;
   }
+}
+
+// gathered products on the 128 x 128 tile (variant 24): mode 1 (forward, k-contiguous A and B or
+// B pre-split), mode 2 (weight gradient, m-contiguous A, n-contiguous gathered B)
+static void launch_x6_gather(hipStream_t s, int mode, X6Args& g) {
+  g.tiles_m = g.M / 128;
+  g.tiles_n = g.N / 128;
+  const dim3 grid(g.units), block(256);
+  if (mode == 1 && g.bpl)
+    hipLaunchKernelGGL((gemm_x6_kernel<4, 4, 2, 2, true, true, false, true, true, 1>), grid, block,
+                       0, s, g);
+  else if (mode == 1)
+    hipLaunchKernelGGL((gemm_x6_kernel<4, 4, 2, 2, true, true, false, true, false, 1>), grid, block,
+                       0, s, g);
+  else
+    hipLaunchKernelGGL((gemm_x6_kernel<4, 4, 2, 2, false, false, false, true, false, 2>), grid,
+                       block, 0, s, g);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -838,4 +958,54 @@ extern "C" int ocppo_gemm_x6(ocppo_stream_t stream, const float* a, int64_t sam,
   const bool akc = sak == 1, bkc = sbk == 1;
   OCPPO_REQUIRE(launch_x6(s, tile, akc, bkc, g), "ocppo_gemm_x6: variant %d not built", tile);
   return check_launch("ocppo_gemm_x6");
+}
+
+// ocppo_gemm_x6 with one operand's rows gathered through a row table (include/ocppo.h)
+extern "C" int ocppo_gemm_x6_gather(ocppo_stream_t stream, const float* a, int64_t sam,
+                                    int64_t sak, const float* b, int64_t sbn, int64_t sbk,
+                                    float* c, int64_t ldc, int64_t M, int64_t N, int64_t K,
+                                    int64_t splits, int64_t split_c, const float* bias, int relu,
+                                    const void* b_planes, const int32_t* gidx, int64_t gw,
+                                    int64_t gseg, int mode) {
+  OCPPO_REQUIRE(M >= 128 && N >= 128 && K >= 32 && splits >= 1 && M <= INT32_MAX &&
+                    N <= INT32_MAX && K <= INT32_MAX && M % 128 == 0 && N % 128 == 0 &&
+                    K % kX6BK == 0 && (K / kX6BK) % splits == 0,
+                "ocppo_gemm_x6_gather: bad sizes M=%lld N=%lld K=%lld splits=%lld (128 x 128 "
+                "tiles, K / 32 steps split evenly)", (long long)M, (long long)N, (long long)K,
+                (long long)splits);
+  OCPPO_REQUIRE(a && (b || b_planes) && c && gidx, "ocppo_gemm_x6_gather: null pointer");
+  OCPPO_REQUIRE(mode == 1 || mode == 2, "ocppo_gemm_x6_gather: mode %d (1: A rows, 2: B rows)",
+                mode);
+  OCPPO_REQUIRE(reinterpret_cast<uintptr_t>(a) % 16 == 0 && reinterpret_cast<uintptr_t>(b) % 16 == 0,
+                "ocppo_gemm_x6_gather: A and B must be 16-B aligned");
+  OCPPO_REQUIRE(ldc >= N && (splits == 1 || (bias == nullptr && !relu)),
+                "ocppo_gemm_x6_gather: ldc >= N; bias / ReLU need splits == 1");
+  const int64_t kps = K / splits;  // K per split
+  if (mode == 1) {
+    // A(m, k) = a[gidx[m * gw + k / gseg] * sam + k % gseg]: each split's K range in one segment
+    OCPPO_REQUIRE(sak == 1 && sam % 4 == 0 && gw >= 1 && gseg % kX6BK == 0 && gw * gseg == K &&
+                      gseg % kps == 0,
+                  "ocppo_gemm_x6_gather: mode 1 needs a k-contiguous A (row stride %% 4 == 0), "
+                  "K = gw x gseg and every split inside one segment (gw=%lld gseg=%lld K=%lld "
+                  "splits=%lld)", (long long)gw, (long long)gseg, (long long)K, (long long)splits);
+    OCPPO_REQUIRE(b_planes != nullptr || (sbk == 1 && sbn >= K && sbn % 4 == 0),
+                  "ocppo_gemm_x6_gather: mode 1 needs a k-contiguous B or its planes");
+  } else {
+    // B(n, k) = b[gidx[k * gw + n / gseg] * sbk + n % gseg]: each 128-column tile in one segment
+    OCPPO_REQUIRE(sbn == 1 && sbk % 4 == 0 && gw >= 1 && gseg % 128 == 0 && gw * gseg == N &&
+                      kps <= kX6GTbl && b_planes == nullptr,
+                  "ocppo_gemm_x6_gather: mode 2 needs an n-contiguous B (row stride %% 4 == 0), "
+                  "N = gw x gseg with gseg %% 128 == 0, K / splits <= %d rows and no planes",
+                  kX6GTbl);
+    OCPPO_REQUIRE(sam == 1 && sak >= M && sak % 4 == 0,
+                  "ocppo_gemm_x6_gather: mode 2 needs an m-contiguous A");
+  }
+  const int64_t units = splits * (M / 128) * (N / 128);
+  OCPPO_REQUIRE(units <= INT32_MAX / 2, "ocppo_gemm_x6_gather: too large");
+  X6Args g{a, sam, sak, b_planes ? nullptr : b, sbn, sbk, c, ldc, bias, relu ? 1 : 0, (int)M,
+           (int)N, (int)K, 0, 0, (int)units, (int)splits, split_c, nullptr, 0, nullptr, nullptr,
+           nullptr, 0, static_cast<const uint16_t*>(b_planes), K, N * K, gidx, gw, gseg};
+  clear_stale_error();
+  launch_x6_gather(as_stream(stream), mode, g);
+  return check_launch("ocppo_gemm_x6_gather");
 }

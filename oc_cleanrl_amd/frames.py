@@ -154,6 +154,111 @@ class _FramesExpand(torch.autograd.Function):
         return denc, None, None, None, None, None, None, None, None, None, None
 
 
+# The decoder's Linear+ReLU reading its input rows straight from the distinct-frame encodings
+# (frames_expand never materialised): forward and weight gradient gather the rows through an
+# [M, W] row table (ocppo_gemm_x6_gather), dX goes to the frame scatter as before.
+FUSED_DECODE_GATHER = True
+
+
+class _DecodeFrames(torch.autograd.Function):
+    """hidden = relu(expand(enc) Wd^T + bd) (architectures/ppo.py:77-80 on the Flatten of the
+    stacked frame encodings) without the [M, W * E] copy: idx = frames_expand_index(...) holds
+    each (sample, slot)'s source row; the forward is W K-splits of gemm_x6 whose A rows are
+    gathered through idx (split k = stack slot k) + the combine with bias / ReLU
+    (ocppo_sum_splits_act); backward: dX = g' Wd on gemm_x6 -> the frame scatter (with the last
+    encoder layer's ReLU backward when enc carries its box, as _FramesExpand), dW = g'^T
+    expand(enc) with the rows gathered again (mode 2) + the split-K combine, which also runs the
+    heads-loss finish when one is pending. g' = the grad masked by the fused heads (box
+    premasked, bias grad already written) or masked here."""
+
+    @staticmethod
+    def forward(ctx, enc, w, b, pos_of, perm, dones, uniq, inv, mb, T, N, W, enc_box, box):
+        from . import agents
+
+        E = enc.shape[1]
+        idx = ops.timed("frames_expand_index",
+                        lambda: ops.frames_expand_index(pos_of, perm, dones, T, N, W))
+        out = ops.linear_x6_split(enc, w, b, True, W, planes=agents._planes(w, "fwd"),
+                                  gather=(idx, E))
+        fuse = (FUSED_SCATTER_RELU and enc_box is not None and not enc_box["premasked"] and
+                E % 4 == 0)
+        if fuse:
+            enc_box["premasked"] = True
+        ctx.save_for_backward(enc, idx, uniq, inv, dones, out)
+        ctx.params, ctx.box, ctx.enc_box = (w, b), box, (enc_box if fuse else None)
+        ctx.geom = (int(mb), T, N, W, perm.numel())
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        from . import agents
+
+        enc, idx, uniq, inv, dones, out = ctx.saved_tensors
+        w, b = ctx.params
+        box = ctx.box
+        mb, T, N, W, M = ctx.geom
+        g = g.contiguous()
+        if box["premasked"]:
+            gp = g
+        else:
+            gp = torch.ops.aten.threshold_backward(g, out, 0)
+            torch.sum(gp, 0, out=b.grad)
+        dh = agents._dx(gp, w, True, agents._planes(w, "dx")).view(M, W, -1)
+        if ctx.enc_box is not None:
+            denc, part = ops.timed("frames_scatter_relu", lambda: ops.frames_scatter_relu(
+                dh, uniq, inv, mb, dones, T, N, W, out=enc))
+            ctx.enc_box["dbp"] = part
+        else:
+            denc = ops.timed("frames_scatter", lambda: ops.frames_scatter(dh, uniq, inv, mb, dones,
+                                                                          T, N, W))
+        S = agents._x6_splits(M, w.shape[0], w.shape[1])[0]
+        wpart = ops.dw_x6_parts_gather(gp, enc, idx, S)
+        fin = box.get("finish")
+        if fin is not None and fin.pending:
+            ops.timed(f"sum_splits_fin_{S}x{w.shape[0]}x{w.shape[1]}",
+                      lambda: ops.sum_splits(wpart, w.grad, finish=fin))
+            fin.run()  # no-op: the combine took it
+        else:
+            ops.timed(f"sum_splits_{S}x{w.shape[0]}x{w.shape[1]}",
+                      lambda: ops.sum_splits(wpart, w.grad))
+        return (denc,) + (None,) * 13
+
+
+def _decode_gather_ok(agent, enc, M: int, W: int) -> bool:
+    """The decoder is one Linear+ReLU on the Flatten of the W frame encodings, with FlatAdam-owned
+    grads on the gemm_x6 route, at shapes ocppo_gemm_x6_gather takes (128 x 128 tiles; one split
+    per stack slot; <= 1024 rows per weight-gradient split)."""
+    from . import agents
+
+    net = agent.network
+    flat = getattr(agent, "_flat", None)
+    if not (FUSED_DECODE_GATHER and agents.X6_FWD_SPLITK and flat is not None and
+            torch.is_grad_enabled() and enc.is_cuda and enc.dtype == torch.float32 and
+            len(net) == flat + 3 and isinstance(net[flat], torch.nn.Flatten) and
+            isinstance(net[flat + 1], torch.nn.Linear) and isinstance(net[flat + 2], torch.nn.ReLU)):
+        return False
+    lin = net[flat + 1]
+    C, E = enc.shape
+    H = lin.out_features
+    st = agents._x6_splits(M, H, W * E) if M % 32 == 0 else None
+    return (lin.bias is not None and lin.in_features == W * E and agents.x6_route(lin.weight)
+            and agents._direct(lin.weight) and agents._direct(lin.bias)
+            and lin.weight.is_contiguous() and lin.weight.data_ptr() % 16 == 0
+            and lin.bias.data_ptr() % 16 == 0 and enc.is_contiguous() and enc.data_ptr() % 16 == 0
+            and M % 128 == 0 and H % 128 == 0 and E % 128 == 0 and (M // 32) % W == 0
+            and st is not None and st[1] == ops.X6_AUTO and (M // 32) % st[0] == 0
+            and M // st[0] <= 1024 and W * (M // 128) * (H // 128) >= 256)
+
+
+def _decode_frames(agent, enc, pos_of, perm, dones, uniq, inv, mb, T, N, W):
+    lin = agent.network[agent._flat + 1]
+    box = {"premasked": False, "bias": lin.bias}
+    hidden = _DecodeFrames.apply(enc, lin.weight, lin.bias, pos_of, perm, dones, uniq, inv, mb,
+                                 T, N, W, getattr(enc, "_ocppo_box", None), box)
+    hidden._ocppo_box = box
+    return hidden
+
+
 # The frame gather and the encoder's first Linear(+ReLU) as one HIP launch
 # (ops.frames_gather_linear) when that layer has <= 16 inputs and FlatAdam-owned grads; its
 # backward is the one-pass ReLU-backward + bias + weight gradient (ops.relu_bias_wgrad).
@@ -222,6 +327,9 @@ def minibatch_hidden(agent, obs, dones, uniq, pos_of, inv, perm, mb: int, split:
             cut = (low, low_d)
         else:
             enc = fused_trunk(agent.network[2:agent._flat], h1)
+        if _decode_gather_ok(agent, enc, perm.numel(), W):
+            hidden = _decode_frames(agent, enc, pos_of, perm, dones, uniq, inv, mb, T, N, W)
+            return (hidden, cut) if split else hidden
         h = _FramesExpand.apply(enc.contiguous(), pos_of, perm, dones, uniq, inv, mb, T, N, W,
                                 getattr(enc, "_ocppo_box", None))
         hidden = agent.decode(h)

@@ -1021,15 +1021,43 @@ def x6_fwd_splits(M: int, N: int, K: int):
     return None
 
 
-def linear_x6_split(x, w, b, relu, splits, out=None, planes=None):
+def gemm_x6_gather(a, sam, sak, b, sbn, sbk, c, ldc, M, N, K, gidx, gw, gseg, mode, splits=1,
+                   split_c=0, bias=None, relu=False, b_planes=None):
+    """ocppo_gemm_x6_gather: gemm_x6 on the 128 x 128 tile with one operand's rows read through
+    the row table gidx [rows, gw] (mode 1: A(m, k) = a[gidx[m, k // gseg] * sam + k % gseg];
+    mode 2: B(n, k) = b[gidx[k, n // gseg] * sbk + n % gseg]). Same products as gemm_x6 on the
+    materialised operand, bitwise."""
+    dev = c.device
+    f = torch.float32
+    args = (a.data_ptr(), sam, sak, None if b_planes is not None else b.data_ptr(), sbn, sbk,
+            c.data_ptr(), ldc, M, N, K, splits, split_c, _opt(bias, "bias", f, dev),
+            int(bool(relu)), None if b_planes is None else b_planes.data_ptr(),
+            _check(gidx, "gidx", torch.int32, dev), gw, gseg, int(mode))
+    keep = (a, b, c, bias, b_planes, gidx)
+    timed(f"gemm_x6_{M}x{N}x{K}s{splits}",
+          lambda: call("ocppo_gemm_x6_gather", _stream(dev), *args) or keep)
+    return c
+
+
+def linear_x6_split(x, w, b, relu, splits, out=None, planes=None, gather=None):
     """act(x W^T + b) as `splits` K-split gemm_x6 partials + ocppo_sum_splits_act (the partials
-    added in split order in f64, then + bias, then ReLU)."""
-    M, K = x.shape
+    added in split order in f64, then + bias, then ReLU). gather = (idx [M, W], E): x is the
+    [C, E] row source and the product's input row m is the concatenation of x[idx[m, 0..W)]
+    (frames_expand never materialised; one split per stack slot, splits == W)."""
+    if gather is None:
+        M, K = x.shape
+    else:
+        idx, E = gather
+        M, K = idx.shape[0], idx.shape[1] * E
     N = w.shape[0]
     dev = x.device
     part = torch.empty((splits, M, N), dtype=torch.float32, device=dev)
-    gemm_x6(x, x.stride(0), 1, w, w.stride(0), 1, part, N, M, N, K, splits=splits, split_c=M * N,
-            tile=X6_AUTO, b_planes=planes)
+    if gather is None:
+        gemm_x6(x, x.stride(0), 1, w, w.stride(0), 1, part, N, M, N, K, splits=splits,
+                split_c=M * N, tile=X6_AUTO, b_planes=planes)
+    else:
+        gemm_x6_gather(x, x.stride(0), 1, w, w.stride(0), 1, part, N, M, N, K, idx, idx.shape[1],
+                       E, 1, splits=splits, split_c=M * N, b_planes=planes)
     out = torch.empty((M, N), dtype=torch.float32, device=dev) if out is None else out
     f = torch.float32
     args = (part.data_ptr(), splits, M, N, _opt(b, "bias", f, dev, N), int(bool(relu)),
@@ -1145,6 +1173,19 @@ def dw_x6_parts(g, x, splits: int, part=None, tile=None):
                    split_c=N * K, tile=tile)
 
 
+def dw_x6_parts_gather(g, src, idx, splits: int, part=None):
+    """dw_x6_parts with x never materialised: x[r] = concat(src[idx[r, 0..W)]) (src [C, E],
+    idx [rows, W] int32; the 128 x 128 tile, rows / splits <= 1024) -> [splits, N, W * E]."""
+    rows, N = g.shape
+    W = idx.shape[1]
+    E = src.shape[1]
+    K = W * E
+    part = (torch.empty((splits, N, K), dtype=torch.float32, device=g.device)
+            if part is None else part)
+    return gemm_x6_gather(g, 1, g.stride(0), src, 1, src.stride(0), part, K, N, K, rows, idx, W,
+                          E, 2, splits=splits, split_c=N * K)
+
+
 # ---------------------------------------------------------------------------------------------
 # Frame-deduplicated PPObj minibatch encoder (ppo_atari_oc.py:566 through architectures/ppo.py:60-84)
 # ---------------------------------------------------------------------------------------------
@@ -1203,6 +1244,21 @@ def frames_expand(enc, pos_of, perm, dones, T: int, N: int, W: int, out=None):
          _check(perm, "perm", torch.int64, dev), M,
          _check(dones, "dones", torch.float32, dev, (T + 1) * N), T, N, W,
          _check(out, "out", torch.float32, dev, M * W * E))
+    return out
+
+
+def frames_expand_index(pos_of, perm, dones, T: int, N: int, W: int, out=None):
+    """idx[i, k] = pos_of[timeline id of slot k of sample perm[i]] -> [M, W] int32: the source
+    rows frames_expand copies, for the gathered decoder GEMMs (gemm_x6_gather)."""
+    M = perm.numel()
+    dev = perm.device
+    if out is None:
+        out = torch.empty((M, W), dtype=torch.int32, device=dev)
+    call("ocppo_frames_expand_index", _stream(dev),
+         _check(pos_of, "pos_of", torch.int32, dev, (T + W - 1) * N),
+         _check(perm, "perm", torch.int64, dev), M,
+         _check(dones, "dones", torch.float32, dev, (T + 1) * N), T, N, W,
+         _check(out, "idx", torch.int32, dev, M * W))
     return out
 
 

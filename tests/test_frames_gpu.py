@@ -172,3 +172,35 @@ def test_trainer_dedup_update_matches_per_slot_update(dev):
         scale = g2.abs().max()
         torch.testing.assert_close(g1, g2, rtol=0, atol=2e-5 * float(scale))
         assert not torch.equal(g1, torch.zeros_like(g1))
+
+
+def test_gathered_decoder_gemms_equal_the_materialised_ones(dev):
+    """ocppo_frames_expand_index + ocppo_gemm_x6_gather at config 2 sizes: idx rows ARE
+    frames_expand's sources; the gathered forward (mode 1, one split per stack slot) and weight
+    gradient (mode 2) are bitwise the same gemm_x6 products on the materialised [M, W * E] input."""
+    T, N, W, F, M, E, nmb = 128, 128, 4, 12, 4096, 4, 4
+    Ed, H = 512, 512
+    s = _setup(T, N, W, F, M, E, nmb, 1 / 50, 7, dev)
+    du, dp, di = s["d_plan"]
+    g = torch.Generator(device=dev).manual_seed(2)
+    enc = torch.relu(torch.randn((s["cap"], Ed), device=dev, generator=g))
+    w = torch.randn((H, W * Ed), device=dev, generator=g) * (W * Ed) ** -0.5
+    b = torch.randn(H, device=dev, generator=g) * 0.1
+    gp = torch.randn((M, H), device=dev, generator=g)
+    for j in (0, 9):
+        perm = s["d_perm"][j * M:(j + 1) * M]
+        idx = ops.frames_expand_index(dp[j], perm, s["d_dones"], T, N, W)
+        x = ops.frames_expand(enc, dp[j], perm, s["d_dones"], T, N, W).view(M, W * Ed)
+        assert torch.equal(enc[idx.long()].view(M, W * Ed), x)
+        for planes in (False, True):
+            pl = None
+            if planes:
+                ops.WeightPlanes(fwd=[w]).refresh()
+                pl = w._ocppo_planes["fwd"]
+            got = ops.linear_x6_split(enc, w, b, True, W, planes=pl, gather=(idx, Ed))
+            want = ops.linear_x6_split(x, w, b, True, W, planes=pl)
+            assert torch.equal(got, want)
+        for S in (8, 4):
+            pg = ops.dw_x6_parts_gather(gp, enc, idx, S)
+            pw = ops.dw_x6_parts(gp, x, S, tile=ops.X6_AUTO)
+            assert torch.equal(pg, pw)

@@ -603,3 +603,31 @@ def test_sample_records_are_bitwise_the_soa_gather(dev):
     assert a.records is not None and b.records is None
     for p, q in zip(a.agent.parameters(), b.agent.parameters()):
         assert torch.equal(p, q)
+
+
+def test_gathered_decoder_matches_the_expanded_one(dev):
+    """The trainer's decoder reading its rows straight from the frame encodings
+    (frames.FUSED_DECODE_GATHER: ocppo_gemm_x6_gather forward and weight gradient, no
+    frames_expand copy) leaves the parameters bitwise where the expanded path does: same products
+    in the same order, over two iterations at config 2's network."""
+    from oc_cleanrl_amd import frames
+    from oc_cleanrl_amd.args import Args, finalize
+    from oc_cleanrl_amd.trainer import PPOTrainer
+
+    def run(on):
+        frames.FUSED_DECODE_GATHER = on
+        try:
+            args = finalize(Args(env_id="ALE/Pong-v5", obs_mode="obj", architecture="PPO_OBJ",
+                                 num_envs=128, num_steps=32, num_minibatches=1, update_epochs=1,
+                                 total_timesteps=128 * 32 * 4, save_model=False), 1)
+            tr = PPOTrainer(args, dev, log=False)
+            for _ in range(2):
+                tr.train_iteration()
+            torch.cuda.synchronize()
+            return tr
+        finally:
+            frames.FUSED_DECODE_GATHER = True
+
+    a, b = run(True), run(False)
+    assert a.param_checksum() == b.param_checksum()
+    assert torch.equal(a.stats, b.stats)
