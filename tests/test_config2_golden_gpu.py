@@ -184,7 +184,7 @@ def _f64_under_decisions(tr, j, saved):
     566-602, in f64) through the same network at the chain's current parameters, with every
     ReLU taking the decision the chain's own f32 forward took. saved = the tensors the chain's
     forward saved for backward: the distinct frames' features and ReLU outputs [cap, .] and the
-    decoder's input / output [M, .]."""
+    decoder's input (or its row table into the encodings) / output [M, .]."""
     ag = tr.agent
     M, cap = tr.M, tr.plan[0].shape[1]
     uniq = []
@@ -195,7 +195,13 @@ def _f64_under_decisions(tr, j, saved):
     frames_ = [t for t in uniq if t.shape[0] == cap]
     dec = [t for t in uniq if t.shape[0] == M]
     x0, relu_outs = frames_[0], frames_[1:]
-    dec_in, h5 = dec[0], dec[1]
+    # the gathered decoder (frames._DecodeFrames) saves its [M, W] row table instead of the
+    # [M, W * E] input it never materialises
+    rows = [t for t in saved if t.dtype == torch.int32 and t.dim() == 2 and t.shape[0] == M]
+    if rows:
+        dec_in, h5 = None, dec[0]
+    else:
+        dec_in, h5 = dec[0], dec[1]
     lins = [m for m in ag.network if isinstance(m, torch.nn.Linear)]
     assert [t.shape[1] for t in relu_outs] == [m.out_features for m in lins[:4]]
     P = {n: p.detach().double().clone().requires_grad_(True) for n, p in ag.named_parameters()}
@@ -213,11 +219,14 @@ def _f64_under_decisions(tr, j, saved):
         # padding rows (id -1) are all-zero frames no sample reads
         flips.append(int(((h > 0) != (zs[i] > 0))[:int((tr.plan[0][j] >= 0).sum())].sum()))
     enc = relu_outs[-1]
-    # which encoding row each decoder-input slot holds (exact bit match)
-    he, order = torch.sort(_row_hash(enc))
-    chunks = dec_in.reshape(M * tr.obs_shape[0], enc.shape[1])
-    pos = order[torch.searchsorted(he, _row_hash(chunks))]
-    assert torch.equal(enc[pos], chunks)
+    if dec_in is None:
+        pos = rows[0].long().reshape(-1)
+    else:
+        # which encoding row each decoder-input slot holds (exact bit match)
+        he, order = torch.sort(_row_hash(enc))
+        chunks = dec_in.reshape(M * tr.obs_shape[0], enc.shape[1])
+        pos = order[torch.searchsorted(he, _row_hash(chunks))]
+        assert torch.equal(enc[pos], chunks)
     d = x[pos].reshape(M, -1)
     dn = tr.agent._flat + 1
     with torch.no_grad():
