@@ -59,6 +59,12 @@ extern "C" {
 #define OCPPO_NUM_STATS 9
 
 typedef void* ocppo_stream_t; /* hipStream_t */
+/* A deferred finish (ocppo_heads_loss_rows, ocppo_relu_bias_wgrad_rows): a plain host record of
+ * device pointers and sizes, run later by ocppo_sum_splits_finish / ocppo_sum_splits_db_finish /
+ * ocppo_deferred_finish_run. */
+typedef struct ocppo_deferred_finish {
+  uint64_t opaque[64];
+} ocppo_deferred_finish_t;
 
 #if defined(__GNUC__) || defined(__clang__)
 #define OCPPO_API __attribute__((visibility("default")))
@@ -444,6 +450,19 @@ OCPPO_API size_t ocppo_relu_bias_wgrad_workspace_bytes(int64_t R, int64_t N, int
 OCPPO_API int ocppo_relu_bias_wgrad(ocppo_stream_t stream, const float* g, const float* out,
                           const float* x, int64_t ldx, float* dw, float* db, int64_t R,
                           int64_t N, int64_t K, void* workspace, size_t workspace_bytes);
+/* Deferred form: the rows launch only; the finish (the tree over the row-range records that
+ * writes dw and db) goes into *finish (R >= 1), to ride in the split-K combine the backward runs
+ * next (ocppo_sum_splits_db_finish = ocppo_sum_splits_db, bitwise, plus the finish workgroups in
+ * the same launch) or alone (ocppo_deferred_finish_run). Same results as ocppo_relu_bias_wgrad,
+ * bitwise; run once, before anything reads dw / db or reuses the workspace. */
+OCPPO_API int ocppo_relu_bias_wgrad_rows(ocppo_stream_t stream, const float* g, const float* out,
+                                         const float* x, int64_t ldx, float* dw, float* db,
+                                         int64_t R, int64_t N, int64_t K, void* workspace,
+                                         size_t workspace_bytes, ocppo_deferred_finish_t* finish);
+OCPPO_API int ocppo_sum_splits_db_finish(ocppo_stream_t stream, const float* part, int64_t S,
+                                         int64_t n, float* out, const float* db_partials,
+                                         int64_t chunks, int64_t N, float* db,
+                                         const ocppo_deferred_finish_t* finish);
 
 /* ---------------------------------------------------------------------------------------------
  * Policy heads + decoder ReLU backward in ONE pass — replaces, inside `loss.backward()`
@@ -659,9 +678,6 @@ OCPPO_API int ocppo_heads_loss_fwd_bwd(ocppo_stream_t stream, const float* h, in
  * (ocppo_sum_splits_finish = ocppo_sum_splits, bitwise, plus the finish workgroups in the same
  * launch) or alone (ocppo_deferred_finish_run). Same results as ocppo_heads_loss_fwd_bwd, bitwise.
  * The record holds device pointers only; it may be copied and run once per rows launch. */
-typedef struct ocppo_deferred_finish {
-  uint64_t opaque[64];
-} ocppo_deferred_finish_t;
 OCPPO_API int ocppo_heads_loss_rows(ocppo_stream_t stream, const float* h, int64_t M, int64_t H,
                                     const float* w_actor, const float* b_actor,
                                     const float* w_critic, const float* b_critic, int64_t A,

@@ -61,6 +61,8 @@ SIGNATURES: dict[str, tuple[type, list]] = {
     "ocppo_sum_splits_db": (I, [P, P, I64, I64, P, P, I64, I64, P]),
     "ocppo_relu_bias_wgrad_workspace_bytes": (SZ, [I64, I64, I64]),
     "ocppo_relu_bias_wgrad": (I, [P, P, P, P, I64, P, P, I64, I64, I64, P, SZ]),
+    "ocppo_relu_bias_wgrad_rows": (I, [P, P, P, P, I64, P, P, I64, I64, I64, P, SZ, P]),
+    "ocppo_sum_splits_db_finish": (I, [P, P, I64, I64, P, P, I64, I64, P, P]),
     "ocppo_heads_bwd_workspace_bytes": (SZ, [I64, I64, I64]),
     "ocppo_heads_bwd": (I, [P, P, P, P, P, P, P, P, P, P, P, P, I64, I64, I64, I, P, SZ]),
     "ocppo_bias_act": (I, [P, P, P, I64, I64, I]),

@@ -195,6 +195,9 @@ def _weight_grad_core(g, x, out, db, x6, finish):
     else:
         part = torch.bmm(g.view(s, rows // s, n).transpose(1, 2), x.view(s, rows // s, k))
     if db is not None:
+        if finish is not None:
+            return ops.timed(f"sum_splits_db_fin_{s}x{n}x{k}",
+                             lambda: ops.sum_splits_db(part, out, *db, finish=finish))
         return ops.timed(f"sum_splits_db_{s}x{n}x{k}", lambda: ops.sum_splits_db(part, out, *db))
     if out is not None and HIP_SUM_SPLITS and ops.sum_splits_ok(part, out):
         if finish is not None:
@@ -251,6 +254,10 @@ def _cols_from_nhwc(w_nhwc, chw, out=None):
 # gradient's split-K combine (ops.relu_bias_grad_partial + ops.sum_splits_db).
 DEFER_BIAS_GRAD = True
 
+# The second encoder layer's weight gradient computed after the first layer's rows launch, so
+# that launch's finish rides in its split-K combine (ops.sum_splits_db(..., finish=)).
+DEFER_WGRAD_AFTER_FIRST_LAYER = True
+
 
 # Split-K partials of FlatAdam-owned weight gradients summed by one HIP pass (ops.sum_splits).
 HIP_SUM_SPLITS = True
@@ -268,7 +275,7 @@ class _LinearAct(torch.autograd.Function):
     for FlatAdam-owned parameters dW/db are written straight into the flat grad buffer."""
 
     @staticmethod
-    def forward(ctx, x, w, b, relu: bool, box=None, chw=None, below=None):
+    def forward(ctx, x, w, b, relu: bool, box=None, chw=None, below=None, wslot=None):
         # chw = (C, H, W): x is a channels_last activation flattened in its memory (H, W, C)
         # order, so the weight's columns are permuted to match instead (linear_act_nhwc)
         wm = _cols_to_nhwc(w, chw) if chw is not None else w
@@ -302,13 +309,16 @@ class _LinearAct(torch.autograd.Function):
         ctx.w, ctx.b = w, b
         ctx.chw, ctx.wm = chw, (wm if chw is not None else None)
         ctx.box = box  # _Heads sets box["premasked"]: g arrives masked, bias grad already written
+        # wslot: x is the first encoder layer's output (frames._GatherLinear1), whose backward
+        # runs after this one; this layer's weight gradient may wait for it (see _backward)
+        ctx.wslot = wslot
         return out
 
     @staticmethod
     def backward(ctx, g):
         chw = ctx.chw
         if chw is None:
-            return _LinearAct._backward(ctx, g, ctx.w.grad) + (None,)
+            return _LinearAct._backward(ctx, g, ctx.w.grad) + (None, None)
         # permuted columns: weight gradient formed in the NHWC column order, then put back
         direct = _direct(ctx.w)
         wgrad = torch.empty_like(ctx.wm) if direct else None
@@ -317,7 +327,7 @@ class _LinearAct(torch.autograd.Function):
             _cols_from_nhwc(wgrad, chw, out=ctx.w.grad)
         if dw is not None:
             dw = _cols_from_nhwc(dw, chw)
-        return dx, dw, db, None, None, None, None
+        return dx, dw, db, None, None, None, None, None
 
     @staticmethod
     def _dx_of(ctx, g, w):
@@ -358,7 +368,15 @@ class _LinearAct(torch.autograd.Function):
             if dbp is None:
                 _weight_grad(g, x, out=wgrad, x6=ctx.x6, finish=ctx.box.get("finish"))
             elif _defer_db_ok(g, x, wgrad, ctx.b):
-                _weight_grad(g, x, out=wgrad, db=(dbp, ctx.b.grad), x6=ctx.x6)
+                if ctx.wslot is not None and DEFER_WGRAD_AFTER_FIRST_LAYER:
+                    # after the first layer's rows launch, with its finish in this combine
+                    # (frames._GatherLinear1.backward runs it: the finish-carrying
+                    # sum_splits_db saves the finish's own launch)
+                    bg, x6 = ctx.b.grad, ctx.x6
+                    ctx.wslot["run"] = lambda fin, g=g, x=x, wg=wgrad: _weight_grad(
+                        g, x, out=wg, db=(dbp, bg), x6=x6, finish=fin)
+                else:
+                    _weight_grad(g, x, out=wgrad, db=(dbp, ctx.b.grad), x6=ctx.x6)
             else:
                 _weight_grad(g, x, out=wgrad, x6=ctx.x6)
                 torch.sum(dbp[0], 0, out=ctx.b.grad)
@@ -600,7 +618,7 @@ def linear_act(x, lin: nn.Linear, relu: bool, chw=None):
             _direct(lin.bias):
         box = {"premasked": False, "bias": lin.bias}
     y = _LinearAct.apply(x2, lin.weight, lin.bias, relu, box, chw,
-                         getattr(x, "_ocppo_box", None))
+                         getattr(x, "_ocppo_box", None), getattr(x, "_ocppo_wslot", None))
     y = y.view(*lead, y.shape[-1])
     if box is not None:
         y._ocppo_box = box

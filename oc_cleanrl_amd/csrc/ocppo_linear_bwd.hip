@@ -21,6 +21,8 @@
 // one agent-scope atomic add; the last arriver reads with sc1 loads). Tickets re-arm themselves.
 // Roofline: HBM / Infinity-Cache stream, 12 B per element (relu) or 4 B (no relu) + 4 B per
 // partial; no flops to speak of.
+#include <cstring>
+
 #include "ocppo_common.h"
 
 namespace ocppo {
@@ -403,14 +405,13 @@ struct d4 {
   double x, y, z, w;
 };
 template <int S>
-__global__ __launch_bounds__(256) void sum_splits_db_kernel(const float4* __restrict__ part,
-                                                            int64_t n4, float4* __restrict__ out,
-                                                            int nsb, const float* __restrict__ dbp,
-                                                            int chunks, int64_t N,
-                                                            float* __restrict__ db) {
-  if (static_cast<int>(blockIdx.x) < nsb) {
+__device__ __forceinline__ void sum_splits_db_block(const float4* __restrict__ part, int64_t n4,
+                                                    float4* __restrict__ out, int nsb,
+                                                    const float* __restrict__ dbp, int chunks,
+                                                    int64_t N, float* __restrict__ db, int blk) {
+  if (blk < nsb) {
     const int64_t stride = static_cast<int64_t>(nsb) * blockDim.x;
-    for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n4;
+    for (int64_t i = static_cast<int64_t>(blk) * blockDim.x + threadIdx.x; i < n4;
          i += stride) {
       float4 v[S];
 #pragma unroll
@@ -426,7 +427,7 @@ __global__ __launch_bounds__(256) void sum_splits_db_kernel(const float4* __rest
     return;
   }
   __shared__ d4 red[256 / kWave][kDbQuads];
-  const int cb = blockIdx.x - nsb;
+  const int cb = blk - nsb;
   const int q = threadIdx.x % kDbQuads, gi = threadIdx.x / kDbQuads;  // column quad, chunk group
   const int64_t col = static_cast<int64_t>(cb) * (4 * kDbQuads) + 4 * q;
   const int cpg = (chunks + kDbGroups - 1) / kDbGroups;
@@ -464,6 +465,15 @@ __global__ __launch_bounds__(256) void sum_splits_db_kernel(const float4* __rest
         make_float4(static_cast<float>(t.x), static_cast<float>(t.y), static_cast<float>(t.z),
                     static_cast<float>(t.w));
   }
+}
+
+template <int S>
+__global__ __launch_bounds__(256) void sum_splits_db_kernel(const float4* __restrict__ part,
+                                                            int64_t n4, float4* __restrict__ out,
+                                                            int nsb, const float* __restrict__ dbp,
+                                                            int chunks, int64_t N,
+                                                            float* __restrict__ db) {
+  sum_splits_db_block<S>(part, n4, out, nsb, dbp, chunks, N, db, blockIdx.x);
 }
 
 extern "C" int ocppo_sum_splits_db(ocppo_stream_t stream, const float* part, int64_t S, int64_t n,
@@ -737,12 +747,21 @@ __global__ __launch_bounds__(64 * kWrWaves) void relu_bias_wgrad_rows_kernel(
 // flight, each batch summed pairwise, then the 8 group sums pairwise through LDS.
 // Output o = (column group, value v, column): v = 0 the bias gradient, 1..K the weight columns.
 constexpr int kWfOut = 32, kWfGroups = 8, kWfBatch = 32;
-__global__ __launch_bounds__(256) void relu_bias_wgrad_finish_kernel(
-    const float* __restrict__ partials, int G, int64_t npw, int NV, int64_t N, int K,
-    float* __restrict__ dw, float* __restrict__ db) {
+// everything the finish needs, fixed at the rows launch (ocppo_relu_bias_wgrad_rows hands it to
+// the caller as an ocppo_deferred_finish_t so it can ride in a later launch)
+struct WgFinish {
+  const float* partials;
+  int G, NV, K, blocks;
+  int64_t npw, N;
+  float *dw, *db;
+};
+__device__ __forceinline__ void wg_finish_block(const WgFinish& f, int blk) {
   __shared__ float red[kWfGroups][kWfOut + 1];
   const int o = threadIdx.x % kWfOut, gi = threadIdx.x / kWfOut;
-  const int64_t idx = static_cast<int64_t>(blockIdx.x) * kWfOut + o;
+  const int64_t idx = static_cast<int64_t>(blk) * kWfOut + o;
+  const float* __restrict__ partials = f.partials;
+  const int G = f.G;
+  const int64_t npw = f.npw;
   float s = 0.f;
   if (idx < npw) {
     for (int g0 = gi; g0 < G; g0 += kWfGroups * kWfBatch) {
@@ -767,19 +786,37 @@ __global__ __launch_bounds__(256) void relu_bias_wgrad_finish_kernel(
   }
   if (gi != 0 || idx >= npw) return;
   const float t = red[0][o];
-  const int64_t per = static_cast<int64_t>(kWrCols) * NV;
+  const int64_t per = static_cast<int64_t>(kWrCols) * f.NV;
   const int64_t cgi = idx / per, rem = idx - cgi * per;
   const int v = static_cast<int>(rem / kWrCols);
   const int64_t col = cgi * kWrCols + (rem - static_cast<int64_t>(v) * kWrCols);
-  if (col >= N) return;
-  if (v == 0) db[col] = t;
-  else if (v - 1 < K) dw[col * K + (v - 1)] = t;
+  if (col >= f.N) return;
+  if (v == 0) f.db[col] = t;
+  else if (v - 1 < f.K) f.dw[col * f.K + (v - 1)] = t;
+}
+
+__global__ __launch_bounds__(256) void relu_bias_wgrad_finish_kernel(WgFinish f) {
+  wg_finish_block(f, blockIdx.x);
+}
+
+// the finish folded into a later split-K combine of the same backward (the second encoder
+// layer's weight gradient, which runs after the first layer's rows when the trainer defers it):
+// workgroups [0, f.blocks) finish, the rest are sum_splits_db's
+template <int S>
+__global__ __launch_bounds__(256) void sum_splits_db_wgfin_kernel(
+    const float4* __restrict__ part, int64_t n4, float4* __restrict__ out, int nsb,
+    const float* __restrict__ dbp, int chunks, int64_t N, float* __restrict__ db, WgFinish f) {
+  if (static_cast<int>(blockIdx.x) < f.blocks) {
+    wg_finish_block(f, blockIdx.x);
+    return;
+  }
+  sum_splits_db_block<S>(part, n4, out, nsb, dbp, chunks, N, db, blockIdx.x - f.blocks);
 }
 
 template <bool RELU>
-static void launch_wgrad_rows(hipStream_t s, int K, const float* g, const float* out,
-                              const float* x, int64_t ldx, float* dw, float* db, int64_t R,
-                              int64_t N, float* partials) {
+static WgFinish launch_wgrad_rows(hipStream_t s, int K, const float* g, const float* out,
+                                  const float* x, int64_t ldx, float* dw, float* db, int64_t R,
+                                  int64_t N, float* partials) {
   const int64_t rpw = wr_rows_per_wg(R);
   const int G = static_cast<int>((R + rpw - 1) / rpw);
   const int ncg = static_cast<int>((N + kWrCols - 1) / kWrCols);
@@ -795,8 +832,8 @@ static void launch_wgrad_rows(hipStream_t s, int K, const float* g, const float*
   else OCPPO_WR(16);
 #undef OCPPO_WR
   const int64_t npw = static_cast<int64_t>(ncg) * kWrCols * (KP + 1);
-  hipLaunchKernelGGL(relu_bias_wgrad_finish_kernel, dim3((npw + kWfOut - 1) / kWfOut), dim3(256),
-                     0, s, partials, G, npw, KP + 1, N, K, dw, db);
+  return WgFinish{partials, G, KP + 1, K, static_cast<int>((npw + kWfOut - 1) / kWfOut), npw, N,
+                  dw, db};
 }
 
 inline int wg_kp(int64_t K) { return K <= 4 ? 4 : K <= 8 ? 8 : K <= 12 ? 12 : 16; }
@@ -811,10 +848,10 @@ extern "C" size_t ocppo_relu_bias_wgrad_workspace_bytes(int64_t R, int64_t N, in
   return static_cast<size_t>(G * ncg * ocppo::kWrCols * (ocppo::wg_kp(K) + 1)) * sizeof(float);
 }
 
-extern "C" int ocppo_relu_bias_wgrad(ocppo_stream_t stream, const float* g, const float* out,
-                                     const float* x, int64_t ldx, float* dw, float* db, int64_t R,
-                                     int64_t N, int64_t K, void* workspace,
-                                     size_t workspace_bytes) {
+static int relu_bias_wgrad_impl(ocppo_stream_t stream, const float* g, const float* out,
+                                const float* x, int64_t ldx, float* dw, float* db, int64_t R,
+                                int64_t N, int64_t K, void* workspace, size_t workspace_bytes,
+                                WgFinish* fin_out) {
   OCPPO_REQUIRE(R >= 0 && N >= 4 && N % 4 == 0 && N <= 16384 && K >= 1 && K <= 16 && ldx >= K,
                 "ocppo_relu_bias_wgrad: bad sizes R=%lld N=%lld K=%lld ldx=%lld (N %% 4 == 0, "
                 "N <= 16384, 1 <= K <= 16, ldx >= K)", (long long)R, (long long)N, (long long)K,
@@ -836,11 +873,96 @@ extern "C" int ocppo_relu_bias_wgrad(ocppo_stream_t stream, const float* g, cons
                 "ocppo_relu_bias_wgrad: workspace too small (%zu < %zu)", workspace_bytes,
                 ocppo_relu_bias_wgrad_workspace_bytes(R, N, K));
   float* partials = static_cast<float*>(workspace);
-  if (out)
-    launch_wgrad_rows<true>(s, (int)K, g, out, x, ldx, dw, db, R, N, partials);
-  else
-    launch_wgrad_rows<false>(s, (int)K, g, out, x, ldx, dw, db, R, N, partials);
-  return check_launch("ocppo_relu_bias_wgrad");
+  const WgFinish f = out ? launch_wgrad_rows<true>(s, (int)K, g, out, x, ldx, dw, db, R, N, partials)
+                         : launch_wgrad_rows<false>(s, (int)K, g, out, x, ldx, dw, db, R, N, partials);
+  if (int rc = check_launch("ocppo_relu_bias_wgrad")) return rc;
+  if (fin_out) {
+    *fin_out = f;
+    return OCPPO_OK;
+  }
+  hipLaunchKernelGGL(relu_bias_wgrad_finish_kernel, dim3(f.blocks), dim3(256), 0, s, f);
+  return check_launch("ocppo_relu_bias_wgrad/finish");
+}
+
+extern "C" int ocppo_relu_bias_wgrad(ocppo_stream_t stream, const float* g, const float* out,
+                                     const float* x, int64_t ldx, float* dw, float* db, int64_t R,
+                                     int64_t N, int64_t K, void* workspace,
+                                     size_t workspace_bytes) {
+  return relu_bias_wgrad_impl(stream, g, out, x, ldx, dw, db, R, N, K, workspace,
+                              workspace_bytes, nullptr);
+}
+
+// the deferred-finish record behind the C-ABI's opaque ocppo_deferred_finish_t (heads-loss
+// records carry another tag, ocppo_loss.hip)
+constexpr uint64_t kDeferWgrad = 0x6f63707077676631ull;
+struct DeferredWgrad {
+  uint64_t tag;
+  WgFinish f;
+};
+static_assert(sizeof(DeferredWgrad) <= sizeof(ocppo_deferred_finish_t),
+              "ocppo_deferred_finish_t too small");
+
+extern "C" int ocppo_relu_bias_wgrad_rows(ocppo_stream_t stream, const float* g, const float* out,
+                                          const float* x, int64_t ldx, float* dw, float* db,
+                                          int64_t R, int64_t N, int64_t K, void* workspace,
+                                          size_t workspace_bytes,
+                                          ocppo_deferred_finish_t* finish) {
+  OCPPO_REQUIRE(finish && R >= 1, "ocppo_relu_bias_wgrad_rows: null finish record or R == 0");
+  DeferredWgrad d;
+  d.tag = kDeferWgrad;
+  if (int rc = relu_bias_wgrad_impl(stream, g, out, x, ldx, dw, db, R, N, K, workspace,
+                                    workspace_bytes, &d.f))
+    return rc;
+  memset(finish, 0, sizeof(*finish));
+  memcpy(finish, &d, sizeof(d));
+  return OCPPO_OK;
+}
+
+namespace ocppo {
+// ocppo_deferred_finish_run for a relu_bias_wgrad record (1: done; 0: not such a record)
+int wgrad_finish_run(hipStream_t s, const ocppo_deferred_finish_t* finish) {
+  DeferredWgrad d;
+  memcpy(&d, finish, sizeof(d));
+  if (d.tag != kDeferWgrad) return 0;
+  hipLaunchKernelGGL(relu_bias_wgrad_finish_kernel, dim3(d.f.blocks), dim3(256), 0, s, d.f);
+  return 1;
+}
+}  // namespace ocppo
+
+extern "C" int ocppo_sum_splits_db_finish(ocppo_stream_t stream, const float* part, int64_t S,
+                                          int64_t n, float* out, const float* db_partials,
+                                          int64_t chunks, int64_t N, float* db,
+                                          const ocppo_deferred_finish_t* finish) {
+  OCPPO_REQUIRE(n >= 4 && n % 4 == 0 && (S == 1 || S == 2 || S == 4 || S == 8 || S == 16) &&
+                    N >= 4 && N % 4 == 0 && chunks >= 1,
+                "ocppo_sum_splits_db_finish: bad sizes S=%lld n=%lld N=%lld chunks=%lld",
+                (long long)S, (long long)n, (long long)N, (long long)chunks);
+  OCPPO_REQUIRE(part && out && db_partials && db && finish,
+                "ocppo_sum_splits_db_finish: null pointer");
+  OCPPO_REQUIRE((reinterpret_cast<uintptr_t>(part) | reinterpret_cast<uintptr_t>(out) |
+                 reinterpret_cast<uintptr_t>(db_partials) | reinterpret_cast<uintptr_t>(db)) % 16 == 0,
+                "ocppo_sum_splits_db_finish: pointers must be 16-B aligned");
+  DeferredWgrad d;
+  memcpy(&d, finish, sizeof(d));
+  OCPPO_REQUIRE(d.tag == kDeferWgrad,
+                "ocppo_sum_splits_db_finish: not a finish record of ocppo_relu_bias_wgrad_rows");
+  clear_stale_error();
+  const int64_t n4 = n / 4;
+  const int nsb = grid_for(n4, 256);
+  const int ndb = static_cast<int>((N + 4 * kDbQuads - 1) / (4 * kDbQuads));
+  const dim3 grid(d.f.blocks + nsb + ndb), block(256);
+  hipStream_t s = as_stream(stream);
+  const float4* p4 = reinterpret_cast<const float4*>(part);
+  float4* o4 = reinterpret_cast<float4*>(out);
+  const int c = static_cast<int>(chunks);
+  switch (S) {
+    case 1: hipLaunchKernelGGL(sum_splits_db_wgfin_kernel<1>, grid, block, 0, s, p4, n4, o4, nsb, db_partials, c, N, db, d.f); break;
+    case 2: hipLaunchKernelGGL(sum_splits_db_wgfin_kernel<2>, grid, block, 0, s, p4, n4, o4, nsb, db_partials, c, N, db, d.f); break;
+    case 4: hipLaunchKernelGGL(sum_splits_db_wgfin_kernel<4>, grid, block, 0, s, p4, n4, o4, nsb, db_partials, c, N, db, d.f); break;
+    case 8: hipLaunchKernelGGL(sum_splits_db_wgfin_kernel<8>, grid, block, 0, s, p4, n4, o4, nsb, db_partials, c, N, db, d.f); break;
+    default: hipLaunchKernelGGL(sum_splits_db_wgfin_kernel<16>, grid, block, 0, s, p4, n4, o4, nsb, db_partials, c, N, db, d.f); break;
+  }
+  return check_launch("ocppo_sum_splits_db_finish");
 }
 
 // ---- policy heads + decoder ReLU backward in ONE pass ---------------------------------------------

@@ -2062,11 +2062,18 @@ static int deferred_of(const ocppo_deferred_finish_t* finish, DeferredFinish& d,
   return OCPPO_OK;
 }
 
+namespace ocppo {
+int wgrad_finish_run(hipStream_t s, const ocppo_deferred_finish_t* finish);  // ocppo_linear_bwd.hip
+}
+
 extern "C" int ocppo_deferred_finish_run(ocppo_stream_t stream,
                                          const ocppo_deferred_finish_t* finish) {
+  OCPPO_REQUIRE(finish, "ocppo_deferred_finish_run: null finish record");
+  clear_stale_error();
+  if (ocppo::wgrad_finish_run(as_stream(stream), finish))
+    return check_launch("ocppo_deferred_finish_run");
   DeferredFinish d;
   if (int rc = deferred_of(finish, d, "ocppo_deferred_finish_run")) return rc;
-  clear_stale_error();
   hipLaunchKernelGGL(heads_loss_finish_kernel, dim3(d.f.blocks), dim3(256), 0, as_stream(stream),
                      d.f);
   return check_launch("ocppo_deferred_finish_run");

@@ -267,14 +267,16 @@ FUSED_GATHER_L1 = True
 
 class _GatherLinear1(torch.autograd.Function):
     """h1 = relu(frames_gather(obs, uniq) @ W1^T + b1); backward = dW1 / db1 only (the frames
-    need no gradient), written into the FlatAdam-owned grads."""
+    need no gradient), written into the FlatAdam-owned grads. slot: a dict the next layer's
+    backward may leave its weight-gradient step in ("run"); it then runs here, after this layer's
+    rows launch, carrying this layer's finish in its split-K combine (no finish launch)."""
 
     @staticmethod
-    def forward(ctx, w, b, obs, uniq):
+    def forward(ctx, w, b, obs, uniq, slot=None):
         x, h1 = ops.timed("frames_gather_linear",
                           lambda: ops.frames_gather_linear(obs, uniq, w, b, relu=True))
         ctx.save_for_backward(x, h1)
-        ctx.params = (w, b)
+        ctx.params, ctx.slot = (w, b), slot
         return h1
 
     @staticmethod
@@ -282,9 +284,19 @@ class _GatherLinear1(torch.autograd.Function):
         x, h1 = ctx.saved_tensors
         w, b = ctx.params
         g = g.contiguous()
+        run = ctx.slot.pop("run", None) if ctx.slot is not None else None
+        if run is None or g.shape[0] == 0:
+            ops.timed(f"relu_bias_wgrad_{g.shape[0]}x{g.shape[1]}x{x.shape[1]}",
+                      lambda: ops.relu_bias_wgrad(g, h1, x, dw=w.grad, db=b.grad))
+            if run is not None:
+                run(None)
+            return None, None, None, None, None
+        fin = ops.DeferredFinish(g.device)
         ops.timed(f"relu_bias_wgrad_{g.shape[0]}x{g.shape[1]}x{x.shape[1]}",
-                  lambda: ops.relu_bias_wgrad(g, h1, x, dw=w.grad, db=b.grad))
-        return None, None, None, None
+                  lambda: ops.relu_bias_wgrad(g, h1, x, dw=w.grad, db=b.grad, defer=fin))
+        run(fin)
+        fin.run()  # no-op when the combine took it
+        return None, None, None, None, None
 
 
 def _gather_l1_ok(agent, obs, split: int) -> bool:
@@ -319,7 +331,9 @@ def minibatch_hidden(agent, obs, dones, uniq, pos_of, inv, perm, mb: int, split:
     cut = None
     if _gather_l1_ok(agent, obs, split):
         l1 = agent.network[0]
-        h1 = _GatherLinear1.apply(l1.weight, l1.bias, obs, uniq)
+        slot = {}
+        h1 = _GatherLinear1.apply(l1.weight, l1.bias, obs, uniq, slot)
+        h1._ocppo_wslot = slot
         if split:
             low = fused_trunk(agent.network[2:split], h1)
             low_d = low.detach().requires_grad_()

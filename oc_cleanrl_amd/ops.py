@@ -250,9 +250,10 @@ def heads_loss_ok(h, A: int) -> bool:
 
 class DeferredFinish:
     """The finish of ocppo_heads_loss_rows (the tree over the heads-loss records that writes the
-    heads' and decoder-bias gradients and the loss statistics), held as the C-ABI's host record
-    until a later launch on the same stream runs it: sum_splits(..., finish=) folds it into a
-    split-K combine, run() launches it alone. It must run exactly once (pending: not yet)."""
+    heads' and decoder-bias gradients and the loss statistics) or of ocppo_relu_bias_wgrad_rows
+    (the first layer's dw / db), held as the C-ABI's host record until a later launch on the same
+    stream runs it: sum_splits(..., finish=) / sum_splits_db(..., finish=) fold it into a split-K
+    combine, run() launches it alone. It must run exactly once (pending: not yet)."""
 
     def __init__(self, device):
         self.device = device
@@ -729,18 +730,25 @@ def relu_bias_grad_partial(g, out=None, gp=None):
     return (gp if out is not None else g), buf
 
 
-def sum_splits_db(part, out, db_part, db):
+def sum_splits_db(part, out, db_part, db, finish=None):
     """sum_splits(part, out) and db = db_part.sum(0) in a fixed order, one launch
-    (db_part = the (partials, chunks) of relu_bias_grad_partial)."""
+    (db_part = the (partials, chunks) of relu_bias_grad_partial). finish = a filled
+    DeferredFinish of relu_bias_wgrad(..., defer=): run by extra workgroups of the same launch
+    (ocppo_sum_splits_db_finish; out / db bitwise the same)."""
     S = part.shape[0]
     dev = part.device
     f = torch.float32
     parts, chunks = db_part
     N = parts.shape[1]
     n = part[0].numel()
-    call("ocppo_sum_splits_db", _stream(dev), _check(part, "part", f, dev), S, n,
-         _check(out, "out", f, dev, n), _check(parts, "db_partials", f, dev, chunks * N), chunks,
-         N, _check(db, "db", f, dev, N))
+    args = (_check(part, "part", f, dev), S, n, _check(out, "out", f, dev, n),
+            _check(parts, "db_partials", f, dev, chunks * N), chunks, N,
+            _check(db, "db", f, dev, N))
+    if finish is not None and finish.filled:
+        finish.pending = False
+        call("ocppo_sum_splits_db_finish", _stream(dev), *args, finish.ptr())
+    else:
+        call("ocppo_sum_splits_db", _stream(dev), *args)
     return out, db
 
 
@@ -749,10 +757,12 @@ def relu_bias_wgrad_ok(g, x) -> bool:
             and 1 <= x.shape[1] <= 16 and x.shape[0] == g.shape[0] and x.stride(1) == 1)
 
 
-def relu_bias_wgrad(g, out, x, dw=None, db=None):
+def relu_bias_wgrad(g, out, x, dw=None, db=None, defer=None):
     """(dw, db) of a Linear(+ReLU) layer whose input needs no gradient, in one pass:
     gp = threshold_backward(g, out, 0) (g when out is None, never materialised),
-    db = gp.sum(0), dw = gp^T x. g [R, N] f32 (N % 4 == 0), x [R, K] f32 (K <= 16)."""
+    db = gp.sum(0), dw = gp^T x. g [R, N] f32 (N % 4 == 0), x [R, K] f32 (K <= 16).
+    defer = a DeferredFinish (R >= 1): only the rows launch runs now (ocppo_relu_bias_wgrad_rows);
+    dw and db are written when the caller runs the finish (sum_splits_db(..., finish=) or run())."""
     if g.dim() != 2 or x.dim() != 2 or x.shape[0] != g.shape[0]:
         raise ValueError(f"g [R, N] and x [R, K] expected, got {tuple(g.shape)}, {tuple(x.shape)}")
     R, N = g.shape
@@ -773,11 +783,14 @@ def relu_bias_wgrad(g, out, x, dw=None, db=None):
     if ws is None:
         nb = int(_lib.LIB.ocppo_relu_bias_wgrad_workspace_bytes(R, N, K))
         ws = _RB_WS[key] = torch.zeros(nb, dtype=torch.uint8, device=dev)
-    call("ocppo_relu_bias_wgrad", _stream(dev), _check(g, "g", f, dev),
+    call("ocppo_relu_bias_wgrad_rows" if defer is not None else "ocppo_relu_bias_wgrad",
+         _stream(dev), _check(g, "g", f, dev),
          _opt(out, "out", f, dev, R * N),
          _check(x, "x", f, dev) if x.is_contiguous() else x.data_ptr(), ldx,
          _check(dw, "dw", f, dev, N * K), _check(db, "db", f, dev, N), R, N, K, ws.data_ptr(),
-         ws.numel())
+         ws.numel(), *((defer.ptr(),) if defer is not None else ()))
+    if defer is not None:
+        defer.pending = defer.filled = True
     return dw, db
 
 

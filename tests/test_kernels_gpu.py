@@ -986,6 +986,26 @@ def test_relu_bias_wgrad_vs_torch(ops, dev, R, N, K, relu):
     assert ((db.double() - ref_b).abs() / sb).max().item() < 1e-6
     dw2, db2 = ops.relu_bias_wgrad(g, out, x)  # deterministic; tickets re-armed
     assert torch.equal(dw, dw2) and torch.equal(db, db2)
+    # deferred finish: folded into a sum_splits_db launch, or run alone: bitwise the same, and
+    # the combine's own outputs unchanged
+    S, n2, N2 = 4, 512 * 256, 512
+    part = torch.randn(S, n2, device=dev)
+    dbp = torch.randn(90, N2, device=dev)
+    o_ref, b_ref = torch.empty(n2, device=dev), torch.empty(N2, device=dev)
+    ops.sum_splits_db(part, o_ref, (dbp, 90), b_ref)
+    for fold in (True, False):
+        fin = ops.DeferredFinish(dev)
+        dw3, db3 = torch.full_like(dw, float("nan")), torch.full_like(db, float("nan"))
+        ops.relu_bias_wgrad(g, out, x, dw=dw3, db=db3, defer=fin)
+        assert fin.pending
+        if fold:
+            o, b_ = torch.empty(n2, device=dev), torch.empty(N2, device=dev)
+            ops.sum_splits_db(part, o, (dbp, 90), b_, finish=fin)
+            assert torch.equal(o, o_ref) and torch.equal(b_, b_ref)
+        else:
+            fin.run()
+        assert not fin.pending
+        assert torch.equal(dw3, dw) and torch.equal(db3, db)
 
 
 def test_relu_bias_wgrad_graph_replay_and_zero_rows(ops, dev):

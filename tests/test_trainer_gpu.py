@@ -605,17 +605,23 @@ def test_sample_records_are_bitwise_the_soa_gather(dev):
         assert torch.equal(p, q)
 
 
-def test_gathered_decoder_matches_the_expanded_one(dev):
+@pytest.mark.parametrize("toggle", ["decode_gather", "wgrad_after_first_layer"])
+def test_gathered_decoder_matches_the_expanded_one(dev, toggle):
     """The trainer's decoder reading its rows straight from the frame encodings
     (frames.FUSED_DECODE_GATHER: ocppo_gemm_x6_gather forward and weight gradient, no
-    frames_expand copy) leaves the parameters bitwise where the expanded path does: same products
-    in the same order, over two iterations at config 2's network."""
-    from oc_cleanrl_amd import frames
+    frames_expand copy), and the second encoder layer's weight gradient deferred past the first
+    layer's rows launch so that launch's finish rides in its combine
+    (agents.DEFER_WGRAD_AFTER_FIRST_LAYER), each leave the parameters bitwise where the plain path
+    does: same products in the same order, over two iterations at config 2's network."""
+    from oc_cleanrl_amd import agents, frames
     from oc_cleanrl_amd.args import Args, finalize
     from oc_cleanrl_amd.trainer import PPOTrainer
 
+    mod, name = ((frames, "FUSED_DECODE_GATHER") if toggle == "decode_gather"
+                 else (agents, "DEFER_WGRAD_AFTER_FIRST_LAYER"))
+
     def run(on):
-        frames.FUSED_DECODE_GATHER = on
+        setattr(mod, name, on)
         try:
             args = finalize(Args(env_id="ALE/Pong-v5", obs_mode="obj", architecture="PPO_OBJ",
                                  num_envs=128, num_steps=32, num_minibatches=1, update_epochs=1,
@@ -626,7 +632,7 @@ def test_gathered_decoder_matches_the_expanded_one(dev):
             torch.cuda.synchronize()
             return tr
         finally:
-            frames.FUSED_DECODE_GATHER = True
+            setattr(mod, name, True)
 
     a, b = run(True), run(False)
     assert a.param_checksum() == b.param_checksum()
