@@ -331,9 +331,13 @@ def minibatch_hidden(agent, obs, dones, uniq, pos_of, inv, perm, mb: int, split:
     cut = None
     if _gather_l1_ok(agent, obs, split):
         l1 = agent.network[0]
-        slot = {}
+        # the second layer's weight gradient may wait for this layer's backward only when both
+        # run in the same backward phase: a DP cut between them (split == 2) would all-reduce
+        # that gradient (the buffer's tail) while the lower phase still writes it
+        slot = {} if split == 0 or split >= 4 else None
         h1 = _GatherLinear1.apply(l1.weight, l1.bias, obs, uniq, slot)
-        h1._ocppo_wslot = slot
+        if slot is not None:
+            h1._ocppo_wslot = slot
         if split:
             low = fused_trunk(agent.network[2:split], h1)
             low_d = low.detach().requires_grad_()

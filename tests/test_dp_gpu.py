@@ -51,6 +51,20 @@ def test_two_ranks_share_one_gpu_over_gloo(fused_opt, graphs):
     assert not torch.equal(a0, a1), "ranks must roll out different env shards"
 
 
+def test_overlapped_exchange_equals_the_whole_buffer_exchange():
+    """The split exchange (the tail all-reduced while the lower layers' backward still runs)
+    leaves the same parameters as one all-reduce after the whole backward: nothing the lower
+    phase writes lies in the tail (a weight gradient deferred across the cut would race its
+    all-reduce; encoder_dims (32, 64) puts the cut between the two encoder layers)."""
+    res = []
+    for overlap in (True, False):
+        mgr = mp.Manager()
+        out = mgr.dict()
+        mp.spawn(_worker, args=(2, _port(), out, True, True, overlap), nprocs=2, join=True)
+        res.append(out[0][0])
+    assert torch.equal(res[0], res[1])
+
+
 
 def _rccl_worker(rank, world, port, out, overlap, graphs, collectives=False):
     """The RCCL exchange path at world size 1: nccl (= RCCL) process group bound to cuda:0,
