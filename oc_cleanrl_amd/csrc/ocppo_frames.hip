@@ -26,12 +26,18 @@ namespace ocppo {
 constexpr int kFramesMaxW = 16;
 
 // Latest reset step in (t-(W-1), t] of env n, or INT_MIN when there is none.
+// the latest r in (t - (W-1), t] with dones[r, n] != 0 (INT32_MIN: none). The W - 1 loads are
+// independent (no early exit): issued together, one memory round trip instead of up to W - 1
+// dependent ones on the scatter's and the row table's setup path.
 __device__ __forceinline__ int latest_reset(const float* __restrict__ dones, int t, int64_t n,
                                             int64_t N, int W) {
-  const int lo = t - W + 2 > 0 ? t - W + 2 : 0;
-  for (int r = t; r >= lo; --r)
-    if (dones[r * N + n] != 0.f) return r;
-  return INT32_MIN;
+  int res = INT32_MIN;
+#pragma unroll
+  for (int i = kFramesMaxW - 2; i >= 0; --i) {  // r = t - i, oldest first: the last hit wins
+    const int r = t - i;
+    if (i <= W - 2 && r >= 0 && dones[r * N + n] != 0.f) res = r;
+  }
+  return res;
 }
 
 // x_out[c, :] = f32(frame of timeline id uniq[c]) (zeros for padding ids < 0)

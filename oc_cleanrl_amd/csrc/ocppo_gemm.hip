@@ -833,10 +833,30 @@ __global__ __launch_bounds__(256) void split_planes_kernel(SplitJobs J) {
   const int tl = b - jb.tile0, tr = tl / jb.tiles_c, tc = tl - tr * jb.tiles_c;
   const int r0 = 64 * tr, c0 = 64 * tc;
   __shared__ float tile[64][65];
-  for (int e = threadIdx.x; e < 64 * 64; e += 256) {
-    const int r = e >> 6, c = e & 63;
-    tile[r][c] = r0 + r < jb.R && c0 + c < jb.C ? jb.src[static_cast<int64_t>(r0 + r) * jb.ld + c0 + c]
-                                                  : 0.f;
+  if ((jb.C & 3) == 0 && (jb.ld & 3) == 0 && (reinterpret_cast<uintptr_t>(jb.src) & 15) == 0) {
+    // 16-B loads: 4 per thread, all issued before the LDS stores
+    float4 v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = threadIdx.x + 256 * i, r = e >> 4, c = 4 * (e & 15);
+      v[i] = r0 + r < jb.R && c0 + c < jb.C
+                 ? *reinterpret_cast<const float4*>(jb.src + static_cast<int64_t>(r0 + r) * jb.ld + c0 + c)
+                 : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = threadIdx.x + 256 * i, r = e >> 4, c = 4 * (e & 15);
+      tile[r][c] = v[i].x;
+      tile[r][c + 1] = v[i].y;
+      tile[r][c + 2] = v[i].z;
+      tile[r][c + 3] = v[i].w;
+    }
+  } else {
+    for (int e = threadIdx.x; e < 64 * 64; e += 256) {
+      const int r = e >> 6, c = e & 63;
+      tile[r][c] = r0 + r < jb.R && c0 + c < jb.C
+                       ? jb.src[static_cast<int64_t>(r0 + r) * jb.ld + c0 + c] : 0.f;
+    }
   }
   __syncthreads();
   const int oR = jb.trans ? jb.C : jb.R, oC = jb.trans ? jb.R : jb.C;
