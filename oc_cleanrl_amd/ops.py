@@ -916,8 +916,8 @@ def x6_tile(M: int, N: int, splits: int = 1, tile: int | None = None) -> int | N
     >= 256 workgroups (one per CU; 128 x 128 is the fastest at every config-2 shape that has
     that many, tools/exp_gemm_x6.py), else the one giving the most; None if none divides."""
     if tile is not None:
-        if not 0 <= tile < len(X6_TILES) or X6_TILES[tile][0] == 0:
-            return None  # no such variant
+        if tile not in X6_BUILT:
+            return None  # no such variant in the library
         bm, bn = X6_TILES[tile]
         if tile == X6_MIXED and splits != 1:
             return None

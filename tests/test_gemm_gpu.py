@@ -291,3 +291,31 @@ def test_forward_split_k_with_bias_relu_combine(M, N, K, planes):
     assert torch.equal(ops.linear_x6_split(x, w, b, True, S, planes=pl), out)  # repeatable
     nob = ops.linear_x6_split(x, w, None, False, S)
     assert torch.equal(nob, acc.float())
+
+
+@pytest.mark.parametrize("tile", [24, 56])
+@pytest.mark.parametrize("kind", ["fwd", "dw"])
+def test_one_accumulator_variants_at_long_k(tile, kind):
+    """The shipped one-accumulator variants (24, and the mixed 56) at K = 4096 in one split — the
+    longest reduction config 2 runs (the decoder's weight gradient over 4096 sample rows) — at f32
+    accuracy against f64 and beside hipBLASLt's f32 GEMM."""
+    g = torch.Generator(device=DEV).manual_seed(4096 + tile)
+    M, N, K = 256, 384, 4096
+    if kind == "fwd":
+        x = _rand(M, K, gen=g)
+        w = _rand(N, K, gen=g, scale=K ** -0.5)
+        ref = x.double() @ w.double().t()
+        scale = x.double().abs() @ w.double().abs().t()
+        out = torch.empty(M, N, device=DEV)
+        ops.gemm_x6(x, K, 1, w, K, 1, out, N, M, N, K, tile=tile)
+        _check(out, ref, scale, x @ w.t())
+    else:
+        if tile == 56:
+            pytest.skip("the mixed tiles are not split-K / m-contiguous weight-gradient variants")
+        gg = _rand(K, M, gen=g)  # dW [M, N] = g^T x over K rows, both operands row-contiguous
+        x = _rand(K, N, gen=g)
+        ref = gg.double().t() @ x.double()
+        scale = gg.double().abs().t() @ x.double().abs()
+        out = torch.empty(M, N, device=DEV)
+        ops.gemm_x6(gg, 1, M, x, 1, N, out, N, M, N, K, tile=tile)
+        _check(out, ref, scale, gg.t() @ x)
