@@ -150,19 +150,23 @@ def kernel_flops(tr) -> dict:
 
 
 def gemm_x6_shape(name: str):
-    """(M, N, K, splits, masked) of an ops.gemm_x6 timer site `gemm_x6_{M}x{N}x{K}s{S}[m]`."""
+    """(M, N, K, splits, form) of an ops.gemm_x6 timer site `gemm_x6_{M}x{N}x{K}s{S}[m|w]`
+    (form "m": the masked dX epilogue; "w": the lower layer's weight gradient in the epilogue)."""
     spec = name[len("gemm_x6_"):]
-    masked = spec.endswith("m")
-    dims, S = spec.rstrip("m").split("s")
+    form = spec[-1] if spec[-1] in "mw" else ""
+    dims, S = spec.rstrip("mw").split("s")
     M, N, K = (int(v) for v in dims.split("x"))
-    return M, N, K, int(S), masked
+    return M, N, K, int(S), form
 
 
 def gemm_x6_bytes(name: str) -> int:
     """A [M, K] + B [N, K] f32 in, C [splits, M, N] f32 out (+ the [M, N] ReLU bitmask read,
-    1 bit per element, and the bias-gradient partials written, in the masked dX form)."""
-    M, N, K, S, masked = gemm_x6_shape(name)
-    return 4 * (M * K + N * K + S * M * N) + ((M * N) // 8 + 4 * N * (M // 128) if masked else 0)
+    1 bit per element, and the bias-gradient partials written, in the masked dX form; the "w"
+    form writes no C but reads the lower layer's f32 ReLU output [M, N] as its mask)."""
+    M, N, K, S, form = gemm_x6_shape(name)
+    if form == "w":
+        return 4 * (M * K + N * K + M * N)
+    return 4 * (M * K + N * K + S * M * N) + ((M * N) // 8 + 4 * N * (M // 128) if form == "m" else 0)
 
 
 def mfma_bound(flops, nbytes) -> bool:

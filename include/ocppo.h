@@ -379,6 +379,24 @@ OCPPO_API int ocppo_gemm_x6(ocppo_stream_t stream, const float* a, int64_t sam, 
  * splits == 1; b_planes (mode 1) as ocppo_gemm_x6's. Bitwise ocppo_gemm_x6 on the gathered
  * operand written out.
  * ------------------------------------------------------------------------------------------- */
+/* ---------------------------------------------------------------------------------------------
+ * The dX product of a layer above a Linear+ReLU whose input needs no gradient, with that lower
+ * layer's whole backward in the epilogue (the PPObj encoder's second layer above the first,
+ * ppo_atari_oc.py:605 through architectures/ppo.py:60-84): with C = A B as ocppo_gemm_x6 (A = g'
+ * [M, K] k-contiguous, B(n, k) = W[k, n] n-contiguous: dX = g' W), gp = mask > 0 ? C : 0 (mask
+ * [M, N] = the lower layer's ReLU output, row stride ldm) is never stored; instead
+ *   db[n] = sum_m gp[m, n],   dw[n, k1] = sum_m gp[m, n] x[m, k1]   (x [M, K1], K1 <= 16)
+ * are formed as per-row-tile records in `records` (>= (M / tile rows) * ceil(N / 256) * 256 *
+ * (K1 padded to 4 / 8 / 12 / 16, + 1) floats) and finished later from *finish (as
+ * ocppo_relu_bias_wgrad_rows': ocppo_sum_splits_db_finish or ocppo_deferred_finish_run).
+ * tile 27 (64 x 64) or 24 (128 x 128); M, N multiples of the tile, K % 32 == 0. Deterministic.
+ * ------------------------------------------------------------------------------------------- */
+OCPPO_API int ocppo_gemm_x6_wgrad(ocppo_stream_t stream, const float* a, int64_t sam, int64_t sak,
+                                  const float* b, int64_t sbn, int64_t sbk, int64_t M, int64_t N,
+                                  int64_t K, const float* mask, int64_t ldm, const float* x,
+                                  int64_t ldx, int64_t K1, float* dw, float* db, float* records,
+                                  int64_t records_floats, int tile,
+                                  ocppo_deferred_finish_t* finish);
 OCPPO_API int ocppo_gemm_x6_gather(ocppo_stream_t stream, const float* a, int64_t sam, int64_t sak,
                                    const float* b, int64_t sbn, int64_t sbk, float* c, int64_t ldc,
                                    int64_t M, int64_t N, int64_t K, int64_t splits,

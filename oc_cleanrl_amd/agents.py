@@ -258,6 +258,10 @@ DEFER_BIAS_GRAD = True
 # that launch's finish rides in its split-K combine (ops.sum_splits_db(..., finish=)).
 DEFER_WGRAD_AFTER_FIRST_LAYER = True
 
+# The second encoder layer's dX on gemm_x6 with the first layer's whole backward in its epilogue
+# (ops.dx_x6_wgrad): the dX is never stored and relu_bias_wgrad's rows launch is gone.
+FUSED_L1_IN_DX = True
+
 
 # Split-K partials of FlatAdam-owned weight gradients summed by one HIP pass (ops.sum_splits).
 HIP_SUM_SPLITS = True
@@ -363,8 +367,21 @@ class _LinearAct(torch.autograd.Function):
             # the consumer already applied this layer's ReLU mask: the fused heads backward
             # (_Heads) also wrote its bias gradient; the frame scatter (frames._FramesExpand)
             # left the bias-gradient partials in the box ("dbp"). Only dX and dW remain.
-            dx = _LinearAct._dx_of(ctx, g, w) if ctx.needs_input_grad[0] else None
             dbp = ctx.box.get("dbp")
+            l1 = ctx.wslot.get("l1") if ctx.wslot is not None else None
+            if (l1 is not None and dbp is not None and FUSED_L1_IN_DX and ctx.x6 and
+                    ctx.needs_input_grad[0] and _defer_db_ok(g, x, wgrad, ctx.b) and
+                    ops.dx_x6_wgrad_ok(g, w, x, l1[0])):
+                # this layer's dX is never stored: its epilogue runs the first layer's backward
+                # (mask = x, that layer's ReLU output; ops.dx_x6_wgrad), finished in this layer's
+                # weight-gradient combine; no gradient flows down (the slot says "done")
+                xf, w1, b1 = l1
+                fin = ops.DeferredFinish(g.device)
+                ops.dx_x6_wgrad(g, w, x, xf, w1.grad, b1.grad, fin)
+                ctx.wslot["done"] = True
+                _weight_grad(g, x, out=wgrad, db=(dbp, ctx.b.grad), x6=ctx.x6, finish=fin)
+                return None, None, None, None, None, None
+            dx = _LinearAct._dx_of(ctx, g, w) if ctx.needs_input_grad[0] else None
             if dbp is None:
                 _weight_grad(g, x, out=wgrad, x6=ctx.x6, finish=ctx.box.get("finish"))
             elif _defer_db_ok(g, x, wgrad, ctx.b):

@@ -39,6 +39,12 @@ inline hipStream_t as_stream(ocppo_stream_t s) { return reinterpret_cast<hipStre
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 constexpr int kWave = 64;  // CDNA wavefront width
+// The first-layer weight-gradient record layout (relu_bias_wgrad's rows kernel and gemm_x6's
+// wgrad epilogue write it, relu_bias_wgrad's finish reads it): per row range, for each group of
+// kWgRecCols columns, [value v][column] with v = 0 the bias gradient and v = 1..K the weight
+// columns, K padded to wg_kp(K)
+constexpr int kWgRecCols = 256;
+__host__ __device__ inline int wg_kp(int64_t K) { return K <= 4 ? 4 : K <= 8 ? 8 : K <= 12 ? 12 : 16; }
 
 // ---- element conversions ----------------------------------------------------------------------
 // f32 -> bf16 round-to-nearest-even through the hardware converter (NaN stays NaN).

@@ -92,6 +92,14 @@ struct X6Args {
   // dimension is gw segments of gseg, segment s of row r read from source row gidx[r * gw + s]
   const int32_t* gidx;
   int64_t gw, gseg;
+  // wgrad epilogue (ocppo_gemm_x6_wgrad): the product is the dX of a layer above a Linear+ReLU
+  // whose input rows wx [M, wk] need no gradient; instead of writing dX, each tile writes that
+  // layer's weight / bias-gradient partials (the relu_bias_wgrad record layout, record = row tile)
+  const float* wx;
+  int64_t ldwx;
+  int wk;
+  float* wrec;
+  int64_t wnpw;
 };
 
 // Where one tile's outputs go: its row tiles start at row0_base, its dbp partial row is
@@ -377,7 +385,7 @@ constexpr int kX6GTbl = 1024;
 // segment); 2 B's K index gathered (row-contiguous B, the tile's N range in one segment; gtbl =
 // kX6GTbl ints of LDS)
 template <int FM, int FN, int WGM, int WGN, bool AKC, bool BKC, bool LO, bool PF2, bool BPL = false,
-          int GATH = 0>
+          int GATH = 0, int WGE = 0>
 __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int u, X6Place pl_,
                                         int32_t* gtbl = nullptr) {
   constexpr int NT = 64 * WGM * WGN;
@@ -600,6 +608,81 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
 #endif
   float* __restrict__ Cp = g.c + s * g.split_c;
   const int wr0 = m0 + wm * 16 * FM, wc0 = n0 + wn * 16 * FN;
+  if constexpr (WGE > 0) {
+    // the layer below's backward (relu_bias_wgrad's arithmetic on this tile): gp = mask > 0 ?
+    // acc : 0 is never stored; per column, db = sum_rows gp and dw[k] = sum_rows gp x[row, k],
+    // rows of a lane in order, then the 4 lane row groups (xor 16, 32), then the wave rows in
+    // order; one record slice per tile (record = row tile, columns n0 ..). WGE = K padded.
+    constexpr int KP = WGE, XLD = KP + 1, NV = KP + 1;
+    static_assert(WGM * BN * XLD * 4 <= x6_lds_bytes<FM, FN, WGM, WGN, AKC, BKC>() &&
+                      BM * XLD * 4 <= x6_lds_bytes<FM, FN, WGM, WGN, AKC, BKC>(), "wgrad LDS");
+    const int K1 = g.wk;
+    float* xs = reinterpret_cast<float*>(lds);  // [BM][XLD], zero-padded to KP; the K loop
+    for (int e = t; e < BM * KP; e += NT) {     // ended with a barrier
+      const int r = e / KP, k = e - r * KP;
+      xs[r * XLD + k] = k < K1 ? g.wx[static_cast<int64_t>(m0 + r) * g.ldwx + k] : 0.f;
+    }
+    __syncthreads();
+    float acc[FN][NV];
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int v = 0; v < NV; ++v) acc[j][v] = 0.f;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int lrow = wm * 16 * FM + 16 * i + 4 * fc + r;
+        const int64_t row = m0 + lrow;
+        float xr[KP];
+#pragma unroll
+        for (int k = 0; k < KP; ++k) xr[k] = xs[lrow * XLD + k];
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const float gp = g.mask[row * g.ldm + wc0 + 16 * j + fr] > 0.f ? hi[i][j][r] : 0.f;
+          acc[j][0] += gp;
+#pragma unroll
+          for (int k = 0; k < KP; ++k) acc[j][1 + k] = fmaf(gp, xr[k], acc[j][1 + k]);
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        acc[j][v] += __shfl_xor(acc[j][v], 16, kWave);
+        acc[j][v] += __shfl_xor(acc[j][v], 32, kWave);
+      }
+    __syncthreads();  // xs reads done: the LDS holds the wave-row partials next
+    float* red = reinterpret_cast<float*>(lds);  // [WGM - 1][BN][XLD]
+    if (wm > 0 && fc == 0) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int lc = wn * 16 * FN + 16 * j + fr;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) red[((wm - 1) * BN + lc) * XLD + v] = acc[j][v];
+      }
+    }
+    __syncthreads();
+    if (wm == 0 && fc == 0) {
+      float* rec = g.wrec + static_cast<int64_t>(tm) * g.wnpw;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int lc = wn * 16 * FN + 16 * j + fr;
+        const int col = n0 + lc;
+        const int cgi = col / kWgRecCols;
+        float* rc = rec + static_cast<int64_t>(cgi) * kWgRecCols * NV + (col - cgi * kWgRecCols);
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+          float sv = acc[j][v];
+#pragma unroll
+          for (int q = 0; q + 1 < WGM; ++q) sv += red[(q * BN + lc) * XLD + v];
+          rc[static_cast<int64_t>(v) * kWgRecCols] = sv;
+        }
+      }
+    }
+    return;
+  }
   if (g.mask || g.mbits_in) {
     // threshold_backward(acc, mask, 0) and the tile's column sums: rows of a lane (i, r) in
     // order, then the wave's 4 row groups (xor 16, 32), then the two wave rows through LDS
@@ -669,15 +752,15 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
 }
 
 template <int FM, int FN, int WGM, int WGN, bool AKC, bool BKC, bool LO, bool PF2, bool BPL = false,
-          int GATH = 0>
+          int GATH = 0, int WGE = 0>
 __global__ __launch_bounds__(64 * WGM * WGN, OCPPO_X6_OCC) void gemm_x6_kernel(X6Args g) {
   __shared__ __attribute__((aligned(16)))
   unsigned char lds[x6_lds_bytes<FM, FN, WGM, WGN, AKC, BKC>()];
   __shared__ int32_t gtbl[GATH == 2 ? kX6GTbl : 1];
   const int u = x6_remap(blockIdx.x, gridDim.x);
   if (u >= g.units) return;
-  x6_unit<FM, FN, WGM, WGN, AKC, BKC, LO, PF2, BPL, GATH>(g, lds, u,
-                                                         X6Place{g.tiles_m, 0, 0, 1, 0}, gtbl);
+  x6_unit<FM, FN, WGM, WGN, AKC, BKC, LO, PF2, BPL, GATH, WGE>(
+      g, lds, u, X6Place{g.tiles_m, 0, 0, 1, 0}, gtbl);
 }
 
 // Mixed tiles: workgroups [0, nbig) take the 128 x 128 tiles of rows [0, mbig) (dispatched
@@ -1028,4 +1111,60 @@ extern "C" int ocppo_gemm_x6_gather(ocppo_stream_t stream, const float* a, int64
   clear_stale_error();
   launch_x6_gather(as_stream(stream), mode, g);
   return check_launch("ocppo_gemm_x6_gather");
+}
+
+namespace ocppo {
+void wgrad_record(ocppo_deferred_finish_t* out, const float* partials, int G, int64_t N, int K,
+                  float* dw, float* db);  // ocppo_linear_bwd.hip
+}
+
+// dX of a layer above a Linear+ReLU with the lower layer's whole backward in the epilogue
+extern "C" int ocppo_gemm_x6_wgrad(ocppo_stream_t stream, const float* a, int64_t sam,
+                                   int64_t sak, const float* b, int64_t sbn, int64_t sbk,
+                                   int64_t M, int64_t N, int64_t K, const float* mask,
+                                   int64_t ldm, const float* x, int64_t ldx, int64_t K1,
+                                   float* dw, float* db, float* records, int64_t records_floats,
+                                   int tile, ocppo_deferred_finish_t* finish) {
+  OCPPO_REQUIRE(tile == 24 || tile == 27, "ocppo_gemm_x6_wgrad: tile %d (24 or 27)", tile);
+  const X6Tile tc = kX6Tiles[tile & 7];
+  const int64_t bm = 16 * tc.fm * tc.wgm, bn = 16 * tc.fn * tc.wgn;
+  OCPPO_REQUIRE(M >= bm && N >= bn && M % bm == 0 && N % bn == 0 && K >= 32 && K % kX6BK == 0 &&
+                    M <= INT32_MAX && N <= INT32_MAX && K <= INT32_MAX && K1 >= 1 && K1 <= 16,
+                "ocppo_gemm_x6_wgrad: bad sizes M=%lld N=%lld K=%lld K1=%lld", (long long)M,
+                (long long)N, (long long)K, (long long)K1);
+  OCPPO_REQUIRE(a && b && mask && x && dw && db && records && finish,
+                "ocppo_gemm_x6_wgrad: null pointer");
+  OCPPO_REQUIRE(sak == 1 && sam >= K && sam % 4 == 0 && sbn == 1 && sbk >= N && sbk % 4 == 0 &&
+                    ldm >= N && ldx >= K1,
+                "ocppo_gemm_x6_wgrad: a k-contiguous A, an n-contiguous B (a dX product), "
+                "ldm >= N, ldx >= K1");
+  OCPPO_REQUIRE(reinterpret_cast<uintptr_t>(a) % 16 == 0 && reinterpret_cast<uintptr_t>(b) % 16 == 0,
+                "ocppo_gemm_x6_wgrad: A and B must be 16-B aligned");
+  const int64_t tiles_m = M / bm;
+  const int64_t npw = ((N + kWgRecCols - 1) / kWgRecCols) * kWgRecCols * (wg_kp(K1) + 1);
+  OCPPO_REQUIRE(records_floats >= tiles_m * npw,
+                "ocppo_gemm_x6_wgrad: records need %lld floats", (long long)(tiles_m * npw));
+  X6Args g{a, sam, sak, b, sbn, sbk, nullptr, N, nullptr, 0, (int)M, (int)N, (int)K,
+           (int)tiles_m, (int)(N / bn), (int)(tiles_m * (N / bn)), 1, 0, mask, ldm, nullptr,
+           nullptr, nullptr, 0, nullptr, 0, 0, nullptr, 0, 0, x, ldx, (int)K1, records, npw};
+  clear_stale_error();
+  hipStream_t s = as_stream(stream);
+  const dim3 grid(g.units), block(64 * tc.wgm * tc.wgn);
+  // the 64 x 64 tile (the fastest for the PPObj second layer's dX [11520 x 256] from K = 512,
+  // tools/exp_gemm_x6.py) and the 128 x 128 one, K1 padded to 4 / 8 / 12 / 16
+#define OCPPO_X6W(FM_, FN_, KP_)                                                                  \
+  hipLaunchKernelGGL((gemm_x6_kernel<FM_, FN_, 2, 2, true, false, false, true, false, 0, KP_>),   \
+                     grid, block, 0, s, g)
+  const int kp = wg_kp(K1);
+  if (tile == 27) {
+    if (kp == 4) OCPPO_X6W(2, 2, 4); else if (kp == 8) OCPPO_X6W(2, 2, 8);
+    else if (kp == 12) OCPPO_X6W(2, 2, 12); else OCPPO_X6W(2, 2, 16);
+  } else {
+    if (kp == 4) OCPPO_X6W(4, 4, 4); else if (kp == 8) OCPPO_X6W(4, 4, 8);
+    else if (kp == 12) OCPPO_X6W(4, 4, 12); else OCPPO_X6W(4, 4, 16);
+  }
+#undef OCPPO_X6W
+  if (int rc = check_launch("ocppo_gemm_x6_wgrad")) return rc;
+  ocppo::wgrad_record(finish, records, static_cast<int>(tiles_m), N, static_cast<int>(K1), dw, db);
+  return OCPPO_OK;
 }

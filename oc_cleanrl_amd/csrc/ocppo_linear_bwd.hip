@@ -645,7 +645,7 @@ inline int wg_chunks(int64_t R, int64_t N) {
 #ifndef OCPPO_WR_GRID
 #define OCPPO_WR_GRID 256
 #endif
-constexpr int kWrCols = 256;       // columns per workgroup (64 lanes x 4)
+constexpr int kWrCols = kWgRecCols;  // columns per workgroup (64 lanes x 4)
 constexpr int kWrWaves = OCPPO_WR_WAVES;  // 2 waves per SIMD: enough loads in flight per CU
 constexpr int kWrU = 8;            // rows in flight per wave
 constexpr int kWrStage = 128;      // rows of x staged in LDS at a time
@@ -836,7 +836,6 @@ static WgFinish launch_wgrad_rows(hipStream_t s, int K, const float* g, const fl
                   dw, db};
 }
 
-inline int wg_kp(int64_t K) { return K <= 4 ? 4 : K <= 8 ? 8 : K <= 12 ? 12 : 16; }
 
 }  // namespace ocppo
 
@@ -919,6 +918,21 @@ extern "C" int ocppo_relu_bias_wgrad_rows(ocppo_stream_t stream, const float* g,
 }
 
 namespace ocppo {
+// a relu_bias_wgrad finish record over G row-range records written by another kernel (gemm_x6's
+// wgrad epilogue) in the same layout
+void wgrad_record(ocppo_deferred_finish_t* out, const float* partials, int G, int64_t N, int K,
+                  float* dw, float* db) {
+  const int KP = wg_kp(K);
+  const int64_t ncg = (N + kWrCols - 1) / kWrCols;
+  const int64_t npw = ncg * kWrCols * (KP + 1);
+  DeferredWgrad d;
+  d.tag = kDeferWgrad;
+  d.f = WgFinish{partials, G, KP + 1, K, static_cast<int>((npw + kWfOut - 1) / kWfOut), npw, N,
+                 dw, db};
+  memset(out, 0, sizeof(*out));
+  memcpy(out, &d, sizeof(d));
+}
+
 // ocppo_deferred_finish_run for a relu_bias_wgrad record (1: done; 0: not such a record)
 int wgrad_finish_run(hipStream_t s, const ocppo_deferred_finish_t* finish) {
   DeferredWgrad d;

@@ -277,12 +277,21 @@ class _GatherLinear1(torch.autograd.Function):
                           lambda: ops.frames_gather_linear(obs, uniq, w, b, relu=True))
         ctx.save_for_backward(x, h1)
         ctx.params, ctx.slot = (w, b), slot
+        if slot is not None:
+            # the next layer's dX may run this layer's backward in its epilogue
+            # (ops.dx_x6_wgrad); it then marks the slot "done" and passes no gradient down
+            slot["l1"] = (x, w, b)
+            ctx.set_materialize_grads(False)
         return h1
 
     @staticmethod
     def backward(ctx, g):
         x, h1 = ctx.saved_tensors
         w, b = ctx.params
+        if ctx.slot is not None:
+            ctx.slot.pop("l1", None)
+            if ctx.slot.pop("done", False) or g is None:
+                return None, None, None, None, None
         g = g.contiguous()
         run = ctx.slot.pop("run", None) if ctx.slot is not None else None
         if run is None or g.shape[0] == 0:

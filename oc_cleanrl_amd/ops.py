@@ -1096,6 +1096,48 @@ def dx_x6(g, w, out=None, planes=None):
                    b_planes=planes)
 
 
+_WG_REC = {}
+
+
+def dx_x6_wgrad_ok(g, w, mask, x) -> bool:
+    """dX = g W with the lower layer's backward in the epilogue (dx_x6_wgrad) applies."""
+    M, N = g.shape
+    K = w.shape[1]
+    return (_x6_operand_ok(g) and w.is_cuda and w.dtype == torch.float32 and w.dim() == 2
+            and w.stride(1) == 1 and w.stride(0) % 4 == 0 and w.data_ptr() % 16 == 0
+            and w.shape[0] == N and N % 32 == 0 and M % 64 == 0 and K % 64 == 0
+            and mask.is_cuda and mask.dtype == torch.float32 and mask.shape == (M, K)
+            and mask.stride(1) == 1 and x.is_cuda and x.dtype == torch.float32 and x.dim() == 2
+            and x.shape[0] == M and 1 <= x.shape[1] <= 16 and x.stride(1) == 1)
+
+
+def dx_x6_wgrad(g, w, mask, x, dw, db, defer, tile=27):
+    """The lower Linear+ReLU layer's (dw, db) from this layer's dX = g W without storing dX:
+    gp = mask > 0 ? g W : 0, db = gp.sum(0), dw = gp^T x (ocppo_gemm_x6_wgrad; g [M, N], W [N, K],
+    mask [M, K] the lower layer's ReLU output, x [M, K1] its input rows). The per-row-tile records
+    are finished by the filled DeferredFinish `defer` (sum_splits_db(..., finish=) or run())."""
+    M, N = g.shape
+    K = w.shape[1]
+    K1 = x.shape[1]
+    dev = g.device
+    bm = 64 if tile == 27 else 128
+    kp = 4 if K1 <= 4 else 8 if K1 <= 8 else 12 if K1 <= 12 else 16
+    nrec = (M // bm) * ((K + 255) // 256) * 256 * (kp + 1)
+    key = (dev, M, K, kp, tile)
+    rec = _WG_REC.get(key)
+    if rec is None:
+        rec = _WG_REC[key] = torch.empty(nrec, dtype=torch.float32, device=dev)
+    f = torch.float32
+    args = (g.data_ptr(), g.stride(0), 1, w.data_ptr(), 1, w.stride(0), M, K, N,
+            mask.data_ptr(), mask.stride(0), x.data_ptr(), x.stride(0), K1,
+            _check(dw, "dw", f, dev, K * K1), _check(db, "db", f, dev, K), rec.data_ptr(),
+            rec.numel(), int(tile), defer.ptr())
+    keep = (g, w, mask, x, dw, db, rec)
+    timed(f"gemm_x6_{M}x{K}x{N}s1w", lambda: call("ocppo_gemm_x6_wgrad", _stream(dev), *args)
+          or keep)
+    defer.pending = defer.filled = True
+
+
 def dx_x6_relu(g, w, mask, mbits=None, planes=None):
     """gp = threshold_backward(g W, mask, 0) for the Linear+ReLU layer below whose output is
     `mask` [M, K], with that layer's bias-gradient partials: returns (gp, dbp [M / tile rows, K])

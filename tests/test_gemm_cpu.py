@@ -51,8 +51,11 @@ def test_mbits_words():
 
 
 def test_bench_parses_gemm_sites():
-    assert bench.gemm_x6_shape("gemm_x6_11520x1024x512s1m") == (11520, 1024, 512, 1, True)
-    assert bench.gemm_x6_shape("gemm_x6_512x1024x11520s16") == (512, 1024, 11520, 16, False)
+    assert bench.gemm_x6_shape("gemm_x6_11520x1024x512s1m") == (11520, 1024, 512, 1, "m")
+    assert bench.gemm_x6_shape("gemm_x6_512x1024x11520s16") == (512, 1024, 11520, 16, "")
+    assert bench.gemm_x6_shape("gemm_x6_11520x256x512s1w") == (11520, 256, 512, 1, "w")
+    assert bench.gemm_x6_bytes("gemm_x6_11520x256x512s1w") == 4 * (
+        11520 * 512 + 256 * 512 + 11520 * 256)
     M, N, K = 11520, 1024, 512
     assert bench.gemm_x6_bytes("gemm_x6_11520x1024x512s1") == 4 * (M * K + N * K + M * N)
     assert bench.gemm_x6_bytes("gemm_x6_11520x1024x512s1m") == (

@@ -319,3 +319,66 @@ def test_one_accumulator_variants_at_long_k(tile, kind):
         out = torch.empty(M, N, device=DEV)
         ops.gemm_x6(gg, 1, M, x, 1, N, out, N, M, N, K, tile=tile)
         _check(out, ref, scale, gg.t() @ x)
+
+
+@pytest.mark.parametrize("tile", [27, 24])
+@pytest.mark.parametrize("M,N,K,K1", [(4096, 256, 256, 12), (2048, 512, 256, 6), (128, 64, 64, 16),
+                                      (8192, 256, 512, 3), (1024, 96, 128, 9)])
+def test_dx_with_lower_layer_backward_epilogue(tile, M, N, K, K1):
+    """ocppo_gemm_x6_wgrad: dX = g W is never stored; the epilogue forms gp = (mask > 0 ? dX : 0)
+    and the lower layer's per-row-tile (gp^T x, gp.sum) records, finished by a deferred finish
+    (alone or folded into a sum_splits_db combine). Checked against f64 threshold_backward(g W) ->
+    gp^T x / gp.sum(0), scaled by (|g| |W|) masked, times |x| — f32 accuracy of both products."""
+    if tile == 24 and (K % 128 or M % 128):
+        pytest.skip("the 128 x 128 tile needs M and K multiples of 128")
+    gen = torch.Generator(device=DEV).manual_seed(M + N + K + K1 + tile)
+    g = _rand(M, N, gen=gen)
+    w = _rand(N, K, gen=gen, scale=0.1)
+    mask = torch.relu(_rand(M, K, gen=gen))
+    mask[::7, ::3] = 0.0
+    xs = _rand(M, K1 + 2, gen=gen)
+    x = xs[:, 1:K1 + 1]  # row stride K1 + 2
+    assert ops.dx_x6_wgrad_ok(g, w, mask, x)
+    live = (mask > 0).double()
+    gp = (g.double() @ w.double()) * live
+    ref_w, ref_b = gp.t() @ x.double(), gp.sum(0)
+    sgp = (g.double().abs() @ w.double().abs()) * live
+    sw, sb = sgp.t() @ x.double().abs(), sgp.sum(0)
+    outs = []
+    for fold in (False, True):
+        dw = torch.full((K, K1), float("nan"), device=DEV)
+        db = torch.full((K,), float("nan"), device=DEV)
+        fin = ops.DeferredFinish(DEV)
+        ops.dx_x6_wgrad(g, w, mask, x, dw, db, fin, tile=tile)
+        assert fin.pending
+        if fold:
+            part = _rand(4, 256 * 64, gen=gen)
+            dbp = _rand(30, 128, gen=gen)
+            o_ref, b_ref = torch.empty(256 * 64, device=DEV), torch.empty(128, device=DEV)
+            ops.sum_splits_db(part, o_ref, (dbp, 30), b_ref)
+            o, b_ = torch.empty_like(o_ref), torch.empty_like(b_ref)
+            ops.sum_splits_db(part, o, (dbp, 30), b_, finish=fin)
+            assert torch.equal(o, o_ref) and torch.equal(b_, b_ref)
+        else:
+            fin.run()
+        assert not fin.pending
+        torch.cuda.synchronize()
+        assert ((dw.double() - ref_w).abs() / sw.clamp_min(1e-30)).max().item() < 1e-6
+        assert ((db.double() - ref_b).abs() / sb.clamp_min(1e-30)).max().item() < 1e-6
+        outs.append((dw, db))
+    # alone or folded, bitwise the same (one fixed order)
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+def test_dx_with_lower_layer_backward_rejects_bad_sizes():
+    g = torch.randn(4096, 256, device=DEV)
+    w = torch.randn(256, 256, device=DEV)
+    mask = torch.relu(torch.randn(4096, 256, device=DEV))
+    fin = ops.DeferredFinish(DEV)
+    dw, db = torch.empty(256, 17, device=DEV), torch.empty(256, device=DEV)
+    with pytest.raises(RuntimeError, match="bad sizes"):
+        ops.dx_x6_wgrad(g, w, mask, torch.randn(4096, 17, device=DEV), dw, db, fin)
+    assert not fin.pending
+    with pytest.raises(RuntimeError, match="bad sizes"):
+        ops.dx_x6_wgrad(g[:4032], w, mask[:4032], torch.randn(4032, 12, device=DEV),
+                        torch.empty(256, 12, device=DEV), db, fin, tile=24)  # M % 128

@@ -620,20 +620,95 @@ def test_gathered_decoder_matches_the_expanded_one(dev, toggle):
     mod, name = ((frames, "FUSED_DECODE_GATHER") if toggle == "decode_gather"
                  else (agents, "DEFER_WGRAD_AFTER_FIRST_LAYER"))
 
+    from oc_cleanrl_amd import ops
+
+    # the switched path must actually run at these sizes: count its own entry's calls
+    probe = "dw_x6_parts_gather" if toggle == "decode_gather" else "relu_bias_wgrad"
+
     def run(on):
         setattr(mod, name, on)
+        fused = agents.FUSED_L1_IN_DX
+        agents.FUSED_L1_IN_DX = False  # the fused first-layer backward bypasses both paths
+        real, calls = getattr(ops, probe), []
+
+        def spy(*a, **k):
+            if probe == "dw_x6_parts_gather" or k.get("defer") is not None:
+                calls.append(1)
+            return real(*a, **k)
+
+        setattr(ops, probe, spy)
         try:
+            # config 2's minibatch (11520 distinct frames): the sizes where the encoder's dX
+            # products run on gemm_x6 with the lower layer's ReLU backward claimed
             args = finalize(Args(env_id="ALE/Pong-v5", obs_mode="obj", architecture="PPO_OBJ",
-                                 num_envs=128, num_steps=32, num_minibatches=1, update_epochs=1,
-                                 total_timesteps=128 * 32 * 4, save_model=False), 1)
+                                 num_envs=128, num_steps=128, num_minibatches=4, update_epochs=1,
+                                 num_features=12, total_timesteps=128 * 128 * 4,
+                                 save_model=False), 1)
             tr = PPOTrainer(args, dev, log=False)
             for _ in range(2):
                 tr.train_iteration()
             torch.cuda.synchronize()
+            tr.probe_calls = len(calls)
             return tr
         finally:
             setattr(mod, name, True)
+            agents.FUSED_L1_IN_DX = fused
+            setattr(ops, probe, real)
 
     a, b = run(True), run(False)
+    assert a.probe_calls > 0 and b.probe_calls == 0, (a.probe_calls, b.probe_calls)
     assert a.param_checksum() == b.param_checksum()
     assert torch.equal(a.stats, b.stats)
+
+
+def test_first_layer_backward_in_second_layer_dx(dev):
+    """agents.FUSED_L1_IN_DX: the second encoder layer's dX runs the first layer's backward in its
+    epilogue (ocppo_gemm_x6_wgrad; dX never stored, no rows launch) — the same sums in another
+    order, so the parameters after two iterations at config 2's network agree to f32 rounding
+    carried through two Adam steps, and the fused kernel is the one that ran."""
+    from oc_cleanrl_amd import agents, ops
+    from oc_cleanrl_amd.args import Args, finalize
+    from oc_cleanrl_amd.trainer import PPOTrainer
+
+    def run(on):
+        old = agents.FUSED_L1_IN_DX
+        agents.FUSED_L1_IN_DX = on
+        calls = []
+        real = ops.dx_x6_wgrad
+
+        def spy(*a, **k):
+            calls.append(a[0].shape)
+            return real(*a, **k)
+
+        ok_real = ops.dx_x6_wgrad_ok
+        seen = []
+
+        def ok_spy(g, w, mask, x):
+            r = ok_real(g, w, mask, x)
+            seen.append((tuple(g.shape), tuple(w.shape), tuple(x.shape), g.stride(), r))
+            return r
+
+        ops.dx_x6_wgrad = spy
+        ops.dx_x6_wgrad_ok = ok_spy
+        try:
+            # config 2's minibatch (11520 distinct frames): the sizes where the encoder's dX
+            # products run on gemm_x6 with the lower layer's ReLU backward claimed
+            args = finalize(Args(env_id="ALE/Pong-v5", obs_mode="obj", architecture="PPO_OBJ",
+                                 num_envs=128, num_steps=128, num_minibatches=4, update_epochs=1,
+                                 num_features=12, total_timesteps=128 * 128 * 4,
+                                 save_model=False), 1)
+            tr = PPOTrainer(args, dev, log=False)
+            for _ in range(2):
+                tr.train_iteration()
+            torch.cuda.synchronize()
+            return tr, (calls, seen)
+        finally:
+            agents.FUSED_L1_IN_DX = old
+            ops.dx_x6_wgrad = real
+            ops.dx_x6_wgrad_ok = ok_real
+
+    (a, ca), (b, cb) = run(True), run(False)
+    assert ca[0] and not cb[0], (ca, cb)
+    for p, q in zip(a.agent.parameters(), b.agent.parameters()):
+        assert (p - q).abs().max().item() < 2e-5
+    assert torch.allclose(a.stats, b.stats, rtol=1e-3, atol=1e-3)  # a clip flip: 1/4096
