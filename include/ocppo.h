@@ -663,6 +663,22 @@ OCPPO_API int ocppo_synth_env_step(ocppo_stream_t stream, uint64_t seed, const i
                          int64_t step_offset, const int64_t* actions, int64_t N, int64_t D, int pixel_mode,
                          void* frame_out, float* reward_out, float* done_out, float* ep_state);
 
+/* The rollout policy head (ocppo_policy_head_sample, one wave per env) with the synthetic env's
+ * object-frame step fused behind it: the wave that sampled env n's action writes env n's next
+ * frame / reward / done / episode counters exactly as ocppo_synth_env_step(pixel_mode 0) would
+ * from action_out -- one launch for architectures/ppo.py:89-95 + the env step of
+ * ppo_atari_oc.py:506-511. Entropy and logits are not produced.
+ *   N <= 3072 (<= 2048 when H > 512), H in {256, 512, 768, 1024}, A <= 7, D <= 4096; hidden and
+ *   the head weights 16-B aligned (else OCPPO_ERR_INVALID: use the two launches). */
+OCPPO_API int ocppo_policy_head_env_step(ocppo_stream_t stream, const float* hidden, int64_t N,
+                                         int64_t H, const float* w_actor, const float* b_actor,
+                                         const float* w_critic, const float* b_critic,
+                                         const float* noise, int64_t A, int64_t* action_out,
+                                         float* logprob_out, float* value_out, uint64_t seed,
+                                         const int64_t* step_base, int64_t step_offset, int64_t D,
+                                         float* frame_out, float* reward_out, float* done_out,
+                                         float* ep_state);
+
 /* ---------------------------------------------------------------------------------------------
  * Policy heads forward + fused PPO loss + heads backward in one pass over the decoder output
  * (ppo_atari_oc.py:566-605 from h = relu(z) on; architectures/ppo.py:81-84):

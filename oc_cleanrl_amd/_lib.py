@@ -81,6 +81,8 @@ SIGNATURES: dict[str, tuple[type, list]] = {
     "ocppo_epsilon_greedy": (I, [P, P, I64, I64, U64, P, I64, D, D, D, P, P]),
     "ocppo_td_loss_fwd_bwd": (I, [P, P, P, P, P, P, I64, I64, D, P, P]),
     "ocppo_synth_env_step": (I, [P, U64, P, I64, P, I64, I64, I, P, P, P, P]),
+    "ocppo_policy_head_env_step": (I, [P, P, I64, I64, P, P, P, P, P, I64, P, P, P, U64, P, I64,
+                                       I64, P, P, P, P]),
     "ocppo_cartpole_step": (I, [P, U64, P, I64, P, P, P, P, P, P]),
     "ocppo_heads_loss_workspace_bytes": (SZ, [I64, I64, I64]),
     "ocppo_heads_loss_fwd_bwd": (I, [P, P, I64, I64, P, P, P, P, I64, P, P, P, P, P, P, D, D, D, I,

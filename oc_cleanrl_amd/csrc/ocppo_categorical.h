@@ -57,7 +57,7 @@ __device__ __forceinline__ float categorical_entropy(const float (&ln)[AMAX],
 
 // Categorical tail for one environment given its A logits (l[7] = value) and Exp(1) noise:
 // writes action, log-prob, value, entropy, logits.
-__device__ __forceinline__ void head_tail(const float (&l)[8], const float (&nzj)[7], int A,
+__device__ __forceinline__ int head_tail(const float (&l)[8], const float (&nzj)[7], int A,
                                           int64_t n, int64_t* __restrict__ action_out,
                                           float* __restrict__ logprob_out,
                                           float* __restrict__ entropy_out,
@@ -80,7 +80,7 @@ __device__ __forceinline__ void head_tail(const float (&l)[8], const float (&nzj
 #pragma unroll
   for (int j = 0; j < 7; ++j)
     if (j == best) lp = ln[j];
-  if (!store) return;
+  if (!store) return best;
   action_out[n] = best;
   logprob_out[n] = lp;
   value_out[n] = l[7];
@@ -90,6 +90,7 @@ __device__ __forceinline__ void head_tail(const float (&l)[8], const float (&nzj
     for (int j = 0; j < 7; ++j)
       if (j < A) logits_out[n * A + j] = l[j];
   }
+  return best;
 }
 
 // The policy head's row access for H = 256*CH (lane = float4 columns c*64 + lane of the row) and

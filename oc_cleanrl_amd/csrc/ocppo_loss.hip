@@ -21,6 +21,7 @@
 
 #include "ocppo_common.h"
 #include "ocppo_categorical.h"
+#include "ocppo_synth_env.h"
 
 namespace ocppo {
 
@@ -861,13 +862,28 @@ __global__ __launch_bounds__(256) void policy_head_sample_kernel(
 // HBM-bound) and the per-env outputs are stored coalesced.
 constexpr int kHeadWavesPerBlock = 4;
 
-template <int CH>
+// The synthetic env's step fused behind the head (ENV: E = 1, object frames): the wave that
+// sampled env n's action steps env n right away -- lanes k < D write frame element k, lane 0 the
+// reward / done / episode counters -- so the rollout step needs no env launch (the env of step t
+// depends only on env n's own action).
+struct HeadEnv {
+  uint64_t seed;
+  const int64_t* step_base;
+  int64_t step_offset;
+  int64_t D;
+  float* frame;
+  float* reward;
+  float* done;
+  float* ep;
+};
+
+template <int CH, bool ENV = false>
 __global__ __launch_bounds__(256) void policy_head_fast_kernel(
     const float* __restrict__ hidden, int64_t N, int E, const float* __restrict__ wa,
     const float* __restrict__ ba, const float* __restrict__ wc, const float* __restrict__ bc,
     const float* __restrict__ noise, int A, int64_t* __restrict__ action_out,
     float* __restrict__ logprob_out, float* __restrict__ entropy_out,
-    float* __restrict__ value_out, float* __restrict__ logits_out) {
+    float* __restrict__ value_out, float* __restrict__ logits_out, HeadEnv env = HeadEnv{}) {
   constexpr int H = 256 * CH;
   __shared__ float s_logit[kHeadWavesPerBlock][kWave][9];  // [wave][env in group][8 (+pad)]
   const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
@@ -899,9 +915,17 @@ __global__ __launch_bounds__(256) void policy_head_fast_kernel(
 #pragma unroll
       for (int j = 0; j < 7; ++j)
         nzj[j] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(nz), j));
-      head_tail(l, nzj, A, g, action_out, logprob_out, entropy_out, value_out, nullptr, lane == 0);
+      const int best =
+          head_tail(l, nzj, A, g, action_out, logprob_out, entropy_out, value_out, nullptr, lane == 0);
       const float mine = __shfl(t, 8 * (lane & 7));  // all lanes take part in the permute
       if (logits_out && lane < A) logits_out[g * A + lane] = mine;
+      if (ENV) {  // best is wave-uniform (every lane ran the same tail on readlane'd values)
+        const uint64_t key =
+            synth_env_key(env.seed, static_cast<uint64_t>(env.step_base[0] + env.step_offset), g);
+        for (int64_t k = lane; k < env.D; k += kWave)
+          env.frame[g * env.D + k] = synth_env_obj(key, k, best);
+        if (lane == 0) synth_env_outcome(key, g, env.reward, env.done, env.ep);
+      }
       if (g + nwaves < ngroups) {
         head_load_row<CH>(hidden, g + nwaves, lane, x);
         nz = lane < A ? noise[(g + nwaves) * A + lane] : 1.f;
@@ -1191,6 +1215,43 @@ extern "C" int ocppo_policy_head_sample(ocppo_stream_t stream, const float* hidd
                        (int)H, w_actor, b_actor, w_critic, b_critic, noise, (int)A, action_out,
                        logprob_out, entropy_out, value_out, logits_out);
   return check_launch("ocppo_policy_head_sample");
+}
+
+extern "C" int ocppo_policy_head_env_step(ocppo_stream_t stream, const float* hidden, int64_t N,
+                                          int64_t H, const float* w_actor, const float* b_actor,
+                                          const float* w_critic, const float* b_critic,
+                                          const float* noise, int64_t A, int64_t* action_out,
+                                          float* logprob_out, float* value_out, uint64_t seed,
+                                          const int64_t* step_base, int64_t step_offset,
+                                          int64_t D, float* frame_out, float* reward_out,
+                                          float* done_out, float* ep_state) {
+  OCPPO_REQUIRE(N >= 1 && N <= 256 * 12 && H >= 256 && H % 256 == 0 && H <= 1024 && A >= 1 &&
+                    A <= 7 && D >= 1 && D <= 4096 && (H <= 512 || N <= 256 * 8),
+                "ocppo_policy_head_env_step: bad sizes N=%lld H=%lld A=%lld D=%lld", (long long)N,
+                (long long)H, (long long)A, (long long)D);
+  OCPPO_REQUIRE(hidden && w_actor && b_actor && w_critic && b_critic && noise && action_out &&
+                    logprob_out && value_out && step_base && frame_out && reward_out && done_out,
+                "ocppo_policy_head_env_step: null pointer");
+  OCPPO_REQUIRE(((reinterpret_cast<uintptr_t>(hidden) | reinterpret_cast<uintptr_t>(w_actor) |
+                  reinterpret_cast<uintptr_t>(w_critic)) & 15) == 0,
+                "ocppo_policy_head_env_step: hidden and head weights must be 16-B aligned");
+  clear_stale_error();
+  hipStream_t s = as_stream(stream);
+  // one wave per environment (the E = 1 form of ocppo_policy_head_sample: same head results)
+  const dim3 hgrid(static_cast<unsigned>(ceil_div(N, static_cast<int64_t>(kHeadWavesPerBlock))));
+  const HeadEnv env{seed, step_base, step_offset, D, frame_out, reward_out, done_out, ep_state};
+#define OCPPO_HEAD(CH)                                                                          \
+  hipLaunchKernelGGL((policy_head_fast_kernel<CH, true>), hgrid, dim3(kWave * kHeadWavesPerBlock), \
+                     0, s, hidden, N, 1, w_actor, b_actor, w_critic, b_critic, noise, (int)A,     \
+                     action_out, logprob_out, nullptr, value_out, nullptr, env)
+  switch (H / 256) {
+    case 1: OCPPO_HEAD(1); break;
+    case 2: OCPPO_HEAD(2); break;
+    case 3: OCPPO_HEAD(3); break;
+    default: OCPPO_HEAD(4); break;
+  }
+#undef OCPPO_HEAD
+  return check_launch("ocppo_policy_head_env_step");
 }
 
 extern "C" int ocppo_minibatch_prepare(ocppo_stream_t stream, const int64_t* perm, int64_t M,

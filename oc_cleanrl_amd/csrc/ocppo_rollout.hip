@@ -8,6 +8,7 @@
 #include <cstdlib>
 #include "ocppo_common.h"
 #include "ocppo_store.h"
+#include "ocppo_synth_env.h"
 
 namespace ocppo {
 
@@ -144,17 +145,7 @@ __global__ __launch_bounds__(256) void store_vecnorm_kernel(
                                 out, net, nullptr, done_out, net_scale, reset_prev);
 }
 
-// ---- synthetic env ------------------------------------------------------------------------------
-__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
-  x += 0x9E3779B97F4A7C15ull;
-  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
-  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
-  return x ^ (x >> 31);
-}
-__device__ __forceinline__ float unit24(uint64_t h) {  // exact multiple of 2^-24 in [0, 1)
-  return static_cast<float>(h >> 40) * (1.0f / 16777216.0f);
-}
-
+// ---- synthetic env (per-element step: ocppo_synth_env.h) --------------------------------------
 template <bool PIXELS>
 __global__ __launch_bounds__(256) void synth_env_kernel(uint64_t seed,
                                                         const int64_t* __restrict__ step_base,
@@ -171,43 +162,11 @@ __global__ __launch_bounds__(256) void synth_env_kernel(uint64_t seed,
        g += stride) {
     const int64_t n = g / D;
     const int64_t k = g - n * D;
-    const uint64_t key = splitmix64(splitmix64(splitmix64(seed) + step) + static_cast<uint64_t>(n));
-    const uint64_t h = splitmix64(key + static_cast<uint64_t>(k));
+    const uint64_t key = synth_env_key(seed, step, n);
     const int64_t a = actions ? actions[n] : 0;
-    if (PIXELS) {
-      uint32_t v = (h % 10u == 0u) ? static_cast<uint32_t>((h >> 8) & 0xFFu) : 0u;
-      if (k < 84) v = static_cast<uint32_t>((a * 37) & 0xFF);
-      static_cast<uint8_t*>(frame_out)[g] = static_cast<uint8_t>(v);
-    } else {
-      const int field = static_cast<int>(k & 3);
-      uint64_t v;
-      if (field == 0) v = h % 160u;
-      else if (field == 1) v = (k == 1) ? (h % 210u + 7u * static_cast<uint64_t>(a)) % 210u : h % 210u;
-      else v = 1u + h % 16u;
-      static_cast<float*>(frame_out)[g] = static_cast<float>(v);
-    }
-    if (k == 0) {
-      const float ur = unit24(splitmix64(key ^ 0x5DEECE66Dull));
-      const float r = ur < 0.005f ? 1.f : (ur < 0.01f ? -1.f : 0.f);
-      const float ud = unit24(splitmix64(key ^ 0xB5297A4Dull));
-      const float d = ud < (1.0f / 3500.0f) ? 1.f : 0.f;
-      reward_out[n] = r;
-      done_out[n] = d;
-      if (ep) {
-        float* e = ep + n * 5;
-        const float run_ret = e[0] + r, run_len = e[1] + 1.f;
-        if (d != 0.f) {
-          e[2] += run_ret;
-          e[3] += run_len;
-          e[4] += 1.f;
-          e[0] = 0.f;
-          e[1] = 0.f;
-        } else {
-          e[0] = run_ret;
-          e[1] = run_len;
-        }
-      }
-    }
+    if (PIXELS) static_cast<uint8_t*>(frame_out)[g] = synth_env_pixel(key, k, a);
+    else static_cast<float*>(frame_out)[g] = synth_env_obj(key, k, a);
+    if (k == 0) synth_env_outcome(key, n, reward_out, done_out, ep);
   }
 }
 

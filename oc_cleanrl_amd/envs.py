@@ -26,6 +26,7 @@ class SyntheticAtariEnv:
     """
 
     integer_obs = True  # integer coordinates <= 210 / u8 pixels: bf16 / u8 storage is exact
+    synthetic = True    # its step is ocppo_synth_env_step's (the policy head may fuse it)
 
     def __init__(self, env_id: str, obs_mode: str, num_envs: int, num_features: int, seed: int,
                  device, window: int = 4):

@@ -393,6 +393,43 @@ def policy_head_sample(hidden, w_actor, b_actor, w_critic, b_critic, noise, acti
     return action_out, logprob_out, value_out
 
 
+def policy_head_env_ok(hidden, w_actor, w_critic, env) -> bool:
+    """policy_head_env_step applies: the E = 1 head form and an object-frame synthetic env."""
+    N, H = hidden.shape
+    A = w_actor.shape[0]
+    fr = getattr(env, "frame", None)
+    return (getattr(env, "synthetic", False) and fr is not None and fr.dtype == torch.float32
+            and fr.is_contiguous() and 1 <= fr.shape[1] <= 4096 and fr.shape[0] == N
+            and 1 <= N <= (3072 if H <= 512 else 2048) and H % 256 == 0 and 256 <= H <= 1024
+            and 1 <= A <= 7 and hidden.is_contiguous() and w_actor.is_contiguous()
+            and w_critic.is_contiguous()
+            and (hidden.data_ptr() | w_actor.data_ptr() | w_critic.data_ptr()) % 16 == 0)
+
+
+def policy_head_env_step(hidden, w_actor, b_actor, w_critic, b_critic, noise, action_out,
+                         logprob_out, value_out, env, step_offset: int):
+    """policy_head_sample + env.step(action_out, step_offset) in one launch
+    (ocppo_policy_head_env_step; env a SyntheticAtariEnv with object frames)."""
+    N, H = hidden.shape
+    A = w_actor.shape[0]
+    dev = hidden.device
+    f = torch.float32
+    if tuple(w_actor.shape) != (A, H) or w_critic.numel() != H or b_actor.numel() != A:
+        raise ValueError("head weights do not match hidden")
+    D = env.frame.shape[1]
+    call("ocppo_policy_head_env_step", _stream(dev), _check(hidden, "hidden", f, dev), N, H,
+         _check(w_actor, "w_actor", f, dev), _check(b_actor, "b_actor", f, dev, A),
+         _check(w_critic, "w_critic", f, dev, H), _check(b_critic, "b_critic", f, dev, 1),
+         _check(noise, "noise", f, dev, N * A), A,
+         _check(action_out, "action_out", torch.int64, dev, N),
+         _check(logprob_out, "logprob_out", f, dev, N), _check(value_out, "value_out", f, dev, N),
+         env.seed & 0xFFFFFFFFFFFFFFFF, _check(env.step_base, "step_base", torch.int64, dev, 1),
+         int(step_offset), D, _check(env.frame, "frame", f, dev, N * D),
+         _check(env.reward, "reward", f, dev, N), _check(env.done, "done", f, dev, N),
+         _opt(env.ep_state, "ep_state", f, dev, N * 5))
+    return action_out, logprob_out, value_out
+
+
 class _CategoricalLogProbEntropy(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, actions):

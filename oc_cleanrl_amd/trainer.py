@@ -52,6 +52,11 @@ def storage_dtype(args: Args, pixels: bool, integer_obs: bool = True) -> torch.d
     return {"f32": torch.float32, "bf16": torch.bfloat16, "u8": torch.uint8}[choice]
 
 
+# The rollout's synthetic object-frame env step fused into the policy head's launch
+# (ops.policy_head_env_step: bitwise the two-launch step; one launch fewer per env step).
+FUSED_HEAD_ENV = True
+
+
 class FlatGrads:
     """All parameter grads as views of ONE persistent f32 buffer: the DP all-reduce is a single
     in-place RCCL call (ppo_atari_multigpu.py:360-374 builds the same flat vector with torch.cat
@@ -567,13 +572,16 @@ class PPOTrainer:
     def _rollout_step(self, t: int):
         """One env step of the rollout (:500-514): network trunk (PyTorch) → fused HIP policy
         head (actor+critic GEMVs + Categorical sample, writes actions/logprobs/values rows) →
-        env → fused HIP store (+ VecNormalize) of the next obs slot and reward/done rows."""
-        self._act(t)
-        self.timer.bracket("env_step", lambda: self.env.step(self.actions[t], t))
+        env → fused HIP store (+ VecNormalize) of the next obs slot and reward/done rows. With
+        the synthetic object-frame env the env step rides in the head's launch
+        (ops.policy_head_env_step)."""
+        if not self._act(t, env_step=True):
+            self.timer.bracket("env_step", lambda: self.env.step(self.actions[t], t))
         if not self.rollout_fusion:  # else the store rides in step t+1's encoder launch
             self._store(t)
 
-    def _act(self, t: int):
+    def _act(self, t: int, env_step: bool = False) -> bool:
+        """Actions / log-probs / values of step t; True when the env step ran too."""
         ag = self.agent
         if self.args.per_step_noise:
             # the reference's stream: one Exp(1) draw of [N, A] per step (Categorical.sample at
@@ -581,6 +589,13 @@ class PPOTrainer:
             self.noise[t].exponential_()
         if self.fused_head:
             hidden = self._policy_hidden(t)
+            if env_step and FUSED_HEAD_ENV and ops.policy_head_env_ok(
+                    hidden, ag.actor.weight, ag.critic.weight, self.env):
+                self.timer.bracket("action_head_env", lambda: ops.policy_head_env_step(
+                    hidden, ag.actor.weight, ag.actor.bias, ag.critic.weight, ag.critic.bias,
+                    self.noise[t], self.actions[t], self.logprobs[t], self.values[t], self.env,
+                    t))
+                return True
             self.timer.bracket("action_head", lambda: ops.policy_head_sample(
                 hidden, ag.actor.weight, ag.actor.bias, ag.critic.weight, ag.critic.bias,
                 self.noise[t], self.actions[t], self.logprobs[t], self.values[t]))
@@ -589,6 +604,7 @@ class PPOTrainer:
             self.timer.bracket("action_head", lambda: ops.categorical_sample(
                 logits, self.noise[t], self.actions[t], self.logprobs[t], None, value.view(-1),
                 self.values[t]))
+        return False
 
     def _store(self, t: int):
         a = self.args

@@ -512,6 +512,49 @@ def test_policy_head_sample(ops, dev, N, H, A):
     assert torch.equal(act, a2) and torch.equal(lp, lp2) and torch.equal(ent, e2)
 
 
+@pytest.mark.parametrize("N,H,A,D", [(128, 512, 6, 12), (1, 256, 3, 4), (3072, 512, 7, 12),
+                                     (2048, 1024, 6, 100), (77, 768, 1, 65)])
+def test_policy_head_env_step_is_bitwise_the_two_launches(ops, dev, N, H, A, D):
+    """ocppo_policy_head_env_step = ocppo_policy_head_sample then ocppo_synth_env_step on its
+    actions: bit for bit (actions, log-probs, values, next frame, reward, done, episode counters),
+    over several steps so the counters carry."""
+    from oc_cleanrl_amd.envs import SyntheticAtariEnv
+
+    g = torch.Generator(device=dev).manual_seed(N + H + A + D)
+    hidden = torch.relu(torch.randn(N, H, device=dev, generator=g))
+    wa = torch.randn(A, H, device=dev, generator=g) * 0.05
+    ba = torch.randn(A, device=dev, generator=g) * 0.1
+    wc = torch.randn(1, H, device=dev, generator=g)
+    bc = torch.randn(1, device=dev, generator=g)
+    envs = [SyntheticAtariEnv("ALE/Pong-v5", "obj", N, D, 5, dev) for _ in range(2)]
+    for e in envs:
+        e.reset()
+    envs[0].ep_state.uniform_(0, 3, generator=g)
+    envs[1].ep_state.copy_(envs[0].ep_state)
+    assert ops.policy_head_env_ok(hidden, wa, wc, envs[0])
+    for t in range(4):
+        noise = torch.empty(N, A, device=dev).exponential_(generator=g)
+        a0, l0, v0 = ops.policy_head_sample(hidden, wa, ba, wc, bc, noise)
+        envs[0].step(a0, t)
+        a1, l1, v1 = (torch.empty_like(a0), torch.empty_like(l0), torch.empty_like(v0))
+        ops.policy_head_env_step(hidden, wa, ba, wc, bc, noise, a1, l1, v1, envs[1], t)
+        torch.cuda.synchronize()
+        assert torch.equal(a0, a1) and torch.equal(l0, l1) and torch.equal(v0, v1)
+        for k in ("frame", "reward", "done", "ep_state"):
+            assert torch.equal(getattr(envs[0], k), getattr(envs[1], k)), (t, k)
+        hidden = torch.relu(hidden + 0.01 * torch.randn(N, H, device=dev, generator=g))
+    # past one env per wave (N > 3072): the host gate says no and the C entry refuses
+    n = 3073
+    e = SyntheticAtariEnv("ALE/Pong-v5", "obj", n, D, 5, dev)
+    big, w5, c5 = (torch.zeros(n, 512, device=dev), torch.zeros(A, 512, device=dev),
+                   torch.zeros(1, 512, device=dev))
+    assert not ops.policy_head_env_ok(big, w5, c5, e)
+    with pytest.raises(RuntimeError, match="bad sizes"):
+        ops.policy_head_env_step(big, w5, ba, c5, bc, torch.ones(n, A, device=dev),
+                                 torch.empty(n, dtype=torch.int64, device=dev),
+                                 torch.empty(n, device=dev), torch.empty(n, device=dev), e, 0)
+
+
 @pytest.mark.parametrize("pixel,N,D", [(False, 128, 12), (True, 16, 7056), (False, 1000, 6)])
 def test_store_vecnorm_equals_separate_kernels(ops, dev, pixel, N, D):
     rng = np.random.default_rng(N)

@@ -429,6 +429,36 @@ def test_rollout_cache_ring_is_bitwise_the_shifted_cache(dev):
         assert torch.equal(p, q)
 
 
+def test_head_env_fusion_is_bitwise_the_two_launch_step(dev):
+    """trainer.FUSED_HEAD_ENV: the synthetic env's step in the policy head's launch leaves the
+    rollout buffers and the parameters bit for bit where the two-launch step does (two iterations,
+    captured rollouts), and the fused launch is the one that ran."""
+    from oc_cleanrl_amd import ops as _ops, trainer
+
+    runs = []
+    for on in (False, True):
+        old, real, calls = trainer.FUSED_HEAD_ENV, _ops.policy_head_env_step, []
+
+        def spy(*a, **k):
+            calls.append(1)
+            return real(*a, **k)
+
+        trainer.FUSED_HEAD_ENV, _ops.policy_head_env_step = on, spy
+        try:
+            tr, _ = run_iters(small_args(encoder_dims=(32, 64, 48, 64), decoder_dims=(256,),
+                                         num_steps=18, cuda_graphs=True), 2, dev)
+            torch.cuda.synchronize()
+        finally:
+            trainer.FUSED_HEAD_ENV, _ops.policy_head_env_step = old, real
+        assert bool(calls) == on
+        runs.append(tr)
+    a, b = runs
+    for k in ("obs", "actions", "logprobs", "values", "rewards", "dones", "advantages"):
+        assert torch.equal(getattr(a, k), getattr(b, k)), k
+    assert torch.equal(a.env.ep_state, b.env.ep_state)
+    assert a.param_checksum() == b.param_checksum()
+
+
 def test_fused_heads_loss_updates_match_reference_golden(dev):
     """The update tail as ONE HIP op (heads forward + PPO loss + heads backward with the decoder's
     ReLU mask): two minibatch updates against the reference's own update block
