@@ -751,23 +751,6 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
   if (g.mbits_out) g.mbits_out[tile_id * NT + t] = bits;
 }
 
-// Experiments (tools/build_variant.py): the second workgroup dispatched to each CU of the first
-// wave (XCD-local index 32..63) starts OCPPO_X6_STAGGER x 64 cycles late, or at s_setprio 1
-// (OCPPO_X6_PRIO), so the two co-resident workgroups' split (VALU) and MFMA phases alternate
-// instead of running in lockstep (MI355X_MICROARCH.md, two waves per SIMD)
-__device__ __forceinline__ void x6_stagger() {
-#if defined(OCPPO_X6_STAGGER) || defined(OCPPO_X6_PRIO)
-  if (((blockIdx.x >> 3) & 63) >= 32) {
-#ifdef OCPPO_X6_STAGGER
-    __builtin_amdgcn_s_sleep(OCPPO_X6_STAGGER);
-#endif
-#ifdef OCPPO_X6_PRIO
-    __builtin_amdgcn_s_setprio(1);
-#endif
-  }
-#endif
-}
-
 template <int FM, int FN, int WGM, int WGN, bool AKC, bool BKC, bool LO, bool PF2, bool BPL = false,
           int GATH = 0, int WGE = 0>
 __global__ __launch_bounds__(64 * WGM * WGN, OCPPO_X6_OCC) void gemm_x6_kernel(X6Args g) {
@@ -776,7 +759,6 @@ __global__ __launch_bounds__(64 * WGM * WGN, OCPPO_X6_OCC) void gemm_x6_kernel(X
   __shared__ int32_t gtbl[GATH == 2 ? kX6GTbl : 1];
   const int u = x6_remap(blockIdx.x, gridDim.x);
   if (u >= g.units) return;
-  x6_stagger();
   x6_unit<FM, FN, WGM, WGN, AKC, BKC, LO, PF2, BPL, GATH, WGE>(
       g, lds, u, X6Place{g.tiles_m, 0, 0, 1, 0}, gtbl);
 }
@@ -789,7 +771,6 @@ __global__ __launch_bounds__(256, OCPPO_X6_OCC) void gemm_x6_mixed_kernel(X6Args
   __shared__ __attribute__((aligned(16))) unsigned char lds[x6_lds_bytes<4, 4, 2, 2, AKC, BKC>()];
   const int nbig = (g.mbig / 128) * g.tiles_n;
   const int b = blockIdx.x;
-  x6_stagger();
   if (b < nbig) {
     x6_unit<4, 4, 2, 2, AKC, BKC, false, true, BPL>(g, lds, x6_remap(b, nbig),
                                                     X6Place{g.mbig / 128, 0, 0, 2, 0});
