@@ -907,6 +907,15 @@ __global__ __launch_bounds__(256) void policy_head_fast_kernel(
     float4 x[CH];
     head_load_row<CH>(hidden, g, lane, x);
     for (; g < ngroups; g += nwaves) {
+      // ENV: everything of env g's step that does not depend on its action -- the frame hashes
+      // and the reward / done / episode counters -- while this row's loads are in flight
+      uint64_t key = 0;
+      uint32_t base = 0;
+      if (ENV) {
+        key = synth_env_key(env.seed, static_cast<uint64_t>(env.step_base[0] + env.step_offset), g);
+        if (lane < env.D) base = synth_env_obj_base(key, lane);
+        if (lane == 0) synth_env_outcome(key, g, env.reward, env.done, env.ep);
+      }
       const float t = head_dots<CH>(x, w, lane) + bias;
       float l[8], nzj[7];
 #pragma unroll
@@ -920,11 +929,9 @@ __global__ __launch_bounds__(256) void policy_head_fast_kernel(
       const float mine = __shfl(t, 8 * (lane & 7));  // all lanes take part in the permute
       if (logits_out && lane < A) logits_out[g * A + lane] = mine;
       if (ENV) {  // best is wave-uniform (every lane ran the same tail on readlane'd values)
-        const uint64_t key =
-            synth_env_key(env.seed, static_cast<uint64_t>(env.step_base[0] + env.step_offset), g);
-        for (int64_t k = lane; k < env.D; k += kWave)
+        if (lane < env.D) env.frame[g * env.D + lane] = synth_env_obj_act(base, lane, best);
+        for (int64_t k = lane + kWave; k < env.D; k += kWave)
           env.frame[g * env.D + k] = synth_env_obj(key, k, best);
-        if (lane == 0) synth_env_outcome(key, g, env.reward, env.done, env.ep);
       }
       if (g + nwaves < ngroups) {
         head_load_row<CH>(hidden, g + nwaves, lane, x);

@@ -22,15 +22,22 @@ __device__ __forceinline__ uint64_t synth_env_key(uint64_t seed, uint64_t step, 
   return splitmix64(splitmix64(splitmix64(seed) + step) + static_cast<uint64_t>(n));
 }
 
-// object frames: element k of the newest frame (x, y, w/h fields; y of object 0 follows the action)
-__device__ __forceinline__ float synth_env_obj(uint64_t key, int64_t k, int64_t a) {
+// object frames: element k of the newest frame (x, y, w/h fields; y of object 0 follows the
+// action), in two parts so that a caller can hash before it knows the action: the action-free
+// value, then the action applied (element 1 only)
+__device__ __forceinline__ uint32_t synth_env_obj_base(uint64_t key, int64_t k) {
   const uint64_t h = splitmix64(key + static_cast<uint64_t>(k));
   const int field = static_cast<int>(k & 3);
-  uint64_t v;
-  if (field == 0) v = h % 160u;
-  else if (field == 1) v = (k == 1) ? (h % 210u + 7u * static_cast<uint64_t>(a)) % 210u : h % 210u;
-  else v = 1u + h % 16u;
+  if (field == 0) return static_cast<uint32_t>(h % 160u);
+  if (field == 1) return static_cast<uint32_t>(h % 210u);
+  return static_cast<uint32_t>(1u + h % 16u);
+}
+__device__ __forceinline__ float synth_env_obj_act(uint32_t base, int64_t k, int64_t a) {
+  const uint64_t v = (k == 1) ? (base + 7u * static_cast<uint64_t>(a)) % 210u : base;
   return static_cast<float>(v);
+}
+__device__ __forceinline__ float synth_env_obj(uint64_t key, int64_t k, int64_t a) {
+  return synth_env_obj_act(synth_env_obj_base(key, k), k, a);
 }
 
 // pixel frames: byte k (row 0 encodes the action)
