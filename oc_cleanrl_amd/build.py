@@ -35,6 +35,12 @@ HIP_FLAGS = [
 ]
 
 
+# Per-source extra flags. ocppo_gemm.hip: no SLP packing of scalar f32 ops into v_pk_* (same
+# results) -- beside MFMAs a packed f32 op costs more issue time than the two scalar ones
+# (gemm_x6's operand split: config-2 GEMMs 730 -> 704 us, bench +2.4 %).
+FILE_FLAGS = {"ocppo_gemm.hip": ["-fno-slp-vectorize"]}
+
+
 def sources() -> list[Path]:
     return sorted(CSRC.glob("*.hip"))
 
@@ -59,7 +65,7 @@ def build_hip(force: bool = False, verbose: bool = False) -> Path:
     for src in srcs:
         obj = objdir / (src.stem + ".o")
         objs.append(obj)
-        cmd = [HIPCC, *HIP_FLAGS, "-c", str(src), "-o", str(obj)]
+        cmd = [HIPCC, *HIP_FLAGS, *FILE_FLAGS.get(src.name, []), "-c", str(src), "-o", str(obj)]
         if verbose:
             print(" ".join(cmd))
         procs.append((src, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))

@@ -111,7 +111,7 @@ struct X6Place {
 };
 
 // The three bf16 pieces of an f32 pair (exact: x == x0 + x1 + x2 for finite normal x), packed:
-// p_i = (x_i of a) | (x_i of b) << 16 (v_cvt_pk_bf16_f32 and packed f32 subtractions: 9 VALU
+// p_i = (x_i of a) | (x_i of b) << 16 (v_cvt_pk_bf16_f32 and scalar f32 subtractions: 11 VALU
 // instructions per pair).
 typedef float x6f2 __attribute__((ext_vector_type(2)));
 typedef __bf16 x6h2 __attribute__((ext_vector_type(2)));
@@ -133,11 +133,15 @@ __device__ __forceinline__ void x6_split2(x6f2 v, uint32_t& p0, uint32_t& p1, ui
     p2 = p1;
     return;
   }
+  // the residuals as scalar subtractions (build.py: -fno-slp-vectorize keeps them apart): a
+  // packed f32 VALU op issued beside MFMAs costs more than two scalar ones (MI355X_MICROARCH.md,
+  // filler prices) -- config-2 shapes 730 -> 704 us, bench +2.4 % (profiles/r04/exp_x6_scalar_sub)
   p0 = x6_pk(v);
-  const x6f2 r1 = v - x6_unpk(p0);
-  p1 = x6_pk(r1);
-  const x6f2 r2 = r1 - x6_unpk(p1);
-  p2 = x6_pk(r2);
+  const x6f2 h0 = x6_unpk(p0);
+  const float r1x = v.x - h0.x, r1y = v.y - h0.y;
+  p1 = x6_pk(x6f2{r1x, r1y});
+  const x6f2 h1 = x6_unpk(p1);
+  p2 = x6_pk(x6f2{r1x - h1.x, r1y - h1.y});
 }
 
 // LDS plane layout: rows in pairs of 128 B (row r's 64 B = 16-B chunks 4 (r & 1) .. + 3 of pair

@@ -21,7 +21,8 @@ def main():
         for src in b.sources():
             o = Path(td) / (src.stem + ".o")
             objs.append(o)
-            procs.append(subprocess.Popen([b.HIPCC, *b.HIP_FLAGS, *defs, "-c", str(src), "-o", str(o)]))
+            procs.append(subprocess.Popen([b.HIPCC, *b.HIP_FLAGS, *b.FILE_FLAGS.get(src.name, []),
+                                          *defs, "-c", str(src), "-o", str(o)]))
         assert all(p.wait() == 0 for p in procs)
         subprocess.run([b.HIPCC, f"--offload-arch={b.ARCH}", "-shared", "-fPIC", "-o", str(out),
                         *map(str, objs), "-Wl,-rpath,/opt/rocm/lib",
