@@ -206,6 +206,42 @@ struct X6Stage {
     }
   }
 
+  // Buffer-resource form of load: the piece offsets are fixed per unit (VGPRs, set once) and the
+  // K advance is the scalar offset, so a step's loads need no 64-bit address VALU (41 fewer
+  // v_lshl_add_u64 in the forward kernel). Base = the unit's first (row, k) element; the host
+  // checks that a unit's window fits the 32-bit offsets (x6_windows_ok).
+  struct Buf {
+    __amdgpu_buffer_rsrc_t rs;
+    int32_t vo[kPer][4];
+  };
+  __device__ static void buf_setup(const float* __restrict__ src, int64_t srow, int64_t sk,
+                                   int row0, int kbase, int t, Buf& b) {
+    const float* base = KC ? src + static_cast<int64_t>(row0) * srow + kbase
+                           : src + static_cast<int64_t>(kbase) * sk + row0;
+    b.rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, 0x7fffffff, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int p = t + NT * i;
+      int rq, kq;
+      piece_of(p < kPieces ? p : 0, rq, kq);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        b.vo[i][j] = static_cast<int32_t>(4 * (KC ? (4 * rq + j) * srow + 4 * kq
+                                                  : (4 * kq + j) * sk + 4 * rq));
+    }
+  }
+  __device__ static void load_buf(const Buf& b, int t, int32_t soff, floatx4 (&r)[kPer][4]) {
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int p = t + NT * i;
+      if (kPieces % NT != 0 && p >= kPieces) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        r[i][j] = __builtin_bit_cast(
+            floatx4, __builtin_amdgcn_raw_buffer_load_b128(b.rs, b.vo[i][j], soff, 0));
+    }
+  }
+
   // k-contiguous operand with gathered rows: roff[i][j] = element offset of piece row (i, j)
   // (its source row times the row stride, minus the segment start), fixed for a unit whose K
   // range lies in one segment
@@ -430,12 +466,32 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
       gtbl[r] = g.gidx[static_cast<int64_t>(kb * kX6BK + r) * g.gw + segn];
     __syncthreads();
   }
+  // plain operands load through buffer resources (X6Stage::load_buf): config-2 GEMM set
+  // 715 -> 682 us (profiles/r04/exp_x6_bufld); the pointer form stays for the inline-asm
+  // experiment (OCPPO_X6_ASMLD)
+#ifdef OCPPO_X6_ASMLD
+  constexpr bool kBuf = false;
+#else
+  constexpr bool kBuf = GATH == 0;
+#endif
+  typename SA::Buf bufA;
+  typename SB::Buf bufB;
+  if constexpr (kBuf) {
+    SA::buf_setup(A, g.sam, g.sak, m0, kb * kX6BK, t, bufA);
+    SB::buf_setup(B, g.sbn, g.sbk, n0, kb * kX6BK, t, bufB);
+  }
   auto loadA = [&](int k0, floatx4 (&r)[SA::kPer][4]) {
     if constexpr (GATH == 1) SA::load_rows(A, roffA, k0, t, r);
+    else if constexpr (kBuf)
+      SA::load_buf(bufA, t, static_cast<int32_t>(4 * (AKC ? (k0 - kb * kX6BK)
+                                                        : (k0 - kb * kX6BK) * g.sak)), r);
     else SA::load(A, g.sam, g.sak, m0, k0, t, r);
   };
   auto loadB = [&](int k0, floatx4 (&r)[SB::kPer][4]) {
     if constexpr (GATH == 2) SB::load_ktbl(B, g.sbk, gtbl, kb * kX6BK, coffB, n0, k0, t, r);
+    else if constexpr (kBuf)
+      SB::load_buf(bufB, t, static_cast<int32_t>(4 * (BKC ? (k0 - kb * kX6BK)
+                                                        : (k0 - kb * kX6BK) * g.sbk)), r);
     else SB::load(B, g.sbn, g.sbk, n0, k0, t, r);
   };
 
@@ -539,7 +595,7 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
     constexpr int kLoads = 4 * (SA::kPer + SB::kPer);  // loads per step per thread
     static_assert(!ASM || kLoads == 8, "x6_vmwait counts assume 8 loads per step");
     floatx4 rb[SB::kPer][4], qa[SA::kPer][4], qb[SB::kPer][4];
-    if constexpr (GATH != 0) {
+    if constexpr (GATH != 0 || kBuf) {
       loadA(kb * kX6BK, ra);
       loadB(kb * kX6BK, rb);
       if (nk > 1) {
@@ -570,7 +626,7 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
                     floatx4 (&stA)[SA::kPer][4], floatx4 (&stB)[SB::kPer][4]) {
       const bool issue = kt + 2 < nk;
       if (issue) {
-        if constexpr (GATH != 0) {
+        if constexpr (GATH != 0 || kBuf) {
           loadA((kb + kt + 2) * kX6BK, ldA);
           loadB((kb + kt + 2) * kX6BK, ldB);
         } else {
@@ -1000,6 +1056,15 @@ extern "C" int ocppo_split_planes(ocppo_stream_t stream, int n, const float* con
   return check_launch("ocppo_split_planes");
 }
 
+// A unit's operand window (<= 256 rows x its K range, either layout) addressed by the 32-bit
+// buffer offsets of X6Stage::load_buf
+static bool x6_windows_ok(int64_t sam, int64_t sak, int64_t sbn, int64_t sbk, int64_t K,
+                          int64_t splits, bool b_planes) {
+  const int64_t ks = ((K / kX6BK + splits - 1) / splits + 1) * kX6BK;
+  auto win = [&](int64_t srow, int64_t sk) { return 4 * (256 * srow + ks * sk + 256); };
+  return win(sam, sak) < INT32_MAX && (b_planes || win(sbn, sbk) < INT32_MAX);
+}
+
 extern "C" int ocppo_gemm_x6(ocppo_stream_t stream, const float* a, int64_t sam, int64_t sak,
                              const float* b, int64_t sbn, int64_t sbk, float* c, int64_t ldc,
                              int64_t M, int64_t N, int64_t K, int64_t splits, int64_t split_c,
@@ -1029,6 +1094,9 @@ extern "C" int ocppo_gemm_x6(ocppo_stream_t stream, const float* a, int64_t sam,
   OCPPO_REQUIRE(ldc >= N, "ocppo_gemm_x6: ldc=%lld < N", (long long)ldc);
   OCPPO_REQUIRE(reinterpret_cast<uintptr_t>(a) % 16 == 0 && reinterpret_cast<uintptr_t>(b) % 16 == 0,
                 "ocppo_gemm_x6: A and B must be 16-B aligned");
+  OCPPO_REQUIRE(x6_windows_ok(sam, sak, sbn, sbk, K, splits, b_planes != nullptr),
+                "ocppo_gemm_x6: an operand window of one tile exceeds 2 GiB (32-bit buffer "
+                "offsets): split the product");
   if (b_planes) b = nullptr;
   OCPPO_REQUIRE(K % kX6BK == 0 && K / kX6BK >= splits,
                 "ocppo_gemm_x6: K=%lld must be a multiple of %d with >= 1 step per split",
@@ -1144,6 +1212,8 @@ extern "C" int ocppo_gemm_x6_wgrad(ocppo_stream_t stream, const float* a, int64_
                 "ldm >= N, ldx >= K1");
   OCPPO_REQUIRE(reinterpret_cast<uintptr_t>(a) % 16 == 0 && reinterpret_cast<uintptr_t>(b) % 16 == 0,
                 "ocppo_gemm_x6_wgrad: A and B must be 16-B aligned");
+  OCPPO_REQUIRE(x6_windows_ok(sam, sak, sbn, sbk, K, 1, false),
+                "ocppo_gemm_x6_wgrad: an operand window of one tile exceeds 2 GiB");
   const int64_t tiles_m = M / bm;
   const int64_t npw = ((N + kWgRecCols - 1) / kWgRecCols) * kWgRecCols * (wg_kp(K1) + 1);
   OCPPO_REQUIRE(records_floats >= tiles_m * npw,

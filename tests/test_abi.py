@@ -110,3 +110,15 @@ def test_gemm_x6_mbig_only_for_the_mixed_tile(lib):
             None, None, None]
     assert lib.LIB.ocppo_gemm_x6(*args, 24, 512, None, 0, 0) == lib.OCPPO_E_INVALID
     assert b"mbig" in lib.LIB.ocppo_last_error()
+
+
+def test_gemm_x6_rejects_operand_windows_past_32_bit_offsets(lib):
+    """The x6 kernels address a tile's operand window with 32-bit buffer offsets: a row stride
+    that puts one 128-row window past 2 GiB is refused before any launch (validation only)."""
+    dummy = ctypes.c_void_p(256)
+    ok = [None, dummy, 64, 1, dummy, 64, 1, dummy, 128, 128, 128, 64, 1, 0, None, 0, None, 0,
+          None, None, None, 24, -1, None, 0, 0]
+    big = list(ok)
+    big[2] = 1 << 22  # A row stride 4M floats: 256 rows x 16 MB
+    assert lib.LIB.ocppo_gemm_x6(*big) == lib.OCPPO_E_INVALID
+    assert b"2 GiB" in lib.LIB.ocppo_last_error()
