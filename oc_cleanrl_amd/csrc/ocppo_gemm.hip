@@ -111,8 +111,8 @@ struct X6Place {
 };
 
 // The three bf16 pieces of an f32 pair (exact: x == x0 + x1 + x2 for finite normal x), packed:
-// p_i = (x_i of a) | (x_i of b) << 16 (v_cvt_pk_bf16_f32 and scalar f32 subtractions: 11 VALU
-// instructions per pair).
+// p_i = (x_i of a) | (x_i of b) << 16 (5 v_cvt_pk_bf16_f32, 4 scalar f32 subtractions and 2
+// v_perm_b32 per pair).
 typedef float x6f2 __attribute__((ext_vector_type(2)));
 typedef __bf16 x6h2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t x6_pk(x6f2 v) {
@@ -136,12 +136,17 @@ __device__ __forceinline__ void x6_split2(x6f2 v, uint32_t& p0, uint32_t& p1, ui
   // the residuals as scalar subtractions (build.py: -fno-slp-vectorize keeps them apart): a
   // packed f32 VALU op issued beside MFMAs costs more than two scalar ones (MI355X_MICROARCH.md,
   // filler prices) -- config-2 shapes 730 -> 704 us, bench +2.4 % (profiles/r04/exp_x6_scalar_sub)
-  p0 = x6_pk(v);
-  const x6f2 h0 = x6_unpk(p0);
-  const float r1x = v.x - h0.x, r1y = v.y - h0.y;
-  p1 = x6_pk(x6f2{r1x, r1y});
-  const x6f2 h1 = x6_unpk(p1);
-  p2 = x6_pk(x6f2{r1x - h1.x, r1y - h1.y});
+  // each lead piece as an f32 straight from the converter (bf16(0) in the low half: the register
+  // IS the rounded value) instead of unpacked from the packed pair by a shift and a mask; the
+  // packed planes words by one byte permute (GEMM set 676 -> 673 us, profiles/r04/exp_x6_split)
+  const float h0x = __uint_as_float(x6_pk(x6f2{0.f, v.x}));
+  const float h0y = __uint_as_float(x6_pk(x6f2{0.f, v.y}));
+  const float r1x = v.x - h0x, r1y = v.y - h0y;
+  const float h1x = __uint_as_float(x6_pk(x6f2{0.f, r1x}));
+  const float h1y = __uint_as_float(x6_pk(x6f2{0.f, r1y}));
+  p0 = __builtin_amdgcn_perm(__float_as_uint(h0y), __float_as_uint(h0x), 0x07060302u);
+  p1 = __builtin_amdgcn_perm(__float_as_uint(h1y), __float_as_uint(h1x), 0x07060302u);
+  p2 = x6_pk(x6f2{r1x - h1x, r1y - h1y});
 }
 
 // LDS plane layout: rows in pairs of 128 B (row r's 64 B = 16-B chunks 4 (r & 1) .. + 3 of pair
