@@ -240,21 +240,68 @@ def needs_launch(gpus: int, env=os.environ) -> bool:
     return gpus > 1 and "WORLD_SIZE" not in env
 
 
-def launch(argv, gpus: int, script=None) -> int:
+DEADLINE_S = 540.0  # whole-run bound, under the driver's 600 s per run
+
+
+def launch(argv, gpus: int, script=None, deadline_s: float | None = None) -> int:
     """Run the N ranks as ONE child process tree (not an exec), before this process makes any GPU
     call. Rank 0's JSON line is forwarded to stdout as it arrives; anything else the ranks print
     on stdout (gloo's connection chatter) goes to stderr, so stdout holds the line alone.
-    Returns the child's exit code."""
+    Returns the child's exit code. The ranks write their phases under a status directory
+    (oc_cleanrl_amd.watch); if the tree outlives `deadline_s` (the ranks' own watchdogs did not
+    end it), it is killed as a whole and an error line naming every rank's phase is printed
+    instead, exit code 3."""
+    import shutil
+    import signal
     import subprocess
+    import tempfile
+    import threading
+
+    from oc_cleanrl_amd.watch import behind, read_status
 
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    status = tempfile.mkdtemp(prefix="ocppo_watch_")
+    env["OCPPO_WATCH_DIR"] = status
+    t0 = time.monotonic()
     p = subprocess.Popen(launcher_cmd(argv, gpus, free_port(), script), env=env,
-                         stdout=subprocess.PIPE, text=True, bufsize=1)
-    for line in p.stdout:
-        (sys.stdout if line.startswith("{") else sys.stderr).write(line)
-        (sys.stdout if line.startswith("{") else sys.stderr).flush()
-    return p.wait()
+                         stdout=subprocess.PIPE, text=True, bufsize=1, start_new_session=True)
+    sent = []
+
+    def forward():
+        for line in p.stdout:
+            dst = sys.stdout if line.startswith("{") else sys.stderr
+            if dst is sys.stdout:
+                sent.append(line)
+            dst.write(line)
+            dst.flush()
+
+    reader = threading.Thread(target=forward, daemon=True)
+    reader.start()
+    try:
+        rc = p.wait(timeout=deadline_s)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        p.wait()
+        ranks = read_status(status)
+        rec = {"metric": None, "value": None, "n_gpus": gpus, "error": "launcher deadline",
+               "elapsed_s": round(time.monotonic() - t0, 1),
+               "ranks": {str(k): v["phase"] for k, v in sorted(ranks.items())},
+               "behind": behind(ranks)}
+        print(json.dumps(rec), file=sys.stderr if sent else sys.stdout, flush=True)
+        sent.append("deadline")
+        rc = 3
+    reader.join(timeout=5)
+    if rc != 0 and not sent:  # the ranks died without a line: say where they were
+        ranks = read_status(status)
+        print(json.dumps({"metric": None, "value": None, "n_gpus": gpus,
+                          "error": f"ranks exited with code {rc}",
+                          "ranks": {str(k): v["phase"] for k, v in sorted(ranks.items())},
+                          "failed": {str(k): v["failed"] for k, v in sorted(ranks.items())
+                                     if v.get("failed")},
+                          "behind": behind(ranks)}), flush=True)
+    shutil.rmtree(status, ignore_errors=True)
+    return rc
 
 
 def replica_check(tr, world: int, device) -> dict:
@@ -270,6 +317,16 @@ def replica_check(tr, world: int, device) -> dict:
     if not equal:
         raise SystemExit(f"DP replicas diverged: parameter checksums {sums}")
     return {"param_checksums": [f"{s:016x}" for s in sums], "equal": equal}
+
+
+def own_stdout():
+    """A private handle on this process's stdout for the one JSON line, with fd 1 itself sent to
+    stderr for the rest of the run: native libraries print there (RCCL's version banner at
+    communicator init), and the line must be the only thing on stdout."""
+    sys.stdout.flush()
+    out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+    return out
 
 
 def main():
@@ -298,34 +355,108 @@ def main():
                     help="GPU of this rank (default LOCAL_RANK; 0 for the shared-GPU rehearsal)")
     ap.add_argument("--set", action="append", default=[], metavar="FIELD=VALUE",
                     help="override an Args field (experiments; e.g. --set rollout_frame_cache=0)")
+    ap.add_argument("--deadline", type=float, default=DEADLINE_S,
+                    help="whole-run bound in s: a rank past it (or the self-launch parent, 30 s "
+                         "later) ends the run with an error line naming every rank's phase")
+    ap.add_argument("--stall", type=float, default=120.0,
+                    help="bound in s on one timed iteration (warm-up iterations, which capture "
+                         "the graphs: 2.5x; init and rendezvous: 300 s)")
+    ap.add_argument("--dist-timeout", type=float, default=300.0,
+                    help="torch.distributed timeout in s (process-group collectives)")
+    ap.add_argument("--rehearse-stall", type=int, default=None, metavar="RANK",
+                    help="CPU rehearsal of the fail-fast path (gloo, no GPU): the ranks run "
+                         "all-reduce iterations and RANK stops before its second one")
     opt = ap.parse_args()
     if needs_launch(opt.gpus):
         # nothing has touched the GPU yet in this process
-        raise SystemExit(launch(sys.argv[1:], opt.gpus))
+        raise SystemExit(launch(sys.argv[1:], opt.gpus, deadline_s=opt.deadline + 30))
+    line_out = own_stdout()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    watch = rank_watch(opt, rank, world, line_out)
+    try:
+        run_rank(opt, rank, world, line_out, watch)
+    except BaseException as e:  # noqa: BLE001 -- every failure ends with a line naming its phase
+        if isinstance(e, SystemExit) and not e.code:
+            raise
+        import traceback
+
+        traceback.print_exc()
+        watch.fire(f"{type(e).__name__}: {e}",
+                   exit_code=e.code if isinstance(e, SystemExit) and isinstance(e.code, int) else 1)
+    watch.stop()
+
+
+def emit_error(rec: dict, rank: int, world: int, line_out):
+    """The error line: on rank 0's stdout handle (the bench line's place), else on stderr."""
+    line = json.dumps({"metric": None, "value": None, "n_gpus": world, **rec})
+    print(line, file=line_out if rank == 0 else sys.stderr, flush=True)
+
+
+def rank_watch(opt, rank: int, world: int, line_out):
+    """This rank's RankWatch: status files in the launcher's directory (or one per master port
+    under the driver's own torch.distributed.run launch), the run's deadline, the error line as
+    its last word."""
+    from oc_cleanrl_amd.watch import RankWatch
+
+    status = os.environ.get("OCPPO_WATCH_DIR") or (
+        f"/tmp/ocppo_watch_{os.environ.get('MASTER_PORT', os.getpid())}")
+    return RankWatch(rank, world, status, stall_s=opt.stall, deadline_s=opt.deadline,
+                     on_fire=lambda rec: emit_error(rec, rank, world, line_out))
+
+
+def rehearse_stall(opt, rank: int, world: int, line_out, watch):
+    """--rehearse-stall R: the fail-fast path on CPU. gloo process group with the bench's
+    timeout; iterations of one all-reduce each, every rank naming its phase; rank R stops before
+    its second all-reduce, the others wait in it until a watchdog ends the run."""
+    from datetime import timedelta
+
+    watch.phase("init", stall_s=300.0)
+    dist.init_process_group("gloo", timeout=timedelta(seconds=opt.dist_timeout))
+    t = torch.ones(1024)
+    for i in range(opt.steps):
+        watch.phase(f"timed {i}")
+        if rank == opt.rehearse_stall and i == 1:
+            while True:  # stuck before its collective: the others wait inside theirs
+                time.sleep(1.0)
+        watch.phase(f"timed {i} all-reduce")
+        dist.all_reduce(t)
+    watch.phase("report")
+    if rank == 0:
+        print(json.dumps({"rehearsal": "no stall", "value": float(t[0])}), file=line_out,
+              flush=True)
+    dist.destroy_process_group()
+
+
+def run_rank(opt, rank: int, world: int, line_out, watch):
+    """One rank of the bench (the whole run at N = 1)."""
+    if opt.rehearse_stall is not None:
+        return rehearse_stall(opt, rank, world, line_out, watch)
+    from datetime import timedelta
 
     from oc_cleanrl_amd.args import Args, finalize
     from oc_cleanrl_amd import gemm_table
     from oc_cleanrl_amd.trainer import PPOTrainer
 
-    rank = int(os.environ.get("RANK", "0"))
+    watch.phase("init", stall_s=300.0)
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != opt.gpus:
         raise SystemExit(f"--gpus {opt.gpus} under a launch of WORLD_SIZE={world}")
     device = torch.device(f"cuda:{local_rank if opt.device_index is None else opt.device_index}")
     torch.cuda.set_device(device)
+    timeout = timedelta(seconds=opt.dist_timeout)
     if world > 1:
         if opt.backend == "nccl":
-            dist.init_process_group("nccl", device_id=device)
+            dist.init_process_group("nccl", device_id=device, timeout=timeout)
         else:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=timeout)
     elif opt.dp_exchange:
         # the data-parallel step structure (per-minibatch graphs around an RCCL all-reduce of the
         # flat gradient buffer, /world folded into Adam) over a 1-rank group: what N > 1 runs,
         # minus the xGMI transfer
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", str(free_port()))
-        dist.init_process_group(opt.backend, rank=0, world_size=1,
+        dist.init_process_group(opt.backend, rank=0, world_size=1, timeout=timeout,
                                 **({"device_id": device} if opt.backend == "nccl" else {}))
         opt.set.append("dp_exchange=1")
 
@@ -363,19 +494,26 @@ def main():
             dist.barrier()
         torch.cuda.synchronize(device)
 
-    for _ in range(opt.warmup):
+    for i in range(opt.warmup):
+        watch.phase(f"warmup {i}", stall_s=2.5 * opt.stall)
         tr.train_iteration(collect_metrics=True)
+    watch.phase("barrier")
     barrier()
     t0 = time.perf_counter()
-    for _ in range(opt.steps):
+    for i in range(opt.steps):
+        watch.phase(f"timed {i}")
         tr.train_iteration(collect_metrics=True)
+    watch.phase("barrier")
     barrier()
     dt = time.perf_counter() - t0
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t)
+    watch.phase("replica check")
     replicas = replica_check(tr, world, device)
+    # after the timed region, the kernel timer's replays, the scaled cases and the CPU legs
+    watch.phase("report", stall_s=max(opt.deadline, 600.0))
 
     env_steps = opt.steps * args.num_steps * args.local_num_envs * world
     updates = opt.steps * args.update_epochs * args.num_minibatches
@@ -545,13 +683,15 @@ def main():
                            "steps/s; a few seconds of search in the warm-up)"}
                           if opt.config == 3 else {}),
                        "conv_benchmark": args.conv_benchmark,
-                       "sampling_noise": ("per step: one Exp(1) draw of [N, A] per rollout step "
-                                          "(the reference's Categorical.sample stream)"
-                                          if args.per_step_noise else
-                                          "per rollout: one Exp(1) draw of [T, N, A] (the "
-                                          "reference's stream is --set per_step_noise=1: "
-                                          "770.7k vs 779.9k env steps/s, -1.2 %, "
-                                          "profiles/r03/noise_ab.json)"),
+                       "sampling_noise": {
+                           "kernel": "the reference's stream: Categorical.sample's per-step [N, A] "
+                                     "Exp(1) draws on the device generator (torch's Philox "
+                                     "exponential_ restated), generated inside the sampling "
+                                     "kernel; bitwise torch's draws (tests/test_kernels_gpu.py)",
+                           "torch": "the reference's stream from torch's exponential_, one "
+                                    "launch per step",
+                           "rollout": "one [T, N, A] Exp(1) draw per rollout (not the "
+                                      "reference's stream)"}[args.sampling_noise],
                        "parallelism": f"dp{world}",
                        **({"dist_backend": opt.backend} if world > 1 else {})},
             "replicas": replicas,
@@ -563,7 +703,8 @@ def main():
             "kernels": kernels,
             "cpu_baseline": cpu,
         }
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=line_out, flush=True)
+    tr.close()
     if dist.is_initialized():
         dist.destroy_process_group()
 

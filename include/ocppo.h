@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define OCPPO_ABI_VERSION 21
+#define OCPPO_ABI_VERSION 22
 
 /* status codes */
 #define OCPPO_OK 0
@@ -205,24 +205,52 @@ OCPPO_API int ocppo_clip_adam_step(ocppo_stream_t stream, float* params, const f
  *   entropy_out : [N] f32 or NULL
  *   value_in / value_out : critic output [N] copied into &values[t*N] (both NULL to skip)
  * ------------------------------------------------------------------------------------------- */
-OCPPO_API int ocppo_categorical_sample(ocppo_stream_t stream, const float* logits, const float* noise,
-                             int64_t N, int64_t A, int64_t* action_out, float* logprob_out,
-                             float* entropy_out, const float* value_in, float* value_out);
+OCPPO_API int ocppo_categorical_sample(ocppo_stream_t stream, const float* logits, float* noise,
+                             const int64_t* philox_state, int64_t philox_offset,
+                             int64_t philox_stride, int64_t N, int64_t A, int64_t* action_out,
+                             float* logprob_out, float* entropy_out, const float* value_in,
+                             float* value_out);
+
+/* The sampling entries' Exp(1) values (ocppo_categorical_sample, ocppo_policy_head_sample,
+ * ocppo_policy_head_env_step) come from one of two places:
+ *   philox_state == NULL : noise [N, A] is read (any source);
+ *   philox_state != NULL : the kernel draws them itself, bit for bit the values
+ *     torch.empty(N, A, device=...).exponential_() returns on the CUDA/HIP generator whose
+ *     (seed, philox offset) is (philox_state[0], philox_state[1] + philox_offset) -- the stream
+ *     Categorical.sample() consumes per step in the reference (architectures/ppo.py:92-94 via
+ *     torch.multinomial's Exp(1) path; ppo_atari_oc.py:505-506) -- with philox_stride = torch's
+ *     grid stride for N*A elements (ocppo_torch_exponential_geometry); noise, when non-NULL,
+ *     receives them. philox_state is device memory [2] (graph-capturable: a replay reads the
+ *     generator state of that replay). */
+
+/* torch's launch geometry of exponential_ over `numel` elements (ATen DistributionTemplates.h
+ * calc_execution_policy): the grid stride (256 * grid, grid <= cus * max_threads_per_cu / 256) and
+ * the generator's philox-offset increment per draw. Host only. */
+OCPPO_API int ocppo_torch_exponential_geometry(int64_t numel, int64_t cus, int64_t max_threads_per_cu,
+                                               int64_t* stride, int64_t* offset_increment);
+
+/* out[numel] = torch.empty(numel).exponential_() at generator (philox_state[0], philox_state[1] +
+ * philox_offset), grid stride philox_stride (the reference stream of the sampling entries,
+ * on its own: tests, and callers that need the draws as a tensor). */
+OCPPO_API int ocppo_philox_exponential(ocppo_stream_t stream, float* out, int64_t numel,
+                                       const int64_t* philox_state, int64_t philox_offset,
+                                       int64_t philox_stride);
 
 /* Fused rollout policy head: logits = hidden @ w_actor^T + b_actor, value = hidden . w_critic +
  * b_critic, then the sampler above — replaces the actor/critic Linear layers AND the sampler of
  * architectures/ppo.py:89-95 for one rollout step (PPObj / PPODefault, shared hidden layer).
  *   hidden : [N, H] f32 (decoder output);  w_actor : [A, H];  b_actor : [A];  w_critic : [H];
- *   b_critic : [1];  noise : [N, A] Exp(1);  value_out : [N] (&values[t*N]);
+ *   b_critic : [1];  noise : [N, A] Exp(1) (or drawn: philox_*, above);  value_out : [N];
  *   entropy_out, logits_out ([N, A]) may be NULL.
  * Logits differ from a GEMM's only by f32 summation order; actions are bit-exact w.r.t. the
  * sampler applied to the logits this kernel computes (returned in logits_out). */
 OCPPO_API int ocppo_policy_head_sample(ocppo_stream_t stream, const float* hidden, int64_t N,
                                        int64_t H, const float* w_actor, const float* b_actor,
                                        const float* w_critic, const float* b_critic,
-                                       const float* noise, int64_t A, int64_t* action_out,
-                                       float* logprob_out, float* entropy_out, float* value_out,
-                                       float* logits_out);
+                                       float* noise, const int64_t* philox_state,
+                                       int64_t philox_offset, int64_t philox_stride, int64_t A,
+                                       int64_t* action_out, float* logprob_out,
+                                       float* entropy_out, float* value_out, float* logits_out);
 
 /* log_prob(action) and entropy() of Categorical(logits) for given actions (architectures/ppo.py
  * :92-95 with `action` passed) and the matching backward. */
@@ -673,7 +701,9 @@ OCPPO_API int ocppo_synth_env_step(ocppo_stream_t stream, uint64_t seed, const i
 OCPPO_API int ocppo_policy_head_env_step(ocppo_stream_t stream, const float* hidden, int64_t N,
                                          int64_t H, const float* w_actor, const float* b_actor,
                                          const float* w_critic, const float* b_critic,
-                                         const float* noise, int64_t A, int64_t* action_out,
+                                         float* noise, const int64_t* philox_state,
+                                         int64_t philox_offset, int64_t philox_stride,
+                                         int64_t A, int64_t* action_out,
                                          float* logprob_out, float* value_out, uint64_t seed,
                                          const int64_t* step_base, int64_t step_offset, int64_t D,
                                          float* frame_out, float* reward_out, float* done_out,

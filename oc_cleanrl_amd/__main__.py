@@ -23,12 +23,18 @@ def main(argv=None, defaults: dict | None = None):
         device = torch.device(f"cuda:{local_rank}")
     torch.cuda.set_device(device)
     if world > 1:
-        dist.init_process_group(args.backend_dist, device_id=device)
+        from datetime import timedelta
+
+        dist.init_process_group(args.backend_dist, timeout=timedelta(seconds=args.dist_timeout),
+                                **({"device_id": device} if args.backend_dist == "nccl" else {}))
+    tr = None
     try:
         tr = run(args, device, rank, world)
         if rank == 0 and tr.last_metrics:
             print({k: round(v, 5) for k, v in tr.last_metrics.items()})
     finally:
+        if tr is not None:
+            tr.close()
         if world > 1:
             dist.destroy_process_group()
     return tr

@@ -22,7 +22,7 @@ LIB_PATH = Path(os.environ.get("OCPPO_LIB", PKG / "lib" / "libocppo_hip.so"))
 HEADER = PKG.parent / "include" / "ocppo.h"
 
 # constants mirrored from include/ocppo.h (checked against the header by tests/test_abi.py)
-OCPPO_ABI_VERSION = 21
+OCPPO_ABI_VERSION = 22
 OCPPO_OK, OCPPO_E_INVALID, OCPPO_E_LAUNCH, OCPPO_E_WORKSPACE = 0, 1, 2, 3
 OCPPO_F32, OCPPO_BF16, OCPPO_U8 = 0, 1, 2
 STAT_NAMES = ("loss", "pg_loss", "v_loss", "entropy", "old_approx_kl", "approx_kl", "clipfrac",
@@ -43,8 +43,11 @@ SIGNATURES: dict[str, tuple[type, list]] = {
                                    P, SZ]),
     "ocppo_clip_adam_workspace_bytes": (SZ, [I64]),
     "ocppo_clip_adam_step": (I, [P, P, P, P, P, I64, P, D, D, D, D, D, P, P, SZ]),
-    "ocppo_categorical_sample": (I, [P, P, P, I64, I64, P, P, P, P, P]),
-    "ocppo_policy_head_sample": (I, [P, P, I64, I64, P, P, P, P, P, I64, P, P, P, P, P]),
+    "ocppo_categorical_sample": (I, [P, P, P, P, I64, I64, I64, I64, P, P, P, P, P]),
+    "ocppo_policy_head_sample": (I, [P, P, I64, I64, P, P, P, P, P, P, I64, I64, I64, P, P, P, P,
+                                     P]),
+    "ocppo_torch_exponential_geometry": (I, [I64, I64, I64, P, P]),
+    "ocppo_philox_exponential": (I, [P, P, I64, P, I64, I64]),
     "ocppo_categorical_logprob_entropy": (I, [P, P, P, I64, I64, P, P]),
     "ocppo_categorical_logprob_entropy_bwd": (I, [P, P, P, P, P, I64, I64, P]),
     "ocppo_rollout_store": (I, [P, P, I, P, P, I64, I64, I64, P, P, I, P, P, P, I, P]),
@@ -81,8 +84,8 @@ SIGNATURES: dict[str, tuple[type, list]] = {
     "ocppo_epsilon_greedy": (I, [P, P, I64, I64, U64, P, I64, D, D, D, P, P]),
     "ocppo_td_loss_fwd_bwd": (I, [P, P, P, P, P, P, I64, I64, D, P, P]),
     "ocppo_synth_env_step": (I, [P, U64, P, I64, P, I64, I64, I, P, P, P, P]),
-    "ocppo_policy_head_env_step": (I, [P, P, I64, I64, P, P, P, P, P, I64, P, P, P, U64, P, I64,
-                                       I64, P, P, P, P]),
+    "ocppo_policy_head_env_step": (I, [P, P, I64, I64, P, P, P, P, P, P, I64, I64, I64, P, P, P,
+                                       U64, P, I64, I64, P, P, P, P]),
     "ocppo_cartpole_step": (I, [P, U64, P, I64, P, P, P, P, P, P]),
     "ocppo_heads_loss_workspace_bytes": (SZ, [I64, I64, I64]),
     "ocppo_heads_loss_fwd_bwd": (I, [P, P, I64, I64, P, P, P, P, I64, P, P, P, P, P, P, D, D, D, I,

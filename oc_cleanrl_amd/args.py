@@ -122,8 +122,12 @@ class Args:
     rollout_cache_ring: bool = True  # ... the cache as a ring the decoder reads rotated (no shift)
     update_frame_dedup: bool = True  # PPO_OBJ update: encode each distinct frame of a minibatch once
     prefetch_shuffle: bool = True  # shuffle (+ frame plan) of the next iteration while the GPU runs
-    per_step_noise: bool = False  # rollout sampling noise drawn per step ([N, A], the reference's
-                                  # generator stream) instead of once per rollout ([T, N, A])
+    sampling_noise: str = "kernel"  # the rollout sampler's Exp(1) draws: "kernel" = the reference's
+                                    # per-step stream (torch's [N, A] exponential_ per step, as
+                                    # Categorical.sample draws it) generated inside the sampling
+                                    # kernel (ops.TorchExpStream); "torch" = the same stream from
+                                    # torch's exponential_ (a launch per step); "rollout" = one
+                                    # [T, N, A] draw per rollout (not the reference's stream)
     fused_heads_loss: bool = True  # update: policy heads fwd + PPO loss + heads bwd in one HIP op
     dp_overlap: bool = True  # DP: all-reduce the decoder-side gradients during the encoder backward
     sample_records_min: int = 131072  # local batches of at least this many samples: GAE also
@@ -131,9 +135,16 @@ class Args:
                                       # reads one record instead of five arrays (-1: never).
                                       # It pays at scale (1M samples: GAE + prepare 454 -> 427
                                       # us), not at config 2's 16K (+1-2 us), profiles/r04
-    dp_graph_collectives: bool = False  # DP: capture each epoch's minibatches WITH their RCCL
-                                        # all-reduces in one hipGraph (else one graph per phase,
-                                        # the collectives launched eagerly between them)
+    dp_collectives: str = "rccl"  # DP exchange: "rccl" = this package's own RCCL communicator
+                                  # (oc_cleanrl_amd.rccl), its all-reduces captured with each
+                                  # epoch's minibatches in one hipGraph; "torch" = torch.distributed
+                                  # collectives (the only choice on gloo)
+    dp_graph_collectives: bool = False  # DP, "torch" collectives: capture each epoch's minibatches
+                                        # WITH their all-reduces in one hipGraph (else one graph
+                                        # per phase, the collectives launched eagerly between them)
+    dist_timeout: float = 300.0  # s: torch.distributed collectives / rendezvous of the DP ranks
+    stall_timeout: float = 0.0  # s: > 0 ends a rank whose iteration makes no progress for this
+                                # long, naming every rank's phase (oc_cleanrl_amd.watch); 0: off
     dp_exchange: bool = False  # run the DP exchange path (per-minibatch graphs + all-reduce) even
                                # at world size 1, over an initialised 1-rank process group
     conv_channels_last: bool = True  # pixel NatureCNN in NHWC (MIOpen NHWC kernels, no transposes)
@@ -221,6 +232,11 @@ def finalize(args: Args, world_size: int = 1) -> Args:
         raise AssertionError('"obj" observations only work with "PPO_OBJ" architecture!')
     if args.local_batch_size % args.num_minibatches:
         raise ValueError("local batch size must be divisible by num_minibatches")
+    if args.sampling_noise not in ("kernel", "torch", "rollout"):
+        raise ValueError(f"sampling_noise must be kernel, torch or rollout, got "
+                         f"{args.sampling_noise!r}")
+    if args.dp_collectives not in ("rccl", "torch"):
+        raise ValueError(f"dp_collectives must be rccl or torch, got {args.dp_collectives!r}")
     return args
 
 

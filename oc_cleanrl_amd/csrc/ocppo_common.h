@@ -46,6 +46,14 @@ constexpr int kWave = 64;  // CDNA wavefront width
 constexpr int kWgRecCols = 256;
 __host__ __device__ inline int wg_kp(int64_t K) { return K <= 4 ? 4 : K <= 8 ? 8 : K <= 12 ? 12 : 16; }
 
+// ReLU as torch computes it (clamp_min: NaN propagates). v_max_f32 alone returns the non-NaN
+// operand, which would clamp a diverging layer's NaNs to 0 instead of surfacing them in the loss;
+// for every non-NaN input the result is fmaxf's, bit for bit.
+__device__ __forceinline__ float relu_f(float v) { return v != v ? v : fmaxf(v, 0.f); }
+__device__ __forceinline__ float4 relu_f4(float4 v) {
+  return make_float4(relu_f(v.x), relu_f(v.y), relu_f(v.z), relu_f(v.w));
+}
+
 // ---- element conversions ----------------------------------------------------------------------
 // f32 -> bf16 round-to-nearest-even through the hardware converter (NaN stays NaN).
 __device__ __forceinline__ uint16_t f32_to_bf16(float x) {

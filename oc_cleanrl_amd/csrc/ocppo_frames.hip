@@ -135,8 +135,8 @@ __global__ __launch_bounds__(256) void frames_gather_linear_kernel(
   a.x += bv.x; a.y += bv.y; a.z += bv.z; a.w += bv.w;
   bb.x += bv.x; bb.y += bv.y; bb.z += bv.z; bb.w += bv.w;
   if (RELU) {
-    a = make_float4(fmaxf(a.x, 0.f), fmaxf(a.y, 0.f), fmaxf(a.z, 0.f), fmaxf(a.w, 0.f));
-    bb = make_float4(fmaxf(bb.x, 0.f), fmaxf(bb.y, 0.f), fmaxf(bb.z, 0.f), fmaxf(bb.w, 0.f));
+    a = relu_f4(a);
+    bb = relu_f4(bb);
   }
   *reinterpret_cast<float4*>(h_out + ca * N1 + col) = a;
   if (cb < C) *reinterpret_cast<float4*>(h_out + cb * N1 + col) = bb;
@@ -428,7 +428,7 @@ __global__ __launch_bounds__(256) void frames_gather_linear_wide_kernel(
     if (c >= C) break;
     float4 a = acc[i];
     a.x += bv.x; a.y += bv.y; a.z += bv.z; a.w += bv.w;
-    if (RELU) a = make_float4(fmaxf(a.x, 0.f), fmaxf(a.y, 0.f), fmaxf(a.z, 0.f), fmaxf(a.w, 0.f));
+    if (RELU) a = relu_f4(a);
     *reinterpret_cast<float4*>(h_out + c * N1 + col) = a;
   }
 }

@@ -704,7 +704,7 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
         for (int k = 0; k < KP; ++k) xr[k] = xs[lrow * XLD + k];
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
-          const float gp = g.mask[row * g.ldm + wc0 + 16 * j + fr] > 0.f ? hi[i][j][r] : 0.f;
+          const float gp = g.mask[row * g.ldm + wc0 + 16 * j + fr] <= 0.f ? 0.f : hi[i][j][r];
           acc[j][0] += gp;
 #pragma unroll
           for (int k = 0; k < KP; ++k) acc[j][1 + k] = fmaf(gp, xr[k], acc[j][1 + k]);
@@ -807,7 +807,7 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
         const int64_t row = wr0 + 16 * i + 4 * fc + r;
         float v = LO ? hi[i][j][r] + lo[LO ? i : 0][LO ? j : 0][r] : hi[i][j][r];
         if (g.bias) v += bv;
-        if (g.relu) v = fmaxf(v, 0.f);
+        if (g.relu) v = relu_f(v);
         Cp[row * g.ldc + col] = v;
         bits |= static_cast<uint64_t>(v > 0.f) << ((i * FN + j) * 4 + r);
       }

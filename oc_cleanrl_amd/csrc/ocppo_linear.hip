@@ -263,7 +263,7 @@ __global__ __launch_bounds__(64 * S) void linear_rows_kernel(
     const int orow = tm * 16 + 4 * g + r;
     if (orow < M) {
       float v = acc[r] + bv;
-      if (RELU) v = fmaxf(v, 0.f);
+      if (RELU) v = relu_f(v);
       if (CACHE) {
         const int W = cache.W;
         float* e = cache.enc + static_cast<int64_t>(orow) * W * N + ocol;
@@ -518,7 +518,7 @@ __global__ __launch_bounds__(64 * S) void conv_rows_kernel(
     const int orow = tm * 16 + 4 * g + r;
     if (orow < M) {
       float v = acc[r] + bv;
-      if (RELU) v = fmaxf(v, 0.f);
+      if (RELU) v = relu_f(v);
       y[static_cast<int64_t>(orow) * N + col] = v;
     }
   }
@@ -702,7 +702,7 @@ __device__ __forceinline__ void linear2_tile(
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float v = acc[r] + bv;
-        if (RELU1) v = fmaxf(v, 0.f);
+        if (RELU1) v = relu_f(v);
         h1[(4 * g + r) * ldh + col] = v;  // C layout: column lane & 15, rows 4 * (lane >> 4) + r
       }
     }
@@ -739,7 +739,7 @@ __device__ __forceinline__ void linear2_tile(
     const int orow = tm * 16 + 4 * g + r;
     if (orow < M) {
       float v = acc[r] + bv2;
-      if (RELU2) v = fmaxf(v, 0.f);
+      if (RELU2) v = relu_f(v);
       y[static_cast<int64_t>(orow) * ldy + col2] = v;
     }
   }

@@ -284,7 +284,7 @@ __global__ __launch_bounds__(256) void bias_act_kernel(float* __restrict__ y,
     const float4 bb = *reinterpret_cast<const float4*>(b + c);
     v.x = v.x + bb.x; v.y = v.y + bb.y; v.z = v.z + bb.z; v.w = v.w + bb.w;
     if (RELU) {
-      v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+      v = relu_f4(v);
     }
     reinterpret_cast<float4*>(y)[q] = v;
   }
@@ -333,7 +333,7 @@ __global__ __launch_bounds__(256) void bias_act_nchw_kernel(const float* __restr
   for (int i = threadIdx.x; i < P * C; i += 256) {
     const int c = i / P, p = i - c * P;
     float v = tile[p * ld + c] + bias[c];
-    if (RELU) v = fmaxf(v, 0.f);
+    if (RELU) v = relu_f(v);
     dst[i] = v;
   }
 }
@@ -564,7 +564,7 @@ __global__ __launch_bounds__(256) void sum_splits_act_kernel(const float4* __res
       r.x += b.x; r.y += b.y; r.z += b.z; r.w += b.w;
     }
     if (relu) {
-      r.x = fmaxf(r.x, 0.f); r.y = fmaxf(r.y, 0.f); r.z = fmaxf(r.z, 0.f); r.w = fmaxf(r.w, 0.f);
+      r = relu_f4(r);
     }
     out[i] = r;
   }

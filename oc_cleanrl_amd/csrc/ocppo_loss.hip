@@ -21,6 +21,7 @@
 
 #include "ocppo_common.h"
 #include "ocppo_categorical.h"
+#include "ocppo_philox.h"
 #include "ocppo_synth_env.h"
 
 namespace ocppo {
@@ -700,9 +701,23 @@ __global__ __launch_bounds__(kLossThreads) void ppo_loss_vec_kernel(LossParams P
 }
 
 // ---- Categorical action head ---------------------------------------------------------------------
+// The sampler's Exp(1) values: read from `in`, or -- pn.state set -- drawn here as torch's
+// exponential_ would have drawn them (ocppo_philox.h) and, when `out` is set, written there.
+struct NoiseSrc {
+  const float* in;
+  float* out;
+  PhiloxNoise pn;
+  __device__ __forceinline__ float get(int64_t i) const {
+    if (pn.state == nullptr) return in[i];
+    const float v = philox_noise(pn, i);
+    if (out) out[i] = v;
+    return v;
+  }
+};
+
 template <int AMAX>
 __global__ __launch_bounds__(256) void categorical_sample_kernel(
-    const float* __restrict__ logits, const float* __restrict__ noise, int64_t N, int A,
+    const float* __restrict__ logits, NoiseSrc noise, int64_t N, int A,
     int64_t* __restrict__ action_out, float* __restrict__ logprob_out,
     float* __restrict__ entropy_out, const float* __restrict__ value_in,
     float* __restrict__ value_out) {
@@ -715,11 +730,11 @@ __global__ __launch_bounds__(256) void categorical_sample_kernel(
   categorical_row<AMAX>(l, A, lse, ln, p);
   // torch.multinomial(probs, 1) fast path: argmax(probs / q), q ~ Exp(1); first index on ties
   int best = 0;
-  float best_q = p[0] / noise[n * A];
+  float best_q = p[0] / noise.get(n * A);
 #pragma unroll
   for (int j = 1; j < AMAX; ++j)
     if (j < A) {
-      const float q = p[j] / noise[n * A + j];
+      const float q = p[j] / noise.get(n * A + j);
       if (q > best_q || (q != q && best_q == best_q)) {  // argmax propagates NaN like ATen
         best_q = q;
         best = j;
@@ -787,7 +802,7 @@ template <int AMAX>
 __global__ __launch_bounds__(256) void policy_head_sample_kernel(
     const float* __restrict__ hidden, int64_t N, int H, const float* __restrict__ wa,
     const float* __restrict__ ba, const float* __restrict__ wc, const float* __restrict__ bc,
-    const float* __restrict__ noise, int A, int64_t* __restrict__ action_out,
+    NoiseSrc noise, int A, int64_t* __restrict__ action_out,
     float* __restrict__ logprob_out, float* __restrict__ entropy_out,
     float* __restrict__ value_out, float* __restrict__ logits_out) {
   const int lane = threadIdx.x & (kWave - 1);
@@ -826,11 +841,11 @@ __global__ __launch_bounds__(256) void policy_head_sample_kernel(
   float ln[AMAX], p[AMAX], lse;
   categorical_row<AMAX>(l, A, lse, ln, p);
   int best = 0;
-  float best_q = p[0] / noise[n * A];
+  float best_q = p[0] / noise.get(n * A);
 #pragma unroll
   for (int j = 1; j < AMAX; ++j)
     if (j < A) {
-      const float q = p[j] / noise[n * A + j];
+      const float q = p[j] / noise.get(n * A + j);
       if (q > best_q || (q != q && best_q == best_q)) {
         best_q = q;
         best = j;
@@ -881,7 +896,7 @@ template <int CH, bool ENV = false>
 __global__ __launch_bounds__(256) void policy_head_fast_kernel(
     const float* __restrict__ hidden, int64_t N, int E, const float* __restrict__ wa,
     const float* __restrict__ ba, const float* __restrict__ wc, const float* __restrict__ bc,
-    const float* __restrict__ noise, int A, int64_t* __restrict__ action_out,
+    NoiseSrc noise, int A, int64_t* __restrict__ action_out,
     float* __restrict__ logprob_out, float* __restrict__ entropy_out,
     float* __restrict__ value_out, float* __restrict__ logits_out, HeadEnv env = HeadEnv{}) {
   constexpr int H = 256 * CH;
@@ -903,7 +918,7 @@ __global__ __launch_bounds__(256) void policy_head_fast_kernel(
                                   : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   if (E == 1) {  // config sizes: one environment per wave, wave-uniform tail via v_readlane
-    float nz = lane < A ? noise[g * A + lane] : 1.f;
+    float nz = lane < A ? noise.get(g * A + lane) : 1.f;
     float4 x[CH];
     head_load_row<CH>(hidden, g, lane, x);
     for (; g < ngroups; g += nwaves) {
@@ -935,7 +950,7 @@ __global__ __launch_bounds__(256) void policy_head_fast_kernel(
       }
       if (g + nwaves < ngroups) {
         head_load_row<CH>(hidden, g + nwaves, lane, x);
-        nz = lane < A ? noise[(g + nwaves) * A + lane] : 1.f;
+        nz = lane < A ? noise.get((g + nwaves) * A + lane) : 1.f;
       }
     }
     return;
@@ -946,7 +961,7 @@ __global__ __launch_bounds__(256) void policy_head_fast_kernel(
     const int64_t nt = n0 + lane;  // this lane's environment in the tail
     float nzj[7];
 #pragma unroll
-    for (int j = 0; j < 7; ++j) nzj[j] = (lane < cnt && j < A) ? noise[nt * A + j] : 1.f;
+    for (int j = 0; j < 7; ++j) nzj[j] = (lane < cnt && j < A) ? noise.get(nt * A + j) : 1.f;
     float4 x[CH], xn[CH];
     head_load_row<CH>(hidden, n0, lane, x);
     for (int e = 0; e < cnt; ++e) {
@@ -1115,24 +1130,43 @@ extern "C" int ocppo_ppo_loss_fwd_bwd(ocppo_stream_t stream, const float* logits
   return check_launch("ocppo_ppo_loss_fwd_bwd");
 }
 
-extern "C" int ocppo_categorical_sample(ocppo_stream_t stream, const float* logits,
-                                        const float* noise, int64_t N, int64_t A,
+// The sampling entries' noise operand: `noise` read, or (philox_state set) drawn in the kernel at
+// torch's (seed, offset) = philox_state[0..1] + (0, philox_offset) with grid stride philox_stride
+// and written to `noise` when that is non-NULL.
+static int noise_src(const char* what, float* noise, const int64_t* philox_state,
+                     int64_t philox_offset, int64_t philox_stride, NoiseSrc* out) {
+  OCPPO_REQUIRE(philox_state || noise, "%s: neither noise nor philox_state", what);
+  OCPPO_REQUIRE(!philox_state || (philox_stride > 0 && philox_stride % 256 == 0 &&
+                                  philox_offset >= 0),
+                "%s: bad philox stride %lld / offset %lld", what, (long long)philox_stride,
+                (long long)philox_offset);
+  *out = NoiseSrc{noise, philox_state ? noise : nullptr,
+                  PhiloxNoise{philox_state, philox_offset, philox_stride}};
+  return OCPPO_OK;
+}
+
+extern "C" int ocppo_categorical_sample(ocppo_stream_t stream, const float* logits, float* noise,
+                                        const int64_t* philox_state, int64_t philox_offset,
+                                        int64_t philox_stride, int64_t N, int64_t A,
                                         int64_t* action_out, float* logprob_out,
                                         float* entropy_out, const float* value_in,
                                         float* value_out) {
   OCPPO_REQUIRE(N >= 0 && A > 0 && A <= kMaxActions, "ocppo_categorical_sample: bad sizes");
   if (N == 0) return OCPPO_OK;
-  OCPPO_REQUIRE(logits && noise && action_out && logprob_out,
-                "ocppo_categorical_sample: null pointer");
+  OCPPO_REQUIRE(logits && action_out && logprob_out, "ocppo_categorical_sample: null pointer");
+  NoiseSrc ns;
+  if (int rc = noise_src("ocppo_categorical_sample", noise, philox_state, philox_offset,
+                         philox_stride, &ns))
+    return rc;
   const dim3 grid(ceil_div(N, 256));
   clear_stale_error();
   hipStream_t s = as_stream(stream);
   if (A <= 8)
-    hipLaunchKernelGGL(categorical_sample_kernel<8>, grid, dim3(256), 0, s, logits, noise, N,
+    hipLaunchKernelGGL(categorical_sample_kernel<8>, grid, dim3(256), 0, s, logits, ns, N,
                        (int)A, action_out, logprob_out, entropy_out, value_in, value_out);
   else
     hipLaunchKernelGGL(categorical_sample_kernel<kMaxActions>, grid, dim3(256), 0, s, logits,
-                       noise, N, (int)A, action_out, logprob_out, entropy_out, value_in, value_out);
+                       ns, N, (int)A, action_out, logprob_out, entropy_out, value_in, value_out);
   return check_launch("ocppo_categorical_sample");
 }
 
@@ -1179,16 +1213,21 @@ extern "C" int ocppo_categorical_logprob_entropy_bwd(ocppo_stream_t stream, cons
 extern "C" int ocppo_policy_head_sample(ocppo_stream_t stream, const float* hidden, int64_t N,
                                         int64_t H, const float* w_actor, const float* b_actor,
                                         const float* w_critic, const float* b_critic,
-                                        const float* noise, int64_t A, int64_t* action_out,
-                                        float* logprob_out, float* entropy_out, float* value_out,
-                                        float* logits_out) {
+                                        float* noise, const int64_t* philox_state,
+                                        int64_t philox_offset, int64_t philox_stride, int64_t A,
+                                        int64_t* action_out, float* logprob_out,
+                                        float* entropy_out, float* value_out, float* logits_out) {
   OCPPO_REQUIRE(N >= 0 && H > 0 && H <= INT32_MAX && A > 0 && A <= kMaxActions,
                 "ocppo_policy_head_sample: bad sizes N=%lld H=%lld A=%lld", (long long)N,
                 (long long)H, (long long)A);
   if (N == 0) return OCPPO_OK;
-  OCPPO_REQUIRE(hidden && w_actor && b_actor && w_critic && b_critic && noise && action_out &&
+  OCPPO_REQUIRE(hidden && w_actor && b_actor && w_critic && b_critic && action_out &&
                     logprob_out && value_out,
                 "ocppo_policy_head_sample: null pointer");
+  NoiseSrc ns;
+  if (int rc = noise_src("ocppo_policy_head_sample", noise, philox_state, philox_offset,
+                         philox_stride, &ns))
+    return rc;
   const dim3 grid(static_cast<unsigned>(ceil_div(N, 4))), block(256);
   clear_stale_error();
   hipStream_t s = as_stream(stream);
@@ -1204,7 +1243,7 @@ extern "C" int ocppo_policy_head_sample(ocppo_stream_t stream, const float* hidd
     const dim3 hgrid(static_cast<unsigned>(ceil_div(waves, kHeadWavesPerBlock)));
 #define OCPPO_HEAD(CH)                                                                           \
   hipLaunchKernelGGL(policy_head_fast_kernel<CH>, hgrid, dim3(kWave * kHeadWavesPerBlock), 0, s, \
-                     hidden, N, E, w_actor, b_actor, w_critic, b_critic, noise, (int)A,          \
+                     hidden, N, E, w_actor, b_actor, w_critic, b_critic, ns, (int)A,             \
                      action_out, logprob_out, entropy_out, value_out, logits_out)
     switch (H / 256) {
       case 1: OCPPO_HEAD(1); break;
@@ -1215,11 +1254,11 @@ extern "C" int ocppo_policy_head_sample(ocppo_stream_t stream, const float* hidd
 #undef OCPPO_HEAD
   } else if (A <= 8)
     hipLaunchKernelGGL(policy_head_sample_kernel<8>, grid, block, 0, s, hidden, N, (int)H, w_actor,
-                       b_actor, w_critic, b_critic, noise, (int)A, action_out, logprob_out,
+                       b_actor, w_critic, b_critic, ns, (int)A, action_out, logprob_out,
                        entropy_out, value_out, logits_out);
   else
     hipLaunchKernelGGL(policy_head_sample_kernel<kMaxActions>, grid, block, 0, s, hidden, N,
-                       (int)H, w_actor, b_actor, w_critic, b_critic, noise, (int)A, action_out,
+                       (int)H, w_actor, b_actor, w_critic, b_critic, ns, (int)A, action_out,
                        logprob_out, entropy_out, value_out, logits_out);
   return check_launch("ocppo_policy_head_sample");
 }
@@ -1227,7 +1266,9 @@ extern "C" int ocppo_policy_head_sample(ocppo_stream_t stream, const float* hidd
 extern "C" int ocppo_policy_head_env_step(ocppo_stream_t stream, const float* hidden, int64_t N,
                                           int64_t H, const float* w_actor, const float* b_actor,
                                           const float* w_critic, const float* b_critic,
-                                          const float* noise, int64_t A, int64_t* action_out,
+                                          float* noise, const int64_t* philox_state,
+                                          int64_t philox_offset, int64_t philox_stride,
+                                          int64_t A, int64_t* action_out,
                                           float* logprob_out, float* value_out, uint64_t seed,
                                           const int64_t* step_base, int64_t step_offset,
                                           int64_t D, float* frame_out, float* reward_out,
@@ -1236,9 +1277,13 @@ extern "C" int ocppo_policy_head_env_step(ocppo_stream_t stream, const float* hi
                     A <= 7 && D >= 1 && D <= 4096 && (H <= 512 || N <= 256 * 8),
                 "ocppo_policy_head_env_step: bad sizes N=%lld H=%lld A=%lld D=%lld", (long long)N,
                 (long long)H, (long long)A, (long long)D);
-  OCPPO_REQUIRE(hidden && w_actor && b_actor && w_critic && b_critic && noise && action_out &&
+  OCPPO_REQUIRE(hidden && w_actor && b_actor && w_critic && b_critic && action_out &&
                     logprob_out && value_out && step_base && frame_out && reward_out && done_out,
                 "ocppo_policy_head_env_step: null pointer");
+  NoiseSrc ns;
+  if (int rc = noise_src("ocppo_policy_head_env_step", noise, philox_state, philox_offset,
+                         philox_stride, &ns))
+    return rc;
   OCPPO_REQUIRE(((reinterpret_cast<uintptr_t>(hidden) | reinterpret_cast<uintptr_t>(w_actor) |
                   reinterpret_cast<uintptr_t>(w_critic)) & 15) == 0,
                 "ocppo_policy_head_env_step: hidden and head weights must be 16-B aligned");
@@ -1249,7 +1294,7 @@ extern "C" int ocppo_policy_head_env_step(ocppo_stream_t stream, const float* hi
   const HeadEnv env{seed, step_base, step_offset, D, frame_out, reward_out, done_out, ep_state};
 #define OCPPO_HEAD(CH)                                                                          \
   hipLaunchKernelGGL((policy_head_fast_kernel<CH, true>), hgrid, dim3(kWave * kHeadWavesPerBlock), \
-                     0, s, hidden, N, 1, w_actor, b_actor, w_critic, b_critic, noise, (int)A,     \
+                     0, s, hidden, N, 1, w_actor, b_actor, w_critic, b_critic, ns, (int)A,        \
                      action_out, logprob_out, nullptr, value_out, nullptr, env)
   switch (H / 256) {
     case 1: OCPPO_HEAD(1); break;
@@ -2174,4 +2219,46 @@ extern "C" int ocppo_sum_splits_finish(ocppo_stream_t stream, const float* part,
     default: hipLaunchKernelGGL(sum_splits_hlfin_kernel<16>, grid, block, 0, s, p4, n4, o4, ns, d.f); break;
   }
   return check_launch("ocppo_sum_splits_finish");
+}
+
+// ---- torch's exponential_ on its own (ocppo_philox.h) ---------------------------------------------
+namespace ocppo {
+__global__ __launch_bounds__(256) void philox_exponential_kernel(float* __restrict__ out,
+                                                                 int64_t numel, PhiloxNoise pn) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < numel;
+       i += stride)
+    out[i] = philox_noise(pn, i);
+}
+}  // namespace ocppo
+
+extern "C" int ocppo_torch_exponential_geometry(int64_t numel, int64_t cus,
+                                                int64_t max_threads_per_cu, int64_t* stride,
+                                                int64_t* offset_increment) {
+  OCPPO_REQUIRE(numel > 0 && cus > 0 && max_threads_per_cu >= 256 && stride && offset_increment,
+                "ocppo_torch_exponential_geometry: bad arguments");
+  // ATen calc_execution_policy: 256-thread blocks, grid capped at CUs * (threads per CU / 256),
+  // ((numel - 1) / (256 * grid * 4) + 1) * 4 philox offsets per draw (unroll 4: float4 uniforms)
+  int64_t grid = ceil_div(numel, 256);
+  const int64_t cap = cus * (max_threads_per_cu / 256);
+  if (grid > cap) grid = cap;
+  *stride = 256 * grid;
+  *offset_increment = ((numel - 1) / (*stride * 4) + 1) * 4;
+  return OCPPO_OK;
+}
+
+extern "C" int ocppo_philox_exponential(ocppo_stream_t stream, float* out, int64_t numel,
+                                        const int64_t* philox_state, int64_t philox_offset,
+                                        int64_t philox_stride) {
+  OCPPO_REQUIRE(numel >= 0, "ocppo_philox_exponential: bad size");
+  if (numel == 0) return OCPPO_OK;
+  OCPPO_REQUIRE(out && philox_state, "ocppo_philox_exponential: null pointer");
+  OCPPO_REQUIRE(philox_stride > 0 && philox_stride % 256 == 0 && philox_offset >= 0,
+                "ocppo_philox_exponential: bad philox stride %lld / offset %lld",
+                (long long)philox_stride, (long long)philox_offset);
+  clear_stale_error();
+  const dim3 grid(static_cast<unsigned>(grid_for(numel, 256))), block(256);
+  hipLaunchKernelGGL(philox_exponential_kernel, grid, block, 0, as_stream(stream), out, numel,
+                     PhiloxNoise{philox_state, philox_offset, philox_stride});
+  return check_launch("ocppo_philox_exponential");
 }

@@ -158,6 +158,11 @@ class _FramesExpand(torch.autograd.Function):
 # (frames_expand never materialised): forward and weight gradient gather the rows through an
 # [M, W] row table (ocppo_gemm_x6_gather), dX goes to the frame scatter as before.
 FUSED_DECODE_GATHER = True
+# ... its dX reading the weight's pre-split planes. Off: once the planes were really read
+# (round 5: the backward reads them from ctx, not from the forward thread's scope) they measured
+# slower than the in-kernel split at config 2 (979.0 / 962.8k vs 986.0 / 982.7k env steps/s,
+# tools/ab_toggle.py, profiles/r05/ab_decoder_dx_planes.txt), so the trainer does not build them
+DECODE_DX_PLANES = False
 
 
 class _DecodeFrames(torch.autograd.Function):
@@ -186,6 +191,9 @@ class _DecodeFrames(torch.autograd.Function):
             enc_box["premasked"] = True
         ctx.save_for_backward(enc, idx, uniq, inv, dones, out)
         ctx.params, ctx.box, ctx.enc_box = (w, b), box, (enc_box if fuse else None)
+        # the dX planes are read here: the weight_planes() scope is the forward thread's, and
+        # autograd runs this node's backward on its device thread
+        ctx.pdx = agents._planes(w, "dx") if DECODE_DX_PLANES else None
         ctx.geom = (int(mb), T, N, W, perm.numel())
         return out
 
@@ -203,7 +211,7 @@ class _DecodeFrames(torch.autograd.Function):
         else:
             gp = torch.ops.aten.threshold_backward(g, out, 0)
             torch.sum(gp, 0, out=b.grad)
-        dh = agents._dx(gp, w, True, agents._planes(w, "dx")).view(M, W, -1)
+        dh = agents._dx(gp, w, True, ctx.pdx).view(M, W, -1)
         if ctx.enc_box is not None:
             denc, part = ops.timed("frames_scatter_relu", lambda: ops.frames_scatter_relu(
                 dh, uniq, inv, mb, dones, T, N, W, out=enc))
@@ -240,13 +248,27 @@ def _decode_gather_ok(agent, enc, M: int, W: int) -> bool:
     lin = net[flat + 1]
     C, E = enc.shape
     H = lin.out_features
-    st = agents._x6_splits(M, H, W * E) if M % 32 == 0 else None
     return (lin.bias is not None and lin.in_features == W * E and agents.x6_route(lin.weight)
             and agents._direct(lin.weight) and agents._direct(lin.bias)
             and lin.weight.is_contiguous() and lin.weight.data_ptr() % 16 == 0
             and lin.bias.data_ptr() % 16 == 0 and enc.is_contiguous() and enc.data_ptr() % 16 == 0
-            and M % 128 == 0 and H % 128 == 0 and E % 128 == 0 and (M // 32) % W == 0
-            and st is not None and st[1] == ops.X6_AUTO and (M // 32) % st[0] == 0
+            and decode_gather_shape_ok(M, H, E, W))
+
+
+# K-split counts ocppo_sum_splits_act combines (the gathered forward runs one split per slot)
+DECODE_SPLITS = (1, 2, 4, 8, 16)
+
+
+def decode_gather_shape_ok(M: int, H: int, E: int, W: int) -> bool:
+    """The shape part of _decode_gather_ok: the forward's W K-splits (one per stack slot) must be a
+    split count the combine takes, the tiles 128 x 128, the weight gradient's splits even over
+    32-row steps with <= 1024 rows each."""
+    from . import agents
+
+    if W not in DECODE_SPLITS or M % 128 or H % 128 or E % 128 or (M // 32) % W:
+        return False
+    st = agents._x6_splits(M, H, W * E)
+    return (st is not None and st[1] == ops.X6_AUTO and (M // 32) % st[0] == 0
             and M // st[0] <= 1024 and W * (M // 128) * (H // 128) >= 256)
 
 
@@ -291,6 +313,11 @@ class _GatherLinear1(torch.autograd.Function):
         if ctx.slot is not None:
             ctx.slot.pop("l1", None)
             if ctx.slot.pop("done", False) or g is None:
+                # a weight-gradient step the next layer left here must still run (with no
+                # finish to carry: this layer wrote nothing to finish)
+                run = ctx.slot.pop("run", None)
+                if run is not None:
+                    run(None)
                 return None, None, None, None, None
         g = g.contiguous()
         run = ctx.slot.pop("run", None) if ctx.slot is not None else None

@@ -65,6 +65,17 @@ def timed(name: str, fn):
     return TIMER.bracket(name, fn) if TIMER is not None else fn()
 
 
+# gemm_x6 launches issued with pre-split weight planes, by (M, N, K): host-side bookkeeping at
+# issue time (under capture: once per captured launch), so tests can see that the planes a
+# WeightPlanes refresh writes are actually read
+PLANE_USES: dict = {}
+
+
+def _note_planes(b_planes, M: int, N: int, K: int):
+    if b_planes is not None:
+        PLANE_USES[(M, N, K)] = PLANE_USES.get((M, N, K), 0) + 1
+
+
 def _stream(device: torch.device) -> int:
     if device.type != "cuda":
         raise ValueError(f"HIP kernels need GPU tensors, got device {device} (no CPU fallback)")
@@ -348,9 +359,69 @@ def ppo_loss(logits, new_value, b_actions, b_logprobs, b_advantages, b_returns, 
 # ---------------------------------------------------------------------------------------------
 # Categorical action head (architectures/ppo.py:89-95)
 # ---------------------------------------------------------------------------------------------
+class TorchExpStream:
+    """The reference's sampling stream for the sampling kernels to draw themselves: the Exp(1)
+    values torch.empty(N, A).exponential_() would return on `device`'s default generator, one
+    [N, A] draw per rollout step (Categorical.sample, architectures/ppo.py:92-94, called at
+    ppo_atari_oc.py:505-506). `claim(steps)` (host, before the rollout, outside any graph) takes
+    the generator's current (seed, philox offset), advances the generator past `steps` draws as
+    `steps` exponential_ calls would, and writes both into the device `state` the captured
+    kernels read; `philox(t)` is step t's (state, offset, stride) argument."""
+
+    def __init__(self, numel: int, device):
+        self.device = torch.device(device)
+        self.gen = torch.cuda.default_generators[self.device.index
+                                                 if self.device.index is not None else 0]
+        self.stride, self.increment = torch_exponential_geometry(numel, self.device)
+        self.state = torch.zeros(2, dtype=torch.int64, device=self.device)
+        self._seed = None
+
+    def claim(self, steps: int):
+        base = self.gen.get_offset()
+        self.gen.set_offset(base + steps * self.increment)
+        seed = self.gen.initial_seed()
+        if seed != self._seed:
+            self.state[0].fill_(seed if seed < 1 << 63 else seed - (1 << 64))
+            self._seed = seed
+        self.state[1].fill_(base)  # a fill launch with the value as argument: no host sync
+
+    def philox(self, t: int):
+        return self.state, t * self.increment, self.stride
+
+
+def torch_exponential_geometry(numel: int, device) -> tuple[int, int]:
+    """(grid stride, philox-offset increment) of torch's exponential_ over `numel` elements on
+    `device` (ocppo_torch_exponential_geometry)."""
+    props = torch.cuda.get_device_properties(device)
+    stride, inc = ctypes.c_int64(), ctypes.c_int64()
+    call("ocppo_torch_exponential_geometry", numel, props.multi_processor_count,
+         props.max_threads_per_multi_processor, ctypes.byref(stride), ctypes.byref(inc))
+    return stride.value, inc.value
+
+
+def philox_exponential(out, state, offset: int, stride: int):
+    """out[:] = torch's exponential_ draws at generator state[0..1] + (0, offset)."""
+    dev = out.device
+    call("ocppo_philox_exponential", _stream(dev), _check(out, "out", torch.float32, dev),
+         out.numel(), _check(state, "philox_state", torch.int64, dev, 2), int(offset), int(stride))
+    return out
+
+
+def _noise_args(noise, philox, n, dev):
+    """(noise pointer, philox state pointer, offset, stride) of a sampling entry: noise read, or
+    philox = (state, offset, stride) drawn in the kernel (noise then optional, written)."""
+    f = torch.float32
+    if philox is None:
+        return (_check(noise, "noise", f, dev, n), None, 0, 0)
+    state, off, stride = philox
+    return (_opt(noise, "noise", f, dev, n), _check(state, "philox_state", torch.int64, dev, 2),
+            int(off), int(stride))
+
+
 def categorical_sample(logits, noise, action_out=None, logprob_out=None, entropy_out=None,
-                       value_in=None, value_out=None):
-    """argmax(softmax(logits) / noise) with log_prob and entropy; noise ~ Exp(1) [N, A]."""
+                       value_in=None, value_out=None, philox=None):
+    """argmax(softmax(logits) / noise) with log_prob and entropy; noise ~ Exp(1) [N, A] (or drawn
+    in the kernel: philox = TorchExpStream.philox(t), noise then receives the draws if given)."""
     N, A = logits.shape
     dev = logits.device
     f = torch.float32
@@ -361,7 +432,7 @@ def categorical_sample(logits, noise, action_out=None, logprob_out=None, entropy
     if (value_in is None) != (value_out is None):
         raise ValueError("value_in and value_out go together")
     call("ocppo_categorical_sample", _stream(dev), _check(logits, "logits", f, dev),
-         _check(noise, "noise", f, dev, N * A), N, A,
+         *_noise_args(noise, philox, N * A, dev), N, A,
          _check(action_out, "action_out", torch.int64, dev, N),
          _check(logprob_out, "logprob_out", f, dev, N), _opt(entropy_out, "entropy_out", f, dev, N),
          _opt(value_in, "value_in", f, dev, N), _opt(value_out, "value_out", f, dev, N))
@@ -369,7 +440,8 @@ def categorical_sample(logits, noise, action_out=None, logprob_out=None, entropy
 
 
 def policy_head_sample(hidden, w_actor, b_actor, w_critic, b_critic, noise, action_out=None,
-                       logprob_out=None, value_out=None, entropy_out=None, logits_out=None):
+                       logprob_out=None, value_out=None, entropy_out=None, logits_out=None,
+                       philox=None):
     """Fused actor/critic heads + Categorical sample for a rollout step (no autograd)."""
     N, H = hidden.shape
     A = w_actor.shape[0]
@@ -386,7 +458,7 @@ def policy_head_sample(hidden, w_actor, b_actor, w_critic, b_critic, noise, acti
     call("ocppo_policy_head_sample", _stream(dev), _check(hidden, "hidden", f, dev), N, H,
          _check(w_actor, "w_actor", f, dev), _check(b_actor, "b_actor", f, dev, A),
          _check(w_critic, "w_critic", f, dev, H), _check(b_critic, "b_critic", f, dev, 1),
-         _check(noise, "noise", f, dev, N * A), A,
+         *_noise_args(noise, philox, N * A, dev), A,
          _check(action_out, "action_out", torch.int64, dev, N),
          _check(logprob_out, "logprob_out", f, dev, N), _opt(entropy_out, "entropy_out", f, dev, N),
          _check(value_out, "value_out", f, dev, N), _opt(logits_out, "logits_out", f, dev, N * A))
@@ -407,7 +479,7 @@ def policy_head_env_ok(hidden, w_actor, w_critic, env) -> bool:
 
 
 def policy_head_env_step(hidden, w_actor, b_actor, w_critic, b_critic, noise, action_out,
-                         logprob_out, value_out, env, step_offset: int):
+                         logprob_out, value_out, env, step_offset: int, philox=None):
     """policy_head_sample + env.step(action_out, step_offset) in one launch
     (ocppo_policy_head_env_step; env a SyntheticAtariEnv with object frames)."""
     N, H = hidden.shape
@@ -420,7 +492,7 @@ def policy_head_env_step(hidden, w_actor, b_actor, w_critic, b_critic, noise, ac
     call("ocppo_policy_head_env_step", _stream(dev), _check(hidden, "hidden", f, dev), N, H,
          _check(w_actor, "w_actor", f, dev), _check(b_actor, "b_actor", f, dev, A),
          _check(w_critic, "w_critic", f, dev, H), _check(b_critic, "b_critic", f, dev, 1),
-         _check(noise, "noise", f, dev, N * A), A,
+         *_noise_args(noise, philox, N * A, dev), A,
          _check(action_out, "action_out", torch.int64, dev, N),
          _check(logprob_out, "logprob_out", f, dev, N), _check(value_out, "value_out", f, dev, N),
          env.seed & 0xFFFFFFFFFFFFFFFF, _check(env.step_base, "step_base", torch.int64, dev, 1),
@@ -1028,6 +1100,7 @@ def gemm_x6(a, sam, sak, b, sbn, sbk, c, ldc, M, N, K, splits=1, split_c=0, bias
     masked = mask is not None or mbits_in is not None
     name = f"gemm_x6_{M}x{N}x{K}s{splits}{'m' if masked else ''}"
     keep = (a, b, c, bias, mask, dbp, mbits_out, mbits_in, b_planes)
+    _note_planes(b_planes, M, N, K)
     timed(name, lambda: call("ocppo_gemm_x6", _stream(dev), *args) or keep)
     return c
 
@@ -1084,6 +1157,7 @@ def gemm_x6_gather(a, sam, sak, b, sbn, sbk, c, ldc, M, N, K, gidx, gw, gseg, mo
             int(bool(relu)), None if b_planes is None else b_planes.data_ptr(),
             _check(gidx, "gidx", torch.int32, dev), gw, gseg, int(mode))
     keep = (a, b, c, bias, b_planes, gidx)
+    _note_planes(b_planes, M, N, K)
     timed(f"gemm_x6_{M}x{N}x{K}s{splits}",
           lambda: call("ocppo_gemm_x6_gather", _stream(dev), *args) or keep)
     return c

@@ -33,6 +33,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from . import agents, frames, gemm_table, ops
+from .rccl import RcclComm, RcclExchange
 from .agents import NormalizeImg, PPObj, fused_trunk, linear_relu, make_agent
 from .args import Args
 from .envs import HostVecEnv, make_device_env
@@ -230,12 +231,16 @@ def _quiesce_rccl():
         dist.distributed_c10d._get_default_group()._wait_for_pending_works()
 
 
-def _graph_capture(graph, pool=None):
+def _graph_capture(graph, pool=None, quiesce: bool = False):
     """hipGraph capture in thread-local mode: the RCCL process group's watchdog thread polls its
     work events (hipEventQuery) while this thread captures, which global-mode capture turns into
     hipErrorStreamCaptureUnsupported and a process abort (seen once in 3 runs of the 1-rank nccl
-    test, tests/test_dp_gpu.py). Only this thread's calls are restricted, as they must be."""
-    _quiesce_rccl()
+    test, tests/test_dp_gpu.py). Only this thread's calls are restricted, as they must be.
+    quiesce: the capture will issue torch.distributed collectives (dp_collectives="torch" with
+    dp_graph_collectives), which join the process group's stream: wait for its older work first
+    (_quiesce_rccl). The package's own communicator (oc_cleanrl_amd.rccl) needs none of this."""
+    if quiesce:
+        _quiesce_rccl()
     return torch.cuda.graph(graph, pool=pool, capture_error_mode="thread_local")
 
 
@@ -251,6 +256,15 @@ class PPOTrainer:
         # at world size 1 only on request (dp_exchange), over an initialised 1-rank group
         self.dp = world_size > 1 or (args.dp_exchange and dist.is_available()
                                      and dist.is_initialized())
+        # the exchange's own RCCL communicator (oc_cleanrl_amd.rccl) over an nccl process group:
+        # its all-reduces are captured with each epoch's minibatches; a side stream carries the
+        # tail's all-reduce while the lower encoder layers run their backward
+        self.comm = self.side = None
+        if (self.dp and args.dp_collectives == "rccl" and torch.device(device).type == "cuda"
+                and dist.get_backend() == "nccl"):
+            torch.cuda.set_device(device)
+            self.comm = RcclComm(rank, dist.get_world_size())
+            self.side = torch.cuda.Stream(device)
         self.log_enabled = log and rank == 0
         a = args
         if envs is None and a.backend != "Synthetic":
@@ -343,9 +357,12 @@ class PPOTrainer:
         self.values = torch.zeros((T + 1, N), dtype=f32, device=dev)
         self.advantages = torch.zeros((T, N), dtype=f32, device=dev)
         self.returns = torch.zeros((T, N), dtype=f32, device=dev)
-        # the Exp(1) draws torch's Categorical.sample makes ([N, A] per step), for the whole rollout
-        # in one generator call instead of T launches
+        # the Exp(1) draws torch's Categorical.sample makes ([N, A] per step): by default drawn
+        # inside the sampling kernels as torch's exponential_ would (ops.TorchExpStream), which
+        # also write them here; or torch's exponential_ per step / per rollout (Args.sampling_noise)
         self.noise = torch.zeros((T, N, self.A), dtype=f32, device=dev)
+        self.exp_stream = (ops.TorchExpStream(N * self.A, dev) if a.sampling_noise == "kernel"
+                           else None)
         self.enc_cache = (torch.zeros((N, self.obs_shape[0], self.agent.encoding_dim), dtype=f32,
                                       device=dev) if self.frame_cache else None)
         # frame cache + fusions: the store of step t-1 rides in the launch of step t's first two
@@ -424,6 +441,10 @@ class PPOTrainer:
         # captures and replays it at 16 and 256 envs, deterministic or not, NHWC or NCHW,
         # profiles/r02/c3_capture.log)
         self.graph_update = a.cuda_graphs
+        # DP: the all-reduces inside the per-epoch update graphs (own communicator, or torch's
+        # collectives captured on request), else eager between per-phase graphs
+        self.captured_exchange = self.dp and (self.comm is not None or a.dp_graph_collectives)
+        self.quiesce = self.dp and self.comm is None and a.dp_graph_collectives
         self.timer = KernelTimer(kernel_timing)
         if kernel_timing:
             ops.TIMER = self.timer  # launch sites inside autograd (relu_bias_grad, frames_*)
@@ -464,7 +485,9 @@ class PPOTrainer:
                     agents.X6_FWD_SPLITK and m.in_features % 32 == 0 and
                     ops.x6_fwd_splits(rows, m.out_features, m.in_features) is not None):
                 fwd.append(m.weight)
-            if pays(rows, m.in_features, m.out_features):
+            # (the decoder's dX planes only where measured to pay: frames.DECODE_DX_PLANES)
+            if pays(rows, m.in_features, m.out_features) and (i < ag._flat or
+                                                              frames.DECODE_DX_PLANES):
                 dx.append(m.weight)
         return ops.WeightPlanes(fwd, dx) if fwd or dx else None
 
@@ -583,10 +606,11 @@ class PPOTrainer:
     def _act(self, t: int, env_step: bool = False) -> bool:
         """Actions / log-probs / values of step t; True when the env step ran too."""
         ag = self.agent
-        if self.args.per_step_noise:
+        if self.args.sampling_noise == "torch":
             # the reference's stream: one Exp(1) draw of [N, A] per step (Categorical.sample at
             # ppo_atari_oc.py:506), from the same device generator
             self.noise[t].exponential_()
+        px = self.exp_stream.philox(t) if self.exp_stream is not None else None
         if self.fused_head:
             hidden = self._policy_hidden(t)
             if env_step and FUSED_HEAD_ENV and ops.policy_head_env_ok(
@@ -594,16 +618,16 @@ class PPOTrainer:
                 self.timer.bracket("action_head_env", lambda: ops.policy_head_env_step(
                     hidden, ag.actor.weight, ag.actor.bias, ag.critic.weight, ag.critic.bias,
                     self.noise[t], self.actions[t], self.logprobs[t], self.values[t], self.env,
-                    t))
+                    t, philox=px))
                 return True
             self.timer.bracket("action_head", lambda: ops.policy_head_sample(
                 hidden, ag.actor.weight, ag.actor.bias, ag.critic.weight, ag.critic.bias,
-                self.noise[t], self.actions[t], self.logprobs[t], self.values[t]))
+                self.noise[t], self.actions[t], self.logprobs[t], self.values[t], philox=px))
         else:
             logits, value = ag.logits_and_value(self.net_obs, self.prescale)
             self.timer.bracket("action_head", lambda: ops.categorical_sample(
                 logits, self.noise[t], self.actions[t], self.logprobs[t], None, value.view(-1),
-                self.values[t]))
+                self.values[t], philox=px))
         return False
 
     def _store(self, t: int):
@@ -624,7 +648,7 @@ class PPOTrainer:
         T = self.T
         self.obs[0].copy_(self.obs[T])
         self.dones[0].copy_(self.dones[T])
-        if not self.args.per_step_noise:
+        if self.args.sampling_noise == "rollout":
             self.noise.exponential_()  # the whole rollout's Exp(1) draws in one generator call
 
     def _rollout_end(self):
@@ -781,7 +805,11 @@ class PPOTrainer:
         buffer's tail (the last encoder layer, decoder and heads); its all-reduce runs on RCCL's
         stream while the second phase (the encoder layers below the cut) runs on ours, then the
         head of the buffer follows."""
-        ex = GradExchange(self.grad_buf, self.tail_off, self.world, self.args.fused_optimizer)
+        if self.comm is not None:
+            ex = RcclExchange(self.grad_buf, self.tail_off, self.world, self.args.fused_optimizer,
+                              self.comm, self.side)
+        else:
+            ex = GradExchange(self.grad_buf, self.tail_off, self.world, self.args.fused_optimizer)
         if not self.split:
             ex.whole()
         elif replay:
@@ -899,12 +927,12 @@ class PPOTrainer:
                 self.g_host.append(g)
         if not self.graph_update:
             pass
-        elif not self.dp or self.args.dp_graph_collectives:
-            # (DP: the epoch's all-reduces captured with it; ProcessGroupNCCL records no watchdog
-            # work for collectives issued under capture)
+        elif not self.dp or self.captured_exchange:
+            # (DP: the epoch's all-reduces captured with it -- the package's own communicator, or
+            # torch's collectives, for which ProcessGroupNCCL records no watchdog work)
             for e in range(self.E):
                 g = torch.cuda.CUDAGraph()
-                with _graph_capture(g, pool):
+                with _graph_capture(g, pool, quiesce=self.quiesce):
                     self._update_epoch(e)
                 self.g_update.append(g)
                 pool = pool if pool is not None else g.pool()
@@ -932,7 +960,7 @@ class PPOTrainer:
         self.executed_mb = 0
         for e in range(self.E):
             if self.graphs_ready and self.graph_update:
-                if not self.dp or a.dp_graph_collectives:
+                if not self.dp or self.captured_exchange:
                     self.g_update[e].replay()
                 else:
                     for k in range(self.nmb):
@@ -962,6 +990,10 @@ class PPOTrainer:
         use_graphs = a.cuda_graphs and self.iteration > 1
         if use_graphs and not self.graphs_ready:
             self._capture()
+        if self.exp_stream is not None:
+            # the rollout's T draws of the reference stream: the generator state they start at
+            # (read by the sampling kernels, captured or not) and the generator advanced past them
+            self.exp_stream.claim(self.T)
         if self.host_env:
             self._rollout_host()
         elif self.graphs_ready:
@@ -1016,6 +1048,13 @@ class PPOTrainer:
     def save(self, path):
         torch.save(self.state_dict_checkpoint(), path)
 
+    def close(self):
+        """Release the exchange's RCCL communicator (before the process group is destroyed)."""
+        if self.comm is not None:
+            torch.cuda.synchronize(self.dev)
+            self.comm.close()
+            self.comm = None
+
     def param_checksum(self) -> int:
         """An exact, order-sensitive checksum of every parameter's f32 bit pattern (int64 sum of
         bits × (position mod 65521 + 1)). The DP replicas of ppo_atari_multigpu.py:360-377 start
@@ -1046,8 +1085,21 @@ def run(args: Args, device=None, rank: int = 0, world_size: int = 1) -> PPOTrain
         run_dir.mkdir(parents=True, exist_ok=True)
         (run_dir / "args.json").write_text(json.dumps(asdict(args), indent=1, default=str))
         writer = open(run_dir / "metrics.jsonl", "w")
+    watch = None
+    if args.stall_timeout > 0:  # fail fast: a rank stuck in an iteration ends the run, with a record
+        import sys
+
+        from .watch import RankWatch
+
+        port = os.environ.get("MASTER_PORT", str(os.getpid()))
+        watch = RankWatch(rank, world_size, os.environ.get("OCPPO_WATCH_DIR",
+                                                           f"/tmp/ocppo_watch_{port}"),
+                          stall_s=args.stall_timeout,
+                          on_fire=lambda rec: print(json.dumps(rec), file=sys.stderr, flush=True))
     start = time.time()
     for it in range(1, args.num_iterations + 1):
+        if watch is not None:  # the first two iterations also capture the graphs
+            watch.phase(f"iteration {it}", stall_s=args.stall_timeout * (3 if it <= 2 else 1))
         if it % args.checkpoint_interval == 0 and rank == 0 and args.save_model:
             tr.save(run_dir / f"{args.exp_name}_{it}.cleanrl_model")
         collect = (it % args.metrics_every == 0) or it == args.num_iterations
@@ -1075,4 +1127,6 @@ def run(args: Args, device=None, rank: int = 0, world_size: int = 1) -> PPOTrain
             writer.write(json.dumps(summ) + "\n")
     if writer:
         writer.close()
+    if watch is not None:
+        watch.stop()
     return tr

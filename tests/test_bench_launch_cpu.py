@@ -111,3 +111,53 @@ def test_replica_check_gloo_world2(diverge):
         assert all("diverged" in out[r] for r in range(2))
     else:
         assert out[0] == out[1] and out[0]["equal"] and len(out[0]["param_checksums"]) == 2
+
+
+def test_stalled_rank_fails_fast_with_a_line_naming_it(capfd):
+    """The fail-fast path: 2 ranks over gloo, rank 1 stops
+    before its second all-reduce while rank 0 waits inside it. Rank 0's watchdog fires after the
+    stall bound, its line names both ranks' phases and rank 1 as the one behind, and the run
+    exits non-zero well inside the bound -- the same RankWatch / launcher the GPU bench uses."""
+    import time
+
+    t0 = time.monotonic()
+    rc = bench.launch(["--gpus", "2", "--backend", "gloo", "--rehearse-stall", "1", "--stall", "4",
+                       "--deadline", "60", "--steps", "3"], 2, deadline_s=90)
+    elapsed = time.monotonic() - t0
+    assert rc != 0
+    assert elapsed < 45, elapsed
+    lines = capfd.readouterr().out.splitlines()
+    assert len(lines) == 1
+    rec = json.loads(lines[0])
+    assert rec["value"] is None and rec["error"] in ("stall", "rank 1 failed")
+    assert rec["ranks"] == {"0": "timed 1 all-reduce", "1": "timed 1"}
+    assert rec["behind"] == [1]
+
+
+HANG = """
+import time
+while True:
+    time.sleep(1)
+"""
+
+
+def test_launcher_deadline_kills_a_hung_tree(tmp_path, capfd):
+    """Ranks that never finish (and whose own watchdog never fires) are killed as a process group
+    at the launcher's deadline; exit code 3 and one error line."""
+    import time
+
+    probe = tmp_path / "hang.py"
+    probe.write_text(HANG)
+    t0 = time.monotonic()
+    rc = bench.launch(["--gpus", "2"], 2, script=probe, deadline_s=3)
+    assert rc == 3 and time.monotonic() - t0 < 30
+    rec = json.loads(capfd.readouterr().out.splitlines()[-1])
+    assert rec["error"] == "launcher deadline" and rec["value"] is None
+
+
+def test_rehearsal_without_a_stall_completes(capfd):
+    rc = bench.launch(["--gpus", "2", "--backend", "gloo", "--rehearse-stall", "7", "--stall", "20",
+                       "--steps", "3"], 2, deadline_s=90)
+    assert rc == 0
+    rec = json.loads(capfd.readouterr().out.splitlines()[-1])
+    assert rec == {"rehearsal": "no stall", "value": 8.0}

@@ -66,10 +66,13 @@ def test_overlapped_exchange_equals_the_whole_buffer_exchange():
 
 
 
-def _rccl_worker(rank, world, port, out, overlap, graphs, collectives=False):
+def _rccl_worker(rank, world, port, out, overlap, graphs, mode="rccl"):
     """The RCCL exchange path at world size 1: nccl (= RCCL) process group bound to cuda:0,
-    per-minibatch graphs, the async tail all-reduce overlapped with the g_low replay, the head
-    all-reduce, g_opt -- against the plain single-GPU trainer in the same process."""
+    against the plain single-GPU trainer in the same process. mode "rccl": the package's own
+    communicator, each epoch's all-reduces captured in its graph (the tail's on a side stream
+    during the lower backward); "torch": torch.distributed collectives between per-minibatch
+    graphs (async tail all-reduce overlapped with the g_low replay, the head, g_opt);
+    "torch-graph": torch's collectives captured with the epoch."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
@@ -82,7 +85,8 @@ def _rccl_worker(rank, world, port, out, overlap, graphs, collectives=False):
                              total_timesteps=32 * 16 * 10, encoder_dims=(32, 64, 48),
                              decoder_dims=(64,), save_model=False, cuda_graphs=graphs,
                              dp_overlap=overlap, dp_exchange=dp,
-                             dp_graph_collectives=collectives), 1)
+                             dp_collectives="rccl" if mode == "rccl" else "torch",
+                             dp_graph_collectives=mode == "torch-graph"), 1)
 
     plain = PPOTrainer(args(False), dev)
     for _ in range(3):
@@ -93,10 +97,11 @@ def _rccl_worker(rank, world, port, out, overlap, graphs, collectives=False):
     assert dist.get_backend() == "nccl"
     tr = PPOTrainer(args(True), dev)
     assert tr.dp and bool(tr.split) == overlap
+    assert (tr.comm is not None) == (mode == "rccl")
     for _ in range(3):
         tr.train_iteration()
     torch.cuda.synchronize()
-    if graphs and collectives:
+    if graphs and mode != "torch":
         assert tr.graphs_ready and len(tr.g_update) == tr.E and tr.g_opt is None
     elif graphs:
         assert tr.graphs_ready and len(tr.g_update) == tr.E * tr.nmb and tr.g_opt is not None
@@ -104,20 +109,23 @@ def _rccl_worker(rank, world, port, out, overlap, graphs, collectives=False):
     flat = lambda t: torch.cat([p.detach().flatten() for p in t.agent.parameters()]).cpu()  # noqa
     out["plain"], out["dp"] = flat(plain), flat(tr)
     out["same_actions"] = bool(torch.equal(plain.actions, tr.actions))
+    tr.close()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("overlap,graphs,collectives", [(True, True, False), (False, True, False),
-                                                        (True, False, False), (True, True, True),
-                                                        (False, True, True)])
-def test_rccl_exchange_one_rank_matches_single_gpu(overlap, graphs, collectives):
+@pytest.mark.parametrize("overlap,graphs,mode", [
+    (True, True, "rccl"), (False, True, "rccl"), (True, False, "rccl"),
+    (True, True, "torch"), (False, True, "torch"), (True, False, "torch"),
+    (True, True, "torch-graph"), (False, True, "torch-graph")])
+def test_rccl_exchange_one_rank_matches_single_gpu(overlap, graphs, mode):
     """ppo_atari_multigpu.py:174-183, 360-377 over RCCL on the one-GPU box: the DP flow with a
     1-rank nccl group leaves parameters bit-identical to the single-GPU trainer after 3
-    iterations (SUM over one rank, /1 folded into Adam); also with each epoch's all-reduces
-    captured inside its hipGraph (dp_graph_collectives)."""
+    iterations (SUM over one rank, /1 folded into Adam) -- through the package's own RCCL
+    communicator with the all-reduces captured in each epoch's graph (the default), through
+    torch's collectives between per-minibatch graphs, and through torch's collectives captured."""
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_rccl_worker, args=(1, _port(), out, overlap, graphs, collectives), nprocs=1,
+    mp.spawn(_rccl_worker, args=(1, _port(), out, overlap, graphs, mode), nprocs=1,
              join=True)
     assert out["same_actions"]
     assert torch.equal(out["plain"], out["dp"]), \

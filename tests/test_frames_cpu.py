@@ -90,3 +90,18 @@ def test_scatter_is_the_adjoint_of_expand():
         np.testing.assert_allclose(np.vdot(h.astype(np.float64), dh), np.vdot(enc.astype(np.float64), denc),
                                    rtol=1e-5)
         assert np.all(denc[pl.counts[j]:] == 0)
+
+
+@pytest.mark.parametrize("M,H,E,W,ok", [
+    (4096, 512, 512, 4, True),    # config 2: the gathered decoder runs
+    (6144, 512, 512, 3, False),   # a 3-frame stack: no 3-way split combine -> the expand path
+    (6144, 512, 512, 2, True),
+    (4096, 512, 512, 5, False),
+])
+def test_decode_gather_gate_only_takes_combinable_stack_widths(M, H, E, W, ok):
+    """ocppo_sum_splits_act combines 1/2/4/8/16 splits and the gathered decoder forward runs one
+    split per stack slot: any other buffer_window_size must take the _FramesExpand path instead
+    of failing inside the update."""
+    from oc_cleanrl_amd import frames
+
+    assert frames.decode_gather_shape_ok(M, H, E, W) is ok

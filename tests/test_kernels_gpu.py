@@ -246,6 +246,98 @@ def test_sample_matches_torch_categorical_on_device(ops, dev, A):
     torch.testing.assert_close(lp, dist.log_prob(a), rtol=1e-6, atol=2e-6)
 
 
+def _gen_state(gen, dev):
+    """A generator's (seed, philox offset) as the device [2] state the sampling kernels read."""
+    seed = gen.initial_seed()
+    return torch.tensor([seed if seed < 1 << 63 else seed - (1 << 64), gen.get_offset()],
+                        dtype=torch.int64, device=dev)
+
+
+@pytest.mark.parametrize("numel", [1, 6, 768, 1000, 3072 * 7, 256 * 2048 + 5,
+                                   4 * 256 * 2048 + 17, 9 * 256 * 2048 + 1])
+@pytest.mark.parametrize("seed", [0, 1, 2 ** 63 + 12345])
+def test_philox_exponential_is_torch_exponential(ops, dev, numel, seed):
+    """ocppo_philox_exponential = torch.empty(numel).exponential_() on the device generator,
+    bit for bit: torch's grid geometry (one uniform4 per thread up to 4 grid strides, components
+    1-3 and later draws beyond), its Philox counter layout, uniform conversion and log transform
+    (ocppo_philox.h); and the generator advances by the increment the geometry reports."""
+    g = torch.cuda.default_generators[dev.index or 0]
+    g.manual_seed(seed)
+    g.set_offset(8 * 4)
+    state = _gen_state(g, dev)
+    stride, inc = ops.torch_exponential_geometry(numel, dev)
+    ref = torch.empty(numel, device=dev).exponential_()
+    assert g.get_offset() == 8 * 4 + inc
+    out = ops.philox_exponential(torch.empty(numel, device=dev), state, 0, stride)
+    assert torch.equal(out, ref), int((out != ref).sum())
+    # the next draw of the same shape: offset + inc
+    ref2 = torch.empty(numel, device=dev).exponential_()
+    out2 = ops.philox_exponential(torch.empty(numel, device=dev), state, inc, stride)
+    assert torch.equal(out2, ref2)
+
+
+@pytest.mark.parametrize("N,H,A", [(128, 512, 6), (7, 64, 18), (300001, 512, 6), (33, 100, 6)])
+def test_policy_head_draws_the_torch_stream_itself(ops, dev, N, H, A):
+    """The sampling kernels with philox state: the Exp(1) values they draw (and write) are
+    torch's exponential_ at that generator state, and every output equals the same kernel fed
+    torch's noise tensor -- fast head (E = 1 and E > 1), generic head, categorical sampler."""
+    g = torch.Generator(device=dev).manual_seed(N + H + A)
+    hidden = torch.relu(torch.randn(N, H, device=dev, generator=g))
+    wa = torch.randn(A, H, device=dev, generator=g) * 0.05
+    ba = torch.randn(A, device=dev, generator=g) * 0.1
+    wc = torch.randn(1, H, device=dev, generator=g)
+    bc = torch.randn(1, device=dev, generator=g)
+    dg = torch.cuda.default_generators[dev.index or 0]
+    dg.manual_seed(77)
+    state = _gen_state(dg, dev)
+    stride, inc = ops.torch_exponential_geometry(N * A, dev)
+    for step in range(2):
+        ref_noise = torch.empty(N, A, device=dev).exponential_()
+        ref = ops.policy_head_sample(hidden, wa, ba, wc, bc, ref_noise,
+                                     entropy_out=torch.empty(N, device=dev))
+        drawn = torch.empty(N, A, device=dev)
+        got = ops.policy_head_sample(hidden, wa, ba, wc, bc, drawn,
+                                     entropy_out=torch.empty(N, device=dev),
+                                     philox=(state, step * inc, stride))
+        assert torch.equal(drawn, ref_noise), step
+        for x, y in zip(got, ref):
+            assert torch.equal(x, y), step
+        logits = torch.randn(N, A, device=dev, generator=g)
+        a_ref, lp_ref, _ = ops.categorical_sample(logits, ref_noise)
+        a, lp, _ = ops.categorical_sample(logits, None, philox=(state, step * inc, stride))
+        assert torch.equal(a, a_ref) and torch.equal(lp, lp_ref)
+
+
+def test_policy_head_env_step_draws_the_torch_stream_itself(ops, dev):
+    from oc_cleanrl_amd.envs import SyntheticAtariEnv
+
+    N, H, A, D = 128, 512, 6, 12
+    g = torch.Generator(device=dev).manual_seed(3)
+    hidden = torch.relu(torch.randn(N, H, device=dev, generator=g))
+    wa = torch.randn(A, H, device=dev, generator=g) * 0.05
+    ba = torch.randn(A, device=dev, generator=g) * 0.1
+    wc = torch.randn(1, H, device=dev, generator=g)
+    bc = torch.randn(1, device=dev, generator=g)
+    envs = [SyntheticAtariEnv("ALE/Pong-v5", "obj", N, D, 5, dev) for _ in range(2)]
+    for e in envs:
+        e.reset()
+    dg = torch.cuda.default_generators[dev.index or 0]
+    dg.manual_seed(5)
+    state = _gen_state(dg, dev)
+    stride, inc = ops.torch_exponential_geometry(N * A, dev)
+    for t in range(3):
+        noise = torch.empty(N, A, device=dev).exponential_()
+        outs = [(torch.empty(N, dtype=torch.int64, device=dev), torch.empty(N, device=dev),
+                 torch.empty(N, device=dev)) for _ in range(2)]
+        ops.policy_head_env_step(hidden, wa, ba, wc, bc, noise, *outs[0], envs[0], t)
+        ops.policy_head_env_step(hidden, wa, ba, wc, bc, None, *outs[1], envs[1], t,
+                                 philox=(state, t * inc, stride))
+        for x, y in zip(*outs):
+            assert torch.equal(x, y), t
+        for k in ("frame", "reward", "done", "ep_state"):
+            assert torch.equal(getattr(envs[0], k), getattr(envs[1], k)), (t, k)
+
+
 @pytest.mark.parametrize("A", [4, 18])
 def test_logprob_entropy_fwd_bwd_vs_torch(ops, dev, A):
     N = 3000

@@ -514,15 +514,19 @@ def test_fused_heads_loss_trainer_matches_unfused(dev):
         torch.testing.assert_close(p, q, rtol=1e-3, atol=2e-5)
 
 
-@pytest.mark.parametrize("graphs", [True, False])
-def test_per_step_noise_is_the_reference_sampling_stream(dev, graphs):
-    """per_step_noise: the rollout's Exp(1) draws are exactly the [N, A] draws the reference's
+@pytest.mark.parametrize("graphs,mode", [(True, "kernel"), (False, "kernel"), (True, "torch"),
+                                         (False, "torch")])
+def test_per_step_noise_is_the_reference_sampling_stream(dev, graphs, mode):
+    """The rollout's Exp(1) draws are exactly the [N, A] draws the reference's
     Categorical.sample makes step after step (ppo_atari_oc.py:506) from the device generator
-    seeded like the trainer -- eager and graph-replayed iterations alike."""
+    seeded like the trainer -- eager and graph-replayed iterations alike; drawn inside the
+    sampling kernel (the default, ops.TorchExpStream: torch's Philox stream restated) or by
+    torch's exponential_ per step."""
     from oc_cleanrl_amd.trainer import PPOTrainer
 
-    a = small_args(per_step_noise=True, cuda_graphs=graphs)
+    a = small_args(sampling_noise=mode, cuda_graphs=graphs)
     tr = PPOTrainer(a, dev)
+    assert (tr.exp_stream is not None) == (mode == "kernel")
     got = []
     for _ in range(3):
         tr.train_iteration()
@@ -617,10 +621,20 @@ def test_weight_planes_are_bitwise_the_in_kernel_split(dev, graphs):
     same rollouts, same parameters after three iterations at config-2 dims."""
     kw = dict(num_envs=128, num_steps=128, encoder_dims=(256, 512, 1024, 512),
               decoder_dims=(512,), update_epochs=1, cuda_graphs=graphs)
+    from oc_cleanrl_amd import ops
+
+    ops.PLANE_USES.clear()
     a, _ = run_iters(small_args(x6_weight_planes=True, **kw), 3, dev)
+    used = dict(ops.PLANE_USES)
     b, _ = run_iters(small_args(x6_weight_planes=False, **kw), 3, dev)
     assert a.wplanes is not None and b.wplanes is None
     assert len(a.wplanes.jobs) >= 3
+    # every plane set a refresh writes is read by some product (the decoder's dX planes too: its
+    # backward runs on autograd's device thread, outside the trainer's weight_planes() scope)
+    nk = {(n, k) for (_, n, k) in used}
+    for w, trans, _ in a.wplanes.jobs:
+        want = (w.shape[1], w.shape[0]) if trans else (w.shape[0], w.shape[1])
+        assert want in nk, (tuple(w.shape), trans, sorted(used))
     for p, q in zip(a.agent.parameters(), b.agent.parameters()):
         assert torch.equal(p, q)
 
