@@ -334,10 +334,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, default=2, choices=(1, 2, 3),
+    ap.add_argument("--config", type=int, default=2, choices=(1, 2, 3, 5),
                     help="BASELINE config: 2 = Pong obj PPO_OBJ (the headline; 4 = 2 per GPU), "
                          "3 = Breakout dqn-pixels NatureCNN, 256 envs, 1 = ppo.py CartPole-v1 "
-                         "(4 envs; its CPU leg is the reference's own CPU path)")
+                         "(4 envs; its CPU leg is the reference's own CPU path), 5 = "
+                         "dqn_atari_oc.py SpaceInvaders obj, 1M-row HBM replay (a step = 1000 "
+                         "global steps)")
     ap.add_argument("--envs-per-gpu", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-iterations", type=int, default=3)
@@ -428,10 +430,82 @@ def rehearse_stall(opt, rank: int, world: int, line_out, watch):
     dist.destroy_process_group()
 
 
+DQN_STEPS_PER_BENCH_STEP = 1000
+
+
+def run_dqn(opt, rank: int, world: int, line_out, watch):
+    """BASELINE config 5: the training phase of dqn_atari_oc.py:341-400 on one GPU (obj mode,
+    1 env, a 1M-transition HBM replay; acting, env step, store, replay add every global step, a
+    batch-32 TD update every 4, the target copy every 1000, as replayed hipGraph chunks). One bench
+    step = DQN_STEPS_PER_BENCH_STEP global steps, all past learning_starts. The CPU leg is the
+    same loop on CPU torch (oracle/cpu_learner.time_cpu_dqn)."""
+    from oc_cleanrl_amd.dqn import DQNArgs, DQNTrainer
+
+    if world != 1:
+        raise SystemExit("--config 5 is a one-GPU configuration")
+    watch.phase("init", stall_s=300.0)
+    dev = torch.device("cuda:0" if opt.device_index is None else f"cuda:{opt.device_index}")
+    torch.cuda.set_device(dev)
+    envs = opt.envs_per_gpu or 1
+    args = DQNArgs(env_id="ALE/SpaceInvaders-v5", obs_mode="obj", num_envs=envs,
+                   buffer_size=1_000_000, learning_starts=1000, total_timesteps=10_000_000,
+                   save_model=False, cuda_graphs=not opt.no_graphs)
+    for kv in opt.set:
+        k, v = kv.split("=", 1)
+        cur = getattr(args, k)
+        setattr(args, k, (v.lower() in ("1", "true", "yes")) if isinstance(cur, bool) else type(cur)(v))
+    tr = DQNTrainer(args, dev, log=False)
+    K = DQN_STEPS_PER_BENCH_STEP
+    watch.phase("warmup", stall_s=600.0)
+    tr.steps(args.learning_starts + opt.warmup * K)
+    torch.cuda.synchronize(dev)
+    watch.phase("timed")
+    t0 = time.perf_counter()
+    for i in range(opt.steps):
+        tr.steps(K)
+        watch.beat()
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    m = tr.metrics()
+    watch.phase("report", stall_s=max(opt.deadline, 600.0))
+    cpu = None
+    if not opt.no_cpu_baseline:
+        from oracle.cpu_learner import host_info, time_cpu_dqn, usable_threads
+
+        threads = usable_threads()
+        r = time_cpu_dqn(steps=opt.cpu_iterations * 1000, threads=threads, num_envs=envs)
+        cpu = {"value": round(r["sps"], 1), "unit": "env steps/s", "cores": threads,
+               "kind": "port", "updates_per_sec": round(r["updates_per_sec"], 2),
+               "sample": f"{r['steps']} global steps of dqn_atari_oc.py:341-400 (QNetworkObj, "
+                         f"{envs} env, batch-32 TD update every 4 steps) on CPU torch, "
+                         f"{r['seconds']:.1f} s", "host": host_info()}
+    steps = opt.steps * K
+    line = {
+        "metric": "env steps/sec + DQN updates/sec, dqn_atari_oc.py SpaceInvaders-v5 obj, 1 MI355X",
+        "value": round(steps * envs / dt, 1), "unit": "env steps/s", "n_gpus": 1,
+        "steps": opt.steps, "warmup": opt.warmup, "ms_per_step": round(1e3 * dt / opt.steps, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic (device-resident SpaceInvaders-obj env; random-init Q-network)",
+        "config": {"workload": "dqn_atari_oc.py SpaceInvaders-v5 obj (BASELINE config 5)",
+                   "global_steps_per_step": K, "num_envs": envs, "replay_rows": tr.rb.size,
+                   "replay_obs_dtype": str(tr.obs_dtype).replace("torch.", ""),
+                   "replay_bytes": tr.rb.obs.numel() * tr.rb.obs.element_size(),
+                   "batch_size": args.batch_size, "train_frequency": args.train_frequency,
+                   "cuda_graphs": tr._graphable(), "parallelism": "dp1"},
+        "updates_per_sec": round(steps / args.train_frequency / dt, 2),
+        "us_per_global_step": round(dt / steps * 1e6, 3),
+        "td_loss": m["losses/td_loss"],
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), file=line_out, flush=True)
+
+
 def run_rank(opt, rank: int, world: int, line_out, watch):
     """One rank of the bench (the whole run at N = 1)."""
     if opt.rehearse_stall is not None:
         return rehearse_stall(opt, rank, world, line_out, watch)
+    if opt.config == 5:
+        return run_dqn(opt, rank, world, line_out, watch)
     from datetime import timedelta
 
     from oc_cleanrl_amd.args import Args, finalize

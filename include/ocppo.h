@@ -383,7 +383,10 @@ OCPPO_API int ocppo_bias_act_nchw(ocppo_stream_t stream, const float* y, const f
  * Pre-split B (b_planes != NULL; b is then ignored and may be NULL): the three bf16 pieces of
  * B(n, k) at b_planes[p * bp_stride + n * bp_ld + k] (p = 0, 1, 2; ocppo_split_planes wrote them
  * from the f32 B, so the result is bitwise that of the f32 B): staged by copy, no split in the
- * K loop. Needs sak == 1, bp_ld % 8 == 0, 16-B aligned planes, tile 24..27 or 56.
+ * K loop. Needs sak == 1, bp_ld % 8 == 0, 16-B aligned planes, tile 24..27, 56, 57 or 58.
+ * Tiles 57-60 (the pipelined family): 256 x 128, 128 x 256 (8 waves), 128 x 128 (4 waves) and
+ * 128 x 128 (8 waves) with two LDS stages and one barrier per K step (the next step's operand
+ * split in the MFMAs' shadow); one workgroup per CU.
  * Deterministic (fixed MFMA order, no atomics).
  * ------------------------------------------------------------------------------------------- */
 OCPPO_API int ocppo_gemm_x6(ocppo_stream_t stream, const float* a, int64_t sam, int64_t sak,
@@ -392,7 +395,18 @@ OCPPO_API int ocppo_gemm_x6(ocppo_stream_t stream, const float* a, int64_t sam, 
                             const float* bias, int relu, const float* mask, int64_t ldm,
                             float* dbp, uint64_t* mbits_out, const uint64_t* mbits_in,
                             int tile, int mbig, const void* b_planes, int64_t bp_ld,
-                            int64_t bp_stride);
+                            int64_t bp_stride, void* sk_workspace, size_t sk_workspace_bytes);
+
+/* Bytes of the stream-K workspace of a pipelined tile (57, 58; 0 for every other tile). With
+ * sk_workspace != NULL ocppo_gemm_x6 runs a pipelined product (tiles 57 / 58: 256 x 128 /
+ * 128 x 256, two LDS stages, one workgroup per CU) as a persistent stream-K launch: the tiles are
+ * dealt to the 8 XCDs, each XCD's CUs share its tiles' K steps in equal contiguous ranges, and a
+ * tile split between two workgroups is finished by the one holding its first K steps, after the
+ * later parts' partial accumulators arrive through the workspace (same XCD, so its L2) — every
+ * CU busy to the end at any tile count. splits == 1; the workspace must be 256-B aligned and
+ * zero before the first launch (its flags return to zero after every launch). Same products in
+ * the same order within a part; the parts are added in K order: deterministic. */
+OCPPO_API size_t ocppo_gemm_x6_sk_workspace_bytes(int tile);
 
 /* ---------------------------------------------------------------------------------------------
  * ocppo_gemm_x6 with one operand's rows read through a row table (the update's decoder on the

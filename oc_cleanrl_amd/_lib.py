@@ -109,7 +109,8 @@ SIGNATURES: dict[str, tuple[type, list]] = {
     "ocppo_q_head_epsilon_greedy": (I, [P, P, I64, I64, P, P, I64, U64, P, I64, D, D, D, P, P, P]),
     "ocppo_frames_scatter_relu": (I, [P, P, I64, I64, P, I64, P, I64, P, I64, I64, I64, P, P, P]),
     "ocppo_gemm_x6": (I, [P, P, I64, I64, P, I64, I64, P, I64, I64, I64, I64, I64, I64, P, I, P,
-                          I64, P, P, P, I, I, P, I64, I64]),
+                          I64, P, P, P, I, I, P, I64, I64, P, SZ]),
+    "ocppo_gemm_x6_sk_workspace_bytes": (SZ, [I]),
     "ocppo_split_planes": (I, [P, I, P, P, P, P, P, P]),
     "ocppo_gae_records": (I, [P, P, P, P, P, P, I64, I64, D, D, P, P, P, P, P]),
     "ocppo_minibatch_prepare_records": (I, [P, P, I64, I64, P, P, P, P, P, P, P]),

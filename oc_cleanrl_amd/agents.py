@@ -135,6 +135,29 @@ def _x6_dw(n: int, k: int, rows: int, on: bool = True) -> bool:
     return on and n * k >= X6_MIN_TILES_DW * 16384 and rows >= 1024
 
 
+# The pipelined gemm_x6 tile (ops.X6_PIPE: 128 x 256, two LDS stages, one workgroup per CU) for
+# the products that fill exactly one wave of 256 workgroups with it: the encoder weight
+# gradients [1024 x 512] / [512 x 1024] as 16 row splits (63.6 / 63.3 vs 71.2 / 69.9 us with the
+# combine) and the decoder's dX [4096 x 2048] (44.7 vs 49.8 us), profiles/r05/exp_x6_pipe.txt
+X6_PIPE = True
+
+
+def x6_pipe_tile(M: int, N: int, splits: int = 1):
+    """58 when [M x N] x splits is exactly 256 tiles of 128 x 256, else None."""
+    if not X6_PIPE or M % 128 or N % 256:
+        return None
+    return 58 if splits * (M // 128) * (N // 256) == 256 else None
+
+
+def _x6_pipe_splits(rows: int, n: int, k: int):
+    """(splits, 58) for dW = g^T x [n, k] when some split count in 1..16 gives exactly 256
+    pipelined tiles with >= 8 K steps per split; else None."""
+    for s in (1, 2, 4, 8, 16):
+        if x6_pipe_tile(n, k, s) and rows % (32 * s) == 0 and rows // (32 * s) >= 8:
+            return s, 58
+    return None
+
+
 def _x6_splits(rows: int, n: int, k: int):
     """(splits, variant) of dW = g^T x on gemm_x6 (rows in steps of 32, split evenly): the
     largest tile that reaches >= 512 workgroups (two per CU) over the [n, k] output with at most
@@ -183,7 +206,8 @@ def _weight_grad_core(g, x, out, db, x6, finish):
     rows, n = g.shape
     k = x.shape[1]
     s = _splitk(rows, k, n)
-    st = _x6_splits(rows, n, k) if _x6_dw(n, k, rows, x6) else None
+    st = ((_x6_pipe_splits(rows, n, k) or _x6_splits(rows, n, k)) if _x6_dw(n, k, rows, x6)
+          else None)
     if st is not None and ops.dw_x6_ok(g, x, st[0]):
         s6, t6 = st
         if s6 == 1 and out is not None and db is None and out.is_contiguous():
@@ -217,7 +241,7 @@ def _dx(g, w, x6: bool = True, planes=None):
     M, N = g.shape
     K = w.shape[1]
     if _x6(M, K, N, x6) and ops.dx_x6_ok(g, w):
-        return ops.dx_x6(g, w, planes=planes)
+        return ops.dx_x6(g, w, planes=planes, tile=x6_pipe_tile(M, K))
     if (HIP_SMALL_DX and g.is_cuda and M <= 256 and K <= 256 and N >= 256 and N % 16 == 0 and
             g.dtype == torch.float32 and g.is_contiguous()):
         return ops.linear_act(g, w.t().contiguous())

@@ -100,7 +100,48 @@ struct X6Args {
   int wk;
   float* wrec;
   int64_t wnpw;
+  // probe builds only (-DOCPPO_X6_STAMPS, tools/exp_x6_stamps.py): per workgroup clock stamps
+  int64_t* stamps;
+  // stream-K (x6p persistent launches, sk != 0): partial-accumulator slots and their flags (one
+  // per workgroup, zero between launches)
+  int sk;
+  float* skws;
+  int* skflag;
 };
+
+// Stream-K geometry of an x6p persistent launch: the tiles (row-major) are dealt to the 8 XCDs in
+// contiguous ranges; XCD x's P = grid / 8 workgroups (blockIdx b: XCD b % 8, rank b / 8) share
+// its tiles' K steps evenly, each a contiguous range [r I / P, (r + 1) I / P) of I = tiles x nk
+struct X6pGeom {
+  int xcd, rank, P, t0, t1, nk;
+  int64_t I;
+};
+__device__ __forceinline__ X6pGeom x6p_geom(const X6Args& g, int b, int grid) {
+  X6pGeom q;
+  q.xcd = b & 7;
+  q.rank = b >> 3;
+  q.P = grid >> 3;
+  const int T = g.tiles_m * g.tiles_n;
+  q.t0 = q.xcd * T / 8;
+  q.t1 = (q.xcd + 1) * T / 8;
+  q.nk = g.K / kX6BK;
+  q.I = static_cast<int64_t>(q.t1 - q.t0) * q.nk;
+  return q;
+}
+
+
+#ifdef OCPPO_X6_STAMPS
+// stamp s of the workgroup (thread 0): [0] start, [1] prologue done, [2] K loop done, [3] stores
+// done (shader clock), [4] / [5] start / end on the 100 MHz real-time clock
+#define X6_STAMP(g, s, v)                                                            \
+  do {                                                                               \
+    if ((g).stamps && threadIdx.x == 0) (g).stamps[blockIdx.x * 8 + (s)] = (v);      \
+  } while (0)
+#else
+#define X6_STAMP(g, s, v) \
+  do {                    \
+  } while (0)
+#endif
 
 // Where one tile's outputs go: its row tiles start at row0_base, its dbp partial row is
 // db_base + db_mult tm (db_mult 2: the second of the two 64-row partials is written as zeros),
@@ -108,6 +149,11 @@ struct X6Args {
 struct X6Place {
   int tiles_m, row0_base, db_base, db_mult;
   int64_t id_base;
+  // stream-K segment (x6p persistent launches): mode -1 = the unit u as usual; else tile seg_tile,
+  // K steps [seg_kb, seg_kb + seg_nk), and mode 0 = the whole tile (epilogue), 1 = a later part
+  // of a split tile (partial accumulators to workspace slot seg_slot, then its flag), 2 = the
+  // tile's first part (adds the later parts' partials, then the epilogue)
+  int seg_mode = -1, seg_tile = 0, seg_kb = 0, seg_nk = 0, seg_slot = 0;
 };
 
 // The three bf16 pieces of an f32 pair (exact: x == x0 + x1 + x2 for finite normal x), packed:
@@ -298,28 +344,32 @@ struct X6Stage {
     }
   }
 
+  // split row j (4 elements) of staged piece i and write it into the three planes
+  template <bool PROBE = false>
+  __device__ static void stash_row(unsigned char* lds, int t, const floatx4 (&r)[kPer][4], int i,
+                                   int j) {
+    const int p = t + NT * i;
+    if (kPieces % NT != 0 && p >= kPieces) return;
+    int rq, kq;
+    piece_of(p, rq, kq);
+    const x6f2 v01 = KC ? x6f2{r[i][j][0], r[i][j][1]} : x6f2{r[i][0][j], r[i][1][j]};
+    const x6f2 v23 = KC ? x6f2{r[i][j][2], r[i][j][3]} : x6f2{r[i][2][j], r[i][3][j]};
+    uint32_t a0, a1, a2, b0, b1, b2;
+    x6_split2<PROBE>(v01, a0, a1, a2);
+    x6_split2<PROBE>(v23, b0, b1, b2);
+    const int off = x6_off(4 * rq + j, 4 * kq);
+    *reinterpret_cast<uint2*>(lds + off) = uint2{a0, b0};
+    *reinterpret_cast<uint2*>(lds + kPlane + off) = uint2{a1, b1};
+    *reinterpret_cast<uint2*>(lds + 2 * kPlane + off) = uint2{a2, b2};
+  }
+
   // split the staged pieces and write the three planes (plane p at lds + p * kPlane)
   template <bool PROBE = false>
   __device__ static void stash(unsigned char* lds, int t, const floatx4 (&r)[kPer][4]) {
 #pragma unroll
-    for (int i = 0; i < kPer; ++i) {
-      const int p = t + NT * i;
-      if (kPieces % NT != 0 && p >= kPieces) continue;
-      int rq, kq;
-      piece_of(p, rq, kq);
+    for (int i = 0; i < kPer; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {  // row 4 rq + j of the piece
-        const x6f2 v01 = KC ? x6f2{r[i][j][0], r[i][j][1]} : x6f2{r[i][0][j], r[i][1][j]};
-        const x6f2 v23 = KC ? x6f2{r[i][j][2], r[i][j][3]} : x6f2{r[i][2][j], r[i][3][j]};
-        uint32_t a0, a1, a2, b0, b1, b2;
-        x6_split2<PROBE>(v01, a0, a1, a2);
-        x6_split2<PROBE>(v23, b0, b1, b2);
-        const int off = x6_off(4 * rq + j, 4 * kq);
-        *reinterpret_cast<uint2*>(lds + off) = uint2{a0, b0};
-        *reinterpret_cast<uint2*>(lds + kPlane + off) = uint2{a1, b1};
-        *reinterpret_cast<uint2*>(lds + 2 * kPlane + off) = uint2{a2, b2};
-      }
-    }
+      for (int j = 0; j < 4; ++j) stash_row<PROBE>(lds, t, r, i, j);  // row 4 rq + j of the piece
   }
 };
 
@@ -351,15 +401,16 @@ struct X6StagePl {
                                              k0 + 8 * ch);
     }
   }
+  __device__ static void stash_chunk(unsigned char* lds, int t, const u32x4 (&r)[kPer], int i) {
+    const int c = t + NT * i;
+    if (kChunks % NT != 0 && c >= kChunks) return;
+    int plane, row, ch;
+    at(c, plane, row, ch);
+    *reinterpret_cast<u32x4*>(lds + plane * kPlane + x6_chunk_off(row, ch)) = r[i];
+  }
   __device__ static void stash(unsigned char* lds, int t, const u32x4 (&r)[kPer]) {
 #pragma unroll
-    for (int i = 0; i < kPer; ++i) {
-      const int c = t + NT * i;
-      if (kChunks % NT != 0 && c >= kChunks) continue;
-      int plane, row, ch;
-      at(c, plane, row, ch);
-      *reinterpret_cast<u32x4*>(lds + plane * kPlane + x6_chunk_off(row, ch)) = r[i];
-    }
+    for (int i = 0; i < kPer; ++i) stash_chunk(lds, t, r, i);
   }
 };
 
@@ -429,8 +480,9 @@ constexpr int kX6GTbl = 1024;
 // GATH: 0 plain operands; 1 A's rows gathered (k-contiguous A, the unit's K range in one
 // segment); 2 B's K index gathered (row-contiguous B, the tile's N range in one segment; gtbl =
 // kX6GTbl ints of LDS)
+// PIPE: the double-buffered loop (x6p kernels: lds holds two stages)
 template <int FM, int FN, int WGM, int WGN, bool AKC, bool BKC, bool LO, bool PF2, bool BPL = false,
-          int GATH = 0, int WGE = 0>
+          int GATH = 0, int WGE = 0, bool PIPE = false>
 __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int u, X6Place pl_,
                                         int32_t* gtbl = nullptr) {
   constexpr int NT = 64 * WGM * WGN;
@@ -440,15 +492,17 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
   unsigned char* la = lds;
   unsigned char* lb = lds + 3 * SA::kPlane;
   const int per_split = pl_.tiles_m * g.tiles_n;
-  const int s = u / per_split, rem = u - s * per_split;
+  const bool seg = PIPE && pl_.seg_mode >= 0;
+  const int s = seg ? 0 : u / per_split, rem = seg ? pl_.seg_tile : u - s * per_split;
   const int tm = rem / g.tiles_n, tn = rem - tm * g.tiles_n;
   const int m0 = pl_.row0_base + tm * BM, n0 = tn * BN;
   const float* __restrict__ A = g.a;
   const float* __restrict__ B = g.b;
   // split s reduces K steps [kb, kb + nk): an even partition of the K / 32 steps
   const int nall = g.K / kX6BK;
-  const int kb = static_cast<int>(static_cast<int64_t>(s) * nall / g.splits);
-  const int nk = static_cast<int>(static_cast<int64_t>(s + 1) * nall / g.splits) - kb;
+  const int kb = seg ? pl_.seg_kb : static_cast<int>(static_cast<int64_t>(s) * nall / g.splits);
+  const int nk = seg ? pl_.seg_nk
+                     : static_cast<int>(static_cast<int64_t>(s + 1) * nall / g.splits) - kb;
 
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int wm = wv / WGN, wn = wv % WGN;
@@ -532,7 +586,103 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
     }
   };
   floatx4 ra[SA::kPer][4];
-  if constexpr (BPL) {
+  if constexpr (PIPE) {
+    // Two LDS stages, ONE barrier per K step, the fragment reads pipelined across it:
+    //   * step kt's MFMAs for block columns [0, FN - 1) from stage kt % 2, each column followed
+    //     by its share of the split + stash of step kt + 1 (raw tiles loaded during step kt - 1)
+    //     into the other stage -- one basic block, so the split's VALU and LDS writes issue in
+    //     the MFMAs' shadow instead of in a phase of their own between two barriers;
+    //   * the barrier; then step kt + 2's loads (into the registers just stashed: one set,
+    //     clamped to the last step, so no branch), and the LAST column's MFMAs of step kt, each
+    //     A block's MFMAs followed by the read of that block's fragments of step kt + 1 from the
+    //     stage just completed -- so the next step starts on fragments already in registers
+    //     instead of every wave waiting on its reads behind the barrier.
+    // The stash is unconditional (the last step rewrites a stage nobody reads again).
+    // BPL: B arrives pre-split (X6StagePl: its stash is a 16-B copy per chunk, no VALU)
+    static_assert(!LO && GATH == 0 && WGE == 0 && FN >= 2,
+                  "pipelined loop: the plain family, >= 2 block columns per wave");
+    using PB = X6StagePl<BN, NT>;
+    constexpr int kStage = 3 * SA::kPlane + 3 * SB::kPlane;
+    constexpr int kRowsA = 4 * SA::kPer, kRows = kRowsA + (BPL ? PB::kPer : 4 * SB::kPer);
+    floatx4 rb[BPL ? 1 : SB::kPer][4];
+    u32x4 pb[BPL ? PB::kPer : 1];
+    auto loadBB = [&](int k0) {
+      if constexpr (BPL) PB::load(g.bpl, g.bpl_ld, g.bpl_ps, n0, k0, t, pb);
+      else loadB(k0, rb);
+    };
+    // stash unit q of the step held in registers: A rows first, then B rows / plane chunks
+    auto stash_unit = [&](unsigned char* st, int q) {
+      if (q < kRowsA)
+        SA::template stash_row<kProbeA>(st, t, ra, q >> 2, q & 3);
+      else if constexpr (BPL)
+        PB::stash_chunk(st + 3 * SA::kPlane, t, pb, q - kRowsA);
+      else
+        SB::template stash_row<kProbeB>(st + 3 * SA::kPlane, t, rb, (q - kRowsA) >> 2,
+                                        (q - kRowsA) & 3);
+    };
+    constexpr int kSj = FN - 1;  // columns carrying the stash
+    loadA(kb * kX6BK, ra);
+    loadBB(kb * kX6BK);
+#pragma unroll
+    for (int q = 0; q < kRows; ++q) stash_unit(lds, q);
+    loadA((kb + (nk > 1 ? 1 : 0)) * kX6BK, ra);
+    loadBB((kb + (nk > 1 ? 1 : 0)) * kX6BK);
+    __syncthreads();
+    X6_STAMP(g, 1, static_cast<int64_t>(__builtin_readcyclecounter()));
+    auto readA = [&](const unsigned char* st, int i, bf16x8 (&a)[3]) {
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        a[pl] = x6_frag(st + pl * SA::kPlane, wm * 16 * FM + 16 * i + fr, fc);
+    };
+    auto readB = [&](const unsigned char* st, int j, bf16x8 (&b)[3]) {
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        b[pl] = x6_frag(st + 3 * SA::kPlane + pl * SB::kPlane, wn * 16 * FN + 16 * j + fr, fc);
+    };
+    bf16x8 af[FM][3], bf0[3];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) readA(lds, i, af[i]);
+    readB(lds, 0, bf0);
+    auto pstep = [&](int kt, const unsigned char* cur, unsigned char* nxt) {
+#pragma unroll
+      for (int j = 0; j < FN - 1; ++j) {
+        bf16x8 bf[3];
+        if (j == 0) {
+#pragma unroll
+          for (int pl = 0; pl < 3; ++pl) bf[pl] = bf0[pl];
+        } else {
+          readB(cur, j, bf);
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i) x6_mfma6<false>(af[i], bf, hi[i][j], lo[0][0]);
+#ifndef OCPPO_X6P_PROBE_NOSTASH  // probe builds only: the loop without its split and stash
+#pragma unroll
+        for (int q = j * kRows / kSj; q < (j + 1) * kRows / kSj; ++q) stash_unit(nxt, q);
+#endif
+      }
+      bf16x8 bl[3];
+      readB(cur, FN - 1, bl);
+      __syncthreads();
+#ifndef OCPPO_X6P_PROBE_NOLOAD
+      const int kl = kt + 2 < nk ? kt + 2 : nk - 1;
+      loadA((kb + kl) * kX6BK, ra);
+      loadBB((kb + kl) * kX6BK);
+#endif
+      readB(nxt, 0, bf0);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        x6_mfma6<false>(af[i], bl, hi[i][FN - 1], lo[0][0]);
+        readA(nxt, i, af[i]);
+      }
+    };
+    int kt = 0;
+    for (; kt + 1 < nk; kt += 2) {
+      pstep(kt, lds, lds + kStage);
+      pstep(kt + 1, lds + kStage, lds);
+    }
+    if (kt < nk) pstep(kt, lds, lds + kStage);
+    X6_STAMP(g, 2, static_cast<int64_t>(__builtin_readcyclecounter()));
+  } else if constexpr (BPL) {
     // A two K steps ahead (register sets ra / qa, as below), the pre-split B one step ahead:
     // its loads of step kt + 1 are issued before A's of step kt + 2, so the stash of step
     // kt + 1 waits for them without draining A's
@@ -667,6 +817,55 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
     if (kt < nk) step(kt, ra, rb, qa, qb);
   }
 
+  if constexpr (PIPE) {
+    // stream-K: a later part of a split tile hands its accumulators over; the first part takes
+    // them before its epilogue. Slots are [block (i, j)][thread] float4s (coalesced both ways);
+    // the parts of one tile run on one XCD (x6p_streamk), whose L2 holds the slot: the data as
+    // plain stores, drained (vmcnt) before the flag, which is written and polled at agent scope
+    constexpr int kSlot = FM * FN * NT;  // float4 per slot
+    if (seg && pl_.seg_mode == 1) {
+      floatx4* ws = reinterpret_cast<floatx4*>(g.skws) + static_cast<int64_t>(pl_.seg_slot) * kSlot;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) ws[(i * FN + j) * NT + t] = hi[i][j];
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (t == 0) __hip_atomic_store(g.skflag + pl_.seg_slot, 1, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    if (seg && pl_.seg_mode == 2) {
+      // the later parts of this tile are the first segments of the next ranks of this XCD (the
+      // ones whose non-empty ranges start inside it)
+      const X6pGeom G = x6p_geom(g, pl_.seg_slot, gridDim.x);
+      const int64_t tl = rem - G.t0;
+      for (int r = G.rank + 1; r < G.P; ++r) {
+        const int64_t sr = static_cast<int64_t>(r) * G.I / G.P;
+        if (sr >= (tl + 1) * G.nk) break;
+        if (static_cast<int64_t>(r + 1) * G.I / G.P == sr) continue;  // an empty range
+        const int slot = G.xcd + 8 * r;  // that rank's blockIdx
+        if (t == 0) {  // bounded wait: a lost part ends in wrong numbers, never in a hang
+          for (int it = 0; it < (1 << 22); ++it) {
+            if (__hip_atomic_load(g.skflag + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+              break;
+            __builtin_amdgcn_s_sleep(2);
+          }
+        }
+        __syncthreads();
+        const floatx4* ws = reinterpret_cast<const floatx4*>(g.skws) + static_cast<int64_t>(slot) * kSlot;
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            const floatx4 v = ws[(i * FN + j) * NT + t];
+            hi[i][j] += v;
+          }
+        if (t == 0) __hip_atomic_store(g.skflag + slot, 0, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
   // epilogue: MFMA result C[4 fc + r][fr] of block (i, j)
 #ifdef OCPPO_X6_ASMLD
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no inline-asm load left in flight
@@ -828,6 +1027,85 @@ __global__ __launch_bounds__(64 * WGM * WGN, OCPPO_X6_OCC) void gemm_x6_kernel(X
       g, lds, u, X6Place{g.tiles_m, 0, 0, 1, 0}, gtbl);
 }
 
+// The pipelined family (variants 57-60, x6_unit PIPE): two LDS stages per workgroup, so one
+// workgroup per CU (the 8-wave forms: two waves per SIMD, 256 registers each; the 4-wave form:
+// one wave per SIMD, 512 registers)
+template <int FM, int FN, int WGM, int WGN, bool AKC, bool BKC, int OCC, bool BPL = false,
+          bool SK = false>
+__global__ __launch_bounds__(64 * WGM * WGN, OCC) void gemm_x6p_kernel(X6Args g) {
+  __shared__ __attribute__((aligned(16)))
+  unsigned char lds[2 * x6_lds_bytes<FM, FN, WGM, WGN, AKC, BKC>()];
+  X6_STAMP(g, 0, static_cast<int64_t>(__builtin_readcyclecounter()));
+  X6_STAMP(g, 4, static_cast<int64_t>(__builtin_amdgcn_s_memrealtime()));
+  if constexpr (SK) {
+    // stream-K: this workgroup's range of its XCD's K steps, tile segment by tile segment
+    const X6pGeom G = x6p_geom(g, blockIdx.x, gridDim.x);
+    int64_t s = static_cast<int64_t>(G.rank) * G.I / G.P;
+    const int64_t e = static_cast<int64_t>(G.rank + 1) * G.I / G.P;
+    while (s < e) {
+      const int tl = static_cast<int>(s / G.nk), k0 = static_cast<int>(s - static_cast<int64_t>(tl) * G.nk);
+      const int k1 = static_cast<int>(e - s < G.nk - k0 ? k0 + (e - s) : G.nk);
+      X6Place pl{g.tiles_m, 0, 0, 1, 0};
+      pl.seg_mode = k0 > 0 ? 1 : (k1 < G.nk ? 2 : 0);
+      pl.seg_tile = G.t0 + tl;
+      pl.seg_kb = k0;
+      pl.seg_nk = k1 - k0;
+      pl.seg_slot = blockIdx.x;
+      x6_unit<FM, FN, WGM, WGN, AKC, BKC, false, true, BPL, 0, 0, true>(g, lds, 0, pl);
+      s += k1 - k0;
+      __syncthreads();  // the next segment's prologue rewrites the LDS stages
+    }
+  } else {
+    const int u = x6_remap(blockIdx.x, gridDim.x);
+    if (u >= g.units) return;
+    x6_unit<FM, FN, WGM, WGN, AKC, BKC, false, true, BPL, 0, 0, true>(
+        g, lds, u, X6Place{g.tiles_m, 0, 0, 1, 0});
+  }
+#ifdef OCPPO_X6_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  X6_STAMP(g, 3, static_cast<int64_t>(__builtin_readcyclecounter()));
+  X6_STAMP(g, 5, static_cast<int64_t>(__builtin_amdgcn_s_memrealtime()));
+#endif
+}
+
+template <int FM, int FN, int WGM, int WGN, int OCC>
+static void launch_x6p_t(hipStream_t s, bool akc, bool bkc, X6Args& g) {
+  g.tiles_m = g.M / (16 * FM * WGM);
+  g.tiles_n = g.N / (16 * FN * WGN);
+  const dim3 grid(g.units), block(64 * WGM * WGN);
+  if constexpr (OCC == 2 && FM == 4) {  // 57, 58: the stream-K forms
+    if (g.sk) {
+      if (g.bpl)
+        hipLaunchKernelGGL((gemm_x6p_kernel<FM, FN, WGM, WGN, true, true, OCC, true, true>), grid,
+                           block, 0, s, g);
+      else if (akc && bkc)
+        hipLaunchKernelGGL((gemm_x6p_kernel<FM, FN, WGM, WGN, true, true, OCC, false, true>),
+                           grid, block, 0, s, g);
+      else if (akc)
+        hipLaunchKernelGGL((gemm_x6p_kernel<FM, FN, WGM, WGN, true, false, OCC, false, true>),
+                           grid, block, 0, s, g);
+      else if (bkc)
+        hipLaunchKernelGGL((gemm_x6p_kernel<FM, FN, WGM, WGN, false, true, OCC, false, true>),
+                           grid, block, 0, s, g);
+      else
+        hipLaunchKernelGGL((gemm_x6p_kernel<FM, FN, WGM, WGN, false, false, OCC, false, true>),
+                           grid, block, 0, s, g);
+      return;
+    }
+  }
+  if (g.bpl)  // pre-split B (the caller checked akc)
+    hipLaunchKernelGGL((gemm_x6p_kernel<FM, FN, WGM, WGN, true, true, OCC, true>), grid, block, 0,
+                       s, g);
+  else if (akc && bkc)
+    hipLaunchKernelGGL((gemm_x6p_kernel<FM, FN, WGM, WGN, true, true, OCC>), grid, block, 0, s, g);
+  else if (akc)
+    hipLaunchKernelGGL((gemm_x6p_kernel<FM, FN, WGM, WGN, true, false, OCC>), grid, block, 0, s, g);
+  else if (bkc)
+    hipLaunchKernelGGL((gemm_x6p_kernel<FM, FN, WGM, WGN, false, true, OCC>), grid, block, 0, s, g);
+  else
+    hipLaunchKernelGGL((gemm_x6p_kernel<FM, FN, WGM, WGN, false, false, OCC>), grid, block, 0, s, g);
+}
+
 // Mixed tiles: workgroups [0, nbig) take the 128 x 128 tiles of rows [0, mbig) (dispatched
 // first, the longest units), the rest the 64 x 128 tiles of rows [mbig, M) as slots free up;
 // each range keeps its own XCD remap (nbig is a multiple of 8, so XCD b & 7 is the same in both)
@@ -896,11 +1174,21 @@ struct X6Tile {
 };
 constexpr X6Tile kX6Tiles[] = {{4, 4, 2, 2}, {2, 4, 2, 2}, {4, 2, 2, 2}, {2, 2, 2, 2},
                                {4, 2, 2, 4}, {2, 2, 2, 4}, {2, 4, 4, 2}, {2, 2, 4, 2}};
+// the pipelined family, variants 57-60: 256 x 128 and 128 x 256 (8 waves), 128 x 128 (4 waves,
+// one per SIMD), 128 x 128 (8 waves)
+constexpr X6Tile kX6PTiles[] = {{4, 4, 4, 2}, {4, 4, 2, 4}, {4, 4, 2, 2}, {2, 4, 4, 2}};
 
 // variant: shape (bits 0-2) | PF2 (bit 3) | one accumulator (bit 4); instantiated: every shape
 // with PF2 + one accumulator (the product family), shapes 0-3 with one-step loads (+/- LO)
 static bool launch_x6(hipStream_t s, int tile, bool akc, bool bkc, X6Args& g) {
   const int shape = tile & 7;
+  switch (tile) {  // the pipelined family
+    case 57: launch_x6p_t<4, 4, 4, 2, 2>(s, akc, bkc, g); return true;
+    case 58: launch_x6p_t<4, 4, 2, 4, 2>(s, akc, bkc, g); return true;
+    case 59: launch_x6p_t<4, 4, 2, 2, 1>(s, akc, bkc, g); return true;
+    case 60: launch_x6p_t<2, 4, 4, 2, 2>(s, akc, bkc, g); return true;
+    default: break;
+  }
   if (tile & 32) {  // mixed 128 x 128 / 64 x 128 tiles (variant 56 only)
     if (tile != 56) return false;
     g.tiles_n = g.N / 128;
@@ -1061,6 +1349,15 @@ extern "C" int ocppo_split_planes(ocppo_stream_t stream, int n, const float* con
   return check_launch("ocppo_split_planes");
 }
 
+#ifdef OCPPO_X6_STAMPS
+static int64_t* g_x6_stamps = nullptr;
+// probe builds only: the stamps buffer (>= 8 int64 per workgroup) of the following launches
+extern "C" __attribute__((visibility("default"))) int ocppo_x6_probe_set_stamps(int64_t* p) {
+  g_x6_stamps = p;
+  return OCPPO_OK;
+}
+#endif
+
 // A unit's operand window (<= 256 rows x its K range, either layout) addressed by the 32-bit
 // buffer offsets of X6Stage::load_buf
 static bool x6_windows_ok(int64_t sam, int64_t sak, int64_t sbn, int64_t sbk, int64_t K,
@@ -1070,13 +1367,38 @@ static bool x6_windows_ok(int64_t sam, int64_t sak, int64_t sbn, int64_t sbk, in
   return win(sam, sak) < INT32_MAX && (b_planes || win(sbn, sbk) < INT32_MAX);
 }
 
+// Stream-K launches of the pipelined tiles: one workgroup per CU (a multiple of 8: every XCD's
+// share equal), workspace = a partial-accumulator slot + an int flag per workgroup
+static int x6p_sk_grid() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 8)
+      n = 256;
+    cus = n / 8 * 8;
+  }
+  return cus;
+}
+static int64_t x6p_slot_bytes(int tile) {
+  const X6Tile tc = kX6PTiles[tile - 57];
+  return static_cast<int64_t>(tc.fm) * tc.fn * 64 * tc.wgm * tc.wgn * 16;
+}
+
+extern "C" size_t ocppo_gemm_x6_sk_workspace_bytes(int tile) {
+  if (tile != 57 && tile != 58) return 0;
+  const int grid = x6p_sk_grid();
+  return static_cast<size_t>(grid) * x6p_slot_bytes(tile) + static_cast<size_t>(grid) * 4;
+}
+
 extern "C" int ocppo_gemm_x6(ocppo_stream_t stream, const float* a, int64_t sam, int64_t sak,
                              const float* b, int64_t sbn, int64_t sbk, float* c, int64_t ldc,
                              int64_t M, int64_t N, int64_t K, int64_t splits, int64_t split_c,
                              const float* bias, int relu,
                              const float* mask, int64_t ldm, float* dbp, uint64_t* mbits_out,
                              const uint64_t* mbits_in, int tile, int mbig,
-                             const void* b_planes, int64_t bp_ld, int64_t bp_stride) {
+                             const void* b_planes, int64_t bp_ld, int64_t bp_stride,
+                             void* sk_workspace, size_t sk_workspace_bytes) {
   OCPPO_REQUIRE(M >= 1 && N >= 1 && K >= 1 && splits >= 1 && M <= INT32_MAX && N <= INT32_MAX &&
                     K <= INT32_MAX,
                 "ocppo_gemm_x6: bad sizes M=%lld N=%lld K=%lld splits=%lld", (long long)M,
@@ -1092,9 +1414,10 @@ extern "C" int ocppo_gemm_x6(ocppo_stream_t stream, const float* a, int64_t sam,
   OCPPO_REQUIRE(b_planes == nullptr ||
                     (sak == 1 && bp_ld >= K && bp_ld % 8 == 0 && bp_stride >= bp_ld * N &&
                      bp_stride % 8 == 0 && reinterpret_cast<uintptr_t>(b_planes) % 16 == 0 &&
-                     ((tile >= 24 && tile < 28) || tile == 56)),
+                     ((tile >= 24 && tile < 28) || tile == 56 || tile == 57 || tile == 58)),
                 "ocppo_gemm_x6: pre-split B needs a k-contiguous A, 16-B aligned k-contiguous "
-                "planes (ld %lld, stride %lld) and a tile of 24..27 or 56", (long long)bp_ld,
+                "planes (ld %lld, stride %lld) and a tile of 24..27, 56, 57 or 58",
+                (long long)bp_ld,
                 (long long)bp_stride);
   OCPPO_REQUIRE(ldc >= N, "ocppo_gemm_x6: ldc=%lld < N", (long long)ldc);
   OCPPO_REQUIRE(reinterpret_cast<uintptr_t>(a) % 16 == 0 && reinterpret_cast<uintptr_t>(b) % 16 == 0,
@@ -1107,10 +1430,13 @@ extern "C" int ocppo_gemm_x6(ocppo_stream_t stream, const float* a, int64_t sam,
                 "ocppo_gemm_x6: K=%lld must be a multiple of %d with >= 1 step per split",
                 (long long)K, kX6BK);
   OCPPO_REQUIRE(tile >= 0 && tile < 64, "ocppo_gemm_x6: tile=%d", tile);
-  OCPPO_REQUIRE(!(tile & 32) || splits == 1, "ocppo_gemm_x6: mixed tiles need splits == 1");
-  OCPPO_REQUIRE(mbig == -1 || ((tile & 32) && mbig >= 0),
+  const bool pipe = tile >= 57 && tile <= 60;
+  OCPPO_REQUIRE(tile != 56 || splits == 1, "ocppo_gemm_x6: mixed tiles need splits == 1");
+  OCPPO_REQUIRE(!(tile & 32) || tile == 56 || pipe, "ocppo_gemm_x6: tile=%d not built", tile);
+  OCPPO_REQUIRE(mbig == -1 || (tile == 56 && mbig >= 0),
                 "ocppo_gemm_x6: mbig=%d (-1, or a split of the mixed tile)", mbig);
-  const X6Tile tc = kX6Tiles[(tile & 32) ? 1 : (tile & 7)];  // mixed: divisibility of 64 x 128
+  const X6Tile tc = tile >= 57 && tile <= 60 ? kX6PTiles[tile - 57]
+                    : kX6Tiles[(tile & 32) ? 1 : (tile & 7)];  // mixed: divisibility of 64 x 128
   const int64_t bm = 16 * tc.fm * tc.wgm, bn = 16 * tc.fn * tc.wgn;
   OCPPO_REQUIRE(M % bm == 0 && N % bn == 0,
                 "ocppo_gemm_x6: M=%lld, N=%lld must be multiples of the %lld x %lld tile",
@@ -1128,7 +1454,26 @@ extern "C" int ocppo_gemm_x6(ocppo_stream_t stream, const float* a, int64_t sam,
   X6Args g{a, sam, sak, b, sbn, sbk, c, ldc, bias, relu ? 1 : 0, (int)M, (int)N, (int)K,
            0, 0, (int)units, (int)splits, split_c, mask, ldm, dbp, mbits_out, mbits_in, 0,
            static_cast<const uint16_t*>(b_planes), bp_ld, bp_stride};
-  if (tile & 32) {
+#ifdef OCPPO_X6_STAMPS
+  g.stamps = g_x6_stamps;
+#endif
+  if (sk_workspace) {
+    OCPPO_REQUIRE((tile == 57 || tile == 58) && splits == 1 &&
+                      sk_workspace_bytes >= ocppo_gemm_x6_sk_workspace_bytes(tile) &&
+                      reinterpret_cast<uintptr_t>(sk_workspace) % 256 == 0,
+                  "ocppo_gemm_x6: stream-K needs tile 57 or 58, splits == 1 and a 256-B aligned "
+                  "workspace of ocppo_gemm_x6_sk_workspace_bytes (%zu given)", sk_workspace_bytes);
+    const int grid = x6p_sk_grid();
+    const X6Tile tc = kX6PTiles[tile - 57];
+    const int64_t T = (M / (16 * tc.fm * tc.wgm)) * (N / (16 * tc.fn * tc.wgn));
+    OCPPO_REQUIRE(T >= 8, "ocppo_gemm_x6: stream-K needs >= 8 tiles (one range per XCD)");
+    g.sk = 1;
+    g.skws = static_cast<float*>(sk_workspace);
+    g.skflag = reinterpret_cast<int*>(static_cast<char*>(sk_workspace) +
+                                      static_cast<int64_t>(grid) * x6p_slot_bytes(tile));
+    g.units = grid;
+  }
+  if (tile == 56) {
     g.mbig = mbig >= 0 ? mbig : x6_mixed_mbig((int)M, (int)N);
     OCPPO_REQUIRE(g.mbig >= 0 && g.mbig <= M && g.mbig % 128 == 0 && ((g.mbig / 128) * (N / 128)) % 8 == 0,
                   "ocppo_gemm_x6: mixed split at row %d", g.mbig);

@@ -1010,9 +1010,15 @@ def sum_splits(part, out=None, finish=None):
 # the rest in 64 x 128 (mbig chosen in the library, include/ocppo.h); it divides, and counts its
 # dbp rows and mask words, like 64 x 128
 X6_TILES = ((128, 128), (64, 128), (128, 64), (64, 64),
-            (128, 128), (64, 128), (128, 128), (128, 64)) * 7 + ((64, 128),) + ((0, 0),) * 7
-X6_BUILT = tuple(range(4)) + tuple(range(16, 20)) + tuple(range(24, 32)) + (56,)
+            (128, 128), (64, 128), (128, 128), (128, 64)) * 7 + ((64, 128),) + (
+    (256, 128), (128, 256), (128, 128), (128, 128)) + ((0, 0),) * 3
+# workgroup threads of each variant (the ReLU bitmask holds one 64-bit word per thread and tile)
+X6_THREADS = (256,) * 4 + (512,) * 4
+X6_BUILT = tuple(range(4)) + tuple(range(16, 20)) + tuple(range(24, 32)) + (56, 57, 58, 59, 60)
 X6_MIXED = 56
+# the pipelined family (ocppo_gemm.hip gemm_x6p_kernel): two LDS stages, one barrier per K step
+X6_PIPE = (57, 58, 59, 60)
+X6_PIPE_THREADS = {57: 512, 58: 512, 59: 256, 60: 512}
 
 
 X6_AUTO = 24  # the variant family x6_tile picks from (two K steps of loads in flight, one
@@ -1056,18 +1062,35 @@ def _x6_operand_ok(t) -> bool:
             and t.stride(1) == 1 and t.stride(0) % 4 == 0)
 
 
+_SK_WS: dict = {}
+
+
+def x6_sk_workspace(tile: int, device):
+    """The stream-K workspace of a pipelined tile on `device` (zeroed once; every launch leaves
+    its flags at zero again). Shared by the launches of one stream: they run one after another."""
+    key = (tile, str(device))
+    if key not in _SK_WS:
+        n = _lib.LIB.ocppo_gemm_x6_sk_workspace_bytes(tile)
+        if n == 0:
+            raise ValueError(f"gemm_x6: tile {tile} has no stream-K form")
+        _SK_WS[key] = torch.zeros(n, dtype=torch.uint8, device=device)
+    return _SK_WS[key]
+
+
 def x6_mbits_words(M: int, N: int, tile: int) -> int:
     """64-bit words of a gemm_x6 ReLU bitmask over an [M, N] output with `tile`."""
     bm, bn = X6_TILES[tile]
-    return (M // bm) * (N // bn) * (512 if (tile & 7) >= 4 else 256)
+    nt = X6_PIPE_THREADS[tile] if tile in X6_PIPE_THREADS else X6_THREADS[tile & 7]
+    return (M // bm) * (N // bn) * nt
 
 
 def gemm_x6(a, sam, sak, b, sbn, sbk, c, ldc, M, N, K, splits=1, split_c=0, bias=None,
             relu=False, mask=None, dbp=None, tile=None, mbits_out=None, mbits_in=None, mbig=None,
-            b_planes=None):
+            b_planes=None, stream_k=False):
     """Raw ocppo_gemm_x6 call on tensors a, b, c (their data pointers; strides as given).
     mbig: rows in 128 x 128 tiles for the mixed variant (None: the library's choice).
-    b_planes: B pre-split, bf16 [3, N, K] (split_planes of B); b may then be None."""
+    b_planes: B pre-split, bf16 [3, N, K] (split_planes of B); b may then be None.
+    stream_k: a pipelined tile (57 / 58) as a persistent stream-K launch (x6_sk_workspace)."""
     t = x6_tile(M, N, splits, tile)
     if t is None:
         raise ValueError(f"gemm_x6: no tile divides {M} x {N}")
@@ -1075,7 +1098,7 @@ def gemm_x6(a, sam, sak, b, sbn, sbk, c, ldc, M, N, K, splits=1, split_c=0, bias
     if b_planes is not None:
         if (b_planes.dtype != torch.bfloat16 or tuple(b_planes.shape) != (3, N, K)
                 or not b_planes.is_contiguous() or b_planes.device != dev or sak != 1
-                or K % 8 or not (X6_AUTO <= t < X6_AUTO + 4 or t == X6_MIXED)):
+                or K % 8 or not (X6_AUTO <= t < X6_AUTO + 4 or t in (X6_MIXED, 57, 58))):
             raise ValueError("gemm_x6: b_planes must be a contiguous bf16 [3, N, K] on the "
                              "output's device, with a k-contiguous A and a tile of the x6 family")
     if mask is not None:
@@ -1094,7 +1117,9 @@ def gemm_x6(a, sam, sak, b, sbn, sbk, c, ldc, M, N, K, splits=1, split_c=0, bias
             0 if mask is None else mask.stride(0), None if dbp is None else dbp.data_ptr(),
             None if mbits_out is None else mbits_out.data_ptr(),
             None if mbits_in is None else mbits_in.data_ptr(), t, -1 if mbig is None else int(mbig),
-            None if b_planes is None else b_planes.data_ptr(), K, N * K)
+            None if b_planes is None else b_planes.data_ptr(), K, N * K,
+            *((x6_sk_workspace(t, dev).data_ptr(), x6_sk_workspace(t, dev).numel())
+              if stream_k else (None, 0)))
     # timer site name: the product's shape (bench.py's gemm_x6 roofline parses it); the closure
     # keeps the operand tensors alive for the timer's replays
     masked = mask is not None or mbits_in is not None
@@ -1198,13 +1223,13 @@ def dx_x6_ok(g, w) -> bool:
             and g.shape[1] % 32 == 0 and x6_tile(g.shape[0], w.shape[1]) is not None)
 
 
-def dx_x6(g, w, out=None, planes=None):
-    """g W; planes: W^T's pre-split bf16 [3, K, N] (WeightPlanes)."""
+def dx_x6(g, w, out=None, planes=None, tile=None):
+    """g W; planes: W^T's pre-split bf16 [3, K, N] (WeightPlanes); tile: None = x6_tile's."""
     M, N = g.shape
     K = w.shape[1]
     out = torch.empty((M, K), dtype=torch.float32, device=g.device) if out is None else out
     return gemm_x6(g, g.stride(0), 1, w, 1, w.stride(0), out, out.stride(0), M, K, N,
-                   b_planes=planes)
+                   b_planes=planes, tile=tile)
 
 
 _WG_REC = {}

@@ -373,3 +373,106 @@ def time_cpu_baseline(iterations=2, threads=16, **kw) -> dict:
     dt = time.perf_counter() - t0
     return {"env_steps": steps, "seconds": dt, "sps": steps / dt, "threads": threads,
             "updates_per_sec": iterations * lr.E * lr.nmb / dt}
+
+
+class CpuQNetObj(nn.Module):
+    """oc_cleanrl_amd.dqn.QNetworkObj in plain torch (per-frame Linear encoder, Flatten, Linear
+    decoder, Q head; default PyTorch init like the reference's QNetwork, architectures/dqn.py)."""
+
+    def __init__(self, obs_shape, n_actions, enc=(256, 512, 1024, 512), dec=(512,)):
+        super().__init__()
+        layers, d = [], obs_shape[-1]
+        for n in enc:
+            layers += [nn.Linear(d, n), nn.ReLU()]
+            d = n
+        layers.append(nn.Flatten())
+        d *= obs_shape[0]
+        for n in dec:
+            layers += [nn.Linear(d, n), nn.ReLU()]
+            d = n
+        layers.append(nn.Linear(d, n_actions))
+        self.network = nn.Sequential(*layers)
+
+    def forward(self, x):
+        return self.network(x)
+
+
+def time_cpu_dqn(steps=4000, threads=16, num_envs=1, num_features=12, n_actions=6,
+                 buffer_size=100_000, batch_size=32, train_frequency=4,
+                 target_network_frequency=1000, seed=1) -> dict:
+    """The training phase of cleanrl/dqn_atari_oc.py:341-400 on CPU torch, op for op: epsilon-
+    greedy acting with the Q-network (:345-350), the synthetic env + VecNormalize reward, an SB3-
+    style replay (optimize_memory_usage: next obs = the following row, cleanrl_utils/buffers.py),
+    every `train_frequency` steps a batch of 32: target max, TD target, MSE, backward, Adam (:377-
+    392), the target copy every `target_network_frequency` steps (:396-400). The buffer is filled
+    with `batch_size` steps first (untimed): the timed steps are all past learning_starts."""
+    import random
+
+    torch.set_num_threads(threads)
+    torch.manual_seed(seed)
+    random.seed(seed)
+    rng = np.random.default_rng(seed)
+    W, F, N = 4, num_features, num_envs
+    obs_shape = (W, F)
+    q, target = CpuQNetObj(obs_shape, n_actions), CpuQNetObj(obs_shape, n_actions)
+    target.load_state_dict(q.state_dict())
+    opt = torch.optim.Adam(q.parameters(), lr=1e-4)
+    rows = max(buffer_size // N, 1)
+    rb_obs = np.zeros((rows, N) + obs_shape, np.float32)
+    rb_act = np.zeros((rows, N), np.int64)
+    rb_rew = np.zeros((rows, N), np.float32)
+    rb_done = np.zeros((rows, N), np.float32)
+    pos, full = 0, False
+    step_id = 0
+    f, _, _ = O.synth_env_step(seed, step_id, None, N, F, False)
+    stack = np.repeat(f[:, None, :], W, 1)
+    ret, rms = np.zeros(N), (0.0, 1.0, 1e-4)
+    epsilon = 0.05
+
+    def one_step(global_step):
+        nonlocal stack, ret, rms, pos, full, step_id
+        if random.random() < epsilon:
+            actions = rng.integers(0, n_actions, N)
+        else:
+            with torch.no_grad():
+                actions = torch.argmax(q(torch.tensor(stack, dtype=torch.float32)), 1).numpy()
+        frame, r, d = O.synth_env_step(seed, step_id, actions, N, F, False)
+        step_id += 1
+        r, ret, rms = O.vecnorm_reward(r, d, ret, rms)
+        nxt = np.concatenate([stack[:, 1:], frame[:, None]], 1)
+        nxt[d != 0] = frame[d != 0][:, None]
+        rb_obs[pos], rb_act[pos], rb_rew[pos], rb_done[pos] = stack, actions, r, d
+        rb_obs[(pos + 1) % rows] = nxt  # optimize_memory_usage: next obs lives in the next row
+        pos = (pos + 1) % rows
+        full = full or pos == 0
+        stack = nxt
+        if global_step % train_frequency == 0:
+            hi = rows if full else pos
+            b = (rng.integers(1, rows, batch_size) + pos) % rows if full else \
+                rng.integers(0, hi, batch_size)
+            e = rng.integers(0, N, batch_size)
+            o = torch.tensor(rb_obs[b, e])
+            no = torch.tensor(rb_obs[(b + 1) % rows, e])
+            a = torch.tensor(rb_act[b, e]).view(-1, 1)
+            rr = torch.tensor(rb_rew[b, e])
+            dd = torch.tensor(rb_done[b, e])
+            with torch.no_grad():
+                target_max, _ = target(no).max(dim=1)
+                td_target = rr + 0.99 * target_max * (1 - dd)
+            old_val = q(o).gather(1, a).squeeze()
+            loss = nn.functional.mse_loss(td_target, old_val)
+            opt.zero_grad()
+            loss.backward()
+            opt.step()
+        if global_step % target_network_frequency == 0:
+            for tp, qp in zip(target.parameters(), q.parameters()):
+                tp.data.copy_(1.0 * qp.data + 0.0 * tp.data)
+
+    for g in range(1, batch_size + 1):  # fill past one batch (untimed)
+        one_step(g * train_frequency + 1)
+    t0 = time.perf_counter()
+    for g in range(1, steps + 1):
+        one_step(g)
+    dt = time.perf_counter() - t0
+    return {"sps": steps * N / dt, "updates_per_sec": steps / train_frequency / dt,
+            "seconds": dt, "steps": steps, "threads": threads}

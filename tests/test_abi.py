@@ -108,7 +108,7 @@ def test_gemm_x6_mbig_only_for_the_mixed_tile(lib):
     dummy = ctypes.c_void_p(256)
     args = [None, dummy, 64, 1, dummy, 64, 1, dummy, 128, 128, 128, 64, 1, 0, None, 0, None, 0,
             None, None, None]
-    assert lib.LIB.ocppo_gemm_x6(*args, 24, 512, None, 0, 0) == lib.OCPPO_E_INVALID
+    assert lib.LIB.ocppo_gemm_x6(*args, 24, 512, None, 0, 0, None, 0) == lib.OCPPO_E_INVALID
     assert b"mbig" in lib.LIB.ocppo_last_error()
 
 
@@ -117,7 +117,7 @@ def test_gemm_x6_rejects_operand_windows_past_32_bit_offsets(lib):
     that puts one 128-row window past 2 GiB is refused before any launch (validation only)."""
     dummy = ctypes.c_void_p(256)
     ok = [None, dummy, 64, 1, dummy, 64, 1, dummy, 128, 128, 128, 64, 1, 0, None, 0, None, 0,
-          None, None, None, 24, -1, None, 0, 0]
+          None, None, None, 24, -1, None, 0, 0, None, 0]
     big = list(ok)
     big[2] = 1 << 22  # A row stride 4M floats: 256 rows x 16 MB
     assert lib.LIB.ocppo_gemm_x6(*big) == lib.OCPPO_E_INVALID

@@ -382,3 +382,101 @@ def test_dx_with_lower_layer_backward_rejects_bad_sizes():
     with pytest.raises(RuntimeError, match="bad sizes"):
         ops.dx_x6_wgrad(g[:4032], w, mask[:4032], torch.randn(4032, 12, device=DEV),
                         torch.empty(256, 12, device=DEV), db, fin, tile=24)  # M % 128
+
+
+@pytest.mark.parametrize("tile", [57, 58, 59, 60])
+def test_pipelined_tiles_every_epilogue(tile):
+    """The pipelined family (two LDS stages, one barrier per K step): forward with bias + ReLU +
+    bitmask, masked dX from the f32 mask and from the bitmask, plain dX and split-K dW -- each at
+    f32 accuracy against f64, the two masked forms bitwise equal."""
+    g = torch.Generator(device=DEV).manual_seed(tile)
+    M, K0, N, N2 = 1024, 288, 512, 256
+    x = _rand(M, K0, gen=g)
+    w = _rand(N, K0, gen=g, scale=K0 ** -0.5)
+    b = _rand(N, gen=g, scale=0.1)
+    h = torch.empty(M, N, device=DEV)
+    bits = torch.zeros(ops.x6_mbits_words(M, N, tile), dtype=torch.int64, device=DEV)
+    ops.gemm_x6(x, K0, 1, w, K0, 1, h, N, M, N, K0, bias=b, relu=True, tile=tile, mbits_out=bits)
+    pre = x.double() @ w.double().t() + b.double()
+    _check(h, pre.clamp_min(0), x.double().abs() @ w.double().abs().t() + b.double().abs(),
+           torch.relu(x @ w.t() + b))
+    gg = _rand(M, N2, gen=g)
+    w2 = _rand(N2, N, gen=g, scale=N2 ** -0.5)
+    bm = ops.X6_TILES[tile][0]
+    gp_f, dbp_f = torch.empty(M, N, device=DEV), torch.empty(M // bm, N, device=DEV)
+    gp_b, dbp_b = torch.empty(M, N, device=DEV), torch.empty(M // bm, N, device=DEV)
+    ops.gemm_x6(gg, N2, 1, w2, 1, N, gp_f, N, M, N, N2, mask=h, dbp=dbp_f, tile=tile)
+    ops.gemm_x6(gg, N2, 1, w2, 1, N, gp_b, N, M, N, N2, dbp=dbp_b, tile=tile, mbits_in=bits)
+    assert torch.equal(gp_f, gp_b) and torch.equal(dbp_f, dbp_b)
+    ref = (gg.double() @ w2.double()) * (h > 0)
+    _check(gp_f, ref, gg.double().abs() @ w2.double().abs(), (gg @ w2) * (h > 0))
+    torch.testing.assert_close(dbp_f.double().sum(0), ref.sum(0), rtol=1e-5, atol=1e-4)
+    out = torch.empty(M, N, device=DEV)
+    ops.gemm_x6(gg, N2, 1, w2, 1, N, out, N, M, N, N2, tile=tile)
+    _check(out, gg.double() @ w2.double(), gg.double().abs() @ w2.double().abs(), gg @ w2)
+    R, S = 2048, 4  # dW [N, K0] = gd [R, N]^T xd [R, K0]
+    gd, xd = _rand(R, N, gen=g), _rand(R, K0, gen=g)
+    if ops.x6_tile(N, K0, S, tile) is None:
+        return
+    part = torch.empty(S, N, K0, device=DEV)
+    ops.gemm_x6(gd, 1, N, xd, 1, K0, part, K0, N, K0, R, splits=S, split_c=N * K0, tile=tile)
+    nk = R // 32
+    for s in range(S):
+        r0, r1 = 32 * (s * nk // S), 32 * ((s + 1) * nk // S)
+        _check(part[s], gd[r0:r1].double().t() @ xd[r0:r1].double(),
+               gd[r0:r1].double().abs().t() @ xd[r0:r1].double().abs(), gd[r0:r1].t() @ xd[r0:r1])
+
+
+@pytest.mark.parametrize("tile", [57, 58])
+def test_pipelined_presplit_b_is_bitwise_the_f32_b(tile):
+    g = torch.Generator(device=DEV).manual_seed(100 + tile)
+    M, K0, N = 1024, 256, 512
+    x = _rand(M, K0, gen=g)
+    w = _rand(N, K0, gen=g, scale=K0 ** -0.5)
+    b = _rand(N, gen=g, scale=0.1)
+    wp = ops.WeightPlanes(fwd=[w])
+    wp.refresh()
+    h_a, h_b = torch.empty(M, N, device=DEV), torch.empty(M, N, device=DEV)
+    ops.gemm_x6(x, K0, 1, w, K0, 1, h_a, N, M, N, K0, bias=b, relu=True, tile=tile)
+    ops.gemm_x6(x, K0, 1, None, K0, 1, h_b, N, M, N, K0, bias=b, relu=True, tile=tile,
+                b_planes=w._ocppo_planes["fwd"])
+    assert torch.equal(h_a, h_b)
+
+
+@pytest.mark.parametrize("tile", [57, 58])
+@pytest.mark.parametrize("M,N,K", [(2048, 1024, 512), (1280, 768, 1024), (768, 1536, 96)])
+def test_stream_k_products(tile, M, N, K):
+    """The persistent stream-K launch (tiles split over the CUs of one XCD in K, finished by the
+    workgroup holding each tile's first K steps): f32 accuracy against f64 with the bias / ReLU /
+    bitmask epilogue and the masked dX, bitwise repeatable, and the workspace flags back at zero.
+    Shapes: 4 parts per tile, uneven XCD shares, and more workgroups than K steps (empty ranges)."""
+    if ops.x6_tile(M, N, 1, tile) is None:
+        pytest.skip("tile does not divide")
+    g = torch.Generator(device=DEV).manual_seed(M + N + K + tile)
+    x = _rand(M, K, gen=g)
+    w = _rand(N, K, gen=g, scale=K ** -0.5)
+    b = _rand(N, gen=g, scale=0.1)
+    h = torch.empty(M, N, device=DEV)
+    bits = torch.zeros(ops.x6_mbits_words(M, N, tile), dtype=torch.int64, device=DEV)
+    ops.gemm_x6(x, K, 1, w, K, 1, h, N, M, N, K, bias=b, relu=True, tile=tile, mbits_out=bits,
+                stream_k=True)
+    pre = x.double() @ w.double().t() + b.double()
+    _check(h, pre.clamp_min(0), x.double().abs() @ w.double().abs().t() + b.double().abs(),
+           torch.relu(x @ w.t() + b))
+    h2 = torch.empty_like(h)
+    for _ in range(3):
+        ops.gemm_x6(x, K, 1, w, K, 1, h2, N, M, N, K, bias=b, relu=True, tile=tile, stream_k=True)
+        assert torch.equal(h, h2)
+    N2 = 256
+    gg = _rand(M, N2, gen=g)
+    w2 = _rand(N2, N, gen=g, scale=N2 ** -0.5)
+    bm = ops.X6_TILES[tile][0]
+    gp, dbp = torch.empty(M, N, device=DEV), torch.empty(M // bm, N, device=DEV)
+    ops.gemm_x6(gg, N2, 1, w2, 1, N, gp, N, M, N, N2, dbp=dbp, tile=tile, mbits_in=bits,
+                stream_k=True)
+    ref = (gg.double() @ w2.double()) * (h > 0)
+    _check(gp, ref, gg.double().abs() @ w2.double().abs(), (gg @ w2) * (h > 0))
+    torch.cuda.synchronize()
+    # the workspace ends with one int32 flag per workgroup (one per CU): all back at zero
+    cus = torch.cuda.get_device_properties(DEV).multi_processor_count // 8 * 8
+    assert int(ops.x6_sk_workspace(tile, DEV).view(torch.int32)[-cus:].abs().sum()) == 0

@@ -51,6 +51,10 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--only", default=None, help="kind,M,N,K: one shape (profiling)")
     ap.add_argument("--tiles", default=None, help="comma-separated variants (default: all built)")
+    ap.add_argument("--stream-k", action="store_true",
+                    help="fwd / dx on tiles 57 / 58: the persistent stream-K launch")
+    ap.add_argument("--planes", action="store_true",
+                    help="fwd / dx: B as pre-split bf16 planes (ops.WeightPlanes' operand)")
     ap.add_argument("--mbig", type=int, default=None,
                     help="rows in 128 x 128 tiles for the mixed variant (ocppo_gemm_x6's mbig)")
     a = ap.parse_args()
@@ -81,7 +85,9 @@ def main():
             scale = x.double().abs() @ w.double().abs().t()
             tfn = lambda: torch.mm(x, w.t())  # noqa: E731
             out = torch.empty(M, N, device=dev)
-            ofn = lambda t: (lambda: ops.gemm_x6(x, K, 1, w, K, 1, out, N, M, N, K, tile=t))  # noqa: E731
+            pl = ops.split_planes_ref(w).contiguous() if a.planes else None
+            ofn = lambda t: (lambda: ops.gemm_x6(x, K, 1, w, K, 1, out, N, M, N, K, tile=t,  # noqa: E731
+                                                 b_planes=pl, stream_k=a.stream_k and t in (57, 58)))
             shape_ok = lambda t: ops.x6_tile(M, N, 1, t) is not None  # noqa: E731
         elif kind == "dx":
             gg = torch.rand(M, N, device=dev, generator=g) * 2 - 1
@@ -90,7 +96,9 @@ def main():
             scale = gg.double().abs() @ w.double().abs()
             tfn = lambda: torch.mm(gg, w)  # noqa: E731
             out = torch.empty(M, K, device=dev)
-            ofn = lambda t: (lambda: ops.gemm_x6(gg, N, 1, w, 1, K, out, K, M, K, N, tile=t))  # noqa: E731
+            plt = ops.split_planes_ref(w.t().contiguous()).contiguous() if a.planes else None
+            ofn = lambda t: (lambda: ops.gemm_x6(gg, N, 1, w, 1, K, out, K, M, K, N, tile=t,  # noqa: E731
+                                                 b_planes=plt, stream_k=a.stream_k and t in (57, 58)))
             shape_ok = lambda t: ops.x6_tile(M, K, 1, t) is not None  # noqa: E731
         else:
             R = M
