@@ -213,18 +213,22 @@ __device__ __forceinline__ int x6_off(int row, int k) {
   return x6_chunk_off(row, k >> 3) + (k & 4) * 2;
 }
 
-// One operand tile [ROWS][32 k] of one K step: PIECES 4 x 4 (row, k) pieces per thread.
-template <int ROWS, bool KC, int NT>
+// One operand tile [ROWS][32 k] of one K step: PR x 4 (row, k) pieces per thread (PR = 4; a
+// k-contiguous operand may use PR = 1, one 16-B row quad per piece, so that every thread of an
+// 8-wave workgroup stages the same share of a 128- or 256-row tile).
+template <int ROWS, bool KC, int NT, int PR = 4>
 struct X6Stage {
   static_assert(ROWS % 32 == 0, "tile rows must be a multiple of 32");
-  static constexpr int kPieces = ROWS / 4 * 8;
+  static_assert(PR == 4 || (PR == 1 && KC), "row-quad pieces are for a k-contiguous operand");
+  static constexpr int kPR = PR;
+  static constexpr int kPieces = ROWS / PR * 8;
   static constexpr int kPer = (kPieces + NT - 1) / NT;
   static constexpr int kPlane = ROWS * 64;  // bytes per bf16 plane
 
   __device__ static void piece_of(int p, int& rq, int& kq) {
     if constexpr (KC) {  // k quads fastest: 8 lanes read one row's 128 B
       kq = p & 7;
-      rq = p >> 3;
+      rq = p >> 3;  // rows PR rq .. PR rq + PR - 1
     } else {  // 8 row quads x 2 k quads per 16 lanes: 8 lanes read 128 contiguous bytes of a
               // k row (the mapping the swizzle's conflict-free stash writes assume)
       constexpr int kRqBlocks = ROWS / 32;  // blocks of 8 row quads
@@ -247,7 +251,8 @@ struct X6Stage {
       piece_of(p, rq, kq);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float* q = KC ? src + static_cast<int64_t>(row0 + 4 * rq + j) * srow + (k0 + 4 * kq)
+        if (j >= PR) break;
+        const float* q = KC ? src + static_cast<int64_t>(row0 + PR * rq + j) * srow + (k0 + 4 * kq)
                             : src + static_cast<int64_t>(k0 + 4 * kq + j) * sk + (row0 + 4 * rq);
         if constexpr (ASM)  // invisible to the compiler's wait insertion: waited by x6_vmwait
           asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r[i][j]) : "v"(q) : "memory");
@@ -277,7 +282,7 @@ struct X6Stage {
       piece_of(p < kPieces ? p : 0, rq, kq);
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        b.vo[i][j] = static_cast<int32_t>(4 * (KC ? (4 * rq + j) * srow + 4 * kq
+        b.vo[i][j] = static_cast<int32_t>(4 * (KC ? (PR * rq + (j < PR ? j : 0)) * srow + 4 * kq
                                                   : (4 * kq + j) * sk + 4 * rq));
     }
   }
@@ -287,7 +292,7 @@ struct X6Stage {
       const int p = t + NT * i;
       if (kPieces % NT != 0 && p >= kPieces) continue;
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < PR; ++j)
         r[i][j] = __builtin_bit_cast(
             floatx4, __builtin_amdgcn_raw_buffer_load_b128(b.rs, b.vo[i][j], soff, 0));
     }
@@ -357,7 +362,7 @@ struct X6Stage {
     uint32_t a0, a1, a2, b0, b1, b2;
     x6_split2<PROBE>(v01, a0, a1, a2);
     x6_split2<PROBE>(v23, b0, b1, b2);
-    const int off = x6_off(4 * rq + j, 4 * kq);
+    const int off = x6_off((KC ? PR : 4) * rq + j, 4 * kq);
     *reinterpret_cast<uint2*>(lds + off) = uint2{a0, b0};
     *reinterpret_cast<uint2*>(lds + kPlane + off) = uint2{a1, b1};
     *reinterpret_cast<uint2*>(lds + 2 * kPlane + off) = uint2{a2, b2};
@@ -369,7 +374,7 @@ struct X6Stage {
 #pragma unroll
     for (int i = 0; i < kPer; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) stash_row<PROBE>(lds, t, r, i, j);  // row 4 rq + j of the piece
+      for (int j = 0; j < PR; ++j) stash_row<PROBE>(lds, t, r, i, j);  // row PR rq + j
   }
 };
 
@@ -480,6 +485,13 @@ constexpr int kX6GTbl = 1024;
 // GATH: 0 plain operands; 1 A's rows gathered (k-contiguous A, the unit's K range in one
 // segment); 2 B's K index gathered (row-contiguous B, the tile's N range in one segment; gtbl =
 // kX6GTbl ints of LDS)
+// piece rows of the staged operands (4; 1 = row quads, k-contiguous operands only: experiments)
+#ifndef OCPPO_X6P_PR_A
+#define OCPPO_X6P_PR_A 4
+#endif
+#ifndef OCPPO_X6P_PR_B
+#define OCPPO_X6P_PR_B 4
+#endif
 // PIPE: the double-buffered loop (x6p kernels: lds holds two stages)
 template <int FM, int FN, int WGM, int WGN, bool AKC, bool BKC, bool LO, bool PF2, bool BPL = false,
           int GATH = 0, int WGE = 0, bool PIPE = false>
@@ -487,8 +499,10 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
                                         int32_t* gtbl = nullptr) {
   constexpr int NT = 64 * WGM * WGN;
   constexpr int BM = 16 * FM * WGM, BN = 16 * FN * WGN;
-  using SA = X6Stage<BM, AKC, NT>;
-  using SB = X6Stage<BN, BKC, NT>;
+  // (row-quad pieces for the pipelined loop's k-contiguous operands, every thread the same
+  // share, measured slower: 58's dX [4096 x 2048] 47.4 vs 44.7 us, profiles/r05/exp_x6_pipe.txt)
+  using SA = X6Stage<BM, AKC, NT, (PIPE && AKC) ? OCPPO_X6P_PR_A : 4>;
+  using SB = X6Stage<BN, BKC, NT, (PIPE && BKC) ? OCPPO_X6P_PR_B : 4>;
   unsigned char* la = lds;
   unsigned char* lb = lds + 3 * SA::kPlane;
   const int per_split = pl_.tiles_m * g.tiles_n;
@@ -603,7 +617,8 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
                   "pipelined loop: the plain family, >= 2 block columns per wave");
     using PB = X6StagePl<BN, NT>;
     constexpr int kStage = 3 * SA::kPlane + 3 * SB::kPlane;
-    constexpr int kRowsA = 4 * SA::kPer, kRows = kRowsA + (BPL ? PB::kPer : 4 * SB::kPer);
+    constexpr int kRowsA = SA::kPR * SA::kPer,
+                  kRows = kRowsA + (BPL ? PB::kPer : SB::kPR * SB::kPer);
     floatx4 rb[BPL ? 1 : SB::kPer][4];
     u32x4 pb[BPL ? PB::kPer : 1];
     auto loadBB = [&](int k0) {
@@ -613,12 +628,12 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
     // stash unit q of the step held in registers: A rows first, then B rows / plane chunks
     auto stash_unit = [&](unsigned char* st, int q) {
       if (q < kRowsA)
-        SA::template stash_row<kProbeA>(st, t, ra, q >> 2, q & 3);
+        SA::template stash_row<kProbeA>(st, t, ra, q / SA::kPR, q % SA::kPR);
       else if constexpr (BPL)
         PB::stash_chunk(st + 3 * SA::kPlane, t, pb, q - kRowsA);
       else
-        SB::template stash_row<kProbeB>(st + 3 * SA::kPlane, t, rb, (q - kRowsA) >> 2,
-                                        (q - kRowsA) & 3);
+        SB::template stash_row<kProbeB>(st + 3 * SA::kPlane, t, rb, (q - kRowsA) / SB::kPR,
+                                        (q - kRowsA) % SB::kPR);
     };
     constexpr int kSj = FN - 1;  // columns carrying the stash
     loadA(kb * kX6BK, ra);
