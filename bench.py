@@ -128,8 +128,12 @@ def kernel_bytes(tr) -> dict:
         kb["frames_expand"] = M * (8 + 8 * W + 8 * W * E)
         # dh rows in, one row out per distinct frame
         kb["frames_scatter"] = 4 * M * W * E + C * (4 + 4 * E)
-        # ... with the last encoder layer's ReLU backward: its output rows in as the mask
-        kb["frames_scatter_relu"] = 4 * M * W * E + C * (4 + 8 * E)
+        # ... with the last encoder layer's ReLU backward: its mask in (the forward's row-major
+        # bitmask, 1 bit per element, or its f32 output rows), its bias-gradient partials out
+        from oc_cleanrl_amd import frames as _fr
+        mask_b = E // 8 if _fr.SCATTER_MBITS and E % 32 == 0 else 4 * E
+        kb["frames_scatter_relu"] = (4 * M * W * E + C * (4 + 4 * E + mask_b) +
+                                     4 * E * -(-C // 16))
     return kb
 
 

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define OCPPO_ABI_VERSION 22
+#define OCPPO_ABI_VERSION 23
 
 /* status codes */
 #define OCPPO_OK 0
@@ -370,7 +370,7 @@ OCPPO_API int ocppo_bias_act_nchw(ocppo_stream_t stream, const float* y, const f
  * bias-gradient partials, [M / tile rows, N], for ocppo_sum_splits_db; splits == 1, no bias/relu.
  * ReLU bitmask (mbits: (M / tile rows) x (N / tile columns) x threads per workgroup (256, or 512
  * for the 8-wave shapes) 64-bit words): a forward with relu writes, per tile and thread, one word
- * of (output > 0) bits in the MFMA fragment order (mbits_out); the mask
+ * of !(output <= 0) bits in the MFMA fragment order (mbits_out); the mask
  * epilogue of a later dX over the same [M, N] with the same tile reads them (mbits_in, mask may
  * then be NULL) instead of the f32 mask. tile: bits 0-2 the tile shape (0: 128 x 128, 1: 64 x
  * 128, 2: 128 x 64, 3: 64 x 64 with 4 waves; 4-7: 8-wave forms), bit 3 loads two K steps ahead,
@@ -384,11 +384,15 @@ OCPPO_API int ocppo_bias_act_nchw(ocppo_stream_t stream, const float* y, const f
  * B(n, k) at b_planes[p * bp_stride + n * bp_ld + k] (p = 0, 1, 2; ocppo_split_planes wrote them
  * from the f32 B, so the result is bitwise that of the f32 B): staged by copy, no split in the
  * K loop. Needs sak == 1, bp_ld % 8 == 0, 16-B aligned planes, tile 24..27, 56, 57 or 58.
+ * relu | OCPPO_X6_MBITS_ROWS (with relu and mbits_out): mbits_out is row-major instead,
+ * (M x N / 32) 32-bit words, bit n % 32 of word [m][n / 32] = !(C[m, n] <= 0) — for a consumer
+ * that walks the output by rows (ocppo_frames_scatter_relu's mbits).
  * Tiles 57-60 (the pipelined family): 256 x 128, 128 x 256 (8 waves), 128 x 128 (4 waves) and
  * 128 x 128 (8 waves) with two LDS stages and one barrier per K step (the next step's operand
  * split in the MFMAs' shadow); one workgroup per CU.
  * Deterministic (fixed MFMA order, no atomics).
  * ------------------------------------------------------------------------------------------- */
+#define OCPPO_X6_MBITS_ROWS 2
 OCPPO_API int ocppo_gemm_x6(ocppo_stream_t stream, const float* a, int64_t sam, int64_t sak,
                             const float* b, int64_t sbn, int64_t sbk, float* c, int64_t ldc,
                             int64_t M, int64_t N, int64_t K, int64_t splits, int64_t split_c,
@@ -588,13 +592,16 @@ OCPPO_API int ocppo_frames_scatter(ocppo_stream_t stream, const float* dh, int64
  *                                                     NULL: no mask, gp_out = denc)
  *   dbp[g, :] = sum of gp_out rows of chunk g (ocppo_frames_scatter_chunks(C) chunks of 16 frames,
  *               summed later in chunk order by ocppo_sum_splits_db); NULL: not written.
+ * mbits (NULL: none): the mask as the row-major ReLU bitmask ocppo_gemm_x6 wrote for `out`
+ * (relu | OCPPO_X6_MBITS_ROWS, [C][E / 32] words, E % 32 == 0) instead of reading out (then
+ * ignored): 1 bit instead of 4 B per element, the same gp_out.
  * E % 4 == 0, dh / out / gp_out / dbp 16-B aligned. Same per-frame sums as frames_scatter. */
 OCPPO_API int64_t ocppo_frames_scatter_chunks(int64_t C);
 OCPPO_API int ocppo_frames_scatter_relu(ocppo_stream_t stream, const float* dh, int64_t M,
                                         int64_t E, const int32_t* uniq, int64_t C,
                                         const int32_t* inv, int64_t mb, const float* dones,
                                         int64_t T, int64_t N, int64_t W, const float* out,
-                                        float* gp_out, float* dbp);
+                                        const uint32_t* mbits, float* gp_out, float* dbp);
 /* frames_gather + the encoder's first Linear(+ReLU) in one pass (the update's first encoder layer
  * over the distinct frames, architectures/ppo.py:60-84 on b_obs[mb_inds], ppo_atari_oc.py:566) (F <= 16, N1 % 4 == 0,
  * N1 <= 1024): x_out [C, F] = the gathered frames (as frames_gather),

@@ -22,9 +22,10 @@ LIB_PATH = Path(os.environ.get("OCPPO_LIB", PKG / "lib" / "libocppo_hip.so"))
 HEADER = PKG.parent / "include" / "ocppo.h"
 
 # constants mirrored from include/ocppo.h (checked against the header by tests/test_abi.py)
-OCPPO_ABI_VERSION = 22
+OCPPO_ABI_VERSION = 23
 OCPPO_OK, OCPPO_E_INVALID, OCPPO_E_LAUNCH, OCPPO_E_WORKSPACE = 0, 1, 2, 3
 OCPPO_F32, OCPPO_BF16, OCPPO_U8 = 0, 1, 2
+OCPPO_X6_MBITS_ROWS = 2
 STAT_NAMES = ("loss", "pg_loss", "v_loss", "entropy", "old_approx_kl", "approx_kl", "clipfrac",
               "adv_mean", "adv_std")
 OCPPO_NUM_STATS = len(STAT_NAMES)
@@ -107,7 +108,8 @@ SIGNATURES: dict[str, tuple[type, list]] = {
     "ocppo_frames_scatter_chunks": (I64, [I64]),
     "ocppo_frames_gather_linear": (I, [P, P, I, I64, I64, I64, I64, P, I64, P, P, I64, I, P, P]),
     "ocppo_q_head_epsilon_greedy": (I, [P, P, I64, I64, P, P, I64, U64, P, I64, D, D, D, P, P, P]),
-    "ocppo_frames_scatter_relu": (I, [P, P, I64, I64, P, I64, P, I64, P, I64, I64, I64, P, P, P]),
+    "ocppo_frames_scatter_relu": (I, [P, P, I64, I64, P, I64, P, I64, P, I64, I64, I64, P, P, P,
+                                      P]),
     "ocppo_gemm_x6": (I, [P, P, I64, I64, P, I64, I64, P, I64, I64, I64, I64, I64, I64, P, I, P,
                           I64, P, P, P, I, I, P, I64, I64, P, SZ]),
     "ocppo_gemm_x6_sk_workspace_bytes": (SZ, [I]),

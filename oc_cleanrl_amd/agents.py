@@ -320,8 +320,11 @@ class _LinearAct(torch.autograd.Function):
               if x6 and X6_FWD_SPLITK else None)
         if _x6(x.shape[0], wm.shape[0], x.shape[1], x6) and ops.linear_x6_ok(x, wm):
             if relu and box is not None:
-                # the ReLU bitmask for the next layer's fused dX epilogue (box consumer)
-                out, box["mbits"] = ops.linear_x6(x, wm, b, relu, mbits=True, planes=pf)
+                # the ReLU bitmask for the box's consumer: the next layer's fused dX epilogue
+                # (fragment order), or the frame scatter (row-major)
+                out, box["mbits"] = ops.linear_x6(x, wm, b, relu,
+                                                  mbits="rows" if box.get("rows") else True,
+                                                  planes=pf)
             else:
                 out = ops.linear_x6(x, wm, b, relu, planes=pf)
         elif fs is not None and ops._x6_operand_ok(x) and ops._x6_operand_ok(wm) and \
@@ -648,7 +651,9 @@ def _hip_linear_ok(x2, lin: nn.Linear) -> bool:
             (M <= 128 and (K <= 256 or (K <= 2048 and K % 16 == 0))) or M <= 8)
 
 
-def linear_act(x, lin: nn.Linear, relu: bool, chw=None):
+def linear_act(x, lin: nn.Linear, relu: bool, chw=None, rows: bool = False):
+    """rows: the output's consumer walks it by rows (the frame scatter, frames.SCATTER_MBITS):
+    its ReLU bitmask, if the forward writes one, in the row-major layout."""
     lead = x.shape[:-1]
     x2 = x.reshape(-1, x.shape[-1])
     if chw is None and _hip_linear_ok(x2, lin):
@@ -657,7 +662,7 @@ def linear_act(x, lin: nn.Linear, relu: bool, chw=None):
     box = None
     if relu and FUSED_HEADS_BWD and torch.is_grad_enabled() and _direct(lin.weight) and \
             _direct(lin.bias):
-        box = {"premasked": False, "bias": lin.bias}
+        box = {"premasked": False, "bias": lin.bias, "rows": rows}
     y = _LinearAct.apply(x2, lin.weight, lin.bias, relu, box, chw,
                          getattr(x, "_ocppo_box", None), getattr(x, "_ocppo_wslot", None))
     y = y.view(*lead, y.shape[-1])
@@ -707,8 +712,8 @@ def linear_act_nhwc(x, lin: nn.Linear, relu: bool):
     return linear_act(x.permute(0, 2, 3, 1).reshape(B, H * W * C), lin, relu, (C, H, W))
 
 
-def linear_relu(x, lin: nn.Linear):
-    return linear_act(x, lin, True)
+def linear_relu(x, lin: nn.Linear, rows: bool = False):
+    return linear_act(x, lin, True, rows=rows)
 
 
 # The first two Linear->ReLU layers of a rollout-sized inference batch as ONE HIP launch
@@ -733,10 +738,11 @@ def linear2_relu(x, l1: nn.Linear, l2: nn.Linear):
     return y.view(*lead, y.shape[-1])
 
 
-def fused_trunk(seq: nn.Sequential, x):
+def fused_trunk(seq: nn.Sequential, x, rows_last: bool = False):
     """Run `seq` with every Linear→ReLU pair as one fused GEMM (same math, fewer launches) and
     every other biased Linear through the same path (so FlatAdam-owned grads are written in place,
-    never accumulated). Used on GPU tensors; module structure and state-dict keys are untouched."""
+    never accumulated). Used on GPU tensors; module structure and state-dict keys are untouched.
+    rows_last: the last Linear→ReLU's output goes to the frame scatter (its bitmask row-major)."""
     mods = list(seq)
     i = 0
     while i < len(mods):
@@ -768,7 +774,7 @@ def fused_trunk(seq: nn.Sequential, x):
             x = linear_act_nhwc(x, mods[i + 1], relu)
             i += 3 if relu else 2
         elif fusable and i + 1 < len(mods) and isinstance(mods[i + 1], nn.ReLU):
-            x = linear_relu(x, m)
+            x = linear_relu(x, m, rows=rows_last and i + 2 == len(mods))
             i += 2
         elif fusable:
             x = linear_act(x, m, False)

@@ -252,25 +252,38 @@ __global__ __launch_bounds__(128) void frames_scatter_kernel(
 // relu_bias_grad would do next -- and the per-workgroup column sums of gp (the layer's
 // bias-gradient partials, dbp [chunks, E], summed in chunk order by ocppo_sum_splits_db).
 // Workgroup = kScatterFrames frames: their uses are resolved in parallel (one thread per
-// (frame, candidate sample)), compacted per frame in (t, k) order, and the data pass keeps two
-// frames in flight per thread pair with the first two uses of every frame loaded before any is
-// summed (almost every frame has one or two uses; further ones are added in order afterwards).
-constexpr int kScatterFrames = 16;
+// (frame, candidate sample)), compacted per frame in (t, k) order into LDS sized for this W, and
+// the data pass runs thread = (frame group h of kScatterGroups, float4 column group): the first
+// two uses + the mask of the group's frames loaded before any is summed (almost every frame has
+// one or two uses; further ones are added in order afterwards). Few registers and little LDS per
+// workgroup: the use-resolution chain (uniq -> inv -> dones) of some workgroups overlaps the data
+// pass of others on the same CU. MK: 0 no mask, 1 the f32 output, 2 its row-major bitmask.
+#ifndef OCPPO_SCATTER_F  // experiments (tools/build_variant.py)
+#define OCPPO_SCATTER_F 16
+#endif
+#ifndef OCPPO_SCATTER_G
+#define OCPPO_SCATTER_G 4
+#endif
+constexpr int kScatterFrames = OCPPO_SCATTER_F;
+constexpr int kScatterGroups = OCPPO_SCATTER_G;
+static_assert(kScatterFrames % kScatterGroups == 0 && 256 % kScatterGroups == 0, "scatter shape");
 
+template <int MK>
 __global__ __launch_bounds__(256) void frames_scatter_relu_kernel(
     const float* __restrict__ dh, int64_t M, int64_t E, const int32_t* __restrict__ uniq,
     int64_t C, const int32_t* __restrict__ inv, int64_t mb, const float* __restrict__ dones,
-    int64_t T, int64_t N, int W, const float* __restrict__ out, float* __restrict__ gp,
-    float* __restrict__ dbp) {
-  constexpr int F = kScatterFrames;
-  __shared__ int32_t uses[F][kFramesMaxW * kFramesMaxW];
-  __shared__ int32_t list[F][kFramesMaxW * kFramesMaxW];
+    int64_t T, int64_t N, int W, const float* __restrict__ out,
+    const uint32_t* __restrict__ mbits, float* __restrict__ gp, float* __restrict__ dbp) {
+  constexpr int F = kScatterFrames, G = kScatterGroups, FG = F / G, QG = 256 / G;
+  extern __shared__ int32_t scatter_lds[];  // uses [F][WW], list [F][WW]
   __shared__ int cnt[F];
-  __shared__ float4 half1[128];
+  __shared__ float4 red[G - 1][QG];
   const int WW = W * W;
+  int32_t* uses = scatter_lds;
+  int32_t* list = scatter_lds + F * WW;
   const int tid = threadIdx.x;
   const int64_t c0 = static_cast<int64_t>(blockIdx.x) * F;
-  for (int q = tid; q < F * WW; q += blockDim.x) uses[q / WW][q % WW] = -1;
+  for (int q = tid; q < F * WW; q += blockDim.x) uses[q] = -1;
   __syncthreads();
   if (tid < F * W) {  // (frame j, candidate sample t = s + i)
     const int j = tid / W, i = tid - j * W;
@@ -288,7 +301,7 @@ __global__ __launch_bounds__(256) void frames_scatter_relu_kernel(
           for (int k = 0; k < W; ++k) {
             int sk = t - (W - 1) + k;
             sk = sk > r ? sk : r;
-            if (sk == s) uses[j][i * W + k] = row * W + k;
+            if (sk == s) uses[j * WW + i * W + k] = row * W + k;
           }
         }
       }
@@ -298,59 +311,72 @@ __global__ __launch_bounds__(256) void frames_scatter_relu_kernel(
   if (tid < F) {  // compact each frame's uses, keeping the (t ascending, k ascending) order
     int m = 0;
     for (int q = 0; q < WW; ++q)
-      if (uses[tid][q] >= 0) list[tid][m++] = uses[tid][q];
+      if (uses[tid * WW + q] >= 0) list[tid * WW + m++] = uses[tid * WW + q];
     cnt[tid] = m;
   }
   __syncthreads();
-  // data pass: thread = (frame parity h, float4 column group q); frames j = 2 p + h
-  const int h = tid >> 7, qg = tid & 127;
-  float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);
+  // data pass: thread = (frame group h, float4 column group qg); frames j = G p + h
+  const int h = tid / QG, qg = tid % QG;
+  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
   // block-uniform trip count (the barriers below are reached by every thread); lanes past E
   // load and store nothing
-  for (int64_t e0 = 0; e0 < E; e0 += 128 * 4) {
+  for (int64_t e0 = 0; e0 < E; e0 += QG * 4) {
     const int64_t e = e0 + static_cast<int64_t>(qg) * 4;
     const bool live = e < E;
-    float4 v0[F / 2], v1[F / 2], mk[F / 2];
+    float4 v0[FG], v1[FG], mk[FG];
+    uint32_t mb4[FG];  // the row-major bitmask's 4 bits of (frame, e .. e + 3)
 #pragma unroll
-    for (int p = 0; p < F / 2; ++p) {  // first two uses + the mask of every frame, in flight
-      const int j = 2 * p + h;
+    for (int p = 0; p < FG; ++p) {  // first two uses + the mask of every frame, in flight
+      const int j = G * p + h;
       const int n = live ? cnt[j] : 0;
-      const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-      v0[p] = n > 0 ? *reinterpret_cast<const float4*>(dh + static_cast<int64_t>(list[j][0]) * E + e) : z;
-      v1[p] = n > 1 ? *reinterpret_cast<const float4*>(dh + static_cast<int64_t>(list[j][1]) * E + e) : z;
-      mk[p] = (live && out && c0 + j < C)
-                  ? *reinterpret_cast<const float4*>(out + (c0 + j) * E + e)
-                  : make_float4(1.f, 1.f, 1.f, 1.f);
+      v0[p] = n > 0 ? *reinterpret_cast<const float4*>(dh + static_cast<int64_t>(list[j * WW]) * E + e) : z;
+      v1[p] = n > 1 ? *reinterpret_cast<const float4*>(dh + static_cast<int64_t>(list[j * WW + 1]) * E + e) : z;
+      const bool mrow = live && c0 + j < C;
+      if constexpr (MK == 2)
+        mb4[p] = mrow ? (mbits[(c0 + j) * (E >> 5) + (e >> 5)] >> (e & 31)) & 0xfu : 0xfu;
+      if constexpr (MK == 1)
+        mk[p] = mrow ? *reinterpret_cast<const float4*>(out + (c0 + j) * E + e)
+                     : make_float4(1.f, 1.f, 1.f, 1.f);
     }
+    float4 cs = z;
 #pragma unroll
-    for (int p = 0; p < F / 2; ++p) {
-      const int j = 2 * p + h;
+    for (int p = 0; p < FG; ++p) {
+      const int j = G * p + h;
       const int64_t c = c0 + j;
       if (c >= C || !live) continue;
       const int n = cnt[j];
-      float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+      float4 a = z;
       if (n > 0) { a.x += v0[p].x; a.y += v0[p].y; a.z += v0[p].z; a.w += v0[p].w; }
       if (n > 1) { a.x += v1[p].x; a.y += v1[p].y; a.z += v1[p].z; a.w += v1[p].w; }
       for (int m = 2; m < n; ++m) {
-        const float4 x = *reinterpret_cast<const float4*>(dh + static_cast<int64_t>(list[j][m]) * E + e);
+        const float4 x = *reinterpret_cast<const float4*>(dh + static_cast<int64_t>(list[j * WW + m]) * E + e);
         a.x += x.x; a.y += x.y; a.z += x.z; a.w += x.w;
       }
-      a.x = mk[p].x <= 0.f ? 0.f : a.x; a.y = mk[p].y <= 0.f ? 0.f : a.y;
-      a.z = mk[p].z <= 0.f ? 0.f : a.z; a.w = mk[p].w <= 0.f ? 0.f : a.w;
+      if constexpr (MK == 1) {
+        a.x = mk[p].x <= 0.f ? 0.f : a.x; a.y = mk[p].y <= 0.f ? 0.f : a.y;
+        a.z = mk[p].z <= 0.f ? 0.f : a.z; a.w = mk[p].w <= 0.f ? 0.f : a.w;
+      }
+      if constexpr (MK == 2) {
+        const uint32_t m4 = mb4[p];
+        a.x = (m4 & 1u) ? a.x : 0.f; a.y = (m4 & 2u) ? a.y : 0.f;
+        a.z = (m4 & 4u) ? a.z : 0.f; a.w = (m4 & 8u) ? a.w : 0.f;
+      }
       *reinterpret_cast<float4*>(gp + c * E + e) = a;
       cs.x += a.x; cs.y += a.y; cs.z += a.z; cs.w += a.w;
     }
-    if (dbp) {  // the two frame parities of this column group, in h order
-      if (h == 1) half1[qg] = cs;
+    if (dbp) {  // the frame groups of this column group, added in h order
+      if (h > 0) red[h - 1][qg] = cs;
       __syncthreads();
       if (h == 0 && live) {
-        const float4 o = half1[qg];
-        *reinterpret_cast<float4*>(dbp + static_cast<int64_t>(blockIdx.x) * E + e) =
-            make_float4(cs.x + o.x, cs.y + o.y, cs.z + o.z, cs.w + o.w);
+#pragma unroll
+        for (int q = 0; q < G - 1; ++q) {
+          const float4 o = red[q][qg];
+          cs.x += o.x; cs.y += o.y; cs.z += o.z; cs.w += o.w;
+        }
+        *reinterpret_cast<float4*>(dbp + static_cast<int64_t>(blockIdx.x) * E + e) = cs;
       }
       __syncthreads();
     }
-    cs = make_float4(0.f, 0.f, 0.f, 0.f);
   }
 }
 
@@ -533,7 +559,9 @@ extern "C" int ocppo_frames_scatter_relu(ocppo_stream_t stream, const float* dh,
                                          int64_t E, const int32_t* uniq, int64_t C,
                                          const int32_t* inv, int64_t mb, const float* dones,
                                          int64_t T, int64_t N, int64_t W, const float* out,
-                                         float* gp_out, float* dbp) {
+                                         const uint32_t* mbits, float* gp_out, float* dbp) {
+  OCPPO_REQUIRE(!mbits || E % 32 == 0,
+                "ocppo_frames_scatter_relu: the row-major bitmask needs E %% 32 == 0");
   OCPPO_REQUIRE(M >= 1 && E >= 4 && E % 4 == 0 && C >= 0 && mb >= 0 && T >= 1 && N >= 1 &&
                     W >= 1 && W <= kFramesMaxW && (T + W - 1) * N < INT32_MAX &&
                     T * N < INT32_MAX && M * W < INT32_MAX,
@@ -546,9 +574,18 @@ extern "C" int ocppo_frames_scatter_relu(ocppo_stream_t stream, const float* dh,
   clear_stale_error();
   const int64_t g = ocppo_frames_scatter_chunks(C);
   OCPPO_REQUIRE(g <= INT32_MAX, "ocppo_frames_scatter_relu: too large");
-  hipLaunchKernelGGL(frames_scatter_relu_kernel, dim3(static_cast<unsigned>(g)), dim3(256), 0,
-                     as_stream(stream), dh, M, E, uniq, C, inv, mb, dones, T, N, (int)W, out,
-                     gp_out, dbp);
+  const size_t lds = 2 * sizeof(int32_t) * kScatterFrames * W * W;
+  const dim3 grid(static_cast<unsigned>(g)), block(256);
+  hipStream_t s = as_stream(stream);
+  if (mbits)
+    hipLaunchKernelGGL(frames_scatter_relu_kernel<2>, grid, block, lds, s, dh, M, E, uniq, C, inv,
+                       mb, dones, T, N, (int)W, out, mbits, gp_out, dbp);
+  else if (out)
+    hipLaunchKernelGGL(frames_scatter_relu_kernel<1>, grid, block, lds, s, dh, M, E, uniq, C, inv,
+                       mb, dones, T, N, (int)W, out, mbits, gp_out, dbp);
+  else
+    hipLaunchKernelGGL(frames_scatter_relu_kernel<0>, grid, block, lds, s, dh, M, E, uniq, C, inv,
+                       mb, dones, T, N, (int)W, out, mbits, gp_out, dbp);
   return check_launch("ocppo_frames_scatter_relu");
 }
 

@@ -107,6 +107,10 @@ struct X6Args {
   int sk;
   float* skws;
   int* skflag;
+  // mbits_out in the row-major layout instead (ocppo_gemm_x6's relu & OCPPO_X6_MBITS_ROWS): bit
+  // n % 32 of 32-bit word [m][n / 32] is !(C[m, n] <= 0), for a consumer that walks the output
+  // by rows (the frame scatter of the encoder's last ReLU backward, ocppo_frames_scatter_relu)
+  int mbits_rows;
 };
 
 // Stream-K geometry of an x6p persistent launch: the tiles (row-major) are dealt to the 8 XCDs in
@@ -1023,11 +1027,43 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
         if (g.bias) v += bv;
         if (g.relu) v = relu_f(v);
         Cp[row * g.ldc + col] = v;
-        bits |= static_cast<uint64_t>(v > 0.f) << ((i * FN + j) * 4 + r);
+        bits |= static_cast<uint64_t>(!(v <= 0.f)) << ((i * FN + j) * 4 + r);
       }
     }
   }
-  if (g.mbits_out) g.mbits_out[tile_id * NT + t] = bits;
+  if (!g.mbits_out) return;
+  if (!g.mbits_rows) {
+    g.mbits_out[tile_id * NT + t] = bits;
+    return;
+  }
+  if constexpr (FN % 2 == 0) {
+    // row-major words: the ballot of fragment (i, j, r) holds, for lane group fc, the 16 columns
+    // 16 j + [0, 16) of row 16 i + 4 fc + r; word (row, p) = columns 32 p + [0, 32) of the wave's
+    // 16 FM rows x 16 FN columns, assembled by the lane that stores it
+    constexpr int WPR = FN / 2, WORDS = 16 * FM * WPR;
+    uint32_t* rows = reinterpret_cast<uint32_t*>(g.mbits_out);
+    const int64_t ldw = g.N / 32;
+#pragma unroll
+    for (int q = 0; q < (WORDS + 63) / 64; ++q) {
+      const int w = lane + 64 * q;
+      const int wrow = w / WPR, p = w - wrow * WPR;
+      const int li = wrow >> 4, lfc = (wrow >> 2) & 3, lr = wrow & 3;
+      uint32_t word = 0;
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const uint64_t bal = __ballot((bits >> ((i * FN + j) * 4 + r)) & 1);
+            const uint32_t half = static_cast<uint32_t>(bal >> (16 * lfc)) & 0xffffu;
+            if (li == i && lr == r && p == (j >> 1)) word |= half << (16 * (j & 1));
+          }
+        }
+      }
+      if (w < WORDS) rows[(wr0 + wrow) * ldw + (wc0 >> 5) + p] = word;
+    }
+  }
 }
 
 template <int FM, int FN, int WGM, int WGN, bool AKC, bool BKC, bool LO, bool PF2, bool BPL = false,
@@ -1466,9 +1502,12 @@ extern "C" int ocppo_gemm_x6(ocppo_stream_t stream, const float* a, int64_t sam,
                 "ocppo_gemm_x6: mbits_out needs splits == 1 and no mask epilogue");
   const int64_t units = splits * (M / bm) * (N / bn);
   OCPPO_REQUIRE(units <= INT32_MAX / 2, "ocppo_gemm_x6: too large");
-  X6Args g{a, sam, sak, b, sbn, sbk, c, ldc, bias, relu ? 1 : 0, (int)M, (int)N, (int)K,
+  OCPPO_REQUIRE(!(relu & OCPPO_X6_MBITS_ROWS) || ((relu & 1) && mbits_out != nullptr),
+                "ocppo_gemm_x6: the row-major bitmask needs the ReLU epilogue and mbits_out");
+  X6Args g{a, sam, sak, b, sbn, sbk, c, ldc, bias, relu & 1, (int)M, (int)N, (int)K,
            0, 0, (int)units, (int)splits, split_c, mask, ldm, dbp, mbits_out, mbits_in, 0,
            static_cast<const uint16_t*>(b_planes), bp_ld, bp_stride};
+  g.mbits_rows = (relu & OCPPO_X6_MBITS_ROWS) ? 1 : 0;
 #ifdef OCPPO_X6_STAMPS
   g.stamps = g_x6_stamps;
 #endif

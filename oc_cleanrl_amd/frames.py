@@ -114,6 +114,15 @@ class FramePlanner:
 # The encoder's last ReLU backward (and its bias-gradient partials) inside the frame scatter
 # (ops.frames_scatter_relu) when enc is the ReLU output of an in-place-grad Linear (its box).
 FUSED_SCATTER_RELU = True
+# ... reading that layer's ReLU mask as the row-major bitmask its forward GEMM wrote
+# (ops.linear_x6(..., mbits="rows")): 1 bit instead of the 4-B output element per (frame, column)
+SCATTER_MBITS = True
+
+
+def _rows_bits(box):
+    """The row-major ReLU bitmask in an encoder box, else None (the scatter reads the output)."""
+    mb = box.get("mbits") if box is not None else None
+    return mb[0] if mb is not None and mb[1] == "rows" else None
 
 
 class _FramesExpand(torch.autograd.Function):
@@ -145,7 +154,7 @@ class _FramesExpand(torch.autograd.Function):
             uniq, inv, dones, enc = ctx.saved_tensors
             box = ctx.box
             gp, part = ops.timed("frames_scatter_relu", lambda: ops.frames_scatter_relu(
-                dh, uniq, inv, mb, dones, T, N, W, out=enc))
+                dh, uniq, inv, mb, dones, T, N, W, out=enc, mbits=_rows_bits(box)))
             box["dbp"] = part
             return gp, None, None, None, None, None, None, None, None, None, None
         uniq, inv, dones = ctx.saved_tensors
@@ -214,7 +223,7 @@ class _DecodeFrames(torch.autograd.Function):
         dh = agents._dx(gp, w, True, ctx.pdx).view(M, W, -1)
         if ctx.enc_box is not None:
             denc, part = ops.timed("frames_scatter_relu", lambda: ops.frames_scatter_relu(
-                dh, uniq, inv, mb, dones, T, N, W, out=enc))
+                dh, uniq, inv, mb, dones, T, N, W, out=enc, mbits=_rows_bits(ctx.enc_box)))
             ctx.enc_box["dbp"] = part
         else:
             denc = ops.timed("frames_scatter", lambda: ops.frames_scatter(dh, uniq, inv, mb, dones,
@@ -377,10 +386,10 @@ def minibatch_hidden(agent, obs, dones, uniq, pos_of, inv, perm, mb: int, split:
         if split:
             low = fused_trunk(agent.network[2:split], h1)
             low_d = low.detach().requires_grad_()
-            enc = fused_trunk(agent.network[split:agent._flat], low_d)
+            enc = fused_trunk(agent.network[split:agent._flat], low_d, rows_last=SCATTER_MBITS)
             cut = (low, low_d)
         else:
-            enc = fused_trunk(agent.network[2:agent._flat], h1)
+            enc = fused_trunk(agent.network[2:agent._flat], h1, rows_last=SCATTER_MBITS)
         if _decode_gather_ok(agent, enc, perm.numel(), W):
             hidden = _decode_frames(agent, enc, pos_of, perm, dones, uniq, inv, mb, T, N, W)
             return (hidden, cut) if split else hidden

@@ -1086,7 +1086,7 @@ def x6_mbits_words(M: int, N: int, tile: int) -> int:
 
 def gemm_x6(a, sam, sak, b, sbn, sbk, c, ldc, M, N, K, splits=1, split_c=0, bias=None,
             relu=False, mask=None, dbp=None, tile=None, mbits_out=None, mbits_in=None, mbig=None,
-            b_planes=None, stream_k=False):
+            b_planes=None, stream_k=False, mbits_rows=False):
     """Raw ocppo_gemm_x6 call on tensors a, b, c (their data pointers; strides as given).
     mbig: rows in 128 x 128 tiles for the mixed variant (None: the library's choice).
     b_planes: B pre-split, bf16 [3, N, K] (split_planes of B); b may then be None.
@@ -1107,13 +1107,18 @@ def gemm_x6(a, sam, sak, b, sbn, sbk, c, ldc, M, N, K, splits=1, split_c=0, bias
             raise ValueError("gemm_x6: mask must be an f32 [M, N] row-major view, with dbp")
     if mask is not None or mbits_in is not None:
         _check(dbp, "dbp", torch.float32, dev, (M // X6_TILES[t][0]) * N)
-    for mb in (mbits_out, mbits_in):
+    if mbits_rows:
+        if not relu or mbits_out is None:
+            raise ValueError("gemm_x6: the row-major bitmask needs relu and mbits_out")
+        _check(mbits_out, "mbits", torch.int32, dev, M * N // 32)
+    for mb in ((mbits_in,) if mbits_rows else (mbits_out, mbits_in)):
         if mb is not None:
             _check(mb, "mbits", torch.int64, dev, x6_mbits_words(M, N, t))
     bp = None if bias is None else _check(bias, "bias", torch.float32, dev, N)
     args = (a.data_ptr(), sam, sak, None if b is None else b.data_ptr(), sbn, sbk, c.data_ptr(),
             ldc, M, N, K, splits,
-            split_c, bp, int(bool(relu)), None if mask is None else mask.data_ptr(),
+            split_c, bp, int(bool(relu)) | (_lib.OCPPO_X6_MBITS_ROWS if mbits_rows else 0),
+            None if mask is None else mask.data_ptr(),
             0 if mask is None else mask.stride(0), None if dbp is None else dbp.data_ptr(),
             None if mbits_out is None else mbits_out.data_ptr(),
             None if mbits_in is None else mbits_in.data_ptr(), t, -1 if mbig is None else int(mbig),
@@ -1138,14 +1143,22 @@ def linear_x6_ok(x, w) -> bool:
 
 def linear_x6(x, w, b=None, relu=False, out=None, mbits=False, planes=None):
     """act(x W^T + b) (torch._addmm_activation's order: sum, + bias, then ReLU). mbits=True
-    (with relu) also returns the output's ReLU bitmask (tensor, tile) for dx_x6_relu. planes:
-    W's pre-split bf16 [3, N, K] (WeightPlanes; bitwise the same result)."""
+    (with relu) also returns the output's ReLU bitmask (tensor, tile) for dx_x6_relu; mbits="rows"
+    the row-major one (int32 [M, N / 32] words, "rows") for frames_scatter_relu. planes: W's
+    pre-split bf16 [3, N, K] (WeightPlanes; bitwise the same result)."""
     M, K = x.shape
     N = w.shape[0]
     out = torch.empty((M, N), dtype=torch.float32, device=x.device) if out is None else out
     if not mbits:
         return gemm_x6(x, x.stride(0), 1, w, w.stride(0), 1, out, out.stride(0), M, N, K, bias=b,
                        relu=relu, b_planes=planes)
+    if mbits == "rows":
+        if not relu or N % 32:
+            raise ValueError("linear_x6: the row-major bitmask needs relu and N % 32 == 0")
+        bits = torch.empty((M, N // 32), dtype=torch.int32, device=x.device)
+        gemm_x6(x, x.stride(0), 1, w, w.stride(0), 1, out, out.stride(0), M, N, K, bias=b,
+                relu=relu, mbits_out=bits, mbits_rows=True, b_planes=planes)
+        return out, (bits, "rows")
     t = x6_tile(M, N)
     bits = torch.empty(x6_mbits_words(M, N, t), dtype=torch.int64, device=x.device)
     gemm_x6(x, x.stride(0), 1, w, w.stride(0), 1, out, out.stride(0), M, N, K, bias=b,
@@ -1476,9 +1489,10 @@ _SCATTER_DBP: dict = {}
 
 
 def frames_scatter_relu(dh, uniq, inv, mb: int, dones, T: int, N: int, W: int, out=None,
-                        gp=None, with_db: bool = True):
+                        gp=None, with_db: bool = True, mbits=None):
     """frames_scatter with the ReLU backward of the layer whose output `out` [C, E] encoded the
-    frames: gp = out <= 0 ? 0 : denc (ocppo_frames_scatter_relu). Returns (gp, (partials,
+    frames: gp = out <= 0 ? 0 : denc (ocppo_frames_scatter_relu). mbits: that output's row-major
+    ReLU bitmask (linear_x6(..., mbits="rows")), read instead of `out`. Returns (gp, (partials,
     chunks)): the bias-gradient chunk sums (16 frames per chunk; a per-shape persistent buffer,
     graph-safe) for sum_splits_db, or (gp, None) without with_db."""
     M = dh.shape[0]
@@ -1500,7 +1514,8 @@ def frames_scatter_relu(dh, uniq, inv, mb: int, dones, T: int, N: int, W: int, o
     call("ocppo_frames_scatter_relu", _stream(dev), _check(dh, "dh", f, dev), M, E,
          _check(uniq, "uniq", torch.int32, dev), C, _check(inv, "inv", torch.int32, dev, T * N),
          int(mb), _check(dones, "dones", f, dev, (T + 1) * N), T, N, W,
-         _opt(out, "out", f, dev, C * E), _check(gp, "gp", f, dev, C * E),
+         _opt(out, "out", f, dev, C * E) if mbits is None else None,
+         _opt(mbits, "mbits", torch.int32, dev, C * E // 32), _check(gp, "gp", f, dev, C * E),
          part[0].data_ptr() if part is not None else None)
     return gp, part
 

@@ -62,6 +62,7 @@ def test_frames_kernels_match_oracle(dev, T, N, W, F, M, E, nmb, p_done):
     (24, 7, 4, 42, 1, 4, 0.0, 64),      # no resets
     (10, 3, 16, 10, 1, 3, 0.1, 12),     # W = 16 (the kernels' maximum)
     (12, 6, 4, 24, 1, 4, 0.1, 516),     # E not a multiple of 512: a partial column pass
+    (12, 6, 4, 24, 1, 4, 0.1, 544),     # ... and a multiple of 32 (the bitmask form)
 ])
 def test_frames_scatter_relu_is_scatter_then_relu_backward(dev, T, N, W, M, E, nmb, p_done, Ed):
     """ocppo_frames_scatter_relu: gp = out <= 0 ? 0 : frames_scatter(...) bit for bit (same
@@ -83,6 +84,15 @@ def test_frames_scatter_relu_is_scatter_then_relu_backward(dev, T, N, W, M, E, n
         assert np.array_equal(gp.cpu().numpy(), want)
         assert chunks == -(-s["cap"] // 16)
         torch.testing.assert_close(part.sum(0).double(), gp.double().sum(0), rtol=1e-5, atol=1e-5)
+        part = part.clone()  # the partials buffer is per shape: the next call rewrites it
+        if Ed % 32 == 0:  # the same mask as the row-major ReLU bitmask of out: the same gp
+            on = (out > 0).astype(np.uint64).reshape(s["cap"], -1, 32)
+            words = (on << np.arange(32, dtype=np.uint64)).sum(-1).astype(np.uint32)
+            gpb, (partb, _) = ops.frames_scatter_relu(
+                torch.from_numpy(dh).to(dev), du[j], di[e], k, s["d_dones"], T, N, W,
+                mbits=torch.from_numpy(words.view(np.int32)).to(dev))
+            assert np.array_equal(gpb.cpu().numpy(), want)
+            assert torch.equal(partb, part)
         plain, none = ops.frames_scatter_relu(torch.from_numpy(dh).to(dev), du[j], di[e], k,
                                               s["d_dones"], T, N, W, with_db=False)
         assert none is None

@@ -5,6 +5,7 @@ product's rounding obeys — next to hipBLASLt's own f32 GEMM on the same operan
 must stay at f32 accuracy (the reference's Linear layers, ppo_atari_oc.py:566-606, are f32 with
 TF32 off)."""
 import pytest
+import numpy as np
 import torch
 
 from oc_cleanrl_amd import ops
@@ -170,6 +171,43 @@ def test_relu_bitmask_roundtrip(tile):
     gp2, _ = ops.dx_x6_relu(gg, w2, y, mbits=mb)
     gp3, _ = ops.dx_x6_relu(gg, w2, y)
     assert torch.equal(gp2, gp3)
+
+
+def _rows_bits_ref(h):
+    """The row-major ReLU bitmask of h [M, N] (bit n % 32 of int32 word [m, n // 32] =
+    !(h <= 0)), built on the host."""
+    on = (~(h <= 0)).cpu().numpy().astype(np.uint64).reshape(h.shape[0], -1, 32)
+    words = (on << np.arange(32, dtype=np.uint64)).sum(-1).astype(np.uint32)
+    return torch.from_numpy(words.view(np.int32))
+
+
+@pytest.mark.parametrize("tile,M,N", [(24, 512, 256), (25, 512, 256), (26, 512, 256),
+                                      (27, 512, 256), (28, 512, 256), (29, 512, 256),
+                                      (56, 1024, 256), (57, 512, 256), (58, 512, 512),
+                                      (59, 512, 256), (60, 512, 256), (56, 11520, 512)])
+def test_relu_bitmask_rows_layout(tile, M, N):
+    """relu | OCPPO_X6_MBITS_ROWS: the forward writes the row-major bitmask of its ReLU output
+    (every tile shape: 4 / 8 waves, 16 FM x 16 FN wave fragments of FN = 2 or 4), the output
+    unchanged; a NaN output (relu keeps it) is 'on', as threshold_backward treats it."""
+    if ops.x6_tile(M, N, tile=tile) is None:
+        pytest.skip("tile not built")
+    g = torch.Generator(device=DEV).manual_seed(91)
+    K0 = 256
+    x = _rand(M, K0, gen=g)
+    w = _rand(N, K0, gen=g, scale=K0 ** -0.5)
+    b = _rand(N, gen=g, scale=0.1)
+    x[3, 5] = float("nan")  # row 3 all NaN
+    h = torch.empty(M, N, device=DEV)
+    bits = torch.full((M, N // 32), -1, dtype=torch.int32, device=DEV)
+    ops.gemm_x6(x, K0, 1, w, K0, 1, h, N, M, N, K0, bias=b, relu=True, tile=tile,
+                mbits_out=bits, mbits_rows=True)
+    h_ref = torch.empty_like(h)
+    ops.gemm_x6(x, K0, 1, w, K0, 1, h_ref, N, M, N, K0, bias=b, relu=True, tile=tile)
+    assert torch.equal(h.nan_to_num(7.0), h_ref.nan_to_num(7.0))
+    assert bool(h[3].isnan().all())
+    assert torch.equal(bits.cpu(), _rows_bits_ref(h))
+    y, (rb, kind) = ops.linear_x6(x, w, b, relu=True, mbits="rows")
+    assert kind == "rows" and torch.equal(rb.cpu(), _rows_bits_ref(y))
 
 
 @pytest.mark.parametrize("mbig", [0, 512, 1024, None])

@@ -67,6 +67,13 @@ SIZES = {
     # Linear layers at config run the deferred form above, ops.relu_bias_grad_partial)
     "relu_bias_grad_tail": {"config": dict(shapes=((12288, 512), (12288, 1024), (12288, 512))),
                             "scaled": dict(shapes=((262144, 1024),))},
+    # the update's frame scatter with the last encoder layer's ReLU backward (config 2: a
+    # 4096-sample minibatch of a [128, 128] rollout, W = 4, E = 512, the planner's 11520 rows):
+    # mask from the forward's row-major bitmask; frames_scatter_relu_f32 reads the f32 output
+    "frames_scatter_relu": {"config": dict(T=128, N=128, W=4, M=4096, E=512),
+                            "scaled": dict(T=128, N=2048, W=4, M=65536, E=512)},
+    "frames_scatter_relu_f32": {"config": dict(T=128, N=128, W=4, M=4096, E=512),
+                                "scaled": dict(T=128, N=2048, W=4, M=65536, E=512)},
     # the rollout's last encoder layer writing the frame-encoding ring (M = 128 envs, 1024 -> 512)
     "cache_linear": {"config": dict(M=128, K=1024, E=512, W=4), "scaled": dict(M=8192, K=1024, E=512, W=4)},
     # the rollout decoder on the frame-encoding ring (128 envs, W*E = 4*512 -> 512, rot 1) and the
@@ -156,7 +163,43 @@ def case_bytes(name: str, p: dict) -> float:
     if name == "gemm_x6":  # x, W (+ bias) in, y out
         M, N, K = p["M"], p["N"], p["K"]
         return 4 * (M * K + N * (K + 1) + M * N)
+    if name in ("frames_scatter_relu", "frames_scatter_relu_f32"):
+        # dh [M, W, E] in; per frame: id 4 + the mask (1 bit or 4 B per element) in, gp out;
+        # the bias-gradient partials (one row per 16 frames) out. C = the plan's capacity.
+        M, W, E = p["M"], p["W"], p["E"]
+        C = p.get("C") or _scatter_plan(p, None)[0]
+        mask = E // 8 if name == "frames_scatter_relu" else 4 * E
+        return 4 * M * W * E + C * (4 + 4 * E + mask) + 4 * E * -(-C // 16)
     raise KeyError(name)
+
+
+_PLANS = {}
+
+
+def _scatter_plan(p: dict, dev):
+    """(C, uniq, inv, dones) of minibatch 0 of a seeded [T, N] rollout's first epoch (the trainer's
+    FramePlanner, 4 minibatches of M); host arrays when dev is None."""
+    key = (p["T"], p["N"], p["W"], p["M"], str(dev))
+    if key not in _PLANS:
+        import numpy as np
+
+        from oc_cleanrl_amd.frames import FramePlanner
+
+        T, N, W, M = p["T"], p["N"], p["W"], p["M"]
+        B = T * N
+        pl = FramePlanner(T, N, W, M, 1, B // M)
+        perm = np.random.default_rng(0).permutation(B).astype(np.int64)
+        used, inv = pl.plan(perm)
+        cap = pl.cap_for(pl.counts)
+        buf = np.zeros(pl.size(cap), np.int32)
+        pl.fill(buf, cap, used, inv)
+        uniq, _, iv = pl.views(buf, cap)
+        dones = (np.random.default_rng(1).random((T + 1, N)) < 1 / 3500).astype(np.float32)
+        if dev is None:
+            return cap, uniq[0], iv[0], dones
+        _PLANS[key] = (cap, torch.from_numpy(uniq[0].copy()).to(dev),
+                       torch.from_numpy(iv[0].copy()).to(dev), torch.from_numpy(dones).to(dev))
+    return _PLANS[key]
 
 
 def make_case(name: str, p: dict, dev):
@@ -330,6 +373,21 @@ def make_case(name: str, p: dict, dev):
         x, h = torch.empty(C, F, device=dev), torch.empty(C, N1, device=dev)
         fn = lambda: ops.frames_gather_linear(obs, uniq, w, b, relu=True, x_out=x, h_out=h)  # noqa: E731
         return fn, case_bytes(name, p)
+    if name in ("frames_scatter_relu", "frames_scatter_relu_f32"):
+        T, N, W, M, E = p["T"], p["N"], p["W"], p["M"], p["E"]
+        C, uniq, inv, dones = _scatter_plan(p, dev)
+        dh = torch.randn(M, W, E, device=dev, generator=g)
+        out = torch.relu(torch.randn(C, E, device=dev, generator=g))
+        on = (out > 0).view(C, E // 32, 32).to(torch.int64) << torch.arange(32, device=dev)
+        bits = on.sum(-1).to(torch.int32)  # bit 31 wraps into the sign: the same 32 bits
+        gp = torch.empty(C, E, device=dev)
+        if name == "frames_scatter_relu":
+            fn = lambda: ops.frames_scatter_relu(dh, uniq, inv, 0, dones, T, N, W,  # noqa: E731
+                                                 gp=gp, mbits=bits)
+        else:
+            fn = lambda: ops.frames_scatter_relu(dh, uniq, inv, 0, dones, T, N, W,  # noqa: E731
+                                                 out=out, gp=gp)
+        return fn, case_bytes(name, dict(p, C=C))
     if name == "cache_linear":
         M, K, E, W = p["M"], p["K"], p["E"], p["W"]
         x = torch.relu(torch.randn(M, K, device=dev, generator=g))

@@ -41,6 +41,8 @@ KERNEL_SUBSTR = {
     "decoder": ("linear_rows_kernel",),
     "encoder_mid": ("linear_rows_kernel",),
     "gemm_x6": ("gemm_x6_kernel",),
+    "frames_scatter_relu": ("frames_scatter_relu_kernel",),
+    "frames_scatter_relu_f32": ("frames_scatter_relu_kernel",),
 }
 
 
