@@ -683,6 +683,27 @@ OCPPO_API int ocppo_q_head_epsilon_greedy(ocppo_stream_t stream, const float* hi
                                           uint64_t seed, const int64_t* step, int64_t step_offset,
                                           double start_e, double end_e, double duration,
                                           int64_t* actions, float* epsilon_out, float* q_out);
+/* One acting step of the DQN loop (dqn_atari_oc.py:345-372) in ONE launch, for the object-frame
+ * synthetic env (ocppo_synth_env_step's, seed env_seed, step id *env_step_base + env_step_offset)
+ * and E <= 64 envs: ocppo_q_head_epsilon_greedy's actions (actions, epsilon_out), the env step on
+ * them (frame [E, D] f32, env_reward / env_done [E], ep_state [E, 5] or NULL), the frame-stack
+ * store of ocppo_rollout_store (prev_obs -> obs_out [E, W, D] in obs_dtype, net_obs f32 or NULL,
+ * done_out; reward_out = the reward, or with vecnorm != 0 ocppo_rollout_store_vecnorm's normalised
+ * reward and (ret_state, rms_state) update) and ocppo_replay_add of (prev_obs, obs_out, actions,
+ * reward_out, done_out) into a replay of obs_dtype (rb_obs [rb_size, E, W * D], rb_state {pos,
+ * full}). advance != 0 then adds advance to *step and *env_step_base (both read before: the
+ * last env step of a captured chunk moves the chunk's counters, replacing two launches). Every
+ * output is bitwise the four launches'. */
+OCPPO_API int ocppo_dqn_act_step(
+    ocppo_stream_t stream, const float* hidden, int64_t E, int64_t H, const float* wq,
+    const float* bq, int64_t A, uint64_t seed, int64_t* step, int64_t step_offset,
+    double start_e, double end_e, double duration, int64_t* actions, float* epsilon_out,
+    uint64_t env_seed, int64_t* env_step_base, int64_t env_step_offset, int64_t D,
+    float* frame, float* env_reward, float* env_done, float* ep_state, int64_t W,
+    const void* prev_obs, void* obs_out, int obs_dtype, float* net_obs, float* done_out,
+    float* reward_out, int vecnorm, double vn_gamma, double vn_epsilon, double vn_clip,
+    double* ret_state, double* rms_state, int64_t* rb_state, int64_t rb_size, void* rb_obs,
+    int64_t* rb_actions, float* rb_rewards, float* rb_dones, int64_t advance);
 OCPPO_API int ocppo_epsilon_greedy(ocppo_stream_t stream, const float* q, int64_t E, int64_t A,
                                    uint64_t seed, const int64_t* step, int64_t step_offset,
                                    double start_e, double end_e, double duration,

@@ -108,6 +108,9 @@ SIGNATURES: dict[str, tuple[type, list]] = {
     "ocppo_frames_scatter_chunks": (I64, [I64]),
     "ocppo_frames_gather_linear": (I, [P, P, I, I64, I64, I64, I64, P, I64, P, P, I64, I, P, P]),
     "ocppo_q_head_epsilon_greedy": (I, [P, P, I64, I64, P, P, I64, U64, P, I64, D, D, D, P, P, P]),
+    "ocppo_dqn_act_step": (I, [P, P, I64, I64, P, P, I64, U64, P, I64, D, D, D, P, P, U64, P, I64,
+                               I64, P, P, P, P, I64, P, P, I, P, P, P, I, D, D, D, P, P, P, I64, P,
+                               P, P, P, I64]),
     "ocppo_frames_scatter_relu": (I, [P, P, I64, I64, P, I64, P, I64, P, I64, I64, I64, P, P, P,
                                       P]),
     "ocppo_gemm_x6": (I, [P, P, I64, I64, P, I64, I64, P, I64, I64, I64, I64, I64, I64, P, I, P,

@@ -12,6 +12,8 @@
 // sampler is by distribution, the TD math is bit-level).
 #include "ocppo_common.h"
 #include "ocppo_categorical.h"
+#include "ocppo_store.h"
+#include "ocppo_synth_env.h"
 
 namespace ocppo {
 
@@ -239,11 +241,218 @@ __global__ __launch_bounds__(1024) void td_loss_kernel(const float* __restrict__
   }
 }
 
+// ---- one acting step of the DQN loop in ONE launch (dqn_atari_oc.py:345-372) --------------------
+// The Q head + epsilon-greedy choice (q_head_eps_kernel's arithmetic), the object-frame synthetic
+// env's step on those actions (synth_env_kernel's), the frame-stack store + VecNormalize
+// (store_vecnorm_kernel's: store_groups / vecnorm_block) and the replay add of (obs, next_obs,
+// action, reward, done) (replay_add_kernel's), as four phases of ONE workgroup separated by
+// barriers: every value is the one the four launches write, in the same order; the step's chain of
+// four dependent launches (4-5 us each at one env) becomes one. E <= 64 envs (one workgroup).
+struct DqnActArgs {
+  const float* hidden;
+  int64_t E;
+  const float* wq;
+  const float* bq;
+  int A;
+  uint64_t seed;
+  int64_t* step;
+  int64_t step_offset;
+  double start_e, end_e, duration;
+  int64_t* actions;
+  float* eps_out;
+  uint64_t env_seed;
+  int64_t* env_step_base;
+  int64_t env_step_offset, D;
+  float* frame;
+  float* env_reward;
+  float* env_done;
+  float* ep;
+  int W;
+  const void* prev;
+  void* out;
+  float* net;
+  float* done_out;
+  float* reward_out;
+  int vecnorm;
+  double vn_gamma, vn_eps, vn_clip;
+  double* ret;
+  double* rms;
+  int64_t* rb_state;
+  int64_t rb_size;
+  void* rb_obs;
+  int64_t* rb_act;
+  float* rb_rew;
+  float* rb_done;
+  int64_t advance;  // added to *step and *env_step_base at the end (the chunk's last env step)
+};
+constexpr int kDqnActMaxE = 64;
+
+template <int CH, int ODT>
+__global__ __launch_bounds__(256) void dqn_act_step_kernel(DqnActArgs p) {
+  __shared__ int64_t s_act[kDqnActMaxE];
+  constexpr int H = 256 * CH;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t E = p.E;
+  // 1. Q head + epsilon-greedy, one wave per env
+  {
+    const int jo = lane >> 3;
+    const float bias = jo < p.A ? p.bq[jo] : 0.f;
+    float4 w[8][CH];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int c = 0; c < CH; ++c)
+        w[j][c] = j < p.A ? reinterpret_cast<const float4*>(p.wq + static_cast<int64_t>(j) * H)[c * kWave + lane]
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
+    const int64_t ts = p.step[0] + p.step_offset;
+    const double slope = (p.end_e - p.start_e) / p.duration;
+    double eps = slope * static_cast<double>(ts) + p.start_e;
+    eps = eps > p.end_e ? eps : p.end_e;
+    const uint64_t hh = mix64(mix64(p.seed ^ 0xA0761D6478BD642Full) + static_cast<uint64_t>(ts));
+    const double coin = static_cast<double>(hh >> 11) * (1.0 / 9007199254740992.0);  // [0, 1)
+    for (int64_t e = wv; e < E; e += 4) {  // wave-uniform
+      float4 x[CH];
+      head_load_row<CH>(p.hidden, e, lane, x);
+      const float t = head_dots<CH>(x, w, lane) + bias;
+      float q[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) q[j] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t), 8 * j));
+      int64_t a;
+      if (coin < eps) {
+        a = static_cast<int64_t>(mix64(hh + static_cast<uint64_t>(e) + 1) % static_cast<uint64_t>(p.A));
+      } else {
+        int best = 0;
+        float bqv = q[0];
+#pragma unroll
+        for (int j = 1; j < 8; ++j)
+          if (j < p.A && (q[j] > bqv || (q[j] != q[j] && bqv == bqv))) {
+            bqv = q[j];
+            best = j;
+          }
+        a = best;
+      }
+      if (lane == 0) {
+        p.actions[e] = a;
+        s_act[e] = a;
+      }
+    }
+    if (p.eps_out && threadIdx.x == 0) p.eps_out[0] = static_cast<float>(eps);
+  }
+  __syncthreads();
+  // 2. the env step on those actions (object frames)
+  {
+    const uint64_t st = static_cast<uint64_t>(p.env_step_base[0] + p.env_step_offset);
+    for (int64_t g = threadIdx.x; g < E * p.D; g += blockDim.x) {
+      const int64_t n = g / p.D, k = g - n * p.D;
+      const uint64_t key = synth_env_key(p.env_seed, st, n);
+      p.frame[g] = synth_env_obj(key, k, s_act[n]);
+      if (k == 0) synth_env_outcome(key, n, p.env_reward, p.env_done, p.ep);
+    }
+  }
+  __syncthreads();
+  // 3. store (+ VecNormalize)
+  if (p.vecnorm) {
+    vecnorm_block(p.env_reward, p.env_done, E, p.vn_gamma, p.vn_eps, p.vn_clip, p.ret, p.rms,
+                  p.reward_out);
+    store_groups<OCPPO_F32, ODT, 1>(0, 1, p.frame, p.env_reward, p.env_done, E, p.W, p.D, p.prev,
+                                    p.out, p.net, nullptr, p.done_out, 1.0f, nullptr);
+  } else {
+    store_groups<OCPPO_F32, ODT, 1>(0, 1, p.frame, p.env_reward, p.env_done, E, p.W, p.D, p.prev,
+                                    p.out, p.net, p.reward_out, p.done_out, 1.0f, nullptr);
+  }
+  __syncthreads();
+  // 4. replay add of (prev, out, action, reward_out, done_out) at pos; pos advanced after
+  const int64_t pos = p.rb_state[0];
+  const int64_t nxt = (pos + 1) % p.rb_size;
+  const int64_t total = E * p.W * p.D;
+  using T = typename Elem<ODT>::T;
+  const T* pv = static_cast<const T*>(p.prev);
+  const T* ov = static_cast<const T*>(p.out);
+  T* rb = static_cast<T*>(p.rb_obs);
+  for (int64_t g = threadIdx.x; g < total; g += blockDim.x) {
+    rb[pos * total + g] = pv[g];
+    rb[nxt * total + g] = ov[g];
+    if (g < E) {
+      p.rb_act[pos * E + g] = s_act[g];
+      p.rb_rew[pos * E + g] = p.reward_out[g];
+      p.rb_done[pos * E + g] = p.done_out[g];
+    }
+  }
+  __syncthreads();  // every thread has read pos
+  if (threadIdx.x == 0) {
+    const int64_t p1 = pos + 1;
+    if (p1 == p.rb_size) {
+      p.rb_state[1] = 1;
+      p.rb_state[0] = 0;
+    } else {
+      p.rb_state[0] = p1;
+    }
+    if (p.advance) {  // both counters were read in phases 1 and 2, before the barriers
+      p.step[0] += p.advance;
+      p.env_step_base[0] += p.advance;
+    }
+  }
+}
+
 }  // namespace ocppo
 
 using namespace ocppo;
 
 extern "C" size_t ocppo_replay_workspace_bytes(void) { return 256; }
+
+extern "C" int ocppo_dqn_act_step(
+    ocppo_stream_t stream, const float* hidden, int64_t E, int64_t H, const float* wq,
+    const float* bq, int64_t A, uint64_t seed, int64_t* step, int64_t step_offset,
+    double start_e, double end_e, double duration, int64_t* actions, float* epsilon_out,
+    uint64_t env_seed, int64_t* env_step_base, int64_t env_step_offset, int64_t D,
+    float* frame, float* env_reward, float* env_done, float* ep_state, int64_t W,
+    const void* prev_obs, void* obs_out, int obs_dtype, float* net_obs, float* done_out,
+    float* reward_out, int vecnorm, double vn_gamma, double vn_epsilon, double vn_clip,
+    double* ret_state, double* rms_state, int64_t* rb_state, int64_t rb_size, void* rb_obs,
+    int64_t* rb_actions, float* rb_rewards, float* rb_dones, int64_t advance) {
+  OCPPO_REQUIRE(E >= 1 && E <= kDqnActMaxE && A >= 1 && A <= 8 && H >= 256 && H % 256 == 0 &&
+                    H <= 1024 && D >= 1 && W >= 1 && W <= 64 && rb_size >= 2 && duration > 0,
+                "ocppo_dqn_act_step: bad sizes E=%lld H=%lld A=%lld D=%lld W=%lld (E <= %d, A <= "
+                "8, H a multiple of 256 <= 1024)", (long long)E, (long long)H, (long long)A,
+                (long long)D, (long long)W, kDqnActMaxE);
+  OCPPO_REQUIRE(hidden && wq && bq && step && actions && env_step_base && frame && env_reward &&
+                    env_done && prev_obs && obs_out && done_out && reward_out && rb_state &&
+                    rb_obs && rb_actions && rb_rewards && rb_dones &&
+                    (!vecnorm || (ret_state && rms_state)),
+                "ocppo_dqn_act_step: null pointer");
+  OCPPO_REQUIRE(((reinterpret_cast<uintptr_t>(hidden) | reinterpret_cast<uintptr_t>(wq)) & 15) == 0,
+                "ocppo_dqn_act_step: hidden and wq must be 16-B aligned");
+  OCPPO_REQUIRE(prev_obs != obs_out && reward_out != env_reward,
+                "ocppo_dqn_act_step: prev_obs / obs_out and reward / reward_out must not alias");
+  OCPPO_REQUIRE(obs_dtype == OCPPO_F32 || obs_dtype == OCPPO_BF16 || obs_dtype == OCPPO_U8,
+                "ocppo_dqn_act_step: bad obs dtype %d", obs_dtype);
+  DqnActArgs p{hidden, E, wq, bq, (int)A, seed, step, step_offset, start_e, end_e, duration,
+               actions, epsilon_out, env_seed, env_step_base, env_step_offset, D, frame,
+               env_reward, env_done, ep_state, (int)W, prev_obs, obs_out, net_obs, done_out,
+               reward_out, vecnorm ? 1 : 0, vn_gamma, vn_epsilon, vn_clip, ret_state, rms_state,
+               rb_state, rb_size, rb_obs, rb_actions, rb_rewards, rb_dones, advance};
+  clear_stale_error();
+  hipStream_t s = as_stream(stream);
+#define OCPPO_DA(CH, O) \
+  hipLaunchKernelGGL((dqn_act_step_kernel<CH, O>), dim3(1), dim3(256), 0, s, p)
+#define OCPPO_DA_CH(O)            \
+  switch (H / 256) {              \
+    case 1: OCPPO_DA(1, O); break; \
+    case 2: OCPPO_DA(2, O); break; \
+    case 3: OCPPO_DA(3, O); break; \
+    default: OCPPO_DA(4, O); break; \
+  }
+  if (obs_dtype == OCPPO_F32) {
+    OCPPO_DA_CH(OCPPO_F32)
+  } else if (obs_dtype == OCPPO_BF16) {
+    OCPPO_DA_CH(OCPPO_BF16)
+  } else {
+    OCPPO_DA_CH(OCPPO_U8)
+  }
+#undef OCPPO_DA_CH
+#undef OCPPO_DA
+  return check_launch("ocppo_dqn_act_step");
+}
 
 extern "C" int ocppo_replay_add(ocppo_stream_t stream, const void* obs, const void* next_obs,
                                 int obs_dtype, const int64_t* actions, const float* rewards,

@@ -157,6 +157,9 @@ class QNetworkObj(Predictor):
 
 # The acting step's Q head + epsilon-greedy choice as one HIP launch (ops.q_head_epsilon_greedy).
 FUSED_ACT = True
+# ... and with an object-frame synthetic env, the whole rest of the step (env, store +
+# VecNormalize, replay add) in the same launch (ops.dqn_act_step)
+FUSED_ACT_STEP = True
 
 
 def make_qnet(args: DQNArgs, obs_shape, n_actions) -> nn.Module:
@@ -252,8 +255,9 @@ class DQNTrainer:
         ops.obs_reset(frame, self.stacks[0], self.net_obs)
 
     # ------------------------------------------------------------------------------------------
-    def _env_step(self, k: int):
-        """One global step (:345-372): act, step, store + VecNormalize, replay add."""
+    def _env_step(self, k: int, advance: int = 0) -> bool:
+        """One global step (:345-372): act, step, store + VecNormalize, replay add. With the
+        fused launch (ops.dqn_act_step), `advance` moves the chunk counters in it: True then."""
         a = self.args
         prev, nxt = self.stacks[self.cur], self.stacks[1 - self.cur]
         # global step = chunk base (step_dev, advanced once per chunk) + k + 1
@@ -262,6 +266,16 @@ class DQNTrainer:
                 net = self.q.network
                 x = self.net_obs / 255.0 if self.pixels else self.net_obs
                 h = fused_trunk(net[:-1], x)
+                if FUSED_ACT_STEP and not self.pixels and ops.dqn_act_step_ok(
+                        h, net[-1].weight, self.env, prev, self.rb):
+                    vn = (self.ret_state, self.rms_state) if a.vecnorm_reward else None
+                    ops.dqn_act_step(h, net[-1].weight, net[-1].bias, a.seed, self.step_dev,
+                                     a.start_e, a.end_e, self.duration, self.actions,
+                                     self.epsilon, k + 1, self.env, k, prev, nxt, self.net_obs,
+                                     self.done_out, self.rew_out, self.rb, vecnorm_state=vn,
+                                     advance=advance)
+                    self.cur = 1 - self.cur
+                    return bool(advance)
                 ops.q_head_epsilon_greedy(h, net[-1].weight, net[-1].bias, a.seed, self.step_dev,
                                           a.start_e, a.end_e, self.duration, self.actions,
                                           self.epsilon, step_offset=k + 1)
@@ -281,6 +295,7 @@ class DQNTrainer:
                               self.net_obs, self.rew_out, self.done_out)
         self.rb.add(prev, nxt, self.actions, self.rew_out, self.done_out)
         self.cur = 1 - self.cur
+        return False
 
     def _train_step(self):
         """:377-392 — sample, TD target + MSE (fused), backward, Adam."""
@@ -304,10 +319,12 @@ class DQNTrainer:
 
     def _chunk(self, train: bool):
         tf = self.args.train_frequency
+        moved = False
         for k in range(tf):
-            self._env_step(k)
-        self.env.advance(tf)
-        self.step_dev.add_(tf)
+            moved = self._env_step(k, advance=tf if k == tf - 1 else 0)
+        if not moved:
+            self.env.advance(tf)
+            self.step_dev.add_(tf)
         if train:
             self._train_step()
 

@@ -1783,6 +1783,57 @@ def q_head_epsilon_greedy(hidden, wq, bq, seed: int, step, start_e: float, end_e
     return actions_out
 
 
+def dqn_act_step_ok(hidden, wq, env, prev_obs, rb) -> bool:
+    """dqn_act_step applies: <= 64 envs, the q_head_epsilon_greedy head shapes, an object-frame
+    synthetic env and a replay in the stacks' dtype."""
+    E, H = hidden.shape
+    fr = getattr(env, "frame", None)
+    return (getattr(env, "synthetic", False) and fr is not None and fr.dtype == torch.float32
+            and fr.is_contiguous() and fr.shape[0] == E and 1 <= E <= 64
+            and H % 256 == 0 and 256 <= H <= 1024 and 1 <= wq.shape[0] <= 8
+            and hidden.is_contiguous() and wq.is_contiguous()
+            and (hidden.data_ptr() | wq.data_ptr()) % 16 == 0
+            and rb.obs.dtype == prev_obs.dtype and rb.E == E and prev_obs.is_contiguous()
+            and rb.D == prev_obs[0].numel())
+
+
+def dqn_act_step(hidden, wq, bq, seed: int, step, start_e: float, end_e: float, duration: float,
+                 actions_out, epsilon_out, step_offset: int, env, env_step_offset: int, prev_obs,
+                 obs_out, net_obs, done_out, reward_out, rb, vecnorm_state=None, gamma=0.99,
+                 epsilon=1e-8, clip_reward=10.0, advance: int = 0):
+    """q_head_epsilon_greedy + env.step + rollout_store(_vecnorm) + rb.add(prev_obs, obs_out,
+    actions, reward_out, done_out) in one launch (ocppo_dqn_act_step; see dqn_act_step_ok);
+    advance: then step += advance and env.advance(advance) in the same launch."""
+    E, H = hidden.shape
+    A = wq.shape[0]
+    dev = hidden.device
+    f = torch.float32
+    W = obs_out.shape[1]
+    D = env.frame.shape[1]
+    if prev_obs.shape != obs_out.shape or prev_obs.dtype != obs_out.dtype or \
+            obs_out[0, 0].numel() != D:
+        raise ValueError("prev_obs / obs_out must be [E, W, D] stacks of one dtype")
+    ret, rms = vecnorm_state if vecnorm_state is not None else (None, None)
+    call("ocppo_dqn_act_step", _stream(dev), _check(hidden, "hidden", f, dev), E, H,
+         _check(wq, "wq", f, dev, A * H), _check(bq, "bq", f, dev, A), A,
+         int(seed) & 0xFFFFFFFFFFFFFFFF, _check(step, "step", torch.int64, dev, 1),
+         int(step_offset), float(start_e), float(end_e), float(duration),
+         _check(actions_out, "actions", torch.int64, dev, E),
+         _opt(epsilon_out, "epsilon_out", f, dev, 1), env.seed & 0xFFFFFFFFFFFFFFFF,
+         _check(env.step_base, "step_base", torch.int64, dev, 1), int(env_step_offset), D,
+         _check(env.frame, "frame", f, dev, E * D), _check(env.reward, "reward", f, dev, E),
+         _check(env.done, "done", f, dev, E), _opt(env.ep_state, "ep_state", f, dev, E * 5), W,
+         _check(prev_obs, "prev_obs", None, dev, E * W * D),
+         _check(obs_out, "obs_out", None, dev, E * W * D), _DTYPE_CODE[obs_out.dtype],
+         _opt(net_obs, "net_obs", f, dev, E * W * D), _check(done_out, "done_out", f, dev, E),
+         _check(reward_out, "reward_out", f, dev, E), int(vecnorm_state is not None),
+         float(gamma), float(epsilon), float(clip_reward),
+         _opt(ret, "ret_state", torch.float64, dev, E), _opt(rms, "rms_state", torch.float64, dev, 3),
+         rb.state.data_ptr(), rb.size, rb.obs.data_ptr(), rb.actions.data_ptr(),
+         rb.rewards.data_ptr(), rb.dones.data_ptr(), int(advance))
+    return actions_out
+
+
 def td_loss_fwd_bwd(q, q_next, actions, rewards, dones, gamma: float, dq=None, stats=None):
     """(stats [2] = {td_loss, mean q(s,a)}, dq [B, A] = d loss / d q)."""
     B, A = q.shape

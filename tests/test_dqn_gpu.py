@@ -112,3 +112,27 @@ def test_run_dqn_writes_metrics(dev, tmp_path):
     assert lines[-1]["global_step"] == 160 and "charts/SPS" in lines[-1]
     ck = torch.load(runs[0] / "dqn_atari_oc.cleanrl_model", weights_only=True)
     assert set(ck) == {"model_weights", "args"}
+
+
+@pytest.mark.parametrize("envs,vecnorm", [(1, True), (4, True), (3, False)])
+def test_fused_act_step_is_the_four_launches(dev, monkeypatch, envs, vecnorm):
+    """ops.dqn_act_step (Q head + epsilon-greedy + env + store/VecNormalize + replay add in one
+    launch) leaves every buffer bitwise as the four launches do, through training chunks."""
+    from oc_cleanrl_amd import dqn
+
+    kw = dict(num_envs=envs, encoder_dims=(32, 64), decoder_dims=(256,), cuda_graphs=True,
+              vecnorm_reward=vecnorm, start_e=0.5, end_e=0.05)
+    monkeypatch.setattr(dqn, "FUSED_ACT_STEP", False)
+    a = run(dqn_args(**kw), 160, dev)
+    monkeypatch.setattr(dqn, "FUSED_ACT_STEP", True)
+    b = run(dqn_args(**kw), 160, dev)
+    assert a.fused_act and b.fused_act
+    for x, y in ((a.rb.state, b.rb.state), (a.rb.obs, b.rb.obs), (a.rb.actions, b.rb.actions),
+                 (a.rb.rewards, b.rb.rewards), (a.rb.dones, b.rb.dones),
+                 (a.stacks[0], b.stacks[0]), (a.stacks[1], b.stacks[1]),
+                 (a.net_obs, b.net_obs), (a.ret_state, b.ret_state), (a.rms_state, b.rms_state),
+                 (a.epsilon, b.epsilon), (a.env.ep_state, b.env.ep_state),
+                 (a.env.frame, b.env.frame)):
+        assert torch.equal(x, y)
+    for p, q in zip(a.q.parameters(), b.q.parameters()):
+        assert torch.equal(p, q)
