@@ -764,8 +764,11 @@ def run_rank(opt, rank: int, world: int, line_out, watch):
                        "sampling_noise": {
                            "kernel": "the reference's stream: Categorical.sample's per-step [N, A] "
                                      "Exp(1) draws on the device generator (torch's Philox "
-                                     "exponential_ restated), generated inside the sampling "
-                                     "kernel; bitwise torch's draws (tests/test_kernels_gpu.py)",
+                                     "exponential_ restated), the rollout's T draws made by one "
+                                     "HIP launch at its start; bitwise torch's draws "
+                                     "(tests/test_kernels_gpu.py, tests/test_trainer_gpu.py)",
+                           "head": "the reference's stream drawn inside each step's sampling "
+                                   "kernel",
                            "torch": "the reference's stream from torch's exponential_, one "
                                     "launch per step",
                            "rollout": "one [T, N, A] Exp(1) draw per rollout (not the "

@@ -235,6 +235,14 @@ OCPPO_API int ocppo_torch_exponential_geometry(int64_t numel, int64_t cus, int64
 OCPPO_API int ocppo_philox_exponential(ocppo_stream_t stream, float* out, int64_t numel,
                                        const int64_t* philox_state, int64_t philox_offset,
                                        int64_t philox_stride);
+/* `steps` such draws back to back, as `steps` successive exponential_ calls of one shape make
+ * them: out[t * numel + i] = element i of the draw at philox offset philox_offset + t * increment
+ * (increment from ocppo_torch_exponential_geometry). One launch for a whole rollout's
+ * Categorical.sample draws (the reference's per-step stream, ppo_atari_oc.py:505-506). */
+OCPPO_API int ocppo_philox_exponential_steps(ocppo_stream_t stream, float* out, int64_t numel,
+                                             int64_t steps, const int64_t* philox_state,
+                                             int64_t philox_offset, int64_t increment,
+                                             int64_t philox_stride);
 
 /* Fused rollout policy head: logits = hidden @ w_actor^T + b_actor, value = hidden . w_critic +
  * b_critic, then the sampler above — replaces the actor/critic Linear layers AND the sampler of

@@ -49,6 +49,7 @@ SIGNATURES: dict[str, tuple[type, list]] = {
                                      P]),
     "ocppo_torch_exponential_geometry": (I, [I64, I64, I64, P, P]),
     "ocppo_philox_exponential": (I, [P, P, I64, P, I64, I64]),
+    "ocppo_philox_exponential_steps": (I, [P, P, I64, I64, P, I64, I64, I64]),
     "ocppo_categorical_logprob_entropy": (I, [P, P, P, I64, I64, P, P]),
     "ocppo_categorical_logprob_entropy_bwd": (I, [P, P, P, P, P, I64, I64, P]),
     "ocppo_rollout_store": (I, [P, P, I, P, P, I64, I64, I64, P, P, I, P, P, P, I, P]),

@@ -124,10 +124,12 @@ class Args:
     prefetch_shuffle: bool = True  # shuffle (+ frame plan) of the next iteration while the GPU runs
     sampling_noise: str = "kernel"  # the rollout sampler's Exp(1) draws: "kernel" = the reference's
                                     # per-step stream (torch's [N, A] exponential_ per step, as
-                                    # Categorical.sample draws it) generated inside the sampling
-                                    # kernel (ops.TorchExpStream); "torch" = the same stream from
-                                    # torch's exponential_ (a launch per step); "rollout" = one
-                                    # [T, N, A] draw per rollout (not the reference's stream)
+                                    # Categorical.sample draws it), all T steps' draws made by one
+                                    # HIP launch at the rollout's start (ops.TorchExpStream.fill);
+                                    # "head" = the same stream drawn inside the sampling kernel of
+                                    # each step; "torch" = the same stream from torch's
+                                    # exponential_ (a launch per step); "rollout" = one [T, N, A]
+                                    # draw per rollout (not the reference's stream)
     fused_heads_loss: bool = True  # update: policy heads fwd + PPO loss + heads bwd in one HIP op
     dp_overlap: bool = True  # DP: all-reduce the decoder-side gradients during the encoder backward
     sample_records_min: int = 131072  # local batches of at least this many samples: GAE also
@@ -232,8 +234,8 @@ def finalize(args: Args, world_size: int = 1) -> Args:
         raise AssertionError('"obj" observations only work with "PPO_OBJ" architecture!')
     if args.local_batch_size % args.num_minibatches:
         raise ValueError("local batch size must be divisible by num_minibatches")
-    if args.sampling_noise not in ("kernel", "torch", "rollout"):
-        raise ValueError(f"sampling_noise must be kernel, torch or rollout, got "
+    if args.sampling_noise not in ("kernel", "head", "torch", "rollout"):
+        raise ValueError(f"sampling_noise must be kernel, head, torch or rollout, got "
                          f"{args.sampling_noise!r}")
     if args.dp_collectives not in ("rccl", "torch"):
         raise ValueError(f"dp_collectives must be rccl or torch, got {args.dp_collectives!r}")

@@ -918,9 +918,10 @@ __global__ __launch_bounds__(256) void policy_head_fast_kernel(
                                   : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   if (E == 1) {  // config sizes: one environment per wave, wave-uniform tail via v_readlane
-    float nz = lane < A ? noise.get(g * A + lane) : 1.f;
     float4 x[CH];
     head_load_row<CH>(hidden, g, lane, x);
+    // the in-kernel Exp(1) draw (Philox rounds) runs while the row's loads are in flight
+    float nz = lane < A ? noise.get(g * A + lane) : 1.f;
     for (; g < ngroups; g += nwaves) {
       // ENV: everything of env g's step that does not depend on its action -- the frame hashes
       // and the reward / done / episode counters -- while this row's loads are in flight
@@ -2230,7 +2231,38 @@ __global__ __launch_bounds__(256) void philox_exponential_kernel(float* __restri
        i += stride)
     out[i] = philox_noise(pn, i);
 }
+// steps draws of one shape back to back: out[t, i] = draw t (philox offset + t * increment)
+__global__ __launch_bounds__(256) void philox_exponential_steps_kernel(float* __restrict__ out,
+                                                                       int64_t numel,
+                                                                       int64_t increment,
+                                                                       PhiloxNoise pn) {
+  const int64_t t = blockIdx.y;
+  pn.step_offset += t * increment;
+  float* o = out + t * numel;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < numel;
+       i += stride)
+    o[i] = philox_noise(pn, i);
+}
 }  // namespace ocppo
+
+extern "C" int ocppo_philox_exponential_steps(ocppo_stream_t stream, float* out, int64_t numel,
+                                              int64_t steps, const int64_t* philox_state,
+                                              int64_t philox_offset, int64_t increment,
+                                              int64_t philox_stride) {
+  OCPPO_REQUIRE(numel >= 1 && steps >= 1 && steps <= 65535 && increment >= 0 && philox_stride >= 1,
+                "ocppo_philox_exponential_steps: bad sizes numel=%lld steps=%lld", (long long)numel,
+                (long long)steps);
+  OCPPO_REQUIRE(out && philox_state, "ocppo_philox_exponential_steps: null pointer");
+  clear_stale_error();
+  int64_t gx = ceil_div(numel, 256);
+  gx = gx < 1024 ? gx : 1024;
+  hipLaunchKernelGGL(philox_exponential_steps_kernel,
+                     dim3(static_cast<unsigned>(gx), static_cast<unsigned>(steps)), dim3(256), 0,
+                     as_stream(stream), out, numel, increment,
+                     PhiloxNoise{philox_state, philox_offset, philox_stride});
+  return check_launch("ocppo_philox_exponential_steps");
+}
 
 extern "C" int ocppo_torch_exponential_geometry(int64_t numel, int64_t cus,
                                                 int64_t max_threads_per_cu, int64_t* stride,

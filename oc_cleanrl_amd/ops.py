@@ -370,6 +370,7 @@ class TorchExpStream:
 
     def __init__(self, numel: int, device):
         self.device = torch.device(device)
+        torch.cuda.init()  # default_generators is empty until the runtime is initialised
         self.gen = torch.cuda.default_generators[self.device.index
                                                  if self.device.index is not None else 0]
         self.stride, self.increment = torch_exponential_geometry(numel, self.device)
@@ -388,6 +389,10 @@ class TorchExpStream:
     def philox(self, t: int):
         return self.state, t * self.increment, self.stride
 
+    def fill(self, noise):
+        """noise [T, ...] = the T claimed draws (one launch; graph-capturable)."""
+        return philox_exponential_steps(noise, self.state, 0, self.increment, self.stride)
+
 
 def torch_exponential_geometry(numel: int, device) -> tuple[int, int]:
     """(grid stride, philox-offset increment) of torch's exponential_ over `numel` elements on
@@ -404,6 +409,17 @@ def philox_exponential(out, state, offset: int, stride: int):
     dev = out.device
     call("ocppo_philox_exponential", _stream(dev), _check(out, "out", torch.float32, dev),
          out.numel(), _check(state, "philox_state", torch.int64, dev, 2), int(offset), int(stride))
+    return out
+
+
+def philox_exponential_steps(out, state, offset: int, increment: int, stride: int):
+    """out[t] = torch's exponential_ draw t of shape out[0] at generator state[0..1] + (0, offset +
+    t * increment): a rollout's per-step draws in one launch (out [steps, ...])."""
+    dev = out.device
+    steps = out.shape[0]
+    call("ocppo_philox_exponential_steps", _stream(dev), _check(out, "out", torch.float32, dev),
+         out[0].numel(), steps, _check(state, "philox_state", torch.int64, dev, 2), int(offset),
+         int(increment), int(stride))
     return out
 
 

@@ -357,12 +357,13 @@ class PPOTrainer:
         self.values = torch.zeros((T + 1, N), dtype=f32, device=dev)
         self.advantages = torch.zeros((T, N), dtype=f32, device=dev)
         self.returns = torch.zeros((T, N), dtype=f32, device=dev)
-        # the Exp(1) draws torch's Categorical.sample makes ([N, A] per step): by default drawn
-        # inside the sampling kernels as torch's exponential_ would (ops.TorchExpStream), which
-        # also write them here; or torch's exponential_ per step / per rollout (Args.sampling_noise)
+        # the Exp(1) draws torch's Categorical.sample makes ([N, A] per step): by default the
+        # rollout's T draws of the reference's stream drawn by one launch at its start as torch's
+        # exponential_ would (ops.TorchExpStream.fill), or inside the sampling kernel step by step
+        # ("head"); or torch's exponential_ per step / per rollout (Args.sampling_noise)
         self.noise = torch.zeros((T, N, self.A), dtype=f32, device=dev)
-        self.exp_stream = (ops.TorchExpStream(N * self.A, dev) if a.sampling_noise == "kernel"
-                           else None)
+        self.exp_stream = (ops.TorchExpStream(N * self.A, dev)
+                           if a.sampling_noise in ("kernel", "head") else None)
         self.enc_cache = (torch.zeros((N, self.obs_shape[0], self.agent.encoding_dim), dtype=f32,
                                       device=dev) if self.frame_cache else None)
         # frame cache + fusions: the store of step t-1 rides in the launch of step t's first two
@@ -610,7 +611,7 @@ class PPOTrainer:
             # the reference's stream: one Exp(1) draw of [N, A] per step (Categorical.sample at
             # ppo_atari_oc.py:506), from the same device generator
             self.noise[t].exponential_()
-        px = self.exp_stream.philox(t) if self.exp_stream is not None else None
+        px = self.exp_stream.philox(t) if self.args.sampling_noise == "head" else None
         if self.fused_head:
             hidden = self._policy_hidden(t)
             if env_step and FUSED_HEAD_ENV and ops.policy_head_env_ok(
@@ -650,6 +651,9 @@ class PPOTrainer:
         self.dones[0].copy_(self.dones[T])
         if self.args.sampling_noise == "rollout":
             self.noise.exponential_()  # the whole rollout's Exp(1) draws in one generator call
+        elif self.args.sampling_noise == "kernel":
+            # the reference's T per-step draws (the claimed generator range), one launch
+            self.timer.bracket("noise_draws", lambda: self.exp_stream.fill(self.noise))
 
     def _rollout_end(self):
         """Bootstrap + GAE (:533-547) + minibatch adv stats (:577-579)."""

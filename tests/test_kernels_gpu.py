@@ -253,6 +253,11 @@ def _gen_state(gen, dev):
                         dtype=torch.int64, device=dev)
 
 
+def _default_gen(dev):
+    torch.cuda.init()  # default_generators is empty until the runtime is initialised
+    return torch.cuda.default_generators[dev.index or 0]
+
+
 @pytest.mark.parametrize("numel", [1, 6, 768, 1000, 3072 * 7, 256 * 2048 + 5,
                                    4 * 256 * 2048 + 17, 9 * 256 * 2048 + 1])
 @pytest.mark.parametrize("seed", [0, 1, 2 ** 63 + 12345])
@@ -261,7 +266,7 @@ def test_philox_exponential_is_torch_exponential(ops, dev, numel, seed):
     bit for bit: torch's grid geometry (one uniform4 per thread up to 4 grid strides, components
     1-3 and later draws beyond), its Philox counter layout, uniform conversion and log transform
     (ocppo_philox.h); and the generator advances by the increment the geometry reports."""
-    g = torch.cuda.default_generators[dev.index or 0]
+    g = _default_gen(dev)
     g.manual_seed(seed)
     g.set_offset(8 * 4)
     state = _gen_state(g, dev)
@@ -276,6 +281,21 @@ def test_philox_exponential_is_torch_exponential(ops, dev, numel, seed):
     assert torch.equal(out2, ref2)
 
 
+@pytest.mark.parametrize("numel,steps", [(768, 128), (6, 3), (256 * 2048 + 5, 2)])
+def test_philox_exponential_steps_are_successive_draws(ops, dev, numel, steps):
+    """ocppo_philox_exponential_steps: `steps` successive torch exponential_ draws of one shape in
+    one launch, bit for bit (a rollout's Categorical.sample noise)."""
+    g = _default_gen(dev)
+    g.manual_seed(77)
+    g.set_offset(4 * 3)
+    state = _gen_state(g, dev)
+    stride, inc = ops.torch_exponential_geometry(numel, dev)
+    ref = torch.stack([torch.empty(numel, device=dev).exponential_() for _ in range(steps)])
+    out = ops.philox_exponential_steps(torch.empty(steps, numel, device=dev), state, 0, inc,
+                                       stride)
+    assert torch.equal(out, ref)
+
+
 @pytest.mark.parametrize("N,H,A", [(128, 512, 6), (7, 64, 18), (300001, 512, 6), (33, 100, 6)])
 def test_policy_head_draws_the_torch_stream_itself(ops, dev, N, H, A):
     """The sampling kernels with philox state: the Exp(1) values they draw (and write) are
@@ -287,7 +307,7 @@ def test_policy_head_draws_the_torch_stream_itself(ops, dev, N, H, A):
     ba = torch.randn(A, device=dev, generator=g) * 0.1
     wc = torch.randn(1, H, device=dev, generator=g)
     bc = torch.randn(1, device=dev, generator=g)
-    dg = torch.cuda.default_generators[dev.index or 0]
+    dg = _default_gen(dev)
     dg.manual_seed(77)
     state = _gen_state(dg, dev)
     stride, inc = ops.torch_exponential_geometry(N * A, dev)
@@ -321,7 +341,7 @@ def test_policy_head_env_step_draws_the_torch_stream_itself(ops, dev):
     envs = [SyntheticAtariEnv("ALE/Pong-v5", "obj", N, D, 5, dev) for _ in range(2)]
     for e in envs:
         e.reset()
-    dg = torch.cuda.default_generators[dev.index or 0]
+    dg = _default_gen(dev)
     dg.manual_seed(5)
     state = _gen_state(dg, dev)
     stride, inc = ops.torch_exponential_geometry(N * A, dev)

@@ -514,8 +514,8 @@ def test_fused_heads_loss_trainer_matches_unfused(dev):
         torch.testing.assert_close(p, q, rtol=1e-3, atol=2e-5)
 
 
-@pytest.mark.parametrize("graphs,mode", [(True, "kernel"), (False, "kernel"), (True, "torch"),
-                                         (False, "torch")])
+@pytest.mark.parametrize("graphs,mode", [(True, "kernel"), (False, "kernel"), (True, "head"),
+                                         (False, "head"), (True, "torch"), (False, "torch")])
 def test_per_step_noise_is_the_reference_sampling_stream(dev, graphs, mode):
     """The rollout's Exp(1) draws are exactly the [N, A] draws the reference's
     Categorical.sample makes step after step (ppo_atari_oc.py:506) from the device generator
@@ -526,7 +526,7 @@ def test_per_step_noise_is_the_reference_sampling_stream(dev, graphs, mode):
 
     a = small_args(sampling_noise=mode, cuda_graphs=graphs)
     tr = PPOTrainer(a, dev)
-    assert (tr.exp_stream is not None) == (mode == "kernel")
+    assert (tr.exp_stream is not None) == (mode in ("kernel", "head"))
     got = []
     for _ in range(3):
         tr.train_iteration()
