@@ -208,11 +208,18 @@ def _f64_under_decisions(tr, j, saved):
     x = x0.double()
     own = x0.double()  # the f64 forward with its own ReLU decisions: the flips of the chain's
     flips = []
+    ulp = []  # p99 / max of |h - z64| / (2^-24 S) where both are > 0 (S = sum |w||x| + |b|)
     with torch.no_grad():
         zs = []
         for i in range(len(relu_outs)):
-            zo = own @ P[f"network.{2 * i}.weight"].t() + P[f"network.{2 * i}.bias"]
+            wi, bi = P[f"network.{2 * i}.weight"], P[f"network.{2 * i}.bias"]
+            zo = own @ wi.t() + bi
             zs.append(zo)
+            h = relu_outs[i]
+            both = (h > 0) & (zo > 0)
+            S = own.abs() @ wi.abs().t() + bi.abs()
+            e = ((h.double() - zo).abs() / S)[both] / 2.0 ** -24
+            ulp.append((round(float(torch.quantile(e[:1 << 24], 0.99)), 2), round(float(e.max()), 2)))
             own = torch.relu(zo)
     for i, h in enumerate(relu_outs):
         x = (x @ P[f"network.{2 * i}.weight"].t() + P[f"network.{2 * i}.bias"]) * (h > 0)
@@ -249,6 +256,7 @@ def _f64_under_decisions(tr, j, saved):
     vl = 0.5 * torch.max((value - ret) ** 2, (vc - ret) ** 2).mean()
     loss = pg - 0.01 * ent.mean() + 0.5 * vl
     loss.backward()
+    _f64_under_decisions.ulp = ulp
     return {n: p.grad for n, p in P.items()}, flips
 
 
@@ -278,8 +286,9 @@ def test_config2_chain_matches_f64_under_its_own_relu_decisions(dev, fixture, x6
         for k, p in params.items():
             mx = float(g64[k].abs().max())
             errs[k] = float((p.grad.double() - g64[k]).abs().max()) / mx
-        print(f"minibatch {j} (x6={x6}): ReLU decisions unlike f64's per layer {flips}; error vs "
-              "f64 under the chain's decisions: "
+        print(f"minibatch {j} (x6={x6}): ReLU decisions unlike f64's per layer {flips}; "
+              f"encoder pre-activation error / (2^-24 S), (p99, max) per layer: "
+              f"{_f64_under_decisions.ulp}; error vs f64 under the chain's decisions: "
               + ", ".join(f"{k} {e:.2g}" for k, e in errs.items()))
         # f32 level: within 3x of the f32 reference's own worst per-tensor error against the f64
         # twin at the same parameters (minibatch 0 of the fixture: 1.7e-6, actor.weight)
