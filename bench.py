@@ -774,7 +774,9 @@ def run_rank(opt, rank: int, world: int, line_out, watch):
                            "rollout": "one [T, N, A] Exp(1) draw per rollout (not the "
                                       "reference's stream)"}[args.sampling_noise],
                        "parallelism": f"dp{world}",
-                       **({"dist_backend": opt.backend} if world > 1 else {})},
+                       **({"dist_backend": opt.backend} if world > 1 else {}),
+                       **({"dp_exchange": tr.dp_form,
+                           "dp_overlap": bool(args.dp_overlap)} if tr.dp else {})},
             "replicas": replicas,
             "updates_per_sec": round(updates / dt, 2),
             "roofline": roofline,

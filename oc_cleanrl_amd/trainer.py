@@ -260,11 +260,15 @@ class PPOTrainer:
         # its all-reduces are captured with each epoch's minibatches; a side stream carries the
         # tail's all-reduce while the lower encoder layers run their backward
         self.comm = self.side = None
+        self.dp_form = None  # the exchange actually in use (bench.py reports it)
         if (self.dp and args.dp_collectives == "rccl" and torch.device(device).type == "cuda"
                 and dist.get_backend() == "nccl"):
             torch.cuda.set_device(device)
-            self.comm = RcclComm(rank, dist.get_world_size())
-            self.side = torch.cuda.Stream(device)
+            self.comm, self.dp_form = self._rccl_comm(rank, dist.get_world_size(), device)
+            if self.comm is not None:
+                self.side = torch.cuda.Stream(device)
+        if self.dp and self.dp_form is None:
+            self.dp_form = "torch collectives"
         self.log_enabled = log and rank == 0
         a = args
         if envs is None and a.backend != "Synthetic":
@@ -1051,6 +1055,30 @@ class PPOTrainer:
 
     def save(self, path):
         torch.save(self.state_dict_checkpoint(), path)
+
+    @staticmethod
+    def _rccl_comm(rank: int, world: int, device):
+        """The package's RCCL communicator, checked with one eager all-reduce before anything is
+        captured around it (every rank takes part; a rank whose check fails aborts its
+        communicator and the ranks agree, through the process group, to use torch's collectives
+        instead: (comm or None, the form in use))."""
+        comm, why = None, ""
+        try:
+            comm = RcclComm(rank, world)
+            t = torch.ones(1, dtype=torch.float32, device=device)
+            comm.all_reduce_sum(t)
+            torch.cuda.synchronize(device)
+            if float(t.item()) != float(world):
+                why = f"check all-reduce gave {float(t.item())} for {world} ranks"
+        except RuntimeError as e:  # ncclResult of init or of the check
+            why = str(e)
+        ok = torch.tensor([0 if why else 1], dtype=torch.int32, device=device)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if int(ok.item()) == 1:
+            return comm, "rccl (own communicator, captured per epoch)"
+        if comm is not None:
+            comm.close(abort=True)
+        return None, f"torch collectives (own RCCL communicator refused: {why or 'on a peer'})"
 
     def close(self):
         """Release the exchange's RCCL communicator (before the process group is destroyed)."""
