@@ -188,11 +188,18 @@ OCPPO_API int ocppo_ppo_loss_fwd_bwd(ocppo_stream_t stream, const float* logits,
 #define OCPPO_OPT_BC2_SQRT 4
 #define OCPPO_OPT_NUM_SCALARS 8
 OCPPO_API size_t ocppo_clip_adam_workspace_bytes(int64_t P);
+/* n_planes (0..8) plane jobs: the new values of the row-major [plane_rows[j], plane_cols[j]]
+ * weight at params + plane_offset[j] (offset % 4 == 0, cols % 4 == 0) are also written as the
+ * three exact bf16 pieces ocppo_split_planes writes for it (trans as plane_trans[j]), piece p at
+ * plane_dst[j] + p * rows * cols: the next update's GEMMs read them without a split launch. */
 OCPPO_API int ocppo_clip_adam_step(ocppo_stream_t stream, float* params, const float* grads,
                                    float* exp_avg, float* exp_avg_sq, int64_t P, const float* lr,
                                    double beta1, double beta2, double eps, double grad_scale,
                                    double max_norm, float* scalars, void* workspace,
-                                   size_t workspace_bytes);
+                                   size_t workspace_bytes, int n_planes,
+                                   const int64_t* plane_offset, const int64_t* plane_rows,
+                                   const int64_t* plane_cols, const int* plane_trans,
+                                   void* const* plane_dst);
 
 /* ---------------------------------------------------------------------------------------------
  * Rollout action head — replaces Categorical(logits).sample() / log_prob / entropy of
@@ -614,12 +621,16 @@ OCPPO_API int ocppo_frames_scatter_relu(ocppo_stream_t stream, const float* dh, 
  * over the distinct frames, architectures/ppo.py:60-84 on b_obs[mb_inds], ppo_atari_oc.py:566) (F <= 16, N1 % 4 == 0,
  * N1 <= 1024): x_out [C, F] = the gathered frames (as frames_gather),
  * h_out [C, N1] = act(x W^T + b)
- * (w [N1, F], b [N1] or NULL; products summed over f in order, then + b, then ReLU if relu). */
+ * (w [N1, F], b [N1] or NULL; products summed over f in order, then + b, then ReLU if relu).  idx_out (NULL: none): also ocppo_frames_expand_index(pos_of, perm, M, dones, T, N, W) into
+ * idx_out [M, W], made by extra workgroups of the same launch (the row table the update's gathered
+ * decoder reads; one launch instead of two). */
 OCPPO_API int ocppo_frames_gather_linear(ocppo_stream_t stream, const void* obs, int obs_dtype,
                                          int64_t T, int64_t N, int64_t W, int64_t F,
                                          const int32_t* uniq, int64_t C, const float* w,
                                          const float* b, int64_t N1, int relu, float* x_out,
-                                         float* h_out);
+                                         float* h_out, const int32_t* pos_of,
+                                         const int64_t* perm, int64_t M, const float* dones,
+                                         int32_t* idx_out);
 
 /* ---------------------------------------------------------------------------------------------
  * Minibatch gather — replaces `b_obs[mb_inds]` of ppo_atari_oc.py:566-567:

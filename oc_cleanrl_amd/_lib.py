@@ -43,7 +43,8 @@ SIGNATURES: dict[str, tuple[type, list]] = {
     "ocppo_ppo_loss_fwd_bwd": (I, [P, P, P, I64, I64, P, P, P, P, P, P, P, D, D, D, I, I, P, P, P,
                                    P, SZ]),
     "ocppo_clip_adam_workspace_bytes": (SZ, [I64]),
-    "ocppo_clip_adam_step": (I, [P, P, P, P, P, I64, P, D, D, D, D, D, P, P, SZ]),
+    "ocppo_clip_adam_step": (I, [P, P, P, P, P, I64, P, D, D, D, D, D, P, P, SZ, I, P, P, P, P,
+                                 P]),
     "ocppo_categorical_sample": (I, [P, P, P, P, I64, I64, I64, I64, P, P, P, P, P]),
     "ocppo_policy_head_sample": (I, [P, P, I64, I64, P, P, P, P, P, P, I64, I64, I64, P, P, P, P,
                                      P]),
@@ -107,7 +108,8 @@ SIGNATURES: dict[str, tuple[type, list]] = {
     "ocppo_linear_act_ring": (I, [P, P, I64, P, P, P, I64, I64, I64, I64, I64, I64, I]),
     "ocppo_conv2d_act": (I, [P, P, I64, I64, I64, I64, P, P, I64, I64, I64, I64, P, I]),
     "ocppo_frames_scatter_chunks": (I64, [I64]),
-    "ocppo_frames_gather_linear": (I, [P, P, I, I64, I64, I64, I64, P, I64, P, P, I64, I, P, P]),
+    "ocppo_frames_gather_linear": (I, [P, P, I, I64, I64, I64, I64, P, I64, P, P, I64, I, P, P, P,
+                                       P, I64, P, P]),
     "ocppo_q_head_epsilon_greedy": (I, [P, P, I64, I64, P, P, I64, U64, P, I64, D, D, D, P, P, P]),
     "ocppo_dqn_act_step": (I, [P, P, I64, I64, P, P, I64, U64, P, I64, D, D, D, P, P, U64, P, I64,
                                I64, P, P, P, P, I64, P, P, I, P, P, P, I, D, D, D, P, P, P, I64, P,

@@ -40,6 +40,17 @@ __device__ __forceinline__ int latest_reset(const float* __restrict__ dones, int
   return res;
 }
 
+// The decoder's row table (frames_expand_index_kernel's) made by workgroups [gblocks, grid) of
+// the same launch, beside the gather: both only read the plan, so they need no ordering
+struct ExpandIdx {
+  const int32_t* pos_of;
+  const int64_t* perm;
+  int64_t M;
+  const float* dones;
+  int32_t* idx;  // NULL: no row table in this launch
+  int gblocks;
+};
+
 // x_out[c, :] = f32(frame of timeline id uniq[c]) (zeros for padding ids < 0)
 template <int DT>
 __global__ __launch_bounds__(256) void frames_gather_kernel(const void* __restrict__ obs,
@@ -82,7 +93,7 @@ template <int DT, bool RELU>
 __global__ __launch_bounds__(256) void frames_gather_linear_kernel(
     const void* __restrict__ obs, int64_t N, int W, int F, const int32_t* __restrict__ uniq,
     int64_t C, const float* __restrict__ w, const float* __restrict__ b, int N1,
-    float* __restrict__ x_out, float* __restrict__ h_out) {
+    float* __restrict__ x_out, float* __restrict__ h_out, ExpandIdx) {
   __shared__ float4 wt4[kGlMaxF * kGlCols / 4];
   __shared__ float4 bs4[kGlCols / 4];
   __shared__ float xs[kGlRows][kGlMaxF];
@@ -396,7 +407,21 @@ template <int DT, bool RELU>
 __global__ __launch_bounds__(256) void frames_gather_linear_wide_kernel(
     const void* __restrict__ obs, int64_t N, int W, int F, const int32_t* __restrict__ uniq,
     int64_t C, const float* __restrict__ w, const float* __restrict__ b, int N1,
-    float* __restrict__ x_out, float* __restrict__ h_out) {
+    float* __restrict__ x_out, float* __restrict__ h_out, ExpandIdx ei) {
+  if (ei.idx != nullptr && static_cast<int>(blockIdx.x) >= ei.gblocks) {  // workgroup-uniform
+    const int64_t j = static_cast<int64_t>(blockIdx.x - ei.gblocks) * blockDim.x + threadIdx.x;
+    if (j >= ei.M * W) return;
+    const int64_t i = j / W;
+    const int k = static_cast<int>(j - i * W);
+    const int64_t bb = ei.perm[i];
+    const int t = static_cast<int>(bb / N);
+    const int64_t n = bb - t * N;
+    const int r = latest_reset(ei.dones, t, n, N, W);
+    int s = t - (W - 1) + k;
+    s = s > r ? s : r;
+    ei.idx[j] = ei.pos_of[(s + W - 1) * N + n];
+    return;
+  }
   __shared__ float4 wt4[kGlMaxF * kGwCols / 4];
   __shared__ float4 bs4[kGwCols / 4];
   __shared__ float xs[kGwRows][kGlMaxF];
@@ -593,13 +618,23 @@ extern "C" int ocppo_frames_gather_linear(ocppo_stream_t stream, const void* obs
                                           int64_t T, int64_t N, int64_t W, int64_t F,
                                           const int32_t* uniq, int64_t C, const float* w,
                                           const float* b, int64_t N1, int relu, float* x_out,
-                                          float* h_out) {
+                                          float* h_out, const int32_t* pos_of,
+                                          const int64_t* perm, int64_t M, const float* dones,
+                                          int32_t* idx_out) {
   OCPPO_REQUIRE(T >= 1 && N >= 1 && W >= 1 && W <= kFramesMaxW && F >= 1 && F <= kGlMaxF &&
                     N1 >= 4 && N1 % 4 == 0 && N1 <= kGlMaxN && C >= 0 &&
                     (T + W - 1) * N < INT32_MAX,
                 "ocppo_frames_gather_linear: bad sizes (F <= %d, N1 %% 4 == 0, N1 <= %d)",
                 kGlMaxF, kGlMaxN);
-  if (C == 0) return OCPPO_OK;
+  OCPPO_REQUIRE(!idx_out || (pos_of && perm && dones && M >= 1 && M * W < INT32_MAX),
+                "ocppo_frames_gather_linear: the row table needs pos_of, perm, dones, M >= 1");
+  if (C == 0) {
+    if (!idx_out) return OCPPO_OK;
+    clear_stale_error();
+    hipLaunchKernelGGL(frames_expand_index_kernel, dim3(static_cast<unsigned>(ceil_div(M * W, 256))),
+                       dim3(256), 0, as_stream(stream), pos_of, perm, M, dones, N, (int)W, idx_out);
+    return check_launch("ocppo_frames_gather_linear/index");
+  }
   OCPPO_REQUIRE(obs && uniq && w && x_out && h_out, "ocppo_frames_gather_linear: null pointer");
   OCPPO_REQUIRE(aligned16(h_out), "ocppo_frames_gather_linear: h_out must be 16-B aligned");
   clear_stale_error();
@@ -607,17 +642,22 @@ extern "C" int ocppo_frames_gather_linear(ocppo_stream_t stream, const void* obs
   const bool wide = N1 <= kGwCols;
   const int64_t g = (C + (wide ? kGwRows : kGlRows) - 1) / (wide ? kGwRows : kGlRows);
   OCPPO_REQUIRE(g <= INT32_MAX, "ocppo_frames_gather_linear: too large");
-  const dim3 grid(static_cast<unsigned>(g),
+  // the decoder's row table in the same launch (wide form), else in its own right after
+  const bool fuse_idx = idx_out != nullptr && wide;
+  const int64_t ib = fuse_idx ? ceil_div(M * W, 256) : 0;
+  OCPPO_REQUIRE(g + ib <= INT32_MAX, "ocppo_frames_gather_linear: too large");
+  const ExpandIdx ei{pos_of, perm, M, dones, fuse_idx ? idx_out : nullptr, static_cast<int>(g)};
+  const dim3 grid(static_cast<unsigned>(g + ib),
                   wide ? 1u : static_cast<unsigned>((N1 + kGlCols - 1) / kGlCols));
   const dim3 block(256);
 #define OCPPO_GL_K(KERN, DT)                                                                      \
   do {                                                                                            \
     if (relu)                                                                                     \
       hipLaunchKernelGGL((KERN<DT, true>), grid, block, 0, s, obs, N, (int)W, (int)F, uniq, C, w, \
-                         b, (int)N1, x_out, h_out);                                               \
+                         b, (int)N1, x_out, h_out, ei);                                           \
     else                                                                                          \
       hipLaunchKernelGGL((KERN<DT, false>), grid, block, 0, s, obs, N, (int)W, (int)F, uniq, C,   \
-                         w, b, (int)N1, x_out, h_out);                                            \
+                         w, b, (int)N1, x_out, h_out, ei);                                        \
   } while (0)
 #define OCPPO_GL(DT)                                                                              \
   do {                                                                                            \
@@ -632,5 +672,11 @@ extern "C" int ocppo_frames_gather_linear(ocppo_stream_t stream, const void* obs
   }
 #undef OCPPO_GL
 #undef OCPPO_GL_K
-  return check_launch("ocppo_frames_gather_linear");
+  if (int rc = check_launch("ocppo_frames_gather_linear")) return rc;
+  if (idx_out && !fuse_idx) {
+    hipLaunchKernelGGL(frames_expand_index_kernel, dim3(static_cast<unsigned>(ceil_div(M * W, 256))),
+                       dim3(256), 0, s, pos_of, perm, M, dones, N, (int)W, idx_out);
+    return check_launch("ocppo_frames_gather_linear/index");
+  }
+  return OCPPO_OK;
 }

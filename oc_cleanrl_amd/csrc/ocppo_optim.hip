@@ -17,8 +17,57 @@
 // ticketed form spent ~7 us of its 11 per minibatch in the 256-way fan-in and the dependent
 // combine at config 2).
 #include "ocppo_common.h"
+#include "ocppo_x6split.h"
 
 namespace ocppo {
+
+// Weight planes written by the step (ocppo_clip_adam_step's plane jobs): the new values of a
+// row-major [R, C] weight at flat offset off (float4 units) as the three exact bf16 pieces
+// ocppo_split_planes writes for it -- plane p at dst + p R C (bf16 units), [R, C] or, trans,
+// [C, R] -- so the next minibatch's GEMMs read them without a split launch
+constexpr int kAdamPlaneJobs = 8;
+struct AdamPlanes {
+  int n;
+  int64_t off4[kAdamPlaneJobs];
+  int64_t len4[kAdamPlaneJobs];
+  int rows[kAdamPlaneJobs];
+  int cols[kAdamPlaneJobs];
+  int trans[kAdamPlaneJobs];
+  uint16_t* dst[kAdamPlaneJobs];
+};
+
+__device__ __forceinline__ void adam_planes_store(const AdamPlanes& pl, int64_t i, float4 v) {
+  for (int j = 0; j < pl.n; ++j) {
+    const int64_t q = i - pl.off4[j];
+    if (q >= 0 && q < pl.len4[j]) {
+      uint32_t a0, a1, a2, b0, b1, b2;
+      x6_split2(x6f2{v.x, v.y}, a0, a1, a2);
+      x6_split2(x6f2{v.z, v.w}, b0, b1, b2);
+      const int64_t ps = 4 * pl.len4[j];  // elements per plane
+      if (!pl.trans[j]) {
+        uint2* d = reinterpret_cast<uint2*>(pl.dst[j]);
+        d[q] = uint2{a0, b0};
+        d[ps / 4 + q] = uint2{a1, b1};
+        d[ps / 2 + q] = uint2{a2, b2};
+      } else {  // element (r, c .. c + 3) -> plane rows c .. c + 3, column r
+        const int64_t e = 4 * q;
+        const int64_t r = e / pl.cols[j], c = e - r * pl.cols[j];
+        const int64_t R = pl.rows[j];
+        uint16_t* d = pl.dst[j] + c * R + r;
+        const uint32_t w[3][2] = {{a0, b0}, {a1, b1}, {a2, b2}};
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          uint16_t* dp = d + p * ps;
+          dp[0] = static_cast<uint16_t>(w[p][0]);
+          dp[R] = static_cast<uint16_t>(w[p][0] >> 16);
+          dp[2 * R] = static_cast<uint16_t>(w[p][1]);
+          dp[3 * R] = static_cast<uint16_t>(w[p][1] >> 16);
+        }
+      }
+      return;
+    }
+  }
+}
 
 constexpr int kOptThreads = 256;
 constexpr int kOptBlocks = 1024;  // grid-stride cap for the norm pass (4 workgroups per CU), at
@@ -114,7 +163,7 @@ __global__ __launch_bounds__(kOptThreads) void adam_kernel(
     float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
     float* __restrict__ v, int64_t P, float grad_scale, float b1, float b2, float eps,
     float max_norm, const float* __restrict__ lr, const float* __restrict__ partials, int nb,
-    float* __restrict__ scalars) {
+    float* __restrict__ scalars, AdamPlanes planes) {
   // the first element group's loads are issued before the scalars are combined: their latency
   // hides the partials' combine (at config 2 every thread has about one group)
   const int64_t P4 = P / 4;
@@ -143,6 +192,7 @@ __global__ __launch_bounds__(kOptThreads) void adam_kernel(
     reinterpret_cast<float4*>(p)[i] = pp;
     reinterpret_cast<float4*>(m)[i] = mm;
     reinterpret_cast<float4*>(v)[i] = vv;
+    if (planes.n) adam_planes_store(planes, i, pp);
     if (i + stride < P4) {
       pp = reinterpret_cast<float4*>(p)[i + stride];
       gg = reinterpret_cast<const float4*>(g)[i + stride];
@@ -168,8 +218,34 @@ extern "C" int ocppo_clip_adam_step(ocppo_stream_t stream, float* params, const 
                                     float* exp_avg, float* exp_avg_sq, int64_t P, const float* lr,
                                     double beta1, double beta2, double eps, double grad_scale,
                                     double max_norm, float* scalars, void* workspace,
-                                    size_t workspace_bytes) {
+                                    size_t workspace_bytes, int n_planes,
+                                    const int64_t* plane_offset, const int64_t* plane_rows,
+                                    const int64_t* plane_cols, const int* plane_trans,
+                                    void* const* plane_dst) {
   OCPPO_REQUIRE(P > 0, "ocppo_clip_adam_step: bad size P=%lld", (long long)P);
+  AdamPlanes planes{};
+  OCPPO_REQUIRE(n_planes >= 0 && n_planes <= kAdamPlaneJobs &&
+                    (n_planes == 0 ||
+                     (plane_offset && plane_rows && plane_cols && plane_trans && plane_dst)),
+                "ocppo_clip_adam_step: n_planes=%d (0..%d) and its arrays", n_planes,
+                kAdamPlaneJobs);
+  planes.n = n_planes;
+  for (int j = 0; j < n_planes; ++j) {
+    const int64_t R = plane_rows[j], C = plane_cols[j];
+    OCPPO_REQUIRE(plane_offset[j] >= 0 && plane_offset[j] % 4 == 0 && R >= 1 && C >= 4 &&
+                      C % 4 == 0 && R <= INT32_MAX && C <= INT32_MAX &&
+                      (plane_trans[j] ? R : C) % 8 == 0 && plane_offset[j] + R * C <= P &&
+                      plane_dst[j] && reinterpret_cast<uintptr_t>(plane_dst[j]) % 16 == 0,
+                  "ocppo_clip_adam_step: plane job %d (offset %lld, %lld x %lld, trans %d): "
+                  "offset %% 4, cols %% 4, plane rows %% 8, inside P, 16-B aligned planes", j,
+                  (long long)plane_offset[j], (long long)R, (long long)C, plane_trans[j]);
+    planes.off4[j] = plane_offset[j] / 4;
+    planes.len4[j] = R * C / 4;
+    planes.rows[j] = static_cast<int>(R);
+    planes.cols[j] = static_cast<int>(C);
+    planes.trans[j] = plane_trans[j] ? 1 : 0;
+    planes.dst[j] = static_cast<uint16_t*>(plane_dst[j]);
+  }
   OCPPO_REQUIRE(params && grads && exp_avg && exp_avg_sq && lr && scalars,
                 "ocppo_clip_adam_step: null pointer");
   OCPPO_REQUIRE((reinterpret_cast<uintptr_t>(params) | reinterpret_cast<uintptr_t>(grads) |
@@ -194,6 +270,6 @@ extern "C" int ocppo_clip_adam_step(ocppo_stream_t stream, float* params, const 
                      grads, exp_avg, exp_avg_sq, P, static_cast<float>(grad_scale),
                      static_cast<float>(beta1), static_cast<float>(beta2),
                      static_cast<float>(eps), static_cast<float>(max_norm), lr, partials,
-                     static_cast<int>(nb), scalars);
+                     static_cast<int>(nb), scalars, planes);
   return check_launch("ocppo_clip_adam_step/adam");
 }

@@ -186,12 +186,14 @@ class _DecodeFrames(torch.autograd.Function):
     premasked, bias grad already written) or masked here."""
 
     @staticmethod
-    def forward(ctx, enc, w, b, pos_of, perm, dones, uniq, inv, mb, T, N, W, enc_box, box):
+    def forward(ctx, enc, w, b, pos_of, perm, dones, uniq, inv, mb, T, N, W, enc_box, box,
+                idx=None):
         from . import agents
 
         E = enc.shape[1]
-        idx = ops.timed("frames_expand_index",
-                        lambda: ops.frames_expand_index(pos_of, perm, dones, T, N, W))
+        if idx is None:  # else made by the frame gather's launch (_GatherLinear1's index)
+            idx = ops.timed("frames_expand_index",
+                            lambda: ops.frames_expand_index(pos_of, perm, dones, T, N, W))
         out = ops.linear_x6_split(enc, w, b, True, W, planes=agents._planes(w, "fwd"),
                                   gather=(idx, E))
         fuse = (FUSED_SCATTER_RELU and enc_box is not None and not enc_box["premasked"] and
@@ -238,7 +240,7 @@ class _DecodeFrames(torch.autograd.Function):
         else:
             ops.timed(f"sum_splits_{S}x{w.shape[0]}x{w.shape[1]}",
                       lambda: ops.sum_splits(wpart, w.grad))
-        return (denc,) + (None,) * 13
+        return (denc,) + (None,) * 14
 
 
 def _decode_gather_ok(agent, enc, M: int, W: int) -> bool:
@@ -281,11 +283,11 @@ def decode_gather_shape_ok(M: int, H: int, E: int, W: int) -> bool:
             and M // st[0] <= 1024 and W * (M // 128) * (H // 128) >= 256)
 
 
-def _decode_frames(agent, enc, pos_of, perm, dones, uniq, inv, mb, T, N, W):
+def _decode_frames(agent, enc, pos_of, perm, dones, uniq, inv, mb, T, N, W, idx=None):
     lin = agent.network[agent._flat + 1]
     box = {"premasked": False, "bias": lin.bias}
     hidden = _DecodeFrames.apply(enc, lin.weight, lin.bias, pos_of, perm, dones, uniq, inv, mb,
-                                 T, N, W, getattr(enc, "_ocppo_box", None), box)
+                                 T, N, W, getattr(enc, "_ocppo_box", None), box, idx)
     hidden._ocppo_box = box
     return hidden
 
@@ -294,6 +296,8 @@ def _decode_frames(agent, enc, pos_of, perm, dones, uniq, inv, mb, T, N, W):
 # (ops.frames_gather_linear) when that layer has <= 16 inputs and FlatAdam-owned grads; its
 # backward is the one-pass ReLU-backward + bias + weight gradient (ops.relu_bias_wgrad).
 FUSED_GATHER_L1 = True
+# ... which also makes the gathered decoder's [M, W] row table (ops.frames_gather_linear's index)
+FUSED_INDEX_IN_GATHER = True
 
 
 class _GatherLinear1(torch.autograd.Function):
@@ -303,9 +307,16 @@ class _GatherLinear1(torch.autograd.Function):
     rows launch, carrying this layer's finish in its split-K combine (no finish launch)."""
 
     @staticmethod
-    def forward(ctx, w, b, obs, uniq, slot=None):
-        x, h1 = ops.timed("frames_gather_linear",
-                          lambda: ops.frames_gather_linear(obs, uniq, w, b, relu=True))
+    def forward(ctx, w, b, obs, uniq, slot=None, index=None):
+        # index = (pos_of, perm, dones, holder): the decoder's row table made by the same launch
+        # (holder["idx"])
+        if index is not None:
+            x, h1, index[3]["idx"] = ops.timed(
+                "frames_gather_linear",
+                lambda: ops.frames_gather_linear(obs, uniq, w, b, relu=True, index=index[:3]))
+        else:
+            x, h1 = ops.timed("frames_gather_linear",
+                              lambda: ops.frames_gather_linear(obs, uniq, w, b, relu=True))
         ctx.save_for_backward(x, h1)
         ctx.params, ctx.slot = (w, b), slot
         if slot is not None:
@@ -327,7 +338,7 @@ class _GatherLinear1(torch.autograd.Function):
                 run = ctx.slot.pop("run", None)
                 if run is not None:
                     run(None)
-                return None, None, None, None, None
+                return None, None, None, None, None, None
         g = g.contiguous()
         run = ctx.slot.pop("run", None) if ctx.slot is not None else None
         if run is None or g.shape[0] == 0:
@@ -335,13 +346,13 @@ class _GatherLinear1(torch.autograd.Function):
                       lambda: ops.relu_bias_wgrad(g, h1, x, dw=w.grad, db=b.grad))
             if run is not None:
                 run(None)
-            return None, None, None, None, None
+            return None, None, None, None, None, None
         fin = ops.DeferredFinish(g.device)
         ops.timed(f"relu_bias_wgrad_{g.shape[0]}x{g.shape[1]}x{x.shape[1]}",
                   lambda: ops.relu_bias_wgrad(g, h1, x, dw=w.grad, db=b.grad, defer=fin))
         run(fin)
         fin.run()  # no-op when the combine took it
-        return None, None, None, None, None
+        return None, None, None, None, None, None
 
 
 def _gather_l1_ok(agent, obs, split: int) -> bool:
@@ -380,7 +391,13 @@ def minibatch_hidden(agent, obs, dones, uniq, pos_of, inv, perm, mb: int, split:
         # run in the same backward phase: a DP cut between them (split == 2) would all-reduce
         # that gradient (the buffer's tail) while the lower phase still writes it
         slot = {} if split == 0 or split >= 4 else None
-        h1 = _GatherLinear1.apply(l1.weight, l1.bias, obs, uniq, slot)
+        # the gathered decoder's row table from the same launch (used when the decoder takes
+        # the gathered path below; an unused table costs the launch a few workgroups)
+        hold = {}
+        index = ((pos_of, perm, dones, hold)
+                 if FUSED_INDEX_IN_GATHER and FUSED_DECODE_GATHER and torch.is_grad_enabled()
+                 else None)
+        h1 = _GatherLinear1.apply(l1.weight, l1.bias, obs, uniq, slot, index)
         if slot is not None:
             h1._ocppo_wslot = slot
         if split:
@@ -391,7 +408,8 @@ def minibatch_hidden(agent, obs, dones, uniq, pos_of, inv, perm, mb: int, split:
         else:
             enc = fused_trunk(agent.network[2:agent._flat], h1, rows_last=SCATTER_MBITS)
         if _decode_gather_ok(agent, enc, perm.numel(), W):
-            hidden = _decode_frames(agent, enc, pos_of, perm, dones, uniq, inv, mb, T, N, W)
+            hidden = _decode_frames(agent, enc, pos_of, perm, dones, uniq, inv, mb, T, N, W,
+                                    idx=hold.get("idx"))
             return (hidden, cut) if split else hidden
         h = _FramesExpand.apply(enc.contiguous(), pos_of, perm, dones, uniq, inv, mb, T, N, W,
                                 getattr(enc, "_ocppo_box", None))

@@ -1431,9 +1431,11 @@ def frames_gather(obs, uniq, out=None):
 
 
 def frames_gather_linear(obs, uniq, weight, bias=None, relu: bool = True, x_out=None,
-                         h_out=None):
+                         h_out=None, index=None):
     """(x, h): frames_gather(obs, uniq) and act(x @ weight.T + bias) in one launch
-    (ocppo_frames_gather_linear: the update's first encoder layer over the distinct frames)."""
+    (ocppo_frames_gather_linear: the update's first encoder layer over the distinct frames).
+    index = (pos_of, perm, dones[, out]): also frames_expand_index's row table in the same launch;
+    returns (x, h, idx) then."""
     T, N, W, F = _obs_TNWF(obs)
     dev = obs.device
     C = uniq.numel()
@@ -1443,12 +1445,20 @@ def frames_gather_linear(obs, uniq, weight, bias=None, relu: bool = True, x_out=
         x_out = torch.empty((C, F), dtype=f, device=dev)
     if h_out is None:
         h_out = torch.empty((C, N1), dtype=f, device=dev)
+    ix, idx = (None, None, 0, None, None), None
+    if index is not None:
+        pos_of, perm, dones = index[:3]
+        M = perm.numel()
+        idx = index[3] if len(index) > 3 else torch.empty((M, W), dtype=torch.int32, device=dev)
+        ix = (_check(pos_of, "pos_of", torch.int32, dev, (T + W - 1) * N),
+              _check(perm, "perm", torch.int64, dev), M,
+              _check(dones, "dones", f, dev, (T + 1) * N), _check(idx, "idx", torch.int32, dev, M * W))
     call("ocppo_frames_gather_linear", _stream(dev), _check(obs, "obs", None, dev),
          _DTYPE_CODE[obs.dtype], T, N, W, F, _check(uniq, "uniq", torch.int32, dev), C,
          _check(weight, "weight", f, dev, N1 * F), _opt(bias, "bias", f, dev, N1), N1,
          int(bool(relu)), _check(x_out, "x_out", f, dev, C * F),
-         _check(h_out, "h_out", f, dev, C * N1))
-    return x_out, h_out
+         _check(h_out, "h_out", f, dev, C * N1), *ix)
+    return (x_out, h_out) if index is None else (x_out, h_out, idx)
 
 
 def frames_expand(enc, pos_of, perm, dones, T: int, N: int, W: int, out=None):
@@ -1692,6 +1702,36 @@ class FlatAdam:
         self.max_grad_norm = float(max_grad_norm)
         nb = _lib.LIB.ocppo_clip_adam_workspace_bytes(n)
         self.ws = torch.zeros(int(nb), dtype=torch.uint8, device=dev)
+        self._planes = (0, None, None, None, None, None)
+
+    def write_planes(self, jobs):
+        """jobs [(weight, trans, planes)] (WeightPlanes.jobs): every step also writes each
+        weight's new values as its three exact bf16 pieces ([3, N, K], or of W^T [3, K, N] with
+        trans) into planes, so the next GEMMs need no split launch (ocppo_clip_adam_step's plane
+        jobs, <= 8)."""
+        jobs = list(jobs)
+        if len(jobs) > 8:
+            raise ValueError("FlatAdam.write_planes: at most 8 weights")
+        base = self.params.data_ptr()
+        offs, rows, cols, trs, dsts = [], [], [], [], []
+        for w, trans, d in jobs:
+            off = (w.data_ptr() - base) // 4
+            if (w.dtype != torch.float32 or w.dim() != 2 or not w.is_contiguous()
+                    or not 0 <= off < self.numel or d.dtype != torch.bfloat16
+                    or d.numel() != 3 * w.numel() or not d.is_contiguous()):
+                raise ValueError("FlatAdam.write_planes: a contiguous 2-D weight of this buffer "
+                                 "and its bf16 [3, ...] planes")
+            offs.append(off)
+            rows.append(w.shape[0])
+            cols.append(w.shape[1])
+            trs.append(int(trans))
+            dsts.append(d.data_ptr())
+        c = ctypes
+        n = len(jobs)
+        self._planes = ((n, (c.c_int64 * n)(*offs), (c.c_int64 * n)(*rows),
+                         (c.c_int64 * n)(*cols), (c.c_int * n)(*trs), (c.c_void_p * n)(*dsts))
+                        if n else (0, None, None, None, None, None))
+        self._plane_keep = [d for _, _, d in jobs]
 
     def zero_grad(self):
         self.grads.zero_()
@@ -1701,7 +1741,8 @@ class FlatAdam:
         call("ocppo_clip_adam_step", _stream(dev), self.params.data_ptr(), self.grads.data_ptr(),
              self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(), self.numel,
              self.lr.data_ptr(), self.betas[0], self.betas[1], self.eps, float(grad_scale),
-             self.max_grad_norm, self.scalars.data_ptr(), self.ws.data_ptr(), self.ws.numel())
+             self.max_grad_norm, self.scalars.data_ptr(), self.ws.data_ptr(), self.ws.numel(),
+             *self._planes)
 
 
 # ---------------------------------------------------------------------------------------------

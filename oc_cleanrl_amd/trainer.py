@@ -56,6 +56,9 @@ def storage_dtype(args: Args, pixels: bool, integer_obs: bool = True) -> torch.d
 # The rollout's synthetic object-frame env step fused into the policy head's launch
 # (ops.policy_head_env_step: bitwise the two-launch step; one launch fewer per env step).
 FUSED_HEAD_ENV = True
+# The weights' bf16 planes for the next minibatch's GEMMs written by the optimizer step itself
+# (ops.FlatAdam.write_planes) instead of a split launch per minibatch.
+ADAM_WRITES_PLANES = True
 
 
 class FlatGrads:
@@ -437,6 +440,7 @@ class PPOTrainer:
         self.hl_finish = ops.DeferredFinish(dev) if self.fused_heads_loss else None
         self.b_obs = self.obs[:T].view((T * N,) + self.obs_shape)
         self.wplanes, self.wplanes_built = None, False  # built at the first minibatch
+        self.planes_by_opt = False
         # GAE's per-sample records for the minibatch gather (ops.sample_records)
         self.records = (ops.sample_records(self.B, dev)
                         if 0 <= a.sample_records_min <= self.B else None)
@@ -729,9 +733,18 @@ class PPOTrainer:
         weights' bf16 planes refreshed first: the previous minibatch's step changed them)."""
         if not self.wplanes_built:
             self.wplanes, self.wplanes_built = self._weight_planes(), True
+            # the optimizer step writes the planes of the weights it just changed (FlatAdam plane
+            # jobs): the split launch then runs once per iteration (weights changed outside the
+            # optimizer between iterations -- checkpoint loads, tests -- are re-split there)
+            self.planes_by_opt = (ADAM_WRITES_PLANES and self.wplanes is not None
+                                  and self.args.fused_optimizer and len(self.wplanes.jobs) <= 8
+                                  and all(w.is_contiguous() for w, _, _ in self.wplanes.jobs))
+            if self.planes_by_opt:
+                self.optimizer.write_planes(self.wplanes.jobs)
         if self.wplanes is None:
             return self._forward_backward_body(j)
-        self.timer.bracket("split_planes", self.wplanes.refresh)
+        if j == 0 or not self.planes_by_opt:
+            self.timer.bracket("split_planes", self.wplanes.refresh)
         with agents.weight_planes():
             return self._forward_backward_body(j)
 

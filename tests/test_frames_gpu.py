@@ -130,6 +130,30 @@ def test_frames_gather_linear_is_gather_then_linear(dev, dtype, T, N, W, F, N1, 
         assert bool(((h.double() - ref).abs() <= (F + 2) * 2.0 ** -24 * scale + 1e-30).all())
 
 
+@pytest.mark.parametrize("N1", [256, 512])  # the wide form (row table in the same launch), narrow
+def test_frames_gather_linear_makes_the_row_table_too(dev, N1):
+    """ocppo_frames_gather_linear with idx_out: x and h bitwise the plain call's, and the row table
+    bitwise ocppo_frames_expand_index's (extra workgroups of the same launch, or a second launch
+    after the narrow form); an empty frame set still writes the table."""
+    T, N, W, F, M, E, nmb = 32, 64, 4, 12, 512, 2, 4
+    s = _setup(T, N, W, F, M, E, nmb, 1 / 20, 9, dev, torch.bfloat16)
+    du, dp, di = s["d_plan"]
+    g = torch.Generator(device=dev).manual_seed(3)
+    w = torch.randn((N1, F), device=dev, generator=g) * F ** -0.5
+    b = torch.randn(N1, device=dev, generator=g)
+    for j in (0, 5):
+        perm = s["d_perm"][j * M:(j + 1) * M]
+        x0, h0 = ops.frames_gather_linear(s["d_obs"], du[j], w, b, relu=True)
+        x1, h1, idx = ops.frames_gather_linear(s["d_obs"], du[j], w, b, relu=True,
+                                               index=(dp[j], perm, s["d_dones"]))
+        assert torch.equal(x0, x1) and torch.equal(h0, h1)
+        assert torch.equal(idx, ops.frames_expand_index(dp[j], perm, s["d_dones"], T, N, W))
+    empty = du[0][:0]
+    _, _, idx = ops.frames_gather_linear(s["d_obs"], empty, w, b, relu=True,
+                                         index=(dp[0], s["d_perm"][:M], s["d_dones"]))
+    assert torch.equal(idx, ops.frames_expand_index(dp[0], s["d_perm"][:M], s["d_dones"], T, N, W))
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32, torch.uint8])
 def test_frames_at_config_size_reproduce_the_minibatch(dev, dtype):
     """Config 2 sizes (T=128, N=128, W=4, F=12, 4 x 4 minibatches of 4096): the deduplicated

@@ -262,6 +262,27 @@ def test_split_planes_is_the_exact_split(R, C, trans):
     assert torch.equal(tot, src.double())
 
 
+def test_adam_step_writes_the_weight_planes():
+    """FlatAdam.write_planes: the optimizer step also writes each registered weight's new values
+    as its three exact bf16 pieces (of W, or of W^T), bitwise what ocppo_split_planes writes."""
+    g = torch.Generator(device=DEV).manual_seed(5)
+    lin1 = torch.nn.Linear(512, 256).to(DEV)
+    lin2 = torch.nn.Linear(136, 1024).to(DEV)
+    opt = ops.FlatAdam(list(lin1.parameters()) + list(lin2.parameters()), lr=1e-3, eps=1e-5,
+                       max_grad_norm=0.5)
+    w1, w2 = lin1.weight, lin2.weight
+    p1 = torch.zeros(3, 256, 512, dtype=torch.bfloat16, device=DEV)
+    p2 = torch.zeros(3, 136, 1024, dtype=torch.bfloat16, device=DEV)  # of W2^T
+    opt.write_planes([(w1, 0, p1), (w2, 1, p2)])
+    for _ in range(2):
+        opt.grads.copy_(torch.randn(opt.numel, device=DEV, generator=g))
+        opt.step()
+    torch.cuda.synchronize()
+    assert torch.equal(p1.view(torch.int16), ops.split_planes_ref(w1.detach()).view(torch.int16))
+    assert torch.equal(p2.view(torch.int16),
+                       ops.split_planes_ref(w2.detach().t().contiguous()).view(torch.int16))
+
+
 @pytest.mark.parametrize("tile", [24, 25, 26, 27, 56])
 def test_gemm_x6_presplit_b_is_bitwise_the_f32_b(tile):
     """The forward (bias + ReLU + bitmask) and the masked dX with B read as pre-split planes

@@ -910,7 +910,7 @@ def test_clip_adam_abi_scalar_tail(ops, dev):
     ws = torch.zeros(int(_lib.LIB.ocppo_clip_adam_workspace_bytes(P)), dtype=torch.uint8, device=dev)
     _lib.call("ocppo_clip_adam_step", torch.cuda.current_stream(dev).cuda_stream, p.data_ptr(),
               g.data_ptr(), m.data_ptr(), v.data_ptr(), P, lr.data_ptr(), 0.9, 0.999, 1e-5, 0.5,
-              0.5, sc.data_ptr(), ws.data_ptr(), ws.numel())
+              0.5, sc.data_ptr(), ws.data_ptr(), ws.numel(), 0, None, None, None, None, None)
     ep, em, ev, step, total = O.clip_adam_step(p0, gr, np.zeros(P, np.float32),
                                                np.zeros(P, np.float32), 0, 1e-3, max_norm=0.5,
                                                grad_scale=0.5)

@@ -639,6 +639,23 @@ def test_weight_planes_are_bitwise_the_in_kernel_split(dev, graphs):
         assert torch.equal(p, q)
 
 
+@pytest.mark.parametrize("graphs", [False, True])
+def test_optimizer_written_planes_are_bitwise_the_split_launch(dev, monkeypatch, graphs):
+    """The weights' planes written by the optimizer step (trainer.ADAM_WRITES_PLANES: one split
+    launch per iteration) leave training bitwise where a split launch per minibatch does."""
+    from oc_cleanrl_amd import trainer as trm
+
+    kw = dict(num_envs=128, num_steps=128, encoder_dims=(256, 512, 1024, 512),
+              decoder_dims=(512,), update_epochs=2, cuda_graphs=graphs, x6_weight_planes=True)
+    monkeypatch.setattr(trm, "ADAM_WRITES_PLANES", True)
+    a, _ = run_iters(small_args(**kw), 3, dev)
+    monkeypatch.setattr(trm, "ADAM_WRITES_PLANES", False)
+    b, _ = run_iters(small_args(**kw), 3, dev)
+    assert a.planes_by_opt and not b.planes_by_opt
+    for p, q in zip(a.agent.parameters(), b.agent.parameters()):
+        assert torch.equal(p, q)
+
+
 def test_sample_records_are_bitwise_the_soa_gather(dev):
     """GAE's 16-B sample records feeding the minibatch gather (Args.sample_records) leave the
     training bitwise unchanged: same parameters after three iterations with graphs."""
@@ -649,7 +666,7 @@ def test_sample_records_are_bitwise_the_soa_gather(dev):
         assert torch.equal(p, q)
 
 
-@pytest.mark.parametrize("toggle", ["decode_gather", "wgrad_after_first_layer"])
+@pytest.mark.parametrize("toggle", ["decode_gather", "wgrad_after_first_layer", "index_in_gather"])
 def test_gathered_decoder_matches_the_expanded_one(dev, toggle):
     """The trainer's decoder reading its rows straight from the frame encodings
     (frames.FUSED_DECODE_GATHER: ocppo_gemm_x6_gather forward and weight gradient, no
@@ -661,13 +678,15 @@ def test_gathered_decoder_matches_the_expanded_one(dev, toggle):
     from oc_cleanrl_amd.args import Args, finalize
     from oc_cleanrl_amd.trainer import PPOTrainer
 
-    mod, name = ((frames, "FUSED_DECODE_GATHER") if toggle == "decode_gather"
-                 else (agents, "DEFER_WGRAD_AFTER_FIRST_LAYER"))
+    mod, name = {"decode_gather": (frames, "FUSED_DECODE_GATHER"),
+                 "index_in_gather": (frames, "FUSED_INDEX_IN_GATHER"),
+                 "wgrad_after_first_layer": (agents, "DEFER_WGRAD_AFTER_FIRST_LAYER")}[toggle]
 
     from oc_cleanrl_amd import ops
 
     # the switched path must actually run at these sizes: count its own entry's calls
-    probe = "dw_x6_parts_gather" if toggle == "decode_gather" else "relu_bias_wgrad"
+    probe = {"decode_gather": "dw_x6_parts_gather", "index_in_gather": "frames_gather_linear",
+             "wgrad_after_first_layer": "relu_bias_wgrad"}[toggle]
 
     def run(on):
         setattr(mod, name, on)
@@ -676,7 +695,8 @@ def test_gathered_decoder_matches_the_expanded_one(dev, toggle):
         real, calls = getattr(ops, probe), []
 
         def spy(*a, **k):
-            if probe == "dw_x6_parts_gather" or k.get("defer") is not None:
+            if (probe == "dw_x6_parts_gather" or k.get("defer") is not None
+                    or k.get("index") is not None):
                 calls.append(1)
             return real(*a, **k)
 
