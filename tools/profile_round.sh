@@ -18,7 +18,8 @@ echo "bench trace done"
 for case in "gae config" "gae scaled" "heads_loss config" "heads_loss scaled" \
             "mb_prepare config" "mb_prepare scaled" "policy_head config" "policy_head scaled" \
             "relu_bias_grad config" "relu_bias_grad scaled" "relu_bias_wgrad config" \
-            "cache_linear config" "store_encode config" "decoder config" "encoder_mid config"; do
+            "cache_linear config" "store_encode config" "decoder config" "encoder_mid config" \
+            "frames_scatter_relu config" "frames_scatter_relu scaled"; do
   set -- $case
   for ctr in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 240 rocprofv3 --pmc "$ctr" --kernel-trace --output-format csv \
