@@ -126,7 +126,8 @@ OCPPO_API int ocppo_minibatch_prepare(ocppo_stream_t stream, const int64_t* perm
  * 16-B gather per sample instead of five scattered 4-8 B ones (the batch arrays of
  * ppo_atari_oc.py:550-555 are the records' fields; the return is advantage + value, GAE's own f32
  * add); outputs and statistics bitwise those of ocppo_minibatch_prepare. records: 16-B aligned,
- * [B]; actions in [0, 2^31).
+ * [B]; actions in [0, 2^31). From 2^20 samples (num_mb x M) on, the statistics are taken by a
+ * second launch from the gathered advantages (contiguous reads; same values, same order). 
  * ------------------------------------------------------------------------------------------- */
 typedef struct {
   float logprob, advantage, value;

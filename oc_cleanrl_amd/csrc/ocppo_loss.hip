@@ -1342,6 +1342,13 @@ extern "C" int ocppo_minibatch_prepare(ocppo_stream_t stream, const int64_t* per
   return check_launch("ocppo_minibatch_prepare");
 }
 
+// samples (num_mb x M) from which the records' minibatch statistics are taken from the gathered
+// (contiguous) advantages in a second launch instead of by the statistics blocks' own gathers
+constexpr int64_t kPrepareSplitStats = int64_t(1) << 20;
+#ifndef OCPPO_PREP_VPT  // records in flight per thread of the gather (experiments: tools/)
+#define OCPPO_PREP_VPT 4
+#endif
+
 extern "C" int ocppo_minibatch_prepare_records(ocppo_stream_t stream, const int64_t* perm,
                                                int64_t M, int64_t num_mb, const void* records,
                                                int64_t* mb_actions, float* mb_logprobs,
@@ -1355,12 +1362,24 @@ extern "C" int ocppo_minibatch_prepare_records(ocppo_stream_t stream, const int6
                 "ocppo_minibatch_prepare_records: null pointer or records not 16-B aligned");
   clear_stale_error();
   hipStream_t s = as_stream(stream);
-  constexpr int VPT = 4;
+  constexpr int VPT = OCPPO_PREP_VPT;
   const int64_t n = M * num_mb;
   const int64_t gb = ceil_div(n, 256 * VPT);
   OCPPO_REQUIRE(gb + num_mb <= INT32_MAX, "ocppo_minibatch_prepare_records: too large");
-  const dim3 grid(static_cast<unsigned>(gb + (adv_stats ? num_mb : 0))), block(256);
   const float4* rec = static_cast<const float4*>(records);
+  if (adv_stats && n >= kPrepareSplitStats) {
+    // streaming sizes: the statistics blocks' own random gathers of the records (one cache line
+    // fill per 4-B advantage) would double the gather's line traffic; instead the gather runs
+    // alone and a second launch reads the gathered advantages contiguously -- the same values
+    // in the same order, so the same figures bitwise
+    hipLaunchKernelGGL((minibatch_prepare_rec_kernel<VPT, 1>), dim3(static_cast<unsigned>(gb)),
+                       dim3(256), 0, s, perm, n, (int)gb, M, rec, mb_actions, mb_logprobs,
+                       mb_advantages, mb_returns, mb_values, nullptr);
+    if (int rc = check_launch("ocppo_minibatch_prepare_records")) return rc;
+    launch_adv_stats(s, mb_advantages, nullptr, M, num_mb, adv_stats);
+    return check_launch("ocppo_minibatch_prepare_records/stats");
+  }
+  const dim3 grid(static_cast<unsigned>(gb + (adv_stats ? num_mb : 0))), block(256);
 #define OCPPO_PREP(SV)                                                                           \
   hipLaunchKernelGGL((minibatch_prepare_rec_kernel<VPT, SV>), grid, block, 0, s, perm, n, (int)gb, \
                      M, rec, mb_actions, mb_logprobs, mb_advantages, mb_returns, mb_values,      \

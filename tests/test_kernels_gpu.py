@@ -1594,8 +1594,11 @@ def test_gae_records_are_the_arrays(ops, dev, T_, N):
     assert torch.equal(f[:, 1] + f[:, 2], r1.view(-1))
 
 
-@pytest.mark.parametrize("M,nmb,B", [(4096, 16, 16384), (100, 7, 700), (16384, 4, 65536)])
+@pytest.mark.parametrize("M,nmb,B", [(4096, 16, 16384), (100, 7, 700), (16384, 4, 65536),
+                                     (16384, 64, 1 << 20), (1000, 1049, 1 << 20)])
 def test_minibatch_prepare_from_records_is_bitwise_the_soa_form(ops, dev, M, nmb, B):
+    """The 16-B record form (at >= 2^20 samples its statistics taken by a second launch from the
+    gathered advantages) is bitwise the SoA form, statistics included."""
     g = torch.Generator(device=dev).manual_seed(M + nmb)
     T_ = 4 if B % 4 == 0 else 1
     acts = torch.randint(0, 6, (B,), device=dev, generator=g)

@@ -33,7 +33,8 @@ KERNEL_SUBSTR = {
     "relu_bias_wgrad": ("relu_bias_wgrad_rows_kernel", "relu_bias_wgrad_finish_kernel"),
     "heads_bwd": ("heads_bwd_kernel",),
     "heads_loss": ("heads_loss_kernel", "heads_loss_finish_kernel"),
-    "mb_prepare": ("minibatch_prepare",),  # the records form (minibatch_prepare_rec_kernel)
+    # the records form (minibatch_prepare_rec_kernel; at >= 2^20 samples + its stats launch)
+    "mb_prepare": ("minibatch_prepare", "adv_stats_kernel"),
     "mb_prepare_soa": ("minibatch_prepare_kernel",),
     "gae_plain": ("ocppo::gae",),
     "cache_linear": ("linear_rows_kernel",),
@@ -57,13 +58,12 @@ def mean_counter(path: Path, substrs):
     """Per-launch counter: the mean over dispatches of each kernel, summed over the kernels."""
     rows = list(csv.DictReader(open(path)))
     total, n = 0.0, []
-    for sub in substrs:
+    for sub in substrs:  # a kernel a case does not launch at this size adds nothing
         vals = [float(r["Counter_Value"]) for r in rows if sub in r["Kernel_Name"]]
-        if not vals:
-            return None, 0
-        total += sum(vals) / len(vals)
+        if vals:
+            total += sum(vals) / len(vals)
         n.append(len(vals))
-    return total, n
+    return (total if any(n) else None), n
 
 
 def main(src, dst):
