@@ -57,8 +57,11 @@ def storage_dtype(args: Args, pixels: bool, integer_obs: bool = True) -> torch.d
 # (ops.policy_head_env_step: bitwise the two-launch step; one launch fewer per env step).
 FUSED_HEAD_ENV = True
 # The weights' bf16 planes for the next minibatch's GEMMs written by the optimizer step itself
-# (ops.FlatAdam.write_planes) instead of a split launch per minibatch.
-ADAM_WRITES_PLANES = True
+# (ops.FlatAdam.write_planes) instead of a split launch per minibatch. Off: at config 2 nearly
+# every parameter has planes (W^T ones among them, scattered 2-B writes from the Adam lanes) and
+# the step took 23.9 instead of 12.3 us against the 5.2 us split launch it replaces
+# (profiles/r05/breakdown_config2.txt vs the round-4 trace)
+ADAM_WRITES_PLANES = False
 
 
 class FlatGrads:
