@@ -39,16 +39,17 @@ MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (the matrix rate ocppo_gemm_x6
 RIDGE = MFMA_F32_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9)  # flop/B where the two bounds meet
 # HBM bytes per launch from rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE, separate passes) of
 # the same launch shapes: tools/profile_round.sh -> tools/summarize_profiles.py
-PMC_SUMMARY = ROOT / "profiles" / "r04" / "pmc_summary.json"
+PMC_SUMMARY = ROOT / "profiles" / "r05" / "pmc_summary.json"
 # in-situ HBM bytes of the bench's own gemm_x6 launches (all shapes, mean per dispatch):
 # tools/pmc_bench.sh -> tools/pmc_bench_summary.py
-PMC_BENCH = ROOT / "profiles" / "r04" / "pmc_bench.json"
+PMC_BENCH = ROOT / "profiles" / "r05" / "pmc_bench.json"
 PMC_KEYS = {"gemm_x6": "gemm_x6", "action_head": "policy_head_config", "gae": "gae_config",
             "ppo_loss": "ppo_loss_prepared_config", "relu_bias_grad": "relu_bias_grad_config",
             "cache_linear": "cache_linear_config", "store_encode": "store_encode_config",
             "heads_bwd": "heads_bwd_config", "relu_bias_wgrad": "relu_bias_wgrad_config",
             "heads_loss": "heads_loss_config", "decoder": "decoder_config",
-            "encoder_mid": "encoder_mid_config", "mb_prepare": "mb_prepare_config"}
+            "encoder_mid": "encoder_mid_config", "mb_prepare": "mb_prepare_config",
+            "frames_scatter_relu": "frames_scatter_relu_config"}
 
 
 def pmc_traffic(key):
@@ -673,7 +674,8 @@ def run_rank(opt, rank: int, world: int, line_out, watch):
         # the fused heads + loss pair) and the largest HBM streams of the iteration, at streaming
         # sizes, every launch after an L3 scrub (cold)
         scaled = {}
-        for name in ("gae", "heads_loss", "mb_prepare", "policy_head", "relu_bias_grad"):
+        for name in ("gae", "heads_loss", "mb_prepare", "policy_head", "relu_bias_grad",
+                     "frames_scatter_relu"):
             r = run_case(name, "scaled", device, reps=10, rounds=5, cold=True)
             traffic, _ = pmc_traffic(f"{name}_scaled")
             scaled[name] = {"params": r["params"], "mean_us": r["mean_us"], "cache": r["cache"],
