@@ -151,9 +151,13 @@ def x6_pipe_tile(M: int, N: int, splits: int = 1):
 
 def _x6_pipe_splits(rows: int, n: int, k: int):
     """(splits, 58) for dW = g^T x [n, k] when some split count in 1..16 gives exactly 256
-    pipelined tiles with >= 8 K steps per split; else None."""
+    pipelined tiles with >= 8 K steps per split (the rows' 32-row steps dealt to the splits as
+    evenly as they go, as gemm_x6 does: 11520 rows = 360 steps, 22-23 per split of 16); else
+    None."""
+    if rows % 32:
+        return None
     for s in (1, 2, 4, 8, 16):
-        if x6_pipe_tile(n, k, s) and rows % (32 * s) == 0 and rows // (32 * s) >= 8:
+        if x6_pipe_tile(n, k, s) and rows // 32 >= 8 * s:
             return s, 58
     return None
 
