@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define OCPPO_ABI_VERSION 23
+#define OCPPO_ABI_VERSION 24
 
 /* status codes */
 #define OCPPO_OK 0
@@ -465,6 +465,30 @@ OCPPO_API int ocppo_gemm_x6_gather(ocppo_stream_t stream, const float* a, int64_
                                    int64_t split_c, const float* bias, int relu,
                                    const void* b_planes, const int32_t* gidx, int64_t gw,
                                    int64_t gseg, int mode);
+
+/* ---------------------------------------------------------------------------------------------
+ * NHWC convolution (no padding, square stride) as an implicit GEMM on ocppo_gemm_x6's exact
+ * three-piece bf16 products (the NatureCNN trunk, cleanrl/architectures/ppo.py:20-31: replaces
+ * the convolution forward / backward cuDNN (MIOpen) runs for nn.Conv2d at ppo_atari_oc.py:506
+ * and :566-606; deterministic: no atomics, split-K partials summed in split order). No im2col
+ * buffer: the convolution rows r = (b, qy, qx) over [B, qh, qw] read element k of their kernel
+ * window at x[b sb + qy ys + qx xs + (k / gseg) segs + k % gseg], geom = {qh, qw, sb, ys, xs,
+ * segs, gseg} (floats; a segment = one kernel row's KW x C taps, contiguous in NHWC; all strides
+ * multiples of 4, x and w 16-B aligned, B qh qw < 2^24).
+ *   mode 0 (forward; and each stride class of the data gradient, over the zero-padded output
+ *          gradient with the flipped weight): c[row(r) + n] = act(sum_k x(r, k) w[n ldw + k] +
+ *          bias[n]) for r < M = B qh qw, n < N, k < K; gseg % 32 == 0; splits == 1; row(r) =
+ *          r ldc, or b sb' + qy ys' + qx xs' + off' with out_geom = {sb', ys', xs', off'}.
+ *   mode 1 (weight gradient): out[m, n] = sum_r w[r ldw + m] x(r, n) (w = the output gradient
+ *          [rows, ldw], m < M = Cout, n < N = KH KW C, r < K = B qh qw); c = split partials
+ *          [splits, M, N], then summed in split order (f64, one rounding) into out; qh qw <= 1024.
+ * tile: 0 = 128 x 32, 2 = 128 x 64, 3 = 64 x 64, 5 = 128 x 128 (mode 0); 1 = 32 x 128, 3, 4 =
+ * 64 x 128, 5 (mode 1); M, N multiples of it; K % 32 == 0, K / 32 >= splits.
+ * ------------------------------------------------------------------------------------------- */
+OCPPO_API int ocppo_conv_x6(ocppo_stream_t stream, int mode, const float* x, const int64_t* geom,
+                            const float* w, int64_t ldw, float* c, int64_t ldc, int64_t M,
+                            int64_t N, int64_t K, int64_t splits, const float* bias, int relu,
+                            const int64_t* out_geom, int tile, float* out);
 
 /* ---------------------------------------------------------------------------------------------
  * The exact three-piece bf16 split ocppo_gemm_x6 forms in its K loop, done once per matrix: the

@@ -607,6 +607,86 @@ class _ConvAct(torch.autograd.Function):
         return dx, dw, (None if direct_b else db_out), None, None, None
 
 
+class _ConvX6(torch.autograd.Function):
+    """y = act(conv2d(x, w) + b) on this package's implicit GEMMs (ops.conv_x6: bias + ReLU in
+    the product's epilogue); backward: ONE HIP pass for ReLU-backward + bias gradient
+    (ops.relu_bias_grad, as _ConvAct), then the weight gradient and, when x needs one, the data
+    gradient on ops.conv_x6_wgrad / conv_x6_dgrad. No MIOpen and no atomics: deterministic, the
+    reference's torch.use_deterministic_algorithms(True) default (ppo_atari_oc.py:200-211) at full
+    speed. nn.Conv2d + nn.ReLU's arithmetic at f32 accuracy (architectures/ppo.py:20-31)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, stride, relu: bool):
+        B, Cin, H, W = x.shape
+        Cout = w.shape[0]
+        y = ops.timed(f"conv_x6_{B}x{Cin}x{H}_{Cout}",
+                      lambda: ops.conv_x6(x, w, b, stride, relu))
+        ctx.conv = (stride, relu)
+        ctx.b = b
+        ctx.save_for_backward(x, w, y if relu else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w, y = ctx.saved_tensors
+        stride, relu = ctx.conv
+        cl = torch.channels_last
+        g = g.contiguous(memory_format=cl)
+        B, C, OH, OW = g.shape
+        g2 = g.permute(0, 2, 3, 1).reshape(-1, C)
+        b = ctx.b
+        direct_b = _direct(b)
+        db_out = b.grad if direct_b else torch.empty_like(b)
+        o2 = y.permute(0, 2, 3, 1).reshape(-1, C) if relu else None
+        gp2, _ = ops.timed(f"relu_bias_grad_{g2.shape[0]}x{C}" + ("" if relu else "_norelu"),
+                           lambda: ops.relu_bias_grad(g2, o2, db=db_out))
+        KH, KW = w.shape[2], w.shape[3]
+        dw = None
+        if ctx.needs_input_grad[1]:
+            if _direct(w) and w.grad.is_contiguous(memory_format=cl):
+                ops.timed(f"conv_x6_wgrad_{C}x{KH * KW * x.shape[1]}",
+                          lambda: ops.conv_x6_wgrad(gp2, x, (KH, KW), stride, out=w.grad))
+            else:
+                dw = ops.conv_x6_wgrad(gp2, x, (KH, KW), stride)
+                dw = dw.view(C, KH, KW, x.shape[1]).permute(0, 3, 1, 2)
+                if _direct(w):
+                    w.grad.copy_(dw)
+                    dw = None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            gp = gp2.view(B, OH, OW, C).permute(0, 3, 1, 2)
+            dx = ops.timed(f"conv_x6_dgrad_{C}x{x.shape[1]}",
+                           lambda: ops.conv_x6_dgrad(gp, w, stride, (x.shape[2], x.shape[3])))
+        return dx, dw, (None if direct_b else db_out), None, None
+
+
+# NatureCNN convolutions on this package's implicit GEMMs (ops.conv_x6, x6 products: no MIOpen,
+# deterministic by construction), in the rollout forward and the update; shapes it does not take
+# (conv_x6_ok: row counts the tiles do not divide, e.g. a few envs) stay on _ConvAct / MIOpen.
+CONV_X6 = True
+
+
+def _conv_x6_ok(x, conv) -> bool:
+    if not (CONV_X6 and isinstance(conv, nn.Conv2d) and conv.bias is not None and x.is_cuda
+            and conv.groups == 1 and conv.dilation == (1, 1) and conv.padding_mode == "zeros"
+            and tuple(conv.padding) == (0, 0) and conv.stride[0] == conv.stride[1]):
+        return False
+    grad = torch.is_grad_enabled()
+    return ops.conv_x6_ok(x, conv.weight, conv.stride[0],
+                          wgrad=grad and conv.weight.requires_grad,
+                          dgrad=grad and x.requires_grad)
+
+
+def _conv_x6(x, conv, relu: bool):
+    s = conv.stride[0]
+    if torch.is_grad_enabled() and (x.requires_grad or conv.weight.requires_grad or
+                                    conv.bias.requires_grad):
+        return _ConvX6.apply(x, conv.weight, conv.bias, s, relu)
+    B, Cin, H, _ = x.shape
+    return ops.timed(f"conv_x6_{B}x{Cin}x{H}_{conv.out_channels}",
+                     lambda: ops.conv_x6(x, conv.weight, conv.bias, s, relu))
+
+
 def _conv_act_ok(x, conv) -> bool:
     return (FUSED_CONV_ACT and isinstance(conv, nn.Conv2d) and conv.bias is not None and x.is_cuda
             and x.dtype == torch.float32 and x.dim() == 4 and conv.groups == 1
@@ -758,6 +838,10 @@ def fused_trunk(seq: nn.Sequential, x, rows_last: bool = False):
                 and _pair_ok(x, m, mods[i + 2])):
             x = linear2_relu(x, m, mods[i + 2])
             i += 4
+        elif _conv_x6_ok(x, m):
+            relu = i + 1 < len(mods) and isinstance(mods[i + 1], nn.ReLU)
+            x = _conv_x6(x, m, relu)
+            i += 2 if relu else 1
         elif _hip_conv_ok(x, m):
             relu = i + 1 < len(mods) and isinstance(mods[i + 1], nn.ReLU)
             x = ops.conv2d_act(x, m.weight, m.bias, m.stride[0], relu)

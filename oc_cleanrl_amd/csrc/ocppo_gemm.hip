@@ -112,7 +112,50 @@ struct X6Args {
   // n % 32 of 32-bit word [m][n / 32] is !(C[m, n] <= 0), for a consumer that walks the output
   // by rows (the frame scatter of the encoder's last ReLU backward, ocppo_frames_scatter_relu)
   int mbits_rows;
+  // implicit-GEMM convolution (ocppo_conv_x6): operand rows r = (b, qy, qx) over [B, cv_qh, cv_qw]
+  // of an NHWC tensor; element k of row r sits at cv_row(r) + cv_seg(k), with
+  //   cv_row(r) = b cv_sb + qy cv_ys + qx cv_xs,  cv_seg(k) = (k / cv_gseg) cv_segs + k % cv_gseg
+  // (a segment = one kernel row's KW x C taps, contiguous in NHWC). GATH 3: A's rows (forward /
+  // data gradient, k-contiguous within a segment); GATH 4: B's K index (weight gradient, B(n, k) =
+  // x[cv_row(k) + cv_seg(n)]). cv_out: C row r written at b co_sb + qy co_ys + qx co_xs + co_off
+  // (GATH 3: one stride class of a strided convolution's data gradient) instead of r ldc.
+  int cv_qh, cv_qw;
+  int64_t cv_sb, cv_ys, cv_xs, cv_segs;
+  int cv_gseg, cv_out;
+  int64_t co_sb, co_ys, co_xs, co_off;
 };
+
+// q = x / d for 0 <= x < 2^24, d >= 1 (f32 reciprocal estimate, corrected to the exact quotient)
+__device__ __forceinline__ int x6_udiv(int x, int d) {
+  int q = static_cast<int>(static_cast<float>(x) * __builtin_amdgcn_rcpf(static_cast<float>(d)));
+  int r = x - q * d;
+  while (r < 0) {
+    --q;
+    r += d;
+  }
+  while (r >= d) {
+    ++q;
+    r -= d;
+  }
+  return q;
+}
+// (b, qy, qx) of convolution row r
+__device__ __forceinline__ void x6_cv_split(const X6Args& g, int r, int& b, int& qy, int& qx) {
+  const int qhw = g.cv_qh * g.cv_qw;
+  b = x6_udiv(r, qhw);
+  const int p = r - b * qhw;
+  qy = x6_udiv(p, g.cv_qw);
+  qx = p - qy * g.cv_qw;
+}
+__device__ __forceinline__ int64_t x6_cv_row(const X6Args& g, int r) {
+  int b, qy, qx;
+  x6_cv_split(g, r, b, qy, qx);
+  return b * g.cv_sb + qy * g.cv_ys + qx * g.cv_xs;
+}
+__device__ __forceinline__ int64_t x6_cv_seg(const X6Args& g, int k) {
+  const int s = k / g.cv_gseg;
+  return s * g.cv_segs + (k - s * g.cv_gseg);
+}
 
 // Stream-K geometry of an x6p persistent launch: the tiles (row-major) are dealt to the 8 XCDs in
 // contiguous ranges; XCD x's P = grid / 8 workgroups (blockIdx b: XCD b % 8, rank b / 8) share
@@ -296,6 +339,51 @@ struct X6Stage {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         r[i][j] = *reinterpret_cast<const floatx4*>(src + roff[i][j] + (k0 + 4 * kq));
+    }
+  }
+  // convolution rows of a k-contiguous operand (GATH 3): roff[i][j] = cv_row of piece row (i, j);
+  // load_rows then takes cv_seg(k0) for k0 (a K step never straddles a segment)
+  __device__ static void conv_rows(const X6Args& g, int row0, int t, int64_t (&roff)[kPer][4]) {
+    static_assert(KC, "convolution rows are for a k-contiguous operand");
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int p = t + NT * i;
+      int rq, kq;
+      piece_of(p < kPieces ? p : 0, rq, kq);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) roff[i][j] = x6_cv_row(g, row0 + 4 * rq + j);
+    }
+  }
+  // row-contiguous operand whose K index is a convolution row (GATH 4): B(n, k) =
+  // src[cv_row(k) + cv_seg(n)]; nseg[i] = cv_seg of piece i's 4 columns (one segment: cv_gseg %
+  // 4 == 0), ptab[p] = qy cv_ys + qx cv_xs of the p-th pixel of an image (LDS)
+  __device__ static void conv_cols(const X6Args& g, int row0, int t, int64_t (&nseg)[kPer]) {
+    static_assert(!KC, "convolution K rows are for a row-contiguous operand");
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int p = t + NT * i;
+      int rq, kq;
+      piece_of(p < kPieces ? p : 0, rq, kq);
+      nseg[i] = x6_cv_seg(g, row0 + 4 * rq);
+    }
+  }
+  __device__ static void load_conv_k(const float* __restrict__ src, const X6Args& g,
+                                     const int64_t (&nseg)[kPer], const int32_t* ptab, int k0,
+                                     int t, floatx4 (&r)[kPer][4]) {
+    const int qhw = g.cv_qh * g.cv_qw;
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int p = t + NT * i;
+      if (kPieces % NT != 0 && p >= kPieces) continue;
+      int rq, kq;
+      piece_of(p, rq, kq);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int kk = k0 + 4 * kq + j;
+        const int b = x6_udiv(kk, qhw);
+        const int64_t off = b * g.cv_sb + ptab[kk - b * qhw];
+        r[i][j] = *reinterpret_cast<const floatx4*>(src + off + nseg[i]);
+      }
     }
   }
   // row-contiguous operand whose K index (a sample row) picks a gathered source row:
@@ -495,12 +583,24 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
   const uint64_t bits_in = g.mbits_in ? g.mbits_in[tile_id * NT + t] : 0;
 
   // operand loads of K step k0 into a register set (GATH: through the gathered row offsets)
-  static_assert(GATH == 0 || (GATH == 1 && AKC) || (GATH == 2 && !BKC && !BPL), "gather modes");
-  int64_t roffA[GATH == 1 ? SA::kPer : 1][4];
+  static_assert(GATH == 0 || (GATH == 1 && AKC) || (GATH == 2 && !BKC && !BPL) ||
+                    (GATH == 3 && AKC && !BPL) || (GATH == 4 && !BKC && !BPL),
+                "gather modes");
+  int64_t roffA[(GATH == 1 || GATH == 3) ? SA::kPer : 1][4];
+  int64_t nsegB[GATH == 4 ? SB::kPer : 1];
   int64_t coffB = 0;
   if constexpr (GATH == 1) {
     const int seg = static_cast<int>((static_cast<int64_t>(kb) * kX6BK) / g.gseg);
     SA::gather_rows(g.gidx, g.gw, seg, g.gseg, g.sam, m0, t, roffA);
+  } else if constexpr (GATH == 3) {
+    SA::conv_rows(g, m0, t, roffA);
+  } else if constexpr (GATH == 4) {
+    SB::conv_cols(g, n0, t, nsegB);
+    for (int p = t; p < g.cv_qh * g.cv_qw; p += NT) {
+      const int qy = p / g.cv_qw;
+      gtbl[p] = static_cast<int32_t>(qy * g.cv_ys + (p - qy * g.cv_qw) * g.cv_xs);
+    }
+    __syncthreads();
   } else if constexpr (GATH == 2) {
     const int segn = static_cast<int>(n0 / g.gseg);
     coffB = -static_cast<int64_t>(segn) * g.gseg;
@@ -524,6 +624,7 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
   }
   auto loadA = [&](int k0, floatx4 (&r)[SA::kPer][4]) {
     if constexpr (GATH == 1) SA::load_rows(A, roffA, k0, t, r);
+    else if constexpr (GATH == 3) SA::load_rows(A, roffA, static_cast<int>(x6_cv_seg(g, k0)), t, r);
     else if constexpr (kBuf)
       SA::load_buf(bufA, t, static_cast<int32_t>(4 * (AKC ? (k0 - kb * kX6BK)
                                                         : (k0 - kb * kX6BK) * g.sak)), r);
@@ -531,6 +632,7 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
   };
   auto loadB = [&](int k0, floatx4 (&r)[SB::kPer][4]) {
     if constexpr (GATH == 2) SB::load_ktbl(B, g.sbk, gtbl, kb * kX6BK, coffB, n0, k0, t, r);
+    else if constexpr (GATH == 4) SB::load_conv_k(B, g, nsegB, gtbl, k0, t, r);
     else if constexpr (kBuf)
       SB::load_buf(bufB, t, static_cast<int32_t>(4 * (BKC ? (k0 - kb * kX6BK)
                                                         : (k0 - kb * kX6BK) * g.sbk)), r);
@@ -978,6 +1080,22 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
     return;
   }
   static_assert(FM * FN * 4 <= 64, "one 64-bit mask word per thread and tile");
+  // output row offsets: r ldc, or a convolution stride class's rows (GATH 3, cv_out)
+  int64_t orow[FM][4];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = wr0 + 16 * i + 4 * fc + r;
+      orow[i][r] = static_cast<int64_t>(row) * g.ldc;
+      if constexpr (GATH == 3) {
+        if (g.cv_out) {
+          int b, qy, qx;
+          x6_cv_split(g, row, b, qy, qx);
+          orow[i][r] = b * g.co_sb + qy * g.co_ys + qx * g.co_xs + g.co_off;
+        }
+      }
+    }
   uint64_t bits = 0;
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
@@ -987,11 +1105,10 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
     for (int i = 0; i < FM; ++i) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int64_t row = wr0 + 16 * i + 4 * fc + r;
         float v = LO ? hi[i][j][r] + lo[LO ? i : 0][LO ? j : 0][r] : hi[i][j][r];
         if (g.bias) v += bv;
         if (g.relu) v = relu_f(v);
-        Cp[row * g.ldc + col] = v;
+        Cp[orow[i][r] + col] = v;
         bits |= static_cast<uint64_t>(!(v <= 0.f)) << ((i * FN + j) * 4 + r);
       }
     }
@@ -1036,7 +1153,7 @@ template <int FM, int FN, int WGM, int WGN, bool AKC, bool BKC, bool LO, bool PF
 __global__ __launch_bounds__(64 * WGM * WGN, OCPPO_X6_OCC) void gemm_x6_kernel(X6Args g) {
   __shared__ __attribute__((aligned(16)))
   unsigned char lds[x6_lds_bytes<FM, FN, WGM, WGN, AKC, BKC>()];
-  __shared__ int32_t gtbl[GATH == 2 ? kX6GTbl : 1];
+  __shared__ int32_t gtbl[(GATH == 2 || GATH == 4) ? kX6GTbl : 1];
   const int u = x6_remap(blockIdx.x, gridDim.x);
   if (u >= g.units) return;
   x6_unit<FM, FN, WGM, WGN, AKC, BKC, LO, PF2, BPL, GATH, WGE>(
@@ -1611,3 +1728,171 @@ extern "C" int ocppo_gemm_x6_wgrad(ocppo_stream_t stream, const float* a, int64_
   ocppo::wgrad_record(finish, records, static_cast<int>(tiles_m), N, static_cast<int>(K1), dw, db);
   return OCPPO_OK;
 }
+
+// ---------------------------------------------------------------------------------------------
+// ocppo_conv_x6: NHWC convolutions (no padding, square stride) as implicit GEMMs on the x6
+// products (the NatureCNN trunk, cleanrl/architectures/ppo.py:20-31, in the rollout forward at
+// ppo_atari_oc.py:506 and the update at :566-606): no im2col buffer -- the loader reads each
+// operand row's kernel-row segments (KW x C contiguous floats of the NHWC input) straight from the
+// activation (X6Args cv_*). Three products per layer, all deterministic (no atomics; split-K
+// partials summed in split order):
+//   forward      y[r, co] = act(sum_k x(r, k) W[co, k] + b[co])       mode 0, GATH 3
+//   weight grad  dW[co, k] = sum_r gp[r, co] x(r, k)                  mode 1, GATH 4 + sum_parts
+//   data grad    the forward form over the zero-padded gradient with the flipped weight, one
+//                launch per stride class (output rows through cv_out)  mode 0, GATH 3
+// Tiles (FM, FN, WGM, WGN): 0 = 128 x 32 (2 waves), 1 = 32 x 128 (2 waves), 2 = 128 x 64,
+// 3 = 64 x 64, 4 = 64 x 128, 5 = 128 x 128 (4 waves).
+namespace ocppo {
+constexpr X6Tile kConvTiles[] = {{4, 2, 2, 1}, {2, 4, 1, 2}, {4, 2, 2, 2},
+                                 {2, 2, 2, 2}, {2, 4, 2, 2}, {4, 4, 2, 2}};
+
+template <int FM, int FN, int WGM, int WGN, int GATH>
+static void launch_conv_t(hipStream_t s, X6Args& g) {
+  g.tiles_m = g.M / (16 * FM * WGM);
+  g.tiles_n = g.N / (16 * FN * WGN);
+  constexpr bool KC = GATH == 3;  // forward form: both operands k-contiguous; wgrad: neither
+  hipLaunchKernelGGL((gemm_x6_kernel<FM, FN, WGM, WGN, KC, KC, false, true, false, GATH>),
+                     dim3(g.units), dim3(64 * WGM * WGN), 0, s, g);
+}
+
+static bool launch_conv(hipStream_t s, int mode, int tile, X6Args& g) {
+  if (mode == 0) {
+    switch (tile) {
+      case 0: launch_conv_t<4, 2, 2, 1, 3>(s, g); return true;
+      case 2: launch_conv_t<4, 2, 2, 2, 3>(s, g); return true;
+      case 3: launch_conv_t<2, 2, 2, 2, 3>(s, g); return true;
+      case 5: launch_conv_t<4, 4, 2, 2, 3>(s, g); return true;
+      default: return false;
+    }
+  }
+  switch (tile) {
+    case 1: launch_conv_t<2, 4, 1, 2, 4>(s, g); return true;
+    case 3: launch_conv_t<2, 2, 2, 2, 4>(s, g); return true;
+    case 4: launch_conv_t<2, 4, 2, 2, 4>(s, g); return true;
+    case 5: launch_conv_t<4, 4, 2, 2, 4>(s, g); return true;
+    default: return false;
+  }
+}
+
+// out[e] = sum_s part[s n + e] for any S: 16 groups of 64 lanes per 64 outputs, group q adding
+// splits [q S / 16, (q + 1) S / 16) in order in f64, the groups added in order (fixed: bitwise
+// reproducible), one f32 rounding
+constexpr int kSumGroups = 16;
+__global__ __launch_bounds__(64 * kSumGroups) void sum_parts_kernel(const float* __restrict__ part,
+                                                                    int S, int64_t n,
+                                                                    float* __restrict__ out) {
+  __shared__ double red[kSumGroups][64];
+  const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int64_t e = static_cast<int64_t>(blockIdx.x) * 64 + lane;
+  const int s0 = q * S / kSumGroups, s1 = (q + 1) * S / kSumGroups;
+  double acc = 0.0;
+  if (e < n) {
+#pragma unroll 8
+    for (int sp = s0; sp < s1; ++sp) acc += static_cast<double>(part[static_cast<int64_t>(sp) * n + e]);
+  }
+  red[q][lane] = acc;
+  __syncthreads();
+  if (q == 0 && e < n) {
+    double v = red[0][lane];
+#pragma unroll
+    for (int r = 1; r < kSumGroups; ++r) v += red[r][lane];
+    out[e] = static_cast<float>(v);
+  }
+}
+
+}  // namespace ocppo
+
+extern "C" int ocppo_conv_x6(ocppo_stream_t stream, int mode, const float* x, const int64_t* geom,
+                             const float* w, int64_t ldw, float* c, int64_t ldc, int64_t M,
+                             int64_t N, int64_t K, int64_t splits, const float* bias, int relu,
+                             const int64_t* out_geom, int tile, float* out) {
+  OCPPO_REQUIRE(mode == 0 || mode == 1, "ocppo_conv_x6: mode %d (0 rows, 1 weight gradient)", mode);
+  OCPPO_REQUIRE(tile >= 0 && tile < 6, "ocppo_conv_x6: tile %d", tile);
+  OCPPO_REQUIRE(x && geom && w && c, "ocppo_conv_x6: null pointer");
+  const int64_t qh = geom[0], qw = geom[1], sb = geom[2], ys = geom[3], xs = geom[4],
+                segs = geom[5], gseg = geom[6];
+  const X6Tile tc = kConvTiles[tile];
+  const int64_t bm = 16 * tc.fm * tc.wgm, bn = 16 * tc.fn * tc.wgn;
+  OCPPO_REQUIRE(M >= bm && N >= bn && M % bm == 0 && N % bn == 0 && K >= kX6BK && K % kX6BK == 0 &&
+                    splits >= 1 && K / kX6BK >= splits && M <= INT32_MAX && N <= INT32_MAX &&
+                    K <= INT32_MAX,
+                "ocppo_conv_x6: bad sizes M=%lld N=%lld K=%lld splits=%lld (tile %lld x %lld)",
+                (long long)M, (long long)N, (long long)K, (long long)splits, (long long)bm,
+                (long long)bn);
+  OCPPO_REQUIRE(qh >= 1 && qw >= 1 && gseg >= 4 && gseg % 4 == 0 && sb % 4 == 0 && ys % 4 == 0 &&
+                    xs % 4 == 0 && segs % 4 == 0 && sb >= 0 && ys >= 0 && xs >= 0 && segs >= 0,
+                "ocppo_conv_x6: bad geometry (qh %lld qw %lld sb %lld ys %lld xs %lld segs %lld "
+                "gseg %lld: strides multiples of 4 floats)", (long long)qh, (long long)qw,
+                (long long)sb, (long long)ys, (long long)xs, (long long)segs, (long long)gseg);
+  OCPPO_REQUIRE(reinterpret_cast<uintptr_t>(x) % 16 == 0 && reinterpret_cast<uintptr_t>(w) % 16 == 0,
+                "ocppo_conv_x6: x and w must be 16-B aligned");
+  const int64_t rows = mode == 0 ? M : K;  // the convolution rows (b, qy, qx)
+  OCPPO_REQUIRE(rows % (qh * qw) == 0 && rows < (int64_t{1} << 24),
+                "ocppo_conv_x6: %lld rows: a whole number of %lld x %lld images, < 2^24",
+                (long long)rows, (long long)qh, (long long)qw);
+  X6Args g{};
+  g.M = (int)M;
+  g.N = (int)N;
+  g.K = (int)K;
+  g.splits = (int)splits;
+  g.units = (int)(splits * (M / bm) * (N / bn));
+  g.cv_qh = (int)qh;
+  g.cv_qw = (int)qw;
+  g.cv_sb = sb;
+  g.cv_ys = ys;
+  g.cv_xs = xs;
+  g.cv_segs = segs;
+  g.cv_gseg = (int)gseg;
+  if (mode == 0) {
+    // A = x gathered, B = W [N, K] (row stride ldw), C [M, N] (ldc) or a stride class's rows
+    OCPPO_REQUIRE(gseg % kX6BK == 0 && ldw >= K && ldw % 4 == 0 && splits == 1 && ldc >= N,
+                  "ocppo_conv_x6: the rows form needs kernel-row segments of a multiple of 32, "
+                  "a k-contiguous W (ldw %lld >= K, %% 4), splits == 1, ldc >= N", (long long)ldw);
+    g.a = x;
+    g.sak = 1;
+    g.b = w;
+    g.sbn = ldw;
+    g.sbk = 1;
+    g.c = c;
+    g.ldc = ldc;
+    g.bias = bias;
+    g.relu = relu ? 1 : 0;
+    if (out_geom) {
+      g.cv_out = 1;
+      g.co_sb = out_geom[0];
+      g.co_ys = out_geom[1];
+      g.co_xs = out_geom[2];
+      g.co_off = out_geom[3];
+    }
+  } else {
+    // A(m = co, k = r) = gp[r ldw + m], B(n, k = r) = x gathered; partials [splits, M, N] in c,
+    // summed in split order into out [M, N]
+    OCPPO_REQUIRE(out && ldw >= M && ldw % 4 == 0 && bias == nullptr && !relu && !out_geom &&
+                      qh * qw <= kX6GTbl && N <= gseg * ((segs > 0) ? (INT32_MAX / segs) : 1),
+                  "ocppo_conv_x6: the weight-gradient form needs out, an m-contiguous gradient "
+                  "(ldw %lld >= M, %% 4), no epilogue, <= %d pixels per image", (long long)ldw,
+                  kX6GTbl);
+    OCPPO_REQUIRE((qh - 1) * ys + (qw - 1) * xs < INT32_MAX, "ocppo_conv_x6: image too large");
+    g.a = w;
+    g.sam = 1;
+    g.sak = ldw;
+    g.b = x;
+    g.sbn = 1;
+    g.c = c;
+    g.ldc = N;
+    g.split_c = M * N;
+  }
+  clear_stale_error();
+  hipStream_t s = as_stream(stream);
+  OCPPO_REQUIRE(launch_conv(s, mode, tile, g), "ocppo_conv_x6: tile %d not built for mode %d",
+                tile, mode);
+  if (int rc = check_launch("ocppo_conv_x6")) return rc;
+  if (mode == 1) {
+    const int64_t n = M * N;
+    hipLaunchKernelGGL(sum_parts_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64 * kSumGroups), 0,
+                       s, c, (int)splits, n, out);
+    return check_launch("ocppo_conv_x6 (sum_parts)");
+  }
+  return OCPPO_OK;
+}
+

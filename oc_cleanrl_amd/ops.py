@@ -687,6 +687,159 @@ def conv2d_act(x, weight, bias=None, stride: int = 1, relu: bool = True, out=Non
     return out
 
 
+# ---- NHWC convolutions as implicit GEMMs on the x6 products (ocppo_conv_x6) ---------------------
+# The NatureCNN trunk (architectures/ppo.py:20-31) without MIOpen: forward, weight gradient and
+# data gradient, deterministic (split-K partials summed in split order), f32-level products.
+_CONV_TILES = {0: (128, 32), 1: (32, 128), 2: (128, 64), 3: (64, 64), 4: (64, 128), 5: (128, 128)}
+
+
+def _conv_fwd_tile(M: int, N: int) -> int | None:
+    for t in ((0,) if N == 32 else (2, 3) if N == 64 else (5, 2, 3)):
+        bm, bn = _CONV_TILES[t]
+        if M % bm == 0 and N % bn == 0:
+            return t
+    return None
+
+
+def _conv_wgrad_tile(M: int, N: int) -> int | None:
+    for t in ((1,) if M == 32 else (4, 3) if M == 64 else (5, 4, 3)):
+        bm, bn = _CONV_TILES[t]
+        if M % bm == 0 and N % bn == 0:
+            return t
+    return None
+
+
+def conv_x6_ok(x, weight, stride: int, wgrad: bool = False, dgrad: bool = False) -> bool:
+    """Shapes ocppo_conv_x6 takes: channels_last f32 x [B, C, H, W] and weight [Cout, C, KH, KW]
+    (square stride, no padding), C % 4 == 0, kernel rows of KW C % 32 == 0 taps, row counts the
+    tiles divide; wgrad / dgrad: also the weight gradient / the data gradient's stride classes."""
+    if not (isinstance(x, torch.Tensor) and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4
+            and weight.dim() == 4 and weight.dtype == torch.float32):
+        return False
+    cl = torch.channels_last
+    if not (x.is_contiguous(memory_format=cl) and weight.is_contiguous(memory_format=cl)):
+        return False
+    B, C, H, W = x.shape
+    Cout, Cw, KH, KW = weight.shape
+    s = int(stride)
+    if Cw != C or C % 4 or (KW * C) % 32 or H < KH or W < KW or (H - KH) % s or (W - KW) % s:
+        return False
+    OH, OW = (H - KH) // s + 1, (W - KW) // s + 1
+    rows = B * OH * OW
+    if rows >= 1 << 24 or _conv_fwd_tile(rows, Cout) is None:
+        return False
+    if wgrad and (OH * OW > 1024 or rows % 32 or _conv_wgrad_tile(Cout, KH * KW * C) is None):
+        return False
+    if dgrad:
+        if KH % s or KW % s or H % s or W % s or Cout % 4 or ((KW // s) * Cout) % 32:
+            return False
+        qrows = B * (H // s) * (W // s)
+        return qrows < 1 << 24 and _conv_fwd_tile(qrows, C) is not None
+    return True
+
+
+def _geom(*v):
+    return (ctypes.c_int64 * len(v))(*[int(t) for t in v])
+
+
+def conv_x6(x, weight, bias=None, stride: int = 1, relu: bool = True, out=None):
+    """act(conv2d(x, weight) + bias) (architectures/ppo.py:20-31's Conv2d + ReLU) on ocppo_conv_x6:
+    channels_last f32 x [B, C, H, W], weight [Cout, C, KH, KW] -> channels_last [B, Cout, OH, OW]
+    (no autograd; agents._ConvX6 is the autograd form)."""
+    if not conv_x6_ok(x, weight, stride):
+        raise ValueError(f"conv_x6: unsupported shapes x {tuple(x.shape)}, weight "
+                         f"{tuple(weight.shape)}, stride {stride} (conv_x6_ok)")
+    B, C, H, W = x.shape
+    Cout, _, KH, KW = weight.shape
+    s = int(stride)
+    OH, OW = (H - KH) // s + 1, (W - KW) // s + 1
+    dev, f = x.device, torch.float32
+    K = KH * KW * C
+    M = B * OH * OW
+    wm = weight.permute(0, 2, 3, 1).reshape(Cout, K)  # a view: [Cout, KH, KW, C] in memory
+    if out is None:
+        out = torch.empty((B, Cout, OH, OW), dtype=f, device=dev, memory_format=torch.channels_last)
+    if tuple(out.shape) != (B, Cout, OH, OW) or not out.is_contiguous(memory_format=torch.channels_last):
+        raise ValueError("conv_x6: out must be a channels_last [B, Cout, OH, OW] tensor")
+    call("ocppo_conv_x6", _stream(dev), 0, x.data_ptr(),
+         _geom(OH, OW, H * W * C, s * W * C, s * C, W * C, KW * C), wm.data_ptr(), K,
+         out.data_ptr(), Cout, M, Cout, K, 1, _opt(bias, "bias", f, dev, Cout), int(bool(relu)),
+         None, _conv_fwd_tile(M, Cout), None)
+    return out
+
+
+_CONV_PARTS: dict = {}
+
+
+def conv_x6_wgrad(gp, x, kernel: tuple, stride: int, out=None):
+    """dW of a convolution (channels_last weight layout [Cout, KH, KW, C] as a [Cout, KH KW C]
+    matrix): sum over the output pixels r of gp[r, co] x(r, (ky, kx, c)); gp [B OH OW, Cout] the
+    output gradient's NHWC rows, x the channels_last input. Split-K partials summed in order."""
+    B, C, H, W = x.shape
+    KH, KW = kernel
+    s = int(stride)
+    OH, OW = (H - KH) // s + 1, (W - KW) // s + 1
+    rows, Cout = gp.shape
+    dev, f = x.device, torch.float32
+    if rows != B * OH * OW or not x.is_contiguous(memory_format=torch.channels_last):
+        raise ValueError("conv_x6_wgrad: gp must be [B OH OW, Cout], x channels_last")
+    N = KH * KW * C
+    tile = _conv_wgrad_tile(Cout, N)
+    if tile is None or rows % 32:
+        raise ValueError(f"conv_x6_wgrad: no tile for [{Cout} x {N}] over {rows} rows")
+    bm, bn = _CONV_TILES[tile]
+    tiles = (Cout // bm) * (N // bn)
+    S = max(1, min(rows // 32 // 32, 2048 // tiles))
+    key = (str(dev), S, Cout, N)
+    if key not in _CONV_PARTS:
+        _CONV_PARTS[key] = torch.empty((S, Cout, N), dtype=f, device=dev)
+    part = _CONV_PARTS[key]
+    if out is None:
+        out = torch.empty((Cout, N), dtype=f, device=dev)
+    if out.numel() != Cout * N or not out.is_contiguous(memory_format=torch.channels_last
+                                                        if out.dim() == 4 else torch.contiguous_format):
+        raise ValueError("conv_x6_wgrad: out must hold [Cout, KH KW C] contiguously")
+    call("ocppo_conv_x6", _stream(dev), 1, x.data_ptr(),
+         _geom(OH, OW, H * W * C, s * W * C, s * C, W * C, KW * C),
+         _check(gp, "gp", f, dev), Cout, part.data_ptr(), N, Cout, N, rows, S, None, 0, None, tile,
+         out.data_ptr())
+    return out
+
+
+def conv_x6_dgrad(gp, weight, stride: int, in_hw: tuple, out=None):
+    """dX of a convolution: gp channels_last [B, Cout, OH, OW] (the output gradient), weight
+    [Cout, C, KH, KW] -> channels_last [B, C, H, W]. Per stride class (py, px) a forward-form
+    product over gp zero-padded by KH / s - 1 with that class's taps flipped; each input pixel
+    gets its <= (KH / s)^2 taps in one fixed order (deterministic)."""
+    B, Cout, OH, OW = gp.shape
+    _, C, KH, KW = weight.shape
+    H, W = in_hw
+    s = int(stride)
+    T, TW = KH // s, KW // s
+    dev, f = gp.device, torch.float32
+    g = gp.permute(0, 2, 3, 1)  # NHWC view
+    if not g.is_contiguous():
+        g = g.contiguous()
+    gpad = torch.nn.functional.pad(g, (0, 0, TW - 1, TW - 1, T - 1, T - 1))
+    Hp, Wp = OH + 2 * (T - 1), OW + 2 * (TW - 1)
+    QH, QW = H // s, W // s
+    M, K = B * QH * QW, T * TW * Cout
+    tile = _conv_fwd_tile(M, C)
+    if out is None:
+        out = torch.empty((B, C, H, W), dtype=f, device=dev, memory_format=torch.channels_last)
+    if tuple(out.shape) != (B, C, H, W) or not out.is_contiguous(memory_format=torch.channels_last):
+        raise ValueError("conv_x6_dgrad: out must be a channels_last [B, C, H, W] tensor")
+    geom = _geom(QH, QW, Hp * Wp * Cout, Wp * Cout, Cout, Wp * Cout, TW * Cout)
+    for py in range(s):
+        for px in range(s):
+            # class taps ky = py + s t, flipped (t' = T - 1 - t), as [C, T, TW, Cout] rows
+            wc = weight[:, :, py::s, px::s].flip(2, 3).permute(1, 2, 3, 0).contiguous()
+            og = None if s == 1 else _geom(H * W * C, s * W * C, s * C, (py * W + px) * C)
+            call("ocppo_conv_x6", _stream(dev), 0, gpad.data_ptr(), geom, wc.data_ptr(), K,
+                 out.data_ptr(), C, M, C, K, 1, None, 0, og, tile, None)
+    return out
+
+
 def linear2_act(x, w1, b1, w2, b2, relu1: bool = True, relu2: bool = True, out=None):
     """y = act2(act1(x @ w1.T + b1) @ w2.T + b2) in ONE launch for rollout-sized batches (no
     autograd): x [M, K1] f32 (unit column stride, K1 <= 64), w1 [N1, K1], w2 [N2, N1]

@@ -259,3 +259,53 @@ def test_config3_full_size_captured_update_matches_eager(dev):
     print(f"config 3 full size: captured vs eager max |diff| {diff:.3g} (bitwise: "
           f"{bool(torch.equal(opt.params, eager))}); largest parameter step {step:.3g}")
     assert step > 0 and diff <= 0.01 * LR
+
+
+def test_config3_deterministic_captured_update_is_bitwise_eager(dev):
+    """Config 3 at the reference's default torch_deterministic=True (ppo_atari_oc.py:200-211):
+    the convolutions run on this package's implicit GEMMs (agents._ConvX6, ops.conv_x6: no
+    MIOpen, no atomics), so the captured update epoch is BITWISE the eager one, and two eager
+    runs from the same start are bitwise equal."""
+    from oc_cleanrl_amd import agents, ops
+    from oc_cleanrl_amd.args import Args, finalize
+    from oc_cleanrl_amd.trainer import PPOTrainer
+
+    assert agents.CONV_X6
+    args = finalize(Args(env_id="ALE/Breakout-v5", obs_mode="dqn", architecture="PPO",
+                         num_envs=256, num_steps=128, update_epochs=1, save_model=False,
+                         torch_deterministic=True, cuda_graphs=False), 1)
+    tr = PPOTrainer(args, dev)
+    assert tr.M == 8192
+    convs = [m for m in tr.agent.modules() if isinstance(m, torch.nn.Conv2d)]
+    x = torch.empty(8192, 4, 84, 84, device=dev).contiguous(memory_format=torch.channels_last)
+    for i, m in enumerate(convs):  # every layer of the update takes the x6 path
+        assert ops.conv_x6_ok(x, m.weight, m.stride[0], wgrad=True, dgrad=i > 0)
+        x = torch.empty(8192, m.out_channels, (x.shape[2] - m.kernel_size[0]) // m.stride[0] + 1,
+                        (x.shape[3] - m.kernel_size[1]) // m.stride[1] + 1, device=dev
+                        ).contiguous(memory_format=torch.channels_last)
+    tr._rollout()
+    tr._prepare_minibatches()
+    opt = tr.optimizer
+    keep = (opt.params, opt.exp_avg, opt.exp_avg_sq, opt.scalars)
+    state0 = [t.clone() for t in keep]
+    tr._update_epoch(0)
+    torch.cuda.synchronize()
+    eager = opt.params.clone()
+    for t, s in zip(keep, state0):
+        t.copy_(s)
+    tr._update_epoch(0)
+    torch.cuda.synchronize()
+    assert torch.equal(opt.params, eager), "two eager update epochs differ"
+    for t, s in zip(keep, state0):
+        t.copy_(s)
+    g = torch.cuda.CUDAGraph()
+    torch.cuda.synchronize()
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        tr._update_epoch(0)
+    for t, s in zip(keep, state0):
+        t.copy_(s)
+    g.replay()
+    torch.cuda.synchronize()
+    step = float((eager - state0[0]).abs().max())
+    assert step > 0
+    assert torch.equal(opt.params, eager), float((opt.params - eager).abs().max())

@@ -1,0 +1,125 @@
+"""ocppo_conv_x6: the NatureCNN convolutions (cleanrl/architectures/ppo.py:20-31) as implicit GEMMs
+on the x6 products — forward (+ bias + ReLU), weight gradient and data gradient (include/ocppo.h).
+
+Accuracy against a float64 convolution on the host, scaled by the same convolution of |x| and |w|
+(the bound an f32 dot product's rounding obeys), next to MIOpen's own f32 convolution on the same
+operands; determinism as bitwise-equal repeats (the reference runs with
+torch.use_deterministic_algorithms(True), ppo_atari_oc.py:200-211)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oc_cleanrl_amd import ops
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda:0")
+CL = torch.channels_last
+
+# (B, C, H, Cout, K, stride): the NatureCNN layers at batches whose row counts the tiles divide
+LAYERS = {
+    "conv1": (16, 4, 84, 32, 8, 4),
+    "conv2": (128, 32, 20, 64, 4, 2),
+    "conv3": (128, 64, 9, 64, 3, 1),
+}
+
+
+def _operands(name, seed=0):
+    B, C, H, Cout, K, s = LAYERS[name]
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    x = torch.rand(B, C, H, H, device=DEV, generator=g).contiguous(memory_format=CL)
+    w = ((torch.rand(Cout, C, K, K, device=DEV, generator=g) * 2 - 1) / (C * K * K) ** 0.5
+         ).contiguous(memory_format=CL)
+    b = (torch.rand(Cout, device=DEV, generator=g) * 2 - 1) * 0.1
+    return x, w, b, s
+
+
+def _rel(y, ref, scale):
+    d = (y.double().cpu() - ref).abs() / scale.clamp_min(1e-300)
+    return float(d.max()), float(d.mean())
+
+
+def _check(y, ref, scale, lib):
+    mx, mean = _rel(y, ref, scale)
+    lmx, lmean = _rel(lib, ref, scale)
+    # f32 level (units of 2^-24 of sum |x w|), and on average no worse than MIOpen's f32
+    # convolution (tolerance for its different summation order)
+    assert mx <= 1e-6, (mx, lmx)
+    assert mean <= 2.0 * lmean + 1e-9, (mean, lmean)
+
+
+@pytest.mark.parametrize("name", list(LAYERS))
+@pytest.mark.parametrize("relu", [True, False])
+def test_forward_bias_relu(name, relu):
+    x, w, b, s = _operands(name)
+    assert ops.conv_x6_ok(x, w, s)
+    y = ops.conv_x6(x, w, b, s, relu)
+    assert y.is_contiguous(memory_format=CL)
+    x64, w64, b64 = x.double().cpu(), w.double().cpu(), b.double().cpu()
+    ref = F.conv2d(x64, w64, b64, stride=s)
+    scale = F.conv2d(x64.abs(), w64.abs(), b64.abs(), stride=s)
+    lib = F.conv2d(x, w, b, stride=s)
+    if relu:
+        ref, lib = ref.clamp_min(0), lib.clamp_min(0)
+    _check(y, ref, scale, lib)
+    assert torch.equal(y, ops.conv_x6(x, w, b, s, relu))  # deterministic
+
+
+@pytest.mark.parametrize("name", list(LAYERS))
+def test_weight_gradient(name):
+    x, w, _, s = _operands(name, 1)
+    Cout, C, K, _ = w.shape
+    OH = (x.shape[2] - K) // s + 1
+    g = torch.Generator(device=DEV).manual_seed(2)
+    gp = (torch.rand(x.shape[0], Cout, OH, OH, device=DEV, generator=g) * 2 - 1
+          ).contiguous(memory_format=CL)
+    rows = gp.permute(0, 2, 3, 1).reshape(-1, Cout)
+    assert ops.conv_x6_ok(x, w, s, wgrad=True)
+    dw = ops.conv_x6_wgrad(rows, x, (K, K), s)  # [Cout, K K C]
+    dw = dw.view(Cout, K, K, C).permute(0, 3, 1, 2)
+    x64, gp64 = x.double().cpu(), gp.double().cpu()
+    ref = torch.nn.grad.conv2d_weight(x64, w.shape, gp64, stride=s)
+    scale = torch.nn.grad.conv2d_weight(x64.abs(), w.shape, gp64.abs(), stride=s)
+    lib = torch.nn.grad.conv2d_weight(x, w.shape, gp, stride=s)
+    _check(dw, ref, scale, lib)
+    dw2 = ops.conv_x6_wgrad(rows, x, (K, K), s).view(Cout, K, K, C).permute(0, 3, 1, 2)
+    assert torch.equal(dw, dw2)  # deterministic: split partials summed in order
+
+
+@pytest.mark.parametrize("name", ["conv2", "conv3"])
+def test_data_gradient(name):
+    x, w, _, s = _operands(name, 3)
+    Cout, C, K, _ = w.shape
+    H = x.shape[2]
+    OH = (H - K) // s + 1
+    g = torch.Generator(device=DEV).manual_seed(4)
+    gp = (torch.rand(x.shape[0], Cout, OH, OH, device=DEV, generator=g) * 2 - 1
+          ).contiguous(memory_format=CL)
+    assert ops.conv_x6_ok(x, w, s, dgrad=True)
+    dx = ops.conv_x6_dgrad(gp, w, s, (H, H))
+    assert dx.is_contiguous(memory_format=CL)
+    w64, gp64 = w.double().cpu(), gp.double().cpu()
+    ref = torch.nn.grad.conv2d_input(x.shape, w64, gp64, stride=s)
+    scale = torch.nn.grad.conv2d_input(x.shape, w64.abs(), gp64.abs(), stride=s)
+    lib = torch.nn.grad.conv2d_input(x.shape, w, gp, stride=s)
+    _check(dx, ref, scale, lib)
+    assert torch.equal(dx, ops.conv_x6_dgrad(gp, w, s, (H, H)))
+
+
+def test_config3_minibatch_shapes_are_taken():
+    """Every layer of config 3's update (minibatch 8192) and rollout (256 envs) forward fits."""
+    for B in (8192, 256):
+        for name, (_, C, H, Cout, K, s) in LAYERS.items():
+            x = torch.empty(B, C, H, H, device=DEV).contiguous(memory_format=CL)
+            w = torch.empty(Cout, C, K, K, device=DEV).contiguous(memory_format=CL)
+            assert ops.conv_x6_ok(x, w, s), (B, name)
+            if B == 8192:
+                assert ops.conv_x6_ok(x, w, s, wgrad=True, dgrad=name != "conv1"), name
+
+
+def test_rejects_bad_shapes():
+    x, w, b, s = _operands("conv2")
+    with pytest.raises(ValueError):
+        ops.conv_x6(x.contiguous(), w, b, s)  # NCHW x
+    with pytest.raises(ValueError):
+        ops.conv_x6(x[:3].contiguous(memory_format=CL), w, b, s)  # 243 rows: no tile divides
