@@ -478,11 +478,14 @@ OCPPO_API int ocppo_gemm_x6_gather(ocppo_stream_t stream, const float* a, int64_
  *   mode 0 (forward; and each stride class of the data gradient, over the zero-padded output
  *          gradient with the flipped weight): c[row(r) + n] = act(sum_k x(r, k) w[n ldw + k] +
  *          bias[n]) for r < M = B qh qw, n < N, k < K; gseg % 32 == 0; splits == 1; row(r) =
- *          r ldc, or b sb' + qy ys' + qx xs' + off' with out_geom = {sb', ys', xs', off'}.
+ *          r ldc, or b sb' + qy ys' + qx xs' + off' with out_geom = {sb', ys', xs', off', cw,
+ *          cs, cy, cx}, column n then at row(r) + (c / cs) cy + (c % cs) cx + n % cw, c = n / cw
+ *          (all stride classes of a data gradient in one product: they read the same rows).
  *   mode 1 (weight gradient): out[m, n] = sum_r w[r ldw + m] x(r, n) (w = the output gradient
  *          [rows, ldw], m < M = Cout, n < N = KH KW C, r < K = B qh qw); c = split partials
  *          [splits, M, N], then summed in split order (f64, one rounding) into out; qh qw <= 1024.
- * tile: 0 = 128 x 32, 2 = 128 x 64, 3 = 64 x 64, 5 = 128 x 128 (mode 0); 1 = 32 x 128, 3, 4 =
+ * tile: 0 = 128 x 32, 2 = 128 x 64, 3 = 64 x 64, 5 = 128 x 128, 6 = 32 x 64 (mode 0); 1 =
+ * 32 x 128, 3, 4 =
  * 64 x 128, 5 (mode 1); M, N multiples of it; K % 32 == 0, K / 32 >= splits.
  * ------------------------------------------------------------------------------------------- */
 OCPPO_API int ocppo_conv_x6(ocppo_stream_t stream, int mode, const float* x, const int64_t* geom,

@@ -119,10 +119,15 @@ struct X6Args {
   // data gradient, k-contiguous within a segment); GATH 4: B's K index (weight gradient, B(n, k) =
   // x[cv_row(k) + cv_seg(n)]). cv_out: C row r written at b co_sb + qy co_ys + qx co_xs + co_off
   // (GATH 3: one stride class of a strided convolution's data gradient) instead of r ldc.
+  // Output columns (cv_out): column n = (class c, channel n % co_cw) of a strided convolution's
+  // data gradient, c = (py, px) with py = c / co_cs, px = c % co_cs, at offset py co_cy + px co_cx
+  // + n % co_cw from the row's (all stride classes read the same gradient rows: one product)
   int cv_qh, cv_qw;
   int64_t cv_sb, cv_ys, cv_xs, cv_segs;
   int cv_gseg, cv_out;
   int64_t co_sb, co_ys, co_xs, co_off;
+  int co_cw, co_cs;
+  int64_t co_cy, co_cx;
 };
 
 // q = x / d for 0 <= x < 2^24, d >= 1 (f32 reciprocal estimate, corrected to the exact quotient)
@@ -367,22 +372,42 @@ struct X6Stage {
       nseg[i] = x6_cv_seg(g, row0 + 4 * rq);
     }
   }
+  // the (image, pixel) of each of this thread's K rows at step k0 (load_conv_k then walks them
+  // one K step of 32 rows per call: the loads of a unit are issued for consecutive steps)
+  __device__ static void conv_k_state(const X6Args& g, int k0, int t, int (&cb)[kPer][4],
+                                      int (&cp)[kPer][4]) {
+    const int qhw = g.cv_qh * g.cv_qw;
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int p = t + NT * i;
+      int rq, kq;
+      piece_of(p < kPieces ? p : 0, rq, kq);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int kk = k0 + 4 * kq + j;
+        cb[i][j] = x6_udiv(kk, qhw);
+        cp[i][j] = kk - cb[i][j] * qhw;
+      }
+    }
+  }
   __device__ static void load_conv_k(const float* __restrict__ src, const X6Args& g,
-                                     const int64_t (&nseg)[kPer], const int32_t* ptab, int k0,
-                                     int t, floatx4 (&r)[kPer][4]) {
+                                     const int64_t (&nseg)[kPer], const int32_t* ptab,
+                                     int (&cb)[kPer][4], int (&cp)[kPer][4], int t,
+                                     floatx4 (&r)[kPer][4]) {
     const int qhw = g.cv_qh * g.cv_qw;
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
       const int p = t + NT * i;
       if (kPieces % NT != 0 && p >= kPieces) continue;
-      int rq, kq;
-      piece_of(p, rq, kq);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int kk = k0 + 4 * kq + j;
-        const int b = x6_udiv(kk, qhw);
-        const int64_t off = b * g.cv_sb + ptab[kk - b * qhw];
+        const int64_t off = cb[i][j] * g.cv_sb + ptab[cp[i][j]];
         r[i][j] = *reinterpret_cast<const floatx4*>(src + off + nseg[i]);
+        cp[i][j] += kX6BK;  // the next step's row
+        while (cp[i][j] >= qhw) {
+          cp[i][j] -= qhw;
+          ++cb[i][j];
+        }
       }
     }
   }
@@ -588,6 +613,7 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
                 "gather modes");
   int64_t roffA[(GATH == 1 || GATH == 3) ? SA::kPer : 1][4];
   int64_t nsegB[GATH == 4 ? SB::kPer : 1];
+  int cbB[GATH == 4 ? SB::kPer : 1][4], cpB[GATH == 4 ? SB::kPer : 1][4];
   int64_t coffB = 0;
   if constexpr (GATH == 1) {
     const int seg = static_cast<int>((static_cast<int64_t>(kb) * kX6BK) / g.gseg);
@@ -596,6 +622,7 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
     SA::conv_rows(g, m0, t, roffA);
   } else if constexpr (GATH == 4) {
     SB::conv_cols(g, n0, t, nsegB);
+    SB::conv_k_state(g, kb * kX6BK, t, cbB, cpB);
     for (int p = t; p < g.cv_qh * g.cv_qw; p += NT) {
       const int qy = p / g.cv_qw;
       gtbl[p] = static_cast<int32_t>(qy * g.cv_ys + (p - qy * g.cv_qw) * g.cv_xs);
@@ -632,7 +659,7 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
   };
   auto loadB = [&](int k0, floatx4 (&r)[SB::kPer][4]) {
     if constexpr (GATH == 2) SB::load_ktbl(B, g.sbk, gtbl, kb * kX6BK, coffB, n0, k0, t, r);
-    else if constexpr (GATH == 4) SB::load_conv_k(B, g, nsegB, gtbl, k0, t, r);
+    else if constexpr (GATH == 4) SB::load_conv_k(B, g, nsegB, gtbl, cbB, cpB, t, r);  // k0: next
     else if constexpr (kBuf)
       SB::load_buf(bufB, t, static_cast<int32_t>(4 * (BKC ? (k0 - kb * kX6BK)
                                                         : (k0 - kb * kX6BK) * g.sbk)), r);
@@ -1101,6 +1128,13 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
   for (int j = 0; j < FN; ++j) {
     const int col = wc0 + 16 * j + fr;
     const float bv = g.bias ? g.bias[col] : 0.f;
+    int64_t ocol = col;
+    if constexpr (GATH == 3) {
+      if (g.cv_out) {
+        const int c = col / g.co_cw, py = c / g.co_cs;
+        ocol = py * g.co_cy + (c - py * g.co_cs) * g.co_cx + (col - c * g.co_cw);
+      }
+    }
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
 #pragma unroll
@@ -1108,7 +1142,7 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
         float v = LO ? hi[i][j][r] + lo[LO ? i : 0][LO ? j : 0][r] : hi[i][j][r];
         if (g.bias) v += bv;
         if (g.relu) v = relu_f(v);
-        Cp[orow[i][r] + col] = v;
+        Cp[orow[i][r] + ocol] = v;
         bits |= static_cast<uint64_t>(!(v <= 0.f)) << ((i * FN + j) * 4 + r);
       }
     }
@@ -1741,10 +1775,11 @@ extern "C" int ocppo_gemm_x6_wgrad(ocppo_stream_t stream, const float* a, int64_
 //   data grad    the forward form over the zero-padded gradient with the flipped weight, one
 //                launch per stride class (output rows through cv_out)  mode 0, GATH 3
 // Tiles (FM, FN, WGM, WGN): 0 = 128 x 32 (2 waves), 1 = 32 x 128 (2 waves), 2 = 128 x 64,
-// 3 = 64 x 64, 4 = 64 x 128, 5 = 128 x 128 (4 waves).
+// 3 = 64 x 64, 4 = 64 x 128, 5 = 128 x 128 (4 waves), 6 = 32 x 64 (2 waves: the rollout's few
+// hundred rows per image batch still fill the CUs).
 namespace ocppo {
-constexpr X6Tile kConvTiles[] = {{4, 2, 2, 1}, {2, 4, 1, 2}, {4, 2, 2, 2},
-                                 {2, 2, 2, 2}, {2, 4, 2, 2}, {4, 4, 2, 2}};
+constexpr X6Tile kConvTiles[] = {{4, 2, 2, 1}, {2, 4, 1, 2}, {4, 2, 2, 2}, {2, 2, 2, 2},
+                                 {2, 4, 2, 2}, {4, 4, 2, 2}, {2, 2, 1, 2}};
 
 template <int FM, int FN, int WGM, int WGN, int GATH>
 static void launch_conv_t(hipStream_t s, X6Args& g) {
@@ -1762,6 +1797,7 @@ static bool launch_conv(hipStream_t s, int mode, int tile, X6Args& g) {
       case 2: launch_conv_t<4, 2, 2, 2, 3>(s, g); return true;
       case 3: launch_conv_t<2, 2, 2, 2, 3>(s, g); return true;
       case 5: launch_conv_t<4, 4, 2, 2, 3>(s, g); return true;
+      case 6: launch_conv_t<2, 2, 1, 2, 3>(s, g); return true;
       default: return false;
     }
   }
@@ -1807,7 +1843,7 @@ extern "C" int ocppo_conv_x6(ocppo_stream_t stream, int mode, const float* x, co
                              int64_t N, int64_t K, int64_t splits, const float* bias, int relu,
                              const int64_t* out_geom, int tile, float* out) {
   OCPPO_REQUIRE(mode == 0 || mode == 1, "ocppo_conv_x6: mode %d (0 rows, 1 weight gradient)", mode);
-  OCPPO_REQUIRE(tile >= 0 && tile < 6, "ocppo_conv_x6: tile %d", tile);
+  OCPPO_REQUIRE(tile >= 0 && tile < 7, "ocppo_conv_x6: tile %d", tile);
   OCPPO_REQUIRE(x && geom && w && c, "ocppo_conv_x6: null pointer");
   const int64_t qh = geom[0], qw = geom[1], sb = geom[2], ys = geom[3], xs = geom[4],
                 segs = geom[5], gseg = geom[6];
@@ -1845,7 +1881,8 @@ extern "C" int ocppo_conv_x6(ocppo_stream_t stream, int mode, const float* x, co
   g.cv_gseg = (int)gseg;
   if (mode == 0) {
     // A = x gathered, B = W [N, K] (row stride ldw), C [M, N] (ldc) or a stride class's rows
-    OCPPO_REQUIRE(gseg % kX6BK == 0 && ldw >= K && ldw % 4 == 0 && splits == 1 && ldc >= N,
+    OCPPO_REQUIRE(gseg % kX6BK == 0 && ldw >= K && ldw % 4 == 0 && splits == 1 &&
+                      (out_geom != nullptr || ldc >= N),
                   "ocppo_conv_x6: the rows form needs kernel-row segments of a multiple of 32, "
                   "a k-contiguous W (ldw %lld >= K, %% 4), splits == 1, ldc >= N", (long long)ldw);
     g.a = x;
@@ -1863,6 +1900,14 @@ extern "C" int ocppo_conv_x6(ocppo_stream_t stream, int mode, const float* x, co
       g.co_ys = out_geom[1];
       g.co_xs = out_geom[2];
       g.co_off = out_geom[3];
+      g.co_cw = static_cast<int>(out_geom[4]);
+      g.co_cs = static_cast<int>(out_geom[5]);
+      g.co_cy = out_geom[6];
+      g.co_cx = out_geom[7];
+      OCPPO_REQUIRE(g.co_cw >= 1 && g.co_cs >= 1 && N % g.co_cw == 0 &&
+                        N / g.co_cw <= static_cast<int64_t>(g.co_cs) * g.co_cs,
+                    "ocppo_conv_x6: output columns: %lld classes of %d", (long long)(N / g.co_cw),
+                    g.co_cw);
     }
   } else {
     // A(m = co, k = r) = gp[r ldw + m], B(n, k = r) = x gathered; partials [splits, M, N] in c,

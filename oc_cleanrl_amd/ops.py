@@ -690,15 +690,22 @@ def conv2d_act(x, weight, bias=None, stride: int = 1, relu: bool = True, out=Non
 # ---- NHWC convolutions as implicit GEMMs on the x6 products (ocppo_conv_x6) ---------------------
 # The NatureCNN trunk (architectures/ppo.py:20-31) without MIOpen: forward, weight gradient and
 # data gradient, deterministic (split-K partials summed in split order), f32-level products.
-_CONV_TILES = {0: (128, 32), 1: (32, 128), 2: (128, 64), 3: (64, 64), 4: (64, 128), 5: (128, 128)}
+_CONV_TILES = {0: (128, 32), 1: (32, 128), 2: (128, 64), 3: (64, 64), 4: (64, 128), 5: (128, 128),
+               6: (32, 64)}
 
 
 def _conv_fwd_tile(M: int, N: int) -> int | None:
-    for t in ((0,) if N == 32 else (2, 3) if N == 64 else (5, 2, 3)):
+    """The largest tile giving >= 512 workgroups (two per CU), else the one giving the most."""
+    best, units = None, 0
+    for t in ((0,) if N == 32 else (2, 3, 6) if N == 64 else (5, 2, 3, 6)):
         bm, bn = _CONV_TILES[t]
         if M % bm == 0 and N % bn == 0:
-            return t
-    return None
+            u = (M // bm) * (N // bn)
+            if u >= 512:
+                return t
+            if u > units:
+                best, units = t, u
+    return best
 
 
 def _conv_wgrad_tile(M: int, N: int) -> int | None:
@@ -734,7 +741,7 @@ def conv_x6_ok(x, weight, stride: int, wgrad: bool = False, dgrad: bool = False)
         if KH % s or KW % s or H % s or W % s or Cout % 4 or ((KW // s) * Cout) % 32:
             return False
         qrows = B * (H // s) * (W // s)
-        return qrows < 1 << 24 and _conv_fwd_tile(qrows, C) is not None
+        return qrows < 1 << 24 and _conv_fwd_tile(qrows, s * s * C) is not None
     return True
 
 
@@ -824,19 +831,20 @@ def conv_x6_dgrad(gp, weight, stride: int, in_hw: tuple, out=None):
     Hp, Wp = OH + 2 * (T - 1), OW + 2 * (TW - 1)
     QH, QW = H // s, W // s
     M, K = B * QH * QW, T * TW * Cout
-    tile = _conv_fwd_tile(M, C)
+    N = s * s * C  # every stride class's C channels: the classes read the same gradient rows
+    tile = _conv_fwd_tile(M, N)
     if out is None:
         out = torch.empty((B, C, H, W), dtype=f, device=dev, memory_format=torch.channels_last)
     if tuple(out.shape) != (B, C, H, W) or not out.is_contiguous(memory_format=torch.channels_last):
         raise ValueError("conv_x6_dgrad: out must be a channels_last [B, C, H, W] tensor")
-    geom = _geom(QH, QW, Hp * Wp * Cout, Wp * Cout, Cout, Wp * Cout, TW * Cout)
-    for py in range(s):
-        for px in range(s):
-            # class taps ky = py + s t, flipped (t' = T - 1 - t), as [C, T, TW, Cout] rows
-            wc = weight[:, :, py::s, px::s].flip(2, 3).permute(1, 2, 3, 0).contiguous()
-            og = None if s == 1 else _geom(H * W * C, s * W * C, s * C, (py * W + px) * C)
-            call("ocppo_conv_x6", _stream(dev), 0, gpad.data_ptr(), geom, wc.data_ptr(), K,
-                 out.data_ptr(), C, M, C, K, 1, None, 0, og, tile, None)
+    # class (py, px)'s taps ky = py + s t, flipped (t' = T - 1 - t), as [C, T, TW, Cout] rows;
+    # the classes stacked class-major: B = [s s C, K]
+    wc = torch.stack([weight[:, :, py::s, px::s].flip(2, 3).permute(1, 2, 3, 0)
+                      for py in range(s) for px in range(s)]).reshape(N, K)
+    og = None if s == 1 else _geom(H * W * C, s * W * C, s * C, 0, C, s, W * C, C)
+    call("ocppo_conv_x6", _stream(dev), 0, gpad.data_ptr(),
+         _geom(QH, QW, Hp * Wp * Cout, Wp * Cout, Cout, Wp * Cout, TW * Cout), wc.data_ptr(), K,
+         out.data_ptr(), C, M, N, K, 1, None, 0, og, tile, None)
     return out
 
 
