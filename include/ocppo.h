@@ -477,7 +477,8 @@ OCPPO_API int ocppo_gemm_x6_gather(ocppo_stream_t stream, const float* a, int64_
  * multiples of 4, x and w 16-B aligned, B qh qw < 2^24).
  *   mode 0 (forward; and each stride class of the data gradient, over the zero-padded output
  *          gradient with the flipped weight): c[row(r) + n] = act(sum_k x(r, k) w[n ldw + k] +
- *          bias[n]) for r < M = B qh qw, n < N, k < K; gseg % 32 == 0; splits == 1; row(r) =
+ *          bias[n]) for r < M = B qh qw, n < N, k < K; gseg % 32 == 0; splits > 1 (no bias,
+ *          ReLU or out_geom, ldc == N): K-split partials [splits, M, N] in c instead; row(r) =
  *          r ldc, or b sb' + qy ys' + qx xs' + off' with out_geom = {sb', ys', xs', off', cw,
  *          cs, cy, cx}, column n then at row(r) + (c / cs) cy + (c % cs) cx + n % cw, c = n / cw
  *          (all stride classes of a data gradient in one product: they read the same rows).

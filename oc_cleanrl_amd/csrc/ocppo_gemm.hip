@@ -1881,7 +1881,8 @@ extern "C" int ocppo_conv_x6(ocppo_stream_t stream, int mode, const float* x, co
   g.cv_gseg = (int)gseg;
   if (mode == 0) {
     // A = x gathered, B = W [N, K] (row stride ldw), C [M, N] (ldc) or a stride class's rows
-    OCPPO_REQUIRE(gseg % kX6BK == 0 && ldw >= K && ldw % 4 == 0 && splits == 1 &&
+    OCPPO_REQUIRE(gseg % kX6BK == 0 && ldw >= K && ldw % 4 == 0 &&
+                      (splits == 1 || (bias == nullptr && !relu && !out_geom && ldc == N)) &&
                       (out_geom != nullptr || ldc >= N),
                   "ocppo_conv_x6: the rows form needs kernel-row segments of a multiple of 32, "
                   "a k-contiguous W (ldw %lld >= K, %% 4), splits == 1, ldc >= N", (long long)ldw);
@@ -1892,6 +1893,7 @@ extern "C" int ocppo_conv_x6(ocppo_stream_t stream, int mode, const float* x, co
     g.sbk = 1;
     g.c = c;
     g.ldc = ldc;
+    g.split_c = M * N;  // splits > 1: partials [splits, M, N] (ocppo_sum_splits_act adds them)
     g.bias = bias;
     g.relu = relu ? 1 : 0;
     if (out_geom) {

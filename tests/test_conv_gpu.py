@@ -50,7 +50,11 @@ def _check(y, ref, scale, lib):
 
 @pytest.mark.parametrize("name", list(LAYERS))
 @pytest.mark.parametrize("relu", [True, False])
-def test_forward_bias_relu(name, relu):
+@pytest.mark.parametrize("splits", [True, False])
+def test_forward_bias_relu(name, relu, splits, monkeypatch):
+    """splits: these batches' few workgroups take K-split partials + ocppo_sum_splits_act (the
+    rollout's form); off: one product with bias + ReLU in its epilogue (the update's form)."""
+    monkeypatch.setattr(ops, "CONV_FWD_SPLITS", splits)
     x, w, b, s = _operands(name)
     assert ops.conv_x6_ok(x, w, s)
     y = ops.conv_x6(x, w, b, s, relu)
