@@ -495,6 +495,24 @@ OCPPO_API int ocppo_conv_x6(ocppo_stream_t stream, int mode, const float* x, con
                             const int64_t* out_geom, int tile, float* out);
 
 /* ---------------------------------------------------------------------------------------------
+ * The first NatureCNN convolution straight from the rollout's u8 frame stacks (ppo_atari_oc.py:566
+ * `b_obs[mb_inds]` -> NormalizeImg -> Conv2d, architectures/ppo.py:17-21), without the f32
+ * minibatch copy: sample b's stack is row idx[b] of src u8 [rows, C, H, W] (NCHW); taps k = (c,
+ * ky, kx) in nn.Conv2d's weight order (w [N, ldw] row-major, k-contiguous). The bytes are exact
+ * bf16 operands; the products are divided by `divisor` (255.0: NormalizeImg's x / 255).
+ *   mode 0: c[r, n] = act(sum_k u(r, k) w[n, k] / divisor + bias[n]), r < M = B OH OW (c [M, N])
+ *   mode 1: out[m, n] = sum_r w[r ldw + m] u(r, n) / divisor (w = the output gradient [K, ldw],
+ *           N = C KH KW taps, K = B OH OW rows); c = split partials [splits, M, N], summed in
+ *           split order in f64 and divided once.
+ * KW, W, stride multiples of 4; no padding; tile 0 / 2 (mode 0), 1 / 4 (mode 1) as ocppo_conv_x6's.
+ * ------------------------------------------------------------------------------------------- */
+OCPPO_API int ocppo_conv_x6_u8(ocppo_stream_t stream, int mode, const uint8_t* src,
+                               const int64_t* idx, int64_t C, int64_t H, int64_t W, int64_t KH,
+                               int64_t KW, int64_t stride, const float* w, int64_t ldw, float* c,
+                               int64_t M, int64_t N, int64_t K, int64_t splits, const float* bias,
+                               int relu, float divisor, int tile, float* out);
+
+/* ---------------------------------------------------------------------------------------------
  * The exact three-piece bf16 split ocppo_gemm_x6 forms in its K loop, done once per matrix: the
  * update's Linear weights (architectures/ppo.py:60-84) as the B operand of the forward (W [N, K],
  * trans 0) and of dX (W^T, trans 1), after every optimizer step (ppo_atari_oc.py:606) instead of

@@ -660,6 +660,51 @@ class _ConvX6(torch.autograd.Function):
         return dx, dw, (None if direct_b else db_out), None, None
 
 
+class _ConvX6U8(torch.autograd.Function):
+    """The first convolution (+ ReLU) of the update's minibatch forward read straight from the
+    rollout's u8 frame stacks through the minibatch indices (ops.conv_x6_u8: NormalizeImg's / 255
+    in the epilogue; no f32 minibatch copy of the observations, ppo_atari_oc.py:566); backward:
+    relu_bias_grad, then the weight gradient from the same u8 rows (the input needs none)."""
+
+    @staticmethod
+    def forward(ctx, w, b, frames, idx, stride, relu: bool, divisor: float):
+        y = ops.timed(f"conv_x6_u8_{idx.numel()}",
+                      lambda: ops.conv_x6_u8(frames, idx, w, b, stride, relu, divisor))
+        ctx.conv = (stride, relu, divisor)
+        ctx.b = b
+        ctx.save_for_backward(w, frames, idx, y if relu else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        w, frames, idx, y = ctx.saved_tensors
+        stride, relu, divisor = ctx.conv
+        g = g.contiguous(memory_format=torch.channels_last)
+        C = g.shape[1]
+        g2 = g.permute(0, 2, 3, 1).reshape(-1, C)
+        b = ctx.b
+        direct_b = _direct(b)
+        db_out = b.grad if direct_b else torch.empty_like(b)
+        o2 = y.permute(0, 2, 3, 1).reshape(-1, C) if relu else None
+        gp2, _ = ops.timed(f"relu_bias_grad_{g2.shape[0]}x{C}" + ("" if relu else "_norelu"),
+                           lambda: ops.relu_bias_grad(g2, o2, db=db_out))
+        dw = None
+        if ctx.needs_input_grad[0]:
+            KH, KW = w.shape[2], w.shape[3]
+            dw = ops.timed(f"conv_x6_u8_wgrad_{C}x{w[0].numel()}",
+                           lambda: ops.conv_x6_u8_wgrad(gp2, frames, idx, (KH, KW), stride,
+                                                        divisor)).view(w.shape)
+            if _direct(w):
+                w.grad.copy_(dw)  # nn.Conv2d's tap order into the channels_last grad
+                dw = None
+        return dw, (None if direct_b else db_out), None, None, None, None, None
+
+
+# The update's first convolution straight from the u8 frame stacks (_ConvX6U8) when the trunk
+# starts [NormalizeImg,] Conv2d: no minibatch gather of f32 observations
+CONV_X6_U8 = True
+
+
 # NatureCNN convolutions on this package's implicit GEMMs (ops.conv_x6, x6 products: no MIOpen,
 # deterministic by construction), in the rollout forward and the update; shapes it does not take
 # (conv_x6_ok: row counts the tiles do not divide, e.g. a few envs) stay on _ConvAct / MIOpen.
@@ -885,6 +930,32 @@ class _ActorCritic(Predictor):
         if prescaled and len(net) and isinstance(net[0], NormalizeImg):
             net = net[1:]
         return fused_trunk(net, x)
+
+    def trunk_frames_ok(self, frames, B: int) -> bool:
+        """trunk_frames applies: a Sequential trunk [NormalizeImg,] Conv2d(+ReLU) ... on the GPU
+        whose first convolution ops.conv_x6_u8 takes for B samples of `frames`."""
+        net = self.network
+        if not (CONV_X6_U8 and CONV_X6 and isinstance(net, nn.Sequential) and len(net) > 2):
+            return False
+        i = 1 if isinstance(net[0], NormalizeImg) else 0
+        conv = net[i]
+        return (isinstance(conv, nn.Conv2d) and conv.bias is not None and conv.groups == 1 and
+                conv.dilation == (1, 1) and tuple(conv.padding) == (0, 0) and
+                conv.stride[0] == conv.stride[1] and conv.weight.is_cuda and
+                ops.conv_x6_u8_ok(frames, conv.weight, conv.stride[0], B,
+                                  wgrad=conv.weight.requires_grad))
+
+    def trunk_frames(self, frames, idx):
+        """trunk(frames[idx]) for u8 frame stacks (NormalizeImg folded into the first
+        convolution's epilogue), the first Conv2d(+ReLU) reading the u8 rows in place."""
+        net = self.network
+        div = 255.0 if isinstance(net[0], NormalizeImg) else 1.0
+        if isinstance(net[0], NormalizeImg):
+            net = net[1:]
+        conv = net[0]
+        relu = isinstance(net[1], nn.ReLU)
+        y = _ConvX6U8.apply(conv.weight, conv.bias, frames, idx, conv.stride[0], relu, div)
+        return fused_trunk(net[2 if relu else 1:], y)
 
     def _head(self, lin, h):
         if isinstance(lin, nn.Linear) and lin.bias is not None and h.is_cuda and \

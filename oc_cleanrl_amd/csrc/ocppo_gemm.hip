@@ -128,6 +128,17 @@ struct X6Args {
   int64_t co_sb, co_ys, co_xs, co_off;
   int co_cw, co_cs;
   int64_t co_cy, co_cx;
+  // the first convolution straight from the rollout's u8 frame stacks (GATH 5: A's rows; GATH 6:
+  // B's K rows): sample b's stack is row u8_idx[b] of u8 [rows, C, H, W] (NCHW bytes, u8_img per
+  // row); k (or n) = (c, ky, kx) in nn.Conv2d's weight order, at c u8_hw + ky u8_w + kx from the
+  // window's corner (cv_row with cv_sb = 0: qy cv_ys + qx cv_xs bytes). The bytes are exact in
+  // bf16; the products are divided by cdiv (255: NormalizeImg) in the epilogue (GATH 5) or in the
+  // split sum (GATH 6).
+  const uint8_t* u8;
+  const int64_t* u8_idx;
+  int64_t u8_img, u8_hw, u8_w;
+  int u8_khw, u8_kw;
+  float cdiv;
 };
 
 // q = x / d for 0 <= x < 2^24, d >= 1 (f32 reciprocal estimate, corrected to the exact quotient)
@@ -411,6 +422,81 @@ struct X6Stage {
       }
     }
   }
+  // u8 frame stacks, k-contiguous (GATH 5): roff[i][j] = byte offset of piece row (i, j)'s window
+  // corner; segtab[q] = byte offset of taps 4q .. 4q + 3 (one kernel row: u8_kw % 4 == 0)
+  __device__ static void u8_rows(const X6Args& g, int row0, int t, int64_t (&roff)[kPer][4]) {
+    static_assert(KC, "u8 rows are for a k-contiguous operand");
+    const int qhw = g.cv_qh * g.cv_qw;
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int p = t + NT * i;
+      int rq, kq;
+      piece_of(p < kPieces ? p : 0, rq, kq);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = row0 + 4 * rq + j, b = x6_udiv(r, qhw), pix = r - b * qhw;
+        const int qy = x6_udiv(pix, g.cv_qw);
+        roff[i][j] = g.u8_idx[b] * g.u8_img + qy * g.cv_ys + (pix - qy * g.cv_qw) * g.cv_xs;
+      }
+    }
+  }
+  __device__ static floatx4 u8x4(uint32_t v) {
+    return floatx4{static_cast<float>(v & 0xffu), static_cast<float>((v >> 8) & 0xffu),
+                   static_cast<float>((v >> 16) & 0xffu), static_cast<float>(v >> 24)};
+  }
+  __device__ static void load_u8_rows(const uint8_t* __restrict__ src,
+                                      const int64_t (&roff)[kPer][4], const int32_t* segtab,
+                                      int k0, int t, floatx4 (&r)[kPer][4]) {
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int p = t + NT * i;
+      if (kPieces % NT != 0 && p >= kPieces) continue;
+      int rq, kq;
+      piece_of(p, rq, kq);
+      const int so = segtab[(k0 >> 2) + kq];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        r[i][j] = u8x4(*reinterpret_cast<const uint32_t*>(src + roff[i][j] + so));
+    }
+  }
+  // u8 frame stacks as a row-contiguous operand whose K index is a convolution row (GATH 6):
+  // nseg[i] = byte offset of piece i's 4 taps; (cb, cp) walk the K rows as conv_k_state's,
+  // cbase = u8_idx[cb] u8_img
+  __device__ static void u8_cols(const X6Args& g, int row0, int t, int64_t (&nseg)[kPer]) {
+    static_assert(!KC, "u8 K rows are for a row-contiguous operand");
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int p = t + NT * i;
+      int rq, kq;
+      piece_of(p < kPieces ? p : 0, rq, kq);
+      const int n = row0 + 4 * rq, c = n / g.u8_khw, rem = n - c * g.u8_khw, ky = rem / g.u8_kw;
+      nseg[i] = c * g.u8_hw + ky * g.u8_w + (rem - ky * g.u8_kw);
+    }
+  }
+  __device__ static void load_u8_k(const uint8_t* __restrict__ src, const X6Args& g,
+                                   const int64_t (&nseg)[kPer], const int32_t* ptab,
+                                   int (&cb)[kPer][4], int (&cp)[kPer][4],
+                                   int64_t (&cbase)[kPer][4], int t, floatx4 (&r)[kPer][4]) {
+    const int qhw = g.cv_qh * g.cv_qw;
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int p = t + NT * i;
+      if (kPieces % NT != 0 && p >= kPieces) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        r[i][j] = u8x4(*reinterpret_cast<const uint32_t*>(src + cbase[i][j] + ptab[cp[i][j]] +
+                                                          nseg[i]));
+        cp[i][j] += kX6BK;
+        if (cp[i][j] >= qhw) {
+          while (cp[i][j] >= qhw) {
+            cp[i][j] -= qhw;
+            ++cb[i][j];
+          }
+          cbase[i][j] = g.u8_idx[cb[i][j]] * g.u8_img;
+        }
+      }
+    }
+  }
   // row-contiguous operand whose K index (a sample row) picks a gathered source row:
   // B(n, k) = src[tbl[k - kbase] * sk + coff + n] (tbl = the unit's rows of gidx, in LDS)
   __device__ static void load_ktbl(const float* __restrict__ src, int64_t sk,
@@ -609,20 +695,37 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
 
   // operand loads of K step k0 into a register set (GATH: through the gathered row offsets)
   static_assert(GATH == 0 || (GATH == 1 && AKC) || (GATH == 2 && !BKC && !BPL) ||
-                    (GATH == 3 && AKC && !BPL) || (GATH == 4 && !BKC && !BPL),
+                    (GATH == 3 && AKC && !BPL) || (GATH == 4 && !BKC && !BPL) ||
+                    (GATH == 5 && AKC && !BPL) || (GATH == 6 && !BKC && !BPL),
                 "gather modes");
-  int64_t roffA[(GATH == 1 || GATH == 3) ? SA::kPer : 1][4];
-  int64_t nsegB[GATH == 4 ? SB::kPer : 1];
-  int cbB[GATH == 4 ? SB::kPer : 1][4], cpB[GATH == 4 ? SB::kPer : 1][4];
+  constexpr bool kKRows = GATH == 4 || GATH == 6;  // B's K index walks convolution rows
+  int64_t roffA[(GATH == 1 || GATH == 3 || GATH == 5) ? SA::kPer : 1][4];
+  int64_t nsegB[kKRows ? SB::kPer : 1];
+  int cbB[kKRows ? SB::kPer : 1][4], cpB[kKRows ? SB::kPer : 1][4];
+  int64_t cbaseB[GATH == 6 ? SB::kPer : 1][4];
   int64_t coffB = 0;
   if constexpr (GATH == 1) {
     const int seg = static_cast<int>((static_cast<int64_t>(kb) * kX6BK) / g.gseg);
     SA::gather_rows(g.gidx, g.gw, seg, g.gseg, g.sam, m0, t, roffA);
   } else if constexpr (GATH == 3) {
     SA::conv_rows(g, m0, t, roffA);
-  } else if constexpr (GATH == 4) {
-    SB::conv_cols(g, n0, t, nsegB);
+  } else if constexpr (GATH == 5) {
+    SA::u8_rows(g, m0, t, roffA);
+    for (int q = t; q < g.K / 4; q += NT) {
+      const int k = 4 * q, c = k / g.u8_khw, rem = k - c * g.u8_khw, ky = rem / g.u8_kw;
+      gtbl[q] = static_cast<int32_t>(c * g.u8_hw + ky * g.u8_w + (rem - ky * g.u8_kw));
+    }
+    __syncthreads();
+  } else if constexpr (kKRows) {
+    if constexpr (GATH == 4) SB::conv_cols(g, n0, t, nsegB);
+    else SB::u8_cols(g, n0, t, nsegB);
     SB::conv_k_state(g, kb * kX6BK, t, cbB, cpB);
+    if constexpr (GATH == 6) {
+#pragma unroll
+      for (int i = 0; i < SB::kPer; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) cbaseB[i][j] = g.u8_idx[cbB[i][j]] * g.u8_img;
+    }
     for (int p = t; p < g.cv_qh * g.cv_qw; p += NT) {
       const int qy = p / g.cv_qw;
       gtbl[p] = static_cast<int32_t>(qy * g.cv_ys + (p - qy * g.cv_qw) * g.cv_xs);
@@ -652,6 +755,7 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
   auto loadA = [&](int k0, floatx4 (&r)[SA::kPer][4]) {
     if constexpr (GATH == 1) SA::load_rows(A, roffA, k0, t, r);
     else if constexpr (GATH == 3) SA::load_rows(A, roffA, static_cast<int>(x6_cv_seg(g, k0)), t, r);
+    else if constexpr (GATH == 5) SA::load_u8_rows(g.u8, roffA, gtbl, k0, t, r);
     else if constexpr (kBuf)
       SA::load_buf(bufA, t, static_cast<int32_t>(4 * (AKC ? (k0 - kb * kX6BK)
                                                         : (k0 - kb * kX6BK) * g.sak)), r);
@@ -660,6 +764,7 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
   auto loadB = [&](int k0, floatx4 (&r)[SB::kPer][4]) {
     if constexpr (GATH == 2) SB::load_ktbl(B, g.sbk, gtbl, kb * kX6BK, coffB, n0, k0, t, r);
     else if constexpr (GATH == 4) SB::load_conv_k(B, g, nsegB, gtbl, cbB, cpB, t, r);  // k0: next
+    else if constexpr (GATH == 6) SB::load_u8_k(g.u8, g, nsegB, gtbl, cbB, cpB, cbaseB, t, r);
     else if constexpr (kBuf)
       SB::load_buf(bufB, t, static_cast<int32_t>(4 * (BKC ? (k0 - kb * kX6BK)
                                                         : (k0 - kb * kX6BK) * g.sbk)), r);
@@ -1140,6 +1245,7 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float v = LO ? hi[i][j][r] + lo[LO ? i : 0][LO ? j : 0][r] : hi[i][j][r];
+        if constexpr (GATH == 5) v = v / g.cdiv;
         if (g.bias) v += bv;
         if (g.relu) v = relu_f(v);
         Cp[orow[i][r] + ocol] = v;
@@ -1187,7 +1293,7 @@ template <int FM, int FN, int WGM, int WGN, bool AKC, bool BKC, bool LO, bool PF
 __global__ __launch_bounds__(64 * WGM * WGN, OCPPO_X6_OCC) void gemm_x6_kernel(X6Args g) {
   __shared__ __attribute__((aligned(16)))
   unsigned char lds[x6_lds_bytes<FM, FN, WGM, WGN, AKC, BKC>()];
-  __shared__ int32_t gtbl[(GATH == 2 || GATH == 4) ? kX6GTbl : 1];
+  __shared__ int32_t gtbl[(GATH == 2 || GATH >= 4) ? kX6GTbl : 1];
   const int u = x6_remap(blockIdx.x, gridDim.x);
   if (u >= g.units) return;
   x6_unit<FM, FN, WGM, WGN, AKC, BKC, LO, PF2, BPL, GATH, WGE>(
@@ -1785,12 +1891,24 @@ template <int FM, int FN, int WGM, int WGN, int GATH>
 static void launch_conv_t(hipStream_t s, X6Args& g) {
   g.tiles_m = g.M / (16 * FM * WGM);
   g.tiles_n = g.N / (16 * FN * WGN);
-  constexpr bool KC = GATH == 3;  // forward form: both operands k-contiguous; wgrad: neither
+  constexpr bool KC = GATH == 3 || GATH == 5;  // forward form: both k-contiguous; wgrad: neither
   hipLaunchKernelGGL((gemm_x6_kernel<FM, FN, WGM, WGN, KC, KC, false, true, false, GATH>),
                      dim3(g.units), dim3(64 * WGM * WGN), 0, s, g);
 }
 
 static bool launch_conv(hipStream_t s, int mode, int tile, X6Args& g) {
+  if (mode == 2) {  // the first convolution from u8 frame stacks: forward / weight gradient
+    if (tile == 0) launch_conv_t<4, 2, 2, 1, 5>(s, g);
+    else if (tile == 2) launch_conv_t<4, 2, 2, 2, 5>(s, g);
+    else return false;
+    return true;
+  }
+  if (mode == 3) {
+    if (tile == 1) launch_conv_t<2, 4, 1, 2, 6>(s, g);
+    else if (tile == 4) launch_conv_t<2, 4, 2, 2, 6>(s, g);
+    else return false;
+    return true;
+  }
   if (mode == 0) {
     switch (tile) {
       case 0: launch_conv_t<4, 2, 2, 1, 3>(s, g); return true;
@@ -1816,7 +1934,8 @@ static bool launch_conv(hipStream_t s, int mode, int tile, X6Args& g) {
 constexpr int kSumGroups = 16;
 __global__ __launch_bounds__(64 * kSumGroups) void sum_parts_kernel(const float* __restrict__ part,
                                                                     int S, int64_t n,
-                                                                    float* __restrict__ out) {
+                                                                    float* __restrict__ out,
+                                                                    double div) {
   __shared__ double red[kSumGroups][64];
   const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
   const int64_t e = static_cast<int64_t>(blockIdx.x) * 64 + lane;
@@ -1832,7 +1951,7 @@ __global__ __launch_bounds__(64 * kSumGroups) void sum_parts_kernel(const float*
     double v = red[0][lane];
 #pragma unroll
     for (int r = 1; r < kSumGroups; ++r) v += red[r][lane];
-    out[e] = static_cast<float>(v);
+    out[e] = static_cast<float>(v / div);
   }
 }
 
@@ -1937,8 +2056,87 @@ extern "C" int ocppo_conv_x6(ocppo_stream_t stream, int mode, const float* x, co
   if (mode == 1) {
     const int64_t n = M * N;
     hipLaunchKernelGGL(sum_parts_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64 * kSumGroups), 0,
-                       s, c, (int)splits, n, out);
+                       s, c, (int)splits, n, out, 1.0);
     return check_launch("ocppo_conv_x6 (sum_parts)");
+  }
+  return OCPPO_OK;
+}
+
+extern "C" int ocppo_conv_x6_u8(ocppo_stream_t stream, int mode, const uint8_t* src,
+                                const int64_t* idx, int64_t C, int64_t H, int64_t W, int64_t KH,
+                                int64_t KW, int64_t stride, const float* w, int64_t ldw, float* c,
+                                int64_t M, int64_t N, int64_t K, int64_t splits, const float* bias,
+                                int relu, float divisor, int tile, float* out) {
+  OCPPO_REQUIRE(mode == 0 || mode == 1, "ocppo_conv_x6_u8: mode %d (0 rows, 1 weight gradient)",
+                mode);
+  OCPPO_REQUIRE(src && idx && w && c && (mode == 0 || out), "ocppo_conv_x6_u8: null pointer");
+  OCPPO_REQUIRE(C >= 1 && KH >= 1 && KW >= 1 && stride >= 1 && H >= KH && W >= KW &&
+                    (H - KH) % stride == 0 && (W - KW) % stride == 0 && KW % 4 == 0 &&
+                    W % 4 == 0 && stride % 4 == 0 && divisor > 0.f,
+                "ocppo_conv_x6_u8: geometry C=%lld H=%lld W=%lld KH=%lld KW=%lld stride=%lld "
+                "(KW, W, stride multiples of 4; no padding)", (long long)C, (long long)H,
+                (long long)W, (long long)KH, (long long)KW, (long long)stride);
+  const int64_t OH = (H - KH) / stride + 1, OW = (W - KW) / stride + 1, taps = C * KH * KW;
+  const int64_t rows = mode == 0 ? M : K;
+  const X6Tile tc = kConvTiles[tile >= 0 && tile < 7 ? tile : 0];
+  const int64_t bm = 16 * tc.fm * tc.wgm, bn = 16 * tc.fn * tc.wgn;
+  OCPPO_REQUIRE(M % bm == 0 && N % bn == 0 && K % kX6BK == 0 && splits >= 1 &&
+                    K / kX6BK >= splits && rows % (OH * OW) == 0 && rows < (int64_t{1} << 24) &&
+                    (mode == 0 ? (N <= INT32_MAX && K == taps && taps / 4 <= kX6GTbl)
+                               : (N == taps && OH * OW <= kX6GTbl)),
+                "ocppo_conv_x6_u8: bad sizes M=%lld N=%lld K=%lld splits=%lld", (long long)M,
+                (long long)N, (long long)K, (long long)splits);
+  OCPPO_REQUIRE(mode == 0 ? (ldw >= K && ldw % 4 == 0 && splits == 1)
+                          : (ldw >= M && ldw % 4 == 0 && bias == nullptr && !relu),
+                "ocppo_conv_x6_u8: operand strides / epilogue (ldw %lld)", (long long)ldw);
+  OCPPO_REQUIRE(reinterpret_cast<uintptr_t>(src) % 4 == 0 && reinterpret_cast<uintptr_t>(w) % 16 == 0,
+                "ocppo_conv_x6_u8: src 4-B and w 16-B aligned");
+  X6Args g{};
+  g.M = (int)M;
+  g.N = (int)N;
+  g.K = (int)K;
+  g.splits = (int)splits;
+  g.units = (int)(splits * (M / bm) * (N / bn));
+  g.cv_qh = (int)OH;
+  g.cv_qw = (int)OW;
+  g.cv_ys = stride * W;
+  g.cv_xs = stride;
+  g.u8 = src;
+  g.u8_idx = idx;
+  g.u8_img = C * H * W;
+  g.u8_hw = H * W;
+  g.u8_w = W;
+  g.u8_khw = (int)(KH * KW);
+  g.u8_kw = (int)KW;
+  g.cdiv = divisor;
+  if (mode == 0) {  // y = act(sum_k u(r, k) w[n, k] / divisor + bias)
+    g.sak = 1;
+    g.b = w;
+    g.sbn = ldw;
+    g.sbk = 1;
+    g.c = c;
+    g.ldc = N;
+    g.bias = bias;
+    g.relu = relu ? 1 : 0;
+  } else {  // dW[m, n] = sum_r gp[r ldw + m] u(r, n) / divisor: split partials, ordered sum
+    g.a = w;
+    g.sam = 1;
+    g.sak = ldw;
+    g.sbn = 1;
+    g.c = c;
+    g.ldc = N;
+    g.split_c = M * N;
+  }
+  clear_stale_error();
+  hipStream_t s = as_stream(stream);
+  OCPPO_REQUIRE(launch_conv(s, mode + 2, tile, g), "ocppo_conv_x6_u8: tile %d not built for mode %d",
+                tile, mode);
+  if (int rc = check_launch("ocppo_conv_x6_u8")) return rc;
+  if (mode == 1) {
+    const int64_t n = M * N;
+    hipLaunchKernelGGL(sum_parts_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64 * kSumGroups), 0,
+                       s, c, (int)splits, n, out, static_cast<double>(divisor));
+    return check_launch("ocppo_conv_x6_u8 (sum_parts)");
   }
   return OCPPO_OK;
 }

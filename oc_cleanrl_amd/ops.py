@@ -881,6 +881,89 @@ def conv_x6_dgrad(gp, weight, stride: int, in_hw: tuple, out=None):
     return out
 
 
+def conv_x6_u8_ok(src, weight, stride: int, B: int, wgrad: bool = False) -> bool:
+    """The first convolution straight from u8 frame stacks src [R, C, H, W] (ocppo_conv_x6_u8):
+    KW, W and the stride multiples of 4, no padding, B samples' rows a tile divides."""
+    if not (isinstance(src, torch.Tensor) and src.is_cuda and src.dtype == torch.uint8 and
+            src.dim() == 4 and src.is_contiguous() and weight.dim() == 4):
+        return False
+    _, C, H, W = src.shape
+    Cout, Cw, KH, KW = weight.shape
+    s = int(stride)
+    if Cw != C or KW % 4 or W % 4 or s % 4 or H < KH or W < KW or (H - KH) % s or (W - KW) % s:
+        return False
+    OH, OW = (H - KH) // s + 1, (W - KW) // s + 1
+    rows, taps = B * OH * OW, C * KH * KW
+    if rows >= 1 << 24 or taps % 32 or taps // 4 > 1024 or _conv_u8_tile(rows, Cout, 0) is None:
+        return False
+    return not wgrad or (OH * OW <= 1024 and rows % 32 == 0 and
+                         _conv_u8_tile(Cout, taps, 1) is not None)
+
+
+def _conv_u8_tile(M: int, N: int, mode: int) -> int | None:
+    for t in (((0,) if N == 32 else (2,) if N == 64 else ()) if mode == 0 else
+              ((1,) if M == 32 else (4,) if M == 64 else ())):
+        bm, bn = _CONV_TILES[t]
+        if M % bm == 0 and N % bn == 0:
+            return t
+    return None
+
+
+def conv_x6_u8(src, idx, weight, bias=None, stride: int = 4, relu: bool = True,
+               divisor: float = 255.0, out=None):
+    """act(conv2d(src[idx] / divisor, weight) + bias) with the u8 frame stacks read in place
+    (ocppo_conv_x6_u8): src [R, C, H, W] u8, idx [B] int64 -> channels_last [B, Cout, OH, OW]."""
+    B = idx.numel()
+    if not conv_x6_u8_ok(src, weight, stride, B):
+        raise ValueError(f"conv_x6_u8: unsupported src {tuple(src.shape)} / weight "
+                         f"{tuple(weight.shape)} / stride {stride} / {B} samples")
+    _, C, H, W = src.shape
+    Cout, _, KH, KW = weight.shape
+    s = int(stride)
+    OH, OW = (H - KH) // s + 1, (W - KW) // s + 1
+    dev, f = src.device, torch.float32
+    K, M = C * KH * KW, B * OH * OW
+    wn = weight.contiguous()  # nn.Conv2d's (c, ky, kx) tap order
+    if out is None:
+        out = torch.empty((B, Cout, OH, OW), dtype=f, device=dev, memory_format=torch.channels_last)
+    if tuple(out.shape) != (B, Cout, OH, OW) or not out.is_contiguous(memory_format=torch.channels_last):
+        raise ValueError("conv_x6_u8: out must be a channels_last [B, Cout, OH, OW] tensor")
+    call("ocppo_conv_x6_u8", _stream(dev), 0, src.data_ptr(), _check(idx, "idx", torch.int64, dev, B),
+         C, H, W, KH, KW, s, wn.data_ptr(), K, out.data_ptr(), M, Cout, K, 1,
+         _opt(bias, "bias", f, dev, Cout), int(bool(relu)), float(divisor),
+         _conv_u8_tile(M, Cout, 0), None)
+    return out
+
+
+def conv_x6_u8_wgrad(gp, src, idx, kernel: tuple, stride: int = 4, divisor: float = 255.0,
+                     out=None):
+    """dW [Cout, C KH KW] (nn.Conv2d's tap order) of conv_x6_u8: sum over the output pixels r of
+    gp[r, co] src[idx[b], c, s oy + ky, s ox + kx] / divisor; split partials summed in order."""
+    B = idx.numel()
+    _, C, H, W = src.shape
+    KH, KW = kernel
+    s = int(stride)
+    OH, OW = (H - KH) // s + 1, (W - KW) // s + 1
+    rows, Cout = gp.shape
+    dev, f = src.device, torch.float32
+    N = C * KH * KW
+    tile = _conv_u8_tile(Cout, N, 1)
+    if rows != B * OH * OW or tile is None or rows % 32:
+        raise ValueError("conv_x6_u8_wgrad: gp must be [B OH OW, Cout] with a tile for it")
+    bm, bn = _CONV_TILES[tile]
+    S = max(1, min(rows // 32 // 32, 2048 // ((Cout // bm) * (N // bn))))
+    key = ("wgrad", str(dev), S, Cout, N)
+    if key not in _CONV_PARTS:
+        _CONV_PARTS[key] = torch.empty((S, Cout, N), dtype=f, device=dev)
+    part = _CONV_PARTS[key]
+    if out is None:
+        out = torch.empty((Cout, N), dtype=f, device=dev)
+    call("ocppo_conv_x6_u8", _stream(dev), 1, src.data_ptr(), _check(idx, "idx", torch.int64, dev, B),
+         C, H, W, KH, KW, s, _check(gp, "gp", f, dev), Cout, part.data_ptr(), Cout, N, rows, S,
+         None, 0, float(divisor), tile, _check(out, "out", f, dev, Cout * N))
+    return out
+
+
 def linear2_act(x, w1, b1, w2, b2, relu1: bool = True, relu2: bool = True, out=None):
     """y = act2(act1(x @ w1.T + b1) @ w2.T + b2) in ONE launch for rollout-sized batches (no
     autograd): x [M, K1] f32 (unit column stride, K1 <= 64), w1 [N1, K1], w2 [N2, N1]

@@ -442,6 +442,10 @@ class PPOTrainer:
                         if self.fused_heads_loss else None)
         self.hl_finish = ops.DeferredFinish(dev) if self.fused_heads_loss else None
         self.b_obs = self.obs[:T].view((T * N,) + self.obs_shape)
+        # pixel trunks: the update's first convolution reads the u8 frame stacks itself
+        self.u8_first_conv = (not self.frame_dedup and self.b_obs.dtype == torch.uint8 and
+                              self.prescale and hasattr(self.agent, "trunk_frames_ok") and
+                              self.agent.trunk_frames_ok(self.b_obs, self.M))
         self.wplanes, self.wplanes_built = None, False  # built at the first minibatch
         self.planes_by_opt = False
         # GAE's per-sample records for the minibatch gather (ops.sample_records)
@@ -762,6 +766,12 @@ class PPOTrainer:
                                              idx, k, split=self.split)
             if self.split:
                 hidden, self.cuts[j] = hidden
+            if self._fused_tail(j, hidden):
+                return
+            logits, value = ag.heads(hidden)
+        elif self.u8_first_conv:
+            # the first convolution reads the u8 frame stacks through idx (no f32 minibatch copy)
+            hidden = ag.trunk_frames(self.b_obs, idx)
             if self._fused_tail(j, hidden):
                 return
             logits, value = ag.heads(hidden)

@@ -127,3 +127,46 @@ def test_rejects_bad_shapes():
         ops.conv_x6(x.contiguous(), w, b, s)  # NCHW x
     with pytest.raises(ValueError):
         ops.conv_x6(x[:3].contiguous(memory_format=CL), w, b, s)  # 243 rows: no tile divides
+
+
+def _frames(R=40, seed=5):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    return torch.randint(0, 256, (R, 4, 84, 84), device=DEV, generator=g, dtype=torch.uint8)
+
+
+@pytest.mark.parametrize("relu", [True, False])
+def test_u8_first_conv_forward(relu):
+    """conv_x6_u8: NormalizeImg + the 8x8/4 convolution read from u8 frame stacks through a sample
+    index, against f64 on the gathered, normalised observations."""
+    src = _frames()
+    _, w, b, s = _operands("conv1")
+    idx = torch.randperm(src.shape[0], device=DEV)[:16]
+    assert ops.conv_x6_u8_ok(src, w, s, 16, wgrad=True)
+    y = ops.conv_x6_u8(src, idx, w, b, s, relu)
+    assert y.is_contiguous(memory_format=CL)
+    x = src[idx].float() / 255.0  # the reference's NormalizeImg (f32)
+    x64, w64, b64 = x.double().cpu(), w.double().cpu(), b.double().cpu()
+    ref = F.conv2d(x64, w64, b64, stride=s)
+    scale = F.conv2d(x64.abs(), w64.abs(), b64.abs(), stride=s)
+    lib = F.conv2d(x, w, b, stride=s)
+    if relu:
+        ref, lib = ref.clamp_min(0), lib.clamp_min(0)
+    _check(y, ref, scale, lib)
+    assert torch.equal(y, ops.conv_x6_u8(src, idx, w, b, s, relu))
+
+
+def test_u8_first_conv_weight_gradient():
+    src = _frames(seed=6)
+    _, w, _, s = _operands("conv1", 7)
+    idx = torch.randperm(src.shape[0], device=DEV)[:16]
+    g = torch.Generator(device=DEV).manual_seed(8)
+    gp = (torch.rand(16, 32, 20, 20, device=DEV, generator=g) * 2 - 1).contiguous(memory_format=CL)
+    rows = gp.permute(0, 2, 3, 1).reshape(-1, 32)
+    dw = ops.conv_x6_u8_wgrad(rows, src, idx, (8, 8), s).view(w.shape)  # (c, ky, kx) order
+    x = src[idx].float() / 255.0
+    x64, gp64 = x.double().cpu(), gp.double().cpu()
+    ref = torch.nn.grad.conv2d_weight(x64, w.shape, gp64, stride=s)
+    scale = torch.nn.grad.conv2d_weight(x64.abs(), w.shape, gp64.abs(), stride=s)
+    lib = torch.nn.grad.conv2d_weight(x.contiguous(memory_format=CL), w.shape, gp, stride=s)
+    _check(dw, ref, scale, lib)
+    assert torch.equal(dw, ops.conv_x6_u8_wgrad(rows, src, idx, (8, 8), s).view(w.shape))
