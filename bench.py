@@ -548,14 +548,13 @@ def run_rank(opt, rank: int, world: int, line_out, watch):
         opt.no_kernel_timing = True
     elif opt.config == 3:
         envs = opt.envs_per_gpu or 256
-        # MIOpen's deterministic convolution algorithms (use_deterministic_algorithms(True), the
-        # reference default) are naive kernels on gfx950, ~30x slower for NatureCNN: config 3 is
-        # measured with torch_deterministic=False (our own HIP kernels are deterministic anyway),
-        # and with MIOpen's Find choosing the convolution solutions (cudnn.benchmark)
+        # the reference's torch_deterministic=True default: the NatureCNN convolutions run on
+        # this package's implicit GEMMs (agents._ConvX6 / _ConvX6U8: no MIOpen, no atomics), so
+        # the determinism costs nothing (MIOpen's deterministic solutions are naive kernels:
+        # 0.9k env steps/s, profiles/r05/c3_deterministic_miopen.txt)
         args = Args(env_id="ALE/Breakout-v5", obs_mode="dqn", architecture="PPO",
                     num_envs=envs * world, num_steps=128, total_timesteps=10_000_000,
-                    cuda_graphs=not opt.no_graphs, save_model=False, torch_deterministic=False,
-                    conv_benchmark=True)
+                    cuda_graphs=not opt.no_graphs, save_model=False, torch_deterministic=True)
     else:
         envs = opt.envs_per_gpu or 128
         args = Args(env_id="ALE/Pong-v5", obs_mode="obj", architecture="PPO_OBJ",
@@ -754,13 +753,10 @@ def run_rank(opt, rank: int, world: int, line_out, watch):
                                        "hipBLASLt's f32 GEMM, tests/test_gemm_gpu.py); "
                                        "products it does not tile on hipBLASLt f32"
                                        if args.x6_gemm else "hipBLASLt f32"),
-                       **({"deviation": "torch_deterministic=False (reference default True): "
-                           "MIOpen's deterministic convolution algorithms are naive kernels on "
-                           "gfx950, 83x slower (1875 vs 22.5 ms per iteration at 16 envs, "
-                           "profiles/r02/c3_capture.log); this package's own HIP kernels are "
-                           "deterministic either way. MIOpen's Find picks the convolution "
-                           "solutions (cudnn.benchmark, conv_benchmark=True: 283k -> 319k env "
-                           "steps/s; a few seconds of search in the warm-up)"}
+                       **({"convolutions": "ocppo_conv_x6 / ocppo_conv_x6_u8: implicit GEMMs "
+                           "on the exact three-piece bf16 products (forward with bias + ReLU, "
+                           "weight gradient, data gradient; the first layer reads the u8 frame "
+                           "stacks through the minibatch indices), deterministic"}
                           if opt.config == 3 else {}),
                        "conv_benchmark": args.conv_benchmark,
                        "sampling_noise": {
