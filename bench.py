@@ -352,6 +352,9 @@ def main():
                     help="skip the per-block CPU timings (GAE, minibatch update, config-3 estimate)")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--sync-metrics", dest="lag_metrics", action="store_false",
+                    help="read each iteration's metrics with a host sync at its end (default: "
+                         "lagged one iteration, trainer.train_iteration(lag=True))")
     ap.add_argument("--no-scaled", action="store_true", help="skip roofline_scaled")
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                     help="torch.distributed backend for N > 1 (nccl = RCCL; gloo only for the "
@@ -572,15 +575,20 @@ def run_rank(opt, rank: int, world: int, line_out, watch):
             dist.barrier()
         torch.cuda.synchronize(device)
 
+    # every iteration's metrics (the reference's per-iteration scalars) are collected inside the
+    # timed region; lagged: gathered on the device behind the iteration's work and read by the
+    # host one iteration later, the last one flushed before the closing barrier
     for i in range(opt.warmup):
         watch.phase(f"warmup {i}", stall_s=2.5 * opt.stall)
-        tr.train_iteration(collect_metrics=True)
+        tr.train_iteration(collect_metrics=True, lag=opt.lag_metrics)
+    tr.flush_metrics()
     watch.phase("barrier")
     barrier()
     t0 = time.perf_counter()
     for i in range(opt.steps):
         watch.phase(f"timed {i}")
-        tr.train_iteration(collect_metrics=True)
+        tr.train_iteration(collect_metrics=True, lag=opt.lag_metrics)
+    tr.flush_metrics()
     watch.phase("barrier")
     barrier()
     dt = time.perf_counter() - t0
@@ -744,6 +752,10 @@ def run_rank(opt, rank: int, world: int, line_out, watch):
                        "num_minibatches": args.num_minibatches,
                        "obs_storage": str(tr.obs_dtype).replace("torch.", ""),
                        "cuda_graphs": args.cuda_graphs,
+                       "metrics": ("every iteration, lagged one iteration (device gather + "
+                                   "non-blocking copy; the host reads them while the next "
+                                   "iteration runs; the last flushed inside the timed region)"
+                                   if opt.lag_metrics else "every iteration, host sync at its end"),
                        "torch_deterministic": args.torch_deterministic,
                        "gemm_table": (str(gemm_table.TABLE.relative_to(ROOT))
                                       if tr.gemm_table else None),

@@ -402,6 +402,7 @@ class PPOTrainer:
         self.staged = False
         self.staged_rng_state = self.current_rng_state = None
         self.executed_mb = self.E * self.nmb  # minibatches the last update ran (target_kl)
+        self._pending_metrics, self._metrics_host = None, None  # train_iteration(lag=True)
         self.perm_event = torch.cuda.Event()
         self.perm_event.record()
         # PPObj update with every distinct frame of a minibatch encoded once (frames.py)
@@ -1013,8 +1014,12 @@ class PPOTrainer:
                     break
 
     # ------------------------------------------------------------------------------------------
-    def train_iteration(self, collect_metrics: bool = True) -> dict:
-        """One PPO iteration (:469-670)."""
+    def train_iteration(self, collect_metrics: bool = True, lag: bool = False) -> dict:
+        """One PPO iteration (:469-670). lag: the iteration's metric scalars are gathered on the
+        device and copied to pinned host memory behind its work, and the PREVIOUS iteration's
+        metrics are returned (flush_metrics() returns the last one): the host never waits for
+        the GPU between iterations, so the next iteration's work is queued while the host turns
+        this one's scalars into the dict (same scalars as lag=False, one iteration later)."""
         a = self.args
         self.iteration += 1
         if a.anneal_lr:
@@ -1040,8 +1045,66 @@ class PPOTrainer:
         self.timer.end_iteration()
         self.global_step += self.N * self.T * self.world
         m = {}
-        if collect_metrics:
-            m = self._metrics()
+        if collect_metrics and lag and self._lag_ok():
+            prev, self._pending_metrics = self._pending_metrics, self._metrics_device()
+            if prev is not None:
+                m = self._metrics_from(prev)
+        elif collect_metrics:
+            m = self.flush_metrics()
+            m.update(self._metrics())
+        return m
+
+    def _lag_ok(self) -> bool:
+        return self.args.target_kl is None and hasattr(self.env, "ep_state")
+
+    def flush_metrics(self) -> dict:
+        """The metrics of the last lagged iteration still pending ({} if none)."""
+        prev, self._pending_metrics = self._pending_metrics, None
+        return self._metrics_from(prev) if prev is not None else {}
+
+    def _metrics_device(self):
+        """_metrics' scalars gathered on the device and copied (non-blocking) into pinned host
+        memory behind this iteration's work: (event, host vector, executed minibatches)."""
+        y_true = self.returns.double().view(-1)
+        y_pred = self.values[:self.T].double().reshape(-1)
+        var_y = torch.var(y_true, unbiased=False)
+        ev = 1 - torch.var(y_true - y_pred, unbiased=False) / var_y
+        ep = self.env.ep_state[:, 2:5].sum(0, dtype=torch.float64)
+        self.env.ep_state[:, 2:5].zero_()
+        n = self.executed_mb
+        vec = torch.cat([var_y.view(1), ev.view(1), self.lr.double().view(1), ep,
+                         self.stats[:n].double().reshape(-1)])
+        if self._metrics_host is None or self._metrics_host.numel() < vec.numel():
+            self._metrics_host = torch.empty(vec.numel(), dtype=torch.float64, pin_memory=True)
+        host = self._metrics_host[:vec.numel()]
+        host.copy_(vec, non_blocking=True)
+        done = torch.cuda.Event()
+        done.record()
+        return done, host, n
+
+    def _metrics_from(self, pend) -> dict:
+        done, host, n = pend
+        done.synchronize()
+        v = host.numpy().copy()
+        var_y, ev, lr = float(v[0]), float(v[1]), float(v[2])
+        ep_ret, ep_len, ep_n = (float(t) for t in v[3:6])
+        stats = v[6:].reshape(n, -1)
+        last = stats[-1]
+        m = {
+            "charts/learning_rate": lr,
+            "losses/value_loss": float(last[2]),
+            "losses/policy_loss": float(last[1]),
+            "losses/entropy": float(last[3]),
+            "losses/old_approx_kl": float(last[4]),
+            "losses/approx_kl": float(last[5]),
+            "losses/clipfrac": float(np.mean(stats[:, 6].astype(np.float32))),
+            "losses/explained_variance": float("nan") if var_y == 0 else ev,
+            "losses/loss": float(last[0]),
+        }
+        if ep_n > 0:
+            m["charts/Episodic_Original_Reward"] = ep_ret / ep_n
+            m["charts/Episodic_Length"] = ep_len / ep_n
+        self.last_metrics = m
         return m
 
     def _metrics(self) -> dict:

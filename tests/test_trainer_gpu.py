@@ -776,3 +776,25 @@ def test_first_layer_backward_in_second_layer_dx(dev):
     for p, q in zip(a.agent.parameters(), b.agent.parameters()):
         assert (p - q).abs().max().item() < 2e-5
     assert torch.allclose(a.stats, b.stats, rtol=1e-3, atol=1e-3)  # a clip flip: 1/4096
+
+
+def test_lagged_metrics_are_the_synced_ones(dev):
+    """train_iteration(lag=True) returns the previous iteration's metrics, gathered on the device
+    behind its work: the same scalars as the synchronous path, one call later."""
+    from oc_cleanrl_amd.args import Args, finalize
+    from oc_cleanrl_amd.trainer import PPOTrainer
+
+    def run(lag):
+        args = finalize(Args(env_id="ALE/Pong-v5", obs_mode="obj", architecture="PPO_OBJ",
+                             num_envs=16, num_steps=16, num_features=12, seed=3,
+                             save_model=False), 1)
+        tr = PPOTrainer(args, dev)
+        out = [tr.train_iteration(collect_metrics=True, lag=lag) for _ in range(3)]
+        return out + [tr.flush_metrics()]
+
+    sync, lagged = run(False), run(True)
+    assert lagged[0] == {} and sync[3] == {}
+    for a, b in zip(sync[:3], lagged[1:]):
+        assert a.keys() == b.keys()
+        for k in a:
+            assert a[k] == b[k] or (a[k] != a[k] and b[k] != b[k]), (k, a[k], b[k])
