@@ -13,7 +13,9 @@ sys.path.insert(0, str(ROOT))
 def main():
     target, value = sys.argv[1], sys.argv[2]
     mod, name = target.rsplit(".", 1)
-    setattr(import_module(f"oc_cleanrl_amd.{mod}"), name, bool(int(value)))
+    m = import_module(f"oc_cleanrl_amd.{mod}")
+    v = int(value)
+    setattr(m, name, bool(v) if isinstance(getattr(m, name), bool) else v)
     sys.argv = [str(ROOT / "bench.py")] + sys.argv[3:]
     runpy.run_path(str(ROOT / "bench.py"), run_name="__main__")
 
