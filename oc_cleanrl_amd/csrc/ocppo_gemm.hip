@@ -517,8 +517,10 @@ struct X6Stage {
     }
   }
 
-  // split row j (4 elements) of staged piece i and write it into the three planes
-  template <bool PROBE = false>
+  // split row j (4 elements) of staged piece i and write it into the three planes; EXACT:
+  // bf16-exact values (u8 bytes), the value itself is the lead piece and only plane 0 is written
+  // (the products never read the others)
+  template <bool PROBE = false, bool EXACT = false>
   __device__ static void stash_row(unsigned char* lds, int t, const floatx4 (&r)[kPer][4], int i,
                                    int j) {
     const int p = t + NT * i;
@@ -527,6 +529,14 @@ struct X6Stage {
     piece_of(p, rq, kq);
     const x6f2 v01 = KC ? x6f2{r[i][j][0], r[i][j][1]} : x6f2{r[i][0][j], r[i][1][j]};
     const x6f2 v23 = KC ? x6f2{r[i][j][2], r[i][j][3]} : x6f2{r[i][2][j], r[i][3][j]};
+    if constexpr (EXACT) {
+      const uint32_t e0 = __builtin_amdgcn_perm(__float_as_uint(v01.y), __float_as_uint(v01.x),
+                                                0x07060302u);
+      const uint32_t e1 = __builtin_amdgcn_perm(__float_as_uint(v23.y), __float_as_uint(v23.x),
+                                                0x07060302u);
+      *reinterpret_cast<uint2*>(lds + x6_off((KC ? PR : 4) * rq + j, 4 * kq)) = uint2{e0, e1};
+      return;
+    }
     uint32_t a0, a1, a2, b0, b1, b2;
     x6_split2<PROBE>(v01, a0, a1, a2);
     x6_split2<PROBE>(v23, b0, b1, b2);
@@ -537,12 +547,12 @@ struct X6Stage {
   }
 
   // split the staged pieces and write the three planes (plane p at lds + p * kPlane)
-  template <bool PROBE = false>
+  template <bool PROBE = false, bool EXACT = false>
   __device__ static void stash(unsigned char* lds, int t, const floatx4 (&r)[kPer][4]) {
 #pragma unroll
     for (int i = 0; i < kPer; ++i)
 #pragma unroll
-      for (int j = 0; j < PR; ++j) stash_row<PROBE>(lds, t, r, i, j);  // row PR rq + j
+      for (int j = 0; j < PR; ++j) stash_row<PROBE, EXACT>(lds, t, r, i, j);  // row PR rq + j
   }
 };
 
@@ -625,6 +635,20 @@ __device__ __forceinline__ void x6_mfma6(const bf16x8 (&a)[3], const bf16x8 (&b)
   s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], s, 0, 0, 0);
   s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], s, 0, 0, 0);
   s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], s, 0, 0, 0);
+}
+
+// One operand bf16-exact (its pieces 1 and 2 are zero: the u8 frame stacks of ocppo_conv_x6_u8):
+// the three products with its lead piece, in x6_mfma6's order
+template <bool AEX>
+__device__ __forceinline__ void x6_mfma3(const bf16x8 (&a)[3], const bf16x8 (&b)[3], floatx4& acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], acc, 0, 0, 0);
+  if constexpr (AEX) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], acc, 0, 0, 0);
+  } else {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], acc, 0, 0, 0);
+  }
 }
 
 // WGM x WGN waves per workgroup, each FM x FN blocks of 16 x 16 (tile BM x BN = 16 FM WGM x
@@ -783,23 +807,26 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
       for (int j = 0; j < FN; ++j) lo[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
   }
 
-  // MFMAs of the step held in LDS
+  // MFMAs of the step held in LDS (an exact operand: its lead plane only, three products)
+  constexpr bool AEX = GATH == 5, BEX = GATH == 6;
   auto compute = [&]() {
     bf16x8 af[FM][3];
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl)
+      for (int pl = 0; pl < (AEX ? 1 : 3); ++pl)
         af[i][pl] = x6_frag(la + pl * SA::kPlane, wm * 16 * FM + 16 * i + fr, fc);
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       bf16x8 bf[3];
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl)
+      for (int pl = 0; pl < (BEX ? 1 : 3); ++pl)
         bf[pl] = x6_frag(lb + pl * SB::kPlane, wn * 16 * FN + 16 * j + fr, fc);
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
-        x6_mfma6<LO>(af[i], bf, hi[i][j], lo[LO ? i : 0][LO ? j : 0]);
+      for (int i = 0; i < FM; ++i) {
+        if constexpr (AEX || BEX) x6_mfma3<AEX>(af[i], bf, hi[i][j]);
+        else x6_mfma6<LO>(af[i], bf, hi[i][j], lo[LO ? i : 0][LO ? j : 0]);
+      }
     }
   };
   floatx4 ra[SA::kPer][4];
@@ -912,7 +939,7 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
     loadA(kb * kX6BK, ra);
     PB::load(Bp, g.bpl_ld, g.bpl_ps, n0, kb * kX6BK, t, pb);
     if (nk > 1) loadA((kb + 1) * kX6BK, qa);
-    SA::template stash<kProbeA>(la, t, ra);
+    SA::template stash<kProbeA, AEX>(la, t, ra);
     PB::stash(lb, t, pb);
     __syncthreads();
     auto step = [&](int kt, floatx4 (&ldA)[SA::kPer][4], floatx4 (&stA)[SA::kPer][4],
@@ -922,7 +949,7 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
       compute();
       __syncthreads();
       if (kt + 1 < nk) {
-        SA::template stash<kProbeA>(la, t, stA);
+        SA::template stash<kProbeA, AEX>(la, t, stA);
         PB::stash(lb, t, pbr);
       }
       __syncthreads();
@@ -937,8 +964,8 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
     floatx4 rb[SB::kPer][4];
     SA::load(A, g.sam, g.sak, m0, kb * kX6BK, t, ra);
     SB::load(B, g.sbn, g.sbk, n0, kb * kX6BK, t, rb);
-    SA::template stash<kProbeA>(la, t, ra);
-    SB::template stash<kProbeB>(lb, t, rb);
+    SA::template stash<kProbeA, AEX>(la, t, ra);
+    SB::template stash<kProbeB, BEX>(lb, t, rb);
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
       const bool more = kt + 1 < nk;
@@ -949,8 +976,8 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
       compute();
       __syncthreads();
       if (more) {
-        SA::template stash<kProbeA>(la, t, ra);
-        SB::template stash<kProbeB>(lb, t, rb);
+        SA::template stash<kProbeA, AEX>(la, t, ra);
+        SB::template stash<kProbeB, BEX>(lb, t, rb);
       }
       __syncthreads();
     }
@@ -992,8 +1019,8 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
         x6_vmwait<0>(rb);
       }
     }
-    SA::template stash<kProbeA>(la, t, ra);
-    SB::template stash<kProbeB>(lb, t, rb);
+    SA::template stash<kProbeA, AEX>(la, t, ra);
+    SB::template stash<kProbeB, BEX>(lb, t, rb);
     __syncthreads();
     auto step = [&](int kt, floatx4 (&ldA)[SA::kPer][4], floatx4 (&ldB)[SB::kPer][4],
                     floatx4 (&stA)[SA::kPer][4], floatx4 (&stB)[SB::kPer][4]) {
@@ -1019,8 +1046,8 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
             x6_vmwait<0>(stB);
           }
         }
-        SA::template stash<kProbeA>(la, t, stA);
-        SB::template stash<kProbeB>(lb, t, stB);
+        SA::template stash<kProbeA, AEX>(la, t, stA);
+        SB::template stash<kProbeB, BEX>(lb, t, stB);
       }
       __syncthreads();
     };
