@@ -134,6 +134,10 @@ struct X6Args {
   // window's corner (cv_row with cv_sb = 0: qy cv_ys + qx cv_xs bytes). The bytes are exact in
   // bf16; the products are divided by cdiv (255: NormalizeImg) in the epilogue (GATH 5) or in the
   // split sum (GATH 6).
+  // GATH 7 (the data gradient without a padded copy): the source is the unpadded output gradient
+  // [B, cv_ih, cv_iw, C]; tap (ty, tx) of row (b, qy, qx) reads pixel (qy + ty - cv_ph, qx + tx -
+  // cv_pw), zero outside (cv_row's offsets are taken from the padded corner)
+  int cv_ph, cv_pw, cv_ih, cv_iw, cv_c;
   const uint8_t* u8;
   const int64_t* u8_idx;
   int64_t u8_img, u8_hw, u8_w;
@@ -368,6 +372,46 @@ struct X6Stage {
       piece_of(p < kPieces ? p : 0, rq, kq);
 #pragma unroll
       for (int j = 0; j < 4; ++j) roff[i][j] = x6_cv_row(g, row0 + 4 * rq + j);
+    }
+  }
+  // GATH 7: conv_rows plus each piece row's (qy, qx) for the bounds; load_rows_bounded zero-fills
+  // the taps outside the unpadded gradient
+  __device__ static void conv_rows_b(const X6Args& g, int row0, int t, int64_t (&roff)[kPer][4],
+                                     int (&qy)[kPer][4], int (&qx)[kPer][4]) {
+    static_assert(KC, "convolution rows are for a k-contiguous operand");
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int p = t + NT * i;
+      int rq, kq;
+      piece_of(p < kPieces ? p : 0, rq, kq);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        int b;
+        x6_cv_split(g, row0 + 4 * rq + j, b, qy[i][j], qx[i][j]);
+        roff[i][j] = b * g.cv_sb + (qy[i][j] - g.cv_ph) * g.cv_ys + (qx[i][j] - g.cv_pw) * g.cv_xs;
+      }
+    }
+  }
+  __device__ static void load_rows_bounded(const float* __restrict__ src, const X6Args& g,
+                                           const int64_t (&roff)[kPer][4], const int (&qy)[kPer][4],
+                                           const int (&qx)[kPer][4], int k0, int t,
+                                           floatx4 (&r)[kPer][4]) {
+    const int ty = k0 / g.cv_gseg, w0 = k0 - ty * g.cv_gseg;
+    const int64_t so = static_cast<int64_t>(ty) * g.cv_segs + w0;
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int p = t + NT * i;
+      if (kPieces % NT != 0 && p >= kPieces) continue;
+      int rq, kq;
+      piece_of(p, rq, kq);
+      const int tx = (w0 + 4 * kq) / g.cv_c;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int iy = qy[i][j] + ty - g.cv_ph, ix = qx[i][j] + tx - g.cv_pw;
+        const bool in = iy >= 0 && iy < g.cv_ih && ix >= 0 && ix < g.cv_iw;
+        r[i][j] = in ? *reinterpret_cast<const floatx4*>(src + roff[i][j] + so + 4 * kq)
+                     : floatx4{0.f, 0.f, 0.f, 0.f};
+      }
     }
   }
   // row-contiguous operand whose K index is a convolution row (GATH 4): B(n, k) =
@@ -720,10 +764,12 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
   // operand loads of K step k0 into a register set (GATH: through the gathered row offsets)
   static_assert(GATH == 0 || (GATH == 1 && AKC) || (GATH == 2 && !BKC && !BPL) ||
                     (GATH == 3 && AKC && !BPL) || (GATH == 4 && !BKC && !BPL) ||
-                    (GATH == 5 && AKC && !BPL) || (GATH == 6 && !BKC && !BPL),
+                    (GATH == 5 && AKC && !BPL) || (GATH == 6 && !BKC && !BPL) ||
+                    (GATH == 7 && AKC && !BPL),
                 "gather modes");
   constexpr bool kKRows = GATH == 4 || GATH == 6;  // B's K index walks convolution rows
-  int64_t roffA[(GATH == 1 || GATH == 3 || GATH == 5) ? SA::kPer : 1][4];
+  int64_t roffA[(GATH == 1 || GATH == 3 || GATH == 5 || GATH == 7) ? SA::kPer : 1][4];
+  int qyA[GATH == 7 ? SA::kPer : 1][4], qxA[GATH == 7 ? SA::kPer : 1][4];
   int64_t nsegB[kKRows ? SB::kPer : 1];
   int cbB[kKRows ? SB::kPer : 1][4], cpB[kKRows ? SB::kPer : 1][4];
   int64_t cbaseB[GATH == 6 ? SB::kPer : 1][4];
@@ -733,6 +779,8 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
     SA::gather_rows(g.gidx, g.gw, seg, g.gseg, g.sam, m0, t, roffA);
   } else if constexpr (GATH == 3) {
     SA::conv_rows(g, m0, t, roffA);
+  } else if constexpr (GATH == 7) {
+    SA::conv_rows_b(g, m0, t, roffA, qyA, qxA);
   } else if constexpr (GATH == 5) {
     SA::u8_rows(g, m0, t, roffA);
     for (int q = t; q < g.K / 4; q += NT) {
@@ -780,6 +828,7 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
     if constexpr (GATH == 1) SA::load_rows(A, roffA, k0, t, r);
     else if constexpr (GATH == 3) SA::load_rows(A, roffA, static_cast<int>(x6_cv_seg(g, k0)), t, r);
     else if constexpr (GATH == 5) SA::load_u8_rows(g.u8, roffA, gtbl, k0, t, r);
+    else if constexpr (GATH == 7) SA::load_rows_bounded(A, g, roffA, qyA, qxA, k0, t, r);
     else if constexpr (kBuf)
       SA::load_buf(bufA, t, static_cast<int32_t>(4 * (AKC ? (k0 - kb * kX6BK)
                                                         : (k0 - kb * kX6BK) * g.sak)), r);
@@ -1247,7 +1296,7 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
     for (int r = 0; r < 4; ++r) {
       const int row = wr0 + 16 * i + 4 * fc + r;
       orow[i][r] = static_cast<int64_t>(row) * g.ldc;
-      if constexpr (GATH == 3) {
+      if constexpr (GATH == 3 || GATH == 7) {
         if (g.cv_out) {
           int b, qy, qx;
           x6_cv_split(g, row, b, qy, qx);
@@ -1261,7 +1310,7 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
     const int col = wc0 + 16 * j + fr;
     const float bv = g.bias ? g.bias[col] : 0.f;
     int64_t ocol = col;
-    if constexpr (GATH == 3) {
+    if constexpr (GATH == 3 || GATH == 7) {
       if (g.cv_out) {
         const int c = col / g.co_cw, py = c / g.co_cs;
         ocol = py * g.co_cy + (c - py * g.co_cs) * g.co_cx + (col - c * g.co_cw);
@@ -1918,7 +1967,7 @@ template <int FM, int FN, int WGM, int WGN, int GATH>
 static void launch_conv_t(hipStream_t s, X6Args& g) {
   g.tiles_m = g.M / (16 * FM * WGM);
   g.tiles_n = g.N / (16 * FN * WGN);
-  constexpr bool KC = GATH == 3 || GATH == 5;  // forward form: both k-contiguous; wgrad: neither
+  constexpr bool KC = GATH == 3 || GATH == 5 || GATH == 7;  // rows forms: k-contiguous; wgrad: neither
   hipLaunchKernelGGL((gemm_x6_kernel<FM, FN, WGM, WGN, KC, KC, false, true, false, GATH>),
                      dim3(g.units), dim3(64 * WGM * WGN), 0, s, g);
 }
@@ -1935,6 +1984,13 @@ static bool launch_conv(hipStream_t s, int mode, int tile, X6Args& g) {
     else if (tile == 4) launch_conv_t<2, 4, 2, 2, 6>(s, g);
     else return false;
     return true;
+  }
+  if (mode == 4) {  // the data gradient from the unpadded output gradient (bounded rows)
+    switch (tile) {
+      case 2: launch_conv_t<4, 2, 2, 2, 7>(s, g); return true;
+      case 5: launch_conv_t<4, 4, 2, 2, 7>(s, g); return true;
+      default: return false;
+    }
   }
   if (mode == 0) {
     switch (tile) {
@@ -1987,7 +2043,7 @@ __global__ __launch_bounds__(64 * kSumGroups) void sum_parts_kernel(const float*
 extern "C" int ocppo_conv_x6(ocppo_stream_t stream, int mode, const float* x, const int64_t* geom,
                              const float* w, int64_t ldw, float* c, int64_t ldc, int64_t M,
                              int64_t N, int64_t K, int64_t splits, const float* bias, int relu,
-                             const int64_t* out_geom, int tile, float* out) {
+                             const int64_t* out_geom, int tile, float* out, const int64_t* pad) {
   OCPPO_REQUIRE(mode == 0 || mode == 1, "ocppo_conv_x6: mode %d (0 rows, 1 weight gradient)", mode);
   OCPPO_REQUIRE(tile >= 0 && tile < 7, "ocppo_conv_x6: tile %d", tile);
   OCPPO_REQUIRE(x && geom && w && c, "ocppo_conv_x6: null pointer");
@@ -2075,9 +2131,27 @@ extern "C" int ocppo_conv_x6(ocppo_stream_t stream, int mode, const float* x, co
     g.ldc = N;
     g.split_c = M * N;
   }
+  int lmode = mode;
+  if (pad) {
+    // x is the UNPADDED gradient [B, ih, iw, C]; geom's strides describe the padded one it stands
+    // for (ys = (iw + 2 pw) C would be the padded row): rebuilt here for the unpadded source
+    OCPPO_REQUIRE(mode == 0 && splits == 1 && pad[0] >= 0 && pad[1] >= 0 && pad[2] >= 1 &&
+                      pad[3] >= 1 && pad[4] >= 4 && pad[4] % 4 == 0 && gseg % pad[4] == 0,
+                  "ocppo_conv_x6: pad = {ph, pw, ih, iw, C} (the rows form only)");
+    g.cv_ph = (int)pad[0];
+    g.cv_pw = (int)pad[1];
+    g.cv_ih = (int)pad[2];
+    g.cv_iw = (int)pad[3];
+    g.cv_c = (int)pad[4];
+    g.cv_sb = pad[2] * pad[3] * pad[4];
+    g.cv_ys = pad[3] * pad[4];
+    g.cv_xs = pad[4];
+    g.cv_segs = pad[3] * pad[4];
+    lmode = 4;
+  }
   clear_stale_error();
   hipStream_t s = as_stream(stream);
-  OCPPO_REQUIRE(launch_conv(s, mode, tile, g), "ocppo_conv_x6: tile %d not built for mode %d",
+  OCPPO_REQUIRE(launch_conv(s, lmode, tile, g), "ocppo_conv_x6: tile %d not built for mode %d",
                 tile, mode);
   if (int rc = check_launch("ocppo_conv_x6")) return rc;
   if (mode == 1) {

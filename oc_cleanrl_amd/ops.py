@@ -778,7 +778,7 @@ def conv_x6(x, weight, bias=None, stride: int = 1, relu: bool = True, out=None):
     if S == 1:
         call("ocppo_conv_x6", _stream(dev), 0, x.data_ptr(), geom, wm.data_ptr(), K,
              out.data_ptr(), Cout, M, Cout, K, 1, _opt(bias, "bias", f, dev, Cout),
-             int(bool(relu)), None, tile, None)
+             int(bool(relu)), None, tile, None, None)
         return out
     # few rows (the rollout's batch): K-split partials, then bias + ReLU on their ordered sum
     key = ("fwd", str(dev), S, M, Cout)
@@ -786,7 +786,7 @@ def conv_x6(x, weight, bias=None, stride: int = 1, relu: bool = True, out=None):
         _CONV_PARTS[key] = torch.empty((S, M, Cout), dtype=f, device=dev)
     part = _CONV_PARTS[key]
     call("ocppo_conv_x6", _stream(dev), 0, x.data_ptr(), geom, wm.data_ptr(), K, part.data_ptr(),
-         Cout, M, Cout, K, S, None, 0, None, tile, None)
+         Cout, M, Cout, K, S, None, 0, None, tile, None, None)
     call("ocppo_sum_splits_act", _stream(dev), part.data_ptr(), S, M, Cout,
          _opt(bias, "bias", f, dev, Cout), int(bool(relu)), out.data_ptr())
     return out
@@ -842,7 +842,7 @@ def conv_x6_wgrad(gp, x, kernel: tuple, stride: int, out=None):
     call("ocppo_conv_x6", _stream(dev), 1, x.data_ptr(),
          _geom(OH, OW, H * W * C, s * W * C, s * C, W * C, KW * C),
          _check(gp, "gp", f, dev), Cout, part.data_ptr(), N, Cout, N, rows, S, None, 0, None, tile,
-         out.data_ptr())
+         out.data_ptr(), None)
     return out
 
 
@@ -860,7 +860,6 @@ def conv_x6_dgrad(gp, weight, stride: int, in_hw: tuple, out=None):
     g = gp.permute(0, 2, 3, 1)  # NHWC view
     if not g.is_contiguous():
         g = g.contiguous()
-    gpad = torch.nn.functional.pad(g, (0, 0, TW - 1, TW - 1, T - 1, T - 1))
     Hp, Wp = OH + 2 * (T - 1), OW + 2 * (TW - 1)
     QH, QW = H // s, W // s
     M, K = B * QH * QW, T * TW * Cout
@@ -875,10 +874,22 @@ def conv_x6_dgrad(gp, weight, stride: int, in_hw: tuple, out=None):
     wc = torch.stack([weight[:, :, py::s, px::s].flip(2, 3).permute(1, 2, 3, 0)
                       for py in range(s) for px in range(s)]).reshape(N, K)
     og = None if s == 1 else _geom(H * W * C, s * W * C, s * C, 0, C, s, W * C, C)
-    call("ocppo_conv_x6", _stream(dev), 0, gpad.data_ptr(),
-         _geom(QH, QW, Hp * Wp * Cout, Wp * Cout, Cout, Wp * Cout, TW * Cout), wc.data_ptr(), K,
-         out.data_ptr(), C, M, N, K, 1, None, 0, og, tile, None)
+    if CONV_DGRAD_PAD_COPY or tile not in (2, 5):
+        gpad = torch.nn.functional.pad(g, (0, 0, TW - 1, TW - 1, T - 1, T - 1))
+        call("ocppo_conv_x6", _stream(dev), 0, gpad.data_ptr(),
+             _geom(QH, QW, Hp * Wp * Cout, Wp * Cout, Cout, Wp * Cout, TW * Cout), wc.data_ptr(),
+             K, out.data_ptr(), C, M, N, K, 1, None, 0, og, tile, None, None)
+        return out
+    # the padding as bounds in the loader: taps outside the gradient read as zeros
+    call("ocppo_conv_x6", _stream(dev), 0, g.data_ptr(),
+         _geom(QH, QW, 0, 0, 0, 0, TW * Cout), wc.data_ptr(), K, out.data_ptr(), C, M, N, K, 1,
+         None, 0, og, tile, None, _geom(T - 1, TW - 1, OH, OW, Cout))
     return out
+
+
+# the data gradient over a zero-padded copy of the output gradient (F.pad: a fill and a copy per
+# layer) instead of the bounded loader
+CONV_DGRAD_PAD_COPY = False
 
 
 def conv_x6_u8_ok(src, weight, stride: int, B: int, wgrad: bool = False) -> bool:

@@ -92,7 +92,10 @@ def test_weight_gradient(name):
 
 
 @pytest.mark.parametrize("name", ["conv2", "conv3"])
-def test_data_gradient(name):
+@pytest.mark.parametrize("pad_copy", [False, True])
+def test_data_gradient(name, pad_copy, monkeypatch):
+    """pad_copy: over an F.pad copy of the output gradient; else the loader's bounds (default)."""
+    monkeypatch.setattr(ops, "CONV_DGRAD_PAD_COPY", pad_copy)
     x, w, _, s = _operands(name, 3)
     Cout, C, K, _ = w.shape
     H = x.shape[2]
