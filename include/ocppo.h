@@ -485,9 +485,13 @@ OCPPO_API int ocppo_gemm_x6_gather(ocppo_stream_t stream, const float* a, int64_
  *   mode 1 (weight gradient): out[m, n] = sum_r w[r ldw + m] x(r, n) (w = the output gradient
  *          [rows, ldw], m < M = Cout, n < N = KH KW C, r < K = B qh qw); c = split partials
  *          [splits, M, N], then summed in split order (f64, one rounding) into out; qh qw <= 1024.
+ * mask (mode 0, or null; needs dbp, no bias / ReLU): the layer below's ReLU backward in the
+ * epilogue, c = mask > 0 ? acc : 0 with mask in c's layout, and each row tile's column sums of c
+ * in dbp [M / tile rows, N] (that layer's bias-gradient partials).
  * pad (mode 0, or null): {ph, pw, ih, iw, C}: x is the UNPADDED [B, ih, iw, C] tensor that the
  * rows index as if zero-padded by ph rows / pw columns on each side (the data gradient's padded
- * output gradient, never materialised; geom's qh, qw, gseg as for the padded one; tile 2 or 5).
+ * output gradient, never materialised; geom's qh, qw, gseg as for the padded one; tile 2, 3,
+ * 5 or 6).
  * tile: 0 = 128 x 32, 2 = 128 x 64, 3 = 64 x 64, 5 = 128 x 128, 6 = 32 x 64 (mode 0); 1 =
  * 32 x 128, 3, 4 =
  * 64 x 128, 5 (mode 1); M, N multiples of it; K % 32 == 0, K / 32 >= splits.
@@ -495,7 +499,8 @@ OCPPO_API int ocppo_gemm_x6_gather(ocppo_stream_t stream, const float* a, int64_
 OCPPO_API int ocppo_conv_x6(ocppo_stream_t stream, int mode, const float* x, const int64_t* geom,
                             const float* w, int64_t ldw, float* c, int64_t ldc, int64_t M,
                             int64_t N, int64_t K, int64_t splits, const float* bias, int relu,
-                            const int64_t* out_geom, int tile, float* out, const int64_t* pad);
+                            const int64_t* out_geom, int tile, float* out, const int64_t* pad,
+                            const float* mask, float* dbp);
 
 /* ---------------------------------------------------------------------------------------------
  * The first NatureCNN convolution straight from the rollout's u8 frame stacks (ppo_atari_oc.py:566

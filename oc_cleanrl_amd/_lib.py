@@ -102,7 +102,8 @@ SIGNATURES: dict[str, tuple[type, list]] = {
     "ocppo_frames_expand_index": (I, [P, P, P, I64, P, I64, I64, I64, P]),
     "ocppo_gemm_x6_wgrad": (I, [P, P, I64, I64, P, I64, I64, I64, I64, I64, P, I64, P, I64, I64,
                                 P, P, P, I64, I, P]),
-    "ocppo_conv_x6": (I, [P, I, P, P, P, I64, P, I64, I64, I64, I64, I64, P, I, P, I, P, P]),
+    "ocppo_conv_x6": (I, [P, I, P, P, P, I64, P, I64, I64, I64, I64, I64, P, I, P, I, P, P, P,
+                          P]),
     "ocppo_conv_x6_u8": (I, [P, I, P, P, I64, I64, I64, I64, I64, I64, P, I64, P, I64, I64, I64,
                              I64, P, I, ctypes.c_float, I, P]),
     "ocppo_deferred_finish_run": (I, [P, P]),

@@ -616,13 +616,14 @@ class _ConvX6(torch.autograd.Function):
     speed. nn.Conv2d + nn.ReLU's arithmetic at f32 accuracy (architectures/ppo.py:20-31)."""
 
     @staticmethod
-    def forward(ctx, x, w, b, stride, relu: bool):
+    def forward(ctx, x, w, b, stride, relu: bool, box=None, below=None):
         B, Cin, H, W = x.shape
         Cout = w.shape[0]
         y = ops.timed(f"conv_x6_{B}x{Cin}x{H}_{Cout}",
                       lambda: ops.conv_x6(x, w, b, stride, relu))
         ctx.conv = (stride, relu)
         ctx.b = b
+        ctx.box, ctx.below = box, below
         ctx.save_for_backward(x, w, y if relu else None)
         return y
 
@@ -635,11 +636,7 @@ class _ConvX6(torch.autograd.Function):
         B, C, OH, OW = g.shape
         g2 = g.permute(0, 2, 3, 1).reshape(-1, C)
         b = ctx.b
-        direct_b = _direct(b)
-        db_out = b.grad if direct_b else torch.empty_like(b)
-        o2 = y.permute(0, 2, 3, 1).reshape(-1, C) if relu else None
-        gp2, _ = ops.timed(f"relu_bias_grad_{g2.shape[0]}x{C}" + ("" if relu else "_norelu"),
-                           lambda: ops.relu_bias_grad(g2, o2, db=db_out))
+        gp2, db_out, direct_b = _conv_relu_backward(ctx.box, g2, y, b, relu)
         KH, KW = w.shape[2], w.shape[3]
         dw = None
         if ctx.needs_input_grad[1]:
@@ -655,9 +652,37 @@ class _ConvX6(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             gp = gp2.view(B, OH, OW, C).permute(0, 3, 1, 2)
-            dx = ops.timed(f"conv_x6_dgrad_{C}x{x.shape[1]}",
-                           lambda: ops.conv_x6_dgrad(gp, w, stride, (x.shape[2], x.shape[3])))
-        return dx, dw, (None if direct_b else db_out), None, None
+            hw = (x.shape[2], x.shape[3])
+            below = ctx.below
+            if below is not None and ops.conv_x6_dgrad_fuses_relu(
+                    B * (hw[0] // stride) * (hw[1] // stride), x.shape[1], stride):
+                # the layer below's ReLU backward + bias gradient in this dX's epilogue
+                bb = below["bias"]
+                db_below = bb.grad if _direct(bb) else torch.empty_like(bb)
+                dx = ops.timed(f"conv_x6_dgrad_relu_{C}x{x.shape[1]}",
+                               lambda: ops.conv_x6_dgrad(gp, w, stride, hw, relu_out=x,
+                                                         db=db_below))
+                below.update(premasked=True, db=db_below)
+            else:
+                dx = ops.timed(f"conv_x6_dgrad_{C}x{x.shape[1]}",
+                               lambda: ops.conv_x6_dgrad(gp, w, stride, hw))
+        return dx, dw, (None if direct_b else db_out), None, None, None, None
+
+
+def _conv_relu_backward(box, g2, y, b, relu: bool):
+    """(gp rows, bias gradient, whether it went to b.grad in place) of a convolution + ReLU whose
+    output gradient rows are g2: one relu_bias_grad pass, or nothing when the layer above's data
+    gradient already applied this ReLU's backward and wrote the bias gradient (box premasked)."""
+    direct_b = _direct(b)
+    if box is not None and box.get("premasked"):
+        box["premasked"] = False
+        return g2, box["db"], direct_b
+    C = g2.shape[1]
+    db_out = b.grad if direct_b else torch.empty_like(b)
+    o2 = y.permute(0, 2, 3, 1).reshape(-1, C) if relu else None
+    gp2, _ = ops.timed(f"relu_bias_grad_{g2.shape[0]}x{C}" + ("" if relu else "_norelu"),
+                       lambda: ops.relu_bias_grad(g2, o2, db=db_out))
+    return gp2, db_out, direct_b
 
 
 class _ConvX6U8(torch.autograd.Function):
@@ -667,11 +692,12 @@ class _ConvX6U8(torch.autograd.Function):
     relu_bias_grad, then the weight gradient from the same u8 rows (the input needs none)."""
 
     @staticmethod
-    def forward(ctx, w, b, frames, idx, stride, relu: bool, divisor: float):
+    def forward(ctx, w, b, frames, idx, stride, relu: bool, divisor: float, box=None):
         y = ops.timed(f"conv_x6_u8_{idx.numel()}",
                       lambda: ops.conv_x6_u8(frames, idx, w, b, stride, relu, divisor))
         ctx.conv = (stride, relu, divisor)
         ctx.b = b
+        ctx.box = box
         ctx.save_for_backward(w, frames, idx, y if relu else None)
         return y
 
@@ -683,11 +709,7 @@ class _ConvX6U8(torch.autograd.Function):
         C = g.shape[1]
         g2 = g.permute(0, 2, 3, 1).reshape(-1, C)
         b = ctx.b
-        direct_b = _direct(b)
-        db_out = b.grad if direct_b else torch.empty_like(b)
-        o2 = y.permute(0, 2, 3, 1).reshape(-1, C) if relu else None
-        gp2, _ = ops.timed(f"relu_bias_grad_{g2.shape[0]}x{C}" + ("" if relu else "_norelu"),
-                           lambda: ops.relu_bias_grad(g2, o2, db=db_out))
+        gp2, db_out, direct_b = _conv_relu_backward(ctx.box, g2, y, b, relu)
         dw = None
         if ctx.needs_input_grad[0]:
             KH, KW = w.shape[2], w.shape[3]
@@ -697,7 +719,7 @@ class _ConvX6U8(torch.autograd.Function):
             if _direct(w):
                 w.grad.copy_(dw)  # nn.Conv2d's tap order into the channels_last grad
                 dw = None
-        return dw, (None if direct_b else db_out), None, None, None, None, None
+        return dw, (None if direct_b else db_out), None, None, None, None, None, None
 
 
 # The update's first convolution straight from the u8 frame stacks (_ConvX6U8) when the trunk
@@ -722,11 +744,24 @@ def _conv_x6_ok(x, conv) -> bool:
                           dgrad=grad and x.requires_grad)
 
 
+# The data gradient of a convolution whose input is another convolution's ReLU output can take
+# that ReLU's backward and bias gradient in its epilogue (ops.conv_x6_dgrad relu_out / db; no
+# relu_bias_grad pass over the input gradient). Measured slower at config 3 (805 / 515 us per
+# update against 371 + 254 / 373 + 105 us unfused: the masked, column-summing epilogue over the
+# stride classes' scattered rows costs more than the streaming pass it removes): off by default
+CONV_DGRAD_RELU = False
+
+
 def _conv_x6(x, conv, relu: bool):
     s = conv.stride[0]
     if torch.is_grad_enabled() and (x.requires_grad or conv.weight.requires_grad or
                                     conv.bias.requires_grad):
-        return _ConvX6.apply(x, conv.weight, conv.bias, s, relu)
+        box = {"bias": conv.bias} if relu and CONV_DGRAD_RELU else None
+        y = _ConvX6.apply(x, conv.weight, conv.bias, s, relu, box,
+                          getattr(x, "_ocppo_cbox", None))
+        if box is not None:
+            y._ocppo_cbox = box
+        return y
     B, Cin, H, _ = x.shape
     return ops.timed(f"conv_x6_{B}x{Cin}x{H}_{conv.out_channels}",
                      lambda: ops.conv_x6(x, conv.weight, conv.bias, s, relu))
@@ -954,7 +989,10 @@ class _ActorCritic(Predictor):
             net = net[1:]
         conv = net[0]
         relu = isinstance(net[1], nn.ReLU)
-        y = _ConvX6U8.apply(conv.weight, conv.bias, frames, idx, conv.stride[0], relu, div)
+        box = {"bias": conv.bias} if relu and CONV_DGRAD_RELU else None
+        y = _ConvX6U8.apply(conv.weight, conv.bias, frames, idx, conv.stride[0], relu, div, box)
+        if box is not None:
+            y._ocppo_cbox = box
         return fused_trunk(net[2 if relu else 1:], y)
 
     def _head(self, lin, h):

@@ -1241,6 +1241,32 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
     }
     return;
   }
+  // output row offsets: r ldc, or a convolution stride class's rows (GATH 3 / 7, cv_out)
+  int64_t orow[FM][4];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = wr0 + 16 * i + 4 * fc + r;
+      orow[i][r] = static_cast<int64_t>(row) * g.ldc;
+      if constexpr (GATH == 3 || GATH == 7) {
+        if (g.cv_out) {
+          int b, qy, qx;
+          x6_cv_split(g, row, b, qy, qx);
+          orow[i][r] = b * g.co_sb + qy * g.co_ys + qx * g.co_xs + g.co_off;
+        }
+      }
+    }
+  // output column offset of column col (a stride class's channel under cv_out)
+  auto ocol_of = [&](int col) -> int64_t {
+    if constexpr (GATH == 3 || GATH == 7) {
+      if (g.cv_out) {
+        const int c = col / g.co_cw, py = c / g.co_cs;
+        return py * g.co_cy + (c - py * g.co_cs) * g.co_cx + (col - c * g.co_cw);
+      }
+    }
+    return col;
+  };
   if (g.mask || g.mbits_in) {
     // threshold_backward(acc, mask, 0) and the tile's column sums: rows of a lane (i, r) in
     // order, then the wave's 4 row groups (xor 16, 32), then the two wave rows through LDS
@@ -1249,6 +1275,7 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int col = wc0 + 16 * j + fr;
+      const int64_t ocol = ocol_of(col);
       float cs = 0.f;
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
@@ -1256,10 +1283,13 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
         for (int r = 0; r < 4; ++r) {
           const int64_t row = wr0 + 16 * i + 4 * fc + r;
           const float acc = LO ? hi[i][j][r] + lo[LO ? i : 0][LO ? j : 0][r] : hi[i][j][r];
+          // the mask shares the output's layout under cv_out (the convolution data gradient)
+          bool cvo = false;
+          if constexpr (GATH == 3 || GATH == 7) cvo = g.cv_out != 0;
           const bool on = g.mbits_in ? ((bits >> ((i * FN + j) * 4 + r)) & 1) != 0
-                                     : g.mask[row * g.ldm + col] > 0.f;
+                                     : g.mask[cvo ? orow[i][r] + ocol : row * g.ldm + col] > 0.f;
           const float v = on ? acc : 0.f;
-          Cp[row * g.ldc + col] = v;
+          Cp[orow[i][r] + ocol] = v;
           cs += v;
         }
       }
@@ -1288,34 +1318,12 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
     return;
   }
   static_assert(FM * FN * 4 <= 64, "one 64-bit mask word per thread and tile");
-  // output row offsets: r ldc, or a convolution stride class's rows (GATH 3, cv_out)
-  int64_t orow[FM][4];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = wr0 + 16 * i + 4 * fc + r;
-      orow[i][r] = static_cast<int64_t>(row) * g.ldc;
-      if constexpr (GATH == 3 || GATH == 7) {
-        if (g.cv_out) {
-          int b, qy, qx;
-          x6_cv_split(g, row, b, qy, qx);
-          orow[i][r] = b * g.co_sb + qy * g.co_ys + qx * g.co_xs + g.co_off;
-        }
-      }
-    }
   uint64_t bits = 0;
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
     const int col = wc0 + 16 * j + fr;
     const float bv = g.bias ? g.bias[col] : 0.f;
-    int64_t ocol = col;
-    if constexpr (GATH == 3 || GATH == 7) {
-      if (g.cv_out) {
-        const int c = col / g.co_cw, py = c / g.co_cs;
-        ocol = py * g.co_cy + (c - py * g.co_cs) * g.co_cx + (col - c * g.co_cw);
-      }
-    }
+    const int64_t ocol = ocol_of(col);
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
 #pragma unroll
@@ -1988,7 +1996,9 @@ static bool launch_conv(hipStream_t s, int mode, int tile, X6Args& g) {
   if (mode == 4) {  // the data gradient from the unpadded output gradient (bounded rows)
     switch (tile) {
       case 2: launch_conv_t<4, 2, 2, 2, 7>(s, g); return true;
+      case 3: launch_conv_t<2, 2, 2, 2, 7>(s, g); return true;
       case 5: launch_conv_t<4, 4, 2, 2, 7>(s, g); return true;
+      case 6: launch_conv_t<2, 2, 1, 2, 7>(s, g); return true;
       default: return false;
     }
   }
@@ -2043,7 +2053,8 @@ __global__ __launch_bounds__(64 * kSumGroups) void sum_parts_kernel(const float*
 extern "C" int ocppo_conv_x6(ocppo_stream_t stream, int mode, const float* x, const int64_t* geom,
                              const float* w, int64_t ldw, float* c, int64_t ldc, int64_t M,
                              int64_t N, int64_t K, int64_t splits, const float* bias, int relu,
-                             const int64_t* out_geom, int tile, float* out, const int64_t* pad) {
+                             const int64_t* out_geom, int tile, float* out, const int64_t* pad,
+                             const float* mask, float* dbp) {
   OCPPO_REQUIRE(mode == 0 || mode == 1, "ocppo_conv_x6: mode %d (0 rows, 1 weight gradient)", mode);
   OCPPO_REQUIRE(tile >= 0 && tile < 7, "ocppo_conv_x6: tile %d", tile);
   OCPPO_REQUIRE(x && geom && w && c, "ocppo_conv_x6: null pointer");
@@ -2098,6 +2109,13 @@ extern "C" int ocppo_conv_x6(ocppo_stream_t stream, int mode, const float* x, co
     g.split_c = M * N;  // splits > 1: partials [splits, M, N] (ocppo_sum_splits_act adds them)
     g.bias = bias;
     g.relu = relu ? 1 : 0;
+    if (mask) {  // the layer below's ReLU backward: c = mask > 0 ? acc : 0, column sums -> dbp
+      OCPPO_REQUIRE(dbp && splits == 1 && bias == nullptr && !relu,
+                    "ocppo_conv_x6: the mask epilogue needs dbp, splits == 1, no bias / ReLU");
+      g.mask = mask;
+      g.ldm = ldc;
+      g.dbp = dbp;
+    }
     if (out_geom) {
       g.cv_out = 1;
       g.co_sb = out_geom[0];

@@ -778,7 +778,7 @@ def conv_x6(x, weight, bias=None, stride: int = 1, relu: bool = True, out=None):
     if S == 1:
         call("ocppo_conv_x6", _stream(dev), 0, x.data_ptr(), geom, wm.data_ptr(), K,
              out.data_ptr(), Cout, M, Cout, K, 1, _opt(bias, "bias", f, dev, Cout),
-             int(bool(relu)), None, tile, None, None)
+             int(bool(relu)), None, tile, None, None, None, None)
         return out
     # few rows (the rollout's batch): K-split partials, then bias + ReLU on their ordered sum
     key = ("fwd", str(dev), S, M, Cout)
@@ -786,7 +786,7 @@ def conv_x6(x, weight, bias=None, stride: int = 1, relu: bool = True, out=None):
         _CONV_PARTS[key] = torch.empty((S, M, Cout), dtype=f, device=dev)
     part = _CONV_PARTS[key]
     call("ocppo_conv_x6", _stream(dev), 0, x.data_ptr(), geom, wm.data_ptr(), K, part.data_ptr(),
-         Cout, M, Cout, K, S, None, 0, None, tile, None, None)
+         Cout, M, Cout, K, S, None, 0, None, tile, None, None, None, None)
     call("ocppo_sum_splits_act", _stream(dev), part.data_ptr(), S, M, Cout,
          _opt(bias, "bias", f, dev, Cout), int(bool(relu)), out.data_ptr())
     return out
@@ -842,15 +842,23 @@ def conv_x6_wgrad(gp, x, kernel: tuple, stride: int, out=None):
     call("ocppo_conv_x6", _stream(dev), 1, x.data_ptr(),
          _geom(OH, OW, H * W * C, s * W * C, s * C, W * C, KW * C),
          _check(gp, "gp", f, dev), Cout, part.data_ptr(), N, Cout, N, rows, S, None, 0, None, tile,
-         out.data_ptr(), None)
+         out.data_ptr(), None, None, None)
     return out
 
 
-def conv_x6_dgrad(gp, weight, stride: int, in_hw: tuple, out=None):
+def conv_x6_dgrad_fuses_relu(M: int, C: int, stride: int) -> bool:
+    """conv_x6_dgrad can take the layer below's ReLU backward (the bounded loader's tiles)."""
+    return not CONV_DGRAD_PAD_COPY and _conv_fwd_tile(M, stride * stride * C) in (2, 3, 5, 6)
+
+
+def conv_x6_dgrad(gp, weight, stride: int, in_hw: tuple, out=None, relu_out=None, db=None):
     """dX of a convolution: gp channels_last [B, Cout, OH, OW] (the output gradient), weight
     [Cout, C, KH, KW] -> channels_last [B, C, H, W]. Per stride class (py, px) a forward-form
     product over gp zero-padded by KH / s - 1 with that class's taps flipped; each input pixel
-    gets its <= (KH / s)^2 taps in one fixed order (deterministic)."""
+    gets its <= (KH / s)^2 taps in one fixed order (deterministic). relu_out: the layer below's
+    ReLU output (channels_last [B, C, H, W]): its ReLU backward in the epilogue (dX masked where
+    relu_out <= 0) and its bias gradient (the masked dX's per-channel sums, row tiles and classes
+    added in order in f64) into db [C]."""
     B, Cout, OH, OW = gp.shape
     _, C, KH, KW = weight.shape
     H, W = in_hw
@@ -874,16 +882,29 @@ def conv_x6_dgrad(gp, weight, stride: int, in_hw: tuple, out=None):
     wc = torch.stack([weight[:, :, py::s, px::s].flip(2, 3).permute(1, 2, 3, 0)
                       for py in range(s) for px in range(s)]).reshape(N, K)
     og = None if s == 1 else _geom(H * W * C, s * W * C, s * C, 0, C, s, W * C, C)
-    if CONV_DGRAD_PAD_COPY or tile not in (2, 5):
+    if CONV_DGRAD_PAD_COPY or tile not in (2, 3, 5, 6):
         gpad = torch.nn.functional.pad(g, (0, 0, TW - 1, TW - 1, T - 1, T - 1))
+        if relu_out is not None:
+            raise ValueError("conv_x6_dgrad: the ReLU epilogue needs the bounded loader")
         call("ocppo_conv_x6", _stream(dev), 0, gpad.data_ptr(),
              _geom(QH, QW, Hp * Wp * Cout, Wp * Cout, Cout, Wp * Cout, TW * Cout), wc.data_ptr(),
-             K, out.data_ptr(), C, M, N, K, 1, None, 0, og, tile, None, None)
+             K, out.data_ptr(), C, M, N, K, 1, None, 0, og, tile, None, None, None, None)
         return out
     # the padding as bounds in the loader: taps outside the gradient read as zeros
+    mask = dbp = None
+    if relu_out is not None:
+        if tuple(relu_out.shape) != (B, C, H, W) or not relu_out.is_contiguous(
+                memory_format=torch.channels_last) or db is None:
+            raise ValueError("conv_x6_dgrad: relu_out must be channels_last [B, C, H, W], with db")
+        mask = relu_out
+        dbp = torch.empty((M // _CONV_TILES[tile][0], N), dtype=f, device=dev)
     call("ocppo_conv_x6", _stream(dev), 0, g.data_ptr(),
          _geom(QH, QW, 0, 0, 0, 0, TW * Cout), wc.data_ptr(), K, out.data_ptr(), C, M, N, K, 1,
-         None, 0, og, tile, None, _geom(T - 1, TW - 1, OH, OW, Cout))
+         None, 0, og, tile, None, _geom(T - 1, TW - 1, OH, OW, Cout),
+         None if mask is None else mask.data_ptr(), None if dbp is None else dbp.data_ptr())
+    if dbp is not None:
+        # row tiles, then stride classes, in order (f64, one rounding)
+        db.copy_(dbp.view(-1, s * s, C).double().sum(0).sum(0))
     return out
 
 

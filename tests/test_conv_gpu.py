@@ -174,3 +174,26 @@ def test_u8_first_conv_weight_gradient():
     lib = torch.nn.grad.conv2d_weight(x.contiguous(memory_format=CL), w.shape, gp, stride=s)
     _check(dw, ref, scale, lib)
     assert torch.equal(dw, ops.conv_x6_u8_wgrad(rows, src, idx, (8, 8), s).view(w.shape))
+
+
+@pytest.mark.parametrize("name", ["conv2", "conv3"])
+def test_data_gradient_takes_the_relu_backward_below(name):
+    """relu_out: the layer below's ReLU backward in the data gradient's epilogue — bitwise the
+    unfused dX masked where relu_out <= 0 — and its bias gradient from the masked sums (f64)."""
+    x, w, _, s = _operands(name, 9)
+    Cout, C, K, _ = w.shape
+    H = x.shape[2]
+    OH = (H - K) // s + 1
+    g = torch.Generator(device=DEV).manual_seed(10)
+    gp = (torch.rand(x.shape[0], Cout, OH, OH, device=DEV, generator=g) * 2 - 1
+          ).contiguous(memory_format=CL)
+    below = (torch.rand(x.shape, device=DEV, generator=g) - 0.4).clamp_min(0).contiguous(
+        memory_format=CL)  # a ReLU output: ~40 % zeros
+    assert ops.conv_x6_dgrad_fuses_relu(x.shape[0] * (H // s) ** 2, C, s)
+    db = torch.empty(C, device=DEV)
+    fused = ops.conv_x6_dgrad(gp, w, s, (H, H), relu_out=below, db=db)
+    plain = ops.conv_x6_dgrad(gp, w, s, (H, H))
+    want = torch.where(below > 0, plain, torch.zeros_like(plain))
+    assert torch.equal(fused, want)
+    ref = want.double().sum((0, 2, 3))
+    assert torch.allclose(db.double(), ref, rtol=1e-6, atol=1e-6 * float(want.abs().sum()) / C)
