@@ -62,6 +62,10 @@ FUSED_HEAD_ENV = True
 # the step took 23.9 instead of 12.3 us against the 5.2 us split launch it replaces
 # (profiles/r05/breakdown_config2.txt vs the round-4 trace)
 ADAM_WRITES_PLANES = False
+# Pixel trunks: the rollout's first convolution reads the u8 frame stacks of the rollout buffer's
+# slot t (agents.trunk_frames: exact bf16 operands, NormalizeImg in the epilogue) instead of the
+# f32 network copy the store writes
+U8_ROLLOUT_CONV = True
 
 
 class FlatGrads:
@@ -447,6 +451,10 @@ class PPOTrainer:
         self.u8_first_conv = (not self.frame_dedup and self.b_obs.dtype == torch.uint8 and
                               self.prescale and hasattr(self.agent, "trunk_frames_ok") and
                               self.agent.trunk_frames_ok(self.b_obs, self.M))
+        # ... and so does the rollout's, from slot t of the rollout buffer (no f32 stack read)
+        self.u8_rollout = (U8_ROLLOUT_CONV and self.u8_first_conv and not self.frame_cache and
+                           self.agent.trunk_frames_ok(self.obs[0], self.N))
+        self.env_rows = torch.arange(self.N, dtype=torch.int64, device=dev)
         self.wplanes, self.wplanes_built = None, False  # built at the first minibatch
         self.planes_by_opt = False
         # GAE's per-sample records for the minibatch gather (ops.sample_records)
@@ -570,6 +578,8 @@ class PPOTrainer:
         frame cache: step 0 encodes all W frames (the weights changed since the last rollout),
         later steps encode only the newest frame and shift the cache with done row t."""
         if not self.frame_cache:
+            if self.u8_rollout:  # the first convolution reads slot t's u8 stacks itself
+                return self.agent.trunk_frames(self.obs[t], self.env_rows)
             return self.agent.trunk(self.net_obs, self.prescale)
         self._policy_encode(t)
         return self._decode_cache(t)
@@ -641,7 +651,8 @@ class PPOTrainer:
                 hidden, ag.actor.weight, ag.actor.bias, ag.critic.weight, ag.critic.bias,
                 self.noise[t], self.actions[t], self.logprobs[t], self.values[t], philox=px))
         else:
-            logits, value = ag.logits_and_value(self.net_obs, self.prescale)
+            logits, value = (ag.heads(ag.trunk_frames(self.obs[t], self.env_rows))
+                             if self.u8_rollout else ag.logits_and_value(self.net_obs, self.prescale))
             self.timer.bracket("action_head", lambda: ops.categorical_sample(
                 logits, self.noise[t], self.actions[t], self.logprobs[t], None, value.view(-1),
                 self.values[t], philox=px))
@@ -678,6 +689,9 @@ class PPOTrainer:
         if self.frame_cache:
             self.values[T].copy_(self.agent._head(self.agent.critic,
                                                   self._policy_hidden(T)).view(-1))
+        elif self.u8_rollout:
+            self.values[T].copy_(self.agent._head(
+                self.agent.critic, self.agent.trunk_frames(self.obs[T], self.env_rows)).view(-1))
         else:
             self.values[T].copy_(self.agent.get_value(self.net_obs, self.prescale).view(-1))
         rec = self.records

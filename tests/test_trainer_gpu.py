@@ -798,3 +798,30 @@ def test_lagged_metrics_are_the_synced_ones(dev):
         assert a.keys() == b.keys()
         for k in a:
             assert a[k] == b[k] or (a[k] != a[k] and b[k] != b[k]), (k, a[k], b[k])
+
+
+def test_pixel_rollout_reads_the_u8_stacks(dev):
+    """Config-3-like pixel rollout: the first convolution from the rollout buffer's u8 slot
+    (trainer.U8_ROLLOUT_CONV) against the f32 network copy path — same actions and values up to
+    the f32 rounding of NormalizeImg's quotient (the u8 path divides the products instead)."""
+    from oc_cleanrl_amd import trainer as trm
+    from oc_cleanrl_amd.args import Args, finalize
+
+    def run(flag):
+        trm.U8_ROLLOUT_CONV = flag
+        try:
+            args = finalize(Args(env_id="ALE/Breakout-v5", obs_mode="dqn", architecture="PPO",
+                                 num_envs=256, num_steps=8, update_epochs=1, seed=5,
+                                 save_model=False, cuda_graphs=False), 1)
+            tr = trm.PPOTrainer(args, dev)
+            assert tr.u8_rollout == flag
+            tr._rollout()
+            torch.cuda.synchronize()
+            return tr.actions.clone(), tr.values.clone()
+        finally:
+            trm.U8_ROLLOUT_CONV = True
+
+    a1, v1 = run(True)
+    a0, v0 = run(False)
+    assert float((v1 - v0).abs().max()) <= 1e-4 * float(v0.abs().max() + 1)
+    assert float((a1 == a0).float().mean()) >= 0.99
