@@ -455,6 +455,8 @@ class PPOTrainer:
         self.u8_rollout = (U8_ROLLOUT_CONV and self.u8_first_conv and not self.frame_cache and
                            self.agent.trunk_frames_ok(self.obs[0], self.N))
         self.env_rows = torch.arange(self.N, dtype=torch.int64, device=dev)
+        # the store's f32 network copy of the stacks: nothing reads it on the u8 rollout path
+        self._store_net = None if self.u8_rollout else self.net_obs
         self.wplanes, self.wplanes_built = None, False  # built at the first minibatch
         self.planes_by_opt = False
         # GAE's per-sample records for the minibatch gather (ops.sample_records)
@@ -567,10 +569,10 @@ class PPOTrainer:
         frame = self.env.frame if self.host_env else self.env.reset()
         if self.reset_stacks:  # the env's own initial stack (envs.HostVecEnv.reset)
             ones = torch.ones(self.N, dtype=torch.float32, device=self.dev)
-            ops.rollout_store(frame, ones, ones, self.obs[0], self.obs[self.T], self.net_obs,
+            ops.rollout_store(frame, ones, ones, self.obs[0], self.obs[self.T], self._store_net,
                               scale255=self.prescale, reset_prev=self.env.reset_prev)
         else:
-            ops.obs_reset(frame, self.obs[self.T], self.net_obs, scale255=self.prescale)
+            ops.obs_reset(frame, self.obs[self.T], self._store_net, scale255=self.prescale)
         self.dones[self.T].zero_()
 
     def _policy_hidden(self, t: int):
@@ -664,12 +666,12 @@ class PPOTrainer:
         if a.vecnorm_reward:
             self.timer.bracket("rollout_store", lambda: ops.rollout_store_vecnorm(
                 self.env.frame, self.env.reward, self.env.done, self.obs[t], self.obs[t + 1],
-                self.net_obs, self.dones[t + 1], self.ret_state, self.rms_state, self.rewards[t],
+                self._store_net, self.dones[t + 1], self.ret_state, self.rms_state, self.rewards[t],
                 scale255=self.prescale, reset_prev=rp))
         else:
             self.timer.bracket("rollout_store", lambda: ops.rollout_store(
                 self.env.frame, self.env.reward, self.env.done, self.obs[t], self.obs[t + 1],
-                self.net_obs, self.rewards[t], self.dones[t + 1], scale255=self.prescale,
+                self._store_net, self.rewards[t], self.dones[t + 1], scale255=self.prescale,
                 reset_prev=rp))
 
     def _rollout_begin(self):
