@@ -141,7 +141,7 @@ struct X6Args {
   const uint8_t* u8;
   const int64_t* u8_idx;
   int64_t u8_img, u8_hw, u8_w;
-  int u8_khw, u8_kw;
+  int u8_khw, u8_kw, u8_nimg;  // u8_nimg: entries of u8_idx (images)
   float cdiv;
 };
 
@@ -536,7 +536,9 @@ struct X6Stage {
             cp[i][j] -= qhw;
             ++cb[i][j];
           }
-          cbase[i][j] = g.u8_idx[cb[i][j]] * g.u8_img;
+          // past the last image after the unit's last step: nothing reads it, and the index
+          // array ends there (no read one past its end)
+          cbase[i][j] = cb[i][j] < g.u8_nimg ? g.u8_idx[cb[i][j]] * g.u8_img : 0;
         }
       }
     }
@@ -2227,6 +2229,7 @@ extern "C" int ocppo_conv_x6_u8(ocppo_stream_t stream, int mode, const uint8_t* 
   g.u8_w = W;
   g.u8_khw = (int)(KH * KW);
   g.u8_kw = (int)KW;
+  g.u8_nimg = (int)(rows / (OH * OW));
   g.cdiv = divisor;
   if (mode == 0) {  // y = act(sum_k u(r, k) w[n, k] / divisor + bias)
     g.sak = 1;
