@@ -62,11 +62,15 @@ def test_pixel_update_graph_replay_matches_eager(dev):
         torch.testing.assert_close(p, q, rtol=1e-4, atol=1e-5)
 
 
-def test_pixel_channels_last_matches_nchw(dev):
+def test_pixel_channels_last_matches_nchw(dev, monkeypatch):
     """The NHWC NatureCNN path (channels_last agent, NHWC store/gather) computes the same network
     as the plain NCHW one: same initial weights and network input, same logits up to the conv
-    kernels' summation order; both train."""
+    kernels' summation order; both train. (The store's f32 network copy is what this compares:
+    the u8 rollout path, which skips it, is test_pixel_rollout_reads_the_u8_stacks.)"""
+    from oc_cleanrl_amd import trainer as trm
     from oc_cleanrl_amd.trainer import PPOTrainer
+
+    monkeypatch.setattr(trm, "U8_ROLLOUT_CONV", False)
 
     trs = []
     for cl in (False, True):
