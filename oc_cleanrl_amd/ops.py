@@ -746,6 +746,16 @@ def conv_x6_ok(x, weight, stride: int, wgrad: bool = False, dgrad: bool = False)
 
 
 _CONV_PARTS: dict = {}
+# weight gradients: K splits for about this many workgroups (each split's partial [Cout, N] summed
+# in split order by the same launch's sum_parts), per tile; measured at config 3's minibatch of
+# 8192 (profiles/r05/ab_conv_wgrad_units.txt): 32 x 128 (the first layer) and 64 x 128 best at
+# 1024, 64 x 64 at 4096. None: the per-tile table; an int: one target for every tile
+CONV_WGRAD_UNITS = None
+_WGRAD_UNITS = {1: 1024, 4: 1024, 3: 4096}
+
+
+def _wgrad_units(tile: int) -> int:
+    return CONV_WGRAD_UNITS if CONV_WGRAD_UNITS else _WGRAD_UNITS.get(tile, 2048)
 
 
 def _geom(*v):
@@ -829,7 +839,7 @@ def conv_x6_wgrad(gp, x, kernel: tuple, stride: int, out=None):
         raise ValueError(f"conv_x6_wgrad: no tile for [{Cout} x {N}] over {rows} rows")
     bm, bn = _CONV_TILES[tile]
     tiles = (Cout // bm) * (N // bn)
-    S = max(1, min(rows // 32 // 32, 2048 // tiles))
+    S = max(1, min(rows // 32 // 32, _wgrad_units(tile) // tiles))
     key = ("wgrad", str(dev), S, Cout, N)
     if key not in _CONV_PARTS:
         _CONV_PARTS[key] = torch.empty((S, Cout, N), dtype=f, device=dev)
@@ -983,7 +993,7 @@ def conv_x6_u8_wgrad(gp, src, idx, kernel: tuple, stride: int = 4, divisor: floa
     if rows != B * OH * OW or tile is None or rows % 32:
         raise ValueError("conv_x6_u8_wgrad: gp must be [B OH OW, Cout] with a tile for it")
     bm, bn = _CONV_TILES[tile]
-    S = max(1, min(rows // 32 // 32, 2048 // ((Cout // bm) * (N // bn))))
+    S = max(1, min(rows // 32 // 32, _wgrad_units(tile) // ((Cout // bm) * (N // bn))))
     key = ("wgrad", str(dev), S, Cout, N)
     if key not in _CONV_PARTS:
         _CONV_PARTS[key] = torch.empty((S, Cout, N), dtype=f, device=dev)
