@@ -694,14 +694,18 @@ _CONV_TILES = {0: (128, 32), 1: (32, 128), 2: (128, 64), 3: (64, 64), 4: (64, 12
                6: (32, 64)}
 
 
+CONV_FWD_MIN_UNITS = 512
+
+
 def _conv_fwd_tile(M: int, N: int) -> int | None:
-    """The largest tile giving >= 512 workgroups (two per CU), else the one giving the most."""
+    """The largest tile giving >= CONV_FWD_MIN_UNITS workgroups (two per CU), else the one giving
+    the most."""
     best, units = None, 0
     for t in ((0,) if N == 32 else (2, 3, 6) if N == 64 else (5, 2, 3, 6)):
         bm, bn = _CONV_TILES[t]
         if M % bm == 0 and N % bn == 0:
             u = (M // bm) * (N // bn)
-            if u >= 512:
+            if u >= CONV_FWD_MIN_UNITS:
                 return t
             if u > units:
                 best, units = t, u
