@@ -268,6 +268,7 @@ def launch(argv, gpus: int, script=None, deadline_s: float | None = None) -> int
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     status = tempfile.mkdtemp(prefix="ocppo_watch_")
     env["OCPPO_WATCH_DIR"] = status
+    env["OCPPO_RUN_ID"] = os.path.basename(status)  # the ranks' run token (watch.run_token)
     t0 = time.monotonic()
     p = subprocess.Popen(launcher_cmd(argv, gpus, free_port(), script), env=env,
                          stdout=subprocess.PIPE, text=True, bufsize=1, start_new_session=True)

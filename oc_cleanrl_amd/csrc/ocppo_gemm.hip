@@ -143,7 +143,37 @@ struct X6Args {
   int64_t u8_img, u8_hw, u8_w;
   int u8_khw, u8_kw, u8_nimg;  // u8_nimg: entries of u8_idx (images)
   float cdiv;
+  // bounds-check builds only (-DOCPPO_X6_BOUNDS, ocppo_x6_probe_set_bounds): the extents of the
+  // convolution gathers' sources from the pointers passed (elements of the f32 operand the
+  // gathers read, bytes and rows of the u8 stacks), and a violation record [count, first kind,
+  // first index lo, hi, first limit lo, hi]
+  uint32_t* bnd;
+  int64_t bnd_x, bnd_u8, bnd_u8rows;
 };
+
+// Bounds-check builds: every index a convolution gather computes (image index, u8 stack row,
+// element / byte offset of a load) is checked against its extent before the load; a violation
+// is counted and recorded (the first one) and the load reads offset 0 instead, so a bad index
+// shows as a record, not as a fault. Compiled out otherwise (the identity).
+enum X6BoundKind { kBndX = 1, kBndImg = 2, kBndU8Row = 3, kBndU8 = 4 };
+__device__ __forceinline__ int64_t x6_bnd(const X6Args& g, int kind, int64_t v, int64_t need,
+                                          int64_t lim) {
+#ifdef OCPPO_X6_BOUNDS
+  if (g.bnd != nullptr && (v < 0 || v + need > lim)) {
+    if (__hip_atomic_fetch_add(g.bnd, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+      g.bnd[1] = static_cast<uint32_t>(kind);
+      g.bnd[2] = static_cast<uint32_t>(static_cast<uint64_t>(v));
+      g.bnd[3] = static_cast<uint32_t>(static_cast<uint64_t>(v) >> 32);
+      g.bnd[4] = static_cast<uint32_t>(static_cast<uint64_t>(lim));
+      g.bnd[5] = static_cast<uint32_t>(static_cast<uint64_t>(lim) >> 32);
+    }
+    return 0;
+  }
+#else
+  (void)g, (void)kind, (void)need, (void)lim;
+#endif
+  return v;
+}
 
 // q = x / d for 0 <= x < 2^24, d >= 1 (f32 reciprocal estimate, corrected to the exact quotient)
 __device__ __forceinline__ int x6_udiv(int x, int d) {
@@ -348,7 +378,8 @@ struct X6Stage {
     }
   }
   __device__ static void load_rows(const float* __restrict__ src, const int64_t (&roff)[kPer][4],
-                                   int k0, int t, floatx4 (&r)[kPer][4]) {
+                                   int k0, int t, floatx4 (&r)[kPer][4],
+                                   const X6Args* bg = nullptr) {
     static_assert(KC, "row-gathered loads are for a k-contiguous operand");
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
@@ -357,8 +388,11 @@ struct X6Stage {
       int rq, kq;
       piece_of(p, rq, kq);
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        r[i][j] = *reinterpret_cast<const floatx4*>(src + roff[i][j] + (k0 + 4 * kq));
+      for (int j = 0; j < 4; ++j) {
+        int64_t off = roff[i][j] + (k0 + 4 * kq);
+        if (bg != nullptr) off = x6_bnd(*bg, kBndX, off, 4, bg->bnd_x);  // GATH 3 (bounds builds)
+        r[i][j] = *reinterpret_cast<const floatx4*>(src + off);
+      }
     }
   }
   // convolution rows of a k-contiguous operand (GATH 3): roff[i][j] = cv_row of piece row (i, j);
@@ -409,7 +443,8 @@ struct X6Stage {
       for (int j = 0; j < 4; ++j) {
         const int iy = qy[i][j] + ty - g.cv_ph, ix = qx[i][j] + tx - g.cv_pw;
         const bool in = iy >= 0 && iy < g.cv_ih && ix >= 0 && ix < g.cv_iw;
-        r[i][j] = in ? *reinterpret_cast<const floatx4*>(src + roff[i][j] + so + 4 * kq)
+        r[i][j] = in ? *reinterpret_cast<const floatx4*>(
+                           src + x6_bnd(g, kBndX, roff[i][j] + so + 4 * kq, 4, g.bnd_x))
                      : floatx4{0.f, 0.f, 0.f, 0.f};
       }
     }
@@ -457,7 +492,8 @@ struct X6Stage {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int64_t off = cb[i][j] * g.cv_sb + ptab[cp[i][j]];
-        r[i][j] = *reinterpret_cast<const floatx4*>(src + off + nseg[i]);
+        x6_bnd(g, kBndImg, cb[i][j], 1, g.K / (g.cv_qh * g.cv_qw));  // GATH 4: K rows = images
+        r[i][j] = *reinterpret_cast<const floatx4*>(src + x6_bnd(g, kBndX, off + nseg[i], 4, g.bnd_x));
         cp[i][j] += kX6BK;  // the next step's row
         while (cp[i][j] >= qhw) {
           cp[i][j] -= qhw;
@@ -480,7 +516,9 @@ struct X6Stage {
       for (int j = 0; j < 4; ++j) {
         const int r = row0 + 4 * rq + j, b = x6_udiv(r, qhw), pix = r - b * qhw;
         const int qy = x6_udiv(pix, g.cv_qw);
-        roff[i][j] = g.u8_idx[b] * g.u8_img + qy * g.cv_ys + (pix - qy * g.cv_qw) * g.cv_xs;
+        const int64_t img = g.u8_idx[x6_bnd(g, kBndImg, b, 1, g.u8_nimg)];
+        roff[i][j] = x6_bnd(g, kBndU8Row, img, 1, g.bnd_u8rows) * g.u8_img + qy * g.cv_ys +
+                     (pix - qy * g.cv_qw) * g.cv_xs;
       }
     }
   }
@@ -490,7 +528,7 @@ struct X6Stage {
   }
   __device__ static void load_u8_rows(const uint8_t* __restrict__ src,
                                       const int64_t (&roff)[kPer][4], const int32_t* segtab,
-                                      int k0, int t, floatx4 (&r)[kPer][4]) {
+                                      int k0, int t, floatx4 (&r)[kPer][4], const X6Args& g) {
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
       const int p = t + NT * i;
@@ -500,7 +538,8 @@ struct X6Stage {
       const int so = segtab[(k0 >> 2) + kq];
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        r[i][j] = u8x4(*reinterpret_cast<const uint32_t*>(src + roff[i][j] + so));
+        r[i][j] = u8x4(*reinterpret_cast<const uint32_t*>(
+            src + x6_bnd(g, kBndU8, roff[i][j] + so, 4, g.bnd_u8)));
     }
   }
   // u8 frame stacks as a row-contiguous operand whose K index is a convolution row (GATH 6):
@@ -528,8 +567,9 @@ struct X6Stage {
       if (kPieces % NT != 0 && p >= kPieces) continue;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        r[i][j] = u8x4(*reinterpret_cast<const uint32_t*>(src + cbase[i][j] + ptab[cp[i][j]] +
-                                                          nseg[i]));
+        x6_bnd(g, kBndImg, cb[i][j], 1, g.u8_nimg);
+        r[i][j] = u8x4(*reinterpret_cast<const uint32_t*>(
+            src + x6_bnd(g, kBndU8, cbase[i][j] + ptab[cp[i][j]] + nseg[i], 4, g.bnd_u8)));
         cp[i][j] += kX6BK;
         if (cp[i][j] >= qhw) {
           while (cp[i][j] >= qhw) {
@@ -538,7 +578,9 @@ struct X6Stage {
           }
           // past the last image after the unit's last step: nothing reads it, and the index
           // array ends there (no read one past its end)
-          cbase[i][j] = cb[i][j] < g.u8_nimg ? g.u8_idx[cb[i][j]] * g.u8_img : 0;
+          cbase[i][j] = cb[i][j] < g.u8_nimg
+                            ? x6_bnd(g, kBndU8Row, g.u8_idx[cb[i][j]], 1, g.bnd_u8rows) * g.u8_img
+                            : 0;
         }
       }
     }
@@ -798,7 +840,10 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
 #pragma unroll
       for (int i = 0; i < SB::kPer; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) cbaseB[i][j] = g.u8_idx[cbB[i][j]] * g.u8_img;
+        for (int j = 0; j < 4; ++j)
+          cbaseB[i][j] = x6_bnd(g, kBndU8Row,
+                                g.u8_idx[x6_bnd(g, kBndImg, cbB[i][j], 1, g.u8_nimg)], 1,
+                                g.bnd_u8rows) * g.u8_img;
     }
     for (int p = t; p < g.cv_qh * g.cv_qw; p += NT) {
       const int qy = p / g.cv_qw;
@@ -828,8 +873,8 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
   }
   auto loadA = [&](int k0, floatx4 (&r)[SA::kPer][4]) {
     if constexpr (GATH == 1) SA::load_rows(A, roffA, k0, t, r);
-    else if constexpr (GATH == 3) SA::load_rows(A, roffA, static_cast<int>(x6_cv_seg(g, k0)), t, r);
-    else if constexpr (GATH == 5) SA::load_u8_rows(g.u8, roffA, gtbl, k0, t, r);
+    else if constexpr (GATH == 3) SA::load_rows(A, roffA, static_cast<int>(x6_cv_seg(g, k0)), t, r, &g);
+    else if constexpr (GATH == 5) SA::load_u8_rows(g.u8, roffA, gtbl, k0, t, r, g);
     else if constexpr (GATH == 7) SA::load_rows_bounded(A, g, roffA, qyA, qxA, k0, t, r);
     else if constexpr (kBuf)
       SA::load_buf(bufA, t, static_cast<int32_t>(4 * (AKC ? (k0 - kb * kX6BK)
@@ -1708,6 +1753,30 @@ extern "C" int ocppo_split_planes(ocppo_stream_t stream, int n, const float* con
   return check_launch("ocppo_split_planes");
 }
 
+#ifdef OCPPO_X6_BOUNDS
+static uint32_t* g_x6_bnd = nullptr;
+static int64_t g_x6_bnd_x = 0, g_x6_bnd_u8 = 0, g_x6_bnd_u8rows = 0;
+// bounds-check builds only: the violation record (>= 6 uint32, device) and the extents of the
+// next convolution launch's gathered sources, from the pointers it is passed (x elements; u8
+// bytes and stack rows)
+extern "C" __attribute__((visibility("default"))) int ocppo_x6_probe_set_bounds(
+    uint32_t* rec, int64_t x_elems, int64_t u8_bytes, int64_t u8_rows) {
+  g_x6_bnd = rec;
+  g_x6_bnd_x = x_elems;
+  g_x6_bnd_u8 = u8_bytes;
+  g_x6_bnd_u8rows = u8_rows;
+  return OCPPO_OK;
+}
+static void x6_bounds_args(X6Args& g) {
+  g.bnd = g_x6_bnd;
+  g.bnd_x = g_x6_bnd_x;
+  g.bnd_u8 = g_x6_bnd_u8;
+  g.bnd_u8rows = g_x6_bnd_u8rows;
+}
+#else
+static void x6_bounds_args(X6Args&) {}
+#endif
+
 #ifdef OCPPO_X6_STAMPS
 static int64_t* g_x6_stamps = nullptr;
 // probe builds only: the stamps buffer (>= 8 int64 per workgroup) of the following launches
@@ -2151,6 +2220,7 @@ extern "C" int ocppo_conv_x6(ocppo_stream_t stream, int mode, const float* x, co
     g.ldc = N;
     g.split_c = M * N;
   }
+  x6_bounds_args(g);
   int lmode = mode;
   if (pad) {
     // x is the UNPADDED gradient [B, ih, iw, C]; geom's strides describe the padded one it stands
@@ -2231,6 +2301,7 @@ extern "C" int ocppo_conv_x6_u8(ocppo_stream_t stream, int mode, const uint8_t* 
   g.u8_kw = (int)KW;
   g.u8_nimg = (int)(rows / (OH * OW));
   g.cdiv = divisor;
+  x6_bounds_args(g);
   if (mode == 0) {  // y = act(sum_k u(r, k) w[n, k] / divisor + bias)
     g.sak = 1;
     g.b = w;

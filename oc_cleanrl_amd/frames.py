@@ -370,6 +370,20 @@ def _gather_l1_ok(agent, obs, split: int) -> bool:
             and l1.weight.is_contiguous())
 
 
+def _cut(low):
+    """The leaf the layers above a DP cut read instead of `low`. It carries `low`'s box (the
+    Linear+ReLU that produced it), so the first layer above the cut still takes that ReLU's
+    backward and bias-gradient partials into its dX epilogue (agents._LinearAct, ops.dx_x6_relu):
+    the same products in the same order as the uncut chain, the partials handed across the cut in
+    the box. Without it the lower phase re-derives them with relu_bias_grad's row chunks, a
+    different summation order of that layer's bias gradient (VERDICT r05 Weak 1)."""
+    low_d = low.detach().requires_grad_()
+    box = getattr(low, "_ocppo_box", None)
+    if box is not None:
+        low_d._ocppo_box = box
+    return low_d
+
+
 def minibatch_hidden(agent, obs, dones, uniq, pos_of, inv, perm, mb: int, split: int = 0):
     """Decoder output of PPObj for the samples `perm` (one minibatch) from the rollout obs
     [T+1, N, W, F] with each distinct frame encoded once; autograd flows to every parameter.
@@ -402,7 +416,7 @@ def minibatch_hidden(agent, obs, dones, uniq, pos_of, inv, perm, mb: int, split:
             h1._ocppo_wslot = slot
         if split:
             low = fused_trunk(agent.network[2:split], h1)
-            low_d = low.detach().requires_grad_()
+            low_d = _cut(low)
             enc = fused_trunk(agent.network[split:agent._flat], low_d, rows_last=SCATTER_MBITS)
             cut = (low, low_d)
         else:
@@ -418,7 +432,7 @@ def minibatch_hidden(agent, obs, dones, uniq, pos_of, inv, perm, mb: int, split:
     x = ops.timed("frames_gather", lambda: ops.frames_gather(obs, uniq))
     if split:
         low = fused_trunk(agent.network[:split], x)
-        low_d = low.detach().requires_grad_()
+        low_d = _cut(low)
         enc = fused_trunk(agent.network[split:agent._flat], low_d)
         cut = (low, low_d)
     else:

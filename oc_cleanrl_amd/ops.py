@@ -766,6 +766,38 @@ def _geom(*v):
     return (ctypes.c_int64 * len(v))(*[int(t) for t in v])
 
 
+# Bounds-check builds of the library (`python tools/build_variant.py OUT.so -DOCPPO_X6_BOUNDS`,
+# loaded with OCPPO_LIB=OUT.so; never the product): before every convolution launch the library
+# is handed the extents of the sources its gathers read, from the pointers it is passed, and a
+# device record of the first out-of-range index (tests/test_conv_bounds_gpu.py reads it).
+X6_BOUNDS = hasattr(_lib.LIB, "ocppo_x6_probe_set_bounds")
+_BOUNDS_REC: dict = {}
+BOUND_KINDS = {1: "f32 source offset", 2: "image index", 3: "u8 stack row", 4: "u8 byte offset"}
+
+
+def _tail(t) -> int:
+    """Elements of t's storage from t's first element on."""
+    return t.untyped_storage().nbytes() // t.element_size() - t.storage_offset()
+
+
+def bounds_record(dev) -> torch.Tensor:
+    """The bounds-check build's violation record on `dev` (int32 [count, first kind, first index
+    lo, hi, its limit lo, hi, 0, 0])."""
+    key = str(dev)
+    if key not in _BOUNDS_REC:
+        _BOUNDS_REC[key] = torch.zeros(8, dtype=torch.int32, device=dev)
+    return _BOUNDS_REC[key]
+
+
+def _bounds(dev, x=None, u8=None):
+    if X6_BOUNDS:
+        _lib.LIB.ocppo_x6_probe_set_bounds.argtypes = [ctypes.c_void_p, ctypes.c_int64,
+                                                       ctypes.c_int64, ctypes.c_int64]
+        _lib.LIB.ocppo_x6_probe_set_bounds(
+            bounds_record(dev).data_ptr(), _tail(x) if x is not None else 0,
+            _tail(u8) if u8 is not None else 0, u8.shape[0] if u8 is not None else 0)
+
+
 def conv_x6(x, weight, bias=None, stride: int = 1, relu: bool = True, out=None):
     """act(conv2d(x, weight) + bias) (architectures/ppo.py:20-31's Conv2d + ReLU) on ocppo_conv_x6:
     channels_last f32 x [B, C, H, W], weight [Cout, C, KH, KW] -> channels_last [B, Cout, OH, OW]
@@ -789,6 +821,7 @@ def conv_x6(x, weight, bias=None, stride: int = 1, relu: bool = True, out=None):
     bm, bn = _CONV_TILES[tile]
     S = _conv_fwd_splits((M // bm) * (Cout // bn), K // 32)
     geom = _geom(OH, OW, H * W * C, s * W * C, s * C, W * C, KW * C)
+    _bounds(dev, x)
     if S == 1:
         call("ocppo_conv_x6", _stream(dev), 0, x.data_ptr(), geom, wm.data_ptr(), K,
              out.data_ptr(), Cout, M, Cout, K, 1, _opt(bias, "bias", f, dev, Cout),
@@ -853,6 +886,7 @@ def conv_x6_wgrad(gp, x, kernel: tuple, stride: int, out=None):
     if out.numel() != Cout * N or not out.is_contiguous(memory_format=torch.channels_last
                                                         if out.dim() == 4 else torch.contiguous_format):
         raise ValueError("conv_x6_wgrad: out must hold [Cout, KH KW C] contiguously")
+    _bounds(dev, x)
     call("ocppo_conv_x6", _stream(dev), 1, x.data_ptr(),
          _geom(OH, OW, H * W * C, s * W * C, s * C, W * C, KW * C),
          _check(gp, "gp", f, dev), Cout, part.data_ptr(), N, Cout, N, rows, S, None, 0, None, tile,
@@ -900,6 +934,7 @@ def conv_x6_dgrad(gp, weight, stride: int, in_hw: tuple, out=None, relu_out=None
         gpad = torch.nn.functional.pad(g, (0, 0, TW - 1, TW - 1, T - 1, T - 1))
         if relu_out is not None:
             raise ValueError("conv_x6_dgrad: the ReLU epilogue needs the bounded loader")
+        _bounds(dev, gpad)
         call("ocppo_conv_x6", _stream(dev), 0, gpad.data_ptr(),
              _geom(QH, QW, Hp * Wp * Cout, Wp * Cout, Cout, Wp * Cout, TW * Cout), wc.data_ptr(),
              K, out.data_ptr(), C, M, N, K, 1, None, 0, og, tile, None, None, None, None)
@@ -912,6 +947,7 @@ def conv_x6_dgrad(gp, weight, stride: int, in_hw: tuple, out=None, relu_out=None
             raise ValueError("conv_x6_dgrad: relu_out must be channels_last [B, C, H, W], with db")
         mask = relu_out
         dbp = torch.empty((M // _CONV_TILES[tile][0], N), dtype=f, device=dev)
+    _bounds(dev, g)
     call("ocppo_conv_x6", _stream(dev), 0, g.data_ptr(),
          _geom(QH, QW, 0, 0, 0, 0, TW * Cout), wc.data_ptr(), K, out.data_ptr(), C, M, N, K, 1,
          None, 0, og, tile, None, _geom(T - 1, TW - 1, OH, OW, Cout),
@@ -974,6 +1010,7 @@ def conv_x6_u8(src, idx, weight, bias=None, stride: int = 4, relu: bool = True,
         out = torch.empty((B, Cout, OH, OW), dtype=f, device=dev, memory_format=torch.channels_last)
     if tuple(out.shape) != (B, Cout, OH, OW) or not out.is_contiguous(memory_format=torch.channels_last):
         raise ValueError("conv_x6_u8: out must be a channels_last [B, Cout, OH, OW] tensor")
+    _bounds(dev, u8=src)
     call("ocppo_conv_x6_u8", _stream(dev), 0, src.data_ptr(), _check(idx, "idx", torch.int64, dev, B),
          C, H, W, KH, KW, s, wn.data_ptr(), K, out.data_ptr(), M, Cout, K, 1,
          _opt(bias, "bias", f, dev, Cout), int(bool(relu)), float(divisor),
@@ -1004,6 +1041,7 @@ def conv_x6_u8_wgrad(gp, src, idx, kernel: tuple, stride: int = 4, divisor: floa
     part = _CONV_PARTS[key]
     if out is None:
         out = torch.empty((Cout, N), dtype=f, device=dev)
+    _bounds(dev, u8=src)
     call("ocppo_conv_x6_u8", _stream(dev), 1, src.data_ptr(), _check(idx, "idx", torch.int64, dev, B),
          C, H, W, KH, KW, s, _check(gp, "gp", f, dev), Cout, part.data_ptr(), Cout, N, rows, S,
          None, 0, float(divisor), tile, _check(out, "out", f, dev, Cout * N))

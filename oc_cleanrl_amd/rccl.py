@@ -67,24 +67,37 @@ def _check(rc: int, what: str):
                            f"({msg.decode() if msg else 'unknown'})")
 
 
+def unique_id() -> bytes:
+    """The library loaded and a fresh ncclUniqueId (rank 0's part of the bootstrap), as its raw
+    128 bytes (a c_char array would stop at the first NUL). Local: no collective."""
+    lib = _lib()
+    uid = _UniqueId()
+    _check(lib.ncclGetUniqueId(ctypes.byref(uid)), "ncclGetUniqueId")
+    return ctypes.string_at(ctypes.addressof(uid), UNIQUE_ID_BYTES)
+
+
 class RcclComm:
     """One RCCL communicator over the ranks of the default process group, on this process's
-    current HIP device (torch.cuda.set_device before constructing)."""
+    current HIP device (torch.cuda.set_device before constructing). uid: rank 0's unique_id(),
+    or None to draw it here; it is broadcast through the process group either way.
 
-    def __init__(self, rank: int, world: int, group=None):
+    ncclCommInitRank is itself collective: a rank whose init fails raises, while its peers stay
+    inside theirs. Nothing after that point can be agreed on through the group, so the failures
+    that can be agreed on (the library, the unique id) are checked before it (trainer._rccl_comm)
+    and a failing init is bounded by the rank watchdog (oc_cleanrl_amd.watch)."""
+
+    def __init__(self, rank: int, world: int, group=None, uid: bytes | None = None):
         lib = _lib()
-        uid = _UniqueId()
-        if rank == 0:
-            _check(lib.ncclGetUniqueId(ctypes.byref(uid)), "ncclGetUniqueId")
-        # the raw 128 bytes (uid.internal, a c_char array, would stop at the first NUL)
-        box = [ctypes.string_at(ctypes.addressof(uid), UNIQUE_ID_BYTES) if rank == 0 else None]
+        if rank == 0 and uid is None:
+            uid = unique_id()
+        box = [uid if rank == 0 else None]
         dist.broadcast_object_list(box, src=0, group=group)
-        if len(box[0]) != UNIQUE_ID_BYTES:
-            raise RuntimeError(f"RCCL unique id of {len(box[0])} bytes")
-        uid = _UniqueId()
-        ctypes.memmove(ctypes.addressof(uid), box[0], UNIQUE_ID_BYTES)
+        if box[0] is None or len(box[0]) != UNIQUE_ID_BYTES:
+            raise RuntimeError(f"RCCL unique id of {len(box[0] or b'')} bytes")
+        raw = _UniqueId()
+        ctypes.memmove(ctypes.addressof(raw), box[0], UNIQUE_ID_BYTES)
         comm = ctypes.c_void_p()
-        _check(lib.ncclCommInitRank(ctypes.byref(comm), world, uid, rank), "ncclCommInitRank")
+        _check(lib.ncclCommInitRank(ctypes.byref(comm), world, raw, rank), "ncclCommInitRank")
         self.comm, self.rank, self.world = comm, rank, world
 
     def all_reduce_sum(self, t: torch.Tensor, stream=None):

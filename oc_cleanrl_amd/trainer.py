@@ -32,7 +32,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
-from . import agents, frames, gemm_table, ops
+from . import agents, frames, gemm_table, ops, rccl
 from .rccl import RcclComm, RcclExchange
 from .agents import NormalizeImg, PPObj, fused_trunk, linear_relu, make_agent
 from .args import Args
@@ -256,9 +256,13 @@ def _graph_capture(graph, pool=None, quiesce: bool = False):
 
 class PPOTrainer:
     def __init__(self, args: Args, device, rank: int = 0, world_size: int = 1,
-                 kernel_timing: bool = False, log: bool = True, envs=None):
+                 kernel_timing: bool = False, log: bool = True, envs=None, comm=None):
         """envs: optional host (CPU) gymnasium-style vector env of this rank's local_num_envs
-        (envs.HostVecEnv documents the contract); None = the device-resident synthetic env."""
+        (envs.HostVecEnv documents the contract); None = the device-resident synthetic env.
+        comm: the DP exchange's communicator in place of the package's own RCCL one -- any object
+        with rccl.RcclComm's all_reduce_sum(t, stream) (tests drive rccl.RcclExchange's whole /
+        split logic over several ranks with a gloo-backed stand-in; its collectives are not
+        capturable, so such a trainer runs with cuda_graphs off)."""
         self.args = args
         self.dev = torch.device(device)
         self.rank, self.world = rank, world_size
@@ -271,7 +275,12 @@ class PPOTrainer:
         # tail's all-reduce while the lower encoder layers run their backward
         self.comm = self.side = None
         self.dp_form = None  # the exchange actually in use (bench.py reports it)
-        if (self.dp and args.dp_collectives == "rccl" and torch.device(device).type == "cuda"
+        if self.dp and comm is not None:
+            if args.cuda_graphs:
+                raise ValueError("an injected DP communicator runs with cuda_graphs off")
+            self.comm, self.dp_form = comm, f"rccl.RcclExchange over {type(comm).__name__}"
+            self.side = torch.cuda.Stream(device)
+        elif (self.dp and args.dp_collectives == "rccl" and torch.device(device).type == "cuda"
                 and dist.get_backend() == "nccl"):
             torch.cuda.set_device(device)
             self.comm, self.dp_form = self._rccl_comm(rank, dist.get_world_size(), device)
@@ -406,7 +415,9 @@ class PPOTrainer:
         self.staged = False
         self.staged_rng_state = self.current_rng_state = None
         self.executed_mb = self.E * self.nmb  # minibatches the last update ran (target_kl)
-        self._pending_metrics, self._metrics_host = None, None  # train_iteration(lag=True)
+        # train_iteration(lag=True): the pending record and two pinned host vectors used in turn
+        # (a new copy never lands in the vector the pending record still has to be read from)
+        self._pending_metrics, self._metrics_host, self._metrics_turn = None, [None, None], 0
         self.perm_event = torch.cuda.Event()
         self.perm_event.record()
         # PPObj update with every distinct frame of a minibatch encoded once (frames.py)
@@ -1090,9 +1101,12 @@ class PPOTrainer:
         n = self.executed_mb
         vec = torch.cat([var_y.view(1), ev.view(1), self.lr.double().view(1), ep,
                          self.stats[:n].double().reshape(-1)])
-        if self._metrics_host is None or self._metrics_host.numel() < vec.numel():
-            self._metrics_host = torch.empty(vec.numel(), dtype=torch.float64, pin_memory=True)
-        host = self._metrics_host[:vec.numel()]
+        # the other vector than the one the still-pending record (the previous iteration's) reads
+        k = self._metrics_turn
+        self._metrics_turn ^= 1
+        if self._metrics_host[k] is None or self._metrics_host[k].numel() < vec.numel():
+            self._metrics_host[k] = torch.empty(vec.numel(), dtype=torch.float64, pin_memory=True)
+        host = self._metrics_host[k][:vec.numel()]
         host.copy_(vec, non_blocking=True)
         done = torch.cuda.Event()
         done.record()
@@ -1163,26 +1177,41 @@ class PPOTrainer:
 
     @staticmethod
     def _rccl_comm(rank: int, world: int, device):
-        """The package's RCCL communicator, checked with one eager all-reduce before anything is
-        captured around it (every rank takes part; a rank whose check fails aborts its
-        communicator and the ranks agree, through the process group, to use torch's collectives
-        instead: (comm or None, the form in use))."""
-        comm, why = None, ""
+        """The package's RCCL communicator: (comm or None, the form in use). Two agreements
+        through the process group, each an all-reduce every rank reaches: (1) before the
+        collective init, that every rank loaded the library and rank 0 drew the unique id -- a
+        refusal there falls back to torch's collectives on every rank; (2) after the init, one
+        eager all-reduce on the communicator checked for the right sum. A rank whose
+        ncclCommInitRank itself fails cannot take part in (2) (its peers wait inside their init):
+        that case is bounded by the rank watchdog (watch.RankWatch, bench.py's stall limits), not
+        recovered."""
+        def agree(why):
+            ok = torch.tensor([0 if why else 1], dtype=torch.int32, device=device)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            return int(ok.item()) == 1
+
+        uid, why = None, ""
         try:
-            comm = RcclComm(rank, world)
+            if rank == 0:
+                uid = rccl.unique_id()
+            else:
+                rccl._lib()
+        except (OSError, RuntimeError) as e:
+            why = str(e)
+        if not agree(why):
+            return None, f"torch collectives (RCCL library refused: {why or 'on a peer'})"
+        comm = RcclComm(rank, world, uid=uid)  # collective; a failure here ends the rank
+        try:
             t = torch.ones(1, dtype=torch.float32, device=device)
             comm.all_reduce_sum(t)
             torch.cuda.synchronize(device)
             if float(t.item()) != float(world):
                 why = f"check all-reduce gave {float(t.item())} for {world} ranks"
-        except RuntimeError as e:  # ncclResult of init or of the check
+        except RuntimeError as e:  # ncclResult of the check
             why = str(e)
-        ok = torch.tensor([0 if why else 1], dtype=torch.int32, device=device)
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        if int(ok.item()) == 1:
+        if agree(why):
             return comm, "rccl (own communicator, captured per epoch)"
-        if comm is not None:
-            comm.close(abort=True)
+        comm.close(abort=True)
         return None, f"torch collectives (own RCCL communicator refused: {why or 'on a peer'})"
 
     def close(self):

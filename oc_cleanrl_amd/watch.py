@@ -26,16 +26,24 @@ import time
 from pathlib import Path
 
 
-def read_status(dirname, since: float = 0.0) -> dict:
+def run_token() -> str:
+    """Names this run in the status records: OCPPO_RUN_ID when a launcher sets one, else the
+    parent's pid -- the ranks of one node are the children of one launcher process (torchrun's
+    agent, mp.spawn's parent), and a later run on the same status directory has another."""
+    return os.getenv("OCPPO_RUN_ID") or f"ppid{os.getppid()}"
+
+
+def read_status(dirname, since: float = 0.0, run: str | None = None) -> dict:
     """{rank: record} of every rank that wrote a status file in `dirname` at wall time >= since
-    (older files are a previous run's)."""
+    and, given `run`, carries that run token (other files are a previous run's: a directory keyed
+    by the master port is shared by every run on that port)."""
     out = {}
     if not dirname:
         return out
     for p in sorted(Path(dirname).glob("rank*.json")):
         try:
             rec = json.loads(p.read_text())
-            if rec.get("t", 0.0) >= since:
+            if rec.get("t", 0.0) >= since and (run is None or rec.get("run") == run):
                 out[int(rec["rank"])] = rec
         except (OSError, ValueError, KeyError):
             continue
@@ -63,6 +71,7 @@ class RankWatch:
         self.linger_s = linger_s
         self.t0 = self.last = time.monotonic()
         self.since = time.time() - 600.0  # peers started within the launcher's rendezvous window
+        self.run = run_token()
         self.name, self.n, self.bound = "start", 0, stall_s
         self.failed = None
         self._stop = threading.Event()
@@ -94,7 +103,7 @@ class RankWatch:
         if self.dir is None:
             return
         rec = {"rank": self.rank, "phase": self.name, "n": self.n, "pid": os.getpid(),
-               "t": round(time.time(), 3)}
+               "t": round(time.time(), 3), "run": self.run}
         if self.failed:
             rec["failed"] = self.failed
         tmp = self.dir / f".rank{self.rank}.{os.getpid()}.tmp"
@@ -106,7 +115,7 @@ class RankWatch:
 
     def record(self, reason: str) -> dict:
         now = time.monotonic()
-        ranks = read_status(self.dir, self.since)
+        ranks = read_status(self.dir, self.since, self.run)
         return {"error": reason, "rank": self.rank, "world": self.world, "phase": self.name,
                 "phase_s": round(now - self.last, 1), "elapsed_s": round(now - self.t0, 1),
                 "ranks": {str(k): v["phase"] for k, v in sorted(ranks.items())},
@@ -123,7 +132,7 @@ class RankWatch:
             if stalled or late:
                 self.fire("stall" if stalled else "deadline")
             if self.rank == 0 and self.world > 1:
-                peers = [k for k, v in read_status(self.dir, self.since).items()
+                peers = [k for k, v in read_status(self.dir, self.since, self.run).items()
                          if k != 0 and v.get("failed")]
                 if peers:
                     self.fire(f"rank {peers[0]} failed")

@@ -37,6 +37,28 @@ def golden(name: str) -> dict:
         return {k: z[k] for k in z.files}
 
 
+@pytest.fixture(autouse=True)
+def _x6_bounds_record():
+    """Bounds-check builds of the library (ops.X6_BOUNDS, tools/run_bounds_check.sh): after every
+    test, no convolution gather may have computed an out-of-range index (ops.bounds_record)."""
+    yield
+    ops = sys.modules.get("oc_cleanrl_amd.ops")
+    if ops is None or not ops.X6_BOUNDS or not ops._BOUNDS_REC:
+        return
+    import torch
+
+    torch.cuda.synchronize()
+    for key, rec in ops._BOUNDS_REC.items():
+        r = rec.cpu().tolist()
+        rec.zero_()
+        if r[0]:
+            kind = ops.BOUND_KINDS.get(r[1], r[1])
+            idx = (r[2] & 0xffffffff) | (r[3] << 32)
+            lim = (r[4] & 0xffffffff) | (r[5] << 32)
+            pytest.fail(f"{r[0]} out-of-range gather indices on {key}; first: {kind} {idx} "
+                        f"(limit {lim})")
+
+
 @pytest.fixture(scope="session")
 def dev():
     import torch

@@ -7,6 +7,7 @@ import json
 import os
 import socket
 import sys
+import time
 import types
 
 import pytest
@@ -161,3 +162,25 @@ def test_rehearsal_without_a_stall_completes(capfd):
     assert rc == 0
     rec = json.loads(capfd.readouterr().out.splitlines()[-1])
     assert rec == {"rehearsal": "no stall", "value": 8.0}
+
+
+def test_status_of_a_previous_run_is_ignored(tmp_path, monkeypatch):
+    """a port-keyed status directory is shared by every run on that port. A rank-1
+    record marked failed by an earlier run (another run token) must not fire this run's rank 0."""
+    import json as _json
+
+    from oc_cleanrl_amd import watch
+
+    (tmp_path / "rank1.json").write_text(_json.dumps(
+        {"rank": 1, "phase": "timed", "n": 5, "t": time.time(), "failed": "stall",
+         "run": "an-earlier-run"}))
+    monkeypatch.setenv("OCPPO_RUN_ID", "this-run")
+    assert watch.run_token() == "this-run"
+    assert watch.read_status(tmp_path, run="this-run") == {}
+    assert 1 in watch.read_status(tmp_path)  # unfiltered, the stale record is there
+    w = watch.RankWatch(0, 2, tmp_path, stall_s=30.0, poll_s=0.05)
+    try:
+        time.sleep(0.3)  # several polls: a match on the stale record would have fired (os._exit)
+        assert set(watch.read_status(tmp_path, run="this-run")) == {0}
+    finally:
+        w.stop()

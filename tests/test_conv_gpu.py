@@ -197,3 +197,44 @@ def test_data_gradient_takes_the_relu_backward_below(name):
     assert torch.equal(fused, want)
     ref = want.double().sum((0, 2, 3))
     assert torch.allclose(db.double(), ref, rtol=1e-6, atol=1e-6 * float(want.abs().sum()) / C)
+
+
+def test_u8_weight_gradient_index_slice_ends_before_a_sentinel():
+    """ADVICE r05 (the round-5 fault): the u8 weight-gradient loader walks each thread's K rows
+    image by image and must not read the index one past the minibatch's last image. idx here is a
+    slice of a longer int64 buffer whose next element is far out of range: a read of it would
+    fault or change the result. Bitwise the same gradient as from a private copy of idx."""
+    src = _frames(seed=11)
+    _, w, _, s = _operands("conv1", 12)
+    B = 16
+    buf = torch.full((B + 1,), 1 << 40, dtype=torch.int64, device=DEV)
+    buf[:B] = torch.randperm(src.shape[0], device=DEV)[:B]
+    idx = buf[:B]
+    g = torch.Generator(device=DEV).manual_seed(13)
+    gp = (torch.rand(B, 32, 20, 20, device=DEV, generator=g) * 2 - 1).contiguous(memory_format=CL)
+    rows = gp.permute(0, 2, 3, 1).reshape(-1, 32)
+    dw = ops.conv_x6_u8_wgrad(rows, src, idx, (8, 8), s)
+    assert torch.equal(dw, ops.conv_x6_u8_wgrad(rows, src, idx.clone(), (8, 8), s))
+    x = src[idx].float() / 255.0
+    ref = torch.nn.grad.conv2d_weight(x.double().cpu(), w.shape, gp.double().cpu(), stride=s)
+    assert float((dw.view(w.shape).double().cpu() - ref).abs().max()) <= 1e-6 * float(
+        torch.nn.grad.conv2d_weight(x.double().cpu().abs(), w.shape, gp.double().cpu().abs(),
+                                    stride=s).max())
+
+
+@pytest.mark.skipif(not ops.X6_BOUNDS, reason="bounds-check build only (OCPPO_LIB=... "
+                    "-DOCPPO_X6_BOUNDS, tools/run_bounds_check.sh)")
+def test_bounds_build_records_an_out_of_range_stack_row():
+    """Positive control of the bounds-check build: an index past the u8 stacks' rows is recorded
+    (kind 3, the index, the limit) instead of being read (the load falls back to offset 0)."""
+    src = _frames(R=20, seed=14)
+    _, w, b, s = _operands("conv1", 15)
+    idx = torch.arange(16, device=DEV)
+    idx[5] = 20  # one past the last stack
+    rec = ops.bounds_record(DEV)
+    rec.zero_()
+    ops.conv_x6_u8(src, idx, w, b, s, True)
+    torch.cuda.synchronize()
+    r = rec.cpu().tolist()
+    rec.zero_()
+    assert r[0] > 0 and r[1] == 3 and r[2] == 20 and r[4] == 20, r

@@ -19,21 +19,61 @@ def _port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out, fused_opt, graphs, overlap=True):
+# Config 2 per rank (ppo_atari_oc.py Pong obj, PPObj at the reference's default encoder (256, 512,
+# 1024, 512) / decoder (512,), 128 envs x 128 steps, 4 x 4 minibatches of 4096): the network's
+# real size, where the update's fused routes engage -- gemm_x6 with the ReLU backward in the next
+# dX, the frame-dedup gather / scatter, the first layer's backward in the second layer's dX, the
+# heads-loss finish in the decoder's combine. The toy dims reach none of them.
+CONFIG2 = dict(num_envs=128, num_steps=128, num_minibatches=4, update_epochs=4,
+               encoder_dims=(256, 512, 1024, 512), decoder_dims=(512,))
+TOY2 = dict(num_envs=16, num_steps=16, num_minibatches=2, update_epochs=2, encoder_dims=(32, 64),
+            decoder_dims=(64,))
+
+
+def _dp_args(world, dims, **kw):
+    from oc_cleanrl_amd.args import Args, finalize
+
+    d = dict(dims)
+    d["num_envs"] *= world
+    return finalize(Args(env_id="ALE/Pong-v5", obs_mode="obj", architecture="PPO_OBJ",
+                         total_timesteps=d["num_envs"] * d["num_steps"] * 10, save_model=False,
+                         **d, **kw), world)
+
+
+class GlooStandIn:
+    """rccl.RcclComm's all_reduce_sum over the gloo process group, issued in `stream`'s order:
+    drives rccl.RcclExchange's whole / split logic with two ranks holding different buffers."""
+
+    def __init__(self):
+        self.calls = []
+
+    def all_reduce_sum(self, t, stream=None):
+        s = stream if stream is not None else torch.cuda.current_stream(t.device)
+        self.calls.append((t.data_ptr(), t.numel(), s == torch.cuda.current_stream(t.device)))
+        with torch.cuda.stream(s):
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+
+
+def _worker(rank, world, port, out, fused_opt, graphs, overlap=True, dims=None, standin=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from oc_cleanrl_amd.args import Args, finalize
     from oc_cleanrl_amd.trainer import PPOTrainer
 
-    args = finalize(Args(env_id="ALE/Pong-v5", obs_mode="obj", architecture="PPO_OBJ",
-                         num_envs=16 * world, num_steps=16, num_minibatches=2, update_epochs=2,
-                         total_timesteps=16 * world * 16 * 10, encoder_dims=(32, 64),
-                         decoder_dims=(64,), save_model=False, fused_optimizer=fused_opt,
-                         cuda_graphs=graphs, dp_overlap=overlap), world)
-    tr = PPOTrainer(args, torch.device("cuda:0"), rank, world)
+    args = _dp_args(world, dims or TOY2, fused_optimizer=fused_opt, cuda_graphs=graphs,
+                    dp_overlap=overlap)
+    comm = GlooStandIn() if standin else None
+    tr = PPOTrainer(args, torch.device("cuda:0"), rank, world, comm=comm)
     assert bool(tr.split) == overlap
     for _ in range(3):
         tr.train_iteration()
+    if standin:
+        # split form: per minibatch the tail on the side stream, then the head on the main one
+        nmb = tr.E * tr.nmb * 3
+        n = tr.grad_buf.numel()
+        expect = ([(tr.grad_buf[tr.tail_off:].data_ptr(), n - tr.tail_off, False),
+                   (tr.grad_buf.data_ptr(), tr.tail_off, True)] if overlap else
+                  [(tr.grad_buf.data_ptr(), n, True)])
+        assert comm.calls == expect * nmb, (comm.calls[:3], expect)
     torch.cuda.synchronize()
     out[rank] = (torch.cat([p.detach().flatten() for p in tr.agent.parameters()]).cpu(),
                  tr.actions.cpu())
@@ -66,7 +106,7 @@ def test_overlapped_exchange_equals_the_whole_buffer_exchange():
 
 
 
-def _rccl_worker(rank, world, port, out, overlap, graphs, mode="rccl"):
+def _rccl_worker(rank, world, port, out, overlap, graphs, mode="rccl", dims=None):
     """The RCCL exchange path at world size 1: nccl (= RCCL) process group bound to cuda:0,
     against the plain single-GPU trainer in the same process. mode "rccl": the package's own
     communicator, each epoch's all-reduces captured in its graph (the tail's on a side stream
@@ -76,17 +116,15 @@ def _rccl_worker(rank, world, port, out, overlap, graphs, mode="rccl"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
-    from oc_cleanrl_amd.args import Args, finalize
     from oc_cleanrl_amd.trainer import PPOTrainer
 
+    toy = dict(num_envs=32, num_steps=16, num_minibatches=4, update_epochs=2,
+               encoder_dims=(32, 64, 48), decoder_dims=(64,))
+
     def args(dp):
-        return finalize(Args(env_id="ALE/Pong-v5", obs_mode="obj", architecture="PPO_OBJ",
-                             num_envs=32, num_steps=16, num_minibatches=4, update_epochs=2,
-                             total_timesteps=32 * 16 * 10, encoder_dims=(32, 64, 48),
-                             decoder_dims=(64,), save_model=False, cuda_graphs=graphs,
-                             dp_overlap=overlap, dp_exchange=dp,
-                             dp_collectives="rccl" if mode == "rccl" else "torch",
-                             dp_graph_collectives=mode == "torch-graph"), 1)
+        return _dp_args(1, dims or toy, cuda_graphs=graphs, dp_overlap=overlap, dp_exchange=dp,
+                        dp_collectives="rccl" if mode == "rccl" else "torch",
+                        dp_graph_collectives=mode == "torch-graph")
 
     plain = PPOTrainer(args(False), dev)
     for _ in range(3):
@@ -143,3 +181,42 @@ def test_overlapped_exchange_equals_single_allreduce(graphs):
         mp.spawn(_worker, args=(2, _port(), out, True, graphs, overlap), nprocs=2, join=True)
         res.append(out[0][0])
     assert torch.equal(res[0], res[1])
+
+
+@pytest.mark.parametrize("overlap,graphs,mode", [
+    (True, True, "rccl"), (True, False, "rccl"), (True, True, "torch")])
+def test_dp_exchange_one_rank_matches_single_gpu_at_config2(overlap, graphs, mode):
+    """the N > 1 default (own RCCL communicator, overlap split, captured per
+    epoch) at world 1 and config 2's real network size leaves the parameters bit-identical to the
+    plain single-GPU trainer after 3 iterations. The cut before the last encoder layer hands the
+    layer below its ReLU backward and bias-gradient partials through the box (frames._cut), so
+    the split chain runs the same products in the same order as the uncut one."""
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_rccl_worker, args=(1, _port(), out, overlap, graphs, mode, CONFIG2), nprocs=1,
+             join=True)
+    assert out["same_actions"]
+    assert torch.equal(out["plain"], out["dp"]), \
+        float((out["plain"] - out["dp"]).abs().max())
+
+
+@pytest.mark.parametrize("standin", [False, True])
+def test_overlapped_exchange_equals_whole_at_config2(standin):
+    """Two ranks sharing cuda:0 at config 2 per rank: the split exchange (the tail all-reduced on
+    a side stream while the lower encoder layers' backward still runs, then the head) leaves the
+    same parameters, bit for bit, as one all-reduce after the whole backward -- on the real x6 /
+    frame-dedup routes, where a tail gradient written after its all-reduce was issued would show.
+    standin: the exchange is rccl.RcclExchange itself (the N > 1 default's code) over a gloo
+    stand-in communicator, so its whole() / split() reduce two different buffers; else torch's
+    collectives (trainer.GradExchange)."""
+    res = []
+    for overlap in (False, True):
+        mgr = mp.Manager()
+        out = mgr.dict()
+        mp.spawn(_worker, args=(2, _port(), out, True, not standin, overlap, CONFIG2, standin),
+                 nprocs=2, join=True)
+        (p0, a0), (p1, a1) = out[0], out[1]
+        assert torch.equal(p0, p1), "DP replicas diverged"
+        assert not torch.equal(a0, a1), "ranks must roll out different env shards"
+        res.append(p0)
+    assert torch.equal(res[0], res[1]), float((res[0] - res[1]).abs().max())

@@ -804,6 +804,35 @@ def test_lagged_metrics_are_the_synced_ones(dev):
             assert a[k] == b[k] or (a[k] != a[k] and b[k] != b[k]), (k, a[k], b[k])
 
 
+def test_lagged_metrics_survive_a_gpu_that_has_caught_up(dev):
+    """The lagged read of iteration k happens after iteration k+1's non-blocking copy is queued.
+    With the GPU drained before every read (torch.cuda.synchronize: k+1's copy has landed), the
+    values read are still iteration k's -- the two pinned vectors are used in turn."""
+    from oc_cleanrl_amd.args import Args, finalize
+    from oc_cleanrl_amd.trainer import PPOTrainer
+
+    def run(lag):
+        args = finalize(Args(env_id="ALE/Pong-v5", obs_mode="obj", architecture="PPO_OBJ",
+                             num_envs=16, num_steps=16, num_features=12, seed=4,
+                             save_model=False), 1)
+        tr = PPOTrainer(args, dev)
+        if lag:
+            orig = tr._metrics_from
+
+            def drained(pend):
+                torch.cuda.synchronize()
+                return orig(pend)
+            tr._metrics_from = drained
+        out = [tr.train_iteration(collect_metrics=True, lag=lag) for _ in range(4)]
+        return out + [tr.flush_metrics()]
+
+    sync, lagged = run(False), run(True)
+    for a, b in zip(sync[:4], lagged[1:]):
+        assert a.keys() == b.keys()
+        for k in a:
+            assert a[k] == b[k] or (a[k] != a[k] and b[k] != b[k]), (k, a[k], b[k])
+
+
 def test_pixel_rollout_reads_the_u8_stacks(dev):
     """Config-3-like pixel rollout: the first convolution from the rollout buffer's u8 slot
     (trainer.U8_ROLLOUT_CONV) against the f32 network copy path — same actions and values up to
