@@ -370,6 +370,11 @@ def _gather_l1_ok(agent, obs, split: int) -> bool:
             and l1.weight.is_contiguous())
 
 
+# The DP cut's leaf carries the box of the layer below it (_cut). Off only to show what the box
+# buys (tests/test_dp_gpu.py: without it the split chain's arithmetic differs from the uncut one)
+CUT_CARRIES_BOX = True
+
+
 def _cut(low):
     """The leaf the layers above a DP cut read instead of `low`. It carries `low`'s box (the
     Linear+ReLU that produced it), so the first layer above the cut still takes that ReLU's
@@ -379,7 +384,7 @@ def _cut(low):
     different summation order of that layer's bias gradient (VERDICT r05 Weak 1)."""
     low_d = low.detach().requires_grad_()
     box = getattr(low, "_ocppo_box", None)
-    if box is not None:
+    if box is not None and CUT_CARRIES_BOX:
         low_d._ocppo_box = box
     return low_d
 

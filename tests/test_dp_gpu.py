@@ -106,7 +106,7 @@ def test_overlapped_exchange_equals_the_whole_buffer_exchange():
 
 
 
-def _rccl_worker(rank, world, port, out, overlap, graphs, mode="rccl", dims=None):
+def _rccl_worker(rank, world, port, out, overlap, graphs, mode="rccl", dims=None, box=True):
     """The RCCL exchange path at world size 1: nccl (= RCCL) process group bound to cuda:0,
     against the plain single-GPU trainer in the same process. mode "rccl": the package's own
     communicator, each epoch's all-reduces captured in its graph (the tail's on a side stream
@@ -116,8 +116,10 @@ def _rccl_worker(rank, world, port, out, overlap, graphs, mode="rccl", dims=None
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
+    from oc_cleanrl_amd import frames
     from oc_cleanrl_amd.trainer import PPOTrainer
 
+    frames.CUT_CARRIES_BOX = box
     toy = dict(num_envs=32, num_steps=16, num_minibatches=4, update_epochs=2,
                encoder_dims=(32, 64, 48), decoder_dims=(64,))
 
@@ -220,3 +222,15 @@ def test_overlapped_exchange_equals_whole_at_config2(standin):
         assert not torch.equal(a0, a1), "ranks must roll out different env shards"
         res.append(p0)
     assert torch.equal(res[0], res[1]), float((res[0] - res[1]).abs().max())
+
+
+def test_config2_cut_without_the_box_is_not_the_plain_chain():
+    """Sensitivity of the test above: with the cut leaf NOT carrying the box (the round-5 form),
+    the layer below the cut re-derives its ReLU backward and bias gradient with relu_bias_grad's
+    row chunks -- another summation order -- and the config-2 parameters differ from the plain
+    chain's after 3 iterations (round 5's checksums 0c39... vs 0ebad...)."""
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_rccl_worker, args=(1, _port(), out, True, True, "rccl", CONFIG2, False), nprocs=1,
+             join=True)
+    assert not torch.equal(out["plain"], out["dp"])
