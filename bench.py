@@ -442,6 +442,44 @@ def rehearse_stall(opt, rank: int, world: int, line_out, watch):
 DQN_STEPS_PER_BENCH_STEP = 1000
 
 
+def dqn_roofline(tr) -> dict:
+    """The dominant kernels of the config-5 step: the acting Q-trunk (agents.fused_trunk over the
+    env's W frame rows: the first two layers in one launch, then one launch per layer), run once
+    per global step. At M = W rows every weight is used for 2 W flops, far below the ridge: a
+    weight stream, HBM-bound by nature. achieved = the trunk's weight + bias bytes (+ the
+    activations) per step / the trunk's launches' device time, timed by replaying exactly those
+    launches in a hipGraph (trainer.replay_time_us): warm as the loop runs them (the 8.9 MB of
+    weights stay Infinity-Cache resident between steps), and cold after an L3 scrub."""
+    import torch.nn as nn
+
+    from oc_cleanrl_amd.agents import fused_trunk
+    from oc_cleanrl_amd.trainer import replay_time_us
+
+    net = tr.q.network[:-1]
+    x = tr.net_obs
+
+    def trunk():
+        with torch.no_grad():
+            fused_trunk(net, x)
+
+    warm = replay_time_us(trunk, reps=64, rounds=5)
+    cold = replay_time_us(trunk, reps=16, rounds=5, cold=True)
+    rows = x.numel() // x.shape[-1]  # encoder rows: every frame of every env's stack
+    nbytes = 0
+    for m in net:
+        if isinstance(m, nn.Flatten):
+            rows = x.shape[0]  # decoder rows: one per env
+        elif isinstance(m, nn.Linear):
+            nbytes += 4 * (m.weight.numel() + m.bias.numel() +
+                           rows * (m.in_features + m.out_features))
+    return {"kernel": "acting Q-trunk (linear2_rows + linear_rows launches, one step)",
+            "bound": "hbm", "achieved": round(nbytes / (cold * 1e-6) / 1e9, 1),
+            "achieved_warm": round(nbytes / (warm * 1e-6) / 1e9, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(nbytes / (cold * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+            "traffic": None, "bytes": nbytes, "launch_us_cold": round(cold, 2),
+            "launch_us_warm": round(warm, 2), "per": "global step"}
+
+
 def run_dqn(opt, rank: int, world: int, line_out, watch):
     """BASELINE config 5: the training phase of dqn_atari_oc.py:341-400 on one GPU (obj mode,
     1 env, a 1M-transition HBM replay; acting, env step, store, replay add every global step, a
@@ -477,17 +515,20 @@ def run_dqn(opt, rank: int, world: int, line_out, watch):
     dt = time.perf_counter() - t0
     m = tr.metrics()
     watch.phase("report", stall_s=max(opt.deadline, 600.0))
+    roofline = dqn_roofline(tr) if not opt.no_kernel_timing else None
     cpu = None
     if not opt.no_cpu_baseline:
         from oracle.cpu_learner import host_info, time_cpu_dqn, usable_threads
 
         threads = usable_threads()
-        r = time_cpu_dqn(steps=opt.cpu_iterations * 1000, threads=threads, num_envs=envs)
+        # the same 1M-transition replay as the GPU side (host numpy rows)
+        r = time_cpu_dqn(steps=opt.cpu_iterations * 1000, threads=threads, num_envs=envs,
+                         buffer_size=args.buffer_size)
         cpu = {"value": round(r["sps"], 1), "unit": "env steps/s", "cores": threads,
                "kind": "port", "updates_per_sec": round(r["updates_per_sec"], 2),
                "sample": f"{r['steps']} global steps of dqn_atari_oc.py:341-400 (QNetworkObj, "
-                         f"{envs} env, batch-32 TD update every 4 steps) on CPU torch, "
-                         f"{r['seconds']:.1f} s", "host": host_info()}
+                         f"{envs} env, {args.buffer_size}-transition replay, batch-32 TD update "
+                         f"every 4 steps) on CPU torch, {r['seconds']:.1f} s", "host": host_info()}
     steps = opt.steps * K
     line = {
         "metric": "env steps/sec + DQN updates/sec, dqn_atari_oc.py SpaceInvaders-v5 obj, 1 MI355X",
@@ -504,6 +545,7 @@ def run_dqn(opt, rank: int, world: int, line_out, watch):
         "updates_per_sec": round(steps / args.train_frequency / dt, 2),
         "us_per_global_step": round(dt / steps * 1e6, 3),
         "td_loss": m["losses/td_loss"],
+        "roofline": roofline,
         "cpu_baseline": cpu,
     }
     print(json.dumps(line), file=line_out, flush=True)

@@ -300,6 +300,23 @@ def _direct(p) -> bool:
     return getattr(p, "_ocppo_direct_grad", False) and p.grad is not None
 
 
+# Autograd forwards of <= SMALL_FWD_ROWS rows on the HIP rollout Linear kernel (ops.linear_act,
+# f32 MFMA, LDS-staged; bias + ReLU epilogue) instead of hipBLASLt: at these sizes both are launch-
+# and latency-bound and the library's kernels take 8-10 us against 4-6 (the DQN train step's
+# forwards at 128 / 32 rows, profiles/r05/dqn/fused_step_kernel_stats.csv)
+SMALL_FWD = True
+SMALL_FWD_ROWS = 128
+
+
+def _small_fwd_ok(x, w) -> bool:
+    if not (SMALL_FWD and x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and
+            w.dtype == torch.float32 and w.is_contiguous()):
+        return False
+    M, K = x.shape
+    return (1 <= M <= SMALL_FWD_ROWS and (M == 1 or x.stride(1) == 1) and
+            (K <= 64 or (K <= 2048 and K % 16 == 0)))
+
+
 class _LinearAct(torch.autograd.Function):
     """y = act(x @ W^T + b), act = ReLU (one hipBLASLt GEMM with a bias+ReLU epilogue,
     torch._addmm_activation) or identity (addmm). Backward = autograd's linear(+ReLU) formulas
@@ -331,6 +348,10 @@ class _LinearAct(torch.autograd.Function):
                                                   planes=pf)
             else:
                 out = ops.linear_x6(x, wm, b, relu, planes=pf)
+        elif chw is None and _small_fwd_ok(x, wm):
+            # a few rows under autograd (the DQN train step's batch of 32, CartPole's minibatch):
+            # the rollout's LDS-staged f32-MFMA kernel instead of a library launch
+            out = ops.linear_act(x, wm, b, relu)
         elif fs is not None and ops._x6_operand_ok(x) and ops._x6_operand_ok(wm) and \
                 (b is None or b.data_ptr() % 16 == 0):
             # K-split partials + the combine with bias / ReLU (no bitmask: a consumer's fused dX
@@ -524,6 +545,8 @@ class _QHead(torch.autograd.Function):
         ctx.box = box
         if box is not None:
             box["premasked"] = True
+        if _small_fwd_ok(h, wq) and bq is not None:
+            return ops.linear_act(h, wq, bq, False)
         return torch.addmm(bq, h, wq.t())
 
     @staticmethod
