@@ -745,6 +745,21 @@ def run_rank(opt, rank: int, world: int, line_out, watch):
                          f"envs x 128 steps, 16 minibatch updates of 128) on CPU torch, 1 thread, "
                          f"{r['seconds']:.1f} s",
                "host": host_info()}
+    if rank == 0 and world == 1 and not opt.no_cpu_baseline and opt.config == 3:
+        # config 3's CPU leg: ONE whole iteration of the oracle's port (256 pixel envs x 128
+        # steps of the NatureCNN + 4 x 4 minibatch updates of 8192) on every usable host thread
+        # (about 30 s on the box's 16 threads), not an extrapolation
+        from oracle.cpu_learner import host_info, time_cpu_baseline, usable_threads
+
+        threads = usable_threads()
+        r = time_cpu_baseline(iterations=1, threads=threads, num_envs=256, num_steps=128,
+                              n_actions=4, pixels=True)
+        cpu = {"value": round(r["sps"], 1), "unit": "env steps/s", "cores": threads,
+               "kind": "port", "updates_per_sec": round(r["updates_per_sec"], 3),
+               "sample": f"1 PPO iteration of config 3 (256 Breakout-pixel envs x 128 steps, "
+                         f"NatureCNN, 16 minibatch updates of 8192) on CPU torch, "
+                         f"{r['seconds']:.1f} s",
+               "host": host_info()}
     if rank == 0 and world == 1 and not opt.no_cpu_baseline and opt.config == 2:
         # CPU baseline leg (the oracle's port of the reference loop), on every host core this
         # process may use (its CPU affinity capped by the cgroup quota)
