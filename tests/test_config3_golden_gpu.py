@@ -5,9 +5,11 @@ tests/golden/update_config3.npz (gen_golden.gen_update_config3) is the reference
 (ppo_atari_oc.py:533-547) and two minibatch updates of 2048 through its update block (:566-610)
 on PPODefault over a rollout-structured 16 x 256 batch of synthetic Breakout frame stacks (the
 frame-stack rule with resets), with a float64 twin of the update at the f32 reference's
-parameters. The trainer runs exactly the bench's config-3 path: u8 -> f32 NHWC gather with
-NormalizeImg folded in, channels_last convolutions on MIOpen (Find-selected solutions, the bench's
-flags) with HIP bias/ReLU and ReLU-backward/bias-grad passes, the 3136 -> 512 Linear on the
+parameters. The trainer runs exactly the bench's config-3 path: the first convolution reading the
+rollout's u8 frame stacks through the minibatch indices (NormalizeImg's / 255 in its epilogue),
+every convolution on this package's implicit GEMMs (ocppo_conv_x6 / ocppo_conv_x6_u8: forward with
+bias + ReLU, weight and data gradients; agents.CONV_X6 is on whatever torch_deterministic says, so
+no MIOpen kernel runs), the HIP ReLU-backward / bias-gradient passes, the 3136 -> 512 Linear on the
 activation's NHWC memory order, HIP loss, clip + Adam; once eagerly and once as the captured
 hipGraph the bench replays.
 """
@@ -156,8 +158,10 @@ def test_config3_gae_matches_reference(dev, fixture):
 def test_config3_update_matches_reference_eager_and_captured(dev, fixture):
     """Two minibatch updates of 2048: eager with per-minibatch checks against the f64 twin and the
     f32 reference, then the same two updates replayed as the captured hipGraph from the same
-    start (parameters, Adam state) -- within MIOpen's run-to-run reordering of the eager run
-    (its Find-selected convolution kernels need not be bitwise repeatable)."""
+    start (parameters, Adam state). The package's convolutions are deterministic (split partials
+    summed in a fixed order), so the captured run is held to a small tolerance, not to MIOpen's
+    run-to-run reordering (the bitwise check at config 3's own size is
+    test_config3_deterministic_captured_update_is_bitwise_eager)."""
     z = fixture
     tr = config3_trainer(dev, z)
     tr.advantages.view(-1).copy_(torch.from_numpy(z["advantages"]).to(dev))
@@ -175,9 +179,11 @@ def test_config3_update_matches_reference_eager_and_captured(dev, fixture):
         print(f"minibatch {j}: grad norm {gn:.8g}, f64 {gn64:.8g}, f32 ref {z['grad_norms'][j]:.8g};"
               " pre-clip error vs f64 per tensor (ours / reference f32): "
               + ", ".join(f"{k} {a:.2g}/{b:.2g}" for k, (a, b) in e.items()))
-        # end-to-end, ReLU decisions included: the f32 reference's own worst is 4e-4 here
+        # end-to-end, ReLU decisions included: the f32 reference's own worst is 4e-4 here (its
+        # ReLU decisions against f64's), ours 5.5e-4 on the package's convolutions (round 5: 2e-3
+        # was MIOpen's bound)
         assert abs(gn - gn64) <= 1e-4 * gn64, (j, gn, gn64)
-        assert max(a for a, _ in e.values()) <= 2e-3, e
+        assert max(a for a, _ in e.values()) <= 1e-3, e
         tr._opt_step()
         torch.cuda.synchronize()
         np.testing.assert_allclose(tr.stats[j].cpu().numpy(), z["stats"][j], rtol=1e-4,
@@ -221,10 +227,11 @@ def test_config3_update_matches_reference_eager_and_captured(dev, fixture):
 
 def test_config3_full_size_captured_update_matches_eager(dev):
     """At config 3's own size (256 envs x 128 steps, minibatches of 8192, the bench's flags): one
-    rollout, then the update epoch eagerly and as the captured hipGraph from the same start. The
-    convolutions are MIOpen's Find-selected solutions (torch_deterministic=False, as the bench
-    line states): the two runs are compared to a tolerance, and whether they are bitwise equal is
-    printed."""
+    rollout, then the update epoch eagerly and as the captured hipGraph from the same start, with
+    torch_deterministic=False (the setting round 4's MIOpen line ran at). The convolutions are
+    this package's implicit GEMMs either way (agents.CONV_X6), so the two runs are compared to a
+    tolerance here and whether they are bitwise equal is printed; the bitwise assertion at
+    torch_deterministic=True is the next test."""
     from oc_cleanrl_amd.args import Args, finalize
     from oc_cleanrl_amd.trainer import PPOTrainer
 
