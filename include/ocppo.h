@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define OCPPO_ABI_VERSION 24
+#define OCPPO_ABI_VERSION 25
 
 /* status codes */
 #define OCPPO_OK 0
@@ -513,6 +513,9 @@ OCPPO_API int ocppo_conv_x6(ocppo_stream_t stream, int mode, const float* x, con
  *           N = C KH KW taps, K = B OH OW rows); c = split partials [splits, M, N], summed in
  *           split order in f64 and divided once.
  * KW, W, stride multiples of 4; no padding; tile 0 / 2 (mode 0), 1 / 4 (mode 1) as ocppo_conv_x6's.
+ * tile 7 (mode 0, ABI 25): each image's stack staged in LDS once, bitwise tile 0's output; needs
+ * C = 4, 8 x 8 taps, stride 4, N = 32, 16 | OH OW, src 16-B aligned, 16 | C H W, 2 C H W <= 64 KB
+ * (NatureCNN's first layer on 4 x 84 x 84 stacks); M a whole number of images, splits 1.
  * ------------------------------------------------------------------------------------------- */
 OCPPO_API int ocppo_conv_x6_u8(ocppo_stream_t stream, int mode, const uint8_t* src,
                                const int64_t* idx, int64_t C, int64_t H, int64_t W, int64_t KH,

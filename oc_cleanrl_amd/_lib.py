@@ -22,7 +22,7 @@ LIB_PATH = Path(os.environ.get("OCPPO_LIB", PKG / "lib" / "libocppo_hip.so"))
 HEADER = PKG.parent / "include" / "ocppo.h"
 
 # constants mirrored from include/ocppo.h (checked against the header by tests/test_abi.py)
-OCPPO_ABI_VERSION = 24
+OCPPO_ABI_VERSION = 25
 OCPPO_OK, OCPPO_E_INVALID, OCPPO_E_LAUNCH, OCPPO_E_WORKSPACE = 0, 1, 2, 3
 OCPPO_F32, OCPPO_BF16, OCPPO_U8 = 0, 1, 2
 OCPPO_X6_MBITS_ROWS = 2

@@ -2119,6 +2119,133 @@ __global__ __launch_bounds__(64 * kSumGroups) void sum_parts_kernel(const float*
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// The first NatureCNN convolution (8 x 8 taps, stride 4, 32 output channels) from the u8 frame
+// stacks with each IMAGE staged in LDS once (ocppo_conv_x6_u8 mode 0, tile 7). The tile loop
+// above gathers every window from L2 (the 8 x 8 / 4 windows overlap 4x, and each loaded byte
+// feeds only 32 output channels); here a workgroup copies a whole C x H x W stack into LDS as
+// exact bf16 (one coalesced read of its bytes, converted once), and every window row of 8 taps
+// is then one 16-B fragment read from LDS. Persistent: a workgroup takes images blockIdx.x,
+// + gridDim.x, ...; the weight's three bf16 pieces stay in registers for all of them (split once
+// per workgroup with x6_split2, the tile loop's own split). Two workgroups per CU: one's image
+// copy overlaps the other's MFMAs.
+// Same products in the same order as the tile loop (tile 0 / 2): per output element the K steps
+// of 32 taps in order, each as the three MFMAs a0 b0, a0 b2, a0 b1 (x6_mfma3<true>) with the
+// same lane <-> tap assignment, then / cdiv, + bias, ReLU: bitwise the same output
+// (tests/test_conv_gpu.py).
+constexpr int kImgCO = 32;   // output channels (two 16-column blocks)
+constexpr int kImgKW = 8;    // taps per kernel row = one 8-bf16 fragment chunk
+constexpr int kImgStride = 4;
+
+struct ConvImgArgs {
+  const uint8_t* src;
+  const int64_t* idx;
+  const float* w;     // [32, ldw], taps (c, ky, kx)
+  int64_t ldw;
+  const float* bias;  // [32] or null
+  float* out;         // [B * P, 32]
+  int B, H, W, OW, P;  // P = OH * OW output positions per image (P % 16 == 0)
+  int relu;
+  float cdiv;
+};
+
+template <int C>
+__global__ __launch_bounds__(256, 2) void conv_u8_img_kernel(ConvImgArgs a) {
+  constexpr int KS = 2 * C;  // K steps of 32 taps: two per channel (kernel rows 0-3, 4-7)
+  extern __shared__ __attribute__((aligned(16))) unsigned char conv_img_raw[];
+  uint16_t* img = reinterpret_cast<uint16_t*>(conv_img_raw);  // [C][H][W] bf16
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int fr = lane & 15, fc = lane >> 4;
+  // the weight's pieces: b[j][kt][pl] = 8 taps k = 32 kt + 8 fc + e of output channel 16 j + fr
+  bf16x8 bw[2][KS][3];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int kt = 0; kt < KS; ++kt) {
+      const float* wr = a.w + static_cast<int64_t>(16 * j + fr) * a.ldw + 32 * kt + 8 * fc;
+      const floatx4 lo = *reinterpret_cast<const floatx4*>(wr);
+      const floatx4 hi = *reinterpret_cast<const floatx4*>(wr + 4);
+      uint32_t p[4][3];
+      x6_split2(x6f2{lo[0], lo[1]}, p[0][0], p[0][1], p[0][2]);
+      x6_split2(x6f2{lo[2], lo[3]}, p[1][0], p[1][1], p[1][2]);
+      x6_split2(x6f2{hi[0], hi[1]}, p[2][0], p[2][1], p[2][2]);
+      x6_split2(x6f2{hi[2], hi[3]}, p[3][0], p[3][1], p[3][2]);
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        bw[j][kt][pl] = __builtin_bit_cast(bf16x8, u32x4{p[0][pl], p[1][pl], p[2][pl], p[3][pl]});
+    }
+  float bias[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) bias[j] = a.bias ? a.bias[16 * j + fr] : 0.f;
+  const int64_t bytes = static_cast<int64_t>(C) * a.H * a.W;  // % 16 == 0 (host check)
+  const int n16 = static_cast<int>(bytes / 16), tiles = a.P / 16;
+  for (int b = blockIdx.x; b < a.B; b += gridDim.x) {
+    // the stack of image b -> LDS as bf16 (a byte v is the bf16 of float(v), exact)
+    const uint4* src = reinterpret_cast<const uint4*>(a.src + a.idx[b] * bytes);
+    __syncthreads();  // the previous image's fragments are all read
+    for (int q = t; q < n16; q += 256) {
+      const uint4 v = src[q];
+      const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+      uint32_t o[8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float f0 = static_cast<float>(wd[i] & 0xffu);
+        const float f1 = static_cast<float>((wd[i] >> 8) & 0xffu);
+        const float f2 = static_cast<float>((wd[i] >> 16) & 0xffu);
+        const float f3 = static_cast<float>(wd[i] >> 24);
+        o[2 * i] = __builtin_amdgcn_perm(__float_as_uint(f1), __float_as_uint(f0), 0x07060302u);
+        o[2 * i + 1] = __builtin_amdgcn_perm(__float_as_uint(f3), __float_as_uint(f2), 0x07060302u);
+      }
+      uint4* d = reinterpret_cast<uint4*>(img) + 2 * q;
+      d[0] = uint4{o[0], o[1], o[2], o[3]};
+      d[1] = uint4{o[4], o[5], o[6], o[7]};
+    }
+    __syncthreads();
+    for (int tile = wv; tile < tiles; tile += 4) {
+      const int pa = 16 * tile + fr;  // this lane's A row: output position (oy, ox)
+      const int oy = pa / a.OW, ox = pa - oy * a.OW;
+      floatx4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int kt = 0; kt < KS; ++kt) {
+        // taps 32 kt + 8 fc + e = channel kt / 2, kernel row 4 (kt % 2) + fc, column e
+        const int c = kt >> 1, ky = 4 * (kt & 1) + fc;
+        const uint16_t* r = img + (c * a.H + kImgStride * oy + ky) * a.W + kImgStride * ox;
+        const uint2 lo = *reinterpret_cast<const uint2*>(r);      // 8-B aligned (ox * 4 bf16)
+        const uint2 hi = *reinterpret_cast<const uint2*>(r + 4);
+        const bf16x8 af = __builtin_bit_cast(bf16x8, u32x4{lo.x, lo.y, hi.x, hi.y});
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bw[j][kt][0], acc[j], 0, 0, 0);
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bw[j][kt][2], acc[j], 0, 0, 0);
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bw[j][kt][1], acc[j], 0, 0, 0);
+        }
+      }
+      // C/D layout: column fr of block j, rows 4 fc + r of the tile
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = acc[j][r] / a.cdiv;
+          if (a.bias) v += bias[j];
+          if (a.relu) v = relu_f(v);
+          a.out[(static_cast<int64_t>(b) * a.P + 16 * tile + 4 * fc + r) * kImgCO + 16 * j + fr] = v;
+        }
+    }
+  }
+}
+
+static int conv_u8_img_grid(int B) {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 1)
+      n = 256;
+    cus = n;
+  }
+  return B < 2 * cus ? B : 2 * cus;
+}
+
 }  // namespace ocppo
 
 extern "C" int ocppo_conv_x6(ocppo_stream_t stream, int mode, const float* x, const int64_t* geom,
@@ -2269,6 +2396,25 @@ extern "C" int ocppo_conv_x6_u8(ocppo_stream_t stream, int mode, const uint8_t* 
                 (long long)W, (long long)KH, (long long)KW, (long long)stride);
   const int64_t OH = (H - KH) / stride + 1, OW = (W - KW) / stride + 1, taps = C * KH * KW;
   const int64_t rows = mode == 0 ? M : K;
+  if (tile == 7) {  // the image-staged forward (conv_u8_img_kernel)
+    const int64_t P = OH * OW, bytes = C * H * W;
+    OCPPO_REQUIRE(mode == 0 && C == 4 && KH == kImgKW && KW == kImgKW && stride == kImgStride &&
+                      N == kImgCO && K == taps && splits == 1 && P % 16 == 0 && M % P == 0 &&
+                      M / P <= INT32_MAX && bytes % 16 == 0 && 2 * bytes <= 64 * 1024 &&
+                      ldw >= K && ldw % 4 == 0 && reinterpret_cast<uintptr_t>(src) % 16 == 0 &&
+                      reinterpret_cast<uintptr_t>(w) % 16 == 0 && M / P >= 1,
+                  "ocppo_conv_x6_u8: tile 7 (image-staged) needs mode 0, C = 4, 8 x 8 taps, "
+                  "stride 4, 32 output channels, 16 | OH OW, a 16-B aligned src with 16 | C H W, "
+                  "2 C H W <= 64 KB (C=%lld H=%lld W=%lld N=%lld M=%lld)", (long long)C,
+                  (long long)H, (long long)W, (long long)N, (long long)M);
+    ConvImgArgs ia{src, idx, w, ldw, bias, c, static_cast<int>(M / P), static_cast<int>(H),
+                   static_cast<int>(W), static_cast<int>(OW), static_cast<int>(P), relu ? 1 : 0,
+                   divisor};
+    clear_stale_error();
+    hipLaunchKernelGGL(conv_u8_img_kernel<4>, dim3(conv_u8_img_grid(ia.B)), dim3(256),
+                       static_cast<size_t>(2 * bytes), as_stream(stream), ia);
+    return check_launch("ocppo_conv_x6_u8 (image-staged)");
+  }
   const X6Tile tc = kConvTiles[tile >= 0 && tile < 7 ? tile : 0];
   const int64_t bm = 16 * tc.fm * tc.wgm, bn = 16 * tc.fn * tc.wgn;
   OCPPO_REQUIRE(M % bm == 0 && N % bn == 0 && K % kX6BK == 0 && splits >= 1 &&

@@ -991,10 +991,27 @@ def _conv_u8_tile(M: int, N: int, mode: int) -> int | None:
     return None
 
 
+# The first convolution's forward with each image's u8 stack staged in LDS once (ocppo_conv_x6_u8
+# tile 7, conv_u8_img_kernel: bitwise the tile loop's output) where the geometry is NatureCNN's
+# first layer (4 x 84 x 84 stacks, 8 x 8 taps, stride 4, 32 channels)
+CONV_U8_IMG = True
+
+
+def _conv_u8_img_ok(src, weight, stride: int) -> bool:
+    _, C, H, W = src.shape
+    Cout, _, KH, KW = weight.shape
+    OH, OW = (H - KH) // stride + 1, (W - KW) // stride + 1
+    return (CONV_U8_IMG and C == 4 and KH == 8 and KW == 8 and stride == 4 and Cout == 32 and
+            (OH * OW) % 16 == 0 and (C * H * W) % 16 == 0 and 2 * C * H * W <= 65536 and
+            src.data_ptr() % 16 == 0)
+
+
 def conv_x6_u8(src, idx, weight, bias=None, stride: int = 4, relu: bool = True,
-               divisor: float = 255.0, out=None):
+               divisor: float = 255.0, out=None, tile: int | None = None):
     """act(conv2d(src[idx] / divisor, weight) + bias) with the u8 frame stacks read in place
-    (ocppo_conv_x6_u8): src [R, C, H, W] u8, idx [B] int64 -> channels_last [B, Cout, OH, OW]."""
+    (ocppo_conv_x6_u8): src [R, C, H, W] u8, idx [B] int64 -> channels_last [B, Cout, OH, OW].
+    tile: None = the image-staged kernel where it applies (CONV_U8_IMG), else the tile loop's;
+    an explicit ocppo_conv_x6_u8 tile forces that form (tests)."""
     B = idx.numel()
     if not conv_x6_u8_ok(src, weight, stride, B):
         raise ValueError(f"conv_x6_u8: unsupported src {tuple(src.shape)} / weight "
@@ -1011,10 +1028,11 @@ def conv_x6_u8(src, idx, weight, bias=None, stride: int = 4, relu: bool = True,
     if tuple(out.shape) != (B, Cout, OH, OW) or not out.is_contiguous(memory_format=torch.channels_last):
         raise ValueError("conv_x6_u8: out must be a channels_last [B, Cout, OH, OW] tensor")
     _bounds(dev, u8=src)
+    if tile is None:
+        tile = 7 if _conv_u8_img_ok(src, weight, s) else _conv_u8_tile(M, Cout, 0)
     call("ocppo_conv_x6_u8", _stream(dev), 0, src.data_ptr(), _check(idx, "idx", torch.int64, dev, B),
          C, H, W, KH, KW, s, wn.data_ptr(), K, out.data_ptr(), M, Cout, K, 1,
-         _opt(bias, "bias", f, dev, Cout), int(bool(relu)), float(divisor),
-         _conv_u8_tile(M, Cout, 0), None)
+         _opt(bias, "bias", f, dev, Cout), int(bool(relu)), float(divisor), tile, None)
     return out
 
 

@@ -238,3 +238,19 @@ def test_bounds_build_records_an_out_of_range_stack_row():
     r = rec.cpu().tolist()
     rec.zero_()
     assert r[0] > 0 and r[1] == 3 and r[2] == 20 and r[4] == 20, r
+
+
+@pytest.mark.parametrize("relu", [True, False])
+@pytest.mark.parametrize("B", [16, 600])
+def test_u8_first_conv_image_staged_is_bitwise_the_tile_loop(relu, B):
+    """ocppo_conv_x6_u8 tile 7 (each image's u8 stack staged in LDS once, the weight's pieces in
+    registers, a persistent loop over images) against the tile loop (tile 0): the same products in
+    the same order, so the same bits; B = 600 images exceeds the persistent grid (512 workgroups)."""
+    src = _frames(R=B + 7, seed=16)
+    _, w, b, s = _operands("conv1", 17)
+    idx = torch.randperm(src.shape[0], device=DEV)[:B]
+    assert ops._conv_u8_img_ok(src, w, s)
+    staged = ops.conv_x6_u8(src, idx, w, b, s, relu, tile=7)
+    loop = ops.conv_x6_u8(src, idx, w, b, s, relu, tile=0)
+    assert torch.equal(staged, loop), float((staged - loop).abs().max())
+    assert torch.equal(staged, ops.conv_x6_u8(src, idx, w, b, s, relu))  # the default routes to 7
