@@ -2123,12 +2123,12 @@ __global__ __launch_bounds__(64 * kSumGroups) void sum_parts_kernel(const float*
 // The first NatureCNN convolution (8 x 8 taps, stride 4, 32 output channels) from the u8 frame
 // stacks with each IMAGE staged in LDS once (ocppo_conv_x6_u8 mode 0, tile 7). The tile loop
 // above gathers every window from L2 (the 8 x 8 / 4 windows overlap 4x, and each loaded byte
-// feeds only 32 output channels); here a workgroup copies a whole C x H x W stack into LDS as
-// exact bf16 (one coalesced read of its bytes, converted once), and every window row of 8 taps
-// is then one 16-B fragment read from LDS. Persistent: a workgroup takes images blockIdx.x,
-// + gridDim.x, ...; the weight's three bf16 pieces stay in registers for all of them (split once
-// per workgroup with x6_split2, the tile loop's own split). Two workgroups per CU: one's image
-// copy overlaps the other's MFMAs.
+// feeds only 32 output channels); here a workgroup copies a whole C x H x W stack into LDS with
+// LDS-DMA (global_load_lds, 16 B per lane: no VGPRs, no wait in the compute path) while it
+// computes the previous image (two image buffers), and every window row of 8 taps is then two
+// dword reads from LDS converted to bf16 in registers (a byte is exact in bf16). Persistent: a
+// workgroup takes images blockIdx.x, + gridDim.x, ...; the weight's three bf16 pieces stay in
+// registers for all of them (split once per workgroup with x6_split2, the tile loop's own split).
 // Same products in the same order as the tile loop (tile 0 / 2): per output element the K steps
 // of 32 taps in order, each as the three MFMAs a0 b0, a0 b2, a0 b1 (x6_mfma3<true>) with the
 // same lane <-> tap assignment, then / cdiv, + bias, ReLU: bitwise the same output
@@ -2136,6 +2136,7 @@ __global__ __launch_bounds__(64 * kSumGroups) void sum_parts_kernel(const float*
 constexpr int kImgCO = 32;   // output channels (two 16-column blocks)
 constexpr int kImgKW = 8;    // taps per kernel row = one 8-bf16 fragment chunk
 constexpr int kImgStride = 4;
+constexpr int kImgChunk = 1024;  // bytes one global_load_lds wave instruction writes
 
 struct ConvImgArgs {
   const uint8_t* src;
@@ -2149,14 +2150,54 @@ struct ConvImgArgs {
   float cdiv;
 };
 
+__device__ __forceinline__ uint32_t img_bf16x2(uint32_t v, int half) {
+  // bytes 2 half, 2 half + 1 of v -> two bf16 (the upper halves of their exact f32 values)
+  const float f0 = static_cast<float>(half ? (v >> 16) & 0xffu : v & 0xffu);
+  const float f1 = static_cast<float>(half ? v >> 24 : (v >> 8) & 0xffu);
+  return __builtin_amdgcn_perm(__float_as_uint(f1), __float_as_uint(f0), 0x07060302u);
+}
+
 template <int C>
 __global__ __launch_bounds__(256, 2) void conv_u8_img_kernel(ConvImgArgs a) {
   constexpr int KS = 2 * C;  // K steps of 32 taps: two per channel (kernel rows 0-3, 4-7)
   extern __shared__ __attribute__((aligned(16))) unsigned char conv_img_raw[];
-  uint16_t* img = reinterpret_cast<uint16_t*>(conv_img_raw);  // [C][H][W] bf16
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int fr = lane & 15, fc = lane >> 4;
-  // the weight's pieces: b[j][kt][pl] = 8 taps k = 32 kt + 8 fc + e of output channel 16 j + fr
+  const int64_t bytes = static_cast<int64_t>(C) * a.H * a.W;  // % 16 == 0 (host check)
+  const int nchunks = static_cast<int>((bytes + kImgChunk - 1) / kImgChunk);
+  const int64_t ibuf = static_cast<int64_t>(nchunks) * kImgChunk;  // one image buffer
+  // one image's bytes -> buffer `buf`: wave wv copies chunks wv, wv + 4, ... (lane-linear 16 B)
+  auto issue = [&](int64_t row, int buf) {
+    const uint8_t* s = a.src + row * bytes;
+    for (int ch = wv; ch < nchunks; ch += 4) {
+      const int64_t off = static_cast<int64_t>(ch) * kImgChunk + 16 * lane;
+      if (off < bytes)
+        __builtin_amdgcn_global_load_lds(
+            reinterpret_cast<const void*>(s + off),
+            (__attribute__((address_space(3))) void*)(conv_img_raw + buf * ibuf +
+                                                      static_cast<int64_t>(ch) * kImgChunk),
+            16, 0, 0);
+    }
+  };
+  int b = blockIdx.x;
+  if (b >= a.B) return;
+  const int grid = static_cast<int>(gridDim.x);
+  // the stack rows of this workgroup's images, 64 iterations at a time in one register (lane L:
+  // iteration w0 + L), read back with readlane: uniform values without a vector load (and its
+  // vmcnt wait, which would drain the LDS-DMA in flight) inside the loop
+  auto window = [&](int it0) -> int64_t {
+    const int bb = b + (it0 + lane) * grid;
+    return bb < a.B ? a.idx[bb] : 0;
+  };
+  auto row_of = [&](int64_t win, int l) -> int64_t {
+    const uint64_t u = static_cast<uint64_t>(win);
+    const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(u), l);
+    const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(u >> 32), l);
+    return static_cast<int64_t>((static_cast<uint64_t>(hi) << 32) | lo);
+  };
+  int64_t win = window(0);
+  issue(row_of(win, 0), 0);  // the first image's copy overlaps the weight split below
+  // the weight's pieces: bw[j][kt][pl] = 8 taps k = 32 kt + 8 fc + e of output channel 16 j + fr
   bf16x8 bw[2][KS][3];
 #pragma unroll
   for (int j = 0; j < 2; ++j)
@@ -2177,30 +2218,19 @@ __global__ __launch_bounds__(256, 2) void conv_u8_img_kernel(ConvImgArgs a) {
   float bias[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) bias[j] = a.bias ? a.bias[16 * j + fr] : 0.f;
-  const int64_t bytes = static_cast<int64_t>(C) * a.H * a.W;  // % 16 == 0 (host check)
-  const int n16 = static_cast<int>(bytes / 16), tiles = a.P / 16;
-  for (int b = blockIdx.x; b < a.B; b += gridDim.x) {
-    // the stack of image b -> LDS as bf16 (a byte v is the bf16 of float(v), exact)
-    const uint4* src = reinterpret_cast<const uint4*>(a.src + a.idx[b] * bytes);
-    __syncthreads();  // the previous image's fragments are all read
-    for (int q = t; q < n16; q += 256) {
-      const uint4 v = src[q];
-      const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
-      uint32_t o[8];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float f0 = static_cast<float>(wd[i] & 0xffu);
-        const float f1 = static_cast<float>((wd[i] >> 8) & 0xffu);
-        const float f2 = static_cast<float>((wd[i] >> 16) & 0xffu);
-        const float f3 = static_cast<float>(wd[i] >> 24);
-        o[2 * i] = __builtin_amdgcn_perm(__float_as_uint(f1), __float_as_uint(f0), 0x07060302u);
-        o[2 * i + 1] = __builtin_amdgcn_perm(__float_as_uint(f3), __float_as_uint(f2), 0x07060302u);
-      }
-      uint4* d = reinterpret_cast<uint4*>(img) + 2 * q;
-      d[0] = uint4{o[0], o[1], o[2], o[3]};
-      d[1] = uint4{o[4], o[5], o[6], o[7]};
-    }
+  const int tiles = a.P / 16;
+  for (int it = 0; b < a.B; b += gridDim.x, ++it) {
+    // this image's copy (and every wave's reads of the buffer the next copy reuses) are done:
+    // vmcnt(0) retires this wave's LDS-DMA (the compiler inserts no wait for it here), the
+    // barrier everyone's
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    const int cur = it & 1;
+    if (b + grid < a.B) {
+      if (((it + 1) & 63) == 0) win = window(it + 1);  // (the copies in flight: none)
+      issue(row_of(win, (it + 1) & 63), cur ^ 1);  // the next image's copy beside these MFMAs
+    }
+    const unsigned char* img = conv_img_raw + cur * ibuf;
     for (int tile = wv; tile < tiles; tile += 4) {
       const int pa = 16 * tile + fr;  // this lane's A row: output position (oy, ox)
       const int oy = pa / a.OW, ox = pa - oy * a.OW;
@@ -2209,10 +2239,12 @@ __global__ __launch_bounds__(256, 2) void conv_u8_img_kernel(ConvImgArgs a) {
       for (int kt = 0; kt < KS; ++kt) {
         // taps 32 kt + 8 fc + e = channel kt / 2, kernel row 4 (kt % 2) + fc, column e
         const int c = kt >> 1, ky = 4 * (kt & 1) + fc;
-        const uint16_t* r = img + (c * a.H + kImgStride * oy + ky) * a.W + kImgStride * ox;
-        const uint2 lo = *reinterpret_cast<const uint2*>(r);      // 8-B aligned (ox * 4 bf16)
-        const uint2 hi = *reinterpret_cast<const uint2*>(r + 4);
-        const bf16x8 af = __builtin_bit_cast(bf16x8, u32x4{lo.x, lo.y, hi.x, hi.y});
+        const uint32_t* r = reinterpret_cast<const uint32_t*>(
+            img + (c * a.H + kImgStride * oy + ky) * a.W + kImgStride * ox);
+        const uint32_t u0 = r[0], u1 = r[1];
+        const bf16x8 af = __builtin_bit_cast(
+            bf16x8, u32x4{img_bf16x2(u0, 0), img_bf16x2(u0, 1), img_bf16x2(u1, 0),
+                          img_bf16x2(u1, 1)});
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bw[j][kt][0], acc[j], 0, 0, 0);
@@ -2400,19 +2432,21 @@ extern "C" int ocppo_conv_x6_u8(ocppo_stream_t stream, int mode, const uint8_t* 
     const int64_t P = OH * OW, bytes = C * H * W;
     OCPPO_REQUIRE(mode == 0 && C == 4 && KH == kImgKW && KW == kImgKW && stride == kImgStride &&
                       N == kImgCO && K == taps && splits == 1 && P % 16 == 0 && M % P == 0 &&
-                      M / P <= INT32_MAX && bytes % 16 == 0 && 2 * bytes <= 64 * 1024 &&
+                      M / P <= INT32_MAX && bytes % 16 == 0 &&
+                      2 * ((bytes + kImgChunk - 1) / kImgChunk) * kImgChunk <= 64 * 1024 &&
                       ldw >= K && ldw % 4 == 0 && reinterpret_cast<uintptr_t>(src) % 16 == 0 &&
                       reinterpret_cast<uintptr_t>(w) % 16 == 0 && M / P >= 1,
                   "ocppo_conv_x6_u8: tile 7 (image-staged) needs mode 0, C = 4, 8 x 8 taps, "
                   "stride 4, 32 output channels, 16 | OH OW, a 16-B aligned src with 16 | C H W, "
-                  "2 C H W <= 64 KB (C=%lld H=%lld W=%lld N=%lld M=%lld)", (long long)C,
+                  "two image buffers of C H W (1 KiB-rounded) <= 64 KB (C=%lld H=%lld W=%lld N=%lld M=%lld)", (long long)C,
                   (long long)H, (long long)W, (long long)N, (long long)M);
     ConvImgArgs ia{src, idx, w, ldw, bias, c, static_cast<int>(M / P), static_cast<int>(H),
                    static_cast<int>(W), static_cast<int>(OW), static_cast<int>(P), relu ? 1 : 0,
                    divisor};
     clear_stale_error();
-    hipLaunchKernelGGL(conv_u8_img_kernel<4>, dim3(conv_u8_img_grid(ia.B)), dim3(256),
-                       static_cast<size_t>(2 * bytes), as_stream(stream), ia);
+    const size_t ibuf = static_cast<size_t>((bytes + kImgChunk - 1) / kImgChunk) * kImgChunk;
+    hipLaunchKernelGGL(conv_u8_img_kernel<4>, dim3(conv_u8_img_grid(ia.B)), dim3(256), 2 * ibuf,
+                       as_stream(stream), ia);
     return check_launch("ocppo_conv_x6_u8 (image-staged)");
   }
   const X6Tile tc = kConvTiles[tile >= 0 && tile < 7 ? tile : 0];
