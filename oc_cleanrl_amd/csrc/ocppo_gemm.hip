@@ -2158,7 +2158,7 @@ __device__ __forceinline__ uint32_t img_bf16x2(uint32_t v, int half) {
 }
 
 template <int C>
-__global__ __launch_bounds__(256, 1) void conv_u8_img_kernel(ConvImgArgs a) {
+__global__ __launch_bounds__(256, 2) void conv_u8_img_kernel(ConvImgArgs a) {
   constexpr int KS = 2 * C;  // K steps of 32 taps: two per channel (kernel rows 0-3, 4-7)
   extern __shared__ __attribute__((aligned(16))) unsigned char conv_img_raw[];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -2231,59 +2231,47 @@ __global__ __launch_bounds__(256, 1) void conv_u8_img_kernel(ConvImgArgs a) {
       issue(row_of(win, (it + 1) & 63), cur ^ 1);  // the next image's copy beside these MFMAs
     }
     const unsigned char* img = conv_img_raw + cur * ibuf;
-    // wave wv's tiles wv, wv + 4, ... two at a time: four independent accumulator chains (the
-    // three products of a K step on one accumulator are dependent) and both A fragments of a
-    // step read together; an odd last tile is paired with itself and stored once
-    const int ntw = (tiles - wv + 3) / 4;
-    for (int q = 0; q < ntw; q += 2) {
-      const int t0 = wv + 4 * q, t1 = q + 1 < ntw ? t0 + 4 : t0;
-      const int pa0 = 16 * t0 + fr, pa1 = 16 * t1 + fr;  // this lane's A rows (positions)
-      const int oy0 = pa0 / a.OW, ox0 = pa0 - oy0 * a.OW;
-      const int oy1 = pa1 / a.OW, ox1 = pa1 - oy1 * a.OW;
-      const unsigned char* r0 = img + kImgStride * (oy0 * a.W + ox0);
-      const unsigned char* r1 = img + kImgStride * (oy1 * a.W + ox1);
-      floatx4 acc[2][2] = {{{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}},
-                           {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}};
+    for (int tile = wv; tile < tiles; tile += 4) {
+      const int pa = 16 * tile + fr;  // this lane's A row: output position (oy, ox)
+      const int oy = pa / a.OW, ox = pa - oy * a.OW;
+      const unsigned char* r0 = img + kImgStride * (oy * a.W + ox);
+      floatx4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+      // taps 32 kt + 8 fc + e = channel kt / 2, kernel row 4 (kt % 2) + fc, column e; the next
+      // step's window row is read before this step's MFMAs
+      auto row_words = [&](int kt, uint32_t& w0, uint32_t& w1) {
+        const uint32_t* q = reinterpret_cast<const uint32_t*>(
+            r0 + ((kt >> 1) * a.H + 4 * (kt & 1) + fc) * a.W);
+        w0 = q[0];
+        w1 = q[1];
+      };
+      uint32_t u0, u1;
+      row_words(0, u0, u1);
 #pragma unroll
       for (int kt = 0; kt < KS; ++kt) {
-        // taps 32 kt + 8 fc + e = channel kt / 2, kernel row 4 (kt % 2) + fc, column e
-        const int c = kt >> 1, ky = 4 * (kt & 1) + fc;
-        const int off = (c * a.H + ky) * a.W;
-        const uint32_t* q0 = reinterpret_cast<const uint32_t*>(r0 + off);
-        const uint32_t* q1 = reinterpret_cast<const uint32_t*>(r1 + off);
-        const uint32_t u00 = q0[0], u01 = q0[1], u10 = q1[0], u11 = q1[1];
-        bf16x8 af[2];
-        af[0] = __builtin_bit_cast(bf16x8, u32x4{img_bf16x2(u00, 0), img_bf16x2(u00, 1),
-                                                 img_bf16x2(u01, 0), img_bf16x2(u01, 1)});
-        af[1] = __builtin_bit_cast(bf16x8, u32x4{img_bf16x2(u10, 0), img_bf16x2(u10, 1),
-                                                 img_bf16x2(u11, 0), img_bf16x2(u11, 1)});
-        // x6_mfma3<true>'s order per accumulator (b0, b2, b1), the four chains interleaved
-        constexpr int kOrd[3] = {0, 2, 1};
+        uint32_t n0 = 0, n1 = 0;
+        if (kt + 1 < KS) row_words(kt + 1, n0, n1);
+        const bf16x8 af = __builtin_bit_cast(
+            bf16x8, u32x4{img_bf16x2(u0, 0), img_bf16x2(u0, 1), img_bf16x2(u1, 0),
+                          img_bf16x2(u1, 1)});
 #pragma unroll
-        for (int o = 0; o < 3; ++o)
-#pragma unroll
-          for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bw[j][kt][kOrd[o]],
-                                                                  acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 2; ++j) {
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bw[j][kt][0], acc[j], 0, 0, 0);
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bw[j][kt][2], acc[j], 0, 0, 0);
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bw[j][kt][1], acc[j], 0, 0, 0);
+        }
+        u0 = n0;
+        u1 = n1;
       }
       // C/D layout: column fr of block j, rows 4 fc + r of the tile
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        if (i == 1 && t1 == t0) break;
-        const int tile = i == 0 ? t0 : t1;
+      for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            float v = acc[i][j][r] / a.cdiv;
-            if (a.bias) v += bias[j];
-            if (a.relu) v = relu_f(v);
-            a.out[(static_cast<int64_t>(b) * a.P + 16 * tile + 4 * fc + r) * kImgCO + 16 * j + fr] =
-                v;
-          }
-      }
+        for (int r = 0; r < 4; ++r) {
+          float v = acc[j][r] / a.cdiv;
+          if (a.bias) v += bias[j];
+          if (a.relu) v = relu_f(v);
+          a.out[(static_cast<int64_t>(b) * a.P + 16 * tile + 4 * fc + r) * kImgCO + 16 * j + fr] = v;
+        }
     }
   }
 }
@@ -2297,7 +2285,7 @@ static int conv_u8_img_grid(int B) {
       n = 256;
     cus = n;
   }
-  return B < cus ? B : cus;
+  return B < 2 * cus ? B : 2 * cus;
 }
 
 }  // namespace ocppo
