@@ -2157,8 +2157,11 @@ __device__ __forceinline__ uint32_t img_bf16x2(uint32_t v, int half) {
   return __builtin_amdgcn_perm(__float_as_uint(f1), __float_as_uint(f0), 0x07060302u);
 }
 
-template <int C>
-__global__ __launch_bounds__(256, 2) void conv_u8_img_kernel(ConvImgArgs a) {
+// NW waves per workgroup: 4 (two workgroups per CU: one's image copy beside the other's MFMAs)
+// for minibatch-sized batches, 8 for a batch of at most one image per CU (the rollout: the
+// image's 25 row tiles over twice the waves)
+template <int C, int NW>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void conv_u8_img_kernel(ConvImgArgs a) {
   constexpr int KS = 2 * C;  // K steps of 32 taps: two per channel (kernel rows 0-3, 4-7)
   extern __shared__ __attribute__((aligned(16))) unsigned char conv_img_raw[];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -2169,7 +2172,7 @@ __global__ __launch_bounds__(256, 2) void conv_u8_img_kernel(ConvImgArgs a) {
   // one image's bytes -> buffer `buf`: wave wv copies chunks wv, wv + 4, ... (lane-linear 16 B)
   auto issue = [&](int64_t row, int buf) {
     const uint8_t* s = a.src + row * bytes;
-    for (int ch = wv; ch < nchunks; ch += 4) {
+    for (int ch = wv; ch < nchunks; ch += NW) {
       const int64_t off = static_cast<int64_t>(ch) * kImgChunk + 16 * lane;
       if (off < bytes)
         __builtin_amdgcn_global_load_lds(
@@ -2231,7 +2234,7 @@ __global__ __launch_bounds__(256, 2) void conv_u8_img_kernel(ConvImgArgs a) {
       issue(row_of(win, (it + 1) & 63), cur ^ 1);  // the next image's copy beside these MFMAs
     }
     const unsigned char* img = conv_img_raw + cur * ibuf;
-    for (int tile = wv; tile < tiles; tile += 4) {
+    for (int tile = wv; tile < tiles; tile += NW) {
       const int pa = 16 * tile + fr;  // this lane's A row: output position (oy, ox)
       const int oy = pa / a.OW, ox = pa - oy * a.OW;
       const unsigned char* r0 = img + kImgStride * (oy * a.W + ox);
@@ -2455,8 +2458,13 @@ extern "C" int ocppo_conv_x6_u8(ocppo_stream_t stream, int mode, const uint8_t* 
                    divisor};
     clear_stale_error();
     const size_t ibuf = static_cast<size_t>((bytes + kImgChunk - 1) / kImgChunk) * kImgChunk;
-    hipLaunchKernelGGL(conv_u8_img_kernel<4>, dim3(conv_u8_img_grid(ia.B)), dim3(256), 2 * ibuf,
-                       as_stream(stream), ia);
+    const int grid = conv_u8_img_grid(ia.B);
+    if (grid <= conv_u8_img_grid(1 << 30) / 2)  // at most one image per CU: 8 waves each
+      hipLaunchKernelGGL((conv_u8_img_kernel<4, 8>), dim3(grid), dim3(512), 2 * ibuf,
+                         as_stream(stream), ia);
+    else
+      hipLaunchKernelGGL((conv_u8_img_kernel<4, 4>), dim3(grid), dim3(256), 2 * ibuf,
+                         as_stream(stream), ia);
     return check_launch("ocppo_conv_x6_u8 (image-staged)");
   }
   const X6Tile tc = kConvTiles[tile >= 0 && tile < 7 ? tile : 0];
