@@ -899,6 +899,58 @@ def linear_act_nhwc(x, lin: nn.Linear, relu: bool):
     return linear_act(x.permute(0, 2, 3, 1).reshape(B, H * W * C), lin, relu, (C, H, W))
 
 
+# Inference (the rollout) through nn.Flatten -> nn.Linear on a channels_last activation (the
+# NatureCNN's last convolution at 256 envs): the Linear reads the activation in its memory order
+# with the weight's columns permuted to match, instead of nn.Flatten's NCHW-order copy of the
+# activation every step (3.2 MB, one ~6 us launch per step). The permuted weight is made once per
+# rollout, inside rollout_inference() only (the trainer's rollout: the parameters cannot change
+# within it; entering it marks the cache stale, and the copy rides in the first step, captured
+# with the rollout graph), and reused by the other steps.
+FLAT_NHWC_INFER = True
+_NHWC_INFER: dict = {}
+_WEIGHTS_GEN = [0]
+_IN_ROLLOUT = [False]
+
+
+class rollout_inference:
+    """Context of one rollout (trainer._rollout): the parameters are fixed inside it, so the
+    inference caches (linear_act_nhwc_infer's permuted weight) are valid; refreshed on entry."""
+
+    def __enter__(self):
+        _WEIGHTS_GEN[0] += 1
+        _IN_ROLLOUT[0] = True
+
+    def __exit__(self, *exc):
+        _IN_ROLLOUT[0] = False
+
+
+def _flat_nhwc_infer_ok(x, flat, lin) -> bool:
+    return (FLAT_NHWC_INFER and _IN_ROLLOUT[0] and not torch.is_grad_enabled()
+            and isinstance(flat, nn.Flatten)
+            and isinstance(lin, nn.Linear) and lin.bias is not None and x.is_cuda
+            and x.dtype == torch.float32 and x.dim() == 4 and flat.start_dim == 1
+            and flat.end_dim in (-1, 3) and x.is_contiguous(memory_format=torch.channels_last)
+            and not x.is_contiguous() and lin.in_features == x[0].numel())
+
+
+def linear_act_nhwc_infer(x, lin: nn.Linear, relu: bool):
+    """act(lin(flatten(x))) without autograd for a channels_last x, reading x in its memory order
+    against a cached column-permuted weight (same products, columns visited in (H, W, C) order)."""
+    B, C, H, W = x.shape
+    key = id(lin)
+    ent = _NHWC_INFER.get(key)
+    if ent is None or ent[0] is not lin.weight:
+        ent = [lin.weight, torch.empty_like(lin.weight), -1]
+        _NHWC_INFER[key] = ent
+    if ent[2] != _WEIGHTS_GEN[0]:
+        ent[1].copy_(_cols_to_nhwc(lin.weight, (C, H, W)))
+        ent[2] = _WEIGHTS_GEN[0]
+    x2 = x.permute(0, 2, 3, 1).reshape(B, H * W * C)
+    if relu:
+        return torch._addmm_activation(lin.bias, x2, ent[1].t(), use_gelu=False)
+    return torch.addmm(lin.bias, x2, ent[1].t())
+
+
 def linear_relu(x, lin: nn.Linear, rows: bool = False):
     return linear_act(x, lin, True, rows=rows)
 
@@ -963,6 +1015,10 @@ def fused_trunk(seq: nn.Sequential, x, rows_last: bool = False):
         elif i + 1 < len(mods) and _flat_nhwc_ok(x, m, mods[i + 1]):
             relu = i + 2 < len(mods) and isinstance(mods[i + 2], nn.ReLU)
             x = linear_act_nhwc(x, mods[i + 1], relu)
+            i += 3 if relu else 2
+        elif i + 1 < len(mods) and _flat_nhwc_infer_ok(x, m, mods[i + 1]):
+            relu = i + 2 < len(mods) and isinstance(mods[i + 2], nn.ReLU)
+            x = linear_act_nhwc_infer(x, mods[i + 1], relu)
             i += 3 if relu else 2
         elif fusable and i + 1 < len(mods) and isinstance(mods[i + 1], nn.ReLU):
             x = linear_relu(x, m, rows=rows_last and i + 2 == len(mods))

@@ -728,7 +728,7 @@ class PPOTrainer:
 
     def _rollout(self):
         """Rollout (:500-530) + bootstrap + GAE (:533-547) + minibatch adv stats (:577-579)."""
-        with torch.no_grad():
+        with torch.no_grad(), agents.rollout_inference():
             self._rollout_begin()
             for t in range(self.T):
                 self._rollout_step(t)

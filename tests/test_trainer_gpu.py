@@ -858,3 +858,30 @@ def test_pixel_rollout_reads_the_u8_stacks(dev):
     a0, v0 = run(False)
     assert float((v1 - v0).abs().max()) <= 1e-4 * float(v0.abs().max() + 1)
     assert float((a1 == a0).float().mean()) >= 0.99
+
+
+def test_rollout_flatten_linear_reads_the_nhwc_activation(dev):
+    """agents.linear_act_nhwc_infer (inside agents.rollout_inference, the trainer's rollout): the
+    NatureCNN's Flatten -> Linear on the channels_last activation against a cached column-permuted
+    weight, no flatten copy -- the same hidden state as the plain no-grad trunk up to the f32
+    summation order, and the cache refreshed when a new rollout begins after the weights change."""
+    from oc_cleanrl_amd import agents
+    from oc_cleanrl_amd.agents import make_agent
+
+    torch.manual_seed(0)
+    ag = make_agent("PPO", (4, 84, 84), 4, dev).to(dev).to(memory_format=torch.channels_last)
+    x = torch.randint(0, 256, (256, 4, 84, 84), device=dev).float().contiguous(
+        memory_format=torch.channels_last)
+    with torch.no_grad():
+        ref = ag.trunk(x)
+        with agents.rollout_inference():
+            got = ag.trunk(x)
+            assert any(k == id(m) for k in agents._NHWC_INFER for m in ag.network)
+        torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-5)
+        lin = [m for m in ag.network if isinstance(m, torch.nn.Linear)][0]
+        lin.weight.mul_(0.5)  # an update between rollouts (in place, as FlatAdam's)
+        ref2 = ag.trunk(x)
+        with agents.rollout_inference():
+            got2 = ag.trunk(x)
+        torch.testing.assert_close(got2, ref2, rtol=1e-5, atol=1e-5)
+        assert not torch.allclose(ref2, ref)
