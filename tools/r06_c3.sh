@@ -11,3 +11,4 @@ for p in 1 2; do
   timeout -k 10 300 python3 tools/ab_toggle.py ops.CONV_U8_IMG 0 $Q > gpurun_out/c3/off_$p.json 2> gpurun_out/c3/off_$p.err
 done
 bash tools/prof_c3.sh r06a > /dev/null 2>&1
+timeout -k 10 300 python3 -u -m pytest -x -q --timeout 200 --timeout-method thread -p no:cacheprovider "tests/test_trainer_gpu.py::test_rollout_flatten_linear_reads_the_nhwc_activation" > gpurun_out/c3/tests2.log 2>&1
