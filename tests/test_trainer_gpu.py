@@ -168,7 +168,9 @@ def test_fused_trunk_matches_module_forward_and_grads(dev, arch, obs):
     x = torch.randint(0, 160, (32,) + obs, device=dev).float()
     h1 = ag.network(x)
     h2 = ag.trunk(x)
-    torch.testing.assert_close(h2, h1, rtol=1e-6, atol=1e-6)
+    # the trunk's autograd forwards of <= 128 rows run on the HIP Linear kernel (agents.SMALL_FWD:
+    # an f32 FMA chain in another summation order than hipBLASLt's), so f32-level agreement
+    torch.testing.assert_close(h2, h1, rtol=1e-5, atol=2e-6 * float(h1.abs().max()))
     g = torch.randn_like(h1)
     gr1 = torch.autograd.grad(h1, list(ag.network.parameters()), g)
     gr2 = torch.autograd.grad(h2, list(ag.network.parameters()), g)
