@@ -516,6 +516,10 @@ OCPPO_API int ocppo_conv_x6(ocppo_stream_t stream, int mode, const float* x, con
  * tile 7 (mode 0, ABI 25): each image's stack staged in LDS once, bitwise tile 0's output; needs
  * C = 4, 8 x 8 taps, stride 4, N = 32, 16 | OH OW, src 16-B aligned, 16 | C H W, 2 C H W <= 64 KB
  * (NatureCNN's first layer on 4 x 84 x 84 stacks); M a whole number of images, splits 1.
+ * tile 8 (mode 1, ABI 25): the weight gradient with each image's stack staged in LDS once; needs
+ * 4 x 84 x 84 stacks, 8 x 8 taps, stride 4, M = 32, K a whole number of images, a 16-B aligned
+ * src; runs splits / 4 workgroups, each writing 4 partials into c [splits, M, N] (summed in
+ * order in f64 and divided once, as the tile loop's); not the tile loop's summation order.
  * ------------------------------------------------------------------------------------------- */
 OCPPO_API int ocppo_conv_x6_u8(ocppo_stream_t stream, int mode, const uint8_t* src,
                                const int64_t* idx, int64_t C, int64_t H, int64_t W, int64_t KH,

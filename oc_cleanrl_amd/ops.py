@@ -1036,10 +1036,31 @@ def conv_x6_u8(src, idx, weight, bias=None, stride: int = 4, relu: bool = True,
     return out
 
 
+# ... and its weight gradient (ocppo_conv_x6_u8 tile 8, conv_u8_wgrad_img_kernel: each image's
+# stack in LDS once, rewritten per channel as tap-column rows; 4 partials per workgroup summed in
+# order) for NatureCNN's first layer on 4 x 84 x 84 stacks
+CONV_U8_IMG_WGRAD = True
+_CUS: dict = {}
+
+
+def _cus(dev) -> int:
+    if str(dev) not in _CUS:
+        _CUS[str(dev)] = torch.cuda.get_device_properties(dev).multi_processor_count
+    return _CUS[str(dev)]
+
+
+def _conv_u8_img_wgrad_ok(src, kernel, stride: int, Cout: int) -> bool:
+    _, C, H, W = src.shape
+    return (CONV_U8_IMG_WGRAD and C == 4 and H == 84 and W == 84 and tuple(kernel) == (8, 8) and
+            stride == 4 and Cout == 32 and src.data_ptr() % 16 == 0)
+
+
 def conv_x6_u8_wgrad(gp, src, idx, kernel: tuple, stride: int = 4, divisor: float = 255.0,
-                     out=None):
+                     out=None, tile: int | None = None):
     """dW [Cout, C KH KW] (nn.Conv2d's tap order) of conv_x6_u8: sum over the output pixels r of
-    gp[r, co] src[idx[b], c, s oy + ky, s ox + kx] / divisor; split partials summed in order."""
+    gp[r, co] src[idx[b], c, s oy + ky, s ox + kx] / divisor; split partials summed in order.
+    tile: None = the image-staged kernel where it applies (CONV_U8_IMG_WGRAD), else the tile
+    loop's; an explicit ocppo_conv_x6_u8 tile forces that form (tests)."""
     B = idx.numel()
     _, C, H, W = src.shape
     KH, KW = kernel
@@ -1048,7 +1069,25 @@ def conv_x6_u8_wgrad(gp, src, idx, kernel: tuple, stride: int = 4, divisor: floa
     rows, Cout = gp.shape
     dev, f = src.device, torch.float32
     N = C * KH * KW
-    tile = _conv_u8_tile(Cout, N, 1)
+    if tile is None and _conv_u8_img_wgrad_ok(src, kernel, s, Cout):
+        tile = 8
+    if tile == 8:
+        if rows != B * OH * OW:
+            raise ValueError("conv_x6_u8_wgrad: gp must be [B OH OW, Cout]")
+        S = 4 * min(_cus(dev), B)  # 4 wave partials per workgroup, <= one workgroup per image
+        key = ("wgrad_img", str(dev), S, Cout, N)
+        if key not in _CONV_PARTS:
+            _CONV_PARTS[key] = torch.empty((S, Cout, N), dtype=f, device=dev)
+        part = _CONV_PARTS[key]
+        if out is None:
+            out = torch.empty((Cout, N), dtype=f, device=dev)
+        _bounds(dev, u8=src)
+        call("ocppo_conv_x6_u8", _stream(dev), 1, src.data_ptr(),
+             _check(idx, "idx", torch.int64, dev, B), C, H, W, KH, KW, s,
+             _check(gp, "gp", f, dev), Cout, part.data_ptr(), Cout, N, rows, S, None, 0,
+             float(divisor), 8, _check(out, "out", f, dev, Cout * N))
+        return out
+    tile = _conv_u8_tile(Cout, N, 1) if tile is None else tile
     if rows != B * OH * OW or tile is None or rows % 32:
         raise ValueError("conv_x6_u8_wgrad: gp must be [B OH OW, Cout] with a tile for it")
     bm, bn = _CONV_TILES[tile]

@@ -254,3 +254,29 @@ def test_u8_first_conv_image_staged_is_bitwise_the_tile_loop(relu, B):
     loop = ops.conv_x6_u8(src, idx, w, b, s, relu, tile=0)
     assert torch.equal(staged, loop), float((staged - loop).abs().max())
     assert torch.equal(staged, ops.conv_x6_u8(src, idx, w, b, s, relu))  # the default routes to 7
+
+
+@pytest.mark.parametrize("B", [16, 300])
+def test_u8_first_conv_image_staged_weight_gradient(B):
+    """ocppo_conv_x6_u8 tile 8 (each image's stack in LDS once, rewritten per channel as
+    tap-column rows; K taken image by image, 4 wave partials per workgroup summed in order)
+    against a float64 weight gradient, next to the tile loop (tile 1), and bitwise repeatable.
+    B = 300 puts several images on some workgroups (one workgroup per CU at most)."""
+    src = _frames(R=B + 5, seed=18)
+    _, w, _, s = _operands("conv1", 19)
+    idx = torch.randperm(src.shape[0], device=DEV)[:B]
+    g = torch.Generator(device=DEV).manual_seed(20)
+    gp = (torch.rand(B, 32, 20, 20, device=DEV, generator=g) * 2 - 1).contiguous(memory_format=CL)
+    rows = gp.permute(0, 2, 3, 1).reshape(-1, 32)
+    assert ops._conv_u8_img_wgrad_ok(src, (8, 8), s, 32)
+    dw = ops.conv_x6_u8_wgrad(rows, src, idx, (8, 8), s, tile=8).view(w.shape)
+    loop = ops.conv_x6_u8_wgrad(rows, src, idx, (8, 8), s, tile=1).view(w.shape)
+    x = src[idx].float() / 255.0
+    x64, gp64 = x.double().cpu(), gp.double().cpu()
+    ref = torch.nn.grad.conv2d_weight(x64, w.shape, gp64, stride=s)
+    scale = torch.nn.grad.conv2d_weight(x64.abs(), w.shape, gp64.abs(), stride=s)
+    lib = torch.nn.grad.conv2d_weight(x.contiguous(memory_format=CL), w.shape, gp, stride=s)
+    _check(dw, ref, scale, lib)
+    _check(loop, ref, scale, lib)
+    assert torch.equal(dw, ops.conv_x6_u8_wgrad(rows, src, idx, (8, 8), s, tile=8).view(w.shape))
+    assert torch.equal(dw, ops.conv_x6_u8_wgrad(rows, src, idx, (8, 8), s).view(w.shape))
