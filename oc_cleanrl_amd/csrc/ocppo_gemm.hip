@@ -2283,11 +2283,12 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_u8_img_kernel(ConvImgArg
 // mode 1, tile 8): dW[co, tap] = sum over images b and positions p of gp[b, p, co] u_b(p, tap) /
 // divisor. The tile loop (GATH 6) walks the K = B OH OW rows through 32-row steps and gathers
 // every window byte from L2; here K is taken image by image: a workgroup copies image b's u8
-// stack into LDS (LDS-DMA, double-buffered as in the forward), then per channel rewrites it as 8
-// tap-column rows T[kx][y][ox] = img[c][y][4 ox + kx] (ox padded to 24 with zeros), so that the
-// 8 positions a lane feeds one MFMA for a fixed tap are 16 contiguous bytes; the kx and kx + 4
-// rows come from the same dwords (one window byte per phase q = kx % 4), so a channel is 9 dword
-// reads and 64 byte conversions per thread. K steps of 32 positions (rows of 24, so a lane's 8
+// stack's bytes into registers one image ahead (each thread the 9 dwords of one row segment per
+// channel), then per channel writes them to LDS as 8 tap-column rows T[kx][y][ox] = img[c][y][4 ox
+// + kx] (ox padded to 24 with zeros), so that the 8 positions a lane feeds one MFMA for a fixed
+// tap are 16 contiguous bytes; the kx and kx + 4 rows come from the same dwords (one window byte
+// per phase q = kx % 4): 64 byte conversions per thread and channel. (An LDS-DMA copy of the raw
+// image, as in the forward, made the compiler drain it before every T write.) K steps of 32 positions (rows of 24, so a lane's 8
 // never cross an output row; 15 steps for a 20 x 20 output) are dealt to the 4 waves; a wave
 // keeps the partial dW of its K steps for all 256 taps x 32 channels (32 accumulator blocks) over
 // all its workgroup's images, and the gradient rows of its K steps in registers (split into the
@@ -2313,134 +2314,120 @@ __global__ __launch_bounds__(256, 1) void conv_u8_wgrad_img_kernel(ConvWgImgArgs
   static_assert(OW <= kWgRow && (OH * kWgRow) % 32 == 0 && W % 4 == 0, "geometry");
   constexpr int P = OH * OW, KS = OH * kWgRow / 32, KSW = (KS + 3) / 4;  // K steps, per wave
   constexpr int64_t bytes = static_cast<int64_t>(C) * H * W;
-  constexpr int nchunks = static_cast<int>((bytes + kImgChunk - 1) / kImgChunk);
-  constexpr int64_t ibuf = static_cast<int64_t>(nchunks) * kImgChunk;
+  constexpr int kItems = H * (kWgRow / 8);  // T rows x 8-position groups per channel
+  static_assert(kItems <= 256, "one T item per thread and channel");
   constexpr int kTRow = kWgRow * 2;  // bytes per T row
-  extern __shared__ __attribute__((aligned(16))) unsigned char conv_wg_raw[];
-  uint16_t* T = reinterpret_cast<uint16_t*>(conv_wg_raw + 2 * ibuf);  // [8][H][24] bf16
+  constexpr int kTChan = 8 * H * kTRow;  // bytes per channel
+  // [c][kx][y][24] bf16: every channel of the image at once (129 KB of the CU's 160)
+  __shared__ __attribute__((aligned(16))) uint16_t T[C * 8 * H * kWgRow];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int fr = lane & 15, fc = lane >> 4;
-  auto issue = [&](int64_t row, int buf) {
-    const uint8_t* sp = a.src + row * bytes;
-    for (int ch = wv; ch < nchunks; ch += 4) {
-      const int64_t off = static_cast<int64_t>(ch) * kImgChunk + 16 * lane;
-      if (off < bytes)
-        __builtin_amdgcn_global_load_lds(
-            reinterpret_cast<const void*>(sp + off),
-            (__attribute__((address_space(3))) void*)(conv_wg_raw + buf * ibuf +
-                                                      static_cast<int64_t>(ch) * kImgChunk),
-            16, 0, 0);
-    }
-  };
+  const int iy = t / (kWgRow / 8), ig = t - iy * (kWgRow / 8);  // this thread's T item
   const int grid = static_cast<int>(gridDim.x);
-  int b = blockIdx.x;
-  auto window = [&](int it0) -> int64_t {
-    const int bb = b + (it0 + lane) * grid;
-    return bb < a.B ? a.idx[bb] : 0;
+  // image bb's window dwords of this thread's item: raw[c][i] = dword i of row iy of channel c
+  // from column 4 (8 ig + i) (phase q of it = img[c][iy][4 (8 ig + i) + q])
+  uint32_t raw[C][9];
+  auto load_raw = [&](int bb) {
+    const bool ok = bb < a.B && t < kItems;
+    const int64_t row = bb < a.B ? a.idx[bb] : 0;
+    const uint8_t* sp = a.src + row * bytes + iy * W;
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int i = 0; i < 9; ++i) {
+        const int col = 4 * (8 * ig + i);
+        raw[c][i] = (ok && col + 4 <= W)
+                        ? *reinterpret_cast<const uint32_t*>(sp + c * H * W + col)
+                        : 0u;
+      }
   };
-  auto row_of = [&](int64_t win, int l) -> int64_t {
-    const uint64_t u = static_cast<uint64_t>(win);
-    const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(u), l);
-    const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(u >> 32), l);
-    return static_cast<int64_t>((static_cast<uint64_t>(hi) << 32) | lo);
+  // the gradient rows of this wave's K step q: gr[q][j][e] = position k = 32 ks + 8 fc + e of
+  // output channel 16 j + fr (zero in the row padding)
+  float gr[KSW][2][8];
+  auto load_g = [&](int bb, int q) {
+    const int ks = wv + 4 * q;
+    const int k0 = 32 * ks + 8 * fc, oy = k0 / kWgRow, ox0 = k0 - oy * kWgRow;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const bool ok = bb < a.B && ks < KS && ox0 + e < OW;
+        gr[q][j][e] =
+            ok ? a.gp[(static_cast<int64_t>(bb) * P + oy * OW + ox0 + e) * a.ldg + 16 * j + fr]
+               : 0.f;
+      }
   };
   floatx4 acc[C * 4][2];  // tap block (c, 16-tap group) x channel block
 #pragma unroll
   for (int i = 0; i < C * 4; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-  int64_t win = 0;
-  if (b < a.B) {
-    win = window(0);
-    issue(row_of(win, 0), 0);
-  }
-  for (int it = 0; b < a.B; b += grid, ++it) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // image b in LDS; the other buffer's and T's readers done
-    const int cur = it & 1;
-    if (b + grid < a.B) {
-      if (((it + 1) & 63) == 0) win = window(it + 1);
-      issue(row_of(win, (it + 1) & 63), cur ^ 1);
-    }
-    const unsigned char* img = conv_wg_raw + cur * ibuf;
-    // the gradient rows of this wave's K steps, as the three bf16 pieces: gf[s][j][pl] = 8
-    // positions k = 32 ks + 8 fc + e of output channel 16 j + fr (zero in the row padding)
-    bf16x8 gf[KSW][2][3];
+  // every register set is refilled for the next image as soon as this image has consumed it, so
+  // the loads run beside the rest of this image's work
+  int b = blockIdx.x;
+  load_raw(b);
 #pragma unroll
-    for (int q = 0; q < KSW; ++q) {
-      const int ks = wv + 4 * q;
-      const int k0 = 32 * ks + 8 * fc, oy = k0 / kWgRow, ox0 = k0 - oy * kWgRow;
+  for (int q = 0; q < KSW; ++q) load_g(b, q);
+  for (; b < a.B; b += grid) {
+    __syncthreads();  // the previous image's T readers done
+    if (t < kItems) {
+      // T[c][kx][iy][8 ig + e] = img[c][iy][4 (8 ig + e) + kx] = phase kx % 4 of dword e + kx / 4
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        float v[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const bool ok = ks < KS && ox0 + e < OW;
-          v[e] = ok ? a.gp[(static_cast<int64_t>(b) * P + oy * OW + ox0 + e) * a.ldg + 16 * j + fr]
-                    : 0.f;
-        }
-        uint32_t pc[4][3];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) x6_split2(x6f2{v[2 * e], v[2 * e + 1]}, pc[e][0], pc[e][1], pc[e][2]);
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl)
-          gf[q][j][pl] = __builtin_bit_cast(bf16x8, u32x4{pc[0][pl], pc[1][pl], pc[2][pl], pc[3][pl]});
-      }
-    }
-#pragma unroll
-    for (int c = 0; c < C; ++c) {
-      if (c > 0) __syncthreads();  // the previous channel's T readers done
-      // T[kx][y][ox] for ox in [8 g, 8 g + 8): thread item (y, g) reads the 9 dwords of window
-      // columns 4 (8 g + i) + [0, 4), i = 0..8 (phase q of dword i = img[y][4 (8 g + i) + q])
-      for (int item = t; item < H * (kWgRow / 8); item += 256) {
-        const int y = item / (kWgRow / 8), g = item - y * (kWgRow / 8);
-        const unsigned char* rowp = img + (c * H + y) * W;
-        uint32_t d[9];
-#pragma unroll
-        for (int i = 0; i < 9; ++i) {
-          const int col = 4 * (8 * g + i);
-          d[i] = col + 4 <= W ? *reinterpret_cast<const uint32_t*>(rowp + col) : 0u;
-        }
+      for (int c = 0; c < C; ++c)
 #pragma unroll
         for (int kx = 0; kx < 8; ++kx) {
           const int q = kx & 3, m = kx >> 2;
           uint32_t o[4];
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const int i0 = 2 * e + m, i1 = 2 * e + 1 + m;
-            const bool ok0 = 8 * g + 2 * e < OW, ok1 = 8 * g + 2 * e + 1 < OW;
-            const float f0 = ok0 ? static_cast<float>((d[i0] >> (8 * q)) & 0xffu) : 0.f;
-            const float f1 = ok1 ? static_cast<float>((d[i1] >> (8 * q)) & 0xffu) : 0.f;
+            const bool ok0 = 8 * ig + 2 * e < OW, ok1 = 8 * ig + 2 * e + 1 < OW;
+            const float f0 = ok0 ? static_cast<float>((raw[c][2 * e + m] >> (8 * q)) & 0xffu) : 0.f;
+            const float f1 =
+                ok1 ? static_cast<float>((raw[c][2 * e + 1 + m] >> (8 * q)) & 0xffu) : 0.f;
             o[e] = __builtin_amdgcn_perm(__float_as_uint(f1), __float_as_uint(f0), 0x07060302u);
           }
-          *reinterpret_cast<uint4*>(reinterpret_cast<unsigned char*>(T) +
-                                    (kx * H + y) * kTRow + 16 * g) = uint4{o[0], o[1], o[2], o[3]};
+          *reinterpret_cast<uint4*>(reinterpret_cast<unsigned char*>(T) + c * kTChan +
+                                    (kx * H + iy) * kTRow + 16 * ig) = uint4{o[0], o[1], o[2], o[3]};
         }
-      }
-      __syncthreads();
-      // this wave's K steps x channel c's 64 taps (4 blocks of 16: tap = 16 tb + fr -> ky =
-      // 2 tb + fr / 8, kx = fr % 8)
+    }
+    load_raw(b + grid);  // the next image's bytes, in flight during this image's MFMAs
+    __syncthreads();
+    // this wave's K steps x all 256 taps (channel c's 4 blocks of 16: tap = 16 tb + fr -> ky =
+    // 2 tb + fr / 8, kx = fr % 8)
 #pragma unroll
-      for (int q = 0; q < KSW; ++q) {
-        const int ks = wv + 4 * q;
-        if (ks >= KS) break;  // wave-uniform
-        const int k0 = 32 * ks + 8 * fc, oy = k0 / kWgRow, ox0 = k0 - oy * kWgRow;
+    for (int q = 0; q < KSW; ++q) {
+      const int ks = wv + 4 * q;
+      if (ks >= KS) break;  // wave-uniform
+      bf16x8 gf[2][3];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        uint32_t pc[4][3];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          x6_split2(x6f2{gr[q][j][2 * e], gr[q][j][2 * e + 1]}, pc[e][0], pc[e][1], pc[e][2]);
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+          gf[j][pl] = __builtin_bit_cast(bf16x8, u32x4{pc[0][pl], pc[1][pl], pc[2][pl], pc[3][pl]});
+      }
+      load_g(b + grid, q);  // the next image's rows of this step
+      const int k0 = 32 * ks + 8 * fc, oy = k0 / kWgRow, ox0 = k0 - oy * kWgRow;
+#pragma unroll
+      for (int c = 0; c < C; ++c)
 #pragma unroll
         for (int tb = 0; tb < 4; ++tb) {
           const int ky = 2 * tb + (fr >> 3), kx = fr & 7;
           const uint4 tv = *reinterpret_cast<const uint4*>(
-              reinterpret_cast<const unsigned char*>(T) + (kx * H + kImgStride * oy + ky) * kTRow +
-              2 * ox0);
+              reinterpret_cast<const unsigned char*>(T) + c * kTChan +
+              (kx * H + kImgStride * oy + ky) * kTRow + 2 * ox0);
           const bf16x8 af = __builtin_bit_cast(bf16x8, u32x4{tv.x, tv.y, tv.z, tv.w});
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
             floatx4& ac = acc[4 * c + tb][j];
-            ac = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, gf[q][j][0], ac, 0, 0, 0);
-            ac = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, gf[q][j][2], ac, 0, 0, 0);
-            ac = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, gf[q][j][1], ac, 0, 0, 0);
+            ac = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, gf[j][0], ac, 0, 0, 0);
+            ac = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, gf[j][2], ac, 0, 0, 0);
+            ac = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, gf[j][1], ac, 0, 0, 0);
           }
         }
-      }
     }
   }
   // this wave's partial, transposed to [co][tap]: block (i, j) element (tap 16 i + 4 fc + r,
@@ -2657,21 +2644,10 @@ extern "C" int ocppo_conv_x6_u8(ocppo_stream_t stream, int mode, const uint8_t* 
                   (long long)C, (long long)H, (long long)W, (long long)M, (long long)K,
                   (long long)splits);
     ConvWgImgArgs wa{src, idx, w, ldw, c, static_cast<int>(K / P)};
-    const int64_t ibuf = (bytes + kImgChunk - 1) / kImgChunk * kImgChunk;
-    const size_t lds = static_cast<size_t>(2 * ibuf + 8 * kH * kWgRow * 2);
-    static bool lds_set = false;  // > 64 KB of dynamic LDS needs the attribute (once)
-    if (!lds_set) {
-      OCPPO_REQUIRE(hipFuncSetAttribute(
-                        reinterpret_cast<const void*>(&conv_u8_wgrad_img_kernel<4, 84, 84, 20, 20>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize,
-                        static_cast<int>(lds)) == hipSuccess,
-                    "ocppo_conv_x6_u8: tile 8 needs %zu bytes of LDS", lds);
-      lds_set = true;
-    }
     clear_stale_error();
     hipStream_t s = as_stream(stream);
     hipLaunchKernelGGL((conv_u8_wgrad_img_kernel<4, 84, 84, 20, 20>),
-                       dim3(static_cast<unsigned>(splits / 4)), dim3(256), lds, s, wa);
+                       dim3(static_cast<unsigned>(splits / 4)), dim3(256), 0, s, wa);
     if (int rc = check_launch("ocppo_conv_x6_u8 (image-staged weight gradient)")) return rc;
     const int64_t n = M * N;
     hipLaunchKernelGGL(sum_parts_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64 * kSumGroups), 0,
