@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define OCPPO_ABI_VERSION 25
+#define OCPPO_ABI_VERSION 26
 
 /* status codes */
 #define OCPPO_OK 0
@@ -520,12 +520,19 @@ OCPPO_API int ocppo_conv_x6(ocppo_stream_t stream, int mode, const float* x, con
  * 4 x 84 x 84 stacks, 8 x 8 taps, stride 4, M = 32, K a whole number of images, a 16-B aligned
  * src; runs splits / 4 workgroups, each writing 4 partials into c [splits, M, N] (summed in
  * order in f64 and divided once, as the tile loop's); not the tile loop's summation order.
+ * mbits (ABI 26, tiles 7 and 8 only, else null; 16-B aligned u32 [M] / [K]): tile 7 (with relu)
+ * writes the output's ReLU mask, bit n of word r = c[r, n] > 0; tile 8 reads it and takes w as
+ * the UNMASKED output gradient, zeroing it where the bit is clear (relu_bias_grad's ReLU
+ * backward, ppo_atari_oc.py:603's loss.backward through nn.ReLU; the same products as on the
+ * masked gradient). dbp / db (tile 8, both or neither): dbp workspace [splits, 32], db [32] the
+ * (masked) gradient's per-channel sums = the layer's bias gradient (summed in order in f64).
  * ------------------------------------------------------------------------------------------- */
 OCPPO_API int ocppo_conv_x6_u8(ocppo_stream_t stream, int mode, const uint8_t* src,
                                const int64_t* idx, int64_t C, int64_t H, int64_t W, int64_t KH,
                                int64_t KW, int64_t stride, const float* w, int64_t ldw, float* c,
                                int64_t M, int64_t N, int64_t K, int64_t splits, const float* bias,
-                               int relu, float divisor, int tile, float* out);
+                               int relu, float divisor, int tile, float* out, uint32_t* mbits,
+                               float* dbp, float* db);
 
 /* ---------------------------------------------------------------------------------------------
  * The exact three-piece bf16 split ocppo_gemm_x6 forms in its K loop, done once per matrix: the

@@ -712,15 +712,26 @@ class _ConvX6U8(torch.autograd.Function):
     """The first convolution (+ ReLU) of the update's minibatch forward read straight from the
     rollout's u8 frame stacks through the minibatch indices (ops.conv_x6_u8: NormalizeImg's / 255
     in the epilogue; no f32 minibatch copy of the observations, ppo_atari_oc.py:566); backward:
-    relu_bias_grad, then the weight gradient from the same u8 rows (the input needs none)."""
+    relu_bias_grad, then the weight gradient from the same u8 rows (the input needs none).
+    Under U8_WGRAD_RELU the forward also leaves the ReLU's bitmask and the backward hands the
+    unmasked gradient to the weight-gradient kernel, which applies the ReLU backward and sums the
+    bias gradient itself (ops.conv_x6_u8_wgrad mbits / db): no relu_bias_grad pass."""
 
     @staticmethod
     def forward(ctx, w, b, frames, idx, stride, relu: bool, divisor: float, box=None):
+        mb = None
+        if (U8_WGRAD_RELU and relu and box is None and ctx.needs_input_grad[0] and
+                ops._conv_u8_img_ok(frames, w, stride) and
+                ops._conv_u8_img_wgrad_ok(frames, tuple(w.shape[2:]), stride, w.shape[0])):
+            P = ((frames.shape[2] - w.shape[2]) // stride + 1) * \
+                ((frames.shape[3] - w.shape[3]) // stride + 1)
+            mb = torch.empty(idx.numel() * P, dtype=torch.int32, device=frames.device)
         y = ops.timed(f"conv_x6_u8_{idx.numel()}",
-                      lambda: ops.conv_x6_u8(frames, idx, w, b, stride, relu, divisor))
+                      lambda: ops.conv_x6_u8(frames, idx, w, b, stride, relu, divisor, mbits=mb))
         ctx.conv = (stride, relu, divisor)
         ctx.b = b
         ctx.box = box
+        ctx.mb = mb
         ctx.save_for_backward(w, frames, idx, y if relu else None)
         return y
 
@@ -732,6 +743,20 @@ class _ConvX6U8(torch.autograd.Function):
         C = g.shape[1]
         g2 = g.permute(0, 2, 3, 1).reshape(-1, C)
         b = ctx.b
+        mb, ctx.mb = ctx.mb, None
+        if mb is not None and ctx.needs_input_grad[0]:
+            # ReLU backward + bias gradient inside the weight-gradient kernel
+            direct_b = _direct(b)
+            db_out = b.grad if direct_b else torch.empty_like(b)
+            KH, KW = w.shape[2], w.shape[3]
+            dw = ops.timed(f"conv_x6_u8_wgrad_relu_{C}x{w[0].numel()}",
+                           lambda: ops.conv_x6_u8_wgrad(g2, frames, idx, (KH, KW), stride,
+                                                        divisor, mbits=mb,
+                                                        db=db_out)).view(w.shape)
+            if _direct(w):
+                w.grad.copy_(dw)
+                dw = None
+            return dw, (None if direct_b else db_out), None, None, None, None, None, None
         gp2, db_out, direct_b = _conv_relu_backward(ctx.box, g2, y, b, relu)
         dw = None
         if ctx.needs_input_grad[0]:
@@ -748,6 +773,11 @@ class _ConvX6U8(torch.autograd.Function):
 # The update's first convolution straight from the u8 frame stacks (_ConvX6U8) when the trunk
 # starts [NormalizeImg,] Conv2d: no minibatch gather of f32 observations
 CONV_X6_U8 = True
+
+# ... its ReLU backward and bias gradient inside the image-staged weight-gradient kernel (the
+# forward's ReLU bitmask, ops.conv_x6_u8 / conv_x6_u8_wgrad mbits): no relu_bias_grad pass over
+# the first layer's [B OH OW, 32] gradient (read twice, written once)
+U8_WGRAD_RELU = True
 
 
 # NatureCNN convolutions on this package's implicit GEMMs (ops.conv_x6, x6 products: no MIOpen,

@@ -2148,6 +2148,7 @@ struct ConvImgArgs {
   int B, H, W, OW, P;  // P = OH * OW output positions per image (P % 16 == 0)
   int relu;
   float cdiv;
+  uint32_t* mbits;    // [B * P] or null: bit co of word r = out[r, co] > 0 (the ReLU mask)
 };
 
 __device__ __forceinline__ uint32_t img_bf16x2(uint32_t v, int half) {
@@ -2266,6 +2267,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_u8_img_kernel(ConvImgArg
         u1 = n1;
       }
       // C/D layout: column fr of block j, rows 4 fc + r of the tile
+      float ov[2][4];
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -2273,8 +2275,22 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_u8_img_kernel(ConvImgArg
           float v = acc[j][r] / a.cdiv;
           if (a.bias) v += bias[j];
           if (a.relu) v = relu_f(v);
+          ov[j][r] = v;
           a.out[(static_cast<int64_t>(b) * a.P + 16 * tile + 4 * fc + r) * kImgCO + 16 * j + fr] = v;
         }
+      if (a.mbits) {
+        // row 4 fc + r's 32 mask bits: lanes 16 fc .. 16 fc + 15 of the two blocks' ballots
+        uint32_t wd[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const uint64_t b0 = __ballot(ov[0][r] > 0.f), b1 = __ballot(ov[1][r] > 0.f);
+          wd[r] = static_cast<uint32_t>((b0 >> (16 * fc)) & 0xffffu) |
+                  (static_cast<uint32_t>((b1 >> (16 * fc)) & 0xffffu) << 16);
+        }
+        if (fr == 0)
+          *reinterpret_cast<uint4*>(a.mbits + static_cast<int64_t>(b) * a.P + 16 * tile + 4 * fc) =
+              uint4{wd[0], wd[1], wd[2], wd[3]};
+      }
     }
   }
 }
@@ -2296,6 +2312,12 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_u8_img_kernel(ConvImgArg
 // order). Each wave writes its partial [32 co][256 taps] to workspace slot 4 blockIdx.x + wave;
 // sum_parts_kernel then adds the 4 grid partials in slot order in f64 and divides once:
 // deterministic (not the tile loop's summation order; tests compare with a float64 convolution).
+// With mbits (the forward's ReLU bitmask, conv_u8_img_kernel) gp is the UNMASKED output gradient:
+// each image's P mask words ride with its bytes (registers one image ahead, then LDS), a lane
+// zeroes its gradient rows where the mask bit is clear before the split (relu_bias_grad's
+// threshold_backward, so the products are those of the masked gradient, bitwise), and with dbp
+// the masked rows' per-channel sums (the bias gradient) are kept per lane, reduced over the wave's
+// row groups and written to dbp [4 grid, 32]: no masked copy of the gradient ever reaches HBM.
 constexpr int kWgRow = 24;  // ox padded to a multiple of 8
 
 struct ConvWgImgArgs {
@@ -2305,6 +2327,8 @@ struct ConvWgImgArgs {
   int64_t ldg;
   float* part;      // [4 grid, 32, 256]
   int B;
+  const uint32_t* mbits;  // [B P] or null
+  float* dbp;             // [4 grid, 32] or null
 };
 
 template <int C, int H, int W, int OH, int OW>
@@ -2320,6 +2344,10 @@ __global__ __launch_bounds__(256, 1) void conv_u8_wgrad_img_kernel(ConvWgImgArgs
   constexpr int kTChan = 8 * H * kTRow;  // bytes per channel
   // [c][kx][y][24] bf16: every channel of the image at once (129 KB of the CU's 160)
   __shared__ __attribute__((aligned(16))) uint16_t T[C * 8 * H * kWgRow];
+  // the image's mask words (a step's last 8-position group may read up to 7 past P: those
+  // positions' gradient rows are zero whatever the word holds)
+  static_assert(P <= 512, "two mask words per thread");
+  __shared__ __attribute__((aligned(16))) uint32_t Mw[P + 8];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int fr = lane & 15, fc = lane >> 4;
   const int iy = t / (kWgRow / 8), ig = t - iy * (kWgRow / 8);  // this thread's T item
@@ -2357,6 +2385,17 @@ __global__ __launch_bounds__(256, 1) void conv_u8_wgrad_img_kernel(ConvWgImgArgs
                : 0.f;
       }
   };
+  // image bb's mask words t, t + 256
+  uint32_t mr[2];
+  const bool masked = a.mbits != nullptr;
+  auto load_m = [&](int bb) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int p = t + 256 * i;
+      mr[i] = (masked && bb < a.B && p < P) ? a.mbits[static_cast<int64_t>(bb) * P + p] : 0u;
+    }
+  };
+  float dbs[2] = {0.f, 0.f};  // this lane's masked gradient sums, channels fr, 16 + fr
   floatx4 acc[C * 4][2];  // tap block (c, 16-tap group) x channel block
 #pragma unroll
   for (int i = 0; i < C * 4; ++i)
@@ -2366,10 +2405,15 @@ __global__ __launch_bounds__(256, 1) void conv_u8_wgrad_img_kernel(ConvWgImgArgs
   // the loads run beside the rest of this image's work
   int b = blockIdx.x;
   load_raw(b);
+  load_m(b);
 #pragma unroll
   for (int q = 0; q < KSW; ++q) load_g(b, q);
   for (; b < a.B; b += grid) {
-    __syncthreads();  // the previous image's T readers done
+    __syncthreads();  // the previous image's T / Mw readers done
+    if (masked) {
+      Mw[t] = mr[0];
+      if (t + 256 < P) Mw[t + 256] = mr[1];
+    }
     if (t < kItems) {
       // T[c][kx][iy][8 ig + e] = img[c][iy][4 (8 ig + e) + kx] = phase kx % 4 of dword e + kx / 4
 #pragma unroll
@@ -2391,6 +2435,7 @@ __global__ __launch_bounds__(256, 1) void conv_u8_wgrad_img_kernel(ConvWgImgArgs
         }
     }
     load_raw(b + grid);  // the next image's bytes, in flight during this image's MFMAs
+    load_m(b + grid);
     __syncthreads();
     // this wave's K steps x all 256 taps (channel c's 4 blocks of 16: tap = 16 tb + fr -> ky =
     // 2 tb + fr / 8, kx = fr % 8)
@@ -2398,6 +2443,24 @@ __global__ __launch_bounds__(256, 1) void conv_u8_wgrad_img_kernel(ConvWgImgArgs
     for (int q = 0; q < KSW; ++q) {
       const int ks = wv + 4 * q;
       if (ks >= KS) break;  // wave-uniform
+      if (masked) {
+        // positions oy OW + ox0 .. + 7 (ox0 % 8 == 0, OW % 4 == 0: 16-B aligned words)
+        const int k0 = 32 * ks + 8 * fc, oy = k0 / kWgRow, ox0 = k0 - oy * kWgRow;
+        const uint4 m0 = *reinterpret_cast<const uint4*>(Mw + oy * OW + ox0);
+        const uint4 m1 = *reinterpret_cast<const uint4*>(Mw + oy * OW + ox0 + 4);
+        const uint32_t mw[8] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (((mw[e] >> (16 * j + fr)) & 1u) == 0u) gr[q][j][e] = 0.f;
+      }
+      if (a.dbp) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) dbs[j] += gr[q][j][e];
+      }
       bf16x8 gf[2][3];
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
@@ -2440,6 +2503,16 @@ __global__ __launch_bounds__(256, 1) void conv_u8_wgrad_img_kernel(ConvWgImgArgs
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         pw[(16 * j + fr) * (C * 64) + 16 * i + 4 * fc + r] = acc[i][j][r];
+  if (a.dbp) {
+    // the wave's 4 row groups (xor 16, 32), then slot 4 blockIdx.x + wave like the weight's
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      float s = dbs[j];
+      s += __shfl_xor(s, 16, kWave);
+      s += __shfl_xor(s, 32, kWave);
+      if (fc == 0) a.dbp[(static_cast<int64_t>(blockIdx.x) * 4 + wv) * kImgCO + 16 * j + fr] = s;
+    }
+  }
 }
 
 static int conv_u8_img_grid(int B) {
@@ -2592,7 +2665,8 @@ extern "C" int ocppo_conv_x6_u8(ocppo_stream_t stream, int mode, const uint8_t* 
                                 const int64_t* idx, int64_t C, int64_t H, int64_t W, int64_t KH,
                                 int64_t KW, int64_t stride, const float* w, int64_t ldw, float* c,
                                 int64_t M, int64_t N, int64_t K, int64_t splits, const float* bias,
-                                int relu, float divisor, int tile, float* out) {
+                                int relu, float divisor, int tile, float* out, uint32_t* mbits,
+                                float* dbp, float* db) {
   OCPPO_REQUIRE(mode == 0 || mode == 1, "ocppo_conv_x6_u8: mode %d (0 rows, 1 weight gradient)",
                 mode);
   OCPPO_REQUIRE(src && idx && w && c && (mode == 0 || out), "ocppo_conv_x6_u8: null pointer");
@@ -2616,9 +2690,11 @@ extern "C" int ocppo_conv_x6_u8(ocppo_stream_t stream, int mode, const uint8_t* 
                   "stride 4, 32 output channels, 16 | OH OW, a 16-B aligned src with 16 | C H W, "
                   "two image buffers of C H W (1 KiB-rounded) <= 64 KB (C=%lld H=%lld W=%lld N=%lld M=%lld)", (long long)C,
                   (long long)H, (long long)W, (long long)N, (long long)M);
+    OCPPO_REQUIRE(!dbp && !db && (!mbits || (relu && reinterpret_cast<uintptr_t>(mbits) % 16 == 0)),
+                  "ocppo_conv_x6_u8: tile 7 takes mbits (16-B aligned, with relu) and no dbp / db");
     ConvImgArgs ia{src, idx, w, ldw, bias, c, static_cast<int>(M / P), static_cast<int>(H),
                    static_cast<int>(W), static_cast<int>(OW), static_cast<int>(P), relu ? 1 : 0,
-                   divisor};
+                   divisor, mbits};
     clear_stale_error();
     const size_t ibuf = static_cast<size_t>((bytes + kImgChunk - 1) / kImgChunk) * kImgChunk;
     const int grid = conv_u8_img_grid(ia.B);
@@ -2643,7 +2719,10 @@ extern "C" int ocppo_conv_x6_u8(ocppo_stream_t stream, int mode, const uint8_t* 
                   "workgroups, a 16-B aligned src (C=%lld H=%lld W=%lld M=%lld K=%lld splits=%lld)",
                   (long long)C, (long long)H, (long long)W, (long long)M, (long long)K,
                   (long long)splits);
-    ConvWgImgArgs wa{src, idx, w, ldw, c, static_cast<int>(K / P)};
+    OCPPO_REQUIRE((dbp == nullptr) == (db == nullptr) &&
+                      (!mbits || reinterpret_cast<uintptr_t>(mbits) % 16 == 0),
+                  "ocppo_conv_x6_u8: tile 8 takes dbp and db together, a 16-B aligned mbits");
+    ConvWgImgArgs wa{src, idx, w, ldw, c, static_cast<int>(K / P), mbits, dbp};
     clear_stale_error();
     hipStream_t s = as_stream(stream);
     hipLaunchKernelGGL((conv_u8_wgrad_img_kernel<4, 84, 84, 20, 20>),
@@ -2652,8 +2731,13 @@ extern "C" int ocppo_conv_x6_u8(ocppo_stream_t stream, int mode, const uint8_t* 
     const int64_t n = M * N;
     hipLaunchKernelGGL(sum_parts_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64 * kSumGroups), 0,
                        s, c, (int)splits, n, out, static_cast<double>(divisor));
-    return check_launch("ocppo_conv_x6_u8 (sum_parts)");
+    if (int rc = check_launch("ocppo_conv_x6_u8 (sum_parts)")) return rc;
+    if (!db) return OCPPO_OK;
+    hipLaunchKernelGGL(sum_parts_kernel, dim3(1), dim3(64 * kSumGroups), 0, s, dbp, (int)splits,
+                       int64_t{kImgCO}, db, 1.0);
+    return check_launch("ocppo_conv_x6_u8 (bias gradient)");
   }
+  OCPPO_REQUIRE(!mbits && !dbp && !db, "ocppo_conv_x6_u8: mbits / dbp / db need tile 7 or 8");
   const X6Tile tc = kConvTiles[tile >= 0 && tile < 7 ? tile : 0];
   const int64_t bm = 16 * tc.fm * tc.wgm, bn = 16 * tc.fn * tc.wgn;
   OCPPO_REQUIRE(M % bm == 0 && N % bn == 0 && K % kX6BK == 0 && splits >= 1 &&

@@ -1007,11 +1007,13 @@ def _conv_u8_img_ok(src, weight, stride: int) -> bool:
 
 
 def conv_x6_u8(src, idx, weight, bias=None, stride: int = 4, relu: bool = True,
-               divisor: float = 255.0, out=None, tile: int | None = None):
+               divisor: float = 255.0, out=None, tile: int | None = None, mbits=None):
     """act(conv2d(src[idx] / divisor, weight) + bias) with the u8 frame stacks read in place
     (ocppo_conv_x6_u8): src [R, C, H, W] u8, idx [B] int64 -> channels_last [B, Cout, OH, OW].
     tile: None = the image-staged kernel where it applies (CONV_U8_IMG), else the tile loop's;
-    an explicit ocppo_conv_x6_u8 tile forces that form (tests)."""
+    an explicit ocppo_conv_x6_u8 tile forces that form (tests). mbits: an int32 [B OH OW] tensor
+    the image-staged kernel fills with the output's ReLU mask (bit co of row r = out > 0), for
+    conv_x6_u8_wgrad's fused ReLU backward."""
     B = idx.numel()
     if not conv_x6_u8_ok(src, weight, stride, B):
         raise ValueError(f"conv_x6_u8: unsupported src {tuple(src.shape)} / weight "
@@ -1030,9 +1032,12 @@ def conv_x6_u8(src, idx, weight, bias=None, stride: int = 4, relu: bool = True,
     _bounds(dev, u8=src)
     if tile is None:
         tile = 7 if _conv_u8_img_ok(src, weight, s) else _conv_u8_tile(M, Cout, 0)
+    if mbits is not None and (tile != 7 or not relu):
+        raise ValueError("conv_x6_u8: mbits needs the image-staged kernel (tile 7) and relu")
     call("ocppo_conv_x6_u8", _stream(dev), 0, src.data_ptr(), _check(idx, "idx", torch.int64, dev, B),
          C, H, W, KH, KW, s, wn.data_ptr(), K, out.data_ptr(), M, Cout, K, 1,
-         _opt(bias, "bias", f, dev, Cout), int(bool(relu)), float(divisor), tile, None)
+         _opt(bias, "bias", f, dev, Cout), int(bool(relu)), float(divisor), tile, None,
+         _opt(mbits, "mbits", torch.int32, dev, M), None, None)
     return out
 
 
@@ -1056,11 +1061,14 @@ def _conv_u8_img_wgrad_ok(src, kernel, stride: int, Cout: int) -> bool:
 
 
 def conv_x6_u8_wgrad(gp, src, idx, kernel: tuple, stride: int = 4, divisor: float = 255.0,
-                     out=None, tile: int | None = None):
+                     out=None, tile: int | None = None, mbits=None, db=None):
     """dW [Cout, C KH KW] (nn.Conv2d's tap order) of conv_x6_u8: sum over the output pixels r of
     gp[r, co] src[idx[b], c, s oy + ky, s ox + kx] / divisor; split partials summed in order.
     tile: None = the image-staged kernel where it applies (CONV_U8_IMG_WGRAD), else the tile
-    loop's; an explicit ocppo_conv_x6_u8 tile forces that form (tests)."""
+    loop's; an explicit ocppo_conv_x6_u8 tile forces that form (tests). Image-staged kernel only:
+    mbits (conv_x6_u8's ReLU mask) makes gp the UNMASKED output gradient, masked in the kernel
+    (relu_bias_grad's ReLU backward); db [Cout] receives the masked gradient's column sums (the
+    bias gradient)."""
     B = idx.numel()
     _, C, H, W = src.shape
     KH, KW = kernel
@@ -1071,6 +1079,8 @@ def conv_x6_u8_wgrad(gp, src, idx, kernel: tuple, stride: int = 4, divisor: floa
     N = C * KH * KW
     if tile is None and _conv_u8_img_wgrad_ok(src, kernel, s, Cout):
         tile = 8
+    if (mbits is not None or db is not None) and tile != 8:
+        raise ValueError("conv_x6_u8_wgrad: mbits / db need the image-staged kernel (tile 8)")
     if tile == 8:
         if rows != B * OH * OW:
             raise ValueError("conv_x6_u8_wgrad: gp must be [B OH OW, Cout]")
@@ -1081,11 +1091,18 @@ def conv_x6_u8_wgrad(gp, src, idx, kernel: tuple, stride: int = 4, divisor: floa
         part = _CONV_PARTS[key]
         if out is None:
             out = torch.empty((Cout, N), dtype=f, device=dev)
+        dbp = None
+        if db is not None:
+            dkey = ("wgrad_img_db", str(dev), S, Cout)
+            if dkey not in _CONV_PARTS:
+                _CONV_PARTS[dkey] = torch.empty((S, Cout), dtype=f, device=dev)
+            dbp = _CONV_PARTS[dkey].data_ptr()
         _bounds(dev, u8=src)
         call("ocppo_conv_x6_u8", _stream(dev), 1, src.data_ptr(),
              _check(idx, "idx", torch.int64, dev, B), C, H, W, KH, KW, s,
              _check(gp, "gp", f, dev), Cout, part.data_ptr(), Cout, N, rows, S, None, 0,
-             float(divisor), 8, _check(out, "out", f, dev, Cout * N))
+             float(divisor), 8, _check(out, "out", f, dev, Cout * N),
+             _opt(mbits, "mbits", torch.int32, dev, rows), dbp, _opt(db, "db", f, dev, Cout))
         return out
     tile = _conv_u8_tile(Cout, N, 1) if tile is None else tile
     if rows != B * OH * OW or tile is None or rows % 32:
@@ -1101,7 +1118,7 @@ def conv_x6_u8_wgrad(gp, src, idx, kernel: tuple, stride: int = 4, divisor: floa
     _bounds(dev, u8=src)
     call("ocppo_conv_x6_u8", _stream(dev), 1, src.data_ptr(), _check(idx, "idx", torch.int64, dev, B),
          C, H, W, KH, KW, s, _check(gp, "gp", f, dev), Cout, part.data_ptr(), Cout, N, rows, S,
-         None, 0, float(divisor), tile, _check(out, "out", f, dev, Cout * N))
+         None, 0, float(divisor), tile, _check(out, "out", f, dev, Cout * N), None, None, None)
     return out
 
 

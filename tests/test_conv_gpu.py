@@ -280,3 +280,38 @@ def test_u8_first_conv_image_staged_weight_gradient(B):
     _check(loop, ref, scale, lib)
     assert torch.equal(dw, ops.conv_x6_u8_wgrad(rows, src, idx, (8, 8), s, tile=8).view(w.shape))
     assert torch.equal(dw, ops.conv_x6_u8_wgrad(rows, src, idx, (8, 8), s).view(w.shape))
+
+
+@pytest.mark.parametrize("B", [16, 304])
+def test_u8_first_conv_relu_backward_fused_into_the_weight_gradient(B):
+    """The forward's ReLU bitmask (tile 7, mbits) handed to the weight-gradient kernel (tile 8)
+    with the UNMASKED output gradient: the kernel's ReLU backward gives bitwise the dW of the
+    masked gradient (relu_bias_grad's threshold_backward first, as the unfused backward does),
+    and its per-channel sums the bias gradient (against relu_bias_grad's and a float64 sum)."""
+    src = _frames(R=B + 5, seed=21)
+    _, w, b, s = _operands("conv1", 22)
+    idx = torch.randperm(src.shape[0], device=DEV)[:B]
+    mb = torch.full((B * 400,), -1, dtype=torch.int32, device=DEV)
+    y = ops.conv_x6_u8(src, idx, w, b, s, True, mbits=mb)
+    assert torch.equal(y, ops.conv_x6_u8(src, idx, w, b, s, True))
+    yr = y.permute(0, 2, 3, 1).reshape(-1, 32)
+    bits = torch.stack([(mb >> c) & 1 for c in range(32)], 1).bool()
+    assert torch.equal(bits, yr > 0)
+    g = torch.Generator(device=DEV).manual_seed(23)
+    gu = (torch.rand(B, 32, 20, 20, device=DEV, generator=g) * 2 - 1).contiguous(memory_format=CL)
+    rows = gu.permute(0, 2, 3, 1).reshape(-1, 32)
+    db_ref = torch.empty(32, device=DEV)
+    gp, _ = ops.relu_bias_grad(rows, yr.contiguous(), db=db_ref)
+    dw_ref = ops.conv_x6_u8_wgrad(gp, src, idx, (8, 8), s, tile=8)
+    db = torch.full((32,), float("nan"), device=DEV)
+    dw = ops.conv_x6_u8_wgrad(rows, src, idx, (8, 8), s, mbits=mb, db=db)
+    assert torch.equal(dw, dw_ref)
+    db64 = torch.where(yr > 0, rows, 0).double().sum(0)
+    scale = rows.abs().double().sum(0)
+    assert float(((db.double() - db64).abs() / scale).max()) < 1e-6
+    assert float(((db_ref.double() - db64).abs() / scale).max()) < 1e-6
+    db2 = torch.empty(32, device=DEV)  # without the mask: the plain column sums
+    ops.conv_x6_u8_wgrad(gp, src, idx, (8, 8), s, db=db2)
+    assert float(((db2.double() - db64).abs() / scale).max()) < 1e-6
+    with pytest.raises(ValueError):
+        ops.conv_x6_u8(src, idx, w, b, s, False, mbits=mb)  # a mask needs the ReLU
