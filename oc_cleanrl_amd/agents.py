@@ -976,9 +976,18 @@ def linear_act_nhwc_infer(x, lin: nn.Linear, relu: bool):
         ent[1].copy_(_cols_to_nhwc(lin.weight, (C, H, W)))
         ent[2] = _WEIGHTS_GEN[0]
     x2 = x.permute(0, 2, 3, 1).reshape(B, H * W * C)
+    if HIP_FLAT_INFER:
+        return ops.timed(f"linear_act_{B}x{lin.out_features}x{H * W * C}",
+                         lambda: ops.linear_act(x2, ent[1], lin.bias, relu))
     if relu:
         return torch._addmm_activation(lin.bias, x2, ent[1].t(), use_gelu=False)
     return torch.addmm(lin.bias, x2, ent[1].t())
+
+
+# ... on the HIP f32-MFMA rows kernel (ops.linear_act: 16 x 16 output tiles, K split over 8 waves,
+# bias + ReLU fused) instead of hipBLASLt's f32 GEMM + epilogue: measured slower at 256 x 3136 ->
+# 512 (17.3 vs 15.0 us, config 3 474.3k vs 476.2k env steps/s, profiles/r06/config3/SUMMARY.txt)
+HIP_FLAT_INFER = False
 
 
 def linear_relu(x, lin: nn.Linear, rows: bool = False):
