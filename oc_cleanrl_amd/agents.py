@@ -718,7 +718,7 @@ class _ConvX6U8(torch.autograd.Function):
     bias gradient itself (ops.conv_x6_u8_wgrad mbits / db): no relu_bias_grad pass."""
 
     @staticmethod
-    def forward(ctx, w, b, frames, idx, stride, relu: bool, divisor: float, box=None):
+    def forward(ctx, w, b, frames, idx, stride, relu: bool, divisor: float, box=None, wn=None):
         mb = None
         if (U8_WGRAD_RELU and relu and box is None and ctx.needs_input_grad[0] and
                 ops._conv_u8_img_ok(frames, w, stride) and
@@ -727,7 +727,8 @@ class _ConvX6U8(torch.autograd.Function):
                 ((frames.shape[3] - w.shape[3]) // stride + 1)
             mb = torch.empty(idx.numel() * P, dtype=torch.int32, device=frames.device)
         y = ops.timed(f"conv_x6_u8_{idx.numel()}",
-                      lambda: ops.conv_x6_u8(frames, idx, w, b, stride, relu, divisor, mbits=mb))
+                      lambda: ops.conv_x6_u8(frames, idx, w, b, stride, relu, divisor, mbits=mb,
+                                             wn=wn))
         ctx.conv = (stride, relu, divisor)
         ctx.b = b
         ctx.box = box
@@ -756,7 +757,7 @@ class _ConvX6U8(torch.autograd.Function):
             if _direct(w):
                 w.grad.copy_(dw)
                 dw = None
-            return dw, (None if direct_b else db_out), None, None, None, None, None, None
+            return dw, (None if direct_b else db_out), None, None, None, None, None, None, None
         gp2, db_out, direct_b = _conv_relu_backward(ctx.box, g2, y, b, relu)
         dw = None
         if ctx.needs_input_grad[0]:
@@ -767,7 +768,7 @@ class _ConvX6U8(torch.autograd.Function):
             if _direct(w):
                 w.grad.copy_(dw)  # nn.Conv2d's tap order into the channels_last grad
                 dw = None
-        return dw, (None if direct_b else db_out), None, None, None, None, None, None
+        return dw, (None if direct_b else db_out), None, None, None, None, None, None, None
 
 
 # The update's first convolution straight from the u8 frame stacks (_ConvX6U8) when the trunk
@@ -963,6 +964,21 @@ def _flat_nhwc_infer_ok(x, flat, lin) -> bool:
             and not x.is_contiguous() and lin.in_features == x[0].numel())
 
 
+_CONTIG_INFER: dict = {}
+
+
+def _contig_infer(w):
+    """A contiguous copy of parameter w, refreshed once per rollout (rollout_inference)."""
+    ent = _CONTIG_INFER.get(id(w))
+    if ent is None or ent[0] is not w:
+        ent = [w, torch.empty(w.shape, dtype=w.dtype, device=w.device), -1]
+        _CONTIG_INFER[id(w)] = ent
+    if ent[2] != _WEIGHTS_GEN[0]:
+        ent[1].copy_(w)
+        ent[2] = _WEIGHTS_GEN[0]
+    return ent[1]
+
+
 def linear_act_nhwc_infer(x, lin: nn.Linear, relu: bool):
     """act(lin(flatten(x))) without autograd for a channels_last x, reading x in its memory order
     against a cached column-permuted weight (same products, columns visited in (H, W, C) order)."""
@@ -1108,7 +1124,11 @@ class _ActorCritic(Predictor):
         conv = net[0]
         relu = isinstance(net[1], nn.ReLU)
         box = {"bias": conv.bias} if relu and CONV_DGRAD_RELU else None
-        y = _ConvX6U8.apply(conv.weight, conv.bias, frames, idx, conv.stride[0], relu, div, box)
+        # the rollout (weights fixed): the weight's tap-order copy made once per rollout
+        wn = (_contig_infer(conv.weight) if _IN_ROLLOUT[0] and not torch.is_grad_enabled()
+              and not conv.weight.is_contiguous() else None)
+        y = _ConvX6U8.apply(conv.weight, conv.bias, frames, idx, conv.stride[0], relu, div, box,
+                            wn)
         if box is not None:
             y._ocppo_cbox = box
         return fused_trunk(net[2 if relu else 1:], y)

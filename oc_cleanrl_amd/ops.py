@@ -926,9 +926,10 @@ def conv_x6_dgrad(gp, weight, stride: int, in_hw: tuple, out=None, relu_out=None
     if tuple(out.shape) != (B, C, H, W) or not out.is_contiguous(memory_format=torch.channels_last):
         raise ValueError("conv_x6_dgrad: out must be a channels_last [B, C, H, W] tensor")
     # class (py, px)'s taps ky = py + s t, flipped (t' = T - 1 - t), as [C, T, TW, Cout] rows;
-    # the classes stacked class-major: B = [s s C, K]
-    wc = torch.stack([weight[:, :, py::s, px::s].flip(2, 3).permute(1, 2, 3, 0)
-                      for py in range(s) for px in range(s)]).reshape(N, K)
+    # the classes stacked class-major: B = [s s C, K] -- one gather through a cached index into
+    # the weight's memory (its [Cout, KH, KW, C] order when channels_last) instead of s^2 flips,
+    # a stack and a layout copy per call
+    wc = _dgrad_weight(weight, s)
     og = None if s == 1 else _geom(H * W * C, s * W * C, s * C, 0, C, s, W * C, C)
     if CONV_DGRAD_PAD_COPY or tile not in (2, 3, 5, 6):
         gpad = torch.nn.functional.pad(g, (0, 0, TW - 1, TW - 1, T - 1, T - 1))
@@ -956,6 +957,25 @@ def conv_x6_dgrad(gp, weight, stride: int, in_hw: tuple, out=None, relu_out=None
         # row tiles, then stride classes, in order (f64, one rounding)
         db.copy_(dbp.view(-1, s * s, C).double().sum(0).sum(0))
     return out
+
+
+_DG_IDX: dict = {}
+
+
+def _dgrad_weight(weight, s: int):
+    """conv_x6_dgrad's B operand [s s C, T TW Cout]: row (py, px, c), column (t, tw, co) =
+    weight[co, c, py + s (T - 1 - t), px + s (TW - 1 - tw)], gathered in one launch."""
+    Cout, C, KH, KW = weight.shape
+    mem = weight.permute(0, 2, 3, 1)  # a view of the memory when channels_last
+    key = (str(weight.device), Cout, C, KH, KW, s)
+    idx = _DG_IDX.get(key)
+    if idx is None:
+        ar = torch.arange(Cout * KH * KW * C).view(Cout, KH, KW, C).permute(0, 3, 1, 2)
+        idx = torch.stack([ar[:, :, py::s, px::s].flip(2, 3).permute(1, 2, 3, 0)
+                           for py in range(s) for px in range(s)])
+        idx = idx.reshape(s * s * C, -1).to(weight.device)
+        _DG_IDX[key] = idx
+    return mem.reshape(-1)[idx]
 
 
 # the data gradient over a zero-padded copy of the output gradient (F.pad: a fill and a copy per
@@ -1007,13 +1027,15 @@ def _conv_u8_img_ok(src, weight, stride: int) -> bool:
 
 
 def conv_x6_u8(src, idx, weight, bias=None, stride: int = 4, relu: bool = True,
-               divisor: float = 255.0, out=None, tile: int | None = None, mbits=None):
+               divisor: float = 255.0, out=None, tile: int | None = None, mbits=None,
+               wn=None):
     """act(conv2d(src[idx] / divisor, weight) + bias) with the u8 frame stacks read in place
     (ocppo_conv_x6_u8): src [R, C, H, W] u8, idx [B] int64 -> channels_last [B, Cout, OH, OW].
     tile: None = the image-staged kernel where it applies (CONV_U8_IMG), else the tile loop's;
     an explicit ocppo_conv_x6_u8 tile forces that form (tests). mbits: an int32 [B OH OW] tensor
     the image-staged kernel fills with the output's ReLU mask (bit co of row r = out > 0), for
-    conv_x6_u8_wgrad's fused ReLU backward."""
+    conv_x6_u8_wgrad's fused ReLU backward. wn: the weight already in nn.Conv2d's contiguous
+    (c, ky, kx) tap order (a cached copy of a channels_last weight), else made here."""
     B = idx.numel()
     if not conv_x6_u8_ok(src, weight, stride, B):
         raise ValueError(f"conv_x6_u8: unsupported src {tuple(src.shape)} / weight "
@@ -1024,7 +1046,10 @@ def conv_x6_u8(src, idx, weight, bias=None, stride: int = 4, relu: bool = True,
     OH, OW = (H - KH) // s + 1, (W - KW) // s + 1
     dev, f = src.device, torch.float32
     K, M = C * KH * KW, B * OH * OW
-    wn = weight.contiguous()  # nn.Conv2d's (c, ky, kx) tap order
+    if wn is None:
+        wn = weight.contiguous()  # nn.Conv2d's (c, ky, kx) tap order
+    elif tuple(wn.shape) != tuple(weight.shape) or not wn.is_contiguous():
+        raise ValueError("conv_x6_u8: wn must be the weight as a contiguous tensor")
     if out is None:
         out = torch.empty((B, Cout, OH, OW), dtype=f, device=dev, memory_format=torch.channels_last)
     if tuple(out.shape) != (B, Cout, OH, OW) or not out.is_contiguous(memory_format=torch.channels_last):

@@ -62,6 +62,10 @@ FUSED_HEAD_ENV = True
 # the step took 23.9 instead of 12.3 us against the 5.2 us split launch it replaces
 # (profiles/r05/breakdown_config2.txt vs the round-4 trace)
 ADAM_WRITES_PLANES = False
+# The fused heads forward + loss + heads backward (ops.heads_loss_fwd_bwd) also for trunks that
+# are not a Linear/ReLU stack (NatureCNN): the grad buffer is zeroed before it, as the unfused
+# path does before its backward
+FUSED_HEADS_LOSS_ANY_TRUNK = True
 # Pixel trunks: the rollout's first convolution reads the u8 frame stacks of the rollout buffer's
 # slot t (agents.trunk_frames: exact bf16 operands, NormalizeImg in the epilogue) instead of the
 # f32 network copy the store writes
@@ -452,8 +456,11 @@ class PPOTrainer:
         self.loss_ws = ops.LossWorkspace(self.M, self.A, dev)
         # heads forward + loss + heads backward fused on the decoder output (needs the in-place
         # grads of FlatAdam and the decoder's ReLU box; see _fused_tail)
-        self.fused_heads_loss = (a.fused_heads_loss and self.direct_grads and self.fused_head and
-                                 self.H in ops.HEADS_LOSS_WIDTHS and self.A <= 7)
+        # (FlatAdam's in-place grads; a trunk that is not a Linear/ReLU stack, e.g. NatureCNN,
+        # gets the grad buffer zeroed first, _fused_tail)
+        self.fused_heads_loss = (a.fused_heads_loss and a.fused_optimizer and self.fused_head and
+                                 self.H in ops.HEADS_LOSS_WIDTHS and self.A <= 7 and
+                                 (self.direct_grads or FUSED_HEADS_LOSS_ANY_TRUNK))
         self.gp_tail = (torch.empty((self.M, self.H), dtype=f32, device=dev)
                         if self.fused_heads_loss else None)
         self.hl_finish = ops.DeferredFinish(dev) if self.fused_heads_loss else None
@@ -839,6 +846,8 @@ class PPOTrainer:
         # the heads-loss finish (heads' and decoder-bias grads, loss statistics) rides in the
         # decoder's split-K weight-gradient combine (agents._weight_grad), or runs alone below
         box["finish"] = self.hl_finish
+        if not self.direct_grads:
+            self.grad_buf.zero_()  # before any of this minibatch's gradient writes
         h = hidden.detach()
         self.timer.bracket("heads_loss", lambda: ops.heads_loss_fwd_bwd(
             h, ag.actor.weight, ag.actor.bias, ag.critic.weight, ag.critic.bias,
