@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define OCPPO_ABI_VERSION 26
+#define OCPPO_ABI_VERSION 27
 
 /* status codes */
 #define OCPPO_OK 0
@@ -495,12 +495,17 @@ OCPPO_API int ocppo_gemm_x6_gather(ocppo_stream_t stream, const float* a, int64_
  * tile: 0 = 128 x 32, 2 = 128 x 64, 3 = 64 x 64, 5 = 128 x 128, 6 = 32 x 64 (mode 0); 1 =
  * 32 x 128, 3, 4 =
  * 64 x 128, 5 (mode 1); M, N multiples of it; K % 32 == 0, K / 32 >= splits.
+ * tile 7 (mode 0, ABI 27): few rows (the rollout's batch) -- a 32-row tile per workgroup with its
+ * K steps split over 8 waves and summed in wave order; N = 32 or 64, 32 | M, splits 1, no
+ * out_geom / pad / mask; the same x6 products per K step, grouped differently over K (not the
+ * other tiles' bits). w_planes (tile 7 only, else null; 16-B aligned): w's three bf16 pieces
+ * [3, N, K] (ocppo_split_planes of w), read instead of splitting w in every workgroup.
  * ------------------------------------------------------------------------------------------- */
 OCPPO_API int ocppo_conv_x6(ocppo_stream_t stream, int mode, const float* x, const int64_t* geom,
                             const float* w, int64_t ldw, float* c, int64_t ldc, int64_t M,
                             int64_t N, int64_t K, int64_t splits, const float* bias, int relu,
                             const int64_t* out_geom, int tile, float* out, const int64_t* pad,
-                            const float* mask, float* dbp);
+                            const float* mask, float* dbp, const uint16_t* w_planes);
 
 /* ---------------------------------------------------------------------------------------------
  * The first NatureCNN convolution straight from the rollout's u8 frame stacks (ppo_atari_oc.py:566

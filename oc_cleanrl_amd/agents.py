@@ -817,8 +817,34 @@ def _conv_x6(x, conv, relu: bool):
             y._ocppo_cbox = box
         return y
     B, Cin, H, _ = x.shape
+    wp = (_planes_infer(conv.weight) if CONV_ROWS_PLANES and _IN_ROLLOUT[0] and
+          not torch.is_grad_enabled() else None)
     return ops.timed(f"conv_x6_{B}x{Cin}x{H}_{conv.out_channels}",
-                     lambda: ops.conv_x6(x, conv.weight, conv.bias, s, relu))
+                     lambda: ops.conv_x6(x, conv.weight, conv.bias, s, relu, w_planes=wp))
+
+
+# The rollout's convolutions (ops.conv_x6's few-rows form) read their weights pre-split into the
+# three bf16 pieces once per rollout (ocppo_split_planes) instead of splitting them in every
+# workgroup
+CONV_ROWS_PLANES = True
+_PLANES_INFER: dict = {}
+
+
+def _planes_infer(w):
+    """bf16 [3, Cout, KH KW C] pieces of a channels_last conv weight's [Cout, KH KW C] matrix,
+    refreshed once per rollout (rollout_inference); None when the weight is not channels_last."""
+    ent = _PLANES_INFER.get(id(w))
+    if ent is None or ent[0] is not w:
+        wm = w.permute(0, 2, 3, 1).reshape(w.shape[0], -1)
+        if wm.data_ptr() != w.data_ptr() or not wm.is_contiguous() or wm.shape[1] % 8:
+            return None
+        wp = ops.WeightPlanes(fwd=(wm,))
+        ent = [w, wp, wm._ocppo_planes["fwd"], -1]
+        _PLANES_INFER[id(w)] = ent
+    if ent[3] != _WEIGHTS_GEN[0]:
+        ent[1].refresh()
+        ent[3] = _WEIGHTS_GEN[0]
+    return ent[2]
 
 
 def _conv_act_ok(x, conv) -> bool:

@@ -2515,6 +2515,124 @@ __global__ __launch_bounds__(256, 1) void conv_u8_wgrad_img_kernel(ConvWgImgArgs
   }
 }
 
+// A convolution forward of FEW rows (the rollout's batch: ocppo_conv_x6 mode 0, tile 7) with the
+// K steps split over the NW waves of a workgroup. The tile loop walks a tile's K steps one after
+// another on 2 waves, so at 256 envs (20736 / 12544 rows of NatureCNN's second / third layer)
+// each launch is a chain of 16-18 dependent load -> split -> MFMA steps (27.7 us). Here a
+// workgroup owns a 32 x 16 FN output tile and wave w of NW takes K steps w, w + NW, ... (NW = 4:
+// fastest of 4 / 8 / 16 at 256 envs, tools/exp_conv_rows.py), each wave's partial is
+// summed with the other waves' through LDS in wave order (deterministic), then + bias, ReLU.
+// Same x6 products per K step as the tile loop (x6_split2 pieces, x6_mfma6's order); the sum over
+// K steps is grouped by wave instead of running in order: not the tile loop's bits, f32-level
+// (tests/test_conv_gpu.py compares with a float64 convolution). Operand rows / taps through the
+// same implicit-GEMM geometry (x6_cv_row / x6_cv_seg); KW C % 32 == 0 so 8 taps of a lane are
+// contiguous.
+#ifndef OCPPO_ROWS_NW  // waves per workgroup (experiments: tools/exp_conv_rows.py)
+#define OCPPO_ROWS_NW 4
+#endif
+constexpr int kRowsNW = OCPPO_ROWS_NW;
+
+// BPL: the weight's three bf16 pieces pre-split (ocppo_split_planes, once per rollout: the
+// weights are fixed within it) -- the same pieces x6_split2 would form, read instead of split
+template <int FN, bool BPL>
+__global__ __launch_bounds__(64 * kRowsNW) void conv_x6_rows_kernel(X6Args g) {
+  constexpr int NB = 2 * FN;  // 16 x 16 blocks of the 32 x 16 FN tile
+  __shared__ __attribute__((aligned(16))) floatx4 red[kRowsNW][NB][kWave];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int fr = lane & 15, fc = lane >> 4;
+  const int m0 = 32 * static_cast<int>(blockIdx.x);
+  const float* __restrict__ x = g.a;
+  const float* __restrict__ w = g.b;
+  int64_t arow[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) arow[i] = x6_cv_row(g, m0 + 16 * i + fr);
+  const int steps = g.K / kX6BK;
+  floatx4 acc[2][FN];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  // one K step's operand values of this lane: A rows 16 i + fr, B columns 16 j + fr, taps
+  // 32 kt + 8 fc .. + 8
+  float4 va[2][2], vb[FN][2];
+  uint4 vp[BPL ? FN : 1][3];
+  auto load = [&](int kt, float4 (&a)[2][2], float4 (&b)[FN][2]) {
+    const int k = kX6BK * kt + 8 * fc;
+    const int64_t seg = x6_cv_seg(g, k);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const float4* p = reinterpret_cast<const float4*>(x + arow[i] + seg);
+      a[i][0] = p[0];
+      a[i][1] = p[1];
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      if constexpr (BPL) {
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+          vp[j][pl] = *reinterpret_cast<const uint4*>(
+              g.bpl + pl * g.bpl_ps + static_cast<int64_t>(16 * j + fr) * g.bpl_ld + k);
+      } else {
+        const float4* p =
+            reinterpret_cast<const float4*>(w + static_cast<int64_t>(16 * j + fr) * g.sbn + k);
+        b[j][0] = p[0];
+        b[j][1] = p[1];
+      }
+    }
+  };
+  auto pieces = [&](const float4 (&v)[2], bf16x8 (&f)[3]) {
+    uint32_t p[4][3];
+    x6_split2(x6f2{v[0].x, v[0].y}, p[0][0], p[0][1], p[0][2]);
+    x6_split2(x6f2{v[0].z, v[0].w}, p[1][0], p[1][1], p[1][2]);
+    x6_split2(x6f2{v[1].x, v[1].y}, p[2][0], p[2][1], p[2][2]);
+    x6_split2(x6f2{v[1].z, v[1].w}, p[3][0], p[3][1], p[3][2]);
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+      f[pl] = __builtin_bit_cast(bf16x8, u32x4{p[0][pl], p[1][pl], p[2][pl], p[3][pl]});
+  };
+  int kt = wv;
+  if (kt < steps) load(kt, va, vb);
+  for (; kt < steps; kt += kRowsNW) {
+    bf16x8 af[2][3];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) pieces(va[i], af[i]);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {  // B's pieces block by block (fewer live registers)
+      bf16x8 bfr[3];
+      if constexpr (BPL) {
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) bfr[pl] = __builtin_bit_cast(bf16x8, vp[j][pl]);
+      } else {
+        pieces(vb[j], bfr);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i) x6_mfma6<false>(af[i], bfr, acc[i][j], acc[i][j]);
+    }
+    if (kt + kRowsNW < steps) load(kt + kRowsNW, va, vb);
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) red[wv][i * FN + j][lane] = acc[i][j];
+  __syncthreads();
+  // block blk = (i, j): the waves' partials in wave order, then bias, ReLU; C/D layout: column
+  // fr of the block, rows 4 fc + r
+  for (int blk = wv; blk < NB; blk += kRowsNW) {
+    floatx4 s = red[0][blk][lane];
+#pragma unroll
+    for (int q = 1; q < kRowsNW; ++q) s += red[q][blk][lane];
+    const int i = blk / FN, j = blk - i * FN;
+    const int col = 16 * j + fr;
+    const float bv = g.bias ? g.bias[col] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float v = s[r] + bv;
+      if (g.relu) v = relu_f(v);
+      g.c[static_cast<int64_t>(m0 + 16 * i + 4 * fc + r) * g.ldc + col] = v;
+    }
+  }
+}
+
 static int conv_u8_img_grid(int B) {
   static int cus = 0;
   if (cus == 0) {
@@ -2533,12 +2651,65 @@ extern "C" int ocppo_conv_x6(ocppo_stream_t stream, int mode, const float* x, co
                              const float* w, int64_t ldw, float* c, int64_t ldc, int64_t M,
                              int64_t N, int64_t K, int64_t splits, const float* bias, int relu,
                              const int64_t* out_geom, int tile, float* out, const int64_t* pad,
-                             const float* mask, float* dbp) {
+                             const float* mask, float* dbp, const uint16_t* w_planes) {
   OCPPO_REQUIRE(mode == 0 || mode == 1, "ocppo_conv_x6: mode %d (0 rows, 1 weight gradient)", mode);
-  OCPPO_REQUIRE(tile >= 0 && tile < 7, "ocppo_conv_x6: tile %d", tile);
+  OCPPO_REQUIRE(tile >= 0 && tile < 8, "ocppo_conv_x6: tile %d", tile);
   OCPPO_REQUIRE(x && geom && w && c, "ocppo_conv_x6: null pointer");
   const int64_t qh = geom[0], qw = geom[1], sb = geom[2], ys = geom[3], xs = geom[4],
                 segs = geom[5], gseg = geom[6];
+  if (tile == 7) {  // few rows: K steps split over the waves of a workgroup (conv_x6_rows_kernel)
+    OCPPO_REQUIRE(mode == 0 && (N == 32 || N == 64) && M >= 32 && M % 32 == 0 && K >= kX6BK &&
+                      K % kX6BK == 0 && splits == 1 && !out_geom && !pad && !mask && !dbp &&
+                      gseg % kX6BK == 0 && ldw >= K && ldw % 4 == 0 && ldc >= N &&
+                      M <= INT32_MAX && K <= INT32_MAX && qh >= 1 && qw >= 1 &&
+                      M % (qh * qw) == 0 && M < (int64_t{1} << 24) && sb % 4 == 0 &&
+                      ys % 4 == 0 && xs % 4 == 0 && segs % 4 == 0 &&
+                      reinterpret_cast<uintptr_t>(x) % 16 == 0 &&
+                      reinterpret_cast<uintptr_t>(w) % 16 == 0,
+                  "ocppo_conv_x6: tile 7 needs mode 0, N = 32 or 64, 32 | M, 32 | K, kernel-row "
+                  "segments of a multiple of 32, splits 1, no output map / pad / mask (M=%lld "
+                  "N=%lld K=%lld)", (long long)M, (long long)N, (long long)K);
+    X6Args g{};
+    g.a = x;
+    g.b = w;
+    g.sbn = ldw;
+    g.sbk = 1;
+    g.c = c;
+    g.ldc = ldc;
+    g.M = (int)M;
+    g.N = (int)N;
+    g.K = (int)K;
+    g.splits = 1;
+    g.bias = bias;
+    g.relu = relu ? 1 : 0;
+    g.cv_qh = (int)qh;
+    g.cv_qw = (int)qw;
+    g.cv_sb = sb;
+    g.cv_ys = ys;
+    g.cv_xs = xs;
+    g.cv_segs = segs;
+    g.cv_gseg = (int)gseg;
+    if (w_planes) {
+      OCPPO_REQUIRE(reinterpret_cast<uintptr_t>(w_planes) % 16 == 0,
+                    "ocppo_conv_x6: w_planes must be 16-B aligned");
+      g.bpl = w_planes;
+      g.bpl_ld = K;
+      g.bpl_ps = N * K;
+    }
+    clear_stale_error();
+    const dim3 grid(static_cast<unsigned>(M / 32)), block(64 * kRowsNW);
+    hipStream_t s = as_stream(stream);
+    if (N == 64 && w_planes)
+      hipLaunchKernelGGL((conv_x6_rows_kernel<4, true>), grid, block, 0, s, g);
+    else if (N == 64)
+      hipLaunchKernelGGL((conv_x6_rows_kernel<4, false>), grid, block, 0, s, g);
+    else if (w_planes)
+      hipLaunchKernelGGL((conv_x6_rows_kernel<2, true>), grid, block, 0, s, g);
+    else
+      hipLaunchKernelGGL((conv_x6_rows_kernel<2, false>), grid, block, 0, s, g);
+    return check_launch("ocppo_conv_x6 (tile 7)");
+  }
+  OCPPO_REQUIRE(!w_planes, "ocppo_conv_x6: w_planes needs tile 7");
   const X6Tile tc = kConvTiles[tile];
   const int64_t bm = 16 * tc.fm * tc.wgm, bn = 16 * tc.fn * tc.wgn;
   OCPPO_REQUIRE(M >= bm && N >= bn && M % bm == 0 && N % bn == 0 && K >= kX6BK && K % kX6BK == 0 &&

@@ -798,10 +798,11 @@ def _bounds(dev, x=None, u8=None):
             _tail(u8) if u8 is not None else 0, u8.shape[0] if u8 is not None else 0)
 
 
-def conv_x6(x, weight, bias=None, stride: int = 1, relu: bool = True, out=None):
+def conv_x6(x, weight, bias=None, stride: int = 1, relu: bool = True, out=None, w_planes=None):
     """act(conv2d(x, weight) + bias) (architectures/ppo.py:20-31's Conv2d + ReLU) on ocppo_conv_x6:
     channels_last f32 x [B, C, H, W], weight [Cout, C, KH, KW] -> channels_last [B, Cout, OH, OW]
-    (no autograd; agents._ConvX6 is the autograd form)."""
+    (no autograd; agents._ConvX6 is the autograd form). w_planes: the weight's [Cout, KH KW C]
+    matrix pre-split into bf16 [3, Cout, KH KW C] (used by the few-rows form only)."""
     if not conv_x6_ok(x, weight, stride):
         raise ValueError(f"conv_x6: unsupported shapes x {tuple(x.shape)}, weight "
                          f"{tuple(weight.shape)}, stride {stride} (conv_x6_ok)")
@@ -817,15 +818,25 @@ def conv_x6(x, weight, bias=None, stride: int = 1, relu: bool = True, out=None):
         out = torch.empty((B, Cout, OH, OW), dtype=f, device=dev, memory_format=torch.channels_last)
     if tuple(out.shape) != (B, Cout, OH, OW) or not out.is_contiguous(memory_format=torch.channels_last):
         raise ValueError("conv_x6: out must be a channels_last [B, Cout, OH, OW] tensor")
+    geom = _geom(OH, OW, H * W * C, s * W * C, s * C, W * C, KW * C)
+    if CONV_FWD_ROWS and M <= CONV_FWD_ROWS_MAX and Cout in (32, 64) and M % 32 == 0:
+        # few rows (the rollout's batch): K steps split over the waves of a workgroup
+        if w_planes is not None and (w_planes.dtype != torch.bfloat16 or tuple(w_planes.shape)
+                                     != (3, Cout, K) or not w_planes.is_contiguous()):
+            raise ValueError("conv_x6: w_planes must be contiguous bf16 [3, Cout, KH KW C]")
+        call("ocppo_conv_x6", _stream(dev), 0, x.data_ptr(), geom, wm.data_ptr(), K,
+             out.data_ptr(), Cout, M, Cout, K, 1, _opt(bias, "bias", f, dev, Cout),
+             int(bool(relu)), None, 7, None, None, None, None,
+             None if w_planes is None else _check(w_planes, "w_planes", torch.bfloat16, dev))
+        return out
     tile = _conv_fwd_tile(M, Cout)
     bm, bn = _CONV_TILES[tile]
     S = _conv_fwd_splits((M // bm) * (Cout // bn), K // 32)
-    geom = _geom(OH, OW, H * W * C, s * W * C, s * C, W * C, KW * C)
     _bounds(dev, x)
     if S == 1:
         call("ocppo_conv_x6", _stream(dev), 0, x.data_ptr(), geom, wm.data_ptr(), K,
              out.data_ptr(), Cout, M, Cout, K, 1, _opt(bias, "bias", f, dev, Cout),
-             int(bool(relu)), None, tile, None, None, None, None)
+             int(bool(relu)), None, tile, None, None, None, None, None)
         return out
     # few rows (the rollout's batch): K-split partials, then bias + ReLU on their ordered sum
     key = ("fwd", str(dev), S, M, Cout)
@@ -833,10 +844,18 @@ def conv_x6(x, weight, bias=None, stride: int = 1, relu: bool = True, out=None):
         _CONV_PARTS[key] = torch.empty((S, M, Cout), dtype=f, device=dev)
     part = _CONV_PARTS[key]
     call("ocppo_conv_x6", _stream(dev), 0, x.data_ptr(), geom, wm.data_ptr(), K, part.data_ptr(),
-         Cout, M, Cout, K, S, None, 0, None, tile, None, None, None, None)
+         Cout, M, Cout, K, S, None, 0, None, tile, None, None, None, None, None)
     call("ocppo_sum_splits_act", _stream(dev), part.data_ptr(), S, M, Cout,
          _opt(bias, "bias", f, dev, Cout), int(bool(relu)), out.data_ptr())
     return out
+
+
+# Forward products of at most CONV_FWD_ROWS_MAX rows (the rollout's batch: 20736 / 12544 rows for
+# NatureCNN's second / third layer at 256 envs) on ocppo_conv_x6 tile 7: a 32-row tile per
+# workgroup, its K steps split over 8 waves and summed through LDS in wave order, instead of the
+# tile loop's chain of 16-18 dependent K steps on 2 waves
+CONV_FWD_ROWS = True
+CONV_FWD_ROWS_MAX = 65536
 
 
 # K splits for a forward product of few workgroups (< 512; the rollout's image batch): measured
@@ -890,7 +909,7 @@ def conv_x6_wgrad(gp, x, kernel: tuple, stride: int, out=None):
     call("ocppo_conv_x6", _stream(dev), 1, x.data_ptr(),
          _geom(OH, OW, H * W * C, s * W * C, s * C, W * C, KW * C),
          _check(gp, "gp", f, dev), Cout, part.data_ptr(), N, Cout, N, rows, S, None, 0, None, tile,
-         out.data_ptr(), None, None, None)
+         out.data_ptr(), None, None, None, None)
     return out
 
 
@@ -938,7 +957,7 @@ def conv_x6_dgrad(gp, weight, stride: int, in_hw: tuple, out=None, relu_out=None
         _bounds(dev, gpad)
         call("ocppo_conv_x6", _stream(dev), 0, gpad.data_ptr(),
              _geom(QH, QW, Hp * Wp * Cout, Wp * Cout, Cout, Wp * Cout, TW * Cout), wc.data_ptr(),
-             K, out.data_ptr(), C, M, N, K, 1, None, 0, og, tile, None, None, None, None)
+             K, out.data_ptr(), C, M, N, K, 1, None, 0, og, tile, None, None, None, None, None)
         return out
     # the padding as bounds in the loader: taps outside the gradient read as zeros
     mask = dbp = None
@@ -952,7 +971,7 @@ def conv_x6_dgrad(gp, weight, stride: int, in_hw: tuple, out=None, relu_out=None
     call("ocppo_conv_x6", _stream(dev), 0, g.data_ptr(),
          _geom(QH, QW, 0, 0, 0, 0, TW * Cout), wc.data_ptr(), K, out.data_ptr(), C, M, N, K, 1,
          None, 0, og, tile, None, _geom(T - 1, TW - 1, OH, OW, Cout),
-         None if mask is None else mask.data_ptr(), None if dbp is None else dbp.data_ptr())
+         None if mask is None else mask.data_ptr(), None if dbp is None else dbp.data_ptr(), None)
     if dbp is not None:
         # row tiles, then stride classes, in order (f64, one rounding)
         db.copy_(dbp.view(-1, s * s, C).double().sum(0).sum(0))

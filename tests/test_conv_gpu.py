@@ -51,11 +51,13 @@ def _check(y, ref, scale, lib):
 
 @pytest.mark.parametrize("name", list(LAYERS))
 @pytest.mark.parametrize("relu", [True, False])
-@pytest.mark.parametrize("splits", [True, False])
-def test_forward_bias_relu(name, relu, splits, monkeypatch):
-    """splits: these batches' few workgroups take K-split partials + ocppo_sum_splits_act (the
-    rollout's form); off: one product with bias + ReLU in its epilogue (the update's form)."""
-    monkeypatch.setattr(ops, "CONV_FWD_SPLITS", splits)
+@pytest.mark.parametrize("form", ["rows", "splits", "loop"])
+def test_forward_bias_relu(name, relu, form, monkeypatch):
+    """rows: tile 7, a 32-row tile per workgroup with its K steps split over 8 waves (the
+    rollout's form, ops.CONV_FWD_ROWS); splits: K-split partials + ocppo_sum_splits_act; loop: one
+    product with bias + ReLU in its epilogue (the update's form)."""
+    monkeypatch.setattr(ops, "CONV_FWD_ROWS", form == "rows")
+    monkeypatch.setattr(ops, "CONV_FWD_SPLITS", form == "splits")
     x, w, b, s = _operands(name)
     assert ops.conv_x6_ok(x, w, s)
     y = ops.conv_x6(x, w, b, s, relu)
@@ -315,3 +317,33 @@ def test_u8_first_conv_relu_backward_fused_into_the_weight_gradient(B):
     assert float(((db2.double() - db64).abs() / scale).max()) < 1e-6
     with pytest.raises(ValueError):
         ops.conv_x6_u8(src, idx, w, b, s, False, mbits=mb)  # a mask needs the ReLU
+
+
+@pytest.mark.parametrize("name,B", [("conv2", 256), ("conv3", 256), ("conv2", 1), ("conv3", 32)])
+def test_forward_rows_tile_at_rollout_sizes(name, B, monkeypatch):
+    """ocppo_conv_x6 tile 7 at the rollout's batch (256 envs: 20736 / 12544 rows) and at odd
+    small batches: against float64, and against the tile loop (the update's form) to f32 level."""
+    _, C, H, Cout, K, s = LAYERS[name]
+    g = torch.Generator(device=DEV).manual_seed(31)
+    x = torch.rand(B, C, H, H, device=DEV, generator=g).contiguous(memory_format=CL)
+    w = ((torch.rand(Cout, C, K, K, device=DEV, generator=g) * 2 - 1) / (C * K * K) ** 0.5
+         ).contiguous(memory_format=CL)
+    b = (torch.rand(Cout, device=DEV, generator=g) * 2 - 1) * 0.1
+    OH = (H - K) // s + 1
+    if (B * OH * OH) % 32:
+        pytest.skip("rows not a multiple of 32")
+    y = ops.conv_x6(x, w, b, s, True)
+    x64, w64, b64 = x.double().cpu(), w.double().cpu(), b.double().cpu()
+    ref = F.conv2d(x64, w64, b64, stride=s).clamp_min(0)
+    scale = F.conv2d(x64.abs(), w64.abs(), b64.abs(), stride=s)
+    _check(y, ref, scale, F.conv2d(x, w, b, stride=s).clamp_min(0))
+    assert torch.equal(y, ops.conv_x6(x, w, b, s, True))
+    # the weight pre-split once (the rollout's form, agents._planes_infer): the same pieces, so
+    # the same bits
+    wm = w.permute(0, 2, 3, 1).reshape(Cout, -1)
+    ops.WeightPlanes(fwd=(wm,)).refresh()
+    assert torch.equal(y, ops.conv_x6(x, w, b, s, True, w_planes=wm._ocppo_planes["fwd"]))
+    if ops.conv_x6_ok(x, w, s):
+        monkeypatch.setattr(ops, "CONV_FWD_ROWS", False)
+        loop = ops.conv_x6(x, w, b, s, True)
+        assert float(((loop.double() - y.double()).abs().cpu() / scale.clamp_min(1e-300)).max()) < 1e-6
