@@ -498,8 +498,9 @@ OCPPO_API int ocppo_gemm_x6_gather(ocppo_stream_t stream, const float* a, int64_
  * tile 7 (mode 0, ABI 27): few rows (the rollout's batch) -- a 32-row tile per workgroup with its
  * K steps split over 8 waves and summed in wave order; N = 32 or 64, 32 | M, splits 1, no
  * out_geom / pad / mask; the same x6 products per K step, grouped differently over K (not the
- * other tiles' bits). w_planes (tile 7 only, else null; 16-B aligned): w's three bf16 pieces
- * [3, N, K] (ocppo_split_planes of w), read instead of splitting w in every workgroup.
+ * other tiles' bits). w_planes (mode 0, else null; 16-B aligned, K % 8 == 0): w's three bf16
+ * pieces [3, N, K] (ocppo_split_planes of w), read instead of splitting w in every workgroup
+ * (the same pieces: the same bits).
  * ------------------------------------------------------------------------------------------- */
 OCPPO_API int ocppo_conv_x6(ocppo_stream_t stream, int mode, const float* x, const int64_t* geom,
                             const float* w, int64_t ldw, float* c, int64_t ldc, int64_t M,

@@ -642,8 +642,9 @@ class _ConvX6(torch.autograd.Function):
     def forward(ctx, x, w, b, stride, relu: bool, box=None, below=None):
         B, Cin, H, W = x.shape
         Cout = w.shape[0]
+        wp = _planes(w, "fwd") if CONV_X6_PLANES else None  # refreshed by the trainer
         y = ops.timed(f"conv_x6_{B}x{Cin}x{H}_{Cout}",
-                      lambda: ops.conv_x6(x, w, b, stride, relu))
+                      lambda: ops.conv_x6(x, w, b, stride, relu, w_planes=wp))
         ctx.conv = (stride, relu)
         ctx.b = b
         ctx.box, ctx.below = box, below
@@ -780,6 +781,11 @@ CONV_X6_U8 = True
 # the first layer's [B OH OW, 32] gradient (read twice, written once)
 U8_WGRAD_RELU = True
 
+
+# The update's convolution forwards read their weight pre-split into bf16 planes (one
+# ocppo_split_planes launch per minibatch for all of them, trainer._weight_planes) instead of
+# splitting it in every workgroup
+CONV_X6_PLANES = True
 
 # NatureCNN convolutions on this package's implicit GEMMs (ops.conv_x6, x6 products: no MIOpen,
 # deterministic by construction), in the rollout forward and the update; shapes it does not take

@@ -807,9 +807,9 @@ __device__ __forceinline__ void x6_unit(const X6Args& g, unsigned char* lds, int
 
   // operand loads of K step k0 into a register set (GATH: through the gathered row offsets)
   static_assert(GATH == 0 || (GATH == 1 && AKC) || (GATH == 2 && !BKC && !BPL) ||
-                    (GATH == 3 && AKC && !BPL) || (GATH == 4 && !BKC && !BPL) ||
+                    (GATH == 3 && AKC) || (GATH == 4 && !BKC && !BPL) ||
                     (GATH == 5 && AKC && !BPL) || (GATH == 6 && !BKC && !BPL) ||
-                    (GATH == 7 && AKC && !BPL),
+                    (GATH == 7 && AKC),
                 "gather modes");
   constexpr bool kKRows = GATH == 4 || GATH == 6;  // B's K index walks convolution rows
   int64_t roffA[(GATH == 1 || GATH == 3 || GATH == 5 || GATH == 7) ? SA::kPer : 1][4];
@@ -2047,6 +2047,13 @@ static void launch_conv_t(hipStream_t s, X6Args& g) {
   g.tiles_m = g.M / (16 * FM * WGM);
   g.tiles_n = g.N / (16 * FN * WGN);
   constexpr bool KC = GATH == 3 || GATH == 5 || GATH == 7;  // rows forms: k-contiguous; wgrad: neither
+  if constexpr (GATH == 3 || GATH == 7) {
+    if (g.bpl) {  // the weight pre-split (ocppo_split_planes): B's stash is a copy, no split
+      hipLaunchKernelGGL((gemm_x6_kernel<FM, FN, WGM, WGN, true, true, false, true, true, GATH>),
+                         dim3(g.units), dim3(64 * WGM * WGN), 0, s, g);
+      return;
+    }
+  }
   hipLaunchKernelGGL((gemm_x6_kernel<FM, FN, WGM, WGN, KC, KC, false, true, false, GATH>),
                      dim3(g.units), dim3(64 * WGM * WGN), 0, s, g);
 }
@@ -2709,7 +2716,9 @@ extern "C" int ocppo_conv_x6(ocppo_stream_t stream, int mode, const float* x, co
       hipLaunchKernelGGL((conv_x6_rows_kernel<2, false>), grid, block, 0, s, g);
     return check_launch("ocppo_conv_x6 (tile 7)");
   }
-  OCPPO_REQUIRE(!w_planes, "ocppo_conv_x6: w_planes needs tile 7");
+  OCPPO_REQUIRE(!w_planes || (mode == 0 && reinterpret_cast<uintptr_t>(w_planes) % 16 == 0 &&
+                                K % 8 == 0),
+                "ocppo_conv_x6: w_planes needs mode 0 (16-B aligned, K %% 8 == 0)");
   const X6Tile tc = kConvTiles[tile];
   const int64_t bm = 16 * tc.fm * tc.wgm, bn = 16 * tc.fn * tc.wgn;
   OCPPO_REQUIRE(M >= bm && N >= bn && M % bm == 0 && N % bn == 0 && K >= kX6BK && K % kX6BK == 0 &&
@@ -2757,6 +2766,11 @@ extern "C" int ocppo_conv_x6(ocppo_stream_t stream, int mode, const float* x, co
     g.c = c;
     g.ldc = ldc;
     g.split_c = M * N;  // splits > 1: partials [splits, M, N] (ocppo_sum_splits_act adds them)
+    if (w_planes) {  // B = w pre-split into three bf16 planes [3, N, K]
+      g.bpl = w_planes;
+      g.bpl_ld = K;
+      g.bpl_ps = N * K;
+    }
     g.bias = bias;
     g.relu = relu ? 1 : 0;
     if (mask) {  // the layer below's ReLU backward: c = mask > 0 ? acc : 0, column sums -> dbp

@@ -798,11 +798,21 @@ def _bounds(dev, x=None, u8=None):
             _tail(u8) if u8 is not None else 0, u8.shape[0] if u8 is not None else 0)
 
 
+def _conv_planes_ptr(w_planes, N: int, K: int, dev):
+    if w_planes is None:
+        return None
+    if w_planes.dtype != torch.bfloat16 or tuple(w_planes.shape) != (3, N, K) or \
+            not w_planes.is_contiguous():
+        raise ValueError(f"conv_x6: w_planes must be contiguous bf16 [3, {N}, {K}]")
+    return _check(w_planes, "w_planes", torch.bfloat16, dev)
+
+
 def conv_x6(x, weight, bias=None, stride: int = 1, relu: bool = True, out=None, w_planes=None):
     """act(conv2d(x, weight) + bias) (architectures/ppo.py:20-31's Conv2d + ReLU) on ocppo_conv_x6:
     channels_last f32 x [B, C, H, W], weight [Cout, C, KH, KW] -> channels_last [B, Cout, OH, OW]
     (no autograd; agents._ConvX6 is the autograd form). w_planes: the weight's [Cout, KH KW C]
-    matrix pre-split into bf16 [3, Cout, KH KW C] (used by the few-rows form only)."""
+    matrix pre-split into bf16 [3, Cout, KH KW C] (ocppo_split_planes: the same pieces as the
+    in-kernel split, so the same bits)."""
     if not conv_x6_ok(x, weight, stride):
         raise ValueError(f"conv_x6: unsupported shapes x {tuple(x.shape)}, weight "
                          f"{tuple(weight.shape)}, stride {stride} (conv_x6_ok)")
@@ -821,22 +831,20 @@ def conv_x6(x, weight, bias=None, stride: int = 1, relu: bool = True, out=None, 
     geom = _geom(OH, OW, H * W * C, s * W * C, s * C, W * C, KW * C)
     if CONV_FWD_ROWS and M <= CONV_FWD_ROWS_MAX and Cout in (32, 64) and M % 32 == 0:
         # few rows (the rollout's batch): K steps split over the waves of a workgroup
-        if w_planes is not None and (w_planes.dtype != torch.bfloat16 or tuple(w_planes.shape)
-                                     != (3, Cout, K) or not w_planes.is_contiguous()):
-            raise ValueError("conv_x6: w_planes must be contiguous bf16 [3, Cout, KH KW C]")
         call("ocppo_conv_x6", _stream(dev), 0, x.data_ptr(), geom, wm.data_ptr(), K,
              out.data_ptr(), Cout, M, Cout, K, 1, _opt(bias, "bias", f, dev, Cout),
              int(bool(relu)), None, 7, None, None, None, None,
-             None if w_planes is None else _check(w_planes, "w_planes", torch.bfloat16, dev))
+             _conv_planes_ptr(w_planes, Cout, K, dev))
         return out
     tile = _conv_fwd_tile(M, Cout)
     bm, bn = _CONV_TILES[tile]
     S = _conv_fwd_splits((M // bm) * (Cout // bn), K // 32)
     _bounds(dev, x)
+    wpp = _conv_planes_ptr(w_planes, Cout, K, dev)
     if S == 1:
         call("ocppo_conv_x6", _stream(dev), 0, x.data_ptr(), geom, wm.data_ptr(), K,
              out.data_ptr(), Cout, M, Cout, K, 1, _opt(bias, "bias", f, dev, Cout),
-             int(bool(relu)), None, tile, None, None, None, None, None)
+             int(bool(relu)), None, tile, None, None, None, None, wpp)
         return out
     # few rows (the rollout's batch): K-split partials, then bias + ReLU on their ordered sum
     key = ("fwd", str(dev), S, M, Cout)
@@ -844,7 +852,7 @@ def conv_x6(x, weight, bias=None, stride: int = 1, relu: bool = True, out=None, 
         _CONV_PARTS[key] = torch.empty((S, M, Cout), dtype=f, device=dev)
     part = _CONV_PARTS[key]
     call("ocppo_conv_x6", _stream(dev), 0, x.data_ptr(), geom, wm.data_ptr(), K, part.data_ptr(),
-         Cout, M, Cout, K, S, None, 0, None, tile, None, None, None, None, None)
+         Cout, M, Cout, K, S, None, 0, None, tile, None, None, None, None, wpp)
     call("ocppo_sum_splits_act", _stream(dev), part.data_ptr(), S, M, Cout,
          _opt(bias, "bias", f, dev, Cout), int(bool(relu)), out.data_ptr())
     return out
@@ -948,7 +956,8 @@ def conv_x6_dgrad(gp, weight, stride: int, in_hw: tuple, out=None, relu_out=None
     # the classes stacked class-major: B = [s s C, K] -- one gather through a cached index into
     # the weight's memory (its [Cout, KH, KW, C] order when channels_last) instead of s^2 flips,
     # a stack and a layout copy per call
-    wc = _dgrad_weight(weight, s)
+    wc, wcp = _dgrad_weight(weight, s, planes=CONV_DGRAD_PLANES)
+    wpp = None if wcp is None else wcp.data_ptr()
     og = None if s == 1 else _geom(H * W * C, s * W * C, s * C, 0, C, s, W * C, C)
     if CONV_DGRAD_PAD_COPY or tile not in (2, 3, 5, 6):
         gpad = torch.nn.functional.pad(g, (0, 0, TW - 1, TW - 1, T - 1, T - 1))
@@ -957,7 +966,7 @@ def conv_x6_dgrad(gp, weight, stride: int, in_hw: tuple, out=None, relu_out=None
         _bounds(dev, gpad)
         call("ocppo_conv_x6", _stream(dev), 0, gpad.data_ptr(),
              _geom(QH, QW, Hp * Wp * Cout, Wp * Cout, Cout, Wp * Cout, TW * Cout), wc.data_ptr(),
-             K, out.data_ptr(), C, M, N, K, 1, None, 0, og, tile, None, None, None, None, None)
+             K, out.data_ptr(), C, M, N, K, 1, None, 0, og, tile, None, None, None, None, wpp)
         return out
     # the padding as bounds in the loader: taps outside the gradient read as zeros
     mask = dbp = None
@@ -971,7 +980,7 @@ def conv_x6_dgrad(gp, weight, stride: int, in_hw: tuple, out=None, relu_out=None
     call("ocppo_conv_x6", _stream(dev), 0, g.data_ptr(),
          _geom(QH, QW, 0, 0, 0, 0, TW * Cout), wc.data_ptr(), K, out.data_ptr(), C, M, N, K, 1,
          None, 0, og, tile, None, _geom(T - 1, TW - 1, OH, OW, Cout),
-         None if mask is None else mask.data_ptr(), None if dbp is None else dbp.data_ptr(), None)
+         None if mask is None else mask.data_ptr(), None if dbp is None else dbp.data_ptr(), wpp)
     if dbp is not None:
         # row tiles, then stride classes, in order (f64, one rounding)
         db.copy_(dbp.view(-1, s * s, C).double().sum(0).sum(0))
@@ -979,11 +988,16 @@ def conv_x6_dgrad(gp, weight, stride: int, in_hw: tuple, out=None, relu_out=None
 
 
 _DG_IDX: dict = {}
+_DG_BUF: dict = {}
+# the data gradients' B operand (the stride classes' flipped weights) pre-split into bf16 planes
+# once per call (ocppo_split_planes) instead of in every workgroup of the product
+CONV_DGRAD_PLANES = True
 
 
-def _dgrad_weight(weight, s: int):
-    """conv_x6_dgrad's B operand [s s C, T TW Cout]: row (py, px, c), column (t, tw, co) =
-    weight[co, c, py + s (T - 1 - t), px + s (TW - 1 - tw)], gathered in one launch."""
+def _dgrad_weight(weight, s: int, planes: bool = False):
+    """(wc, its bf16 planes or None): conv_x6_dgrad's B operand [s s C, T TW Cout], row (py, px,
+    c), column (t, tw, co) = weight[co, c, py + s (T - 1 - t), px + s (TW - 1 - tw)], gathered in
+    one launch into a buffer kept per weight (and split into planes by one more)."""
     Cout, C, KH, KW = weight.shape
     mem = weight.permute(0, 2, 3, 1)  # a view of the memory when channels_last
     key = (str(weight.device), Cout, C, KH, KW, s)
@@ -994,7 +1008,20 @@ def _dgrad_weight(weight, s: int):
                            for py in range(s) for px in range(s)])
         idx = idx.reshape(s * s * C, -1).to(weight.device)
         _DG_IDX[key] = idx
-    return mem.reshape(-1)[idx]
+    bkey = key + (weight.data_ptr(),)
+    ent = _DG_BUF.get(bkey)
+    if ent is None:
+        buf = torch.empty(idx.shape, dtype=torch.float32, device=weight.device)
+        ent = [buf, None]
+        _DG_BUF[bkey] = ent
+    buf = ent[0]
+    torch.index_select(mem.reshape(-1), 0, idx.view(-1), out=buf.view(-1))
+    if not planes or buf.shape[1] % 8:
+        return buf, None
+    if ent[1] is None:
+        ent[1] = WeightPlanes(fwd=(buf,))
+    ent[1].refresh()
+    return buf, buf._ocppo_planes["fwd"]
 
 
 # the data gradient over a zero-padded copy of the output gradient (F.pad: a fill and a copy per

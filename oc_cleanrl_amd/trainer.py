@@ -512,6 +512,24 @@ class PPOTrainer:
         the in-kernel split. Built at the first minibatch (the frame-dedup capacity, the rows the
         encoder sees, is known by then); None when no product qualifies."""
         a, ag = self.args, self.agent
+        if (a.x6_weight_planes and agents.CONV_X6_PLANES and self.dev.type == "cuda" and
+                self.pixels and isinstance(getattr(ag, "network", None), nn.Sequential)):
+            # NatureCNN: the convolutions after the first (which reads the u8 stacks) take their
+            # weight's [Cout, KH KW C] matrix pre-split (ocppo_conv_x6 w_planes)
+            views = []
+            convs = [m for m in ag.network if isinstance(m, nn.Conv2d)]
+            for m in convs[1:]:
+                w = m.weight
+                v = w.permute(0, 2, 3, 1).reshape(w.shape[0], -1)
+                if w.is_cuda and v.data_ptr() == w.data_ptr() and v.is_contiguous() and \
+                        v.shape[1] % 8 == 0:
+                    views.append((w, v))
+            if not views:
+                return None
+            wp = ops.WeightPlanes(fwd=[v for _, v in views])
+            for w, v in views:
+                w._ocppo_planes = v._ocppo_planes
+            return wp
         if not (a.x6_gemm and a.x6_weight_planes and isinstance(ag, PPObj) and self.dev.type == "cuda"):
             return None
         enc_rows = self.planner.cap if self.frame_dedup else self.M * self.obs_shape[0]

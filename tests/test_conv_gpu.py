@@ -347,3 +347,23 @@ def test_forward_rows_tile_at_rollout_sizes(name, B, monkeypatch):
         monkeypatch.setattr(ops, "CONV_FWD_ROWS", False)
         loop = ops.conv_x6(x, w, b, s, True)
         assert float(((loop.double() - y.double()).abs().cpu() / scale.clamp_min(1e-300)).max()) < 1e-6
+
+
+@pytest.mark.parametrize("name", ["conv2", "conv3"])
+def test_pre_split_weight_planes_are_bitwise_the_in_kernel_split(name, monkeypatch):
+    """The forward's weight and the data gradient's class weights pre-split into bf16 planes
+    (ocppo_conv_x6 w_planes, ocppo_split_planes: the update's form) give the same bits as the
+    tile loop splitting them in every workgroup."""
+    monkeypatch.setattr(ops, "CONV_FWD_ROWS", False)
+    x, w, b, s = _operands(name, 41)
+    Cout = w.shape[0]
+    wm = w.permute(0, 2, 3, 1).reshape(Cout, -1)
+    ops.WeightPlanes(fwd=(wm,)).refresh()
+    y = ops.conv_x6(x, w, b, s, True)
+    assert torch.equal(y, ops.conv_x6(x, w, b, s, True, w_planes=wm._ocppo_planes["fwd"]))
+    g = torch.Generator(device=DEV).manual_seed(42)
+    gp = (torch.rand(y.shape, device=DEV, generator=g) * 2 - 1).contiguous(memory_format=CL)
+    monkeypatch.setattr(ops, "CONV_DGRAD_PLANES", False)
+    dx = ops.conv_x6_dgrad(gp, w, s, tuple(x.shape[2:]))
+    monkeypatch.setattr(ops, "CONV_DGRAD_PLANES", True)
+    assert torch.equal(dx, ops.conv_x6_dgrad(gp, w, s, tuple(x.shape[2:])))
