@@ -829,10 +829,12 @@ def _conv_x6(x, conv, relu: bool):
                      lambda: ops.conv_x6(x, conv.weight, conv.bias, s, relu, w_planes=wp))
 
 
-# The rollout's convolutions (ops.conv_x6's few-rows form) read their weights pre-split into the
-# three bf16 pieces once per rollout (ocppo_split_planes) instead of splitting them in every
-# workgroup
-CONV_ROWS_PLANES = True
+# The rollout's convolutions (ops.conv_x6's few-rows form) reading their weights pre-split into
+# the three bf16 pieces once per rollout (ocppo_split_planes) instead of splitting them in every
+# workgroup: measured SLOWER in that kernel (conv2 / conv3 at 256 envs 24.8 / 19.3 us against
+# 21.2 / 16.1 us: the planes' 6 B per element against 4, read straight from L2 without an LDS
+# stage; tools/exp_conv_rows.py, profiles/r06/config3/rows/), so off
+CONV_ROWS_PLANES = False
 _PLANES_INFER: dict = {}
 
 
