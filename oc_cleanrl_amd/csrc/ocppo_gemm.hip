@@ -156,23 +156,27 @@ struct X6Args {
 // is counted and recorded (the first one) and the load reads offset 0 instead, so a bad index
 // shows as a record, not as a fault. Compiled out otherwise (the identity).
 enum X6BoundKind { kBndX = 1, kBndImg = 2, kBndU8Row = 3, kBndU8 = 4 };
-__device__ __forceinline__ int64_t x6_bnd(const X6Args& g, int kind, int64_t v, int64_t need,
-                                          int64_t lim) {
+__device__ __forceinline__ int64_t bnd_check(uint32_t* bnd, int kind, int64_t v, int64_t need,
+                                             int64_t lim) {
 #ifdef OCPPO_X6_BOUNDS
-  if (g.bnd != nullptr && (v < 0 || v + need > lim)) {
-    if (__hip_atomic_fetch_add(g.bnd, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
-      g.bnd[1] = static_cast<uint32_t>(kind);
-      g.bnd[2] = static_cast<uint32_t>(static_cast<uint64_t>(v));
-      g.bnd[3] = static_cast<uint32_t>(static_cast<uint64_t>(v) >> 32);
-      g.bnd[4] = static_cast<uint32_t>(static_cast<uint64_t>(lim));
-      g.bnd[5] = static_cast<uint32_t>(static_cast<uint64_t>(lim) >> 32);
+  if (bnd != nullptr && (v < 0 || v + need > lim)) {
+    if (__hip_atomic_fetch_add(bnd, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+      bnd[1] = static_cast<uint32_t>(kind);
+      bnd[2] = static_cast<uint32_t>(static_cast<uint64_t>(v));
+      bnd[3] = static_cast<uint32_t>(static_cast<uint64_t>(v) >> 32);
+      bnd[4] = static_cast<uint32_t>(static_cast<uint64_t>(lim));
+      bnd[5] = static_cast<uint32_t>(static_cast<uint64_t>(lim) >> 32);
     }
     return 0;
   }
 #else
-  (void)g, (void)kind, (void)need, (void)lim;
+  (void)bnd, (void)kind, (void)need, (void)lim;
 #endif
   return v;
+}
+__device__ __forceinline__ int64_t x6_bnd(const X6Args& g, int kind, int64_t v, int64_t need,
+                                          int64_t lim) {
+  return bnd_check(g.bnd, kind, v, need, lim);
 }
 
 // q = x / d for 0 <= x < 2^24, d >= 1 (f32 reciprocal estimate, corrected to the exact quotient)
@@ -1773,8 +1777,13 @@ static void x6_bounds_args(X6Args& g) {
   g.bnd_u8 = g_x6_bnd_u8;
   g.bnd_u8rows = g_x6_bnd_u8rows;
 }
+static void img_bounds_args(uint32_t*& bnd, int64_t& rows) {
+  bnd = g_x6_bnd;
+  rows = g_x6_bnd_u8rows;
+}
 #else
 static void x6_bounds_args(X6Args&) {}
+static void img_bounds_args(uint32_t*&, int64_t&) {}
 #endif
 
 #ifdef OCPPO_X6_STAMPS
@@ -2156,6 +2165,8 @@ struct ConvImgArgs {
   int relu;
   float cdiv;
   uint32_t* mbits;    // [B * P] or null: bit co of word r = out[r, co] > 0 (the ReLU mask)
+  uint32_t* bnd;      // bounds-check builds: the violation record (else null) and the stack rows
+  int64_t bnd_rows;
 };
 
 __device__ __forceinline__ uint32_t img_bf16x2(uint32_t v, int half) {
@@ -2198,7 +2209,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_u8_img_kernel(ConvImgArg
   // vmcnt wait, which would drain the LDS-DMA in flight) inside the loop
   auto window = [&](int it0) -> int64_t {
     const int bb = b + (it0 + lane) * grid;
-    return bb < a.B ? a.idx[bb] : 0;
+    return bb < a.B ? bnd_check(a.bnd, kBndU8Row, a.idx[bb], 1, a.bnd_rows) : 0;
   };
   auto row_of = [&](int64_t win, int l) -> int64_t {
     const uint64_t u = static_cast<uint64_t>(win);
@@ -2336,6 +2347,8 @@ struct ConvWgImgArgs {
   int B;
   const uint32_t* mbits;  // [B P] or null
   float* dbp;             // [4 grid, 32] or null
+  uint32_t* bnd;          // bounds-check builds (as ConvImgArgs)
+  int64_t bnd_rows;
 };
 
 template <int C, int H, int W, int OH, int OW>
@@ -2364,7 +2377,7 @@ __global__ __launch_bounds__(256, 1) void conv_u8_wgrad_img_kernel(ConvWgImgArgs
   uint32_t raw[C][9];
   auto load_raw = [&](int bb) {
     const bool ok = bb < a.B && t < kItems;
-    const int64_t row = bb < a.B ? a.idx[bb] : 0;
+    const int64_t row = bb < a.B ? bnd_check(a.bnd, kBndU8Row, a.idx[bb], 1, a.bnd_rows) : 0;
     const uint8_t* sp = a.src + row * bytes + iy * W;
 #pragma unroll
     for (int c = 0; c < C; ++c)
@@ -2568,7 +2581,8 @@ __global__ __launch_bounds__(64 * kRowsNW) void conv_x6_rows_kernel(X6Args g) {
     const int64_t seg = x6_cv_seg(g, k);
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const float4* p = reinterpret_cast<const float4*>(x + arow[i] + seg);
+      const float4* p = reinterpret_cast<const float4*>(x + x6_bnd(g, kBndX, arow[i] + seg, 8,
+                                                                   g.bnd_x));
       a[i][0] = p[0];
       a[i][1] = p[1];
     }
@@ -2696,6 +2710,7 @@ extern "C" int ocppo_conv_x6(ocppo_stream_t stream, int mode, const float* x, co
     g.cv_xs = xs;
     g.cv_segs = segs;
     g.cv_gseg = (int)gseg;
+    x6_bounds_args(g);
     if (w_planes) {
       OCPPO_REQUIRE(reinterpret_cast<uintptr_t>(w_planes) % 16 == 0,
                     "ocppo_conv_x6: w_planes must be 16-B aligned");
@@ -2879,7 +2894,8 @@ extern "C" int ocppo_conv_x6_u8(ocppo_stream_t stream, int mode, const uint8_t* 
                   "ocppo_conv_x6_u8: tile 7 takes mbits (16-B aligned, with relu) and no dbp / db");
     ConvImgArgs ia{src, idx, w, ldw, bias, c, static_cast<int>(M / P), static_cast<int>(H),
                    static_cast<int>(W), static_cast<int>(OW), static_cast<int>(P), relu ? 1 : 0,
-                   divisor, mbits};
+                   divisor, mbits, nullptr, 0};
+    img_bounds_args(ia.bnd, ia.bnd_rows);
     clear_stale_error();
     const size_t ibuf = static_cast<size_t>((bytes + kImgChunk - 1) / kImgChunk) * kImgChunk;
     const int grid = conv_u8_img_grid(ia.B);
@@ -2907,7 +2923,8 @@ extern "C" int ocppo_conv_x6_u8(ocppo_stream_t stream, int mode, const uint8_t* 
     OCPPO_REQUIRE((dbp == nullptr) == (db == nullptr) &&
                       (!mbits || reinterpret_cast<uintptr_t>(mbits) % 16 == 0),
                   "ocppo_conv_x6_u8: tile 8 takes dbp and db together, a 16-B aligned mbits");
-    ConvWgImgArgs wa{src, idx, w, ldw, c, static_cast<int>(K / P), mbits, dbp};
+    ConvWgImgArgs wa{src, idx, w, ldw, c, static_cast<int>(K / P), mbits, dbp, nullptr, 0};
+    img_bounds_args(wa.bnd, wa.bnd_rows);
     clear_stale_error();
     hipStream_t s = as_stream(stream);
     hipLaunchKernelGGL((conv_u8_wgrad_img_kernel<4, 84, 84, 20, 20>),

@@ -831,6 +831,7 @@ def conv_x6(x, weight, bias=None, stride: int = 1, relu: bool = True, out=None, 
     geom = _geom(OH, OW, H * W * C, s * W * C, s * C, W * C, KW * C)
     if CONV_FWD_ROWS and M <= CONV_FWD_ROWS_MAX and Cout in (32, 64) and M % 32 == 0:
         # few rows (the rollout's batch): K steps split over the waves of a workgroup
+        _bounds(dev, x)
         call("ocppo_conv_x6", _stream(dev), 0, x.data_ptr(), geom, wm.data_ptr(), K,
              out.data_ptr(), Cout, M, Cout, K, 1, _opt(bias, "bias", f, dev, Cout),
              int(bool(relu)), None, 7, None, None, None, None,

@@ -226,16 +226,22 @@ def test_u8_weight_gradient_index_slice_ends_before_a_sentinel():
 
 @pytest.mark.skipif(not ops.X6_BOUNDS, reason="bounds-check build only (OCPPO_LIB=... "
                     "-DOCPPO_X6_BOUNDS, tools/run_bounds_check.sh)")
-def test_bounds_build_records_an_out_of_range_stack_row():
+@pytest.mark.parametrize("form", ["image", "loop", "wgrad_image", "wgrad_loop"])
+def test_bounds_build_records_an_out_of_range_stack_row(form):
     """Positive control of the bounds-check build: an index past the u8 stacks' rows is recorded
-    (kind 3, the index, the limit) instead of being read (the load falls back to offset 0)."""
+    (kind 3, the index, the limit) instead of being read (the load falls back to row 0), in the
+    image-staged kernels (tiles 7 / 8) and the tile loop's gathers (tiles 0 / 1)."""
     src = _frames(R=20, seed=14)
     _, w, b, s = _operands("conv1", 15)
     idx = torch.arange(16, device=DEV)
     idx[5] = 20  # one past the last stack
     rec = ops.bounds_record(DEV)
     rec.zero_()
-    ops.conv_x6_u8(src, idx, w, b, s, True)
+    if form.startswith("wgrad"):
+        gp = torch.rand(16 * 400, 32, device=DEV)
+        ops.conv_x6_u8_wgrad(gp, src, idx, (8, 8), s, tile=8 if form == "wgrad_image" else 1)
+    else:
+        ops.conv_x6_u8(src, idx, w, b, s, True, tile=7 if form == "image" else 0)
     torch.cuda.synchronize()
     r = rec.cpu().tolist()
     rec.zero_()
