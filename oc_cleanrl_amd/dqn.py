@@ -155,6 +155,10 @@ class QNetworkObj(Predictor):
     predict = QNetwork.predict
 
 
+# The train step's target-network forward on a side stream, concurrent with the online forward
+# (DQNTrainer._train_step; captured into the chunk's hipGraph as a fork / join)
+TARGET_SIDE_STREAM = True
+
 # The acting step's Q head + epsilon-greedy choice as one HIP launch (ops.q_head_epsilon_greedy).
 FUSED_ACT = True
 # ... and with an object-frame synthetic env, the whole rest of the step (env, store +
@@ -239,6 +243,7 @@ class DQNTrainer:
                       "rewards": torch.zeros((B, 1), device=dev),
                       "dones": torch.zeros((B, 1), device=dev)}
         self.dq = torch.zeros((B, self.A), dtype=f32, device=dev)
+        self.side = torch.cuda.Stream(self.dev) if self.dev.type == "cuda" else None
         self.td_stats = torch.zeros(2, dtype=f32, device=dev)
         self.duration = a.exploration_fraction * a.total_timesteps
         # acting: the Q head and the epsilon-greedy choice in one launch
@@ -301,9 +306,21 @@ class DQNTrainer:
         """:377-392 — sample, TD target + MSE (fused), backward, Adam."""
         a = self.args
         d = self.rb.sample(a.batch_size, out=self.batch)
-        with torch.no_grad():
-            q_next = _q_forward(self.target, d["next_observations"])
-        q = _q_forward(self.q, d["observations"])
+        if TARGET_SIDE_STREAM and self.side is not None:
+            # the target network's forward on a side stream beside the online forward: two
+            # independent launch chains (5 launches each) of one sampled batch, joined before the
+            # TD loss -- the same kernels on the same operands, so the same values
+            main = torch.cuda.current_stream(self.dev)
+            self.side.wait_stream(main)
+            with torch.cuda.stream(self.side), torch.no_grad():
+                q_next = _q_forward(self.target, d["next_observations"])
+            q = _q_forward(self.q, d["observations"])
+            main.wait_stream(self.side)
+            q_next.record_stream(main)
+        else:
+            with torch.no_grad():
+                q_next = _q_forward(self.target, d["next_observations"])
+            q = _q_forward(self.q, d["observations"])
         ops.td_loss_fwd_bwd(q.detach(), q_next, d["actions"], d["rewards"], d["dones"], a.gamma,
                             dq=self.dq, stats=self.td_stats)
         if not self.direct_grads:
