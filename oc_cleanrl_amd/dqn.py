@@ -156,8 +156,9 @@ class QNetworkObj(Predictor):
 
 
 # The train step's target-network forward on a side stream, concurrent with the online forward
-# (DQNTrainer._train_step; captured into the chunk's hipGraph as a fork / join)
-TARGET_SIDE_STREAM = True
+# (DQNTrainer._train_step; captured into the chunk's hipGraph as a fork / join): measured slower
+# (config 5 11.3k vs 12.4k env steps/s, profiles/r06/config5_side_stream/), so off
+TARGET_SIDE_STREAM = False
 
 # The acting step's Q head + epsilon-greedy choice as one HIP launch (ops.q_head_epsilon_greedy).
 FUSED_ACT = True
