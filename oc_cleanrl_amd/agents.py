@@ -333,7 +333,8 @@ class _LinearAct(torch.autograd.Function):
         # below = the box of the Linear+ReLU that produced x: its ReLU backward and bias-gradient
         # partials ride in this layer's dX GEMM (ops.dx_x6_relu, mask = x)
         ctx.below = None
-        if (x6 and below is not None and not below["premasked"] and chw is None
+        if (x6 and below is not None and not below["premasked"]
+                and (chw is None or below.get("conv"))
                 and x.requires_grad and _x6_dx_shape_ok(x.shape[0], wm.shape[0], x.shape[1])):
             below["premasked"] = True
             ctx.below = below
@@ -395,6 +396,21 @@ class _LinearAct(torch.autograd.Function):
         if ctx.below is None:
             return _dx(g, w, ctx.x6, ctx.pdx)
         x = ctx.saved_tensors[0]
+        if ctx.below.get("conv"):
+            # a convolution's ReLU output flattened in its (H, W, C) memory order: the bias
+            # gradient sums the masked gradient over rows and positions per channel C
+            C = ctx.chw[0]
+            b = ctx.below["bias"]
+            db = b.grad if _direct(b) else torch.empty_like(b)
+            if ops.dx_x6_ok(g, w):
+                gp, dbp = ops.dx_x6_relu(g, w, x, planes=ctx.pdx)
+                db.copy_(dbp.view(-1, C).double().sum(0))  # row tiles and positions, f64
+            else:
+                dx = _dx(g, w, ctx.x6, ctx.pdx).contiguous()
+                gp, _ = ops.relu_bias_grad(dx.view(-1, C), x.contiguous().view(-1, C), db=db)
+                gp = gp.view(dx.shape)
+            ctx.below["db"] = db
+            return gp
         if ops.dx_x6_ok(g, w):
             gp, dbp = ops.dx_x6_relu(g, w, x, mbits=ctx.below.get("mbits"), planes=ctx.pdx)
             ctx.below["dbp"] = (dbp, dbp.shape[0])  # relu_bias_grad_partial's (partials, chunks)
@@ -678,7 +694,7 @@ class _ConvX6(torch.autograd.Function):
             gp = gp2.view(B, OH, OW, C).permute(0, 3, 1, 2)
             hw = (x.shape[2], x.shape[3])
             below = ctx.below
-            if below is not None and ops.conv_x6_dgrad_fuses_relu(
+            if below is not None and CONV_DGRAD_RELU and ops.conv_x6_dgrad_fuses_relu(
                     B * (hw[0] // stride) * (hw[1] // stride), x.shape[1], stride):
                 # the layer below's ReLU backward + bias gradient in this dX's epilogue
                 bb = below["bias"]
@@ -811,12 +827,23 @@ def _conv_x6_ok(x, conv) -> bool:
 # stride classes' scattered rows costs more than the streaming pass it removes): off by default
 CONV_DGRAD_RELU = False
 
+# The last convolution's ReLU backward and bias gradient in the dX epilogue of the Linear that
+# reads its flattened channels_last output (NatureCNN's 3136 -> 512; ops.dx_x6_relu with the
+# activation as the mask, the bias gradient from the epilogue's column sums over rows and
+# positions in f64): no relu_bias_grad pass over that layer's gradient. Measured slower at config
+# 3 (519.4k vs 522.1k env steps/s: the masked, column-summing epilogue of the 128 x 64-tile dX
+# costs more than the 59 us streaming pass it removes; profiles/r06/config3/flat_dx/), so off
+CONV_RELU_IN_FLAT_DX = False
+
 
 def _conv_x6(x, conv, relu: bool):
     s = conv.stride[0]
     if torch.is_grad_enabled() and (x.requires_grad or conv.weight.requires_grad or
                                     conv.bias.requires_grad):
-        box = {"bias": conv.bias} if relu and CONV_DGRAD_RELU else None
+        # the box lets the consumer of this ReLU output take its backward: the next convolution's
+        # data gradient (CONV_DGRAD_RELU) or the flattened Linear's dX (CONV_RELU_IN_FLAT_DX)
+        box = ({"bias": conv.bias, "premasked": False, "conv": True}
+               if relu and (CONV_DGRAD_RELU or CONV_RELU_IN_FLAT_DX) else None)
         y = _ConvX6.apply(x, conv.weight, conv.bias, s, relu, box,
                           getattr(x, "_ocppo_cbox", None))
         if box is not None:
@@ -903,7 +930,7 @@ def _hip_linear_ok(x2, lin: nn.Linear) -> bool:
             (M <= 128 and (K <= 256 or (K <= 2048 and K % 16 == 0))) or M <= 8)
 
 
-def linear_act(x, lin: nn.Linear, relu: bool, chw=None, rows: bool = False):
+def linear_act(x, lin: nn.Linear, relu: bool, chw=None, rows: bool = False, below=None):
     """rows: the output's consumer walks it by rows (the frame scatter, frames.SCATTER_MBITS):
     its ReLU bitmask, if the forward writes one, in the row-major layout."""
     lead = x.shape[:-1]
@@ -916,7 +943,8 @@ def linear_act(x, lin: nn.Linear, relu: bool, chw=None, rows: bool = False):
             _direct(lin.bias):
         box = {"premasked": False, "bias": lin.bias, "rows": rows}
     y = _LinearAct.apply(x2, lin.weight, lin.bias, relu, box, chw,
-                         getattr(x, "_ocppo_box", None), getattr(x, "_ocppo_wslot", None))
+                         below if below is not None else getattr(x, "_ocppo_box", None),
+                         getattr(x, "_ocppo_wslot", None))
     y = y.view(*lead, y.shape[-1])
     if box is not None:
         y._ocppo_box = box
@@ -961,7 +989,9 @@ def linear_act_nhwc(x, lin: nn.Linear, relu: bool):
     NCHW-order flatten: same products and sums as the reference layer, columns visited in (H, W,
     C) order (the f32 GEMM's summation order over K differs accordingly)."""
     B, C, H, W = x.shape
-    return linear_act(x.permute(0, 2, 3, 1).reshape(B, H * W * C), lin, relu, (C, H, W))
+    below = getattr(x, "_ocppo_cbox", None) if CONV_RELU_IN_FLAT_DX else None
+    return linear_act(x.permute(0, 2, 3, 1).reshape(B, H * W * C), lin, relu, (C, H, W),
+                      below=below)
 
 
 # Inference (the rollout) through nn.Flatten -> nn.Linear on a channels_last activation (the

@@ -887,3 +887,30 @@ def test_rollout_flatten_linear_reads_the_nhwc_activation(dev):
             got2 = ag.trunk(x)
         torch.testing.assert_close(got2, ref2, rtol=1e-5, atol=1e-5)
         assert not torch.allclose(ref2, ref)
+
+
+def test_conv_relu_backward_in_the_flattened_linear_dx(dev, monkeypatch):
+    """agents.CONV_RELU_IN_FLAT_DX: the last convolution's ReLU backward and bias gradient ride
+    in the dX epilogue of the Linear reading its flattened channels_last output (ops.dx_x6_relu,
+    the activation as the mask) -- the gradients of the whole trunk match the unfused chain
+    (relu_bias_grad over that layer's gradient) to f32 level."""
+    from oc_cleanrl_amd import agents, ops
+    from oc_cleanrl_amd.agents import make_agent
+
+    torch.manual_seed(3)
+    ag = make_agent("PPO", (4, 84, 84), 4, dev).to(dev).to(memory_format=torch.channels_last)
+    ops.FlatAdam(ag.parameters(), lr=1e-4)  # in-place grads, as in the trainer
+    x = torch.randint(0, 256, (2048, 4, 84, 84), device=dev).float().contiguous(
+        memory_format=torch.channels_last)
+    g = torch.randn(2048, 512, device=dev)
+    grads = []
+    for on in (True, False):
+        monkeypatch.setattr(agents, "CONV_RELU_IN_FLAT_DX", on)
+        for p in ag.parameters():
+            p.grad.zero_()
+        h = ag.trunk(x)
+        h.backward(g)
+        torch.cuda.synchronize()
+        grads.append([p.grad.clone() for p in ag.parameters()])
+    for a, b in zip(*grads):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5 * float(b.abs().max()))
