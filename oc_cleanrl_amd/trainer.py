@@ -66,6 +66,12 @@ ADAM_WRITES_PLANES = False
 # are not a Linear/ReLU stack (NatureCNN): the grad buffer is zeroed before it, as the unfused
 # path does before its backward
 FUSED_HEADS_LOSS_ANY_TRUNK = True
+# The next iteration's shuffle / frame-plan host-to-device copies on a copy stream of their own
+# (PPOTrainer._stage) instead of the compute stream between the update and the next rollout:
+# measured slower at config 2 (1,002k vs 1,030k env steps/s in three interleaved pairs: the
+# cross-stream event waits cost more than the ~60 us of copies they move off the compute
+# stream; profiles/r06/c2_stage_stream/), so off
+STAGE_ON_SIDE_STREAM = False
 # Pixel trunks: the rollout's first convolution reads the u8 frame stacks of the rollout buffer's
 # slot t (agents.trunk_frames: exact bf16 operands, NormalizeImg in the epilogue) instead of the
 # f32 network copy the store writes
@@ -424,6 +430,13 @@ class PPOTrainer:
         self._pending_metrics, self._metrics_host, self._metrics_turn = None, [None, None], 0
         self.perm_event = torch.cuda.Event()
         self.perm_event.record()
+        # the staging copies (host -> perm_stage / plan_stage) on a stream of their own, so they
+        # run beside this iteration's update instead of between it and the next rollout; they
+        # wait for the previous iteration's reads of the stage (stage_read), and the next
+        # iteration's moves out of the stage wait for them (perm_event)
+        self.copy_stream = (torch.cuda.Stream(dev) if STAGE_ON_SIDE_STREAM and
+                            torch.device(dev).type == "cuda" else None)
+        self.stage_read = torch.cuda.Event()
         # PPObj update with every distinct frame of a minibatch encoded once (frames.py)
         W = self.obs_shape[0]
         self.frame_dedup = (a.update_frame_dedup and isinstance(self.agent, PPObj) and
@@ -944,9 +957,18 @@ class PPOTrainer:
             if cap is None or int(self.planner.counts.max()) > cap:
                 self._alloc_plan(self.planner.cap_for(self.planner.counts))
             self.planner.fill(self.plan_host.numpy(), self.planner.cap, used, inv)
-            self.plan_stage.copy_(self.plan_host, non_blocking=True)
-        self.perm_stage.copy_(self.perm_host, non_blocking=True)
-        self.perm_event.record()
+        if self.copy_stream is not None:
+            self.copy_stream.wait_event(self.stage_read)
+            with torch.cuda.stream(self.copy_stream):
+                if self.frame_dedup:
+                    self.plan_stage.copy_(self.plan_host, non_blocking=True)
+                self.perm_stage.copy_(self.perm_host, non_blocking=True)
+                self.perm_event.record()
+        else:
+            if self.frame_dedup:
+                self.plan_stage.copy_(self.plan_host, non_blocking=True)
+            self.perm_stage.copy_(self.perm_host, non_blocking=True)
+            self.perm_event.record()
         self.staged = True
 
     def load_permutation(self, perm) -> None:
@@ -991,9 +1013,12 @@ class PPOTrainer:
         if not self.staged:
             self._shuffle()
         self.current_rng_state = self.staged_rng_state
+        if self.copy_stream is not None:
+            torch.cuda.current_stream(self.dev).wait_event(self.perm_event)
         self.perm_dev.copy_(self.perm_stage)
         if self.frame_dedup:
             self.plan_dev.copy_(self.plan_stage)
+        self.stage_read.record()  # the next staging copies may overwrite the stage after this
         self.staged = False
 
     def _capture(self):
