@@ -1016,7 +1016,8 @@ def _dgrad_weight(weight, s: int, planes: bool = False):
         ent = [buf, None]
         _DG_BUF[bkey] = ent
     buf = ent[0]
-    torch.index_select(mem.reshape(-1), 0, idx.view(-1), out=buf.view(-1))
+    with torch.no_grad():  # (the kernel timer replays this outside autograd's backward)
+        torch.index_select(mem.reshape(-1), 0, idx.view(-1), out=buf.view(-1))
     if not planes or buf.shape[1] % 8:
         return buf, None
     if ent[1] is None:
