@@ -949,6 +949,9 @@ def conv_x6_dgrad(gp, weight, stride: int, in_hw: tuple, out=None, relu_out=None
     M, K = B * QH * QW, T * TW * Cout
     N = s * s * C  # every stride class's C channels: the classes read the same gradient rows
     tile = _conv_fwd_tile(M, N)
+    if CONV_DGRAD_TILE and M % _CONV_TILES[CONV_DGRAD_TILE][0] == 0 and \
+            N % _CONV_TILES[CONV_DGRAD_TILE][1] == 0:
+        tile = CONV_DGRAD_TILE
     if out is None:
         out = torch.empty((B, C, H, W), dtype=f, device=dev, memory_format=torch.channels_last)
     if tuple(out.shape) != (B, C, H, W) or not out.is_contiguous(memory_format=torch.channels_last):
@@ -1024,6 +1027,10 @@ def _dgrad_weight(weight, s: int, planes: bool = False):
         ent[1] = WeightPlanes(fwd=(buf,))
     ent[1].refresh()
     return buf, buf._ocppo_planes["fwd"]
+
+
+# an explicit tile for the data gradients (0: _conv_fwd_tile's choice; experiments)
+CONV_DGRAD_TILE = 0
 
 
 # the data gradient over a zero-padded copy of the output gradient (F.pad: a fill and a copy per
