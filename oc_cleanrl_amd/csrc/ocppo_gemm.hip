@@ -2319,7 +2319,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_u8_img_kernel(ConvImgArg
 // every window byte from L2; here K is taken image by image: a workgroup copies image b's u8
 // stack's bytes into registers one image ahead (each thread the 9 dwords of one row segment per
 // channel), then per channel writes them to LDS as 8 tap-column rows T[kx][y][ox] = img[c][y][4 ox
-// + kx] (ox padded to 24 with zeros), so that the 8 positions a lane feeds one MFMA for a fixed
+// + kx] (ox padded to 24), so that the 8 positions a lane feeds one MFMA for a fixed
 // tap are 16 contiguous bytes; the kx and kx + 4 rows come from the same dwords (one window byte
 // per phase q = kx % 4): 64 byte conversions per thread and channel. (An LDS-DMA copy of the raw
 // image, as in the forward, made the compiler drain it before every T write.) K steps of 32 positions (rows of 24, so a lane's 8
@@ -2441,13 +2441,13 @@ __global__ __launch_bounds__(256, 1) void conv_u8_wgrad_img_kernel(ConvWgImgArgs
 #pragma unroll
         for (int kx = 0; kx < 8; ++kx) {
           const int q = kx & 3, m = kx >> 2;
+          // (the padding positions ox >= OW take whatever finite byte values the dwords hold:
+          // their gradient rows are zero, so they add exact zeros -- no selects here)
           uint32_t o[4];
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const bool ok0 = 8 * ig + 2 * e < OW, ok1 = 8 * ig + 2 * e + 1 < OW;
-            const float f0 = ok0 ? static_cast<float>((raw[c][2 * e + m] >> (8 * q)) & 0xffu) : 0.f;
-            const float f1 =
-                ok1 ? static_cast<float>((raw[c][2 * e + 1 + m] >> (8 * q)) & 0xffu) : 0.f;
+            const float f0 = static_cast<float>((raw[c][2 * e + m] >> (8 * q)) & 0xffu);
+            const float f1 = static_cast<float>((raw[c][2 * e + 1 + m] >> (8 * q)) & 0xffu);
             o[e] = __builtin_amdgcn_perm(__float_as_uint(f1), __float_as_uint(f0), 0x07060302u);
           }
           *reinterpret_cast<uint4*>(reinterpret_cast<unsigned char*>(T) + c * kTChan +
