@@ -960,7 +960,8 @@ def conv_x6_dgrad(gp, weight, stride: int, in_hw: tuple, out=None, relu_out=None
     # the classes stacked class-major: B = [s s C, K] -- one gather through a cached index into
     # the weight's memory (its [Cout, KH, KW, C] order when channels_last) instead of s^2 flips,
     # a stack and a layout copy per call
-    wc, wcp = _dgrad_weight(weight, s, planes=CONV_DGRAD_PLANES)
+    wc, wcp = _dgrad_weight(weight, s, planes=CONV_DGRAD_PLANES and
+                            (tile != 5 or CONV_DGRAD_PLANES_128))
     wpp = None if wcp is None else wcp.data_ptr()
     og = None if s == 1 else _geom(H * W * C, s * W * C, s * C, 0, C, s, W * C, C)
     if CONV_DGRAD_PAD_COPY or tile not in (2, 3, 5, 6):
@@ -996,6 +997,9 @@ _DG_BUF: dict = {}
 # the data gradients' B operand (the stride classes' flipped weights) pre-split into bf16 planes
 # once per call (ocppo_split_planes) instead of in every workgroup of the product
 CONV_DGRAD_PLANES = True
+# ... also on the 128 x 128 tile (the conv2 data gradient's 4 x 32 class columns), whose pre-split
+# instance spills (experiments: A/B)
+CONV_DGRAD_PLANES_128 = True
 
 
 def _dgrad_weight(weight, s: int, planes: bool = False):
