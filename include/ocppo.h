@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define OCPPO_ABI_VERSION 27
+#define OCPPO_ABI_VERSION 28
 
 /* status codes */
 #define OCPPO_OK 0
@@ -500,13 +500,17 @@ OCPPO_API int ocppo_gemm_x6_gather(ocppo_stream_t stream, const float* a, int64_
  * out_geom / pad / mask; the same x6 products per K step, grouped differently over K (not the
  * other tiles' bits). w_planes (mode 0, else null; 16-B aligned, K % 8 == 0): w's three bf16
  * pieces [3, N, K] (ocppo_split_planes of w), read instead of splitting w in every workgroup
- * (the same pieces: the same bits).
+ * (the same pieces: the same bits). mbits_rows (ABI 28; mode 0 with relu, splits 1, no out_geom /
+ * pad / mask, ldc == N, 32 | N, tiles 0, 2, 3, 5, 6; else null): the output's ReLU mask as a
+ * row-major bitmask u32 [M, N / 32], bit n % 32 of word m N / 32 + n / 32 = !(c[m, n] <= 0) --
+ * read by ocppo_relu_bias_grad_bits instead of the f32 output.
  * ------------------------------------------------------------------------------------------- */
 OCPPO_API int ocppo_conv_x6(ocppo_stream_t stream, int mode, const float* x, const int64_t* geom,
                             const float* w, int64_t ldw, float* c, int64_t ldc, int64_t M,
                             int64_t N, int64_t K, int64_t splits, const float* bias, int relu,
                             const int64_t* out_geom, int tile, float* out, const int64_t* pad,
-                            const float* mask, float* dbp, const uint16_t* w_planes);
+                            const float* mask, float* dbp, const uint16_t* w_planes,
+                            uint32_t* mbits_rows);
 
 /* ---------------------------------------------------------------------------------------------
  * The first NatureCNN convolution straight from the rollout's u8 frame stacks (ppo_atari_oc.py:566
@@ -574,6 +578,13 @@ OCPPO_API size_t ocppo_relu_bias_grad_workspace_bytes(int64_t R, int64_t N);
 OCPPO_API int ocppo_relu_bias_grad(ocppo_stream_t stream, const float* g, const float* out,
                          float* gp, float* db, int64_t R, int64_t N, void* workspace,
                          size_t workspace_bytes);
+/* ocppo_relu_bias_grad with the ReLU mask read from a row-major bitmask (ABI 28): gp[r, n] =
+ * bit(r, n) ? g[r, n] : 0 with bit(r, n) = bit n % 32 of mbits[r N / 32 + n / 32] (the forward
+ * epilogue's ocppo_conv_x6 mbits_rows: the same rule as out <= 0 -> 0), db = sum_r gp[r, n].
+ * R >= 1, 32 | N <= 16384; g / gp 16-B aligned; workspace as ocppo_relu_bias_grad's. */
+OCPPO_API int ocppo_relu_bias_grad_bits(ocppo_stream_t stream, const float* g,
+                                        const uint32_t* mbits, float* gp, float* db, int64_t R,
+                                        int64_t N, void* workspace, size_t workspace_bytes);
 
 /* ---------------------------------------------------------------------------------------------
  * First-layer backward in ONE pass — replaces threshold_backward + the split-K weight-gradient

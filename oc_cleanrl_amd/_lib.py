@@ -22,7 +22,7 @@ LIB_PATH = Path(os.environ.get("OCPPO_LIB", PKG / "lib" / "libocppo_hip.so"))
 HEADER = PKG.parent / "include" / "ocppo.h"
 
 # constants mirrored from include/ocppo.h (checked against the header by tests/test_abi.py)
-OCPPO_ABI_VERSION = 27
+OCPPO_ABI_VERSION = 28
 OCPPO_OK, OCPPO_E_INVALID, OCPPO_E_LAUNCH, OCPPO_E_WORKSPACE = 0, 1, 2, 3
 OCPPO_F32, OCPPO_BF16, OCPPO_U8 = 0, 1, 2
 OCPPO_X6_MBITS_ROWS = 2
@@ -62,6 +62,7 @@ SIGNATURES: dict[str, tuple[type, list]] = {
     "ocppo_linear2_act": (I, [P, P, I64, P, P, P, P, P, I64, I64, I64, I64, I64, I, I]),
     "ocppo_relu_bias_grad_workspace_bytes": (SZ, [I64, I64]),
     "ocppo_relu_bias_grad": (I, [P, P, P, P, P, I64, I64, P, SZ]),
+    "ocppo_relu_bias_grad_bits": (I, [P, P, P, P, P, I64, I64, P, SZ]),
     "ocppo_relu_bias_grad_chunks": (I64, [I64, I64]),
     "ocppo_relu_bias_grad_partial": (I, [P, P, P, P, P, I64, I64]),
     "ocppo_sum_splits_db": (I, [P, P, I64, I64, P, P, I64, I64, P]),
@@ -103,7 +104,7 @@ SIGNATURES: dict[str, tuple[type, list]] = {
     "ocppo_gemm_x6_wgrad": (I, [P, P, I64, I64, P, I64, I64, I64, I64, I64, P, I64, P, I64, I64,
                                 P, P, P, I64, I, P]),
     "ocppo_conv_x6": (I, [P, I, P, P, P, I64, P, I64, I64, I64, I64, I64, P, I, P, I, P, P, P,
-                          P, P]),
+                          P, P, P]),
     "ocppo_conv_x6_u8": (I, [P, I, P, P, I64, I64, I64, I64, I64, I64, P, I64, P, I64, I64, I64,
                              I64, P, I, ctypes.c_float, I, P, P, P, P]),
     "ocppo_deferred_finish_run": (I, [P, P]),

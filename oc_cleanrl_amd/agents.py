@@ -659,10 +659,15 @@ class _ConvX6(torch.autograd.Function):
         B, Cin, H, W = x.shape
         Cout = w.shape[0]
         wp = _planes(w, "fwd") if CONV_X6_PLANES else None  # refreshed by the trainer
+        OH = (H - w.shape[2]) // stride + 1
+        mb = (torch.empty(B * OH * OH * Cout // 32, dtype=torch.int32, device=x.device)
+              if CONV_RELU_BITS and relu and Cout % 32 == 0 and H == W and
+              not ops._conv_rows_form(B * OH * OH, Cout) else None)
         y = ops.timed(f"conv_x6_{B}x{Cin}x{H}_{Cout}",
-                      lambda: ops.conv_x6(x, w, b, stride, relu, w_planes=wp))
+                      lambda: ops.conv_x6(x, w, b, stride, relu, w_planes=wp, mbits=mb))
         ctx.conv = (stride, relu)
         ctx.b = b
+        ctx.mb = mb
         ctx.box, ctx.below = box, below
         ctx.save_for_backward(x, w, y if relu else None)
         return y
@@ -676,7 +681,8 @@ class _ConvX6(torch.autograd.Function):
         B, C, OH, OW = g.shape
         g2 = g.permute(0, 2, 3, 1).reshape(-1, C)
         b = ctx.b
-        gp2, db_out, direct_b = _conv_relu_backward(ctx.box, g2, y, b, relu)
+        mb, ctx.mb = ctx.mb, None
+        gp2, db_out, direct_b = _conv_relu_backward(ctx.box, g2, y, b, relu, bits=mb)
         KH, KW = w.shape[2], w.shape[3]
         dw = None
         if ctx.needs_input_grad[1]:
@@ -709,7 +715,7 @@ class _ConvX6(torch.autograd.Function):
         return dx, dw, (None if direct_b else db_out), None, None, None, None
 
 
-def _conv_relu_backward(box, g2, y, b, relu: bool):
+def _conv_relu_backward(box, g2, y, b, relu: bool, bits=None):
     """(gp rows, bias gradient, whether it went to b.grad in place) of a convolution + ReLU whose
     output gradient rows are g2: one relu_bias_grad pass, or nothing when the layer above's data
     gradient already applied this ReLU's backward and wrote the bias gradient (box premasked)."""
@@ -719,6 +725,10 @@ def _conv_relu_backward(box, g2, y, b, relu: bool):
         return g2, box["db"], direct_b
     C = g2.shape[1]
     db_out = b.grad if direct_b else torch.empty_like(b)
+    if relu and bits is not None:  # the forward epilogue's row-major ReLU bitmask
+        gp2, _ = ops.timed(f"relu_bias_grad_bits_{g2.shape[0]}x{C}",
+                           lambda: ops.relu_bias_grad(g2, db=db_out, bits=bits))
+        return gp2, db_out, direct_b
     o2 = y.permute(0, 2, 3, 1).reshape(-1, C) if relu else None
     gp2, _ = ops.timed(f"relu_bias_grad_{g2.shape[0]}x{C}" + ("" if relu else "_norelu"),
                        lambda: ops.relu_bias_grad(g2, o2, db=db_out))
@@ -834,6 +844,11 @@ CONV_DGRAD_RELU = False
 # 3 (519.4k vs 522.1k env steps/s: the masked, column-summing epilogue of the 128 x 64-tile dX
 # costs more than the 59 us streaming pass it removes; profiles/r06/config3/flat_dx/), so off
 CONV_RELU_IN_FLAT_DX = False
+
+# The update's convolution forwards (+ ReLU) also write their ReLU mask as a row-major bitmask
+# (ops.conv_x6 mbits, the tile loop's epilogue), which the backward's ReLU pass reads instead of
+# the f32 output (ops.relu_bias_grad bits=): 4 B -> 1 bit of mask traffic per element
+CONV_RELU_BITS = True
 
 
 def _conv_x6(x, conv, relu: bool):

@@ -2672,7 +2672,8 @@ extern "C" int ocppo_conv_x6(ocppo_stream_t stream, int mode, const float* x, co
                              const float* w, int64_t ldw, float* c, int64_t ldc, int64_t M,
                              int64_t N, int64_t K, int64_t splits, const float* bias, int relu,
                              const int64_t* out_geom, int tile, float* out, const int64_t* pad,
-                             const float* mask, float* dbp, const uint16_t* w_planes) {
+                             const float* mask, float* dbp, const uint16_t* w_planes,
+                             uint32_t* mbits_rows) {
   OCPPO_REQUIRE(mode == 0 || mode == 1, "ocppo_conv_x6: mode %d (0 rows, 1 weight gradient)", mode);
   OCPPO_REQUIRE(tile >= 0 && tile < 8, "ocppo_conv_x6: tile %d", tile);
   OCPPO_REQUIRE(x && geom && w && c, "ocppo_conv_x6: null pointer");
@@ -2681,6 +2682,7 @@ extern "C" int ocppo_conv_x6(ocppo_stream_t stream, int mode, const float* x, co
   if (tile == 7) {  // few rows: K steps split over the waves of a workgroup (conv_x6_rows_kernel)
     OCPPO_REQUIRE(mode == 0 && (N == 32 || N == 64) && M >= 32 && M % 32 == 0 && K >= kX6BK &&
                       K % kX6BK == 0 && splits == 1 && !out_geom && !pad && !mask && !dbp &&
+                      !mbits_rows &&
                       gseg % kX6BK == 0 && ldw >= K && ldw % 4 == 0 && ldc >= N &&
                       M <= INT32_MAX && K <= INT32_MAX && qh >= 1 && qw >= 1 &&
                       M % (qh * qw) == 0 && M < (int64_t{1} << 24) && sb % 4 == 0 &&
@@ -2734,6 +2736,11 @@ extern "C" int ocppo_conv_x6(ocppo_stream_t stream, int mode, const float* x, co
   OCPPO_REQUIRE(!w_planes || (mode == 0 && reinterpret_cast<uintptr_t>(w_planes) % 16 == 0 &&
                                 K % 8 == 0),
                 "ocppo_conv_x6: w_planes needs mode 0 (16-B aligned, K %% 8 == 0)");
+  OCPPO_REQUIRE(!mbits_rows || (mode == 0 && relu && splits == 1 && !out_geom && !pad && !mask &&
+                                N % 32 == 0 && ldc == N && kConvTiles[tile].fn % 2 == 0 &&
+                                reinterpret_cast<uintptr_t>(mbits_rows) % 4 == 0),
+                "ocppo_conv_x6: mbits_rows needs the forward with relu, splits 1, ldc == N, "
+                "32 | N and a tile of an even number of block columns");
   const X6Tile tc = kConvTiles[tile];
   const int64_t bm = 16 * tc.fm * tc.wgm, bn = 16 * tc.fn * tc.wgn;
   OCPPO_REQUIRE(M >= bm && N >= bn && M % bm == 0 && N % bn == 0 && K >= kX6BK && K % kX6BK == 0 &&
@@ -2785,6 +2792,10 @@ extern "C" int ocppo_conv_x6(ocppo_stream_t stream, int mode, const float* x, co
       g.bpl = w_planes;
       g.bpl_ld = K;
       g.bpl_ps = N * K;
+    }
+    if (mbits_rows) {  // the ReLU mask as a row-major bitmask [M, N / 32] (relu_bias_grad_bits)
+      g.mbits_out = reinterpret_cast<uint64_t*>(mbits_rows);
+      g.mbits_rows = 1;
     }
     g.bias = bias;
     g.relu = relu ? 1 : 0;

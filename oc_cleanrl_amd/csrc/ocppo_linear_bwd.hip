@@ -75,14 +75,19 @@ inline RbPlan rb_plan(int64_t R, int64_t N) {
 // TAIL = false: every workgroup stores its partial column sums (plain stores) and is done; the
 // chunk sums are left to a later kernel of the same stream (ocppo_sum_splits_db, which runs after
 // the layer's split-K weight gradient anyway): no ticket, no last-arriver tail on this launch.
-template <bool RELU, bool TAIL = true>
+// MB: the ReLU mask read as a row-major bitmask (bit c % 32 of word r N / 32 + c / 32 = out[r, c]
+// > 0, the producing forward's epilogue: ocppo_conv_x6 mbits_out) instead of the f32 output --
+// 4 B -> 1 bit of mask traffic per element
+template <bool RELU, bool TAIL = true, bool MB = false>
 __global__ __launch_bounds__(256) void relu_bias_grad_kernel(const float* __restrict__ g,
                                                              const float* __restrict__ out,
                                                              float* __restrict__ gp,
                                                              float* __restrict__ db, int64_t R,
                                                              int64_t N, int L, int chunks,
                                                              unsigned* __restrict__ tickets,
-                                                             float* __restrict__ partials) {
+                                                             float* __restrict__ partials,
+                                                             const uint32_t* __restrict__ mbits =
+                                                                 nullptr) {
   __shared__ float4 red[4][64];
   __shared__ float tail[256];
   __shared__ int s_last;
@@ -101,13 +106,25 @@ __global__ __launch_bounds__(256) void relu_bias_grad_kernel(const float* __rest
   const int64_t step = 4 * RP;  // rows per block-wide sweep (4 waves x RP rows)
 
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int64_t wpr = N / 32;                       // MB: mask words per row
+  const int msh = static_cast<int>(c0 & 31);        // MB: this lane's 4 bits in its word
+  auto mask4 = [&](float4& a, int64_t r) {
+    const uint32_t w = mbits[r * wpr + (c0 >> 5)] >> msh;
+    a.x = (w & 1u) ? a.x : 0.f; a.y = (w & 2u) ? a.y : 0.f;
+    a.z = (w & 4u) ? a.z : 0.f; a.w = (w & 8u) ? a.w : 0.f;
+  };
   if (live) {
     int64_t r = r0 + wv * RP + lrow;
     // two rows in flight per lane and iteration
     for (; r + step < r1; r += 2 * step) {
       float4 a = *reinterpret_cast<const float4*>(g + r * N + c0);
       float4 b = *reinterpret_cast<const float4*>(g + (r + step) * N + c0);
-      if (RELU) {
+      if constexpr (MB) {
+        mask4(a, r);
+        mask4(b, r + step);
+        *reinterpret_cast<float4*>(gp + r * N + c0) = a;
+        *reinterpret_cast<float4*>(gp + (r + step) * N + c0) = b;
+      } else if (RELU) {
         const float4 oa = *reinterpret_cast<const float4*>(out + r * N + c0);
         const float4 ob = *reinterpret_cast<const float4*>(out + (r + step) * N + c0);
         a.x = oa.x <= 0.f ? 0.f : a.x; a.y = oa.y <= 0.f ? 0.f : a.y;
@@ -122,7 +139,10 @@ __global__ __launch_bounds__(256) void relu_bias_grad_kernel(const float* __rest
     }
     for (; r < r1; r += step) {
       float4 a = *reinterpret_cast<const float4*>(g + r * N + c0);
-      if (RELU) {
+      if constexpr (MB) {
+        mask4(a, r);
+        *reinterpret_cast<float4*>(gp + r * N + c0) = a;
+      } else if (RELU) {
         const float4 oa = *reinterpret_cast<const float4*>(out + r * N + c0);
         a.x = oa.x <= 0.f ? 0.f : a.x; a.y = oa.y <= 0.f ? 0.f : a.y;
         a.z = oa.z <= 0.f ? 0.f : a.z; a.w = oa.w <= 0.f ? 0.f : a.w;
@@ -237,6 +257,32 @@ extern "C" int ocppo_relu_bias_grad(ocppo_stream_t stream, const float* g, const
     hipLaunchKernelGGL(relu_bias_grad_kernel<false>, grid, block, 0, s, g, out, gp, db, R, N,
                        p.L, p.chunks, tickets, partials);
   return check_launch("ocppo_relu_bias_grad");
+}
+
+extern "C" int ocppo_relu_bias_grad_bits(ocppo_stream_t stream, const float* g,
+                                         const uint32_t* mbits, float* gp, float* db, int64_t R,
+                                         int64_t N, void* workspace, size_t workspace_bytes) {
+  OCPPO_REQUIRE(R >= 1 && N >= 32 && N % 32 == 0 && N <= kRbMaxStripes * 256,
+                "ocppo_relu_bias_grad_bits: bad sizes R=%lld N=%lld (N %% 32 == 0, 32 <= N <= "
+                "16384)", (long long)R, (long long)N);
+  OCPPO_REQUIRE(g && mbits && gp && db && workspace, "ocppo_relu_bias_grad_bits: null pointer");
+  OCPPO_REQUIRE(reinterpret_cast<uintptr_t>(g) % 16 == 0 &&
+                    reinterpret_cast<uintptr_t>(gp) % 16 == 0 &&
+                    reinterpret_cast<uintptr_t>(mbits) % 4 == 0 &&
+                    reinterpret_cast<uintptr_t>(workspace) % 256 == 0,
+                "ocppo_relu_bias_grad_bits: g/gp 16-B aligned, mbits 4-B, workspace 256-B");
+  OCPPO_REQUIRE(workspace_bytes >= ocppo_relu_bias_grad_workspace_bytes(R, N),
+                "ocppo_relu_bias_grad_bits: workspace too small (%zu < %zu)", workspace_bytes,
+                ocppo_relu_bias_grad_workspace_bytes(R, N));
+  clear_stale_error();
+  hipStream_t s = as_stream(stream);
+  const RbPlan p = rb_plan(R, N);
+  unsigned* tickets = static_cast<unsigned*>(workspace);
+  float* partials = reinterpret_cast<float*>(static_cast<char*>(workspace) + kRbTicketBytes);
+  const dim3 grid(static_cast<unsigned>(p.stripes * p.chunks)), block(256);
+  hipLaunchKernelGGL((relu_bias_grad_kernel<true, true, true>), grid, block, 0, s, g, nullptr, gp,
+                     db, R, N, p.L, p.chunks, tickets, partials, mbits);
+  return check_launch("ocppo_relu_bias_grad_bits");
 }
 
 extern "C" int64_t ocppo_relu_bias_grad_chunks(int64_t R, int64_t N) {

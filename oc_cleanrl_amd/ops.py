@@ -798,6 +798,11 @@ def _bounds(dev, x=None, u8=None):
             _tail(u8) if u8 is not None else 0, u8.shape[0] if u8 is not None else 0)
 
 
+def _conv_rows_form(M: int, Cout: int) -> bool:
+    """conv_x6 takes the few-rows form (ocppo_conv_x6 tile 7) for this product."""
+    return CONV_FWD_ROWS and M <= CONV_FWD_ROWS_MAX and Cout in (32, 64) and M % 32 == 0
+
+
 def _conv_planes_ptr(w_planes, N: int, K: int, dev):
     if w_planes is None:
         return None
@@ -807,12 +812,15 @@ def _conv_planes_ptr(w_planes, N: int, K: int, dev):
     return _check(w_planes, "w_planes", torch.bfloat16, dev)
 
 
-def conv_x6(x, weight, bias=None, stride: int = 1, relu: bool = True, out=None, w_planes=None):
+def conv_x6(x, weight, bias=None, stride: int = 1, relu: bool = True, out=None, w_planes=None,
+            mbits=None):
     """act(conv2d(x, weight) + bias) (architectures/ppo.py:20-31's Conv2d + ReLU) on ocppo_conv_x6:
     channels_last f32 x [B, C, H, W], weight [Cout, C, KH, KW] -> channels_last [B, Cout, OH, OW]
     (no autograd; agents._ConvX6 is the autograd form). w_planes: the weight's [Cout, KH KW C]
     matrix pre-split into bf16 [3, Cout, KH KW C] (ocppo_split_planes: the same pieces as the
-    in-kernel split, so the same bits)."""
+    in-kernel split, so the same bits). mbits: an int32 [B OH OW Cout / 32] tensor the tile loop's
+    epilogue fills with the output's ReLU mask, row-major (relu_bias_grad's bits= form); the
+    few-rows form (no autograd) takes none."""
     if not conv_x6_ok(x, weight, stride):
         raise ValueError(f"conv_x6: unsupported shapes x {tuple(x.shape)}, weight "
                          f"{tuple(weight.shape)}, stride {stride} (conv_x6_ok)")
@@ -829,23 +837,28 @@ def conv_x6(x, weight, bias=None, stride: int = 1, relu: bool = True, out=None, 
     if tuple(out.shape) != (B, Cout, OH, OW) or not out.is_contiguous(memory_format=torch.channels_last):
         raise ValueError("conv_x6: out must be a channels_last [B, Cout, OH, OW] tensor")
     geom = _geom(OH, OW, H * W * C, s * W * C, s * C, W * C, KW * C)
-    if CONV_FWD_ROWS and M <= CONV_FWD_ROWS_MAX and Cout in (32, 64) and M % 32 == 0:
+    if _conv_rows_form(M, Cout):
         # few rows (the rollout's batch): K steps split over the waves of a workgroup
+        if mbits is not None:
+            raise ValueError("conv_x6: the few-rows form writes no ReLU bitmask")
         _bounds(dev, x)
         call("ocppo_conv_x6", _stream(dev), 0, x.data_ptr(), geom, wm.data_ptr(), K,
              out.data_ptr(), Cout, M, Cout, K, 1, _opt(bias, "bias", f, dev, Cout),
              int(bool(relu)), None, 7, None, None, None, None,
-             _conv_planes_ptr(w_planes, Cout, K, dev))
+             _conv_planes_ptr(w_planes, Cout, K, dev), None)
         return out
     tile = _conv_fwd_tile(M, Cout)
     bm, bn = _CONV_TILES[tile]
     S = _conv_fwd_splits((M // bm) * (Cout // bn), K // 32)
     _bounds(dev, x)
     wpp = _conv_planes_ptr(w_planes, Cout, K, dev)
+    if mbits is not None and (S != 1 or not relu or Cout % 32):
+        raise ValueError("conv_x6: mbits needs one product with relu, 32 | Cout")
     if S == 1:
         call("ocppo_conv_x6", _stream(dev), 0, x.data_ptr(), geom, wm.data_ptr(), K,
              out.data_ptr(), Cout, M, Cout, K, 1, _opt(bias, "bias", f, dev, Cout),
-             int(bool(relu)), None, tile, None, None, None, None, wpp)
+             int(bool(relu)), None, tile, None, None, None, None, wpp,
+             _opt(mbits, "mbits", torch.int32, dev, M * Cout // 32))
         return out
     # few rows (the rollout's batch): K-split partials, then bias + ReLU on their ordered sum
     key = ("fwd", str(dev), S, M, Cout)
@@ -853,7 +866,7 @@ def conv_x6(x, weight, bias=None, stride: int = 1, relu: bool = True, out=None, 
         _CONV_PARTS[key] = torch.empty((S, M, Cout), dtype=f, device=dev)
     part = _CONV_PARTS[key]
     call("ocppo_conv_x6", _stream(dev), 0, x.data_ptr(), geom, wm.data_ptr(), K, part.data_ptr(),
-         Cout, M, Cout, K, S, None, 0, None, tile, None, None, None, None, wpp)
+         Cout, M, Cout, K, S, None, 0, None, tile, None, None, None, None, wpp, None)
     call("ocppo_sum_splits_act", _stream(dev), part.data_ptr(), S, M, Cout,
          _opt(bias, "bias", f, dev, Cout), int(bool(relu)), out.data_ptr())
     return out
@@ -918,7 +931,7 @@ def conv_x6_wgrad(gp, x, kernel: tuple, stride: int, out=None):
     call("ocppo_conv_x6", _stream(dev), 1, x.data_ptr(),
          _geom(OH, OW, H * W * C, s * W * C, s * C, W * C, KW * C),
          _check(gp, "gp", f, dev), Cout, part.data_ptr(), N, Cout, N, rows, S, None, 0, None, tile,
-         out.data_ptr(), None, None, None, None)
+         out.data_ptr(), None, None, None, None, None)
     return out
 
 
@@ -971,7 +984,7 @@ def conv_x6_dgrad(gp, weight, stride: int, in_hw: tuple, out=None, relu_out=None
         _bounds(dev, gpad)
         call("ocppo_conv_x6", _stream(dev), 0, gpad.data_ptr(),
              _geom(QH, QW, Hp * Wp * Cout, Wp * Cout, Cout, Wp * Cout, TW * Cout), wc.data_ptr(),
-             K, out.data_ptr(), C, M, N, K, 1, None, 0, og, tile, None, None, None, None, wpp)
+             K, out.data_ptr(), C, M, N, K, 1, None, 0, og, tile, None, None, None, None, wpp, None)
         return out
     # the padding as bounds in the loader: taps outside the gradient read as zeros
     mask = dbp = None
@@ -985,7 +998,7 @@ def conv_x6_dgrad(gp, weight, stride: int, in_hw: tuple, out=None, relu_out=None
     call("ocppo_conv_x6", _stream(dev), 0, g.data_ptr(),
          _geom(QH, QW, 0, 0, 0, 0, TW * Cout), wc.data_ptr(), K, out.data_ptr(), C, M, N, K, 1,
          None, 0, og, tile, None, _geom(T - 1, TW - 1, OH, OW, Cout),
-         None if mask is None else mask.data_ptr(), None if dbp is None else dbp.data_ptr(), wpp)
+         None if mask is None else mask.data_ptr(), None if dbp is None else dbp.data_ptr(), wpp, None)
     if dbp is not None:
         # row tiles, then stride classes, in order (f64, one rounding)
         db.copy_(dbp.view(-1, s * s, C).double().sum(0).sum(0))
@@ -1333,9 +1346,10 @@ def relu_bias_grad_ok(g) -> bool:
             and 4 <= g.shape[1] <= 16384 and g.is_contiguous() and g.data_ptr() % 16 == 0)
 
 
-def relu_bias_grad(g, out=None, db=None, gp=None):
+def relu_bias_grad(g, out=None, db=None, gp=None, bits=None):
     """(gp, db): gp = threshold_backward(g, out, 0) (g itself when out is None), db = gp.sum(0),
-    in one pass over g [R, N] f32 (N % 4 == 0). Deterministic."""
+    in one pass over g [R, N] f32 (N % 4 == 0). Deterministic. bits: the ReLU mask as the
+    forward epilogue's row-major bitmask (int32 [R N / 32], conv_x6(..., mbits=)) instead of out."""
     if g.dim() != 2:
         raise ValueError(f"g must be [R, N], got {tuple(g.shape)}")
     R, N = g.shape
@@ -1343,6 +1357,13 @@ def relu_bias_grad(g, out=None, db=None, gp=None):
     f = torch.float32
     if db is None:
         db = torch.empty(N, dtype=f, device=dev)
+    if bits is not None:
+        gp = torch.empty_like(g) if gp is None else gp
+        ws = _relu_bias_ws(R, N, dev)
+        call("ocppo_relu_bias_grad_bits", _stream(dev), _check(g, "g", f, dev),
+             _check(bits, "bits", torch.int32, dev, R * N // 32), _check(gp, "gp", f, dev, R * N),
+             _check(db, "db", f, dev, N), R, N, ws.data_ptr(), ws.numel())
+        return gp, db
     if out is not None and gp is None:
         gp = torch.empty_like(g)
     ws = _relu_bias_ws(R, N, dev)

@@ -373,3 +373,27 @@ def test_pre_split_weight_planes_are_bitwise_the_in_kernel_split(name, monkeypat
     dx = ops.conv_x6_dgrad(gp, w, s, tuple(x.shape[2:]))
     monkeypatch.setattr(ops, "CONV_DGRAD_PLANES", True)
     assert torch.equal(dx, ops.conv_x6_dgrad(gp, w, s, tuple(x.shape[2:])))
+
+
+@pytest.mark.parametrize("name", ["conv2", "conv3"])
+def test_forward_relu_bitmask_feeds_relu_bias_grad(name, monkeypatch):
+    """The tile loop's forward epilogue writes the ReLU mask row-major (ocppo_conv_x6
+    mbits_rows): bit = output > 0; ocppo_relu_bias_grad_bits reading it gives bitwise the gp and
+    db of ocppo_relu_bias_grad reading the f32 output."""
+    monkeypatch.setattr(ops, "CONV_FWD_ROWS", False)
+    x, w, b, s = _operands(name, 51)
+    Cout = w.shape[0]
+    y0 = ops.conv_x6(x, w, b, s, True)
+    M = y0.numel() // Cout
+    mb = torch.full((M * Cout // 32,), -1, dtype=torch.int32, device=DEV)
+    y = ops.conv_x6(x, w, b, s, True, mbits=mb)
+    assert torch.equal(y, y0)
+    yr = y.permute(0, 2, 3, 1).reshape(-1, Cout)
+    words = mb.view(M, Cout // 32)
+    bits = torch.stack([(words[:, c // 32] >> (c % 32)) & 1 for c in range(Cout)], 1).bool()
+    assert torch.equal(bits, yr > 0)
+    g = torch.Generator(device=DEV).manual_seed(52)
+    g2 = torch.rand(M, Cout, device=DEV, generator=g) * 2 - 1
+    gp_ref, db_ref = ops.relu_bias_grad(g2, yr.contiguous())
+    gp, db = ops.relu_bias_grad(g2, bits=mb)
+    assert torch.equal(gp, gp_ref) and torch.equal(db, db_ref)
