@@ -210,8 +210,12 @@ def roofline_of(name, k, flops, traffic, src):
 
 
 def relu_bias_grad_bytes(name: str):
-    """relu_bias_grad_{R}x{N}[_norelu]: g (+ out in, gp out) f32 [R, N] + db [N] out."""
+    """relu_bias_grad_{R}x{N}[_norelu]: g (+ out in, gp out) f32 [R, N] + db [N] out;
+    relu_bias_grad_bits_{R}x{N}: g in, gp out f32 [R, N], the mask 1 bit per element, db out."""
     spec = name[len("relu_bias_grad_"):]
+    if spec.startswith("bits_"):
+        R, N = (int(v) for v in spec[len("bits_"):].split("x"))
+        return R * N * 8 + R * N // 8 + 4 * N
     relu = not spec.endswith("_norelu")
     R, N = (int(v) for v in spec.replace("_norelu", "").split("x"))
     return R * N * (12 if relu else 4) + 4 * N
