@@ -184,3 +184,13 @@ def test_status_of_a_previous_run_is_ignored(tmp_path, monkeypatch):
         assert set(watch.read_status(tmp_path, run="this-run")) == {0}
     finally:
         w.stop()
+
+
+def test_kernel_site_byte_counts():
+    """The bench's algorithmic bytes per timer site (the line's HBM rooflines): the f32-mask and
+    bitmask ReLU-backward passes, and the unmasked (no ReLU) form."""
+    R, N = 401408, 64
+    assert bench.relu_bias_grad_bytes(f"relu_bias_grad_{R}x{N}") == R * N * 12 + 4 * N
+    assert bench.relu_bias_grad_bytes(f"relu_bias_grad_{R}x{N}_norelu") == R * N * 4 + 4 * N
+    assert bench.relu_bias_grad_bytes(f"relu_bias_grad_bits_{R}x{N}") == \
+        R * N * 8 + R * N // 8 + 4 * N
